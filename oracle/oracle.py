@@ -1,0 +1,175 @@
+"""ctypes wrapper over oracle/_build/liboracle.so — the CPU restatement of Flink's WindowOperator.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, never by the product package flink_amd/.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+
+TUMBLING, SLIDING, SESSION = 0, 1, 2
+VAL_I64, VAL_I32, VAL_F64 = 0, 1, 2
+_ASSIGNERS = {"tumbling": TUMBLING, "sliding": SLIDING, "session": SESSION}
+_VALTYPES = {"i64": VAL_I64, "i32": VAL_I32, "f64": VAL_F64}
+
+
+class OracleCfg(ctypes.Structure):
+    _fields_ = [("assigner", ctypes.c_int32), ("value_type", ctypes.c_int32), ("size", ctypes.c_int64),
+                ("slide", ctypes.c_int64), ("offset", ctypes.c_int64), ("gap", ctypes.c_int64),
+                ("lateness", ctypes.c_int64), ("purging", ctypes.c_int32), ("side_output", ctypes.c_int32)]
+
+
+ROW_DTYPE = np.dtype([("key", "<i8"), ("start", "<i8"), ("end", "<i8"), ("count", "<i8"), ("sum", "<i8"),
+                      ("min", "<i8"), ("max", "<i8"), ("epoch", "<i8")])
+SIDE_DTYPE = np.dtype([("key", "<i8"), ("ts", "<i8"), ("val", "<i8"), ("epoch", "<i8")])
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        I64P = ctypes.POINTER(ctypes.c_int64)
+        I32P = ctypes.POINTER(ctypes.c_int32)
+        L.oracle_create.restype = P
+        L.oracle_create.argtypes = [ctypes.POINTER(OracleCfg)]
+        L.oracle_destroy.argtypes = [P]
+        L.oracle_process.argtypes = [P, I64P, I64P, I64P, ctypes.c_int64]
+        L.oracle_watermark.argtypes = [P, ctypes.c_int64]
+        for f in ("oracle_num_rows", "oracle_num_side_rows", "oracle_late_dropped", "oracle_num_state_entries",
+                  "oracle_num_timers", "oracle_current_watermark"):
+            getattr(L, f).restype = ctypes.c_int64
+            getattr(L, f).argtypes = [P]
+        L.oracle_get_rows.argtypes = [P, P]
+        L.oracle_get_side_rows.argtypes = [P, P]
+        L.oracle_clear_rows.argtypes = [P]
+        L.oracle_long_hash.restype = ctypes.c_int32
+        L.oracle_long_hash.argtypes = [ctypes.c_int64]
+        L.oracle_murmur_hash.restype = ctypes.c_int32
+        L.oracle_murmur_hash.argtypes = [ctypes.c_int32]
+        L.oracle_key_group.restype = ctypes.c_int32
+        L.oracle_key_group.argtypes = [ctypes.c_int32, ctypes.c_int32]
+        L.oracle_operator_index.restype = ctypes.c_int32
+        L.oracle_operator_index.argtypes = [ctypes.c_int32] * 3
+        L.oracle_key_group_range.argtypes = [ctypes.c_int32] * 3 + [I32P, I32P]
+        L.oracle_key_groups_long.argtypes = [I64P, ctypes.c_int64, ctypes.c_int32, I32P]
+        L.oracle_window_start.restype = ctypes.c_int64
+        L.oracle_window_start.argtypes = [ctypes.c_int64] * 3
+        L.oracle_string_hash.restype = ctypes.c_int32
+        L.oracle_string_hash.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+        L.oracle_run_parallel.restype = ctypes.c_int64
+        L.oracle_run_parallel.argtypes = [ctypes.POINTER(OracleCfg), I64P, I64P, I64P, ctypes.c_int64, ctypes.c_int64,
+                                          I64P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, I64P]
+        _lib = L
+    return _lib
+
+
+def _i64p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+
+
+def make_cfg(assigner="tumbling", size=0, slide=0, offset=0, gap=0, lateness=0, purging=False, side_output=False,
+             value_type="i64"):
+    return OracleCfg(_ASSIGNERS[assigner], _VALTYPES[value_type], size, slide, offset, gap, lateness, int(purging),
+                     int(side_output))
+
+
+class OracleError(RuntimeError):
+    def __init__(self, code):
+        super().__init__(f"oracle error {code}")
+        self.code = code
+
+
+class WindowOperatorOracle:
+    """Element-by-element WindowOperator restatement (see window_oracle.h)."""
+
+    def __init__(self, **cfg):
+        self.cfg = make_cfg(**cfg)
+        self._h = lib().oracle_create(ctypes.byref(self.cfg))
+
+    def close(self):
+        if self._h:
+            lib().oracle_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def process(self, keys, ts, vals):
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        vals = np.ascontiguousarray(vals)
+        if vals.dtype == np.float64:
+            vals = vals.view(np.int64)
+        vals = np.ascontiguousarray(vals, dtype=np.int64)
+        rc = lib().oracle_process(self._h, _i64p(keys), _i64p(ts), _i64p(vals), len(keys))
+        if rc != 0:
+            raise OracleError(rc)
+
+    def watermark(self, wm):
+        rc = lib().oracle_watermark(self._h, int(wm))
+        if rc != 0:
+            raise OracleError(rc)
+
+    def rows(self):
+        n = lib().oracle_num_rows(self._h)
+        out = np.zeros(n, dtype=ROW_DTYPE)
+        if n:
+            lib().oracle_get_rows(self._h, out.ctypes.data)
+        return out
+
+    def clear_rows(self):
+        lib().oracle_clear_rows(self._h)
+
+    def side_rows(self):
+        n = lib().oracle_num_side_rows(self._h)
+        out = np.zeros(n, dtype=SIDE_DTYPE)
+        if n:
+            lib().oracle_get_side_rows(self._h, out.ctypes.data)
+        return out
+
+    @property
+    def late_dropped(self):
+        return lib().oracle_late_dropped(self._h)
+
+    @property
+    def num_state_entries(self):
+        return lib().oracle_num_state_entries(self._h)
+
+    @property
+    def num_timers(self):
+        return lib().oracle_num_timers(self._h)
+
+
+def key_groups_long(keys, max_par):
+    keys = np.ascontiguousarray(keys, dtype=np.int64)
+    out = np.zeros(len(keys), dtype=np.int32)
+    lib().oracle_key_groups_long(_i64p(keys), len(keys), max_par, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return out
+
+
+def run_parallel(cfg, keys, ts, vals, batch, wms, max_par, threads):
+    c = make_cfg(**cfg)
+    late = np.zeros(1, dtype=np.int64)
+    wms = np.ascontiguousarray(wms, dtype=np.int64)
+    keys = np.ascontiguousarray(keys, dtype=np.int64)
+    ts = np.ascontiguousarray(ts, dtype=np.int64)
+    vals = np.ascontiguousarray(vals)
+    if vals.dtype == np.float64:
+        vals = vals.view(np.int64)
+    rows = lib().oracle_run_parallel(ctypes.byref(c), _i64p(keys), _i64p(ts), _i64p(vals), len(keys), batch,
+                                     _i64p(wms), len(wms), max_par, threads, _i64p(late))
+    return rows, int(late[0])

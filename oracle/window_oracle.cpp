@@ -1,0 +1,573 @@
+// window_oracle.cpp — CPU restatement of Flink's keyed event-time WindowOperator.
+// TEST INFRASTRUCTURE ONLY (parity checker + cpu_baseline).  See window_oracle.h for
+// the list of reference files restated here.  Paths below are relative to
+// /root/reference/flink-streaming-java/src/main/java/org/apache/flink/streaming/ unless
+// they start with flink-*.
+#include "window_oracle.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <queue>
+#include <set>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------- Java arithmetic
+inline int64_t jadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+inline int64_t jsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+const int64_t LMAX = INT64_MAX;
+const int64_t LMIN = INT64_MIN;
+
+// flink-core/src/main/java/org/apache/flink/util/MathUtils.java:191-198
+inline int32_t bit_mix(int32_t in) {
+  uint32_t x = (uint32_t)in;
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return (int32_t)x;
+}
+inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+// MathUtils.java:134-154
+inline int32_t murmur(int32_t code) {
+  uint32_t c = (uint32_t)code;
+  c *= 0xcc9e2d51u;
+  c = rotl32(c, 15);
+  c *= 0x1b873593u;
+  c = rotl32(c, 13);
+  c = c * 5u + 0xe6546b64u;
+  c ^= 4u;
+  int32_t r = bit_mix((int32_t)c);
+  if (r >= 0) return r;
+  if (r != INT32_MIN) return -r;
+  return 0;
+}
+inline int32_t long_hash(int64_t v) { return (int32_t)(v ^ (int64_t)((uint64_t)v >> 32)); }
+
+// TimeWindow.java:254-256  (Java: timestamp - (timestamp - offset + windowSize) % windowSize)
+inline int64_t window_start(int64_t ts, int64_t offset, int64_t size) {
+  int64_t t = jadd(jsub(ts, offset), size);
+  return jsub(ts, t % size);
+}
+
+// Double.doubleToLongBits (canonical NaN) and Double.compare ordering as a signed key.
+inline int64_t dbits(double d) {
+  if (std::isnan(d)) return 0x7ff8000000000000LL;
+  int64_t b;
+  memcpy(&b, &d, 8);
+  return b;
+}
+inline double bitsd(int64_t b) {
+  double d;
+  memcpy(&d, &b, 8);
+  return d;
+}
+inline int java_double_compare(double a, double b) {
+  if (a < b) return -1;
+  if (a > b) return 1;
+  int64_t x = dbits(a), y = dbits(b);
+  return x == y ? 0 : (x < y ? -1 : 1);
+}
+
+// ---------------------------------------------------------------- TimeWindow
+struct TW {
+  int64_t start, end;
+  int64_t maxTs() const { return jsub(end, 1); }  // TimeWindow.java:83-85
+  bool operator==(const TW& o) const { return start == o.start && end == o.end; }
+  bool operator<(const TW& o) const { return start != o.start ? start < o.start : end < o.end; }
+  bool intersects(const TW& o) const { return start <= o.end && end >= o.start; }  // :117-119
+  TW cover(const TW& o) const { return TW{std::min(start, o.start), std::max(end, o.end)}; }  // :124-126
+};
+
+struct Acc {
+  int64_t cnt = 0;
+  int64_t isum = 0;
+  double dsum = 0.0;
+  int64_t imn = 0, imx = 0;
+  double dmn = 0.0, dmx = 0.0;
+};
+
+struct KW {
+  int64_t key;
+  TW w;
+  bool operator==(const KW& o) const { return key == o.key && w == o.w; }
+};
+inline uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+struct KWHash {
+  size_t operator()(const KW& k) const {
+    return mix64((uint64_t)k.key * 0x9E3779B97F4A7C15ULL ^ mix64((uint64_t)k.w.start) ^ ((uint64_t)k.w.end << 1));
+  }
+};
+
+// InternalTimer: (timestamp, key, namespace).  Ordering by timestamp only
+// (InternalTimer.java:62-64); ties are broken deterministically here — the
+// reference leaves them in PriorityQueue heap order, i.e. undefined.
+struct Timer {
+  int64_t ts, key;
+  TW w;
+  bool operator==(const Timer& o) const { return ts == o.ts && key == o.key && w == o.w; }
+};
+struct TimerHash {
+  size_t operator()(const Timer& t) const { return KWHash()(KW{t.key, t.w}) ^ mix64((uint64_t)t.ts); }
+};
+struct TimerGreater {
+  bool operator()(const Timer& a, const Timer& b) const {
+    if (a.ts != b.ts) return a.ts > b.ts;
+    if (a.key != b.key) return a.key > b.key;
+    return b.w < a.w;
+  }
+};
+
+struct OpError {
+  int code;
+};
+
+class WindowOperatorOracle {
+ public:
+  explicit WindowOperatorOracle(const oracle_cfg& c) : cfg(c) {}
+
+  oracle_cfg cfg;
+  int64_t wm = LMIN;  // HeapInternalTimerService.currentWatermark initial value
+  int64_t epoch = 0;
+  int64_t late_dropped = 0;
+  std::vector<oracle_row> rows;
+  std::vector<oracle_side_row> side;
+
+  std::unordered_map<KW, Acc, KWHash> state;  // window-contents (key, namespace) -> ACC
+  // event-time timers: dedup set + min-heap with lazy deletion
+  std::unordered_set<Timer, TimerHash> timer_set;
+  std::priority_queue<Timer, std::vector<Timer>, TimerGreater> timer_q;
+  // MergingWindowSet per key: window -> state window
+  std::unordered_map<int64_t, std::map<TW, TW>> merging;
+
+  bool is_merging() const { return cfg.assigner == OR_SESSION; }
+
+  // ------------------------------------------------ accumulator (CountSumMinMax)
+  void acc_add(Acc& a, int64_t v) const {
+    if (cfg.value_type == OR_VAL_F64) {
+      double d = bitsd(v);
+      if (a.cnt == 0) {
+        a.dmn = a.dmx = d;
+      } else {
+        if (java_double_compare(d, a.dmn) < 0) a.dmn = d;
+        if (java_double_compare(d, a.dmx) > 0) a.dmx = d;
+      }
+      a.dsum += d;
+    } else {
+      if (a.cnt == 0) {
+        a.imn = a.imx = v;
+      } else {
+        a.imn = std::min(a.imn, v);
+        a.imx = std::max(a.imx, v);
+      }
+      a.isum = jadd(a.isum, v);
+    }
+    a.cnt += 1;
+  }
+  // AggregateFunction.merge(a, b)
+  Acc acc_merge(const Acc& a, const Acc& b) const {
+    if (a.cnt == 0) return b;
+    if (b.cnt == 0) return a;
+    Acc r = a;
+    r.cnt = a.cnt + b.cnt;
+    if (cfg.value_type == OR_VAL_F64) {
+      r.dsum = a.dsum + b.dsum;
+      r.dmn = java_double_compare(b.dmn, a.dmn) < 0 ? b.dmn : a.dmn;
+      r.dmx = java_double_compare(b.dmx, a.dmx) > 0 ? b.dmx : a.dmx;
+    } else {
+      r.isum = jadd(a.isum, b.isum);
+      r.imn = std::min(a.imn, b.imn);
+      r.imx = std::max(a.imx, b.imx);
+    }
+    return r;
+  }
+
+  // ------------------------------------------------ timers (HeapInternalTimerService.java:224-248)
+  void register_timer(int64_t ts, int64_t key, const TW& w) {
+    Timer t{ts, key, w};
+    if (timer_set.insert(t).second) timer_q.push(t);
+  }
+  void delete_timer(int64_t ts, int64_t key, const TW& w) { timer_set.erase(Timer{ts, key, w}); }
+
+  // ------------------------------------------------ WindowOperator.java:576-651
+  int64_t cleanup_time(const TW& w) const {
+    int64_t c = jadd(w.maxTs(), cfg.lateness);
+    return c >= w.maxTs() ? c : LMAX;
+  }
+  bool is_window_late(const TW& w) const { return cleanup_time(w) <= wm; }
+  bool is_element_late(int64_t ts) const { return jadd(ts, cfg.lateness) <= wm; }
+  void register_cleanup_timer(int64_t key, const TW& w) {
+    int64_t c = cleanup_time(w);
+    if (c == LMAX) return;
+    register_timer(c, key, w);
+  }
+  void delete_cleanup_timer(int64_t key, const TW& w) {
+    int64_t c = cleanup_time(w);
+    if (c == LMAX) return;
+    delete_timer(c, key, w);
+  }
+
+  void emit(int64_t key, const TW& w, const Acc& a) {
+    oracle_row r;
+    r.key = key;
+    r.start = w.start;
+    r.end = w.end;
+    r.count = a.cnt;
+    if (cfg.value_type == OR_VAL_F64) {
+      r.sum = dbits(a.dsum);
+      r.min = dbits(a.dmn);
+      r.max = dbits(a.dmx);
+      // keep raw (non-canonical) sum bits: sums are compared with tolerance
+      memcpy(&r.sum, &a.dsum, 8);
+    } else {
+      r.sum = cfg.value_type == OR_VAL_I32 ? (int64_t)(int32_t)a.isum : a.isum;
+      r.min = a.imn;
+      r.max = a.imx;
+    }
+    r.epoch = epoch;
+    rows.push_back(r);
+  }
+
+  // ------------------------------------------------ assigners
+  void assign(int64_t ts, std::vector<TW>& out) const {
+    out.clear();
+    if (cfg.assigner == OR_SESSION) {  // EventTimeSessionWindows.java:59-61
+      out.push_back(TW{ts, jadd(ts, cfg.gap)});
+      return;
+    }
+    if (ts == LMIN) throw OpError{OR_ERR_NO_TIMESTAMP};
+    if (cfg.assigner == OR_TUMBLING) {  // TumblingEventTimeWindows.java:63-73
+      int64_t s = window_start(ts, cfg.offset, cfg.size);
+      out.push_back(TW{s, jadd(s, cfg.size)});
+      return;
+    }
+    // SlidingEventTimeWindows.java:67-81
+    int64_t last = window_start(ts, cfg.offset, cfg.slide);
+    for (int64_t s = last; s > jsub(ts, cfg.size); s = jsub(s, cfg.slide)) out.push_back(TW{s, jadd(s, cfg.size)});
+  }
+
+  // ------------------------------------------------ MergingWindowSet.java:150-225 (+ TimeWindow.mergeWindows)
+  // Returns the window the new window ended up in; calls the merge function of
+  // WindowOperator.java:305-339 inline.
+  TW add_window(int64_t key, std::map<TW, TW>& mapping, const TW& nw) {
+    std::vector<TW> ws;
+    ws.reserve(mapping.size() + 1);
+    for (auto& kv : mapping) ws.push_back(kv.first);
+    ws.push_back(nw);
+    std::stable_sort(ws.begin(), ws.end(), [](const TW& a, const TW& b) { return a.start < b.start; });
+    // sweep (TimeWindow.java:201-244)
+    std::vector<std::pair<TW, std::set<TW>>> merged;
+    bool have = false;
+    std::pair<TW, std::set<TW>> cur;
+    for (const TW& c : ws) {
+      if (!have) {
+        cur.first = c;
+        cur.second.clear();
+        cur.second.insert(c);
+        have = true;
+      } else if (cur.first.intersects(c)) {
+        cur.first = cur.first.cover(c);
+        cur.second.insert(c);
+      } else {
+        merged.push_back(cur);
+        cur.first = c;
+        cur.second.clear();
+        cur.second.insert(c);
+      }
+    }
+    if (have) merged.push_back(cur);
+    std::vector<std::pair<TW, std::set<TW>>> results;
+    for (auto& m : merged)
+      if (m.second.size() > 1) results.push_back(m);
+
+    TW result = nw;
+    bool merged_new = false;
+    for (auto& r : results) {
+      const TW merge_result = r.first;
+      std::set<TW> mws = r.second;
+      if (mws.erase(nw)) {
+        merged_new = true;
+        result = merge_result;
+      }
+      // "pick any of the merged windows": deterministic first here (the reference uses
+      // HashSet iteration order; the choice only decides where state lives).
+      TW merged_state_window = mapping.at(*mws.begin());
+      std::vector<TW> merged_state_windows;
+      for (const TW& m : mws) {
+        auto it = mapping.find(m);
+        if (it != mapping.end()) {
+          merged_state_windows.push_back(it->second);
+          mapping.erase(it);
+        }
+      }
+      mapping[merge_result] = merged_state_window;
+      merged_state_windows.erase(
+          std::remove(merged_state_windows.begin(), merged_state_windows.end(), merged_state_window),
+          merged_state_windows.end());
+      if (!(mws.count(merge_result) && mws.size() == 1)) {
+        merge_function(key, merge_result, mws, mapping[merge_result], merged_state_windows);
+      }
+    }
+    if (results.empty() || (result == nw && !merged_new)) mapping[result] = result;
+    return result;
+  }
+
+  // WindowOperator.java:308-339
+  void merge_function(int64_t key, const TW& merge_result, const std::set<TW>& merged_windows,
+                      const TW& state_window_result, const std::vector<TW>& merged_state_windows) {
+    if (jadd(merge_result.maxTs(), cfg.lateness) <= wm) throw OpError{OR_ERR_MERGE_LATE};
+    // EventTimeTrigger.onMerge (EventTimeTrigger.java:70-73): unconditional registration
+    register_timer(merge_result.maxTs(), key, merge_result);
+    for (const TW& m : merged_windows) {
+      delete_timer(m.maxTs(), key, m);  // triggerContext.clear() -> EventTimeTrigger.clear
+      delete_cleanup_timer(key, m);
+    }
+    // AbstractHeapMergingState.mergeNamespaces (:67-93)
+    if (merged_state_windows.empty()) return;
+    bool have = false;
+    Acc acc;
+    for (const TW& s : merged_state_windows) {
+      auto it = state.find(KW{key, s});
+      if (it == state.end()) continue;
+      Acc src = it->second;
+      state.erase(it);
+      acc = have ? acc_merge(acc, src) : src;
+      have = true;
+    }
+    if (have) {
+      auto it = state.find(KW{key, state_window_result});
+      if (it != state.end())
+        it->second = acc_merge(it->second, acc);
+      else
+        state[KW{key, state_window_result}] = acc;
+    }
+  }
+
+  // ------------------------------------------------ WindowOperator.processElement (:291-421)
+  std::vector<TW> wbuf;
+  void process_element(int64_t key, int64_t ts, int64_t val) {
+    assign(ts, wbuf);
+    bool skipped = true;
+    if (is_merging()) {
+      std::map<TW, TW>& mapping = merging[key];
+      for (const TW& w : wbuf) {
+        TW actual = add_window(key, mapping, w);
+        if (is_window_late(actual)) {
+          // MergingWindowSet.retireWindow
+          if (!mapping.erase(actual)) throw OpError{OR_ERR_ILLEGAL_STATE};
+          continue;
+        }
+        skipped = false;
+        auto it = mapping.find(actual);
+        if (it == mapping.end()) throw OpError{OR_ERR_ILLEGAL_STATE};
+        TW sw = it->second;
+        Acc& a = state[KW{key, sw}];
+        acc_add(a, val);
+        // EventTimeTrigger.onElement
+        if (actual.maxTs() <= wm) {
+          emit(key, actual, a);
+          if (cfg.purging) state.erase(KW{key, sw});
+        } else {
+          register_timer(actual.maxTs(), key, actual);
+        }
+        register_cleanup_timer(key, actual);
+      }
+      if (mapping.empty()) merging.erase(key);
+    } else {
+      for (const TW& w : wbuf) {
+        if (is_window_late(w)) continue;
+        skipped = false;
+        KW kw{key, w};
+        Acc& a = state[kw];
+        acc_add(a, val);
+        if (w.maxTs() <= wm) {
+          emit(key, w, a);
+          if (cfg.purging) state.erase(kw);
+        } else {
+          register_timer(w.maxTs(), key, w);
+        }
+        register_cleanup_timer(key, w);
+      }
+    }
+    if (skipped && is_element_late(ts)) {
+      if (cfg.side_output)
+        side.push_back(oracle_side_row{key, ts, val, epoch});
+      else
+        late_dropped++;
+    }
+  }
+
+  // ------------------------------------------------ WindowOperator.onEventTime (:424-469)
+  void on_event_time(const Timer& t) {
+    const int64_t key = t.key;
+    const TW& w = t.w;
+    TW sw = w;
+    std::map<TW, TW>* mapping = nullptr;
+    if (is_merging()) {
+      auto mit = merging.find(key);
+      if (mit == merging.end()) return;
+      auto it = mit->second.find(w);
+      if (it == mit->second.end()) return;
+      sw = it->second;
+      mapping = &mit->second;
+    }
+    KW kw{key, sw};
+    auto it = state.find(kw);
+    if (it != state.end()) {
+      if (t.ts == w.maxTs()) {  // EventTimeTrigger.onEventTime
+        emit(key, w, it->second);
+        if (cfg.purging) state.erase(kw);
+      }
+    }
+    if (t.ts == cleanup_time(w)) {  // isCleanupTime -> clearAllState (:526-538)
+      state.erase(kw);
+      delete_timer(w.maxTs(), key, w);
+      if (mapping) {
+        if (!mapping->erase(w)) throw OpError{OR_ERR_ILLEGAL_STATE};
+        if (mapping->empty()) merging.erase(key);
+      }
+    }
+  }
+
+  // ------------------------------------------------ AbstractStreamOperator.processWatermark (:735-740)
+  void process_watermark(int64_t w) {
+    wm = w;  // HeapInternalTimerService.advanceWatermark (:276-290)
+    while (!timer_q.empty() && timer_q.top().ts <= w) {
+      Timer t = timer_q.top();
+      timer_q.pop();
+      auto it = timer_set.find(t);
+      if (it == timer_set.end()) continue;  // lazily deleted
+      timer_set.erase(it);
+      on_event_time(t);
+    }
+    epoch++;
+  }
+};
+
+}  // namespace
+
+// =========================================================================== C API
+extern "C" {
+
+void* oracle_create(const oracle_cfg* cfg) { return new WindowOperatorOracle(*cfg); }
+void oracle_destroy(void* op) { delete static_cast<WindowOperatorOracle*>(op); }
+
+int oracle_process(void* p, const int64_t* key, const int64_t* ts, const int64_t* val, int64_t n) {
+  auto* op = static_cast<WindowOperatorOracle*>(p);
+  try {
+    for (int64_t i = 0; i < n; i++) op->process_element(key[i], ts[i], val[i]);
+  } catch (const OpError& e) {
+    return e.code;
+  }
+  return OR_OK;
+}
+int oracle_watermark(void* p, int64_t wm) {
+  try {
+    static_cast<WindowOperatorOracle*>(p)->process_watermark(wm);
+  } catch (const OpError& e) {
+    return e.code;
+  }
+  return OR_OK;
+}
+int64_t oracle_num_rows(void* p) { return (int64_t) static_cast<WindowOperatorOracle*>(p)->rows.size(); }
+void oracle_get_rows(void* p, oracle_row* out) {
+  auto* op = static_cast<WindowOperatorOracle*>(p);
+  if (!op->rows.empty()) memcpy(out, op->rows.data(), op->rows.size() * sizeof(oracle_row));
+}
+void oracle_clear_rows(void* p) { static_cast<WindowOperatorOracle*>(p)->rows.clear(); }
+int64_t oracle_num_side_rows(void* p) { return (int64_t) static_cast<WindowOperatorOracle*>(p)->side.size(); }
+void oracle_get_side_rows(void* p, oracle_side_row* out) {
+  auto* op = static_cast<WindowOperatorOracle*>(p);
+  if (!op->side.empty()) memcpy(out, op->side.data(), op->side.size() * sizeof(oracle_side_row));
+}
+int64_t oracle_late_dropped(void* p) { return static_cast<WindowOperatorOracle*>(p)->late_dropped; }
+int64_t oracle_num_state_entries(void* p) { return (int64_t) static_cast<WindowOperatorOracle*>(p)->state.size(); }
+int64_t oracle_num_timers(void* p) { return (int64_t) static_cast<WindowOperatorOracle*>(p)->timer_set.size(); }
+int64_t oracle_current_watermark(void* p) { return static_cast<WindowOperatorOracle*>(p)->wm; }
+
+int32_t oracle_long_hash(int64_t v) { return long_hash(v); }
+int32_t oracle_murmur_hash(int32_t code) { return murmur(code); }
+int32_t oracle_key_group(int32_t h, int32_t max_par) { return murmur(h) % max_par; }
+int32_t oracle_operator_index(int32_t max_par, int32_t par, int32_t kg) { return kg * par / max_par; }
+void oracle_key_group_range(int32_t max_par, int32_t par, int32_t idx, int32_t* s, int32_t* e) {
+  *s = (idx * max_par + par - 1) / par;
+  *e = ((idx + 1) * max_par - 1) / par;
+}
+void oracle_key_groups_long(const int64_t* keys, int64_t n, int32_t max_par, int32_t* out) {
+  for (int64_t i = 0; i < n; i++) out[i] = murmur(long_hash(keys[i])) % max_par;
+}
+int64_t oracle_window_start(int64_t ts, int64_t offset, int64_t size) { return window_start(ts, offset, size); }
+int32_t oracle_string_hash(const char* s, int64_t len) {
+  uint32_t h = 0;
+  for (int64_t i = 0; i < len; i++) h = 31u * h + (uint32_t)(unsigned char)s[i];
+  return (int32_t)h;
+}
+
+int64_t oracle_run_parallel(const oracle_cfg* cfg, const int64_t* key, const int64_t* ts, const int64_t* val,
+                            int64_t n, int64_t batch, const int64_t* wms, int64_t n_wms, int32_t max_par,
+                            int32_t threads, int64_t* late_dropped) {
+  if (threads < 1) threads = 1;
+  // Phase 1 (the upstream KeyGroupStreamPartitioner, KeyGroupStreamPartitioner.java:53-65):
+  // chunk-parallel routing of record indices to subtasks, arrival order kept per subtask.
+  const int64_t chunk = (n + threads - 1) / threads;
+  std::vector<std::vector<std::vector<int64_t>>> routed(threads, std::vector<std::vector<int64_t>>(threads));
+  auto router = [&](int c) {
+    int64_t lo = c * chunk, hi = std::min(n, lo + chunk);
+    for (int64_t i = lo; i < hi; i++) {
+      int32_t kg = murmur(long_hash(key[i])) % max_par;
+      routed[c][kg * threads / max_par].push_back(i);
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int c = 1; c < threads; c++) th.emplace_back(router, c);
+    router(0);
+    for (auto& t : th) t.join();
+  }
+  // Phase 2: one WindowOperator per subtask; watermark after each `batch` input records.
+  std::vector<int64_t> total_rows(threads, 0), total_late(threads, 0);
+  auto worker = [&](int t) {
+    WindowOperatorOracle op(*cfg);
+    int64_t b = 0;  // next watermark index
+    for (int c = 0; c < threads; c++) {
+      for (int64_t i : routed[c][t]) {
+        while (b < n_wms && i >= (b + 1) * batch) {
+          op.process_watermark(wms[b++]);
+          total_rows[t] += (int64_t)op.rows.size();  // discarding sink
+          op.rows.clear();
+        }
+        op.process_element(key[i], ts[i], val[i]);
+      }
+    }
+    for (; b < n_wms; b++) op.process_watermark(wms[b]);
+    total_rows[t] += (int64_t)op.rows.size();
+    total_late[t] = op.late_dropped;
+  };
+  std::vector<std::thread> ts_;
+  for (int t = 1; t < threads; t++) ts_.emplace_back(worker, t);
+  worker(0);
+  for (auto& th : ts_) th.join();
+  int64_t rows = 0, late = 0;
+  for (int t = 0; t < threads; t++) {
+    rows += total_rows[t];
+    late += total_late[t];
+  }
+  if (late_dropped) *late_dropped = late;
+  return rows;
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+/*
+ * window_oracle.h — CPU restatement of Flink's keyed event-time WindowOperator.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity checker ("oracle") for the
+ * MI355X path in flink_amd/.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load it.  The product path never links or
+ * calls anything under oracle/.
+ *
+ * It restates, element by element and with Java arithmetic (two's-complement
+ * wrap, truncating %), the semantics of (paths relative to /root/reference):
+ *   flink-core/src/main/java/org/apache/flink/util/MathUtils.java:134-198         murmurHash, bitMix
+ *   flink-runtime/.../state/KeyGroupRangeAssignment.java:47-135                    key groups / operator index
+ *   flink-streaming-java/.../api/windowing/windows/TimeWindow.java:83-256         maxTimestamp, intersects, cover,
+ *                                                                                  mergeWindows, getWindowStartWithOffset
+ *   .../api/windowing/assigners/TumblingEventTimeWindows.java:63-73               tumbling assignment
+ *   .../api/windowing/assigners/SlidingEventTimeWindows.java:67-81                sliding assignment
+ *   .../api/windowing/assigners/EventTimeSessionWindows.java:59-61                session assignment
+ *   .../api/windowing/triggers/EventTimeTrigger.java:37-73, PurgingTrigger.java    trigger results
+ *   .../runtime/operators/windowing/WindowOperator.java:291-651                   processElement/onEventTime/lateness
+ *   .../runtime/operators/windowing/MergingWindowSet.java:81-225                  addWindow / retireWindow
+ *   .../api/operators/HeapInternalTimerService.java:224-290                       timer dedup + advanceWatermark
+ *   flink-runtime/.../state/heap/AbstractHeapMergingState.java:67-93              mergeNamespaces
+ *
+ * Aggregation: the build's built-in AggregateFunction "CountSumMinMax" over a
+ * value column (i64, i32 with 32-bit wrap of the sum, or f64 with
+ * Double.compare ordering for min/max and canonical NaN), i.e. the accumulator
+ * {count, sum, min, max} — see DESIGN.md §"Aggregates".
+ */
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { OR_TUMBLING = 0, OR_SLIDING = 1, OR_SESSION = 2 };
+enum { OR_VAL_I64 = 0, OR_VAL_I32 = 1, OR_VAL_F64 = 2 };
+
+/* error codes returned by oracle_process / oracle_watermark */
+enum {
+  OR_OK = 0,
+  OR_ERR_NO_TIMESTAMP = -1,   /* Long.MIN_VALUE timestamp: TumblingEventTimeWindows.java:69-71 */
+  OR_ERR_MERGE_LATE = -2,     /* UnsupportedOperationException, WindowOperator.java:313-317 */
+  OR_ERR_ILLEGAL_STATE = -3,  /* IllegalStateException, MergingWindowSet.java:127 / WindowOperator.java:355 */
+};
+
+typedef struct {
+  int32_t assigner;      /* OR_TUMBLING / OR_SLIDING / OR_SESSION */
+  int32_t value_type;    /* OR_VAL_* */
+  int64_t size;          /* tumbling/sliding window size */
+  int64_t slide;         /* sliding slide */
+  int64_t offset;        /* tumbling/sliding offset */
+  int64_t gap;           /* session gap */
+  int64_t lateness;      /* allowedLateness */
+  int32_t purging;       /* PurgingTrigger.of(EventTimeTrigger) */
+  int32_t side_output;   /* late records go to the side output instead of numLateRecordsDropped */
+} oracle_cfg;
+
+/* One fired row.  sum/min/max hold i64 values (I64/I32) or f64 bit patterns (F64).
+ * epoch = number of watermarks fully processed before the row was emitted, so
+ * every row preceding the k-th output watermark has epoch k (TestHarnessUtil
+ * compares watermark positions exactly and records sorted in between). */
+typedef struct {
+  int64_t key, start, end, count, sum, min, max, epoch;
+} oracle_row;
+
+typedef struct {
+  int64_t key, ts, val, epoch;
+} oracle_side_row;
+
+void*   oracle_create(const oracle_cfg* cfg);
+void    oracle_destroy(void* op);
+/* process n elements in order; val holds i64 values or f64 bits */
+int     oracle_process(void* op, const int64_t* key, const int64_t* ts, const int64_t* val, int64_t n);
+int     oracle_watermark(void* op, int64_t wm);
+int64_t oracle_num_rows(void* op);
+void    oracle_get_rows(void* op, oracle_row* out);       /* copies all rows emitted so far */
+void    oracle_clear_rows(void* op);
+int64_t oracle_num_side_rows(void* op);
+void    oracle_get_side_rows(void* op, oracle_side_row* out);
+int64_t oracle_late_dropped(void* op);
+int64_t oracle_num_state_entries(void* op);  /* ≙ numKeyedStateEntries (window-contents) */
+int64_t oracle_num_timers(void* op);         /* ≙ numEventTimeTimers */
+int64_t oracle_current_watermark(void* op);
+
+/* Java hashing / key-group restatement (MathUtils.java:134-198, KeyGroupRangeAssignment.java:47-135) */
+int32_t oracle_long_hash(int64_t v);              /* Long.hashCode */
+int32_t oracle_murmur_hash(int32_t code);         /* MathUtils.murmurHash */
+int32_t oracle_key_group(int32_t key_hash, int32_t max_parallelism);
+int32_t oracle_operator_index(int32_t max_par, int32_t par, int32_t key_group);
+void    oracle_key_group_range(int32_t max_par, int32_t par, int32_t op_index, int32_t* start, int32_t* end);
+void    oracle_key_groups_long(const int64_t* keys, int64_t n, int32_t max_par, int32_t* out);
+int64_t oracle_window_start(int64_t ts, int64_t offset, int64_t size);
+int32_t oracle_string_hash(const char* s, int64_t len);  /* String.hashCode over UTF-16 units (ASCII input) */
+
+/* Multi-threaded CPU baseline: p subtasks, each a WindowOperator over its KeyGroupRange
+ * (computeKeyGroupRangeForOperatorIndex), fed the records routed to it (murmur key groups),
+ * with a watermark after every `batch` records (wms[b]) and a final watermark if given.
+ * Returns total fired rows; *late_dropped gets the sum over subtasks. */
+int64_t oracle_run_parallel(const oracle_cfg* cfg, const int64_t* key, const int64_t* ts,
+                            const int64_t* val, int64_t n, int64_t batch, const int64_t* wms,
+                            int64_t n_wms, int32_t max_par, int32_t threads, int64_t* late_dropped);
+
+#ifdef __cplusplus
+}
+#endif

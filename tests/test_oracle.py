@@ -1,0 +1,124 @@
+"""Pins the CPU oracle (oracle/) against the reference's own known-answer tests
+(tests/golden/reference_kats.json, transcribed with provenance by tests/golden/make_golden.py)."""
+from collections import Counter
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests.kat_util import expected_counters, load_kats, replay, row_counters
+
+KATS = load_kats()
+KEYMAP = KATS["keys"]
+
+
+def _make_oracle(cfg):
+    return orc.WindowOperatorOracle(assigner=cfg["assigner"], size=cfg["size"], slide=cfg["slide"],
+                                    offset=cfg["offset"], gap=cfg["gap"], lateness=cfg["lateness"],
+                                    purging=cfg["purging"], side_output=cfg["side_output"],
+                                    value_type=cfg["value_type"])
+
+
+@pytest.mark.parametrize("case", KATS["operator_cases"], ids=[c["name"] for c in KATS["operator_cases"]])
+def test_window_operator_kats(case):
+    op = replay(case, KEYMAP, _make_oracle, flush_elements=False)
+    got, got_side = row_counters(op.rows(), op.side_rows(), case, with_window=True)
+    exp, exp_side = expected_counters(case, KEYMAP, with_window=True)
+    assert got == exp
+    assert got_side == exp_side
+    if not case["cfg"]["side_output"]:
+        # elements the KAT sends to a side output are counted as dropped when no tag is set
+        assert op.late_dropped == 0 or case["expected_side"] == []
+
+
+def test_key_group_kats():
+    kg = KATS["key_groups"]
+    L = orc.lib()
+    for key, group in kg["key_group"]:
+        # Integer.hashCode() == value
+        assert L.oracle_key_group(key, kg["max_parallelism"]) == group
+    for max_par, par, group, idx in kg["operator_index"]:
+        assert L.oracle_operator_index(max_par, par, group) == idx
+
+
+def test_window_start_kats():
+    L = orc.lib()
+    for ts, off, size, exp in KATS["window_start"]["cases"]:
+        assert L.oracle_window_start(ts, off, size) == exp
+
+
+def test_assigner_kats():
+    for kind, size, slide, offset, ts, wins in KATS["assigners"]["cases"]:
+        # assignment observed through the operator: one element, then a final watermark
+        op = orc.WindowOperatorOracle(assigner=kind, size=size, slide=slide, offset=offset)
+        op.process(np.array([1]), np.array([ts]), np.array([7]))
+        op.watermark((1 << 63) - 1)
+        rows = op.rows()
+        got = sorted((int(r["start"]), int(r["end"])) for r in rows)
+        assert got == sorted(tuple(w) for w in wins)
+        assert all(r["count"] == 1 and r["sum"] == 7 for r in rows)
+
+
+def test_session_example_kat():
+    ex = KATS["session_example"]
+    names = sorted({r[0] for r in ex["input"]})
+    ids = {n: i for i, n in enumerate(names)}
+    op = orc.WindowOperatorOracle(assigner="session", gap=ex["gap"], value_type="i32")
+    for name, ts, val in ex["input"]:
+        op.process(np.array([ids[name]]), np.array([ts]), np.array([val]))
+        op.watermark(ts - 1)
+    op.watermark((1 << 63) - 1)
+    got = Counter((names[int(r["key"])], int(r["start"]), int(r["sum"])) for r in op.rows())
+    assert got == Counter(tuple(e) for e in ex["expected"])
+
+
+def _closed_form_stream(num_keys, n_per_key):
+    keys, ts, vals, wms = [], [], [], []
+    for nxt in range(n_per_key):
+        for k in range(num_keys):
+            keys.append(k)
+            ts.append(nxt)
+            vals.append(nxt)
+        wms.append(nxt)
+    return (np.array(keys, dtype=np.int64), np.array(ts, dtype=np.int64), np.array(vals, dtype=np.int64),
+            wms)
+
+
+@pytest.mark.parametrize("slide", [100, 50])
+def test_closed_form_validator(slide):
+    cf = KATS["closed_form"]
+    nk, npk, size = cf["num_keys"], cf["num_elements_per_key"], cf["window_size"]
+    keys, ts, vals, wms = _closed_form_stream(nk, npk)
+    assigner = "tumbling" if slide == size else "sliding"
+    op = orc.WindowOperatorOracle(assigner=assigner, size=size, slide=slide, value_type="i32")
+    for i, wm in enumerate(wms):
+        sl = slice(i * nk, (i + 1) * nk)
+        op.process(keys[sl], ts[sl], vals[sl])
+        op.watermark(wm)
+    op.watermark((1 << 63) - 1)
+    rows = op.rows()
+    per_key = Counter()
+    for r in rows:
+        # closed form of EWC:713-719; windows past the last element (only with slide < size) are partial
+        exp = sum(i for i in range(int(r["start"]), min(int(r["end"]), npk)) if i > 0)
+        assert int(r["sum"]) == exp
+        per_key[int(r["key"])] += 1
+    # ValidatingSink: numElementsPerKey / windowSlide windows per key (full windows only, EWC:683);
+    # sliding adds the (size/slide - 1) trailing partial windows that close at the final watermark.
+    expected_windows = npk // slide + (size // slide - 1)
+    assert set(per_key.values()) == {expected_windows}
+
+
+def test_string_hash_matches_java():
+    L = orc.lib()
+    # "hello".hashCode() == 99162322 (JLS String.hashCode definition)
+    assert L.oracle_string_hash(b"hello", 5) == 99162322
+    assert L.oracle_string_hash(b"", 0) == 0
+
+
+def test_long_hash_java():
+    L = orc.lib()
+    assert L.oracle_long_hash(0) == 0
+    assert L.oracle_long_hash(-1) == 0
+    assert L.oracle_long_hash(1 << 32) == 1
+    assert L.oracle_long_hash(123456789) == 123456789
