@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Benchmark of the keyed event-time window aggregation path (BASELINE.json metric:
+"records/sec keyed windowed aggregation at 1/2/4/8 GPUs; % of HBM roofline").
+
+Workload (BASELINE.json configs[1]): 1 s tumbling event-time windows, 1M uniform
+Long keys, built-in count/sum/min/max AggregateFunction, bounded out-of-orderness watermarks (200 ms,
+punctuated after every batch), synthetic counter-based stream at 1e8 records per event-second.
+One step = one micro-batch of `--batch` records per GPU pushed through the operator plus the
+watermark that follows it (every window whose end passed fires).  Inputs are generated into HBM
+before the timed region.  With N > 1 (torchrun, one process per GPU over RCCL) each rank owns the
+KeyGroupRange computeKeyGroupRangeForOperatorIndex(128, N, rank), generates `--batch` records of the
+global stream per step and the keyBy exchange (route + RCCL all_to_all) and the watermark min
+(all_reduce) run inside the timed region: weak scaling.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md §Chip-level parameters
+
+
+def kernel_bytes(name, n, merged, live_slots_scanned=0):
+    """Algorithmic bytes of one launch."""
+    if name == "k_classify_hist":
+        return 16 * n                      # key + ts
+    if name == "k_scatter":
+        return 24 * n + 24 * n             # read key/ts/val, write the partitioned copy
+    if name == "k_aggregate":
+        return 24 * n + 128 * merged       # read the partitioned records, RMW one 64-B entry per delta
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--batch", type=int, default=1 << 24)
+    ap.add_argument("--keys", type=int, default=1_000_000)
+    ap.add_argument("--rate", type=int, default=100_000_000, help="records per event-second (whole job)")
+    ap.add_argument("--bound", type=int, default=200, help="out-of-orderness bound (ms)")
+    ap.add_argument("--jitter", type=int, default=200)
+    ap.add_argument("--window", type=int, default=1000)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 24)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from flink_amd import TumblingEventTimeWindows
+    from flink_amd import _native as N
+    from flink_amd.datagen import generate_device
+    from flink_amd.exchange import KeyGroupExchange
+    from flink_amd.operator import GpuWindowOperator
+
+    max_par = 128
+    exch = KeyGroupExchange(max_par, world, rank)
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(args.window), key_group_range=exch.key_group_range,
+                           device=local_rank, max_parallelism=max_par,
+                           expected_entries=2 * args.keys // world,
+                           max_batch=args.batch if world == 1 else 2 * args.batch)
+    steps_total = args.warmup + args.steps
+    seed = 0x5EED
+    batches, local_max = [], []
+    for s in range(steps_total):
+        first = (s * world + rank) * args.batch  # global record index of this rank's slice of step s
+        k, t, v, mx = generate_device(seed, first, args.batch, args.keys, ts_base=0, rate=args.rate,
+                                      jitter=args.jitter, device=local_rank)
+        batches.append((k, t, v))
+        local_max.append(mx)
+    torch.cuda.synchronize()
+    # punctuated watermark of this rank's source after each batch: max ts so far - bound
+    local_wm = []
+    m = -(1 << 63)
+    for mx in local_max:
+        m = max(m, int(mx.item()))
+        local_wm.append(m - args.bound)
+
+    def step(s):
+        k, t, v = batches[s]
+        wm = local_wm[s]
+        if world > 1:
+            k, t, v = exch.exchange(k, t, v)
+            wm = exch.combine_watermark(wm, device=dev)
+        op.process_batch(k, t, v)
+        op.advance_watermark(wm)
+        op.clear_pending()  # discarding sink: fired rows were materialised in HBM
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    for s in range(args.warmup):
+        step(s)
+    L = N.lib()
+    if not args.no_profile:
+        L.fw_profile(op._h, 1)
+        L.fw_profile_read(op._h, None, None, 1)
+    st0 = op.stats()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.warmup, steps_total):
+        step(s)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    st1 = op.stats()
+
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    records = args.batch * world * args.steps
+    value = records / elapsed
+    fired = st1["fired_rows_total"] - st0["fired_rows_total"]
+
+    roofline = None
+    kernels = {}
+    if not args.no_profile:
+        import ctypes
+        ms = (ctypes.c_double * N.FW_NUM_KERNELS)()
+        nl = (ctypes.c_int64 * N.FW_NUM_KERNELS)()
+        L.fw_profile_read(op._h, ms, nl, 1)
+        merged = st1["state_merges"] - st0["state_merges"]
+        for i in range(N.FW_NUM_KERNELS):
+            name = L.fw_kernel_name(i).decode()
+            if nl[i]:
+                kernels[name] = {"launches": int(nl[i]), "avg_ms": ms[i] / nl[i], "total_ms": ms[i]}
+        dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
+        per_launch_records = records / world / args.steps
+        b = kernel_bytes(dom, per_launch_records, merged / args.steps)
+        traffic = None
+        if os.path.exists(args.traffic):
+            with open(args.traffic) as f:
+                tr = json.load(f)
+            traffic = tr.get("per_launch_bytes", {}).get(dom)
+        if b is not None:
+            achieved = b / (kernels[dom]["avg_ms"] * 1e-3) / 1e9
+            roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                        "traffic": traffic, "alg_bytes_per_launch": int(b)}
+    # whole-path roofline with SURVEY §8d's B_alg for C2: 24 + 104 F/N bytes per record
+    b_alg = 24 + 104 * fired / max(1, records / world)
+    path_frac = value * b_alg / (world * HBM_PEAK_GBS * 1e9)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        line = {
+            "metric": "records/sec keyed windowed aggregation at 1/2/4/8 GPUs; % of HBM roofline",
+            "value": round(value, 1), "unit": "records/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic (splitmix64 counter stream)",
+            "config": {"workload": "C2 tumbling 1s event-time window, count/sum/min/max, 1M uniform Long keys, "
+                                   "bounded out-of-orderness 200 ms",
+                       "records_per_step_per_gpu": args.batch, "keys": args.keys, "window_ms": args.window,
+                       "records_per_event_second": args.rate, "watermark_bound_ms": args.bound,
+                       "max_parallelism": 128, "parallelism": f"keygroup{world}"},
+            "roofline": roofline,
+            "path_roofline": {"b_alg_bytes_per_record": round(b_alg, 3), "frac": round(path_frac, 4),
+                              "fired_rows": int(fired)},
+            "cpu_baseline": cpu,
+            "kernels": kernels,
+        }
+        print(json.dumps(line), flush=True)
+    op.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args):
+    """CPU restatement of WindowOperator (oracle/, kind "port"): p threads = p subtasks over their
+    KeyGroupRanges, the same generator and punctuated watermarks, on a bounded sample."""
+    import numpy as np
+    from flink_amd.datagen import generate_host
+    from oracle import oracle as orc
+    n = args.cpu_sample
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    k, t, v = generate_host(0x5EED, 0, n, args.keys, ts_base=0, rate=args.rate, jitter=args.jitter)
+    batch = min(args.batch, n)
+    wms, m = [], -(1 << 63)
+    for b in range(0, n, batch):
+        m = max(m, int(t[b:b + batch].max()))
+        wms.append(m - args.bound)
+    t0 = time.perf_counter()
+    orc.run_parallel(dict(assigner="tumbling", size=args.window), k, t, v, batch, np.array(wms), 128, threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 1), "unit": "records/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} records of the same C2 stream, {threads} subtasks (threads), watermark every "
+                      f"{batch} records; CPU restatement of WindowOperator semantics (oracle/), not the Java "
+                      f"reference (no JDK on the box)"}
+
+
+if __name__ == "__main__":
+    main()

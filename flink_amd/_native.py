@@ -1,0 +1,109 @@
+"""ctypes binding of include/flink_window.h (libflinkwin.so, built for gfx950 by
+flink_amd/csrc/Makefile).  There is no fallback: if the library is missing the import fails."""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libflinkwin.so")
+CSRC = os.path.join(_HERE, "csrc")
+
+FW_OK = 0
+FW_ERR_ARG = -1
+FW_ERR_HIP = -2
+FW_ERR_NO_TIMESTAMP = -3
+FW_ERR_KEY_GROUP = -4
+FW_ERR_CAPACITY = -5
+FW_ERR_UNSUPPORTED = -6
+FW_ERR_STATE = -7
+
+FW_TUMBLING, FW_SLIDING, FW_SESSION = 0, 1, 2
+FW_VAL_I64, FW_VAL_I32, FW_VAL_F64 = 0, 1, 2
+FW_KEY_LONG, FW_KEY_INT, FW_KEY_HASHED = 0, 1, 2
+FW_NUM_KERNELS = 6
+
+I64P = ctypes.POINTER(ctypes.c_int64)
+I32P = ctypes.POINTER(ctypes.c_int32)
+VP = ctypes.c_void_p
+
+
+class FwConfig(ctypes.Structure):
+    _fields_ = [("assigner", ctypes.c_int32), ("value_type", ctypes.c_int32), ("key_kind", ctypes.c_int32),
+                ("purging", ctypes.c_int32), ("side_output", ctypes.c_int32), ("max_parallelism", ctypes.c_int32),
+                ("key_group_start", ctypes.c_int32), ("key_group_end", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("sub_partitions", ctypes.c_int32), ("size", ctypes.c_int64), ("slide", ctypes.c_int64),
+                ("offset", ctypes.c_int64), ("gap", ctypes.c_int64), ("allowed_lateness", ctypes.c_int64),
+                ("expected_entries", ctypes.c_int64), ("max_batch", ctypes.c_int64)]
+
+
+class FwRows(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("key", "start", "end", "count", "sum", "min", "max")]
+
+
+class FwSideRows(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("key", "ts", "val")]
+
+
+class FwStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in (
+        "records_in", "late_records_dropped", "keyed_state_entries", "event_time_timers", "current_watermark",
+        "fired_rows_total", "pending_rows", "pending_side_rows", "table_capacity", "table_grows",
+        "slow_path_records", "state_merges")]
+
+
+# every exported symbol with its ctypes signature (restype, argtypes); mirrors include/flink_window.h
+SIGNATURES = {
+    "fw_create": (ctypes.c_int, [ctypes.POINTER(FwConfig), ctypes.POINTER(VP)]),
+    "fw_destroy": (None, [VP]),
+    "fw_last_error": (ctypes.c_char_p, [VP]),
+    "fw_push_batch": (ctypes.c_int, [VP, VP, VP, VP, VP, ctypes.c_int64]),
+    "fw_push_batch_device": (ctypes.c_int, [VP, VP, VP, VP, VP, ctypes.c_int64]),
+    "fw_advance_watermark": (ctypes.c_int, [VP, ctypes.c_int64, I64P]),
+    "fw_pending": (ctypes.c_int, [VP, I64P, I64P]),
+    "fw_drain_rows": (ctypes.c_int, [VP, ctypes.POINTER(FwRows), ctypes.c_int64, I64P]),
+    "fw_drain_side": (ctypes.c_int, [VP, ctypes.POINTER(FwSideRows), ctypes.c_int64, I64P]),
+    "fw_rows_device": (ctypes.c_int, [VP, ctypes.POINTER(FwRows), I64P]),
+    "fw_clear_pending": (ctypes.c_int, [VP]),
+    "fw_get_stats": (ctypes.c_int, [VP, ctypes.POINTER(FwStats)]),
+    "fw_synchronize": (ctypes.c_int, [VP]),
+    "fw_profile": (ctypes.c_int, [VP, ctypes.c_int]),
+    "fw_profile_read": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_double), I64P, ctypes.c_int]),
+    "fw_kernel_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "fw_stream": (VP, [VP]),
+    "fw_key_groups_device": (ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, VP, VP]),
+    "fw_route_device": (ctypes.c_int, [VP, VP, VP, VP, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
+                                       ctypes.c_int32, VP, VP, VP, VP, VP, VP, ctypes.c_int64, VP]),
+    "fw_route_scratch_bytes": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
+    "fw_generate_device": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, VP,
+                                          ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, VP, VP, VP, VP, VP]),
+}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def lib():
+    """Load libflinkwin.so.  Raises if it was not built — the GPU path has no CPU fallback."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `make -C {CSRC}` "
+                              "(or __graft_entry__.build()); flink_amd has no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, handle=None):
+    if rc != FW_OK:
+        msg = lib().fw_last_error(handle).decode() if handle else "error"
+        raise NativeError(rc, msg)
+    return rc

@@ -1,0 +1,1224 @@
+// fw_device.hip — HIP kernels (gfx950) of the MI355X keyed event-time window operator.
+//
+// Per micro-batch (fw_push_*), with the watermark wm constant over the batch:
+//   k_classify_hist  — KeyGroupRangeAssignment murmur hash -> state partition, window assignment
+//                      and lateness class of every record; per-tile partition histogram.
+//   k_scan_*         — exclusive scan of the (partition, tile) histogram.
+//   k_scatter        — records of the order-independent class ("normal": every window of the
+//                      record ends after wm) scattered into per-partition runs; records that need
+//                      arrival order (late firing, partially late, sessions) compacted in order
+//                      into the ordered list; fully late records to the side output / counter.
+//   k_aggregate      — one workgroup per state partition: LDS open-addressing pre-aggregation of
+//                      the partition's (key, window) accumulators (64-bit LDS atomics), flushed
+//                      into the partition's HBM region with plain read-modify-write (the region
+//                      is owned by exactly one workgroup, so no global atomics on the data).
+//   k_slow           — ordered replay of the ordered list, one thread per key, element by element
+//                      exactly as WindowOperator.processElement (WindowOperator.java:291-421),
+//                      including MergingWindowSet.addWindow for sessions.
+// Per watermark (fw_advance_watermark):
+//   k_fire           — HeapInternalTimerService.advanceWatermark as a scan/compaction: every region
+//                      whose earliest timer is <= wm emits its fired windows and is rebuilt, without
+//                      the cleaned-up entries, into the region's other buffer.
+#include <hip/hip_runtime.h>
+
+#include "../../include/flink_window.h"
+#include "fw_internal.h"
+
+namespace {
+
+constexpr int64_t LMAX = INT64_MAX;
+constexpr int64_t LMIN = INT64_MIN;
+
+// ------------------------------------------------------------------ Java arithmetic
+__device__ __forceinline__ int64_t jadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+__device__ __forceinline__ int64_t jsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+// flink-core/src/main/java/org/apache/flink/util/MathUtils.java:191-198
+__device__ __forceinline__ int32_t bit_mix(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return (int32_t)x;
+}
+// MathUtils.java:134-154
+__device__ __forceinline__ int32_t murmur(int32_t code) {
+  uint32_t c = (uint32_t)code;
+  c *= 0xcc9e2d51u;
+  c = rotl32(c, 15);
+  c *= 0x1b873593u;
+  c = rotl32(c, 13);
+  c = c * 5u + 0xe6546b64u;
+  c ^= 4u;
+  int32_t r = bit_mix(c);
+  return r >= 0 ? r : (r != INT32_MIN ? -r : 0);
+}
+__device__ __forceinline__ uint64_t fmix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+__device__ __forceinline__ int32_t key_hash_of(int32_t kind, int64_t key, const int32_t* kh, int64_t i) {
+  if (kind == FW_KEY_HASHED) return kh[i];
+  if (kind == FW_KEY_INT) return (int32_t)key;
+  return (int32_t)(key ^ (int64_t)((uint64_t)key >> 32));  // Long.hashCode
+}
+// KeyGroupRangeAssignment.computeKeyGroupForKeyHash (KeyGroupRangeAssignment.java:69-71)
+__device__ __forceinline__ int32_t key_group(int32_t h, int32_t max_par) { return murmur(h) % max_par; }
+// state partition of a key inside the handle's KeyGroupRange, -1 when outside it
+__device__ __forceinline__ int32_t partition_of(const DevCfg& c, int64_t key, int32_t h) {
+  int32_t local = key_group(h, c.max_par) - c.kg0;
+  if ((uint32_t)local >= (uint32_t)c.n_kg) return -1;
+  uint32_t sub = c.log_s ? (uint32_t)(fmix64((uint64_t)key ^ 0x5851F42D4C957F2Dull) >> (64 - c.log_s)) : 0u;
+  return (local << c.log_s) | (int32_t)sub;
+}
+
+// TimeWindow.getWindowStartWithOffset (TimeWindow.java:254-256), Java overflow semantics
+__device__ __forceinline__ int64_t wstart(int64_t ts, int64_t off, int64_t size) {
+  int64_t t = jadd(jsub(ts, off), size);
+  return jsub(ts, t % size);
+}
+// WindowOperator.cleanupTime (WindowOperator.java:637-644) of window [., end)
+__device__ __forceinline__ int64_t cleanup_of(int64_t end, int64_t lateness) {
+  int64_t mx = jsub(end, 1);
+  int64_t c = jadd(mx, lateness);
+  return c >= mx ? c : LMAX;
+}
+// earliest pending timer of an entry: trigger timer at maxTimestamp if registered, else GC timer
+__device__ __forceinline__ int64_t timer_of(const Entry& e, int64_t lateness) {
+  return (e.meta & FW_TIMER) ? jsub(e.end, 1) : cleanup_of(e.end, lateness);
+}
+
+// Double.compare order as a signed 64-bit key (canonical NaN, Double.doubleToLongBits)
+__device__ __forceinline__ int64_t f64_sortable(int64_t bits) {
+  if ((bits & 0x7ff0000000000000ll) == 0x7ff0000000000000ll && (bits & 0x000fffffffffffffll)) bits = 0x7ff8000000000000ll;
+  return bits >= 0 ? bits : (bits ^ 0x7fffffffffffffffll);
+}
+__device__ __forceinline__ int64_t f64_unsortable(int64_t s) { return s >= 0 ? s : (s ^ 0x7fffffffffffffffll); }
+
+// ------------------------------------------------------------------ record classes
+enum { CLS_NORMAL = 0, CLS_SLOW = 1, CLS_LATE = 2, CLS_SKIP = 3, CLS_BADTS = 4 };
+
+// Windows of a record, newest first (SlidingEventTimeWindows.java:71-75 loop order).
+__device__ __forceinline__ int num_windows(const DevCfg& c, int64_t ts, int64_t* last_start) {
+  if (c.assigner == FW_TUMBLING) {
+    *last_start = wstart(ts, c.offset, c.size);
+    return 1;
+  }
+  int64_t last = wstart(ts, c.offset, c.slide);
+  *last_start = last;
+  int k = 0;
+  const int64_t lo = jsub(ts, c.size);
+  for (int64_t s = last; s > lo && k <= c.wpr; s = jsub(s, c.slide)) k++;
+  return k;
+}
+
+__device__ __forceinline__ int classify(const DevCfg& c, int64_t wm, int64_t ts) {
+  if (c.assigner == FW_SESSION) return CLS_SLOW;
+  if (ts == LMIN) return CLS_BADTS;  // TumblingEventTimeWindows.java:69-71
+  int64_t last;
+  int k = num_windows(c, ts, &last);
+  if (k == 0) return jadd(ts, c.lateness) <= wm ? CLS_LATE : CLS_SKIP;
+  const int64_t newest_end = jadd(last, c.size);
+  const int64_t oldest_end = jadd(jsub(last, (int64_t)(k - 1) * c.slide), c.size);
+  if (jsub(oldest_end, 1) > wm) return CLS_NORMAL;  // every window: maxTimestamp > wm
+  if (cleanup_of(newest_end, c.lateness) <= wm)     // every window late (isWindowLate)
+    return jadd(ts, c.lateness) <= wm ? CLS_LATE : CLS_SKIP;  // isElementLate
+  return CLS_SLOW;
+}
+
+__device__ __forceinline__ uint32_t slot_hash(const DevCfg& c, int64_t key, int64_t start) {
+  uint64_t h = (uint64_t)key * 0x9E3779B97F4A7C15ull;
+  if (c.assigner != FW_SESSION) h ^= fmix64((uint64_t)start + 0x632BE59BD9B4E019ull);
+  return (uint32_t)fmix64(h);
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const uint32_t lane = __lane_id();
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+__device__ __forceinline__ uint32_t ld_state(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------ output
+__device__ __forceinline__ void write_row(const DevCfg& c, const DevRows& out, unsigned long long pos, const Entry& e) {
+  out.key[pos] = e.key;
+  out.start[pos] = e.start;
+  out.end[pos] = e.end;
+  out.cnt[pos] = e.cnt;
+  if (c.vtype == FW_VAL_F64) {
+    out.sum[pos] = e.sum;
+    out.mn[pos] = f64_unsortable(e.mn);
+    out.mx[pos] = f64_unsortable(e.mx);
+  } else {
+    out.sum[pos] = c.vtype == FW_VAL_I32 ? (int64_t)(int32_t)e.sum : e.sum;
+    out.mn[pos] = e.mn;
+    out.mx[pos] = e.mx;
+  }
+}
+// single-lane emission (ordered path)
+__device__ __forceinline__ void emit_one(const DevCfg& c, const DevRows& out, Status* st, const Entry& e) {
+  unsigned long long pos = atomicAdd(&st->out_rows, 1ull);
+  if ((int64_t)pos < out.cap)
+    write_row(c, out, pos, e);
+  else
+    atomicOr(&st->flags, FW_STATUS_OUT_FULL);
+}
+__device__ __forceinline__ void side_one(const DevSide& sd, Status* st, int64_t k, int64_t t, int64_t v) {
+  unsigned long long pos = atomicAdd(&st->side_rows, 1ull);
+  if ((int64_t)pos < sd.cap) {
+    sd.key[pos] = k;
+    sd.ts[pos] = t;
+    sd.val[pos] = v;
+  } else {
+    atomicOr(&st->flags, FW_STATUS_SIDE_FULL);
+  }
+}
+
+// accumulate one value (AggregateFunction.add of the built-in count/sum/min/max)
+__device__ __forceinline__ void acc_add(const DevCfg& c, Entry& e, int64_t v) {
+  e.cnt += 1;
+  if (c.vtype == FW_VAL_F64) {
+    double s = __longlong_as_double(e.sum) + __longlong_as_double(v);
+    e.sum = __double_as_longlong(s);
+    int64_t sv = f64_sortable(v);
+    e.mn = sv < e.mn ? sv : e.mn;
+    e.mx = sv > e.mx ? sv : e.mx;
+  } else {
+    e.sum = jadd(e.sum, v);
+    e.mn = v < e.mn ? v : e.mn;
+    e.mx = v > e.mx ? v : e.mx;
+  }
+}
+// AggregateFunction.merge
+__device__ __forceinline__ void acc_merge(const DevCfg& c, Entry& a, const Entry& b) {
+  if (b.cnt == 0) return;
+  a.cnt += b.cnt;
+  if (c.vtype == FW_VAL_F64)
+    a.sum = __double_as_longlong(__longlong_as_double(a.sum) + __longlong_as_double(b.sum));
+  else
+    a.sum = jadd(a.sum, b.sum);
+  a.mn = b.mn < a.mn ? b.mn : a.mn;
+  a.mx = b.mx > a.mx ? b.mx : a.mx;
+}
+__device__ __forceinline__ void acc_clear(Entry& e) {
+  e.cnt = 0;
+  e.sum = 0;
+  e.mn = LMAX;
+  e.mx = LMIN;
+}
+
+// ------------------------------------------------------------------ HBM regions
+struct Region {
+  Entry* ent;
+  uint32_t* state;
+  uint32_t mask;
+};
+__device__ __forceinline__ Region region_of(const DevCfg& c, const DevTable& tb, int32_t p, int which) {
+  const int64_t base = (int64_t)p << c.log_r;
+  Region r;
+  r.ent = tb.ent[which] + base;
+  r.state = tb.state[which] + base;
+  r.mask = (1u << c.log_r) - 1u;
+  return r;
+}
+// find the live slot of (key, start, end), -1 if absent (linear probing up to the first EMPTY)
+__device__ __forceinline__ int32_t region_find(const Region& r, uint32_t h, int64_t key, int64_t start, int64_t end) {
+  for (uint32_t i = 0; i <= r.mask; i++) {
+    const uint32_t s = (h + i) & r.mask;
+    const uint32_t st = ld_state(r.state + s);
+    if (st == SLOT_EMPTY) return -1;
+    if (st == SLOT_LIVE) {
+      const Entry& e = r.ent[s];
+      if (e.key == key && e.start == start && e.end == end) return (int32_t)s;
+    }
+  }
+  return -1;
+}
+// claim the first EMPTY slot of the probe sequence (state -> `to`), -1 if the region is full
+__device__ __forceinline__ int32_t region_claim(const Region& r, uint32_t h, uint32_t to) {
+  for (uint32_t i = 0; i <= r.mask; i++) {
+    const uint32_t s = (h + i) & r.mask;
+    if (ld_state(r.state + s) != SLOT_EMPTY) continue;
+    if (atomicCAS(r.state + s, SLOT_EMPTY, to) == SLOT_EMPTY) return (int32_t)s;
+  }
+  return -1;
+}
+__device__ __forceinline__ void publish_live(uint32_t* st) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // entry bytes before the LIVE state word
+  __hip_atomic_store(st, SLOT_LIVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ============================================================================== kernels
+
+// ---- K1: classify + partition histogram.  hist is (P+1) x T, partition-major; row P counts
+// the records of each tile that go to the ordered path.
+__global__ __launch_bounds__(FW_TILE_THREADS) void k_classify_hist(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
+                                                                   const int64_t* __restrict__ ts,
+                                                                   const int32_t* __restrict__ kh, int64_t n, int32_t T,
+                                                                   uint32_t* __restrict__ hist, Status* st) {
+  extern __shared__ uint32_t lh[];
+  for (int i = threadIdx.x; i <= c.P; i += blockDim.x) lh[i] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * FW_TILE;
+  const int64_t end = min(n, base + (int64_t)FW_TILE);
+  int bad_kg = 0, bad_ts = 0;
+  unsigned slow = 0;
+  for (int64_t i = base + threadIdx.x; i < end; i += blockDim.x) {
+    const int64_t k = key[i];
+    const int32_t p = partition_of(c, k, key_hash_of(c.key_kind, k, kh, i));
+    if (p < 0) {
+      bad_kg++;
+      continue;
+    }
+    const int cls = classify(c, wm, ts[i]);
+    if (cls == CLS_NORMAL)
+      atomicAdd(&lh[p], 1u);
+    else if (cls == CLS_SLOW)
+      slow++;
+    else if (cls == CLS_BADTS)
+      bad_ts++;
+  }
+  if (slow) atomicAdd(&lh[c.P], slow);
+  __syncthreads();
+  for (int i = threadIdx.x; i <= c.P; i += blockDim.x) hist[(int64_t)i * T + blockIdx.x] = lh[i];
+  if (threadIdx.x == 0 && lh[c.P]) atomicAdd(&st->slow_count, (unsigned long long)lh[c.P]);
+  if (bad_kg) atomicAdd(&st->kg_errors, bad_kg);
+  if (bad_ts) atomicAdd(&st->ts_errors, bad_ts);
+}
+
+// ---- generic in-place exclusive scan of uint32 (block = 1024 threads x 4 elements)
+constexpr int SCAN_T = 1024, SCAN_E = 4, SCAN_B = SCAN_T * SCAN_E;
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sw, uint32_t* total) {
+  // wave inclusive scan
+  const int lane = __lane_id(), wid = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sw[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    const int nw = blockDim.x >> 6;
+    for (int w = 0; w < nw; w++) {
+      uint32_t t = sw[w];
+      sw[w] = run;
+      run += t;
+    }
+    sw[nw] = run;
+  }
+  __syncthreads();
+  *total = sw[blockDim.x >> 6];
+  uint32_t r = sw[wid] + x - v;
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_blocks(uint32_t* data, int64_t m, uint32_t* sums) {
+  __shared__ uint32_t sw[SCAN_T / 64 + 1];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_B + (int64_t)threadIdx.x * SCAN_E;
+  uint32_t v[SCAN_E];
+  uint32_t local = 0;
+#pragma unroll
+  for (int e = 0; e < SCAN_E; e++) {
+    v[e] = base + e < m ? data[base + e] : 0u;
+    local += v[e];
+  }
+  uint32_t total;
+  uint32_t off = block_excl_scan(local, sw, &total);
+#pragma unroll
+  for (int e = 0; e < SCAN_E; e++) {
+    if (base + e < m) data[base + e] = off;
+    off += v[e];
+  }
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+__global__ __launch_bounds__(SCAN_T) void k_scan_top(uint32_t* sums, int64_t nb) {
+  __shared__ uint32_t sw[SCAN_T / 64 + 1];
+  uint32_t carry = 0;
+  for (int64_t b0 = 0; b0 < nb; b0 += SCAN_T) {
+    const int64_t i = b0 + threadIdx.x;
+    uint32_t v = i < nb ? sums[i] : 0u, total;
+    uint32_t off = block_excl_scan(v, sw, &total);
+    if (i < nb) sums[i] = off + carry;
+    carry += total;
+  }
+}
+__global__ __launch_bounds__(SCAN_T) void k_scan_add(uint32_t* data, int64_t m, const uint32_t* sums) {
+  const uint32_t add = sums[blockIdx.x];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_B;
+  for (int e = threadIdx.x; e < SCAN_B; e += SCAN_T)
+    if (base + e < m) data[base + e] += add;
+}
+
+// ---- K2: scatter.  Normal records -> their partition's run (any order inside the run);
+// ordered-path records -> the ordered list, arrival order kept; late records -> side / counter.
+__global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
+                                                             const int64_t* __restrict__ ts,
+                                                             const int64_t* __restrict__ val,
+                                                             const int32_t* __restrict__ kh, int64_t n, int32_t T,
+                                                             const uint32_t* __restrict__ offs, int64_t* __restrict__ pk,
+                                                             int64_t* __restrict__ pt, int64_t* __restrict__ pv,
+                                                             int64_t* __restrict__ sk, int64_t* __restrict__ stt,
+                                                             int64_t* __restrict__ sv, int32_t* __restrict__ skh,
+                                                             DevSide side, Status* st) {
+  extern __shared__ uint32_t sm[];
+  uint32_t* base = sm;              // P
+  uint32_t* cnt = sm + c.P;         // P
+  uint32_t* wtot = sm + 2 * c.P;    // 16 waves + 1
+  for (int i = threadIdx.x; i < c.P; i += blockDim.x) {
+    base[i] = offs[(int64_t)i * T + blockIdx.x];
+    cnt[i] = 0;
+  }
+  const uint32_t slow_base = offs[(int64_t)c.P * T + blockIdx.x] - offs[(int64_t)c.P * T];
+  __syncthreads();
+  const int64_t tbase = (int64_t)blockIdx.x * FW_TILE;
+  const int64_t tend = min(n, tbase + (int64_t)FW_TILE);
+  const int lane = __lane_id(), wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t running = 0;
+  unsigned long long late = 0;
+  for (int64_t j = tbase; j < tend; j += blockDim.x) {
+    const int64_t i = j + threadIdx.x;
+    int cls = CLS_SKIP;
+    int32_t p = -1, h = 0;
+    int64_t k = 0, t = 0, v = 0;
+    if (i < tend) {
+      k = key[i];
+      t = ts[i];
+      v = val[i];
+      h = key_hash_of(c.key_kind, k, kh, i);
+      p = partition_of(c, k, h);
+      if (p >= 0) cls = classify(c, wm, t);
+    }
+    if (cls == CLS_NORMAL) {
+      const uint32_t pos = base[p] + atomicAdd(&cnt[p], 1u);
+      pk[pos] = k;
+      pt[pos] = t;
+      pv[pos] = v;
+    }
+    // ordered compaction of the ordered-path records
+    const bool is_slow = cls == CLS_SLOW;
+    const uint64_t ball = __ballot(is_slow);
+    if (lane == 0) wtot[wid] = (uint32_t)__popcll(ball);
+    __syncthreads();
+    uint32_t woff = 0, tot = 0;
+    for (int w = 0; w < nw; w++) {
+      const uint32_t x = wtot[w];
+      woff += w < wid ? x : 0u;
+      tot += x;
+    }
+    if (is_slow) {
+      const uint32_t pos = slow_base + running + woff + (uint32_t)__popcll(ball & lanemask_lt());
+      sk[pos] = k;
+      stt[pos] = t;
+      sv[pos] = v;
+      skh[pos] = h;
+    }
+    running += tot;
+    __syncthreads();
+    if (cls == CLS_LATE) {
+      if (c.side_output)
+        side_one(side, st, k, t, v);
+      else
+        late++;
+    }
+  }
+  if (late) atomicAdd(&st->late_dropped, late);
+}
+
+// ---- K3: per-partition LDS pre-aggregation + flush into the HBM region
+struct AggLds {
+  int64_t key[FW_LDS_SLOTS];
+  int64_t start[FW_LDS_SLOTS];
+  unsigned long long cnt[FW_LDS_SLOTS];
+  int64_t sum[FW_LDS_SLOTS];
+  int64_t mn[FW_LDS_SLOTS];
+  int64_t mx[FW_LDS_SLOTS];
+  uint32_t state[FW_LDS_SLOTS];
+  int fill;
+  int anyfail;
+  int inserted;
+  int overflowed;
+  int64_t min_timer;
+};
+enum : uint32_t { LS_EMPTY = 0, LS_BUSY = 1, LS_READY = 2, LS_DONE = 3 };
+
+__device__ __forceinline__ uint32_t lds_hash(int64_t key, int64_t start) {
+  return (uint32_t)fmix64((uint64_t)key ^ ((uint64_t)start * 0xD6E8FEB86659FD93ull));
+}
+
+// insert-or-accumulate one value into the LDS table; false when the table is at its fill limit
+// (the caller flushes and retries).  One loop, no early exit, so a lane that claims a slot
+// finishes publishing it inside the same iteration as the lanes that wait on it.
+__device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, int64_t start, int64_t v) {
+  uint32_t h = lds_hash(key, start) & (FW_LDS_SLOTS - 1);
+  bool done = false, ok = false;
+  int guard = 0;
+  while (!done) {
+    const uint32_t s = __hip_atomic_load(&L.state[h], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    int target = -1;
+    if (s == LS_READY) {
+      if (L.key[h] == key && L.start[h] == start)
+        target = (int)h;
+      else {
+        h = (h + 1) & (FW_LDS_SLOTS - 1);
+        if (++guard >= FW_LDS_SLOTS) done = true;  // full circle: table full
+      }
+    } else if (s == LS_EMPTY) {
+      if (__hip_atomic_load(&L.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= FW_LDS_FILL_LIMIT) {
+        done = true;
+      } else if (atomicCAS(&L.state[h], LS_EMPTY, LS_BUSY) == LS_EMPTY) {
+        atomicAdd(&L.fill, 1);
+        L.key[h] = key;
+        L.start[h] = start;
+        L.cnt[h] = 0;
+        L.sum[h] = 0;
+        L.mn[h] = LMAX;
+        L.mx[h] = LMIN;
+        __hip_atomic_store(&L.state[h], LS_READY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        target = (int)h;
+      }
+    }
+    if (target >= 0) {
+      atomicAdd(&L.cnt[target], 1ull);
+      if (vtype == FW_VAL_F64) {
+        atomicAdd((double*)&L.sum[target], __longlong_as_double(v));
+        const int64_t sv = f64_sortable(v);
+        atomicMin((long long*)&L.mn[target], (long long)sv);
+        atomicMax((long long*)&L.mx[target], (long long)sv);
+      } else {
+        atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)v);
+        atomicMin((long long*)&L.mn[target], (long long)v);
+        atomicMax((long long*)&L.mx[target], (long long)v);
+      }
+      ok = true;
+      done = true;
+    }
+  }
+  return ok;
+}
+
+// merge every READY LDS slot into the partition's HBM region; resets the LDS table
+__device__ void agg_flush(const DevCfg& c, AggLds& L, const Region& r, int32_t p, DevOverflow ov, Status* st) {
+  __syncthreads();
+  // phase 1: windows already in the region: read-modify-write (distinct slots, no races)
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
+    if (L.state[h] != LS_READY) continue;
+    const int64_t k = L.key[h], s = L.start[h], e = jadd(s, c.size);
+    const int32_t slot = region_find(r, slot_hash(c, k, s), k, s, e);
+    if (slot < 0) continue;
+    Entry d;
+    d.cnt = (int64_t)L.cnt[h];
+    d.sum = L.sum[h];
+    d.mn = L.mn[h];
+    d.mx = L.mx[h];
+    Entry& x = r.ent[slot];
+    Entry cur = x;
+    acc_merge(c, cur, d);
+    cur.meta |= FW_TIMER;
+    x = cur;
+    L.state[h] = LS_DONE;
+  }
+  __syncthreads();
+  // phase 2: new windows: claim an EMPTY slot
+  int ins = 0;
+  unsigned long long nflush = 0;
+  int64_t mt = LMAX;
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
+    const uint32_t ls = L.state[h];
+    if (ls != LS_READY && ls != LS_DONE) continue;
+    nflush++;
+    const int64_t k = L.key[h], s = L.start[h];
+    Entry e;
+    e.key = k;
+    e.start = s;
+    e.end = jadd(s, c.size);
+    e.cnt = (int64_t)L.cnt[h];
+    e.sum = L.sum[h];
+    e.mn = L.mn[h];
+    e.mx = L.mx[h];
+    e.meta = FW_TIMER;
+    mt = min(mt, jsub(e.end, 1));
+    if (ls == LS_DONE) continue;
+    const int32_t slot = region_claim(r, slot_hash(c, k, s), SLOT_LIVE);
+    if (slot >= 0) {
+      r.ent[slot] = e;
+      ins++;
+    } else {
+      const unsigned long long pos = atomicAdd(&st->overflow_count, 1ull);
+      if ((int64_t)pos < ov.cap) {
+        ov.ent[pos] = e;
+        ov.part[pos] = p;
+      } else {
+        atomicOr(&st->flags, FW_STATUS_OVERFLOW_LOST);
+      }
+    }
+  }
+  if (ins) atomicAdd(&L.inserted, ins);
+  if (mt != LMAX) atomicMin((long long*)&L.min_timer, (long long)mt);
+  if (nflush) atomicAdd(&st->merged, nflush);
+  __syncthreads();
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.state[h] = LS_EMPTY;
+  if (threadIdx.x == 0) L.fill = 0;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(FW_AGG_THREADS) void k_aggregate(DevCfg c, int64_t wm, const int64_t* __restrict__ pk,
+                                                              const int64_t* __restrict__ pt,
+                                                              const int64_t* __restrict__ pv,
+                                                              const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
+                                                              DevOverflow ov, Status* st) {
+  __shared__ AggLds L;
+  const int32_t p = blockIdx.x;
+  const int64_t begin = offs[(int64_t)p * T], end = offs[(int64_t)(p + 1) * T];
+  if (begin == end) return;
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.state[h] = LS_EMPTY;
+  if (threadIdx.x == 0) {
+    L.fill = 0;
+    L.anyfail = 0;
+    L.inserted = 0;
+    L.min_timer = LMAX;
+  }
+  __syncthreads();
+  const Region r = region_of(c, tb, p, tb.cur[p]);
+  for (int64_t rb = begin; rb < end; rb += blockDim.x) {
+    const int64_t i = rb + threadIdx.x;
+    const bool have = i < end;
+    int64_t k = 0, t = 0, v = 0, last = 0;
+    int nwin = 0;
+    if (have) {
+      k = pk[i];
+      t = pt[i];
+      v = pv[i];
+      nwin = num_windows(c, t, &last);
+    }
+    int wi = 0;
+    for (;;) {
+      while (wi < nwin) {
+        const int64_t s = jsub(last, (int64_t)wi * c.slide);
+        if (!lds_upsert(L, c.vtype, k, s, v)) break;
+        wi++;
+      }
+      if (wi < nwin) L.anyfail = 1;
+      __syncthreads();
+      const int need = L.anyfail;
+      __syncthreads();
+      if (!need) break;
+      agg_flush(c, L, r, p, ov, st);
+      if (threadIdx.x == 0) L.anyfail = 0;
+      __syncthreads();
+    }
+  }
+  agg_flush(c, L, r, p, ov, st);
+  if (threadIdx.x == 0) {
+    const int32_t live = tb.live[p] + L.inserted;
+    tb.live[p] = live;
+    atomicMax(&st->max_live, live);
+    if (L.min_timer < tb.next_timer[p]) tb.next_timer[p] = L.min_timer;
+  }
+}
+
+// ---- K_slow: ordered replay (one workgroup; one thread per key inside each chunk)
+constexpr int SLOW_CHUNK = FW_SLOW_THREADS;
+constexpr int MAX_SESSIONS = 64;  // in-flight sessions of one key visible to one replay step
+
+struct SlowCtx {
+  DevCfg c;
+  int64_t wm;
+  DevTable tb;
+  DevRows out;
+  DevSide side;
+  Status* st;
+};
+
+__device__ __forceinline__ void note_timer(const SlowCtx& x, int32_t p, const Entry& e) {
+  atomicMin((long long*)&x.tb.next_timer[p], (long long)timer_of(e, x.c.lateness));
+}
+__device__ __forceinline__ void kill_slot(const SlowCtx& x, const Region& r, int32_t p, int32_t s) {
+  __hip_atomic_store(r.state + s, SLOT_DEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  atomicSub(&x.tb.live[p], 1);
+}
+__device__ __forceinline__ int32_t new_slot(const SlowCtx& x, const Region& r, int32_t p, uint32_t h, const Entry& e) {
+  const int32_t s = region_claim(r, h, SLOT_BUSY);
+  if (s < 0) {
+    atomicOr(&x.st->flags, FW_STATUS_OVERFLOW_LOST);
+    return -1;
+  }
+  r.ent[s] = e;
+  publish_live(r.state + s);
+  const int live = atomicAdd(&x.tb.live[p], 1) + 1;
+  atomicMax(&x.st->max_live, live);
+  return s;
+}
+
+// WindowOperator.processElement, non-merging branch (WindowOperator.java:371-407)
+__device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int64_t t, int64_t v, bool* skipped) {
+  const DevCfg& c = x.c;
+  const Region r = region_of(c, x.tb, p, x.tb.cur[p]);
+  int64_t last;
+  const int nwin = num_windows(c, t, &last);
+  for (int wi = 0; wi < nwin; wi++) {
+    const int64_t s = jsub(last, (int64_t)wi * c.slide);
+    const int64_t e = jadd(s, c.size);
+    if (cleanup_of(e, c.lateness) <= x.wm) continue;  // isWindowLate
+    *skipped = false;
+    const uint32_t h = slot_hash(c, k, s);
+    int32_t slot = region_find(r, h, k, s, e);
+    if (slot < 0) {
+      Entry ne;
+      ne.key = k;
+      ne.start = s;
+      ne.end = e;
+      acc_clear(ne);
+      ne.meta = 0;
+      slot = new_slot(x, r, p, h, ne);
+      if (slot < 0) continue;
+    }
+    Entry en = r.ent[slot];
+    acc_add(c, en, v);
+    bool keep = true;
+    if (jsub(e, 1) <= x.wm) {  // EventTimeTrigger.onElement -> FIRE (WindowOperator.java:395-401)
+      emit_one(c, x.out, x.st, en);
+      if (c.purging) keep = false;  // FIRE_AND_PURGE
+    } else {
+      en.meta |= FW_TIMER;  // registerEventTimeTimer(maxTimestamp)
+    }
+    if (keep) {
+      r.ent[slot] = en;
+      note_timer(x, p, en);
+    } else {
+      kill_slot(x, r, p, slot);
+    }
+  }
+}
+
+// WindowOperator.processElement, merging branch (WindowOperator.java:297-370) with
+// MergingWindowSet.addWindow (MergingWindowSet.java:150-225) over the key's in-flight sessions.
+__device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t, int64_t v, bool* skipped) {
+  const DevCfg& c = x.c;
+  const Region r = region_of(c, x.tb, p, x.tb.cur[p]);
+  const uint32_t h = slot_hash(c, k, 0);
+  // in-flight windows of the key: every live entry of the key sits on its probe chain
+  int32_t sl[MAX_SESSIONS];
+  int ns = 0;
+  for (uint32_t i = 0; i <= r.mask; i++) {
+    const uint32_t s = (h + i) & r.mask;
+    const uint32_t stt = ld_state(r.state + s);
+    if (stt == SLOT_EMPTY) break;
+    if (stt == SLOT_LIVE) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (r.ent[s].key == k) {
+        if (ns == MAX_SESSIONS) {
+          atomicOr(&x.st->flags, FW_STATUS_OVERFLOW_LOST);
+          return;
+        }
+        sl[ns++] = (int32_t)s;
+      }
+    }
+  }
+  const int64_t ws = t, we = jadd(t, c.gap);  // EventTimeSessionWindows.assignWindows
+  // TimeWindow.mergeWindows: the connected component of the new window (in-flight windows are
+  // pairwise disjoint and non-touching, so only this component can merge).
+  int64_t cs = ws, ce = we;
+  uint64_t in_group = 0;
+  bool grew = true;
+  while (grew) {
+    grew = false;
+    for (int j = 0; j < ns; j++) {
+      if (in_group >> j & 1) continue;
+      const Entry& e = r.ent[sl[j]];
+      if (cs <= e.end && ce >= e.start) {  // TimeWindow.intersects
+        in_group |= 1ull << j;
+        cs = min(cs, e.start);
+        ce = max(ce, e.end);
+        grew = true;
+      }
+    }
+  }
+  int32_t actual = -1;
+  bool fresh = false;
+  if (in_group == 0) {
+    Entry ne;
+    ne.key = k;
+    ne.start = ws;
+    ne.end = we;
+    acc_clear(ne);
+    ne.meta = 0;
+    actual = new_slot(x, r, p, h, ne);
+    if (actual < 0) return;
+    fresh = true;
+  } else {
+    const int first = __ffsll((unsigned long long)in_group) - 1;
+    const Entry& f = r.ent[sl[first]];
+    const bool contained = __popcll(in_group) == 1 && f.start == cs && f.end == ce;
+    actual = sl[first];
+    if (!contained) {
+      // merge function (WindowOperator.java:308-339)
+      if (jadd(jsub(ce, 1), c.lateness) <= x.wm) {
+        atomicOr(&x.st->flags, FW_STATUS_MERGE_LATE);
+        return;
+      }
+      Entry m = f;
+      for (int j = first + 1; j < ns; j++) {
+        if (!(in_group >> j & 1)) continue;
+        acc_merge(c, m, r.ent[sl[j]]);  // mergeNamespaces
+        kill_slot(x, r, p, sl[j]);
+      }
+      m.start = cs;
+      m.end = ce;
+      m.meta = FW_TIMER;  // EventTimeTrigger.onMerge registers maxTimestamp unconditionally
+      r.ent[actual] = m;
+    }
+  }
+  Entry en = r.ent[actual];
+  if (cleanup_of(en.end, c.lateness) <= x.wm) {  // isWindowLate(actualWindow) -> retireWindow
+    if (fresh) kill_slot(x, r, p, actual);
+    return;
+  }
+  *skipped = false;
+  acc_add(c, en, v);
+  if (jsub(en.end, 1) <= x.wm) {
+    emit_one(c, x.out, x.st, en);
+    if (c.purging) acc_clear(en);  // FIRE_AND_PURGE clears the contents; the window stays in flight
+  } else {
+    en.meta |= FW_TIMER;
+  }
+  r.ent[actual] = en;
+  note_timer(x, p, en);
+}
+
+__global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, const int64_t* __restrict__ sk,
+                                                          const int64_t* __restrict__ stt,
+                                                          const int64_t* __restrict__ sv,
+                                                          const int32_t* __restrict__ skh, DevTable tb, DevRows out,
+                                                          DevSide side, Status* st) {
+  const int64_t n = (int64_t)st->slow_count;
+  if (n == 0) return;
+  __shared__ int64_t ck[SLOW_CHUNK];
+  __shared__ int32_t ci[SLOW_CHUNK];
+  SlowCtx x{c, wm, tb, out, side, st};
+  unsigned long long late = 0;
+  for (int64_t b0 = 0; b0 < n; b0 += SLOW_CHUNK) {
+    const int m = (int)min((int64_t)SLOW_CHUNK, n - b0);
+    const int tid = threadIdx.x;
+    ck[tid] = tid < m ? sk[b0 + tid] : LMAX;
+    ci[tid] = tid < m ? tid : INT32_MAX;
+    __syncthreads();
+    // bitonic sort by (key, arrival index)
+    for (int kk = 2; kk <= SLOW_CHUNK; kk <<= 1) {
+      for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+        const int o = tid ^ jj;
+        if (o > tid) {
+          const bool up = (tid & kk) == 0;
+          const int64_t a = ck[tid], b = ck[o];
+          const int32_t ia = ci[tid], ib = ci[o];
+          const bool gt = a > b || (a == b && ia > ib);
+          if (gt == up) {
+            ck[tid] = b;
+            ck[o] = a;
+            ci[tid] = ib;
+            ci[o] = ia;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    if (tid < m && (tid == 0 || ck[tid - 1] != ck[tid])) {
+      for (int j = tid; j < m && ck[j] == ck[tid]; j++) {
+        const int64_t i = b0 + ci[j];
+        const int64_t k = sk[i], t = stt[i], v = sv[i];
+        const int32_t p = partition_of(c, k, skh[i]);
+        bool skipped = true;
+        if (c.assigner == FW_SESSION)
+          replay_session(x, p, k, t, v, &skipped);
+        else
+          replay_time_windows(x, p, k, t, v, &skipped);
+        if (skipped && jadd(t, c.lateness) <= wm) {  // isSkippedElement && isElementLate
+          if (c.side_output)
+            side_one(side, st, k, t, v);
+          else
+            late++;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (late) atomicAdd(&st->late_dropped, late);
+  if (threadIdx.x == 0) atomicAdd(&st->slow_total, (unsigned long long)n);
+}
+
+// ---- K_fire: watermark.  Regions with next_timer <= wm emit and are rebuilt into the other buffer.
+__global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, DevTable tb, DevRows out, Status* st) {
+  const int32_t p = blockIdx.x;
+  if (tb.next_timer[p] > wm) return;
+  __shared__ int live_s;
+  __shared__ long long next_s;
+  __shared__ unsigned long long wbase[FW_FIRE_THREADS / 64];
+  const int X = tb.cur[p], Y = X ^ 1;
+  const Region rx = region_of(c, tb, p, X), ry = region_of(c, tb, p, Y);
+  const uint32_t R = rx.mask + 1;
+  for (uint32_t s = threadIdx.x; s < R; s += blockDim.x) ry.state[s] = SLOT_EMPTY;
+  if (threadIdx.x == 0) {
+    live_s = 0;
+    next_s = LMAX;
+  }
+  __syncthreads();
+  const int lane = __lane_id(), wid = threadIdx.x >> 6;
+  int live = 0;
+  int64_t nt = LMAX;
+  unsigned long long fired = 0;
+  for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x) {
+    const uint32_t s = s0 + threadIdx.x;
+    bool fire = false, keep = false;
+    Entry e;
+    if (s < R && ld_state(rx.state + s) == SLOT_LIVE) {
+      e = rx.ent[s];
+      keep = true;
+      if ((e.meta & FW_TIMER) && jsub(e.end, 1) <= wm) {  // trigger timer fires (EventTimeTrigger.onEventTime)
+        e.meta &= ~(int64_t)FW_TIMER;
+        fire = e.cnt > 0;                                 // contents != null (WindowOperator.java:452-459)
+        if (c.purging) {
+          if (c.assigner == FW_SESSION)
+            acc_clear(e);
+          else
+            keep = false;
+        }
+      }
+      const int64_t cl = cleanup_of(e.end, c.lateness);
+      if (cl != LMAX && cl <= wm) keep = false;  // GC timer: clearAllState (WindowOperator.java:461-463)
+    }
+    const uint64_t ball = __ballot(fire);
+    if (lane == 0 && ball) wbase[wid] = atomicAdd(&st->out_rows, (unsigned long long)__popcll(ball));
+    __syncthreads();
+    if (fire) {
+      const unsigned long long pos = wbase[wid] + (unsigned long long)__popcll(ball & lanemask_lt());
+      if ((int64_t)pos < out.cap)
+        write_row(c, out, pos, e);
+      else
+        atomicOr(&st->flags, FW_STATUS_OUT_FULL);
+      fired++;
+    }
+    if (keep) {
+      const int32_t d = region_claim(ry, slot_hash(c, e.key, e.start), SLOT_LIVE);
+      if (d >= 0) {
+        ry.ent[d] = e;
+        live++;
+        nt = min(nt, timer_of(e, c.lateness));
+      } else {
+        atomicOr(&st->flags, FW_STATUS_OVERFLOW_LOST);
+      }
+    }
+    __syncthreads();
+  }
+  if (live) atomicAdd(&live_s, live);
+  if (nt != LMAX) atomicMin(&next_s, (long long)nt);
+  if (fired) atomicAdd(&st->fired_total, fired);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    tb.cur[p] = (uint8_t)Y;
+    tb.live[p] = live_s;
+    tb.next_timer[p] = next_s;
+  }
+}
+
+// ---- table growth: re-insert every live entry of the old table into the new one (buffer 0)
+__global__ __launch_bounds__(FW_FIRE_THREADS) void k_rehash(DevCfg oc, DevTable ot, DevCfg nc, DevTable nt) {
+  const int32_t p = blockIdx.x;
+  const Region ro = region_of(oc, ot, p, ot.cur[p]);
+  const Region rn = region_of(nc, nt, p, 0);
+  const uint32_t R = ro.mask + 1;
+  for (uint32_t s = threadIdx.x; s < R; s += blockDim.x) {
+    if (ld_state(ro.state + s) != SLOT_LIVE) continue;
+    const Entry e = ro.ent[s];
+    // the new region is larger than the old one's live count, so a slot is always found
+    const int32_t d = region_claim(rn, slot_hash(nc, e.key, e.start), SLOT_LIVE);
+    if (d >= 0) rn.ent[d] = e;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    nt.cur[p] = 0;
+    nt.live[p] = ot.live[p];
+    nt.next_timer[p] = ot.next_timer[p];
+  }
+}
+
+// ---- overflow deltas (parked by k_aggregate) merged into the grown table; one lane per region
+__global__ void k_merge_overflow(DevCfg c, DevTable tb, DevOverflow ov, const Status* st) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= c.P) return;
+  const int64_t n = min((int64_t)st->overflow_count, ov.cap);
+  const Region r = region_of(c, tb, p, tb.cur[p]);
+  int live = tb.live[p];
+  int64_t nt = tb.next_timer[p];
+  for (int64_t i = 0; i < n; i++) {
+    if (ov.part[i] != p) continue;
+    const Entry d = ov.ent[i];
+    const uint32_t h = slot_hash(c, d.key, d.start);
+    int32_t s = region_find(r, h, d.key, d.start, d.end);
+    if (s >= 0) {
+      Entry e = r.ent[s];
+      acc_merge(c, e, d);
+      e.meta |= d.meta;
+      r.ent[s] = e;
+    } else {
+      s = region_claim(r, h, SLOT_LIVE);
+      if (s < 0) continue;  // cannot happen: the table was grown to hold every parked delta
+      r.ent[s] = d;
+      live++;
+    }
+    nt = min(nt, timer_of(d, c.lateness));
+  }
+  tb.live[p] = live;
+  tb.next_timer[p] = nt;
+}
+
+__global__ void k_reset_regions(DevCfg c, DevTable tb) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= c.P) return;
+  tb.cur[p] = 0;
+  tb.live[p] = 0;
+  tb.next_timer[p] = LMAX;
+}
+
+// out3 = {live entries, event-time timers, max region load}
+__global__ __launch_bounds__(FW_FIRE_THREADS) void k_table_stats(DevCfg c, DevTable tb, unsigned long long* out3) {
+  const int32_t p = blockIdx.x;
+  const Region r = region_of(c, tb, p, tb.cur[p]);
+  unsigned long long live = 0, timers = 0;
+  for (uint32_t s = threadIdx.x; s <= r.mask; s += blockDim.x) {
+    if (ld_state(r.state + s) != SLOT_LIVE) continue;
+    const Entry& e = r.ent[s];
+    live++;
+    const int64_t mx = jsub(e.end, 1), cl = cleanup_of(e.end, c.lateness);
+    if (e.meta & FW_TIMER) timers++;
+    if (cl != LMAX && !((e.meta & FW_TIMER) && cl == mx)) timers++;
+  }
+  if (live) atomicAdd(&out3[0], live);
+  if (timers) atomicAdd(&out3[1], timers);
+}
+
+// ---- keyBy routing: key groups and stable grouping by destination operator index
+__global__ void k_key_groups(const int64_t* key, const int32_t* kh, int32_t kind, int64_t n, int32_t max_par,
+                             int32_t* kg) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    kg[i] = key_group(key_hash_of(kind, key[i], kh, i), max_par);
+}
+
+__device__ __forceinline__ int32_t dest_of(const int64_t* key, const int32_t* kh, int32_t kind, int64_t i,
+                                           int32_t max_par, int32_t par) {
+  // KeyGroupRangeAssignment.computeOperatorIndexForKeyGroup (KeyGroupRangeAssignment.java:115-117)
+  return key_group(key_hash_of(kind, key[i], kh, i), max_par) * par / max_par;
+}
+
+__global__ __launch_bounds__(FW_TILE_THREADS) void k_route_hist(const int64_t* key, const int32_t* kh, int32_t kind,
+                                                                int64_t n, int32_t max_par, int32_t par, int32_t T,
+                                                                uint32_t* hist) {
+  extern __shared__ uint32_t lh[];
+  for (int i = threadIdx.x; i < par; i += blockDim.x) lh[i] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * FW_TILE, end = min(n, base + (int64_t)FW_TILE);
+  for (int64_t i = base + threadIdx.x; i < end; i += blockDim.x) atomicAdd(&lh[dest_of(key, kh, kind, i, max_par, par)], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < par; i += blockDim.x) hist[(int64_t)i * T + blockIdx.x] = lh[i];
+}
+
+__global__ __launch_bounds__(FW_TILE_THREADS) void k_route_scatter(const int64_t* key, const int64_t* ts,
+                                                                   const int64_t* val, const int32_t* kh, int32_t kind,
+                                                                   int64_t n, int32_t max_par, int32_t par, int32_t T,
+                                                                   const uint32_t* offs, int64_t* ko, int64_t* to,
+                                                                   int64_t* vo, int32_t* ho) {
+  extern __shared__ uint32_t sm[];
+  const int nw = blockDim.x >> 6;
+  uint32_t* run = sm;            // par
+  uint32_t* wc = sm + par;       // nw * par
+  for (int d = threadIdx.x; d < par; d += blockDim.x) run[d] = offs[(int64_t)d * T + blockIdx.x];
+  __syncthreads();
+  const int lane = __lane_id(), wid = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * FW_TILE, end = min(n, base + (int64_t)FW_TILE);
+  for (int64_t j = base; j < end; j += blockDim.x) {
+    const int64_t i = j + threadIdx.x;
+    const int32_t d = i < end ? dest_of(key, kh, kind, i, max_par, par) : -1;
+    uint32_t rank = 0;
+    for (int q = 0; q < par; q++) {
+      const uint64_t b = __ballot(d == q);
+      if (d == q) rank = (uint32_t)__popcll(b & lanemask_lt());
+      if (lane == 0) wc[wid * par + q] = (uint32_t)__popcll(b);
+    }
+    __syncthreads();
+    if (d >= 0) {
+      uint32_t pos = run[d] + rank;
+      for (int w = 0; w < wid; w++) pos += wc[w * par + d];
+      ko[pos] = key[i];
+      to[pos] = ts[i];
+      vo[pos] = val[i];
+      ho[pos] = key_hash_of(kind, key[i], kh, i);
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < par; q += blockDim.x) {
+      uint32_t t = 0;
+      for (int w = 0; w < nw; w++) t += wc[w * par + q];
+      run[q] += t;
+    }
+    __syncthreads();
+  }
+}
+__global__ void k_route_counts(const uint32_t* offs, int32_t par, int32_t T, int64_t n, int64_t* counts) {
+  const int d = threadIdx.x;
+  if (d >= par) return;
+  const int64_t b = offs[(int64_t)d * T];
+  const int64_t e = d + 1 < par ? (int64_t)offs[(int64_t)(d + 1) * T] : n;
+  counts[d] = e - b;
+}
+
+// ---- synthetic source (splitmix64 counter-based; see fw_generate_device)
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void k_generate(uint64_t seed, int64_t first, int64_t n, int64_t num_keys,
+                                                  const double* cdf, int64_t ts_base, int64_t rate, int64_t jitter,
+                                                  int64_t* key, int64_t* ts, int64_t* val, int64_t* max_ts) {
+  int64_t mx = LMIN;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = (uint64_t)(first + j);
+    const uint64_t r0 = splitmix64(seed ^ (4 * i)), r1 = splitmix64(seed ^ (4 * i + 1)),
+                   r2 = splitmix64(seed ^ (4 * i + 2));
+    int64_t k;
+    if (cdf) {
+      const double u = (double)(r0 >> 11) * (1.0 / 9007199254740992.0);
+      int64_t lo = 0, hi = num_keys;  // first index with cdf[idx] > u
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (cdf[mid] > u)
+          hi = mid;
+        else
+          lo = mid + 1;
+      }
+      k = lo < num_keys ? lo : num_keys - 1;
+    } else {
+      k = (int64_t)(r0 % (uint64_t)num_keys);
+    }
+    const int64_t t = ts_base + (int64_t)((i * 1000ull) / (uint64_t)rate) - (jitter > 0 ? (int64_t)(r2 % (uint64_t)jitter) : 0);
+    key[j] = k;
+    ts[j] = t;
+    val[j] = (int64_t)(int32_t)(uint32_t)r1;
+    mx = t > mx ? t : mx;
+  }
+  if (max_ts) {
+    for (int o = 32; o > 0; o >>= 1) {
+      const int64_t y = __shfl_xor(mx, o, 64);
+      mx = y > mx ? y : mx;
+    }
+    if (__lane_id() == 0 && mx != LMIN) atomicMax((long long*)max_ts, (long long)mx);
+  }
+}
+
+}  // namespace
+
+// ============================================================================== launchers
+namespace fwdev {
+
+static inline int32_t ntiles(int64_t n) { return (int32_t)((n + FW_TILE - 1) / FW_TILE); }
+
+void launch_classify_hist(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int32_t* kh,
+                          int64_t n, int32_t T, uint32_t* hist, Status* st, hipStream_t s) {
+  hipLaunchKernelGGL(k_classify_hist, dim3(T), dim3(FW_TILE_THREADS), (c.P + 1) * sizeof(uint32_t), s, c, wm, key, ts,
+                     kh, n, T, hist, st);
+}
+
+void launch_scan(uint32_t* data, int64_t m, uint32_t* scratch, hipStream_t s) {
+  const int64_t nb = (m + SCAN_B - 1) / SCAN_B;
+  hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nb), dim3(SCAN_T), 0, s, data, m, scratch);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, scratch, nb);
+  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(SCAN_T), 0, s, data, m, (const uint32_t*)scratch);
+}
+
+void launch_scatter(const DevCfg& c, int64_t wm, int64_t /*ordinal_base*/, const int64_t* key, const int64_t* ts,
+                    const int64_t* val, const int32_t* kh, int64_t n, int32_t T, const uint32_t* offs, int64_t* pk,
+                    int64_t* pt, int64_t* pv, int64_t* sk, int64_t* stt, int64_t* sv, int32_t* skh, DevSide side,
+                    Status* st, hipStream_t s) {
+  const size_t lds = (2 * (size_t)c.P + 17) * sizeof(uint32_t);
+  hipLaunchKernelGGL(k_scatter, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, val, kh, n, T, offs, pk, pt, pv,
+                     sk, stt, sv, skh, side, st);
+}
+
+void launch_aggregate(const DevCfg& c, int64_t wm, const int64_t* pk, const int64_t* pt, const int64_t* pv,
+                      const uint32_t* offs, int32_t T, DevTable tb, DevOverflow ov, Status* st, hipStream_t s) {
+  hipLaunchKernelGGL(k_aggregate, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, pk, pt, pv, offs, T, tb, ov, st);
+}
+
+void launch_slow(const DevCfg& c, int64_t wm, const int64_t* sk, const int64_t* stt, const int64_t* sv,
+                 const int32_t* skh, DevTable tb, DevRows out, DevSide side, Status* st, hipStream_t s) {
+  hipLaunchKernelGGL(k_slow, dim3(1), dim3(FW_SLOW_THREADS), 0, s, c, wm, sk, stt, sv, skh, tb, out, side, st);
+}
+
+void launch_fire(const DevCfg& c, int64_t wm, DevTable tb, DevRows out, Status* st, hipStream_t s) {
+  hipLaunchKernelGGL(k_fire, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, wm, tb, out, st);
+}
+
+void launch_rehash(const DevCfg& oc, DevTable ot, const DevCfg& nc, DevTable nt, hipStream_t s) {
+  hipLaunchKernelGGL(k_rehash, dim3(oc.P), dim3(FW_FIRE_THREADS), 0, s, oc, ot, nc, nt);
+}
+
+void launch_merge_overflow(const DevCfg& c, DevTable tb, DevOverflow ov, const Status* st, hipStream_t s) {
+  hipLaunchKernelGGL(k_merge_overflow, dim3((c.P + 63) / 64), dim3(64), 0, s, c, tb, ov, st);
+}
+
+void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t s) {
+  hipLaunchKernelGGL(k_table_stats, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, tb, out3);
+}
+
+void launch_reset_regions(const DevCfg& c, DevTable tb, hipStream_t s) {
+  hipLaunchKernelGGL(k_reset_regions, dim3((c.P + 255) / 256), dim3(256), 0, s, c, tb);
+}
+
+void launch_key_groups(const int64_t* key, const int32_t* kh, int32_t kind, int64_t n, int32_t max_par, int32_t* kg,
+                       hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  if (blocks > 0) hipLaunchKernelGGL(k_key_groups, dim3((unsigned)blocks), dim3(256), 0, s, key, kh, kind, n, max_par, kg);
+}
+
+void launch_route(const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int32_t kind,
+                  int64_t n, int32_t max_par, int32_t par, int64_t* ko, int64_t* to, int64_t* vo, int32_t* ho,
+                  int64_t* counts, uint32_t* scratch, hipStream_t s) {
+  const int32_t T = ntiles(n);
+  const int64_t m = (int64_t)par * T;
+  uint32_t* hist = scratch;
+  uint32_t* scan_tmp = scratch + m;
+  if (T > 0) {
+    hipLaunchKernelGGL(k_route_hist, dim3(T), dim3(FW_TILE_THREADS), par * sizeof(uint32_t), s, key, kh, kind, n,
+                       max_par, par, T, hist);
+    launch_scan(hist, m, scan_tmp, s);
+    const size_t lds = (size_t)par * (1 + FW_TILE_THREADS / 64) * sizeof(uint32_t);
+    hipLaunchKernelGGL(k_route_scatter, dim3(T), dim3(FW_TILE_THREADS), lds, s, key, ts, val, kh, kind, n, max_par, par,
+                       T, (const uint32_t*)hist, ko, to, vo, ho);
+    hipLaunchKernelGGL(k_route_counts, dim3(1), dim3(std::max(64, ((par + 63) / 64) * 64)), 0, s, (const uint32_t*)hist,
+                       par, T, n, counts);
+  } else {
+    (void)hipMemsetAsync(counts, 0, par * sizeof(int64_t), s);
+  }
+}
+
+void launch_generate(uint64_t seed, int64_t first, int64_t n, int64_t num_keys, const double* cdf, int64_t ts_base,
+                     int64_t rate, int64_t jitter, int64_t* key, int64_t* ts, int64_t* val, int64_t* max_ts,
+                     hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+  if (blocks > 0)
+    hipLaunchKernelGGL(k_generate, dim3((unsigned)blocks), dim3(256), 0, s, seed, first, n, num_keys, cdf, ts_base, rate,
+                       jitter, key, ts, val, max_ts);
+}
+
+}  // namespace fwdev

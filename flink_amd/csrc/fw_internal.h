@@ -1,0 +1,108 @@
+// fw_internal.h — shared device/host definitions of the MI355X window operator.
+//
+// HBM layout of the keyed state ("window-contents" + event-time timers):
+//   The KeyGroupRange owned by a handle is split into P = nKG << logS state partitions
+//   (a key group keeps its partitions contiguous, so a per-key-group snapshot is a contiguous
+//   slice — HeapKeyedStateBackend.java:370-381 writes state per key group the same way).
+//   Partition p owns a region of R = 1 << logR open-addressing slots in each of two table
+//   buffers; cur[p] says which buffer is live.  A slot is a 64-byte Entry (one cache line:
+//   key, window start/end, the accumulator and timer flags) plus a 4-byte state word kept in
+//   a separate dense array so an empty region is cleared with a contiguous 4R-byte memset.
+//   The event-time timers of HeapInternalTimerService (HeapInternalTimerService.java:224-290)
+//   are not materialised: an entry's trigger timer is the FW_TIMER flag (set when an element
+//   is added while maxTimestamp > watermark, EventTimeTrigger.java:37-45; cleared when it
+//   fires) and its GC timer is implied by the entry's existence (cleanupTime,
+//   WindowOperator.java:637-644).  next_timer[p] is the earliest timer in region p, so a
+//   watermark only visits regions that have something to fire or clean.
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#define FW_TILE 32768          // records per classify/scatter workgroup
+#define FW_TILE_THREADS 1024
+#define FW_AGG_THREADS 512     // aggregate workgroup
+#define FW_LDS_SLOTS 1024      // LDS pre-aggregation slots per aggregate workgroup
+#define FW_LDS_FILL_LIMIT 820  // ~0.8 * FW_LDS_SLOTS: a new slot is not claimed beyond this fill
+#define FW_FIRE_THREADS 256
+#define FW_SLOW_THREADS 1024   // ordered replay workgroup (one workgroup)
+
+enum : uint32_t { SLOT_EMPTY = 0, SLOT_LIVE = 1, SLOT_DEAD = 2, SLOT_BUSY = 3 };
+enum : int64_t { FW_TIMER = 1 };
+
+struct DevCfg {
+  int32_t assigner, vtype, key_kind, purging;
+  int32_t side_output, max_par, kg0, n_kg;
+  int32_t log_s, P, log_r, wpr;  // wpr = max windows per record
+  int64_t size, slide, offset, gap, lateness;
+};
+
+struct __attribute__((aligned(64))) Entry {
+  int64_t key, start, end, cnt, sum, mn, mx, meta;
+};
+
+struct Status {
+  unsigned long long out_rows;        // rows in the output buffer (pending)
+  unsigned long long side_rows;       // rows in the side buffer (pending)
+  unsigned long long late_dropped;    // numLateRecordsDropped
+  unsigned long long slow_count;      // records of the last push routed to the ordered path
+  unsigned long long overflow_count;  // deltas parked in the overflow list
+  unsigned long long fired_total;
+  unsigned long long slow_total;
+  unsigned long long merged;          // LDS deltas merged into HBM regions (k_aggregate)
+  int32_t max_live;                   // max live slots over regions touched since reset
+  int32_t flags;                      // FW_STATUS_*
+  int32_t kg_errors;
+  int32_t ts_errors;
+};
+enum { FW_STATUS_OVERFLOW_LOST = 1, FW_STATUS_OUT_FULL = 2, FW_STATUS_MERGE_LATE = 4, FW_STATUS_SIDE_FULL = 8 };
+
+struct DevTable {
+  Entry* ent[2];
+  uint32_t* state[2];
+  uint8_t* cur;
+  int32_t* live;
+  int64_t* next_timer;
+};
+
+struct DevRows {
+  int64_t *key, *start, *end, *cnt, *sum, *mn, *mx;
+  int64_t cap;
+};
+struct DevSide {
+  int64_t *key, *ts, *val;
+  int64_t cap;
+};
+struct DevOverflow {  // deltas that did not fit their region; merged after the table grows
+  Entry* ent;
+  int32_t* part;
+  int64_t cap;
+};
+
+// ---------------------------------------------------------------- launchers (fw_device.hip)
+typedef hipStream_t hipStream_t_;
+namespace fwdev {
+void launch_classify_hist(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int32_t* kh,
+                          int64_t n, int32_t T, uint32_t* hist, Status* st, hipStream_t_ s);
+void launch_scan(uint32_t* data, int64_t m, uint32_t* scratch, hipStream_t_ s);  // in-place exclusive
+void launch_scatter(const DevCfg& c, int64_t wm, int64_t ordinal_base, const int64_t* key, const int64_t* ts,
+                    const int64_t* val, const int32_t* kh, int64_t n, int32_t T, const uint32_t* offs,
+                    int64_t* pk, int64_t* pt, int64_t* pv, int64_t* sk, int64_t* stt, int64_t* sv, int32_t* skh,
+                    DevSide side, Status* st, hipStream_t_ s);
+void launch_aggregate(const DevCfg& c, int64_t wm, const int64_t* pk, const int64_t* pt, const int64_t* pv,
+                      const uint32_t* offs, int32_t T, DevTable tb, DevOverflow ov, Status* st, hipStream_t_ s);
+void launch_slow(const DevCfg& c, int64_t wm, const int64_t* sk, const int64_t* stt, const int64_t* sv,
+                 const int32_t* skh, DevTable tb, DevRows out, DevSide side, Status* st, hipStream_t_ s);
+void launch_fire(const DevCfg& c, int64_t wm, DevTable tb, DevRows out, Status* st, hipStream_t_ s);
+void launch_rehash(const DevCfg& old_c, DevTable old_t, const DevCfg& new_c, DevTable new_t, hipStream_t_ s);
+void launch_merge_overflow(const DevCfg& c, DevTable tb, DevOverflow ov, const Status* st, hipStream_t_ s);
+void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t_ s);
+void launch_reset_regions(const DevCfg& c, DevTable tb, hipStream_t_ s);
+void launch_key_groups(const int64_t* key, const int32_t* kh, int32_t key_kind, int64_t n, int32_t max_par,
+                       int32_t* kg, hipStream_t_ s);
+void launch_route(const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int32_t key_kind,
+                  int64_t n, int32_t max_par, int32_t par, int64_t* ko, int64_t* to, int64_t* vo, int32_t* ho,
+                  int64_t* counts, uint32_t* scratch, hipStream_t_ s);
+void launch_generate(uint64_t seed, int64_t first, int64_t n, int64_t num_keys, const double* cdf, int64_t ts_base,
+                     int64_t rate, int64_t jitter, int64_t* key, int64_t* ts, int64_t* val, int64_t* max_ts,
+                     hipStream_t_ s);
+}  // namespace fwdev

@@ -1,0 +1,221 @@
+"""GpuWindowOperator: the drop-in for WindowOperator + heap keyed state backend + event-time timer
+service on one MI355X.  Mirrors the reference operator's interface in batch form:
+
+  WindowOperator(windowAssigner, ..., stateDesc, windowFunction, trigger, allowedLateness, lateDataOutputTag)
+      (flink-streaming-java/.../runtime/operators/windowing/WindowOperator.java:179-212)
+  processElement(StreamRecord)   -> process_batch(keys, timestamps, values)    (:291-421)
+  processWatermark(Watermark)    -> process_watermark(wm) -> fired rows         (AbstractStreamOperator.java:735-740)
+  numLateRecordsDropped, numKeyedStateEntries, numEventTimeTimers               (WindowOperator.java:138-140;
+                                                                                 KeyedOneInputStreamOperatorTestHarness:71-81)
+
+Inputs are either numpy arrays (host; copied to HBM by the library) or torch tensors already on the
+GPU (consumed in place).  Every call goes through libflinkwin.so; there is no CPU implementation.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from .keygroups import KeyGroupRange
+from .windowing import CountSumMinMax, EventTimeTrigger, Trigger, WindowAssigner
+
+ROW_FIELDS = ("key", "start", "end", "count", "sum", "min", "max")
+ROW_DTYPE = np.dtype([(f, "<i8") for f in ROW_FIELDS] + [("epoch", "<i8")])
+SIDE_DTYPE = np.dtype([("key", "<i8"), ("ts", "<i8"), ("val", "<i8"), ("epoch", "<i8")])
+
+_KEY_KINDS = {"long": N.FW_KEY_LONG, "int": N.FW_KEY_INT, "hashed": N.FW_KEY_HASHED}
+
+
+def _is_torch(x):
+    return type(x).__module__.startswith("torch")
+
+
+class GpuWindowOperator:
+    def __init__(self, assigner: WindowAssigner, aggregate=CountSumMinMax(), trigger: Trigger = None,
+                 allowed_lateness=0, side_output=False, key_type="long", max_parallelism=128,
+                 key_group_range: KeyGroupRange = None, device=0, expected_entries=0, max_batch=0,
+                 sub_partitions=0):
+        trigger = trigger or EventTimeTrigger.create()
+        if allowed_lateness < 0:
+            raise ValueError("The allowed lateness cannot be negative.")
+        kgr = key_group_range or KeyGroupRange(0, max_parallelism - 1)
+        c = N.FwConfig()
+        for k, v in assigner.config().items():
+            setattr(c, k, v)
+        c.value_type = aggregate.native()
+        c.key_kind = _KEY_KINDS[key_type]
+        c.purging = int(trigger.purging)
+        c.side_output = int(side_output)
+        c.max_parallelism = max_parallelism
+        c.key_group_start = kgr.start_key_group
+        c.key_group_end = kgr.end_key_group
+        c.device = device
+        c.sub_partitions = sub_partitions
+        c.allowed_lateness = allowed_lateness
+        c.expected_entries = expected_entries
+        c.max_batch = max_batch
+        self.assigner, self.aggregate, self.trigger = assigner, aggregate, trigger
+        self.allowed_lateness = allowed_lateness
+        self.side_output_enabled = bool(side_output)
+        self.key_group_range = kgr
+        self.max_parallelism = max_parallelism
+        self.device = device
+        self._cfg = c
+        self._h = ctypes.c_void_p()
+        L = N.lib()
+        rc = L.fw_create(ctypes.byref(c), ctypes.byref(self._h))
+        if rc != N.FW_OK:
+            msg = L.fw_last_error(self._h).decode() if self._h else "fw_create failed"
+            L.fw_destroy(self._h)
+            self._h = None
+            raise N.NativeError(rc, msg)
+        self.epoch = 0  # watermarks processed so far
+        self._rows = []
+        self._side = []
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().fw_destroy(self._h)
+            self._h = None
+
+    dispose = close
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def stream(self):
+        return N.lib().fw_stream(self._h)
+
+    # ------------------------------------------------------------------ processElement
+    def process_batch(self, keys, timestamps, values, key_hash=None):
+        """Hands a micro-batch (all records between two watermarks, or a part of them) to the GPU."""
+        L = N.lib()
+        if _is_torch(keys):
+            import torch
+            n = keys.numel()
+            for t in (keys, timestamps, values) + ((key_hash,) if key_hash is not None else ()):
+                if not t.is_cuda or not t.is_contiguous() or t.numel() != n:
+                    raise ValueError("device columns must be contiguous CUDA tensors of equal length")
+            if keys.dtype != torch.int64 or timestamps.dtype != torch.int64:
+                raise ValueError("keys and timestamps must be int64")
+            # the library stream must see the producer's writes of these tensors
+            torch.cuda.current_stream(keys.device).synchronize()
+            rc = L.fw_push_batch_device(self._h, keys.data_ptr(), timestamps.data_ptr(), values.data_ptr(),
+                                        key_hash.data_ptr() if key_hash is not None else None, n)
+        else:
+            keys = np.ascontiguousarray(keys, dtype=np.int64)
+            timestamps = np.ascontiguousarray(timestamps, dtype=np.int64)
+            values = np.asarray(values)
+            values = np.ascontiguousarray(values, dtype=np.float64 if self.aggregate.value_type == "double"
+                                          else np.int64)
+            kh = None
+            if key_hash is not None:
+                key_hash = np.ascontiguousarray(key_hash, dtype=np.int32)
+                kh = key_hash.ctypes.data
+            n = len(keys)
+            if len(timestamps) != n or len(values) != n:
+                raise ValueError("columns must have equal length")
+            rc = L.fw_push_batch(self._h, keys.ctypes.data, timestamps.ctypes.data, values.ctypes.data, kh, n)
+        N.check(rc, self._h)
+
+    processElements = process_batch
+
+    # ------------------------------------------------------------------ processWatermark
+    def advance_watermark(self, wm):
+        """Fires due windows; returns the number of rows pending in HBM (not copied)."""
+        n = ctypes.c_int64()
+        N.check(N.lib().fw_advance_watermark(self._h, int(wm), ctypes.byref(n)), self._h)
+        self.epoch += 1
+        return n.value
+
+    def process_watermark(self, wm):
+        """processWatermark: returns every row emitted since the previous watermark (late firings
+        during process_batch, then the timer firings of this watermark) as a structured array."""
+        self.advance_watermark(wm)
+        rows = self.drain_rows(self.epoch - 1)
+        if self.side_output_enabled:
+            self._side.append(self.drain_side(self.epoch - 1))
+        return rows
+
+    processWatermark = process_watermark
+
+    def drain_rows(self, epoch=-1):
+        L = N.lib()
+        n_rows = ctypes.c_int64()
+        N.check(L.fw_pending(self._h, ctypes.byref(n_rows), None), self._h)
+        out = np.zeros(n_rows.value, dtype=ROW_DTYPE)
+        cols = {f: np.zeros(n_rows.value, dtype=np.int64) for f in ROW_FIELDS}
+        dst = N.FwRows(**{f: cols[f].ctypes.data for f in ROW_FIELDS})
+        got = ctypes.c_int64()
+        N.check(L.fw_drain_rows(self._h, ctypes.byref(dst), n_rows.value, ctypes.byref(got)), self._h)
+        for f in ROW_FIELDS:
+            out[f] = cols[f][:got.value]
+        out["epoch"] = epoch
+        return out
+
+    def drain_side(self, epoch=-1):
+        L = N.lib()
+        n_side = ctypes.c_int64()
+        N.check(L.fw_pending(self._h, None, ctypes.byref(n_side)), self._h)
+        k, t, v = (np.zeros(n_side.value, dtype=np.int64) for _ in range(3))
+        dst = N.FwSideRows(key=k.ctypes.data, ts=t.ctypes.data, val=v.ctypes.data)
+        got = ctypes.c_int64()
+        N.check(L.fw_drain_side(self._h, ctypes.byref(dst), n_side.value, ctypes.byref(got)), self._h)
+        out = np.zeros(got.value, dtype=SIDE_DTYPE)
+        out["key"], out["ts"], out["val"], out["epoch"] = k[:got.value], t[:got.value], v[:got.value], epoch
+        return out
+
+    def rows_device(self):
+        """Device view of the pending rows: (dict of column -> raw device pointer, n)."""
+        view = N.FwRows()
+        n = ctypes.c_int64()
+        N.check(N.lib().fw_rows_device(self._h, ctypes.byref(view), ctypes.byref(n)), self._h)
+        return {f: getattr(view, f) for f in ROW_FIELDS}, n.value
+
+    def clear_pending(self):
+        N.check(N.lib().fw_clear_pending(self._h), self._h)
+
+    def synchronize(self):
+        N.check(N.lib().fw_synchronize(self._h), self._h)
+
+    # ------------------------------------------------------------------ harness-style interface
+    # (the shape of OneInputStreamOperatorTestHarness used by tests/kat_util.replay)
+    def process(self, keys, ts, vals, key_hash=None):
+        self.process_batch(keys, ts, vals, key_hash)
+
+    def watermark(self, wm):
+        self._rows.append(self.process_watermark(wm))
+
+    def rows(self):
+        return np.concatenate(self._rows) if self._rows else np.zeros(0, dtype=ROW_DTYPE)
+
+    def side_rows(self):
+        return np.concatenate(self._side) if self._side else np.zeros(0, dtype=SIDE_DTYPE)
+
+    # ------------------------------------------------------------------ metrics
+    def stats(self):
+        s = N.FwStats()
+        N.check(N.lib().fw_get_stats(self._h, ctypes.byref(s)), self._h)
+        return {f: getattr(s, f) for f, _ in N.FwStats._fields_}
+
+    @property
+    def late_dropped(self):
+        return self.stats()["late_records_dropped"]
+
+    numLateRecordsDropped = late_dropped
+
+    @property
+    def num_keyed_state_entries(self):
+        return self.stats()["keyed_state_entries"]
+
+    @property
+    def num_event_time_timers(self):
+        return self.stats()["event_time_timers"]

@@ -1,0 +1,158 @@
+"""Window assigners, triggers, time and the built-in aggregate of the GPU path — the host mirror
+of the reference's API objects.  They only carry parameters (validated exactly as the reference's
+constructors do); assignment itself runs in the HIP kernels.
+
+Reference (flink-streaming-java/src/main/java/org/apache/flink/streaming/api/):
+  windowing/assigners/TumblingEventTimeWindows.java:53-126
+  windowing/assigners/SlidingEventTimeWindows.java:50-146
+  windowing/assigners/EventTimeSessionWindows.java:45-113
+  windowing/triggers/EventTimeTrigger.java, PurgingTrigger.java
+  windowing/time/Time.java
+"""
+from dataclasses import dataclass
+
+from . import _native as N
+
+
+class Time:
+    """windowing/time/Time.java: a size in milliseconds."""
+
+    def __init__(self, ms):
+        self.ms = int(ms)
+
+    @staticmethod
+    def milliseconds(v):
+        return Time(v)
+
+    @staticmethod
+    def seconds(v):
+        return Time(v * 1000)
+
+    @staticmethod
+    def minutes(v):
+        return Time(v * 60_000)
+
+    @staticmethod
+    def hours(v):
+        return Time(v * 3_600_000)
+
+    @staticmethod
+    def days(v):
+        return Time(v * 86_400_000)
+
+    def to_milliseconds(self):
+        return self.ms
+
+
+def _ms(t):
+    return t.ms if isinstance(t, Time) else int(t)
+
+
+class WindowAssigner:
+    kind = None
+    is_event_time = True
+
+    def config(self):
+        raise NotImplementedError
+
+
+class TumblingEventTimeWindows(WindowAssigner):
+    """TumblingEventTimeWindows.of(size[, offset]) (TumblingEventTimeWindows.java:53-58,104-121)."""
+    kind = N.FW_TUMBLING
+
+    def __init__(self, size, offset=0):
+        if offset < 0 or offset >= size:
+            raise ValueError("TumblingEventTimeWindows parameters must satisfy 0 <= offset < size")
+        self.size, self.offset = size, offset
+
+    @staticmethod
+    def of(size, offset=0):
+        return TumblingEventTimeWindows(_ms(size), _ms(offset))
+
+    def config(self):
+        return dict(assigner=self.kind, size=self.size, slide=self.size, offset=self.offset)
+
+    def __repr__(self):
+        return f"TumblingEventTimeWindows({self.size})"
+
+
+class SlidingEventTimeWindows(WindowAssigner):
+    """SlidingEventTimeWindows.of(size, slide[, offset]) (SlidingEventTimeWindows.java:57-64,120-141)."""
+    kind = N.FW_SLIDING
+
+    def __init__(self, size, slide, offset=0):
+        if offset < 0 or offset >= slide or size <= 0:
+            raise ValueError("SlidingEventTimeWindows parameters must satisfy 0 <= offset < slide and size > 0")
+        self.size, self.slide, self.offset = size, slide, offset
+
+    @staticmethod
+    def of(size, slide, offset=0):
+        return SlidingEventTimeWindows(_ms(size), _ms(slide), _ms(offset))
+
+    def config(self):
+        return dict(assigner=self.kind, size=self.size, slide=self.slide, offset=self.offset)
+
+    def __repr__(self):
+        return f"SlidingEventTimeWindows({self.size}, {self.slide})"
+
+
+class EventTimeSessionWindows(WindowAssigner):
+    """EventTimeSessionWindows.withGap(gap) (EventTimeSessionWindows.java:52-57,94-96)."""
+    kind = N.FW_SESSION
+
+    def __init__(self, gap):
+        if gap <= 0:
+            raise ValueError("EventTimeSessionWindows parameters must satisfy 0 < size")
+        self.gap = gap
+
+    @staticmethod
+    def with_gap(gap):
+        return EventTimeSessionWindows(_ms(gap))
+
+    withGap = with_gap
+
+    def config(self):
+        return dict(assigner=self.kind, gap=self.gap)
+
+    def __repr__(self):
+        return f"EventTimeSessionWindows({self.gap})"
+
+
+class Trigger:
+    purging = False
+
+
+class EventTimeTrigger(Trigger):
+    """EventTimeTrigger.create() (EventTimeTrigger.java:37-73)."""
+
+    @staticmethod
+    def create():
+        return EventTimeTrigger()
+
+
+class PurgingTrigger(Trigger):
+    """PurgingTrigger.of(EventTimeTrigger.create()) (PurgingTrigger.java:45-59)."""
+    purging = True
+
+    def __init__(self, nested):
+        if not isinstance(nested, EventTimeTrigger):
+            raise ValueError("the GPU path offers PurgingTrigger only around EventTimeTrigger")
+        self.nested = nested
+
+    @staticmethod
+    def of(nested):
+        return PurgingTrigger(nested)
+
+
+@dataclass(frozen=True)
+class CountSumMinMax:
+    """The built-in AggregateFunction of the GPU path: ACC = OUT = (count, sum, min, max) of one
+    numeric field.  `value_type` is "long" (sum wraps at 64 bits), "int" (SumFunction.IntSum:
+    wraps at 32 bits, so `sum(pos)` on an Integer field) or "double" (min/max by Double.compare,
+    sum within 1e-6 relative of the reference's left-to-right order).
+    sum/min/max of WindowedStream (WindowedStream.java:1354-1535) are projections of this
+    accumulator onto one field."""
+    value_type: str = "long"
+
+    def native(self):
+        return {"long": N.FW_VAL_I64, "int": N.FW_VAL_I32, "double": N.FW_VAL_F64}[self.value_type]

@@ -1,0 +1,196 @@
+/*
+ * flink_window.h — C-ABI of the MI355X keyed event-time window operator ("fw_").
+ *
+ * Drop-in boundary for Flink's WindowOperator + heap keyed state backend + event-time
+ * timer service (paths relative to /root/reference/flink-streaming-java/src/main/java/
+ * org/apache/flink/streaming/ unless they start with flink-*).  Plain pointers and sizes,
+ * no C++ or torch types; every call returns an int status (FW_OK = 0, < 0 error) and
+ * fw_last_error() gives the message (the Java shim throws IOException(message), as
+ * HeapAggregatingState.java:90-92 wraps state errors).  Calls on one handle are serialised
+ * by the caller (one handle per subtask, as one task thread owns one operator:
+ * runtime/io/StreamInputProcessor.java:211-222); handles on different GPUs may be driven
+ * concurrently.
+ *
+ * Micro-batch contract: records handed to one fw_push_* call are processed against the
+ * current watermark exactly as WindowOperator.processElement would process them one by one
+ * (WindowOperator.java:291-421); fw_advance_watermark is processWatermark
+ * (api/operators/AbstractStreamOperator.java:735-740 -> HeapInternalTimerService.java:276-290).
+ * The host therefore cuts batches at watermarks.
+ */
+#ifndef FLINK_WINDOW_H
+#define FLINK_WINDOW_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define FW_OK 0
+#define FW_ERR_ARG (-1)          /* invalid argument (IllegalArgumentException in the reference) */
+#define FW_ERR_HIP (-2)          /* HIP runtime failure */
+#define FW_ERR_NO_TIMESTAMP (-3) /* Long.MIN_VALUE timestamp: TumblingEventTimeWindows.java:69-71 */
+#define FW_ERR_KEY_GROUP (-4)    /* key outside the handle's KeyGroupRange (KeyGroupRangeOffsets / StateTable) */
+#define FW_ERR_CAPACITY (-5)     /* state table could not absorb a batch (see fw_config.expected_entries) */
+#define FW_ERR_UNSUPPORTED (-6)  /* configuration not offered on the GPU path */
+#define FW_ERR_STATE (-7)        /* corrupted / inconsistent handle state */
+
+/* ---- assigner, value and key kinds ---- */
+#define FW_TUMBLING 0 /* api/windowing/assigners/TumblingEventTimeWindows.java:53-73 */
+#define FW_SLIDING 1  /* api/windowing/assigners/SlidingEventTimeWindows.java:57-81   */
+#define FW_SESSION 2  /* api/windowing/assigners/EventTimeSessionWindows.java:59-61  */
+
+#define FW_VAL_I64 0 /* Long field: sum wraps at 64 bits (SumFunction.LongSum)            */
+#define FW_VAL_I32 1 /* Integer field: sum wraps at 32 bits (SumFunction.IntSum)          */
+#define FW_VAL_F64 2 /* Double field: min/max by Double.compare, sum within 1e-6 relative */
+
+#define FW_KEY_LONG 0   /* key is a Long: hashCode = (int)(v ^ (v >>> 32))               */
+#define FW_KEY_INT 1    /* key is an Integer: hashCode = value                              */
+#define FW_KEY_HASHED 2 /* caller passes key.hashCode() per record (String, Tuple, POJO);
+                           the i64 key column is then the caller's dictionary id of the key */
+
+/* Operator configuration: the arguments of the WindowOperator constructor
+ * (runtime/operators/windowing/WindowOperator.java:179-212) restricted to the GPU-eligible
+ * shapes (event-time assigner above, EventTimeTrigger or PurgingTrigger.of(EventTimeTrigger),
+ * AggregatingStateDescriptor/ReducingStateDescriptor with the built-in count/sum/min/max
+ * accumulator), plus the keyed-backend arguments of
+ * flink-runtime/.../state/StateBackend.java:130 (numberOfKeyGroups, keyGroupRange). */
+typedef struct fw_config {
+  int32_t assigner;            /* FW_TUMBLING / FW_SLIDING / FW_SESSION                      */
+  int32_t value_type;          /* FW_VAL_*                                                   */
+  int32_t key_kind;            /* FW_KEY_*                                                   */
+  int32_t purging;             /* 1 = PurgingTrigger.of(EventTimeTrigger.create())           */
+  int32_t side_output;         /* 1 = late records go to the side output (lateDataOutputTag) */
+  int32_t max_parallelism;     /* number of key groups (0 -> 128, ExecutionJobVertex.java:176) */
+  int32_t key_group_start;     /* KeyGroupRange owned by this handle, inclusive             */
+  int32_t key_group_end;       /*   (-1/-1 -> the whole range [0, max_parallelism-1])        */
+  int32_t device;              /* HIP device ordinal                                         */
+  int32_t sub_partitions;      /* state partitions per key group, power of two (0 = auto)   */
+  int64_t size;                /* window size (tumbling, sliding)                            */
+  int64_t slide;               /* slide (sliding)                                            */
+  int64_t offset;              /* window offset (tumbling, sliding)                          */
+  int64_t gap;                 /* session gap (session)                                      */
+  int64_t allowed_lateness;    /* WindowedStream.allowedLateness, >= 0                       */
+  int64_t expected_entries;    /* sizing hint: live (key, window) pairs (0 = default)        */
+  int64_t max_batch;           /* largest n passed to one push (0 = 1 << 24)                */
+} fw_config;
+
+typedef struct fw_op fw_op;
+
+/* Fired window rows (struct of arrays).  One row per emitted window result:
+ * the built-in AggregateFunction.getResult {count, sum, min, max} plus the key and the
+ * TimeWindow; the record timestamp of the row is end - 1 = TimeWindow.maxTimestamp()
+ * (TimestampedCollector.setAbsoluteTimestamp, WindowOperator.java:544-548).  For
+ * FW_VAL_F64, sum/min/max hold IEEE-754 bit patterns. */
+typedef struct fw_rows {
+  int64_t* key;
+  int64_t* start;
+  int64_t* end;
+  int64_t* count;
+  int64_t* sum;
+  int64_t* min;
+  int64_t* max;
+} fw_rows;
+
+/* Late records routed to the side output (WindowOperator.sideOutput, :556-558). */
+typedef struct fw_side_rows {
+  int64_t* key;
+  int64_t* ts;
+  int64_t* val;
+} fw_side_rows;
+
+typedef struct fw_stats {
+  int64_t records_in;             /* numRecordsIn                                            */
+  int64_t late_records_dropped;   /* numLateRecordsDropped (WindowOperator.java:138-140,418) */
+  int64_t keyed_state_entries;    /* numKeyedStateEntries of "window-contents"               */
+  int64_t event_time_timers;      /* numEventTimeTimers                                      */
+  int64_t current_watermark;      /* InternalTimerService.currentWatermark()                 */
+  int64_t fired_rows_total;       /* all rows emitted since creation                         */
+  int64_t pending_rows;           /* rows emitted and not yet drained                        */
+  int64_t pending_side_rows;      /* side-output rows not yet drained                        */
+  int64_t table_capacity;         /* slots in the HBM state table                            */
+  int64_t table_grows;            /* times the table was resized                             */
+  int64_t slow_path_records;      /* records replayed in arrival order (late firing / drop)  */
+  int64_t state_merges;           /* pre-aggregated (key, window) deltas merged into HBM       */
+} fw_stats;
+
+/* Lifecycle — StreamOperator.setup/open/close/dispose (api/operators/StreamOperator.java:57-127). */
+int fw_create(const fw_config* cfg, fw_op** out);
+void fw_destroy(fw_op* op);
+const char* fw_last_error(const fw_op* op);
+
+/* processElement for a micro-batch (WindowOperator.java:291-421).
+ *   fw_push_batch:        host buffers (a Java DirectByteBuffer in native byte order);
+ *                         copied to HBM before the call returns.
+ *   fw_push_batch_device: device pointers already resident in HBM on the handle's device;
+ *                         enqueued on the handle's stream, the buffers must stay valid until
+ *                         the next fw_* call on the handle returns.
+ * key_hash may be NULL unless key_kind == FW_KEY_HASHED.  val points to n int64 (FW_VAL_I64 /
+ * FW_VAL_I32, the latter already sign-extended) or n doubles (FW_VAL_F64). */
+int fw_push_batch(fw_op* op, const int64_t* key, const int64_t* ts, const void* val, const int32_t* key_hash,
+                  int64_t n);
+int fw_push_batch_device(fw_op* op, const int64_t* key, const int64_t* ts, const void* val, const int32_t* key_hash,
+                         int64_t n);
+
+/* processWatermark: fires every (key, window) whose event-time timer is <= wm, clears state
+ * whose cleanup time (maxTimestamp + allowedLateness, WindowOperator.java:637-644) is <= wm,
+ * and returns the number of rows now pending (emitted since the last drain, including
+ * late firings emitted while processing elements).  Rows pending at this point all precede
+ * the watermark in the operator's output (AbstractStreamOperator.java:735-740). */
+int fw_advance_watermark(fw_op* op, int64_t wm, int64_t* n_pending_rows);
+
+/* Pending output.  *_host copy into caller-owned host arrays of capacity cap and clear the
+ * pending set; fw_rows_device exposes the pending rows in HBM without copying (valid until the
+ * next fw_* call) and fw_clear_pending drops them. */
+int fw_pending(fw_op* op, int64_t* n_rows, int64_t* n_side_rows);
+int fw_drain_rows(fw_op* op, const fw_rows* host_dst, int64_t cap, int64_t* n);
+int fw_drain_side(fw_op* op, const fw_side_rows* host_dst, int64_t cap, int64_t* n);
+int fw_rows_device(fw_op* op, fw_rows* dev_view, int64_t* n);
+int fw_clear_pending(fw_op* op);
+
+int fw_get_stats(fw_op* op, fw_stats* out);
+
+/* Per-kernel timing with HIP events recorded around every launch on the handle's stream
+ * (rocprofv3 --kernel-trace measures the same launches from outside).  Kernel kinds, in order:
+ * classify_hist, scan, scatter, aggregate, slow, fire.  fw_profile_read returns accumulated
+ * milliseconds and launch counts per kind (arrays of FW_NUM_KERNELS) and optionally resets them. */
+#define FW_NUM_KERNELS 6
+int fw_profile(fw_op* op, int enable);
+int fw_profile_read(fw_op* op, double* ms, int64_t* launches, int reset);
+const char* fw_kernel_name(int kind);
+int fw_synchronize(fw_op* op);
+void* fw_stream(fw_op* op); /* the hipStream_t the handle enqueues on */
+
+/* Key routing (both sides of keyBy).
+ *   fw_key_groups_device: kg[i] = KeyGroupRangeAssignment.assignToKeyGroup(key_i, maxParallelism)
+ *     (flink-runtime/.../state/KeyGroupRangeAssignment.java:58-71, MathUtils.java:134-154).
+ *   fw_route_device: KeyGroupStreamPartitioner.selectChannels (runtime/partitioner/
+ *     KeyGroupStreamPartitioner.java:53-65): groups the batch by destination operator index
+ *     computeOperatorIndexForKeyGroup(maxPar, parallelism, kg) (KeyGroupRangeAssignment.java:115-117),
+ *     keeping arrival order inside each destination; writes the reordered columns and
+ *     counts[parallelism] (int64, device).  All pointers are device pointers on `device`;
+ *     the call is asynchronous on `stream` (a hipStream_t, NULL = default stream). */
+int fw_key_groups_device(const int64_t* key, const int32_t* key_hash, int32_t key_kind, int64_t n,
+                         int32_t max_parallelism, int32_t* kg_out, void* stream);
+int fw_route_device(const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* key_hash,
+                    int32_t key_kind, int64_t n, int32_t max_parallelism, int32_t parallelism, int64_t* key_out,
+                    int64_t* ts_out, int64_t* val_out, int32_t* hash_out, int64_t* counts, void* scratch,
+                    int64_t scratch_bytes, void* stream);
+int64_t fw_route_scratch_bytes(int64_t n, int32_t parallelism);
+
+/* Synthetic source used by the benchmarks (the same counter-based generator as the CPU
+ * baseline and the tests): record i of stream `seed` has
+ *   key = splitmix64(seed ^ 4i) mod num_keys  (uniform)  or Zipf(zipf_s) over num_keys,
+ *   val = (int32) splitmix64(seed ^ (4i+1)),
+ *   ts  = ts_base + floor(i * 1000 / rate) - (splitmix64(seed ^ (4i+2)) mod jitter).
+ * Writes records [first, first + n) to device buffers; returns max(ts) over them in *max_ts
+ * (device int64, may be NULL).  zipf_cdf (device, num_keys doubles) is used when non-NULL. */
+int fw_generate_device(uint64_t seed, int64_t first, int64_t n, int64_t num_keys, const double* zipf_cdf,
+                       int64_t ts_base, int64_t rate, int64_t jitter, int64_t* key, int64_t* ts, int64_t* val,
+                       int64_t* max_ts, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLINK_WINDOW_H */

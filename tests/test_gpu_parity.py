@@ -1,0 +1,204 @@
+"""GPU parity: GpuWindowOperator (libflinkwin.so, HIP gfx950) against the oracle and the reference KATs.
+Bar: bit-exact keys, window bounds, counts and integer sum/min/max; f64 sums within 1e-6 relative."""
+import numpy as np
+import pytest
+
+from flink_amd import (EventTimeSessionWindows, KeyGroupRange, PurgingTrigger, SlidingEventTimeWindows,
+                       EventTimeTrigger, TumblingEventTimeWindows)
+from flink_amd.datagen import generate_host
+from flink_amd.windowing import CountSumMinMax
+from oracle import oracle as orc
+from tests.kat_util import expected_counters, load_kats, replay, row_counters
+from tests.parity_util import assert_rows_equal, assert_side_equal
+
+pytestmark = pytest.mark.gpu
+
+KATS = load_kats()
+_VT = {"i64": "long", "i32": "int", "f64": "double"}
+
+
+def _gpu_op(assigner, size=0, slide=0, offset=0, gap=0, lateness=0, purging=False, side_output=False,
+            value_type="i64", **kw):
+    from flink_amd.operator import GpuWindowOperator
+    if assigner == "tumbling":
+        a = TumblingEventTimeWindows.of(size, offset)
+    elif assigner == "sliding":
+        a = SlidingEventTimeWindows.of(size, slide, offset)
+    else:
+        a = EventTimeSessionWindows.with_gap(gap)
+    trig = PurgingTrigger.of(EventTimeTrigger.create()) if purging else EventTimeTrigger.create()
+    return GpuWindowOperator(a, CountSumMinMax(_VT[value_type]), trig, allowed_lateness=lateness,
+                             side_output=side_output, **kw)
+
+
+def _from_case_cfg(cfg):
+    return _gpu_op(cfg["assigner"], cfg["size"], cfg["slide"], cfg["offset"], cfg["gap"], cfg["lateness"],
+                   cfg["purging"], cfg["side_output"], cfg["value_type"])
+
+
+@pytest.mark.parametrize("case", KATS["operator_cases"], ids=[c["name"] for c in KATS["operator_cases"]])
+def test_gpu_reference_kats(case):
+    keymap = KATS["keys"]
+    op = replay(case, keymap, _from_case_cfg, flush_elements=True)
+    got, got_side = row_counters(op.rows(), op.side_rows(), case, with_window=True)
+    exp, exp_side = expected_counters(case, keymap, with_window=True)
+    assert got == exp
+    assert got_side == exp_side
+    op.close()
+
+
+def _run_both(cfg, batches, wms, **gpu_kw):
+    gpu = _gpu_op(**cfg, **gpu_kw)
+    ref = orc.WindowOperatorOracle(**cfg)
+    for (k, t, v), wm in zip(batches, wms):
+        gpu.process(k, t, v)
+        ref.process(k, t, v)
+        gpu.watermark(wm)
+        ref.watermark(wm)
+    out = gpu.rows(), ref.rows(), gpu.side_rows(), ref.side_rows(), gpu.late_dropped, ref.late_dropped
+    st = gpu.stats()
+    assert st["keyed_state_entries"] == ref.num_state_entries or cfg.get("purging") or cfg["assigner"] == "session"
+    gpu.close()
+    return out
+
+
+def _stream(n, batch, num_keys, bound, jitter, rate, seed=0x5EED, value_type="i64", zipf=None, final=True):
+    keys, ts, vals = generate_host(seed, 0, n, num_keys, ts_base=1_000_000, rate=rate, jitter=jitter, zipf_s=zipf)
+    if value_type == "f64":
+        vals = ((vals & 0xFFFFF).astype(np.float64) / 7.0)
+    batches, wms, mx = [], [], -(1 << 63)
+    for b in range(0, n, batch):
+        sl = slice(b, min(n, b + batch))
+        batches.append((keys[sl], ts[sl], vals[sl]))
+        mx = max(mx, int(ts[sl].max()))
+        wms.append(mx - bound)
+    if final:
+        batches.append((keys[:0], ts[:0], vals[:0]))
+        wms.append((1 << 63) - 1)
+    return batches, wms
+
+
+CONFIGS = [
+    dict(assigner="tumbling", size=1000),
+    dict(assigner="tumbling", size=1000, offset=250, value_type="i32"),
+    dict(assigner="tumbling", size=1000, value_type="f64"),
+    dict(assigner="sliding", size=3000, slide=1000),
+    dict(assigner="sliding", size=2500, slide=1000, offset=300, value_type="f64"),
+    dict(assigner="tumbling", size=1000, lateness=700),
+    dict(assigner="tumbling", size=1000, lateness=700, purging=True, side_output=True),
+    dict(assigner="sliding", size=2000, slide=500, lateness=300, side_output=True),
+    dict(assigner="session", gap=300),
+    dict(assigner="session", gap=300, lateness=200, purging=True, side_output=True),
+    dict(assigner="session", gap=300, lateness=400, value_type="f64"),
+]
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=[str(i) for i in range(len(CONFIGS))])
+def test_gpu_vs_oracle_out_of_order(cfg):
+    # heavy disorder (jitter 1.5 s against a 0.4 s bound) exercises late drops, late firings and
+    # partially late sliding records; rate 1e5/s over 5000 keys keeps sessions open and merging
+    vt = cfg.get("value_type", "i64")
+    batches, wms = _stream(120_000, 10_000, 5000, bound=400, jitter=1500, rate=100_000, value_type=vt)
+    g, r, gs, rs, gl, rl = _run_both(cfg, batches, wms)
+    assert_rows_equal(g, r, _VT[vt])
+    assert_side_equal(gs, rs)
+    assert gl == rl
+
+
+def test_gpu_vs_oracle_c2_shape():
+    # configs[1] shape at parity size: 2^22 records, 1M uniform Long keys, 1 s tumbling,
+    # bounded out-of-orderness 200 ms, count/sum/min/max
+    cfg = dict(assigner="tumbling", size=1000)
+    batches, wms = _stream(1 << 22, 1 << 20, 1_000_000, bound=200, jitter=200, rate=100_000_000)
+    g, r, gs, rs, gl, rl = _run_both(cfg, batches, wms)
+    assert len(g) > 1_000_000
+    assert_rows_equal(g, r)
+    assert gl == rl == 0
+
+
+def test_gpu_zipf_hot_keys():
+    cfg = dict(assigner="tumbling", size=100)
+    batches, wms = _stream(400_000, 50_000, 100_000, bound=50, jitter=100, rate=1_000_000, zipf=1.1)
+    g, r, *_ = _run_both(cfg, batches, wms)
+    assert_rows_equal(g, r)
+
+
+def test_gpu_table_growth():
+    # tiny initial table: forces overflow parking and region growth mid-stream
+    cfg = dict(assigner="tumbling", size=10_000)
+    batches, wms = _stream(300_000, 100_000, 200_000, bound=100, jitter=100, rate=1_000_000)
+    g, r, *_ = _run_both(cfg, batches, wms, expected_entries=1000)
+    assert_rows_equal(g, r)
+
+
+def test_gpu_key_group_range_subtask():
+    # one subtask of parallelism 4 (KeyedOneInputStreamOperatorTestHarness(maxPar, numSubtasks, idx))
+    from flink_amd.keygroups import compute_key_group_range_for_operator_index
+    from flink_amd.operator import GpuWindowOperator
+    kgr = compute_key_group_range_for_operator_index(128, 4, 2)
+    keys, ts, vals = generate_host(7, 0, 50_000, 10_000, ts_base=0, rate=100_000, jitter=0)
+    kg = orc.key_groups_long(keys, 128)
+    sel = (kg >= kgr.start_key_group) & (kg <= kgr.end_key_group)
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(100), key_group_range=kgr)
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=100)
+    op.process(keys[sel], ts[sel], vals[sel])
+    ref.process(keys[sel], ts[sel], vals[sel])
+    op.watermark((1 << 63) - 1)
+    ref.watermark((1 << 63) - 1)
+    assert_rows_equal(op.rows(), ref.rows())
+    # a key outside the range is an error, as in the heap backend
+    bad = keys[~sel][:1]
+    with pytest.raises(RuntimeError):
+        op.process(bad, ts[:1], vals[:1])
+
+
+def test_gpu_no_timestamp_marker():
+    from flink_amd.operator import GpuWindowOperator
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(100))
+    with pytest.raises(RuntimeError, match="Long.MIN_VALUE"):
+        op.process(np.array([1]), np.array([-(1 << 63)]), np.array([1]))
+
+
+def test_gpu_device_resident_push_and_generator():
+    import torch
+    from flink_amd.datagen import generate_device
+    from flink_amd.operator import GpuWindowOperator
+    n = 1 << 20
+    k, t, v, mx = generate_device(0x5EED, 0, n, 1_000_000, ts_base=0, rate=100_000_000, jitter=200)
+    hk, ht, hv = generate_host(0x5EED, 0, n, 1_000_000, ts_base=0, rate=100_000_000, jitter=200)
+    assert np.array_equal(k.cpu().numpy(), hk) and np.array_equal(t.cpu().numpy(), ht)
+    assert np.array_equal(v.cpu().numpy(), hv) and int(mx.item()) == int(ht.max())
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(1000))
+    op.process(k, t, v)
+    op.watermark((1 << 63) - 1)
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000)
+    ref.process(hk, ht, hv)
+    ref.watermark((1 << 63) - 1)
+    assert_rows_equal(op.rows(), ref.rows())
+    del torch
+
+
+def test_gpu_key_groups_and_route():
+    import ctypes
+    import torch
+    from flink_amd import _native as N
+    from flink_amd.exchange import route_device
+    keys, ts, vals = generate_host(11, 0, 300_001, 1 << 40, ts_base=0, rate=1000, jitter=0)
+    dk = torch.from_numpy(keys).cuda()
+    kg = torch.empty(len(keys), dtype=torch.int32, device="cuda")
+    N.check(N.lib().fw_key_groups_device(dk.data_ptr(), None, N.FW_KEY_LONG, len(keys), 128, kg.data_ptr(), None))
+    torch.cuda.synchronize()
+    assert np.array_equal(kg.cpu().numpy(), orc.key_groups_long(keys, 128))
+    for par in (1, 2, 3, 8):
+        cols, counts = route_device(dk, torch.from_numpy(ts).cuda(), torch.from_numpy(vals).cuda(), 128, par)
+        counts = counts.cpu().numpy()
+        rk = cols[0].cpu().numpy()
+        dest = orc.key_groups_long(keys, 128).astype(np.int64) * par // 128
+        off = 0
+        for d in range(par):
+            sel = dest == d
+            assert counts[d] == sel.sum()
+            # stable: arrival order kept inside each destination
+            assert np.array_equal(rk[off:off + counts[d]], keys[sel])
+            off += counts[d]
+    del ctypes

@@ -1,0 +1,76 @@
+"""CPU-side checks of the C-ABI boundary: the library loads, exports every symbol include/flink_window.h
+declares, and validates configurations exactly as the reference's constructors do (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from flink_amd import _native as N
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "flink_window.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(fw_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_boundary():
+    fns = declared_functions()
+    for required in ("fw_create", "fw_push_batch", "fw_push_batch_device", "fw_advance_watermark", "fw_destroy",
+                     "fw_last_error", "fw_get_stats", "fw_route_device", "fw_key_groups_device"):
+        assert required in fns
+
+
+def test_library_exports_every_declared_symbol():
+    L = N.lib()
+    fns = declared_functions()
+    missing = [f for f in fns if not hasattr(L, f)]
+    assert not missing, missing
+    # and the Python binding types every one of them
+    assert set(fns) == set(N.SIGNATURES), set(fns) ^ set(N.SIGNATURES)
+
+
+def _create(**kw):
+    c = N.FwConfig()
+    for k, v in kw.items():
+        setattr(c, k, v)
+    h = ctypes.c_void_p()
+    rc = N.lib().fw_create(ctypes.byref(c), ctypes.byref(h))
+    msg = N.lib().fw_last_error(h).decode()
+    N.lib().fw_destroy(h)
+    return rc, msg
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(assigner=N.FW_TUMBLING, size=100, offset=100), "TumblingEventTimeWindows parameters must satisfy"),
+    (dict(assigner=N.FW_TUMBLING, size=-1), "TumblingEventTimeWindows parameters must satisfy"),
+    (dict(assigner=N.FW_SLIDING, size=100, slide=10, offset=10), "SlidingEventTimeWindows parameters must"),
+    (dict(assigner=N.FW_SLIDING, size=0, slide=10), "SlidingEventTimeWindows parameters must"),
+    (dict(assigner=N.FW_SESSION, gap=0), "EventTimeSessionWindows parameters must satisfy"),
+    (dict(assigner=N.FW_TUMBLING, size=10, allowed_lateness=-1), "The allowed lateness cannot be negative"),
+    (dict(assigner=N.FW_TUMBLING, size=10, max_parallelism=(1 << 15) + 1), "Operator parallelism not within"),
+    (dict(assigner=N.FW_TUMBLING, size=10, key_group_start=5, key_group_end=200), "invalid KeyGroupRange"),
+])
+def test_create_rejects_invalid_config(kw, msg):
+    rc, m = _create(**kw)
+    assert rc == N.FW_ERR_ARG
+    assert msg in m
+
+
+def test_kernel_names():
+    names = [N.lib().fw_kernel_name(i).decode() for i in range(N.FW_NUM_KERNELS)]
+    assert names == ["k_classify_hist", "k_scan", "k_scatter", "k_aggregate", "k_slow", "k_fire"]
+
+
+def test_route_scratch_size_positive():
+    assert N.lib().fw_route_scratch_bytes(1 << 20, 8) > 8 * 32 * 4
+
+
+def test_struct_layouts_match_header():
+    # fw_config: 10 int32 + 7 int64 = 96 bytes; fw_rows 7 pointers; fw_stats 12 int64
+    assert ctypes.sizeof(N.FwConfig) == 96
+    assert ctypes.sizeof(N.FwRows) == 56
+    assert ctypes.sizeof(N.FwStats) == 12 * 8
