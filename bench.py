@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--sub-partitions", type=int, default=0, help="state partitions per key group (0 = auto)")
     args = ap.parse_args()
 
     import torch
@@ -76,7 +77,8 @@ def main():
     op = GpuWindowOperator(TumblingEventTimeWindows.of(args.window), key_group_range=exch.key_group_range,
                            device=local_rank, max_parallelism=max_par,
                            expected_entries=2 * args.keys // world,
-                           max_batch=args.batch if world == 1 else 2 * args.batch)
+                           max_batch=args.batch if world == 1 else 2 * args.batch,
+                           sub_partitions=args.sub_partitions)
     steps_total = args.warmup + args.steps
     seed = 0x5EED
     batches, local_max = [], []

@@ -1,24 +1,26 @@
 // fw_device.hip — HIP kernels (gfx950) of the MI355X keyed event-time window operator.
 //
 // Per micro-batch (fw_push_*), with the watermark wm constant over the batch:
-//   k_classify_hist  — KeyGroupRangeAssignment murmur hash -> state partition, window assignment
-//                      and lateness class of every record; per-tile partition histogram.
-//   k_scan_*         — exclusive scan of the (partition, tile) histogram.
-//   k_scatter        — records of the order-independent class ("normal": every window of the
-//                      record ends after wm) scattered into per-partition runs; records that need
-//                      arrival order (late firing, partially late, sessions) compacted in order
-//                      into the ordered list; fully late records to the side output / counter.
-//   k_aggregate      — one workgroup per state partition: LDS open-addressing pre-aggregation of
-//                      the partition's (key, window) accumulators (64-bit LDS atomics), flushed
-//                      into the partition's HBM region with plain read-modify-write (the region
-//                      is owned by exactly one workgroup, so no global atomics on the data).
-//   k_slow           — ordered replay of the ordered list, one thread per key, element by element
-//                      exactly as WindowOperator.processElement (WindowOperator.java:291-421),
-//                      including MergingWindowSet.addWindow for sessions.
+//   k_classify_hist   — KeyGroupRangeAssignment murmur hash -> state partition, window assignment
+//                       and lateness class of every record; per-tile partition histogram.
+//   k_scan_*          — exclusive scan of the (partition, tile) histogram.
+//   k_scatter         — records of the order-independent class ("normal": every window of the
+//                       record ends after wm) scattered into per-partition runs as whole 32-byte
+//                       sectors; fully late records to the side output / late counter.
+//   k_scatter_ordered — records that need arrival order (late firing, partially late, sessions)
+//                       compacted in order into the ordered list (tiles without any exit at once).
+//   k_aggregate       — one workgroup per state partition: pre-aggregation of the partition's
+//                       (key, window) accumulators in a bucketized, fingerprint-tagged LDS hash
+//                       table (64-bit LDS atomics), flushed into the partition's HBM region with
+//                       plain read-modify-write (the region is owned by exactly one workgroup, so
+//                       no global atomics on the data).
+//   k_slow            — ordered replay of the ordered list, one thread per key, element by element
+//                       exactly as WindowOperator.processElement (WindowOperator.java:291-421),
+//                       including MergingWindowSet.addWindow for sessions.
 // Per watermark (fw_advance_watermark):
-//   k_fire           — HeapInternalTimerService.advanceWatermark as a scan/compaction: every region
-//                      whose earliest timer is <= wm emits its fired windows and is rebuilt, without
-//                      the cleaned-up entries, into the region's other buffer.
+//   k_fire            — HeapInternalTimerService.advanceWatermark as a scan/compaction: every region
+//                       whose earliest timer is <= wm emits its fired windows and is rebuilt, without
+//                       the cleaned-up entries, into the region's other buffer.
 #include <hip/hip_runtime.h>
 
 #include "../../include/flink_window.h"
@@ -28,6 +30,8 @@ namespace {
 
 constexpr int64_t LMAX = INT64_MAX;
 constexpr int64_t LMIN = INT64_MIN;
+typedef long long i64x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------ Java arithmetic
 __device__ __forceinline__ int64_t jadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
@@ -78,10 +82,23 @@ __device__ __forceinline__ int32_t partition_of(const DevCfg& c, int64_t key, in
   return (local << c.log_s) | (int32_t)sub;
 }
 
+// unsigned n / d for an invariant d via its reciprocal (m, l) from make_div_inv (Granlund and
+// Montgomery, "Division by invariant integers using multiplication", Fig. 4.1): exact for every n
+__device__ __forceinline__ uint64_t div_inv(uint64_t n, uint64_t m, int32_t l) {
+  if (l == 0) return n;  // d == 1
+  const uint64_t t1 = __umul64hi(m, n);
+  return (t1 + ((n - t1) >> 1)) >> (l - 1);
+}
+// Java's truncating `t % d` for d > 0 (sign of the dividend), through the reciprocal
+__device__ __forceinline__ int64_t jrem(int64_t t, int64_t d, uint64_t m, int32_t l) {
+  const uint64_t u = t < 0 ? (uint64_t)0 - (uint64_t)t : (uint64_t)t;  // |t|, also for Long.MIN_VALUE
+  const uint64_t r = u - div_inv(u, m, l) * (uint64_t)d;
+  return t < 0 ? -(int64_t)r : (int64_t)r;
+}
 // TimeWindow.getWindowStartWithOffset (TimeWindow.java:254-256), Java overflow semantics
-__device__ __forceinline__ int64_t wstart(int64_t ts, int64_t off, int64_t size) {
+__device__ __forceinline__ int64_t wstart(int64_t ts, int64_t off, int64_t size, uint64_t m, int32_t l) {
   int64_t t = jadd(jsub(ts, off), size);
-  return jsub(ts, t % size);
+  return jsub(ts, jrem(t, size, m, l));
 }
 // WindowOperator.cleanupTime (WindowOperator.java:637-644) of window [., end)
 __device__ __forceinline__ int64_t cleanup_of(int64_t end, int64_t lateness) {
@@ -107,10 +124,10 @@ enum { CLS_NORMAL = 0, CLS_SLOW = 1, CLS_LATE = 2, CLS_SKIP = 3, CLS_BADTS = 4 }
 // Windows of a record, newest first (SlidingEventTimeWindows.java:71-75 loop order).
 __device__ __forceinline__ int num_windows(const DevCfg& c, int64_t ts, int64_t* last_start) {
   if (c.assigner == FW_TUMBLING) {
-    *last_start = wstart(ts, c.offset, c.size);
+    *last_start = wstart(ts, c.offset, c.size, c.mag_size, c.l_size);
     return 1;
   }
-  int64_t last = wstart(ts, c.offset, c.slide);
+  int64_t last = wstart(ts, c.offset, c.slide, c.mag_slide, c.l_slide);
   *last_start = last;
   int k = 0;
   const int64_t lo = jsub(ts, c.size);
@@ -118,11 +135,17 @@ __device__ __forceinline__ int num_windows(const DevCfg& c, int64_t ts, int64_t*
   return k;
 }
 
-__device__ __forceinline__ int classify(const DevCfg& c, int64_t wm, int64_t ts) {
+// class of a record against watermark wm; for CLS_NORMAL also its windows (newest start, count)
+__device__ __forceinline__ int classify(const DevCfg& c, int64_t wm, int64_t ts, int64_t* last_out = nullptr,
+                                        int* k_out = nullptr) {
   if (c.assigner == FW_SESSION) return CLS_SLOW;
   if (ts == LMIN) return CLS_BADTS;  // TumblingEventTimeWindows.java:69-71
   int64_t last;
   int k = num_windows(c, ts, &last);
+  if (last_out) {
+    *last_out = last;
+    *k_out = k;
+  }
   if (k == 0) return jadd(ts, c.lateness) <= wm ? CLS_LATE : CLS_SKIP;
   const int64_t newest_end = jadd(last, c.size);
   const int64_t oldest_end = jadd(jsub(last, (int64_t)(k - 1) * c.slide), c.size);
@@ -132,10 +155,23 @@ __device__ __forceinline__ int classify(const DevCfg& c, int64_t wm, int64_t ts)
   return CLS_SLOW;
 }
 
-__device__ __forceinline__ uint32_t slot_hash(const DevCfg& c, int64_t key, int64_t start) {
+// slot hash of (key, window): low 32 bits pick the slot, bits 40..63 are the state-word fingerprint.
+// Sessions hash the key only, so every in-flight session of a key sits on one probe chain.
+__device__ __forceinline__ uint64_t slot_hash(const DevCfg& c, int64_t key, int64_t start) {
   uint64_t h = (uint64_t)key * 0x9E3779B97F4A7C15ull;
   if (c.assigner != FW_SESSION) h ^= fmix64((uint64_t)start + 0x632BE59BD9B4E019ull);
-  return (uint32_t)fmix64(h);
+  return fmix64(h);
+}
+__device__ __forceinline__ uint32_t tag_of(uint64_t h) { return (uint32_t)(h >> 40) << 8; }
+__device__ __forceinline__ uint32_t live_word(uint64_t h) { return SLOT_LIVE | tag_of(h); }
+
+// a[j] for a runtime j without demoting the register array to scratch (select chain)
+template <int N>
+__device__ __forceinline__ int64_t pick(const int64_t (&a)[N], int j) {
+  int64_t r = a[0];
+#pragma unroll
+  for (int q = 1; q < N; q++) r = j == q ? a[q] : r;
+  return r;
 }
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
@@ -229,37 +265,36 @@ __device__ __forceinline__ Region region_of(const DevCfg& c, const DevTable& tb,
   r.mask = (1u << c.log_r) - 1u;
   return r;
 }
-// find the live slot of (key, start, end), -1 if absent (linear probing up to the first EMPTY)
-__device__ __forceinline__ int32_t region_find(const Region& r, uint32_t h, int64_t key, int64_t start, int64_t end) {
+// find the live slot of (key, start, end), -1 if absent (linear probing up to the first EMPTY).
+// The fingerprint in the state word skips foreign slots without touching their entries.
+__device__ __forceinline__ int32_t region_find(const Region& r, uint64_t h, int64_t key, int64_t start, int64_t end) {
+  const uint32_t want = live_word(h);
   for (uint32_t i = 0; i <= r.mask; i++) {
-    const uint32_t s = (h + i) & r.mask;
+    const uint32_t s = ((uint32_t)h + i) & r.mask;
     const uint32_t st = ld_state(r.state + s);
     if (st == SLOT_EMPTY) return -1;
-    if (st == SLOT_LIVE) {
+    if (st == want) {
       const Entry& e = r.ent[s];
       if (e.key == key && e.start == start && e.end == end) return (int32_t)s;
     }
   }
   return -1;
 }
-// claim the first EMPTY slot of the probe sequence (state -> `to`), -1 if the region is full
-__device__ __forceinline__ int32_t region_claim(const Region& r, uint32_t h, uint32_t to) {
+// claim the first EMPTY slot of the probe sequence (state -> `word`), -1 if the region is full
+__device__ __forceinline__ int32_t region_claim(const Region& r, uint64_t h, uint32_t word) {
   for (uint32_t i = 0; i <= r.mask; i++) {
-    const uint32_t s = (h + i) & r.mask;
+    const uint32_t s = ((uint32_t)h + i) & r.mask;
     if (ld_state(r.state + s) != SLOT_EMPTY) continue;
-    if (atomicCAS(r.state + s, SLOT_EMPTY, to) == SLOT_EMPTY) return (int32_t)s;
+    if (atomicCAS(r.state + s, SLOT_EMPTY, word) == SLOT_EMPTY) return (int32_t)s;
   }
   return -1;
-}
-__device__ __forceinline__ void publish_live(uint32_t* st) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // entry bytes before the LIVE state word
-  __hip_atomic_store(st, SLOT_LIVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ============================================================================== kernels
 
 // ---- K1: classify + partition histogram.  hist is (P+1) x T, partition-major; row P counts
-// the records of each tile that go to the ordered path.
+// the records of each tile that go to the ordered path (scanned with the partitions), row P+1
+// keeps that count unscanned for k_scatter_ordered.
 __global__ __launch_bounds__(FW_TILE_THREADS) void k_classify_hist(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
                                                                    const int64_t* __restrict__ ts,
                                                                    const int32_t* __restrict__ kh, int64_t n, int32_t T,
@@ -271,25 +306,41 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_classify_hist(DevCfg c, int
   const int64_t end = min(n, base + (int64_t)FW_TILE);
   int bad_kg = 0, bad_ts = 0;
   unsigned slow = 0;
-  for (int64_t i = base + threadIdx.x; i < end; i += blockDim.x) {
-    const int64_t k = key[i];
-    const int32_t p = partition_of(c, k, key_hash_of(c.key_kind, k, kh, i));
-    if (p < 0) {
-      bad_kg++;
-      continue;
+  for (int64_t b = base; b < end; b += (int64_t)blockDim.x * FW_RPT) {
+    int64_t k[FW_RPT], t[FW_RPT];
+    int32_t h[FW_RPT];
+#pragma unroll
+    for (int j = 0; j < FW_RPT; j++) {  // all loads in flight before any use
+      const int64_t i = b + (int64_t)j * blockDim.x + threadIdx.x;
+      k[j] = i < end ? key[i] : 0;
+      t[j] = i < end ? ts[i] : 0;
+      h[j] = i < end && c.key_kind == FW_KEY_HASHED ? kh[i] : 0;
     }
-    const int cls = classify(c, wm, ts[i]);
-    if (cls == CLS_NORMAL)
-      atomicAdd(&lh[p], 1u);
-    else if (cls == CLS_SLOW)
-      slow++;
-    else if (cls == CLS_BADTS)
-      bad_ts++;
+#pragma unroll
+    for (int j = 0; j < FW_RPT; j++) {
+      const int64_t i = b + (int64_t)j * blockDim.x + threadIdx.x;
+      if (i >= end) continue;
+      const int32_t p = partition_of(c, k[j], c.key_kind == FW_KEY_HASHED ? h[j] : key_hash_of(c.key_kind, k[j], kh, i));
+      if (p < 0) {
+        bad_kg++;
+        continue;
+      }
+      const int cls = classify(c, wm, t[j]);
+      if (cls == CLS_NORMAL)
+        atomicAdd(&lh[p], 1u);
+      else if (cls == CLS_SLOW)
+        slow++;
+      else if (cls == CLS_BADTS)
+        bad_ts++;
+    }
   }
   if (slow) atomicAdd(&lh[c.P], slow);
   __syncthreads();
   for (int i = threadIdx.x; i <= c.P; i += blockDim.x) hist[(int64_t)i * T + blockIdx.x] = lh[i];
-  if (threadIdx.x == 0 && lh[c.P]) atomicAdd(&st->slow_count, (unsigned long long)lh[c.P]);
+  if (threadIdx.x == 0) {
+    hist[(int64_t)(c.P + 1) * T + blockIdx.x] = lh[c.P];
+    if (lh[c.P]) atomicAdd(&st->slow_count, (unsigned long long)lh[c.P]);
+  }
   if (bad_kg) atomicAdd(&st->kg_errors, bad_kg);
   if (bad_ts) atomicAdd(&st->ts_errors, bad_ts);
 }
@@ -298,7 +349,6 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_classify_hist(DevCfg c, int
 constexpr int SCAN_T = 1024, SCAN_E = 4, SCAN_B = SCAN_T * SCAN_E;
 
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sw, uint32_t* total) {
-  // wave inclusive scan
   const int lane = __lane_id(), wid = threadIdx.x >> 6;
   uint32_t x = v;
 #pragma unroll
@@ -362,32 +412,81 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_add(uint32_t* data, int64_t m, 
     if (base + e < m) data[base + e] += add;
 }
 
-// ---- K2: scatter.  Normal records -> their partition's run (any order inside the run);
-// ordered-path records -> the ordered list, arrival order kept; late records -> side / counter.
+// ---- K2: scatter.  Normal records -> their partition's run (any order inside the run), one
+// 32-byte sector per record; late records -> side output / counter.
 __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
                                                              const int64_t* __restrict__ ts,
                                                              const int64_t* __restrict__ val,
                                                              const int32_t* __restrict__ kh, int64_t n, int32_t T,
-                                                             const uint32_t* __restrict__ offs, int64_t* __restrict__ pk,
-                                                             int64_t* __restrict__ pt, int64_t* __restrict__ pv,
-                                                             int64_t* __restrict__ sk, int64_t* __restrict__ stt,
-                                                             int64_t* __restrict__ sv, int32_t* __restrict__ skh,
+                                                             const uint32_t* __restrict__ offs, PRec* __restrict__ part,
                                                              DevSide side, Status* st) {
-  extern __shared__ uint32_t sm[];
-  uint32_t* base = sm;              // P
-  uint32_t* cnt = sm + c.P;         // P
-  uint32_t* wtot = sm + 2 * c.P;    // 16 waves + 1
-  for (int i = threadIdx.x; i < c.P; i += blockDim.x) {
-    base[i] = offs[(int64_t)i * T + blockIdx.x];
-    cnt[i] = 0;
-  }
-  const uint32_t slow_base = offs[(int64_t)c.P * T + blockIdx.x] - offs[(int64_t)c.P * T];
+  extern __shared__ uint32_t base[];  // P: next free slot of each partition's run for this tile
+  for (int i = threadIdx.x; i < c.P; i += blockDim.x) base[i] = offs[(int64_t)i * T + blockIdx.x];
   __syncthreads();
+  const int64_t tbase = (int64_t)blockIdx.x * FW_TILE;
+  const int64_t tend = min(n, tbase + (int64_t)FW_TILE);
+  unsigned long long late = 0;
+  for (int64_t b = tbase; b < tend; b += (int64_t)blockDim.x * FW_RPT) {
+    int64_t k[FW_RPT], t[FW_RPT], v[FW_RPT];
+    int32_t hh[FW_RPT];
+#pragma unroll
+    for (int j = 0; j < FW_RPT; j++) {  // all loads in flight before any use
+      const int64_t i = b + (int64_t)j * blockDim.x + threadIdx.x;
+      const bool in = i < tend;
+      k[j] = in ? key[i] : 0;
+      t[j] = in ? ts[i] : 0;
+      v[j] = in ? val[i] : 0;
+      hh[j] = in && c.key_kind == FW_KEY_HASHED ? kh[i] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < FW_RPT; j++) {
+      const int64_t i = b + (int64_t)j * blockDim.x + threadIdx.x;
+      if (i >= tend) continue;
+      const int32_t h = c.key_kind == FW_KEY_HASHED ? hh[j] : key_hash_of(c.key_kind, k[j], kh, i);
+      const int32_t p = partition_of(c, k[j], h);
+      if (p < 0) continue;
+      int64_t last;
+      int nwin;
+      const int cls = classify(c, wm, t[j], &last, &nwin);
+      if (cls == CLS_NORMAL) {
+        uint32_t pos = atomicAdd(&base[p], 1u);
+        if (c.diag & (DIAG_SCATTER_NO_STORE | DIAG_SCATTER_LINEAR)) {
+          if (c.diag & DIAG_SCATTER_NO_STORE) {
+            asm volatile("" ::"v"(pos), "v"(k[j]), "v"(last), "v"(v[j]));
+            continue;
+          }
+          pos = (uint32_t)(i - tbase) + (uint32_t)tbase;
+        }
+        i64x2* dst = reinterpret_cast<i64x2*>(part + pos);
+        dst[0] = i64x2{k[j], last};
+        dst[1] = i64x2{v[j], (long long)nwin};
+      } else if (cls == CLS_LATE) {
+        if (c.side_output)
+          side_one(side, st, k[j], t[j], v[j]);
+        else
+          late++;
+      }
+    }
+  }
+  if (late) atomicAdd(&st->late_dropped, late);
+}
+
+// ---- K2b: ordered compaction of the ordered-path records of a tile (skipped by tiles that have none)
+__global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_ordered(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
+                                                                     const int64_t* __restrict__ ts,
+                                                                     const int64_t* __restrict__ val,
+                                                                     const int32_t* __restrict__ kh, int64_t n,
+                                                                     int32_t T, const uint32_t* __restrict__ offs,
+                                                                     const uint32_t* __restrict__ tile_slow,
+                                                                     int64_t* __restrict__ sk, int64_t* __restrict__ stt,
+                                                                     int64_t* __restrict__ sv, int32_t* __restrict__ skh) {
+  if (tile_slow[blockIdx.x] == 0) return;
+  __shared__ uint32_t wtot[FW_TILE_THREADS / 64];
+  const uint32_t slow_base = offs[(int64_t)c.P * T + blockIdx.x] - offs[(int64_t)c.P * T];
   const int64_t tbase = (int64_t)blockIdx.x * FW_TILE;
   const int64_t tend = min(n, tbase + (int64_t)FW_TILE);
   const int lane = __lane_id(), wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   uint32_t running = 0;
-  unsigned long long late = 0;
   for (int64_t j = tbase; j < tend; j += blockDim.x) {
     const int64_t i = j + threadIdx.x;
     int cls = CLS_SKIP;
@@ -401,13 +500,6 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter(DevCfg c, int64_t w
       p = partition_of(c, k, h);
       if (p >= 0) cls = classify(c, wm, t);
     }
-    if (cls == CLS_NORMAL) {
-      const uint32_t pos = base[p] + atomicAdd(&cnt[p], 1u);
-      pk[pos] = k;
-      pt[pos] = t;
-      pv[pos] = v;
-    }
-    // ordered compaction of the ordered-path records
     const bool is_slow = cls == CLS_SLOW;
     const uint64_t ball = __ballot(is_slow);
     if (lane == 0) wtot[wid] = (uint32_t)__popcll(ball);
@@ -427,81 +519,98 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter(DevCfg c, int64_t w
     }
     running += tot;
     __syncthreads();
-    if (cls == CLS_LATE) {
-      if (c.side_output)
-        side_one(side, st, k, t, v);
-      else
-        late++;
-    }
   }
-  if (late) atomicAdd(&st->late_dropped, late);
 }
 
-// ---- K3: per-partition LDS pre-aggregation + flush into the HBM region
+// ---- K3: per-partition LDS pre-aggregation + flush into the HBM region.
+// LDS table: FW_LDS_SLOTS slots in buckets of 4.  tag[] holds 0 = empty, 1 = being claimed, or a
+// fingerprint >= 2 of (key, window); one ds_read_b128 checks a whole bucket, so a lookup is one
+// LDS read for almost every record and the wave does not wait on a long probe tail.
+constexpr int LDS_BUCKETS = FW_LDS_SLOTS / 4;
 struct AggLds {
-  int64_t key[FW_LDS_SLOTS];
-  int64_t start[FW_LDS_SLOTS];
-  unsigned long long cnt[FW_LDS_SLOTS];
+  uint32_t tag[FW_LDS_SLOTS];
+  uint32_t cnt[FW_LDS_SLOTS];  // per LDS epoch: at most one batch of one partition, < 2^32
+  i64x2 kv[FW_LDS_SLOTS];      // {key, window start}: one ds_read_b128 per comparison
+  i64x2 mm[FW_LDS_SLOTS];      // {min, max}: one ds_read_b128 decides both conditional atomics
   int64_t sum[FW_LDS_SLOTS];
-  int64_t mn[FW_LDS_SLOTS];
-  int64_t mx[FW_LDS_SLOTS];
-  uint32_t state[FW_LDS_SLOTS];
+  uint8_t done[FW_LDS_SLOTS];  // flush bookkeeping
   int fill;
   int anyfail;
   int inserted;
-  int overflowed;
+  int pad_;
+  unsigned long long flushed;
   int64_t min_timer;
 };
-enum : uint32_t { LS_EMPTY = 0, LS_BUSY = 1, LS_READY = 2, LS_DONE = 3 };
-
-__device__ __forceinline__ uint32_t lds_hash(int64_t key, int64_t start) {
-  return (uint32_t)fmix64((uint64_t)key ^ ((uint64_t)start * 0xD6E8FEB86659FD93ull));
-}
+enum : uint32_t { LT_EMPTY = 0, LT_BUSY = 1 };
 
 // insert-or-accumulate one value into the LDS table; false when the table is at its fill limit
 // (the caller flushes and retries).  One loop, no early exit, so a lane that claims a slot
 // finishes publishing it inside the same iteration as the lanes that wait on it.
-__device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, int64_t start, int64_t v) {
-  uint32_t h = lds_hash(key, start) & (FW_LDS_SLOTS - 1);
+__device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, int64_t start, int64_t v,
+                                           int diag = 0) {
+  const uint64_t hh = fmix64((uint64_t)key ^ ((uint64_t)start * 0xD6E8FEB86659FD93ull));
+  const uint32_t fp = (uint32_t)(hh >> 32) | 2u;  // >= 2
+  uint32_t b = (uint32_t)hh & (LDS_BUCKETS - 1);
   bool done = false, ok = false;
   int guard = 0;
   while (!done) {
-    const uint32_t s = __hip_atomic_load(&L.state[h], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    int target = -1;
-    if (s == LS_READY) {
-      if (L.key[h] == key && L.start[h] == start)
-        target = (int)h;
-      else {
-        h = (h + 1) & (FW_LDS_SLOTS - 1);
-        if (++guard >= FW_LDS_SLOTS) done = true;  // full circle: table full
-      }
-    } else if (s == LS_EMPTY) {
-      if (__hip_atomic_load(&L.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= FW_LDS_FILL_LIMIT) {
-        done = true;
-      } else if (atomicCAS(&L.state[h], LS_EMPTY, LS_BUSY) == LS_EMPTY) {
-        atomicAdd(&L.fill, 1);
-        L.key[h] = key;
-        L.start[h] = start;
-        L.cnt[h] = 0;
-        L.sum[h] = 0;
-        L.mn[h] = LMAX;
-        L.mx[h] = LMIN;
-        __hip_atomic_store(&L.state[h], LS_READY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        target = (int)h;
+    asm volatile("" ::: "memory");  // re-read the bucket every iteration (it may be claimed meanwhile)
+    const u32x4 t4 = *reinterpret_cast<const u32x4*>(&L.tag[b * 4]);
+    const uint32_t tg[4] = {t4.x, t4.y, t4.z, t4.w};
+    int target = -1, empty = -1;
+    bool busy = false;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (tg[q] == fp && target < 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int s = (int)b * 4 + q;
+        const i64x2 kv = L.kv[s];
+        if (kv.x == key && kv.y == start) target = s;
+      } else if (tg[q] == LT_EMPTY && empty < 0) {
+        empty = q;
+      } else if (tg[q] == LT_BUSY) {
+        busy = true;
       }
     }
-    if (target >= 0) {
-      atomicAdd(&L.cnt[target], 1ull);
-      if (vtype == FW_VAL_F64) {
-        atomicAdd((double*)&L.sum[target], __longlong_as_double(v));
-        const int64_t sv = f64_sortable(v);
-        atomicMin((long long*)&L.mn[target], (long long)sv);
-        atomicMax((long long*)&L.mx[target], (long long)sv);
+    if (target < 0 && !busy) {
+      if (empty >= 0) {
+        if (__hip_atomic_load(&L.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= FW_LDS_FILL_LIMIT) {
+          done = true;  // table full: flush first
+        } else {
+          const int s = (int)b * 4 + empty;
+          if (atomicCAS(&L.tag[s], LT_EMPTY, LT_BUSY) == LT_EMPTY) {
+            atomicAdd(&L.fill, 1);
+            L.kv[s] = i64x2{key, start};
+            L.cnt[s] = 0;
+            L.sum[s] = 0;
+            L.mm[s] = i64x2{LMAX, LMIN};
+            __hip_atomic_store(&L.tag[s], fp, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            target = s;
+          }
+          // lost the claim race: re-read the bucket
+        }
       } else {
-        atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)v);
-        atomicMin((long long*)&L.mn[target], (long long)v);
-        atomicMax((long long*)&L.mx[target], (long long)v);
+        b = (b + 1) & (LDS_BUCKETS - 1);  // bucket full without a match
+        if (++guard >= LDS_BUCKETS) done = true;
       }
+    }
+    if (target >= 0 && (diag & DIAG_AGG_NO_ACCUM)) {
+      ok = true;
+      done = true;
+    } else if (target >= 0) {
+      atomicAdd(&L.cnt[target], 1u);
+      // min/max only change while a value beats the current extreme; a plain read first skips the
+      // atomic otherwise (the extremes only move one way, so a stale read can only cause an extra
+      // atomic, never a missed one)
+      const int64_t sv = vtype == FW_VAL_F64 ? f64_sortable(v) : v;
+      if (vtype == FW_VAL_F64)
+        atomicAdd((double*)&L.sum[target], __longlong_as_double(v));
+      else
+        atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)v);
+      const i64x2 cur = L.mm[target];
+      long long* mmp = reinterpret_cast<long long*>(&L.mm[target]);
+      if (sv < cur.x) atomicMin(mmp, (long long)sv);
+      if (sv > cur.y) atomicMax(mmp + 1, (long long)sv);
       ok = true;
       done = true;
     }
@@ -509,49 +618,58 @@ __device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, in
   return ok;
 }
 
-// merge every READY LDS slot into the partition's HBM region; resets the LDS table
+// merge every LDS slot into the partition's HBM region, then reset the LDS table.  Phase 1 updates
+// windows already in the region (distinct slots, plain read-modify-write); phase 2, after a barrier,
+// claims EMPTY slots for the new ones (so no thread ever reads an entry that is being written).
 __device__ void agg_flush(const DevCfg& c, AggLds& L, const Region& r, int32_t p, DevOverflow ov, Status* st) {
   __syncthreads();
-  // phase 1: windows already in the region: read-modify-write (distinct slots, no races)
+  if (c.diag & DIAG_AGG_NO_FLUSH) {
+    for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
+    if (threadIdx.x == 0) L.fill = 0;
+    __syncthreads();
+    return;
+  }
+  int64_t mt = LMAX;
+  unsigned long long nflush = 0;
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
-    if (L.state[h] != LS_READY) continue;
-    const int64_t k = L.key[h], s = L.start[h], e = jadd(s, c.size);
+    L.done[h] = 0;
+    if (L.tag[h] < 2) continue;
+    nflush++;
+    const i64x2 kv = L.kv[h];
+    const int64_t k = kv.x, s = kv.y, e = jadd(s, c.size);
+    mt = min(mt, jsub(e, 1));
     const int32_t slot = region_find(r, slot_hash(c, k, s), k, s, e);
     if (slot < 0) continue;
     Entry d;
+    const i64x2 mm = L.mm[h];
     d.cnt = (int64_t)L.cnt[h];
     d.sum = L.sum[h];
-    d.mn = L.mn[h];
-    d.mx = L.mx[h];
+    d.mn = mm.x;
+    d.mx = mm.y;
     Entry& x = r.ent[slot];
     Entry cur = x;
     acc_merge(c, cur, d);
     cur.meta |= FW_TIMER;
     x = cur;
-    L.state[h] = LS_DONE;
+    L.done[h] = 1;
   }
   __syncthreads();
-  // phase 2: new windows: claim an EMPTY slot
   int ins = 0;
-  unsigned long long nflush = 0;
-  int64_t mt = LMAX;
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
-    const uint32_t ls = L.state[h];
-    if (ls != LS_READY && ls != LS_DONE) continue;
-    nflush++;
-    const int64_t k = L.key[h], s = L.start[h];
+    if (L.tag[h] < 2 || L.done[h]) continue;
+    const i64x2 kv = L.kv[h], mm = L.mm[h];
+    const int64_t k = kv.x, s = kv.y;
     Entry e;
     e.key = k;
     e.start = s;
     e.end = jadd(s, c.size);
     e.cnt = (int64_t)L.cnt[h];
     e.sum = L.sum[h];
-    e.mn = L.mn[h];
-    e.mx = L.mx[h];
+    e.mn = mm.x;
+    e.mx = mm.y;
     e.meta = FW_TIMER;
-    mt = min(mt, jsub(e.end, 1));
-    if (ls == LS_DONE) continue;
-    const int32_t slot = region_claim(r, slot_hash(c, k, s), SLOT_LIVE);
+    const uint64_t hs = slot_hash(c, k, s);
+    const int32_t slot = region_claim(r, hs, live_word(hs));
     if (slot >= 0) {
       r.ent[slot] = e;
       ins++;
@@ -567,50 +685,73 @@ __device__ void agg_flush(const DevCfg& c, AggLds& L, const Region& r, int32_t p
   }
   if (ins) atomicAdd(&L.inserted, ins);
   if (mt != LMAX) atomicMin((long long*)&L.min_timer, (long long)mt);
-  if (nflush) atomicAdd(&st->merged, nflush);
+  if (nflush) atomicAdd(&L.flushed, nflush);
   __syncthreads();
-  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.state[h] = LS_EMPTY;
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
   if (threadIdx.x == 0) L.fill = 0;
   __syncthreads();
 }
 
-__global__ __launch_bounds__(FW_AGG_THREADS) void k_aggregate(DevCfg c, int64_t wm, const int64_t* __restrict__ pk,
-                                                              const int64_t* __restrict__ pt,
-                                                              const int64_t* __restrict__ pv,
+__global__ __launch_bounds__(FW_AGG_THREADS) void k_aggregate(DevCfg c, int64_t wm, const PRec* __restrict__ part,
                                                               const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
                                                               DevOverflow ov, Status* st) {
   __shared__ AggLds L;
   const int32_t p = blockIdx.x;
   const int64_t begin = offs[(int64_t)p * T], end = offs[(int64_t)(p + 1) * T];
   if (begin == end) return;
-  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.state[h] = LS_EMPTY;
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
   if (threadIdx.x == 0) {
     L.fill = 0;
     L.anyfail = 0;
     L.inserted = 0;
+    L.flushed = 0;
     L.min_timer = LMAX;
   }
   __syncthreads();
   const Region r = region_of(c, tb, p, tb.cur[p]);
-  for (int64_t rb = begin; rb < end; rb += blockDim.x) {
-    const int64_t i = rb + threadIdx.x;
-    const bool have = i < end;
-    int64_t k = 0, t = 0, v = 0, last = 0;
-    int nwin = 0;
-    if (have) {
-      k = pk[i];
-      t = pt[i];
-      v = pv[i];
-      nwin = num_windows(c, t, &last);
-    }
-    int wi = 0;
-    for (;;) {
-      while (wi < nwin) {
-        const int64_t s = jsub(last, (int64_t)wi * c.slide);
-        if (!lds_upsert(L, c.vtype, k, s, v)) break;
-        wi++;
+  for (int64_t rb = begin; rb < end; rb += (int64_t)blockDim.x * FW_AGG_RPT) {
+    int64_t k[FW_AGG_RPT], t[FW_AGG_RPT], v[FW_AGG_RPT];
+    int nw[FW_AGG_RPT];
+#pragma unroll
+    for (int j = 0; j < FW_AGG_RPT; j++) {  // all loads in flight before any use
+      const int64_t i = rb + (int64_t)j * blockDim.x + threadIdx.x;
+      i64x2 a = {0, 0}, b2 = {0, 0};
+      if (i < end) {
+        const i64x2* src = reinterpret_cast<const i64x2*>(part + i);
+        a = src[0];
+        b2 = src[1];
       }
-      if (wi < nwin) L.anyfail = 1;
+      k[j] = a.x;
+      t[j] = a.y;  // newest window start (assigned by k_scatter)
+      v[j] = b2.x;
+      nw[j] = (int)b2.y;
+    }
+    if (c.diag & DIAG_AGG_NO_LDS) {
+#pragma unroll
+      for (int j = 0; j < FW_AGG_RPT; j++) asm volatile("" ::"v"(k[j]), "v"(t[j]), "v"(v[j]), "v"(nw[j]));
+      continue;
+    }
+    // progress (record rj, window rwi) survives a flush-and-retry when the LDS table fills up;
+    // the record loop is unrolled so the register arrays are only indexed by constants
+    int rj = 0, rwi = 0;
+    for (;;) {
+      bool failed = false;
+#pragma unroll
+      for (int j = 0; j < FW_AGG_RPT; j++) {
+        if (failed || j < rj || rb + (int64_t)j * blockDim.x + threadIdx.x >= end) continue;
+        for (int wi = j == rj ? rwi : 0; wi < nw[j]; wi++) {
+          if (!lds_upsert(L, c.vtype, k[j], jsub(t[j], (int64_t)wi * c.slide), v[j], c.diag)) {
+            failed = true;
+            rj = j;
+            rwi = wi;
+            break;
+          }
+        }
+      }
+      if (failed)
+        L.anyfail = 1;
+      else
+        rj = FW_AGG_RPT;  // all done: a retry pass after another thread's flush skips every record
       __syncthreads();
       const int need = L.anyfail;
       __syncthreads();
@@ -626,6 +767,7 @@ __global__ __launch_bounds__(FW_AGG_THREADS) void k_aggregate(DevCfg c, int64_t 
     tb.live[p] = live;
     atomicMax(&st->max_live, live);
     if (L.min_timer < tb.next_timer[p]) tb.next_timer[p] = L.min_timer;
+    atomicAdd(&st->merged, L.flushed);
   }
 }
 
@@ -649,14 +791,16 @@ __device__ __forceinline__ void kill_slot(const SlowCtx& x, const Region& r, int
   __hip_atomic_store(r.state + s, SLOT_DEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   atomicSub(&x.tb.live[p], 1);
 }
-__device__ __forceinline__ int32_t new_slot(const SlowCtx& x, const Region& r, int32_t p, uint32_t h, const Entry& e) {
+// new entry: claim BUSY, write, publish LIVE with the fingerprint (readers never see a torn entry)
+__device__ __forceinline__ int32_t new_slot(const SlowCtx& x, const Region& r, int32_t p, uint64_t h, const Entry& e) {
   const int32_t s = region_claim(r, h, SLOT_BUSY);
   if (s < 0) {
     atomicOr(&x.st->flags, FW_STATUS_OVERFLOW_LOST);
     return -1;
   }
   r.ent[s] = e;
-  publish_live(r.state + s);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __hip_atomic_store(r.state + s, live_word(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int live = atomicAdd(&x.tb.live[p], 1) + 1;
   atomicMax(&x.st->max_live, live);
   return s;
@@ -673,7 +817,7 @@ __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int6
     const int64_t e = jadd(s, c.size);
     if (cleanup_of(e, c.lateness) <= x.wm) continue;  // isWindowLate
     *skipped = false;
-    const uint32_t h = slot_hash(c, k, s);
+    const uint64_t h = slot_hash(c, k, s);
     int32_t slot = region_find(r, h, k, s, e);
     if (slot < 0) {
       Entry ne;
@@ -708,15 +852,16 @@ __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int6
 __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t, int64_t v, bool* skipped) {
   const DevCfg& c = x.c;
   const Region r = region_of(c, x.tb, p, x.tb.cur[p]);
-  const uint32_t h = slot_hash(c, k, 0);
+  const uint64_t h = slot_hash(c, k, 0);
+  const uint32_t want = live_word(h);
   // in-flight windows of the key: every live entry of the key sits on its probe chain
   int32_t sl[MAX_SESSIONS];
   int ns = 0;
   for (uint32_t i = 0; i <= r.mask; i++) {
-    const uint32_t s = (h + i) & r.mask;
+    const uint32_t s = ((uint32_t)h + i) & r.mask;
     const uint32_t stt = ld_state(r.state + s);
     if (stt == SLOT_EMPTY) break;
-    if (stt == SLOT_LIVE) {
+    if (stt == want) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       if (r.ent[s].key == k) {
         if (ns == MAX_SESSIONS) {
@@ -859,12 +1004,36 @@ __global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, 
 }
 
 // ---- K_fire: watermark.  Regions with next_timer <= wm emit and are rebuilt into the other buffer.
+// Pass 1 decides every slot, re-inserts the survivors into the other buffer and counts the fired
+// rows; one reservation per workgroup in the output; pass 2 re-decides and writes the rows.
+struct FireDecision {
+  bool fire, keep;
+};
+__device__ __forceinline__ FireDecision fire_decide(const DevCfg& c, int64_t wm, Entry& e, Entry& fe) {
+  FireDecision d{false, true};
+  if ((e.meta & FW_TIMER) && jsub(e.end, 1) <= wm) {  // trigger timer fires (EventTimeTrigger.onEventTime)
+    e.meta &= ~(int64_t)FW_TIMER;
+    fe = e;
+    d.fire = e.cnt > 0;                                 // contents != null (WindowOperator.java:452-459)
+    if (c.purging) {                                    // FIRE_AND_PURGE
+      if (c.assigner == FW_SESSION)
+        acc_clear(e);                                   // the session stays in the MergingWindowSet
+      else
+        d.keep = false;
+    }
+  }
+  const int64_t cl = cleanup_of(e.end, c.lateness);
+  if (cl != LMAX && cl <= wm) d.keep = false;  // GC timer: clearAllState (WindowOperator.java:461-463)
+  return d;
+}
+
 __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, DevTable tb, DevRows out, Status* st) {
   const int32_t p = blockIdx.x;
   if (tb.next_timer[p] > wm) return;
   __shared__ int live_s;
   __shared__ long long next_s;
-  __shared__ unsigned long long wbase[FW_FIRE_THREADS / 64];
+  __shared__ uint32_t sw[FW_FIRE_THREADS / 64 + 1];
+  __shared__ unsigned long long base_s;
   const int X = tb.cur[p], Y = X ^ 1;
   const Region rx = region_of(c, tb, p, X), ry = region_of(c, tb, p, Y);
   const uint32_t R = rx.mask + 1;
@@ -874,58 +1043,46 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, 
     next_s = LMAX;
   }
   __syncthreads();
-  const int lane = __lane_id(), wid = threadIdx.x >> 6;
   int live = 0;
+  uint32_t nfire = 0;
   int64_t nt = LMAX;
-  unsigned long long fired = 0;
-  for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x) {
-    const uint32_t s = s0 + threadIdx.x;
-    bool fire = false, keep = false;
-    Entry e;
-    if (s < R && ld_state(rx.state + s) == SLOT_LIVE) {
-      e = rx.ent[s];
-      keep = true;
-      if ((e.meta & FW_TIMER) && jsub(e.end, 1) <= wm) {  // trigger timer fires (EventTimeTrigger.onEventTime)
-        e.meta &= ~(int64_t)FW_TIMER;
-        fire = e.cnt > 0;                                 // contents != null (WindowOperator.java:452-459)
-        if (c.purging) {
-          if (c.assigner == FW_SESSION)
-            acc_clear(e);
-          else
-            keep = false;
-        }
-      }
-      const int64_t cl = cleanup_of(e.end, c.lateness);
-      if (cl != LMAX && cl <= wm) keep = false;  // GC timer: clearAllState (WindowOperator.java:461-463)
+  for (uint32_t s = threadIdx.x; s < R; s += blockDim.x) {
+    if (st_kind(ld_state(rx.state + s)) != SLOT_LIVE) continue;
+    Entry e = rx.ent[s], fe;
+    const FireDecision d = fire_decide(c, wm, e, fe);
+    nfire += d.fire;
+    if (!d.keep) continue;
+    const uint64_t h = slot_hash(c, e.key, e.start);
+    const int32_t dst = region_claim(ry, h, live_word(h));
+    if (dst >= 0) {
+      ry.ent[dst] = e;
+      live++;
+      nt = min(nt, timer_of(e, c.lateness));
+    } else {
+      atomicOr(&st->flags, FW_STATUS_OVERFLOW_LOST);
     }
-    const uint64_t ball = __ballot(fire);
-    if (lane == 0 && ball) wbase[wid] = atomicAdd(&st->out_rows, (unsigned long long)__popcll(ball));
-    __syncthreads();
-    if (fire) {
-      const unsigned long long pos = wbase[wid] + (unsigned long long)__popcll(ball & lanemask_lt());
-      if ((int64_t)pos < out.cap)
-        write_row(c, out, pos, e);
-      else
-        atomicOr(&st->flags, FW_STATUS_OUT_FULL);
-      fired++;
-    }
-    if (keep) {
-      const int32_t d = region_claim(ry, slot_hash(c, e.key, e.start), SLOT_LIVE);
-      if (d >= 0) {
-        ry.ent[d] = e;
-        live++;
-        nt = min(nt, timer_of(e, c.lateness));
-      } else {
-        atomicOr(&st->flags, FW_STATUS_OVERFLOW_LOST);
-      }
-    }
-    __syncthreads();
   }
+  uint32_t total;
+  uint32_t pos0 = block_excl_scan(nfire, sw, &total);
+  if (threadIdx.x == 0) base_s = total ? atomicAdd(&st->out_rows, (unsigned long long)total) : 0ull;
   if (live) atomicAdd(&live_s, live);
   if (nt != LMAX) atomicMin(&next_s, (long long)nt);
-  if (fired) atomicAdd(&st->fired_total, fired);
   __syncthreads();
+  if (nfire) {
+    unsigned long long pos = base_s + pos0;
+    for (uint32_t s = threadIdx.x; s < R; s += blockDim.x) {
+      if (st_kind(ld_state(rx.state + s)) != SLOT_LIVE) continue;
+      Entry e = rx.ent[s], fe;
+      if (!fire_decide(c, wm, e, fe).fire) continue;
+      if ((int64_t)pos < out.cap)
+        write_row(c, out, pos, fe);
+      else
+        atomicOr(&st->flags, FW_STATUS_OUT_FULL);
+      pos++;
+    }
+  }
   if (threadIdx.x == 0) {
+    if (total) atomicAdd(&st->fired_total, (unsigned long long)total);
     tb.cur[p] = (uint8_t)Y;
     tb.live[p] = live_s;
     tb.next_timer[p] = next_s;
@@ -939,10 +1096,11 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_rehash(DevCfg oc, DevTable 
   const Region rn = region_of(nc, nt, p, 0);
   const uint32_t R = ro.mask + 1;
   for (uint32_t s = threadIdx.x; s < R; s += blockDim.x) {
-    if (ld_state(ro.state + s) != SLOT_LIVE) continue;
+    if (st_kind(ld_state(ro.state + s)) != SLOT_LIVE) continue;
     const Entry e = ro.ent[s];
     // the new region is larger than the old one's live count, so a slot is always found
-    const int32_t d = region_claim(rn, slot_hash(nc, e.key, e.start), SLOT_LIVE);
+    const uint64_t h = slot_hash(nc, e.key, e.start);
+    const int32_t d = region_claim(rn, h, live_word(h));
     if (d >= 0) rn.ent[d] = e;
   }
   __syncthreads();
@@ -964,7 +1122,7 @@ __global__ void k_merge_overflow(DevCfg c, DevTable tb, DevOverflow ov, const St
   for (int64_t i = 0; i < n; i++) {
     if (ov.part[i] != p) continue;
     const Entry d = ov.ent[i];
-    const uint32_t h = slot_hash(c, d.key, d.start);
+    const uint64_t h = slot_hash(c, d.key, d.start);
     int32_t s = region_find(r, h, d.key, d.start, d.end);
     if (s >= 0) {
       Entry e = r.ent[s];
@@ -972,7 +1130,7 @@ __global__ void k_merge_overflow(DevCfg c, DevTable tb, DevOverflow ov, const St
       e.meta |= d.meta;
       r.ent[s] = e;
     } else {
-      s = region_claim(r, h, SLOT_LIVE);
+      s = region_claim(r, h, live_word(h));
       if (s < 0) continue;  // cannot happen: the table was grown to hold every parked delta
       r.ent[s] = d;
       live++;
@@ -991,13 +1149,13 @@ __global__ void k_reset_regions(DevCfg c, DevTable tb) {
   tb.next_timer[p] = LMAX;
 }
 
-// out3 = {live entries, event-time timers, max region load}
+// out3 = {live entries, event-time timers}
 __global__ __launch_bounds__(FW_FIRE_THREADS) void k_table_stats(DevCfg c, DevTable tb, unsigned long long* out3) {
   const int32_t p = blockIdx.x;
   const Region r = region_of(c, tb, p, tb.cur[p]);
   unsigned long long live = 0, timers = 0;
   for (uint32_t s = threadIdx.x; s <= r.mask; s += blockDim.x) {
-    if (ld_state(r.state + s) != SLOT_LIVE) continue;
+    if (st_kind(ld_state(r.state + s)) != SLOT_LIVE) continue;
     const Entry& e = r.ent[s];
     live++;
     const int64_t mx = jsub(e.end, 1), cl = cleanup_of(e.end, c.lateness);
@@ -1146,18 +1304,18 @@ void launch_scan(uint32_t* data, int64_t m, uint32_t* scratch, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(SCAN_T), 0, s, data, m, (const uint32_t*)scratch);
 }
 
-void launch_scatter(const DevCfg& c, int64_t wm, int64_t /*ordinal_base*/, const int64_t* key, const int64_t* ts,
-                    const int64_t* val, const int32_t* kh, int64_t n, int32_t T, const uint32_t* offs, int64_t* pk,
-                    int64_t* pt, int64_t* pv, int64_t* sk, int64_t* stt, int64_t* sv, int32_t* skh, DevSide side,
-                    Status* st, hipStream_t s) {
-  const size_t lds = (2 * (size_t)c.P + 17) * sizeof(uint32_t);
-  hipLaunchKernelGGL(k_scatter, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, val, kh, n, T, offs, pk, pt, pv,
-                     sk, stt, sv, skh, side, st);
+void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
+                    const int32_t* kh, int64_t n, int32_t T, uint32_t* offs, PRec* part, int64_t* sk, int64_t* stt,
+                    int64_t* sv, int32_t* skh, DevSide side, Status* st, hipStream_t s) {
+  hipLaunchKernelGGL(k_scatter, dim3(T), dim3(FW_TILE_THREADS), (size_t)c.P * sizeof(uint32_t), s, c, wm, key, ts, val,
+                     kh, n, T, (const uint32_t*)offs, part, side, st);
+  hipLaunchKernelGGL(k_scatter_ordered, dim3(T), dim3(FW_TILE_THREADS), 0, s, c, wm, key, ts, val, kh, n, T,
+                     (const uint32_t*)offs, (const uint32_t*)(offs + (int64_t)(c.P + 1) * T), sk, stt, sv, skh);
 }
 
-void launch_aggregate(const DevCfg& c, int64_t wm, const int64_t* pk, const int64_t* pt, const int64_t* pv,
-                      const uint32_t* offs, int32_t T, DevTable tb, DevOverflow ov, Status* st, hipStream_t s) {
-  hipLaunchKernelGGL(k_aggregate, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, pk, pt, pv, offs, T, tb, ov, st);
+void launch_aggregate(const DevCfg& c, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
+                      DevOverflow ov, Status* st, hipStream_t s) {
+  hipLaunchKernelGGL(k_aggregate, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb, ov, st);
 }
 
 void launch_slow(const DevCfg& c, int64_t wm, const int64_t* sk, const int64_t* stt, const int64_t* sv,

@@ -20,6 +20,8 @@
 
 #define FW_TILE 32768          // records per classify/scatter workgroup
 #define FW_TILE_THREADS 1024
+#define FW_RPT 8               // records per thread kept in flight by the streaming kernels
+#define FW_AGG_RPT 4           // the same for k_aggregate (its LDS probe loops are unrolled per record)
 #define FW_AGG_THREADS 512     // aggregate workgroup
 #define FW_LDS_SLOTS 1024      // LDS pre-aggregation slots per aggregate workgroup
 #define FW_LDS_FILL_LIMIT 820  // ~0.8 * FW_LDS_SLOTS: a new slot is not claimed beyond this fill
@@ -34,11 +36,44 @@ struct DevCfg {
   int32_t side_output, max_par, kg0, n_kg;
   int32_t log_s, P, log_r, wpr;  // wpr = max windows per record
   int64_t size, slide, offset, gap, lateness;
+  int32_t diag, pad_;            // FW_DIAG ablation bits (diagnostic builds of the timing only; 0 in production)
+  // invariant-divisor reciprocals (Granlund-Montgomery round-up method) for `% size` / `% slide`
+  uint64_t mag_size, mag_slide;
+  int32_t l_size, l_slide;
+};
+
+// host: reciprocal of d >= 1 for div_inv(): m = floor(2^64 (2^l - d) / d) + 1, l = ceil(log2 d)
+inline void make_div_inv(uint64_t d, uint64_t* m, int32_t* l) {
+  int32_t L = 0;
+  while (L < 64 && (1ull << L) < d) L++;
+  const unsigned __int128 two_l = (unsigned __int128)1 << L;
+  *m = (uint64_t)((((unsigned __int128)1 << 64) * (two_l - d)) / d + 1);
+  *l = L;
+}
+// FW_DIAG bits: results are WRONG when any is set; used only to price one stage of a kernel
+enum {
+  DIAG_AGG_NO_FLUSH = 1,
+  DIAG_AGG_NO_LDS = 2,
+  DIAG_SCATTER_NO_STORE = 4,
+  DIAG_SCATTER_LINEAR = 8,
+  DIAG_AGG_NO_ACCUM = 16  // LDS lookup/claim only, no accumulate atomics
 };
 
 struct __attribute__((aligned(64))) Entry {
   int64_t key, start, end, cnt, sum, mn, mx, meta;
 };
+
+// a record in its partition's run: one 32-byte sector per record, so the scatter writes whole
+// sectors (three 8-byte columns scattered separately cost ~4x the bytes in partial writes).
+// The window assignment is done once, by the scatter: `last` is the newest window's start and
+// `nwin` the number of windows (1 for tumbling), newest first as SlidingEventTimeWindows emits them.
+struct __attribute__((aligned(32))) PRec {
+  int64_t key, last, val, nwin;
+};
+
+// region state word: kind in bits 0-1, 24-bit fingerprint of the slot hash in bits 8-31, so a
+// probe rejects most foreign slots without reading the 64-byte entry
+__host__ __device__ inline uint32_t st_kind(uint32_t s) { return s & 3u; }
 
 struct Status {
   unsigned long long out_rows;        // rows in the output buffer (pending)
@@ -84,12 +119,11 @@ namespace fwdev {
 void launch_classify_hist(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int32_t* kh,
                           int64_t n, int32_t T, uint32_t* hist, Status* st, hipStream_t_ s);
 void launch_scan(uint32_t* data, int64_t m, uint32_t* scratch, hipStream_t_ s);  // in-place exclusive
-void launch_scatter(const DevCfg& c, int64_t wm, int64_t ordinal_base, const int64_t* key, const int64_t* ts,
-                    const int64_t* val, const int32_t* kh, int64_t n, int32_t T, const uint32_t* offs,
-                    int64_t* pk, int64_t* pt, int64_t* pv, int64_t* sk, int64_t* stt, int64_t* sv, int32_t* skh,
-                    DevSide side, Status* st, hipStream_t_ s);
-void launch_aggregate(const DevCfg& c, int64_t wm, const int64_t* pk, const int64_t* pt, const int64_t* pv,
-                      const uint32_t* offs, int32_t T, DevTable tb, DevOverflow ov, Status* st, hipStream_t_ s);
+void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
+                    const int32_t* kh, int64_t n, int32_t T, uint32_t* offs, PRec* part, int64_t* sk,
+                    int64_t* stt, int64_t* sv, int32_t* skh, DevSide side, Status* st, hipStream_t_ s);
+void launch_aggregate(const DevCfg& c, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
+                      DevOverflow ov, Status* st, hipStream_t_ s);
 void launch_slow(const DevCfg& c, int64_t wm, const int64_t* sk, const int64_t* stt, const int64_t* sv,
                  const int32_t* skh, DevTable tb, DevRows out, DevSide side, Status* st, hipStream_t_ s);
 void launch_fire(const DevCfg& c, int64_t wm, DevTable tb, DevRows out, Status* st, hipStream_t_ s);

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -43,7 +44,7 @@ struct fw_op {
   int64_t *in_key = nullptr, *in_ts = nullptr, *in_val = nullptr;
   int32_t* in_kh = nullptr;
   uint32_t *hist = nullptr, *scan_tmp = nullptr;
-  int64_t *pk = nullptr, *pt = nullptr, *pv = nullptr;
+  PRec* part = nullptr;  // partitioned records of the current batch
   int64_t *sk = nullptr, *stt = nullptr, *sv = nullptr;
   int32_t* skh = nullptr;
 
@@ -310,12 +311,11 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   });
   timed(op, K_SCAN, [&] { fwdev::launch_scan(op->hist, m, op->scan_tmp, op->stream); });
   timed(op, K_SCATTER, [&] {
-    fwdev::launch_scatter(cc, op->wm, op->records_in, key, ts, val, kh, n, T, op->hist, op->pk, op->pt, op->pv,
-                          op->sk, op->stt, op->sv, op->skh, op->side, op->d_status, op->stream);
+    fwdev::launch_scatter(cc, op->wm, key, ts, val, kh, n, T, op->hist, op->part, op->sk, op->stt, op->sv, op->skh,
+                          op->side, op->d_status, op->stream);
   });
   timed(op, K_AGGREGATE, [&] {
-    fwdev::launch_aggregate(cc, op->wm, op->pk, op->pt, op->pv, op->hist, T, op->tb, op->ov, op->d_status,
-                            op->stream);
+    fwdev::launch_aggregate(cc, op->wm, op->part, op->hist, T, op->tb, op->ov, op->d_status, op->stream);
   });
   timed(op, K_SLOW, [&] {
     fwdev::launch_slow(cc, op->wm, op->sk, op->stt, op->sv, op->skh, op->tb, op->out, op->side, op->d_status,
@@ -398,7 +398,13 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   c.offset = cfg.offset;
   c.gap = cfg.gap;
   c.lateness = cfg.allowed_lateness;
+  // FW_DIAG: ablation bits for pricing kernel stages in diagnostic runs only (results are wrong)
+  if (const char* d = getenv("FW_DIAG")) c.diag = atoi(d);
   c.wpr = cfg.assigner == FW_SLIDING ? (int32_t)((cfg.size + cfg.slide - 1) / cfg.slide) : 1;
+  if (cfg.assigner != FW_SESSION) {
+    make_div_inv((uint64_t)c.size, &c.mag_size, &c.l_size);
+    make_div_inv((uint64_t)c.slide, &c.mag_slide, &c.l_slide);
+  }
   const int64_t expected = cfg.expected_entries > 0 ? cfg.expected_entries : (int64_t)c.P * 512;
   c.log_r = std::max(8, ilog2(4 * ((expected + c.P - 1) / c.P)));
   op->table_slots = (int64_t)c.P << c.log_r;
@@ -409,16 +415,14 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   if (rc) return rc;
   fwdev::launch_reset_regions(c, op->tb, op->stream);
   const int64_t mb = op->max_batch;
-  const int64_t m = (int64_t)(c.P + 1) * op->tmax;
+  const int64_t m = (int64_t)(c.P + 2) * op->tmax;  // P partition rows + ordered row (scanned) + per-tile ordered counts
   HIP_OR_RETURN(op, dmalloc(&op->in_key, mb));
   HIP_OR_RETURN(op, dmalloc(&op->in_ts, mb));
   HIP_OR_RETURN(op, dmalloc(&op->in_val, mb));
   HIP_OR_RETURN(op, dmalloc(&op->in_kh, mb));
   HIP_OR_RETURN(op, dmalloc(&op->hist, m));
   HIP_OR_RETURN(op, dmalloc(&op->scan_tmp, m / 4096 + 2));
-  HIP_OR_RETURN(op, dmalloc(&op->pk, mb));
-  HIP_OR_RETURN(op, dmalloc(&op->pt, mb));
-  HIP_OR_RETURN(op, dmalloc(&op->pv, mb));
+  HIP_OR_RETURN(op, dmalloc(&op->part, mb));
   HIP_OR_RETURN(op, dmalloc(&op->sk, mb));
   HIP_OR_RETURN(op, dmalloc(&op->stt, mb));
   HIP_OR_RETURN(op, dmalloc(&op->sv, mb));
@@ -454,9 +458,7 @@ void fw_destroy(fw_op* op) {
   dfree(op->in_kh);
   dfree(op->hist);
   dfree(op->scan_tmp);
-  dfree(op->pk);
-  dfree(op->pt);
-  dfree(op->pv);
+  dfree(op->part);
   dfree(op->sk);
   dfree(op->stt);
   dfree(op->sv);

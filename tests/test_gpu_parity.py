@@ -123,6 +123,16 @@ def test_gpu_zipf_hot_keys():
     assert_rows_equal(g, r)
 
 
+@pytest.mark.parametrize("cfg", [dict(assigner="tumbling", size=1000),
+                                 dict(assigner="sliding", size=5000, slide=1000)], ids=["tumbling", "sliding"])
+def test_gpu_lds_flush_and_retry(cfg):
+    # ~8K distinct (key, window) pairs per state partition and batch: the LDS pre-aggregation table
+    # (1024 slots) fills many times inside one round, so flush-and-retry is exercised heavily
+    batches, wms = _stream(1 << 20, 1 << 20, 1 << 40, bound=100, jitter=100, rate=1_000_000)
+    g, r, *_ = _run_both(cfg, batches, wms, sub_partitions=1)
+    assert_rows_equal(g, r)
+
+
 def test_gpu_table_growth():
     # tiny initial table: forces overflow parking and region growth mid-stream
     cfg = dict(assigner="tumbling", size=10_000)

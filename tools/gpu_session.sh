@@ -14,7 +14,7 @@ rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/gpu_tests.log
 if fatal $rc; then exit $rc; fi
 
 if [ "${SKIP_BENCH:-0}" = "0" ]; then
-  timeout -k 10 300 python -u bench.py --steps ${STEPS:-10} --warmup ${WARMUP:-3} ${BENCH_ARGS:-} \
+  timeout -k 10 240 python -u bench.py --steps ${STEPS:-10} --warmup ${WARMUP:-3} ${BENCH_ARGS:-} \
       > gpurun_out/bench.log 2>&1
   rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
   if fatal $rc; then exit $rc; fi
