@@ -31,9 +31,9 @@ def kernel_bytes(name, n, merged, live_slots_scanned=0):
     if name == "k_classify_hist":
         return 16 * n                      # key + ts
     if name == "k_scatter":
-        return 24 * n + 24 * n             # read key/ts/val, write the partitioned copy
+        return 24 * n + 32 * n             # read key/ts/val, write the 32-B partitioned record
     if name == "k_aggregate":
-        return 24 * n + 128 * merged       # read the partitioned records, RMW one 64-B entry per delta
+        return 32 * n + 128 * merged       # read the partitioned records, RMW one 64-B entry per delta
     return None
 
 
@@ -102,8 +102,8 @@ def main():
         if world > 1:
             k, t, v = exch.exchange(k, t, v)
             wm = exch.combine_watermark(wm, device=dev)
-        op.process_batch(k, t, v)
-        op.advance_watermark(wm)
+        op.process_batch(k, t, v)          # queued; settles the previous step's sequence
+        op.advance_watermark(wm, wait=False)  # queued behind the push
         op.clear_pending()  # discarding sink: fired rows were materialised in HBM
 
     def barrier():
@@ -123,6 +123,7 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.warmup, steps_total):
         step(s)
+    op.synchronize()  # settles the last step (resumes it if it suspended)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0

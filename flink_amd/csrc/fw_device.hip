@@ -337,10 +337,7 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_classify_hist(DevCfg c, int
   if (slow) atomicAdd(&lh[c.P], slow);
   __syncthreads();
   for (int i = threadIdx.x; i <= c.P; i += blockDim.x) hist[(int64_t)i * T + blockIdx.x] = lh[i];
-  if (threadIdx.x == 0) {
-    hist[(int64_t)(c.P + 1) * T + blockIdx.x] = lh[c.P];
-    if (lh[c.P]) atomicAdd(&st->slow_count, (unsigned long long)lh[c.P]);
-  }
+  if (threadIdx.x == 0) hist[(int64_t)(c.P + 1) * T + blockIdx.x] = lh[c.P];
   if (bad_kg) atomicAdd(&st->kg_errors, bad_kg);
   if (bad_ts) atomicAdd(&st->ts_errors, bad_ts);
 }
@@ -533,11 +530,11 @@ struct AggLds {
   i64x2 kv[FW_LDS_SLOTS];      // {key, window start}: one ds_read_b128 per comparison
   i64x2 mm[FW_LDS_SLOTS];      // {min, max}: one ds_read_b128 decides both conditional atomics
   int64_t sum[FW_LDS_SLOTS];
-  uint8_t done[FW_LDS_SLOTS];  // flush bookkeeping
+  int32_t slot[FW_LDS_SLOTS];  // flush: the window's slot in the region, -1 if new
   int fill;
   int anyfail;
-  int inserted;
-  int pad_;
+  int nnew;    // flush: windows of this LDS epoch not yet in the region
+  int live;    // occupied slots of the region
   unsigned long long flushed;
   int64_t min_timer;
 };
@@ -618,98 +615,124 @@ __device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, in
   return ok;
 }
 
-// merge every LDS slot into the partition's HBM region, then reset the LDS table.  Phase 1 updates
-// windows already in the region (distinct slots, plain read-modify-write); phase 2, after a barrier,
-// claims EMPTY slots for the new ones (so no thread ever reads an entry that is being written).
-__device__ void agg_flush(const DevCfg& c, AggLds& L, const Region& r, int32_t p, DevOverflow ov, Status* st) {
+// merge every LDS window into the partition's HBM region, then reset the LDS table.
+// Phase A locates each window in the region (read-only) and counts the new ones; if the region
+// cannot take them within its load limit the flush changes nothing and returns false (the kernel
+// suspends and resumes after the table grows).  Phase B then updates the found entries in place
+// (plain read-modify-write: the workgroup owns the region) and claims EMPTY slots for the new ones.
+__device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* st) {
   __syncthreads();
   if (c.diag & DIAG_AGG_NO_FLUSH) {
     for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
     if (threadIdx.x == 0) L.fill = 0;
     __syncthreads();
-    return;
+    return true;
+  }
+  int nnew = 0;
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
+    if (L.tag[h] < 2) continue;
+    const i64x2 kv = L.kv[h];
+    const int64_t k = kv.x, s = kv.y;
+    const int32_t slot = region_find(r, slot_hash(c, k, s), k, s, jadd(s, c.size));
+    L.slot[h] = slot;
+    nnew += slot < 0;
+  }
+  if (nnew) atomicAdd(&L.nnew, nnew);
+  __syncthreads();
+  const int32_t need = L.live + L.nnew;
+  if (need > region_limit(c.log_r)) {
+    if (threadIdx.x == 0) atomicMax(&st->need_live, need);
+    return false;
   }
   int64_t mt = LMAX;
   unsigned long long nflush = 0;
+  int lost = 0;
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
-    L.done[h] = 0;
     if (L.tag[h] < 2) continue;
     nflush++;
-    const i64x2 kv = L.kv[h];
-    const int64_t k = kv.x, s = kv.y, e = jadd(s, c.size);
-    mt = min(mt, jsub(e, 1));
-    const int32_t slot = region_find(r, slot_hash(c, k, s), k, s, e);
-    if (slot < 0) continue;
+    const i64x2 kv = L.kv[h], mm = L.mm[h];
     Entry d;
-    const i64x2 mm = L.mm[h];
+    d.key = kv.x;
+    d.start = kv.y;
+    d.end = jadd(kv.y, c.size);
     d.cnt = (int64_t)L.cnt[h];
     d.sum = L.sum[h];
     d.mn = mm.x;
     d.mx = mm.y;
-    Entry& x = r.ent[slot];
-    Entry cur = x;
-    acc_merge(c, cur, d);
-    cur.meta |= FW_TIMER;
-    x = cur;
-    L.done[h] = 1;
-  }
-  __syncthreads();
-  int ins = 0;
-  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
-    if (L.tag[h] < 2 || L.done[h]) continue;
-    const i64x2 kv = L.kv[h], mm = L.mm[h];
-    const int64_t k = kv.x, s = kv.y;
-    Entry e;
-    e.key = k;
-    e.start = s;
-    e.end = jadd(s, c.size);
-    e.cnt = (int64_t)L.cnt[h];
-    e.sum = L.sum[h];
-    e.mn = mm.x;
-    e.mx = mm.y;
-    e.meta = FW_TIMER;
-    const uint64_t hs = slot_hash(c, k, s);
-    const int32_t slot = region_claim(r, hs, live_word(hs));
+    d.meta = FW_TIMER;
+    mt = min(mt, jsub(d.end, 1));
+    const int32_t slot = L.slot[h];
     if (slot >= 0) {
-      r.ent[slot] = e;
-      ins++;
+      Entry& x = r.ent[slot];
+      Entry cur = x;
+      acc_merge(c, cur, d);
+      cur.meta |= FW_TIMER;
+      x = cur;
     } else {
-      const unsigned long long pos = atomicAdd(&st->overflow_count, 1ull);
-      if ((int64_t)pos < ov.cap) {
-        ov.ent[pos] = e;
-        ov.part[pos] = p;
-      } else {
-        atomicOr(&st->flags, FW_STATUS_OVERFLOW_LOST);
-      }
+      const uint64_t hs = slot_hash(c, d.key, d.start);
+      const int32_t ns = region_claim(r, hs, live_word(hs));
+      if (ns >= 0)
+        r.ent[ns] = d;
+      else
+        lost++;  // cannot happen below the load limit
     }
   }
-  if (ins) atomicAdd(&L.inserted, ins);
+  if (lost) atomicOr(&st->flags, FW_STATUS_STATE_LOST);
   if (mt != LMAX) atomicMin((long long*)&L.min_timer, (long long)mt);
   if (nflush) atomicAdd(&L.flushed, nflush);
   __syncthreads();
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
-  if (threadIdx.x == 0) L.fill = 0;
+  if (threadIdx.x == 0) {
+    L.fill = 0;
+    L.live = need;
+    L.nnew = 0;
+  }
   __syncthreads();
+  return true;
+}
+
+// write back what the workgroup learnt about its region (on completion and on suspension)
+__device__ __forceinline__ void agg_publish(const DevCfg& c, AggLds& L, DevTable& tb, int32_t p, Status* st) {
+  tb.live[p] = L.live;
+  if (L.min_timer < tb.next_timer[p]) tb.next_timer[p] = L.min_timer;
+  if (L.flushed) atomicAdd(&st->merged, L.flushed);
+  if (L.live > (1 << c.log_r) / 2) st->need_grow = 1;
 }
 
 __global__ __launch_bounds__(FW_AGG_THREADS) void k_aggregate(DevCfg c, int64_t wm, const PRec* __restrict__ part,
                                                               const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
-                                                              DevOverflow ov, Status* st) {
+                                                              AggProg prog, int resume, Status* st) {
   __shared__ AggLds L;
   const int32_t p = blockIdx.x;
+  if (resume && prog.done[p]) return;
   const int64_t begin = offs[(int64_t)p * T], end = offs[(int64_t)(p + 1) * T];
-  if (begin == end) return;
+  if (begin == end) {
+    if (threadIdx.x == 0) prog.done[p] = 1;
+    return;
+  }
+  // resume point: round start srb and this thread's (record, window) inside that round; it moves
+  // forward after every flush that succeeds
+  int64_t srb = begin;
+  int srj = 0, srwi = 0;
+  if (resume) {
+    srb = prog.rb[p];
+    const uint32_t tp = prog.tp[(int64_t)p * FW_AGG_THREADS + threadIdx.x];
+    srj = (int)(tp & 0xffu);
+    srwi = (int)(tp >> 8);
+  }
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
   if (threadIdx.x == 0) {
     L.fill = 0;
     L.anyfail = 0;
-    L.inserted = 0;
+    L.nnew = 0;
+    L.live = tb.live[p];
     L.flushed = 0;
     L.min_timer = LMAX;
   }
   __syncthreads();
   const Region r = region_of(c, tb, p, tb.cur[p]);
-  for (int64_t rb = begin; rb < end; rb += (int64_t)blockDim.x * FW_AGG_RPT) {
+  bool ok = true, first = true;
+  for (int64_t rb = srb; rb < end && ok; rb += (int64_t)blockDim.x * FW_AGG_RPT) {
     int64_t k[FW_AGG_RPT], t[FW_AGG_RPT], v[FW_AGG_RPT];
     int nw[FW_AGG_RPT];
 #pragma unroll
@@ -733,7 +756,8 @@ __global__ __launch_bounds__(FW_AGG_THREADS) void k_aggregate(DevCfg c, int64_t 
     }
     // progress (record rj, window rwi) survives a flush-and-retry when the LDS table fills up;
     // the record loop is unrolled so the register arrays are only indexed by constants
-    int rj = 0, rwi = 0;
+    int rj = first ? srj : 0, rwi = first ? srwi : 0;
+    first = false;
     for (;;) {
       bool failed = false;
 #pragma unroll
@@ -756,19 +780,29 @@ __global__ __launch_bounds__(FW_AGG_THREADS) void k_aggregate(DevCfg c, int64_t 
       const int need = L.anyfail;
       __syncthreads();
       if (!need) break;
-      agg_flush(c, L, r, p, ov, st);
+      if (!agg_flush(c, L, r, st)) {
+        ok = false;
+        break;
+      }
+      srb = rb;
+      srj = rj;
+      srwi = rwi;
       if (threadIdx.x == 0) L.anyfail = 0;
       __syncthreads();
     }
   }
-  agg_flush(c, L, r, p, ov, st);
-  if (threadIdx.x == 0) {
-    const int32_t live = tb.live[p] + L.inserted;
-    tb.live[p] = live;
-    atomicMax(&st->max_live, live);
-    if (L.min_timer < tb.next_timer[p]) tb.next_timer[p] = L.min_timer;
-    atomicAdd(&st->merged, L.flushed);
+  if (ok) ok = agg_flush(c, L, r, st);
+  if (!ok) {  // suspend: everything up to the last successful flush is in the region
+    prog.tp[(int64_t)p * FW_AGG_THREADS + threadIdx.x] = (uint32_t)srj | ((uint32_t)srwi << 8);
+    if (threadIdx.x == 0) {
+      prog.rb[p] = srb;
+      prog.done[p] = 0;
+      atomicOr(&st->suspended, (int)FW_SUSP_AGG);
+    }
+  } else if (threadIdx.x == 0) {
+    prog.done[p] = 1;
   }
+  if (threadIdx.x == 0) agg_publish(c, L, tb, p, st);
 }
 
 // ---- K_slow: ordered replay (one workgroup; one thread per key inside each chunk)
@@ -788,21 +822,21 @@ __device__ __forceinline__ void note_timer(const SlowCtx& x, int32_t p, const En
   atomicMin((long long*)&x.tb.next_timer[p], (long long)timer_of(e, x.c.lateness));
 }
 __device__ __forceinline__ void kill_slot(const SlowCtx& x, const Region& r, int32_t p, int32_t s) {
+  // the slot stays occupied (tb.live counts occupied slots) until the region is rebuilt by k_fire
   __hip_atomic_store(r.state + s, SLOT_DEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  atomicSub(&x.tb.live[p], 1);
 }
 // new entry: claim BUSY, write, publish LIVE with the fingerprint (readers never see a torn entry)
 __device__ __forceinline__ int32_t new_slot(const SlowCtx& x, const Region& r, int32_t p, uint64_t h, const Entry& e) {
   const int32_t s = region_claim(r, h, SLOT_BUSY);
-  if (s < 0) {
-    atomicOr(&x.st->flags, FW_STATUS_OVERFLOW_LOST);
+  if (s < 0) {  // cannot happen: k_slow checked the region's room for the chunk
+    atomicOr(&x.st->flags, FW_STATUS_STATE_LOST);
     return -1;
   }
   r.ent[s] = e;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __hip_atomic_store(r.state + s, live_word(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int live = atomicAdd(&x.tb.live[p], 1) + 1;
-  atomicMax(&x.st->max_live, live);
+  if (live > (1 << x.c.log_r) / 2) x.st->need_grow = 1;
   return s;
 }
 
@@ -865,7 +899,7 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       if (r.ent[s].key == k) {
         if (ns == MAX_SESSIONS) {
-          atomicOr(&x.st->flags, FW_STATUS_OVERFLOW_LOST);
+          atomicOr(&x.st->flags, FW_STATUS_STATE_LOST);
           return;
         }
         sl[ns++] = (int32_t)s;
@@ -943,47 +977,95 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
   note_timer(x, p, en);
 }
 
-__global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, const int64_t* __restrict__ sk,
+__global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, const uint32_t* __restrict__ offs,
+                                                          int32_t T, const int64_t* __restrict__ sk,
                                                           const int64_t* __restrict__ stt,
                                                           const int64_t* __restrict__ sv,
                                                           const int32_t* __restrict__ skh, DevTable tb, DevRows out,
-                                                          DevSide side, Status* st) {
-  const int64_t n = (int64_t)st->slow_count;
-  if (n == 0) return;
+                                                          DevSide side, Status* st, int resume) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // resumed later
+  // list length: row P of the scan (ordered-path offsets per tile) plus the last tile's own count
+  const int64_t rowP = (int64_t)c.P * T;
+  const int64_t n = (int64_t)(offs[rowP + T - 1] - offs[rowP]) + offs[rowP + T + T - 1];
+  const int64_t first = resume ? st->slow_resume : 0;
+  if (first >= n) return;
   __shared__ int64_t ck[SLOW_CHUNK];
-  __shared__ int32_t ci[SLOW_CHUNK];
+  __shared__ int32_t ci[SLOW_CHUNK], cp[SLOW_CHUNK], cd[SLOW_CHUNK];
+  __shared__ int bad;
   SlowCtx x{c, wm, tb, out, side, st};
   unsigned long long late = 0;
-  for (int64_t b0 = 0; b0 < n; b0 += SLOW_CHUNK) {
+  const int tid = threadIdx.x;
+  const int64_t row_bound = c.assigner == FW_SESSION ? 1 : c.wpr;  // fired rows per record, at most
+  int64_t b0 = first;
+  for (; b0 < n; b0 += SLOW_CHUNK) {
     const int m = (int)min((int64_t)SLOW_CHUNK, n - b0);
-    const int tid = threadIdx.x;
-    ck[tid] = tid < m ? sk[b0 + tid] : LMAX;
-    ci[tid] = tid < m ? tid : INT32_MAX;
+    if (tid == 0) bad = 0;
+    if (tid < m) {
+      const int64_t i = b0 + tid;
+      ck[tid] = sk[i];
+      cp[tid] = partition_of(c, ck[tid], skh[i]);
+      int64_t last;
+      cd[tid] = c.assigner == FW_SESSION ? 1 : num_windows(c, stt[i], &last);  // new windows, at most
+      ci[tid] = tid;
+    } else {
+      ck[tid] = LMAX;
+      cp[tid] = INT32_MAX;
+      cd[tid] = 0;
+      ci[tid] = INT32_MAX;
+    }
     __syncthreads();
-    // bitonic sort by (key, arrival index)
+    // bitonic sort by (partition, key, arrival index): a key's records stay in arrival order and a
+    // partition's records are contiguous, so its demand on the region is one segmented sum
     for (int kk = 2; kk <= SLOW_CHUNK; kk <<= 1) {
       for (int jj = kk >> 1; jj > 0; jj >>= 1) {
         const int o = tid ^ jj;
         if (o > tid) {
           const bool up = (tid & kk) == 0;
+          const int32_t pa = cp[tid], pb = cp[o];
           const int64_t a = ck[tid], b = ck[o];
           const int32_t ia = ci[tid], ib = ci[o];
-          const bool gt = a > b || (a == b && ia > ib);
+          const bool gt = pa > pb || (pa == pb && (a > b || (a == b && ia > ib)));
           if (gt == up) {
+            cp[tid] = pb;
+            cp[o] = pa;
             ck[tid] = b;
             ck[o] = a;
             ci[tid] = ib;
             ci[o] = ia;
+            const int32_t da = cd[tid];
+            cd[tid] = cd[o];
+            cd[o] = da;
           }
         }
         __syncthreads();
       }
     }
-    if (tid < m && (tid == 0 || ck[tid - 1] != ck[tid])) {
-      for (int j = tid; j < m && ck[j] == ck[tid]; j++) {
+    // capacity: every region the chunk touches must take its new windows within the load limit,
+    // and the fired-row buffer must take every row the chunk may fire; otherwise suspend here
+    if (tid < m && (tid == 0 || cp[tid - 1] != cp[tid])) {
+      int64_t demand = 0;
+      for (int j = tid; j < m && cp[j] == cp[tid]; j++) demand += cd[j];
+      const int64_t want = (int64_t)tb.live[cp[tid]] + demand;
+      if (want > region_limit(c.log_r)) {
+        bad = 1;
+        atomicMax(&st->need_live, (int32_t)min(want, (int64_t)INT32_MAX));
+      }
+    }
+    if (tid == 0) {
+      const int64_t want = (int64_t)__hip_atomic_load(&st->out_rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+                           (int64_t)m * row_bound;
+      if (want > out.slow_limit) {
+        bad = 1;
+        atomicMax((long long*)&st->need_out, (long long)want);
+      }
+    }
+    __syncthreads();
+    if (bad) break;
+    if (tid < m && (tid == 0 || ck[tid - 1] != ck[tid] || cp[tid - 1] != cp[tid])) {
+      for (int j = tid; j < m && ck[j] == ck[tid] && cp[j] == cp[tid]; j++) {
         const int64_t i = b0 + ci[j];
         const int64_t k = sk[i], t = stt[i], v = sv[i];
-        const int32_t p = partition_of(c, k, skh[i]);
+        const int32_t p = cp[j];
         bool skipped = true;
         if (c.assigner == FW_SESSION)
           replay_session(x, p, k, t, v, &skipped);
@@ -1000,7 +1082,13 @@ __global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, 
     __syncthreads();
   }
   if (late) atomicAdd(&st->late_dropped, late);
-  if (threadIdx.x == 0) atomicAdd(&st->slow_total, (unsigned long long)n);
+  if (tid == 0) {
+    atomicAdd(&st->slow_total, (unsigned long long)(min(b0, n) - first));
+    if (b0 < n) {
+      st->slow_resume = b0;
+      atomicOr(&st->suspended, (int)FW_SUSP_SLOW);
+    }
+  }
 }
 
 // ---- K_fire: watermark.  Regions with next_timer <= wm emit and are rebuilt into the other buffer.
@@ -1029,7 +1117,8 @@ __device__ __forceinline__ FireDecision fire_decide(const DevCfg& c, int64_t wm,
 
 __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, DevTable tb, DevRows out, Status* st) {
   const int32_t p = blockIdx.x;
-  if (tb.next_timer[p] > wm) return;
+  // a suspended push has not finished updating the state: the host resumes it and fires again
+  if (tb.next_timer[p] > wm || __hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   __shared__ int live_s;
   __shared__ long long next_s;
   __shared__ uint32_t sw[FW_FIRE_THREADS / 64 + 1];
@@ -1059,7 +1148,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, 
       live++;
       nt = min(nt, timer_of(e, c.lateness));
     } else {
-      atomicOr(&st->flags, FW_STATUS_OVERFLOW_LOST);
+      atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // cannot happen: the survivors fit the region they came from
     }
   }
   uint32_t total;
@@ -1089,56 +1178,35 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, 
   }
 }
 
-// ---- table growth: re-insert every live entry of the old table into the new one (buffer 0)
+// ---- table growth: re-insert every live entry of the old table into the new one (buffer 0);
+// DEAD slots are dropped, so the region's occupied count becomes its live count
 __global__ __launch_bounds__(FW_FIRE_THREADS) void k_rehash(DevCfg oc, DevTable ot, DevCfg nc, DevTable nt) {
+  __shared__ int live_s;
   const int32_t p = blockIdx.x;
   const Region ro = region_of(oc, ot, p, ot.cur[p]);
   const Region rn = region_of(nc, nt, p, 0);
   const uint32_t R = ro.mask + 1;
+  if (threadIdx.x == 0) live_s = 0;
+  __syncthreads();
+  int live = 0;
   for (uint32_t s = threadIdx.x; s < R; s += blockDim.x) {
     if (st_kind(ld_state(ro.state + s)) != SLOT_LIVE) continue;
     const Entry e = ro.ent[s];
-    // the new region is larger than the old one's live count, so a slot is always found
+    // the new region is larger than the old one, so a slot is always found
     const uint64_t h = slot_hash(nc, e.key, e.start);
     const int32_t d = region_claim(rn, h, live_word(h));
-    if (d >= 0) rn.ent[d] = e;
+    if (d >= 0) {
+      rn.ent[d] = e;
+      live++;
+    }
   }
+  if (live) atomicAdd(&live_s, live);
   __syncthreads();
   if (threadIdx.x == 0) {
     nt.cur[p] = 0;
-    nt.live[p] = ot.live[p];
+    nt.live[p] = live_s;
     nt.next_timer[p] = ot.next_timer[p];
   }
-}
-
-// ---- overflow deltas (parked by k_aggregate) merged into the grown table; one lane per region
-__global__ void k_merge_overflow(DevCfg c, DevTable tb, DevOverflow ov, const Status* st) {
-  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= c.P) return;
-  const int64_t n = min((int64_t)st->overflow_count, ov.cap);
-  const Region r = region_of(c, tb, p, tb.cur[p]);
-  int live = tb.live[p];
-  int64_t nt = tb.next_timer[p];
-  for (int64_t i = 0; i < n; i++) {
-    if (ov.part[i] != p) continue;
-    const Entry d = ov.ent[i];
-    const uint64_t h = slot_hash(c, d.key, d.start);
-    int32_t s = region_find(r, h, d.key, d.start, d.end);
-    if (s >= 0) {
-      Entry e = r.ent[s];
-      acc_merge(c, e, d);
-      e.meta |= d.meta;
-      r.ent[s] = e;
-    } else {
-      s = region_claim(r, h, live_word(h));
-      if (s < 0) continue;  // cannot happen: the table was grown to hold every parked delta
-      r.ent[s] = d;
-      live++;
-    }
-    nt = min(nt, timer_of(d, c.lateness));
-  }
-  tb.live[p] = live;
-  tb.next_timer[p] = nt;
 }
 
 __global__ void k_reset_regions(DevCfg c, DevTable tb) {
@@ -1314,13 +1382,15 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
 }
 
 void launch_aggregate(const DevCfg& c, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
-                      DevOverflow ov, Status* st, hipStream_t s) {
-  hipLaunchKernelGGL(k_aggregate, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb, ov, st);
+                      AggProg prog, int resume, Status* st, hipStream_t s) {
+  hipLaunchKernelGGL(k_aggregate, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb, prog, resume, st);
 }
 
-void launch_slow(const DevCfg& c, int64_t wm, const int64_t* sk, const int64_t* stt, const int64_t* sv,
-                 const int32_t* skh, DevTable tb, DevRows out, DevSide side, Status* st, hipStream_t s) {
-  hipLaunchKernelGGL(k_slow, dim3(1), dim3(FW_SLOW_THREADS), 0, s, c, wm, sk, stt, sv, skh, tb, out, side, st);
+void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* offs, int32_t T, const int64_t* sk, const int64_t* stt,
+                 const int64_t* sv, const int32_t* skh, DevTable tb, DevRows out, DevSide side, Status* st, int resume,
+                 hipStream_t s) {
+  hipLaunchKernelGGL(k_slow, dim3(1), dim3(FW_SLOW_THREADS), 0, s, c, wm, offs, T, sk, stt, sv, skh, tb, out, side,
+                     st, resume);
 }
 
 void launch_fire(const DevCfg& c, int64_t wm, DevTable tb, DevRows out, Status* st, hipStream_t s) {
@@ -1331,9 +1401,6 @@ void launch_rehash(const DevCfg& oc, DevTable ot, const DevCfg& nc, DevTable nt,
   hipLaunchKernelGGL(k_rehash, dim3(oc.P), dim3(FW_FIRE_THREADS), 0, s, oc, ot, nc, nt);
 }
 
-void launch_merge_overflow(const DevCfg& c, DevTable tb, DevOverflow ov, const Status* st, hipStream_t s) {
-  hipLaunchKernelGGL(k_merge_overflow, dim3((c.P + 63) / 64), dim3(64), 0, s, c, tb, ov, st);
-}
 
 void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t s) {
   hipLaunchKernelGGL(k_table_stats, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, tb, out3);

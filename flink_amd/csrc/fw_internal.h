@@ -76,20 +76,39 @@ struct __attribute__((aligned(32))) PRec {
 __host__ __device__ inline uint32_t st_kind(uint32_t s) { return s & 3u; }
 
 struct Status {
-  unsigned long long out_rows;        // rows in the output buffer (pending)
-  unsigned long long side_rows;       // rows in the side buffer (pending)
+  unsigned long long out_rows;        // rows written to the output buffer (monotonic until reset)
+  unsigned long long side_rows;       // rows written to the side buffer (monotonic until reset)
   unsigned long long late_dropped;    // numLateRecordsDropped
-  unsigned long long slow_count;      // records of the last push routed to the ordered path
-  unsigned long long overflow_count;  // deltas parked in the overflow list
   unsigned long long fired_total;
   unsigned long long slow_total;
   unsigned long long merged;          // LDS deltas merged into HBM regions (k_aggregate)
-  int32_t max_live;                   // max live slots over regions touched since reset
+  long long slow_resume;              // ordered path: first list index not yet replayed
+  long long need_out;                 // fired-row capacity the ordered path asked for when it suspended
+  int32_t need_live;                  // largest live count a region asked for when it suspended
   int32_t flags;                      // FW_STATUS_*
   int32_t kg_errors;
   int32_t ts_errors;
+  int32_t suspended;                  // FW_SUSP_*: later kernels of the push / watermark skip themselves
+  int32_t need_grow;                  // some region is over half full: grow before it has to suspend
 };
-enum { FW_STATUS_OVERFLOW_LOST = 1, FW_STATUS_OUT_FULL = 2, FW_STATUS_MERGE_LATE = 4, FW_STATUS_SIDE_FULL = 8 };
+enum {
+  FW_STATUS_STATE_LOST = 1,  // a window could not be stored (more in-flight sessions of one key than supported)
+  FW_STATUS_OUT_FULL = 2,
+  FW_STATUS_MERGE_LATE = 4,
+  FW_STATUS_SIDE_FULL = 8
+};
+// a region takes new windows only up to this load; beyond it the kernel suspends and the table grows
+__host__ __device__ inline int32_t region_limit(int32_t log_r) { return (int32_t)((3ll << log_r) >> 2); }
+// suspension: a kernel stopped before changing anything it cannot keep (a region or the fired-row
+// buffer lacked room); the host grows the table / buffer and resumes exactly where it stopped
+enum { FW_SUSP_AGG = 1, FW_SUSP_SLOW = 2 };
+
+// k_aggregate progress, kept per partition so a suspended launch can be resumed
+struct AggProg {
+  long long* rb;     // [P] first record of the round to restart from
+  uint32_t* tp;      // [P * FW_AGG_THREADS] per thread: record (bits 0-7), window (bits 8-31) in that round
+  uint8_t* done;     // [P] partition finished in this push
+};
 
 struct DevTable {
   Entry* ent[2];
@@ -102,14 +121,10 @@ struct DevTable {
 struct DevRows {
   int64_t *key, *start, *end, *cnt, *sum, *mn, *mx;
   int64_t cap;
+  int64_t slow_limit;  // the ordered path stops here, leaving room for one watermark's firing (cap - table slots)
 };
 struct DevSide {
   int64_t *key, *ts, *val;
-  int64_t cap;
-};
-struct DevOverflow {  // deltas that did not fit their region; merged after the table grows
-  Entry* ent;
-  int32_t* part;
   int64_t cap;
 };
 
@@ -123,12 +138,12 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
                     const int32_t* kh, int64_t n, int32_t T, uint32_t* offs, PRec* part, int64_t* sk,
                     int64_t* stt, int64_t* sv, int32_t* skh, DevSide side, Status* st, hipStream_t_ s);
 void launch_aggregate(const DevCfg& c, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
-                      DevOverflow ov, Status* st, hipStream_t_ s);
-void launch_slow(const DevCfg& c, int64_t wm, const int64_t* sk, const int64_t* stt, const int64_t* sv,
-                 const int32_t* skh, DevTable tb, DevRows out, DevSide side, Status* st, hipStream_t_ s);
+                      AggProg prog, int resume, Status* st, hipStream_t_ s);
+void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* offs, int32_t T, const int64_t* sk,
+                 const int64_t* stt, const int64_t* sv, const int32_t* skh, DevTable tb, DevRows out, DevSide side,
+                 Status* st, int resume, hipStream_t_ s);
 void launch_fire(const DevCfg& c, int64_t wm, DevTable tb, DevRows out, Status* st, hipStream_t_ s);
 void launch_rehash(const DevCfg& old_c, DevTable old_t, const DevCfg& new_c, DevTable new_t, hipStream_t_ s);
-void launch_merge_overflow(const DevCfg& c, DevTable tb, DevOverflow ov, const Status* st, hipStream_t_ s);
 void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t_ s);
 void launch_reset_regions(const DevCfg& c, DevTable tb, hipStream_t_ s);
 void launch_key_groups(const int64_t* key, const int32_t* kh, int32_t key_kind, int64_t n, int32_t max_par,

@@ -4,6 +4,17 @@
 // KeyGroupRange, the per-batch scratch, the fired-row buffer and one HIP stream.  Every public
 // call is serialised by the caller (the Flink task thread holds the checkpoint lock around
 // processElement / processWatermark, StreamInputProcessor.java:211-222).
+//
+// Asynchrony.  Device pushes and count-less watermarks only queue work; every queued sequence ends
+// with a copy of the device Status into pinned memory and an event (the "snapshot").  The next call
+// that needs the status waits for the snapshot and settles the sequence: if a kernel suspended
+// because a state region or the fired-row buffer lacked room, the table / buffer is grown and the
+// suspended kernels are resumed where they stopped (and a watermark the suspension skipped is fired
+// again); errors the sequence detected are returned by that call.
+//
+// A push queues its classify / scan / scatter kernels BEFORE it waits for the previous snapshot:
+// they only read the batch and write this push's scratch set (two sets alternate), so they run
+// while the host waits and settles, and the state kernels are queued before the GPU drains.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -19,9 +30,15 @@
 
 namespace {
 
-struct DevBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
+// per-batch scratch; two sets alternate so a push can be resumed while the next one is classified
+struct Scratch {
+  uint32_t* hist = nullptr;      // (P+2) x T histogram, scanned in place into offsets
+  uint32_t* scan_tmp = nullptr;
+  PRec* part = nullptr;          // the batch's normal records, partition-major
+  int64_t *sk = nullptr, *stt = nullptr, *sv = nullptr;  // ordered-path list
+  int32_t* skh = nullptr;
+  int32_t T = 0;                 // tiles of the batch that used this set
+  int64_t wm = INT64_MIN;        // watermark the batch was classified against
 };
 
 }  // namespace
@@ -43,20 +60,26 @@ struct fw_op {
   int32_t tmax = 0;
   int64_t *in_key = nullptr, *in_ts = nullptr, *in_val = nullptr;
   int32_t* in_kh = nullptr;
-  uint32_t *hist = nullptr, *scan_tmp = nullptr;
-  PRec* part = nullptr;  // partitioned records of the current batch
-  int64_t *sk = nullptr, *stt = nullptr, *sv = nullptr;
-  int32_t* skh = nullptr;
+  Scratch sc[2];
+  int last_sc = 1;   // set of the most recent push
+  AggProg prog{};    // k_aggregate resume points
 
   DevRows out{};
   DevSide side{};
-  DevOverflow ov{};
+  int64_t out_base = 0, side_base = 0;  // rows already handed to the caller
   Status* d_status = nullptr;
-  Status* h_status = nullptr;
+  Status* h_status = nullptr;           // written by the snapshot copy: read only when settled
   unsigned long long* d_stats3 = nullptr;
 
   int64_t wm = INT64_MIN;
   int64_t records_in = 0;
+
+  // the queued, not yet settled sequence
+  hipEvent_t snap = nullptr;
+  bool unsynced = false;
+  bool push_unsettled = false;  // it holds a push (in scratch set last_sc)
+  bool fire_unsettled = false;  // it holds a watermark (fired again if the push suspended)
+  bool clear_deferred = false;  // fw_clear_pending was called meanwhile
 
   // optional per-kernel event timing (fw_profile)
   bool prof = false;
@@ -133,14 +156,42 @@ int alloc_table(fw_op* op, DevTable& t, const DevCfg& c, bool with_meta) {
   return FW_OK;
 }
 
-int ensure_out_capacity(fw_op* op, int64_t need) {
-  if (need <= op->out.cap) return FW_OK;
+int alloc_scratch(fw_op* op, Scratch& s, int64_t mb, int64_t m) {
+  HIP_OR_RETURN(op, dmalloc(&s.hist, m));
+  HIP_OR_RETURN(op, dmalloc(&s.scan_tmp, m / 4096 + 2));
+  HIP_OR_RETURN(op, dmalloc(&s.part, mb));
+  HIP_OR_RETURN(op, dmalloc(&s.sk, mb));
+  HIP_OR_RETURN(op, dmalloc(&s.stt, mb));
+  HIP_OR_RETURN(op, dmalloc(&s.sv, mb));
+  HIP_OR_RETURN(op, dmalloc(&s.skh, mb));
+  return FW_OK;
+}
+void free_scratch(Scratch& s) {
+  dfree(s.hist);
+  dfree(s.scan_tmp);
+  dfree(s.part);
+  dfree(s.sk);
+  dfree(s.stt);
+  dfree(s.sv);
+  dfree(s.skh);
+}
+
+// the ordered path may fill the fired-row buffer up to cap - table slots, so a watermark always has
+// room to fire every live window
+void set_slow_limit(fw_op* op) { op->out.slow_limit = std::max<int64_t>(0, op->out.cap - op->table_slots); }
+
+// grow the fired-row buffer to hold `need` rows, keeping the first `keep` (stream idle on exit)
+int ensure_out_capacity(fw_op* op, int64_t need, int64_t keep) {
+  if (need <= op->out.cap) {
+    set_slow_limit(op);
+    return FW_OK;
+  }
   const int64_t cap = std::max(need, op->out.cap * 2);
   DevRows n{};
   int64_t** cols_new[7] = {&n.key, &n.start, &n.end, &n.cnt, &n.sum, &n.mn, &n.mx};
   int64_t** cols_old[7] = {&op->out.key, &op->out.start, &op->out.end, &op->out.cnt,
                            &op->out.sum, &op->out.mn, &op->out.mx};
-  const int64_t keep = std::min<int64_t>((int64_t)op->h_status->out_rows, op->out.cap);
+  keep = std::min(keep, op->out.cap);
   for (int i = 0; i < 7; i++) {
     HIP_OR_RETURN(op, dmalloc(cols_new[i], (size_t)cap));
     if (keep > 0 && *cols_old[i])
@@ -151,16 +202,17 @@ int ensure_out_capacity(fw_op* op, int64_t need) {
   for (int i = 0; i < 7; i++) dfree(*cols_old[i]);
   n.cap = cap;
   op->out = n;
+  set_slow_limit(op);
   return FW_OK;
 }
 
-int ensure_side_capacity(fw_op* op, int64_t need) {
+int ensure_side_capacity(fw_op* op, int64_t need, int64_t keep) {
   if (need <= op->side.cap) return FW_OK;
   const int64_t cap = std::max(need, op->side.cap * 2);
   DevSide n{};
   int64_t** cols_new[3] = {&n.key, &n.ts, &n.val};
   int64_t** cols_old[3] = {&op->side.key, &op->side.ts, &op->side.val};
-  const int64_t keep = std::min<int64_t>((int64_t)op->h_status->side_rows, op->side.cap);
+  keep = std::min(keep, op->side.cap);
   for (int i = 0; i < 3; i++) {
     HIP_OR_RETURN(op, dmalloc(cols_new[i], (size_t)cap));
     if (keep > 0 && *cols_old[i])
@@ -201,8 +253,15 @@ void timed(fw_op* op, int kind, F&& launch) {
   (void)hipEventRecord(pr.b, op->stream);
   op->prof_pending.push_back(pr);
 }
+// fold the completed intervals into the totals (intervals still in flight stay pending)
 void prof_collect(fw_op* op) {
-  for (auto& pr : op->prof_pending) {
+  size_t keep = 0;
+  for (size_t i = 0; i < op->prof_pending.size(); i++) {
+    fw_op::Pair& pr = op->prof_pending[i];
+    if (hipEventQuery(pr.b) != hipSuccess) {
+      op->prof_pending[keep++] = pr;
+      continue;
+    }
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, pr.a, pr.b) == hipSuccess) {
       op->prof_ms[pr.kind] += ms;
@@ -211,9 +270,18 @@ void prof_collect(fw_op* op) {
     op->prof_free.push_back(pr.a);
     op->prof_free.push_back(pr.b);
   }
-  op->prof_pending.clear();
+  op->prof_pending.resize(keep);
 }
 
+// queue the status snapshot that ends a sequence
+int snapshot(fw_op* op) {
+  HIP_OR_RETURN(op, hipMemcpyAsync(op->h_status, op->d_status, sizeof(Status), hipMemcpyDeviceToHost, op->stream));
+  HIP_OR_RETURN(op, hipEventRecord(op->snap, op->stream));
+  op->unsynced = true;
+  return FW_OK;
+}
+
+// status of everything queued so far (stream idle on exit)
 int sync_status(fw_op* op) {
   HIP_OR_RETURN(op, hipMemcpyAsync(op->h_status, op->d_status, sizeof(Status), hipMemcpyDeviceToHost, op->stream));
   HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
@@ -221,7 +289,8 @@ int sync_status(fw_op* op) {
   return FW_OK;
 }
 
-// write one field of the device status from the host copy
+// write one field of the device status from the host copy.  Only fields no queued kernel writes
+// (the suspension bookkeeping, or counters while the stream is idle) are written this way.
 template <class T>
 int put_status_field(fw_op* op, T Status::*field) {
   const size_t off = (size_t)((char*)&(op->h_status->*field) - (char*)op->h_status);
@@ -230,8 +299,9 @@ int put_status_field(fw_op* op, T Status::*field) {
   return FW_OK;
 }
 
-// grow every region to new_log_r, re-inserting the live entries and then the parked overflow
+// grow every region to new_log_r, re-inserting the live entries (stream idle on exit)
 int grow_table(fw_op* op, int new_log_r) {
+  if (new_log_r > 30) return set_err(op, FW_ERR_CAPACITY, "state region would exceed 2^30 slots");
   DevCfg nc = op->dc;
   nc.log_r = new_log_r;
   DevTable nt{};
@@ -239,9 +309,12 @@ int grow_table(fw_op* op, int new_log_r) {
   nt.live = op->tb.live;
   nt.next_timer = op->tb.next_timer;
   int rc = alloc_table(op, nt, nc, false);
-  if (rc) return rc;
+  if (rc) {
+    free_table(nt);
+    return set_err(op, FW_ERR_CAPACITY, "cannot grow the state table to %lld slots: %s",
+                   (long long)((int64_t)nc.P << nc.log_r), op->err.c_str());
+  }
   fwdev::launch_rehash(op->dc, op->tb, nc, nt, op->stream);
-  if (op->h_status->overflow_count > 0) fwdev::launch_merge_overflow(nc, nt, op->ov, op->d_status, op->stream);
   HIP_OR_RETURN(op, hipGetLastError());
   HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
   free_table(op->tb);
@@ -249,26 +322,69 @@ int grow_table(fw_op* op, int new_log_r) {
   op->dc = nc;
   op->table_slots = (int64_t)nc.P << nc.log_r;
   op->grows++;
-  op->h_status->overflow_count = 0;
-  if ((rc = put_status_field(op, &Status::overflow_count))) return rc;
-  // the parked deltas may have been larger than the slack: re-grow the overflow list with the table
-  const int64_t ovcap = std::max<int64_t>(op->table_slots / 2, 1 << 16);
-  if (ovcap > op->ov.cap) {
-    dfree(op->ov.ent);
-    dfree(op->ov.part);
-    HIP_OR_RETURN(op, dmalloc(&op->ov.ent, (size_t)ovcap));
-    HIP_OR_RETURN(op, dmalloc(&op->ov.part, (size_t)ovcap));
-    op->ov.cap = ovcap;
-  }
-  return ensure_out_capacity(op, (int64_t)op->h_status->out_rows + op->table_slots);
+  const int64_t rows = (int64_t)op->h_status->out_rows;
+  return ensure_out_capacity(op, rows + op->table_slots, rows);
 }
 
-// after every push / watermark: surface errors, grow the table when a region is over half full
-int after_sync(fw_op* op) {
+// smallest region size whose load limit leaves half the region free for `need` occupied slots
+int log_r_for(const fw_op* op, int64_t need) {
+  int log_r = op->dc.log_r + 1;
+  while ((int64_t(1) << log_r) < 2 * need) log_r++;
+  return log_r;
+}
+
+// Wait for the queued sequence and settle it (see the file comment).  Kernels queued after the
+// snapshot (the next push's classify / scan / scatter) may still be running: they use the other
+// scratch set and write no status field that is rewritten here.
+int settle(fw_op* op) {
+  if (!op->unsynced) return FW_OK;
+  HIP_OR_RETURN(op, hipEventSynchronize(op->snap));
+  if (!op->prof_pending.empty()) prof_collect(op);
   Status& s = *op->h_status;
-  if (s.flags & FW_STATUS_OVERFLOW_LOST)
+  int rc;
+  int rounds = 0;
+  while (s.suspended) {
+    if (++rounds > 64) return set_err(op, FW_ERR_STATE, "suspended push did not complete after 64 resumptions");
+    const int susp = s.suspended;
+    if (s.need_live > region_limit(op->dc.log_r) && (rc = grow_table(op, log_r_for(op, s.need_live)))) return rc;
+    if (s.need_out > op->out.slow_limit &&
+        (rc = ensure_out_capacity(op, (int64_t)s.need_out + op->table_slots, (int64_t)s.out_rows)))
+      return rc;
+    s.suspended = 0;
+    s.need_live = 0;
+    s.need_out = 0;
+    if ((rc = put_status_field(op, &Status::suspended)) || (rc = put_status_field(op, &Status::need_live)) ||
+        (rc = put_status_field(op, &Status::need_out)))
+      return rc;
+    const DevCfg& c = op->dc;
+    const Scratch& S = op->sc[op->last_sc];
+    if (susp & FW_SUSP_AGG)
+      timed(op, K_AGGREGATE, [&] {
+        fwdev::launch_aggregate(c, S.wm, S.part, S.hist, S.T, op->tb, op->prog, 1, op->d_status, op->stream);
+      });
+    // after an aggregate suspension the ordered path never started; otherwise it resumes
+    timed(op, K_SLOW, [&] {
+      fwdev::launch_slow(c, S.wm, S.hist, S.T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status,
+                         (susp & FW_SUSP_AGG) ? 0 : 1, op->stream);
+    });
+    // a watermark queued behind the push skipped itself; firing at the latest one is the same as
+    // firing at each (nothing was pushed in between)
+    if (op->fire_unsettled)
+      timed(op, K_FIRE, [&] { fwdev::launch_fire(c, op->wm, op->tb, op->out, op->d_status, op->stream); });
+    HIP_OR_RETURN(op, hipGetLastError());
+    if ((rc = sync_status(op))) return rc;
+  }
+  op->unsynced = op->push_unsettled = op->fire_unsettled = false;
+  if (op->clear_deferred) {
+    // rows the next push's scatter may have added since are side rows; side output never queues
+    // early (push_device), so both counts are exactly those of the cleared sequence
+    op->out_base = (int64_t)s.out_rows;
+    op->side_base = (int64_t)s.side_rows;
+    op->clear_deferred = false;
+  }
+  if (s.flags & FW_STATUS_STATE_LOST)
     return set_err(op, FW_ERR_CAPACITY,
-                   "state table overflowed beyond its overflow list (raise fw_config.expected_entries)");
+                   "a window could not be stored (more than 64 in-flight sessions of one key)");
   if (s.flags & FW_STATUS_OUT_FULL) return set_err(op, FW_ERR_STATE, "fired-row buffer overflow");
   if (s.flags & FW_STATUS_SIDE_FULL) return set_err(op, FW_ERR_STATE, "side-output buffer overflow");
   if (s.kg_errors) return set_err(op, FW_ERR_KEY_GROUP, "%d record(s) outside KeyGroupRange [%d, %d]", s.kg_errors,
@@ -282,49 +398,80 @@ int after_sync(fw_op* op) {
                    "The end timestamp of an event-time window cannot become earlier than the current watermark by "
                    "merging. Current watermark: %lld",
                    (long long)op->wm);
-  const int64_t R = int64_t(1) << op->dc.log_r;
-  int log_r = op->dc.log_r;
-  if (s.overflow_count > 0 || s.max_live > R / 2) {
-    int64_t need = std::max<int64_t>(s.max_live, 1) + (int64_t)s.overflow_count;
-    while ((int64_t(1) << log_r) < 2 * need || log_r == op->dc.log_r) log_r++;
-    int rc = grow_table(op, log_r);
-    if (rc) return rc;
+  if (s.need_grow) {  // grow ahead of need, before a region has to suspend
+    if ((rc = grow_table(op, op->dc.log_r + 1))) return rc;
+    s.need_grow = 0;
+    if ((rc = put_status_field(op, &Status::need_grow))) return rc;
   }
-  s.max_live = 0;
-  return put_status_field(op, &Status::max_live);
+  return FW_OK;
+}
+
+// rows handed out are forgotten lazily: the counters restart at 0 once everything was consumed
+// and the buffer is a quarter full (one status write every few watermarks, not per call).
+// Settled only; no queued kernel writes these counters (side output never queues early).
+int maybe_restart_rows(fw_op* op) {
+  Status& s = *op->h_status;
+  int rc;
+  if (op->out_base == (int64_t)s.out_rows && s.out_rows > 0 && (int64_t)s.out_rows > op->out.cap / 4) {
+    s.out_rows = 0;
+    op->out_base = 0;
+    if ((rc = put_status_field(op, &Status::out_rows))) return rc;
+  }
+  if (op->side_base == (int64_t)s.side_rows && s.side_rows > 0 && (int64_t)s.side_rows > op->side.cap / 4) {
+    s.side_rows = 0;
+    op->side_base = 0;
+    if ((rc = put_status_field(op, &Status::side_rows))) return rc;
+  }
+  return FW_OK;
 }
 
 int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int64_t n) {
   if (n == 0) return FW_OK;
   int rc;
   const DevCfg& c = op->dc;
-  // every record may be replayed on the ordered path and late-fire all its windows
-  if ((rc = ensure_out_capacity(op, (int64_t)op->h_status->out_rows + op->table_slots + n * c.wpr))) return rc;
-  if (c.side_output && (rc = ensure_side_capacity(op, (int64_t)op->h_status->side_rows + n))) return rc;
-  const DevCfg& cc = op->dc;
+  // queue the batch-only kernels before waiting for the previous sequence, except with side
+  // output (the scatter appends late records to the side buffer, whose capacity and counters the
+  // settle below must see unchanged)
+  const bool early = op->unsynced && !c.side_output;
+  if (!early && (rc = settle(op))) return rc;
+  if (!early && c.side_output) {
+    const int64_t rows = (int64_t)op->h_status->side_rows;
+    if ((rc = ensure_side_capacity(op, rows + n, rows))) return rc;
+  }
+  const int nxt = op->last_sc ^ 1;
+  Scratch& S = op->sc[nxt];
   const int32_t T = (int32_t)((n + FW_TILE - 1) / FW_TILE);
-  const int64_t m = (int64_t)(cc.P + 1) * T;
-  op->h_status->slow_count = 0;
-  if ((rc = put_status_field(op, &Status::slow_count))) return rc;
+  const int64_t m = (int64_t)(c.P + 1) * T;
   timed(op, K_CLASSIFY, [&] {
-    fwdev::launch_classify_hist(cc, op->wm, key, ts, kh, n, T, op->hist, op->d_status, op->stream);
+    fwdev::launch_classify_hist(c, op->wm, key, ts, kh, n, T, S.hist, op->d_status, op->stream);
   });
-  timed(op, K_SCAN, [&] { fwdev::launch_scan(op->hist, m, op->scan_tmp, op->stream); });
+  timed(op, K_SCAN, [&] { fwdev::launch_scan(S.hist, m, S.scan_tmp, op->stream); });
   timed(op, K_SCATTER, [&] {
-    fwdev::launch_scatter(cc, op->wm, key, ts, val, kh, n, T, op->hist, op->part, op->sk, op->stt, op->sv, op->skh,
-                          op->side, op->d_status, op->stream);
+    fwdev::launch_scatter(c, op->wm, key, ts, val, kh, n, T, S.hist, S.part, S.sk, S.stt, S.sv, S.skh, op->side,
+                          op->d_status, op->stream);
   });
+  HIP_OR_RETURN(op, hipGetLastError());
+  if (early && (rc = settle(op))) return rc;
+  if ((rc = maybe_restart_rows(op))) return rc;
+  // the ordered path checks its room per chunk and suspends when it runs out; one chunk always fits
+  const int64_t rows = (int64_t)op->h_status->out_rows;
+  const int64_t chunk_rows = (int64_t)FW_SLOW_THREADS * (c.assigner == FW_SESSION ? 1 : c.wpr);
+  if ((rc = ensure_out_capacity(op, rows + op->table_slots + chunk_rows, rows))) return rc;
+  const DevCfg& cc = op->dc;  // settle may have grown the table
   timed(op, K_AGGREGATE, [&] {
-    fwdev::launch_aggregate(cc, op->wm, op->part, op->hist, T, op->tb, op->ov, op->d_status, op->stream);
+    fwdev::launch_aggregate(cc, op->wm, S.part, S.hist, T, op->tb, op->prog, 0, op->d_status, op->stream);
   });
   timed(op, K_SLOW, [&] {
-    fwdev::launch_slow(cc, op->wm, op->sk, op->stt, op->sv, op->skh, op->tb, op->out, op->side, op->d_status,
+    fwdev::launch_slow(cc, op->wm, S.hist, T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status, 0,
                        op->stream);
   });
   HIP_OR_RETURN(op, hipGetLastError());
+  S.T = T;
+  S.wm = op->wm;
+  op->last_sc = nxt;
   op->records_in += n;
-  if ((rc = sync_status(op))) return rc;
-  return after_sync(op);
+  op->push_unsettled = true;
+  return snapshot(op);
 }
 
 }  // namespace
@@ -346,6 +493,8 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     if (cfg.offset < 0 || cfg.offset >= cfg.slide || cfg.size <= 0 || cfg.slide <= 0)
       snprintf(msg, sizeof msg,
                "SlidingEventTimeWindows parameters must satisfy 0 <= offset < slide and size > 0");
+    else if ((cfg.size + cfg.slide - 1) / cfg.slide > (1 << 20))
+      snprintf(msg, sizeof msg, "a sliding window may overlap at most 2^20 others (size / slide)");
   } else if (cfg.assigner == FW_SESSION) {
     if (cfg.gap <= 0) snprintf(msg, sizeof msg, "EventTimeSessionWindows parameters must satisfy 0 < size");
   } else {
@@ -379,6 +528,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   op->device = cfg.device;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   HIP_OR_RETURN(op, hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking));
+  HIP_OR_RETURN(op, hipEventCreateWithFlags(&op->snap, hipEventDisableTiming));
 
   DevCfg& c = op->dc;
   c.assigner = cfg.assigner;
@@ -420,24 +570,18 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   HIP_OR_RETURN(op, dmalloc(&op->in_ts, mb));
   HIP_OR_RETURN(op, dmalloc(&op->in_val, mb));
   HIP_OR_RETURN(op, dmalloc(&op->in_kh, mb));
-  HIP_OR_RETURN(op, dmalloc(&op->hist, m));
-  HIP_OR_RETURN(op, dmalloc(&op->scan_tmp, m / 4096 + 2));
-  HIP_OR_RETURN(op, dmalloc(&op->part, mb));
-  HIP_OR_RETURN(op, dmalloc(&op->sk, mb));
-  HIP_OR_RETURN(op, dmalloc(&op->stt, mb));
-  HIP_OR_RETURN(op, dmalloc(&op->sv, mb));
-  HIP_OR_RETURN(op, dmalloc(&op->skh, mb));
-  const int64_t ovcap = std::max<int64_t>(op->table_slots / 2, 1 << 16);
-  HIP_OR_RETURN(op, dmalloc(&op->ov.ent, ovcap));
-  HIP_OR_RETURN(op, dmalloc(&op->ov.part, ovcap));
-  op->ov.cap = ovcap;
+  for (Scratch& sc : op->sc)
+    if ((rc = alloc_scratch(op, sc, mb, m))) return rc;
+  HIP_OR_RETURN(op, dmalloc(&op->prog.rb, (size_t)c.P));
+  HIP_OR_RETURN(op, dmalloc(&op->prog.tp, (size_t)c.P * FW_AGG_THREADS));
+  HIP_OR_RETURN(op, dmalloc(&op->prog.done, (size_t)c.P));
   HIP_OR_RETURN(op, dmalloc(&op->d_status, 1));
   HIP_OR_RETURN(op, dmalloc(&op->d_stats3, 4));
   HIP_OR_RETURN(op, hipMemsetAsync(op->d_status, 0, sizeof(Status), op->stream));
   HIP_OR_RETURN(op, hipHostMalloc((void**)&op->h_status, sizeof(Status), hipHostMallocDefault));
   memset(op->h_status, 0, sizeof(Status));
-  if ((rc = ensure_out_capacity(op, 2 * op->table_slots))) return rc;
-  if ((rc = ensure_side_capacity(op, cfg.side_output ? mb : 1))) return rc;
+  if ((rc = ensure_out_capacity(op, 2 * op->table_slots, 0))) return rc;
+  if ((rc = ensure_side_capacity(op, cfg.side_output ? mb : 1, 0))) return rc;
   HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
   return FW_OK;
 }
@@ -456,15 +600,10 @@ void fw_destroy(fw_op* op) {
   dfree(op->in_ts);
   dfree(op->in_val);
   dfree(op->in_kh);
-  dfree(op->hist);
-  dfree(op->scan_tmp);
-  dfree(op->part);
-  dfree(op->sk);
-  dfree(op->stt);
-  dfree(op->sv);
-  dfree(op->skh);
-  dfree(op->ov.ent);
-  dfree(op->ov.part);
+  for (Scratch& sc : op->sc) free_scratch(sc);
+  dfree(op->prog.rb);
+  dfree(op->prog.tp);
+  dfree(op->prog.done);
   for (int64_t** col : {&op->out.key, &op->out.start, &op->out.end, &op->out.cnt, &op->out.sum, &op->out.mn,
                         &op->out.mx, &op->side.key, &op->side.ts, &op->side.val})
     dfree(*col);
@@ -475,6 +614,7 @@ void fw_destroy(fw_op* op) {
     (void)hipEventDestroy(pr.b);
   }
   for (hipEvent_t e : op->prof_free) (void)hipEventDestroy(e);
+  if (op->snap) (void)hipEventDestroy(op->snap);
   if (op->h_status) (void)hipHostFree(op->h_status);
   if (op->stream) (void)hipStreamDestroy(op->stream);
   delete op;
@@ -498,7 +638,7 @@ int fw_push_batch(fw_op* op, const int64_t* key, const int64_t* ts, const void* 
     int rc = push_device(op, op->in_key, op->in_ts, op->in_val, op->in_kh, m);
     if (rc) return rc;
   }
-  return FW_OK;
+  return settle(op);  // host columns: the caller may reuse them when this returns
 }
 
 int fw_push_batch_device(fw_op* op, const int64_t* key, const int64_t* ts, const void* val, const int32_t* key_hash,
@@ -518,28 +658,42 @@ int fw_push_batch_device(fw_op* op, const int64_t* key, const int64_t* ts, const
 int fw_advance_watermark(fw_op* op, int64_t wm, int64_t* n_pending) {
   if (!op) return FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
-  int rc = ensure_out_capacity(op, (int64_t)op->h_status->out_rows + op->table_slots);
-  if (rc) return rc;
+  int rc;
+  // settled: the host knows the row count; unsettled: the ordered path left cap - table slots free
+  // and an earlier watermark of the sequence found the buffer with that room as well
+  if (!op->unsynced) {
+    const int64_t rows = (int64_t)op->h_status->out_rows;
+    if ((rc = ensure_out_capacity(op, rows + op->table_slots, rows))) return rc;
+  } else if (op->fire_unsettled && (rc = settle(op))) {
+    return rc;  // two watermarks in one sequence: the second needs the first's row count
+  }
   timed(op, K_FIRE, [&] { fwdev::launch_fire(op->dc, wm, op->tb, op->out, op->d_status, op->stream); });
   HIP_OR_RETURN(op, hipGetLastError());
   op->wm = wm;  // HeapInternalTimerService.advanceWatermark: currentWatermark = time
-  if ((rc = sync_status(op))) return rc;
-  if ((rc = after_sync(op))) return rc;
-  if (n_pending) *n_pending = (int64_t)op->h_status->out_rows;
+  op->fire_unsettled = true;
+  if ((rc = snapshot(op))) return rc;
+  if (!n_pending) return FW_OK;  // asynchronous: the count is left to the next settling call
+  if ((rc = settle(op))) return rc;
+  *n_pending = (int64_t)op->h_status->out_rows - op->out_base;
   return FW_OK;
 }
 
 int fw_pending(fw_op* op, int64_t* n_rows, int64_t* n_side) {
   if (!op) return FW_ERR_ARG;
-  if (n_rows) *n_rows = (int64_t)op->h_status->out_rows;
-  if (n_side) *n_side = (int64_t)op->h_status->side_rows;
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  int rc = settle(op);
+  if (rc) return rc;
+  if (n_rows) *n_rows = (int64_t)op->h_status->out_rows - op->out_base;
+  if (n_side) *n_side = (int64_t)op->h_status->side_rows - op->side_base;
   return FW_OK;
 }
 
 int fw_drain_rows(fw_op* op, const fw_rows* dst, int64_t cap, int64_t* n) {
   if (!op || !dst) return FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
-  const int64_t have = (int64_t)op->h_status->out_rows;
+  int rc = settle(op);
+  if (rc) return rc;
+  const int64_t base = op->out_base, have = (int64_t)op->h_status->out_rows - base;
   if (cap < have) {
     if (n) *n = have;
     return set_err(op, FW_ERR_ARG, "drain capacity %lld < pending rows %lld", (long long)cap, (long long)have);
@@ -548,20 +702,20 @@ int fw_drain_rows(fw_op* op, const fw_rows* dst, int64_t cap, int64_t* n) {
     int64_t* d[7] = {dst->key, dst->start, dst->end, dst->count, dst->sum, dst->min, dst->max};
     int64_t* s[7] = {op->out.key, op->out.start, op->out.end, op->out.cnt, op->out.sum, op->out.mn, op->out.mx};
     for (int i = 0; i < 7; i++)
-      if (d[i]) HIP_OR_RETURN(op, hipMemcpyAsync(d[i], s[i], have * 8, hipMemcpyDeviceToHost, op->stream));
+      if (d[i]) HIP_OR_RETURN(op, hipMemcpyAsync(d[i], s[i] + base, have * 8, hipMemcpyDeviceToHost, op->stream));
   }
-  op->h_status->out_rows = 0;
-  int rc = put_status_field(op, &Status::out_rows);
-  if (rc) return rc;
   HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
+  op->out_base += have;
   if (n) *n = have;
-  return FW_OK;
+  return maybe_restart_rows(op);
 }
 
 int fw_drain_side(fw_op* op, const fw_side_rows* dst, int64_t cap, int64_t* n) {
   if (!op || !dst) return FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
-  const int64_t have = (int64_t)op->h_status->side_rows;
+  int rc = settle(op);
+  if (rc) return rc;
+  const int64_t base = op->side_base, have = (int64_t)op->h_status->side_rows - base;
   if (cap < have) {
     if (n) *n = have;
     return set_err(op, FW_ERR_ARG, "drain capacity %lld < pending side rows %lld", (long long)cap, (long long)have);
@@ -570,48 +724,53 @@ int fw_drain_side(fw_op* op, const fw_side_rows* dst, int64_t cap, int64_t* n) {
     int64_t* d[3] = {dst->key, dst->ts, dst->val};
     int64_t* s[3] = {op->side.key, op->side.ts, op->side.val};
     for (int i = 0; i < 3; i++)
-      if (d[i]) HIP_OR_RETURN(op, hipMemcpyAsync(d[i], s[i], have * 8, hipMemcpyDeviceToHost, op->stream));
+      if (d[i]) HIP_OR_RETURN(op, hipMemcpyAsync(d[i], s[i] + base, have * 8, hipMemcpyDeviceToHost, op->stream));
   }
-  op->h_status->side_rows = 0;
-  int rc = put_status_field(op, &Status::side_rows);
-  if (rc) return rc;
   HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
+  op->side_base += have;
   if (n) *n = have;
-  return FW_OK;
+  return maybe_restart_rows(op);
 }
 
 int fw_rows_device(fw_op* op, fw_rows* view, int64_t* n) {
   if (!op || !view) return FW_ERR_ARG;
-  view->key = op->out.key;
-  view->start = op->out.start;
-  view->end = op->out.end;
-  view->count = op->out.cnt;
-  view->sum = op->out.sum;
-  view->min = op->out.mn;
-  view->max = op->out.mx;
-  if (n) *n = (int64_t)op->h_status->out_rows;
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  int rc = settle(op);
+  if (rc) return rc;
+  const int64_t b = op->out_base;
+  view->key = op->out.key + b;
+  view->start = op->out.start + b;
+  view->end = op->out.end + b;
+  view->count = op->out.cnt + b;
+  view->sum = op->out.sum + b;
+  view->min = op->out.mn + b;
+  view->max = op->out.mx + b;
+  if (n) *n = (int64_t)op->h_status->out_rows - b;
   return FW_OK;
 }
 
 int fw_clear_pending(fw_op* op) {
   if (!op) return FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
-  op->h_status->out_rows = 0;
-  op->h_status->side_rows = 0;
-  int rc = put_status_field(op, &Status::out_rows);
-  if (!rc) rc = put_status_field(op, &Status::side_rows);
-  return rc;
+  if (op->unsynced) {  // applied when the queued sequence settles: no wait here
+    op->clear_deferred = true;
+    return FW_OK;
+  }
+  op->out_base = (int64_t)op->h_status->out_rows;
+  op->side_base = (int64_t)op->h_status->side_rows;
+  return maybe_restart_rows(op);
 }
 
 int fw_get_stats(fw_op* op, fw_stats* o) {
   if (!op || !o) return FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
+  int rc = settle(op);
+  if (rc) return rc;
   HIP_OR_RETURN(op, hipMemsetAsync(op->d_stats3, 0, 4 * sizeof(unsigned long long), op->stream));
   fwdev::launch_table_stats(op->dc, op->tb, op->d_stats3, op->stream);
   unsigned long long h3[4];
   HIP_OR_RETURN(op, hipMemcpyAsync(h3, op->d_stats3, sizeof h3, hipMemcpyDeviceToHost, op->stream));
-  int rc = sync_status(op);
-  if (rc) return rc;
+  if ((rc = sync_status(op))) return rc;
   const Status& s = *op->h_status;
   o->records_in = op->records_in;
   o->late_records_dropped = (int64_t)s.late_dropped;
@@ -619,8 +778,8 @@ int fw_get_stats(fw_op* op, fw_stats* o) {
   o->event_time_timers = (int64_t)h3[1];
   o->current_watermark = op->wm;
   o->fired_rows_total = (int64_t)s.fired_total;
-  o->pending_rows = (int64_t)s.out_rows;
-  o->pending_side_rows = (int64_t)s.side_rows;
+  o->pending_rows = (int64_t)s.out_rows - op->out_base;
+  o->pending_side_rows = (int64_t)s.side_rows - op->side_base;
   o->table_capacity = op->table_slots;
   o->table_grows = op->grows;
   o->slow_path_records = (int64_t)s.slow_total;
@@ -653,6 +812,9 @@ const char* fw_kernel_name(int kind) { return kind >= 0 && kind < FW_NUM_KERNELS
 
 int fw_synchronize(fw_op* op) {
   if (!op) return FW_ERR_ARG;
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  int rc = settle(op);
+  if (rc) return rc;
   HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
   return FW_OK;
 }

@@ -69,6 +69,7 @@ class GpuWindowOperator:
             L.fw_destroy(self._h)
             self._h = None
             raise N.NativeError(rc, msg)
+        self._inflight = None  # device columns of a push the library may still be reading
         self.epoch = 0  # watermarks processed so far
         self._rows = []
         self._side = []
@@ -76,8 +77,9 @@ class GpuWindowOperator:
     # ------------------------------------------------------------------ lifecycle
     def close(self):
         if getattr(self, "_h", None):
-            N.lib().fw_destroy(self._h)
+            N.lib().fw_destroy(self._h)  # waits for the stream
             self._h = None
+        self._inflight = None
 
     dispose = close
 
@@ -94,6 +96,14 @@ class GpuWindowOperator:
     def stream(self):
         return N.lib().fw_stream(self._h)
 
+    def _torch_stream(self, device):
+        """The library's HIP stream as a torch stream object (for stream-ordered handoffs)."""
+        s = getattr(self, "_tstream", None)
+        if s is None:
+            import torch
+            s = self._tstream = torch.cuda.ExternalStream(self.stream, device=device)
+        return s
+
     # ------------------------------------------------------------------ processElement
     def process_batch(self, keys, timestamps, values, key_hash=None):
         """Hands a micro-batch (all records between two watermarks, or a part of them) to the GPU."""
@@ -106,10 +116,12 @@ class GpuWindowOperator:
                     raise ValueError("device columns must be contiguous CUDA tensors of equal length")
             if keys.dtype != torch.int64 or timestamps.dtype != torch.int64:
                 raise ValueError("keys and timestamps must be int64")
-            # the library stream must see the producer's writes of these tensors
-            torch.cuda.current_stream(keys.device).synchronize()
+            # stream-ordered handoff: the library stream waits for the producer's writes.  The push
+            # is asynchronous; the columns are referenced until the next push has settled it.
+            self._torch_stream(keys.device).wait_stream(torch.cuda.current_stream(keys.device))
             rc = L.fw_push_batch_device(self._h, keys.data_ptr(), timestamps.data_ptr(), values.data_ptr(),
                                         key_hash.data_ptr() if key_hash is not None else None, n)
+            self._inflight = (keys, timestamps, values, key_hash)
         else:
             keys = np.ascontiguousarray(keys, dtype=np.int64)
             timestamps = np.ascontiguousarray(timestamps, dtype=np.int64)
@@ -129,10 +141,16 @@ class GpuWindowOperator:
     processElements = process_batch
 
     # ------------------------------------------------------------------ processWatermark
-    def advance_watermark(self, wm):
-        """Fires due windows; returns the number of rows pending in HBM (not copied)."""
+    def advance_watermark(self, wm, wait=True):
+        """Fires due windows; returns the number of rows pending in HBM (not copied).  With
+        wait=False the firing is only queued and None is returned (errors surface at the next call)."""
+        if not wait:
+            N.check(N.lib().fw_advance_watermark(self._h, int(wm), None), self._h)
+            self.epoch += 1
+            return None
         n = ctypes.c_int64()
         N.check(N.lib().fw_advance_watermark(self._h, int(wm), ctypes.byref(n)), self._h)
+        self._inflight = None
         self.epoch += 1
         return n.value
 
@@ -185,11 +203,14 @@ class GpuWindowOperator:
 
     def synchronize(self):
         N.check(N.lib().fw_synchronize(self._h), self._h)
+        self._inflight = None
 
     # ------------------------------------------------------------------ harness-style interface
     # (the shape of OneInputStreamOperatorTestHarness used by tests/kat_util.replay)
     def process(self, keys, ts, vals, key_hash=None):
+        # processElement raises at once in the reference: wait for the batch and surface its errors
         self.process_batch(keys, ts, vals, key_hash)
+        self.synchronize()
 
     def watermark(self, wm):
         self._rows.append(self.process_watermark(wm))

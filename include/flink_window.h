@@ -32,7 +32,7 @@ extern "C" {
 #define FW_ERR_HIP (-2)          /* HIP runtime failure */
 #define FW_ERR_NO_TIMESTAMP (-3) /* Long.MIN_VALUE timestamp: TumblingEventTimeWindows.java:69-71 */
 #define FW_ERR_KEY_GROUP (-4)    /* key outside the handle's KeyGroupRange (KeyGroupRangeOffsets / StateTable) */
-#define FW_ERR_CAPACITY (-5)     /* state table could not absorb a batch (see fw_config.expected_entries) */
+#define FW_ERR_CAPACITY (-5)     /* state could not be stored (HBM exhausted, or > 64 in-flight sessions of a key) */
 #define FW_ERR_UNSUPPORTED (-6)  /* configuration not offered on the GPU path */
 #define FW_ERR_STATE (-7)        /* corrupted / inconsistent handle state */
 
@@ -121,11 +121,17 @@ void fw_destroy(fw_op* op);
 const char* fw_last_error(const fw_op* op);
 
 /* processElement for a micro-batch (WindowOperator.java:291-421).
- *   fw_push_batch:        host buffers (a Java DirectByteBuffer in native byte order);
- *                         copied to HBM before the call returns.
+ *   fw_push_batch:        host buffers (a Java DirectByteBuffer in native byte order); the
+ *                         batch is processed completely before the call returns, and errors
+ *                         (FW_ERR_KEY_GROUP, FW_ERR_NO_TIMESTAMP, ...) are returned by it.
  *   fw_push_batch_device: device pointers already resident in HBM on the handle's device;
- *                         enqueued on the handle's stream, the buffers must stay valid until
- *                         the next fw_* call on the handle returns.
+ *                         enqueued on the handle's stream and returns without waiting.  The
+ *                         buffers must stay valid until the stream has passed the push (the
+ *                         next fw_* call that returns a count, or fw_synchronize).  Errors the
+ *                         batch raised are returned by that next call.
+ * The state table grows on demand: a kernel that finds a region (or the fired-row buffer) short
+ * of room stops before changing anything it could not keep, and the next synchronising call
+ * grows the table and resumes it where it stopped, so no batch size is too large for the state.
  * key_hash may be NULL unless key_kind == FW_KEY_HASHED.  val points to n int64 (FW_VAL_I64 /
  * FW_VAL_I32, the latter already sign-extended) or n doubles (FW_VAL_F64). */
 int fw_push_batch(fw_op* op, const int64_t* key, const int64_t* ts, const void* val, const int32_t* key_hash,
@@ -142,7 +148,8 @@ int fw_advance_watermark(fw_op* op, int64_t wm, int64_t* n_pending_rows);
 
 /* Pending output.  *_host copy into caller-owned host arrays of capacity cap and clear the
  * pending set; fw_rows_device exposes the pending rows in HBM without copying (valid until the
- * next fw_* call) and fw_clear_pending drops them. */
+ * next fw_* call) and fw_clear_pending drops them.  Each of these first settles an unsettled
+ * device push. */
 int fw_pending(fw_op* op, int64_t* n_rows, int64_t* n_side_rows);
 int fw_drain_rows(fw_op* op, const fw_rows* host_dst, int64_t cap, int64_t* n);
 int fw_drain_side(fw_op* op, const fw_side_rows* host_dst, int64_t cap, int64_t* n);
@@ -159,6 +166,7 @@ int fw_get_stats(fw_op* op, fw_stats* out);
 int fw_profile(fw_op* op, int enable);
 int fw_profile_read(fw_op* op, double* ms, int64_t* launches, int reset);
 const char* fw_kernel_name(int kind);
+/* wait for every queued push / watermark and return the error any of them raised */
 int fw_synchronize(fw_op* op);
 void* fw_stream(fw_op* op); /* the hipStream_t the handle enqueues on */
 

@@ -134,11 +134,94 @@ def test_gpu_lds_flush_and_retry(cfg):
 
 
 def test_gpu_table_growth():
-    # tiny initial table: forces overflow parking and region growth mid-stream
+    # tiny initial table: regions run out of room mid-aggregate, the push suspends, the table grows
+    # and the push resumes (several times per push)
     cfg = dict(assigner="tumbling", size=10_000)
     batches, wms = _stream(300_000, 100_000, 200_000, bound=100, jitter=100, rate=1_000_000)
     g, r, *_ = _run_both(cfg, batches, wms, expected_entries=1000)
     assert_rows_equal(g, r)
+
+
+def _run_device(cfg, batches, wms, **gpu_kw):
+    """Like _run_both, but the GPU side gets HBM-resident torch columns: pushes are asynchronous and
+    are only settled by the watermark that follows them."""
+    import torch
+    gpu = _gpu_op(**cfg, **gpu_kw)
+    ref = orc.WindowOperatorOracle(**cfg)
+    rows = []
+    for (k, t, v), wm in zip(batches, wms):
+        if len(k):
+            gpu.process_batch(*(torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (k, t, v)))
+        ref.process(k, t, v)
+        rows.append(gpu.process_watermark(wm))
+        ref.watermark(wm)
+    st = gpu.stats()
+    gpu.close()
+    return np.concatenate(rows), ref.rows(), st
+
+
+def test_gpu_burst_suspends_and_resumes_async():
+    # 2^20 distinct keys x 5 sliding windows in ONE asynchronous push into a table sized for 1000
+    # entries: k_aggregate suspends over and over; the watermark queued behind the push is skipped
+    # on the device and fired again after the host grew the table and resumed the push
+    cfg = dict(assigner="sliding", size=5000, slide=1000)
+    batches, wms = _stream(1 << 20, 1 << 20, 1 << 40, bound=100, jitter=100, rate=1_000_000)
+    g, r, st = _run_device(cfg, batches, wms, expected_entries=1000)
+    assert st["table_grows"] >= 3
+    assert_rows_equal(g, r)
+
+
+@pytest.mark.parametrize("cfg", [dict(assigner="tumbling", size=1000),
+                                 dict(assigner="sliding", size=3000, slide=1000, lateness=500)],
+                         ids=["tumbling", "sliding-late"])
+def test_gpu_async_pipeline_deferred_clear(cfg):
+    # the bench's step shape: device push, watermark queued without waiting, pending rows cleared
+    # without waiting (applied when the next push settles the sequence).  Rows of odd epochs are
+    # cleared, rows of even epochs kept; the kept rows must be exactly the oracle's rows of those epochs.
+    import torch
+    batches, wms = _stream(400_000, 20_000, 50_000, bound=300, jitter=900, rate=200_000)
+    gpu = _gpu_op(**cfg, expected_entries=1000)
+    ref = orc.WindowOperatorOracle(**cfg)
+    kept = []
+    for e, ((k, t, v), wm) in enumerate(zip(batches, wms)):
+        if len(k):
+            gpu.process_batch(*(torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (k, t, v)))
+        ref.process(k, t, v)
+        gpu.advance_watermark(wm, wait=False)
+        ref.watermark(wm)
+        if e % 2:
+            gpu.clear_pending()
+        else:
+            kept.append(gpu.drain_rows(e))
+    g = np.concatenate(kept)
+    r = ref.rows()
+    r = r[r["epoch"] % 2 == 0]
+    assert_rows_equal(g, r)
+    assert gpu.stats()["late_records_dropped"] == ref.late_dropped
+    gpu.close()
+
+
+def test_gpu_late_burst_suspends_ordered_path():
+    # a burst of late records for new keys, all within the allowed lateness: each one creates a
+    # window on the ordered path and fires it at once, so k_slow runs out of region room and of
+    # fired-row buffer, suspends, and is resumed chunk-exactly after the host grows both
+    cfg = dict(assigner="tumbling", size=1000, lateness=1 << 40)
+    n = 1 << 20
+    k1 = np.arange(n, dtype=np.int64)
+    k2 = np.arange(n, 2 * n, dtype=np.int64) * 7919
+    t1, t2 = k1 % 1000, (k2 % 997)
+    batches = [(k1, t1, k1 & 0xFF), (k2, t2, k2 & 0xFFF), (k1[:0], t1[:0], k1[:0])]
+    wms = [5000, 6000, (1 << 63) - 1]
+    for device in (False, True):
+        if device:
+            g, r, st = _run_device(cfg, batches, wms, expected_entries=1000)
+        else:
+            g, r, *_ = _run_both(cfg, batches, wms, expected_entries=1000)
+            st = None
+        assert len(r) == 2 * n
+        assert_rows_equal(g, r)
+        if st is not None:
+            assert st["slow_path_records"] == n and st["table_grows"] >= 1
 
 
 def test_gpu_key_group_range_subtask():
