@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc passes (tools/pmc.sh) into per-kernel, per-launch HBM bytes.
+
+Reads gpurun_out/pmc/p*/run_counter_collection.csv, averages each counter over the dispatches of
+each kernel, and derives HBM bytes as MI355X_MICROARCH.md §HBM prescribes:
+  read  bytes = FETCH_SIZE (KiB) * 1024 * 2   (gfx950 tallies a 128-B request of a wide coalesced
+                                               read as 64 B: the counter reads half the bytes)
+  write bytes = WRITE_SIZE (KiB) * 1024       (exact for 16-B-per-lane streaming stores)
+The correction factor for reads is checked against k_classify_hist, whose reads are known exactly
+(16 B per record: key + ts), and the calibration is printed beside the result.
+
+usage: tools/traffic.py [pmc_dir] [--records N] [--out profiles/traffic_rNN.json]
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+
+def short(name):
+    n = name.replace("(anonymous namespace)::", "")
+    return n.split("(")[0].replace("void ", "").strip()
+
+
+def load(pmc_dir):
+    vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per-dispatch values]
+    for f in sorted(glob.glob(os.path.join(pmc_dir, "p*", "run_counter_collection.csv"))):
+        per = defaultdict(float)
+        names = {}
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                key = (r["Dispatch_Id"], r["Counter_Name"])
+                per[key] += float(r["Counter_Value"])  # sum over dimensions (XCDs / instances)
+                names[r["Dispatch_Id"]] = short(r["Kernel_Name"])
+        for (d, cn), v in per.items():
+            vals[names[d]][cn].append(v)
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} | {"_dispatches": max(len(v) for v in cs.values())}
+            for k, cs in vals.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("pmc_dir", nargs="?", default="gpurun_out/pmc")
+    ap.add_argument("--records", type=int, default=1 << 24, help="records per push (bench --batch)")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    k = load(a.pmc_dir)
+    res = {}
+    for name, c in sorted(k.items()):
+        rd = c.get("FETCH_SIZE")
+        wr = c.get("WRITE_SIZE")
+        res[name] = {
+            "dispatches": c["_dispatches"],
+            "fetch_size_kib": rd,
+            "write_size_kib": wr,
+            "read_bytes": None if rd is None else rd * 1024 * 2,
+            "write_bytes": None if wr is None else wr * 1024,
+        }
+        for extra in ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"):
+            if extra in c:
+                res[name][extra] = c[extra]
+        r = res[name]
+        if r["read_bytes"] is not None and r["write_bytes"] is not None:
+            r["hbm_bytes"] = r["read_bytes"] + r["write_bytes"]
+    cal = None
+    if "k_classify_hist" in res and res["k_classify_hist"]["read_bytes"]:
+        cal = res["k_classify_hist"]["read_bytes"] / (16.0 * a.records)
+    out = {"note": "per-launch averages; read = FETCH_SIZE*1024*2 (gfx950 half-count correction), "
+                   "write = WRITE_SIZE*1024; Infinity-Cache hits are counted by these counters",
+           "records_per_launch": a.records,
+           "read_calibration_k_classify_hist": cal,
+           "per_launch_bytes": {n: r.get("hbm_bytes") for n, r in res.items()},
+           "kernels": res}
+    for n, r in res.items():
+        hb = r.get("hbm_bytes")
+        print(f"{n:28s} n={r['dispatches']:3d} read={r['read_bytes'] or 0:14.0f} write={r['write_bytes'] or 0:14.0f}"
+              f" per_rec={(hb or 0) / a.records:7.2f} B")
+    print("read calibration (k_classify_hist measured / 16 B per record):", cal)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
