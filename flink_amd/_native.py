@@ -4,7 +4,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libflinkwin.so")
+# FW_LIB selects a diagnostic build variant (tools/variants.sh); the product build is _lib/libflinkwin.so
+LIB_PATH = os.environ.get("FW_LIB") or os.path.join(_HERE, "_lib", "libflinkwin.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 FW_OK = 0

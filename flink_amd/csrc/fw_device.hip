@@ -409,9 +409,32 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_add(uint32_t* data, int64_t m, 
     if (base + e < m) data[base + e] += add;
 }
 
+// Store a 32-byte record per lane as whole sectors written by lane pairs: lanes 2i and 2i+1 first
+// write lane 2i's record (16 B each, contiguous), then lane 2i+1's.  The halves and positions are
+// swapped between the pair with DPP (quad_perm [1,0,3,2]); a wave's store then addresses 32 sectors
+// instead of 64 scattered 16-byte halves.  Every lane of the wave must reach this call.
+__device__ __forceinline__ uint32_t dpp_swap1(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int64_t dpp_swap1(int64_t x) {
+  const uint32_t lo = dpp_swap1((uint32_t)(uint64_t)x), hi = dpp_swap1((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ void store_pair(PRec* part, bool valid, uint32_t pos, i64x2 a, i64x2 b) {
+  const bool odd = __lane_id() & 1;
+  const i64x2 send = odd ? a : b;
+  const i64x2 recv = {dpp_swap1((int64_t)send.x), dpp_swap1((int64_t)send.y)};
+  const uint32_t ppos = dpp_swap1(pos);
+  const bool pval = dpp_swap1((uint32_t)valid) != 0;
+  // the even lane's record: the even lane writes its first half, the odd lane its second half
+  if (odd ? pval : valid) reinterpret_cast<i64x2*>(part + (odd ? ppos : pos))[odd] = odd ? recv : a;
+  // the odd lane's record
+  if (odd ? valid : pval) reinterpret_cast<i64x2*>(part + (odd ? pos : ppos))[odd] = odd ? b : recv;
+}
+
 // ---- K2: scatter.  Normal records -> their partition's run (any order inside the run), one
 // 32-byte sector per record; late records -> side output / counter.
-__global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
+__global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
                                                              const int64_t* __restrict__ ts,
                                                              const int64_t* __restrict__ val,
                                                              const int32_t* __restrict__ kh, int64_t n, int32_t T,
@@ -438,31 +461,40 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter(DevCfg c, int64_t w
 #pragma unroll
     for (int j = 0; j < FW_RPT; j++) {
       const int64_t i = b + (int64_t)j * blockDim.x + threadIdx.x;
-      if (i >= tend) continue;
-      const int32_t h = c.key_kind == FW_KEY_HASHED ? hh[j] : key_hash_of(c.key_kind, k[j], kh, i);
-      const int32_t p = partition_of(c, k[j], h);
-      if (p < 0) continue;
-      int64_t last;
-      int nwin;
-      const int cls = classify(c, wm, t[j], &last, &nwin);
-      if (cls == CLS_NORMAL) {
-        uint32_t pos = atomicAdd(&base[p], 1u);
-        if (c.diag & (DIAG_SCATTER_NO_STORE | DIAG_SCATTER_LINEAR)) {
-          if (c.diag & DIAG_SCATTER_NO_STORE) {
-            asm volatile("" ::"v"(pos), "v"(k[j]), "v"(last), "v"(v[j]));
-            continue;
+      bool norm = false;
+      uint32_t pos = 0;
+      int64_t last = 0;
+      int nwin = 0;
+      if (i < tend) {
+        const int32_t h = c.key_kind == FW_KEY_HASHED ? hh[j] : key_hash_of(c.key_kind, k[j], kh, i);
+        const int32_t p = partition_of(c, k[j], h);
+        if (p >= 0) {
+          const int cls = classify(c, wm, t[j], &last, &nwin);
+          if (cls == CLS_NORMAL) {
+            pos = atomicAdd(&base[p], 1u);
+            norm = true;
+          } else if (cls == CLS_LATE) {
+            if (c.side_output)
+              side_one(side, st, k[j], t[j], v[j]);
+            else
+              late++;
           }
-          pos = (uint32_t)(i - tbase) + (uint32_t)tbase;
         }
-        i64x2* dst = reinterpret_cast<i64x2*>(part + pos);
-        dst[0] = i64x2{k[j], last};
-        dst[1] = i64x2{v[j], (long long)nwin};
-      } else if (cls == CLS_LATE) {
-        if (c.side_output)
-          side_one(side, st, k[j], t[j], v[j]);
-        else
-          late++;
       }
+      if (c.diag & (DIAG_SCATTER_NO_STORE | DIAG_SCATTER_LINEAR | DIAG_SCATTER_SINGLE)) {
+        if (c.diag & DIAG_SCATTER_NO_STORE) {
+          asm volatile("" ::"v"(pos), "v"(k[j]), "v"(last), "v"(v[j]));
+          continue;
+        }
+        if (c.diag & DIAG_SCATTER_LINEAR) pos = (uint32_t)i;
+        if (norm) {
+          i64x2* dst = reinterpret_cast<i64x2*>(part + pos);
+          dst[0] = i64x2{k[j], last};
+          dst[1] = i64x2{v[j], (long long)nwin};
+        }
+        continue;
+      }
+      store_pair(part, norm, pos, i64x2{k[j], last}, i64x2{v[j], (long long)nwin});
     }
   }
   if (late) atomicAdd(&st->late_dropped, late);
@@ -528,7 +560,8 @@ struct AggLds {
   uint32_t tag[FW_LDS_SLOTS];
   uint32_t cnt[FW_LDS_SLOTS];  // per LDS epoch: at most one batch of one partition, < 2^32
   i64x2 kv[FW_LDS_SLOTS];      // {key, window start}: one ds_read_b128 per comparison
-  i64x2 mm[FW_LDS_SLOTS];      // {min, max}: one ds_read_b128 decides both conditional atomics
+  int64_t mn[FW_LDS_SLOTS];
+  int64_t mx[FW_LDS_SLOTS];
   int64_t sum[FW_LDS_SLOTS];
   int32_t slot[FW_LDS_SLOTS];  // flush: the window's slot in the region, -1 if new
   int fill;
@@ -540,86 +573,124 @@ struct AggLds {
 };
 enum : uint32_t { LT_EMPTY = 0, LT_BUSY = 1 };
 
+// LDS slot hash of (key, window start): 32-bit multiplies only (full-rate VALU), independent of
+// the fmix64 bits that chose the partition.  Low bits pick the bucket, the rest is the fingerprint.
+__device__ __forceinline__ uint32_t lds_hash(int64_t key, int64_t start) {
+  const uint64_t uk = (uint64_t)key, us = (uint64_t)start;
+  uint32_t h = (uint32_t)uk * 0x9E3779B1u ^ (uint32_t)(uk >> 32) * 0x85EBCA77u ^
+               ((uint32_t)us ^ (uint32_t)(us >> 32)) * 0xC2B2AE3Du;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return h;
+}
+__device__ __forceinline__ uint32_t lds_fp(uint32_t h) { return (h >> 8) | 2u; }  // >= 2, never EMPTY/BUSY
+
 // insert-or-accumulate one value into the LDS table; false when the table is at its fill limit
-// (the caller flushes and retries).  One loop, no early exit, so a lane that claims a slot
-// finishes publishing it inside the same iteration as the lanes that wait on it.
+// (the caller flushes and retries).  A lane that claims a slot publishes it inside the same loop
+// iteration (CAS EMPTY -> BUSY, write the key, store the fingerprint), so lanes of its own wave that
+// wait on the BUSY tag see the fingerprint on their next iteration.  LDS operations of one wave
+// complete in order, so a reader that sees the fingerprint reads the key written before it.
 __device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, int64_t start, int64_t v,
                                            int diag = 0) {
-  const uint64_t hh = fmix64((uint64_t)key ^ ((uint64_t)start * 0xD6E8FEB86659FD93ull));
-  const uint32_t fp = (uint32_t)(hh >> 32) | 2u;  // >= 2
-  uint32_t b = (uint32_t)hh & (LDS_BUCKETS - 1);
-  bool done = false, ok = false;
-  int guard = 0;
-  while (!done) {
+  const uint32_t h = lds_hash(key, start), fp = lds_fp(h);
+  uint32_t b = h & (LDS_BUCKETS - 1);
+  int target = -1;
+  for (int guard = 0; guard < 4 * LDS_BUCKETS;) {
     asm volatile("" ::: "memory");  // re-read the bucket every iteration (it may be claimed meanwhile)
     const u32x4 t4 = *reinterpret_cast<const u32x4*>(&L.tag[b * 4]);
-    const uint32_t tg[4] = {t4.x, t4.y, t4.z, t4.w};
-    int target = -1, empty = -1;
-    bool busy = false;
+    // branch-free scan of the bucket: one fingerprint candidate (the first; a second candidate with
+    // the same fingerprint is looked at on the next iteration), the first EMPTY slot, any BUSY slot
+    const int cand = t4.x == fp ? 0 : t4.y == fp ? 1 : t4.z == fp ? 2 : t4.w == fp ? 3 : -1;
+    const int empty = t4.x == LT_EMPTY ? 0 : t4.y == LT_EMPTY ? 1 : t4.z == LT_EMPTY ? 2 : t4.w == LT_EMPTY ? 3 : -1;
+    const bool busy = t4.x == LT_BUSY || t4.y == LT_BUSY || t4.z == LT_BUSY || t4.w == LT_BUSY;
+    if (cand >= 0) {
+      asm volatile("" ::: "memory");
+      const i64x2 kv = L.kv[b * 4 + cand];
+      if (kv.x == key && kv.y == start) {
+        target = (int)b * 4 + cand;
+        break;
+      }
+      // fingerprint collision: compare the bucket's other candidates one by one
+      bool found = false;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      if (tg[q] == fp && target < 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        const int s = (int)b * 4 + q;
-        const i64x2 kv = L.kv[s];
-        if (kv.x == key && kv.y == start) target = s;
-      } else if (tg[q] == LT_EMPTY && empty < 0) {
-        empty = q;
-      } else if (tg[q] == LT_BUSY) {
-        busy = true;
-      }
-    }
-    if (target < 0 && !busy) {
-      if (empty >= 0) {
-        if (__hip_atomic_load(&L.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= FW_LDS_FILL_LIMIT) {
-          done = true;  // table full: flush first
-        } else {
-          const int s = (int)b * 4 + empty;
-          if (atomicCAS(&L.tag[s], LT_EMPTY, LT_BUSY) == LT_EMPTY) {
-            atomicAdd(&L.fill, 1);
-            L.kv[s] = i64x2{key, start};
-            L.cnt[s] = 0;
-            L.sum[s] = 0;
-            L.mm[s] = i64x2{LMAX, LMIN};
-            __hip_atomic_store(&L.tag[s], fp, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            target = s;
+      for (int q = 0; q < 4; q++) {
+        const uint32_t tq = q == 0 ? t4.x : q == 1 ? t4.y : q == 2 ? t4.z : t4.w;
+        if (q > cand && tq == fp && !found) {
+          const i64x2 kq = L.kv[b * 4 + q];
+          if (kq.x == key && kq.y == start) {
+            target = (int)b * 4 + q;
+            found = true;
           }
-          // lost the claim race: re-read the bucket
         }
-      } else {
-        b = (b + 1) & (LDS_BUCKETS - 1);  // bucket full without a match
-        if (++guard >= LDS_BUCKETS) done = true;
       }
+      if (found) break;
     }
-    if (target >= 0 && (diag & DIAG_AGG_NO_ACCUM)) {
-      ok = true;
-      done = true;
-    } else if (target >= 0) {
-      atomicAdd(&L.cnt[target], 1u);
-      // min/max only change while a value beats the current extreme; a plain read first skips the
-      // atomic otherwise (the extremes only move one way, so a stale read can only cause an extra
-      // atomic, never a missed one)
-      const int64_t sv = vtype == FW_VAL_F64 ? f64_sortable(v) : v;
-      if (vtype == FW_VAL_F64)
-        atomicAdd((double*)&L.sum[target], __longlong_as_double(v));
-      else
-        atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)v);
-      const i64x2 cur = L.mm[target];
-      long long* mmp = reinterpret_cast<long long*>(&L.mm[target]);
-      if (sv < cur.x) atomicMin(mmp, (long long)sv);
-      if (sv > cur.y) atomicMax(mmp + 1, (long long)sv);
-      ok = true;
-      done = true;
+    if (busy) {  // a slot of this bucket is being published: re-read it
+      guard++;
+      continue;
     }
+    if (empty >= 0) {
+      if (__hip_atomic_load(&L.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= FW_LDS_FILL_LIMIT)
+        return false;  // table full: flush first
+      const int s = (int)b * 4 + empty;
+      if (atomicCAS(&L.tag[s], LT_EMPTY, LT_BUSY) == LT_EMPTY) {
+        atomicAdd(&L.fill, 1);
+        L.kv[s] = i64x2{key, start};
+        L.cnt[s] = 0;
+        L.sum[s] = 0;
+        L.mn[s] = LMAX;
+        L.mx[s] = LMIN;
+        __hip_atomic_store(&L.tag[s], fp, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        target = s;
+        break;
+      }
+      continue;  // lost the claim race: re-read the bucket
+    }
+    b = (b + 1) & (LDS_BUCKETS - 1);  // bucket full without a match
+    guard++;
   }
-  return ok;
+  if (target < 0) return false;
+  if (diag & DIAG_AGG_NO_ACCUM) return true;
+  // no-return LDS atomics: nothing below waits on the LDS
+  atomicAdd(&L.cnt[target], 1u);
+  if (vtype == FW_VAL_F64) {
+    atomicAdd((double*)&L.sum[target], __longlong_as_double(v));
+    const int64_t sv = f64_sortable(v);
+    atomicMin((long long*)&L.mn[target], (long long)sv);
+    atomicMax((long long*)&L.mx[target], (long long)sv);
+  } else {
+    atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)v);
+    atomicMin((long long*)&L.mn[target], (long long)v);
+    atomicMax((long long*)&L.mx[target], (long long)v);
+  }
+  return true;
+}
+
+// the LDS delta of slot h as a region entry
+__device__ __forceinline__ Entry lds_delta(const DevCfg& c, const AggLds& L, int h) {
+  const i64x2 kv = L.kv[h];
+  Entry d;
+  d.key = kv.x;
+  d.start = kv.y;
+  d.end = jadd(kv.y, c.size);
+  d.cnt = (int64_t)L.cnt[h];
+  d.sum = L.sum[h];
+  d.mn = L.mn[h];
+  d.mx = L.mx[h];
+  d.meta = FW_TIMER;
+  return d;
 }
 
 // merge every LDS window into the partition's HBM region, then reset the LDS table.
-// Phase A locates each window in the region (read-only) and counts the new ones; if the region
-// cannot take them within its load limit the flush changes nothing and returns false (the kernel
-// suspends and resumes after the table grows).  Phase B then updates the found entries in place
-// (plain read-modify-write: the workgroup owns the region) and claims EMPTY slots for the new ones.
+// Phase A locates each window in the region (read-only: its probe chain) and counts the new ones;
+// if the region cannot take them within its load limit the flush changes nothing and returns false
+// (the kernel suspends and resumes after the table grows).  Phase B then updates the found entries
+// in place (plain read-modify-write: the workgroup owns the region) and claims EMPTY slots for the
+// new ones.  (A front-to-back sweep of the region instead of probe chains measured slower at C2:
+// its dependent loads per thread are longer than a probe chain at a region's load.)
 __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* st) {
   __syncthreads();
   if (c.diag & DIAG_AGG_NO_FLUSH) {
@@ -632,8 +703,7 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
     if (L.tag[h] < 2) continue;
     const i64x2 kv = L.kv[h];
-    const int64_t k = kv.x, s = kv.y;
-    const int32_t slot = region_find(r, slot_hash(c, k, s), k, s, jadd(s, c.size));
+    const int32_t slot = region_find(r, slot_hash(c, kv.x, kv.y), kv.x, kv.y, jadd(kv.y, c.size));
     L.slot[h] = slot;
     nnew += slot < 0;
   }
@@ -649,17 +719,8 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
   int lost = 0;
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
     if (L.tag[h] < 2) continue;
+    const Entry d = lds_delta(c, L, h);
     nflush++;
-    const i64x2 kv = L.kv[h], mm = L.mm[h];
-    Entry d;
-    d.key = kv.x;
-    d.start = kv.y;
-    d.end = jadd(kv.y, c.size);
-    d.cnt = (int64_t)L.cnt[h];
-    d.sum = L.sum[h];
-    d.mn = mm.x;
-    d.mx = mm.y;
-    d.meta = FW_TIMER;
     mt = min(mt, jsub(d.end, 1));
     const int32_t slot = L.slot[h];
     if (slot >= 0) {
@@ -699,7 +760,11 @@ __device__ __forceinline__ void agg_publish(const DevCfg& c, AggLds& L, DevTable
   if (L.live > (1 << c.log_r) / 2) st->need_grow = 1;
 }
 
-__global__ __launch_bounds__(FW_AGG_THREADS) void k_aggregate(DevCfg c, int64_t wm, const PRec* __restrict__ part,
+// DIAG_AGG_TIMING: per-workgroup phase clocks (s_memtime), summed over the launch and printed by the
+// last workgroup to finish: [0] record loop, [1] flushes, [2] whole workgroup, [3] finished workgroups
+__device__ unsigned long long g_aggt[4];
+template <int RPT>
+__global__ __launch_bounds__(FW_AGG_THREADS, FW_AGG_WAVES) void k_aggregate(DevCfg c, int64_t wm, const PRec* __restrict__ part,
                                                               const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
                                                               AggProg prog, int resume, Status* st) {
   __shared__ AggLds L;
@@ -732,11 +797,13 @@ __global__ __launch_bounds__(FW_AGG_THREADS) void k_aggregate(DevCfg c, int64_t 
   __syncthreads();
   const Region r = region_of(c, tb, p, tb.cur[p]);
   bool ok = true, first = true;
-  for (int64_t rb = srb; rb < end && ok; rb += (int64_t)blockDim.x * FW_AGG_RPT) {
-    int64_t k[FW_AGG_RPT], t[FW_AGG_RPT], v[FW_AGG_RPT];
-    int nw[FW_AGG_RPT];
+  const bool timing = c.diag & DIAG_AGG_TIMING;
+  unsigned long long tw0 = timing ? __builtin_amdgcn_s_memtime() : 0, tflush = 0;
+  for (int64_t rb = srb; rb < end && ok; rb += (int64_t)blockDim.x * RPT) {
+    int64_t k[RPT], t[RPT], v[RPT];
+    int nw[RPT];
 #pragma unroll
-    for (int j = 0; j < FW_AGG_RPT; j++) {  // all loads in flight before any use
+    for (int j = 0; j < RPT; j++) {  // all loads in flight before any use
       const int64_t i = rb + (int64_t)j * blockDim.x + threadIdx.x;
       i64x2 a = {0, 0}, b2 = {0, 0};
       if (i < end) {
@@ -751,7 +818,7 @@ __global__ __launch_bounds__(FW_AGG_THREADS) void k_aggregate(DevCfg c, int64_t 
     }
     if (c.diag & DIAG_AGG_NO_LDS) {
 #pragma unroll
-      for (int j = 0; j < FW_AGG_RPT; j++) asm volatile("" ::"v"(k[j]), "v"(t[j]), "v"(v[j]), "v"(nw[j]));
+      for (int j = 0; j < RPT; j++) asm volatile("" ::"v"(k[j]), "v"(t[j]), "v"(v[j]), "v"(nw[j]));
       continue;
     }
     // progress (record rj, window rwi) survives a flush-and-retry when the LDS table fills up;
@@ -761,7 +828,7 @@ __global__ __launch_bounds__(FW_AGG_THREADS) void k_aggregate(DevCfg c, int64_t 
     for (;;) {
       bool failed = false;
 #pragma unroll
-      for (int j = 0; j < FW_AGG_RPT; j++) {
+      for (int j = 0; j < RPT; j++) {
         if (failed || j < rj || rb + (int64_t)j * blockDim.x + threadIdx.x >= end) continue;
         for (int wi = j == rj ? rwi : 0; wi < nw[j]; wi++) {
           if (!lds_upsert(L, c.vtype, k[j], jsub(t[j], (int64_t)wi * c.slide), v[j], c.diag)) {
@@ -775,12 +842,15 @@ __global__ __launch_bounds__(FW_AGG_THREADS) void k_aggregate(DevCfg c, int64_t 
       if (failed)
         L.anyfail = 1;
       else
-        rj = FW_AGG_RPT;  // all done: a retry pass after another thread's flush skips every record
+        rj = RPT;  // all done: a retry pass after another thread's flush skips every record
       __syncthreads();
       const int need = L.anyfail;
       __syncthreads();
       if (!need) break;
-      if (!agg_flush(c, L, r, st)) {
+      const unsigned long long tf0 = timing ? __builtin_amdgcn_s_memtime() : 0;
+      const bool fl = agg_flush(c, L, r, st);
+      if (timing) tflush += __builtin_amdgcn_s_memtime() - tf0;
+      if (!fl) {
         ok = false;
         break;
       }
@@ -791,7 +861,21 @@ __global__ __launch_bounds__(FW_AGG_THREADS) void k_aggregate(DevCfg c, int64_t 
       __syncthreads();
     }
   }
+  const unsigned long long tl = timing ? __builtin_amdgcn_s_memtime() : 0;
   if (ok) ok = agg_flush(c, L, r, st);
+  if (timing && threadIdx.x == 0) {
+    const unsigned long long te = __builtin_amdgcn_s_memtime();
+    atomicAdd(&g_aggt[0], tl - tw0 - tflush);
+    atomicAdd(&g_aggt[1], tflush + (te - tl));
+    atomicAdd(&g_aggt[2], te - tw0);
+    if (atomicAdd(&g_aggt[3], 1ull) == gridDim.x - 1) {
+      __threadfence();
+      const double n = (double)gridDim.x;
+      printf("agg timing: per WG loop %.0f flush %.0f total %.0f clocks (%d WGs)\n", g_aggt[0] / n, g_aggt[1] / n,
+             g_aggt[2] / n, (int)gridDim.x);
+      g_aggt[0] = g_aggt[1] = g_aggt[2] = g_aggt[3] = 0;
+    }
+  }
   if (!ok) {  // suspend: everything up to the last successful flush is in the region
     prog.tp[(int64_t)p * FW_AGG_THREADS + threadIdx.x] = (uint32_t)srj | ((uint32_t)srwi << 8);
     if (threadIdx.x == 0) {
@@ -1383,7 +1467,11 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
 
 void launch_aggregate(const DevCfg& c, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
                       AggProg prog, int resume, Status* st, hipStream_t s) {
-  hipLaunchKernelGGL(k_aggregate, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb, prog, resume, st);
+  if (c.diag & DIAG_AGG_RPT8)
+    hipLaunchKernelGGL(k_aggregate<8>, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb, prog, resume, st);
+  else
+    hipLaunchKernelGGL(k_aggregate<FW_AGG_RPT>, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb, prog, resume,
+                       st);
 }
 
 void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* offs, int32_t T, const int64_t* sk, const int64_t* stt,

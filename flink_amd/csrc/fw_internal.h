@@ -20,8 +20,19 @@
 
 #define FW_TILE 32768          // records per classify/scatter workgroup
 #define FW_TILE_THREADS 1024
+#ifndef FW_RPT
 #define FW_RPT 8               // records per thread kept in flight by the streaming kernels
-#define FW_AGG_RPT 4           // the same for k_aggregate (its LDS probe loops are unrolled per record)
+#endif
+#ifndef FW_AGG_RPT
+#define FW_AGG_RPT 2           // the same for k_aggregate: 2 keeps it at 80 VGPRs = 3 workgroups per CU
+#endif
+// minimum waves per SIMD the compiler must leave room for (register budget); 1 = no constraint
+#ifndef FW_AGG_WAVES
+#define FW_AGG_WAVES 1
+#endif
+#ifndef FW_SCATTER_WAVES
+#define FW_SCATTER_WAVES 1
+#endif
 #define FW_AGG_THREADS 512     // aggregate workgroup
 #define FW_LDS_SLOTS 1024      // LDS pre-aggregation slots per aggregate workgroup
 #define FW_LDS_FILL_LIMIT 820  // ~0.8 * FW_LDS_SLOTS: a new slot is not claimed beyond this fill
@@ -56,7 +67,10 @@ enum {
   DIAG_AGG_NO_LDS = 2,
   DIAG_SCATTER_NO_STORE = 4,
   DIAG_SCATTER_LINEAR = 8,
-  DIAG_AGG_NO_ACCUM = 16  // LDS lookup/claim only, no accumulate atomics
+  DIAG_AGG_NO_ACCUM = 16,  // LDS lookup/claim only, no accumulate atomics
+  DIAG_AGG_RPT8 = 64,      // k_aggregate with 8 records per thread in flight
+  DIAG_SCATTER_SINGLE = 128, // k_scatter: each lane stores its own record (no lane-pair sectors)
+  DIAG_AGG_TIMING = 256      // k_aggregate prints per-workgroup phase clocks
 };
 
 struct __attribute__((aligned(64))) Entry {
