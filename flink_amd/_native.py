@@ -44,6 +44,10 @@ class FwSideRows(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("key", "ts", "val")]
 
 
+class FwStateRows(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("key", "start", "end", "count", "sum", "min", "max", "timer")]
+
+
 class FwStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
         "records_in", "late_records_dropped", "keyed_state_entries", "event_time_timers", "current_watermark",
@@ -70,6 +74,8 @@ SIGNATURES = {
     "fw_profile_read": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_double), I64P, ctypes.c_int]),
     "fw_kernel_name": (ctypes.c_char_p, [ctypes.c_int]),
     "fw_stream": (VP, [VP]),
+    "fw_snapshot_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), ctypes.c_int64, I64P]),
+    "fw_restore_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), ctypes.c_int64]),
     "fw_key_groups_device": (ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, VP, VP]),
     "fw_route_device": (ctypes.c_int, [VP, VP, VP, VP, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
                                        ctypes.c_int32, VP, VP, VP, VP, VP, VP, ctypes.c_int64, VP]),

@@ -1301,6 +1301,104 @@ __global__ void k_reset_regions(DevCfg c, DevTable tb) {
   tb.next_timer[p] = LMAX;
 }
 
+// ---- keyed-state snapshot of one key group (HeapKeyedStateBackend.snapshot writes per key group,
+// HeapKeyedStateBackend.java:370-381): one workgroup per partition of the key group; each compacts
+// its region's live entries into the output columns behind one atomic reservation.
+__global__ __launch_bounds__(FW_FIRE_THREADS) void k_snapshot(DevCfg c, DevTable tb, int32_t p0, StateCols out,
+                                                             unsigned long long* count) {
+  __shared__ uint32_t sw[FW_FIRE_THREADS / 64 + 1];
+  __shared__ unsigned long long base_s;
+  const int32_t p = p0 + blockIdx.x;
+  const Region r = region_of(c, tb, p, tb.cur[p]);
+  const uint32_t R = r.mask + 1;
+  // one pass per block of the region: count, reserve, write
+  for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x) {
+    const uint32_t s = s0 + threadIdx.x;
+    const bool live = s < R && st_kind(ld_state(r.state + s)) == SLOT_LIVE;
+    uint32_t total;
+    const uint32_t pos = block_excl_scan(live ? 1u : 0u, sw, &total);
+    if (threadIdx.x == 0) base_s = total ? atomicAdd(count, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    if (live) {
+      const Entry e = r.ent[s];
+      const unsigned long long o = base_s + pos;
+      out.key[o] = e.key;
+      out.start[o] = e.start;
+      out.end[o] = e.end;
+      out.cnt[o] = e.cnt;
+      if (c.vtype == FW_VAL_F64) {
+        out.sum[o] = e.sum;
+        out.mn[o] = f64_unsortable(e.mn);
+        out.mx[o] = f64_unsortable(e.mx);
+      } else {
+        out.sum[o] = c.vtype == FW_VAL_I32 ? (int64_t)(int32_t)e.sum : e.sum;
+        out.mn[o] = e.mn;
+        out.mx[o] = e.mx;
+      }
+      out.timer[o] = (e.meta & FW_TIMER) ? 1 : 0;
+    }
+    __syncthreads();
+  }
+}
+
+// partition of a restored row of key group kg (the caller vouches for hashed keys); -1 when a
+// Long/Integer key does not belong to kg
+__device__ __forceinline__ int32_t restore_partition(const DevCfg& c, int32_t kg, int64_t key) {
+  if (c.key_kind != FW_KEY_HASHED && key_group(key_hash_of(c.key_kind, key, nullptr, 0), c.max_par) != kg) return -1;
+  const uint32_t sub = c.log_s ? (uint32_t)(fmix64((uint64_t)key ^ 0x5851F42D4C957F2Dull) >> (64 - c.log_s)) : 0u;
+  return ((kg - c.kg0) << c.log_s) | (int32_t)sub;
+}
+
+// demand of a restore per partition (to grow the table before inserting) and key-group errors
+__global__ void k_restore_count(DevCfg c, int32_t kg, StateCols in, int64_t n, int32_t* demand, Status* st) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t p = restore_partition(c, kg, in.key[i]);
+  if (p < 0)
+    atomicAdd(&st->kg_errors, 1);
+  else
+    atomicAdd(&demand[p], 1);
+}
+
+// insert (or merge) restored rows; the table has room for all of them (k_restore_count + growth)
+__global__ void k_restore(DevCfg c, int32_t kg, StateCols in, int64_t n, DevTable tb, Status* st) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t p = restore_partition(c, kg, in.key[i]);
+  if (p < 0) return;
+  Entry d;
+  d.key = in.key[i];
+  d.start = in.start[i];
+  d.end = in.end[i];
+  d.cnt = in.cnt[i];
+  d.sum = in.sum[i];
+  d.mn = c.vtype == FW_VAL_F64 ? f64_sortable(in.mn[i]) : in.mn[i];
+  d.mx = c.vtype == FW_VAL_F64 ? f64_sortable(in.mx[i]) : in.mx[i];
+  d.meta = in.timer[i] ? FW_TIMER : 0;
+  const Region r = region_of(c, tb, p, tb.cur[p]);
+  const uint64_t h = slot_hash(c, d.key, c.assigner == FW_SESSION ? 0 : d.start);
+  const int32_t found = region_find(r, h, d.key, d.start, d.end);
+  if (found >= 0) {  // the same window restored twice: AggregateFunction.merge
+    Entry& x = r.ent[found];
+    Entry cur = x;
+    acc_merge(c, cur, d);
+    cur.meta |= d.meta;
+    x = cur;
+    atomicMin((long long*)&tb.next_timer[p], (long long)timer_of(cur, c.lateness));
+    return;
+  }
+  const int32_t s = region_claim(r, h, SLOT_BUSY);
+  if (s < 0) {
+    atomicOr(&st->flags, FW_STATUS_STATE_LOST);
+    return;
+  }
+  r.ent[s] = d;
+  __threadfence();
+  __hip_atomic_store(r.state + s, live_word(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  atomicAdd(&tb.live[p], 1);
+  atomicMin((long long*)&tb.next_timer[p], (long long)timer_of(d, c.lateness));
+}
+
 // out3 = {live entries, event-time timers}
 __global__ __launch_bounds__(FW_FIRE_THREADS) void k_table_stats(DevCfg c, DevTable tb, unsigned long long* out3) {
   const int32_t p = blockIdx.x;
@@ -1489,6 +1587,20 @@ void launch_rehash(const DevCfg& oc, DevTable ot, const DevCfg& nc, DevTable nt,
   hipLaunchKernelGGL(k_rehash, dim3(oc.P), dim3(FW_FIRE_THREADS), 0, s, oc, ot, nc, nt);
 }
 
+
+void launch_snapshot(const DevCfg& c, DevTable tb, int32_t p0, int32_t np, StateCols out, unsigned long long* count,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(k_snapshot, dim3(np), dim3(FW_FIRE_THREADS), 0, s, c, tb, p0, out, count);
+}
+void launch_restore(const DevCfg& c, int32_t kg, StateCols in, int64_t n, int32_t* demand, DevTable tb, Status* st,
+                    hipStream_t s) {
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  if (!blocks) return;
+  if (demand)
+    hipLaunchKernelGGL(k_restore_count, dim3(blocks), dim3(256), 0, s, c, kg, in, n, demand, st);
+  else
+    hipLaunchKernelGGL(k_restore, dim3(blocks), dim3(256), 0, s, c, kg, in, n, tb, st);
+}
 
 void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t s) {
   hipLaunchKernelGGL(k_table_stats, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, tb, out3);

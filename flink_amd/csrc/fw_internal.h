@@ -137,6 +137,10 @@ struct DevRows {
   int64_t cap;
   int64_t slow_limit;  // the ordered path stops here, leaving room for one watermark's firing (cap - table slots)
 };
+// columns of keyed-state snapshot rows (fw_state_rows, device side)
+struct StateCols {
+  int64_t *key, *start, *end, *cnt, *sum, *mn, *mx, *timer;
+};
 struct DevSide {
   int64_t *key, *ts, *val;
   int64_t cap;
@@ -160,6 +164,11 @@ void launch_fire(const DevCfg& c, int64_t wm, DevTable tb, DevRows out, Status* 
 void launch_rehash(const DevCfg& old_c, DevTable old_t, const DevCfg& new_c, DevTable new_t, hipStream_t_ s);
 void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t_ s);
 void launch_reset_regions(const DevCfg& c, DevTable tb, hipStream_t_ s);
+void launch_snapshot(const DevCfg& c, DevTable tb, int32_t p0, int32_t np, StateCols out, unsigned long long* count,
+                     hipStream_t_ s);
+// demand != NULL: count rows per partition (and key-group errors); NULL: insert the rows
+void launch_restore(const DevCfg& c, int32_t kg, StateCols in, int64_t n, int32_t* demand, DevTable tb, Status* st,
+                    hipStream_t_ s);
 void launch_key_groups(const int64_t* key, const int32_t* kh, int32_t key_kind, int64_t n, int32_t max_par,
                        int32_t* kg, hipStream_t_ s);
 void launch_route(const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int32_t key_kind,

@@ -821,6 +821,112 @@ int fw_synchronize(fw_op* op) {
 
 void* fw_stream(fw_op* op) { return op ? (void*)op->stream : nullptr; }
 
+// ---- keyed-state snapshot / restore per key group (see flink_window.h)
+namespace {
+int kg_check(fw_op* op, int32_t kg) {
+  if (kg < op->dc.kg0 || kg >= op->dc.kg0 + op->dc.n_kg)
+    return set_err(op, FW_ERR_KEY_GROUP, "key group %d is not in this operator's KeyGroupRange [%d, %d]", kg,
+                   op->dc.kg0, op->dc.kg0 + op->dc.n_kg - 1);
+  return FW_OK;
+}
+int alloc_state_cols(fw_op* op, StateCols& c, int64_t n) {
+  int64_t** cols[8] = {&c.key, &c.start, &c.end, &c.cnt, &c.sum, &c.mn, &c.mx, &c.timer};
+  for (int i = 0; i < 8; i++) HIP_OR_RETURN(op, dmalloc(cols[i], (size_t)std::max<int64_t>(n, 1)));
+  return FW_OK;
+}
+void free_state_cols(StateCols& c) {
+  int64_t** cols[8] = {&c.key, &c.start, &c.end, &c.cnt, &c.sum, &c.mn, &c.mx, &c.timer};
+  for (int i = 0; i < 8; i++) dfree(*cols[i]);
+}
+}  // namespace
+
+int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64_t cap, int64_t* n) {
+  if (!op || !n) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  int rc;
+  if ((rc = kg_check(op, kg)) || (rc = settle(op))) return rc;
+  const DevCfg& c = op->dc;
+  const int32_t np = 1 << c.log_s, p0 = (kg - c.kg0) << c.log_s;
+  // occupied slots of the key group's regions bound its live entries
+  std::vector<int32_t> live(np);
+  HIP_OR_RETURN(op, hipMemcpyAsync(live.data(), op->tb.live + p0, np * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                   op->stream));
+  HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
+  int64_t bound = 0;
+  for (int32_t v : live) bound += v;
+  StateCols d{};
+  if ((rc = alloc_state_cols(op, d, bound))) {
+    free_state_cols(d);
+    return rc;
+  }
+  HIP_OR_RETURN(op, hipMemsetAsync(op->d_stats3, 0, sizeof(unsigned long long), op->stream));
+  fwdev::launch_snapshot(c, op->tb, p0, np, d, op->d_stats3, op->stream);
+  unsigned long long got = 0;
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(&got, op->d_stats3, sizeof got, hipMemcpyDeviceToHost, op->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(op->stream);
+  if (e == hipSuccess && dst && cap >= (int64_t)got && got > 0) {
+    int64_t* hs[8] = {dst->key, dst->start, dst->end, dst->count, dst->sum, dst->min, dst->max, dst->timer};
+    int64_t* ds[8] = {d.key, d.start, d.end, d.cnt, d.sum, d.mn, d.mx, d.timer};
+    for (int i = 0; i < 8 && e == hipSuccess; i++)
+      if (hs[i]) e = hipMemcpyAsync(hs[i], ds[i], got * sizeof(int64_t), hipMemcpyDeviceToHost, op->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(op->stream);
+  }
+  free_state_cols(d);
+  if (e != hipSuccess) return set_err(op, FW_ERR_HIP, "snapshot: %s", hipGetErrorString(e));
+  *n = (int64_t)got;
+  return FW_OK;
+}
+
+int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_t n) {
+  if (!op || (n > 0 && !src) || n < 0) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  int rc;
+  if ((rc = kg_check(op, kg)) || (rc = settle(op))) return rc;
+  if (n == 0) return FW_OK;
+  const int64_t* hs[8] = {src->key, src->start, src->end, src->count, src->sum, src->min, src->max, src->timer};
+  for (const int64_t* h : hs)
+    if (!h) return set_err(op, FW_ERR_ARG, "null state column");
+  StateCols d{};
+  int32_t* demand = nullptr;
+  auto fail = [&](int code) {
+    free_state_cols(d);
+    dfree(demand);
+    return code;
+  };
+  if ((rc = alloc_state_cols(op, d, n))) return fail(rc);
+  int64_t* ds[8] = {d.key, d.start, d.end, d.cnt, d.sum, d.mn, d.mx, d.timer};
+  for (int i = 0; i < 8; i++)
+    if (hipMemcpyAsync(ds[i], hs[i], n * sizeof(int64_t), hipMemcpyHostToDevice, op->stream) != hipSuccess)
+      return fail(set_err(op, FW_ERR_HIP, "restore: copy failed"));
+  // the rows' demand per partition: grow the table first if a region would pass its load limit
+  const int32_t P = op->dc.P;
+  if (dmalloc(&demand, (size_t)P) != hipSuccess || hipMemsetAsync(demand, 0, P * sizeof(int32_t), op->stream) != hipSuccess)
+    return fail(set_err(op, FW_ERR_HIP, "restore: allocation failed"));
+  fwdev::launch_restore(op->dc, kg, d, n, demand, op->tb, op->d_status, op->stream);
+  std::vector<int32_t> dem(P), live(P);
+  if (hipMemcpyAsync(dem.data(), demand, P * sizeof(int32_t), hipMemcpyDeviceToHost, op->stream) != hipSuccess ||
+      hipMemcpyAsync(live.data(), op->tb.live, P * sizeof(int32_t), hipMemcpyDeviceToHost, op->stream) != hipSuccess ||
+      (rc = sync_status(op)))
+    return fail(rc ? rc : set_err(op, FW_ERR_HIP, "restore: copy failed"));
+  if (op->h_status->kg_errors) {
+    const int bad = op->h_status->kg_errors;
+    op->h_status->kg_errors = 0;
+    put_status_field(op, &Status::kg_errors);
+    return fail(set_err(op, FW_ERR_KEY_GROUP, "%d restored row(s) do not belong to key group %d", bad, kg));
+  }
+  int64_t need = 0;
+  for (int32_t p = 0; p < P; p++) need = std::max<int64_t>(need, (int64_t)live[p] + dem[p]);
+  if (need > region_limit(op->dc.log_r) && (rc = grow_table(op, log_r_for(op, need)))) return fail(rc);
+  fwdev::launch_restore(op->dc, kg, d, n, nullptr, op->tb, op->d_status, op->stream);
+  if (hipGetLastError() != hipSuccess || (rc = sync_status(op)))
+    return fail(rc ? rc : set_err(op, FW_ERR_HIP, "restore kernel failed"));
+  fail(FW_OK);
+  if (op->h_status->flags & FW_STATUS_STATE_LOST) return set_err(op, FW_ERR_CAPACITY, "restore: region full");
+  const int64_t rows = (int64_t)op->h_status->out_rows;
+  return ensure_out_capacity(op, rows + op->table_slots, rows);  // a watermark may fire every restored window
+}
+
 int fw_key_groups_device(const int64_t* key, const int32_t* key_hash, int32_t key_kind, int64_t n,
                          int32_t max_parallelism, int32_t* kg_out, void* stream) {
   if (n < 0 || max_parallelism < 1 || (key_kind == FW_KEY_HASHED && !key_hash)) return FW_ERR_ARG;

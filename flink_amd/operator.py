@@ -21,6 +21,8 @@ from .windowing import CountSumMinMax, EventTimeTrigger, Trigger, WindowAssigner
 
 ROW_FIELDS = ("key", "start", "end", "count", "sum", "min", "max")
 ROW_DTYPE = np.dtype([(f, "<i8") for f in ROW_FIELDS] + [("epoch", "<i8")])
+STATE_FIELDS = ("key", "start", "end", "count", "sum", "min", "max", "timer")
+STATE_DTYPE = np.dtype([(f, "<i8") for f in STATE_FIELDS])
 SIDE_DTYPE = np.dtype([("key", "<i8"), ("ts", "<i8"), ("val", "<i8"), ("epoch", "<i8")])
 
 _KEY_KINDS = {"long": N.FW_KEY_LONG, "int": N.FW_KEY_INT, "hashed": N.FW_KEY_HASHED}
@@ -220,6 +222,44 @@ class GpuWindowOperator:
 
     def side_rows(self):
         return np.concatenate(self._side) if self._side else np.zeros(0, dtype=SIDE_DTYPE)
+
+    # ------------------------------------------------------------------ snapshot / restore
+    # AbstractStreamOperator.snapshotState writes keyed state per key group
+    # (HeapKeyedStateBackend.java:289-399, per-key-group offsets :370-381; timers via
+    # InternalTimeServiceManager.snapshotStateForKeyGroup :114); a restore may hand the key groups
+    # to operators with a different KeyGroupRange (rescaling).
+    def snapshot_key_group(self, kg):
+        """Live (key, window) accumulators of key group kg as a STATE_DTYPE array (no order)."""
+        L = N.lib()
+        n = ctypes.c_int64()
+        N.check(L.fw_snapshot_key_group(self._h, int(kg), None, 0, ctypes.byref(n)), self._h)
+        cols = {f: np.zeros(n.value, dtype=np.int64) for f in STATE_FIELDS}
+        dst = N.FwStateRows(**{f: cols[f].ctypes.data for f in STATE_FIELDS})
+        got = ctypes.c_int64()
+        N.check(L.fw_snapshot_key_group(self._h, int(kg), ctypes.byref(dst), n.value, ctypes.byref(got)), self._h)
+        out = np.zeros(got.value, dtype=STATE_DTYPE)
+        for f in STATE_FIELDS:
+            out[f] = cols[f][:got.value]
+        return out
+
+    def snapshot_state(self):
+        """{key group: STATE_DTYPE rows} for every key group of this operator's KeyGroupRange."""
+        return {kg: self.snapshot_key_group(kg) for kg in self.key_group_range}
+
+    def restore_key_group(self, kg, rows):
+        rows = np.ascontiguousarray(rows, dtype=STATE_DTYPE)
+        cols = {f: np.ascontiguousarray(rows[f]) for f in STATE_FIELDS}
+        src = N.FwStateRows(**{f: cols[f].ctypes.data for f in STATE_FIELDS})
+        N.check(N.lib().fw_restore_key_group(self._h, int(kg), ctypes.byref(src), len(rows)), self._h)
+
+    def initialize_state(self, snapshot):
+        """Restores the key groups of `snapshot` ({kg: rows}) that this operator owns; others are skipped,
+        as a subtask reads only the key groups of its own KeyGroupRange."""
+        for kg, rows in snapshot.items():
+            if kg in self.key_group_range and len(rows):
+                self.restore_key_group(kg, rows)
+
+    snapshotState, initializeState = snapshot_state, initialize_state
 
     # ------------------------------------------------------------------ metrics
     def stats(self):

@@ -170,6 +170,32 @@ const char* fw_kernel_name(int kind);
 int fw_synchronize(fw_op* op);
 void* fw_stream(fw_op* op); /* the hipStream_t the handle enqueues on */
 
+/* Keyed-state snapshot and restore, one key group at a time: the heap backend writes its state per
+ * key group (flink-runtime/.../state/heap/HeapKeyedStateBackend.java:289-399, offsets per key group
+ * :370-381) and the timers likewise (api/operators/InternalTimeServiceManager.java:114), which is
+ * what lets a restore re-shard the key groups over a different parallelism.  One row per live
+ * (key, window) accumulator of "window-contents"; `timer` = 1 when the window's event-time trigger
+ * timer (maxTimestamp) is registered, 0 when only its cleanup timer is pending (the cleanup timer is
+ * implied by the window: cleanupTime, WindowOperator.java:637-644).  sum/min/max are in the form of
+ * the fired rows (fw_rows).  Rows come out in no particular order.
+ *   fw_snapshot_key_group: copies the key group's rows into caller-owned host arrays of capacity cap;
+ *     with cap too small (or dst NULL) it only returns the row count in *n.
+ *   fw_restore_key_group: inserts rows into the handle (which must own the key group); a row whose
+ *     (key, window) is already present is merged into it (AggregateFunction.merge).  Long/Integer
+ *     keys outside the key group are refused with FW_ERR_KEY_GROUP. */
+typedef struct fw_state_rows {
+  int64_t* key;
+  int64_t* start;
+  int64_t* end;
+  int64_t* count;
+  int64_t* sum;
+  int64_t* min;
+  int64_t* max;
+  int64_t* timer;
+} fw_state_rows;
+int fw_snapshot_key_group(fw_op* op, int32_t key_group, const fw_state_rows* host_dst, int64_t cap, int64_t* n);
+int fw_restore_key_group(fw_op* op, int32_t key_group, const fw_state_rows* host_src, int64_t n);
+
 /* Key routing (both sides of keyBy).
  *   fw_key_groups_device: kg[i] = KeyGroupRangeAssignment.assignToKeyGroup(key_i, maxParallelism)
  *     (flink-runtime/.../state/KeyGroupRangeAssignment.java:58-71, MathUtils.java:134-154).

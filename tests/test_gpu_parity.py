@@ -295,3 +295,73 @@ def test_gpu_key_groups_and_route():
             assert np.array_equal(rk[off:off + counts[d]], keys[sel])
             off += counts[d]
     del ctypes
+
+
+# ---- keyed-state snapshot / restore per key group, with rescaling.
+# Reference: AbstractStreamOperator.snapshotState writes keyed state per key group
+# (flink-runtime/.../state/heap/HeapKeyedStateBackend.java:289-399, :370-381) and a restore hands the key
+# groups to the subtasks of the new parallelism (KeyGroupRangeAssignment.computeKeyGroupRangeForOperatorIndex,
+# KeyGroupRangeAssignment.java:85-99).  The run split by a snapshot must emit exactly the rows of an
+# uninterrupted run (here: the oracle's).
+@pytest.mark.parametrize("cfg,new_par", [
+    (dict(assigner="tumbling", size=100), 3),
+    (dict(assigner="sliding", size=300, slide=100), 2),
+    (dict(assigner="session", gap=40), 2),
+    (dict(assigner="tumbling", size=100, lateness=150), 1),
+])
+def test_gpu_snapshot_restore_rescale(cfg, new_par):
+    from flink_amd.keygroups import (assign_to_key_group, compute_key_group_range_for_operator_index,
+                                     long_hash_code)
+    batches, wms = _stream(120_000, 15_000, 3_000, bound=50, jitter=80, rate=200_000)
+    ref = orc.WindowOperatorOracle(**cfg)
+    for (k, t, v), wm in zip(batches, wms):
+        ref.process(k, t, v)
+        ref.watermark(wm)
+    exp = ref.rows()
+    cut = len(batches) // 2
+    a = _gpu_op(**cfg, max_parallelism=128)
+    for (k, t, v), wm in zip(batches[:cut], wms[:cut]):
+        a.process(k, t, v)
+        a.watermark(wm)
+    first = a.rows()
+    entries = a.num_keyed_state_entries
+    snap = a.snapshot_state()
+    assert sum(len(r) for r in snap.values()) == entries
+    a.close()
+    parts = []
+    for idx in range(new_par):
+        kgr = compute_key_group_range_for_operator_index(128, new_par, idx)
+        op = _gpu_op(**cfg, max_parallelism=128, key_group_range=kgr)
+        op.initialize_state(snap)
+        parts.append((kgr, op))
+    assert sum(op.num_keyed_state_entries for _, op in parts) == entries
+    got = [first]
+    for (k, t, v), wm in zip(batches[cut:], wms[cut:]):
+        kg = np.array([assign_to_key_group(long_hash_code(int(x)), 128) for x in k], dtype=np.int64)
+        for kgr, op in parts:
+            m = (kg >= kgr.start_key_group) & (kg <= kgr.end_key_group)
+            op.process(k[m], t[m], v[m])
+            op.watermark(wm)
+    for _, op in parts:
+        r = op.rows()
+        r["epoch"] += cut
+        got.append(r)
+        op.close()
+    assert_rows_equal(np.concatenate(got), exp)
+
+
+def test_gpu_restore_refuses_foreign_key_group():
+    from flink_amd import _native as N
+    from flink_amd.keygroups import assign_to_key_group
+    from flink_amd.operator import STATE_DTYPE
+    op = _gpu_op("tumbling", 100, max_parallelism=128, key_group_range=KeyGroupRange(0, 63))
+    key = next(x for x in range(1000) if assign_to_key_group(x, 128) == 5)
+    rows = np.zeros(1, dtype=STATE_DTYPE)
+    rows["key"], rows["start"], rows["end"], rows["count"] = key, 0, 100, 1
+    with pytest.raises(N.NativeError):
+        op.restore_key_group(7, rows)   # the row's key belongs to key group 5
+    with pytest.raises(N.NativeError):
+        op.restore_key_group(100, rows)  # key group outside the operator's range
+    op.restore_key_group(5, rows)
+    assert op.num_keyed_state_entries == 1
+    op.close()
