@@ -12,6 +12,9 @@ KeyGroupRange computeKeyGroupRangeForOperatorIndex(128, N, rank), generates `--b
 global stream per step and the keyBy exchange (route + RCCL all_to_all) and the watermark min
 (all_reduce) run inside the timed region: weak scaling.
 
+--workload c4 runs SURVEY §8d C4 instead (EventTimeSessionWindows gap 30 s, 1M Zipf(1.1) keys, 1e5
+records per event-second, bound 1 s); the default line is C2.
+
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -24,6 +27,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md §Chip-level parameters
+
+# SURVEY.md §8d workloads.  c2 is BASELINE.json configs[1] (the default, the headline line); c4 is the
+# session-window config, benchmarked on request (--workload c4).
+PRESETS = {
+    "c2": dict(rate=100_000_000, bound=200, jitter=200, zipf=None, keys=1_000_000, cpu_sample=1 << 24,
+               workload="C2 tumbling 1s event-time window, count/sum/min/max, 1M uniform Long keys, "
+                        "bounded out-of-orderness 200 ms"),
+    "c4": dict(rate=100_000, bound=1000, jitter=1000, zipf=1.1, keys=1_000_000, cpu_sample=1 << 22,
+               workload="C4 EventTimeSessionWindows gap 30 s, count/sum/min/max, 1M Zipf(1.1) Long keys, "
+                        "bounded out-of-orderness 1 s"),
+}
 
 
 def kernel_bytes(name, n, merged, live_slots_scanned=0):
@@ -42,19 +56,27 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--workload", choices=sorted(PRESETS), default="c2")
     ap.add_argument("--batch", type=int, default=1 << 24)
-    ap.add_argument("--keys", type=int, default=1_000_000)
-    ap.add_argument("--rate", type=int, default=100_000_000, help="records per event-second (whole job)")
-    ap.add_argument("--bound", type=int, default=200, help="out-of-orderness bound (ms)")
-    ap.add_argument("--jitter", type=int, default=200)
-    ap.add_argument("--window", type=int, default=1000)
-    ap.add_argument("--cpu-sample", type=int, default=1 << 24)
+    ap.add_argument("--keys", type=int, default=None)
+    ap.add_argument("--rate", type=int, default=None, help="records per event-second (whole job)")
+    ap.add_argument("--bound", type=int, default=None, help="out-of-orderness bound (ms)")
+    ap.add_argument("--jitter", type=int, default=None)
+    ap.add_argument("--window", type=int, default=1000, help="tumbling window (ms, c2)")
+    ap.add_argument("--gap", type=int, default=30_000, help="session gap (ms, c4)")
+    ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     ap.add_argument("--sub-partitions", type=int, default=0, help="state partitions per key group (0 = auto)")
     args = ap.parse_args()
+    preset = PRESETS[args.workload]
+    for name in ("keys", "rate", "bound", "jitter", "cpu_sample"):
+        if getattr(args, name) is None:
+            setattr(args, name, preset[name])
+    args.zipf = preset["zipf"]
+    sessions = args.workload == "c4"
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -66,15 +88,17 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    from flink_amd import TumblingEventTimeWindows
+    from flink_amd import EventTimeSessionWindows, TumblingEventTimeWindows
     from flink_amd import _native as N
-    from flink_amd.datagen import generate_device
+    from flink_amd.datagen import generate_device, zipf_cdf
     from flink_amd.exchange import KeyGroupExchange
     from flink_amd.operator import GpuWindowOperator
 
     max_par = 128
     exch = KeyGroupExchange(max_par, world, rank)
-    op = GpuWindowOperator(TumblingEventTimeWindows.of(args.window), key_group_range=exch.key_group_range,
+    assigner = EventTimeSessionWindows.with_gap(args.gap) if sessions else TumblingEventTimeWindows.of(args.window)
+    cdf = torch.from_numpy(zipf_cdf(args.keys, args.zipf)).to(dev) if args.zipf else None
+    op = GpuWindowOperator(assigner, key_group_range=exch.key_group_range,
                            device=local_rank, max_parallelism=max_par,
                            expected_entries=2 * args.keys // world,
                            max_batch=args.batch if world == 1 else 2 * args.batch,
@@ -85,7 +109,7 @@ def main():
     for s in range(steps_total):
         first = (s * world + rank) * args.batch  # global record index of this rank's slice of step s
         k, t, v, mx = generate_device(seed, first, args.batch, args.keys, ts_base=0, rate=args.rate,
-                                      jitter=args.jitter, device=local_rank)
+                                      jitter=args.jitter, cdf_dev=cdf, device=local_rank)
         batches.append((k, t, v))
         local_max.append(mx)
     torch.cuda.synchronize()
@@ -163,8 +187,8 @@ def main():
             roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                         "traffic": traffic, "alg_bytes_per_launch": int(b)}
-    # whole-path roofline with SURVEY §8d's B_alg for C2: 24 + 104 F/N bytes per record
-    b_alg = 24 + 104 * fired / max(1, records / world)
+    # whole-path roofline with SURVEY §8d's B_alg: C2 24 + 104 F/N, C4 24 + 112 F/N bytes per record
+    b_alg = 24 + (112 if sessions else 104) * fired / max(1, records / world)
     path_frac = value * b_alg / (world * HBM_PEAK_GBS * 1e9)
 
     cpu = None
@@ -177,9 +201,9 @@ def main():
             "value": round(value, 1), "unit": "records/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic (splitmix64 counter stream)",
-            "config": {"workload": "C2 tumbling 1s event-time window, count/sum/min/max, 1M uniform Long keys, "
-                                   "bounded out-of-orderness 200 ms",
-                       "records_per_step_per_gpu": args.batch, "keys": args.keys, "window_ms": args.window,
+            "config": {"workload": preset["workload"],
+                       "records_per_step_per_gpu": args.batch, "keys": args.keys,
+                       **({"gap_ms": args.gap, "zipf_s": args.zipf} if sessions else {"window_ms": args.window}),
                        "records_per_event_second": args.rate, "watermark_bound_ms": args.bound,
                        "max_parallelism": 128, "parallelism": f"keygroup{world}"},
             "roofline": roofline,
@@ -203,17 +227,18 @@ def cpu_baseline(args):
     from oracle import oracle as orc
     n = args.cpu_sample
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    k, t, v = generate_host(0x5EED, 0, n, args.keys, ts_base=0, rate=args.rate, jitter=args.jitter)
+    k, t, v = generate_host(0x5EED, 0, n, args.keys, ts_base=0, rate=args.rate, jitter=args.jitter, zipf_s=args.zipf)
     batch = min(args.batch, n)
     wms, m = [], -(1 << 63)
     for b in range(0, n, batch):
         m = max(m, int(t[b:b + batch].max()))
         wms.append(m - args.bound)
     t0 = time.perf_counter()
-    orc.run_parallel(dict(assigner="tumbling", size=args.window), k, t, v, batch, np.array(wms), 128, threads)
+    cfg = dict(assigner="session", gap=args.gap) if args.workload == "c4" else dict(assigner="tumbling", size=args.window)
+    orc.run_parallel(cfg, k, t, v, batch, np.array(wms), 128, threads)
     dt = time.perf_counter() - t0
     return {"value": round(n / dt, 1), "unit": "records/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} records of the same C2 stream, {threads} subtasks (threads), watermark every "
+            "sample": f"first {n} records of the same {args.workload.upper()} stream, {threads} subtasks (threads), watermark every "
                       f"{batch} records; CPU restatement of WindowOperator semantics (oracle/), not the Java "
                       f"reference (no JDK on the box)"}
 

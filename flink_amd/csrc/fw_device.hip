@@ -120,6 +120,7 @@ __device__ __forceinline__ int64_t f64_unsortable(int64_t s) { return s >= 0 ? s
 
 // ------------------------------------------------------------------ record classes
 enum { CLS_NORMAL = 0, CLS_SLOW = 1, CLS_LATE = 2, CLS_SKIP = 3, CLS_BADTS = 4 };
+constexpr int MAX_SESSIONS = 64;  // in-flight sessions of one key visible to one merge step
 
 // Windows of a record, newest first (SlidingEventTimeWindows.java:71-75 loop order).
 __device__ __forceinline__ int num_windows(const DevCfg& c, int64_t ts, int64_t* last_start) {
@@ -135,10 +136,39 @@ __device__ __forceinline__ int num_windows(const DevCfg& c, int64_t ts, int64_t*
   return k;
 }
 
-// class of a record against watermark wm; for CLS_NORMAL also its windows (newest start, count)
+// sessions: is `key` in the batch's taint set (keys with an ordered-path record in the batch)?
+__device__ __forceinline__ uint32_t taint_slot0(const DevCfg& c, int64_t key) {
+  return (uint32_t)(fmix64((uint64_t)key ^ 0x2545F4914F6CDD1Dull)) & c.taint_mask;
+}
+__device__ __forceinline__ bool taint_has(const DevCfg& c, int64_t key) {
+  for (uint32_t i = 0, s = taint_slot0(c, key); i <= c.taint_mask; i++, s = (s + 1) & c.taint_mask) {
+    if (c.taint_state[s] != c.taint_epoch) return false;
+    if (c.taint_key[s] == (uint64_t)key) return true;
+  }
+  return false;
+}
+// a session element that may fire, merge into a fired window or be dropped: it needs arrival order
+__device__ __forceinline__ bool session_ordered(const DevCfg& c, int64_t wm, int64_t ts) {
+  return ts == LMIN || jsub(jadd(ts, c.gap), 1) <= wm;
+}
+
+// class of a record against watermark wm; for CLS_NORMAL also its windows (newest start, count).
+// taint: the batch's Status.taint_any (sessions only).
 __device__ __forceinline__ int classify(const DevCfg& c, int64_t wm, int64_t ts, int64_t* last_out = nullptr,
-                                        int* k_out = nullptr) {
-  if (c.assigner == FW_SESSION) return CLS_SLOW;
+                                        int* k_out = nullptr, int64_t key = 0, int taint = 0) {
+  if (c.assigner == FW_SESSION) {
+    // A session element whose window [ts, ts + gap) ends after wm is added without firing, and every
+    // merge it takes part in ends after wm too, so such elements commute (MergingWindowSet.addWindow
+    // builds the connected components of the in-flight windows in any order): they take the parallel
+    // path unless their key also has an element that needs arrival order in this batch.
+    if (session_ordered(c, wm, ts)) return CLS_SLOW;
+    if (taint == 2 || (taint == 1 && taint_has(c, key))) return CLS_SLOW;
+    if (last_out) {
+      *last_out = ts;
+      *k_out = 1;
+    }
+    return CLS_NORMAL;
+  }
   if (ts == LMIN) return CLS_BADTS;  // TumblingEventTimeWindows.java:69-71
   int64_t last;
   int k = num_windows(c, ts, &last);
@@ -292,6 +322,41 @@ __device__ __forceinline__ int32_t region_claim(const Region& r, uint64_t h, uin
 
 // ============================================================================== kernels
 
+// ---- K0 (sessions): the batch's taint set.  Keys with an element that needs arrival order
+// (session_ordered) go into an open-addressing set whose slots are stamped with the batch's epoch, so
+// the set is never cleared between batches.  Status.taint_any = 1 when some key was inserted, 2 when
+// the set overflowed (then every record of the batch takes the ordered path).
+constexpr uint32_t TAINT_BUSY = 0x80000000u;
+constexpr int TAINT_MAX_PROBES = 64;
+__device__ __forceinline__ bool taint_insert(const DevCfg& c, int64_t key) {
+  uint32_t s = taint_slot0(c, key);
+  for (int probes = 0; probes < TAINT_MAX_PROBES;) {
+    const uint32_t cur = __hip_atomic_load(&c.taint_state[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == c.taint_epoch) {
+      if (c.taint_key[s] == (uint64_t)key) return true;
+      s = (s + 1) & c.taint_mask;
+      probes++;
+      continue;
+    }
+    if (cur == (c.taint_epoch | TAINT_BUSY)) continue;  // being published by another lane: re-read
+    if (atomicCAS(&c.taint_state[s], cur, c.taint_epoch | TAINT_BUSY) == cur) {
+      c.taint_key[s] = (uint64_t)key;
+      __hip_atomic_store(&c.taint_state[s], c.taint_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      return true;
+    }
+  }
+  return false;
+}
+__global__ __launch_bounds__(256) void k_taint(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
+                                               const int64_t* __restrict__ ts, int64_t n, Status* st) {
+  int any = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!session_ordered(c, wm, ts[i])) continue;
+    any = max(any, taint_insert(c, key[i]) ? 1 : 2);
+  }
+  if (any) atomicMax(&st->taint_any, any);
+}
+
 // ---- K1: classify + partition histogram.  hist is (P+1) x T, partition-major; row P counts
 // the records of each tile that go to the ordered path (scanned with the partitions), row P+1
 // keeps that count unscanned for k_scatter_ordered.
@@ -306,6 +371,7 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_classify_hist(DevCfg c, int
   const int64_t end = min(n, base + (int64_t)FW_TILE);
   int bad_kg = 0, bad_ts = 0;
   unsigned slow = 0;
+  const int taint = c.assigner == FW_SESSION ? st->taint_any : 0;
   for (int64_t b = base; b < end; b += (int64_t)blockDim.x * FW_RPT) {
     int64_t k[FW_RPT], t[FW_RPT];
     int32_t h[FW_RPT];
@@ -325,7 +391,7 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_classify_hist(DevCfg c, int
         bad_kg++;
         continue;
       }
-      const int cls = classify(c, wm, t[j]);
+      const int cls = classify(c, wm, t[j], nullptr, nullptr, k[j], taint);
       if (cls == CLS_NORMAL)
         atomicAdd(&lh[p], 1u);
       else if (cls == CLS_SLOW)
@@ -446,6 +512,7 @@ __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(D
   const int64_t tbase = (int64_t)blockIdx.x * FW_TILE;
   const int64_t tend = min(n, tbase + (int64_t)FW_TILE);
   unsigned long long late = 0;
+  const int taint = c.assigner == FW_SESSION ? st->taint_any : 0;
   for (int64_t b = tbase; b < tend; b += (int64_t)blockDim.x * FW_RPT) {
     int64_t k[FW_RPT], t[FW_RPT], v[FW_RPT];
     int32_t hh[FW_RPT];
@@ -469,7 +536,7 @@ __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(D
         const int32_t h = c.key_kind == FW_KEY_HASHED ? hh[j] : key_hash_of(c.key_kind, k[j], kh, i);
         const int32_t p = partition_of(c, k[j], h);
         if (p >= 0) {
-          const int cls = classify(c, wm, t[j], &last, &nwin);
+          const int cls = classify(c, wm, t[j], &last, &nwin, k[j], taint);
           if (cls == CLS_NORMAL) {
             pos = atomicAdd(&base[p], 1u);
             norm = true;
@@ -508,8 +575,9 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_ordered(DevCfg c, i
                                                                      int32_t T, const uint32_t* __restrict__ offs,
                                                                      const uint32_t* __restrict__ tile_slow,
                                                                      int64_t* __restrict__ sk, int64_t* __restrict__ stt,
-                                                                     int64_t* __restrict__ sv, int32_t* __restrict__ skh) {
+                                                                     int64_t* __restrict__ sv, int32_t* __restrict__ skh, const Status* st) {
   if (tile_slow[blockIdx.x] == 0) return;
+  const int taint = c.assigner == FW_SESSION ? st->taint_any : 0;
   __shared__ uint32_t wtot[FW_TILE_THREADS / 64];
   const uint32_t slow_base = offs[(int64_t)c.P * T + blockIdx.x] - offs[(int64_t)c.P * T];
   const int64_t tbase = (int64_t)blockIdx.x * FW_TILE;
@@ -527,7 +595,7 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_ordered(DevCfg c, i
       v = val[i];
       h = key_hash_of(c.key_kind, k, kh, i);
       p = partition_of(c, k, h);
-      if (p >= 0) cls = classify(c, wm, t);
+      if (p >= 0) cls = classify(c, wm, t, nullptr, nullptr, k, taint);
     }
     const bool is_slow = cls == CLS_SLOW;
     const uint64_t ball = __ballot(is_slow);
@@ -587,6 +655,21 @@ __device__ __forceinline__ uint32_t lds_hash(int64_t key, int64_t start) {
   return h;
 }
 __device__ __forceinline__ uint32_t lds_fp(uint32_t h) { return (h >> 8) | 2u; }  // >= 2, never EMPTY/BUSY
+
+// accumulate one value into LDS slot `target` with no-return LDS atomics (nothing waits on the LDS)
+__device__ __forceinline__ void lds_acc(AggLds& L, int target, int vtype, int64_t v) {
+  atomicAdd(&L.cnt[target], 1u);
+  if (vtype == FW_VAL_F64) {
+    atomicAdd((double*)&L.sum[target], __longlong_as_double(v));
+    const int64_t sv = f64_sortable(v);
+    atomicMin((long long*)&L.mn[target], (long long)sv);
+    atomicMax((long long*)&L.mx[target], (long long)sv);
+  } else {
+    atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)v);
+    atomicMin((long long*)&L.mn[target], (long long)v);
+    atomicMax((long long*)&L.mx[target], (long long)v);
+  }
+}
 
 // insert-or-accumulate one value into the LDS table; false when the table is at its fill limit
 // (the caller flushes and retries).  A lane that claims a slot publishes it inside the same loop
@@ -654,18 +737,7 @@ __device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, in
   }
   if (target < 0) return false;
   if (diag & DIAG_AGG_NO_ACCUM) return true;
-  // no-return LDS atomics: nothing below waits on the LDS
-  atomicAdd(&L.cnt[target], 1u);
-  if (vtype == FW_VAL_F64) {
-    atomicAdd((double*)&L.sum[target], __longlong_as_double(v));
-    const int64_t sv = f64_sortable(v);
-    atomicMin((long long*)&L.mn[target], (long long)sv);
-    atomicMax((long long*)&L.mx[target], (long long)sv);
-  } else {
-    atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)v);
-    atomicMin((long long*)&L.mn[target], (long long)v);
-    atomicMax((long long*)&L.mx[target], (long long)v);
-  }
+  lds_acc(L, target, vtype, v);
   return true;
 }
 
@@ -752,6 +824,225 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
   return true;
 }
 
+// ---- sessions on the parallel path (EventTimeSessionWindows + MergingWindowSet.addWindow).
+// Only in-time elements of untainted keys get here (classify), so nothing fires and no merge result
+// is late: a key's in-flight sessions after the batch are the connected components
+// (TimeWindow.intersects) of its sessions before the batch and the batch's element windows
+// [ts, ts + gap), whatever the order of the elements, each with the merged accumulator of its parts.
+// LDS: a slot holds one interval [start, end) of a key (the hull of the element windows that joined
+// it, which is always connected) and its accumulator; `end` lives in the separate array E.  An element
+// joins a slot of its key whose interval intersects its window and widens it with LDS min/max, or
+// claims a new slot.  Slots of one key that come to overlap are joined by the flush.
+__device__ __forceinline__ bool lds_session_upsert(AggLds& L, int64_t* E, int vtype, int64_t key, int64_t ws,
+                                                   int64_t we, int64_t v) {
+  const uint32_t h = lds_hash(key, 0), fp = lds_fp(h);
+  uint32_t b = h & (LDS_BUCKETS - 1);
+  int target = -1;
+  for (int guard = 0; guard < 4 * LDS_BUCKETS;) {
+    asm volatile("" ::: "memory");  // re-read the bucket every iteration (it may be claimed meanwhile)
+    const u32x4 t4 = *reinterpret_cast<const u32x4*>(&L.tag[b * 4]);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t tq = q == 0 ? t4.x : q == 1 ? t4.y : q == 2 ? t4.z : t4.w;
+      if (target < 0 && tq == fp) {
+        const int s = (int)b * 4 + q;
+        const i64x2 kv = L.kv[s];
+        if (kv.x == key && kv.y <= we && E[s] >= ws) target = s;  // TimeWindow.intersects
+      }
+    }
+    if (target >= 0) break;
+    const int empty = t4.x == LT_EMPTY ? 0 : t4.y == LT_EMPTY ? 1 : t4.z == LT_EMPTY ? 2 : t4.w == LT_EMPTY ? 3 : -1;
+    const bool busy = t4.x == LT_BUSY || t4.y == LT_BUSY || t4.z == LT_BUSY || t4.w == LT_BUSY;
+    if (busy) {
+      guard++;
+      continue;
+    }
+    if (empty >= 0) {
+      if (__hip_atomic_load(&L.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= FW_LDS_FILL_LIMIT)
+        return false;
+      const int s = (int)b * 4 + empty;
+      if (atomicCAS(&L.tag[s], LT_EMPTY, LT_BUSY) == LT_EMPTY) {
+        atomicAdd(&L.fill, 1);
+        L.kv[s] = i64x2{key, ws};
+        E[s] = we;
+        L.cnt[s] = 0;
+        L.sum[s] = 0;
+        L.mn[s] = LMAX;
+        L.mx[s] = LMIN;
+        __hip_atomic_store(&L.tag[s], fp, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        target = s;
+        break;
+      }
+      continue;
+    }
+    b = (b + 1) & (LDS_BUCKETS - 1);
+    guard++;
+  }
+  if (target < 0) return false;
+  atomicMin(reinterpret_cast<long long*>(&L.kv[target]) + 1, (long long)ws);  // TimeWindow.cover
+  atomicMax((long long*)&E[target], (long long)we);
+  lds_acc(L, target, vtype, v);
+  return true;
+}
+
+// MergingWindowSet.addWindow (MergingWindowSet.java:156-225) of a session delta d (an interval with
+// its accumulator) into the key's in-flight sessions of region r: d's connected component becomes one
+// session (merge function + mergeNamespaces, WindowOperator.java:308-339,
+// AbstractHeapMergingState.java:67-93; EventTimeTrigger.onMerge/onElement register maxTimestamp,
+// which is after the watermark).  Only the thread that owns d.key touches the key's entries; new
+// slots are published BUSY -> LIVE because other threads walk the same probe chains.
+// Returns the region slots newly taken; *timer = maxTimestamp of the resulting session.
+__device__ int session_add(const DevCfg& c, const Region& r, const Entry& d, int64_t* timer, Status* st) {
+  const uint64_t h = slot_hash(c, d.key, 0);
+  const uint32_t want = live_word(h);
+  int32_t sl[MAX_SESSIONS];
+  int ns = 0;
+  *timer = LMAX;
+  for (uint32_t i = 0; i <= r.mask; i++) {
+    const uint32_t s = ((uint32_t)h + i) & r.mask;
+    const uint32_t stt = ld_state(r.state + s);
+    if (stt == SLOT_EMPTY) break;
+    if (stt == want) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (r.ent[s].key == d.key) {
+        if (ns == MAX_SESSIONS) {
+          atomicOr(&st->flags, FW_STATUS_STATE_LOST);
+          return 0;
+        }
+        sl[ns++] = (int32_t)s;
+      }
+    }
+  }
+  int64_t cs = d.start, ce = d.end;
+  uint64_t in_group = 0;
+  for (bool grew = true; grew;) {
+    grew = false;
+    for (int j = 0; j < ns; j++) {
+      if (in_group >> j & 1) continue;
+      const Entry& e = r.ent[sl[j]];
+      if (cs <= e.end && ce >= e.start) {  // TimeWindow.intersects
+        in_group |= 1ull << j;
+        cs = min(cs, e.start);
+        ce = max(ce, e.end);
+        grew = true;
+      }
+    }
+  }
+  *timer = jsub(ce, 1);
+  if (in_group == 0) {  // a new session
+    const int32_t s = region_claim(r, h, SLOT_BUSY);
+    if (s < 0) {  // cannot happen below the load limit (checked by the flush)
+      atomicOr(&st->flags, FW_STATUS_STATE_LOST);
+      return 0;
+    }
+    r.ent[s] = d;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __hip_atomic_store(r.state + s, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 1;
+  }
+  const int first = __ffsll((unsigned long long)in_group) - 1;
+  Entry m = r.ent[sl[first]];
+  for (int j = first + 1; j < ns; j++) {
+    if (!(in_group >> j & 1)) continue;
+    acc_merge(c, m, r.ent[sl[j]]);
+    // the slot stays occupied (live counts occupied slots) until k_fire rebuilds the region
+    __hip_atomic_store(r.state + sl[j], SLOT_DEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  acc_merge(c, m, d);
+  m.start = cs;
+  m.end = ce;
+  m.meta = FW_TIMER;
+  r.ent[sl[first]] = m;
+  return 0;
+}
+
+// flush of the session LDS table.  Every LDS slot takes at most one new region slot, so the load limit
+// is checked up front (live + fill), before anything changes.  A key's slots lie in the buckets from
+// its home bucket to the first one with an EMPTY slot (a bucket fills front to back and is passed only
+// when full); the first of them in that order owns the key and adds all of them, in that order.
+__device__ bool agg_flush_session(const DevCfg& c, AggLds& L, const int64_t* E, const Region& r, Status* st) {
+  __syncthreads();
+  const int32_t need = L.live + L.fill;
+  if (need > region_limit(c.log_r)) {
+    if (threadIdx.x == 0) atomicMax(&st->need_live, need);
+    return false;
+  }
+  int nnew = 0;
+  int64_t mt = LMAX;
+  unsigned long long nflush = 0;
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
+    if (L.tag[h] < 2) continue;
+    const int64_t key = L.kv[h].x;
+    const uint32_t hk = lds_hash(key, 0), fp = lds_fp(hk);
+    int owner = -1;
+    bool end = false;
+    for (uint32_t i = 0, b = hk & (LDS_BUCKETS - 1); i < LDS_BUCKETS && owner < 0 && !end;
+         i++, b = (b + 1) & (LDS_BUCKETS - 1)) {
+      for (int q = 0; q < 4; q++) {
+        const int s = (int)b * 4 + q;
+        const uint32_t t = L.tag[s];
+        if (t == LT_EMPTY) {
+          end = true;
+          break;
+        }
+        if (t == fp && L.kv[s].x == key) {
+          owner = s;
+          break;
+        }
+      }
+    }
+    if (owner != h) continue;
+    end = false;
+    for (uint32_t i = 0, b = hk & (LDS_BUCKETS - 1); i < LDS_BUCKETS && !end; i++, b = (b + 1) & (LDS_BUCKETS - 1)) {
+      for (int q = 0; q < 4; q++) {
+        const int s = (int)b * 4 + q;
+        const uint32_t t = L.tag[s];
+        if (t == LT_EMPTY) {
+          end = true;
+          break;
+        }
+        if (t != fp) continue;
+        const i64x2 kv = L.kv[s];
+        if (kv.x != key) continue;
+        Entry d;
+        d.key = key;
+        d.start = kv.y;
+        d.end = E[s];
+        d.cnt = (int64_t)L.cnt[s];
+        d.sum = L.sum[s];
+        d.mn = L.mn[s];
+        d.mx = L.mx[s];
+        d.meta = FW_TIMER;
+        int64_t tm;
+        nnew += session_add(c, r, d, &tm, st);
+        mt = min(mt, tm);
+        nflush++;
+      }
+    }
+  }
+  if (nnew) atomicAdd(&L.nnew, nnew);
+  if (mt != LMAX) atomicMin((long long*)&L.min_timer, (long long)mt);
+  if (nflush) atomicAdd(&L.flushed, nflush);
+  __syncthreads();
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
+  if (threadIdx.x == 0) {
+    L.fill = 0;
+    L.live += L.nnew;
+    L.nnew = 0;
+  }
+  __syncthreads();
+  return true;
+}
+
+template <bool SESS>
+__device__ __forceinline__ bool agg_flush_any(const DevCfg& c, AggLds& L, const int64_t* E, const Region& r,
+                                              Status* st) {
+  if constexpr (SESS)
+    return agg_flush_session(c, L, E, r, st);
+  else
+    return agg_flush(c, L, r, st);
+}
+
 // write back what the workgroup learnt about its region (on completion and on suspension)
 __device__ __forceinline__ void agg_publish(const DevCfg& c, AggLds& L, DevTable& tb, int32_t p, Status* st) {
   tb.live[p] = L.live;
@@ -763,11 +1054,12 @@ __device__ __forceinline__ void agg_publish(const DevCfg& c, AggLds& L, DevTable
 // DIAG_AGG_TIMING: per-workgroup phase clocks (s_memtime), summed over the launch and printed by the
 // last workgroup to finish: [0] record loop, [1] flushes, [2] whole workgroup, [3] finished workgroups
 __device__ unsigned long long g_aggt[4];
-template <int RPT>
+template <int RPT, bool SESS>
 __global__ __launch_bounds__(FW_AGG_THREADS, FW_AGG_WAVES) void k_aggregate(DevCfg c, int64_t wm, const PRec* __restrict__ part,
                                                               const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
                                                               AggProg prog, int resume, Status* st) {
   __shared__ AggLds L;
+  __shared__ int64_t sess_end[SESS ? FW_LDS_SLOTS : 1];  // sessions: interval end of each LDS slot
   const int32_t p = blockIdx.x;
   if (resume && prog.done[p]) return;
   const int64_t begin = offs[(int64_t)p * T], end = offs[(int64_t)(p + 1) * T];
@@ -831,7 +1123,12 @@ __global__ __launch_bounds__(FW_AGG_THREADS, FW_AGG_WAVES) void k_aggregate(DevC
       for (int j = 0; j < RPT; j++) {
         if (failed || j < rj || rb + (int64_t)j * blockDim.x + threadIdx.x >= end) continue;
         for (int wi = j == rj ? rwi : 0; wi < nw[j]; wi++) {
-          if (!lds_upsert(L, c.vtype, k[j], jsub(t[j], (int64_t)wi * c.slide), v[j], c.diag)) {
+          bool in;
+          if constexpr (SESS)
+            in = lds_session_upsert(L, sess_end, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j]);
+          else
+            in = lds_upsert(L, c.vtype, k[j], jsub(t[j], (int64_t)wi * c.slide), v[j], c.diag);
+          if (!in) {
             failed = true;
             rj = j;
             rwi = wi;
@@ -848,7 +1145,7 @@ __global__ __launch_bounds__(FW_AGG_THREADS, FW_AGG_WAVES) void k_aggregate(DevC
       __syncthreads();
       if (!need) break;
       const unsigned long long tf0 = timing ? __builtin_amdgcn_s_memtime() : 0;
-      const bool fl = agg_flush(c, L, r, st);
+      const bool fl = agg_flush_any<SESS>(c, L, sess_end, r, st);
       if (timing) tflush += __builtin_amdgcn_s_memtime() - tf0;
       if (!fl) {
         ok = false;
@@ -862,7 +1159,7 @@ __global__ __launch_bounds__(FW_AGG_THREADS, FW_AGG_WAVES) void k_aggregate(DevC
     }
   }
   const unsigned long long tl = timing ? __builtin_amdgcn_s_memtime() : 0;
-  if (ok) ok = agg_flush(c, L, r, st);
+  if (ok) ok = agg_flush_any<SESS>(c, L, sess_end, r, st);
   if (timing && threadIdx.x == 0) {
     const unsigned long long te = __builtin_amdgcn_s_memtime();
     atomicAdd(&g_aggt[0], tl - tw0 - tflush);
@@ -891,7 +1188,6 @@ __global__ __launch_bounds__(FW_AGG_THREADS, FW_AGG_WAVES) void k_aggregate(DevC
 
 // ---- K_slow: ordered replay (one workgroup; one thread per key inside each chunk)
 constexpr int SLOW_CHUNK = FW_SLOW_THREADS;
-constexpr int MAX_SESSIONS = 64;  // in-flight sessions of one key visible to one replay step
 
 struct SlowCtx {
   DevCfg c;
@@ -1554,22 +1850,33 @@ void launch_scan(uint32_t* data, int64_t m, uint32_t* scratch, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(SCAN_T), 0, s, data, m, (const uint32_t*)scratch);
 }
 
+void launch_taint(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, int64_t n, Status* st,
+                  hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 2048);
+  if (blocks > 0) hipLaunchKernelGGL(k_taint, dim3((unsigned)blocks), dim3(256), 0, s, c, wm, key, ts, n, st);
+}
+
 void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
                     const int32_t* kh, int64_t n, int32_t T, uint32_t* offs, PRec* part, int64_t* sk, int64_t* stt,
                     int64_t* sv, int32_t* skh, DevSide side, Status* st, hipStream_t s) {
   hipLaunchKernelGGL(k_scatter, dim3(T), dim3(FW_TILE_THREADS), (size_t)c.P * sizeof(uint32_t), s, c, wm, key, ts, val,
                      kh, n, T, (const uint32_t*)offs, part, side, st);
   hipLaunchKernelGGL(k_scatter_ordered, dim3(T), dim3(FW_TILE_THREADS), 0, s, c, wm, key, ts, val, kh, n, T,
-                     (const uint32_t*)offs, (const uint32_t*)(offs + (int64_t)(c.P + 1) * T), sk, stt, sv, skh);
+                     (const uint32_t*)offs, (const uint32_t*)(offs + (int64_t)(c.P + 1) * T), sk, stt, sv, skh,
+                     (const Status*)st);
 }
 
 void launch_aggregate(const DevCfg& c, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
                       AggProg prog, int resume, Status* st, hipStream_t s) {
-  if (c.diag & DIAG_AGG_RPT8)
-    hipLaunchKernelGGL(k_aggregate<8>, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb, prog, resume, st);
+  if (c.assigner == FW_SESSION)
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true>), dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb,
+                       prog, resume, st);
+  else if (c.diag & DIAG_AGG_RPT8)
+    hipLaunchKernelGGL((k_aggregate<8, false>), dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb, prog,
+                       resume, st);
   else
-    hipLaunchKernelGGL(k_aggregate<FW_AGG_RPT>, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb, prog, resume,
-                       st);
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false>), dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb,
+                       prog, resume, st);
 }
 
 void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* offs, int32_t T, const int64_t* sk, const int64_t* stt,

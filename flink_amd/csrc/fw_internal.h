@@ -51,6 +51,12 @@ struct DevCfg {
   // invariant-divisor reciprocals (Granlund-Montgomery round-up method) for `% size` / `% slide`
   uint64_t mag_size, mag_slide;
   int32_t l_size, l_slide;
+  // sessions: keys that have an ordered-path record in the current batch ("tainted": all their records
+  // of the batch are replayed in arrival order).  Open addressing; a slot belongs to the batch whose
+  // epoch it holds, so the set is never cleared.
+  uint64_t* taint_key;
+  uint32_t* taint_state;
+  uint32_t taint_mask, taint_epoch;
 };
 
 // host: reciprocal of d >= 1 for div_inv(): m = floor(2^64 (2^l - d) / d) + 1, l = ceil(log2 d)
@@ -104,6 +110,7 @@ struct Status {
   int32_t ts_errors;
   int32_t suspended;                  // FW_SUSP_*: later kernels of the push / watermark skip themselves
   int32_t need_grow;                  // some region is over half full: grow before it has to suspend
+  int32_t taint_any;                  // sessions: 0 no tainted key in the batch, 1 check the set, 2 set full: all
 };
 enum {
   FW_STATUS_STATE_LOST = 1,  // a window could not be stored (more in-flight sessions of one key than supported)
@@ -157,6 +164,8 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
                     int64_t* stt, int64_t* sv, int32_t* skh, DevSide side, Status* st, hipStream_t_ s);
 void launch_aggregate(const DevCfg& c, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
                       AggProg prog, int resume, Status* st, hipStream_t_ s);
+void launch_taint(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, int64_t n, Status* st,
+                  hipStream_t_ s);
 void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* offs, int32_t T, const int64_t* sk,
                  const int64_t* stt, const int64_t* sv, const int32_t* skh, DevTable tb, DevRows out, DevSide side,
                  Status* st, int resume, hipStream_t_ s);

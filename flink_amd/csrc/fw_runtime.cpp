@@ -63,6 +63,7 @@ struct fw_op {
   Scratch sc[2];
   int last_sc = 1;   // set of the most recent push
   AggProg prog{};    // k_aggregate resume points
+  uint32_t taint_epoch = 0;  // sessions: epoch of the latest batch's taint set (DevCfg.taint_*)
 
   DevRows out{};
   DevSide side{};
@@ -428,7 +429,7 @@ int maybe_restart_rows(fw_op* op) {
 int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int64_t n) {
   if (n == 0) return FW_OK;
   int rc;
-  const DevCfg& c = op->dc;
+  DevCfg c = op->dc;  // by value: a session batch stamps its taint epoch into it
   // queue the batch-only kernels before waiting for the previous sequence, except with side
   // output (the scatter appends late records to the side buffer, whose capacity and counters the
   // settle below must see unchanged)
@@ -442,7 +443,17 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   Scratch& S = op->sc[nxt];
   const int32_t T = (int32_t)((n + FW_TILE - 1) / FW_TILE);
   const int64_t m = (int64_t)(c.P + 1) * T;
+  if (c.assigner == FW_SESSION) {
+    // a new epoch empties the taint set; its slots are cleared only when the epochs wrap
+    if (++op->taint_epoch >= 0x80000000u) {
+      HIP_OR_RETURN(op, hipMemsetAsync(c.taint_state, 0, ((size_t)c.taint_mask + 1) * sizeof(uint32_t), op->stream));
+      op->taint_epoch = 1;
+    }
+    c.taint_epoch = op->taint_epoch;
+    HIP_OR_RETURN(op, hipMemsetAsync(&op->d_status->taint_any, 0, sizeof(int32_t), op->stream));
+  }
   timed(op, K_CLASSIFY, [&] {
+    if (c.assigner == FW_SESSION) fwdev::launch_taint(c, op->wm, key, ts, n, op->d_status, op->stream);
     fwdev::launch_classify_hist(c, op->wm, key, ts, kh, n, T, S.hist, op->d_status, op->stream);
   });
   timed(op, K_SCAN, [&] { fwdev::launch_scan(S.hist, m, S.scan_tmp, op->stream); });
@@ -572,6 +583,15 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   HIP_OR_RETURN(op, dmalloc(&op->in_kh, mb));
   for (Scratch& sc : op->sc)
     if ((rc = alloc_scratch(op, sc, mb, m))) return rc;
+  if (c.assigner == FW_SESSION) {
+    // the batches' taint set (k_taint): 2x the batch, at most 2^22 slots; a batch whose ordered-path
+    // keys overflow it replays all of its records in arrival order
+    const int64_t cap = std::min<int64_t>(next_pow2(2 * mb), int64_t(1) << 22);
+    HIP_OR_RETURN(op, dmalloc(&c.taint_key, (size_t)cap));
+    HIP_OR_RETURN(op, dmalloc(&c.taint_state, (size_t)cap));
+    HIP_OR_RETURN(op, hipMemsetAsync(c.taint_state, 0, (size_t)cap * sizeof(uint32_t), op->stream));
+    c.taint_mask = (uint32_t)(cap - 1);
+  }
   HIP_OR_RETURN(op, dmalloc(&op->prog.rb, (size_t)c.P));
   HIP_OR_RETURN(op, dmalloc(&op->prog.tp, (size_t)c.P * FW_AGG_THREADS));
   HIP_OR_RETURN(op, dmalloc(&op->prog.done, (size_t)c.P));
@@ -604,6 +624,8 @@ void fw_destroy(fw_op* op) {
   dfree(op->prog.rb);
   dfree(op->prog.tp);
   dfree(op->prog.done);
+  dfree(op->dc.taint_key);
+  dfree(op->dc.taint_state);
   for (int64_t** col : {&op->out.key, &op->out.start, &op->out.end, &op->out.cnt, &op->out.sum, &op->out.mn,
                         &op->out.mx, &op->side.key, &op->side.ts, &op->side.val})
     dfree(*col);

@@ -124,7 +124,8 @@ def test_gpu_zipf_hot_keys():
 
 
 @pytest.mark.parametrize("cfg", [dict(assigner="tumbling", size=1000),
-                                 dict(assigner="sliding", size=5000, slide=1000)], ids=["tumbling", "sliding"])
+                                 dict(assigner="sliding", size=5000, slide=1000),
+                                 dict(assigner="session", gap=50)], ids=["tumbling", "sliding", "session"])
 def test_gpu_lds_flush_and_retry(cfg):
     # ~8K distinct (key, window) pairs per state partition and batch: the LDS pre-aggregation table
     # (1024 slots) fills many times inside one round, so flush-and-retry is exercised heavily
@@ -133,13 +134,68 @@ def test_gpu_lds_flush_and_retry(cfg):
     assert_rows_equal(g, r)
 
 
-def test_gpu_table_growth():
+@pytest.mark.parametrize("cfg", [dict(assigner="tumbling", size=10_000), dict(assigner="session", gap=100)],
+                         ids=["tumbling", "session"])
+def test_gpu_table_growth(cfg):
     # tiny initial table: regions run out of room mid-aggregate, the push suspends, the table grows
     # and the push resumes (several times per push)
-    cfg = dict(assigner="tumbling", size=10_000)
     batches, wms = _stream(300_000, 100_000, 200_000, bound=100, jitter=100, rate=1_000_000)
     g, r, *_ = _run_both(cfg, batches, wms, expected_entries=1000)
     assert_rows_equal(g, r)
+
+
+def test_gpu_session_merges_across_flushes():
+    # one state partition per key group and ~1500 keys per partition: the LDS table flushes several
+    # times per batch, so a key's session is built from LDS intervals of different flushes that the
+    # flush joins into the region's sessions (connected components); keys recur about every 10 ms
+    # against a 50 ms gap, so sessions grow long and merge across batches too
+    cfg = dict(assigner="session", gap=50)
+    batches, wms = _stream(1 << 20, 1 << 18, 200_000, bound=100, jitter=100, rate=20_000_000)
+    g, r, *_ = _run_both(cfg, batches, wms, sub_partitions=1)
+    assert_rows_equal(g, r)
+
+
+def test_gpu_sessions_take_parallel_path():
+    # in-order enough (jitter < bound): every element's window ends after the watermark, no key is
+    # tainted, and the ordered path replays nothing
+    cfg = dict(assigner="session", gap=300)
+    batches, wms = _stream(200_000, 20_000, 5000, bound=400, jitter=300, rate=100_000)
+    gpu = _gpu_op(**cfg)
+    ref = orc.WindowOperatorOracle(**cfg)
+    for (k, t, v), wm in zip(batches, wms):
+        gpu.process(k, t, v)
+        ref.process(k, t, v)
+        gpu.watermark(wm)
+        ref.watermark(wm)
+    assert gpu.stats()["slow_path_records"] == 0
+    assert_rows_equal(gpu.rows(), ref.rows())
+    gpu.close()
+
+
+def test_gpu_session_taint_orders_mixed_keys():
+    # key 7 has in-time elements and, in the same batch, one whose window [880, 980) ends before the
+    # watermark 1000 but within the allowed lateness: it merges into the session the in-time elements
+    # build, so all of key 7's elements are replayed in arrival order; key 8 stays on the parallel path
+    cfg = dict(assigner="session", gap=100, lateness=1000, side_output=True)
+    gpu = _gpu_op(**cfg)
+    ref = orc.WindowOperatorOracle(**cfg)
+    steps = [
+        (np.array([7, 8], dtype=np.int64), np.array([500, 510], dtype=np.int64), 1000),
+        (np.array([7, 8, 7, 8, 7, 7, 9], dtype=np.int64), np.array([950, 960, 1040, 1100, 880, 990, 20], dtype=np.int64),
+         1200),
+        (np.array([7, 8], dtype=np.int64), np.array([1150, 1250], dtype=np.int64), (1 << 63) - 1),
+    ]
+    for k, t, wm in steps:
+        v = (k * 10 + t).astype(np.int64)
+        gpu.process(k, t, v)
+        ref.process(k, t, v)
+        gpu.watermark(wm)
+        ref.watermark(wm)
+    assert gpu.stats()["slow_path_records"] > 0
+    assert_rows_equal(gpu.rows(), ref.rows())
+    assert_side_equal(gpu.side_rows(), ref.side_rows())
+    assert gpu.late_dropped == ref.late_dropped
+    gpu.close()
 
 
 def _run_device(cfg, batches, wms, **gpu_kw):
