@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--window", type=int, default=1000, help="tumbling window (ms, c2)")
     ap.add_argument("--gap", type=int, default=30_000, help="session gap (ms, c4)")
     ap.add_argument("--cpu-sample", type=int, default=None)
+    ap.add_argument("--zipf", type=float, default=None, help="Zipf exponent of the keys (0 = uniform)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
@@ -75,7 +76,9 @@ def main():
     for name in ("keys", "rate", "bound", "jitter", "cpu_sample"):
         if getattr(args, name) is None:
             setattr(args, name, preset[name])
-    args.zipf = preset["zipf"]
+    if args.zipf is None:
+        args.zipf = preset["zipf"]
+    args.zipf = args.zipf or None
     sessions = args.workload == "c4"
 
     import torch

@@ -634,6 +634,8 @@ struct AggLds {
   int32_t slot[FW_LDS_SLOTS];  // flush: the window's slot in the region, -1 if new
   int fill;
   int anyfail;
+  int spill;   // split partition: deltas this chunk wrote
+  int last;    // split partition: this workgroup finished the partition's last chunk
   int nnew;    // flush: windows of this LDS epoch not yet in the region
   int live;    // occupied slots of the region
   unsigned long long flushed;
@@ -671,13 +673,32 @@ __device__ __forceinline__ void lds_acc(AggLds& L, int target, int vtype, int64_
   }
 }
 
-// insert-or-accumulate one value into the LDS table; false when the table is at its fill limit
+// take one of the FW_LDS_FILL_LIMIT slot tickets before claiming a slot: concurrent claims then
+// cannot fill the table past the limit, so every probe chain ends at an EMPTY slot
+__device__ __forceinline__ bool lds_reserve(AggLds& L) {
+  if (__hip_atomic_load(&L.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= FW_LDS_FILL_LIMIT) return false;
+  if (atomicAdd(&L.fill, 1) < FW_LDS_FILL_LIMIT) return true;
+  atomicSub(&L.fill, 1);
+  return false;
+}
+
+// merge a delta (an accumulator in Entry form) into LDS slot `target` (AggregateFunction.merge)
+__device__ __forceinline__ void lds_acc_delta(AggLds& L, int target, int vtype, const Entry& d) {
+  atomicAdd(&L.cnt[target], (uint32_t)d.cnt);
+  if (vtype == FW_VAL_F64)
+    atomicAdd((double*)&L.sum[target], __longlong_as_double(d.sum));
+  else
+    atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)d.sum);
+  atomicMin((long long*)&L.mn[target], (long long)d.mn);
+  atomicMax((long long*)&L.mx[target], (long long)d.mx);
+}
+
+// find or claim the LDS slot of (key, window start); -1 when the table is at its fill limit
 // (the caller flushes and retries).  A lane that claims a slot publishes it inside the same loop
 // iteration (CAS EMPTY -> BUSY, write the key, store the fingerprint), so lanes of its own wave that
 // wait on the BUSY tag see the fingerprint on their next iteration.  LDS operations of one wave
 // complete in order, so a reader that sees the fingerprint reads the key written before it.
-__device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, int64_t start, int64_t v,
-                                           int diag = 0) {
+__device__ __forceinline__ int lds_slot(AggLds& L, int64_t key, int64_t start) {
   const uint32_t h = lds_hash(key, start), fp = lds_fp(h);
   uint32_t b = h & (LDS_BUCKETS - 1);
   int target = -1;
@@ -716,11 +737,9 @@ __device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, in
       continue;
     }
     if (empty >= 0) {
-      if (__hip_atomic_load(&L.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= FW_LDS_FILL_LIMIT)
-        return false;  // table full: flush first
+      if (!lds_reserve(L)) return -1;  // table full: flush first
       const int s = (int)b * 4 + empty;
       if (atomicCAS(&L.tag[s], LT_EMPTY, LT_BUSY) == LT_EMPTY) {
-        atomicAdd(&L.fill, 1);
         L.kv[s] = i64x2{key, start};
         L.cnt[s] = 0;
         L.sum[s] = 0;
@@ -730,11 +749,17 @@ __device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, in
         target = s;
         break;
       }
+      atomicSub(&L.fill, 1);
       continue;  // lost the claim race: re-read the bucket
     }
     b = (b + 1) & (LDS_BUCKETS - 1);  // bucket full without a match
     guard++;
   }
+  return target;
+}
+__device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, int64_t start, int64_t v,
+                                           int diag = 0) {
+  const int target = lds_slot(L, key, start);
   if (target < 0) return false;
   if (diag & DIAG_AGG_NO_ACCUM) return true;
   lds_acc(L, target, vtype, v);
@@ -833,8 +858,7 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
 // it, which is always connected) and its accumulator; `end` lives in the separate array E.  An element
 // joins a slot of its key whose interval intersects its window and widens it with LDS min/max, or
 // claims a new slot.  Slots of one key that come to overlap are joined by the flush.
-__device__ __forceinline__ bool lds_session_upsert(AggLds& L, int64_t* E, int vtype, int64_t key, int64_t ws,
-                                                   int64_t we, int64_t v) {
+__device__ __forceinline__ int lds_session_slot(AggLds& L, int64_t* E, int64_t key, int64_t ws, int64_t we) {
   const uint32_t h = lds_hash(key, 0), fp = lds_fp(h);
   uint32_t b = h & (LDS_BUCKETS - 1);
   int target = -1;
@@ -858,11 +882,9 @@ __device__ __forceinline__ bool lds_session_upsert(AggLds& L, int64_t* E, int vt
       continue;
     }
     if (empty >= 0) {
-      if (__hip_atomic_load(&L.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= FW_LDS_FILL_LIMIT)
-        return false;
+      if (!lds_reserve(L)) return -1;
       const int s = (int)b * 4 + empty;
       if (atomicCAS(&L.tag[s], LT_EMPTY, LT_BUSY) == LT_EMPTY) {
-        atomicAdd(&L.fill, 1);
         L.kv[s] = i64x2{key, ws};
         E[s] = we;
         L.cnt[s] = 0;
@@ -873,14 +895,21 @@ __device__ __forceinline__ bool lds_session_upsert(AggLds& L, int64_t* E, int vt
         target = s;
         break;
       }
+      atomicSub(&L.fill, 1);
       continue;
     }
     b = (b + 1) & (LDS_BUCKETS - 1);
     guard++;
   }
-  if (target < 0) return false;
+  if (target < 0) return -1;
   atomicMin(reinterpret_cast<long long*>(&L.kv[target]) + 1, (long long)ws);  // TimeWindow.cover
   atomicMax((long long*)&E[target], (long long)we);
+  return target;
+}
+__device__ __forceinline__ bool lds_session_upsert(AggLds& L, int64_t* E, int vtype, int64_t key, int64_t ws,
+                                                   int64_t we, int64_t v) {
+  const int target = lds_session_slot(L, E, key, ws, we);
+  if (target < 0) return false;
   lds_acc(L, target, vtype, v);
   return true;
 }
@@ -892,7 +921,9 @@ __device__ __forceinline__ bool lds_session_upsert(AggLds& L, int64_t* E, int vt
 // which is after the watermark).  Only the thread that owns d.key touches the key's entries; new
 // slots are published BUSY -> LIVE because other threads walk the same probe chains.
 // Returns the region slots newly taken; *timer = maxTimestamp of the resulting session.
-__device__ int session_add(const DevCfg& c, const Region& r, const Entry& d, int64_t* timer, Status* st) {
+// DIAG_AGG_TIMING clocks of the session flush (thread 0): [0] flushes, [1] linking, [2] adding, [3] tail
+__device__ unsigned long long g_sess[4];
+__device__ __noinline__ int session_add_many(const DevCfg& c, const Region& r, const Entry& d, int64_t* timer, Status* st) {
   const uint64_t h = slot_hash(c, d.key, 0);
   const uint32_t want = live_word(h);
   int32_t sl[MAX_SESSIONS];
@@ -956,20 +987,97 @@ __device__ int session_add(const DevCfg& c, const Region& r, const Entry& d, int
   return 0;
 }
 
+// session_add with the key's in-flight sessions held in registers (the common case: at most
+// SESS_REG sessions of one key); more go through session_add_many, which holds up to MAX_SESSIONS
+constexpr int SESS_REG = 4;
+__device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, const Entry& d, int64_t* timer, Status* st) {
+  const uint64_t h = slot_hash(c, d.key, 0);
+  const uint32_t want = live_word(h);
+  uint32_t sl[SESS_REG];
+  int64_t ss[SESS_REG], se[SESS_REG];
+  int ns = 0;
+  for (uint32_t i = 0; i <= r.mask; i++) {
+    const uint32_t s = ((uint32_t)h + i) & r.mask;
+    const uint32_t stt = ld_state(r.state + s);
+    if (stt == SLOT_EMPTY) break;
+    if (stt != want) continue;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const Entry& e = r.ent[s];
+    if (e.key != d.key) continue;
+    if (ns == SESS_REG) return session_add_many(c, r, d, timer, st);
+    const int64_t es = e.start, ee = e.end;
+#pragma unroll
+    for (int q = 0; q < SESS_REG; q++) {
+      if (q == ns) {
+        sl[q] = s;
+        ss[q] = es;
+        se[q] = ee;
+      }
+    }
+    ns++;
+  }
+  int64_t cs = d.start, ce = d.end;
+  uint32_t in_group = 0;
+  for (bool grew = true; grew;) {
+    grew = false;
+#pragma unroll
+    for (int q = 0; q < SESS_REG; q++) {
+      if (q < ns && !(in_group >> q & 1) && cs <= se[q] && ce >= ss[q]) {  // TimeWindow.intersects
+        in_group |= 1u << q;
+        cs = min(cs, ss[q]);
+        ce = max(ce, se[q]);
+        grew = true;
+      }
+    }
+  }
+  *timer = jsub(ce, 1);
+  if (in_group == 0) {  // a new session
+    const int32_t s = region_claim(r, h, SLOT_BUSY);
+    if (s < 0) {  // cannot happen below the load limit (checked by the flush)
+      atomicOr(&st->flags, FW_STATUS_STATE_LOST);
+      return 0;
+    }
+    r.ent[s] = d;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __hip_atomic_store(r.state + s, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 1;
+  }
+  const int first = __ffs(in_group) - 1;
+  uint32_t target = sl[0];
+#pragma unroll
+  for (int q = 1; q < SESS_REG; q++) target = q == first ? sl[q] : target;
+  Entry m = r.ent[target];
+#pragma unroll
+  for (int q = 0; q < SESS_REG; q++) {
+    if (q <= first || !(in_group >> q & 1)) continue;
+    acc_merge(c, m, r.ent[sl[q]]);
+    // the slot stays occupied (live counts occupied slots) until k_fire rebuilds the region
+    __hip_atomic_store(r.state + sl[q], SLOT_DEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  acc_merge(c, m, d);
+  m.start = cs;
+  m.end = ce;
+  m.meta = FW_TIMER;
+  r.ent[target] = m;
+  return 0;
+}
+
 // flush of the session LDS table.  Every LDS slot takes at most one new region slot, so the load limit
 // is checked up front (live + fill), before anything changes.  A key's slots lie in the buckets from
 // its home bucket to the first one with an EMPTY slot (a bucket fills front to back and is passed only
-// when full); the first of them in that order owns the key and adds all of them, in that order.
-__device__ bool agg_flush_session(const DevCfg& c, AggLds& L, const int64_t* E, const Region& r, Status* st) {
+// when full).  Pass 1 links each key's slots in that order through L.slot (next slot + 1, bit 16 =
+// first slot, which owns the key); pass 2 lets every owner add its key's slots one per step, so the
+// lanes of a wave call session_add together instead of one after another.
+__device__ __forceinline__ bool agg_flush_session(const DevCfg& c, AggLds& L, const int64_t* E, const Region& r,
+                                                  Status* st) {
   __syncthreads();
+  const bool timing = c.diag & DIAG_AGG_TIMING;
+  const unsigned long long ts0 = timing ? __builtin_amdgcn_s_memtime() : 0;
   const int32_t need = L.live + L.fill;
   if (need > region_limit(c.log_r)) {
     if (threadIdx.x == 0) atomicMax(&st->need_live, need);
     return false;
   }
-  int nnew = 0;
-  int64_t mt = LMAX;
-  unsigned long long nflush = 0;
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
     if (L.tag[h] < 2) continue;
     const int64_t key = L.kv[h].x;
@@ -991,35 +1099,51 @@ __device__ bool agg_flush_session(const DevCfg& c, AggLds& L, const int64_t* E, 
         }
       }
     }
-    if (owner != h) continue;
+    int nxt = -1;
     end = false;
-    for (uint32_t i = 0, b = hk & (LDS_BUCKETS - 1); i < LDS_BUCKETS && !end; i++, b = (b + 1) & (LDS_BUCKETS - 1)) {
-      for (int q = 0; q < 4; q++) {
+    for (uint32_t i = 0, b = (uint32_t)h / 4; i < LDS_BUCKETS && nxt < 0 && !end;
+         i++, b = (b + 1) & (LDS_BUCKETS - 1)) {
+      for (int q = i == 0 ? h % 4 + 1 : 0; q < 4; q++) {
         const int s = (int)b * 4 + q;
         const uint32_t t = L.tag[s];
         if (t == LT_EMPTY) {
           end = true;
           break;
         }
-        if (t != fp) continue;
-        const i64x2 kv = L.kv[s];
-        if (kv.x != key) continue;
-        Entry d;
-        d.key = key;
-        d.start = kv.y;
-        d.end = E[s];
-        d.cnt = (int64_t)L.cnt[s];
-        d.sum = L.sum[s];
-        d.mn = L.mn[s];
-        d.mx = L.mx[s];
-        d.meta = FW_TIMER;
-        int64_t tm;
-        nnew += session_add(c, r, d, &tm, st);
-        mt = min(mt, tm);
-        nflush++;
+        if (t == fp && L.kv[s].x == key) {
+          nxt = s;
+          break;
+        }
       }
     }
+    L.slot[h] = (nxt + 1) | (owner == h ? 1 << 16 : 0);
   }
+  __syncthreads();
+  const unsigned long long ts1 = timing ? __builtin_amdgcn_s_memtime() : 0;
+  int nnew = 0;
+  int64_t mt = LMAX;
+  unsigned long long nflush = 0;
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
+    int j = L.tag[h] >= 2 && (L.slot[h] >> 16) ? h : -1;
+    while (j >= 0) {
+      const i64x2 kv = L.kv[j];
+      Entry d;
+      d.key = kv.x;
+      d.start = kv.y;
+      d.end = E[j];
+      d.cnt = (int64_t)L.cnt[j];
+      d.sum = L.sum[j];
+      d.mn = L.mn[j];
+      d.mx = L.mx[j];
+      d.meta = FW_TIMER;
+      int64_t tm;
+      nnew += session_add(c, r, d, &tm, st);
+      mt = min(mt, tm);
+      nflush++;
+      j = (L.slot[j] & 0xffff) - 1;
+    }
+  }
+  const unsigned long long ts2 = timing ? __builtin_amdgcn_s_memtime() : 0;
   if (nnew) atomicAdd(&L.nnew, nnew);
   if (mt != LMAX) atomicMin((long long*)&L.min_timer, (long long)mt);
   if (nflush) atomicAdd(&L.flushed, nflush);
@@ -1031,6 +1155,12 @@ __device__ bool agg_flush_session(const DevCfg& c, AggLds& L, const int64_t* E, 
     L.nnew = 0;
   }
   __syncthreads();
+  if (timing && threadIdx.x == 0) {
+    atomicAdd(&g_sess[0], 1ull);
+    atomicAdd(&g_sess[1], ts1 - ts0);
+    atomicAdd(&g_sess[2], ts2 - ts1);
+    atomicAdd(&g_sess[3], __builtin_amdgcn_s_memtime() - ts2);
+  }
   return true;
 }
 
@@ -1051,16 +1181,218 @@ __device__ __forceinline__ void agg_publish(const DevCfg& c, AggLds& L, DevTable
   if (L.live > (1 << c.log_r) / 2) st->need_grow = 1;
 }
 
+// ---- split partitions (hot keys, see AggHot).  Chunks per partition, for the scan that maps
+// workgroups to (partition, chunk); a resumed launch keeps the plan of the launch it resumes.
+__global__ void k_chunk_plan(DevCfg c, const uint32_t* __restrict__ offs, int32_t T, AggHot hot) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p > c.P) return;
+  if (p == c.P) {
+    hot.chunk_base[p] = 0;
+    return;
+  }
+  const int64_t len = (int64_t)offs[(int64_t)(p + 1) * T] - offs[(int64_t)p * T];
+  hot.chunk_base[p] = len > FW_AGG_CHUNK ? (uint32_t)((len + FW_AGG_CHUNK - 1) / FW_AGG_CHUNK) : 1u;
+  hot.pdone[p] = 0;
+}
+
+// write the LDS entries of a chunk as deltas (Entry form, accumulators as in the LDS) and empty the table
+template <bool SESS>
+__device__ void agg_spill(const DevCfg& c, AggLds& L, const int64_t* E, Entry* out) {
+  __syncthreads();
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
+    if (L.tag[h] < 2) continue;
+    Entry d = lds_delta(c, L, h);
+    if constexpr (SESS) d.end = E[h];
+    out[atomicAdd(&L.spill, 1)] = d;
+  }
+  __syncthreads();
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
+  if (threadIdx.x == 0) L.fill = 0;
+  __syncthreads();
+}
+
+// One chunk of a split partition.  Phase 1 (every chunk): pre-aggregate the chunk's records, spilling
+// the LDS table as deltas whenever it fills (no region access, so no suspension).  The workgroup that
+// finishes the partition's last chunk (release/acquire through pdone) runs phase 2: it merges every
+// chunk's deltas into the region with the LDS table and the usual flush, which may suspend; a resumed
+// launch continues phase 2 in the partition's chunk-0 workgroup (prog.rb = delta round, prog.tp = delta
+// of the round per thread).
+template <int RPT, bool SESS>
+__device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __restrict__ part, int64_t begin,
+                          int64_t end, int32_t p, int32_t ch, int32_t nch, DevTable& tb, const AggProg& prog,
+                          int resume, const AggHot& hot, Status* st) {
+  const int32_t c0 = (int32_t)hot.chunk_base[p];
+  if (resume && (ch != 0 || prog.done[p])) return;
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
+  if (threadIdx.x == 0) {
+    L.fill = 0;
+    L.anyfail = 0;
+    L.spill = 0;
+    L.last = 0;
+  }
+  __syncthreads();
+  if (!resume) {
+    const int64_t cb = begin + (int64_t)ch * FW_AGG_CHUNK, ce = min(end, cb + (int64_t)FW_AGG_CHUNK);
+    for (int64_t rb = cb; rb < ce; rb += (int64_t)blockDim.x * RPT) {
+      int64_t k[RPT], t[RPT], v[RPT];
+#pragma unroll
+      for (int j = 0; j < RPT; j++) {
+        const int64_t i = rb + (int64_t)j * blockDim.x + threadIdx.x;
+        i64x2 a = {0, 0}, b2 = {0, 0};
+        if (i < ce) {
+          const i64x2* src = reinterpret_cast<const i64x2*>(part + i);
+          a = src[0];
+          b2 = src[1];
+        }
+        k[j] = a.x;
+        t[j] = a.y;
+        v[j] = b2.x;
+      }
+      int rj = 0;
+      for (;;) {
+        bool failed = false;
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+          if (failed || j < rj || rb + (int64_t)j * blockDim.x + threadIdx.x >= ce) continue;
+          bool in;
+          if constexpr (SESS)
+            in = lds_session_upsert(L, E, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j]);
+          else
+            in = lds_upsert(L, c.vtype, k[j], t[j], v[j]);
+          if (!in) {
+            failed = true;
+            rj = j;
+          }
+        }
+        if (failed)
+          L.anyfail = 1;
+        else
+          rj = RPT;
+        __syncthreads();
+        const int need = L.anyfail;
+        __syncthreads();
+        if (!need) break;
+        agg_spill<SESS>(c, L, E, hot.delta + cb);
+        if (threadIdx.x == 0) L.anyfail = 0;
+        __syncthreads();
+      }
+    }
+    agg_spill<SESS>(c, L, E, hot.delta + cb);
+    if (threadIdx.x == 0) hot.nd[c0 + ch] = L.spill;
+    __threadfence();  // release this chunk's deltas to the workgroup that merges them
+    __syncthreads();
+    if (threadIdx.x == 0) L.last = atomicAdd(&hot.pdone[p], 1u) == (uint32_t)(nch - 1);
+    __syncthreads();
+    if (!L.last) return;
+    __threadfence();  // acquire the other chunks' deltas
+  }
+  // phase 2: merge the deltas of every chunk into the region
+  int64_t srb = begin;
+  int srj = 0;
+  if (resume) {
+    srb = prog.rb[p];
+    srj = (int)(prog.tp[(int64_t)p * FW_AGG_THREADS + threadIdx.x] & 0xffu);
+  }
+  if (threadIdx.x == 0) {
+    L.anyfail = 0;
+    L.nnew = 0;
+    L.live = tb.live[p];
+    L.flushed = 0;
+    L.min_timer = LMAX;
+  }
+  __syncthreads();
+  const Region r = region_of(c, tb, p, tb.cur[p]);
+  bool ok = true, first = true;
+  for (int32_t j = (int32_t)((srb - begin) / FW_AGG_CHUNK); j < nch && ok; j++) {
+    const int64_t db = begin + (int64_t)j * FW_AGG_CHUNK, de = db + hot.nd[c0 + j];
+    for (int64_t rb = max(db, srb); rb < de && ok; rb += (int64_t)blockDim.x * RPT) {
+      Entry d[RPT];
+#pragma unroll
+      for (int q = 0; q < RPT; q++) {
+        const int64_t i = rb + (int64_t)q * blockDim.x + threadIdx.x;
+        if (i < de) d[q] = hot.delta[i];
+      }
+      int rj = first ? srj : 0;
+      first = false;
+      for (;;) {
+        bool failed = false;
+#pragma unroll
+        for (int q = 0; q < RPT; q++) {
+          if (failed || q < rj || rb + (int64_t)q * blockDim.x + threadIdx.x >= de) continue;
+          int tg;
+          if constexpr (SESS)
+            tg = lds_session_slot(L, E, d[q].key, d[q].start, d[q].end);
+          else
+            tg = lds_slot(L, d[q].key, d[q].start);
+          if (tg < 0) {
+            failed = true;
+            rj = q;
+          } else {
+            lds_acc_delta(L, tg, c.vtype, d[q]);
+          }
+        }
+        if (failed)
+          L.anyfail = 1;
+        else
+          rj = RPT;
+        __syncthreads();
+        const int need = L.anyfail;
+        __syncthreads();
+        if (!need) break;
+        if (!agg_flush_any<SESS>(c, L, E, r, st)) {
+          ok = false;
+          break;
+        }
+        srb = rb;
+        srj = rj;
+        if (threadIdx.x == 0) L.anyfail = 0;
+        __syncthreads();
+      }
+    }
+  }
+  if (ok) ok = agg_flush_any<SESS>(c, L, E, r, st);
+  if (!ok) {
+    prog.tp[(int64_t)p * FW_AGG_THREADS + threadIdx.x] = (uint32_t)srj;
+    if (threadIdx.x == 0) {
+      prog.rb[p] = srb;
+      prog.done[p] = 0;
+      atomicOr(&st->suspended, (int)FW_SUSP_AGG);
+    }
+  } else if (threadIdx.x == 0) {
+    prog.done[p] = 1;
+  }
+  if (threadIdx.x == 0) agg_publish(c, L, tb, p, st);
+}
+
 // DIAG_AGG_TIMING: per-workgroup phase clocks (s_memtime), summed over the launch and printed by the
 // last workgroup to finish: [0] record loop, [1] flushes, [2] whole workgroup, [3] finished workgroups
 __device__ unsigned long long g_aggt[4];
 template <int RPT, bool SESS>
-__global__ __launch_bounds__(FW_AGG_THREADS, FW_AGG_WAVES) void k_aggregate(DevCfg c, int64_t wm, const PRec* __restrict__ part,
+__global__ __launch_bounds__(FW_AGG_THREADS, SESS ? 4 : FW_AGG_WAVES) void k_aggregate(DevCfg c, int64_t wm, const PRec* __restrict__ part,
                                                               const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
-                                                              AggProg prog, int resume, Status* st) {
+                                                              AggProg prog, int resume, Status* st, AggHot hot) {
   __shared__ AggLds L;
   __shared__ int64_t sess_end[SESS ? FW_LDS_SLOTS : 1];  // sessions: interval end of each LDS slot
-  const int32_t p = blockIdx.x;
+  int32_t p = blockIdx.x;
+  if (hot.chunk_base) {  // workgroup -> (partition, chunk): last partition whose first chunk <= blockIdx.x
+    if (blockIdx.x >= hot.chunk_base[c.P]) return;
+    int32_t lo = 0, hi = c.P - 1;
+    while (lo < hi) {
+      const int32_t mid = (lo + hi + 1) >> 1;
+      if (hot.chunk_base[mid] <= blockIdx.x)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    p = lo;
+    const int32_t nch = (int32_t)(hot.chunk_base[p + 1] - hot.chunk_base[p]);
+    if (nch > 1) {
+      const int64_t b0 = offs[(int64_t)p * T], e0 = offs[(int64_t)(p + 1) * T];
+      agg_split<RPT, SESS>(c, L, sess_end, part, b0, e0, p, (int32_t)(blockIdx.x - hot.chunk_base[p]), nch, tb, prog,
+                           resume, hot, st);
+      return;
+    }
+  }
   if (resume && prog.done[p]) return;
   const int64_t begin = offs[(int64_t)p * T], end = offs[(int64_t)(p + 1) * T];
   if (begin == end) {
@@ -1165,12 +1497,18 @@ __global__ __launch_bounds__(FW_AGG_THREADS, FW_AGG_WAVES) void k_aggregate(DevC
     atomicAdd(&g_aggt[0], tl - tw0 - tflush);
     atomicAdd(&g_aggt[1], tflush + (te - tl));
     atomicAdd(&g_aggt[2], te - tw0);
-    if (atomicAdd(&g_aggt[3], 1ull) == gridDim.x - 1) {
+    if (atomicAdd(&g_aggt[3], 1ull) == (unsigned long long)c.P - 1) {  // (counts unsplit partitions only)
       __threadfence();
       const double n = (double)gridDim.x;
       printf("agg timing: per WG loop %.0f flush %.0f total %.0f clocks (%d WGs)\n", g_aggt[0] / n, g_aggt[1] / n,
              g_aggt[2] / n, (int)gridDim.x);
+      if (SESS)
+        printf("session flush (thread 0, per flush): %llu flushes, link %.0f, add %.0f, tail %.0f clocks\n",
+               g_sess[0], (double)g_sess[1] / (g_sess[0] + 1), (double)g_sess[2] / (g_sess[0] + 1),
+               (double)g_sess[3] / (g_sess[0] + 1));
+
       g_aggt[0] = g_aggt[1] = g_aggt[2] = g_aggt[3] = 0;
+      g_sess[0] = g_sess[1] = g_sess[2] = g_sess[3] = 0;
     }
   }
   if (!ok) {  // suspend: everything up to the last successful flush is in the region
@@ -1867,16 +2205,26 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
 }
 
 void launch_aggregate(const DevCfg& c, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
-                      AggProg prog, int resume, Status* st, hipStream_t s) {
+                      AggProg prog, int resume, const AggHot* hot, int64_t n, Status* st, hipStream_t s) {
+  AggHot h{};
+  unsigned grid = (unsigned)c.P;
+  if (hot) {  // at most n / FW_AGG_CHUNK chunks beyond one per partition
+    h = *hot;
+    grid += (unsigned)((n + FW_AGG_CHUNK - 1) / FW_AGG_CHUNK);
+    if (!resume) {
+      hipLaunchKernelGGL(k_chunk_plan, dim3((c.P + 1 + 255) / 256), dim3(256), 0, s, c, offs, T, h);
+      launch_scan(h.chunk_base, (int64_t)c.P + 1, h.scan_tmp, s);
+    }
+  }
   if (c.assigner == FW_SESSION)
-    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true>), dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb,
-                       prog, resume, st);
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb,
+                       prog, resume, st, h);
   else if (c.diag & DIAG_AGG_RPT8)
-    hipLaunchKernelGGL((k_aggregate<8, false>), dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb, prog,
-                       resume, st);
+    hipLaunchKernelGGL((k_aggregate<8, false>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb, prog,
+                       resume, st, h);
   else
-    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false>), dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb,
-                       prog, resume, st);
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T,
+                       tb, prog, resume, st, h);
 }
 
 void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* offs, int32_t T, const int64_t* sk, const int64_t* stt,

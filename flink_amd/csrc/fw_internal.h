@@ -34,6 +34,7 @@
 #define FW_SCATTER_WAVES 1
 #endif
 #define FW_AGG_THREADS 512     // aggregate workgroup
+#define FW_AGG_CHUNK 16384     // records per aggregate workgroup of a partition that is split (hot keys)
 #define FW_LDS_SLOTS 1024      // LDS pre-aggregation slots per aggregate workgroup
 #define FW_LDS_FILL_LIMIT 820  // ~0.8 * FW_LDS_SLOTS: a new slot is not claimed beyond this fill
 #define FW_FIRE_THREADS 256
@@ -131,6 +132,18 @@ struct AggProg {
   uint8_t* done;     // [P] partition finished in this push
 };
 
+// Partitions longer than FW_AGG_CHUNK records (hot keys) are split: one k_aggregate workgroup per
+// chunk pre-aggregates its records in LDS and writes the LDS entries as deltas (Entry form) at the
+// chunk's own record indices; the last chunk of the partition to finish merges all the deltas into
+// the region.  Tumbling windows and sessions only (one delta per record at most).
+struct AggHot {
+  Entry* delta;          // [max_batch]
+  uint32_t* chunk_base;  // [P + 1] exclusive scan of the chunks per partition; nullptr = no splitting
+  uint32_t* scan_tmp;
+  int32_t* nd;           // [chunks] deltas written by each chunk
+  uint32_t* pdone;       // [P] chunks of the partition finished
+};
+
 struct DevTable {
   Entry* ent[2];
   uint32_t* state[2];
@@ -162,8 +175,9 @@ void launch_scan(uint32_t* data, int64_t m, uint32_t* scratch, hipStream_t_ s); 
 void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
                     const int32_t* kh, int64_t n, int32_t T, uint32_t* offs, PRec* part, int64_t* sk,
                     int64_t* stt, int64_t* sv, int32_t* skh, DevSide side, Status* st, hipStream_t_ s);
+// hot: chunk splitting of long partitions (nullptr = one workgroup per partition); n = records of the push
 void launch_aggregate(const DevCfg& c, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
-                      AggProg prog, int resume, Status* st, hipStream_t_ s);
+                      AggProg prog, int resume, const AggHot* hot, int64_t n, Status* st, hipStream_t_ s);
 void launch_taint(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, int64_t n, Status* st,
                   hipStream_t_ s);
 void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* offs, int32_t T, const int64_t* sk,

@@ -38,6 +38,8 @@ struct Scratch {
   int64_t *sk = nullptr, *stt = nullptr, *sv = nullptr;  // ordered-path list
   int32_t* skh = nullptr;
   int32_t T = 0;                 // tiles of the batch that used this set
+  int64_t n = 0;                 // records of the batch
+  bool split = false;            // its aggregate split long partitions (fw_op::hot)
   int64_t wm = INT64_MIN;        // watermark the batch was classified against
 };
 
@@ -64,6 +66,7 @@ struct fw_op {
   int last_sc = 1;   // set of the most recent push
   AggProg prog{};    // k_aggregate resume points
   uint32_t taint_epoch = 0;  // sessions: epoch of the latest batch's taint set (DevCfg.taint_*)
+  AggHot hot{};              // split-partition buffers (allocated by the first batch that may need them)
 
   DevRows out{};
   DevSide side{};
@@ -175,6 +178,27 @@ void free_scratch(Scratch& s) {
   dfree(s.stt);
   dfree(s.sv);
   dfree(s.skh);
+}
+
+// buffers of the split-partition aggregate (AggHot): deltas at record indices, so one Entry per record
+// of the largest batch; one chunk count per partition and per FW_AGG_CHUNK records
+int ensure_hot(fw_op* op) {
+  if (op->hot.delta) return FW_OK;
+  const int64_t P = op->dc.P;
+  AggHot& h = op->hot;
+  HIP_OR_RETURN(op, dmalloc(&h.delta, (size_t)op->max_batch));
+  HIP_OR_RETURN(op, dmalloc(&h.chunk_base, (size_t)P + 1));
+  HIP_OR_RETURN(op, dmalloc(&h.scan_tmp, 64));
+  HIP_OR_RETURN(op, dmalloc(&h.nd, (size_t)(P + op->max_batch / FW_AGG_CHUNK + 1)));
+  HIP_OR_RETURN(op, dmalloc(&h.pdone, (size_t)P));
+  return FW_OK;
+}
+void free_hot(AggHot& h) {
+  dfree(h.delta);
+  dfree(h.chunk_base);
+  dfree(h.scan_tmp);
+  dfree(h.nd);
+  dfree(h.pdone);
 }
 
 // the ordered path may fill the fired-row buffer up to cap - table slots, so a watermark always has
@@ -361,7 +385,8 @@ int settle(fw_op* op) {
     const Scratch& S = op->sc[op->last_sc];
     if (susp & FW_SUSP_AGG)
       timed(op, K_AGGREGATE, [&] {
-        fwdev::launch_aggregate(c, S.wm, S.part, S.hist, S.T, op->tb, op->prog, 1, op->d_status, op->stream);
+        fwdev::launch_aggregate(c, S.wm, S.part, S.hist, S.T, op->tb, op->prog, 1, S.split ? &op->hot : nullptr, S.n,
+                                op->d_status, op->stream);
       });
     // after an aggregate suspension the ordered path never started; otherwise it resumes
     timed(op, K_SLOW, [&] {
@@ -469,8 +494,12 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   const int64_t chunk_rows = (int64_t)FW_SLOW_THREADS * (c.assigner == FW_SESSION ? 1 : c.wpr);
   if ((rc = ensure_out_capacity(op, rows + op->table_slots + chunk_rows, rows))) return rc;
   const DevCfg& cc = op->dc;  // settle may have grown the table
+  // a partition can outgrow one aggregate workgroup (hot keys) only when the batch is longer than a chunk
+  const bool split = cc.wpr == 1 && n > FW_AGG_CHUNK;
+  if (split && (rc = ensure_hot(op))) return rc;
   timed(op, K_AGGREGATE, [&] {
-    fwdev::launch_aggregate(cc, op->wm, S.part, S.hist, T, op->tb, op->prog, 0, op->d_status, op->stream);
+    fwdev::launch_aggregate(cc, op->wm, S.part, S.hist, T, op->tb, op->prog, 0, split ? &op->hot : nullptr, n,
+                            op->d_status, op->stream);
   });
   timed(op, K_SLOW, [&] {
     fwdev::launch_slow(cc, op->wm, S.hist, T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status, 0,
@@ -478,6 +507,8 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   });
   HIP_OR_RETURN(op, hipGetLastError());
   S.T = T;
+  S.n = n;
+  S.split = split;
   S.wm = op->wm;
   op->last_sc = nxt;
   op->records_in += n;
@@ -626,6 +657,7 @@ void fw_destroy(fw_op* op) {
   dfree(op->prog.done);
   dfree(op->dc.taint_key);
   dfree(op->dc.taint_state);
+  free_hot(op->hot);
   for (int64_t** col : {&op->out.key, &op->out.start, &op->out.end, &op->out.cnt, &op->out.sum, &op->out.mn,
                         &op->out.mx, &op->side.key, &op->side.ts, &op->side.val})
     dfree(*col);

@@ -144,6 +144,20 @@ def test_gpu_table_growth(cfg):
     assert_rows_equal(g, r)
 
 
+@pytest.mark.parametrize("small_table", [False, True], ids=["table", "tiny-table"])
+@pytest.mark.parametrize("cfg", [dict(assigner="tumbling", size=100), dict(assigner="session", gap=20),
+                                 dict(assigner="tumbling", size=100, value_type="f64")],
+                         ids=["tumbling", "session", "tumbling-f64"])
+def test_gpu_hot_keys_split_partitions(cfg, small_table):
+    # Zipf(1.3) over 100K keys: the hottest key is ~20% of a 2^20-record batch, so its state partition
+    # is split into chunks that separate workgroups pre-aggregate and the last one merges (AggHot);
+    # with a tiny table that merge runs out of region room, suspends and resumes after the growth
+    vt = cfg.get("value_type", "i64")
+    batches, wms = _stream(1 << 21, 1 << 20, 100_000, bound=50, jitter=50, rate=1_000_000, zipf=1.3, value_type=vt)
+    g, r, *_ = _run_both(cfg, batches, wms, **(dict(expected_entries=1000) if small_table else {}))
+    assert_rows_equal(g, r, _VT[vt])
+
+
 def test_gpu_session_merges_across_flushes():
     # one state partition per key group and ~1500 keys per partition: the LDS table flushes several
     # times per batch, so a key's session is built from LDS intervals of different flushes that the

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # GPU parity tests, then the C2 bench and a short C4 (sessions) bench.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread \
     > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/gpu_tests.log
 [ $rc -eq 0 ] || exit $rc
