@@ -12,8 +12,10 @@ KeyGroupRange computeKeyGroupRangeForOperatorIndex(128, N, rank), generates `--b
 global stream per step and the keyBy exchange (route + RCCL all_to_all) and the watermark min
 (all_reduce) run inside the timed region: weak scaling.
 
---workload c4 runs SURVEY §8d C4 instead (EventTimeSessionWindows gap 30 s, 1M Zipf(1.1) keys, 1e5
-records per event-second, bound 1 s); the default line is C2.
+--workload c3 runs SURVEY §8d C3 (SlidingEventTimeWindows 60 s / 1 s, 60 windows per record, 2M uniform
+keys per GPU = 16M at 8 GPUs, 1e8 records per event-second per GPU, bound 200 ms); --workload c4 runs C4
+(EventTimeSessionWindows gap 30 s, 1M Zipf(1.1) keys, 1e5 records per event-second, bound 1 s).  The
+default line is C2.
 
 Prints ONE JSON line on rank 0.
 """
@@ -34,6 +36,9 @@ PRESETS = {
     "c2": dict(rate=100_000_000, bound=200, jitter=200, zipf=None, keys=1_000_000, cpu_sample=1 << 24,
                workload="C2 tumbling 1s event-time window, count/sum/min/max, 1M uniform Long keys, "
                         "bounded out-of-orderness 200 ms"),
+    "c3": dict(rate=100_000_000, bound=200, jitter=200, zipf=None, keys=2_000_000, cpu_sample=1 << 19,
+               workload="C3 sliding 60s/1s event-time windows (60x fan-out), count/sum/min/max, 2M uniform Long keys "
+                        "per GPU (16M at 8 GPUs), bounded out-of-orderness 200 ms"),
     "c4": dict(rate=100_000, bound=1000, jitter=1000, zipf=1.1, keys=1_000_000, cpu_sample=1 << 22,
                workload="C4 EventTimeSessionWindows gap 30 s, count/sum/min/max, 1M Zipf(1.1) Long keys, "
                         "bounded out-of-orderness 1 s"),
@@ -64,6 +69,8 @@ def main():
     ap.add_argument("--jitter", type=int, default=None)
     ap.add_argument("--window", type=int, default=1000, help="tumbling window (ms, c2)")
     ap.add_argument("--gap", type=int, default=30_000, help="session gap (ms, c4)")
+    ap.add_argument("--size", type=int, default=60_000, help="sliding window size (ms, c3)")
+    ap.add_argument("--slide", type=int, default=1000, help="sliding window slide (ms, c3)")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--zipf", type=float, default=None, help="Zipf exponent of the keys (0 = uniform)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -80,6 +87,7 @@ def main():
         args.zipf = preset["zipf"]
     args.zipf = args.zipf or None
     sessions = args.workload == "c4"
+    sliding = args.workload == "c3"
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -91,7 +99,7 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    from flink_amd import EventTimeSessionWindows, TumblingEventTimeWindows
+    from flink_amd import EventTimeSessionWindows, SlidingEventTimeWindows, TumblingEventTimeWindows
     from flink_amd import _native as N
     from flink_amd.datagen import generate_device, zipf_cdf
     from flink_amd.exchange import KeyGroupExchange
@@ -99,11 +107,21 @@ def main():
 
     max_par = 128
     exch = KeyGroupExchange(max_par, world, rank)
-    assigner = EventTimeSessionWindows.with_gap(args.gap) if sessions else TumblingEventTimeWindows.of(args.window)
+    if sliding:
+        # weak scaling: the key space and the event rate grow with the GPU count (16M keys at 8 GPUs)
+        args.keys *= world
+        args.rate *= world
+    if sessions:
+        assigner = EventTimeSessionWindows.with_gap(args.gap)
+    elif sliding:
+        assigner = SlidingEventTimeWindows.of(args.size, args.slide)
+    else:
+        assigner = TumblingEventTimeWindows.of(args.window)
+    live_windows = (args.size // args.slide + 1) if sliding else 2
     cdf = torch.from_numpy(zipf_cdf(args.keys, args.zipf)).to(dev) if args.zipf else None
     op = GpuWindowOperator(assigner, key_group_range=exch.key_group_range,
                            device=local_rank, max_parallelism=max_par,
-                           expected_entries=2 * args.keys // world,
+                           expected_entries=live_windows * args.keys // world,
                            max_batch=args.batch if world == 1 else 2 * args.batch,
                            sub_partitions=args.sub_partitions)
     steps_total = args.warmup + args.steps
@@ -190,8 +208,13 @@ def main():
             roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                         "traffic": traffic, "alg_bytes_per_launch": int(b)}
-    # whole-path roofline with SURVEY §8d's B_alg: C2 24 + 104 F/N, C4 24 + 112 F/N bytes per record
-    b_alg = 24 + (112 if sessions else 104) * fired / max(1, records / world)
+    # whole-path roofline with SURVEY §8d's B_alg: C2 24 + 104 F/N, C4 24 + 112 F/N bytes per record;
+    # C3 (pane model) 24 + 96 + (60*48 + 56) F/N, plus the exchange 2*24*(G-1)/G
+    fpr = fired / max(1, records / world)
+    if sliding:
+        b_alg = 24 + 96 + (args.size // args.slide * 48 + 56) * fpr + 48 * (world - 1) / world
+    else:
+        b_alg = 24 + (112 if sessions else 104) * fpr
     path_frac = value * b_alg / (world * HBM_PEAK_GBS * 1e9)
 
     cpu = None
@@ -206,7 +229,8 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic (splitmix64 counter stream)",
             "config": {"workload": preset["workload"],
                        "records_per_step_per_gpu": args.batch, "keys": args.keys,
-                       **({"gap_ms": args.gap, "zipf_s": args.zipf} if sessions else {"window_ms": args.window}),
+                       **({"gap_ms": args.gap, "zipf_s": args.zipf} if sessions else
+                          {"size_ms": args.size, "slide_ms": args.slide} if sliding else {"window_ms": args.window}),
                        "records_per_event_second": args.rate, "watermark_bound_ms": args.bound,
                        "max_parallelism": 128, "parallelism": f"keygroup{world}"},
             "roofline": roofline,
@@ -237,7 +261,12 @@ def cpu_baseline(args):
         m = max(m, int(t[b:b + batch].max()))
         wms.append(m - args.bound)
     t0 = time.perf_counter()
-    cfg = dict(assigner="session", gap=args.gap) if args.workload == "c4" else dict(assigner="tumbling", size=args.window)
+    if args.workload == "c4":
+        cfg = dict(assigner="session", gap=args.gap)
+    elif args.workload == "c3":
+        cfg = dict(assigner="sliding", size=args.size, slide=args.slide)
+    else:
+        cfg = dict(assigner="tumbling", size=args.window)
     orc.run_parallel(cfg, k, t, v, batch, np.array(wms), 128, threads)
     dt = time.perf_counter() - t0
     return {"value": round(n / dt, 1), "unit": "records/s", "cores": threads, "kind": "port",
