@@ -20,6 +20,7 @@ FW_ERR_STATE = -7
 FW_TUMBLING, FW_SLIDING, FW_SESSION = 0, 1, 2
 FW_VAL_I64, FW_VAL_I32, FW_VAL_F64 = 0, 1, 2
 FW_KEY_LONG, FW_KEY_INT, FW_KEY_HASHED = 0, 1, 2
+FW_AGG_COUNT_SUM_MIN_MAX, FW_AGG_HLL = 0, 1
 FW_NUM_KERNELS = 6
 
 I64P = ctypes.POINTER(ctypes.c_int64)
@@ -33,7 +34,8 @@ class FwConfig(ctypes.Structure):
                 ("key_group_start", ctypes.c_int32), ("key_group_end", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("sub_partitions", ctypes.c_int32), ("size", ctypes.c_int64), ("slide", ctypes.c_int64),
                 ("offset", ctypes.c_int64), ("gap", ctypes.c_int64), ("allowed_lateness", ctypes.c_int64),
-                ("expected_entries", ctypes.c_int64), ("max_batch", ctypes.c_int64)]
+                ("expected_entries", ctypes.c_int64), ("max_batch", ctypes.c_int64),
+                ("aggregate", ctypes.c_int32), ("hll_precision", ctypes.c_int32)]
 
 
 class FwRows(ctypes.Structure):

@@ -110,6 +110,29 @@ __device__ __forceinline__ int64_t cleanup_of(int64_t end, int64_t lateness) {
 __device__ __forceinline__ int64_t timer_of(const Entry& e, int64_t lateness) {
   return (e.meta & FW_TIMER) ? jsub(e.end, 1) : cleanup_of(e.end, lateness);
 }
+// end of the state entry that starts at `start`: the window's, or the pane's when sliding windows are
+// kept as panes (DevCfg::panes)
+__device__ __forceinline__ int64_t wend(const DevCfg& c, int64_t start) {
+  return jadd(start, c.panes ? c.slide : c.size);
+}
+// ---- HyperLogLog (FW_AGG_HLL; the definition is restated in oracle/window_oracle.h)
+// a zeroed register block for a new (key, window) entry: the free stack first, then the pool's tail
+__device__ __forceinline__ int64_t hll_alloc(const DevCfg& c, Status* st) {
+  const int32_t t = atomicSub(&c.hll_ctr[0], 1) - 1;
+  if (t >= 0) return (int64_t)c.hll_free[t];
+  atomicAdd(&c.hll_ctr[0], 1);  // nothing is pushed while the aggregate runs (k_fire pushes)
+  const int32_t b = atomicAdd(&c.hll_ctr[1], 1);
+  if ((int64_t)b >= c.hll_blocks) {
+    atomicOr(&st->flags, FW_STATUS_HLL_POOL);
+    return 0;
+  }
+  return b;
+}
+__device__ __forceinline__ uint64_t hll_block_of(const Entry& e) { return (uint64_t)e.meta >> 1; }
+// earliest pending timer of an entry; a pane's is its meta (the next window end it belongs to)
+__device__ __forceinline__ int64_t entry_timer(const DevCfg& c, const Entry& e) {
+  return c.panes ? e.meta : timer_of(e, c.lateness);
+}
 
 // Double.compare order as a signed 64-bit key (canonical NaN, Double.doubleToLongBits)
 __device__ __forceinline__ int64_t f64_sortable(int64_t bits) {
@@ -170,6 +193,18 @@ __device__ __forceinline__ int classify(const DevCfg& c, int64_t wm, int64_t ts,
     return CLS_NORMAL;
   }
   if (ts == LMIN) return CLS_BADTS;  // TumblingEventTimeWindows.java:69-71
+  if (c.panes) {
+    // allowedLateness 0: a window whose maxTimestamp <= wm has fired (or had no contents) and is never
+    // evaluated again, so adding the element to its pane adds it to exactly the windows that are not
+    // late (WindowOperator.java:379-407); only when the newest window is late is the element dropped
+    const int64_t last = wstart(ts, c.offset, c.slide, c.mag_slide, c.l_slide);
+    if (last_out) {
+      *last_out = last;
+      *k_out = 1;
+    }
+    if (cleanup_of(jadd(last, c.size), 0) > wm) return CLS_NORMAL;
+    return ts <= wm ? CLS_LATE : CLS_SKIP;
+  }
   int64_t last;
   int k = num_windows(c, ts, &last);
   if (last_out) {
@@ -772,12 +807,13 @@ __device__ __forceinline__ Entry lds_delta(const DevCfg& c, const AggLds& L, int
   Entry d;
   d.key = kv.x;
   d.start = kv.y;
-  d.end = jadd(kv.y, c.size);
+  d.end = wend(c, kv.y);
   d.cnt = (int64_t)L.cnt[h];
   d.sum = L.sum[h];
   d.mn = L.mn[h];
   d.mx = L.mx[h];
-  d.meta = FW_TIMER;
+  // a new pane belongs to the windows that end after the watermark, from its first window on
+  d.meta = c.panes ? max(jsub(d.end, 1), c.nt_floor) : (int64_t)FW_TIMER;  // (+ HLL block: agg_flush)
   return d;
 }
 
@@ -800,7 +836,7 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
     if (L.tag[h] < 2) continue;
     const i64x2 kv = L.kv[h];
-    const int32_t slot = region_find(r, slot_hash(c, kv.x, kv.y), kv.x, kv.y, jadd(kv.y, c.size));
+    const int32_t slot = region_find(r, slot_hash(c, kv.x, kv.y), kv.x, kv.y, wend(c, kv.y));
     L.slot[h] = slot;
     nnew += slot < 0;
   }
@@ -818,21 +854,27 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
     if (L.tag[h] < 2) continue;
     const Entry d = lds_delta(c, L, h);
     nflush++;
-    mt = min(mt, jsub(d.end, 1));
+    mt = min(mt, c.panes ? d.meta : jsub(d.end, 1));
     const int32_t slot = L.slot[h];
     if (slot >= 0) {
       Entry& x = r.ent[slot];
       Entry cur = x;
       acc_merge(c, cur, d);
-      cur.meta |= FW_TIMER;
+      if (c.panes)
+        cur.meta = min(cur.meta, d.meta);
+      else
+        cur.meta |= FW_TIMER;
       x = cur;
     } else {
       const uint64_t hs = slot_hash(c, d.key, d.start);
       const int32_t ns = region_claim(r, hs, live_word(hs));
-      if (ns >= 0)
-        r.ent[ns] = d;
-      else
+      if (ns >= 0) {
+        Entry n = d;
+        if (c.agg == FW_AGG_HLL) n.meta |= hll_alloc(c, st) << 1;
+        r.ent[ns] = n;
+      } else {
         lost++;  // cannot happen below the load limit
+      }
     }
   }
   if (lost) atomicOr(&st->flags, FW_STATUS_STATE_LOST);
@@ -1812,6 +1854,113 @@ __global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, 
 // ---- K_fire: watermark.  Regions with next_timer <= wm emit and are rebuilt into the other buffer.
 // Pass 1 decides every slot, re-inserts the survivors into the other buffer and counts the fired
 // rows; one reservation per workgroup in the output; pass 2 re-decides and writes the rows.
+// one wave per fired row: estimate from the row's register block (out.mn holds its id), then zero the
+// block and push it on the free stack.  S = sum_j 2^(65-p-M[j]) exactly: per lane in 64 bits (at most
+// m/64 terms of at most 2^(65-p)), across the wave in 128 bits.
+__device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row) {
+  const int lane = __lane_id();
+  const int p = c.hll_p, rmax = 65 - p;
+  const int64_t m = (int64_t)1 << p;
+  const uint64_t blk = (uint64_t)out.mn[row];
+  uint8_t* regs = c.hll_regs + blk * (uint64_t)m;
+  uint64_t s = 0;
+  uint32_t zeros = 0;
+  uint4* q = reinterpret_cast<uint4*>(regs);
+  const int64_t nq = m / 16;  // 16-byte chunks, four in flight per lane
+  for (int64_t j0 = lane; j0 < nq; j0 += 256) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = j0 + u * 64 < nq ? q[j0 + u * 64] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (j0 + u * 64 >= nq) continue;
+      const uint32_t ws[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const uint32_t r = (ws[k] >> (8 * b)) & 0xffu;
+          s += 1ull << (rmax - (int)r);
+          zeros += r == 0;
+        }
+      q[j0 + u * 64] = make_uint4(0, 0, 0, 0);
+    }
+  }
+  uint64_t hi = 0, lo = s;
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t lo2 = __shfl_xor(lo, o, 64), hi2 = __shfl_xor(hi, o, 64);
+    const uint64_t t = lo + lo2;
+    hi = hi + hi2 + (t < lo ? 1ull : 0ull);
+    lo = t;
+    zeros += __shfl_xor(zeros, o, 64);
+  }
+  if (lane == 0) {
+    const double sd = (double)hi * 18446744073709551616.0 + (double)lo;
+    const double md = (double)m;
+    const double alpha = m == 16 ? 0.673 : m == 32 ? 0.697 : m == 64 ? 0.709 : 0.7213 / (1.0 + 1.079 / md);
+    const double raw = (alpha * md * md) * ldexp(1.0, rmax) / sd;
+    const double est = (raw <= 2.5 * md && zeros > 0) ? md * log(md / (double)zeros) : raw;
+    out.sum[row] = __double_as_longlong(est);
+    out.mn[row] = (int64_t)zeros;
+    out.mx[row] = (int64_t)lo;
+    __threadfence();  // the zeroed block is visible before it can be handed out again
+    c.hll_free[atomicAdd(&c.hll_ctr[0], 1)] = (uint32_t)blk;
+  }
+}
+
+// fold each partitioned record's item into the registers of its (key, window): M[j] = max(M[j], rank).
+// One workgroup per FW_HLL_CHUNK records; a record's partition is found from the scan offsets.  Byte
+// registers are raised with a CAS on their 32-bit word, only when the rank is larger (max is idempotent,
+// so a resumed push may run this again over the whole batch).
+constexpr int FW_HLL_CHUNK = 4096;
+__global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __restrict__ part,
+                                                    const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
+                                                    Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int64_t total = offs[(int64_t)c.P * T];
+  const int64_t i0 = (int64_t)blockIdx.x * FW_HLL_CHUNK;
+  if (i0 >= total) return;
+  __shared__ int32_t p0_s;
+  if (threadIdx.x == 0) {  // partition of the chunk's first record: last p with offs[p*T] <= i0
+    int32_t lo = 0, hi = c.P - 1;
+    while (lo < hi) {
+      const int32_t mid = (lo + hi + 1) >> 1;
+      if ((int64_t)offs[(int64_t)mid * T] <= i0)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    p0_s = lo;
+  }
+  __syncthreads();
+  const int p = c.hll_p;
+  const int64_t i1 = min(total, i0 + (int64_t)FW_HLL_CHUNK);
+  int32_t pp = p0_s;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
+    const PRec rec = part[i];
+    const Region r = region_of(c, tb, pp, tb.cur[pp]);
+    const int32_t slot = region_find(r, slot_hash(c, rec.key, rec.last), rec.key, rec.last, wend(c, rec.last));
+    if (slot < 0) {
+      atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's window
+      continue;
+    }
+    const uint64_t blk = hll_block_of(r.ent[slot]);
+    const uint64_t h = fmix64((uint64_t)rec.val);
+    const uint64_t j = h >> (64 - p);
+    const uint32_t rank = (uint32_t)__clzll((long long)((h << p) | (1ull << (p - 1)))) + 1u;
+    uint32_t* w = reinterpret_cast<uint32_t*>(c.hll_regs + blk * ((uint64_t)1 << p) + (j & ~3ull));
+    const int sh = (int)(j & 3) * 8;
+    uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (((old >> sh) & 0xffu) < rank) {
+      const uint32_t nw = (old & ~(0xffu << sh)) | (rank << sh);
+      if (__hip_atomic_compare_exchange_strong(w, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT))
+        break;
+    }
+  }
+}
+
 struct FireDecision {
   bool fire, keep;
 };
@@ -1858,6 +2007,13 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, 
     Entry e = rx.ent[s], fe;
     const FireDecision d = fire_decide(c, wm, e, fe);
     nfire += d.fire;
+    if (!d.keep && !d.fire && c.agg == FW_AGG_HLL) {  // GC without a row: zero and free its block here
+      const uint64_t blk = hll_block_of(e);
+      uint32_t* w = reinterpret_cast<uint32_t*>(c.hll_regs + (blk << c.hll_p));
+      for (int64_t j = 0; j < ((int64_t)1 << c.hll_p) / 4; j++) w[j] = 0u;
+      __threadfence();
+      c.hll_free[atomicAdd(&c.hll_ctr[0], 1)] = (uint32_t)blk;
+    }
     if (!d.keep) continue;
     const uint64_t h = slot_hash(c, e.key, e.start);
     const int32_t dst = region_claim(ry, h, live_word(h));
@@ -1881,18 +2037,250 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, 
       if (st_kind(ld_state(rx.state + s)) != SLOT_LIVE) continue;
       Entry e = rx.ent[s], fe;
       if (!fire_decide(c, wm, e, fe).fire) continue;
-      if ((int64_t)pos < out.cap)
+      if ((int64_t)pos < out.cap) {
         write_row(c, out, pos, fe);
-      else
+        if (c.agg == FW_AGG_HLL) out.mn[pos] = (int64_t)hll_block_of(fe);  // read back by hll_finish
+      } else {
         atomicOr(&st->flags, FW_STATUS_OUT_FULL);
+      }
       pos++;
     }
+  }
+  if (c.agg == FW_AGG_HLL && total) {
+    __threadfence_block();
+    __syncthreads();
+    const uint64_t end = min((unsigned long long)out.cap, base_s + total);
+    for (uint64_t r = base_s + (threadIdx.x >> 6); r < end; r += blockDim.x >> 6) hll_finish(c, out, r);
   }
   if (threadIdx.x == 0) {
     if (total) atomicAdd(&st->fired_total, (unsigned long long)total);
     tb.cur[p] = (uint8_t)Y;
     tb.live[p] = live_s;
     tb.next_timer[p] = next_s;
+  }
+}
+
+// ---- K_fire for sliding windows kept as panes (DevCfg::panes).  A window [s, s + size) of a key is
+// the AggregateFunction.merge of the key's panes p in [s, s + size - slide]; its contents are non-null
+// (WindowOperator.java:452-459) iff one of those panes exists.  A pane's pending windows are those
+// whose maxTimestamp E lies in [max(meta, pane_floor), p + size - 1]: meta excludes the windows that
+// were already late when the pane was created, pane_floor the ones formed by earlier watermarks.
+// For each pending E <= wm in increasing order (EventTimeTrigger fires in timer order; the operator's
+// output order per watermark is not part of the contract, TestHarnessUtil.java:70-108), the region's
+// panes of E are merged per key in an LDS table and emitted as rows; when a region holds more keys
+// than the table, E is formed in slices of the key-hash space.  Panes whose last window has been
+// formed are dead (GC timer at maxTimestamp, allowedLateness 0): they are tombstoned in place and the
+// region is compacted into the other buffer once tombstones pass R/8.  A slice whose rows do not fit
+// the output suspends the launch at (E, slice); the host grows the buffer and fires again.
+constexpr int PF_THREADS = 1024;
+constexpr int PF_SLOTS = 2048;
+constexpr int PF_LIMIT = 1536;
+struct PaneLds {
+  uint32_t tag[PF_SLOTS];  // 0 empty, 1 being claimed, 2 full
+  int64_t key[PF_SLOTS];
+  unsigned long long cnt[PF_SLOTS];
+  int64_t sum[PF_SLOTS], mn[PF_SLOTS], mx[PF_SLOTS];
+  int fill, over, wpos, dead, susp;
+  long long enext, ntmin;
+  unsigned long long base;
+};
+__device__ __forceinline__ uint32_t pf_hash(int64_t key) { return (uint32_t)(fmix64((uint64_t)key ^ 0x243F6A8885A308D3ull) >> 32); }
+
+__device__ __forceinline__ bool pf_upsert(const DevCfg& c, PaneLds& L, const Entry& e, uint32_t h) {
+  uint32_t s = (h * 0x9E3779B1u) >> (32 - 11);  // PF_SLOTS = 2^11
+  for (int i = 0, spin = 0; i < PF_SLOTS;) {
+    if (++spin > (1 << 24)) return false;  // a slot never published: cannot happen; the pass reports overflow
+    const uint32_t t = __hip_atomic_load(&L.tag[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (t == 2) {
+      if (L.key[s] == e.key) break;
+      s = (s + 1) & (PF_SLOTS - 1);
+      i++;
+      continue;
+    }
+    if (t == 1) continue;  // being published by a lane of this loop iteration
+    if (__hip_atomic_load(&L.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= PF_LIMIT) return false;
+    if (atomicAdd(&L.fill, 1) >= PF_LIMIT) {
+      atomicSub(&L.fill, 1);
+      return false;
+    }
+    if (atomicCAS(&L.tag[s], 0u, 1u) == 0u) {
+      L.key[s] = e.key;
+      L.cnt[s] = 0;
+      L.sum[s] = 0;
+      L.mn[s] = LMAX;
+      L.mx[s] = LMIN;
+      __hip_atomic_store(&L.tag[s], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      break;
+    }
+    atomicSub(&L.fill, 1);  // lost the claim: re-read the slot
+  }
+  atomicAdd(&L.cnt[s], (unsigned long long)e.cnt);
+  if (c.vtype == FW_VAL_F64)
+    atomicAdd((double*)&L.sum[s], __longlong_as_double(e.sum));
+  else
+    atomicAdd((unsigned long long*)&L.sum[s], (unsigned long long)e.sum);
+  atomicMin((long long*)&L.mn[s], (long long)e.mn);
+  atomicMax((long long*)&L.mx[s], (long long)e.mx);
+  return true;
+}
+
+__global__ __launch_bounds__(PF_THREADS) void k_fire_panes(DevCfg c, int64_t wm, DevTable tb, DevRows out, Status* st) {
+  const int32_t p = blockIdx.x;
+  // LMAX = no pending window (also when wm is Long.MAX_VALUE, the end-of-input watermark)
+  if (tb.next_timer[p] > wm || tb.next_timer[p] == LMAX ||
+      __hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    return;
+  __shared__ PaneLds L;
+  const int tid = threadIdx.x;
+  const int X = tb.cur[p];
+  const Region rx = region_of(c, tb, p, X);
+  const uint32_t R = rx.mask + 1;
+  const int64_t floor0 = tb.pane_floor[p];
+  const bool resumed = tb.fire_e[p] != LMIN;
+  int64_t E = resumed ? tb.fire_e[p] : tb.next_timer[p];
+  uint64_t lo = resumed ? tb.fire_lo[p] : 0ull;
+  uint64_t width = 1ull << 32;
+  int64_t ntmin = LMAX;
+  int dead = 0;
+  for (;;) {
+    for (int h = tid; h < PF_SLOTS; h += PF_THREADS) L.tag[h] = 0;
+    if (tid == 0) {
+      L.fill = 0;
+      L.over = 0;
+      L.wpos = 0;
+      L.dead = 0;
+      L.enext = LMAX;
+      L.ntmin = LMAX;
+    }
+    __syncthreads();
+    // otherwise: a last pass that only gathers tombstones and the next timer
+    const bool forming = E <= wm && E != LMAX;
+    int64_t en = LMAX, nt = LMAX;
+    int dd = 0;
+    bool over = false;
+    for (uint32_t s = tid; s < R; s += PF_THREADS) {
+      const uint32_t w = ld_state(rx.state + s);
+      if (st_kind(w) != SLOT_LIVE) {
+        dd += st_kind(w) == SLOT_DEAD;
+        continue;
+      }
+      const Entry e = rx.ent[s];
+      const int64_t last_end = jsub(jadd(e.start, c.size), 1);  // maxTimestamp of the pane's last window
+      const int64_t lo_e = max(e.meta, floor0);
+      if (lo_e > last_end) {  // every window formed by an earlier watermark: GC
+        __hip_atomic_store(rx.state + s, (uint32_t)SLOT_DEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dd++;
+        continue;
+      }
+      const int64_t hi_e = min(wm, last_end);
+      if (last_end > wm) nt = min(nt, max(lo_e, c.nt_floor));  // survives this watermark
+      if (!forming) continue;
+      if (lo_e <= E && E <= hi_e) {
+        const uint32_t h = pf_hash(e.key);
+        if (!over && (uint64_t)h >= lo && (uint64_t)h < lo + width && !pf_upsert(c, L, e, h)) over = true;
+      }
+      const int64_t cand = max(lo_e, E + c.slide);
+      if (E < LMAX - c.slide && cand <= hi_e) en = min(en, cand);
+    }
+    if (over) L.over = 1;
+    if (en != LMAX) atomicMin(&L.enext, (long long)en);
+    if (nt != LMAX) atomicMin(&L.ntmin, (long long)nt);
+    if (dd) atomicAdd(&L.dead, dd);
+    __syncthreads();
+    dead = L.dead;
+    ntmin = L.ntmin;
+    const int ov = L.over;
+    const uint32_t n = (uint32_t)L.fill;
+    const int64_t enext = L.enext;
+    __syncthreads();  // every thread has read the pass's results before thread 0 writes L again
+    if (!forming) break;
+    if (ov) {
+      if (width == 1) {  // cannot happen: one hash value never holds PF_LIMIT keys of one region
+        if (tid == 0) atomicOr(&st->flags, FW_STATUS_STATE_LOST);
+        return;
+      }
+      width >>= 1;
+      continue;
+    }
+    if (tid == 0) {
+      bool ok = true;
+      unsigned long long cur = __hip_atomic_load(&st->out_rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (n) {
+        if ((int64_t)(cur + n) > out.cap) {
+          ok = false;
+          break;
+        }
+        if (__hip_atomic_compare_exchange_strong(&st->out_rows, &cur, cur + n, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+          break;
+      }
+      L.base = cur;
+      if (!ok) {  // suspend at (E, lo): the host grows the output and fires again
+        tb.fire_e[p] = E;
+        tb.fire_lo[p] = lo;
+        atomicMax((long long*)&st->need_out, (long long)(cur + n));
+        atomicOr(&st->suspended, (int)FW_SUSP_FIRE);
+      }
+      L.susp = ok ? 0 : 1;
+    }
+    __syncthreads();
+    if (L.susp) return;
+    if (n) {
+      const int64_t ws = jsub(jadd(E, 1), c.size);
+      for (int h = tid; h < PF_SLOTS; h += PF_THREADS) {
+        if (L.tag[h] != 2) continue;
+        Entry r;
+        r.key = L.key[h];
+        r.start = ws;
+        r.end = jadd(E, 1);
+        r.cnt = (int64_t)L.cnt[h];
+        r.sum = L.sum[h];
+        r.mn = L.mn[h];
+        r.mx = L.mx[h];
+        write_row(c, out, L.base + (unsigned long long)atomicAdd(&L.wpos, 1), r);
+      }
+      if (tid == 0) atomicAdd(&st->fired_total, (unsigned long long)n);
+    }
+    __syncthreads();  // the rows are read out of L before the next pass clears it
+    lo += width;
+    if (lo >= (1ull << 32)) {
+      lo = 0;
+      width = 1ull << 32;
+      E = enext;
+      if (E > wm || E == LMAX) break;  // this pass saw every slot: its tombstone count and next timer are final
+    }
+  }
+  // every pending window <= wm is formed
+  if (dead * 8 > (int)R) {  // compact: re-insert the live panes into the other buffer
+    const Region ry = region_of(c, tb, p, X ^ 1);
+    for (uint32_t s = tid; s < R; s += PF_THREADS) ry.state[s] = SLOT_EMPTY;
+    __syncthreads();
+    int live = 0;
+    for (uint32_t s = tid; s < R; s += PF_THREADS) {
+      if (st_kind(ld_state(rx.state + s)) != SLOT_LIVE) continue;
+      const Entry e = rx.ent[s];
+      const uint64_t h = slot_hash(c, e.key, e.start);
+      const int32_t d = region_claim(ry, h, live_word(h));
+      if (d >= 0) {
+        ry.ent[d] = e;
+        live++;
+      } else {
+        atomicOr(&st->flags, FW_STATUS_STATE_LOST);
+      }
+    }
+    if (tid == 0) L.wpos = 0;
+    __syncthreads();
+    if (live) atomicAdd(&L.wpos, live);
+    __syncthreads();
+    if (tid == 0) {
+      tb.cur[p] = (uint8_t)(X ^ 1);
+      tb.live[p] = L.wpos;
+    }
+  }
+  if (tid == 0) {
+    tb.pane_floor[p] = max(floor0, c.nt_floor);
+    tb.next_timer[p] = ntmin;
+    tb.fire_e[p] = LMIN;
   }
 }
 
@@ -1933,6 +2321,9 @@ __global__ void k_reset_regions(DevCfg c, DevTable tb) {
   tb.cur[p] = 0;
   tb.live[p] = 0;
   tb.next_timer[p] = LMAX;
+  tb.fire_e[p] = LMIN;
+  tb.fire_lo[p] = 0;
+  tb.pane_floor[p] = LMIN;
 }
 
 // ---- keyed-state snapshot of one key group (HeapKeyedStateBackend.snapshot writes per key group,
@@ -1948,7 +2339,9 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_snapshot(DevCfg c, DevTable
   // one pass per block of the region: count, reserve, write
   for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x) {
     const uint32_t s = s0 + threadIdx.x;
-    const bool live = s < R && st_kind(ld_state(r.state + s)) == SLOT_LIVE;
+    bool live = s < R && st_kind(ld_state(r.state + s)) == SLOT_LIVE;
+    if (live && c.panes && max(r.ent[s].meta, tb.pane_floor[p]) > jsub(jadd(r.ent[s].start, c.size), 1))
+      live = false;  // a pane whose windows have all been formed (GC'd at the next watermark)
     uint32_t total;
     const uint32_t pos = block_excl_scan(live ? 1u : 0u, sw, &total);
     if (threadIdx.x == 0) base_s = total ? atomicAdd(count, (unsigned long long)total) : 0ull;
@@ -1969,7 +2362,8 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_snapshot(DevCfg c, DevTable
         out.mn[o] = e.mn;
         out.mx[o] = e.mx;
       }
-      out.timer[o] = (e.meta & FW_TIMER) ? 1 : 0;
+      // a pane's timer: the maxTimestamp of its next window to form
+      out.timer[o] = c.panes ? max(e.meta, tb.pane_floor[p]) : (e.meta & FW_TIMER) ? 1 : 0;
     }
     __syncthreads();
   }
@@ -2008,7 +2402,7 @@ __global__ void k_restore(DevCfg c, int32_t kg, StateCols in, int64_t n, DevTabl
   d.sum = in.sum[i];
   d.mn = c.vtype == FW_VAL_F64 ? f64_sortable(in.mn[i]) : in.mn[i];
   d.mx = c.vtype == FW_VAL_F64 ? f64_sortable(in.mx[i]) : in.mx[i];
-  d.meta = in.timer[i] ? FW_TIMER : 0;
+  d.meta = c.panes ? in.timer[i] : in.timer[i] ? FW_TIMER : 0;
   const Region r = region_of(c, tb, p, tb.cur[p]);
   const uint64_t h = slot_hash(c, d.key, c.assigner == FW_SESSION ? 0 : d.start);
   const int32_t found = region_find(r, h, d.key, d.start, d.end);
@@ -2016,9 +2410,9 @@ __global__ void k_restore(DevCfg c, int32_t kg, StateCols in, int64_t n, DevTabl
     Entry& x = r.ent[found];
     Entry cur = x;
     acc_merge(c, cur, d);
-    cur.meta |= d.meta;
+    cur.meta = c.panes ? min(cur.meta, d.meta) : (cur.meta | d.meta);
     x = cur;
-    atomicMin((long long*)&tb.next_timer[p], (long long)timer_of(cur, c.lateness));
+    atomicMin((long long*)&tb.next_timer[p], (long long)entry_timer(c, cur));
     return;
   }
   const int32_t s = region_claim(r, h, SLOT_BUSY);
@@ -2030,7 +2424,7 @@ __global__ void k_restore(DevCfg c, int32_t kg, StateCols in, int64_t n, DevTabl
   __threadfence();
   __hip_atomic_store(r.state + s, live_word(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   atomicAdd(&tb.live[p], 1);
-  atomicMin((long long*)&tb.next_timer[p], (long long)timer_of(d, c.lateness));
+  atomicMin((long long*)&tb.next_timer[p], (long long)entry_timer(c, d));
 }
 
 // out3 = {live entries, event-time timers}
@@ -2041,6 +2435,12 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_table_stats(DevCfg c, DevTa
   for (uint32_t s = threadIdx.x; s <= r.mask; s += blockDim.x) {
     if (st_kind(ld_state(r.state + s)) != SLOT_LIVE) continue;
     const Entry& e = r.ent[s];
+    if (c.panes) {  // one pending timer per pane (its next window end); formed-out panes are garbage
+      if (max(e.meta, tb.pane_floor[p]) > jsub(jadd(e.start, c.size), 1)) continue;
+      live++;
+      timers++;
+      continue;
+    }
     live++;
     const int64_t mx = jsub(e.end, 1), cl = cleanup_of(e.end, c.lateness);
     if (e.meta & FW_TIMER) timers++;
@@ -2204,8 +2604,20 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
                      (const Status*)st);
 }
 
-void launch_aggregate(const DevCfg& c, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
+// panes: maxTimestamp of the earliest window ending after wm (windows [s, s + size), s = offset mod slide)
+int64_t pane_nt_floor(const DevCfg& c, int64_t wm) {
+  if (!c.panes) return 0;
+  const __int128 x = (__int128)wm - c.size + 2;  // first start s with s + size - 1 > wm
+  __int128 r = ((__int128)c.offset - x) % c.slide;
+  if (r < 0) r += c.slide;
+  const __int128 e = x + r + c.size - 1;
+  return e > (__int128)LMAX ? LMAX : e < (__int128)LMIN ? LMIN : (int64_t)e;
+}
+
+void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
                       AggProg prog, int resume, const AggHot* hot, int64_t n, Status* st, hipStream_t s) {
+  DevCfg c = c0;
+  c.nt_floor = pane_nt_floor(c, wm);
   AggHot h{};
   unsigned grid = (unsigned)c.P;
   if (hot) {  // at most n / FW_AGG_CHUNK chunks beyond one per partition
@@ -2227,6 +2639,13 @@ void launch_aggregate(const DevCfg& c, int64_t wm, const PRec* part, const uint3
                        tb, prog, resume, st, h);
 }
 
+void launch_hll_update(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
+                       Status* st, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_hll_update, dim3((unsigned)((n + FW_HLL_CHUNK - 1) / FW_HLL_CHUNK)), dim3(256), 0, s, c, part,
+                     offs, T, tb, st);
+}
+
 void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* offs, int32_t T, const int64_t* sk, const int64_t* stt,
                  const int64_t* sv, const int32_t* skh, DevTable tb, DevRows out, DevSide side, Status* st, int resume,
                  hipStream_t s) {
@@ -2234,7 +2653,13 @@ void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* offs, int32_t T, c
                      st, resume);
 }
 
-void launch_fire(const DevCfg& c, int64_t wm, DevTable tb, DevRows out, Status* st, hipStream_t s) {
+void launch_fire(const DevCfg& c0, int64_t wm, DevTable tb, DevRows out, Status* st, hipStream_t s) {
+  DevCfg c = c0;
+  c.nt_floor = pane_nt_floor(c, wm);
+  if (c.panes) {
+    hipLaunchKernelGGL(k_fire_panes, dim3(c.P), dim3(PF_THREADS), 0, s, c, wm, tb, out, st);
+    return;
+  }
   hipLaunchKernelGGL(k_fire, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, wm, tb, out, st);
 }
 

@@ -48,7 +48,22 @@ struct DevCfg {
   int32_t side_output, max_par, kg0, n_kg;
   int32_t log_s, P, log_r, wpr;  // wpr = max windows per record
   int64_t size, slide, offset, gap, lateness;
-  int32_t diag, pad_;            // FW_DIAG ablation bits (diagnostic builds of the timing only; 0 in production)
+  int32_t diag;                  // FW_DIAG ablation bits (diagnostic builds of the timing only; 0 in production)
+  // sliding windows as panes (size % slide == 0, allowedLateness 0): the state holds one entry per
+  // (key, pane) = (key, [p, p + slide)), and a window [s, s + size) is the merge of its size/slide
+  // panes, formed when it fires.  An entry's meta is then the end - 1 of the earliest window it has
+  // not yet been fired into (its timer); nt_floor = the earliest window end after the launch's
+  // watermark (set per launch by the host).
+  int32_t panes;
+  int64_t nt_floor;
+  // HyperLogLog AggregateFunction (FW_AGG_HLL): 2^hll_p one-byte registers per (key, window) in a block
+  // of a pool; an entry's block id is meta >> 1.  Free blocks (zeroed) are kept on a stack:
+  // hll_ctr[0] = stack height, hll_ctr[1] = blocks ever handed out from the end of the pool.
+  int32_t agg, hll_p;
+  uint8_t* hll_regs;
+  uint32_t* hll_free;
+  int32_t* hll_ctr;
+  int64_t hll_blocks;
   // invariant-divisor reciprocals (Granlund-Montgomery round-up method) for `% size` / `% slide`
   uint64_t mag_size, mag_slide;
   int32_t l_size, l_slide;
@@ -117,13 +132,14 @@ enum {
   FW_STATUS_STATE_LOST = 1,  // a window could not be stored (more in-flight sessions of one key than supported)
   FW_STATUS_OUT_FULL = 2,
   FW_STATUS_MERGE_LATE = 4,
-  FW_STATUS_SIDE_FULL = 8
+  FW_STATUS_SIDE_FULL = 8,
+  FW_STATUS_HLL_POOL = 16    // the HyperLogLog register pool ran out of blocks
 };
 // a region takes new windows only up to this load; beyond it the kernel suspends and the table grows
 __host__ __device__ inline int32_t region_limit(int32_t log_r) { return (int32_t)((3ll << log_r) >> 2); }
 // suspension: a kernel stopped before changing anything it cannot keep (a region or the fired-row
 // buffer lacked room); the host grows the table / buffer and resumes exactly where it stopped
-enum { FW_SUSP_AGG = 1, FW_SUSP_SLOW = 2 };
+enum { FW_SUSP_AGG = 1, FW_SUSP_SLOW = 2, FW_SUSP_FIRE = 4 };
 
 // k_aggregate progress, kept per partition so a suspended launch can be resumed
 struct AggProg {
@@ -150,6 +166,9 @@ struct DevTable {
   uint8_t* cur;
   int32_t* live;
   int64_t* next_timer;
+  int64_t* fire_e;     // panes: window maxTimestamp a suspended k_fire resumes at, LMIN = from the start
+  uint64_t* fire_lo;   // panes: first key hash of that window not yet emitted
+  int64_t* pane_floor; // panes: every window of the region with maxTimestamp < pane_floor has been formed
 };
 
 struct DevRows {
@@ -184,6 +203,10 @@ void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* offs, int32_t T, c
                  const int64_t* stt, const int64_t* sv, const int32_t* skh, DevTable tb, DevRows out, DevSide side,
                  Status* st, int resume, hipStream_t_ s);
 void launch_fire(const DevCfg& c, int64_t wm, DevTable tb, DevRows out, Status* st, hipStream_t_ s);
+int64_t pane_nt_floor(const DevCfg& c, int64_t wm);  // host: DevCfg::nt_floor of a launch at watermark wm
+// FW_AGG_HLL: fold the batch's records into the registers of their (key, window) entries (after aggregate)
+void launch_hll_update(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
+                       Status* st, hipStream_t_ s);
 void launch_rehash(const DevCfg& old_c, DevTable old_t, const DevCfg& new_c, DevTable new_t, hipStream_t_ s);
 void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t_ s);
 void launch_reset_regions(const DevCfg& c, DevTable tb, hipStream_t_ s);

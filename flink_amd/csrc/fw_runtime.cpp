@@ -156,6 +156,9 @@ int alloc_table(fw_op* op, DevTable& t, const DevCfg& c, bool with_meta) {
     HIP_OR_RETURN(op, dmalloc(&t.cur, (size_t)c.P));
     HIP_OR_RETURN(op, dmalloc(&t.live, (size_t)c.P));
     HIP_OR_RETURN(op, dmalloc(&t.next_timer, (size_t)c.P));
+    HIP_OR_RETURN(op, dmalloc(&t.fire_e, (size_t)c.P));
+    HIP_OR_RETURN(op, dmalloc(&t.fire_lo, (size_t)c.P));
+    HIP_OR_RETURN(op, dmalloc(&t.pane_floor, (size_t)c.P));
   }
   return FW_OK;
 }
@@ -333,6 +336,9 @@ int grow_table(fw_op* op, int new_log_r) {
   nt.cur = op->tb.cur;
   nt.live = op->tb.live;
   nt.next_timer = op->tb.next_timer;
+  nt.fire_e = op->tb.fire_e;
+  nt.fire_lo = op->tb.fire_lo;
+  nt.pane_floor = op->tb.pane_floor;
   int rc = alloc_table(op, nt, nc, false);
   if (rc) {
     free_table(nt);
@@ -371,6 +377,18 @@ int settle(fw_op* op) {
   while (s.suspended) {
     if (++rounds > 64) return set_err(op, FW_ERR_STATE, "suspended push did not complete after 64 resumptions");
     const int susp = s.suspended;
+    if (susp == FW_SUSP_FIRE) {  // pane windows did not fit the fired-row buffer: grow it and fire again
+      if ((rc = ensure_out_capacity(op, std::max<int64_t>(2 * op->out.cap, (int64_t)s.need_out + op->table_slots),
+                                    (int64_t)s.out_rows)))
+        return rc;
+      s.suspended = 0;
+      s.need_out = 0;
+      if ((rc = put_status_field(op, &Status::suspended)) || (rc = put_status_field(op, &Status::need_out))) return rc;
+      timed(op, K_FIRE, [&] { fwdev::launch_fire(op->dc, op->wm, op->tb, op->out, op->d_status, op->stream); });
+      HIP_OR_RETURN(op, hipGetLastError());
+      if ((rc = sync_status(op))) return rc;
+      continue;
+    }
     if (s.need_live > region_limit(op->dc.log_r) && (rc = grow_table(op, log_r_for(op, s.need_live)))) return rc;
     if (s.need_out > op->out.slow_limit &&
         (rc = ensure_out_capacity(op, (int64_t)s.need_out + op->table_slots, (int64_t)s.out_rows)))
@@ -387,6 +405,9 @@ int settle(fw_op* op) {
       timed(op, K_AGGREGATE, [&] {
         fwdev::launch_aggregate(c, S.wm, S.part, S.hist, S.T, op->tb, op->prog, 1, S.split ? &op->hot : nullptr, S.n,
                                 op->d_status, op->stream);
+        // the update skipped itself behind the suspension; register max is idempotent, so it reruns whole
+        if (c.agg == FW_AGG_HLL)
+          fwdev::launch_hll_update(c, S.part, S.hist, S.T, S.n, op->tb, op->d_status, op->stream);
       });
     // after an aggregate suspension the ordered path never started; otherwise it resumes
     timed(op, K_SLOW, [&] {
@@ -412,6 +433,9 @@ int settle(fw_op* op) {
     return set_err(op, FW_ERR_CAPACITY,
                    "a window could not be stored (more than 64 in-flight sessions of one key)");
   if (s.flags & FW_STATUS_OUT_FULL) return set_err(op, FW_ERR_STATE, "fired-row buffer overflow");
+  if (s.flags & FW_STATUS_HLL_POOL)
+    return set_err(op, FW_ERR_CAPACITY, "HyperLogLog register pool exhausted (%lld blocks; raise expected_entries)",
+                   (long long)op->dc.hll_blocks);
   if (s.flags & FW_STATUS_SIDE_FULL) return set_err(op, FW_ERR_STATE, "side-output buffer overflow");
   if (s.kg_errors) return set_err(op, FW_ERR_KEY_GROUP, "%d record(s) outside KeyGroupRange [%d, %d]", s.kg_errors,
                                    op->dc.kg0, op->dc.kg0 + op->dc.n_kg - 1);
@@ -495,11 +519,12 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   if ((rc = ensure_out_capacity(op, rows + op->table_slots + chunk_rows, rows))) return rc;
   const DevCfg& cc = op->dc;  // settle may have grown the table
   // a partition can outgrow one aggregate workgroup (hot keys) only when the batch is longer than a chunk
-  const bool split = cc.wpr == 1 && n > FW_AGG_CHUNK;
+  const bool split = (cc.wpr == 1 || cc.panes) && n > FW_AGG_CHUNK;
   if (split && (rc = ensure_hot(op))) return rc;
   timed(op, K_AGGREGATE, [&] {
     fwdev::launch_aggregate(cc, op->wm, S.part, S.hist, T, op->tb, op->prog, 0, split ? &op->hot : nullptr, n,
                             op->d_status, op->stream);
+    if (cc.agg == FW_AGG_HLL) fwdev::launch_hll_update(cc, S.part, S.hist, T, n, op->tb, op->d_status, op->stream);
   });
   timed(op, K_SLOW, [&] {
     fwdev::launch_slow(cc, op->wm, S.hist, T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status, 0,
@@ -559,12 +584,24 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     snprintf(msg, sizeof msg, "invalid KeyGroupRange [%d, %d]", cfg.key_group_start, cfg.key_group_end);
   if (!msg[0] && cfg.sub_partitions != 0 && (cfg.sub_partitions & (cfg.sub_partitions - 1)))
     snprintf(msg, sizeof msg, "sub_partitions must be a power of two");
+  if (!msg[0] && (cfg.aggregate < FW_AGG_COUNT_SUM_MIN_MAX || cfg.aggregate > FW_AGG_HLL))
+    snprintf(msg, sizeof msg, "unknown aggregate %d", cfg.aggregate);
+  const int32_t hll_p = cfg.hll_precision ? cfg.hll_precision : 14;
+  if (!msg[0] && cfg.aggregate == FW_AGG_HLL && (hll_p < 4 || hll_p > 16))
+    snprintf(msg, sizeof msg, "HyperLogLog precision must be in [4, 16], got %d", hll_p);
+  bool unsupported = false;
+  if (!msg[0] && cfg.aggregate == FW_AGG_HLL &&
+      (cfg.assigner != FW_TUMBLING || cfg.allowed_lateness != 0 || cfg.value_type != FW_VAL_I64)) {
+    snprintf(msg, sizeof msg, "the HyperLogLog aggregate is offered for tumbling windows without allowed lateness "
+                              "over a Long item column");
+    unsupported = true;
+  }
   fw_op* op = new fw_op();
   op->cfg = cfg;
   if (msg[0]) {
     op->err = msg;
     *out = op;
-    return FW_ERR_ARG;
+    return unsupported ? FW_ERR_UNSUPPORTED : FW_ERR_ARG;
   }
   *out = op;
   op->device = cfg.device;
@@ -593,11 +630,27 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   // FW_DIAG: ablation bits for pricing kernel stages in diagnostic runs only (results are wrong)
   if (const char* d = getenv("FW_DIAG")) c.diag = atoi(d);
   c.wpr = cfg.assigner == FW_SLIDING ? (int32_t)((cfg.size + cfg.slide - 1) / cfg.slide) : 1;
+  // sliding windows whose size is a multiple of the slide, without allowed lateness, are kept as panes:
+  // one state update per element instead of size/slide (DevCfg::panes; FW_NO_PANES=1 disables it)
+  c.panes = cfg.assigner == FW_SLIDING && cfg.allowed_lateness == 0 && cfg.size > cfg.slide &&
+            cfg.size % cfg.slide == 0 && !(getenv("FW_NO_PANES") && atoi(getenv("FW_NO_PANES")));
   if (cfg.assigner != FW_SESSION) {
     make_div_inv((uint64_t)c.size, &c.mag_size, &c.l_size);
     make_div_inv((uint64_t)c.slide, &c.mag_slide, &c.l_slide);
   }
   const int64_t expected = cfg.expected_entries > 0 ? cfg.expected_entries : (int64_t)c.P * 512;
+  if (cfg.aggregate == FW_AGG_HLL) {
+    // register pool: one 2^p-byte block per live (key, window); expected_entries live entries, plus
+    // a quarter for entries created before the watermark that retires their predecessors
+    c.agg = FW_AGG_HLL;
+    c.hll_p = hll_p;
+    c.hll_blocks = std::max<int64_t>(1024, expected + expected / 4);
+    HIP_OR_RETURN(op, dmalloc(&c.hll_regs, (size_t)(c.hll_blocks << hll_p)));
+    HIP_OR_RETURN(op, hipMemsetAsync(c.hll_regs, 0, (size_t)(c.hll_blocks << hll_p), op->stream));
+    HIP_OR_RETURN(op, dmalloc(&c.hll_free, (size_t)c.hll_blocks));
+    HIP_OR_RETURN(op, dmalloc(&c.hll_ctr, 2));
+    HIP_OR_RETURN(op, hipMemsetAsync(c.hll_ctr, 0, 2 * sizeof(int32_t), op->stream));
+  }
   c.log_r = std::max(8, ilog2(4 * ((expected + c.P - 1) / c.P)));
   op->table_slots = (int64_t)c.P << c.log_r;
 
@@ -647,6 +700,9 @@ void fw_destroy(fw_op* op) {
   dfree(op->tb.cur);
   dfree(op->tb.live);
   dfree(op->tb.next_timer);
+  dfree(op->tb.fire_e);
+  dfree(op->tb.fire_lo);
+  dfree(op->tb.pane_floor);
   dfree(op->in_key);
   dfree(op->in_ts);
   dfree(op->in_val);
@@ -656,6 +712,9 @@ void fw_destroy(fw_op* op) {
   dfree(op->prog.tp);
   dfree(op->prog.done);
   dfree(op->dc.taint_key);
+  dfree(op->dc.hll_regs);
+  dfree(op->dc.hll_free);
+  dfree(op->dc.hll_ctr);
   dfree(op->dc.taint_state);
   free_hot(op->hot);
   for (int64_t** col : {&op->out.key, &op->out.start, &op->out.end, &op->out.cnt, &op->out.sum, &op->out.mn,
@@ -895,6 +954,8 @@ void free_state_cols(StateCols& c) {
 }  // namespace
 
 int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64_t cap, int64_t* n) {
+  if (op && op->dc.agg == FW_AGG_HLL)  // registers are not part of fw_state_rows
+    return set_err(op, FW_ERR_UNSUPPORTED, "keyed-state snapshots of the HyperLogLog aggregate are not offered");
   if (!op || !n) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;
@@ -933,6 +994,8 @@ int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64
 }
 
 int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_t n) {
+  if (op && op->dc.agg == FW_AGG_HLL)  // registers are not part of fw_state_rows
+    return set_err(op, FW_ERR_UNSUPPORTED, "keyed-state snapshots of the HyperLogLog aggregate are not offered");
   if (!op || (n > 0 && !src) || n < 0) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;

@@ -45,6 +45,14 @@ extern "C" {
 #define FW_VAL_I32 1 /* Integer field: sum wraps at 32 bits (SumFunction.IntSum)          */
 #define FW_VAL_F64 2 /* Double field: min/max by Double.compare, sum within 1e-6 relative */
 
+/* the AggregateFunction (fw_config.aggregate) */
+#define FW_AGG_COUNT_SUM_MIN_MAX 0 /* built-in {count, sum, min, max} accumulator                        */
+#define FW_AGG_HLL 1               /* HyperLogLog distinct count of the value column read as a u64 item
+                                      (definition in DESIGN.md §HLL): fired rows carry
+                                      count, sum = estimate (f64 bits), min = zero registers, max = the
+                                      low 64 bits of sum_j 2^(65-p-M[j]).  Tumbling windows, no allowed
+                                      lateness; expected_entries sizes the register pool (2^p B/entry). */
+
 #define FW_KEY_LONG 0   /* key is a Long: hashCode = (int)(v ^ (v >>> 32))               */
 #define FW_KEY_INT 1    /* key is an Integer: hashCode = value                              */
 #define FW_KEY_HASHED 2 /* caller passes key.hashCode() per record (String, Tuple, POJO);
@@ -74,6 +82,8 @@ typedef struct fw_config {
   int64_t allowed_lateness;    /* WindowedStream.allowedLateness, >= 0                       */
   int64_t expected_entries;    /* sizing hint: live (key, window) pairs (0 = default)        */
   int64_t max_batch;           /* largest n passed to one push (0 = 1 << 24)                */
+  int32_t aggregate;           /* FW_AGG_* (0 = count/sum/min/max)                           */
+  int32_t hll_precision;       /* FW_AGG_HLL: p in [4, 16], m = 2^p registers (0 -> 14)       */
 } fw_config;
 
 typedef struct fw_op fw_op;

@@ -21,7 +21,8 @@ _VALTYPES = {"i64": VAL_I64, "i32": VAL_I32, "f64": VAL_F64}
 class OracleCfg(ctypes.Structure):
     _fields_ = [("assigner", ctypes.c_int32), ("value_type", ctypes.c_int32), ("size", ctypes.c_int64),
                 ("slide", ctypes.c_int64), ("offset", ctypes.c_int64), ("gap", ctypes.c_int64),
-                ("lateness", ctypes.c_int64), ("purging", ctypes.c_int32), ("side_output", ctypes.c_int32)]
+                ("lateness", ctypes.c_int64), ("purging", ctypes.c_int32), ("side_output", ctypes.c_int32),
+                ("aggregate", ctypes.c_int32), ("hll_p", ctypes.c_int32)]
 
 
 ROW_DTYPE = np.dtype([("key", "<i8"), ("start", "<i8"), ("end", "<i8"), ("count", "<i8"), ("sum", "<i8"),
@@ -81,10 +82,14 @@ def _i64p(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
 
 
+AGG_COUNT_SUM_MIN_MAX, AGG_HLL = 0, 1
+
+
 def make_cfg(assigner="tumbling", size=0, slide=0, offset=0, gap=0, lateness=0, purging=False, side_output=False,
-             value_type="i64"):
+             value_type="i64", hll_p=0):
+    """hll_p > 0 selects the HyperLogLog AggregateFunction with 2^hll_p registers (window_oracle.h)."""
     return OracleCfg(_ASSIGNERS[assigner], _VALTYPES[value_type], size, slide, offset, gap, lateness, int(purging),
-                     int(side_output))
+                     int(side_output), AGG_HLL if hll_p else AGG_COUNT_SUM_MIN_MAX, int(hll_p))
 
 
 class OracleError(RuntimeError):

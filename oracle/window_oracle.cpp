@@ -92,7 +92,48 @@ struct Acc {
   double dsum = 0.0;
   int64_t imn = 0, imx = 0;
   double dmn = 0.0, dmx = 0.0;
+  std::vector<uint8_t> regs;  // OR_AGG_HLL registers (2^p)
 };
+
+// ---------------------------------------------------------------- HyperLogLog (window_oracle.h)
+inline uint64_t hll_fmix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+inline void hll_add(std::vector<uint8_t>& regs, int p, uint64_t item) {
+  const uint64_t h = hll_fmix64(item);
+  const uint64_t j = h >> (64 - p);
+  const uint64_t w = (h << p) | (1ULL << (p - 1));
+  const uint8_t rank = (uint8_t)(__builtin_clzll(w) + 1);
+  if (regs[j] < rank) regs[j] = rank;
+}
+inline double hll_alpha(int64_t m) {
+  if (m == 16) return 0.673;
+  if (m == 32) return 0.697;
+  if (m == 64) return 0.709;
+  return 0.7213 / (1.0 + 1.079 / (double)m);
+}
+// estimate, zero-register count V, and the low 64 bits of S
+inline void hll_result(const std::vector<uint8_t>& regs, int p, double* est, int64_t* zeros, int64_t* lo64) {
+  const int64_t m = (int64_t)1 << p;
+  const int rmax = 65 - p;
+  unsigned __int128 S = 0;
+  int64_t V = 0;
+  for (int64_t j = 0; j < m; j++) {
+    S += (unsigned __int128)1 << (rmax - regs[j]);
+    V += regs[j] == 0;
+  }
+  const uint64_t hi = (uint64_t)(S >> 64), lo = (uint64_t)S;
+  const double sd = (double)hi * 18446744073709551616.0 + (double)lo;
+  const double raw = (hll_alpha(m) * (double)m * (double)m) * std::ldexp(1.0, rmax) / sd;
+  *est = (raw <= 2.5 * (double)m && V > 0) ? (double)m * std::log((double)m / (double)V) : raw;
+  *zeros = V;
+  *lo64 = (int64_t)lo;
+}
 
 struct KW {
   int64_t key;
@@ -158,6 +199,12 @@ class WindowOperatorOracle {
 
   // ------------------------------------------------ accumulator (CountSumMinMax)
   void acc_add(Acc& a, int64_t v) const {
+    if (cfg.aggregate == OR_AGG_HLL) {
+      if (a.regs.empty()) a.regs.assign((size_t)1 << cfg.hll_p, 0);
+      hll_add(a.regs, cfg.hll_p, (uint64_t)v);
+      a.cnt += 1;
+      return;
+    }
     if (cfg.value_type == OR_VAL_F64) {
       double d = bitsd(v);
       if (a.cnt == 0) {
@@ -184,6 +231,10 @@ class WindowOperatorOracle {
     if (b.cnt == 0) return a;
     Acc r = a;
     r.cnt = a.cnt + b.cnt;
+    if (cfg.aggregate == OR_AGG_HLL) {
+      for (size_t j = 0; j < r.regs.size(); j++) r.regs[j] = std::max(r.regs[j], b.regs[j]);
+      return r;
+    }
     if (cfg.value_type == OR_VAL_F64) {
       r.dsum = a.dsum + b.dsum;
       r.dmn = java_double_compare(b.dmn, a.dmn) < 0 ? b.dmn : a.dmn;
@@ -227,7 +278,11 @@ class WindowOperatorOracle {
     r.start = w.start;
     r.end = w.end;
     r.count = a.cnt;
-    if (cfg.value_type == OR_VAL_F64) {
+    if (cfg.aggregate == OR_AGG_HLL) {
+      double est;
+      hll_result(a.regs, cfg.hll_p, &est, &r.min, &r.max);
+      memcpy(&r.sum, &est, 8);
+    } else if (cfg.value_type == OR_VAL_F64) {
       r.sum = dbits(a.dsum);
       r.min = dbits(a.dmn);
       r.max = dbits(a.dmx);

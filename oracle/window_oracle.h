@@ -54,7 +54,21 @@ typedef struct {
   int64_t lateness;      /* allowedLateness */
   int32_t purging;       /* PurgingTrigger.of(EventTimeTrigger) */
   int32_t side_output;   /* late records go to the side output instead of numLateRecordsDropped */
+  int32_t aggregate;     /* OR_AGG_* */
+  int32_t hll_p;         /* HyperLogLog precision p (registers m = 2^p), OR_AGG_HLL only */
 } oracle_cfg;
+
+/* The user AggregateFunctions of SURVEY.md §8d C5.  OR_AGG_HLL is a HyperLogLog distinct count
+ * (Flajolet, Fusy, Gandouet, Meunier 2007) over the value column read as a u64 item:
+ *   h = fmix64(item) (MurmurHash3's 64-bit finaliser); register j = h >> (64 - p);
+ *   rank = clz64((h << p) | (1 << (p - 1))) + 1  (1 .. 65 - p);  M[j] = max(M[j], rank);
+ *   S = sum_j 2^(65 - p - M[j]) (exact, 128-bit); V = #{j : M[j] == 0};
+ *   raw = (alpha_m * m * m) * 2^(65 - p) / S, S converted as hi * 2^64 + lo (two doubles);
+ *   E = raw <= 2.5 m && V > 0 ? m * log(m / V) : raw  (small-range correction; no large-range
+ *   correction with a 64-bit hash).
+ * Row: count = elements, sum = E (f64 bits), min = V, max = low 64 bits of S (an exact register
+ * checksum).  AggregateFunction.merge = register-wise max. */
+enum { OR_AGG_COUNT_SUM_MIN_MAX = 0, OR_AGG_HLL = 1 };
 
 /* One fired row.  sum/min/max hold i64 values (I64/I32) or f64 bit patterns (F64).
  * epoch = number of watermarks fully processed before the row was emitted, so

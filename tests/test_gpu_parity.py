@@ -47,6 +47,12 @@ def test_gpu_reference_kats(case):
     op.close()
 
 
+def _panes(cfg):
+    """The operator keeps sliding windows as panes (fw_runtime.cpp fw_create: size % slide == 0, no lateness)."""
+    return (cfg["assigner"] == "sliding" and not cfg.get("lateness") and cfg["size"] > cfg["slide"]
+            and cfg["size"] % cfg["slide"] == 0)
+
+
 def _run_both(cfg, batches, wms, **gpu_kw):
     gpu = _gpu_op(**cfg, **gpu_kw)
     ref = orc.WindowOperatorOracle(**cfg)
@@ -57,7 +63,9 @@ def _run_both(cfg, batches, wms, **gpu_kw):
         ref.watermark(wm)
     out = gpu.rows(), ref.rows(), gpu.side_rows(), ref.side_rows(), gpu.late_dropped, ref.late_dropped
     st = gpu.stats()
-    assert st["keyed_state_entries"] == ref.num_state_entries or cfg.get("purging") or cfg["assigner"] == "session"
+    # with sliding windows kept as panes the state entries are panes, not (key, window) pairs
+    assert (st["keyed_state_entries"] == ref.num_state_entries or cfg.get("purging") or cfg["assigner"] == "session"
+            or _panes(cfg))
     gpu.close()
     return out
 
@@ -87,6 +95,9 @@ CONFIGS = [
     dict(assigner="tumbling", size=1000, lateness=700),
     dict(assigner="tumbling", size=1000, lateness=700, purging=True, side_output=True),
     dict(assigner="sliding", size=2000, slide=500, lateness=300, side_output=True),
+    # panes: size % slide == 0 and no allowed lateness (partially late elements go to their pane)
+    dict(assigner="sliding", size=3000, slide=500, offset=200, value_type="i32", purging=True, side_output=True),
+    dict(assigner="sliding", size=4000, slide=1000, value_type="f64"),
     dict(assigner="session", gap=300),
     dict(assigner="session", gap=300, lateness=200, purging=True, side_output=True),
     dict(assigner="session", gap=300, lateness=400, value_type="f64"),
@@ -114,6 +125,32 @@ def test_gpu_vs_oracle_c2_shape():
     assert len(g) > 1_000_000
     assert_rows_equal(g, r)
     assert gl == rl == 0
+
+
+def test_gpu_panes_c3_shape():
+    # SURVEY §8d C3 shape at parity size: sliding 60 s / 1 s (60 windows per element, kept as panes),
+    # 20K uniform keys, 2e5 records per event-second, bound 200 ms, a watermark every 2^15 records
+    cfg = dict(assigner="sliding", size=60_000, slide=1000)
+    batches, wms = _stream(1 << 18, 1 << 15, 20_000, bound=200, jitter=200, rate=200_000)
+    g, r, gs, rs, gl, rl = _run_both(cfg, batches, wms)
+    assert len(g) > 1_000_000
+    assert_rows_equal(g, r)
+    assert gl == rl
+
+
+def test_gpu_panes_fire_suspends_and_resumes():
+    # one element per key in a small table: the final watermark forms 60 windows per pane, more rows than
+    # the fired-row buffer holds, so k_fire_panes suspends per (window, key-hash slice) and resumes
+    cfg = dict(assigner="sliding", size=60_000, slide=1000)
+    n = 30_000
+    keys = np.arange(n, dtype=np.int64)
+    ts = (np.arange(n, dtype=np.int64) * 37) % 50_000
+    vals = np.arange(n, dtype=np.int64) * 3 - 7
+    batches = [(keys, ts, vals), (keys[:0], ts[:0], vals[:0])]
+    wms = [10_000, (1 << 63) - 1]
+    g, r, *_ = _run_both(cfg, batches, wms, expected_entries=1000)
+    assert len(g) == 60 * n
+    assert_rows_equal(g, r)
 
 
 def test_gpu_zipf_hot_keys():
@@ -230,14 +267,15 @@ def _run_device(cfg, batches, wms, **gpu_kw):
     return np.concatenate(rows), ref.rows(), st
 
 
-def test_gpu_burst_suspends_and_resumes_async():
-    # 2^20 distinct keys x 5 sliding windows in ONE asynchronous push into a table sized for 1000
-    # entries: k_aggregate suspends over and over; the watermark queued behind the push is skipped
-    # on the device and fired again after the host grew the table and resumed the push
-    cfg = dict(assigner="sliding", size=5000, slide=1000)
+@pytest.mark.parametrize("cfg", [dict(assigner="sliding", size=5000, slide=1000, lateness=1),
+                                 dict(assigner="sliding", size=5000, slide=1000)], ids=["windows", "panes"])
+def test_gpu_burst_suspends_and_resumes_async(cfg):
+    # 2^20 distinct keys x 5 sliding windows (or one pane) in ONE asynchronous push into a table sized
+    # for 1000 entries: k_aggregate suspends over and over; the watermark queued behind the push is
+    # skipped on the device and fired again after the host grew the table and resumed the push
     batches, wms = _stream(1 << 20, 1 << 20, 1 << 40, bound=100, jitter=100, rate=1_000_000)
     g, r, st = _run_device(cfg, batches, wms, expected_entries=1000)
-    assert st["table_grows"] >= 3
+    assert st["table_grows"] >= (1 if _panes(cfg) else 3)
     assert_rows_equal(g, r)
 
 

@@ -69,8 +69,20 @@ def test_route_scratch_size_positive():
     assert N.lib().fw_route_scratch_bytes(1 << 20, 8) > 8 * 32 * 4
 
 
-def test_struct_layouts_match_header():
-    # fw_config: 10 int32 + 7 int64 = 96 bytes; fw_rows 7 pointers; fw_stats 12 int64
-    assert ctypes.sizeof(N.FwConfig) == 96
+def test_struct_layouts_match_header(tmp_path):
+    # the ctypes mirror against the C compiler's layout of include/flink_window.h, field by field
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    fields = [f for f, _ in N.FwConfig._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "flink_window.h"\nint main(void) {\n'
+                   '  printf("%zu\\n", sizeof(fw_config));\n' +
+                   "".join(f'  printf("%zu\\n", offsetof(fw_config, {f}));\n' for f in fields) + "  return 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)])
+    out = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert ctypes.sizeof(N.FwConfig) == out[0]
+    assert [getattr(N.FwConfig, f).offset for f in fields] == out[1:]
     assert ctypes.sizeof(N.FwRows) == 56
     assert ctypes.sizeof(N.FwStats) == 12 * 8
