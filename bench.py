@@ -39,14 +39,20 @@ PRESETS = {
     "c3": dict(rate=100_000_000, bound=200, jitter=200, zipf=None, keys=2_000_000, cpu_sample=1 << 19,
                workload="C3 sliding 60s/1s event-time windows (60x fan-out), count/sum/min/max, 2M uniform Long keys "
                         "per GPU (16M at 8 GPUs), bounded out-of-orderness 200 ms"),
+    "c5": dict(rate=100_000_000, bound=200, jitter=200, zipf=1.1, keys=1_000_000, cpu_sample=1 << 20,
+               workload="C5 tumbling 1s event-time window, HyperLogLog (p=14) distinct count per key and window, "
+                        "1M Zipf(1.1) Long keys, bounded out-of-orderness 200 ms"),
     "c4": dict(rate=100_000, bound=1000, jitter=1000, zipf=1.1, keys=1_000_000, cpu_sample=1 << 22,
                workload="C4 EventTimeSessionWindows gap 30 s, count/sum/min/max, 1M Zipf(1.1) Long keys, "
                         "bounded out-of-orderness 1 s"),
 }
 
 
-def kernel_bytes(name, n, merged, live_slots_scanned=0):
+def kernel_bytes(name, n, merged, fired=0, hll_p=0):
     """Algorithmic bytes of one launch."""
+    if name == "k_fire" and hll_p:
+        # per fired (key, window): read the 64-B entry, read + zero its 2^p register block, write the 56-B row
+        return fired * (64 + 2 * (1 << hll_p) + 56)
     if name == "k_classify_hist":
         return 16 * n                      # key + ts
     if name == "k_scatter":
@@ -71,6 +77,7 @@ def main():
     ap.add_argument("--gap", type=int, default=30_000, help="session gap (ms, c4)")
     ap.add_argument("--size", type=int, default=60_000, help="sliding window size (ms, c3)")
     ap.add_argument("--slide", type=int, default=1000, help="sliding window slide (ms, c3)")
+    ap.add_argument("--hll-p", type=int, default=14, help="HyperLogLog precision (c5)")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--zipf", type=float, default=None, help="Zipf exponent of the keys (0 = uniform)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -88,6 +95,7 @@ def main():
     args.zipf = args.zipf or None
     sessions = args.workload == "c4"
     sliding = args.workload == "c3"
+    hll = args.workload == "c5"
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -99,7 +107,8 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    from flink_amd import EventTimeSessionWindows, SlidingEventTimeWindows, TumblingEventTimeWindows
+    from flink_amd import (CountSumMinMax, EventTimeSessionWindows, HyperLogLog, SlidingEventTimeWindows,
+                           TumblingEventTimeWindows)
     from flink_amd import _native as N
     from flink_amd.datagen import generate_device, zipf_cdf
     from flink_amd.exchange import KeyGroupExchange
@@ -119,7 +128,8 @@ def main():
         assigner = TumblingEventTimeWindows.of(args.window)
     live_windows = (args.size // args.slide + 1) if sliding else 2
     cdf = torch.from_numpy(zipf_cdf(args.keys, args.zipf)).to(dev) if args.zipf else None
-    op = GpuWindowOperator(assigner, key_group_range=exch.key_group_range,
+    op = GpuWindowOperator(assigner, HyperLogLog(args.hll_p) if hll else CountSumMinMax(),
+                           key_group_range=exch.key_group_range,
                            device=local_rank, max_parallelism=max_par,
                            expected_entries=live_windows * args.keys // world,
                            max_batch=args.batch if world == 1 else 2 * args.batch,
@@ -197,12 +207,15 @@ def main():
                 kernels[name] = {"launches": int(nl[i]), "avg_ms": ms[i] / nl[i], "total_ms": ms[i]}
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
         per_launch_records = records / world / args.steps
-        b = kernel_bytes(dom, per_launch_records, merged / args.steps)
+        b = kernel_bytes(dom, per_launch_records, merged / args.steps,
+                         fired=fired / kernels[dom]["launches"], hll_p=args.hll_p if hll else 0)
         traffic = None
         if os.path.exists(args.traffic):
             with open(args.traffic) as f:
                 tr = json.load(f)
-            traffic = tr.get("per_launch_bytes", {}).get(dom)
+            # PMC bytes per launch were measured on one workload (tools/traffic.py); other workloads: null
+            if tr.get("workload", "c2") == args.workload:
+                traffic = tr.get("per_launch_bytes", {}).get(dom)
         if b is not None:
             achieved = b / (kernels[dom]["avg_ms"] * 1e-3) / 1e9
             roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -213,6 +226,8 @@ def main():
     fpr = fired / max(1, records / world)
     if sliding:
         b_alg = 24 + 96 + (args.size // args.slide * 48 + 56) * fpr + 48 * (world - 1) / world
+    elif hll:  # C5-HLL: 24 + B_x + 2 + (2^p + 56) F/N
+        b_alg = 24 + 48 * (world - 1) / world + 2 + ((1 << args.hll_p) + 56) * fpr
     else:
         b_alg = 24 + (112 if sessions else 104) * fpr
     path_frac = value * b_alg / (world * HBM_PEAK_GBS * 1e9)
@@ -230,7 +245,9 @@ def main():
             "config": {"workload": preset["workload"],
                        "records_per_step_per_gpu": args.batch, "keys": args.keys,
                        **({"gap_ms": args.gap, "zipf_s": args.zipf} if sessions else
-                          {"size_ms": args.size, "slide_ms": args.slide} if sliding else {"window_ms": args.window}),
+                          {"size_ms": args.size, "slide_ms": args.slide} if sliding else
+                          {"window_ms": args.window, "hll_precision": args.hll_p, "zipf_s": args.zipf} if hll else
+                          {"window_ms": args.window}),
                        "records_per_event_second": args.rate, "watermark_bound_ms": args.bound,
                        "max_parallelism": 128, "parallelism": f"keygroup{world}"},
             "roofline": roofline,
@@ -265,6 +282,8 @@ def cpu_baseline(args):
         cfg = dict(assigner="session", gap=args.gap)
     elif args.workload == "c3":
         cfg = dict(assigner="sliding", size=args.size, slide=args.slide)
+    elif args.workload == "c5":
+        cfg = dict(assigner="tumbling", size=args.window, hll_p=args.hll_p)
     else:
         cfg = dict(assigner="tumbling", size=args.window)
     orc.run_parallel(cfg, k, t, v, batch, np.array(wms), 128, threads)

@@ -1855,15 +1855,14 @@ __global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, 
 // Pass 1 decides every slot, re-inserts the survivors into the other buffer and counts the fired
 // rows; one reservation per workgroup in the output; pass 2 re-decides and writes the rows.
 // one wave per fired row: estimate from the row's register block (out.mn holds its id), then zero the
-// block and push it on the free stack.  S = sum_j 2^(65-p-M[j]) exactly: per lane in 64 bits (at most
-// m/64 terms of at most 2^(65-p)), across the wave in 128 bits.
+// block and push it on the free stack.  S = sum_j 2^(65-p-M[j]) exactly, in 128 bits.
 __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row) {
   const int lane = __lane_id();
   const int p = c.hll_p, rmax = 65 - p;
   const int64_t m = (int64_t)1 << p;
   const uint64_t blk = (uint64_t)out.mn[row];
   uint8_t* regs = c.hll_regs + blk * (uint64_t)m;
-  uint64_t s = 0;
+  uint64_t s = 0, sh = 0;
   uint32_t zeros = 0;
   uint4* q = reinterpret_cast<uint4*>(regs);
   const int64_t nq = m / 16;  // 16-byte chunks, four in flight per lane
@@ -1880,13 +1879,15 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row) {
 #pragma unroll
         for (int b = 0; b < 4; b++) {
           const uint32_t r = (ws[k] >> (8 * b)) & 0xffu;
-          s += 1ull << (rmax - (int)r);
+          const uint64_t t = s + (1ull << (rmax - (int)r));
+          sh += t < s;  // 16 terms of up to 2^61 per chunk overflow 64 bits at small p
+          s = t;
           zeros += r == 0;
         }
       q[j0 + u * 64] = make_uint4(0, 0, 0, 0);
     }
   }
-  uint64_t hi = 0, lo = s;
+  uint64_t hi = sh, lo = s;
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t lo2 = __shfl_xor(lo, o, 64), hi2 = __shfl_xor(hi, o, 64);
     const uint64_t t = lo + lo2;

@@ -156,3 +156,24 @@ class CountSumMinMax:
 
     def native(self):
         return {"long": N.FW_VAL_I64, "int": N.FW_VAL_I32, "double": N.FW_VAL_F64}[self.value_type]
+
+    def hll_precision(self):
+        return 0
+
+
+@dataclass(frozen=True)
+class HyperLogLog:
+    """User AggregateFunction of SURVEY §8d C5: a HyperLogLog distinct count of a Long item field with
+    2^precision one-byte registers per (key, window) (definition: DESIGN.md §HLL, restated in
+    oracle/window_oracle.h).  add = register max of the item's hash; merge = register-wise max;
+    getResult = (count, estimate).  Fired rows: count, sum = estimate (f64 bits), min = zero registers,
+    max = the low 64 bits of sum_j 2^(65 - p - M[j]) (an exact register checksum).  Offered on the GPU
+    for tumbling windows without allowed lateness."""
+    precision: int = 14
+    value_type: str = "long"
+
+    def native(self):
+        return N.FW_VAL_I64
+
+    def hll_precision(self):
+        return self.precision

@@ -473,3 +473,62 @@ def test_gpu_restore_refuses_foreign_key_group():
     op.restore_key_group(5, rows)
     assert op.num_keyed_state_entries == 1
     op.close()
+
+
+def _hll_rows_equal(g, r):
+    ks = lambda a: a[np.lexsort((a["start"], a["key"], a["epoch"]))]  # noqa: E731
+    g, r = ks(g), ks(r)
+    assert len(g) == len(r) and len(g) > 0
+    for f in ("epoch", "key", "start", "end", "count", "min", "max"):
+        assert np.array_equal(g[f], r[f]), f
+    np.testing.assert_allclose(g["sum"].view(np.float64), r["sum"].view(np.float64), rtol=1e-9)
+
+
+@pytest.mark.parametrize("p,zipf", [(14, 1.1), (8, None), (4, 1.1)], ids=["p14-zipf", "p8-uniform", "p4-zipf"])
+def test_gpu_hll_vs_oracle(p, zipf):
+    # SURVEY §8d C5 shape at parity size: tumbling windows, HyperLogLog per key and window over the value
+    # column as items; Zipf keys put most records on a few hot (key, window) register blocks
+    from flink_amd import HyperLogLog
+    from flink_amd.operator import GpuWindowOperator
+    batches, wms = _stream(300_000, 50_000, 20_000, bound=200, jitter=200, rate=200_000, zipf=zipf)
+    gpu = GpuWindowOperator(TumblingEventTimeWindows.of(1000), HyperLogLog(p), expected_entries=60_000)
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000, hll_p=p)
+    for (k, t, v), wm in zip(batches, wms):
+        gpu.process(k, t, v)
+        ref.process(k, t, v)
+        gpu.watermark(wm)
+        ref.watermark(wm)
+    assert gpu.late_dropped == ref.late_dropped
+    _hll_rows_equal(gpu.rows(), ref.rows())
+    gpu.close()
+
+
+def test_gpu_hll_register_blocks_are_recycled():
+    # many windows over few keys with a pool sized for one window's entries: every fired block must be
+    # zeroed and reused, or the pool runs out (FW_ERR_CAPACITY) or stale registers inflate the estimates
+    from flink_amd import HyperLogLog
+    from flink_amd.operator import GpuWindowOperator
+    batches, wms = _stream(400_000, 10_000, 500, bound=50, jitter=50, rate=100_000)
+    gpu = GpuWindowOperator(TumblingEventTimeWindows.of(100), HyperLogLog(10), expected_entries=1500)
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=100, hll_p=10)
+    for (k, t, v), wm in zip(batches, wms):
+        gpu.process(k, t, v)
+        ref.process(k, t, v)
+        gpu.watermark(wm)
+        ref.watermark(wm)
+    _hll_rows_equal(gpu.rows(), ref.rows())
+    gpu.close()
+
+
+def test_gpu_hll_refuses_unsupported_shapes():
+    from flink_amd import HyperLogLog
+    from flink_amd import _native as N
+    from flink_amd.operator import GpuWindowOperator
+    with pytest.raises(N.NativeError) as e:
+        GpuWindowOperator(SlidingEventTimeWindows.of(3000, 1000), HyperLogLog(12))
+    assert e.value.code == N.FW_ERR_UNSUPPORTED
+    with pytest.raises(N.NativeError) as e:
+        GpuWindowOperator(TumblingEventTimeWindows.of(1000), HyperLogLog(12), allowed_lateness=10)
+    assert e.value.code == N.FW_ERR_UNSUPPORTED
+    with pytest.raises(N.NativeError):
+        GpuWindowOperator(TumblingEventTimeWindows.of(1000), HyperLogLog(20))
