@@ -116,18 +116,6 @@ __device__ __forceinline__ int64_t wend(const DevCfg& c, int64_t start) {
   return jadd(start, c.panes ? c.slide : c.size);
 }
 // ---- HyperLogLog (FW_AGG_HLL; the definition is restated in oracle/window_oracle.h)
-// a zeroed register block for a new (key, window) entry: the free stack first, then the pool's tail
-__device__ __forceinline__ int64_t hll_alloc(const DevCfg& c, Status* st) {
-  const int32_t t = atomicSub(&c.hll_ctr[0], 1) - 1;
-  if (t >= 0) return (int64_t)c.hll_free[t];
-  atomicAdd(&c.hll_ctr[0], 1);  // nothing is pushed while the aggregate runs (k_fire pushes)
-  const int32_t b = atomicAdd(&c.hll_ctr[1], 1);
-  if ((int64_t)b >= c.hll_blocks) {
-    atomicOr(&st->flags, FW_STATUS_HLL_POOL);
-    return 0;
-  }
-  return b;
-}
 __device__ __forceinline__ uint64_t hll_block_of(const Entry& e) { return (uint64_t)e.meta >> 1; }
 // earliest pending timer of an entry; a pane's is its meta (the next window end it belongs to)
 __device__ __forceinline__ int64_t entry_timer(const DevCfg& c, const Entry& e) {
@@ -675,6 +663,8 @@ struct AggLds {
   int live;    // occupied slots of the region
   unsigned long long flushed;
   int64_t min_timer;
+  int hl_lo, hl_take, hl_idx;  // FW_AGG_HLL: this flush's register blocks (free-stack slice, then pool tail)
+  long long hl_bump;
 };
 enum : uint32_t { LT_EMPTY = 0, LT_BUSY = 1 };
 
@@ -847,6 +837,30 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
     if (threadIdx.x == 0) atomicMax(&st->need_live, need);
     return false;
   }
+  if (c.agg == FW_AGG_HLL) {  // one reservation of register blocks for every new window of the flush
+    if (threadIdx.x == 0) {
+      const int k = L.nnew;
+      int take = 0, lo = 0;
+      long long bump = 0;
+      if (k) {
+        // pop k from the free stack (nothing is pushed while the aggregate runs); what the stack
+        // lacks comes from the pool's tail
+        const int t = atomicSub(&c.hll_ctr[0], k);
+        take = max(0, min(t, k));
+        lo = t - take;
+        if (take < k) {
+          atomicAdd(&c.hll_ctr[0], k - take);
+          bump = atomicAdd(&c.hll_ctr[1], k - take);
+          if (bump + (k - take) > c.hll_blocks) atomicOr(&st->flags, FW_STATUS_HLL_POOL);
+        }
+      }
+      L.hl_lo = lo;
+      L.hl_take = take;
+      L.hl_bump = bump;
+      L.hl_idx = 0;
+    }
+    __syncthreads();
+  }
   int64_t mt = LMAX;
   unsigned long long nflush = 0;
   int lost = 0;
@@ -870,7 +884,12 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
       const int32_t ns = region_claim(r, hs, live_word(hs));
       if (ns >= 0) {
         Entry n = d;
-        if (c.agg == FW_AGG_HLL) n.meta |= hll_alloc(c, st) << 1;
+        if (c.agg == FW_AGG_HLL) {
+          const int i = atomicAdd(&L.hl_idx, 1);
+          int64_t blk = i < L.hl_take ? (int64_t)c.hll_free[L.hl_lo + i] : L.hl_bump + (i - L.hl_take);
+          if (blk >= c.hll_blocks) blk = 0;  // pool exhausted: flagged above, the push fails
+          n.meta |= blk << 1;
+        }
         r.ent[ns] = n;
       } else {
         lost++;  // cannot happen below the load limit
@@ -1856,7 +1875,7 @@ __global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, 
 // rows; one reservation per workgroup in the output; pass 2 re-decides and writes the rows.
 // one wave per fired row: estimate from the row's register block (out.mn holds its id), then zero the
 // block and push it on the free stack.  S = sum_j 2^(65-p-M[j]) exactly, in 128 bits.
-__device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row) {
+__device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, int64_t stack_slot) {
   const int lane = __lane_id();
   const int p = c.hll_p, rmax = 65 - p;
   const int64_t m = (int64_t)1 << p;
@@ -1904,8 +1923,7 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row) {
     out.sum[row] = __double_as_longlong(est);
     out.mn[row] = (int64_t)zeros;
     out.mx[row] = (int64_t)lo;
-    __threadfence();  // the zeroed block is visible before it can be handed out again
-    c.hll_free[atomicAdd(&c.hll_ctr[0], 1)] = (uint32_t)blk;
+    c.hll_free[stack_slot] = (uint32_t)blk;  // zeroed before the next kernel can hand it out
   }
 }
 
@@ -2048,10 +2066,13 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, 
     }
   }
   if (c.agg == FW_AGG_HLL && total) {
+    __shared__ int hl_sb;
     __threadfence_block();
+    if (threadIdx.x == 0) hl_sb = atomicAdd(&c.hll_ctr[0], (int)total);  // free-stack slots for this workgroup
     __syncthreads();
     const uint64_t end = min((unsigned long long)out.cap, base_s + total);
-    for (uint64_t r = base_s + (threadIdx.x >> 6); r < end; r += blockDim.x >> 6) hll_finish(c, out, r);
+    for (uint64_t r = base_s + (threadIdx.x >> 6); r < end; r += blockDim.x >> 6)
+      hll_finish(c, out, r, hl_sb + (int64_t)(r - base_s));
   }
   if (threadIdx.x == 0) {
     if (total) atomicAdd(&st->fired_total, (unsigned long long)total);
