@@ -8,8 +8,8 @@ on the receiving side; watermarks are broadcast to every channel and the receive
 over channels (flink-streaming-java/.../runtime/streamstatus/StatusWatermarkValve.java:173-191).
 
 On MI355X: the batch is grouped by destination on the GPU (fw_route_device, stable), the per-peer
-counts are exchanged (all_to_all_single of P int64), then the 24-byte records go peer-to-peer in one
-all_to_all_single (RCCL over xGMI: each peer pair has its own link).  The watermark is one int64
+counts are exchanged (all_to_all_single of P int64), then the key, timestamp and value columns go
+peer-to-peer, one all_to_all_single each (RCCL over xGMI: each peer pair has its own link).  The watermark is one int64
 all_reduce(MIN).  The collectives are torch.distributed's, so the same code runs over "nccl" (RCCL) on
 the GPU box and over "gloo" in the CPU tests, where the caller supplies the routing function.
 """
@@ -61,17 +61,19 @@ class KeyGroupExchange:
         (k, t, v, _), counts = self.route_fn(keys, ts, vals, self.max_parallelism, self.world)
         recv_counts = torch.empty_like(counts)
         dist.all_to_all_single(recv_counts, counts, group=self.group)
-        send = torch.stack([k, t, v.view(torch.int64) if v.dtype != torch.int64 else v], dim=1)
         in_split = counts.tolist()
         out_split = recv_counts.tolist()
-        recv = torch.empty((sum(out_split), 3), dtype=torch.int64, device=send.device)
-        dist.all_to_all_single(recv, send, output_split_sizes=out_split, input_split_sizes=in_split,
-                               group=self.group)
+        total = sum(out_split)
+        # one all-to-all per SoA column, straight from the routed columns into the operator's input
+        # columns: no interleave before the send or split after it (each would cost 48 B/record of HBM)
+        out = []
+        for col in (k, t, v):
+            r = torch.empty(total, dtype=col.dtype, device=col.device)
+            dist.all_to_all_single(r, col, output_split_sizes=out_split, input_split_sizes=in_split,
+                                   group=self.group)
+            out.append(r)
         self.bytes_sent += 24 * (sum(in_split) - in_split[self.rank])
-        rv = recv[:, 2].contiguous()
-        if vals.dtype != torch.int64:
-            rv = rv.view(vals.dtype)
-        return recv[:, 0].contiguous(), recv[:, 1].contiguous(), rv
+        return out[0], out[1], out[2]
 
     def combine_watermark(self, local_wm, device=None):
         """StatusWatermarkValve: the operator's input watermark is the minimum over its channels."""
