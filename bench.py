@@ -83,10 +83,14 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic", default=None,
+                    help="PMC traffic summary (tools/traffic.py); default profiles/traffic_r01[_<workload>].json")
     ap.add_argument("--sub-partitions", type=int, default=0, help="state partitions per key group (0 = auto)")
     args = ap.parse_args()
     preset = PRESETS[args.workload]
+    if args.traffic is None:
+        args.traffic = os.path.join(ROOT, "profiles", "traffic_r01.json" if args.workload == "c2"
+                                    else f"traffic_r01_{args.workload}.json")
     for name in ("keys", "rate", "bound", "jitter", "cpu_sample"):
         if getattr(args, name) is None:
             setattr(args, name, preset[name])
