@@ -78,6 +78,8 @@ def main():
     ap.add_argument("--size", type=int, default=60_000, help="sliding window size (ms, c3)")
     ap.add_argument("--slide", type=int, default=1000, help="sliding window slide (ms, c3)")
     ap.add_argument("--hll-p", type=int, default=14, help="HyperLogLog precision (c5)")
+    ap.add_argument("--no-steady", dest="steady", action="store_false",
+                    help="c3: do not extend the warmup to one window size of event time")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--zipf", type=float, default=None, help="Zipf exponent of the keys (0 = uniform)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -138,26 +140,38 @@ def main():
                            expected_entries=live_windows * args.keys // world,
                            max_batch=args.batch if world == 1 else 2 * args.batch,
                            sub_partitions=args.sub_partitions)
+    if sliding and args.steady:
+        # steady state: the warmup covers one window size of event time, so the timed steps see the
+        # full pane population (size/slide + 1 panes per key) and windows merging size/slide panes
+        event_ms_per_step = args.batch * world * 1000.0 / args.rate
+        args.warmup = max(args.warmup, int(args.size / event_ms_per_step) + 2)
     steps_total = args.warmup + args.steps
     seed = 0x5EED
-    batches, local_max = [], []
-    for s in range(steps_total):
+
+    def generate(s):
         first = (s * world + rank) * args.batch  # global record index of this rank's slice of step s
-        k, t, v, mx = generate_device(seed, first, args.batch, args.keys, ts_base=0, rate=args.rate,
-                                      jitter=args.jitter, cdf_dev=cdf, device=local_rank)
-        batches.append((k, t, v))
-        local_max.append(mx)
-    torch.cuda.synchronize()
+        return generate_device(seed, first, args.batch, args.keys, ts_base=0, rate=args.rate,
+                               jitter=args.jitter, cdf_dev=cdf, device=local_rank)
+
+    # warmup batches are generated step by step (untimed); the timed ones are staged in HBM up front.
     # punctuated watermark of this rank's source after each batch: max ts so far - bound
-    local_wm = []
+    batches, local_wm = {}, {}
     m = -(1 << 63)
-    for mx in local_max:
-        m = max(m, int(mx.item()))
-        local_wm.append(m - args.bound)
+    for s in range(args.warmup, steps_total):
+        k, t, v, mx = generate(s)
+        batches[s] = (k, t, v)
+        local_wm[s] = int(mx.item())  # this batch's max; made cumulative once the warmup's is known
+    torch.cuda.synchronize()
 
     def step(s):
-        k, t, v = batches[s]
-        wm = local_wm[s]
+        nonlocal m
+        if s < args.warmup:
+            k, t, v, mx = generate(s)
+            m = max(m, int(mx.item()))
+            wm = m - args.bound
+        else:
+            k, t, v = batches[s]
+            wm = local_wm[s]
         if world > 1:
             k, t, v = exch.exchange(k, t, v)
             wm = exch.combine_watermark(wm, device=dev)
@@ -172,6 +186,9 @@ def main():
 
     for s in range(args.warmup):
         step(s)
+    for j in range(args.warmup, steps_total):  # fold the warmup's running max into the staged batch maxima
+        m = max(m, local_wm[j])
+        local_wm[j] = m - args.bound
     L = N.lib()
     if not args.no_profile:
         L.fw_profile(op._h, 1)
@@ -259,6 +276,8 @@ def main():
                               "fired_rows": int(fired)},
             "cpu_baseline": cpu,
             "kernels": kernels,
+            "state": {"table_slots": int(st1["table_capacity"]), "table_grows_in_timed_region":
+                      int(st1["table_grows"] - st0["table_grows"]), "live_entries": int(st1["keyed_state_entries"])},
         }
         print(json.dumps(line), flush=True)
     op.close()
