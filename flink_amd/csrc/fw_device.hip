@@ -2097,6 +2097,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, 
 constexpr int PF_THREADS = 1024;
 constexpr int PF_SLOTS = 2048;
 constexpr int PF_LIMIT = 1536;
+constexpr int PF_U = 4;  // region slots per thread in flight in the pane scan
 struct PaneLds {
   uint32_t tag[PF_SLOTS];  // 0 empty, 1 being claimed, 2 full
   int64_t key[PF_SLOTS];
@@ -2180,13 +2181,27 @@ __global__ __launch_bounds__(PF_THREADS) void k_fire_panes(DevCfg c, int64_t wm,
     int64_t en = LMAX, nt = LMAX;
     int dd = 0;
     bool over = false;
-    for (uint32_t s = tid; s < R; s += PF_THREADS) {
-      const uint32_t w = ld_state(rx.state + s);
-      if (st_kind(w) != SLOT_LIVE) {
-        dd += st_kind(w) == SLOT_DEAD;
+    // PF_U slots per thread per step: their state words, then their live entries, are loaded before
+    // any is used, so each thread keeps PF_U loads in flight (one at a time left the scan latency-bound)
+    for (uint32_t s0 = 0; s0 < R; s0 += PF_THREADS * PF_U) {
+      uint32_t w[PF_U];
+#pragma unroll
+      for (int u = 0; u < PF_U; u++) {
+        const uint32_t s = s0 + u * PF_THREADS + tid;
+        w[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
+      }
+      Entry eu[PF_U];
+#pragma unroll
+      for (int u = 0; u < PF_U; u++)
+        if (st_kind(w[u]) == SLOT_LIVE) eu[u] = rx.ent[s0 + u * PF_THREADS + tid];
+#pragma unroll
+      for (int u = 0; u < PF_U; u++) {
+      const uint32_t s = s0 + u * PF_THREADS + tid;
+      if (st_kind(w[u]) != SLOT_LIVE) {
+        dd += st_kind(w[u]) == SLOT_DEAD;
         continue;
       }
-      const Entry e = rx.ent[s];
+      const Entry& e = eu[u];
       const int64_t last_end = jsub(jadd(e.start, c.size), 1);  // maxTimestamp of the pane's last window
       const int64_t lo_e = max(e.meta, floor0);
       if (lo_e > last_end) {  // every window formed by an earlier watermark: GC
@@ -2203,6 +2218,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_fire_panes(DevCfg c, int64_t wm,
       }
       const int64_t cand = max(lo_e, E + c.slide);
       if (E < LMAX - c.slide && cand <= hi_e) en = min(en, cand);
+      }
     }
     if (over) L.over = 1;
     if (en != LMAX) atomicMin(&L.enext, (long long)en);
