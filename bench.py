@@ -48,11 +48,14 @@ PRESETS = {
 }
 
 
-def kernel_bytes(name, n, merged, fired=0, hll_p=0):
-    """Algorithmic bytes of one launch."""
-    if name == "k_fire" and hll_p:
-        # per fired (key, window): read the 64-B entry, read + zero its 2^p register block, write the 56-B row
-        return fired * (64 + 2 * (1 << hll_p) + 56)
+def kernel_bytes(name, n, merged, fired=0, hll_p=0, panes_per_window=0):
+    """Algorithmic bytes of one launch.  `fired` = rows fired per launch."""
+    if name == "k_fire":
+        if hll_p:  # per fired (key, window): the 64-B entry, read + zero its 2^p register block, the 56-B row
+            return fired * (64 + 2 * (1 << hll_p) + 56)
+        if panes_per_window:  # per fired window: its size/slide 64-B panes read, one 56-B row written
+            return fired * (64 * panes_per_window + 56)
+        return fired * (64 + 56)  # per fired window: its entry read, its row written
     if name == "k_classify_hist":
         return 16 * n                      # key + ts
     if name == "k_scatter":
@@ -226,10 +229,15 @@ def main():
             name = L.fw_kernel_name(i).decode()
             if nl[i]:
                 kernels[name] = {"launches": int(nl[i]), "avg_ms": ms[i] / nl[i], "total_ms": ms[i]}
-        dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
         per_launch_records = records / world / args.steps
-        b = kernel_bytes(dom, per_launch_records, merged / args.steps,
-                         fired=fired / kernels[dom]["launches"], hll_p=args.hll_p if hll else 0)
+        # the dominant kernel among those with an algorithmic byte count (all but the tiny scan/slow ones)
+        b = None
+        for dom in sorted(kernels, key=lambda k: -kernels[k]["total_ms"]):
+            b = kernel_bytes(dom, per_launch_records, merged / args.steps,
+                             fired=fired / kernels[dom]["launches"], hll_p=args.hll_p if hll else 0,
+                             panes_per_window=args.size // args.slide if sliding else 0)
+            if b is not None:
+                break
         traffic = None
         if os.path.exists(args.traffic):
             with open(args.traffic) as f:

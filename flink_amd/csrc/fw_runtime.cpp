@@ -619,7 +619,15 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   c.kg0 = cfg.key_group_start;
   c.n_kg = cfg.key_group_end - cfg.key_group_start + 1;
   int64_t s = cfg.sub_partitions;
-  if (s == 0) s = std::max<int64_t>(1, next_pow2(std::max<int64_t>(1, 2048 / c.n_kg)));
+  if (s == 0) {
+    // about 2048 partitions, more when the expected keys would put more than ~512 keys in one: a
+    // partition's (key, window) deltas of a batch must fit k_aggregate's LDS table, or it flushes
+    // several times into its region (C3, 2M keys: 4096 partitions halve k_aggregate's time)
+    const int64_t wins = cfg.assigner == FW_SLIDING ? cfg.size / cfg.slide + 1 : 2;  // live windows per key
+    const int64_t keys = cfg.expected_entries > 0 ? cfg.expected_entries / wins : 0;
+    const int64_t target = std::min<int64_t>(16384, std::max<int64_t>(2048, next_pow2(std::max<int64_t>(1, keys / 512))));
+    s = std::max<int64_t>(1, next_pow2(std::max<int64_t>(1, target / c.n_kg)));
+  }
   c.log_s = ilog2(s);
   c.P = c.n_kg << c.log_s;
   c.size = cfg.size;
