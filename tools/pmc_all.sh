@@ -7,9 +7,9 @@ for w in ${WORKLOADS:-c2 c3 c5}; do
   for counters in FETCH_SIZE WRITE_SIZE; do
     i=$((i+1))
     (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $counters -d "$d/p$i" -o run --output-format csv \
-        -- python3 "$R/bench.py" --workload $w --steps 3 --warmup 1 --no-cpu-baseline --no-profile \
+        -- python3 "$R/bench.py" --workload $w --steps ${PMC_STEPS:-3} --warmup 1 --no-cpu-baseline --no-profile \
         > "$d/p$i.log" 2>&1) || { echo "$w pass $i rc=$?"; tail -5 "$d/p$i.log"; exit 1; }
     echo "$w pass $i ok: $counters"
   done
-  python3 tools/traffic.py "$d" --workload $w --out "gpurun_out/traffic_$w.json" | tail -12
+  python3 tools/traffic.py "$d" --workload $w --last ${PMC_STEPS:-3} --out "gpurun_out/traffic_$w.json" | tail -12
 done

@@ -24,7 +24,7 @@ def short(name):
     return n.split("(")[0].replace("void ", "").split("<")[0].strip()  # k_aggregate<2, false> -> k_aggregate
 
 
-def load(pmc_dir):
+def load(pmc_dir, last=0):
     vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per-dispatch values]
     for f in sorted(glob.glob(os.path.join(pmc_dir, "p*", "run_counter_collection.csv"))):
         per = defaultdict(float)
@@ -36,7 +36,9 @@ def load(pmc_dir):
                 names[r["Dispatch_Id"]] = short(r["Kernel_Name"])
         for (d, cn), v in per.items():
             vals[names[d]][cn].append(v)
-    return {k: {c: sum(v) / len(v) for c, v in cs.items()} | {"_dispatches": max(len(v) for v in cs.values())}
+    # `last`: average only each kernel's last dispatches (the bench's timed steps follow its warmup)
+    cut = (lambda v: v[-last:]) if last else (lambda v: v)
+    return {k: {c: sum(cut(v)) / len(cut(v)) for c, v in cs.items()} | {"_dispatches": max(len(cut(v)) for v in cs.values())}
             for k, cs in vals.items()}
 
 
@@ -46,8 +48,9 @@ def main():
     ap.add_argument("--records", type=int, default=1 << 24, help="records per push (bench --batch)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--workload", default="c2", help="bench --workload the passes ran (recorded for bench.py)")
+    ap.add_argument("--last", type=int, default=0, help="average only each kernel's last N dispatches")
     a = ap.parse_args()
-    k = load(a.pmc_dir)
+    k = load(a.pmc_dir, a.last)
     res = {}
     for name, c in sorted(k.items()):
         rd = c.get("FETCH_SIZE")
