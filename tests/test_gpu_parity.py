@@ -532,3 +532,39 @@ def test_gpu_hll_refuses_unsupported_shapes():
     assert e.value.code == N.FW_ERR_UNSUPPORTED
     with pytest.raises(N.NativeError):
         GpuWindowOperator(TumblingEventTimeWindows.of(1000), HyperLogLog(20))
+
+
+def test_gpu_panes_key_hash_slices():
+    # one state region (maxParallelism 1, one sub-partition) holding 20K keys: a window has more keys
+    # than k_fire_panes' LDS table, so it is formed in slices of the key-hash space
+    cfg = dict(assigner="sliding", size=3000, slide=1000)
+    batches, wms = _stream(200_000, 25_000, 20_000, bound=200, jitter=300, rate=50_000)
+    g, r, *_ = _run_both(cfg, batches, wms, max_parallelism=1, sub_partitions=1, expected_entries=100_000)
+    assert len(g) > 50_000
+    assert_rows_equal(g, r)
+
+
+def test_gpu_panes_hot_partition_split():
+    # Zipf keys in 200K-record batches: the hottest partitions exceed one aggregate workgroup's chunk and
+    # are split (chunk deltas merged by the last chunk) on the pane path
+    cfg = dict(assigner="sliding", size=4000, slide=1000)
+    batches, wms = _stream(600_000, 200_000, 1000, bound=200, jitter=300, rate=100_000, zipf=1.1)
+    g, r, *_ = _run_both(cfg, batches, wms)
+    assert_rows_equal(g, r)
+
+
+def test_gpu_hll_hot_partition_split():
+    # the same split path with HyperLogLog register blocks (blocks are assigned when the merged deltas
+    # are claimed in the region)
+    from flink_amd import HyperLogLog
+    from flink_amd.operator import GpuWindowOperator
+    batches, wms = _stream(600_000, 200_000, 1000, bound=200, jitter=300, rate=100_000, zipf=1.1)
+    gpu = GpuWindowOperator(TumblingEventTimeWindows.of(1000), HyperLogLog(12), expected_entries=10_000)
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000, hll_p=12)
+    for (k, t, v), wm in zip(batches, wms):
+        gpu.process(k, t, v)
+        ref.process(k, t, v)
+        gpu.watermark(wm)
+        ref.watermark(wm)
+    _hll_rows_equal(gpu.rows(), ref.rows())
+    gpu.close()
