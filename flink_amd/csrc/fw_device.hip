@@ -245,11 +245,11 @@ __device__ __forceinline__ void write_row(const DevCfg& c, const DevRows& out, u
   if (c.vtype == FW_VAL_F64) {
     out.sum[pos] = e.sum;
     out.mn[pos] = f64_unsortable(e.mn);
-    out.mx[pos] = f64_unsortable(e.mx);
+    out.mx[pos] = c.agg == FW_AGG_FIRST ? ~e.mx : f64_unsortable(e.mx);
   } else {
     out.sum[pos] = c.vtype == FW_VAL_I32 ? (int64_t)(int32_t)e.sum : e.sum;
     out.mn[pos] = e.mn;
-    out.mx[pos] = e.mx;
+    out.mx[pos] = c.agg == FW_AGG_FIRST ? ~e.mx : e.mx;
   }
 }
 // single-lane emission (ordered path)
@@ -272,19 +272,20 @@ __device__ __forceinline__ void side_one(const DevSide& sd, Status* st, int64_t 
 }
 
 // accumulate one value (AggregateFunction.add of the built-in count/sum/min/max)
-__device__ __forceinline__ void acc_add(const DevCfg& c, Entry& e, int64_t v) {
+// (FW_AGG_FIRST: mx takes ~ordinal `fo` of the record, so the max keeps the first element's ordinal)
+__device__ __forceinline__ void acc_add(const DevCfg& c, Entry& e, int64_t v, int64_t fo) {
   e.cnt += 1;
+  int64_t sv = v;
   if (c.vtype == FW_VAL_F64) {
     double s = __longlong_as_double(e.sum) + __longlong_as_double(v);
     e.sum = __double_as_longlong(s);
-    int64_t sv = f64_sortable(v);
-    e.mn = sv < e.mn ? sv : e.mn;
-    e.mx = sv > e.mx ? sv : e.mx;
+    sv = f64_sortable(v);
   } else {
     e.sum = jadd(e.sum, v);
-    e.mn = v < e.mn ? v : e.mn;
-    e.mx = v > e.mx ? v : e.mx;
   }
+  e.mn = sv < e.mn ? sv : e.mn;
+  const int64_t xv = c.agg == FW_AGG_FIRST ? ~fo : sv;
+  e.mx = xv > e.mx ? xv : e.mx;
 }
 // AggregateFunction.merge
 __device__ __forceinline__ void acc_merge(const DevCfg& c, Entry& a, const Entry& b) {
@@ -584,7 +585,9 @@ __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(D
         }
         continue;
       }
-      store_pair(part, norm, pos, i64x2{k[j], last}, i64x2{v[j], (long long)nwin});
+      // FW_AGG_FIRST: the record's arrival ordinal rides above the window count (nwin < 2^16)
+      const int64_t nwf = c.agg == FW_AGG_FIRST ? ((c.ord_base + i) << 16) | nwin : (int64_t)nwin;
+      store_pair(part, norm, pos, i64x2{k[j], last}, i64x2{v[j], (long long)nwf});
     }
   }
   if (late) atomicAdd(&st->late_dropped, late);
@@ -636,6 +639,7 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_ordered(DevCfg c, i
       stt[pos] = t;
       sv[pos] = v;
       skh[pos] = h;
+      if (c.agg == FW_AGG_FIRST) c.slow_ord[pos] = c.ord_base + i;
     }
     running += tot;
     __syncthreads();
@@ -684,17 +688,18 @@ __device__ __forceinline__ uint32_t lds_hash(int64_t key, int64_t start) {
 __device__ __forceinline__ uint32_t lds_fp(uint32_t h) { return (h >> 8) | 2u; }  // >= 2, never EMPTY/BUSY
 
 // accumulate one value into LDS slot `target` with no-return LDS atomics (nothing waits on the LDS)
-__device__ __forceinline__ void lds_acc(AggLds& L, int target, int vtype, int64_t v) {
+// (first = FW_AGG_FIRST: the max lane takes ~fo, fo = the record's arrival ordinal)
+__device__ __forceinline__ void lds_acc(AggLds& L, int target, int vtype, int64_t v, int64_t fo, bool first) {
   atomicAdd(&L.cnt[target], 1u);
   if (vtype == FW_VAL_F64) {
     atomicAdd((double*)&L.sum[target], __longlong_as_double(v));
     const int64_t sv = f64_sortable(v);
     atomicMin((long long*)&L.mn[target], (long long)sv);
-    atomicMax((long long*)&L.mx[target], (long long)sv);
+    atomicMax((long long*)&L.mx[target], (long long)(first ? ~fo : sv));
   } else {
     atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)v);
     atomicMin((long long*)&L.mn[target], (long long)v);
-    atomicMax((long long*)&L.mx[target], (long long)v);
+    atomicMax((long long*)&L.mx[target], (long long)(first ? ~fo : v));
   }
 }
 
@@ -783,11 +788,11 @@ __device__ __forceinline__ int lds_slot(AggLds& L, int64_t key, int64_t start) {
   return target;
 }
 __device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, int64_t start, int64_t v,
-                                           int diag = 0) {
+                                           int diag = 0, int64_t fo = 0, bool first = false) {
   const int target = lds_slot(L, key, start);
   if (target < 0) return false;
   if (diag & DIAG_AGG_NO_ACCUM) return true;
-  lds_acc(L, target, vtype, v);
+  lds_acc(L, target, vtype, v, fo, first);
   return true;
 }
 
@@ -968,10 +973,10 @@ __device__ __forceinline__ int lds_session_slot(AggLds& L, int64_t* E, int64_t k
   return target;
 }
 __device__ __forceinline__ bool lds_session_upsert(AggLds& L, int64_t* E, int vtype, int64_t key, int64_t ws,
-                                                   int64_t we, int64_t v) {
+                                                   int64_t we, int64_t v, int64_t fo = 0, bool first = false) {
   const int target = lds_session_slot(L, E, key, ws, we);
   if (target < 0) return false;
-  lds_acc(L, target, vtype, v);
+  lds_acc(L, target, vtype, v, fo, first);
   return true;
 }
 
@@ -1278,7 +1283,7 @@ __device__ void agg_spill(const DevCfg& c, AggLds& L, const int64_t* E, Entry* o
 // chunk's deltas into the region with the LDS table and the usual flush, which may suspend; a resumed
 // launch continues phase 2 in the partition's chunk-0 workgroup (prog.rb = delta round, prog.tp = delta
 // of the round per thread).
-template <int RPT, bool SESS>
+template <int RPT, bool SESS, bool FIRST>
 __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __restrict__ part, int64_t begin,
                           int64_t end, int32_t p, int32_t ch, int32_t nch, DevTable& tb, const AggProg& prog,
                           int resume, const AggHot& hot, Status* st) {
@@ -1295,7 +1300,7 @@ __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __
   if (!resume) {
     const int64_t cb = begin + (int64_t)ch * FW_AGG_CHUNK, ce = min(end, cb + (int64_t)FW_AGG_CHUNK);
     for (int64_t rb = cb; rb < ce; rb += (int64_t)blockDim.x * RPT) {
-      int64_t k[RPT], t[RPT], v[RPT];
+      int64_t k[RPT], t[RPT], v[RPT], o[RPT];
 #pragma unroll
       for (int j = 0; j < RPT; j++) {
         const int64_t i = rb + (int64_t)j * blockDim.x + threadIdx.x;
@@ -1308,6 +1313,7 @@ __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __
         k[j] = a.x;
         t[j] = a.y;
         v[j] = b2.x;
+        o[j] = FIRST ? (int64_t)b2.y >> 16 : 0;
       }
       int rj = 0;
       for (;;) {
@@ -1317,9 +1323,9 @@ __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __
           if (failed || j < rj || rb + (int64_t)j * blockDim.x + threadIdx.x >= ce) continue;
           bool in;
           if constexpr (SESS)
-            in = lds_session_upsert(L, E, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j]);
+            in = lds_session_upsert(L, E, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j], o[j], FIRST);
           else
-            in = lds_upsert(L, c.vtype, k[j], t[j], v[j]);
+            in = lds_upsert(L, c.vtype, k[j], t[j], v[j], 0, o[j], FIRST);
           if (!in) {
             failed = true;
             rj = j;
@@ -1428,7 +1434,7 @@ __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __
 // DIAG_AGG_TIMING: per-workgroup phase clocks (s_memtime), summed over the launch and printed by the
 // last workgroup to finish: [0] record loop, [1] flushes, [2] whole workgroup, [3] finished workgroups
 __device__ unsigned long long g_aggt[4];
-template <int RPT, bool SESS>
+template <int RPT, bool SESS, bool FIRST>
 __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? 4 : FW_AGG_WAVES) void k_aggregate(DevCfg c, int64_t wm, const PRec* __restrict__ part,
                                                               const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
                                                               AggProg prog, int resume, Status* st, AggHot hot) {
@@ -1449,7 +1455,7 @@ __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? 4 : FW_AGG_WAVES) void k_agg
     const int32_t nch = (int32_t)(hot.chunk_base[p + 1] - hot.chunk_base[p]);
     if (nch > 1) {
       const int64_t b0 = offs[(int64_t)p * T], e0 = offs[(int64_t)(p + 1) * T];
-      agg_split<RPT, SESS>(c, L, sess_end, part, b0, e0, p, (int32_t)(blockIdx.x - hot.chunk_base[p]), nch, tb, prog,
+      agg_split<RPT, SESS, FIRST>(c, L, sess_end, part, b0, e0, p, (int32_t)(blockIdx.x - hot.chunk_base[p]), nch, tb, prog,
                            resume, hot, st);
       return;
     }
@@ -1485,7 +1491,7 @@ __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? 4 : FW_AGG_WAVES) void k_agg
   const bool timing = c.diag & DIAG_AGG_TIMING;
   unsigned long long tw0 = timing ? __builtin_amdgcn_s_memtime() : 0, tflush = 0;
   for (int64_t rb = srb; rb < end && ok; rb += (int64_t)blockDim.x * RPT) {
-    int64_t k[RPT], t[RPT], v[RPT];
+    int64_t k[RPT], t[RPT], v[RPT], o[RPT];
     int nw[RPT];
 #pragma unroll
     for (int j = 0; j < RPT; j++) {  // all loads in flight before any use
@@ -1499,7 +1505,8 @@ __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? 4 : FW_AGG_WAVES) void k_agg
       k[j] = a.x;
       t[j] = a.y;  // newest window start (assigned by k_scatter)
       v[j] = b2.x;
-      nw[j] = (int)b2.y;
+      nw[j] = FIRST ? (int)(b2.y & 0xffff) : (int)b2.y;
+      o[j] = FIRST ? (int64_t)b2.y >> 16 : 0;  // FW_AGG_FIRST: arrival ordinal
     }
     if (c.diag & DIAG_AGG_NO_LDS) {
 #pragma unroll
@@ -1518,9 +1525,9 @@ __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? 4 : FW_AGG_WAVES) void k_agg
         for (int wi = j == rj ? rwi : 0; wi < nw[j]; wi++) {
           bool in;
           if constexpr (SESS)
-            in = lds_session_upsert(L, sess_end, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j]);
+            in = lds_session_upsert(L, sess_end, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j], o[j], FIRST);
           else
-            in = lds_upsert(L, c.vtype, k[j], jsub(t[j], (int64_t)wi * c.slide), v[j], c.diag);
+            in = lds_upsert(L, c.vtype, k[j], jsub(t[j], (int64_t)wi * c.slide), v[j], c.diag, o[j], FIRST);
           if (!in) {
             failed = true;
             rj = j;
@@ -1620,7 +1627,7 @@ __device__ __forceinline__ int32_t new_slot(const SlowCtx& x, const Region& r, i
 }
 
 // WindowOperator.processElement, non-merging branch (WindowOperator.java:371-407)
-__device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int64_t t, int64_t v, bool* skipped) {
+__device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int64_t t, int64_t v, int64_t fo, bool* skipped) {
   const DevCfg& c = x.c;
   const Region r = region_of(c, x.tb, p, x.tb.cur[p]);
   int64_t last;
@@ -1643,7 +1650,7 @@ __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int6
       if (slot < 0) continue;
     }
     Entry en = r.ent[slot];
-    acc_add(c, en, v);
+    acc_add(c, en, v, fo);
     bool keep = true;
     if (jsub(e, 1) <= x.wm) {  // EventTimeTrigger.onElement -> FIRE (WindowOperator.java:395-401)
       emit_one(c, x.out, x.st, en);
@@ -1662,7 +1669,7 @@ __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int6
 
 // WindowOperator.processElement, merging branch (WindowOperator.java:297-370) with
 // MergingWindowSet.addWindow (MergingWindowSet.java:150-225) over the key's in-flight sessions.
-__device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t, int64_t v, bool* skipped) {
+__device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t, int64_t v, int64_t fo, bool* skipped) {
   const DevCfg& c = x.c;
   const Region r = region_of(c, x.tb, p, x.tb.cur[p]);
   const uint64_t h = slot_hash(c, k, 0);
@@ -1745,7 +1752,7 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
     return;
   }
   *skipped = false;
-  acc_add(c, en, v);
+  acc_add(c, en, v, fo);
   if (jsub(en.end, 1) <= x.wm) {
     emit_one(c, x.out, x.st, en);
     if (c.purging) acc_clear(en);  // FIRE_AND_PURGE clears the contents; the window stays in flight
@@ -1844,12 +1851,13 @@ __global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, 
       for (int j = tid; j < m && ck[j] == ck[tid] && cp[j] == cp[tid]; j++) {
         const int64_t i = b0 + ci[j];
         const int64_t k = sk[i], t = stt[i], v = sv[i];
+        const int64_t fo = c.agg == FW_AGG_FIRST ? c.slow_ord[i] : 0;
         const int32_t p = cp[j];
         bool skipped = true;
         if (c.assigner == FW_SESSION)
-          replay_session(x, p, k, t, v, &skipped);
+          replay_session(x, p, k, t, v, fo, &skipped);
         else
-          replay_time_windows(x, p, k, t, v, &skipped);
+          replay_time_windows(x, p, k, t, v, fo, &skipped);
         if (skipped && jadd(t, c.lateness) <= wm) {  // isSkippedElement && isElementLate
           if (c.side_output)
             side_one(side, st, k, t, v);
@@ -2394,11 +2402,11 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_snapshot(DevCfg c, DevTable
       if (c.vtype == FW_VAL_F64) {
         out.sum[o] = e.sum;
         out.mn[o] = f64_unsortable(e.mn);
-        out.mx[o] = f64_unsortable(e.mx);
+        out.mx[o] = c.agg == FW_AGG_FIRST ? ~e.mx : f64_unsortable(e.mx);
       } else {
         out.sum[o] = c.vtype == FW_VAL_I32 ? (int64_t)(int32_t)e.sum : e.sum;
         out.mn[o] = e.mn;
-        out.mx[o] = e.mx;
+        out.mx[o] = c.agg == FW_AGG_FIRST ? ~e.mx : e.mx;
       }
       // a pane's timer: the maxTimestamp of its next window to form
       out.timer[o] = c.panes ? max(e.meta, tb.pane_floor[p]) : (e.meta & FW_TIMER) ? 1 : 0;
@@ -2439,7 +2447,7 @@ __global__ void k_restore(DevCfg c, int32_t kg, StateCols in, int64_t n, DevTabl
   d.cnt = in.cnt[i];
   d.sum = in.sum[i];
   d.mn = c.vtype == FW_VAL_F64 ? f64_sortable(in.mn[i]) : in.mn[i];
-  d.mx = c.vtype == FW_VAL_F64 ? f64_sortable(in.mx[i]) : in.mx[i];
+  d.mx = c.agg == FW_AGG_FIRST ? ~in.mx[i] : c.vtype == FW_VAL_F64 ? f64_sortable(in.mx[i]) : in.mx[i];
   d.meta = c.panes ? in.timer[i] : in.timer[i] ? FW_TIMER : 0;
   const Region r = region_of(c, tb, p, tb.cur[p]);
   const uint64_t h = slot_hash(c, d.key, c.assigner == FW_SESSION ? 0 : d.start);
@@ -2666,15 +2674,22 @@ void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint
       launch_scan(h.chunk_base, (int64_t)c.P + 1, h.scan_tmp, s);
     }
   }
-  if (c.assigner == FW_SESSION)
-    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb,
-                       prog, resume, st, h);
+  const bool first = c.agg == FW_AGG_FIRST;
+  if (c.assigner == FW_SESSION && first)
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true, true>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs,
+                       T, tb, prog, resume, st, h);
+  else if (c.assigner == FW_SESSION)
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true, false>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs,
+                       T, tb, prog, resume, st, h);
+  else if (first)
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false, true>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part,
+                       offs, T, tb, prog, resume, st, h);
   else if (c.diag & DIAG_AGG_RPT8)
-    hipLaunchKernelGGL((k_aggregate<8, false>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb, prog,
-                       resume, st, h);
+    hipLaunchKernelGGL((k_aggregate<8, false, false>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb,
+                       prog, resume, st, h);
   else
-    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T,
-                       tb, prog, resume, st, h);
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false, false>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part,
+                       offs, T, tb, prog, resume, st, h);
 }
 
 void launch_hll_update(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,

@@ -60,6 +60,10 @@ struct DevCfg {
   // of a pool; an entry's block id is meta >> 1.  Free blocks (zeroed) are kept on a stack:
   // hll_ctr[0] = stack height, hll_ctr[1] = blocks ever handed out from the end of the pool.
   int32_t agg, hll_p;
+  // FW_AGG_FIRST: arrival ordinal of record 0 of the launch's batch (set per push by the host).  The
+  // entry's mx holds ~ordinal of the window's first element, so the max merges everywhere keep it.
+  int64_t ord_base;
+  int64_t* slow_ord;  // [max_batch] ordinal of each ordered-path record (the push's scratch set)
   uint8_t* hll_regs;
   uint32_t* hll_free;
   int32_t* hll_ctr;

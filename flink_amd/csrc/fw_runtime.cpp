@@ -37,6 +37,7 @@ struct Scratch {
   PRec* part = nullptr;          // the batch's normal records, partition-major
   int64_t *sk = nullptr, *stt = nullptr, *sv = nullptr;  // ordered-path list
   int32_t* skh = nullptr;
+  int64_t* so = nullptr;         // FW_AGG_FIRST: arrival ordinal of each ordered-path record
   int32_t T = 0;                 // tiles of the batch that used this set
   int64_t n = 0;                 // records of the batch
   bool split = false;            // its aggregate split long partitions (fw_op::hot)
@@ -171,6 +172,7 @@ int alloc_scratch(fw_op* op, Scratch& s, int64_t mb, int64_t m) {
   HIP_OR_RETURN(op, dmalloc(&s.stt, mb));
   HIP_OR_RETURN(op, dmalloc(&s.sv, mb));
   HIP_OR_RETURN(op, dmalloc(&s.skh, mb));
+  if (op->cfg.aggregate == FW_AGG_FIRST) HIP_OR_RETURN(op, dmalloc(&s.so, mb));
   return FW_OK;
 }
 void free_scratch(Scratch& s) {
@@ -181,6 +183,7 @@ void free_scratch(Scratch& s) {
   dfree(s.stt);
   dfree(s.sv);
   dfree(s.skh);
+  dfree(s.so);
 }
 
 // buffers of the split-partition aggregate (AggHot): deltas at record indices, so one Entry per record
@@ -399,8 +402,9 @@ int settle(fw_op* op) {
     if ((rc = put_status_field(op, &Status::suspended)) || (rc = put_status_field(op, &Status::need_live)) ||
         (rc = put_status_field(op, &Status::need_out)))
       return rc;
-    const DevCfg& c = op->dc;
     const Scratch& S = op->sc[op->last_sc];
+    DevCfg c = op->dc;
+    c.slow_ord = S.so;
     if (susp & FW_SUSP_AGG)
       timed(op, K_AGGREGATE, [&] {
         fwdev::launch_aggregate(c, S.wm, S.part, S.hist, S.T, op->tb, op->prog, 1, S.split ? &op->hot : nullptr, S.n,
@@ -490,6 +494,8 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   }
   const int nxt = op->last_sc ^ 1;
   Scratch& S = op->sc[nxt];
+  c.ord_base = op->records_in;  // FW_AGG_FIRST: arrival ordinals of this batch start here
+  c.slow_ord = S.so;
   const int32_t T = (int32_t)((n + FW_TILE - 1) / FW_TILE);
   const int64_t m = (int64_t)(c.P + 1) * T;
   if (c.assigner == FW_SESSION) {
@@ -517,7 +523,9 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   const int64_t rows = (int64_t)op->h_status->out_rows;
   const int64_t chunk_rows = (int64_t)FW_SLOW_THREADS * (c.assigner == FW_SESSION ? 1 : c.wpr);
   if ((rc = ensure_out_capacity(op, rows + op->table_slots + chunk_rows, rows))) return rc;
-  const DevCfg& cc = op->dc;  // settle may have grown the table
+  DevCfg cc = op->dc;  // settle may have grown the table
+  cc.ord_base = c.ord_base;
+  cc.slow_ord = S.so;
   // a partition can outgrow one aggregate workgroup (hot keys) only when the batch is longer than a chunk
   const bool split = (cc.wpr == 1 || cc.panes) && n > FW_AGG_CHUNK;
   if (split && (rc = ensure_hot(op))) return rc;
@@ -584,7 +592,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     snprintf(msg, sizeof msg, "invalid KeyGroupRange [%d, %d]", cfg.key_group_start, cfg.key_group_end);
   if (!msg[0] && cfg.sub_partitions != 0 && (cfg.sub_partitions & (cfg.sub_partitions - 1)))
     snprintf(msg, sizeof msg, "sub_partitions must be a power of two");
-  if (!msg[0] && (cfg.aggregate < FW_AGG_COUNT_SUM_MIN_MAX || cfg.aggregate > FW_AGG_HLL))
+  if (!msg[0] && (cfg.aggregate < FW_AGG_COUNT_SUM_MIN_MAX || cfg.aggregate > FW_AGG_FIRST))
     snprintf(msg, sizeof msg, "unknown aggregate %d", cfg.aggregate);
   const int32_t hll_p = cfg.hll_precision ? cfg.hll_precision : 14;
   if (!msg[0] && cfg.aggregate == FW_AGG_HLL && (hll_p < 4 || hll_p > 16))
@@ -594,6 +602,11 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
       (cfg.assigner != FW_TUMBLING || cfg.allowed_lateness != 0 || cfg.value_type != FW_VAL_I64)) {
     snprintf(msg, sizeof msg, "the HyperLogLog aggregate is offered for tumbling windows without allowed lateness "
                               "over a Long item column");
+    unsupported = true;
+  }
+  if (!msg[0] && cfg.aggregate == FW_AGG_FIRST && cfg.assigner == FW_SLIDING && cfg.slide > 0 &&
+      (cfg.size + cfg.slide - 1) / cfg.slide > 65535) {
+    snprintf(msg, sizeof msg, "the first-element aggregate takes at most 65535 windows per element");
     unsupported = true;
   }
   fw_op* op = new fw_op();
@@ -647,6 +660,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     make_div_inv((uint64_t)c.slide, &c.mag_slide, &c.l_slide);
   }
   const int64_t expected = cfg.expected_entries > 0 ? cfg.expected_entries : (int64_t)c.P * 512;
+  if (cfg.aggregate == FW_AGG_FIRST) c.agg = FW_AGG_FIRST;
   if (cfg.aggregate == FW_AGG_HLL) {
     // register pool: one 2^p-byte block per live (key, window); expected_entries live entries, plus
     // a quarter for entries created before the watermark that retires their predecessors

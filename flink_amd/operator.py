@@ -46,7 +46,7 @@ class GpuWindowOperator:
             setattr(c, k, v)
         c.value_type = aggregate.native()
         c.hll_precision = aggregate.hll_precision()
-        c.aggregate = N.FW_AGG_HLL if c.hll_precision else N.FW_AGG_COUNT_SUM_MIN_MAX
+        c.aggregate = aggregate.aggregate_kind()
         c.key_kind = _KEY_KINDS[key_type]
         c.purging = int(trigger.purging)
         c.side_output = int(side_output)

@@ -160,6 +160,44 @@ class CountSumMinMax:
     def hll_precision(self):
         return 0
 
+    def aggregate_kind(self):
+        return N.FW_AGG_COUNT_SUM_MIN_MAX
+
+
+@dataclass(frozen=True)
+class FirstElementReduce:
+    """The reduce aggregations `sum(pos)` / `min(pos)` of WindowedStream (WindowedStream.java:1354-1439):
+    a ReducingState (HeapReducingState.add, HeapReducingState.java:72-84) whose reduce keeps a copy of
+    its FIRST argument with the field replaced (SumAggregator.reduce, SumAggregator.java:66-76;
+    ComparableAggregator.reduce, ComparableAggregator.java:72-94).  The GPU keeps count/sum/min of the
+    field and the arrival ordinal of the window's first element (fired rows: max = that ordinal);
+    `first_element_results` rebuilds the reference's output tuples from it.  Merged sessions keep the
+    earlier element (the reference's choice follows HashSet order: parity unpinned)."""
+    value_type: str = "int"
+
+    def native(self):
+        return {"long": N.FW_VAL_I64, "int": N.FW_VAL_I32, "double": N.FW_VAL_F64}[self.value_type]
+
+    def hll_precision(self):
+        return 0
+
+    def aggregate_kind(self):
+        return N.FW_AGG_FIRST
+
+
+def first_element_results(rows, elements, pos, field="sum"):
+    """The output tuples of `sum(pos)` (field "sum") or `min(pos)` (field "min") from fired rows of a
+    FirstElementReduce operator: a copy of the window's first element (its arrival ordinal is the row's
+    `max`) with field `pos` replaced, as SumAggregator.reduce / ComparableAggregator.reduce leave it
+    (SumAggregator.java:66-76, ComparableAggregator.java:72-94).  `elements[i]` is the i-th element the
+    operator was given (the caller keeps the passthrough fields; the GPU keeps only the ordinal)."""
+    out = []
+    for r in rows:
+        t = list(elements[int(r["max"])])
+        t[pos] = int(r[field])
+        out.append(tuple(t))
+    return out
+
 
 @dataclass(frozen=True)
 class HyperLogLog:
@@ -177,3 +215,6 @@ class HyperLogLog:
 
     def hll_precision(self):
         return self.precision
+
+    def aggregate_kind(self):
+        return N.FW_AGG_HLL

@@ -52,6 +52,15 @@ extern "C" {
                                       count, sum = estimate (f64 bits), min = zero registers, max = the
                                       low 64 bits of sum_j 2^(65-p-M[j]).  Tumbling windows, no allowed
                                       lateness; expected_entries sizes the register pool (2^p B/entry). */
+#define FW_AGG_FIRST 2             /* the reduce aggregations sum(pos) / min(pos) of DataStream / WindowedStream
+                                      (SumAggregator.java:66-76, ComparableAggregator.java:72-94 over
+                                      HeapReducingState.add, HeapReducingState.java:72-84): the result is a
+                                      copy of the FIRST element of the window with the field replaced.  Rows
+                                      carry count, sum, min as usual and max = the arrival ordinal of that
+                                      first element (0-based index of the record among all records pushed
+                                      into the handle), from which the caller takes the passthrough fields.
+                                      Merged sessions keep the smaller ordinal.  At most 65535 windows per
+                                      record. */
 
 #define FW_KEY_LONG 0   /* key is a Long: hashCode = (int)(v ^ (v >>> 32))               */
 #define FW_KEY_INT 1    /* key is an Integer: hashCode = value                              */

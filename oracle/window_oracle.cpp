@@ -93,6 +93,7 @@ struct Acc {
   int64_t imn = 0, imx = 0;
   double dmn = 0.0, dmx = 0.0;
   std::vector<uint8_t> regs;  // OR_AGG_HLL registers (2^p)
+  int64_t first = 0;          // OR_AGG_FIRST: arrival ordinal of the element that created the state
 };
 
 // ---------------------------------------------------------------- HyperLogLog (window_oracle.h)
@@ -198,7 +199,11 @@ class WindowOperatorOracle {
   bool is_merging() const { return cfg.assigner == OR_SESSION; }
 
   // ------------------------------------------------ accumulator (CountSumMinMax)
+  // (OR_AGG_FIRST: HeapReducingState.add, HeapReducingState.java:72-84 — the element that finds no
+  // state becomes it, and SumAggregator.reduce / ComparableAggregator.reduce keep a copy of their first
+  // argument (SumAggregator.java:66-76, ComparableAggregator.java:72-94): the first element survives)
   void acc_add(Acc& a, int64_t v) const {
+    if (a.cnt == 0) a.first = ordinal;
     if (cfg.aggregate == OR_AGG_HLL) {
       if (a.regs.empty()) a.regs.assign((size_t)1 << cfg.hll_p, 0);
       hll_add(a.regs, cfg.hll_p, (uint64_t)v);
@@ -231,6 +236,10 @@ class WindowOperatorOracle {
     if (b.cnt == 0) return a;
     Acc r = a;
     r.cnt = a.cnt + b.cnt;
+    // OR_AGG_FIRST: mergeState(a, b) = reduce(a, b) keeps a's first element (HeapReducingState.java:91-93),
+    // and which state window is `a` follows HashSet order in the reference (AbstractHeapMergingState.java
+    // :67-93, MergingWindowSet.java:190-205): parity unpinned, defined here as the earlier element
+    r.first = std::min(a.first, b.first);
     if (cfg.aggregate == OR_AGG_HLL) {
       for (size_t j = 0; j < r.regs.size(); j++) r.regs[j] = std::max(r.regs[j], b.regs[j]);
       return r;
@@ -293,6 +302,7 @@ class WindowOperatorOracle {
       r.min = a.imn;
       r.max = a.imx;
     }
+    if (cfg.aggregate == OR_AGG_FIRST) r.max = a.first;
     r.epoch = epoch;
     rows.push_back(r);
   }
@@ -414,7 +424,9 @@ class WindowOperatorOracle {
 
   // ------------------------------------------------ WindowOperator.processElement (:291-421)
   std::vector<TW> wbuf;
+  int64_t ordinal = -1;  // arrival ordinal of the element being processed
   void process_element(int64_t key, int64_t ts, int64_t val) {
+    ordinal++;
     assign(ts, wbuf);
     bool skipped = true;
     if (is_merging()) {

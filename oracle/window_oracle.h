@@ -68,7 +68,9 @@ typedef struct {
  *   correction with a 64-bit hash).
  * Row: count = elements, sum = E (f64 bits), min = V, max = low 64 bits of S (an exact register
  * checksum).  AggregateFunction.merge = register-wise max. */
-enum { OR_AGG_COUNT_SUM_MIN_MAX = 0, OR_AGG_HLL = 1 };
+/* OR_AGG_FIRST: count/sum/min with max = arrival ordinal of the window's first element (the passthrough
+ * fields of sum(pos)/min(pos)); ordinals count every element processed, from 0. */
+enum { OR_AGG_COUNT_SUM_MIN_MAX = 0, OR_AGG_HLL = 1, OR_AGG_FIRST = 2 };
 
 /* One fired row.  sum/min/max hold i64 values (I64/I32) or f64 bit patterns (F64).
  * epoch = number of watermarks fully processed before the row was emitted, so

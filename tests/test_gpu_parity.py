@@ -6,7 +6,7 @@ import pytest
 from flink_amd import (EventTimeSessionWindows, KeyGroupRange, PurgingTrigger, SlidingEventTimeWindows,
                        EventTimeTrigger, TumblingEventTimeWindows)
 from flink_amd.datagen import generate_host
-from flink_amd.windowing import CountSumMinMax
+from flink_amd.windowing import CountSumMinMax, FirstElementReduce, first_element_results
 from oracle import oracle as orc
 from tests.kat_util import expected_counters, load_kats, replay, row_counters
 from tests.parity_util import assert_rows_equal, assert_side_equal
@@ -18,7 +18,7 @@ _VT = {"i64": "long", "i32": "int", "f64": "double"}
 
 
 def _gpu_op(assigner, size=0, slide=0, offset=0, gap=0, lateness=0, purging=False, side_output=False,
-            value_type="i64", **kw):
+            value_type="i64", first=False, **kw):
     from flink_amd.operator import GpuWindowOperator
     if assigner == "tumbling":
         a = TumblingEventTimeWindows.of(size, offset)
@@ -27,7 +27,8 @@ def _gpu_op(assigner, size=0, slide=0, offset=0, gap=0, lateness=0, purging=Fals
     else:
         a = EventTimeSessionWindows.with_gap(gap)
     trig = PurgingTrigger.of(EventTimeTrigger.create()) if purging else EventTimeTrigger.create()
-    return GpuWindowOperator(a, CountSumMinMax(_VT[value_type]), trig, allowed_lateness=lateness,
+    agg = FirstElementReduce(_VT[value_type]) if first else CountSumMinMax(_VT[value_type])
+    return GpuWindowOperator(a, agg, trig, allowed_lateness=lateness,
                              side_output=side_output, **kw)
 
 
@@ -114,6 +115,48 @@ def test_gpu_vs_oracle_out_of_order(cfg):
     assert_rows_equal(g, r, _VT[vt])
     assert_side_equal(gs, rs)
     assert gl == rl
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=[str(i) for i in range(len(CONFIGS))])
+def test_gpu_first_element_vs_oracle(cfg):
+    # a9: sum(pos)/min(pos) keep the window's first element; the rows' max is its arrival ordinal,
+    # carried through the parallel path (k_scatter -> k_aggregate), the ordered replay (late firings,
+    # sessions of tainted keys), pane windows and session merges
+    vt = cfg.get("value_type", "i64")
+    batches, wms = _stream(120_000, 10_000, 5000, bound=400, jitter=1500, rate=100_000, value_type=vt)
+    g, r, gs, rs, gl, rl = _run_both(dict(cfg, first=True), batches, wms)
+    assert_rows_equal(g, r, _VT[vt])
+    assert_side_equal(gs, rs)
+    assert gl == rl
+
+
+@pytest.mark.parametrize("cfg", [dict(assigner="tumbling", size=100), dict(assigner="session", gap=20),
+                                 dict(assigner="sliding", size=400, slide=100)], ids=["tumbling", "session", "panes"])
+def test_gpu_first_element_hot_keys(cfg):
+    # Zipf keys over multi-batch pushes: hot partitions are split over aggregate workgroups and the
+    # chunks' deltas merged, with the first element's ordinal surviving the merge
+    batches, wms = _stream(1 << 19, 1 << 18, 10_000, bound=50, jitter=50, rate=1_000_000, zipf=1.1)
+    g, r, gs, rs, gl, rl = _run_both(dict(cfg, first=True), batches, wms)
+    assert_rows_equal(g, r)
+    assert gl == rl
+
+
+def test_gpu_session_example_sum_passthrough():
+    # SessionWindowing example (SWE:57-83): keyBy(0).window(sessions, gap 3).sum(2) emits a copy of the
+    # session's first element with field 2 summed; EXPECTED (SWD:26-27) pinned exactly
+    ex = KATS["session_example"]
+    names = sorted({r[0] for r in ex["input"]})
+    ids = {n: i for i, n in enumerate(names)}
+    op = _gpu_op("session", gap=ex["gap"], value_type="i32", first=True, key_type="int")
+    rows = []
+    for name, ts, val in ex["input"]:
+        op.process(np.array([ids[name]], dtype=np.int64), np.array([ts], dtype=np.int64),
+                   np.array([val], dtype=np.int64))
+        op.watermark(ts - 1)
+    op.watermark((1 << 63) - 1)
+    got = first_element_results(op.rows(), [tuple(e) for e in ex["input"]], 2, "sum")
+    op.close()
+    assert sorted(got) == sorted(tuple(e) for e in ex["expected"])
 
 
 def test_gpu_vs_oracle_c2_shape():

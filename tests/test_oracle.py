@@ -72,6 +72,38 @@ def test_session_example_kat():
     assert got == Counter(tuple(e) for e in ex["expected"])
 
 
+def test_session_example_sum_passthrough_kat():
+    # a9: sum(2) keeps the session's FIRST element (SumAggregator.java:66-76); the first-element reduce
+    # reports its arrival ordinal, from which the passthrough fields are taken
+    from flink_amd.windowing import first_element_results
+    ex = KATS["session_example"]
+    names = sorted({r[0] for r in ex["input"]})
+    ids = {n: i for i, n in enumerate(names)}
+    op = orc.WindowOperatorOracle(assigner="session", gap=ex["gap"], value_type="i32", first=True)
+    for name, ts, val in ex["input"]:
+        op.process(np.array([ids[name]]), np.array([ts]), np.array([val]))
+        op.watermark(ts - 1)
+    op.watermark((1 << 63) - 1)
+    got = first_element_results(op.rows(), [tuple(e) for e in ex["input"]], 2, "sum")
+    assert sorted(got) == sorted(tuple(e) for e in ex["expected"])
+
+
+def test_first_element_reduce_keeps_first_across_merges():
+    # tumbling: the ordinal is the first element added to each window; sessions: a bridging element
+    # merges two sessions and the earlier first element survives
+    op = orc.WindowOperatorOracle(assigner="tumbling", size=10, first=True)
+    op.process(np.array([1, 2, 1, 1]), np.array([5, 3, 2, 15]), np.array([10, 20, 30, 40]))
+    op.watermark((1 << 63) - 1)
+    got = sorted((int(r["key"]), int(r["start"]), int(r["count"]), int(r["sum"]), int(r["min"]), int(r["max"]))
+                 for r in op.rows())
+    assert got == [(1, 0, 2, 40, 10, 0), (1, 10, 1, 40, 40, 3), (2, 0, 1, 20, 20, 1)]
+    op = orc.WindowOperatorOracle(assigner="session", gap=30, first=True)
+    op.process(np.array([7, 7, 7]), np.array([100, 50, 75]), np.array([1, 2, 3]))
+    op.watermark((1 << 63) - 1)
+    rows = op.rows()
+    assert len(rows) == 1 and rows[0]["count"] == 3 and rows[0]["max"] == 0 and rows[0]["start"] == 50
+
+
 def _closed_form_stream(num_keys, n_per_key):
     keys, ts, vals, wms = [], [], [], []
     for nxt in range(n_per_key):
