@@ -74,6 +74,13 @@ def lib():
         L.oracle_run_parallel.restype = ctypes.c_int64
         L.oracle_run_parallel.argtypes = [ctypes.POINTER(OracleCfg), I64P, I64P, I64P, ctypes.c_int64, ctypes.c_int64,
                                           I64P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, I64P]
+        L.oracle_count_create.restype = P
+        L.oracle_count_create.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]
+        L.oracle_count_destroy.argtypes = [P]
+        L.oracle_count_process.argtypes = [P, I64P, I64P, ctypes.c_int64]
+        L.oracle_count_num_rows.restype = ctypes.c_int64
+        L.oracle_count_num_rows.argtypes = [P]
+        L.oracle_count_get_rows.argtypes = [P, P]
         _lib = L
     return _lib
 
@@ -160,6 +167,37 @@ class WindowOperatorOracle:
     @property
     def num_timers(self):
         return lib().oracle_num_timers(self._h)
+
+
+class CountWindowOracle:
+    """a14: countWindow(size, slide).sum(pos) — GlobalWindows + CountTrigger + CountEvictor (evict before the
+    window function, or after it with evict_after=True); see window_oracle.h.  Rows have max = the arrival
+    ordinal of the first reduced element (flink_amd.windowing.first_element_results rebuilds the tuples)."""
+
+    def __init__(self, size, slide, evict_after=False, value_type="i32"):
+        self._h = lib().oracle_count_create(size, slide, int(evict_after), _VALTYPES[value_type])
+        if not self._h:
+            raise ValueError("count window size and slide must be positive")
+
+    def close(self):
+        if self._h:
+            lib().oracle_count_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def process(self, keys, vals):
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        vals = np.ascontiguousarray(vals, dtype=np.int64)
+        lib().oracle_count_process(self._h, _i64p(keys), _i64p(vals), len(keys))
+
+    def rows(self):
+        n = lib().oracle_count_num_rows(self._h)
+        out = np.zeros(n, dtype=ROW_DTYPE)
+        if n:
+            lib().oracle_count_get_rows(self._h, out.ctypes.data)
+        return out
 
 
 def key_groups_long(keys, max_par):

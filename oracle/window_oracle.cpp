@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <queue>
 #include <set>
@@ -528,7 +529,75 @@ class WindowOperatorOracle {
 }  // namespace
 
 // =========================================================================== C API
+// ---------------------------------------------------------------- a14: count windows (C1 CPU reference)
+// KeyedStream.countWindow(size, slide) = window(GlobalWindows.create()).evictor(CountEvictor.of(size))
+//   .trigger(CountTrigger.of(slide)) (KeyedStream.java:383-397).
+// EvictingWindowOperator.processElement (EvictingWindowOperator.java:102-239): the element is appended to
+// the window's ListState; CountTrigger.onElement (CountTrigger.java:47-55) adds 1 to its count and FIREs
+// (clearing the count) when it reaches `slide`.  emitWindowContents (:334-366): evictBefore, the window
+// function over the remaining elements, evictAfter; the evictor removes from the front
+// (CountEvictor.evict, CountEvictor.java:63-78: keep the last maxCount).  GlobalWindow never fires by time.
+struct CountWindowOracle {
+  CountWindowOracle(int64_t sz, int64_t sl, bool after, int32_t vt)
+      : size(sz), slide(sl), evict_after(after), value_type(vt) {}
+  int64_t size, slide;
+  bool evict_after;
+  int32_t value_type;
+  int64_t ordinal = -1;
+  struct Elem {
+    int64_t val, ord;
+  };
+  struct KeyState {
+    std::deque<Elem> list;
+    int64_t count = 0;  // CountTrigger's ReducingState
+  };
+  std::unordered_map<int64_t, KeyState> state;
+  std::vector<oracle_row> rows;
+
+  void evict(std::deque<Elem>& l) const {
+    while ((int64_t)l.size() > size) l.pop_front();
+  }
+  void process(int64_t key, int64_t val) {
+    ordinal++;
+    KeyState& s = state[key];
+    s.list.push_back(Elem{val, ordinal});
+    if (++s.count < slide) return;
+    s.count = 0;
+    if (!evict_after) evict(s.list);
+    // ReduceApplyWindowFunction over the iterable, SumAggregator.reduce: first element kept, field summed
+    oracle_row r{};
+    r.key = key;
+    r.start = LMIN;
+    r.end = LMAX;
+    r.count = (int64_t)s.list.size();
+    r.min = LMAX;
+    for (const Elem& e : s.list) {
+      r.sum = jadd(r.sum, e.val);
+      r.min = std::min(r.min, e.val);
+    }
+    if (value_type == OR_VAL_I32) r.sum = (int64_t)(int32_t)r.sum;
+    r.max = s.list.front().ord;
+    rows.push_back(r);
+    if (evict_after) evict(s.list);
+  }
+};
+
 extern "C" {
+
+void* oracle_count_create(int64_t size, int64_t slide, int32_t evict_after, int32_t value_type) {
+  if (size <= 0 || slide <= 0) return nullptr;
+  return new CountWindowOracle(size, slide, evict_after != 0, value_type);
+}
+void oracle_count_destroy(void* op) { delete static_cast<CountWindowOracle*>(op); }
+void oracle_count_process(void* op, const int64_t* key, const int64_t* val, int64_t n) {
+  auto* o = static_cast<CountWindowOracle*>(op);
+  for (int64_t i = 0; i < n; i++) o->process(key[i], val[i]);
+}
+int64_t oracle_count_num_rows(void* op) { return (int64_t)static_cast<CountWindowOracle*>(op)->rows.size(); }
+void oracle_count_get_rows(void* op, oracle_row* out) {
+  auto* o = static_cast<CountWindowOracle*>(op);
+  std::copy(o->rows.begin(), o->rows.end(), out);
+}
 
 void* oracle_create(const oracle_cfg* cfg) { return new WindowOperatorOracle(*cfg); }
 void oracle_destroy(void* op) { delete static_cast<WindowOperatorOracle*>(op); }

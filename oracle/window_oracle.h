@@ -90,6 +90,18 @@ void    oracle_destroy(void* op);
 int     oracle_process(void* op, const int64_t* key, const int64_t* ts, const int64_t* val, int64_t n);
 int     oracle_watermark(void* op, int64_t wm);
 int64_t oracle_num_rows(void* op);
+/* a14 — count windows (SURVEY §8a, config C1 CPU reference): GlobalWindows + CountTrigger.of(slide) +
+ * CountEvictor.of(size, evict_after) over a ListState of elements, the window function reducing the
+ * remaining elements in order with sum (KeyedStream.countWindow(size, slide).sum(pos),
+ * KeyedStream.java:383-397; EvictingWindowOperator.java:102-239,334-366).  Rows: start = Long.MIN_VALUE,
+ * end = Long.MAX_VALUE (GlobalWindow; row timestamp Long.MAX_VALUE), count = elements reduced,
+ * sum (wrapped to value_type width), min, max = arrival ordinal of the first reduced element (the
+ * passthrough fields of sum(pos), as OR_AGG_FIRST). */
+void*   oracle_count_create(int64_t size, int64_t slide, int32_t evict_after, int32_t value_type);
+void    oracle_count_destroy(void* op);
+void    oracle_count_process(void* op, const int64_t* key, const int64_t* val, int64_t n);
+int64_t oracle_count_num_rows(void* op);
+void    oracle_count_get_rows(void* op, oracle_row* out);
 void    oracle_get_rows(void* op, oracle_row* out);       /* copies all rows emitted so far */
 void    oracle_clear_rows(void* op);
 int64_t oracle_num_side_rows(void* op);

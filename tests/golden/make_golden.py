@@ -11,6 +11,7 @@ Paths are relative to /root/reference.  Abbreviations:
   CEP = flink-libraries/flink-cep/src/test/java/org/apache/flink/cep/operator/CEPRescalingTest.java
   SWD = flink-examples/flink-examples-streaming/src/main/java/org/apache/flink/streaming/examples/windowing/util/SessionWindowingData.java
   SWE = flink-examples/flink-examples-streaming/src/main/java/org/apache/flink/streaming/examples/windowing/SessionWindowing.java
+  EWO = flink-streaming-java/src/test/java/org/apache/flink/streaming/runtime/operators/windowing/EvictingWindowOperatorTest.java
   EWC = flink-tests/src/test/java/org/apache/flink/test/checkpointing/AbstractEventTimeWindowCheckpointingITCase.java
 
 Operator cases use the vocabulary of the harness: ("e", key, value, timestamp) is
@@ -157,6 +158,21 @@ SESSION_EXAMPLE = {
     "expected": [["a", 1, 1], ["c", 6, 1], ["c", 11, 1], ["b", 1, 3], ["a", 10, 1]],
 }
 
+# a14: EvictingWindowOperator over GlobalWindows with CountTrigger.of(slide) and CountEvictor.of(size[, after]);
+# elements ("key", value) in order (timestamps are ignored by GlobalWindows); `expected` rows are
+# (key, summed value) with timestamp Long.MAX_VALUE, compared as a sorted multiset after each phase.
+_EW_INPUT = [["key2", 1], ["key2", 1], ["key1", 1], ["key1", 1], ["key1", 1], ["key2", 1], ["key2", 1],
+             ["key2", 1]]
+COUNT_WINDOWS = [
+    {"name": "count_evictor_evict_after", "source": "EWO:73-142", "size": 4, "slide": 2, "evict_after": True,
+     "phases": [{"input": _EW_INPUT, "expected": [["key2", 2], ["key2", 4], ["key1", 2]]},
+                {"input": [["key1", 1], ["key2", 1]], "expected": [["key1", 4], ["key2", 6]]},
+                {"input": [["key2", 1], ["key2", 1]], "expected": [["key2", 6]]}]},
+    {"name": "count_trigger_evict_before", "source": "EWO:505-572", "size": 4, "slide": 2, "evict_after": False,
+     "phases": [{"input": _EW_INPUT, "expected": [["key2", 2], ["key2", 4], ["key1", 2]]},
+                {"input": [["key1", 1], ["key2", 1]], "expected": [["key1", 4], ["key2", 4]]}]},
+]
+
 KEY_GROUPS = {
     "source": "CEP:71-82,170-215 (Integer keys: hashCode == value)",
     "max_parallelism": 10,
@@ -207,7 +223,7 @@ CLOSED_FORM = {"source": "EWC:571-629,659-740,865-877", "num_keys": 20, "num_ele
 
 
 def main():
-    out = {"keys": KEYS, "operator_cases": CASES, "session_example": SESSION_EXAMPLE, "key_groups": KEY_GROUPS,
+    out = {"keys": KEYS, "operator_cases": CASES, "session_example": SESSION_EXAMPLE, "count_windows": COUNT_WINDOWS, "key_groups": KEY_GROUPS,
            "window_start": WINDOW_START, "assigners": ASSIGNERS, "closed_form": CLOSED_FORM}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_kats.json")
     with open(path, "w") as f:

@@ -159,6 +159,44 @@ def test_gpu_session_example_sum_passthrough():
     assert sorted(got) == sorted(tuple(e) for e in ex["expected"])
 
 
+def _word_stream(n, n_words, seed=0x5EED):
+    """C1 shape: uniformly drawn words (String keys: the key column is the word's dictionary id,
+    key_hash its String.hashCode), value 1 (Integer), ts = i / 2000 ms (5 s of event time per 1e7 tokens)."""
+    from flink_amd.keygroups import string_hash_code
+    words = [f"w{j}" for j in range(n_words)]
+    hashes = np.array([string_hash_code(w) for w in words], dtype=np.int32)
+    keys, _, _ = generate_host(seed, 0, n, n_words, ts_base=0, rate=1000, jitter=1)
+    ts = np.arange(n, dtype=np.int64) // 2000
+    return words, keys, hashes[keys], ts, np.ones(n, dtype=np.int64)
+
+
+@pytest.mark.parametrize("first", [False, True], ids=["count_sum", "sum_passthrough"])
+def test_gpu_word_count_hashed_keys(first):
+    # C1 (ii): keyBy(word).window(TumblingEventTimeWindows.of(5 s)).sum(1) with String keys hashed by the host
+    # (FW_KEY_HASHED: key groups from String.hashCode, KeyGroupRangeAssignment.java:58-71) on the GPU
+    words, keys, kh, ts, vals = _word_stream(200_000, 170)
+    gpu = _gpu_op("tumbling", size=5000, value_type="i32", first=first, key_type="hashed")
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=5000, value_type="i32", first=first)
+    step = 25_000
+    for b in range(0, len(keys), step):
+        sl = slice(b, b + step)
+        gpu.process(keys[sl], ts[sl], vals[sl], key_hash=kh[sl])
+        ref.process(keys[sl], ts[sl], vals[sl])
+        gpu.watermark(int(ts[sl].max()))
+        ref.watermark(int(ts[sl].max()))
+    gpu.watermark((1 << 63) - 1)
+    ref.watermark((1 << 63) - 1)
+    g, r = gpu.rows(), ref.rows()
+    gpu.close()
+    assert_rows_equal(g, r, "int")
+    assert int(g["count"].sum()) == len(keys)
+    if first:
+        elements = [(words[k], 1) for k in keys]
+        got = first_element_results(g, elements, 1, "sum")
+        assert sorted(got) == sorted(first_element_results(r, elements, 1, "sum"))
+        assert all(t[0] == words[int(row["key"])] for t, row in zip(got, g))
+
+
 def test_gpu_vs_oracle_c2_shape():
     # configs[1] shape at parity size: 2^22 records, 1M uniform Long keys, 1 s tumbling,
     # bounded out-of-orderness 200 ms, count/sum/min/max

@@ -104,6 +104,35 @@ def test_first_element_reduce_keeps_first_across_merges():
     assert len(rows) == 1 and rows[0]["count"] == 3 and rows[0]["max"] == 0 and rows[0]["start"] == 50
 
 
+@pytest.mark.parametrize("case", KATS["count_windows"], ids=[c["name"] for c in KATS["count_windows"]])
+def test_count_window_kats(case):
+    # a14: EvictingWindowOperatorTest count-trigger / count-evictor sequences, output compared as a sorted
+    # multiset after each phase (TestHarnessUtil.assertOutputEqualsSorted)
+    op = orc.CountWindowOracle(case["size"], case["slide"], case["evict_after"])
+    ids = {"key1": 1, "key2": 2}
+    names = {v: k for k, v in ids.items()}
+    expected = Counter()
+    for ph in case["phases"]:
+        op.process(np.array([ids[k] for k, _ in ph["input"]]), np.array([v for _, v in ph["input"]]))
+        expected.update(tuple(e) for e in ph["expected"])
+        got = Counter((names[int(r["key"])], int(r["sum"])) for r in op.rows())
+        assert got == expected
+    assert all(r["end"] == (1 << 63) - 1 for r in op.rows())
+
+
+def test_count_window_word_count_shape():
+    # WindowWordCount (countWindow(10, 5).sum(1)): every 5th element of a key fires the sum of its last
+    # <= 10 elements; the first reduced element is the oldest one kept by the evictor
+    op = orc.CountWindowOracle(10, 5)
+    keys = np.array([3] * 17)
+    vals = np.arange(17)
+    op.process(keys, vals)
+    rows = op.rows()
+    assert [int(r["sum"]) for r in rows] == [sum(range(5)), sum(range(10)), sum(range(5, 15))]
+    assert [int(r["max"]) for r in rows] == [0, 0, 5]
+    assert [int(r["count"]) for r in rows] == [5, 10, 10]
+
+
 def _closed_form_stream(num_keys, n_per_key):
     keys, ts, vals, wms = [], [], [], []
     for nxt in range(n_per_key):
