@@ -237,6 +237,22 @@ __device__ __forceinline__ uint32_t ld_state(const uint32_t* p) {
 }
 
 // ------------------------------------------------------------------ output
+// FW_AGG_FIRST / MINBY / MAXBY carry the records' arrival ordinals
+__host__ __device__ __forceinline__ bool agg_ordinal(const DevCfg& c) { return c.agg >= FW_AGG_FIRST; }
+// MINBY / MAXBY: the (field, ordinal) pair as one 64-bit key whose minimum is the selected element
+// (MAXBY flips the i32 field with ~, which reverses its order exactly)
+__device__ __forceinline__ int64_t by_key(int agg, int64_t v, int64_t ord) {
+  const int32_t f = agg == FW_AGG_MAXBY ? ~(int32_t)v : (int32_t)v;
+  return (int64_t)(((uint64_t)(int64_t)f << 32) | (uint32_t)ord);
+}
+// MINBY / MAXBY row: the selected field, and its full ordinal from the first element's (~mx) and
+// the low 32 ordinal bits kept in the key
+__device__ __forceinline__ void by_row(int agg, const Entry& e, int64_t* field, int64_t* ord) {
+  const int32_t f = (int32_t)(e.mn >> 32);
+  *field = agg == FW_AGG_MAXBY ? (int64_t)~f : (int64_t)f;
+  const int64_t first = ~e.mx;
+  *ord = first + (int64_t)(uint32_t)((uint32_t)e.mn - (uint32_t)first);
+}
 __device__ __forceinline__ void write_row(const DevCfg& c, const DevRows& out, unsigned long long pos, const Entry& e) {
   out.key[pos] = e.key;
   out.start[pos] = e.start;
@@ -250,6 +266,7 @@ __device__ __forceinline__ void write_row(const DevCfg& c, const DevRows& out, u
     out.sum[pos] = c.vtype == FW_VAL_I32 ? (int64_t)(int32_t)e.sum : e.sum;
     out.mn[pos] = e.mn;
     out.mx[pos] = c.agg == FW_AGG_FIRST ? ~e.mx : e.mx;
+    if (c.agg == FW_AGG_MINBY || c.agg == FW_AGG_MAXBY) by_row(c.agg, e, &out.mn[pos], &out.mx[pos]);
   }
 }
 // single-lane emission (ordered path)
@@ -283,8 +300,9 @@ __device__ __forceinline__ void acc_add(const DevCfg& c, Entry& e, int64_t v, in
   } else {
     e.sum = jadd(e.sum, v);
   }
-  e.mn = sv < e.mn ? sv : e.mn;
-  const int64_t xv = c.agg == FW_AGG_FIRST ? ~fo : sv;
+  const int64_t nv = c.agg > FW_AGG_FIRST ? by_key(c.agg, v, fo) : sv;
+  e.mn = nv < e.mn ? nv : e.mn;
+  const int64_t xv = agg_ordinal(c) ? ~fo : sv;
   e.mx = xv > e.mx ? xv : e.mx;
 }
 // AggregateFunction.merge
@@ -586,7 +604,7 @@ __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(D
         continue;
       }
       // FW_AGG_FIRST: the record's arrival ordinal rides above the window count (nwin < 2^16)
-      const int64_t nwf = c.agg == FW_AGG_FIRST ? ((c.ord_base + i) << 16) | nwin : (int64_t)nwin;
+      const int64_t nwf = agg_ordinal(c) ? ((c.ord_base + i) << 16) | nwin : (int64_t)nwin;
       store_pair(part, norm, pos, i64x2{k[j], last}, i64x2{v[j], (long long)nwf});
     }
   }
@@ -639,7 +657,7 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_ordered(DevCfg c, i
       stt[pos] = t;
       sv[pos] = v;
       skh[pos] = h;
-      if (c.agg == FW_AGG_FIRST) c.slow_ord[pos] = c.ord_base + i;
+      if (agg_ordinal(c)) c.slow_ord[pos] = c.ord_base + i;
     }
     running += tot;
     __syncthreads();
@@ -689,7 +707,7 @@ __device__ __forceinline__ uint32_t lds_fp(uint32_t h) { return (h >> 8) | 2u; }
 
 // accumulate one value into LDS slot `target` with no-return LDS atomics (nothing waits on the LDS)
 // (first = FW_AGG_FIRST: the max lane takes ~fo, fo = the record's arrival ordinal)
-__device__ __forceinline__ void lds_acc(AggLds& L, int target, int vtype, int64_t v, int64_t fo, bool first) {
+__device__ __forceinline__ void lds_acc(AggLds& L, int target, int vtype, int64_t v, int64_t fo, int first) {
   atomicAdd(&L.cnt[target], 1u);
   if (vtype == FW_VAL_F64) {
     atomicAdd((double*)&L.sum[target], __longlong_as_double(v));
@@ -698,7 +716,7 @@ __device__ __forceinline__ void lds_acc(AggLds& L, int target, int vtype, int64_
     atomicMax((long long*)&L.mx[target], (long long)(first ? ~fo : sv));
   } else {
     atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)v);
-    atomicMin((long long*)&L.mn[target], (long long)v);
+    atomicMin((long long*)&L.mn[target], (long long)(first > FW_AGG_FIRST ? by_key(first, v, fo) : v));
     atomicMax((long long*)&L.mx[target], (long long)(first ? ~fo : v));
   }
 }
@@ -788,7 +806,7 @@ __device__ __forceinline__ int lds_slot(AggLds& L, int64_t key, int64_t start) {
   return target;
 }
 __device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, int64_t start, int64_t v,
-                                           int diag = 0, int64_t fo = 0, bool first = false) {
+                                           int diag = 0, int64_t fo = 0, int first = 0) {
   const int target = lds_slot(L, key, start);
   if (target < 0) return false;
   if (diag & DIAG_AGG_NO_ACCUM) return true;
@@ -973,7 +991,7 @@ __device__ __forceinline__ int lds_session_slot(AggLds& L, int64_t* E, int64_t k
   return target;
 }
 __device__ __forceinline__ bool lds_session_upsert(AggLds& L, int64_t* E, int vtype, int64_t key, int64_t ws,
-                                                   int64_t we, int64_t v, int64_t fo = 0, bool first = false) {
+                                                   int64_t we, int64_t v, int64_t fo = 0, int first = 0) {
   const int target = lds_session_slot(L, E, key, ws, we);
   if (target < 0) return false;
   lds_acc(L, target, vtype, v, fo, first);
@@ -1323,9 +1341,9 @@ __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __
           if (failed || j < rj || rb + (int64_t)j * blockDim.x + threadIdx.x >= ce) continue;
           bool in;
           if constexpr (SESS)
-            in = lds_session_upsert(L, E, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j], o[j], FIRST);
+            in = lds_session_upsert(L, E, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j], o[j], FIRST ? c.agg : 0);
           else
-            in = lds_upsert(L, c.vtype, k[j], t[j], v[j], 0, o[j], FIRST);
+            in = lds_upsert(L, c.vtype, k[j], t[j], v[j], 0, o[j], FIRST ? c.agg : 0);
           if (!in) {
             failed = true;
             rj = j;
@@ -1525,9 +1543,9 @@ __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? 4 : FW_AGG_WAVES) void k_agg
         for (int wi = j == rj ? rwi : 0; wi < nw[j]; wi++) {
           bool in;
           if constexpr (SESS)
-            in = lds_session_upsert(L, sess_end, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j], o[j], FIRST);
+            in = lds_session_upsert(L, sess_end, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j], o[j], FIRST ? c.agg : 0);
           else
-            in = lds_upsert(L, c.vtype, k[j], jsub(t[j], (int64_t)wi * c.slide), v[j], c.diag, o[j], FIRST);
+            in = lds_upsert(L, c.vtype, k[j], jsub(t[j], (int64_t)wi * c.slide), v[j], c.diag, o[j], FIRST ? c.agg : 0);
           if (!in) {
             failed = true;
             rj = j;
@@ -1851,7 +1869,7 @@ __global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, 
       for (int j = tid; j < m && ck[j] == ck[tid] && cp[j] == cp[tid]; j++) {
         const int64_t i = b0 + ci[j];
         const int64_t k = sk[i], t = stt[i], v = sv[i];
-        const int64_t fo = c.agg == FW_AGG_FIRST ? c.slow_ord[i] : 0;
+        const int64_t fo = agg_ordinal(c) ? c.slow_ord[i] : 0;
         const int32_t p = cp[j];
         bool skipped = true;
         if (c.assigner == FW_SESSION)
@@ -2674,7 +2692,7 @@ void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint
       launch_scan(h.chunk_base, (int64_t)c.P + 1, h.scan_tmp, s);
     }
   }
-  const bool first = c.agg == FW_AGG_FIRST;
+  const bool first = agg_ordinal(c);
   if (c.assigner == FW_SESSION && first)
     hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true, true>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs,
                        T, tb, prog, resume, st, h);

@@ -172,7 +172,7 @@ int alloc_scratch(fw_op* op, Scratch& s, int64_t mb, int64_t m) {
   HIP_OR_RETURN(op, dmalloc(&s.stt, mb));
   HIP_OR_RETURN(op, dmalloc(&s.sv, mb));
   HIP_OR_RETURN(op, dmalloc(&s.skh, mb));
-  if (op->cfg.aggregate == FW_AGG_FIRST) HIP_OR_RETURN(op, dmalloc(&s.so, mb));
+  if (op->cfg.aggregate >= FW_AGG_FIRST) HIP_OR_RETURN(op, dmalloc(&s.so, mb));
   return FW_OK;
 }
 void free_scratch(Scratch& s) {
@@ -592,7 +592,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     snprintf(msg, sizeof msg, "invalid KeyGroupRange [%d, %d]", cfg.key_group_start, cfg.key_group_end);
   if (!msg[0] && cfg.sub_partitions != 0 && (cfg.sub_partitions & (cfg.sub_partitions - 1)))
     snprintf(msg, sizeof msg, "sub_partitions must be a power of two");
-  if (!msg[0] && (cfg.aggregate < FW_AGG_COUNT_SUM_MIN_MAX || cfg.aggregate > FW_AGG_FIRST))
+  if (!msg[0] && (cfg.aggregate < FW_AGG_COUNT_SUM_MIN_MAX || cfg.aggregate > FW_AGG_MAXBY))
     snprintf(msg, sizeof msg, "unknown aggregate %d", cfg.aggregate);
   const int32_t hll_p = cfg.hll_precision ? cfg.hll_precision : 14;
   if (!msg[0] && cfg.aggregate == FW_AGG_HLL && (hll_p < 4 || hll_p > 16))
@@ -604,7 +604,11 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
                               "over a Long item column");
     unsupported = true;
   }
-  if (!msg[0] && cfg.aggregate == FW_AGG_FIRST && cfg.assigner == FW_SLIDING && cfg.slide > 0 &&
+  if (!msg[0] && (cfg.aggregate == FW_AGG_MINBY || cfg.aggregate == FW_AGG_MAXBY) && cfg.value_type != FW_VAL_I32) {
+    snprintf(msg, sizeof msg, "minBy / maxBy are offered over an Integer field");
+    unsupported = true;
+  }
+  if (!msg[0] && cfg.aggregate >= FW_AGG_FIRST && cfg.assigner == FW_SLIDING && cfg.slide > 0 &&
       (cfg.size + cfg.slide - 1) / cfg.slide > 65535) {
     snprintf(msg, sizeof msg, "the first-element aggregate takes at most 65535 windows per element");
     unsupported = true;
@@ -660,7 +664,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     make_div_inv((uint64_t)c.slide, &c.mag_slide, &c.l_slide);
   }
   const int64_t expected = cfg.expected_entries > 0 ? cfg.expected_entries : (int64_t)c.P * 512;
-  if (cfg.aggregate == FW_AGG_FIRST) c.agg = FW_AGG_FIRST;
+  if (cfg.aggregate >= FW_AGG_FIRST) c.agg = cfg.aggregate;
   if (cfg.aggregate == FW_AGG_HLL) {
     // register pool: one 2^p-byte block per live (key, window); expected_entries live entries, plus
     // a quarter for entries created before the watermark that retires their predecessors
@@ -976,8 +980,8 @@ void free_state_cols(StateCols& c) {
 }  // namespace
 
 int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64_t cap, int64_t* n) {
-  if (op && op->dc.agg == FW_AGG_HLL)  // registers are not part of fw_state_rows
-    return set_err(op, FW_ERR_UNSUPPORTED, "keyed-state snapshots of the HyperLogLog aggregate are not offered");
+  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_MINBY || op->dc.agg == FW_AGG_MAXBY))  // not in fw_state_rows
+    return set_err(op, FW_ERR_UNSUPPORTED, "keyed-state snapshots of the HyperLogLog, minBy and maxBy aggregates are not offered");
   if (!op || !n) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;
@@ -1016,8 +1020,8 @@ int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64
 }
 
 int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_t n) {
-  if (op && op->dc.agg == FW_AGG_HLL)  // registers are not part of fw_state_rows
-    return set_err(op, FW_ERR_UNSUPPORTED, "keyed-state snapshots of the HyperLogLog aggregate are not offered");
+  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_MINBY || op->dc.agg == FW_AGG_MAXBY))  // not in fw_state_rows
+    return set_err(op, FW_ERR_UNSUPPORTED, "keyed-state snapshots of the HyperLogLog, minBy and maxBy aggregates are not offered");
   if (!op || (n > 0 && !src) || n < 0) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;

@@ -185,6 +185,30 @@ class FirstElementReduce:
         return N.FW_AGG_FIRST
 
 
+@dataclass(frozen=True)
+class ExtremalElementReduce:
+    """`minBy(pos)` / `maxBy(pos)` of WindowedStream (first = true): the whole element whose field is the
+    smallest (largest), the earlier one among equal fields (ComparableAggregator.reduce,
+    ComparableAggregator.java:72-94; Comparator MinBy/MaxBy).  Integer fields.  Fired rows: min = the
+    selected field, max = the selected element's arrival ordinal (`selected_elements` returns the elements)."""
+    kind: str = "min"
+    value_type: str = "int"
+
+    def native(self):
+        return N.FW_VAL_I32
+
+    def hll_precision(self):
+        return 0
+
+    def aggregate_kind(self):
+        return N.FW_AGG_MINBY if self.kind == "min" else N.FW_AGG_MAXBY
+
+
+def selected_elements(rows, elements):
+    """The output elements of minBy/maxBy: the element at each row's ordinal (`max`)."""
+    return [tuple(elements[int(r["max"])]) for r in rows]
+
+
 def first_element_results(rows, elements, pos, field="sum"):
     """The output tuples of `sum(pos)` (field "sum") or `min(pos)` (field "min") from fired rows of a
     FirstElementReduce operator: a copy of the window's first element (its arrival ordinal is the row's

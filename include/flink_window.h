@@ -61,6 +61,14 @@ extern "C" {
                                       into the handle), from which the caller takes the passthrough fields.
                                       Merged sessions keep the smaller ordinal.  At most 65535 windows per
                                       record. */
+#define FW_AGG_MINBY 3             /* minBy(pos) / maxBy(pos) with the first-tie rule (ComparableAggregator.java
+                                      :72-94, Comparator.java MinBy/MaxBy): the whole element with the smallest
+                                      (largest) field, the earlier one among equal fields.  Integer fields
+                                      (FW_VAL_I32) only.  Rows carry count, sum, min = the selected field value
+                                      and max = the arrival ordinal of the selected element.  Exact while the
+                                      elements of one window span fewer than 2^32 arrival ordinals.  Keyed-state
+                                      snapshots are refused. */
+#define FW_AGG_MAXBY 4
 
 #define FW_KEY_LONG 0   /* key is a Long: hashCode = (int)(v ^ (v >>> 32))               */
 #define FW_KEY_INT 1    /* key is an Integer: hashCode = value                              */

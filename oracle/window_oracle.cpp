@@ -95,6 +95,7 @@ struct Acc {
   double dmn = 0.0, dmx = 0.0;
   std::vector<uint8_t> regs;  // OR_AGG_HLL registers (2^p)
   int64_t first = 0;          // OR_AGG_FIRST: arrival ordinal of the element that created the state
+  int64_t by_val = 0, by_ord = 0;  // OR_AGG_MINBY / MAXBY: the selected element's field and ordinal
 };
 
 // ---------------------------------------------------------------- HyperLogLog (window_oracle.h)
@@ -205,6 +206,13 @@ class WindowOperatorOracle {
   // argument (SumAggregator.java:66-76, ComparableAggregator.java:72-94): the first element survives)
   void acc_add(Acc& a, int64_t v) const {
     if (a.cnt == 0) a.first = ordinal;
+    // minBy/maxBy (Comparator.MinByComparator / MaxByComparator, first = true): a strictly smaller (larger)
+    // field replaces the kept element; an equal one leaves the earlier element
+    if (a.cnt == 0 || (cfg.aggregate == OR_AGG_MINBY && v < a.by_val) ||
+        (cfg.aggregate == OR_AGG_MAXBY && v > a.by_val)) {
+      a.by_val = v;
+      a.by_ord = ordinal;
+    }
     if (cfg.aggregate == OR_AGG_HLL) {
       if (a.regs.empty()) a.regs.assign((size_t)1 << cfg.hll_p, 0);
       hll_add(a.regs, cfg.hll_p, (uint64_t)v);
@@ -241,6 +249,15 @@ class WindowOperatorOracle {
     // and which state window is `a` follows HashSet order in the reference (AbstractHeapMergingState.java
     // :67-93, MergingWindowSet.java:190-205): parity unpinned, defined here as the earlier element
     r.first = std::min(a.first, b.first);
+    // minBy/maxBy merge: the reference keeps reduce(a, b)'s first argument on a tie, `a` chosen by HashSet
+    // order (parity unpinned); defined here as the earlier element, like the accumulation order
+    const bool b_wins = cfg.aggregate == OR_AGG_MINBY   ? (b.by_val < a.by_val || (b.by_val == a.by_val && b.by_ord < a.by_ord))
+                        : cfg.aggregate == OR_AGG_MAXBY ? (b.by_val > a.by_val || (b.by_val == a.by_val && b.by_ord < a.by_ord))
+                                                        : false;
+    if (b_wins) {
+      r.by_val = b.by_val;
+      r.by_ord = b.by_ord;
+    }
     if (cfg.aggregate == OR_AGG_HLL) {
       for (size_t j = 0; j < r.regs.size(); j++) r.regs[j] = std::max(r.regs[j], b.regs[j]);
       return r;
@@ -304,6 +321,10 @@ class WindowOperatorOracle {
       r.max = a.imx;
     }
     if (cfg.aggregate == OR_AGG_FIRST) r.max = a.first;
+    if (cfg.aggregate == OR_AGG_MINBY || cfg.aggregate == OR_AGG_MAXBY) {
+      r.min = a.by_val;
+      r.max = a.by_ord;
+    }
     r.epoch = epoch;
     rows.push_back(r);
   }

@@ -6,7 +6,7 @@ import pytest
 from flink_amd import (EventTimeSessionWindows, KeyGroupRange, PurgingTrigger, SlidingEventTimeWindows,
                        EventTimeTrigger, TumblingEventTimeWindows)
 from flink_amd.datagen import generate_host
-from flink_amd.windowing import CountSumMinMax, FirstElementReduce, first_element_results
+from flink_amd.windowing import CountSumMinMax, ExtremalElementReduce, FirstElementReduce, first_element_results
 from oracle import oracle as orc
 from tests.kat_util import expected_counters, load_kats, replay, row_counters
 from tests.parity_util import assert_rows_equal, assert_side_equal
@@ -18,7 +18,7 @@ _VT = {"i64": "long", "i32": "int", "f64": "double"}
 
 
 def _gpu_op(assigner, size=0, slide=0, offset=0, gap=0, lateness=0, purging=False, side_output=False,
-            value_type="i64", first=False, **kw):
+            value_type="i64", first=False, by=None, **kw):
     from flink_amd.operator import GpuWindowOperator
     if assigner == "tumbling":
         a = TumblingEventTimeWindows.of(size, offset)
@@ -27,7 +27,8 @@ def _gpu_op(assigner, size=0, slide=0, offset=0, gap=0, lateness=0, purging=Fals
     else:
         a = EventTimeSessionWindows.with_gap(gap)
     trig = PurgingTrigger.of(EventTimeTrigger.create()) if purging else EventTimeTrigger.create()
-    agg = FirstElementReduce(_VT[value_type]) if first else CountSumMinMax(_VT[value_type])
+    agg = (FirstElementReduce(_VT[value_type]) if first else ExtremalElementReduce(by) if by
+           else CountSumMinMax(_VT[value_type]))
     return GpuWindowOperator(a, agg, trig, allowed_lateness=lateness,
                              side_output=side_output, **kw)
 
@@ -157,6 +158,30 @@ def test_gpu_session_example_sum_passthrough():
     got = first_element_results(op.rows(), [tuple(e) for e in ex["input"]], 2, "sum")
     op.close()
     assert sorted(got) == sorted(tuple(e) for e in ex["expected"])
+
+
+BY_CONFIGS = [
+    dict(assigner="tumbling", size=1000),
+    dict(assigner="tumbling", size=1000, lateness=700),
+    dict(assigner="sliding", size=3000, slide=500),
+    dict(assigner="sliding", size=2000, slide=500, lateness=300, side_output=True),
+    dict(assigner="session", gap=300),
+    dict(assigner="session", gap=300, lateness=200, purging=True),
+]
+
+
+@pytest.mark.parametrize("by", ["min", "max"])
+@pytest.mark.parametrize("cfg", BY_CONFIGS, ids=[str(i) for i in range(len(BY_CONFIGS))])
+def test_gpu_min_by_max_by_vs_oracle(cfg, by):
+    # a9 minBy/maxBy (first = true): the selected element's field and arrival ordinal; fields drawn from
+    # 5 values so most windows break ties by arrival order
+    batches, wms = _stream(120_000, 10_000, 5000, bound=400, jitter=1500, rate=100_000)
+    batches = [(k, t, v % 5) for k, t, v in batches]
+    cfg = dict(cfg, value_type="i32", by=by)
+    g, r, gs, rs, gl, rl = _run_both(cfg, batches, wms)
+    assert_rows_equal(g, r, "int")
+    assert_side_equal(gs, rs)
+    assert gl == rl
 
 
 def _word_stream(n, n_words, seed=0x5EED):

@@ -133,6 +133,23 @@ def test_count_window_word_count_shape():
     assert [int(r["count"]) for r in rows] == [5, 10, 10]
 
 
+@pytest.mark.parametrize("by", ["min", "max"])
+def test_min_by_max_by_first_tie_rule(by):
+    # ComparableAggregator.reduce with byAggregate and first = true (ComparableAggregator.java:72-94):
+    # a strictly better field replaces the element, an equal one keeps the earlier
+    op = orc.WindowOperatorOracle(assigner="tumbling", size=10, value_type="i32", by=by)
+    op.process(np.array([1] * 6), np.array([0, 1, 2, 3, 4, 5]), np.array([5, 3, 7, 3, 7, 4]))
+    op.watermark((1 << 63) - 1)
+    (r,) = op.rows()
+    assert (int(r["min"]), int(r["max"])) == ((3, 1) if by == "min" else (7, 2))
+    # sessions: two sessions bridged by a third element; the merged state keeps the earlier of equal fields
+    op = orc.WindowOperatorOracle(assigner="session", gap=30, value_type="i32", by=by)
+    op.process(np.array([7, 7, 7]), np.array([100, 50, 75]), np.array([2, 2, 9 if by == "min" else -9]))
+    op.watermark((1 << 63) - 1)
+    (r,) = op.rows()
+    assert (int(r["min"]), int(r["max"]), int(r["count"])) == (2, 0, 3)
+
+
 def _closed_form_stream(num_keys, n_per_key):
     keys, ts, vals, wms = [], [], [], []
     for nxt in range(n_per_key):
