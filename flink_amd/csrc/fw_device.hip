@@ -253,21 +253,30 @@ __device__ __forceinline__ void by_row(int agg, const Entry& e, int64_t* field, 
   const int64_t first = ~e.mx;
   *ord = first + (int64_t)(uint32_t)((uint32_t)e.mn - (uint32_t)first);
 }
+__device__ __forceinline__ bool agg_first(int agg) { return agg == FW_AGG_FIRST || agg == FW_AGG_FIRST_MAX; }
+__device__ __forceinline__ bool agg_by(int agg) { return agg == FW_AGG_MINBY || agg == FW_AGG_MAXBY; }
+// the value the entry's mn lane takes for one record (sv: the field, f64 in sortable form): FIRST_MAX keeps
+// ~field so the min is the max; MINBY / MAXBY the (field, ordinal) key
+__device__ __forceinline__ int64_t mn_in(int agg, int64_t sv, int64_t v, int64_t fo) {
+  return agg_by(agg) ? by_key(agg, v, fo) : agg == FW_AGG_FIRST_MAX ? ~sv : sv;
+}
+// row / snapshot columns of an entry's mn and mx (MINBY / MAXBY: by_row)
+__device__ __forceinline__ int64_t mn_out(const DevCfg& c, int64_t mn) {
+  const int64_t s = c.agg == FW_AGG_FIRST_MAX ? ~mn : mn;
+  return c.vtype == FW_VAL_F64 ? f64_unsortable(s) : s;
+}
+__device__ __forceinline__ int64_t mx_out(const DevCfg& c, int64_t mx) {
+  return agg_first(c.agg) ? ~mx : c.vtype == FW_VAL_F64 ? f64_unsortable(mx) : mx;
+}
 __device__ __forceinline__ void write_row(const DevCfg& c, const DevRows& out, unsigned long long pos, const Entry& e) {
   out.key[pos] = e.key;
   out.start[pos] = e.start;
   out.end[pos] = e.end;
   out.cnt[pos] = e.cnt;
-  if (c.vtype == FW_VAL_F64) {
-    out.sum[pos] = e.sum;
-    out.mn[pos] = f64_unsortable(e.mn);
-    out.mx[pos] = c.agg == FW_AGG_FIRST ? ~e.mx : f64_unsortable(e.mx);
-  } else {
-    out.sum[pos] = c.vtype == FW_VAL_I32 ? (int64_t)(int32_t)e.sum : e.sum;
-    out.mn[pos] = e.mn;
-    out.mx[pos] = c.agg == FW_AGG_FIRST ? ~e.mx : e.mx;
-    if (c.agg == FW_AGG_MINBY || c.agg == FW_AGG_MAXBY) by_row(c.agg, e, &out.mn[pos], &out.mx[pos]);
-  }
+  out.sum[pos] = c.vtype == FW_VAL_I32 ? (int64_t)(int32_t)e.sum : e.sum;
+  out.mn[pos] = mn_out(c, e.mn);
+  out.mx[pos] = mx_out(c, e.mx);
+  if (agg_by(c.agg)) by_row(c.agg, e, &out.mn[pos], &out.mx[pos]);
 }
 // single-lane emission (ordered path)
 __device__ __forceinline__ void emit_one(const DevCfg& c, const DevRows& out, Status* st, const Entry& e) {
@@ -300,7 +309,7 @@ __device__ __forceinline__ void acc_add(const DevCfg& c, Entry& e, int64_t v, in
   } else {
     e.sum = jadd(e.sum, v);
   }
-  const int64_t nv = c.agg > FW_AGG_FIRST ? by_key(c.agg, v, fo) : sv;
+  const int64_t nv = mn_in(c.agg, sv, v, fo);
   e.mn = nv < e.mn ? nv : e.mn;
   const int64_t xv = agg_ordinal(c) ? ~fo : sv;
   e.mx = xv > e.mx ? xv : e.mx;
@@ -712,11 +721,11 @@ __device__ __forceinline__ void lds_acc(AggLds& L, int target, int vtype, int64_
   if (vtype == FW_VAL_F64) {
     atomicAdd((double*)&L.sum[target], __longlong_as_double(v));
     const int64_t sv = f64_sortable(v);
-    atomicMin((long long*)&L.mn[target], (long long)sv);
+    atomicMin((long long*)&L.mn[target], (long long)(first ? mn_in(first, sv, v, fo) : sv));
     atomicMax((long long*)&L.mx[target], (long long)(first ? ~fo : sv));
   } else {
     atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)v);
-    atomicMin((long long*)&L.mn[target], (long long)(first > FW_AGG_FIRST ? by_key(first, v, fo) : v));
+    atomicMin((long long*)&L.mn[target], (long long)(first ? mn_in(first, v, v, fo) : v));
     atomicMax((long long*)&L.mx[target], (long long)(first ? ~fo : v));
   }
 }
@@ -2417,15 +2426,9 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_snapshot(DevCfg c, DevTable
       out.start[o] = e.start;
       out.end[o] = e.end;
       out.cnt[o] = e.cnt;
-      if (c.vtype == FW_VAL_F64) {
-        out.sum[o] = e.sum;
-        out.mn[o] = f64_unsortable(e.mn);
-        out.mx[o] = c.agg == FW_AGG_FIRST ? ~e.mx : f64_unsortable(e.mx);
-      } else {
-        out.sum[o] = c.vtype == FW_VAL_I32 ? (int64_t)(int32_t)e.sum : e.sum;
-        out.mn[o] = e.mn;
-        out.mx[o] = c.agg == FW_AGG_FIRST ? ~e.mx : e.mx;
-      }
+      out.sum[o] = c.vtype == FW_VAL_I32 ? (int64_t)(int32_t)e.sum : e.sum;
+      out.mn[o] = mn_out(c, e.mn);
+      out.mx[o] = mx_out(c, e.mx);
       // a pane's timer: the maxTimestamp of its next window to form
       out.timer[o] = c.panes ? max(e.meta, tb.pane_floor[p]) : (e.meta & FW_TIMER) ? 1 : 0;
     }
@@ -2465,7 +2468,8 @@ __global__ void k_restore(DevCfg c, int32_t kg, StateCols in, int64_t n, DevTabl
   d.cnt = in.cnt[i];
   d.sum = in.sum[i];
   d.mn = c.vtype == FW_VAL_F64 ? f64_sortable(in.mn[i]) : in.mn[i];
-  d.mx = c.agg == FW_AGG_FIRST ? ~in.mx[i] : c.vtype == FW_VAL_F64 ? f64_sortable(in.mx[i]) : in.mx[i];
+  if (c.agg == FW_AGG_FIRST_MAX) d.mn = ~d.mn;
+  d.mx = agg_first(c.agg) ? ~in.mx[i] : c.vtype == FW_VAL_F64 ? f64_sortable(in.mx[i]) : in.mx[i];
   d.meta = c.panes ? in.timer[i] : in.timer[i] ? FW_TIMER : 0;
   const Region r = region_of(c, tb, p, tb.cur[p]);
   const uint64_t h = slot_hash(c, d.key, c.assigner == FW_SESSION ? 0 : d.start);

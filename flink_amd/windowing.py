@@ -172,8 +172,10 @@ class FirstElementReduce:
     ComparableAggregator.reduce, ComparableAggregator.java:72-94).  The GPU keeps count/sum/min of the
     field and the arrival ordinal of the window's first element (fired rows: max = that ordinal);
     `first_element_results` rebuilds the reference's output tuples from it.  Merged sessions keep the
-    earlier element (the reference's choice follows HashSet order: parity unpinned)."""
+    earlier element (the reference's choice follows HashSet order: parity unpinned).
+    `field="max"` is `max(pos)`: the rows' min column then holds the field's maximum."""
     value_type: str = "int"
+    field: str = "sum"
 
     def native(self):
         return {"long": N.FW_VAL_I64, "int": N.FW_VAL_I32, "double": N.FW_VAL_F64}[self.value_type]
@@ -182,7 +184,7 @@ class FirstElementReduce:
         return 0
 
     def aggregate_kind(self):
-        return N.FW_AGG_FIRST
+        return N.FW_AGG_FIRST_MAX if self.field == "max" else N.FW_AGG_FIRST
 
 
 @dataclass(frozen=True)

@@ -69,6 +69,9 @@ extern "C" {
                                       elements of one window span fewer than 2^32 arrival ordinals.  Keyed-state
                                       snapshots are refused. */
 #define FW_AGG_MAXBY 4
+#define FW_AGG_FIRST_MAX 5         /* max(pos) (ComparableAggregator.java:72-94, Comparator.MaxComparator): as
+                                      FW_AGG_FIRST, but the min column holds the field's MAXIMUM (the first
+                                      element with the field replaced by the max) */
 
 #define FW_KEY_LONG 0   /* key is a Long: hashCode = (int)(v ^ (v >>> 32))               */
 #define FW_KEY_INT 1    /* key is an Integer: hashCode = value                              */

@@ -89,7 +89,7 @@ def _i64p(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
 
 
-AGG_COUNT_SUM_MIN_MAX, AGG_HLL, AGG_FIRST, AGG_MINBY, AGG_MAXBY = 0, 1, 2, 3, 4
+AGG_COUNT_SUM_MIN_MAX, AGG_HLL, AGG_FIRST, AGG_MINBY, AGG_MAXBY, AGG_FIRST_MAX = 0, 1, 2, 3, 4, 5
 
 
 def make_cfg(assigner="tumbling", size=0, slide=0, offset=0, gap=0, lateness=0, purging=False, side_output=False,
@@ -97,7 +97,7 @@ def make_cfg(assigner="tumbling", size=0, slide=0, offset=0, gap=0, lateness=0, 
     """hll_p > 0 selects the HyperLogLog AggregateFunction with 2^hll_p registers; first=True the
     first-element reduce of sum(pos)/min(pos) (max = arrival ordinal of the window's first element;
     window_oracle.h)."""
-    agg = (AGG_HLL if hll_p else AGG_FIRST if first else {"min": AGG_MINBY, "max": AGG_MAXBY}[by] if by
+    agg = (AGG_HLL if hll_p else AGG_FIRST_MAX if first == "max" else AGG_FIRST if first else {"min": AGG_MINBY, "max": AGG_MAXBY}[by] if by
            else AGG_COUNT_SUM_MIN_MAX)
     return OracleCfg(_ASSIGNERS[assigner], _VALTYPES[value_type], size, slide, offset, gap, lateness, int(purging),
                      int(side_output), agg, int(hll_p))

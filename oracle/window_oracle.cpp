@@ -248,7 +248,7 @@ class WindowOperatorOracle {
     // OR_AGG_FIRST: mergeState(a, b) = reduce(a, b) keeps a's first element (HeapReducingState.java:91-93),
     // and which state window is `a` follows HashSet order in the reference (AbstractHeapMergingState.java
     // :67-93, MergingWindowSet.java:190-205): parity unpinned, defined here as the earlier element
-    r.first = std::min(a.first, b.first);
+    r.first = std::min(a.first, b.first);  // (OR_AGG_FIRST and OR_AGG_FIRST_MAX)
     // minBy/maxBy merge: the reference keeps reduce(a, b)'s first argument on a tie, `a` chosen by HashSet
     // order (parity unpinned); defined here as the earlier element, like the accumulation order
     const bool b_wins = cfg.aggregate == OR_AGG_MINBY   ? (b.by_val < a.by_val || (b.by_val == a.by_val && b.by_ord < a.by_ord))
@@ -321,6 +321,10 @@ class WindowOperatorOracle {
       r.max = a.imx;
     }
     if (cfg.aggregate == OR_AGG_FIRST) r.max = a.first;
+    if (cfg.aggregate == OR_AGG_FIRST_MAX) {  // max(pos): the first element with the field's maximum
+      r.min = cfg.value_type == OR_VAL_F64 ? dbits(a.dmx) : a.imx;
+      r.max = a.first;
+    }
     if (cfg.aggregate == OR_AGG_MINBY || cfg.aggregate == OR_AGG_MAXBY) {
       r.min = a.by_val;
       r.max = a.by_ord;

@@ -72,7 +72,8 @@ typedef struct {
  * fields of sum(pos)/min(pos)); ordinals count every element processed, from 0. */
 /* OR_AGG_MINBY / OR_AGG_MAXBY: minBy(pos) / maxBy(pos) with first = true (ComparableAggregator.java:72-94):
  * min = the selected field value, max = the arrival ordinal of the selected element. */
-enum { OR_AGG_COUNT_SUM_MIN_MAX = 0, OR_AGG_HLL = 1, OR_AGG_FIRST = 2, OR_AGG_MINBY = 3, OR_AGG_MAXBY = 4 };
+enum { OR_AGG_COUNT_SUM_MIN_MAX = 0, OR_AGG_HLL = 1, OR_AGG_FIRST = 2, OR_AGG_MINBY = 3, OR_AGG_MAXBY = 4,
+       OR_AGG_FIRST_MAX = 5 /* max(pos): as OR_AGG_FIRST with min = the field's maximum */ };
 
 /* One fired row.  sum/min/max hold i64 values (I64/I32) or f64 bit patterns (F64).
  * epoch = number of watermarks fully processed before the row was emitted, so

@@ -27,7 +27,8 @@ def _gpu_op(assigner, size=0, slide=0, offset=0, gap=0, lateness=0, purging=Fals
     else:
         a = EventTimeSessionWindows.with_gap(gap)
     trig = PurgingTrigger.of(EventTimeTrigger.create()) if purging else EventTimeTrigger.create()
-    agg = (FirstElementReduce(_VT[value_type]) if first else ExtremalElementReduce(by) if by
+    agg = (FirstElementReduce(_VT[value_type], "max" if first == "max" else "sum") if first
+           else ExtremalElementReduce(by) if by
            else CountSumMinMax(_VT[value_type]))
     return GpuWindowOperator(a, agg, trig, allowed_lateness=lateness,
                              side_output=side_output, **kw)
@@ -119,13 +120,14 @@ def test_gpu_vs_oracle_out_of_order(cfg):
 
 
 @pytest.mark.parametrize("cfg", CONFIGS, ids=[str(i) for i in range(len(CONFIGS))])
-def test_gpu_first_element_vs_oracle(cfg):
+@pytest.mark.parametrize("first", [True, "max"], ids=["sum_min", "max"])
+def test_gpu_first_element_vs_oracle(cfg, first):
     # a9: sum(pos)/min(pos) keep the window's first element; the rows' max is its arrival ordinal,
     # carried through the parallel path (k_scatter -> k_aggregate), the ordered replay (late firings,
     # sessions of tainted keys), pane windows and session merges
     vt = cfg.get("value_type", "i64")
     batches, wms = _stream(120_000, 10_000, 5000, bound=400, jitter=1500, rate=100_000, value_type=vt)
-    g, r, gs, rs, gl, rl = _run_both(dict(cfg, first=True), batches, wms)
+    g, r, gs, rs, gl, rl = _run_both(dict(cfg, first=first), batches, wms)
     assert_rows_equal(g, r, _VT[vt])
     assert_side_equal(gs, rs)
     assert gl == rl

@@ -88,6 +88,15 @@ def test_session_example_sum_passthrough_kat():
     assert sorted(got) == sorted(tuple(e) for e in ex["expected"])
 
 
+def test_max_pos_keeps_first_element():
+    # max(pos) (Comparator.MaxComparator, non-by aggregation): the first element with the field set to the max
+    op = orc.WindowOperatorOracle(assigner="tumbling", size=10, first="max")
+    op.process(np.array([1, 1, 1]), np.array([1, 2, 3]), np.array([4, 9, -2]))
+    op.watermark((1 << 63) - 1)
+    (r,) = op.rows()
+    assert (int(r["min"]), int(r["max"]), int(r["count"])) == (9, 0, 3)
+
+
 def test_first_element_reduce_keeps_first_across_merges():
     # tumbling: the ordinal is the first element added to each window; sessions: a bridging element
     # merges two sessions and the earlier first element survives
