@@ -1030,6 +1030,10 @@ int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_
   const int64_t* hs[8] = {src->key, src->start, src->end, src->count, src->sum, src->min, src->max, src->timer};
   for (const int64_t* h : hs)
     if (!h) return set_err(op, FW_ERR_ARG, "null state column");
+  // first-element reduces: records pushed after the restore are numbered after every restored first
+  // element, so the earlier element keeps winning in the caller's numbering
+  if (op->dc.agg == FW_AGG_FIRST || op->dc.agg == FW_AGG_FIRST_MAX)
+    for (int64_t i = 0; i < n; i++) op->records_in = std::max(op->records_in, src->max[i] + 1);
   StateCols d{};
   int32_t* demand = nullptr;
   auto fail = [&](int code) {

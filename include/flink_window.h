@@ -212,7 +212,9 @@ void* fw_stream(fw_op* op); /* the hipStream_t the handle enqueues on */
  *     with cap too small (or dst NULL) it only returns the row count in *n.
  *   fw_restore_key_group: inserts rows into the handle (which must own the key group); a row whose
  *     (key, window) is already present is merged into it (AggregateFunction.merge).  Long/Integer
- *     keys outside the key group are refused with FW_ERR_KEY_GROUP. */
+ *     keys outside the key group are refused with FW_ERR_KEY_GROUP.  First-element reduces (FW_AGG_FIRST,
+ *     FW_AGG_FIRST_MAX): `max` is the first element's ordinal, and later pushes are numbered after the largest
+ *     restored one.  HyperLogLog, minBy and maxBy state is refused (FW_ERR_UNSUPPORTED). */
 typedef struct fw_state_rows {
   int64_t* key;
   int64_t* start;

@@ -566,6 +566,40 @@ def test_gpu_snapshot_restore_rescale(cfg, new_par):
     assert_rows_equal(np.concatenate(got), exp)
 
 
+@pytest.mark.parametrize("first", [True, "max"], ids=["sum_min", "max"])
+@pytest.mark.parametrize("cfg", [dict(assigner="tumbling", size=100), dict(assigner="sliding", size=300, slide=100),
+                                 dict(assigner="session", gap=40)], ids=["tumbling", "panes", "session"])
+def test_gpu_first_element_snapshot_restore(cfg, first):
+    # the first element's ordinal (and max(pos)'s maximum) survive fw_snapshot_key_group / fw_restore_key_group
+    # onto two handles; the final watermark then fires the restored windows exactly as the oracle does
+    from flink_amd.keygroups import compute_key_group_range_for_operator_index
+    cfg = dict(cfg, first=first)
+    batches, wms = _stream(60_000, 15_000, 3_000, bound=50, jitter=80, rate=200_000, final=False)
+    ref = orc.WindowOperatorOracle(**cfg)
+    a = _gpu_op(**cfg, max_parallelism=128)
+    for (k, t, v), wm in zip(batches, wms):
+        ref.process(k, t, v)
+        ref.watermark(wm)
+        a.process(k, t, v)
+        a.watermark(wm)
+    ref.watermark((1 << 63) - 1)
+    exp = ref.rows()
+    got = [a.rows()]
+    snap = a.snapshot_state()
+    a.close()
+    for idx in range(2):
+        op = _gpu_op(**cfg, max_parallelism=128,
+                     key_group_range=compute_key_group_range_for_operator_index(128, 2, idx))
+        op.initialize_state(snap)
+        op.watermark((1 << 63) - 1)
+        r = op.rows()
+        r["epoch"] = len(batches)
+        got.append(r)
+        op.close()
+    exp["epoch"] = np.minimum(exp["epoch"], len(batches))
+    assert_rows_equal(np.concatenate(got), exp)
+
+
 def test_gpu_restore_refuses_foreign_key_group():
     from flink_amd import _native as N
     from flink_amd.keygroups import assign_to_key_group
