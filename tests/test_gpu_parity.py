@@ -138,7 +138,7 @@ def test_gpu_first_element_vs_oracle(cfg, first):
 def test_gpu_first_element_hot_keys(cfg):
     # Zipf keys over multi-batch pushes: hot partitions are split over aggregate workgroups and the
     # chunks' deltas merged, with the first element's ordinal surviving the merge
-    batches, wms = _stream(1 << 19, 1 << 18, 10_000, bound=50, jitter=50, rate=1_000_000, zipf=1.1)
+    batches, wms = _stream(1 << 20, 1 << 19, 10_000, bound=50, jitter=50, rate=1_000_000, zipf=1.1)
     g, r, gs, rs, gl, rl = _run_both(dict(cfg, first=True), batches, wms)
     assert_rows_equal(g, r)
     assert gl == rl
