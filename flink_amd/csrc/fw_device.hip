@@ -1462,7 +1462,7 @@ __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __
 // last workgroup to finish: [0] record loop, [1] flushes, [2] whole workgroup, [3] finished workgroups
 __device__ unsigned long long g_aggt[4];
 template <int RPT, bool SESS, bool FIRST>
-__global__ __launch_bounds__(FW_AGG_THREADS, SESS ? 4 : FW_AGG_WAVES) void k_aggregate(DevCfg c, int64_t wm, const PRec* __restrict__ part,
+__global__ __launch_bounds__(FW_AGG_THREADS, SESS ? FW_SESS_WAVES : FW_AGG_WAVES) void k_aggregate(DevCfg c, int64_t wm, const PRec* __restrict__ part,
                                                               const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
                                                               AggProg prog, int resume, Status* st, AggHot hot) {
   __shared__ AggLds L;
@@ -1966,7 +1966,10 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, in
 // One workgroup per FW_HLL_CHUNK records; a record's partition is found from the scan offsets.  Byte
 // registers are raised with a CAS on their 32-bit word, only when the rank is larger (max is idempotent,
 // so a resumed push may run this again over the whole batch).
-constexpr int FW_HLL_CHUNK = 4096;
+#ifndef FW_HLL_CHUNK_N
+#define FW_HLL_CHUNK_N 4096
+#endif
+constexpr int FW_HLL_CHUNK = FW_HLL_CHUNK_N;
 __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __restrict__ part,
                                                     const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
                                                     Status* st) {

@@ -30,6 +30,9 @@
 #ifndef FW_AGG_WAVES
 #define FW_AGG_WAVES 6  // 80 VGPRs: 3 workgroups of 512 per CU (86 unconstrained gave 2; measured 0.425 -> 0.371 ms at C2)
 #endif
+#ifndef FW_SESS_WAVES
+#define FW_SESS_WAVES 4  // the same for the session instantiation
+#endif
 #ifndef FW_SCATTER_WAVES
 #define FW_SCATTER_WAVES 1
 #endif
