@@ -710,3 +710,38 @@ def test_gpu_hll_hot_partition_split():
         ref.watermark(wm)
     _hll_rows_equal(gpu.rows(), ref.rows())
     gpu.close()
+
+
+def test_gpu_c2_full_size_properties():
+    # BASELINE configs[1] at full size (four 2^24-record batches generated in HBM, 1M keys, 1 s tumbling,
+    # bounded out-of-orderness 200 ms), beyond what the oracle finishes in seconds: size-independent
+    # properties instead of row-by-row parity.  Conservation of counts, checksum of sums, global min/max,
+    # one row per distinct (key, window), and aligned window bounds.
+    import torch
+    from flink_amd.datagen import generate_device
+    n, steps, num_keys, rate = 1 << 24, 4, 1_000_000, 100_000_000
+    gpu = _gpu_op("tumbling", size=1000)
+    total = 0
+    vsum = 0
+    vmin, vmax = 1 << 63, -(1 << 63)
+    ids = []
+    for s in range(steps):
+        k, t, v, mx = generate_device(0x5EED, s * n, n, num_keys, ts_base=1_000_000, rate=rate, jitter=200)
+        torch.cuda.synchronize()
+        total += n
+        vsum += int(v.sum().item())
+        vmin, vmax = min(vmin, int(v.min().item())), max(vmax, int(v.max().item()))
+        ids.append(k * 100_000 + (t - 1_000_000) // 1000)  # (key, window index): ts stays above the base
+        gpu.process_batch(k, t, v)
+        gpu.watermark(int(mx.item()) - 200)
+    gpu.watermark((1 << 63) - 1)
+    rows = gpu.rows()
+    assert gpu.late_dropped == 0
+    gpu.close()
+    assert int(rows["count"].sum()) == total
+    assert int(rows["sum"].astype(np.int64).sum()) == vsum
+    assert int(rows["min"].min()) == vmin and int(rows["max"].max()) == vmax
+    assert np.all(rows["end"] - rows["start"] == 1000) and np.all(rows["start"] % 1000 == 0)
+    distinct = torch.unique(torch.cat(ids)).numel()
+    assert len(rows) == distinct
+    assert len(np.unique(rows["key"] * 100_000 + (rows["start"] - 1_000_000) // 1000)) == distinct
