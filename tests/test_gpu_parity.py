@@ -745,3 +745,41 @@ def test_gpu_c2_full_size_properties():
     distinct = torch.unique(torch.cat(ids)).numel()
     assert len(rows) == distinct
     assert len(np.unique(rows["key"] * 100_000 + (rows["start"] - 1_000_000) // 1000)) == distinct
+
+
+@pytest.mark.parametrize("workload", ["c3", "c4", "c5"])
+def test_gpu_full_size_count_conservation(workload):
+    # SURVEY §8d C3/C4/C5 shapes at full batch size (2^24 records per push, generated in HBM): every record
+    # is counted once per window it belongs to (60 sliding windows at C3; one session or one tumbling window
+    # at C4/C5) once the final watermark has fired everything; no record is late (bound >= jitter)
+    import torch
+    from flink_amd.datagen import generate_device, zipf_cdf
+    from flink_amd.windowing import HyperLogLog
+    n, steps = 1 << 24, 2
+    if workload == "c3":
+        cfg, keys, rate, jitter, per = dict(assigner="sliding", size=60_000, slide=1000), 2_000_000, 100_000_000, 200, 60
+    elif workload == "c4":
+        cfg, keys, rate, jitter, per = dict(assigner="session", gap=30_000), 1_000_000, 100_000, 1000, 1
+    else:
+        cfg, keys, rate, jitter, per = dict(assigner="tumbling", size=1000), 1_000_000, 100_000_000, 200, 1
+    cdf = None if workload == "c3" else torch.tensor(zipf_cdf(keys, 1.1), dtype=torch.float64, device="cuda")
+    if workload == "c5":
+        from flink_amd.operator import GpuWindowOperator
+        gpu = GpuWindowOperator(TumblingEventTimeWindows.of(1000, 0), HyperLogLog(14),
+                                expected_entries=2_000_000)  # 2 live windows of up to 1M keys (40 GB pool)
+    else:
+        gpu = _gpu_op(**cfg)
+    for s in range(steps):
+        k, t, v, mx = generate_device(0x5EED, s * n, n, keys, ts_base=1_000_000, rate=rate, jitter=jitter,
+                                      cdf_dev=cdf)
+        gpu.process_batch(k, t, v)
+        gpu.watermark(int(mx.item()) - jitter)
+    gpu.watermark((1 << 63) - 1)
+    rows = gpu.rows()
+    assert gpu.late_dropped == 0
+    gpu.close()
+    assert int(rows["count"].sum()) == per * n * steps
+    if workload == "c4":  # sessions of one key never overlap or touch (gap-separated)
+        r = rows[np.lexsort((rows["start"], rows["key"]))]
+        same = r["key"][1:] == r["key"][:-1]
+        assert np.all(r["start"][1:][same] > r["end"][:-1][same])
