@@ -41,7 +41,9 @@
 #define FW_AGG_CHUNK 32768     // records per aggregate workgroup of a split partition (hot keys); 16384 -> 32768: C4 6.9e9 -> 7.7e9, C5 6.1e9 -> 6.7e9 records/s
 #endif
 #define FW_LDS_SLOTS 1024      // LDS pre-aggregation slots per aggregate workgroup
+#ifndef FW_LDS_FILL_LIMIT
 #define FW_LDS_FILL_LIMIT 820  // ~0.8 * FW_LDS_SLOTS: a new slot is not claimed beyond this fill
+#endif
 #define FW_FIRE_THREADS 256
 #define FW_SLOW_THREADS 1024   // ordered replay workgroup (one workgroup)
 
