@@ -74,14 +74,23 @@ __device__ __forceinline__ int32_t key_hash_of(int32_t kind, int64_t key, const 
 }
 // KeyGroupRangeAssignment.computeKeyGroupForKeyHash (KeyGroupRangeAssignment.java:69-71)
 __device__ __forceinline__ int32_t key_group(int32_t h, int32_t max_par) { return murmur(h) % max_par; }
+// fmix64 is a bijection: its inverse (multiplicative inverses of the two constants mod 2^64)
+__device__ __forceinline__ uint64_t fmix64_inv(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0x9cb4b2f8129337dbull;
+  x ^= x >> 33;
+  x *= 0x4f74430c22a54005ull;
+  x ^= x >> 33;
+  return x;
+}
+constexpr uint64_t SUB_SALT = 0x5851F42D4C957F2Dull;
 // state partition of a key inside the handle's KeyGroupRange, -1 when outside it
 __device__ __forceinline__ int32_t partition_of(const DevCfg& c, int64_t key, int32_t h) {
   int32_t local = key_group(h, c.max_par) - c.kg0;
   if ((uint32_t)local >= (uint32_t)c.n_kg) return -1;
-  uint32_t sub = c.log_s ? (uint32_t)(fmix64((uint64_t)key ^ 0x5851F42D4C957F2Dull) >> (64 - c.log_s)) : 0u;
+  uint32_t sub = c.log_s ? (uint32_t)(fmix64((uint64_t)key ^ SUB_SALT) >> (64 - c.log_s)) : 0u;
   return (local << c.log_s) | (int32_t)sub;
 }
-
 // unsigned n / d for an invariant d via its reciprocal (m, l) from make_div_inv (Granlund and
 // Montgomery, "Division by invariant integers using multiplication", Fig. 4.1): exact for every n
 __device__ __forceinline__ uint64_t div_inv(uint64_t n, uint64_t m, int32_t l) {
@@ -106,6 +115,26 @@ __device__ __forceinline__ int64_t cleanup_of(int64_t end, int64_t lateness) {
   int64_t c = jadd(mx, lateness);
   return c >= mx ? c : LMAX;
 }
+// ---- compact records (CRec, DevCfg::compact)
+// window delta of a one-window record's window start, or -1 when it has no compact form
+__device__ __forceinline__ int64_t compact_delta(const DevCfg& c, int64_t start) {
+  const uint64_t diff = (uint64_t)start - (uint64_t)c.cbase;
+  const uint64_t d = div_inv(diff, c.mag_slide, c.l_slide);
+  return d < (1ull << c.log_s) ? (int64_t)d : -1;
+}
+__device__ __forceinline__ int64_t compact_encode(const DevCfg& c, int64_t key, int64_t d) {
+  const int sh = 64 - c.log_s;
+  return (int64_t)((fmix64((uint64_t)key ^ SUB_SALT) & ((1ull << sh) - 1)) | ((uint64_t)d << sh));
+}
+// the key and window start of a compact record of partition p
+__device__ __forceinline__ void compact_decode(const DevCfg& c, int32_t p, int64_t kw, int64_t* key, int64_t* start) {
+  const int sh = 64 - c.log_s;
+  const uint64_t sub = (uint64_t)(p & ((1 << c.log_s) - 1));
+  const uint64_t h = ((uint64_t)kw & ((1ull << sh) - 1)) | (sub << sh);
+  *key = (int64_t)(fmix64_inv(h) ^ SUB_SALT);
+  *start = (int64_t)((uint64_t)c.cbase + ((uint64_t)kw >> sh) * (uint64_t)c.slide);
+}
+
 // earliest pending timer of an entry: trigger timer at maxTimestamp if registered, else GC timer
 __device__ __forceinline__ int64_t timer_of(const Entry& e, int64_t lateness) {
   return (e.meta & FW_TIMER) ? jsub(e.end, 1) : cleanup_of(e.end, lateness);
@@ -348,6 +377,20 @@ __device__ __forceinline__ Region region_of(const DevCfg& c, const DevTable& tb,
 }
 // find the live slot of (key, start, end), -1 if absent (linear probing up to the first EMPTY).
 // The fingerprint in the state word skips foreign slots without touching their entries.
+// (from slot h & mask on, for the state word `want`)
+__device__ __forceinline__ int32_t region_find(const Region& r, uint64_t h, int64_t key, int64_t start, int64_t end,
+                                               uint32_t want) {
+  for (uint32_t i = 0; i < r.mask; i++) {
+    const uint32_t s = ((uint32_t)h + i) & r.mask;
+    const uint32_t st = ld_state(r.state + s);
+    if (st == SLOT_EMPTY) return -1;
+    if (st == want) {
+      const Entry& e = r.ent[s];
+      if (e.key == key && e.start == start && e.end == end) return (int32_t)s;
+    }
+  }
+  return -1;
+}
 __device__ __forceinline__ int32_t region_find(const Region& r, uint64_t h, int64_t key, int64_t start, int64_t end) {
   const uint32_t want = live_word(h);
   for (uint32_t i = 0; i <= r.mask; i++) {
@@ -408,6 +451,55 @@ __global__ __launch_bounds__(256) void k_taint(DevCfg c, int64_t wm, const int64
   if (any) atomicMax(&st->taint_any, any);
 }
 
+// ---- streaming input of the classify / scatter tiles.  A round covers blockDim.x * FW_RPT records;
+// lane `tid` holds the pairs (j = 0 .. FW_RPT/2-1) of records rec_index(b, j, e) = b + 2(j*blockDim + tid) + e,
+// loaded as one 16-byte load per column and pair when the columns are 16-byte aligned (DevCfg::vec_in).
+__device__ __forceinline__ int64_t rec_index(int64_t b, int j, int e) {
+  return b + 2 * ((int64_t)j * blockDim.x + threadIdx.x) + e;
+}
+template <int NP, bool VAL>
+__device__ __forceinline__ void load_records(const DevCfg& c, const int64_t* __restrict__ key, const int64_t* __restrict__ ts,
+                                             const int64_t* __restrict__ val, const int32_t* __restrict__ kh, int64_t b,
+                                             int64_t end, int64_t (&k)[2 * NP], int64_t (&t)[2 * NP], int64_t (&v)[2 * NP],
+                                             int32_t (&h)[2 * NP]) {
+  const bool hashed = c.key_kind == FW_KEY_HASHED;
+#pragma unroll
+  for (int j = 0; j < NP; j++) {  // all loads in flight before any use
+    const int64_t i = rec_index(b, j, 0);
+    if (c.vec_in && i + 1 < end) {
+      const i64x2 kk = *reinterpret_cast<const i64x2*>(key + i);
+      const i64x2 tt = *reinterpret_cast<const i64x2*>(ts + i);
+      k[2 * j] = kk.x, k[2 * j + 1] = kk.y;
+      t[2 * j] = tt.x, t[2 * j + 1] = tt.y;
+      if (VAL) {
+        const i64x2 vv = *reinterpret_cast<const i64x2*>(val + i);
+        v[2 * j] = vv.x, v[2 * j + 1] = vv.y;
+      }
+      if (hashed) {
+        const int2 hh = *reinterpret_cast<const int2*>(kh + i);
+        h[2 * j] = hh.x, h[2 * j + 1] = hh.y;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const bool in = i + e < end;
+        k[2 * j + e] = in ? key[i + e] : 0;
+        t[2 * j + e] = in ? ts[i + e] : 0;
+        if (VAL) v[2 * j + e] = in ? val[i + e] : 0;
+        if (hashed) h[2 * j + e] = in ? kh[i + e] : 0;
+      }
+    }
+  }
+}
+// tile of a classify / scatter workgroup: with FW_XCD_TILES, blocks b, b+8, b+16, ... (one XCD) take
+// consecutive tiles, so the partition runs of neighbouring tiles meet in one L2
+__device__ __forceinline__ int32_t tile_of_block(int32_t T) {
+  const int32_t b = blockIdx.x;
+  if (!FW_XCD_TILES) return b;
+  const int32_t per = T >> 3, rem = T & 7, g = b & 7;
+  return g * per + min(g, rem) + (b >> 3);
+}
+
 // ---- K1: classify + partition histogram.  hist is (P+1) x T, partition-major; row P counts
 // the records of each tile that go to the ordered path (scanned with the partitions), row P+1
 // keeps that count unscanned for k_scatter_ordered.
@@ -418,34 +510,32 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_classify_hist(DevCfg c, int
   extern __shared__ uint32_t lh[];
   for (int i = threadIdx.x; i <= c.P; i += blockDim.x) lh[i] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * FW_TILE;
+  const int32_t tile = blockIdx.x;
+  const int64_t base = (int64_t)tile * FW_TILE;
   const int64_t end = min(n, base + (int64_t)FW_TILE);
-  int bad_kg = 0, bad_ts = 0;
+  int bad_kg = 0, bad_ts = 0, wide = 0;
   unsigned slow = 0;
   const int taint = c.assigner == FW_SESSION ? st->taint_any : 0;
   for (int64_t b = base; b < end; b += (int64_t)blockDim.x * FW_RPT) {
-    int64_t k[FW_RPT], t[FW_RPT];
+    int64_t k[FW_RPT], t[FW_RPT], v[FW_RPT];
     int32_t h[FW_RPT];
-#pragma unroll
-    for (int j = 0; j < FW_RPT; j++) {  // all loads in flight before any use
-      const int64_t i = b + (int64_t)j * blockDim.x + threadIdx.x;
-      k[j] = i < end ? key[i] : 0;
-      t[j] = i < end ? ts[i] : 0;
-      h[j] = i < end && c.key_kind == FW_KEY_HASHED ? kh[i] : 0;
-    }
+    load_records<FW_RPT / 2, false>(c, key, ts, nullptr, kh, b, end, k, t, v, h);
 #pragma unroll
     for (int j = 0; j < FW_RPT; j++) {
-      const int64_t i = b + (int64_t)j * blockDim.x + threadIdx.x;
+      const int64_t i = rec_index(b, j >> 1, j & 1);
       if (i >= end) continue;
       const int32_t p = partition_of(c, k[j], c.key_kind == FW_KEY_HASHED ? h[j] : key_hash_of(c.key_kind, k[j], kh, i));
       if (p < 0) {
         bad_kg++;
         continue;
       }
-      const int cls = classify(c, wm, t[j], nullptr, nullptr, k[j], taint);
-      if (cls == CLS_NORMAL)
+      int64_t last = 0;
+      int nw = 0;
+      const int cls = classify(c, wm, t[j], &last, &nw, k[j], taint);
+      if (cls == CLS_NORMAL) {
         atomicAdd(&lh[p], 1u);
-      else if (cls == CLS_SLOW)
+        if (c.compact && compact_delta(c, last) < 0) wide = 1;
+      } else if (cls == CLS_SLOW)
         slow++;
       else if (cls == CLS_BADTS)
         bad_ts++;
@@ -453,10 +543,11 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_classify_hist(DevCfg c, int
   }
   if (slow) atomicAdd(&lh[c.P], slow);
   __syncthreads();
-  for (int i = threadIdx.x; i <= c.P; i += blockDim.x) hist[(int64_t)i * T + blockIdx.x] = lh[i];
-  if (threadIdx.x == 0) hist[(int64_t)(c.P + 1) * T + blockIdx.x] = lh[c.P];
+  for (int i = threadIdx.x; i <= c.P; i += blockDim.x) hist[(int64_t)i * T + tile] = lh[i];
+  if (threadIdx.x == 0) hist[(int64_t)(c.P + 1) * T + tile] = lh[c.P];
   if (bad_kg) atomicAdd(&st->kg_errors, bad_kg);
   if (bad_ts) atomicAdd(&st->ts_errors, bad_ts);
+  if (wide) atomicOr(&st->wide, 1);
 }
 
 // ---- generic in-place exclusive scan of uint32 (block = 1024 threads x 4 elements)
@@ -558,27 +649,21 @@ __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(D
                                                              const uint32_t* __restrict__ offs, PRec* __restrict__ part,
                                                              DevSide side, Status* st) {
   extern __shared__ uint32_t base[];  // P: next free slot of each partition's run for this tile
-  for (int i = threadIdx.x; i < c.P; i += blockDim.x) base[i] = offs[(int64_t)i * T + blockIdx.x];
+  const int32_t tile = tile_of_block(T);
+  for (int i = threadIdx.x; i < c.P; i += blockDim.x) base[i] = offs[(int64_t)i * T + tile];
   __syncthreads();
-  const int64_t tbase = (int64_t)blockIdx.x * FW_TILE;
+  const int64_t tbase = (int64_t)tile * FW_TILE;
   const int64_t tend = min(n, tbase + (int64_t)FW_TILE);
   unsigned long long late = 0;
   const int taint = c.assigner == FW_SESSION ? st->taint_any : 0;
+  const bool cmp = c.compact && !st->wide;  // (uniform: every classify workgroup has finished)
   for (int64_t b = tbase; b < tend; b += (int64_t)blockDim.x * FW_RPT) {
     int64_t k[FW_RPT], t[FW_RPT], v[FW_RPT];
     int32_t hh[FW_RPT];
-#pragma unroll
-    for (int j = 0; j < FW_RPT; j++) {  // all loads in flight before any use
-      const int64_t i = b + (int64_t)j * blockDim.x + threadIdx.x;
-      const bool in = i < tend;
-      k[j] = in ? key[i] : 0;
-      t[j] = in ? ts[i] : 0;
-      v[j] = in ? val[i] : 0;
-      hh[j] = in && c.key_kind == FW_KEY_HASHED ? kh[i] : 0;
-    }
+    load_records<FW_RPT / 2, true>(c, key, ts, val, kh, b, tend, k, t, v, hh);
 #pragma unroll
     for (int j = 0; j < FW_RPT; j++) {
-      const int64_t i = b + (int64_t)j * blockDim.x + threadIdx.x;
+      const int64_t i = rec_index(b, j >> 1, j & 1);
       bool norm = false;
       uint32_t pos = 0;
       int64_t last = 0;
@@ -599,17 +684,36 @@ __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(D
           }
         }
       }
-      if (c.diag & (DIAG_SCATTER_NO_STORE | DIAG_SCATTER_LINEAR | DIAG_SCATTER_SINGLE)) {
+      if (c.diag & (DIAG_SCATTER_NO_STORE | DIAG_SCATTER_LINEAR | DIAG_SCATTER_SINGLE | DIAG_SCATTER_HALF |
+                    DIAG_SCATTER_NT)) {
         if (c.diag & DIAG_SCATTER_NO_STORE) {
           asm volatile("" ::"v"(pos), "v"(k[j]), "v"(last), "v"(v[j]));
           continue;
         }
         if (c.diag & DIAG_SCATTER_LINEAR) pos = (uint32_t)i;
+        if ((c.diag & DIAG_SCATTER_HALF) && norm) {  // 16 B per record (timing of a compact record)
+          i64x2* dst = reinterpret_cast<i64x2*>(part) + pos;
+          if (c.diag & DIAG_SCATTER_NT)
+            __builtin_nontemporal_store(i64x2{k[j] ^ last, v[j]}, dst);
+          else
+            *dst = i64x2{k[j] ^ last, v[j]};
+          continue;
+        }
+        if ((c.diag & DIAG_SCATTER_NT) && norm) {
+          i64x2* dst = reinterpret_cast<i64x2*>(part + pos);
+          __builtin_nontemporal_store(i64x2{k[j], last}, dst);
+          __builtin_nontemporal_store(i64x2{v[j], (long long)nwin}, dst + 1);
+          continue;
+        }
         if (norm) {
           i64x2* dst = reinterpret_cast<i64x2*>(part + pos);
           dst[0] = i64x2{k[j], last};
           dst[1] = i64x2{v[j], (long long)nwin};
         }
+        continue;
+      }
+      if (cmp) {  // CRec: one 16-byte store
+        if (norm) reinterpret_cast<i64x2*>(part)[pos] = i64x2{compact_encode(c, k[j], compact_delta(c, last)), v[j]};
         continue;
       }
       // FW_AGG_FIRST: the record's arrival ordinal rides above the window count (nwin < 2^16)
@@ -823,6 +927,51 @@ __device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, in
   return true;
 }
 
+// One-window records (tumbling, panes), RPT per thread: every record's (key, window) is first looked up in
+// its home bucket with all RPT lookups in flight together (tag bucket, then the candidate's key), and the
+// hits accumulate at once; the rest (new windows, fingerprint collisions, buckets being claimed) go through
+// lds_slot one by one.  dm: bit j = record j is accumulated (or absent); false when the table is full (the
+// caller flushes and calls again with the same dm).
+template <int RPT>
+__device__ __forceinline__ bool lds_upsert_batch(AggLds& L, int vtype, const int64_t (&k)[RPT], const int64_t (&s)[RPT],
+                                                 const int64_t (&v)[RPT], const int64_t (&o)[RPT], int first,
+                                                 uint32_t& dm) {
+  uint32_t b[RPT], fp[RPT];
+  u32x4 t4[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; j++) {
+    const uint32_t h = lds_hash(k[j], s[j]);
+    fp[j] = lds_fp(h);
+    b[j] = h & (LDS_BUCKETS - 1);
+    if (!(dm >> j & 1)) t4[j] = *reinterpret_cast<const u32x4*>(&L.tag[b[j] * 4]);
+  }
+  int cand[RPT];
+  i64x2 kv[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; j++) {
+    cand[j] = -1;
+    if (dm >> j & 1) continue;
+    const u32x4 t = t4[j];
+    cand[j] = t.x == fp[j] ? 0 : t.y == fp[j] ? 1 : t.z == fp[j] ? 2 : t.w == fp[j] ? 3 : -1;
+    if (cand[j] >= 0) kv[j] = L.kv[b[j] * 4 + cand[j]];
+  }
+#pragma unroll
+  for (int j = 0; j < RPT; j++) {
+    if (cand[j] < 0 || kv[j].x != k[j] || kv[j].y != s[j]) continue;
+    lds_acc(L, (int)b[j] * 4 + cand[j], vtype, v[j], o[j], first);
+    dm |= 1u << j;
+  }
+#pragma unroll
+  for (int j = 0; j < RPT; j++) {
+    if (dm >> j & 1) continue;
+    const int target = lds_slot(L, k[j], s[j]);
+    if (target < 0) return false;
+    lds_acc(L, target, vtype, v[j], o[j], first);
+    dm |= 1u << j;
+  }
+  return true;
+}
+
 // the LDS delta of slot h as a region entry
 __device__ __forceinline__ Entry lds_delta(const DevCfg& c, const AggLds& L, int h) {
   const i64x2 kv = L.kv[h];
@@ -846,24 +995,58 @@ __device__ __forceinline__ Entry lds_delta(const DevCfg& c, const AggLds& L, int
 // in place (plain read-modify-write: the workgroup owns the region) and claims EMPTY slots for the
 // new ones.  (A front-to-back sweep of the region instead of probe chains measured slower at C2:
 // its dependent loads per thread are longer than a probe chain at a region's load.)
+// DIAG_AGG_TIMING clocks of the tumbling/sliding flush (thread 0): [0] flushes, [1] phase A, [2] phase B, [3] tail
+__device__ unsigned long long g_flt[4];
 __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* st) {
   __syncthreads();
+  const bool timing = c.diag & DIAG_AGG_TIMING;
+  const unsigned long long tf0 = timing ? __builtin_amdgcn_s_memtime() : 0;
   if (c.diag & DIAG_AGG_NO_FLUSH) {
     for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
     if (threadIdx.x == 0) L.fill = 0;
     __syncthreads();
     return true;
   }
+  // Phase A.  Each thread locates its FS LDS windows with every home slot's state word and entry
+  // identity (key, start, end) loaded together, so the common cases at a region's load (the home slot
+  // holds the window, or is EMPTY) cost one round trip for all of them; longer probe chains continue one
+  // slot at a time.  (Phase B re-reads the entries it merges into from the L2.)
+  constexpr int FS = FW_LDS_SLOTS / FW_AGG_THREADS;
   int nnew = 0;
-  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
-    if (L.tag[h] < 2) continue;
+  bool lv[FS];
+  uint32_t hw[FS];
+  i64x2 hks[FS];
+  int64_t hend[FS];
+#pragma unroll
+  for (int q = 0; q < FS; q++) {
+    const int h = threadIdx.x + q * FW_AGG_THREADS;
+    lv[q] = L.tag[h] >= 2;
+    if (lv[q]) {
+      const i64x2 kv = L.kv[h];
+      const uint32_t home = (uint32_t)slot_hash(c, kv.x, kv.y) & r.mask;
+      hw[q] = ld_state(r.state + home);
+      hks[q] = *reinterpret_cast<const i64x2*>(&r.ent[home].key);
+      hend[q] = r.ent[home].end;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < FS; q++) {
+    if (!lv[q]) continue;
+    const int h = threadIdx.x + q * FW_AGG_THREADS;
     const i64x2 kv = L.kv[h];
-    const int32_t slot = region_find(r, slot_hash(c, kv.x, kv.y), kv.x, kv.y, wend(c, kv.y));
+    const uint64_t hs = slot_hash(c, kv.x, kv.y);
+    const int64_t we = wend(c, kv.y);
+    int32_t slot = -1;
+    if (hw[q] == live_word(hs) && hks[q].x == kv.x && hks[q].y == kv.y && hend[q] == we)
+      slot = (int32_t)((uint32_t)hs & r.mask);
+    else if (hw[q] != SLOT_EMPTY)  // the rest of the probe chain
+      slot = region_find(r, hs + 1, kv.x, kv.y, we, live_word(hs));
     L.slot[h] = slot;
     nnew += slot < 0;
   }
   if (nnew) atomicAdd(&L.nnew, nnew);
   __syncthreads();
+  const unsigned long long tf1 = timing ? __builtin_amdgcn_s_memtime() : 0;
   const int32_t need = L.live + L.nnew;
   if (need > region_limit(c.log_r)) {
     if (threadIdx.x == 0) atomicMax(&st->need_live, need);
@@ -896,21 +1079,22 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
   int64_t mt = LMAX;
   unsigned long long nflush = 0;
   int lost = 0;
-  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
-    if (L.tag[h] < 2) continue;
+#pragma unroll
+  for (int q = 0; q < FS; q++) {
+    if (!lv[q]) continue;
+    const int h = threadIdx.x + q * FW_AGG_THREADS;
     const Entry d = lds_delta(c, L, h);
     nflush++;
     mt = min(mt, c.panes ? d.meta : jsub(d.end, 1));
     const int32_t slot = L.slot[h];
     if (slot >= 0) {
-      Entry& x = r.ent[slot];
-      Entry cur = x;
+      Entry cur = r.ent[slot];
       acc_merge(c, cur, d);
       if (c.panes)
         cur.meta = min(cur.meta, d.meta);
       else
         cur.meta |= FW_TIMER;
-      x = cur;
+      r.ent[slot] = cur;
     } else {
       const uint64_t hs = slot_hash(c, d.key, d.start);
       const int32_t ns = region_claim(r, hs, live_word(hs));
@@ -932,6 +1116,7 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
   if (mt != LMAX) atomicMin((long long*)&L.min_timer, (long long)mt);
   if (nflush) atomicAdd(&L.flushed, nflush);
   __syncthreads();
+  const unsigned long long tf2 = timing ? __builtin_amdgcn_s_memtime() : 0;
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
   if (threadIdx.x == 0) {
     L.fill = 0;
@@ -939,6 +1124,12 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
     L.nnew = 0;
   }
   __syncthreads();
+  if (timing && threadIdx.x == 0) {
+    atomicAdd(&g_flt[0], 1ull);
+    atomicAdd(&g_flt[1], tf1 - tf0);
+    atomicAdd(&g_flt[2], tf2 - tf1);
+    atomicAdd(&g_flt[3], __builtin_amdgcn_s_memtime() - tf2);
+  }
   return true;
 }
 
@@ -1310,12 +1501,45 @@ __device__ void agg_spill(const DevCfg& c, AggLds& L, const int64_t* E, Entry* o
 // chunk's deltas into the region with the LDS table and the usual flush, which may suspend; a resumed
 // launch continues phase 2 in the partition's chunk-0 workgroup (prog.rb = delta round, prog.tp = delta
 // of the round per thread).
+// record i of a partition run: the raw 32 bytes of a PRec, or the 16 bytes of a CRec (cmp), loaded as
+// 16-byte halves, then unpacked once every record of the round is in flight
+__device__ __forceinline__ void load_prec_raw(bool cmp, const PRec* part, int64_t i, bool in, i64x2& a, i64x2& b) {
+  a = i64x2{0, 0};
+  b = i64x2{0, 0};
+  if (!in) return;
+  if (cmp) {
+    a = reinterpret_cast<const i64x2*>(part)[i];
+  } else {
+    const i64x2* src = reinterpret_cast<const i64x2*>(part + i);
+    a = src[0];
+    b = src[1];
+  }
+}
+// key, newest window start, value, window count and (FIRST) arrival ordinal of a record of partition p
+template <bool FIRST>
+__device__ __forceinline__ void unpack_prec(const DevCfg& c, bool cmp, int32_t p, const i64x2& a, const i64x2& b,
+                                            int64_t& k, int64_t& t, int64_t& v, int& nw, int64_t& o) {
+  if (cmp) {
+    compact_decode(c, p, a.x, &k, &t);
+    v = a.y;
+    nw = 1;
+    o = 0;
+    return;
+  }
+  k = a.x;
+  t = a.y;
+  v = b.x;
+  nw = FIRST ? (int)(b.y & 0xffff) : (int)b.y;
+  o = FIRST ? (int64_t)b.y >> 16 : 0;
+}
+
 template <int RPT, bool SESS, bool FIRST>
 __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __restrict__ part, int64_t begin,
                           int64_t end, int32_t p, int32_t ch, int32_t nch, DevTable& tb, const AggProg& prog,
                           int resume, const AggHot& hot, Status* st) {
   const int32_t c0 = (int32_t)hot.chunk_base[p];
   if (resume && (ch != 0 || prog.done[p])) return;
+  const bool cmp = c.compact && !st->wide;
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
   if (threadIdx.x == 0) {
     L.fill = 0;
@@ -1328,19 +1552,16 @@ __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __
     const int64_t cb = begin + (int64_t)ch * FW_AGG_CHUNK, ce = min(end, cb + (int64_t)FW_AGG_CHUNK);
     for (int64_t rb = cb; rb < ce; rb += (int64_t)blockDim.x * RPT) {
       int64_t k[RPT], t[RPT], v[RPT], o[RPT];
+      i64x2 ra[RPT], rbb[RPT];
 #pragma unroll
       for (int j = 0; j < RPT; j++) {
         const int64_t i = rb + (int64_t)j * blockDim.x + threadIdx.x;
-        i64x2 a = {0, 0}, b2 = {0, 0};
-        if (i < ce) {
-          const i64x2* src = reinterpret_cast<const i64x2*>(part + i);
-          a = src[0];
-          b2 = src[1];
-        }
-        k[j] = a.x;
-        t[j] = a.y;
-        v[j] = b2.x;
-        o[j] = FIRST ? (int64_t)b2.y >> 16 : 0;
+        load_prec_raw(cmp, part, i, i < ce, ra[j], rbb[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < RPT; j++) {
+        int nw;
+        unpack_prec<FIRST>(c, cmp, p, ra[j], rbb[j], k[j], t[j], v[j], nw, o[j]);
       }
       int rj = 0;
       for (;;) {
@@ -1461,6 +1682,8 @@ __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __
 // DIAG_AGG_TIMING: per-workgroup phase clocks (s_memtime), summed over the launch and printed by the
 // last workgroup to finish: [0] record loop, [1] flushes, [2] whole workgroup, [3] finished workgroups
 __device__ unsigned long long g_aggt[4];
+__device__ unsigned long long g_occ[3];  // running, sum of running at starts, max running
+__device__ unsigned long long g_loop[3];  // thread 0's record loop: load wait, LDS upsert, barriers
 template <int RPT, bool SESS, bool FIRST>
 __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? FW_SESS_WAVES : FW_AGG_WAVES) void k_aggregate(DevCfg c, int64_t wm, const PRec* __restrict__ part,
                                                               const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
@@ -1488,6 +1711,7 @@ __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? FW_SESS_WAVES : FW_AGG_WAVES
     }
   }
   if (resume && prog.done[p]) return;
+  const bool cmp = c.compact && !st->wide;
   const int64_t begin = offs[(int64_t)p * T], end = offs[(int64_t)(p + 1) * T];
   if (begin == end) {
     if (threadIdx.x == 0) prog.done[p] = 1;
@@ -1515,29 +1739,78 @@ __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? FW_SESS_WAVES : FW_AGG_WAVES
   __syncthreads();
   const Region r = region_of(c, tb, p, tb.cur[p]);
   bool ok = true, first = true;
+  const bool onewin = c.wpr == 1 || c.panes;
   const bool timing = c.diag & DIAG_AGG_TIMING;
   unsigned long long tw0 = timing ? __builtin_amdgcn_s_memtime() : 0, tflush = 0;
+  if (timing && threadIdx.x == 0) {  // concurrency: workgroups running when this one starts
+    const unsigned long long run = atomicAdd(&g_occ[0], 1ull) + 1;
+    atomicAdd(&g_occ[1], run);
+    atomicMax(&g_occ[2], run);
+  }
+  unsigned long long t_ld = 0, t_up = 0, t_bar = 0, ts_a = 0;
   for (int64_t rb = srb; rb < end && ok; rb += (int64_t)blockDim.x * RPT) {
     int64_t k[RPT], t[RPT], v[RPT], o[RPT];
     int nw[RPT];
+    if (timing) ts_a = __builtin_amdgcn_s_memtime();
+    {
+      i64x2 ra[RPT], rbb[RPT];
 #pragma unroll
-    for (int j = 0; j < RPT; j++) {  // all loads in flight before any use
-      const int64_t i = rb + (int64_t)j * blockDim.x + threadIdx.x;
-      i64x2 a = {0, 0}, b2 = {0, 0};
-      if (i < end) {
-        const i64x2* src = reinterpret_cast<const i64x2*>(part + i);
-        a = src[0];
-        b2 = src[1];
+      for (int j = 0; j < RPT; j++) {  // all loads in flight before any use
+        const int64_t i = rb + (int64_t)j * blockDim.x + threadIdx.x;
+        load_prec_raw(cmp, part, i, i < end, ra[j], rbb[j]);
       }
-      k[j] = a.x;
-      t[j] = a.y;  // newest window start (assigned by k_scatter)
-      v[j] = b2.x;
-      nw[j] = FIRST ? (int)(b2.y & 0xffff) : (int)b2.y;
-      o[j] = FIRST ? (int64_t)b2.y >> 16 : 0;  // FW_AGG_FIRST: arrival ordinal
+      if (timing) {
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long x = __builtin_amdgcn_s_memtime();
+        t_ld += x - ts_a;
+        ts_a = x;
+      }
+      // t = newest window start (assigned by k_scatter); o = FW_AGG_FIRST: arrival ordinal
+#pragma unroll
+      for (int j = 0; j < RPT; j++) unpack_prec<FIRST>(c, cmp, p, ra[j], rbb[j], k[j], t[j], v[j], nw[j], o[j]);
     }
     if (c.diag & DIAG_AGG_NO_LDS) {
 #pragma unroll
       for (int j = 0; j < RPT; j++) asm volatile("" ::"v"(k[j]), "v"(t[j]), "v"(v[j]), "v"(nw[j]));
+      continue;
+    }
+    if (!SESS && onewin) {
+      // one window per record: srj / rj is the round's done mask (lds_upsert_batch)
+      uint32_t dm = first ? (uint32_t)srj : 0u;
+      first = false;
+#pragma unroll
+      for (int j = 0; j < RPT; j++)
+        if (rb + (int64_t)j * blockDim.x + threadIdx.x >= end) dm |= 1u << j;
+      for (;;) {
+        if (!lds_upsert_batch<RPT>(L, c.vtype, k, t, v, o, FIRST ? c.agg : 0, dm)) L.anyfail = 1;
+        if (timing) {
+          __builtin_amdgcn_s_waitcnt(0);
+          const unsigned long long x = __builtin_amdgcn_s_memtime();
+          t_up += x - ts_a;
+          ts_a = x;
+        }
+        __syncthreads();
+        const int need = L.anyfail;
+        __syncthreads();
+        if (timing) {
+          const unsigned long long x = __builtin_amdgcn_s_memtime();
+          t_bar += x - ts_a;
+          ts_a = x;
+        }
+        if (!need) break;
+        const unsigned long long tf0 = timing ? __builtin_amdgcn_s_memtime() : 0;
+        const bool fl = agg_flush_any<SESS>(c, L, sess_end, r, st);
+        if (timing) tflush += __builtin_amdgcn_s_memtime() - tf0;
+        if (!fl) {
+          ok = false;
+          break;
+        }
+        srb = rb;
+        srj = (int)dm;
+        srwi = 0;
+        if (threadIdx.x == 0) L.anyfail = 0;
+        __syncthreads();
+      }
       continue;
     }
     // progress (record rj, window rwi) survives a flush-and-retry when the LDS table fills up;
@@ -1567,9 +1840,20 @@ __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? FW_SESS_WAVES : FW_AGG_WAVES
         L.anyfail = 1;
       else
         rj = RPT;  // all done: a retry pass after another thread's flush skips every record
+      if (timing) {
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long x = __builtin_amdgcn_s_memtime();
+        t_up += x - ts_a;
+        ts_a = x;
+      }
       __syncthreads();
       const int need = L.anyfail;
       __syncthreads();
+      if (timing) {
+        const unsigned long long x = __builtin_amdgcn_s_memtime();
+        t_bar += x - ts_a;
+        ts_a = x;
+      }
       if (!need) break;
       const unsigned long long tf0 = timing ? __builtin_amdgcn_s_memtime() : 0;
       const bool fl = agg_flush_any<SESS>(c, L, sess_end, r, st);
@@ -1592,15 +1876,28 @@ __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? FW_SESS_WAVES : FW_AGG_WAVES
     atomicAdd(&g_aggt[0], tl - tw0 - tflush);
     atomicAdd(&g_aggt[1], tflush + (te - tl));
     atomicAdd(&g_aggt[2], te - tw0);
+    atomicSub(&g_occ[0], 1ull);
+    atomicAdd(&g_loop[0], t_ld);
+    atomicAdd(&g_loop[1], t_up);
+    atomicAdd(&g_loop[2], t_bar);
     if (atomicAdd(&g_aggt[3], 1ull) == (unsigned long long)c.P - 1) {  // (counts unsplit partitions only)
       __threadfence();
       const double n = (double)gridDim.x;
-      printf("agg timing: per WG loop %.0f flush %.0f total %.0f clocks (%d WGs)\n", g_aggt[0] / n, g_aggt[1] / n,
-             g_aggt[2] / n, (int)gridDim.x);
+      printf("agg timing: per WG loop %.0f flush %.0f total %.0f clocks (%d WGs); running at start avg %.1f max %llu\n",
+             g_aggt[0] / n, g_aggt[1] / n, g_aggt[2] / n, (int)gridDim.x, (double)g_occ[1] / (double)c.P, g_occ[2]);
+      printf("loop (thread 0, per WG): load %.0f upsert %.0f barriers %.0f clocks\n", g_loop[0] / (double)c.P,
+             g_loop[1] / (double)c.P, g_loop[2] / (double)c.P);
+      g_occ[1] = g_occ[2] = 0;
+      g_loop[0] = g_loop[1] = g_loop[2] = 0;
       if (SESS)
         printf("session flush (thread 0, per flush): %llu flushes, link %.0f, add %.0f, tail %.0f clocks\n",
                g_sess[0], (double)g_sess[1] / (g_sess[0] + 1), (double)g_sess[2] / (g_sess[0] + 1),
                (double)g_sess[3] / (g_sess[0] + 1));
+      else
+        printf("flush (thread 0, per flush): %llu flushes, phase A %.0f, phase B %.0f, tail %.0f clocks\n",
+               g_flt[0], (double)g_flt[1] / (g_flt[0] + 1), (double)g_flt[2] / (g_flt[0] + 1),
+               (double)g_flt[3] / (g_flt[0] + 1));
+      g_flt[0] = g_flt[1] = g_flt[2] = g_flt[3] = 0;
 
       g_aggt[0] = g_aggt[1] = g_aggt[2] = g_aggt[3] = 0;
       g_sess[0] = g_sess[1] = g_sess[2] = g_sess[3] = 0;
@@ -1991,11 +2288,19 @@ __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __rest
   }
   __syncthreads();
   const int p = c.hll_p;
+  const bool cmp = c.compact && !st->wide;
   const int64_t i1 = min(total, i0 + (int64_t)FW_HLL_CHUNK);
   int32_t pp = p0_s;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
-    const PRec rec = part[i];
+    PRec rec;
+    if (cmp) {
+      const i64x2 r = reinterpret_cast<const i64x2*>(part)[i];
+      compact_decode(c, pp, r.x, &rec.key, &rec.last);
+      rec.val = r.y;
+    } else {
+      rec = part[i];
+    }
     const Region r = region_of(c, tb, pp, tb.cur[pp]);
     const int32_t slot = region_find(r, slot_hash(c, rec.key, rec.last), rec.key, rec.last, wend(c, rec.last));
     if (slot < 0) {

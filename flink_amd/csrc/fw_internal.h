@@ -18,10 +18,15 @@
 #include <stdint.h>
 #include <hip/hip_runtime_api.h>
 
+#ifndef FW_TILE
 #define FW_TILE 32768          // records per classify/scatter workgroup
+#endif
 #define FW_TILE_THREADS 1024
 #ifndef FW_RPT
-#define FW_RPT 8               // records per thread kept in flight by the streaming kernels
+#define FW_RPT 8               // records per thread kept in flight by the streaming kernels (even: pairs)
+#endif
+#ifndef FW_XCD_TILES
+#define FW_XCD_TILES 0         // 1: consecutive tiles of a partition's run on one XCD (blocks b, b+8, ...)
 #endif
 #ifndef FW_AGG_RPT
 #define FW_AGG_RPT 2           // the same for k_aggregate: 2 keeps it at 80 VGPRs = 3 workgroups per CU
@@ -84,6 +89,17 @@ struct DevCfg {
   uint64_t* taint_key;
   uint32_t* taint_state;
   uint32_t taint_mask, taint_epoch;
+  // the push's input columns are 16-byte aligned (key_hash 8-byte): the streaming kernels load two
+  // consecutive records per lane with 16-byte loads (8-byte lane loads run at ~0.6x the 16-byte rate)
+  int32_t vec_in;
+  // compact partitioned records (CRec, 16 B instead of PRec's 32 B) for one-window records (tumbling,
+  // panes) of the order-free aggregates: the key is kept as fmix64(key ^ SUB_SALT), whose top log_s bits
+  // are the record's sub-partition (known to the partition's workgroup), so those bits carry the window
+  // instead: d = (start - cbase) / slide in [0, 2^log_s).  `compact` = the configuration allows it (set at
+  // creation; 0 for this launch when the watermark gives no representable base); a batch with a normal
+  // record whose window is out of range sets Status.wide and goes through PRec.
+  int32_t compact;
+  int64_t cbase;
 };
 
 // host: reciprocal of d >= 1 for div_inv(): m = floor(2^64 (2^l - d) / d) + 1, l = ceil(log2 d)
@@ -103,7 +119,9 @@ enum {
   DIAG_AGG_NO_ACCUM = 16,  // LDS lookup/claim only, no accumulate atomics
   DIAG_AGG_RPT8 = 64,      // k_aggregate with 8 records per thread in flight
   DIAG_SCATTER_SINGLE = 128, // k_scatter: each lane stores its own record (no lane-pair sectors)
-  DIAG_AGG_TIMING = 256      // k_aggregate prints per-workgroup phase clocks
+  DIAG_AGG_TIMING = 256,     // k_aggregate prints per-workgroup phase clocks
+  DIAG_SCATTER_HALF = 512,   // k_scatter stores 16 B per record (the timing of a compact record)
+  DIAG_SCATTER_NT = 1024     // k_scatter stores with nontemporal stores
 };
 
 struct __attribute__((aligned(64))) Entry {
@@ -116,6 +134,10 @@ struct __attribute__((aligned(64))) Entry {
 // `nwin` the number of windows (1 for tumbling), newest first as SlidingEventTimeWindows emits them.
 struct __attribute__((aligned(32))) PRec {
   int64_t key, last, val, nwin;
+};
+// compact form (DevCfg::compact): {fmix64(key ^ SUB_SALT) with the window delta in its top log_s bits, val}
+struct __attribute__((aligned(16))) CRec {
+  int64_t kw, val;
 };
 
 // region state word: kind in bits 0-1, 24-bit fingerprint of the slot hash in bits 8-31, so a
@@ -138,6 +160,7 @@ struct Status {
   int32_t suspended;                  // FW_SUSP_*: later kernels of the push / watermark skip themselves
   int32_t need_grow;                  // some region is over half full: grow before it has to suspend
   int32_t taint_any;                  // sessions: 0 no tainted key in the batch, 1 check the set, 2 set full: all
+  int32_t wide;                       // DevCfg::compact: some normal record's window is out of range: PRec
 };
 enum {
   FW_STATUS_STATE_LOST = 1,  // a window could not be stored (more in-flight sessions of one key than supported)

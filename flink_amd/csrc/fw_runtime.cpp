@@ -42,6 +42,8 @@ struct Scratch {
   int64_t n = 0;                 // records of the batch
   bool split = false;            // its aggregate split long partitions (fw_op::hot)
   int64_t wm = INT64_MIN;        // watermark the batch was classified against
+  int32_t compact = 0;           // DevCfg::compact / cbase of the batch (a resumed aggregate reads the same form)
+  int64_t cbase = 0;
 };
 
 }  // namespace
@@ -405,6 +407,8 @@ int settle(fw_op* op) {
     const Scratch& S = op->sc[op->last_sc];
     DevCfg c = op->dc;
     c.slow_ord = S.so;
+    c.compact = S.compact;
+    c.cbase = S.cbase;
     if (susp & FW_SUSP_AGG)
       timed(op, K_AGGREGATE, [&] {
         fwdev::launch_aggregate(c, S.wm, S.part, S.hist, S.T, op->tb, op->prog, 1, S.split ? &op->hot : nullptr, S.n,
@@ -496,6 +500,20 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   Scratch& S = op->sc[nxt];
   c.ord_base = op->records_in;  // FW_AGG_FIRST: arrival ordinals of this batch start here
   c.slow_ord = S.so;
+  auto aligned = [](const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
+  c.vec_in = aligned(key, 16) && aligned(ts, 16) && aligned(val, 16) && (!kh || aligned(kh, 8));
+  if (c.compact) {
+    // compact records: window deltas count from 2^(log_s - 1) windows (or panes) before the watermark's,
+    // so the batch's windows on both sides of the watermark fit; no base for a watermark near Long.MIN_VALUE
+    const __int128 u = c.slide, w = op->wm, off = c.offset;
+    __int128 q = (w - off) / u;
+    if ((w - off) % u < 0) q -= 1;  // floor
+    const __int128 base = q * u + off - ((__int128)1 << (c.log_s - 1)) * u;
+    if (base < (__int128)INT64_MIN || base > (__int128)INT64_MAX)
+      c.compact = 0;
+    else
+      c.cbase = (int64_t)base;
+  }
   const int32_t T = (int32_t)((n + FW_TILE - 1) / FW_TILE);
   const int64_t m = (int64_t)(c.P + 1) * T;
   if (c.assigner == FW_SESSION) {
@@ -507,6 +525,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
     c.taint_epoch = op->taint_epoch;
     HIP_OR_RETURN(op, hipMemsetAsync(&op->d_status->taint_any, 0, sizeof(int32_t), op->stream));
   }
+  if (c.compact) HIP_OR_RETURN(op, hipMemsetAsync(&op->d_status->wide, 0, sizeof(int32_t), op->stream));
   timed(op, K_CLASSIFY, [&] {
     if (c.assigner == FW_SESSION) fwdev::launch_taint(c, op->wm, key, ts, n, op->d_status, op->stream);
     fwdev::launch_classify_hist(c, op->wm, key, ts, kh, n, T, S.hist, op->d_status, op->stream);
@@ -526,6 +545,8 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   DevCfg cc = op->dc;  // settle may have grown the table
   cc.ord_base = c.ord_base;
   cc.slow_ord = S.so;
+  cc.compact = c.compact;
+  cc.cbase = c.cbase;
   // a partition can outgrow one aggregate workgroup (hot keys) only when the batch is longer than a chunk
   const bool split = (cc.wpr == 1 || cc.panes) && n > FW_AGG_CHUNK;
   if (split && (rc = ensure_hot(op))) return rc;
@@ -543,6 +564,8 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   S.n = n;
   S.split = split;
   S.wm = op->wm;
+  S.compact = c.compact;
+  S.cbase = c.cbase;
   op->last_sc = nxt;
   op->records_in += n;
   op->push_unsettled = true;
@@ -663,6 +686,11 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     make_div_inv((uint64_t)c.size, &c.mag_size, &c.l_size);
     make_div_inv((uint64_t)c.slide, &c.mag_slide, &c.l_slide);
   }
+  // compact 16-byte partitioned records (DevCfg::compact): one window per record, an order-free aggregate,
+  // and at least 2 bits of sub-partition to carry the window delta (FW_NO_COMPACT=1 disables them)
+  c.compact = (cfg.assigner == FW_TUMBLING || c.panes) &&
+              (cfg.aggregate == FW_AGG_COUNT_SUM_MIN_MAX || cfg.aggregate == FW_AGG_HLL) && c.log_s >= 2 &&
+              !(getenv("FW_NO_COMPACT") && atoi(getenv("FW_NO_COMPACT")));
   const int64_t expected = cfg.expected_entries > 0 ? cfg.expected_entries : (int64_t)c.P * 512;
   if (cfg.aggregate >= FW_AGG_FIRST) c.agg = cfg.aggregate;
   if (cfg.aggregate == FW_AGG_HLL) {

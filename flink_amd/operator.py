@@ -120,6 +120,13 @@ class GpuWindowOperator:
                     raise ValueError("device columns must be contiguous CUDA tensors of equal length")
             if keys.dtype != torch.int64 or timestamps.dtype != torch.int64:
                 raise ValueError("keys and timestamps must be int64")
+            # fw_push_batch_device reads 8 bytes per value: a narrower column would be read out of bounds,
+            # and a float64 / int64 mix would be reinterpreted as bits
+            want = torch.float64 if self.aggregate.value_type == "double" else torch.int64
+            if values.dtype != want:
+                raise ValueError(f"values must be {want} for a {self.aggregate.value_type!r} aggregate, got {values.dtype}")
+            if key_hash is not None and key_hash.dtype != torch.int32:
+                raise ValueError("key_hash must be int32 (Java hashCode)")
             # stream-ordered handoff: the library stream waits for the producer's writes.  The push
             # is asynchronous; the columns are referenced until the next push has settled it.
             self._torch_stream(keys.device).wait_stream(torch.cuda.current_stream(keys.device))
