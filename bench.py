@@ -6,22 +6,35 @@ Workload (BASELINE.json configs[1]): 1 s tumbling event-time 
 Long keys, built-in count/sum/min/max AggregateFunction, bounded out-of-orderness watermarks (200 ms,
 punctuated after every batch), synthetic counter-based stream at 1e8 records per event-second.
 One step = one micro-batch of `--batch` records per GPU pushed through the operator plus the
-watermark that follows it (every window whose end passed fires).  Inputs are generated into HBM
-before the timed region.  With N > 1 (torchrun, one process per GPU over RCCL) each rank owns the
-KeyGroupRange computeKeyGroupRangeForOperatorIndex(128, N, rank), generates `--batch` records of the
-global stream per step and the keyBy exchange (route + RCCL all_to_all) and the watermark min
-(all_reduce) run inside the timed region: weak scaling.
+watermark that follows it (every window whose end passed fires; the sink discards the fired rows,
+which stay materialised in HBM).  Inputs are generated into HBM before the timed region.  With N > 1
+(torchrun, one process per GPU over RCCL) each rank owns the KeyGroupRange
+computeKeyGroupRangeForOperatorIndex(128, N, rank), generates `--batch` records of the global stream
+per step and the keyBy exchange (route + RCCL all_to_all) and the watermark min (all_reduce) run
+inside the timed region: weak scaling.
 
---workload c3 runs SURVEY §8d C3 (SlidingEventTimeWindows 60 s / 1 s, 60 windows per record, 2M uniform
-keys per GPU = 16M at 8 GPUs, 1e8 records per event-second per GPU, bound 200 ms); --workload c4 runs C4
-(EventTimeSessionWindows gap 30 s, 1M Zipf(1.1) keys, 1e5 records per event-second, bound 1 s).  The
-default line is C2.
+Other SURVEY §8d configs (--workload):
+  c1   WindowWordCount (configs[0]): String keys from WordCountData's 287 tokens (170 words), hashed by the
+       host, window(Tumbling 5 s).sum(1), 10M tokens per step; CPU baseline = the oracle at p = 1 for both
+       C1 pipelines (countWindow(10, 5).sum(1) and the tumbling sum)
+  c3   SlidingEventTimeWindows 60 s / 1 s (60 windows per record), 2M uniform keys per GPU
+  c4   EventTimeSessionWindows gap 30 s, 1M Zipf(1.1) keys, 1e5 records per event-second
+  c5   HyperLogLog (p = 14) per key and 1 s tumbling window, 1M Zipf(1.1) keys
+  c5t  t-digest (delta = 100) quantiles per key and 1 s tumbling window, 1M Zipf(1.1) keys
+
+Roofline: `roofline` prices the dominant kernel at the path's algorithmic bytes B_alg per
+record x the records one launch processes, over that kernel's average HIP-event duration (the kernel
+launches once per step); `impl_bytes` is what the kernel itself must move as built, `traffic` the PMC-measured
+HBM bytes per launch (profiles/traffic_*.json).  `path_roofline` is B_alg x records/s over the whole step.
+A `host_fed` leg (rank 0, N = 1) pushes further batches from pinned host memory through fw_push_batch and
+drains the fired rows to the host: the PCIe-inclusive rate of the JNI drop-in, reported beside `value`.
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -30,9 +43,11 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md §Chip-level parameters
 
-# SURVEY.md §8d workloads.  c2 is BASELINE.json configs[1] (the default, the headline line); c4 is the
-# session-window config, benchmarked on request (--workload c4).
+# SURVEY.md §8d workloads.  c2 is BASELINE.json configs[1] (the default, the headline line).
 PRESETS = {
+    "c1": dict(rate=2_000_000, bound=0, jitter=0, zipf=None, keys=287, cpu_sample=10_000_000, batch=10_000_000,
+               workload="C1 WindowWordCount: keyBy(word).window(Tumbling 5 s).sum(1), String keys (WordCountData, "
+                        "287 tokens / 170 words) hashed by the host, 10M tokens per step, 2000 tokens per ms"),
     "c2": dict(rate=100_000_000, bound=200, jitter=200, zipf=None, keys=1_000_000, cpu_sample=1 << 24,
                workload="C2 tumbling 1s event-time window, count/sum/min/max, 1M uniform Long keys, "
                         "bounded out-of-orderness 200 ms"),
@@ -42,27 +57,80 @@ PRESETS = {
     "c5": dict(rate=100_000_000, bound=200, jitter=200, zipf=1.1, keys=1_000_000, cpu_sample=1 << 20,
                workload="C5 tumbling 1s event-time window, HyperLogLog (p=14) distinct count per key and window, "
                         "1M Zipf(1.1) Long keys, bounded out-of-orderness 200 ms"),
+    "c5t": dict(rate=100_000_000, bound=200, jitter=200, zipf=1.1, keys=1_000_000, cpu_sample=1 << 22,
+                workload="C5 tumbling 1s event-time window, t-digest (delta=100) quantiles p50/p95/p99 of a Double "
+                         "field per key and window, 1M Zipf(1.1) Long keys, bounded out-of-orderness 200 ms"),
     "c4": dict(rate=100_000, bound=1000, jitter=1000, zipf=1.1, keys=1_000_000, cpu_sample=1 << 22,
                workload="C4 EventTimeSessionWindows gap 30 s, count/sum/min/max, 1M Zipf(1.1) Long keys, "
                         "bounded out-of-orderness 1 s"),
 }
 
 
-def kernel_bytes(name, n, merged, fired=0, hll_p=0, panes_per_window=0):
-    """Algorithmic bytes of one launch.  `fired` = rows fired per launch."""
+def b_alg(workload, fired_per_record, world, hll_p=14, panes=60, centroids_per_record=0.0):
+    """SURVEY §8d algorithmic HBM bytes per record (the figure `roofline` and `path_roofline` use):
+    input 24 B (+ 4 B key hash at C1), the keyBy exchange 2 x 24 (G-1)/G, state RMW where §8d counts it,
+    and the fired rows' entry reads + 56-B rows."""
+    bx = 48 * (world - 1) / world
+    f = fired_per_record
+    if workload == "c1":
+        return 28 + 104 * f + bx
+    if workload == "c3":  # pane model: one pane update per record, size/slide pane reads per fired window
+        return 24 + bx + 96 + (panes * 48 + 56) * f
+    if workload == "c4":
+        return 24 + bx + 112 * f
+    if workload == "c5":  # HLL: one register byte RMW per record, the 2^p register block read per fired row
+        return 24 + bx + 2 + ((1 << hll_p) + 56) * f
+    if workload == "c5t":  # t-digest: 16 B per record into the digest, 16 B per fired centroid + the row
+        return 24 + bx + 16 + 16 * centroids_per_record + 56 * f
+    return 24 + bx + 104 * f  # c2
+
+
+def impl_bytes(name, n, merged, fired=0, hll_p=0, panes_per_window=0, compact=True):
+    """What one launch of a kernel moves as built, for the `impl_bytes` field."""
+    rec = 16 if compact else 32  # partitioned record: CRec {key hash | window, val} or PRec
     if name == "k_fire":
-        if hll_p:  # per fired (key, window): the 64-B entry, read + zero its 2^p register block, the 56-B row
+        if hll_p:
             return fired * (64 + 2 * (1 << hll_p) + 56)
-        if panes_per_window:  # per fired window: its size/slide 64-B panes read, one 56-B row written
+        if panes_per_window:
             return fired * (64 * panes_per_window + 56)
-        return fired * (64 + 56)  # per fired window: its entry read, its row written
+        return fired * (64 + 56)
     if name == "k_classify_hist":
-        return 16 * n                      # key + ts
+        return 16 * n
     if name == "k_scatter":
-        return 24 * n + 32 * n             # read key/ts/val, write the 32-B partitioned record
+        return 24 * n + rec * n
     if name == "k_aggregate":
-        return 32 * n + 128 * merged       # read the partitioned records, RMW one 64-B entry per delta
+        return rec * n + 128 * merged
+    if name == "k_tdigest":  # keys (read the record, write 12 B), two radix sorts (8 + 3 passes of 12 B r+w)
+        return rec * n + 12 * n + 11 * 24 * n + 24 * n
     return None
+
+
+def cpu_info():
+    model = platform.processor() or "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
+def wordcount_stream(first, n):
+    """C1 tokens: token i = WordCountData's token splitmix64(0x5EED ^ 4i) mod 287; key = the word's id among
+    the 170 distinct words, key_hash = String.hashCode(word), value = 1, ts = i // 2000 ms."""
+    import numpy as np
+    from flink_amd.datagen import generate_host
+    from flink_amd.keygroups import string_hash_code
+    toks = json.load(open(os.path.join(ROOT, "tests", "golden", "wordcount_tokens.json")))["tokens"]
+    words = sorted(set(toks))
+    wid = np.array([words.index(t) for t in toks], dtype=np.int64)
+    hashes = np.array([string_hash_code(w) for w in words], dtype=np.int32)
+    idx, _, _ = generate_host(0x5EED, first, n, len(toks), ts_base=0, rate=2_000_000, jitter=0)
+    keys = wid[idx]
+    ts = (np.arange(first, first + n, dtype=np.int64) // 2000)
+    return keys, ts, np.ones(n, dtype=np.int64), hashes[keys]
 
 
 def main():
@@ -71,40 +139,46 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--workload", choices=sorted(PRESETS), default="c2")
-    ap.add_argument("--batch", type=int, default=1 << 24)
+    ap.add_argument("--batch", type=int, default=None, help="records per step per GPU (default 2^24; C1 10M)")
     ap.add_argument("--keys", type=int, default=None)
     ap.add_argument("--rate", type=int, default=None, help="records per event-second (whole job)")
     ap.add_argument("--bound", type=int, default=None, help="out-of-orderness bound (ms)")
     ap.add_argument("--jitter", type=int, default=None)
-    ap.add_argument("--window", type=int, default=1000, help="tumbling window (ms, c2)")
+    ap.add_argument("--window", type=int, default=None, help="tumbling window (ms; c2/c5 1000, c1 5000)")
     ap.add_argument("--gap", type=int, default=30_000, help="session gap (ms, c4)")
     ap.add_argument("--size", type=int, default=60_000, help="sliding window size (ms, c3)")
     ap.add_argument("--slide", type=int, default=1000, help="sliding window slide (ms, c3)")
     ap.add_argument("--hll-p", type=int, default=14, help="HyperLogLog precision (c5)")
+    ap.add_argument("--delta", type=int, default=100, help="t-digest compression (c5t)")
     ap.add_argument("--no-steady", dest="steady", action="store_false",
                     help="c3: do not extend the warmup to one window size of event time")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--zipf", type=float, default=None, help="Zipf exponent of the keys (0 = uniform)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="CPU baseline subtasks (16 = this job's CPU share of the GPU box)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-fed-steps", type=int, default=3, help="steps of the host-fed leg (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--traffic", default=None,
-                    help="PMC traffic summary (tools/traffic.py); default profiles/traffic_r01[_<workload>].json")
+                    help="PMC traffic summary (tools/traffic.py); default the newest profiles/traffic_*<workload>.json")
     ap.add_argument("--sub-partitions", type=int, default=0, help="state partitions per key group (0 = auto)")
     args = ap.parse_args()
     preset = PRESETS[args.workload]
-    if args.traffic is None:
-        args.traffic = os.path.join(ROOT, "profiles", "traffic_r01.json" if args.workload == "c2"
-                                    else f"traffic_r01_{args.workload}.json")
-    for name in ("keys", "rate", "bound", "jitter", "cpu_sample"):
+    w = args.workload
+    for name in ("keys", "rate", "bound", "jitter", "cpu_sample", "batch"):
         if getattr(args, name) is None:
-            setattr(args, name, preset[name])
+            setattr(args, name, preset.get(name, 1 << 24))
+    if args.window is None:
+        args.window = 5000 if w == "c1" else 1000
     if args.zipf is None:
         args.zipf = preset["zipf"]
     args.zipf = args.zipf or None
-    sessions = args.workload == "c4"
-    sliding = args.workload == "c3"
-    hll = args.workload == "c5"
+    if args.traffic is None:
+        for cand in (f"traffic_r02_{w}.json", f"traffic_r01_{w}.json" if w != "c2" else "traffic_r01.json"):
+            args.traffic = os.path.join(ROOT, "profiles", cand)
+            if os.path.exists(args.traffic):
+                break
+    sessions, sliding, hll, tdig, c1 = w == "c4", w == "c3", w == "c5", w == "c5t", w == "c1"
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,7 +190,7 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    from flink_amd import (CountSumMinMax, EventTimeSessionWindows, HyperLogLog, SlidingEventTimeWindows,
+    from flink_amd import (CountSumMinMax, EventTimeSessionWindows, HyperLogLog, SlidingEventTimeWindows, TDigest,
                            TumblingEventTimeWindows)
     from flink_amd import _native as N
     from flink_amd.datagen import generate_device, zipf_cdf
@@ -137,10 +211,11 @@ def main():
         assigner = TumblingEventTimeWindows.of(args.window)
     live_windows = (args.size // args.slide + 1) if sliding else 2
     cdf = torch.from_numpy(zipf_cdf(args.keys, args.zipf)).to(dev) if args.zipf else None
-    op = GpuWindowOperator(assigner, HyperLogLog(args.hll_p) if hll else CountSumMinMax(),
-                           key_group_range=exch.key_group_range,
+    agg = (HyperLogLog(args.hll_p) if hll else TDigest(args.delta) if tdig else CountSumMinMax("int") if c1
+           else CountSumMinMax())
+    op = GpuWindowOperator(assigner, agg, key_group_range=exch.key_group_range, key_type="hashed" if c1 else "long",
                            device=local_rank, max_parallelism=max_par,
-                           expected_entries=live_windows * args.keys // world,
+                           expected_entries=(1000 if c1 else live_windows * args.keys // world),
                            max_batch=args.batch if world == 1 else 2 * args.batch,
                            sub_partitions=args.sub_partitions)
     if sliding and args.steady:
@@ -153,32 +228,39 @@ def main():
 
     def generate(s):
         first = (s * world + rank) * args.batch  # global record index of this rank's slice of step s
-        return generate_device(seed, first, args.batch, args.keys, ts_base=0, rate=args.rate,
-                               jitter=args.jitter, cdf_dev=cdf, device=local_rank)
+        if c1:
+            k, t, v, h = wordcount_stream(first, args.batch)
+            dk, dt, dv, dh = (torch.from_numpy(x).to(dev) for x in (k, t, v, h))
+            return dk, dt, dv, torch.tensor([int(t.max())], device=dev), dh
+        k, t, v, mx = generate_device(seed, first, args.batch, args.keys, ts_base=0, rate=args.rate,
+                                      jitter=args.jitter, cdf_dev=cdf, device=local_rank)
+        if tdig:
+            v = v.to(torch.float64)  # the Double field: the generator's int32 values
+        return k, t, v, mx, None
 
     # warmup batches are generated step by step (untimed); the timed ones are staged in HBM up front.
     # punctuated watermark of this rank's source after each batch: max ts so far - bound
     batches, local_wm = {}, {}
     m = -(1 << 63)
     for s in range(args.warmup, steps_total):
-        k, t, v, mx = generate(s)
-        batches[s] = (k, t, v)
+        k, t, v, mx, h = generate(s)
+        batches[s] = (k, t, v, h)
         local_wm[s] = int(mx.item())  # this batch's max; made cumulative once the warmup's is known
     torch.cuda.synchronize()
 
     def step(s):
         nonlocal m
         if s < args.warmup:
-            k, t, v, mx = generate(s)
+            k, t, v, mx, h = generate(s)
             m = max(m, int(mx.item()))
             wm = m - args.bound
         else:
-            k, t, v = batches[s]
+            k, t, v, h = batches[s]
             wm = local_wm[s]
         if world > 1:
             k, t, v = exch.exchange(k, t, v)
             wm = exch.combine_watermark(wm, device=dev)
-        op.process_batch(k, t, v)          # queued; settles the previous step's sequence
+        op.process_batch(k, t, v, h)            # queued; settles the previous step's sequence
         op.advance_watermark(wm, wait=False)  # queued behind the push
         op.clear_pending()  # discarding sink: fired rows were materialised in HBM
 
@@ -216,6 +298,11 @@ def main():
     records = args.batch * world * args.steps
     value = records / elapsed
     fired = st1["fired_rows_total"] - st0["fired_rows_total"]
+    per_gpu_records = records / world
+    fpr = fired / max(1, per_gpu_records)
+    cpr = (st1["digest_centroids_fired"] - st0["digest_centroids_fired"]) / max(1, per_gpu_records)
+    balg = b_alg(w, fpr, world, args.hll_p, args.size // args.slide, cpr)
+    path_frac = value * balg / (world * HBM_PEAK_GBS * 1e9)
 
     roofline = None
     kernels = {}
@@ -224,42 +311,41 @@ def main():
         ms = (ctypes.c_double * N.FW_NUM_KERNELS)()
         nl = (ctypes.c_int64 * N.FW_NUM_KERNELS)()
         L.fw_profile_read(op._h, ms, nl, 1)
-        merged = st1["state_merges"] - st0["state_merges"]
-        for i in range(N.FW_NUM_KERNELS):
-            name = L.fw_kernel_name(i).decode()
-            if nl[i]:
-                kernels[name] = {"launches": int(nl[i]), "avg_ms": ms[i] / nl[i], "total_ms": ms[i]}
-        per_launch_records = records / world / args.steps
-        # the dominant kernel among those with an algorithmic byte count (all but the tiny scan/slow ones)
-        b = None
-        for dom in sorted(kernels, key=lambda k: -kernels[k]["total_ms"]):
-            b = kernel_bytes(dom, per_launch_records, merged / args.steps,
-                             fired=fired / kernels[dom]["launches"], hll_p=args.hll_p if hll else 0,
-                             panes_per_window=args.size // args.slide if sliding else 0)
-            if b is not None:
-                break
-        traffic = None
+        merged = (st1["state_merges"] - st0["state_merges"]) / args.steps
+        per_launch_records = per_gpu_records / args.steps
+        tr = {}
         if os.path.exists(args.traffic):
             with open(args.traffic) as f:
-                tr = json.load(f)
-            # PMC bytes per launch were measured on one workload (tools/traffic.py); other workloads: null
-            if tr.get("workload", "c2") == args.workload:
-                traffic = tr.get("per_launch_bytes", {}).get(dom)
-        if b is not None:
-            achieved = b / (kernels[dom]["avg_ms"] * 1e-3) / 1e9
-            roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                        "traffic": traffic, "alg_bytes_per_launch": int(b)}
-    # whole-path roofline with SURVEY §8d's B_alg: C2 24 + 104 F/N, C4 24 + 112 F/N bytes per record;
-    # C3 (pane model) 24 + 96 + (60*48 + 56) F/N, plus the exchange 2*24*(G-1)/G
-    fpr = fired / max(1, records / world)
-    if sliding:
-        b_alg = 24 + 96 + (args.size // args.slide * 48 + 56) * fpr + 48 * (world - 1) / world
-    elif hll:  # C5-HLL: 24 + B_x + 2 + (2^p + 56) F/N
-        b_alg = 24 + 48 * (world - 1) / world + 2 + ((1 << args.hll_p) + 56) * fpr
-    else:
-        b_alg = 24 + (112 if sessions else 104) * fpr
-    path_frac = value * b_alg / (world * HBM_PEAK_GBS * 1e9)
+                t = json.load(f)
+            if t.get("workload", "c2") == w:  # PMC bytes per launch of this workload (tools/traffic.py)
+                tr = t.get("per_launch_bytes", {})
+        alg = balg * per_launch_records
+        for i in range(N.FW_NUM_KERNELS):
+            name = L.fw_kernel_name(i).decode()
+            if not nl[i]:
+                continue
+            avg = ms[i] / nl[i]
+            ib = impl_bytes(name, per_launch_records, merged, fired=fired / nl[i], hll_p=args.hll_p if hll else 0,
+                            panes_per_window=args.size // args.slide if sliding else 0)
+            kernels[name] = {"launches": int(nl[i]), "avg_ms": round(avg, 5), "total_ms": round(ms[i], 4),
+                             "impl_bytes": None if ib is None else int(ib),
+                             "impl_frac": None if ib is None else round(ib / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "traffic": tr.get(name)}
+        dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
+        kd = kernels[dom]
+        achieved = alg / (kd["avg_ms"] * 1e-3) / 1e9
+        traffic = tr.get(dom)
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "alg_bytes_per_launch": int(alg), "alg_bytes_per_record": round(balg, 3),
+                    "impl_bytes_per_launch": kd["impl_bytes"], "impl_frac": kd["impl_frac"],
+                    "traffic_over_alg": None if traffic is None else round(traffic / alg, 3),
+                    "traffic_per_record": None if traffic is None else round(traffic / per_launch_records, 2),
+                    "basis": "SURVEY §8d B_alg x records per launch / the kernel's average HIP-event duration"}
+
+    host_fed = None
+    if rank == 0 and world == 1 and args.host_fed_steps > 0:
+        host_fed = host_fed_leg(args, op, generate, steps_total, m, c1)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -270,18 +356,22 @@ def main():
             "metric": "records/sec keyed windowed aggregation at 1/2/4/8 GPUs; % of HBM roofline",
             "value": round(value, 1), "unit": "records/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic (splitmix64 counter stream)",
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64" if tdig else "int64", "data": "synthetic (splitmix64 counter stream)",
             "config": {"workload": preset["workload"],
                        "records_per_step_per_gpu": args.batch, "keys": args.keys,
                        **({"gap_ms": args.gap, "zipf_s": args.zipf} if sessions else
                           {"size_ms": args.size, "slide_ms": args.slide} if sliding else
                           {"window_ms": args.window, "hll_precision": args.hll_p, "zipf_s": args.zipf} if hll else
+                          {"window_ms": args.window, "tdigest_delta": args.delta, "zipf_s": args.zipf} if tdig else
                           {"window_ms": args.window}),
                        "records_per_event_second": args.rate, "watermark_bound_ms": args.bound,
-                       "max_parallelism": 128, "parallelism": f"keygroup{world}"},
+                       "max_parallelism": 128, "parallelism": f"keygroup{world}",
+                       "sink": "discarding (fired rows materialised in HBM)"},
             "roofline": roofline,
-            "path_roofline": {"b_alg_bytes_per_record": round(b_alg, 3), "frac": round(path_frac, 4),
+            "path_roofline": {"b_alg_bytes_per_record": round(balg, 3), "frac": round(path_frac, 4),
                               "fired_rows": int(fired)},
+            "host_fed": host_fed,
             "cpu_baseline": cpu,
             "kernels": kernels,
             "state": {"table_slots": int(st1["table_capacity"]), "table_grows_in_timed_region":
@@ -294,15 +384,65 @@ def main():
         dist.destroy_process_group()
 
 
+def host_fed_leg(args, op, generate, first_step, m, c1):
+    """The JNI drop-in path end to end: batches in pinned host memory (a Java DirectByteBuffer's role) pushed
+    with fw_push_batch (H2D copy, processed before the call returns), the watermark, and the fired rows drained
+    to host memory.  Continues the same stream after the timed steps."""
+    import torch
+    staged = []
+    for s in range(first_step, first_step + args.host_fed_steps):
+        k, t, v, mx, h = generate(s)
+        m = max(m, int(mx.item()))
+        cols = [x.cpu().pin_memory() for x in (k, t, v) + ((h,) if h is not None else ())]
+        staged.append((cols, m - args.bound))
+    torch.cuda.synchronize()
+    op.synchronize()
+    op.clear_pending()
+    rows = 0
+    t0 = time.perf_counter()
+    for cols, wm in staged:
+        k, t, v = (x.numpy() for x in cols[:3])
+        op.process_batch(k, t, v, cols[3].numpy() if len(cols) > 3 else None)
+        op.advance_watermark(wm)
+        rows += len(op.drain_rows())
+    dt = time.perf_counter() - t0
+    n = args.batch * args.host_fed_steps
+    return {"value": round(n / dt, 1), "unit": "records/s", "steps": args.host_fed_steps, "fired_rows": rows,
+            "ms_per_step": round(dt / args.host_fed_steps * 1e3, 3),
+            "path": "fw_push_batch from pinned host buffers (H2D inside the call) + fw_advance_watermark + "
+                    "fw_drain_rows to host: PCIe-inclusive, not the headline value"}
+
+
 def cpu_baseline(args):
     """CPU restatement of WindowOperator (oracle/, kind "port"): p threads = p subtasks over their
-    KeyGroupRanges, the same generator and punctuated watermarks, on a bounded sample."""
+    KeyGroupRanges, the same generator and punctuated watermarks, on a bounded sample.  C1 runs at p = 1
+    (LocalStreamEnvironment parallelism 1, BASELINE configs[0]) for both WindowWordCount pipelines."""
     import numpy as np
     from flink_amd.datagen import generate_host
     from oracle import oracle as orc
+    model, nproc = cpu_info()
     n = args.cpu_sample
+    if args.workload == "c1":
+        k, t, v, _ = wordcount_stream(0, n)
+        t0 = time.perf_counter()
+        cw = orc.CountWindowOracle(10, 5, value_type="i32")  # countWindow(10, 5).sum(1), WindowWordCount.java:74-81
+        cw.process(k, v)
+        dt_count = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        tw = orc.WindowOperatorOracle(assigner="tumbling", size=args.window, value_type="i32")
+        tw.process(k, t, v)
+        tw.watermark((1 << 63) - 1)
+        dt = time.perf_counter() - t0
+        return {"value": round(n / dt, 1), "unit": "records/s", "cores": 1, "kind": "port",
+                "count_window_value": round(n / dt_count, 1), "cpu_model": model, "nproc": nproc, "parallelism": 1,
+                "sample": f"all {n} tokens of C1 at p = 1: value = window(Tumbling {args.window} ms).sum(1) (the GPU "
+                          f"line's pipeline), count_window_value = countWindow(10, 5).sum(1); CPU restatement of "
+                          f"WindowOperator / EvictingWindowOperator semantics (oracle/), not the Java reference "
+                          f"(no JDK on the box)"}
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     k, t, v = generate_host(0x5EED, 0, n, args.keys, ts_base=0, rate=args.rate, jitter=args.jitter, zipf_s=args.zipf)
+    if args.workload == "c5t":
+        v = v.astype(np.float64)
     batch = min(args.batch, n)
     wms, m = [], -(1 << 63)
     for b in range(0, n, batch):
@@ -315,14 +455,18 @@ def cpu_baseline(args):
         cfg = dict(assigner="sliding", size=args.size, slide=args.slide)
     elif args.workload == "c5":
         cfg = dict(assigner="tumbling", size=args.window, hll_p=args.hll_p)
+    elif args.workload == "c5t":
+        cfg = dict(assigner="tumbling", size=args.window, tdigest=args.delta)
     else:
         cfg = dict(assigner="tumbling", size=args.window)
     orc.run_parallel(cfg, k, t, v, batch, np.array(wms), 128, threads)
     dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 1), "unit": "records/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} records of the same {args.workload.upper()} stream, {threads} subtasks (threads), watermark every "
-                      f"{batch} records; CPU restatement of WindowOperator semantics (oracle/), not the Java "
-                      f"reference (no JDK on the box)"}
+    return {"value": round(n / dt, 1), "unit": "records/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "nproc": nproc, "parallelism": threads,
+            "sample": f"first {n} records of the same {args.workload.upper()} stream, {threads} subtasks (threads; "
+                      f"p = this job's CPU share of the box, nproc = {nproc}), watermark every {batch} records; CPU "
+                      f"restatement of WindowOperator semantics (oracle/, C++ -O2), not the Java reference (no JDK "
+                      f"on the box)"}
 
 
 if __name__ == "__main__":

@@ -21,7 +21,8 @@ FW_TUMBLING, FW_SLIDING, FW_SESSION = 0, 1, 2
 FW_VAL_I64, FW_VAL_I32, FW_VAL_F64 = 0, 1, 2
 FW_KEY_LONG, FW_KEY_INT, FW_KEY_HASHED = 0, 1, 2
 FW_AGG_COUNT_SUM_MIN_MAX, FW_AGG_HLL, FW_AGG_FIRST, FW_AGG_MINBY, FW_AGG_MAXBY, FW_AGG_FIRST_MAX = 0, 1, 2, 3, 4, 5
-FW_NUM_KERNELS = 6
+FW_AGG_TDIGEST = 6
+FW_NUM_KERNELS = 7
 
 I64P = ctypes.POINTER(ctypes.c_int64)
 I32P = ctypes.POINTER(ctypes.c_int32)
@@ -35,7 +36,9 @@ class FwConfig(ctypes.Structure):
                 ("sub_partitions", ctypes.c_int32), ("size", ctypes.c_int64), ("slide", ctypes.c_int64),
                 ("offset", ctypes.c_int64), ("gap", ctypes.c_int64), ("allowed_lateness", ctypes.c_int64),
                 ("expected_entries", ctypes.c_int64), ("max_batch", ctypes.c_int64),
-                ("aggregate", ctypes.c_int32), ("hll_precision", ctypes.c_int32)]
+                ("aggregate", ctypes.c_int32), ("hll_precision", ctypes.c_int32),
+                ("tdigest_compression", ctypes.c_int32), ("tdigest_export", ctypes.c_int32),
+                ("tdigest_quantiles", ctypes.c_double * 3)]
 
 
 class FwRows(ctypes.Structure):
@@ -54,7 +57,7 @@ class FwStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
         "records_in", "late_records_dropped", "keyed_state_entries", "event_time_timers", "current_watermark",
         "fired_rows_total", "pending_rows", "pending_side_rows", "table_capacity", "table_grows",
-        "slow_path_records", "state_merges")]
+        "slow_path_records", "state_merges", "digest_centroids_fired")]
 
 
 # every exported symbol with its ctypes signature (restype, argtypes); mirrors include/flink_window.h
@@ -70,6 +73,7 @@ SIGNATURES = {
     "fw_drain_side": (ctypes.c_int, [VP, ctypes.POINTER(FwSideRows), ctypes.c_int64, I64P]),
     "fw_rows_device": (ctypes.c_int, [VP, ctypes.POINTER(FwRows), I64P]),
     "fw_clear_pending": (ctypes.c_int, [VP]),
+    "fw_drain_digests": (ctypes.c_int, [VP, VP, VP, VP, ctypes.c_int64, I64P]),
     "fw_get_stats": (ctypes.c_int, [VP, ctypes.POINTER(FwStats)]),
     "fw_synchronize": (ctypes.c_int, [VP]),
     "fw_profile": (ctypes.c_int, [VP, ctypes.c_int]),

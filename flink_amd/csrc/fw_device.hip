@@ -23,6 +23,9 @@
 //                       the cleaned-up entries, into the region's other buffer.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "../../include/flink_window.h"
 #include "fw_internal.h"
 
@@ -145,7 +148,7 @@ __device__ __forceinline__ int64_t wend(const DevCfg& c, int64_t start) {
   return jadd(start, c.panes ? c.slide : c.size);
 }
 // ---- HyperLogLog (FW_AGG_HLL; the definition is restated in oracle/window_oracle.h)
-__device__ __forceinline__ uint64_t hll_block_of(const Entry& e) { return (uint64_t)e.meta >> 1; }
+__device__ __forceinline__ uint64_t pool_block_of(const Entry& e) { return (uint64_t)e.meta >> 1; }
 // earliest pending timer of an entry; a pane's is its meta (the next window end it belongs to)
 __device__ __forceinline__ int64_t entry_timer(const DevCfg& c, const Entry& e) {
   return c.panes ? e.meta : timer_of(e, c.lateness);
@@ -267,7 +270,9 @@ __device__ __forceinline__ uint32_t ld_state(const uint32_t* p) {
 
 // ------------------------------------------------------------------ output
 // FW_AGG_FIRST / MINBY / MAXBY carry the records' arrival ordinals
-__host__ __device__ __forceinline__ bool agg_ordinal(const DevCfg& c) { return c.agg >= FW_AGG_FIRST; }
+__host__ __device__ __forceinline__ bool agg_ordinal(const DevCfg& c) {
+  return c.agg >= FW_AGG_FIRST && c.agg <= FW_AGG_FIRST_MAX;
+}
 // MINBY / MAXBY: the (field, ordinal) pair as one 64-bit key whose minimum is the selected element
 // (MAXBY flips the i32 field with ~, which reverses its order exactly)
 __device__ __forceinline__ int64_t by_key(int agg, int64_t v, int64_t ord) {
@@ -798,7 +803,7 @@ struct AggLds {
   int live;    // occupied slots of the region
   unsigned long long flushed;
   int64_t min_timer;
-  int hl_lo, hl_take, hl_idx;  // FW_AGG_HLL: this flush's register blocks (free-stack slice, then pool tail)
+  int hl_lo, hl_take, hl_idx;  // block pool: this flush's accumulator blocks (free-stack slice, then pool tail)
   long long hl_bump;
 };
 enum : uint32_t { LT_EMPTY = 0, LT_BUSY = 1 };
@@ -1052,7 +1057,7 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
     if (threadIdx.x == 0) atomicMax(&st->need_live, need);
     return false;
   }
-  if (c.agg == FW_AGG_HLL) {  // one reservation of register blocks for every new window of the flush
+  if (c.pool_bytes) {  // one reservation of accumulator blocks for every new window of the flush
     if (threadIdx.x == 0) {
       const int k = L.nnew;
       int take = 0, lo = 0;
@@ -1060,13 +1065,13 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
       if (k) {
         // pop k from the free stack (nothing is pushed while the aggregate runs); what the stack
         // lacks comes from the pool's tail
-        const int t = atomicSub(&c.hll_ctr[0], k);
+        const int t = atomicSub(&c.pool_ctr[0], k);
         take = max(0, min(t, k));
         lo = t - take;
         if (take < k) {
-          atomicAdd(&c.hll_ctr[0], k - take);
-          bump = atomicAdd(&c.hll_ctr[1], k - take);
-          if (bump + (k - take) > c.hll_blocks) atomicOr(&st->flags, FW_STATUS_HLL_POOL);
+          atomicAdd(&c.pool_ctr[0], k - take);
+          bump = atomicAdd(&c.pool_ctr[1], k - take);
+          if (bump + (k - take) > c.pool_blocks) atomicOr(&st->flags, FW_STATUS_POOL);
         }
       }
       L.hl_lo = lo;
@@ -1100,11 +1105,13 @@ __device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* s
       const int32_t ns = region_claim(r, hs, live_word(hs));
       if (ns >= 0) {
         Entry n = d;
-        if (c.agg == FW_AGG_HLL) {
+        if (c.pool_bytes) {
           const int i = atomicAdd(&L.hl_idx, 1);
-          int64_t blk = i < L.hl_take ? (int64_t)c.hll_free[L.hl_lo + i] : L.hl_bump + (i - L.hl_take);
-          if (blk >= c.hll_blocks) blk = 0;  // pool exhausted: flagged above, the push fails
+          int64_t blk = i < L.hl_take ? (int64_t)c.pool_free[L.hl_lo + i] : L.hl_bump + (i - L.hl_take);
+          if (blk >= c.pool_blocks) blk = 0;  // pool exhausted: flagged above, the push fails
           n.meta |= blk << 1;
+          if (c.agg == FW_AGG_TDIGEST)  // an empty digest
+            *reinterpret_cast<TdHead*>(c.pool + (uint64_t)blk * (uint64_t)c.pool_bytes) = TdHead{0, 0, 0};
         }
         r.ent[ns] = n;
       } else {
@@ -2212,7 +2219,7 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, in
   const int p = c.hll_p, rmax = 65 - p;
   const int64_t m = (int64_t)1 << p;
   const uint64_t blk = (uint64_t)out.mn[row];
-  uint8_t* regs = c.hll_regs + blk * (uint64_t)m;
+  uint8_t* regs = c.pool + blk * (uint64_t)m;
   uint64_t s = 0, sh = 0;
   uint32_t zeros = 0;
   uint4* q = reinterpret_cast<uint4*>(regs);
@@ -2255,7 +2262,7 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, in
     out.sum[row] = __double_as_longlong(est);
     out.mn[row] = (int64_t)zeros;
     out.mx[row] = (int64_t)lo;
-    c.hll_free[stack_slot] = (uint32_t)blk;  // zeroed before the next kernel can hand it out
+    c.pool_free[stack_slot] = (uint32_t)blk;  // zeroed before the next kernel can hand it out
   }
 }
 
@@ -2307,11 +2314,11 @@ __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __rest
       atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's window
       continue;
     }
-    const uint64_t blk = hll_block_of(r.ent[slot]);
+    const uint64_t blk = pool_block_of(r.ent[slot]);
     const uint64_t h = fmix64((uint64_t)rec.val);
     const uint64_t j = h >> (64 - p);
     const uint32_t rank = (uint32_t)__clzll((long long)((h << p) | (1ull << (p - 1)))) + 1u;
-    uint32_t* w = reinterpret_cast<uint32_t*>(c.hll_regs + blk * ((uint64_t)1 << p) + (j & ~3ull));
+    uint32_t* w = reinterpret_cast<uint32_t*>(c.pool + blk * ((uint64_t)1 << p) + (j & ~3ull));
     const int sh = (int)(j & 3) * 8;
     uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     while (((old >> sh) & 0xffu) < rank) {
@@ -2320,6 +2327,614 @@ __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __rest
                                                __HIP_MEMORY_SCOPE_AGENT))
         break;
     }
+  }
+}
+
+// ---- t-digest (FW_AGG_TDIGEST).  The definition is oracle/window_oracle.h's OR_AGG_TDIGEST, restated here
+// operation for operation in IEEE double without contraction (the library is built with -ffp-contract=off),
+// so a digest is bit-exact with the oracle's.  Per push, after the aggregate created the entries and their
+// blocks: every record's (entry slot, value) pair is sorted (rocPRIM radix sort by value, then stably by
+// slot), so the batch values of one digest form one run in Double.compare order.  Each digest then merges
+// its run with its centroids into the other half of its block, in one of three tiers by size:
+//   serial  (<= FW_TD_T1 values + centroids): one thread walks the merged sequence;
+//   wave    (<= FW_TD_T3): one wave — each lane places 64 values at a time (its bucket from its merged
+//           position: binary searches over the old centroids in LDS), then per bucket the wave sums the
+//           bucket's values 64 at a time as butterfly trees and folds the old centroids' sums;
+//   large   (> FW_TD_T3, the hottest keys): the placement runs over the whole grid and one wave per
+//           (digest, bucket) forms the bucket's centroid.
+// All three produce the definition's sums: per bucket, the old centroids' sums left to right, the new values
+// in blocks of 64 from the bucket's first value, each block a perfect binary tree over 64 slots, the block
+// sums left to right.
+constexpr int TD_NB_MAX = 250;  // delta <= 500
+__device__ __forceinline__ uint64_t td_key(int64_t bits) { return (uint64_t)f64_sortable(bits) ^ 0x8000000000000000ull; }
+__device__ __forceinline__ double td_val(uint64_t key) {
+  return __longlong_as_double(f64_unsortable((int64_t)(key ^ 0x8000000000000000ull)));
+}
+__device__ __forceinline__ uint64_t td_mean_key(double sum, int64_t w) {
+  return td_key(__double_as_longlong(sum / (double)w));
+}
+__device__ __forceinline__ TdHead* td_head(const DevCfg& c, uint64_t blk) {
+  return reinterpret_cast<TdHead*>(c.pool + blk * (uint64_t)c.pool_bytes);
+}
+__device__ __forceinline__ TdCent* td_half(const DevCfg& c, uint64_t blk, int h) {
+  return reinterpret_cast<TdCent*>(c.pool + blk * (uint64_t)c.pool_bytes + sizeof(TdHead)) + (int64_t)h * c.td_nb;
+}
+// bucket of an item's midpoint: the largest b < nb with W * qb[b] <= mid
+__device__ __forceinline__ int td_bucket(const DevCfg& c, double W, double mid) {
+  int lo = 0, hi = c.td_nb - 1;
+  while (lo < hi) {
+    const int m = (lo + hi + 1) >> 1;
+    if (W * c.td_qb[m] <= mid)
+      lo = m;
+    else
+      hi = m - 1;
+  }
+  return lo;
+}
+__device__ __forceinline__ int64_t td_weight(const TdCent* ce, int32_t j) { return ce[j].cum - (j ? ce[j - 1].cum : 0); }
+// a left-to-right fold of partial sums (`any` = something folded yet)
+__device__ __forceinline__ void td_fold(double& s, bool& any, double x) {
+  s = any ? s + x : x;
+  any = true;
+}
+// one thread's tree sum of a block of up to 64 values (a binary counter of complete subtrees)
+struct TdTree {
+  double st[7];
+  uint32_t cnt;
+  __device__ void push(double x) {
+    double v = x;
+    bool placed = false;
+#pragma unroll
+    for (int l = 0; l < 7; l++) {
+      if (placed) continue;
+      if ((cnt >> l) & 1u) {
+        v = st[l] + v;
+      } else {
+        st[l] = v;
+        placed = true;
+      }
+    }
+    cnt++;
+  }
+  // the block's sum, the subtrees joined from the smallest (rightmost) up
+  __device__ double finish() const {
+    double t = 0.0;
+    bool any = false;
+#pragma unroll
+    for (int l = 0; l < 7; l++) {
+      if (!((cnt >> l) & 1u)) continue;
+      t = any ? st[l] + t : st[l];
+      any = true;
+    }
+    return t;
+  }
+};
+// the wave's tree sum of the 64 lanes' values in lane order (lanes without a value contribute nothing)
+__device__ __forceinline__ double td_wave_tree(double x, bool has) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double ox = __shfl_xor(x, o, 64);
+    const bool oh = __shfl_xor((int)has, o, 64) != 0;
+    if (has && oh)
+      x = x + ox;  // left + right (the upper lane adds right + left: the same IEEE sum)
+    else if (oh)
+      x = ox;
+    has = has || oh;
+  }
+  return x;
+}
+// the wave's S_new of a bucket: its sorted values v[ns, ne) in blocks of 64, tree sums folded left to right
+__device__ double td_wave_new_sum(const uint64_t* __restrict__ v, int64_t ns, int64_t ne) {
+  const int lane = __lane_id();
+  double s = 0.0;
+  bool any = false;
+  int64_t b0 = ns;
+  for (; b0 + 4 * 64 <= ne; b0 += 4 * 64) {  // four full blocks in flight
+    double x[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) x[u] = td_val(v[b0 + u * 64 + lane]);
+#pragma unroll
+    for (int u = 0; u < 4; u++) td_fold(s, any, td_wave_tree(x[u], true));
+  }
+  for (; b0 < ne; b0 += 64) {
+    const bool has = b0 + lane < ne;
+    const double x = has ? td_val(v[b0 + lane]) : 0.0;
+    td_fold(s, any, td_wave_tree(x, has));
+  }
+  return s;
+}
+
+// serial merge of nn sorted values v[beg ..] with the no centroids `old` into `out` (window_oracle.cpp td_compress)
+__device__ int32_t td_merge_serial(const DevCfg& c, const uint64_t* __restrict__ v, int64_t beg, int64_t nn,
+                                   const TdCent* __restrict__ old, int32_t no, TdCent* __restrict__ out, int64_t W) {
+  const double Wd = (double)W;
+  int64_t i = 0, cw = 0, gw = 0, cum_out = 0, prev_old = 0;
+  int32_t j = 0, k = 0;
+  uint64_t mk = no ? td_mean_key(old[0].sum, old[0].cum) : 0;
+  double so = 0.0, sn = 0.0;
+  bool any_o = false, any_n = false;
+  TdTree tr;
+  tr.cnt = 0;
+  int b = 0, cur = -1;
+  auto emit = [&]() {
+    if (tr.cnt) td_fold(sn, any_n, tr.finish());
+    cum_out += gw;
+    out[k++] = TdCent{any_o && any_n ? so + sn : any_o ? so : sn, cum_out};
+    gw = 0;
+    any_o = any_n = false;
+    tr.cnt = 0;
+  };
+  while (i < nn || j < no) {
+    const bool take_new = j == no || (i < nn && v[beg + i] <= mk);
+    double x;
+    int64_t w;
+    if (take_new) {
+      x = td_val(v[beg + i]);
+      w = 1;
+      i++;
+    } else {
+      x = old[j].sum;
+      w = old[j].cum - prev_old;
+      prev_old = old[j].cum;
+      j++;
+      if (j < no) mk = td_mean_key(old[j].sum, old[j].cum - prev_old);
+    }
+    const double mid = (double)cw + (double)w * 0.5;
+    while (b + 1 < c.td_nb && Wd * c.td_qb[b + 1] <= mid) b++;
+    if (b != cur && gw > 0) emit();
+    cur = b;
+    if (take_new) {
+      tr.push(x);
+      if (tr.cnt == 64) {
+        td_fold(sn, any_n, tr.finish());
+        tr.cnt = 0;
+      }
+    } else {
+      td_fold(so, any_o, x);
+    }
+    gw += w;
+    cw += w;
+  }
+  if (gw > 0) emit();
+  return k;
+}
+
+// piecewise-linear quantile through (0, min), (centre_i, mean_i) ..., (W, max) (window_oracle.cpp td_quantile)
+__device__ double td_quantile(const TdCent* ce, int32_t n, int64_t W, double mn, double mx, double qv) {
+  if (n == 0) return __longlong_as_double(0x7ff8000000000000ll);
+  const double Wd = (double)W;
+  const double x = qv * Wd;
+  double x0 = 0.0, y0 = mn;
+  int64_t before = 0;
+  for (int32_t i = 0; i < n; i++) {
+    const int64_t w = ce[i].cum - before;
+    const double t = (double)before + (double)w * 0.5;
+    const double m = ce[i].sum / (double)w;
+    if (t >= x) return y0 + (m - y0) * ((x - x0) / (t - x0));
+    x0 = t;
+    y0 = m;
+    before = ce[i].cum;
+  }
+  return y0 + (mx - y0) * ((x - x0) / (Wd - x0));
+}
+
+// getResult of a fired row (one thread): out.sum holds the block id (k_fire), out.min / out.max the min / max;
+// returns the digest's centroid count
+__device__ int32_t td_finish(const DevCfg& c, const DevRows& out, uint64_t row, int64_t stack_slot) {
+  const uint64_t blk = (uint64_t)out.sum[row];
+  const TdHead h = *td_head(c, blk);
+  const TdCent* ce = td_half(c, blk, h.cur);
+  const double mn = __longlong_as_double(out.mn[row]), mx = __longlong_as_double(out.mx[row]);
+  const double q0 = td_quantile(ce, h.n, h.w, mn, mx, c.td_quant[0]);
+  const double q1 = td_quantile(ce, h.n, h.w, mn, mx, c.td_quant[1]);
+  const double q2 = td_quantile(ce, h.n, h.w, mn, mx, c.td_quant[2]);
+  if (out.dig) {
+    int64_t* d = out.dig + row * (1 + 2 * (int64_t)c.td_nb);
+    d[0] = h.n;
+    for (int32_t k = 0; k < h.n; k++) {
+      d[1 + 2 * k] = __double_as_longlong(ce[k].sum);
+      d[2 + 2 * k] = td_weight(ce, k);
+    }
+  }
+  out.sum[row] = __double_as_longlong(q0);
+  out.mn[row] = __double_as_longlong(q1);
+  out.mx[row] = __double_as_longlong(q2);
+  c.pool_free[stack_slot] = (uint32_t)blk;
+  return h.n;
+}
+
+// sort keys of every batch position: (global slot of the record's entry, value key); positions past the
+// partitioned records get the slot `none` (sorted last, skipped)
+constexpr int TD_CHUNK = 4096;
+__global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restrict__ part, const uint32_t* __restrict__ offs,
+                                                 int32_t T, int64_t n, DevTable tb, uint32_t none, uint32_t* __restrict__ gs,
+                                                 uint64_t* __restrict__ vk, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int64_t total = offs[(int64_t)c.P * T];
+  const int64_t i0 = (int64_t)blockIdx.x * TD_CHUNK;
+  const int64_t i1 = min(n, i0 + (int64_t)TD_CHUNK);
+  __shared__ int32_t p0_s;
+  if (threadIdx.x == 0) {  // partition of the chunk's first record: last p with offs[p*T] <= i0
+    int32_t lo = 0, hi = c.P - 1;
+    while (lo < hi) {
+      const int32_t mid = (lo + hi + 1) >> 1;
+      if ((int64_t)offs[(int64_t)mid * T] <= i0)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    p0_s = lo;
+  }
+  __syncthreads();
+  const bool cmp = c.compact && !st->wide;
+  int32_t pp = p0_s;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    if (i >= total) {
+      gs[i] = none;
+      vk[i] = 0;
+      continue;
+    }
+    while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
+    PRec rec;
+    if (cmp) {
+      const i64x2 r = reinterpret_cast<const i64x2*>(part)[i];
+      compact_decode(c, pp, r.x, &rec.key, &rec.last);
+      rec.val = r.y;
+    } else {
+      rec = part[i];
+    }
+    const Region r = region_of(c, tb, pp, tb.cur[pp]);
+    const int32_t slot = region_find(r, slot_hash(c, rec.key, rec.last), rec.key, rec.last, wend(c, rec.last));
+    if (slot < 0) {
+      atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's window
+      gs[i] = none;
+      vk[i] = 0;
+      continue;
+    }
+    gs[i] = ((uint32_t)pp << c.log_r) | (uint32_t)slot;
+    vk[i] = td_key(rec.val);
+  }
+}
+
+// the touched digests: the first position of every run of one slot in the sorted batch.  A workgroup takes
+// TD_BOUNDS consecutive positions and reserves its digests' places with one atomic.
+constexpr int TD_BOUNDS_PER_THREAD = 16;
+__global__ __launch_bounds__(256) void k_td_bounds(int64_t n, const uint32_t* __restrict__ gs, uint32_t none, TdBuf td,
+                                                   Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  __shared__ uint32_t sw[256 / 64 + 1];
+  __shared__ int base_s;
+  const int64_t i0 = (int64_t)blockIdx.x * 256 * TD_BOUNDS_PER_THREAD + (int64_t)threadIdx.x * TD_BOUNDS_PER_THREAD;
+  uint32_t starts = 0;  // bit u: position i0 + u starts a run
+  uint32_t prev = i0 > 0 && i0 <= n ? gs[i0 - 1] : none;
+#pragma unroll
+  for (int u = 0; u < TD_BOUNDS_PER_THREAD; u++) {
+    const int64_t i = i0 + u;
+    const uint32_t g = i < n ? gs[i] : none;
+    if (g != none && (i == 0 || g != prev)) starts |= 1u << u;
+    prev = g;
+  }
+  uint32_t total;
+  const uint32_t pos = block_excl_scan((uint32_t)__popc(starts), sw, &total);
+  if (threadIdx.x == 0) base_s = total ? atomicAdd(&td.ctr[0], (int)total) : 0;
+  __syncthreads();
+  int k = base_s + (int)pos;
+#pragma unroll
+  for (int u = 0; u < TD_BOUNDS_PER_THREAD; u++) {
+    if (!((starts >> u) & 1u)) continue;
+    td.tslot[k] = gs[i0 + u];
+    td.tbeg[k] = (uint32_t)(i0 + u);
+    k++;
+  }
+}
+
+// each touched digest: merged serially here, or queued for the wave or the grid-wide merge
+__global__ __launch_bounds__(256) void k_td_small(DevCfg c, DevTable tb, TdBuf td, const uint64_t* __restrict__ v, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int32_t nt = td.ctr[0];
+  const uint32_t mask = (1u << c.log_r) - 1u;
+  for (int32_t idx0 = blockIdx.x * blockDim.x; idx0 < nt; idx0 += gridDim.x * blockDim.x) {
+    const int32_t idx = idx0 + (int32_t)threadIdx.x;
+    bool mid = false;
+    if (idx < nt) {
+      const uint32_t g = td.tslot[idx];
+      const int64_t beg = td.tbeg[idx];
+      const int32_t p = (int32_t)(g >> c.log_r);
+      const Region r = region_of(c, tb, p, tb.cur[p]);
+      const Entry& e = r.ent[g & mask];
+      const uint64_t blk = pool_block_of(e);
+      TdHead* hp = td_head(c, blk);
+      const TdHead h = *hp;
+      const int64_t W = e.cnt, nn = W - h.w;
+      const TdCent* old = td_half(c, blk, h.cur);
+      TdCent* out = td_half(c, blk, h.cur ^ 1);
+      td.lidx[g] = -1;
+      if (nn + h.n <= FW_TD_T1) {
+        const int32_t k = td_merge_serial(c, v, beg, nn, old, h.n, out, W);
+        *hp = TdHead{h.cur ^ 1, k, W};
+      } else if (nn + h.n <= FW_TD_T3) {
+        mid = true;
+      } else {
+        const int32_t L = atomicAdd(&td.ctr[1], 1);
+        if (L >= td.max_large) {  // cannot happen: max_large bounds the digests with > FW_TD_T3 - td_nb values
+          atomicOr(&st->flags, FW_STATUS_STATE_LOST);
+        } else {
+          td.lidx[g] = L;
+          td.large[L] = TdLarge{beg, nn, W, h.n, h.cur ^ 1, old, out, hp};
+          for (int b = 0; b < c.td_nb; b++) {
+            td.nstart[(int64_t)L * c.td_nb + b] = -1;
+            td.ostart[(int64_t)L * c.td_nb + b] = -1;
+          }
+        }
+      }
+    }
+    // wave-aggregated reservation of the wave-tier list
+    const uint64_t m = __ballot(mid);
+    if (m) {
+      int base = 0;
+      const int leader = __ffsll((long long)m) - 1;
+      if ((int)__lane_id() == leader) base = atomicAdd(&td.ctr[2], __popcll(m));
+      base = __shfl(base, leader, 64);
+      if (mid) td.mid[base + __popcll(m & lanemask_lt())] = (uint32_t)idx;
+    }
+  }
+}
+
+// placement of one value: the old centroids whose mean is below it precede it (a value goes before an equal
+// mean); keys/cum: the old centroids' mean keys and cumulative weights
+__device__ __forceinline__ int td_bucket_new(const DevCfg& c, const uint64_t* keys, const int64_t* cum, int32_t no,
+                                             double W, int64_t r, uint64_t vkey) {
+  int32_t lo = 0, hi = no;  // first old centroid whose mean key >= vkey
+  while (lo < hi) {
+    const int32_t m = (lo + hi) >> 1;
+    if (keys[m] < vkey)
+      lo = m + 1;
+    else
+      hi = m;
+  }
+  const int64_t cw = r + (lo ? cum[lo - 1] : 0);
+  return td_bucket(c, W, (double)cw + 0.5);
+}
+// placement of old centroid j: the values <= its mean precede it (binary search in the digest's sorted run)
+__device__ __forceinline__ int td_bucket_old(const DevCfg& c, const uint64_t* __restrict__ v, int64_t beg, int64_t nn,
+                                             uint64_t mk, int64_t cum_before, int64_t w, double W) {
+  int64_t lo = 0, hi = nn;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (v[beg + m] <= mk)
+      lo = m + 1;
+    else
+      hi = m;
+  }
+  return td_bucket(c, W, (double)(lo + cum_before) + (double)w * 0.5);
+}
+
+// the wave tier: one wave per digest (its old centroids and bucket starts in LDS)
+constexpr int TD_WAVES = 4;
+__global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb, TdBuf td, const uint64_t* __restrict__ v,
+                                                           Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  __shared__ uint64_t s_key[TD_WAVES][TD_NB_MAX];
+  __shared__ int64_t s_cum[TD_WAVES][TD_NB_MAX];
+  __shared__ int64_t s_ns[TD_WAVES][TD_NB_MAX + 1];  // first value of each bucket (-1: none), then its end
+  __shared__ int32_t s_os[TD_WAVES][TD_NB_MAX + 1];
+  const int wv = threadIdx.x >> 6, lane = __lane_id();
+  const int nb = c.td_nb;
+  uint64_t* keys = s_key[wv];
+  int64_t* cum = s_cum[wv];
+  int64_t* ns = s_ns[wv];
+  int32_t* os = s_os[wv];
+  const int32_t nmid = td.ctr[2];
+  const uint32_t mask = (1u << c.log_r) - 1u;
+  for (int32_t q = blockIdx.x * TD_WAVES + wv; q < nmid; q += gridDim.x * TD_WAVES) {
+    TdLarge d;
+    {
+      const uint32_t idx = td.mid[q];
+      const uint32_t g = td.tslot[idx];
+      const int32_t p = (int32_t)(g >> c.log_r);
+      const Region r = region_of(c, tb, p, tb.cur[p]);
+      const Entry& e = r.ent[g & mask];
+      const uint64_t blk = pool_block_of(e);
+      TdHead* hp = td_head(c, blk);
+      const TdHead h = *hp;
+      d = TdLarge{td.tbeg[idx], e.cnt - h.w, e.cnt, h.n, h.cur ^ 1, td_half(c, blk, h.cur), td_half(c, blk, h.cur ^ 1), hp};
+    }
+    const double W = (double)d.W;
+    for (int32_t j = lane; j < d.no; j += 64) {
+      const int64_t w = td_weight(d.old, j);
+      keys[j] = td_mean_key(d.old[j].sum, w);
+      cum[j] = d.old[j].cum;
+    }
+    for (int b = lane; b < nb; b += 64) {
+      ns[b] = -1;
+      os[b] = -1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // place the values, 64 at a time; a bucket starts where a value's bucket differs from its predecessor's
+    int carry = -1;
+    for (int64_t i0 = 0; i0 < d.nn; i0 += 64) {
+      const int64_t i = i0 + lane;
+      int b = -1;
+      if (i < d.nn) b = td_bucket_new(c, keys, cum, d.no, W, i, v[d.beg + i]);
+      int prev = __shfl_up(b, 1, 64);
+      if (lane == 0) prev = carry;
+      if (i < d.nn && prev != b) ns[b] = d.beg + i;
+      carry = __shfl(b, 63, 64);
+    }
+    carry = -1;
+    for (int32_t j0 = 0; j0 < d.no; j0 += 64) {
+      const int32_t j = j0 + lane;
+      int b = -1;
+      if (j < d.no) b = td_bucket_old(c, v, d.beg, d.nn, keys[j], j ? cum[j - 1] : 0, td_weight(d.old, j), W);
+      int prev = __shfl_up(b, 1, 64);
+      if (lane == 0) prev = carry;
+      if (j < d.no && prev != b) os[b] = j;
+      carry = __shfl(b, 63, 64);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // buckets in order: each non-empty one is a centroid
+    int64_t cum_out = 0, end_n;
+    int32_t k = 0, end_o;
+    for (int b = 0; b < nb; b++) {
+      const int64_t sn = ns[b];
+      const int32_t so = os[b];
+      if (sn < 0 && so < 0) continue;
+      // the end of this bucket's runs: the next bucket that starts one
+      end_n = d.beg + d.nn;
+      end_o = d.no;
+      bool fn = false, fo = false;
+      for (int b2 = b + 1; b2 < nb && !(fn && fo); b2++) {
+        if (!fn && ns[b2] >= 0) {
+          end_n = ns[b2];
+          fn = true;
+        }
+        if (!fo && os[b2] >= 0) {
+          end_o = os[b2];
+          fo = true;
+        }
+      }
+      const int64_t a_n = sn >= 0 ? sn : end_n;
+      const int32_t a_o = so >= 0 ? so : end_o;
+      double s_new = 0.0, s_old = 0.0;
+      bool any_o = false;
+      const bool any_n = end_n > a_n;
+      if (any_n) s_new = td_wave_new_sum(v, a_n, end_n);
+      for (int32_t j = a_o; j < end_o; j++) td_fold(s_old, any_o, d.old[j].sum);
+      const int64_t w = (end_n - a_n) + (end_o > a_o ? cum[end_o - 1] - (a_o ? cum[a_o - 1] : 0) : 0);
+      cum_out += w;
+      if (lane == 0) d.out[k] = TdCent{any_o && any_n ? s_old + s_new : any_o ? s_old : s_new, cum_out};
+      k++;
+    }
+    if (lane == 0) *d.head = TdHead{d.pad, k, d.W};
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// the large tier: placement of every value of a large digest over the whole grid
+__global__ __launch_bounds__(256) void k_td_large_items(DevCfg c, int64_t n, const uint32_t* __restrict__ gs,
+                                                        const uint64_t* __restrict__ v, uint32_t none, TdBuf td, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || td.ctr[1] == 0) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = gs[i];
+    if (g == none) continue;
+    const int32_t L = td.lidx[g];
+    if (L < 0) continue;
+    const TdLarge d = td.large[L];
+    const uint64_t* keys = td.okey + (int64_t)L * c.td_nb;
+    const int64_t r = i - d.beg;
+    int32_t lo = 0, hi = d.no;
+    const uint64_t vk = v[i];
+    while (lo < hi) {
+      const int32_t m = (lo + hi) >> 1;
+      if (keys[m] < vk)
+        lo = m + 1;
+      else
+        hi = m;
+    }
+    const double W = (double)d.W;
+    const int b = td_bucket(c, W, (double)(r + (lo ? d.old[lo - 1].cum : 0)) + 0.5);
+    bool start = r == 0;
+    if (!start) {
+      const uint64_t pk = v[i - 1];
+      int32_t lo2 = 0, hi2 = lo;  // the predecessor's place is at most this value's
+      while (lo2 < hi2) {
+        const int32_t m = (lo2 + hi2) >> 1;
+        if (keys[m] < pk)
+          lo2 = m + 1;
+        else
+          hi2 = m;
+      }
+      start = td_bucket(c, W, (double)(r - 1 + (lo2 ? d.old[lo2 - 1].cum : 0)) + 0.5) != b;
+    }
+    if (start) td.nstart[(int64_t)L * c.td_nb + b] = (int32_t)i;
+  }
+}
+// the old centroids of the large digests (one wave per digest): their mean keys, buckets and bucket starts
+__global__ __launch_bounds__(256) void k_td_large_old(DevCfg c, const uint64_t* __restrict__ v, TdBuf td, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int32_t nl = td.ctr[1];
+  const int lane = __lane_id();
+  for (int32_t L = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); L < nl; L += (gridDim.x * blockDim.x) >> 6) {
+    const TdLarge d = td.large[L];
+    int carry = -1;
+    for (int32_t j0 = 0; j0 < d.no; j0 += 64) {
+      const int32_t j = j0 + lane;
+      int b = -1;
+      if (j < d.no) {
+        const int64_t w = td_weight(d.old, j);
+        const uint64_t mk = td_mean_key(d.old[j].sum, w);
+        td.okey[(int64_t)L * c.td_nb + j] = mk;
+        b = td_bucket_old(c, v, d.beg, d.nn, mk, j ? d.old[j - 1].cum : 0, w, (double)d.W);
+      }
+      int prev = __shfl_up(b, 1, 64);
+      if (lane == 0) prev = carry;
+      if (j < d.no && prev != b) td.ostart[(int64_t)L * c.td_nb + b] = j;
+      carry = __shfl(b, 63, 64);
+    }
+  }
+}
+// one wave per (large digest, bucket): the bucket's centroid; out[b] = {sum, weight} (weight 0: empty)
+__global__ __launch_bounds__(256) void k_td_large_groups(DevCfg c, const uint64_t* __restrict__ v, TdBuf td, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int nb = c.td_nb;
+  const int64_t units = (int64_t)td.ctr[1] * nb;
+  const int lane = __lane_id();
+  for (int64_t u = (int64_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); u < units; u += (gridDim.x * blockDim.x) >> 6) {
+    const int32_t L = (int32_t)(u / nb);
+    const int b = (int)(u - (int64_t)L * nb);
+    const TdLarge d = td.large[L];
+    const int32_t* ns_row = td.nstart + (int64_t)L * nb;
+    const int32_t* os_row = td.ostart + (int64_t)L * nb;
+    int64_t a_n = ns_row[b];
+    int32_t a_o = os_row[b];
+    if (a_n < 0 && a_o < 0) {
+      if (lane == 0) d.out[b] = TdCent{0.0, 0};
+      continue;
+    }
+    // ends: the next bucket that starts anything, else the ends of the runs
+    int64_t end_n = d.beg + d.nn;
+    int32_t end_o = d.no;
+    bool fn = false, fo = false;
+    for (int b0 = b + 1; b0 < nb && !(fn && fo); b0 += 64) {
+      const int bb = b0 + lane;
+      const uint64_t mn = __ballot(bb < nb && ns_row[bb] >= 0), mo = __ballot(bb < nb && os_row[bb] >= 0);
+      if (mn && !fn) {
+        end_n = ns_row[b0 + __ffsll((long long)mn) - 1];
+        fn = true;
+      }
+      if (mo && !fo) {
+        end_o = os_row[b0 + __ffsll((long long)mo) - 1];
+        fo = true;
+      }
+    }
+    if (a_n < 0) a_n = end_n;
+    if (a_o < 0) a_o = end_o;
+    double s_new = 0.0, s_old = 0.0;
+    bool any_o = false;
+    const bool any_n = end_n > a_n;
+    if (any_n) s_new = td_wave_new_sum(v, a_n, end_n);
+    for (int32_t j = a_o; j < end_o; j++) td_fold(s_old, any_o, d.old[j].sum);
+    const int64_t w = (end_n - a_n) + (end_o > a_o ? d.old[end_o - 1].cum - (a_o ? d.old[a_o - 1].cum : 0) : 0);
+    if (lane == 0) d.out[b] = TdCent{any_o && any_n ? s_old + s_new : any_o ? s_old : s_new, w};
+  }
+}
+// compaction of a large digest's buckets into its centroids (in place, in order), then the head
+__global__ __launch_bounds__(64) void k_td_large_compact(DevCfg c, TdBuf td, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int32_t nl = td.ctr[1];
+  for (int32_t L = blockIdx.x * blockDim.x + threadIdx.x; L < nl; L += gridDim.x * blockDim.x) {
+    const TdLarge d = td.large[L];
+    int32_t k = 0;
+    int64_t cum = 0;
+    for (int b = 0; b < c.td_nb; b++) {
+      const TdCent g = d.out[b];
+      if (g.cum == 0) continue;
+      cum += g.cum;
+      d.out[k++] = TdCent{g.sum, cum};
+    }
+    *d.head = TdHead{d.pad, k, d.W};
   }
 }
 
@@ -2369,12 +2984,14 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, 
     Entry e = rx.ent[s], fe;
     const FireDecision d = fire_decide(c, wm, e, fe);
     nfire += d.fire;
-    if (!d.keep && !d.fire && c.agg == FW_AGG_HLL) {  // GC without a row: zero and free its block here
-      const uint64_t blk = hll_block_of(e);
-      uint32_t* w = reinterpret_cast<uint32_t*>(c.hll_regs + (blk << c.hll_p));
-      for (int64_t j = 0; j < ((int64_t)1 << c.hll_p) / 4; j++) w[j] = 0u;
-      __threadfence();
-      c.hll_free[atomicAdd(&c.hll_ctr[0], 1)] = (uint32_t)blk;
+    if (!d.keep && !d.fire && c.pool_bytes) {  // GC without a row: free its block here (HLL: zeroed)
+      const uint64_t blk = pool_block_of(e);
+      if (c.agg == FW_AGG_HLL) {
+        uint32_t* w = reinterpret_cast<uint32_t*>(c.pool + (blk << c.hll_p));
+        for (int64_t j = 0; j < ((int64_t)1 << c.hll_p) / 4; j++) w[j] = 0u;
+        __threadfence();
+      }
+      c.pool_free[atomicAdd(&c.pool_ctr[0], 1)] = (uint32_t)blk;
     }
     if (!d.keep) continue;
     const uint64_t h = slot_hash(c, e.key, e.start);
@@ -2401,21 +3018,34 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, 
       if (!fire_decide(c, wm, e, fe).fire) continue;
       if ((int64_t)pos < out.cap) {
         write_row(c, out, pos, fe);
-        if (c.agg == FW_AGG_HLL) out.mn[pos] = (int64_t)hll_block_of(fe);  // read back by hll_finish
+        if (c.agg == FW_AGG_HLL) out.mn[pos] = (int64_t)pool_block_of(fe);  // read back by hll_finish
+        if (c.agg == FW_AGG_TDIGEST) out.sum[pos] = (int64_t)pool_block_of(fe);  // read back by td_finish
       } else {
         atomicOr(&st->flags, FW_STATUS_OUT_FULL);
       }
       pos++;
     }
   }
-  if (c.agg == FW_AGG_HLL && total) {
+  if (c.pool_bytes && total) {
     __shared__ int hl_sb;
     __threadfence_block();
-    if (threadIdx.x == 0) hl_sb = atomicAdd(&c.hll_ctr[0], (int)total);  // free-stack slots for this workgroup
+    if (threadIdx.x == 0) hl_sb = atomicAdd(&c.pool_ctr[0], (int)total);  // free-stack slots for this workgroup
     __syncthreads();
     const uint64_t end = min((unsigned long long)out.cap, base_s + total);
-    for (uint64_t r = base_s + (threadIdx.x >> 6); r < end; r += blockDim.x >> 6)
-      hll_finish(c, out, r, hl_sb + (int64_t)(r - base_s));
+    if (c.agg == FW_AGG_HLL) {
+      for (uint64_t r = base_s + (threadIdx.x >> 6); r < end; r += blockDim.x >> 6)
+        hll_finish(c, out, r, hl_sb + (int64_t)(r - base_s));
+    } else {
+      __shared__ unsigned long long cent_s;
+      if (threadIdx.x == 0) cent_s = 0;
+      __syncthreads();
+      unsigned long long cent = 0;
+      for (uint64_t r = base_s + threadIdx.x; r < end; r += blockDim.x)
+        cent += td_finish(c, out, r, hl_sb + (int64_t)(r - base_s));
+      if (cent) atomicAdd(&cent_s, cent);
+      __syncthreads();
+      if (threadIdx.x == 0 && cent_s) atomicAdd(&st->td_cent, cent_s);
+    }
   }
   if (threadIdx.x == 0) {
     if (total) atomicAdd(&st->fired_total, (unsigned long long)total);
@@ -3046,6 +3676,42 @@ void launch_fire(const DevCfg& c0, int64_t wm, DevTable tb, DevRows out, Status*
   hipLaunchKernelGGL(k_fire, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, wm, tb, out, st);
 }
 
+size_t tdigest_sort_bytes(int64_t n) {
+  size_t a = 0, b = 0;
+  rocprim::double_buffer<uint64_t> kv(nullptr, nullptr);
+  rocprim::double_buffer<uint32_t> ks(nullptr, nullptr);
+  (void)rocprim::radix_sort_pairs(nullptr, a, kv, ks, (size_t)n, 0, 64);
+  (void)rocprim::radix_sort_pairs(nullptr, b, ks, kv, (size_t)n, 0, 32);
+  return std::max(a, b);
+}
+void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
+                    TdBuf& td, Status* st, hipStream_t s) {
+  if (n <= 0) return;
+  const uint32_t none = (uint32_t)td.lidx_slots;  // no slot has this id (slots are 0 .. table slots - 1)
+  unsigned bits = 1;
+  while (((int64_t)1 << bits) <= td.lidx_slots) bits++;
+  (void)hipMemsetAsync(td.ctr, 0, 3 * sizeof(int32_t), s);
+  hipLaunchKernelGGL(k_td_keys, dim3((unsigned)((n + TD_CHUNK - 1) / TD_CHUNK)), dim3(256), 0, s, c, part, offs, T, n,
+                     tb, none, td.gs[0], td.v[0], st);
+  // by value, then stably by slot: each digest's batch values become one run in Double.compare order
+  rocprim::double_buffer<uint64_t> kv(td.v[0], td.v[1]);
+  rocprim::double_buffer<uint32_t> ks(td.gs[0], td.gs[1]);
+  size_t bytes = td.tmp_bytes;
+  (void)rocprim::radix_sort_pairs(td.tmp, bytes, kv, ks, (size_t)n, 0, 64, s);
+  (void)rocprim::radix_sort_pairs(td.tmp, bytes, ks, kv, (size_t)n, 0, bits, s);
+  const uint32_t* gsorted = ks.current();
+  const uint64_t* vsorted = kv.current();
+  const unsigned grid = (unsigned)std::min<int64_t>(8192, (n + 255) / 256);
+  const int64_t per_block = 256 * TD_BOUNDS_PER_THREAD;
+  hipLaunchKernelGGL(k_td_bounds, dim3((unsigned)((n + per_block - 1) / per_block)), dim3(256), 0, s, n, gsorted, none,
+                     td, st);
+  hipLaunchKernelGGL(k_td_small, dim3(grid), dim3(256), 0, s, c, tb, td, vsorted, st);
+  hipLaunchKernelGGL(k_td_wave, dim3(2048), dim3(64 * TD_WAVES), 0, s, c, tb, td, vsorted, st);
+  hipLaunchKernelGGL(k_td_large_old, dim3(64), dim3(256), 0, s, c, vsorted, td, st);  // (the mean keys: first)
+  hipLaunchKernelGGL(k_td_large_items, dim3(grid), dim3(256), 0, s, c, n, gsorted, vsorted, none, td, st);
+  hipLaunchKernelGGL(k_td_large_groups, dim3(2048), dim3(256), 0, s, c, vsorted, td, st);
+  hipLaunchKernelGGL(k_td_large_compact, dim3(64), dim3(64), 0, s, c, td, st);
+}
 void launch_rehash(const DevCfg& oc, DevTable ot, const DevCfg& nc, DevTable nt, hipStream_t s) {
   hipLaunchKernelGGL(k_rehash, dim3(oc.P), dim3(FW_FIRE_THREADS), 0, s, oc, ot, nc, nt);
 }

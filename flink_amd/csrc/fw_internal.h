@@ -50,6 +50,12 @@
 #define FW_LDS_FILL_LIMIT 820  // ~0.8 * FW_LDS_SLOTS: a new slot is not claimed beyond this fill
 #endif
 #define FW_FIRE_THREADS 256
+#ifndef FW_TD_T1
+#define FW_TD_T1 64            // t-digest: digests with at most this many batch values + centroids merge serially
+#endif
+#ifndef FW_TD_T3
+#define FW_TD_T3 16384         // ... at most this many in one wave; more over the whole grid (the hottest keys)
+#endif
 #define FW_SLOW_THREADS 1024   // ordered replay workgroup (one workgroup)
 
 enum : uint32_t { SLOT_EMPTY = 0, SLOT_LIVE = 1, SLOT_DEAD = 2, SLOT_BUSY = 3 };
@@ -68,18 +74,26 @@ struct DevCfg {
   // watermark (set per launch by the host).
   int32_t panes;
   int64_t nt_floor;
-  // HyperLogLog AggregateFunction (FW_AGG_HLL): 2^hll_p one-byte registers per (key, window) in a block
-  // of a pool; an entry's block id is meta >> 1.  Free blocks (zeroed) are kept on a stack:
-  // hll_ctr[0] = stack height, hll_ctr[1] = blocks ever handed out from the end of the pool.
+  // Block pool of the user AggregateFunctions whose accumulator does not fit an Entry: one block of
+  // pool_bytes per live (key, window), the entry's block id is meta >> 1.  Free blocks are kept on a
+  // stack: pool_ctr[0] = stack height, pool_ctr[1] = blocks ever handed out from the end of the pool.
+  //   FW_AGG_HLL: 2^hll_p one-byte registers (zeroed when freed).
+  //   FW_AGG_TDIGEST: TdHead + two halves of td_nb centroids (TdCent); the live half is TdHead::cur.
   int32_t agg, hll_p;
   // FW_AGG_FIRST: arrival ordinal of record 0 of the launch's batch (set per push by the host).  The
   // entry's mx holds ~ordinal of the window's first element, so the max merges everywhere keep it.
   int64_t ord_base;
   int64_t* slow_ord;  // [max_batch] ordinal of each ordered-path record (the push's scratch set)
-  uint8_t* hll_regs;
-  uint32_t* hll_free;
-  int32_t* hll_ctr;
-  int64_t hll_blocks;
+  uint8_t* pool;
+  uint32_t* pool_free;
+  int32_t* pool_ctr;
+  int64_t pool_blocks;
+  int64_t pool_bytes;     // 0 = no pool
+  // FW_AGG_TDIGEST (definition: oracle/window_oracle.h OR_AGG_TDIGEST): td_nb = delta / 2 buckets of the
+  // k1 scale function, td_qb[0 .. td_nb] their bounds sin(pi b / delta)^2 (device), quantiles of the rows
+  int32_t td_nb;
+  const double* td_qb;
+  double td_quant[3];
   // invariant-divisor reciprocals (Granlund-Montgomery round-up method) for `% size` / `% slide`
   uint64_t mag_size, mag_slide;
   int32_t l_size, l_slide;
@@ -151,6 +165,7 @@ struct Status {
   unsigned long long fired_total;
   unsigned long long slow_total;
   unsigned long long merged;          // LDS deltas merged into HBM regions (k_aggregate)
+  unsigned long long td_cent;         // FW_AGG_TDIGEST: centroids of the fired digests
   long long slow_resume;              // ordered path: first list index not yet replayed
   long long need_out;                 // fired-row capacity the ordered path asked for when it suspended
   int32_t need_live;                  // largest live count a region asked for when it suspended
@@ -167,7 +182,7 @@ enum {
   FW_STATUS_OUT_FULL = 2,
   FW_STATUS_MERGE_LATE = 4,
   FW_STATUS_SIDE_FULL = 8,
-  FW_STATUS_HLL_POOL = 16    // the HyperLogLog register pool ran out of blocks
+  FW_STATUS_POOL = 16        // the accumulator block pool (HyperLogLog registers, t-digests) ran out of blocks
 };
 // a region takes new windows only up to this load; beyond it the kernel suspends and the table grows
 __host__ __device__ inline int32_t region_limit(int32_t log_r) { return (int32_t)((3ll << log_r) >> 2); }
@@ -207,9 +222,49 @@ struct DevTable {
 
 struct DevRows {
   int64_t *key, *start, *end, *cnt, *sum, *mn, *mx;
+  int64_t* dig;        // FW_AGG_TDIGEST with export: per row [n, (sum bits, weight) x td_nb] (nullptr = off)
   int64_t cap;
   int64_t slow_limit;  // the ordered path stops here, leaving room for one watermark's firing (cap - table slots)
 };
+// ---- t-digest blocks (FW_AGG_TDIGEST): a 16-byte head, then two halves of td_nb centroids each
+struct TdHead {
+  int32_t cur;    // live half
+  int32_t n;      // centroids in it
+  int64_t w;      // their total weight (elements compressed so far)
+};
+struct TdCent {
+  double sum;     // the centroid's elements added left to right (mean = sum / weight)
+  int64_t cum;    // total weight of this and every earlier centroid
+};
+// per-push buffers of the t-digest compression (fw_runtime.cpp allocates them for max_batch records)
+struct TdLarge {  // a digest whose batch is compressed bucket-parallel
+  int64_t beg, nn;          // its values in the sorted batch
+  int64_t W;                // total weight after the batch
+  int32_t no;               // old centroids
+  int32_t pad;
+  const TdCent* old;        // live half
+  TdCent* out;              // the other half (group sums per bucket, then the centroids)
+  TdHead* head;
+};
+struct TdBuf {
+  uint32_t* gs[2];          // sort keys: global slot (partition << log_r | slot) of each record's entry
+  uint64_t* v[2];           // sort keys: Double.compare-ordered value
+  void* tmp;                // rocPRIM radix-sort scratch
+  size_t tmp_bytes;
+  uint32_t* tslot;          // touched digests: global slot      [max_batch]
+  uint32_t* tbeg;           //                  first sorted value [max_batch]
+  int32_t* ctr;             // [0] touched digests, [1] large ones, [2] wave-tier ones
+  uint32_t* mid;            // [max_batch] the wave tier's digests (touched indices)
+  TdLarge* large;           // [max_large]
+  int32_t* nstart;          // [max_large * td_nb] first sorted value of each bucket (-1: none)
+  int32_t* ostart;          // [max_large * td_nb] first old centroid of each bucket (-1: none)
+  uint64_t* okey;           // [max_large * td_nb] the large digests' old centroids' mean keys
+  int32_t* lidx;            // [table slots] large index of a touched digest, -1 = compressed serially
+  int64_t lidx_slots;
+  int32_t max_large;
+  int32_t sel;              // which of gs / v holds the sorted batch (set by launch_tdigest)
+};
+
 // columns of keyed-state snapshot rows (fw_state_rows, device side)
 struct StateCols {
   int64_t *key, *start, *end, *cnt, *sum, *mn, *mx, *timer;
@@ -241,6 +296,10 @@ int64_t pane_nt_floor(const DevCfg& c, int64_t wm);  // host: DevCfg::nt_floor o
 // FW_AGG_HLL: fold the batch's records into the registers of their (key, window) entries (after aggregate)
 void launch_hll_update(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
                        Status* st, hipStream_t_ s);
+// FW_AGG_TDIGEST: compress the batch's values into the digests of their (key, window) entries (after aggregate)
+void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
+                    TdBuf& td, Status* st, hipStream_t_ s);
+size_t tdigest_sort_bytes(int64_t n);  // rocPRIM scratch of the two sorts
 void launch_rehash(const DevCfg& old_c, DevTable old_t, const DevCfg& new_c, DevTable new_t, hipStream_t_ s);
 void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t_ s);
 void launch_reset_regions(const DevCfg& c, DevTable tb, hipStream_t_ s);

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -70,6 +71,8 @@ struct fw_op {
   AggProg prog{};    // k_aggregate resume points
   uint32_t taint_epoch = 0;  // sessions: epoch of the latest batch's taint set (DevCfg.taint_*)
   AggHot hot{};              // split-partition buffers (allocated by the first batch that may need them)
+  TdBuf td{};                // FW_AGG_TDIGEST: per-push compression buffers
+  bool td_export = false;    // FW_AGG_TDIGEST: fired rows keep their centroids (DevRows::dig)
 
   DevRows out{};
   DevSide side{};
@@ -174,7 +177,7 @@ int alloc_scratch(fw_op* op, Scratch& s, int64_t mb, int64_t m) {
   HIP_OR_RETURN(op, dmalloc(&s.stt, mb));
   HIP_OR_RETURN(op, dmalloc(&s.sv, mb));
   HIP_OR_RETURN(op, dmalloc(&s.skh, mb));
-  if (op->cfg.aggregate >= FW_AGG_FIRST) HIP_OR_RETURN(op, dmalloc(&s.so, mb));
+  if (op->cfg.aggregate >= FW_AGG_FIRST && op->cfg.aggregate <= FW_AGG_FIRST_MAX) HIP_OR_RETURN(op, dmalloc(&s.so, mb));
   return FW_OK;
 }
 void free_scratch(Scratch& s) {
@@ -231,8 +234,16 @@ int ensure_out_capacity(fw_op* op, int64_t need, int64_t keep) {
       HIP_OR_RETURN(op, hipMemcpyAsync(*cols_new[i], *cols_old[i], keep * sizeof(int64_t), hipMemcpyDeviceToDevice,
                                        op->stream));
   }
+  const int64_t dstride = 1 + 2 * (int64_t)op->dc.td_nb;  // t-digest export: one record per row
+  if (op->td_export) {
+    HIP_OR_RETURN(op, dmalloc(&n.dig, (size_t)(cap * dstride)));
+    if (keep > 0 && op->out.dig)
+      HIP_OR_RETURN(op, hipMemcpyAsync(n.dig, op->out.dig, keep * dstride * sizeof(int64_t), hipMemcpyDeviceToDevice,
+                                       op->stream));
+  }
   HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
   for (int i = 0; i < 7; i++) dfree(*cols_old[i]);
+  dfree(op->out.dig);
   n.cap = cap;
   op->out = n;
   set_slow_limit(op);
@@ -259,9 +270,9 @@ int ensure_side_capacity(fw_op* op, int64_t need, int64_t keep) {
   return FW_OK;
 }
 
-enum { K_CLASSIFY = 0, K_SCAN, K_SCATTER, K_AGGREGATE, K_SLOW, K_FIRE };
-const char* const KERNEL_NAMES[FW_NUM_KERNELS] = {"k_classify_hist", "k_scan", "k_scatter",
-                                                  "k_aggregate",     "k_slow", "k_fire"};
+enum { K_CLASSIFY = 0, K_SCAN, K_SCATTER, K_AGGREGATE, K_SLOW, K_FIRE, K_TDIGEST };
+const char* const KERNEL_NAMES[FW_NUM_KERNELS] = {"k_classify_hist", "k_scan", "k_scatter", "k_aggregate",
+                                                  "k_slow",          "k_fire", "k_tdigest"};
 
 hipEvent_t prof_event(fw_op* op) {
   if (!op->prof_free.empty()) {
@@ -358,6 +369,12 @@ int grow_table(fw_op* op, int new_log_r) {
   op->dc = nc;
   op->table_slots = (int64_t)nc.P << nc.log_r;
   op->grows++;
+  if (op->dc.agg == FW_AGG_TDIGEST) {  // the compression's per-slot index follows the table
+    if (op->table_slots >= (int64_t(1) << 31)) return set_err(op, FW_ERR_CAPACITY, "t-digest table would exceed 2^31 slots");
+    dfree(op->td.lidx);
+    HIP_OR_RETURN(op, dmalloc(&op->td.lidx, (size_t)op->table_slots));
+    op->td.lidx_slots = op->table_slots;
+  }
   const int64_t rows = (int64_t)op->h_status->out_rows;
   return ensure_out_capacity(op, rows + op->table_slots, rows);
 }
@@ -417,6 +434,11 @@ int settle(fw_op* op) {
         if (c.agg == FW_AGG_HLL)
           fwdev::launch_hll_update(c, S.part, S.hist, S.T, S.n, op->tb, op->d_status, op->stream);
       });
+    // the t-digest compression skipped itself too (it runs once, after the aggregate completed)
+    if ((susp & FW_SUSP_AGG) && c.agg == FW_AGG_TDIGEST)
+      timed(op, K_TDIGEST, [&] {
+        fwdev::launch_tdigest(c, S.part, S.hist, S.T, S.n, op->tb, op->td, op->d_status, op->stream);
+      });
     // after an aggregate suspension the ordered path never started; otherwise it resumes
     timed(op, K_SLOW, [&] {
       fwdev::launch_slow(c, S.wm, S.hist, S.T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status,
@@ -441,9 +463,9 @@ int settle(fw_op* op) {
     return set_err(op, FW_ERR_CAPACITY,
                    "a window could not be stored (more than 64 in-flight sessions of one key)");
   if (s.flags & FW_STATUS_OUT_FULL) return set_err(op, FW_ERR_STATE, "fired-row buffer overflow");
-  if (s.flags & FW_STATUS_HLL_POOL)
-    return set_err(op, FW_ERR_CAPACITY, "HyperLogLog register pool exhausted (%lld blocks; raise expected_entries)",
-                   (long long)op->dc.hll_blocks);
+  if (s.flags & FW_STATUS_POOL)
+    return set_err(op, FW_ERR_CAPACITY, "accumulator block pool exhausted (%lld blocks; raise expected_entries)",
+                   (long long)op->dc.pool_blocks);
   if (s.flags & FW_STATUS_SIDE_FULL) return set_err(op, FW_ERR_STATE, "side-output buffer overflow");
   if (s.kg_errors) return set_err(op, FW_ERR_KEY_GROUP, "%d record(s) outside KeyGroupRange [%d, %d]", s.kg_errors,
                                    op->dc.kg0, op->dc.kg0 + op->dc.n_kg - 1);
@@ -555,6 +577,10 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
                             op->d_status, op->stream);
     if (cc.agg == FW_AGG_HLL) fwdev::launch_hll_update(cc, S.part, S.hist, T, n, op->tb, op->d_status, op->stream);
   });
+  if (cc.agg == FW_AGG_TDIGEST)
+    timed(op, K_TDIGEST, [&] {
+      fwdev::launch_tdigest(cc, S.part, S.hist, T, n, op->tb, op->td, op->d_status, op->stream);
+    });
   timed(op, K_SLOW, [&] {
     fwdev::launch_slow(cc, op->wm, S.hist, T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status, 0,
                        op->stream);
@@ -615,7 +641,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     snprintf(msg, sizeof msg, "invalid KeyGroupRange [%d, %d]", cfg.key_group_start, cfg.key_group_end);
   if (!msg[0] && cfg.sub_partitions != 0 && (cfg.sub_partitions & (cfg.sub_partitions - 1)))
     snprintf(msg, sizeof msg, "sub_partitions must be a power of two");
-  if (!msg[0] && (cfg.aggregate < FW_AGG_COUNT_SUM_MIN_MAX || cfg.aggregate > FW_AGG_FIRST_MAX))
+  if (!msg[0] && (cfg.aggregate < FW_AGG_COUNT_SUM_MIN_MAX || cfg.aggregate > FW_AGG_TDIGEST))
     snprintf(msg, sizeof msg, "unknown aggregate %d", cfg.aggregate);
   const int32_t hll_p = cfg.hll_precision ? cfg.hll_precision : 14;
   if (!msg[0] && cfg.aggregate == FW_AGG_HLL && (hll_p < 4 || hll_p > 16))
@@ -627,11 +653,29 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
                               "over a Long item column");
     unsupported = true;
   }
+  const int32_t td_delta = cfg.tdigest_compression ? cfg.tdigest_compression : 100;
+  if (cfg.aggregate == FW_AGG_TDIGEST && cfg.tdigest_quantiles[0] == 0 && cfg.tdigest_quantiles[1] == 0 &&
+      cfg.tdigest_quantiles[2] == 0) {
+    cfg.tdigest_quantiles[0] = 0.5;
+    cfg.tdigest_quantiles[1] = 0.95;
+    cfg.tdigest_quantiles[2] = 0.99;
+  }
+  if (!msg[0] && cfg.aggregate == FW_AGG_TDIGEST && (td_delta < 10 || td_delta > 500 || (td_delta & 1)))
+    snprintf(msg, sizeof msg, "t-digest compression must be even and in [10, 500], got %d", td_delta);
+  for (int i = 0; i < 3 && !msg[0] && cfg.aggregate == FW_AGG_TDIGEST; i++)
+    if (!(cfg.tdigest_quantiles[i] >= 0.0 && cfg.tdigest_quantiles[i] <= 1.0))
+      snprintf(msg, sizeof msg, "t-digest quantiles must be in [0, 1]");
+  if (!msg[0] && cfg.aggregate == FW_AGG_TDIGEST &&
+      (cfg.assigner != FW_TUMBLING || cfg.allowed_lateness != 0 || cfg.value_type != FW_VAL_F64)) {
+    snprintf(msg, sizeof msg, "the t-digest aggregate is offered for tumbling windows without allowed lateness "
+                              "over a Double field");
+    unsupported = true;
+  }
   if (!msg[0] && (cfg.aggregate == FW_AGG_MINBY || cfg.aggregate == FW_AGG_MAXBY) && cfg.value_type != FW_VAL_I32) {
     snprintf(msg, sizeof msg, "minBy / maxBy are offered over an Integer field");
     unsupported = true;
   }
-  if (!msg[0] && cfg.aggregate >= FW_AGG_FIRST && cfg.assigner == FW_SLIDING && cfg.slide > 0 &&
+  if (!msg[0] && cfg.aggregate >= FW_AGG_FIRST && cfg.aggregate <= FW_AGG_FIRST_MAX && cfg.assigner == FW_SLIDING && cfg.slide > 0 &&
       (cfg.size + cfg.slide - 1) / cfg.slide > 65535) {
     snprintf(msg, sizeof msg, "the first-element aggregate takes at most 65535 windows per element");
     unsupported = true;
@@ -689,21 +733,44 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   // compact 16-byte partitioned records (DevCfg::compact): one window per record, an order-free aggregate,
   // and at least 2 bits of sub-partition to carry the window delta (FW_NO_COMPACT=1 disables them)
   c.compact = (cfg.assigner == FW_TUMBLING || c.panes) &&
-              (cfg.aggregate == FW_AGG_COUNT_SUM_MIN_MAX || cfg.aggregate == FW_AGG_HLL) && c.log_s >= 2 &&
+              (cfg.aggregate == FW_AGG_COUNT_SUM_MIN_MAX || cfg.aggregate == FW_AGG_HLL ||
+               cfg.aggregate == FW_AGG_TDIGEST) && c.log_s >= 2 &&
               !(getenv("FW_NO_COMPACT") && atoi(getenv("FW_NO_COMPACT")));
   const int64_t expected = cfg.expected_entries > 0 ? cfg.expected_entries : (int64_t)c.P * 512;
-  if (cfg.aggregate >= FW_AGG_FIRST) c.agg = cfg.aggregate;
+  if (cfg.aggregate >= FW_AGG_FIRST) c.agg = cfg.aggregate;  // (FW_AGG_HLL is set below)
   if (cfg.aggregate == FW_AGG_HLL) {
     // register pool: one 2^p-byte block per live (key, window); expected_entries live entries, plus
     // a quarter for entries created before the watermark that retires their predecessors
     c.agg = FW_AGG_HLL;
     c.hll_p = hll_p;
-    c.hll_blocks = std::max<int64_t>(1024, expected + expected / 4);
-    HIP_OR_RETURN(op, dmalloc(&c.hll_regs, (size_t)(c.hll_blocks << hll_p)));
-    HIP_OR_RETURN(op, hipMemsetAsync(c.hll_regs, 0, (size_t)(c.hll_blocks << hll_p), op->stream));
-    HIP_OR_RETURN(op, dmalloc(&c.hll_free, (size_t)c.hll_blocks));
-    HIP_OR_RETURN(op, dmalloc(&c.hll_ctr, 2));
-    HIP_OR_RETURN(op, hipMemsetAsync(c.hll_ctr, 0, 2 * sizeof(int32_t), op->stream));
+    c.pool_bytes = (int64_t)1 << hll_p;
+  } else if (cfg.aggregate == FW_AGG_TDIGEST) {
+    // digest pool: a head and two halves of delta/2 centroids per live (key, window) (TdHead, TdCent)
+    c.td_nb = td_delta / 2;
+    c.pool_bytes = ((int64_t)sizeof(TdHead) + 2 * c.td_nb * (int64_t)sizeof(TdCent) + 63) / 64 * 64;
+    for (int i = 0; i < 3; i++) c.td_quant[i] = cfg.tdigest_quantiles[i];
+    // the k1 scale function's unit steps qb[b] = sin(pi b / delta)^2 (the oracle computes the same table)
+    std::vector<double> qb(c.td_nb + 1);
+    for (int b = 0; b <= c.td_nb; b++) {
+      const double sn = std::sin(M_PI * (double)b / (double)td_delta);
+      qb[b] = sn * sn;
+    }
+    qb[0] = 0.0;
+    qb[c.td_nb] = 1.0;
+    double* dq = nullptr;
+    HIP_OR_RETURN(op, dmalloc(&dq, qb.size()));
+    HIP_OR_RETURN(op, hipMemcpy(dq, qb.data(), qb.size() * sizeof(double), hipMemcpyHostToDevice));
+    c.td_qb = dq;
+    op->td_export = cfg.tdigest_export != 0;
+  }
+  if (c.pool_bytes) {
+    c.pool_blocks = std::max<int64_t>(1024, expected + expected / 4);
+    HIP_OR_RETURN(op, dmalloc(&c.pool, (size_t)(c.pool_blocks * c.pool_bytes)));
+    if (c.agg == FW_AGG_HLL)  // registers start at zero (and are zeroed when freed)
+      HIP_OR_RETURN(op, hipMemsetAsync(c.pool, 0, (size_t)(c.pool_blocks * c.pool_bytes), op->stream));
+    HIP_OR_RETURN(op, dmalloc(&c.pool_free, (size_t)c.pool_blocks));
+    HIP_OR_RETURN(op, dmalloc(&c.pool_ctr, 2));
+    HIP_OR_RETURN(op, hipMemsetAsync(c.pool_ctr, 0, 2 * sizeof(int32_t), op->stream));
   }
   c.log_r = std::max(8, ilog2(4 * ((expected + c.P - 1) / c.P)));
   op->table_slots = (int64_t)c.P << c.log_r;
@@ -729,6 +796,29 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     HIP_OR_RETURN(op, dmalloc(&c.taint_state, (size_t)cap));
     HIP_OR_RETURN(op, hipMemsetAsync(c.taint_state, 0, (size_t)cap * sizeof(uint32_t), op->stream));
     c.taint_mask = (uint32_t)(cap - 1);
+  }
+  if (c.agg == FW_AGG_TDIGEST) {
+    TdBuf& t = op->td;
+    for (int b = 0; b < 2; b++) {
+      HIP_OR_RETURN(op, dmalloc(&t.gs[b], (size_t)mb));
+      HIP_OR_RETURN(op, dmalloc(&t.v[b], (size_t)mb));
+    }
+    t.tmp_bytes = fwdev::tdigest_sort_bytes(mb);
+    HIP_OR_RETURN(op, dmalloc((uint8_t**)&t.tmp, t.tmp_bytes));
+    HIP_OR_RETURN(op, dmalloc(&t.tslot, (size_t)mb));
+    HIP_OR_RETURN(op, dmalloc(&t.tbeg, (size_t)mb));
+    HIP_OR_RETURN(op, dmalloc(&t.ctr, 3));
+    // a wave-tier digest has more than FW_TD_T1 - delta/2 values in the batch, a large one more than
+    // FW_TD_T3 - delta/2
+    HIP_OR_RETURN(op, dmalloc(&t.mid, (size_t)mb));
+    t.max_large = (int32_t)(mb / std::max<int64_t>(1, FW_TD_T3 - c.td_nb) + 1);
+    HIP_OR_RETURN(op, dmalloc(&t.large, (size_t)t.max_large));
+    HIP_OR_RETURN(op, dmalloc(&t.nstart, (size_t)t.max_large * c.td_nb));
+    HIP_OR_RETURN(op, dmalloc(&t.ostart, (size_t)t.max_large * c.td_nb));
+    HIP_OR_RETURN(op, dmalloc(&t.okey, (size_t)t.max_large * c.td_nb));
+    if (op->table_slots >= (int64_t(1) << 31)) return set_err(op, FW_ERR_CAPACITY, "t-digest table would exceed 2^31 slots");
+    HIP_OR_RETURN(op, dmalloc(&t.lidx, (size_t)op->table_slots));
+    t.lidx_slots = op->table_slots;
   }
   HIP_OR_RETURN(op, dmalloc(&op->prog.rb, (size_t)c.P));
   HIP_OR_RETURN(op, dmalloc(&op->prog.tp, (size_t)c.P * FW_AGG_THREADS));
@@ -766,13 +856,33 @@ void fw_destroy(fw_op* op) {
   dfree(op->prog.tp);
   dfree(op->prog.done);
   dfree(op->dc.taint_key);
-  dfree(op->dc.hll_regs);
-  dfree(op->dc.hll_free);
-  dfree(op->dc.hll_ctr);
+  dfree(op->dc.pool);
+  dfree(op->dc.pool_free);
+  dfree(op->dc.pool_ctr);
+  {
+    double* q = const_cast<double*>(op->dc.td_qb);
+    dfree(q);
+    TdBuf& t = op->td;
+    for (int b = 0; b < 2; b++) {
+      dfree(t.gs[b]);
+      dfree(t.v[b]);
+    }
+    uint8_t* tmp = (uint8_t*)t.tmp;
+    dfree(tmp);
+    dfree(t.tslot);
+    dfree(t.tbeg);
+    dfree(t.ctr);
+    dfree(t.large);
+    dfree(t.mid);
+    dfree(t.okey);
+    dfree(t.nstart);
+    dfree(t.ostart);
+    dfree(t.lidx);
+  }
   dfree(op->dc.taint_state);
   free_hot(op->hot);
   for (int64_t** col : {&op->out.key, &op->out.start, &op->out.end, &op->out.cnt, &op->out.sum, &op->out.mn,
-                        &op->out.mx, &op->side.key, &op->side.ts, &op->side.val})
+                        &op->out.mx, &op->out.dig, &op->side.key, &op->side.ts, &op->side.val})
     dfree(*col);
   dfree(op->d_status);
   dfree(op->d_stats3);
@@ -916,6 +1026,32 @@ int fw_rows_device(fw_op* op, fw_rows* view, int64_t* n) {
   return FW_OK;
 }
 
+int fw_drain_digests(fw_op* op, int64_t* n_cent, double* sum, int64_t* weight, int64_t cap, int64_t* n) {
+  if (!op) return FW_ERR_ARG;
+  if (!op->td_export) return set_err(op, FW_ERR_UNSUPPORTED, "fw_drain_digests needs FW_AGG_TDIGEST with tdigest_export");
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  int rc = settle(op);
+  if (rc) return rc;
+  const int64_t base = op->out_base, have = (int64_t)op->h_status->out_rows - base;
+  if (n) *n = have;
+  if (cap < have) return set_err(op, FW_ERR_ARG, "drain capacity %lld < pending rows %lld", (long long)cap, (long long)have);
+  if (have <= 0) return FW_OK;
+  const int64_t nb = op->dc.td_nb, stride = 1 + 2 * nb;
+  std::vector<int64_t> h((size_t)(have * stride));
+  HIP_OR_RETURN(op, hipMemcpyAsync(h.data(), op->out.dig + base * stride, h.size() * sizeof(int64_t),
+                                   hipMemcpyDeviceToHost, op->stream));
+  HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
+  for (int64_t i = 0; i < have; i++) {
+    const int64_t* d = h.data() + i * stride;
+    if (n_cent) n_cent[i] = d[0];
+    for (int64_t k = 0; k < d[0] && k < nb; k++) {
+      if (sum) memcpy(&sum[i * nb + k], &d[1 + 2 * k], sizeof(double));
+      if (weight) weight[i * nb + k] = d[2 + 2 * k];
+    }
+  }
+  return FW_OK;
+}
+
 int fw_clear_pending(fw_op* op) {
   if (!op) return FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
@@ -951,6 +1087,7 @@ int fw_get_stats(fw_op* op, fw_stats* o) {
   o->table_grows = op->grows;
   o->slow_path_records = (int64_t)s.slow_total;
   o->state_merges = (int64_t)s.merged;
+  o->digest_centroids_fired = (int64_t)s.td_cent;
   return FW_OK;
 }
 
@@ -1008,8 +1145,10 @@ void free_state_cols(StateCols& c) {
 }  // namespace
 
 int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64_t cap, int64_t* n) {
-  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_MINBY || op->dc.agg == FW_AGG_MAXBY))  // not in fw_state_rows
-    return set_err(op, FW_ERR_UNSUPPORTED, "keyed-state snapshots of the HyperLogLog, minBy and maxBy aggregates are not offered");
+  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_MINBY || op->dc.agg == FW_AGG_MAXBY ||
+             op->dc.agg == FW_AGG_TDIGEST))  // not in fw_state_rows
+    return set_err(op, FW_ERR_UNSUPPORTED,
+                   "keyed-state snapshots of the HyperLogLog, t-digest, minBy and maxBy aggregates are not offered");
   if (!op || !n) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;
@@ -1048,8 +1187,10 @@ int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64
 }
 
 int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_t n) {
-  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_MINBY || op->dc.agg == FW_AGG_MAXBY))  // not in fw_state_rows
-    return set_err(op, FW_ERR_UNSUPPORTED, "keyed-state snapshots of the HyperLogLog, minBy and maxBy aggregates are not offered");
+  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_MINBY || op->dc.agg == FW_AGG_MAXBY ||
+             op->dc.agg == FW_AGG_TDIGEST))  // not in fw_state_rows
+    return set_err(op, FW_ERR_UNSUPPORTED,
+                   "keyed-state snapshots of the HyperLogLog, t-digest, minBy and maxBy aggregates are not offered");
   if (!op || (n > 0 && !src) || n < 0) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;

@@ -46,6 +46,11 @@ class GpuWindowOperator:
             setattr(c, k, v)
         c.value_type = aggregate.native()
         c.hll_precision = aggregate.hll_precision()
+        td = aggregate.tdigest()
+        if td is not None:
+            c.tdigest_compression = td.compression
+            c.tdigest_export = int(td.export)
+            c.tdigest_quantiles = (ctypes.c_double * 3)(*td.quantiles)
         c.aggregate = aggregate.aggregate_kind()
         c.key_kind = _KEY_KINDS[key_type]
         c.purging = int(trigger.purging)
@@ -189,6 +194,23 @@ class GpuWindowOperator:
             out[f] = cols[f][:got.value]
         out["epoch"] = epoch
         return out
+
+    def drain_digests(self):
+        """TDigest(export=True): the centroids of the pending rows, as a list of (sums f64[], weights i64[])
+        in row order.  Call before the rows are drained (process_watermark drains them: use
+        advance_watermark, then drain_digests, then drain_rows)."""
+        L = N.lib()
+        n_rows = ctypes.c_int64()
+        N.check(L.fw_pending(self._h, ctypes.byref(n_rows), None), self._h)
+        nb = self.aggregate.compression // 2
+        n = n_rows.value
+        cnt = np.zeros(n, dtype=np.int64)
+        sums = np.zeros(n * nb, dtype=np.float64)
+        ws = np.zeros(n * nb, dtype=np.int64)
+        got = ctypes.c_int64()
+        N.check(L.fw_drain_digests(self._h, cnt.ctypes.data, sums.ctypes.data, ws.ctypes.data, n,
+                                   ctypes.byref(got)), self._h)
+        return [(sums[i * nb:i * nb + cnt[i]].copy(), ws[i * nb:i * nb + cnt[i]].copy()) for i in range(got.value)]
 
     def drain_side(self, epoch=-1):
         L = N.lib()

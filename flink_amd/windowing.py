@@ -160,6 +160,9 @@ class CountSumMinMax:
     def hll_precision(self):
         return 0
 
+    def tdigest(self):
+        return None
+
     def aggregate_kind(self):
         return N.FW_AGG_COUNT_SUM_MIN_MAX
 
@@ -183,6 +186,9 @@ class FirstElementReduce:
     def hll_precision(self):
         return 0
 
+    def tdigest(self):
+        return None
+
     def aggregate_kind(self):
         return N.FW_AGG_FIRST_MAX if self.field == "max" else N.FW_AGG_FIRST
 
@@ -201,6 +207,9 @@ class ExtremalElementReduce:
 
     def hll_precision(self):
         return 0
+
+    def tdigest(self):
+        return None
 
     def aggregate_kind(self):
         return N.FW_AGG_MINBY if self.kind == "min" else N.FW_AGG_MAXBY
@@ -242,5 +251,53 @@ class HyperLogLog:
     def hll_precision(self):
         return self.precision
 
+    def tdigest(self):
+        return None
+
     def aggregate_kind(self):
         return N.FW_AGG_HLL
+
+
+@dataclass(frozen=True)
+class TDigest:
+    """User AggregateFunction of SURVEY §8d C5: quantiles of a Double field per key and window from a merging
+    t-digest with the k1 scale function and compression `compression` (delta; at most delta/2 centroids).
+    Definition: DESIGN.md §t-digest, restated in oracle/window_oracle.h.  add buffers the value; every
+    micro-batch (push) compresses the values it added into the centroids (AggregateFunction.merge of the
+    batch's digest); getResult = (count, the quantiles `quantiles`).  Fired rows: count, sum / min / max =
+    the three quantile estimates (f64 bits).  With export=True the operator also keeps each fired row's
+    centroids (GpuWindowOperator.drain_digests).  Offered for tumbling windows without allowed lateness."""
+    compression: int = 100
+    quantiles: tuple = (0.5, 0.95, 0.99)
+    export: bool = False
+    value_type: str = "double"
+
+    def native(self):
+        return N.FW_VAL_F64
+
+    def hll_precision(self):
+        return 0
+
+    def tdigest(self):
+        return self
+
+    def aggregate_kind(self):
+        return N.FW_AGG_TDIGEST
+
+
+def tdigest_quantile(sums, weights, mn, mx, q):
+    """Quantile q of a digest's centroids (sum, weight) with the window's min / max: the read-out of
+    TDigest's getResult (piecewise-linear through (0, min), (centre_i, mean_i), (W, max)), for a row's
+    exported centroids."""
+    W = float(sum(int(w) for w in weights))
+    if not len(sums):
+        return float("nan")
+    x = q * W
+    x0, y0, before = 0.0, mn, 0.0
+    for s, w in zip(sums, weights):
+        t = before + float(w) * 0.5
+        m = float(s) / float(w)
+        if t >= x:
+            return y0 + (m - y0) * ((x - x0) / (t - x0))
+        x0, y0, before = t, m, before + float(w)
+    return y0 + (mx - y0) * ((x - x0) / (W - x0))

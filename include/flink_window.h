@@ -69,6 +69,14 @@ extern "C" {
                                       elements of one window span fewer than 2^32 arrival ordinals.  Keyed-state
                                       snapshots are refused. */
 #define FW_AGG_MAXBY 4
+#define FW_AGG_TDIGEST 6           /* t-digest quantiles of a Double field (definition in DESIGN.md
+                                      §t-digest and oracle/window_oracle.h): a merging t-digest with the k1 scale
+                                      function, compression tdigest_compression (delta), at most delta/2
+                                      centroids; add buffers, and every push compresses the values it added.
+                                      Rows carry count = elements and sum / min / max = the estimated quantiles
+                                      tdigest_quantiles[0..2] (f64 bits).  Tumbling windows, no allowed lateness,
+                                      FW_VAL_F64; expected_entries sizes the digest pool.  Keyed-state snapshots
+                                      are refused. */
 #define FW_AGG_FIRST_MAX 5         /* max(pos) (ComparableAggregator.java:72-94, Comparator.MaxComparator): as
                                       FW_AGG_FIRST, but the min column holds the field's MAXIMUM (the first
                                       element with the field replaced by the max) */
@@ -104,6 +112,10 @@ typedef struct fw_config {
   int64_t max_batch;           /* largest n passed to one push (0 = 1 << 24)                */
   int32_t aggregate;           /* FW_AGG_* (0 = count/sum/min/max)                           */
   int32_t hll_precision;       /* FW_AGG_HLL: p in [4, 16], m = 2^p registers (0 -> 14)       */
+  int32_t tdigest_compression; /* FW_AGG_TDIGEST: delta, even, in [10, 500] (0 -> 100)         */
+  int32_t tdigest_export;      /* FW_AGG_TDIGEST: 1 = fired rows also keep their centroids for
+                                  fw_drain_digests                                             */
+  double tdigest_quantiles[3]; /* FW_AGG_TDIGEST: the quantiles of a row (all 0 -> .5 .95 .99) */
 } fw_config;
 
 typedef struct fw_op fw_op;
@@ -143,6 +155,7 @@ typedef struct fw_stats {
   int64_t table_grows;            /* times the table was resized                             */
   int64_t slow_path_records;      /* records replayed in arrival order (late firing / drop)  */
   int64_t state_merges;           /* pre-aggregated (key, window) deltas merged into HBM       */
+  int64_t digest_centroids_fired; /* FW_AGG_TDIGEST: centroids of all digests fired so far      */
 } fw_stats;
 
 /* Lifecycle — StreamOperator.setup/open/close/dispose (api/operators/StreamOperator.java:57-127). */
@@ -184,15 +197,19 @@ int fw_pending(fw_op* op, int64_t* n_rows, int64_t* n_side_rows);
 int fw_drain_rows(fw_op* op, const fw_rows* host_dst, int64_t cap, int64_t* n);
 int fw_drain_side(fw_op* op, const fw_side_rows* host_dst, int64_t cap, int64_t* n);
 int fw_rows_device(fw_op* op, fw_rows* dev_view, int64_t* n);
+/* FW_AGG_TDIGEST with tdigest_export: the centroids of the pending rows (the AggregateFunction's accumulator at
+ * getResult), without draining them: for pending row i, n_centroids[i] and the centroids' sums (f64) and
+ * weights at [i * delta/2 + k], k < n_centroids[i].  Call before fw_drain_rows. */
+int fw_drain_digests(fw_op* op, int64_t* n_centroids, double* sum, int64_t* weight, int64_t cap_rows, int64_t* n);
 int fw_clear_pending(fw_op* op);
 
 int fw_get_stats(fw_op* op, fw_stats* out);
 
 /* Per-kernel timing with HIP events recorded around every launch on the handle's stream
  * (rocprofv3 --kernel-trace measures the same launches from outside).  Kernel kinds, in order:
- * classify_hist, scan, scatter, aggregate, slow, fire.  fw_profile_read returns accumulated
+ * classify_hist, scan, scatter, aggregate, slow, fire, tdigest (the t-digest compression of a push).  fw_profile_read returns accumulated
  * milliseconds and launch counts per kind (arrays of FW_NUM_KERNELS) and optionally resets them. */
-#define FW_NUM_KERNELS 6
+#define FW_NUM_KERNELS 7
 int fw_profile(fw_op* op, int enable);
 int fw_profile_read(fw_op* op, double* ms, int64_t* launches, int reset);
 const char* fw_kernel_name(int kind);

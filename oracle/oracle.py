@@ -22,7 +22,8 @@ class OracleCfg(ctypes.Structure):
     _fields_ = [("assigner", ctypes.c_int32), ("value_type", ctypes.c_int32), ("size", ctypes.c_int64),
                 ("slide", ctypes.c_int64), ("offset", ctypes.c_int64), ("gap", ctypes.c_int64),
                 ("lateness", ctypes.c_int64), ("purging", ctypes.c_int32), ("side_output", ctypes.c_int32),
-                ("aggregate", ctypes.c_int32), ("hll_p", ctypes.c_int32)]
+                ("aggregate", ctypes.c_int32), ("hll_p", ctypes.c_int32), ("td_delta", ctypes.c_int32),
+                ("td_pad", ctypes.c_int32), ("td_q", ctypes.c_double * 3)]
 
 
 ROW_DTYPE = np.dtype([("key", "<i8"), ("start", "<i8"), ("end", "<i8"), ("count", "<i8"), ("sum", "<i8"),
@@ -81,6 +82,8 @@ def lib():
         L.oracle_count_num_rows.restype = ctypes.c_int64
         L.oracle_count_num_rows.argtypes = [P]
         L.oracle_count_get_rows.argtypes = [P, P]
+        L.oracle_row_digest.restype = ctypes.c_int64
+        L.oracle_row_digest.argtypes = [P, ctypes.c_int64, P, P, ctypes.c_int64]
         _lib = L
     return _lib
 
@@ -89,18 +92,21 @@ def _i64p(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
 
 
-AGG_COUNT_SUM_MIN_MAX, AGG_HLL, AGG_FIRST, AGG_MINBY, AGG_MAXBY, AGG_FIRST_MAX = 0, 1, 2, 3, 4, 5
+AGG_COUNT_SUM_MIN_MAX, AGG_HLL, AGG_FIRST, AGG_MINBY, AGG_MAXBY, AGG_FIRST_MAX, AGG_TDIGEST = 0, 1, 2, 3, 4, 5, 6
 
 
 def make_cfg(assigner="tumbling", size=0, slide=0, offset=0, gap=0, lateness=0, purging=False, side_output=False,
-             value_type="i64", hll_p=0, first=False, by=None):
+             value_type="i64", hll_p=0, first=False, by=None, tdigest=0, quantiles=(0.5, 0.95, 0.99)):
     """hll_p > 0 selects the HyperLogLog AggregateFunction with 2^hll_p registers; first=True the
     first-element reduce of sum(pos)/min(pos) (max = arrival ordinal of the window's first element;
-    window_oracle.h)."""
-    agg = (AGG_HLL if hll_p else AGG_FIRST_MAX if first == "max" else AGG_FIRST if first else {"min": AGG_MINBY, "max": AGG_MAXBY}[by] if by
-           else AGG_COUNT_SUM_MIN_MAX)
+    window_oracle.h); tdigest = delta > 0 the t-digest of an f64 value column with rows carrying
+    `quantiles`."""
+    agg = (AGG_HLL if hll_p else AGG_TDIGEST if tdigest else AGG_FIRST_MAX if first == "max" else AGG_FIRST if first
+           else {"min": AGG_MINBY, "max": AGG_MAXBY}[by] if by else AGG_COUNT_SUM_MIN_MAX)
+    if tdigest:
+        value_type = "f64"
     return OracleCfg(_ASSIGNERS[assigner], _VALTYPES[value_type], size, slide, offset, gap, lateness, int(purging),
-                     int(side_output), agg, int(hll_p))
+                     int(side_output), agg, int(hll_p), int(tdigest), 0, (ctypes.c_double * 3)(*quantiles))
 
 
 class OracleError(RuntimeError):
@@ -149,6 +155,14 @@ class WindowOperatorOracle:
 
     def clear_rows(self):
         lib().oracle_clear_rows(self._h)
+
+    def digest(self, row):
+        """t-digest centroids (sum f64[], weight i64[]) of emitted row `row`."""
+        n = lib().oracle_row_digest(self._h, row, None, None, 0)
+        s, w = np.zeros(max(n, 0)), np.zeros(max(n, 0), dtype=np.int64)
+        if n > 0:
+            lib().oracle_row_digest(self._h, row, s.ctypes.data, w.ctypes.data, n)
+        return s, w
 
     def side_rows(self):
         n = lib().oracle_num_side_rows(self._h)

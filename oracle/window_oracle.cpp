@@ -96,7 +96,148 @@ struct Acc {
   std::vector<uint8_t> regs;  // OR_AGG_HLL registers (2^p)
   int64_t first = 0;          // OR_AGG_FIRST: arrival ordinal of the element that created the state
   int64_t by_val = 0, by_ord = 0;  // OR_AGG_MINBY / MAXBY: the selected element's field and ordinal
+  std::vector<double> td_sum;      // OR_AGG_TDIGEST: centroids (sum, weight), in order
+  std::vector<int64_t> td_w;
+  std::vector<int64_t> td_buf;     // values added since the last compression (f64 bits)
 };
+
+// ---------------------------------------------------------------- t-digest (window_oracle.h OR_AGG_TDIGEST)
+// Double.compare order of f64 bits as an unsigned key (canonical NaN largest)
+inline uint64_t td_key(int64_t bits) {
+  if ((bits & 0x7ff0000000000000LL) == 0x7ff0000000000000LL && (bits & 0x000fffffffffffffLL)) bits = 0x7ff8000000000000LL;
+  const int64_t s = bits >= 0 ? bits : (bits ^ 0x7fffffffffffffffLL);
+  return (uint64_t)s ^ 0x8000000000000000ULL;
+}
+// qb[b] = sin(pi b / delta)^2, b = 0 .. delta/2 (the k1 scale function's unit steps)
+std::vector<double> td_bounds(int delta) {
+  const int nb = delta / 2;
+  std::vector<double> q(nb + 1);
+  for (int b = 0; b <= nb; b++) {
+    const double s = std::sin(M_PI * (double)b / (double)delta);
+    q[b] = s * s;
+  }
+  q[0] = 0.0;
+  q[nb] = 1.0;
+  return q;
+}
+// group of an item of weight w whose predecessors weigh c (W = total weight): the bucket of its midpoint,
+// the largest b < nb with W*qb[b] <= c + w/2
+inline int td_slot(const std::vector<double>& q, double W, int64_t c, int64_t w) {
+  const int nb = (int)q.size() - 1;
+  const double mid = (double)c + (double)w * 0.5;
+  int lo = 0, hi = nb - 1;
+  while (lo < hi) {
+    const int m = (lo + hi + 1) >> 1;
+    if (W * q[m] <= mid)
+      lo = m;
+    else
+      hi = m - 1;
+  }
+  return lo;
+}
+// sum of up to 64 values as the perfect binary tree over 64 slots in order (empty slots contribute nothing)
+struct TreeSum {
+  double v;
+  bool any;
+};
+TreeSum td_tree(const double* x, int n, int lo, int width) {
+  if (lo >= n) return TreeSum{0.0, false};
+  if (width == 1) return TreeSum{x[lo], true};
+  const TreeSum a = td_tree(x, n, lo, width / 2), b = td_tree(x, n, lo + width / 2, width / 2);
+  if (!b.any) return a;
+  return TreeSum{a.v + b.v, true};
+}
+// merge the buffered values into the centroids (the compression at the end of a batch)
+void td_compress(Acc& a, const std::vector<double>& q) {
+  if (a.td_buf.empty()) return;
+  std::vector<uint64_t> nv(a.td_buf.size());
+  for (size_t i = 0; i < nv.size(); i++) nv[i] = td_key(a.td_buf[i]);
+  std::sort(nv.begin(), nv.end());
+  a.td_buf.clear();
+  int64_t W = 0;
+  for (int64_t w : a.td_w) W += w;
+  W += (int64_t)nv.size();
+  const double Wd = (double)W;
+  std::vector<double> os;
+  std::vector<int64_t> ow;
+  os.swap(a.td_sum);
+  ow.swap(a.td_w);
+  // one group: its old centroid sums added left to right, its new values in blocks of 64 (each a tree sum),
+  // the block sums added left to right
+  struct Group {
+    double old_sum = 0.0, new_sum = 0.0;
+    bool any_old = false, any_new = false;
+    int64_t w = 0;
+    std::vector<double> blk;
+  } g;
+  auto flush_block = [&]() {
+    if (g.blk.empty()) return;
+    const double t = td_tree(g.blk.data(), (int)g.blk.size(), 0, 64).v;
+    g.new_sum = g.any_new ? g.new_sum + t : t;
+    g.any_new = true;
+    g.blk.clear();
+  };
+  auto emit = [&]() {
+    flush_block();
+    if (g.w == 0) return;
+    a.td_sum.push_back(g.any_old && g.any_new ? g.old_sum + g.new_sum : g.any_old ? g.old_sum : g.new_sum);
+    a.td_w.push_back(g.w);
+    g = Group{};
+  };
+  size_t i = 0, j = 0;
+  int64_t c = 0;
+  int cur = -1;
+  while (i < nv.size() || j < os.size()) {
+    bool take_new = j == os.size();
+    if (!take_new && i < nv.size()) {
+      int64_t mb;
+      const double mean = os[j] / (double)ow[j];
+      memcpy(&mb, &mean, 8);
+      take_new = nv[i] <= td_key(mb);
+    }
+    double x;
+    int64_t w;
+    if (take_new) {
+      const int64_t s = (int64_t)(nv[i++] ^ 0x8000000000000000ULL);
+      x = bitsd(s >= 0 ? s : (s ^ 0x7fffffffffffffffLL));
+      w = 1;
+    } else {
+      x = os[j];
+      w = ow[j++];
+    }
+    const int slot = td_slot(q, Wd, c, w);
+    if (slot != cur) emit();
+    cur = slot;
+    if (take_new) {
+      g.blk.push_back(x);
+      if (g.blk.size() == 64) flush_block();
+    } else {
+      g.old_sum = g.any_old ? g.old_sum + x : x;
+      g.any_old = true;
+    }
+    g.w += w;
+    c += w;
+  }
+  emit();
+}
+// piecewise-linear quantile through (0, min), (centre_i, mean_i), (W, max)
+double td_quantile(const Acc& a, double mn, double mx, double qv) {
+  const size_t n = a.td_sum.size();
+  if (n == 0) return NAN;
+  double W = 0.0;
+  for (int64_t w : a.td_w) W += (double)w;
+  const double x = qv * W;
+  double x0 = 0.0, y0 = mn, before = 0.0;
+  for (size_t i = 0; i < n; i++) {
+    const double t = before + (double)a.td_w[i] * 0.5;
+    const double m = a.td_sum[i] / (double)a.td_w[i];
+    if (t >= x) return y0 + (m - y0) * ((x - x0) / (t - x0));
+    x0 = t;
+    y0 = m;
+    before += (double)a.td_w[i];
+  }
+  return y0 + (mx - y0) * ((x - x0) / (W - x0));
+}
 
 // ---------------------------------------------------------------- HyperLogLog (window_oracle.h)
 inline uint64_t hll_fmix64(uint64_t x) {
@@ -182,9 +323,22 @@ struct OpError {
 
 class WindowOperatorOracle {
  public:
-  explicit WindowOperatorOracle(const oracle_cfg& c) : cfg(c) {}
+  explicit WindowOperatorOracle(const oracle_cfg& c) : cfg(c) {
+    if (cfg.aggregate == OR_AGG_TDIGEST) td_q = td_bounds(cfg.td_delta);
+  }
 
   oracle_cfg cfg;
+  std::vector<double> td_q;                                    // OR_AGG_TDIGEST bucket bounds qb[]
+  std::vector<KW> td_touched;                                  // digests with buffered values
+  std::vector<std::vector<std::pair<double, int64_t>>> row_digest;  // per emitted row: its centroids
+  // end of a processElements batch: the t-digests compress their buffered values
+  void end_batch() {
+    for (const KW& k : td_touched) {
+      auto it = state.find(k);
+      if (it != state.end()) td_compress(it->second, td_q);
+    }
+    td_touched.clear();
+  }
   int64_t wm = LMIN;  // HeapInternalTimerService.currentWatermark initial value
   int64_t epoch = 0;
   int64_t late_dropped = 0;
@@ -219,6 +373,7 @@ class WindowOperatorOracle {
       a.cnt += 1;
       return;
     }
+    if (cfg.aggregate == OR_AGG_TDIGEST) a.td_buf.push_back(v);  // compressed at the end of the batch
     if (cfg.value_type == OR_VAL_F64) {
       double d = bitsd(v);
       if (a.cnt == 0) {
@@ -299,12 +454,26 @@ class WindowOperatorOracle {
     delete_timer(c, key, w);
   }
 
-  void emit(int64_t key, const TW& w, const Acc& a) {
+  void emit(int64_t key, const TW& w, const Acc& a_in) {
+    Acc a = a_in;
     oracle_row r;
     r.key = key;
     r.start = w.start;
     r.end = w.end;
     r.count = a.cnt;
+    row_digest.emplace_back();
+    if (cfg.aggregate == OR_AGG_TDIGEST) {
+      if (!a_in.td_buf.empty()) td_compress(a, td_q);  // getResult within a batch (late firing) sees every value
+      const double q[3] = {td_quantile(a, a.dmn, a.dmx, cfg.td_q[0]), td_quantile(a, a.dmn, a.dmx, cfg.td_q[1]),
+                           td_quantile(a, a.dmn, a.dmx, cfg.td_q[2])};
+      memcpy(&r.sum, &q[0], 8);
+      memcpy(&r.min, &q[1], 8);
+      memcpy(&r.max, &q[2], 8);
+      for (size_t i = 0; i < a.td_sum.size(); i++) row_digest.back().emplace_back(a.td_sum[i], a.td_w[i]);
+      r.epoch = epoch;
+      rows.push_back(r);
+      return;
+    }
     if (cfg.aggregate == OR_AGG_HLL) {
       double est;
       hll_result(a.regs, cfg.hll_p, &est, &r.min, &r.max);
@@ -470,6 +639,7 @@ class WindowOperatorOracle {
         TW sw = it->second;
         Acc& a = state[KW{key, sw}];
         acc_add(a, val);
+        if (cfg.aggregate == OR_AGG_TDIGEST && a.td_buf.size() == 1) td_touched.push_back(KW{key, sw});
         // EventTimeTrigger.onElement
         if (actual.maxTs() <= wm) {
           emit(key, actual, a);
@@ -487,6 +657,7 @@ class WindowOperatorOracle {
         KW kw{key, w};
         Acc& a = state[kw];
         acc_add(a, val);
+        if (cfg.aggregate == OR_AGG_TDIGEST && a.td_buf.size() == 1) td_touched.push_back(kw);
         if (w.maxTs() <= wm) {
           emit(key, w, a);
           if (cfg.purging) state.erase(kw);
@@ -632,8 +803,10 @@ int oracle_process(void* p, const int64_t* key, const int64_t* ts, const int64_t
   try {
     for (int64_t i = 0; i < n; i++) op->process_element(key[i], ts[i], val[i]);
   } catch (const OpError& e) {
+    op->end_batch();
     return e.code;
   }
+  op->end_batch();
   return OR_OK;
 }
 int oracle_watermark(void* p, int64_t wm) {
@@ -649,7 +822,20 @@ void oracle_get_rows(void* p, oracle_row* out) {
   auto* op = static_cast<WindowOperatorOracle*>(p);
   if (!op->rows.empty()) memcpy(out, op->rows.data(), op->rows.size() * sizeof(oracle_row));
 }
-void oracle_clear_rows(void* p) { static_cast<WindowOperatorOracle*>(p)->rows.clear(); }
+void oracle_clear_rows(void* p) {
+  static_cast<WindowOperatorOracle*>(p)->rows.clear();
+  static_cast<WindowOperatorOracle*>(p)->row_digest.clear();
+}
+int64_t oracle_row_digest(void* p, int64_t row, double* sum, int64_t* weight, int64_t cap) {
+  auto* op = static_cast<WindowOperatorOracle*>(p);
+  if (row < 0 || row >= (int64_t)op->row_digest.size()) return -1;
+  const auto& d = op->row_digest[(size_t)row];
+  for (int64_t i = 0; i < (int64_t)d.size() && i < cap; i++) {
+    sum[i] = d[(size_t)i].first;
+    weight[i] = d[(size_t)i].second;
+  }
+  return (int64_t)d.size();
+}
 int64_t oracle_num_side_rows(void* p) { return (int64_t) static_cast<WindowOperatorOracle*>(p)->side.size(); }
 void oracle_get_side_rows(void* p, oracle_side_row* out) {
   auto* op = static_cast<WindowOperatorOracle*>(p);
@@ -707,13 +893,16 @@ int64_t oracle_run_parallel(const oracle_cfg* cfg, const int64_t* key, const int
     for (int c = 0; c < threads; c++) {
       for (int64_t i : routed[c][t]) {
         while (b < n_wms && i >= (b + 1) * batch) {
+          op.end_batch();
           op.process_watermark(wms[b++]);
           total_rows[t] += (int64_t)op.rows.size();  // discarding sink
           op.rows.clear();
+          op.row_digest.clear();
         }
         op.process_element(key[i], ts[i], val[i]);
       }
     }
+    op.end_batch();
     for (; b < n_wms; b++) op.process_watermark(wms[b]);
     total_rows[t] += (int64_t)op.rows.size();
     total_late[t] = op.late_dropped;

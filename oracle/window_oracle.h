@@ -56,6 +56,9 @@ typedef struct {
   int32_t side_output;   /* late records go to the side output instead of numLateRecordsDropped */
   int32_t aggregate;     /* OR_AGG_* */
   int32_t hll_p;         /* HyperLogLog precision p (registers m = 2^p), OR_AGG_HLL only */
+  int32_t td_delta;      /* t-digest compression delta (even), OR_AGG_TDIGEST only */
+  int32_t td_pad;
+  double td_q[3];        /* t-digest quantiles reported in a row's sum / min / max */
 } oracle_cfg;
 
 /* The user AggregateFunctions of SURVEY.md §8d C5.  OR_AGG_HLL is a HyperLogLog distinct count
@@ -72,8 +75,27 @@ typedef struct {
  * fields of sum(pos)/min(pos)); ordinals count every element processed, from 0. */
 /* OR_AGG_MINBY / OR_AGG_MAXBY: minBy(pos) / maxBy(pos) with first = true (ComparableAggregator.java:72-94):
  * min = the selected field value, max = the arrival ordinal of the selected element. */
+/* OR_AGG_TDIGEST: a merging t-digest (Dunning & Ertl, "Computing extremely accurate quantiles using
+ * t-digests", 2019) of an f64 value column, compression delta, scale function k1(q) = delta/(2 pi)
+ * asin(2q - 1), in its bucketed form — defined by this build (Flink 1.5 ships no t-digest; SURVEY §8d C5
+ * names it as a user AggregateFunction):
+ *   qb[b] = sin(pi b / delta)^2 for b = 0 .. nb = delta/2 (qb[0] = 0, qb[nb] = 1): the k1 values -delta/4 + b.
+ *   add(v) buffers v; at the end of every processElements batch (a micro-batch / push) each digest with
+ *   buffered values is compressed: the values, sorted by Double.compare order, and the centroids (sum, w)
+ *   in their order are merged into one sequence (a value goes before a centroid whose mean sum/w is
+ *   equal or larger in Double.compare order), W = total weight, and each item, with c = the weight
+ *   before it, falls into the bucket of its midpoint: the largest b < nb with W*qb[b] <= c + w/2.
+ *   Consecutive items of one bucket form one centroid: weight = sum of weights; sum = S_old + S_new, where
+ *   S_old = its old centroids' sums added left to right and S_new = its new values in blocks of 64 (from
+ *   its first new value on), each block summed as the perfect binary tree over its 64 slots in order (an
+ *   empty slot contributes nothing), the block sums added left to right (only S_old or only S_new when
+ *   the group has only old or only new items).  At most delta/2 centroids.
+ *   getResult: count = W; sum / min / max = quantile(td_q[0..2]) as f64 bits, where quantile(q) is the
+ *   piecewise-linear interpolation at x = q*W through (0, min), (cum_{i-1} + w_i/2, mean_i) ..., (W, max).
+ * The arithmetic is IEEE-754 double without fused multiply-add, so the GPU's digests are bit-exact. */
 enum { OR_AGG_COUNT_SUM_MIN_MAX = 0, OR_AGG_HLL = 1, OR_AGG_FIRST = 2, OR_AGG_MINBY = 3, OR_AGG_MAXBY = 4,
-       OR_AGG_FIRST_MAX = 5 /* max(pos): as OR_AGG_FIRST with min = the field's maximum */ };
+       OR_AGG_FIRST_MAX = 5 /* max(pos): as OR_AGG_FIRST with min = the field's maximum */,
+       OR_AGG_TDIGEST = 6 };
 
 /* One fired row.  sum/min/max hold i64 values (I64/I32) or f64 bit patterns (F64).
  * epoch = number of watermarks fully processed before the row was emitted, so
@@ -106,6 +128,9 @@ void    oracle_count_process(void* op, const int64_t* key, const int64_t* val, i
 int64_t oracle_count_num_rows(void* op);
 void    oracle_count_get_rows(void* op, oracle_row* out);
 void    oracle_get_rows(void* op, oracle_row* out);       /* copies all rows emitted so far */
+/* OR_AGG_TDIGEST: centroids (sum, weight) of row `row` (index into the rows emitted so far); returns
+ * their number (copies at most cap) */
+int64_t oracle_row_digest(void* op, int64_t row, double* sum, int64_t* weight, int64_t cap);
 void    oracle_clear_rows(void* op);
 int64_t oracle_num_side_rows(void* op);
 void    oracle_get_side_rows(void* op, oracle_side_row* out);

@@ -1,0 +1,163 @@
+"""GPU t-digest (FW_AGG_TDIGEST, BASELINE configs[4] / SURVEY §8d C5) against the oracle's restatement
+(oracle/window_oracle.h OR_AGG_TDIGEST, itself pinned by tests/test_oracle_tdigest.py).
+
+The bar is bit-exact: every fired row's centroids (sum bits and weights, via TDigest(export=True)) and its
+three quantile estimates equal the oracle's, for digests merged serially and for the hot ones merged
+bucket-parallel (more than FW_TD_SMALL = 2048 values + centroids in one push).  At the full C5 batch size
+(2^24 records per push, generated in HBM) the checks are size-independent: every record is counted once and
+the quantiles of the hottest keys lie within 1% in rank of the exact ones.
+"""
+import numpy as np
+import pytest
+
+from flink_amd import TDigest, TumblingEventTimeWindows
+from flink_amd.datagen import generate_host
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _stream(n, batch, num_keys, rate, zipf=None, values="spread", seed=0x7D16, bound=200, jitter=200):
+    keys, ts, raw = generate_host(seed, 0, n, num_keys, ts_base=1_000_000, rate=rate, jitter=jitter, zipf_s=zipf)
+    if values == "spread":
+        vals = (raw & 0xFFFFFF).astype(np.float64) / 7.0 - 1.0e6  # distinct-ish, negative and positive
+    else:
+        vals = (raw & 0x3F).astype(np.float64) * 0.5  # 64 distinct values: ties with each other and with means
+    batches, wms, mx = [], [], -(1 << 63)
+    for b in range(0, n, batch):
+        sl = slice(b, min(n, b + batch))
+        batches.append((keys[sl], ts[sl], vals[sl]))
+        mx = max(mx, int(ts[sl].max()))
+        wms.append(mx - bound)
+    batches.append((keys[:0], ts[:0], vals[:0]))
+    wms.append((1 << 63) - 1)
+    return batches, wms
+
+
+def _run(batches, wms, delta, quantiles=(0.5, 0.95, 0.99), **kw):
+    from flink_amd.operator import GpuWindowOperator
+    gpu = GpuWindowOperator(TumblingEventTimeWindows.of(1000), TDigest(delta, quantiles, export=True), **kw)
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000, tdigest=delta, quantiles=quantiles)
+    g_rows, g_dig = [], []
+    for epoch, ((k, t, v), wm) in enumerate(zip(batches, wms)):
+        if len(k):
+            gpu.process(k, t, v)
+            ref.process(k, t, v)
+        gpu.advance_watermark(wm)
+        g_dig += gpu.drain_digests()
+        g_rows.append(gpu.drain_rows(epoch))
+        ref.watermark(wm)
+    assert gpu.late_dropped == ref.late_dropped
+    gpu.close()
+    r_rows = ref.rows()
+    r_dig = [ref.digest(i) for i in range(len(r_rows))]
+    return np.concatenate(g_rows), g_dig, r_rows, r_dig
+
+
+def _assert_same(g_rows, g_dig, r_rows, r_dig, delta):
+    assert len(g_rows) == len(r_rows) > 0
+    go = np.lexsort((g_rows["start"], g_rows["key"], g_rows["epoch"]))
+    ro = np.lexsort((r_rows["start"], r_rows["key"], r_rows["epoch"]))
+    for f in ("epoch", "key", "start", "end", "count", "sum", "min", "max"):  # quantiles as f64 bits
+        bad = np.nonzero(g_rows[f][go] != r_rows[f][ro])[0]
+        assert bad.size == 0, f"{f} differs at {bad[:5]}: {g_rows[go][bad[:3]]} vs {r_rows[ro][bad[:3]]}"
+    for a, b in zip(go, ro):
+        gs, gw = g_dig[a]
+        rs, rw = r_dig[b]
+        assert len(gs) == len(rs) <= delta // 2
+        assert np.array_equal(gw, rw), (gw, rw)
+        assert np.array_equal(gs.view(np.int64), rs.view(np.int64)), (gs, rs)
+        assert int(gw.sum()) == g_rows["count"][a]
+
+
+@pytest.mark.parametrize("delta", [100, 20])
+def test_gpu_tdigest_serial_digests(delta):
+    # uniform keys: every digest gets a few values per push (the serial merge)
+    batches, wms = _stream(300_000, 60_000, 20_000, rate=200_000)
+    out = _run(batches, wms, delta, expected_entries=60_000)
+    _assert_same(*out, delta)
+
+
+@pytest.mark.parametrize("delta,values", [(100, "spread"), (100, "ties"), (30, "spread")])
+def test_gpu_tdigest_hot_digests(delta, values):
+    # Zipf(1.1) over 1000 keys in 200K-record pushes: the hottest digests take tens of thousands of values per
+    # push and are merged bucket-parallel; "ties" draws 64 distinct values, so values tie with each other and
+    # with centroid means (a value goes before an equal mean)
+    batches, wms = _stream(800_000, 200_000, 1000, rate=100_000, zipf=1.1, values=values)
+    out = _run(batches, wms, delta, expected_entries=4000)
+    _assert_same(*out, delta)
+    assert max(len(s) for s, _ in out[1]) > delta // 4  # hot digests fill their buckets
+
+
+def test_gpu_tdigest_blocks_are_recycled():
+    # many short windows over few keys with a pool sized for one window's digests: fired blocks are reused
+    batches, wms = _stream(400_000, 10_000, 500, rate=100_000, bound=50, jitter=50)
+    from flink_amd.operator import GpuWindowOperator
+    gpu = GpuWindowOperator(TumblingEventTimeWindows.of(100), TDigest(40, (0.1, 0.5, 0.9)), expected_entries=1500)
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=100, tdigest=40, quantiles=(0.1, 0.5, 0.9))
+    for (k, t, v), wm in zip(batches, wms):
+        if len(k):
+            gpu.process(k, t, v)
+            ref.process(k, t, v)
+        gpu.watermark(wm)
+        ref.watermark(wm)
+    g, r = gpu.rows(), ref.rows()
+    gpu.close()
+    assert len(g) == len(r) > 1000
+    go = np.lexsort((g["start"], g["key"], g["epoch"]))
+    ro = np.lexsort((r["start"], r["key"], r["epoch"]))
+    for f in ("key", "start", "count", "sum", "min", "max"):
+        assert np.array_equal(g[f][go], r[f][ro]), f
+
+
+def test_gpu_tdigest_refuses_unsupported_shapes():
+    from flink_amd import SlidingEventTimeWindows
+    from flink_amd import _native as N
+    from flink_amd.operator import GpuWindowOperator
+    for kw in (dict(assigner=SlidingEventTimeWindows.of(3000, 1000)), dict(allowed_lateness=10)):
+        with pytest.raises(N.NativeError) as e:
+            GpuWindowOperator(kw.pop("assigner", TumblingEventTimeWindows.of(1000)), TDigest(100), **kw)
+        assert e.value.code == N.FW_ERR_UNSUPPORTED
+    with pytest.raises(N.NativeError) as e:
+        GpuWindowOperator(TumblingEventTimeWindows.of(1000), TDigest(99))
+    assert e.value.code == N.FW_ERR_ARG
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(1000), TDigest(100))
+    with pytest.raises(N.NativeError) as e:
+        op.snapshot_key_group(0)
+    assert e.value.code == N.FW_ERR_UNSUPPORTED
+    op.close()
+
+
+def test_gpu_tdigest_full_size():
+    # SURVEY §8d C5 shape: 2^24 records per push generated in HBM (Zipf(1.1) over 1M keys, 1e8 records per
+    # event-second, values = the generator's int32 column as doubles), 3 pushes, then the final watermark
+    import torch
+    from flink_amd.datagen import generate_device, generate_host, zipf_cdf
+    from flink_amd.operator import GpuWindowOperator
+    n, steps, keys = 1 << 24, 3, 1_000_000
+    cdf = torch.tensor(zipf_cdf(keys, 1.1), dtype=torch.float64, device="cuda")
+    gpu = GpuWindowOperator(TumblingEventTimeWindows.of(1000), TDigest(100, (0.5, 0.9, 0.99)),
+                            expected_entries=2_000_000)
+    for s in range(steps):
+        k, t, v, mx = generate_device(0x5EED, s * n, n, keys, ts_base=1_000_000, rate=100_000_000, jitter=200,
+                                      cdf_dev=cdf)
+        gpu.process_batch(k, t, v.to(torch.float64))
+        gpu.watermark(int(mx.item()) - 200)
+    gpu.watermark((1 << 63) - 1)
+    rows = gpu.rows()
+    assert gpu.late_dropped == 0
+    gpu.close()
+    assert int(rows["count"].sum()) == n * steps
+    q = {f: rows[f].view(np.float64) for f in ("sum", "min", "max")}
+    assert np.all(q["sum"] <= q["min"]) and np.all(q["min"] <= q["max"])
+    # exact quantiles of the three hottest (key, window) rows from the same stream generated on the host
+    hk, ht, hv = generate_host(0x5EED, 0, n * steps, keys, ts_base=1_000_000, rate=100_000_000, jitter=200,
+                               zipf_s=1.1)
+    hv = hv.astype(np.float64)
+    for i in np.argsort(-rows["count"])[:3]:
+        r = rows[i]
+        sel = np.sort(hv[(hk == r["key"]) & (ht >= r["start"]) & (ht < r["end"])])
+        assert len(sel) == r["count"]
+        for f, qv in (("sum", 0.5), ("min", 0.9), ("max", 0.99)):
+            rank = np.searchsorted(sel, q[f][i]) / len(sel)
+            assert abs(rank - qv) < 0.01, (r["key"], qv, rank)

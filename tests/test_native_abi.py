@@ -62,7 +62,7 @@ def test_create_rejects_invalid_config(kw, msg):
 
 def test_kernel_names():
     names = [N.lib().fw_kernel_name(i).decode() for i in range(N.FW_NUM_KERNELS)]
-    assert names == ["k_classify_hist", "k_scan", "k_scatter", "k_aggregate", "k_slow", "k_fire"]
+    assert names == ["k_classify_hist", "k_scan", "k_scatter", "k_aggregate", "k_slow", "k_fire", "k_tdigest"]
 
 
 def test_route_scratch_size_positive():
@@ -85,4 +85,4 @@ def test_struct_layouts_match_header(tmp_path):
     assert ctypes.sizeof(N.FwConfig) == out[0]
     assert [getattr(N.FwConfig, f).offset for f in fields] == out[1:]
     assert ctypes.sizeof(N.FwRows) == 56
-    assert ctypes.sizeof(N.FwStats) == 12 * 8
+    assert ctypes.sizeof(N.FwStats) == 13 * 8

@@ -39,6 +39,7 @@ def load(pmc_dir, last=0):
     # `last`: average only each kernel's last dispatches (the bench's timed steps follow its warmup)
     cut = (lambda v: v[-last:]) if last else (lambda v: v)
     return {k: {c: sum(cut(v)) / len(cut(v)) for c, v in cs.items()} | {"_dispatches": max(len(cut(v)) for v in cs.values())}
+            | {"_total_dispatches": max(len(v) for v in cs.values())} | {"_sum_" + c: sum(v) for c, v in cs.items()}
             for k, cs in vals.items()}
 
 
@@ -68,8 +69,14 @@ def main():
         r = res[name]
         if r["read_bytes"] is not None and r["write_bytes"] is not None:
             r["hbm_bytes"] = r["read_bytes"] + r["write_bytes"]
-    # bench.py's timing buckets: the HLL register update is timed with k_aggregate, the pane fire is k_fire
+    # bench.py's timing buckets: the HLL register update is timed with k_aggregate, the pane fire is k_fire,
+    # the t-digest compression (k_td_* and its rocPRIM radix sorts) is k_tdigest
     per_launch = {n: r.get("hbm_bytes") for n, r in res.items()}
+    td_parts = tuple(n for n in res if n.startswith("k_td_") or n.startswith("rocprim"))
+    if "k_td_keys" in k:  # several dispatches per push (the radix sorts' passes): bytes per push over all pushes
+        pushes = k["k_td_keys"]["_total_dispatches"]
+        per_launch["k_tdigest"] = sum(k[x].get("_sum_FETCH_SIZE", 0) * 2048 + k[x].get("_sum_WRITE_SIZE", 0) * 1024
+                                      for x in td_parts) / pushes
     for bucket, parts in (("k_aggregate", ("k_aggregate", "k_hll_update")), ("k_fire", ("k_fire", "k_fire_panes"))):
         vals = [per_launch[x] for x in parts if per_launch.get(x) is not None]
         if vals:
