@@ -273,27 +273,28 @@ __device__ __forceinline__ uint32_t ld_state(const uint32_t* p) {
 __host__ __device__ __forceinline__ bool agg_ordinal(const DevCfg& c) {
   return c.agg >= FW_AGG_FIRST && c.agg <= FW_AGG_FIRST_MAX;
 }
-// MINBY / MAXBY: the (field, ordinal) pair as one 64-bit key whose minimum is the selected element
-// (MAXBY flips the i32 field with ~, which reverses its order exactly)
-__device__ __forceinline__ int64_t by_key(int agg, int64_t v, int64_t ord) {
-  const int32_t f = agg == FW_AGG_MAXBY ? ~(int32_t)v : (int32_t)v;
-  return (int64_t)(((uint64_t)(int64_t)f << 32) | (uint32_t)ord);
+// MINBY / MAXBY (ComparableAggregator.java:72-94 with first = true): the entry's mn holds the selected
+// element's field as a key whose minimum it is (Double.compare order for f64, ~ for maxBy) and mx its full
+// arrival ordinal; a pair (key, ordinal) replaces it when it is lexicographically smaller (a strictly
+// smaller field, or an equal field of an earlier element)
+__device__ __forceinline__ int64_t by_key(int agg, int vtype, int64_t v) {
+  const int64_t k = vtype == FW_VAL_F64 ? f64_sortable(v) : v;
+  return agg == FW_AGG_MAXBY ? ~k : k;
 }
-// MINBY / MAXBY row: the selected field, and its full ordinal from the first element's (~mx) and
-// the low 32 ordinal bits kept in the key
-__device__ __forceinline__ void by_row(int agg, const Entry& e, int64_t* field, int64_t* ord) {
-  const int32_t f = (int32_t)(e.mn >> 32);
-  *field = agg == FW_AGG_MAXBY ? (int64_t)~f : (int64_t)f;
-  const int64_t first = ~e.mx;
-  *ord = first + (int64_t)(uint32_t)((uint32_t)e.mn - (uint32_t)first);
+__device__ __forceinline__ bool by_less(int64_t k, int64_t o, int64_t k2, int64_t o2) {
+  return k < k2 || (k == k2 && o < o2);
+}
+// MINBY / MAXBY row: the selected field and the selected element's ordinal
+__device__ __forceinline__ void by_row(int agg, int vtype, const Entry& e, int64_t* field, int64_t* ord) {
+  const int64_t k = agg == FW_AGG_MAXBY ? ~e.mn : e.mn;
+  *field = vtype == FW_VAL_F64 ? f64_unsortable(k) : k;
+  *ord = e.mx;
 }
 __device__ __forceinline__ bool agg_first(int agg) { return agg == FW_AGG_FIRST || agg == FW_AGG_FIRST_MAX; }
 __device__ __forceinline__ bool agg_by(int agg) { return agg == FW_AGG_MINBY || agg == FW_AGG_MAXBY; }
 // the value the entry's mn lane takes for one record (sv: the field, f64 in sortable form): FIRST_MAX keeps
-// ~field so the min is the max; MINBY / MAXBY the (field, ordinal) key
-__device__ __forceinline__ int64_t mn_in(int agg, int64_t sv, int64_t v, int64_t fo) {
-  return agg_by(agg) ? by_key(agg, v, fo) : agg == FW_AGG_FIRST_MAX ? ~sv : sv;
-}
+// ~field so the min is the max (MINBY / MAXBY update mn and mx together: by_less)
+__device__ __forceinline__ int64_t mn_in(int agg, int64_t sv) { return agg == FW_AGG_FIRST_MAX ? ~sv : sv; }
 // row / snapshot columns of an entry's mn and mx (MINBY / MAXBY: by_row)
 __device__ __forceinline__ int64_t mn_out(const DevCfg& c, int64_t mn) {
   const int64_t s = c.agg == FW_AGG_FIRST_MAX ? ~mn : mn;
@@ -310,7 +311,7 @@ __device__ __forceinline__ void write_row(const DevCfg& c, const DevRows& out, u
   out.sum[pos] = c.vtype == FW_VAL_I32 ? (int64_t)(int32_t)e.sum : e.sum;
   out.mn[pos] = mn_out(c, e.mn);
   out.mx[pos] = mx_out(c, e.mx);
-  if (agg_by(c.agg)) by_row(c.agg, e, &out.mn[pos], &out.mx[pos]);
+  if (agg_by(c.agg)) by_row(c.agg, c.vtype, e, &out.mn[pos], &out.mx[pos]);
 }
 // single-lane emission (ordered path)
 __device__ __forceinline__ void emit_one(const DevCfg& c, const DevRows& out, Status* st, const Entry& e) {
@@ -334,6 +335,13 @@ __device__ __forceinline__ void side_one(const DevSide& sd, Status* st, int64_t 
 // accumulate one value (AggregateFunction.add of the built-in count/sum/min/max)
 // (FW_AGG_FIRST: mx takes ~ordinal `fo` of the record, so the max keeps the first element's ordinal)
 __device__ __forceinline__ void acc_add(const DevCfg& c, Entry& e, int64_t v, int64_t fo) {
+  if (agg_by(c.agg)) {
+    const int64_t k = by_key(c.agg, c.vtype, v);
+    if (e.cnt == 0 || by_less(k, fo, e.mn, e.mx)) {
+      e.mn = k;
+      e.mx = fo;
+    }
+  }
   e.cnt += 1;
   int64_t sv = v;
   if (c.vtype == FW_VAL_F64) {
@@ -343,7 +351,8 @@ __device__ __forceinline__ void acc_add(const DevCfg& c, Entry& e, int64_t v, in
   } else {
     e.sum = jadd(e.sum, v);
   }
-  const int64_t nv = mn_in(c.agg, sv, v, fo);
+  if (agg_by(c.agg)) return;
+  const int64_t nv = mn_in(c.agg, sv);
   e.mn = nv < e.mn ? nv : e.mn;
   const int64_t xv = agg_ordinal(c) ? ~fo : sv;
   e.mx = xv > e.mx ? xv : e.mx;
@@ -351,6 +360,16 @@ __device__ __forceinline__ void acc_add(const DevCfg& c, Entry& e, int64_t v, in
 // AggregateFunction.merge
 __device__ __forceinline__ void acc_merge(const DevCfg& c, Entry& a, const Entry& b) {
   if (b.cnt == 0) return;
+  if (agg_by(c.agg)) {  // the lexicographically smaller (key, ordinal) of the two
+    if (a.cnt == 0 || by_less(b.mn, b.mx, a.mn, a.mx)) {
+      a.mn = b.mn;
+      a.mx = b.mx;
+    }
+    a.cnt += b.cnt;
+    a.sum = c.vtype == FW_VAL_F64 ? __double_as_longlong(__longlong_as_double(a.sum) + __longlong_as_double(b.sum))
+                                  : jadd(a.sum, b.sum);
+    return;
+  }
   a.cnt += b.cnt;
   if (c.vtype == FW_VAL_F64)
     a.sum = __double_as_longlong(__longlong_as_double(a.sum) + __longlong_as_double(b.sum));
@@ -721,8 +740,9 @@ __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(D
         if (norm) reinterpret_cast<i64x2*>(part)[pos] = i64x2{compact_encode(c, k[j], compact_delta(c, last)), v[j]};
         continue;
       }
-      // FW_AGG_FIRST: the record's arrival ordinal rides above the window count (nwin < 2^16)
-      const int64_t nwf = agg_ordinal(c) ? ((c.ord_base + i) << 16) | nwin : (int64_t)nwin;
+      // ordinal aggregates: the record's index in the batch rides above the window count (nwin < 2^16); the
+      // aggregate adds the batch's ordinal base (DevCfg::ord_base), so ordinals are exact to 2^63
+      const int64_t nwf = agg_ordinal(c) ? (i << 16) | nwin : (int64_t)nwin;
       store_pair(part, norm, pos, i64x2{k[j], last}, i64x2{v[j], (long long)nwf});
     }
   }
@@ -805,6 +825,8 @@ struct AggLds {
   int64_t min_timer;
   int hl_lo, hl_take, hl_idx;  // block pool: this flush's accumulator blocks (free-stack slice, then pool tail)
   long long hl_bump;
+  const int64_t* byv;          // MINBY / MAXBY: the batch's value column (DevCfg::by_val)
+  int64_t byb;                 // MINBY / MAXBY: the batch's ordinal base
 };
 enum : uint32_t { LT_EMPTY = 0, LT_BUSY = 1 };
 
@@ -825,16 +847,38 @@ __device__ __forceinline__ uint32_t lds_fp(uint32_t h) { return (h >> 8) | 2u; }
 
 // accumulate one value into LDS slot `target` with no-return LDS atomics (nothing waits on the LDS)
 // (first = FW_AGG_FIRST: the max lane takes ~fo, fo = the record's arrival ordinal)
+// MINBY / MAXBY in LDS: the slot's mx holds the batch index of the element it selects (-1: none yet), whose
+// field is read back from the batch's value column (DevCfg::by_val, copied per push); an element replaces it
+// with one 64-bit CAS when (its key, its index) is lexicographically smaller (lock-free: a failed CAS
+// re-reads the winner and compares again).  The flush turns the index into (key, full ordinal).
+__device__ __forceinline__ void lds_by(AggLds& L, int target, int agg, int vtype, int64_t key, int64_t idx) {
+  int64_t cur = __hip_atomic_load(&L.mx[target], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (true) {
+    if (cur >= 0 && !by_less(key, idx, by_key(agg, vtype, L.byv[cur]), cur)) return;
+    const int64_t prev = atomicCAS((unsigned long long*)&L.mx[target], (unsigned long long)cur, (unsigned long long)idx);
+    if (prev == cur) return;
+    cur = prev;
+  }
+}
 __device__ __forceinline__ void lds_acc(AggLds& L, int target, int vtype, int64_t v, int64_t fo, int first) {
+  if (agg_by(first)) {
+    atomicAdd(&L.cnt[target], 1u);
+    lds_by(L, target, first, vtype, by_key(first, vtype, v), fo - L.byb);
+    if (vtype == FW_VAL_F64)
+      atomicAdd((double*)&L.sum[target], __longlong_as_double(v));
+    else
+      atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)v);
+    return;
+  }
   atomicAdd(&L.cnt[target], 1u);
   if (vtype == FW_VAL_F64) {
     atomicAdd((double*)&L.sum[target], __longlong_as_double(v));
     const int64_t sv = f64_sortable(v);
-    atomicMin((long long*)&L.mn[target], (long long)(first ? mn_in(first, sv, v, fo) : sv));
+    atomicMin((long long*)&L.mn[target], (long long)(first ? mn_in(first, sv) : sv));
     atomicMax((long long*)&L.mx[target], (long long)(first ? ~fo : sv));
   } else {
     atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)v);
-    atomicMin((long long*)&L.mn[target], (long long)(first ? mn_in(first, v, v, fo) : v));
+    atomicMin((long long*)&L.mn[target], (long long)(first ? mn_in(first, v) : v));
     atomicMax((long long*)&L.mx[target], (long long)(first ? ~fo : v));
   }
 }
@@ -849,7 +893,16 @@ __device__ __forceinline__ bool lds_reserve(AggLds& L) {
 }
 
 // merge a delta (an accumulator in Entry form) into LDS slot `target` (AggregateFunction.merge)
-__device__ __forceinline__ void lds_acc_delta(AggLds& L, int target, int vtype, const Entry& d) {
+__device__ __forceinline__ void lds_acc_delta(AggLds& L, int target, int vtype, const Entry& d, int agg) {
+  if (agg_by(agg)) {  // a chunk's delta of the same batch: (key, full ordinal)
+    atomicAdd(&L.cnt[target], (uint32_t)d.cnt);
+    lds_by(L, target, agg, vtype, d.mn, d.mx - L.byb);
+    if (vtype == FW_VAL_F64)
+      atomicAdd((double*)&L.sum[target], __longlong_as_double(d.sum));
+    else
+      atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)d.sum);
+    return;
+  }
   atomicAdd(&L.cnt[target], (uint32_t)d.cnt);
   if (vtype == FW_VAL_F64)
     atomicAdd((double*)&L.sum[target], __longlong_as_double(d.sum));
@@ -988,6 +1041,10 @@ __device__ __forceinline__ Entry lds_delta(const DevCfg& c, const AggLds& L, int
   d.sum = L.sum[h];
   d.mn = L.mn[h];
   d.mx = L.mx[h];
+  if (agg_by(c.agg)) {  // the selected element: its key and full ordinal
+    d.mn = by_key(c.agg, c.vtype, L.byv[d.mx]);
+    d.mx += L.byb;
+  }
   // a new pane belongs to the windows that end after the watermark, from its first window on
   d.meta = c.panes ? max(jsub(d.end, 1), c.nt_floor) : (int64_t)FW_TIMER;  // (+ HLL block: agg_flush)
   return d;
@@ -1426,6 +1483,10 @@ __device__ __forceinline__ bool agg_flush_session(const DevCfg& c, AggLds& L, co
       d.sum = L.sum[j];
       d.mn = L.mn[j];
       d.mx = L.mx[j];
+      if (agg_by(c.agg)) {  // the selected element: its key and full ordinal
+        d.mn = by_key(c.agg, c.vtype, L.byv[d.mx]);
+        d.mx += L.byb;
+      }
       d.meta = FW_TIMER;
       int64_t tm;
       nnew += session_add(c, r, d, &tm, st);
@@ -1537,7 +1598,7 @@ __device__ __forceinline__ void unpack_prec(const DevCfg& c, bool cmp, int32_t p
   t = a.y;
   v = b.x;
   nw = FIRST ? (int)(b.y & 0xffff) : (int)b.y;
-  o = FIRST ? (int64_t)b.y >> 16 : 0;
+  o = FIRST ? c.ord_base + (int64_t)((uint64_t)b.y >> 16) : 0;
 }
 
 template <int RPT, bool SESS, bool FIRST>
@@ -1552,6 +1613,8 @@ __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __
     L.fill = 0;
     L.anyfail = 0;
     L.spill = 0;
+    L.byv = c.by_val;
+    L.byb = c.ord_base;
     L.last = 0;
   }
   __syncthreads();
@@ -1618,6 +1681,8 @@ __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __
   if (threadIdx.x == 0) {
     L.anyfail = 0;
     L.nnew = 0;
+    L.byv = c.by_val;
+    L.byb = c.ord_base;
     L.live = tb.live[p];
     L.flushed = 0;
     L.min_timer = LMAX;
@@ -1650,7 +1715,7 @@ __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __
             failed = true;
             rj = q;
           } else {
-            lds_acc_delta(L, tg, c.vtype, d[q]);
+            lds_acc_delta(L, tg, c.vtype, d[q], c.agg);
           }
         }
         if (failed)
@@ -1739,6 +1804,8 @@ __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? FW_SESS_WAVES : FW_AGG_WAVES
     L.fill = 0;
     L.anyfail = 0;
     L.nnew = 0;
+    L.byv = c.by_val;
+    L.byb = c.ord_base;
     L.live = tb.live[p];
     L.flushed = 0;
     L.min_timer = LMAX;
@@ -3367,6 +3434,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_snapshot(DevCfg c, DevTable
       out.sum[o] = c.vtype == FW_VAL_I32 ? (int64_t)(int32_t)e.sum : e.sum;
       out.mn[o] = mn_out(c, e.mn);
       out.mx[o] = mx_out(c, e.mx);
+      if (agg_by(c.agg)) by_row(c.agg, c.vtype, e, &out.mn[o], &out.mx[o]);
       // a pane's timer: the maxTimestamp of its next window to form
       out.timer[o] = c.panes ? max(e.meta, tb.pane_floor[p]) : (e.meta & FW_TIMER) ? 1 : 0;
     }
@@ -3394,9 +3462,10 @@ __global__ void k_restore_count(DevCfg c, int32_t kg, StateCols in, int64_t n, i
 }
 
 // insert (or merge) restored rows; the table has room for all of them (k_restore_count + growth)
-__global__ void k_restore(DevCfg c, int32_t kg, StateCols in, int64_t n, DevTable tb, Status* st) {
+__global__ void k_restore(DevCfg c, int32_t kg, StateCols in, int64_t n, DevTable tb, Status* st,
+                          const int32_t* round_of, int32_t round) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || (round_of && round_of[i] != round)) return;
   const int32_t p = restore_partition(c, kg, in.key[i]);
   if (p < 0) return;
   Entry d;
@@ -3408,11 +3477,15 @@ __global__ void k_restore(DevCfg c, int32_t kg, StateCols in, int64_t n, DevTabl
   d.mn = c.vtype == FW_VAL_F64 ? f64_sortable(in.mn[i]) : in.mn[i];
   if (c.agg == FW_AGG_FIRST_MAX) d.mn = ~d.mn;
   d.mx = agg_first(c.agg) ? ~in.mx[i] : c.vtype == FW_VAL_F64 ? f64_sortable(in.mx[i]) : in.mx[i];
+  if (agg_by(c.agg)) {  // (the selected field, its ordinal)
+    d.mn = by_key(c.agg, c.vtype, in.mn[i]);
+    d.mx = in.mx[i];
+  }
   d.meta = c.panes ? in.timer[i] : in.timer[i] ? FW_TIMER : 0;
   const Region r = region_of(c, tb, p, tb.cur[p]);
   const uint64_t h = slot_hash(c, d.key, c.assigner == FW_SESSION ? 0 : d.start);
   const int32_t found = region_find(r, h, d.key, d.start, d.end);
-  if (found >= 0) {  // the same window restored twice: AggregateFunction.merge
+  if (found >= 0) {  // the window is already there (restored earlier, or an earlier round): AggregateFunction.merge
     Entry& x = r.ent[found];
     Entry cur = x;
     acc_merge(c, cur, d);
@@ -3722,13 +3795,17 @@ void launch_snapshot(const DevCfg& c, DevTable tb, int32_t p0, int32_t np, State
   hipLaunchKernelGGL(k_snapshot, dim3(np), dim3(FW_FIRE_THREADS), 0, s, c, tb, p0, out, count);
 }
 void launch_restore(const DevCfg& c, int32_t kg, StateCols in, int64_t n, int32_t* demand, DevTable tb, Status* st,
-                    hipStream_t s) {
+                    const int32_t* round_of, int32_t rounds, hipStream_t s) {
   const unsigned blocks = (unsigned)((n + 255) / 256);
   if (!blocks) return;
-  if (demand)
+  if (demand) {
     hipLaunchKernelGGL(k_restore_count, dim3(blocks), dim3(256), 0, s, c, kg, in, n, demand, st);
-  else
-    hipLaunchKernelGGL(k_restore, dim3(blocks), dim3(256), 0, s, c, kg, in, n, tb, st);
+    return;
+  }
+  // rows restoring the same (key, window) twice go in different rounds, so each round inserts a window at
+  // most once and later rounds merge into it (one launch per round, stream-ordered)
+  for (int32_t r = 0; r < std::max(1, rounds); r++)
+    hipLaunchKernelGGL(k_restore, dim3(blocks), dim3(256), 0, s, c, kg, in, n, tb, st, round_of, r);
 }
 
 void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t s) {

@@ -84,6 +84,7 @@ struct DevCfg {
   // entry's mx holds ~ordinal of the window's first element, so the max merges everywhere keep it.
   int64_t ord_base;
   int64_t* slow_ord;  // [max_batch] ordinal of each ordered-path record (the push's scratch set)
+  const int64_t* by_val;  // FW_AGG_MINBY / MAXBY: the batch's value column by batch index (the push's scratch set)
   uint8_t* pool;
   uint32_t* pool_free;
   int32_t* pool_ctr;
@@ -306,8 +307,9 @@ void launch_reset_regions(const DevCfg& c, DevTable tb, hipStream_t_ s);
 void launch_snapshot(const DevCfg& c, DevTable tb, int32_t p0, int32_t np, StateCols out, unsigned long long* count,
                      hipStream_t_ s);
 // demand != NULL: count rows per partition (and key-group errors); NULL: insert the rows
+// (insertion: round_of[i] = the row's round, rows with the same (key, window) in different rounds; NULL = one)
 void launch_restore(const DevCfg& c, int32_t kg, StateCols in, int64_t n, int32_t* demand, DevTable tb, Status* st,
-                    hipStream_t_ s);
+                    const int32_t* round_of, int32_t rounds, hipStream_t_ s);
 void launch_key_groups(const int64_t* key, const int32_t* kh, int32_t key_kind, int64_t n, int32_t max_par,
                        int32_t* kg, hipStream_t_ s);
 void launch_route(const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int32_t key_kind,

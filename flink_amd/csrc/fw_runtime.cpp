@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/flink_window.h"
@@ -39,12 +40,14 @@ struct Scratch {
   int64_t *sk = nullptr, *stt = nullptr, *sv = nullptr;  // ordered-path list
   int32_t* skh = nullptr;
   int64_t* so = nullptr;         // FW_AGG_FIRST: arrival ordinal of each ordered-path record
+  int64_t* byv = nullptr;        // FW_AGG_MINBY / MAXBY: the batch's value column (DevCfg::by_val)
   int32_t T = 0;                 // tiles of the batch that used this set
   int64_t n = 0;                 // records of the batch
   bool split = false;            // its aggregate split long partitions (fw_op::hot)
   int64_t wm = INT64_MIN;        // watermark the batch was classified against
   int32_t compact = 0;           // DevCfg::compact / cbase of the batch (a resumed aggregate reads the same form)
   int64_t cbase = 0;
+  int64_t ord_base = 0;          // arrival ordinal of the batch's first record (ordinal aggregates)
 };
 
 }  // namespace
@@ -178,6 +181,7 @@ int alloc_scratch(fw_op* op, Scratch& s, int64_t mb, int64_t m) {
   HIP_OR_RETURN(op, dmalloc(&s.sv, mb));
   HIP_OR_RETURN(op, dmalloc(&s.skh, mb));
   if (op->cfg.aggregate >= FW_AGG_FIRST && op->cfg.aggregate <= FW_AGG_FIRST_MAX) HIP_OR_RETURN(op, dmalloc(&s.so, mb));
+  if (op->cfg.aggregate == FW_AGG_MINBY || op->cfg.aggregate == FW_AGG_MAXBY) HIP_OR_RETURN(op, dmalloc(&s.byv, mb));
   return FW_OK;
 }
 void free_scratch(Scratch& s) {
@@ -189,6 +193,7 @@ void free_scratch(Scratch& s) {
   dfree(s.sv);
   dfree(s.skh);
   dfree(s.so);
+  dfree(s.byv);
 }
 
 // buffers of the split-partition aggregate (AggHot): deltas at record indices, so one Entry per record
@@ -424,8 +429,10 @@ int settle(fw_op* op) {
     const Scratch& S = op->sc[op->last_sc];
     DevCfg c = op->dc;
     c.slow_ord = S.so;
+    c.by_val = S.byv;
     c.compact = S.compact;
     c.cbase = S.cbase;
+    c.ord_base = S.ord_base;
     if (susp & FW_SUSP_AGG)
       timed(op, K_AGGREGATE, [&] {
         fwdev::launch_aggregate(c, S.wm, S.part, S.hist, S.T, op->tb, op->prog, 1, S.split ? &op->hot : nullptr, S.n,
@@ -557,6 +564,9 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
     fwdev::launch_scatter(c, op->wm, key, ts, val, kh, n, T, S.hist, S.part, S.sk, S.stt, S.sv, S.skh, op->side,
                           op->d_status, op->stream);
   });
+  // minBy / maxBy: the aggregate reads the selected elements' fields back by batch index, possibly after the
+  // caller's columns are gone (a resumed push), so the batch keeps its own copy
+  if (S.byv) HIP_OR_RETURN(op, hipMemcpyAsync(S.byv, val, n * sizeof(int64_t), hipMemcpyDeviceToDevice, op->stream));
   HIP_OR_RETURN(op, hipGetLastError());
   if (early && (rc = settle(op))) return rc;
   if ((rc = maybe_restart_rows(op))) return rc;
@@ -567,6 +577,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   DevCfg cc = op->dc;  // settle may have grown the table
   cc.ord_base = c.ord_base;
   cc.slow_ord = S.so;
+  cc.by_val = S.byv;
   cc.compact = c.compact;
   cc.cbase = c.cbase;
   // a partition can outgrow one aggregate workgroup (hot keys) only when the batch is longer than a chunk
@@ -592,6 +603,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   S.wm = op->wm;
   S.compact = c.compact;
   S.cbase = c.cbase;
+  S.ord_base = c.ord_base;
   op->last_sc = nxt;
   op->records_in += n;
   op->push_unsettled = true;
@@ -671,10 +683,6 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
                               "over a Double field");
     unsupported = true;
   }
-  if (!msg[0] && (cfg.aggregate == FW_AGG_MINBY || cfg.aggregate == FW_AGG_MAXBY) && cfg.value_type != FW_VAL_I32) {
-    snprintf(msg, sizeof msg, "minBy / maxBy are offered over an Integer field");
-    unsupported = true;
-  }
   if (!msg[0] && cfg.aggregate >= FW_AGG_FIRST && cfg.aggregate <= FW_AGG_FIRST_MAX && cfg.assigner == FW_SLIDING && cfg.slide > 0 &&
       (cfg.size + cfg.slide - 1) / cfg.slide > 65535) {
     snprintf(msg, sizeof msg, "the first-element aggregate takes at most 65535 windows per element");
@@ -725,7 +733,8 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   // sliding windows whose size is a multiple of the slide, without allowed lateness, are kept as panes:
   // one state update per element instead of size/slide (DevCfg::panes; FW_NO_PANES=1 disables it)
   c.panes = cfg.assigner == FW_SLIDING && cfg.allowed_lateness == 0 && cfg.size > cfg.slide &&
-            cfg.size % cfg.slide == 0 && !(getenv("FW_NO_PANES") && atoi(getenv("FW_NO_PANES")));
+            cfg.size % cfg.slide == 0 && cfg.aggregate != FW_AGG_MINBY && cfg.aggregate != FW_AGG_MAXBY &&
+            !(getenv("FW_NO_PANES") && atoi(getenv("FW_NO_PANES")));
   if (cfg.assigner != FW_SESSION) {
     make_div_inv((uint64_t)c.size, &c.mag_size, &c.l_size);
     make_div_inv((uint64_t)c.slide, &c.mag_slide, &c.l_slide);
@@ -775,7 +784,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   c.log_r = std::max(8, ilog2(4 * ((expected + c.P - 1) / c.P)));
   op->table_slots = (int64_t)c.P << c.log_r;
 
-  op->max_batch = cfg.max_batch > 0 ? cfg.max_batch : (int64_t(1) << 24);
+  op->max_batch = cfg.max_batch > 0 ? std::min<int64_t>(cfg.max_batch, int64_t(1) << 31) : (int64_t(1) << 24);
   op->tmax = (int32_t)((op->max_batch + FW_TILE - 1) / FW_TILE);
   int rc = alloc_table(op, op->tb, c, true);
   if (rc) return rc;
@@ -1145,10 +1154,9 @@ void free_state_cols(StateCols& c) {
 }  // namespace
 
 int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64_t cap, int64_t* n) {
-  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_MINBY || op->dc.agg == FW_AGG_MAXBY ||
-             op->dc.agg == FW_AGG_TDIGEST))  // not in fw_state_rows
+  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_TDIGEST))  // not in fw_state_rows
     return set_err(op, FW_ERR_UNSUPPORTED,
-                   "keyed-state snapshots of the HyperLogLog, t-digest, minBy and maxBy aggregates are not offered");
+                   "keyed-state snapshots of the HyperLogLog and t-digest aggregates are not offered");
   if (!op || !n) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;
@@ -1187,10 +1195,9 @@ int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64
 }
 
 int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_t n) {
-  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_MINBY || op->dc.agg == FW_AGG_MAXBY ||
-             op->dc.agg == FW_AGG_TDIGEST))  // not in fw_state_rows
+  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_TDIGEST))  // not in fw_state_rows
     return set_err(op, FW_ERR_UNSUPPORTED,
-                   "keyed-state snapshots of the HyperLogLog, t-digest, minBy and maxBy aggregates are not offered");
+                   "keyed-state snapshots of the HyperLogLog and t-digest aggregates are not offered");
   if (!op || (n > 0 && !src) || n < 0) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;
@@ -1201,8 +1208,30 @@ int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_
     if (!h) return set_err(op, FW_ERR_ARG, "null state column");
   // first-element reduces: records pushed after the restore are numbered after every restored first
   // element, so the earlier element keeps winning in the caller's numbering
-  if (op->dc.agg == FW_AGG_FIRST || op->dc.agg == FW_AGG_FIRST_MAX)
+  // (minBy / maxBy: `max` is the selected element's ordinal, likewise)
+  if (op->dc.agg >= FW_AGG_FIRST && op->dc.agg <= FW_AGG_FIRST_MAX)
     for (int64_t i = 0; i < n; i++) op->records_in = std::max(op->records_in, src->max[i] + 1);
+  // rows of this call that restore the same (key, window): a round per repetition (launch_restore)
+  std::vector<int32_t> round_of((size_t)n);
+  int32_t rounds = 1;
+  {
+    struct KW {
+      int64_t k, s, e;
+      bool operator==(const KW& o) const { return k == o.k && s == o.s && e == o.e; }
+    };
+    struct H {
+      size_t operator()(const KW& x) const {
+        return std::hash<int64_t>()(x.k * 0x9E3779B97F4A7C15ll ^ x.s * 0x632BE59BD9B4E019ll ^ x.e);
+      }
+    };
+    std::unordered_map<KW, int32_t, H> seen;
+    seen.reserve((size_t)n);
+    for (int64_t i = 0; i < n; i++) {
+      int32_t& c = seen[KW{src->key[i], src->start[i], src->end[i]}];
+      round_of[(size_t)i] = c++;
+      rounds = std::max(rounds, c);
+    }
+  }
   StateCols d{};
   int32_t* demand = nullptr;
   auto fail = [&](int code) {
@@ -1219,7 +1248,7 @@ int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_
   const int32_t P = op->dc.P;
   if (dmalloc(&demand, (size_t)P) != hipSuccess || hipMemsetAsync(demand, 0, P * sizeof(int32_t), op->stream) != hipSuccess)
     return fail(set_err(op, FW_ERR_HIP, "restore: allocation failed"));
-  fwdev::launch_restore(op->dc, kg, d, n, demand, op->tb, op->d_status, op->stream);
+  fwdev::launch_restore(op->dc, kg, d, n, demand, op->tb, op->d_status, nullptr, 0, op->stream);
   std::vector<int32_t> dem(P), live(P);
   if (hipMemcpyAsync(dem.data(), demand, P * sizeof(int32_t), hipMemcpyDeviceToHost, op->stream) != hipSuccess ||
       hipMemcpyAsync(live.data(), op->tb.live, P * sizeof(int32_t), hipMemcpyDeviceToHost, op->stream) != hipSuccess ||
@@ -1234,9 +1263,17 @@ int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_
   int64_t need = 0;
   for (int32_t p = 0; p < P; p++) need = std::max<int64_t>(need, (int64_t)live[p] + dem[p]);
   if (need > region_limit(op->dc.log_r) && (rc = grow_table(op, log_r_for(op, need)))) return fail(rc);
-  fwdev::launch_restore(op->dc, kg, d, n, nullptr, op->tb, op->d_status, op->stream);
-  if (hipGetLastError() != hipSuccess || (rc = sync_status(op)))
-    return fail(rc ? rc : set_err(op, FW_ERR_HIP, "restore kernel failed"));
+  int32_t* d_round = nullptr;
+  if (rounds > 1) {
+    if (dmalloc(&d_round, (size_t)n) != hipSuccess ||
+        hipMemcpyAsync(d_round, round_of.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, op->stream) != hipSuccess)
+      return fail(set_err(op, FW_ERR_HIP, "restore: allocation failed"));
+  }
+  fwdev::launch_restore(op->dc, kg, d, n, nullptr, op->tb, op->d_status, d_round, rounds, op->stream);
+  const bool launched = hipGetLastError() == hipSuccess;
+  rc = sync_status(op);
+  dfree(d_round);
+  if (!launched || rc) return fail(rc ? rc : set_err(op, FW_ERR_HIP, "restore kernel failed"));
   fail(FW_OK);
   if (op->h_status->flags & FW_STATUS_STATE_LOST) return set_err(op, FW_ERR_CAPACITY, "restore: region full");
   const int64_t rows = (int64_t)op->h_status->out_rows;

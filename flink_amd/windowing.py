@@ -197,13 +197,14 @@ class FirstElementReduce:
 class ExtremalElementReduce:
     """`minBy(pos)` / `maxBy(pos)` of WindowedStream (first = true): the whole element whose field is the
     smallest (largest), the earlier one among equal fields (ComparableAggregator.reduce,
-    ComparableAggregator.java:72-94; Comparator MinBy/MaxBy).  Integer fields.  Fired rows: min = the
-    selected field, max = the selected element's arrival ordinal (`selected_elements` returns the elements)."""
+    ComparableAggregator.java:72-94; Comparator MinBy/MaxBy): Integer ("int"), Long ("long") or Double
+    ("double", Double.compare order) fields.  Fired rows: min = the selected field, max = the selected
+    element's arrival ordinal (`selected_elements` returns the elements)."""
     kind: str = "min"
     value_type: str = "int"
 
     def native(self):
-        return N.FW_VAL_I32
+        return {"long": N.FW_VAL_I64, "int": N.FW_VAL_I32, "double": N.FW_VAL_F64}[self.value_type]
 
     def hll_precision(self):
         return 0

@@ -63,11 +63,11 @@ extern "C" {
                                       record. */
 #define FW_AGG_MINBY 3             /* minBy(pos) / maxBy(pos) with the first-tie rule (ComparableAggregator.java
                                       :72-94, Comparator.java MinBy/MaxBy): the whole element with the smallest
-                                      (largest) field, the earlier one among equal fields.  Integer fields
-                                      (FW_VAL_I32) only.  Rows carry count, sum, min = the selected field value
-                                      and max = the arrival ordinal of the selected element.  Exact while the
-                                      elements of one window span fewer than 2^32 arrival ordinals.  Keyed-state
-                                      snapshots are refused. */
+                                      (largest) field, the earlier one among equal fields; Integer, Long or
+                                      Double (Double.compare order) fields.  Rows carry count, sum, min = the
+                                      selected field value and max = the arrival ordinal of the selected element
+                                      (exact: (field, ordinal) pairs compare in full).  Sliding windows use the
+                                      per-window form (no panes). */
 #define FW_AGG_MAXBY 4
 #define FW_AGG_TDIGEST 6           /* t-digest quantiles of a Double field (definition in DESIGN.md
                                       §t-digest and oracle/window_oracle.h): a merging t-digest with the k1 scale
@@ -230,8 +230,9 @@ void* fw_stream(fw_op* op); /* the hipStream_t the handle enqueues on */
  *   fw_restore_key_group: inserts rows into the handle (which must own the key group); a row whose
  *     (key, window) is already present is merged into it (AggregateFunction.merge).  Long/Integer
  *     keys outside the key group are refused with FW_ERR_KEY_GROUP.  First-element reduces (FW_AGG_FIRST,
- *     FW_AGG_FIRST_MAX): `max` is the first element's ordinal, and later pushes are numbered after the largest
- *     restored one.  HyperLogLog, minBy and maxBy state is refused (FW_ERR_UNSUPPORTED). */
+ *     FW_AGG_FIRST_MAX, FW_AGG_MINBY, FW_AGG_MAXBY): `max` is the element's ordinal, and later pushes are
+ *     numbered after the largest restored one.  Rows of one call that restore the same (key, window) are merged
+ *     in order.  HyperLogLog and t-digest state is refused (FW_ERR_UNSUPPORTED). */
 typedef struct fw_state_rows {
   int64_t* key;
   int64_t* start;

@@ -358,12 +358,18 @@ class WindowOperatorOracle {
   // (OR_AGG_FIRST: HeapReducingState.add, HeapReducingState.java:72-84 — the element that finds no
   // state becomes it, and SumAggregator.reduce / ComparableAggregator.reduce keep a copy of their first
   // argument (SumAggregator.java:66-76, ComparableAggregator.java:72-94): the first element survives)
+  // Comparator.MinByComparator / MaxByComparator order the field with compareTo: Long / Integer by value,
+  // Double by Double.compare (Comparator.java:35-108)
+  int by_cmp(int64_t x, int64_t y) const {
+    if (cfg.value_type == OR_VAL_F64) return java_double_compare(bitsd(x), bitsd(y));
+    return x < y ? -1 : x > y ? 1 : 0;
+  }
   void acc_add(Acc& a, int64_t v) const {
     if (a.cnt == 0) a.first = ordinal;
     // minBy/maxBy (Comparator.MinByComparator / MaxByComparator, first = true): a strictly smaller (larger)
     // field replaces the kept element; an equal one leaves the earlier element
-    if (a.cnt == 0 || (cfg.aggregate == OR_AGG_MINBY && v < a.by_val) ||
-        (cfg.aggregate == OR_AGG_MAXBY && v > a.by_val)) {
+    if (a.cnt == 0 || (cfg.aggregate == OR_AGG_MINBY && by_cmp(v, a.by_val) < 0) ||
+        (cfg.aggregate == OR_AGG_MAXBY && by_cmp(v, a.by_val) > 0)) {
       a.by_val = v;
       a.by_ord = ordinal;
     }
@@ -406,8 +412,9 @@ class WindowOperatorOracle {
     r.first = std::min(a.first, b.first);  // (OR_AGG_FIRST and OR_AGG_FIRST_MAX)
     // minBy/maxBy merge: the reference keeps reduce(a, b)'s first argument on a tie, `a` chosen by HashSet
     // order (parity unpinned); defined here as the earlier element, like the accumulation order
-    const bool b_wins = cfg.aggregate == OR_AGG_MINBY   ? (b.by_val < a.by_val || (b.by_val == a.by_val && b.by_ord < a.by_ord))
-                        : cfg.aggregate == OR_AGG_MAXBY ? (b.by_val > a.by_val || (b.by_val == a.by_val && b.by_ord < a.by_ord))
+    const int cmp = by_cmp(b.by_val, a.by_val);
+    const bool b_wins = cfg.aggregate == OR_AGG_MINBY   ? (cmp < 0 || (cmp == 0 && b.by_ord < a.by_ord))
+                        : cfg.aggregate == OR_AGG_MAXBY ? (cmp > 0 || (cmp == 0 && b.by_ord < a.by_ord))
                                                         : false;
     if (b_wins) {
       r.by_val = b.by_val;

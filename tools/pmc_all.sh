@@ -7,7 +7,7 @@ for w in ${WORKLOADS:-c2 c3 c5}; do
   for counters in FETCH_SIZE WRITE_SIZE; do
     i=$((i+1))
     (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $counters -d "$d/p$i" -o run --output-format csv \
-        -- python3 "$R/bench.py" --workload $w --steps ${PMC_STEPS:-3} --warmup 1 --no-cpu-baseline --no-profile \
+        -- python3 "$R/bench.py" --workload $w --steps ${PMC_STEPS:-3} --warmup 1 --no-cpu-baseline --no-profile --host-fed-steps 0 \
         > "$d/p$i.log" 2>&1) || { echo "$w pass $i rc=$?"; tail -5 "$d/p$i.log"; exit 1; }
     echo "$w pass $i ok: $counters"
   done
