@@ -163,7 +163,6 @@ __device__ __forceinline__ int64_t f64_unsortable(int64_t s) { return s >= 0 ? s
 
 // ------------------------------------------------------------------ record classes
 enum { CLS_NORMAL = 0, CLS_SLOW = 1, CLS_LATE = 2, CLS_SKIP = 3, CLS_BADTS = 4 };
-constexpr int MAX_SESSIONS = 64;  // in-flight sessions of one key visible to one merge step
 
 // Windows of a record, newest first (SlidingEventTimeWindows.java:71-75 loop order).
 __device__ __forceinline__ int num_windows(const DevCfg& c, int64_t ts, int64_t* last_start) {
@@ -1266,146 +1265,55 @@ __device__ __forceinline__ bool lds_session_upsert(AggLds& L, int64_t* E, int vt
 // its accumulator) into the key's in-flight sessions of region r: d's connected component becomes one
 // session (merge function + mergeNamespaces, WindowOperator.java:308-339,
 // AbstractHeapMergingState.java:67-93; EventTimeTrigger.onMerge/onElement register maxTimestamp,
-// which is after the watermark).  Only the thread that owns d.key touches the key's entries; new
-// slots are published BUSY -> LIVE because other threads walk the same probe chains.
+// which is after the watermark).  A key's in-flight sessions are pairwise disjoint and non-touching (any
+// two that intersected were merged), so d's component is exactly the sessions that intersect d: one walk
+// of the key's probe chain merges them into the first one met, whatever their number (no cap on a key's
+// in-flight sessions).  Only the thread that owns d.key touches the key's entries; new slots are published
+// BUSY -> LIVE because other threads walk the same probe chains.
 // Returns the region slots newly taken; *timer = maxTimestamp of the resulting session.
 // DIAG_AGG_TIMING clocks of the session flush (thread 0): [0] flushes, [1] linking, [2] adding, [3] tail
 __device__ unsigned long long g_sess[4];
-__device__ __noinline__ int session_add_many(const DevCfg& c, const Region& r, const Entry& d, int64_t* timer, Status* st) {
-  const uint64_t h = slot_hash(c, d.key, 0);
-  const uint32_t want = live_word(h);
-  int32_t sl[MAX_SESSIONS];
-  int ns = 0;
-  *timer = LMAX;
-  for (uint32_t i = 0; i <= r.mask; i++) {
-    const uint32_t s = ((uint32_t)h + i) & r.mask;
-    const uint32_t stt = ld_state(r.state + s);
-    if (stt == SLOT_EMPTY) break;
-    if (stt == want) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (r.ent[s].key == d.key) {
-        if (ns == MAX_SESSIONS) {
-          atomicOr(&st->flags, FW_STATUS_STATE_LOST);
-          return 0;
-        }
-        sl[ns++] = (int32_t)s;
-      }
-    }
-  }
-  int64_t cs = d.start, ce = d.end;
-  uint64_t in_group = 0;
-  for (bool grew = true; grew;) {
-    grew = false;
-    for (int j = 0; j < ns; j++) {
-      if (in_group >> j & 1) continue;
-      const Entry& e = r.ent[sl[j]];
-      if (cs <= e.end && ce >= e.start) {  // TimeWindow.intersects
-        in_group |= 1ull << j;
-        cs = min(cs, e.start);
-        ce = max(ce, e.end);
-        grew = true;
-      }
-    }
-  }
-  *timer = jsub(ce, 1);
-  if (in_group == 0) {  // a new session
-    const int32_t s = region_claim(r, h, SLOT_BUSY);
-    if (s < 0) {  // cannot happen below the load limit (checked by the flush)
-      atomicOr(&st->flags, FW_STATUS_STATE_LOST);
-      return 0;
-    }
-    r.ent[s] = d;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __hip_atomic_store(r.state + s, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return 1;
-  }
-  const int first = __ffsll((unsigned long long)in_group) - 1;
-  Entry m = r.ent[sl[first]];
-  for (int j = first + 1; j < ns; j++) {
-    if (!(in_group >> j & 1)) continue;
-    acc_merge(c, m, r.ent[sl[j]]);
-    // the slot stays occupied (live counts occupied slots) until k_fire rebuilds the region
-    __hip_atomic_store(r.state + sl[j], SLOT_DEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  acc_merge(c, m, d);
-  m.start = cs;
-  m.end = ce;
-  m.meta = FW_TIMER;
-  r.ent[sl[first]] = m;
-  return 0;
-}
-
-// session_add with the key's in-flight sessions held in registers (the common case: at most
-// SESS_REG sessions of one key); more go through session_add_many, which holds up to MAX_SESSIONS
-constexpr int SESS_REG = 4;
 __device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, const Entry& d, int64_t* timer, Status* st) {
   const uint64_t h = slot_hash(c, d.key, 0);
   const uint32_t want = live_word(h);
-  uint32_t sl[SESS_REG];
-  int64_t ss[SESS_REG], se[SESS_REG];
-  int ns = 0;
+  int32_t target = -1;
+  Entry m;
   for (uint32_t i = 0; i <= r.mask; i++) {
     const uint32_t s = ((uint32_t)h + i) & r.mask;
     const uint32_t stt = ld_state(r.state + s);
     if (stt == SLOT_EMPTY) break;
     if (stt != want) continue;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const Entry& e = r.ent[s];
-    if (e.key != d.key) continue;
-    if (ns == SESS_REG) return session_add_many(c, r, d, timer, st);
-    const int64_t es = e.start, ee = e.end;
-#pragma unroll
-    for (int q = 0; q < SESS_REG; q++) {
-      if (q == ns) {
-        sl[q] = s;
-        ss[q] = es;
-        se[q] = ee;
-      }
+    const Entry e = r.ent[s];
+    if (e.key != d.key || !(d.start <= e.end && d.end >= e.start)) continue;  // TimeWindow.intersects
+    if (target < 0) {
+      target = (int32_t)s;
+      m = e;
+      continue;
     }
-    ns++;
+    acc_merge(c, m, e);
+    m.start = min(m.start, e.start);
+    m.end = max(m.end, e.end);
+    // the slot stays occupied (live counts occupied slots) until k_fire rebuilds the region
+    __hip_atomic_store(r.state + s, SLOT_DEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  int64_t cs = d.start, ce = d.end;
-  uint32_t in_group = 0;
-  for (bool grew = true; grew;) {
-    grew = false;
-#pragma unroll
-    for (int q = 0; q < SESS_REG; q++) {
-      if (q < ns && !(in_group >> q & 1) && cs <= se[q] && ce >= ss[q]) {  // TimeWindow.intersects
-        in_group |= 1u << q;
-        cs = min(cs, ss[q]);
-        ce = max(ce, se[q]);
-        grew = true;
-      }
-    }
-  }
-  *timer = jsub(ce, 1);
-  if (in_group == 0) {  // a new session
-    const int32_t s = region_claim(r, h, SLOT_BUSY);
-    if (s < 0) {  // cannot happen below the load limit (checked by the flush)
+  if (target < 0) {  // a new session
+    *timer = jsub(d.end, 1);
+    const int32_t ns = region_claim(r, h, SLOT_BUSY);
+    if (ns < 0) {  // cannot happen below the load limit (checked by the flush)
       atomicOr(&st->flags, FW_STATUS_STATE_LOST);
       return 0;
     }
-    r.ent[s] = d;
+    r.ent[ns] = d;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __hip_atomic_store(r.state + s, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(r.state + ns, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return 1;
   }
-  const int first = __ffs(in_group) - 1;
-  uint32_t target = sl[0];
-#pragma unroll
-  for (int q = 1; q < SESS_REG; q++) target = q == first ? sl[q] : target;
-  Entry m = r.ent[target];
-#pragma unroll
-  for (int q = 0; q < SESS_REG; q++) {
-    if (q <= first || !(in_group >> q & 1)) continue;
-    acc_merge(c, m, r.ent[sl[q]]);
-    // the slot stays occupied (live counts occupied slots) until k_fire rebuilds the region
-    __hip_atomic_store(r.state + sl[q], SLOT_DEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
   acc_merge(c, m, d);
-  m.start = cs;
-  m.end = ce;
+  m.start = min(m.start, d.start);  // TimeWindow.cover
+  m.end = max(m.end, d.end);
   m.meta = FW_TIMER;
+  *timer = jsub(m.end, 1);
   r.ent[target] = m;
   return 0;
 }
@@ -2072,46 +1980,28 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
   const Region r = region_of(c, x.tb, p, x.tb.cur[p]);
   const uint64_t h = slot_hash(c, k, 0);
   const uint32_t want = live_word(h);
-  // in-flight windows of the key: every live entry of the key sits on its probe chain
-  int32_t sl[MAX_SESSIONS];
-  int ns = 0;
+  const int64_t ws = t, we = jadd(t, c.gap);  // EventTimeSessionWindows.assignWindows
+  // TimeWindow.mergeWindows: in-flight windows are pairwise disjoint and non-touching, so the new window's
+  // connected component is the windows that intersect it.  Every live entry of the key sits on its probe
+  // chain: one walk finds the component (its first slot, its size, its hull), a second merges it.
+  int32_t first = -1, n_in = 0;
+  int64_t cs = ws, ce = we;
   for (uint32_t i = 0; i <= r.mask; i++) {
     const uint32_t s = ((uint32_t)h + i) & r.mask;
     const uint32_t stt = ld_state(r.state + s);
     if (stt == SLOT_EMPTY) break;
-    if (stt == want) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (r.ent[s].key == k) {
-        if (ns == MAX_SESSIONS) {
-          atomicOr(&x.st->flags, FW_STATUS_STATE_LOST);
-          return;
-        }
-        sl[ns++] = (int32_t)s;
-      }
-    }
-  }
-  const int64_t ws = t, we = jadd(t, c.gap);  // EventTimeSessionWindows.assignWindows
-  // TimeWindow.mergeWindows: the connected component of the new window (in-flight windows are
-  // pairwise disjoint and non-touching, so only this component can merge).
-  int64_t cs = ws, ce = we;
-  uint64_t in_group = 0;
-  bool grew = true;
-  while (grew) {
-    grew = false;
-    for (int j = 0; j < ns; j++) {
-      if (in_group >> j & 1) continue;
-      const Entry& e = r.ent[sl[j]];
-      if (cs <= e.end && ce >= e.start) {  // TimeWindow.intersects
-        in_group |= 1ull << j;
-        cs = min(cs, e.start);
-        ce = max(ce, e.end);
-        grew = true;
-      }
-    }
+    if (stt != want) continue;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const Entry& e = r.ent[s];
+    if (e.key != k || !(ws <= e.end && we >= e.start)) continue;  // TimeWindow.intersects
+    if (first < 0) first = (int32_t)s;
+    n_in++;
+    cs = min(cs, e.start);
+    ce = max(ce, e.end);
   }
   int32_t actual = -1;
   bool fresh = false;
-  if (in_group == 0) {
+  if (first < 0) {
     Entry ne;
     ne.key = k;
     ne.start = ws;
@@ -2122,10 +2012,9 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
     if (actual < 0) return;
     fresh = true;
   } else {
-    const int first = __ffsll((unsigned long long)in_group) - 1;
-    const Entry& f = r.ent[sl[first]];
-    const bool contained = __popcll(in_group) == 1 && f.start == cs && f.end == ce;
-    actual = sl[first];
+    const Entry& f = r.ent[first];
+    const bool contained = n_in == 1 && f.start == cs && f.end == ce;
+    actual = first;
     if (!contained) {
       // merge function (WindowOperator.java:308-339)
       if (jadd(jsub(ce, 1), c.lateness) <= x.wm) {
@@ -2133,10 +2022,15 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
         return;
       }
       Entry m = f;
-      for (int j = first + 1; j < ns; j++) {
-        if (!(in_group >> j & 1)) continue;
-        acc_merge(c, m, r.ent[sl[j]]);  // mergeNamespaces
-        kill_slot(x, r, p, sl[j]);
+      for (uint32_t i = 0; i <= r.mask; i++) {
+        const uint32_t s = ((uint32_t)h + i) & r.mask;
+        const uint32_t stt = ld_state(r.state + s);
+        if (stt == SLOT_EMPTY) break;
+        if (stt != want || (int32_t)s == first) continue;
+        const Entry& e = r.ent[s];
+        if (e.key != k || !(ws <= e.end && we >= e.start)) continue;
+        acc_merge(c, m, e);  // mergeNamespaces
+        kill_slot(x, r, p, (int32_t)s);
       }
       m.start = cs;
       m.end = ce;

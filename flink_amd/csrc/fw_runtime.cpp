@@ -467,8 +467,7 @@ int settle(fw_op* op) {
     op->clear_deferred = false;
   }
   if (s.flags & FW_STATUS_STATE_LOST)
-    return set_err(op, FW_ERR_CAPACITY,
-                   "a window could not be stored (more than 64 in-flight sessions of one key)");
+    return set_err(op, FW_ERR_CAPACITY, "a window could not be stored (state region full)");
   if (s.flags & FW_STATUS_OUT_FULL) return set_err(op, FW_ERR_STATE, "fired-row buffer overflow");
   if (s.flags & FW_STATUS_POOL)
     return set_err(op, FW_ERR_CAPACITY, "accumulator block pool exhausted (%lld blocks; raise expected_entries)",

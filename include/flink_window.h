@@ -32,7 +32,7 @@ extern "C" {
 #define FW_ERR_HIP (-2)          /* HIP runtime failure */
 #define FW_ERR_NO_TIMESTAMP (-3) /* Long.MIN_VALUE timestamp: TumblingEventTimeWindows.java:69-71 */
 #define FW_ERR_KEY_GROUP (-4)    /* key outside the handle's KeyGroupRange (KeyGroupRangeOffsets / StateTable) */
-#define FW_ERR_CAPACITY (-5)     /* state could not be stored (HBM exhausted, or > 64 in-flight sessions of a key) */
+#define FW_ERR_CAPACITY (-5)     /* state could not be stored (HBM exhausted) */
 #define FW_ERR_UNSUPPORTED (-6)  /* configuration not offered on the GPU path */
 #define FW_ERR_STATE (-7)        /* corrupted / inconsistent handle state */
 

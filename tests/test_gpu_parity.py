@@ -873,3 +873,36 @@ def test_gpu_restore_merges_repeated_rows():
         assert np.array_equal(got["sum"], 2 * exp["sum"])
         assert np.array_equal(got["min"], exp["min"]) and np.array_equal(got["max"], exp["max"])
     b.close()
+
+
+@pytest.mark.parametrize("purging", [False, True])
+def test_gpu_sessions_many_in_flight_per_key(purging):
+    # one key holding hundreds of in-flight sessions (gap 10 ms, allowedLateness 10 s: a session stays in the
+    # MergingWindowSet until maxTimestamp + 10 s), with late elements that fire them again and elements that
+    # bridge two sessions, modelled on WindowOperatorTest's session lateness cases (WindowOperatorTest.java
+    # :1980-2266).  The reference's MergingWindowSet has no bound on a key's windows.
+    rng = np.random.default_rng(11)
+    base = 1_000_000
+    t0 = base + 18 * np.arange(700)                              # key 0: one session every 18 ms
+    bridge = base + 18 * rng.integers(0, 700, 80) + 8            # [t + 8, t + 18) touches two sessions
+    late = base + 18 * rng.integers(0, 700, 150) + rng.integers(0, 9, 150)
+    k_other = rng.integers(1, 50, 4000)
+    t_other = base + rng.integers(0, 13_000, 4000)
+    keys = np.concatenate([np.zeros(700 + 80 + 150, dtype=np.int64), k_other])
+    ts = np.concatenate([t0, bridge, late, t_other]).astype(np.int64)
+    order = np.argsort(ts + rng.integers(-300, 300, len(ts)), kind="stable")  # mostly in order, 300 ms jitter
+    keys, ts = keys[order], ts[order]
+    vals = rng.integers(-1000, 1000, len(ts))
+    batches, wms, mx = [], [], -(1 << 63)
+    for b in range(0, len(ts), 400):
+        sl = slice(b, b + 400)
+        batches.append((keys[sl], ts[sl], vals[sl]))
+        mx = max(mx, int(ts[sl].max()))
+        wms.append(mx - 500)
+    batches.append((keys[:0], ts[:0], vals[:0]))
+    wms.append((1 << 63) - 1)
+    cfg = dict(assigner="session", gap=10, lateness=10_000, purging=purging)
+    g, r, gs, rs, gl, rl = _run_both(cfg, batches, wms, max_parallelism=1, sub_partitions=1)
+    assert_rows_equal(g, r)
+    assert gl == rl
+    assert (r["key"] == 0).sum() > 600  # the hot key's sessions (and their late firings)
