@@ -198,7 +198,7 @@ def main():
     from flink_amd.operator import GpuWindowOperator
 
     max_par = 128
-    exch = KeyGroupExchange(max_par, world, rank)
+    exch = KeyGroupExchange(max_par, world, rank, key_type="hashed" if c1 else "long")
     if sliding:
         # weak scaling: the key space and the event rate grow with the GPU count (16M keys at 8 GPUs)
         args.keys *= world
@@ -258,7 +258,8 @@ def main():
             k, t, v, h = batches[s]
             wm = local_wm[s]
         if world > 1:
-            k, t, v = exch.exchange(k, t, v)
+            res = exch.exchange(k, t, v, h)
+            k, t, v, h = res if h is not None else res + (None,)
             wm = exch.combine_watermark(wm, device=dev)
         op.process_batch(k, t, v, h)            # queued; settles the previous step's sequence
         op.advance_watermark(wm, wait=False)  # queued behind the push

@@ -86,6 +86,10 @@ SIGNATURES = {
     "fw_route_device": (ctypes.c_int, [VP, VP, VP, VP, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
                                        ctypes.c_int32, VP, VP, VP, VP, VP, VP, ctypes.c_int64, VP]),
     "fw_route_scratch_bytes": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
+    "fw_comm_unique_id": (ctypes.c_int, [VP]),
+    "fw_comm_init": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(VP)]),
+    "fw_comm_destroy": (None, [VP]),
+    "fw_keyby_push_device": (ctypes.c_int, [VP, VP, VP, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, I64P]),
     "fw_generate_device": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, VP,
                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, VP, VP, VP, VP, VP]),
 }

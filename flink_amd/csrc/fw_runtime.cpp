@@ -16,6 +16,7 @@
 // they only read the batch and write this push's scratch set (two sets alternate), so they run
 // while the host waits and settles, and the state kernels are queued before the GPU drains.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -1302,6 +1303,170 @@ int fw_route_device(const int64_t* key, const int64_t* ts, const int64_t* val, c
   fwdev::launch_route(key, ts, val, key_hash, key_kind, n, max_parallelism, parallelism, key_out, ts_out, val_out,
                       hash_out, counts, (uint32_t*)scratch, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? FW_OK : FW_ERR_HIP;
+}
+
+// ---- keyBy exchange over RCCL (see flink_window.h)
+}  // extern "C"
+struct fw_comm {
+  ncclComm_t nc = nullptr;
+  int32_t world = 1, rank = 0, device = 0;
+  int64_t cap = 0;                                        // records the routed / received columns hold
+  int64_t *rk = nullptr, *rt = nullptr, *rv = nullptr;    // received columns
+  int32_t* rh = nullptr;
+  int64_t *sk = nullptr, *st = nullptr, *sv = nullptr;    // routed (send) columns
+  int32_t* sh = nullptr;
+  void* scratch = nullptr;
+  int64_t scratch_bytes = 0;
+  int64_t* counts = nullptr;                              // [2 world + 2]: send counts, recv counts, wm in/out
+  int64_t* h_counts = nullptr;                            // pinned host copy
+};
+namespace {
+template <class T>
+void cfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+int comm_reserve(fw_op* op, fw_comm* c, int64_t need) {
+  if (need <= c->cap) return FW_OK;
+  const int64_t cap = std::max<int64_t>(need, c->cap * 2);
+  for (int64_t** p : {&c->rk, &c->rt, &c->rv, &c->sk, &c->st, &c->sv}) {
+    cfree(*p);
+    HIP_OR_RETURN(op, dmalloc(p, (size_t)cap));
+  }
+  for (int32_t** p : {&c->rh, &c->sh}) {
+    cfree(*p);
+    HIP_OR_RETURN(op, dmalloc(p, (size_t)cap));
+  }
+  cfree(c->scratch);
+  c->scratch_bytes = fw_route_scratch_bytes(cap, c->world);
+  HIP_OR_RETURN(op, dmalloc((uint8_t**)&c->scratch, (size_t)c->scratch_bytes));
+  c->cap = cap;
+  return FW_OK;
+}
+#define NCCL_OR_RETURN(op, expr)                                                                            \
+  do {                                                                                                      \
+    ncclResult_t _r = (expr);                                                                               \
+    if (_r != ncclSuccess) return set_err(op, FW_ERR_HIP, "%s failed: %s", #expr, ncclGetErrorString(_r)); \
+  } while (0)
+}  // namespace
+extern "C" {
+
+int fw_comm_unique_id(void* id128) {
+  if (!id128) return FW_ERR_ARG;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return FW_ERR_HIP;
+  memcpy(id128, &id, sizeof id);
+  return FW_OK;
+}
+
+int fw_comm_init(const void* id128, int32_t world, int32_t rank, int32_t device, fw_comm** out) {
+  if (!id128 || !out || world < 1 || rank < 0 || rank >= world) return FW_ERR_ARG;
+  *out = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return FW_ERR_HIP;
+  fw_comm* c = new fw_comm();
+  c->world = world;
+  c->rank = rank;
+  c->device = device;
+  ncclUniqueId id;
+  memcpy(&id, id128, sizeof id);
+  if (ncclCommInitRank(&c->nc, world, id, rank) != ncclSuccess || dmalloc(&c->counts, 2 * (size_t)world + 2) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_counts, (2 * (size_t)world + 2) * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
+    fw_comm_destroy(c);
+    return FW_ERR_HIP;
+  }
+  *out = c;
+  return FW_OK;
+}
+
+void fw_comm_destroy(fw_comm* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->nc) (void)ncclCommDestroy(c->nc);
+  for (int64_t** p : {&c->rk, &c->rt, &c->rv, &c->sk, &c->st, &c->sv, &c->counts}) cfree(*p);
+  for (int32_t** p : {&c->rh, &c->sh}) cfree(*p);
+  cfree(c->scratch);
+  if (c->h_counts) (void)hipHostFree(c->h_counts);
+  delete c;
+}
+
+int fw_keyby_push_device(fw_comm* c, fw_op* op, const int64_t* key, const int64_t* ts, const void* val,
+                         const int32_t* key_hash, int64_t n, int64_t local_wm, int64_t* combined_wm) {
+  if (!c || !op || n < 0 || (n > 0 && (!key || !ts || !val))) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
+  const bool hashed = op->cfg.key_kind == FW_KEY_HASHED;
+  if (hashed && n > 0 && !key_hash) return set_err(op, FW_ERR_ARG, "key_hash required for FW_KEY_HASHED");
+  int32_t kg0, kg1;
+  {
+    const int32_t M = op->cfg.max_parallelism, W = c->world, r = c->rank;
+    kg0 = (r * M + W - 1) / W;  // KeyGroupRangeAssignment.computeKeyGroupRangeForOperatorIndex (:85-99)
+    kg1 = ((r + 1) * M - 1) / W;
+  }
+  if (op->cfg.key_group_start != kg0 || op->cfg.key_group_end != kg1)
+    return set_err(op, FW_ERR_ARG, "the operator's KeyGroupRange [%d, %d] is not subtask %d of %d's [%d, %d]",
+                   op->cfg.key_group_start, op->cfg.key_group_end, c->rank, c->world, kg0, kg1);
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  int rc;
+  if ((rc = comm_reserve(op, c, std::max<int64_t>(n, 1)))) return rc;
+  const int W = c->world;
+  hipStream_t s = op->stream;
+  // group by destination subtask (stable), counts[W] on the device
+  fwdev::launch_route(key, ts, (const int64_t*)val, key_hash, op->cfg.key_kind, n, op->cfg.max_parallelism, W, c->sk,
+                      c->st, c->sv, c->sh, c->counts, (uint32_t*)c->scratch, s);
+  HIP_OR_RETURN(op, hipGetLastError());
+  c->h_counts[2 * W] = local_wm;
+  HIP_OR_RETURN(op, hipMemcpyAsync(c->counts + 2 * W, c->h_counts + 2 * W, sizeof(int64_t), hipMemcpyHostToDevice, s));
+  NCCL_OR_RETURN(op, ncclGroupStart());
+  NCCL_OR_RETURN(op, ncclAllToAll(c->counts, c->counts + W, 1, ncclInt64, c->nc, s));
+  NCCL_OR_RETURN(op, ncclAllReduce(c->counts + 2 * W, c->counts + 2 * W + 1, 1, ncclInt64, ncclMin, c->nc, s));
+  NCCL_OR_RETURN(op, ncclGroupEnd());
+  // the receive sizes: the one host round trip of the exchange
+  HIP_OR_RETURN(op, hipMemcpyAsync(c->h_counts, c->counts, (2 * W + 2) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HIP_OR_RETURN(op, hipStreamSynchronize(s));
+  std::vector<int64_t> soff(W + 1, 0), roff(W + 1, 0);
+  for (int p = 0; p < W; p++) {
+    soff[p + 1] = soff[p] + c->h_counts[p];
+    roff[p + 1] = roff[p] + c->h_counts[W + p];
+  }
+  const int64_t total = roff[W];
+  if (total > c->cap) {  // skew: more records arrive than this subtask sent; grow (keeping the routed columns)
+    int64_t *k2 = nullptr, *t2 = nullptr, *v2 = nullptr;
+    int32_t* h2 = nullptr;
+    HIP_OR_RETURN(op, dmalloc(&k2, (size_t)n));
+    HIP_OR_RETURN(op, dmalloc(&t2, (size_t)n));
+    HIP_OR_RETURN(op, dmalloc(&v2, (size_t)n));
+    HIP_OR_RETURN(op, dmalloc(&h2, (size_t)n));
+    HIP_OR_RETURN(op, hipMemcpyAsync(k2, c->sk, n * 8, hipMemcpyDeviceToDevice, s));
+    HIP_OR_RETURN(op, hipMemcpyAsync(t2, c->st, n * 8, hipMemcpyDeviceToDevice, s));
+    HIP_OR_RETURN(op, hipMemcpyAsync(v2, c->sv, n * 8, hipMemcpyDeviceToDevice, s));
+    HIP_OR_RETURN(op, hipMemcpyAsync(h2, c->sh, n * 4, hipMemcpyDeviceToDevice, s));
+    HIP_OR_RETURN(op, hipStreamSynchronize(s));
+    if ((rc = comm_reserve(op, c, total))) return rc;
+    HIP_OR_RETURN(op, hipMemcpyAsync(c->sk, k2, n * 8, hipMemcpyDeviceToDevice, s));
+    HIP_OR_RETURN(op, hipMemcpyAsync(c->st, t2, n * 8, hipMemcpyDeviceToDevice, s));
+    HIP_OR_RETURN(op, hipMemcpyAsync(c->sv, v2, n * 8, hipMemcpyDeviceToDevice, s));
+    HIP_OR_RETURN(op, hipMemcpyAsync(c->sh, h2, n * 4, hipMemcpyDeviceToDevice, s));
+    HIP_OR_RETURN(op, hipStreamSynchronize(s));
+    cfree(k2);
+    cfree(t2);
+    cfree(v2);
+    cfree(h2);
+  }
+  // the columns peer to peer: each peer pair over its own xGMI link
+  NCCL_OR_RETURN(op, ncclGroupStart());
+  for (int p = 0; p < W; p++) {
+    const size_t sc = (size_t)c->h_counts[p], rcn = (size_t)c->h_counts[W + p];
+    NCCL_OR_RETURN(op, ncclSend(c->sk + soff[p], sc, ncclInt64, p, c->nc, s));
+    NCCL_OR_RETURN(op, ncclSend(c->st + soff[p], sc, ncclInt64, p, c->nc, s));
+    NCCL_OR_RETURN(op, ncclSend(c->sv + soff[p], sc, ncclInt64, p, c->nc, s));
+    if (hashed) NCCL_OR_RETURN(op, ncclSend(c->sh + soff[p], sc, ncclInt32, p, c->nc, s));
+    NCCL_OR_RETURN(op, ncclRecv(c->rk + roff[p], rcn, ncclInt64, p, c->nc, s));
+    NCCL_OR_RETURN(op, ncclRecv(c->rt + roff[p], rcn, ncclInt64, p, c->nc, s));
+    NCCL_OR_RETURN(op, ncclRecv(c->rv + roff[p], rcn, ncclInt64, p, c->nc, s));
+    if (hashed) NCCL_OR_RETURN(op, ncclRecv(c->rh + roff[p], rcn, ncclInt32, p, c->nc, s));
+  }
+  NCCL_OR_RETURN(op, ncclGroupEnd());
+  if (combined_wm) *combined_wm = c->h_counts[2 * W + 1];
+  // processElement for the received batch (stream-ordered behind the receives)
+  return fw_push_batch_device(op, c->rk, c->rt, c->rv, hashed ? c->rh : nullptr, total);
 }
 
 int fw_generate_device(uint64_t seed, int64_t first, int64_t n, int64_t num_keys, const double* zipf_cdf,

@@ -8,10 +8,12 @@ on the receiving side; watermarks are broadcast to every channel and the receive
 over channels (flink-streaming-java/.../runtime/streamstatus/StatusWatermarkValve.java:173-191).
 
 On MI355X: the batch is grouped by destination on the GPU (fw_route_device, stable), the per-peer
-counts are exchanged (all_to_all_single of P int64), then the key, timestamp and value columns go
-peer-to-peer, one all_to_all_single each (RCCL over xGMI: each peer pair has its own link).  The watermark is one int64
-all_reduce(MIN).  The collectives are torch.distributed's, so the same code runs over "nccl" (RCCL) on
-the GPU box and over "gloo" in the CPU tests, where the caller supplies the routing function.
+counts are exchanged (all_to_all_single of P int64), then the key, timestamp and value columns (and the
+key hashes of String / Tuple keys) go peer-to-peer, one all_to_all_single each (RCCL over xGMI: each peer
+pair has its own link).  The watermark is one int64 all_reduce(MIN).  KeyGroupExchange uses
+torch.distributed's collectives, so the same code runs over "nccl" (RCCL) and over "gloo" (CUDA columns
+staged through host memory); NativeKeyByExchange is the same sequence inside libflinkwin.so
+(fw_keyby_push_device over the library's own RCCL communicator), the path a JNI host calls.
 """
 import ctypes
 
@@ -39,26 +41,41 @@ def route_device(keys, ts, vals, max_parallelism, parallelism, key_hash=None, ke
     return (ko, to, vo, ho), counts
 
 
-class KeyGroupExchange:
-    """Per-batch keyBy shuffle between the `world` operator subtasks (ranks) of one job vertex."""
+_KEY_KINDS = {"long": N.FW_KEY_LONG, "int": N.FW_KEY_INT, "hashed": N.FW_KEY_HASHED}
 
-    def __init__(self, max_parallelism, world, rank, route_fn=route_device, group=None):
+
+class KeyGroupExchange:
+    """Per-batch keyBy shuffle between the `world` operator subtasks (ranks) of one job vertex.
+    key_type: "long" (Long keys), "int" (Integer keys: Integer.hashCode) or "hashed" (the caller passes
+    key.hashCode() per record, which travels with the record)."""
+
+    def __init__(self, max_parallelism, world, rank, route_fn=route_device, group=None, key_type="long"):
         self.max_parallelism = max_parallelism
         self.world = world
         self.rank = rank
         self.route_fn = route_fn
         self.group = group
+        self.key_kind = _KEY_KINDS[key_type]
         self.key_group_range = compute_key_group_range_for_operator_index(max_parallelism, world, rank)
         self.bytes_sent = 0
 
-    def exchange(self, keys, ts, vals):
-        """Returns this rank's (keys, ts, vals): records from rank 0 first, then rank 1, ...,
-        each source's arrival order kept (the per-channel order Flink guarantees)."""
+    def exchange(self, keys, ts, vals, key_hash=None):
+        """Returns this rank's (keys, ts, vals) — and key hashes as a 4th column when key_hash is given:
+        records from rank 0 first, then rank 1, ..., each source's arrival order kept (the per-channel order
+        Flink guarantees)."""
         import torch
         import torch.distributed as dist
+        if self.key_kind == N.FW_KEY_HASHED and key_hash is None:
+            raise ValueError("key_hash is required for hashed (String / Tuple) keys")
         if self.world == 1:
-            return keys, ts, vals
-        (k, t, v, _), counts = self.route_fn(keys, ts, vals, self.max_parallelism, self.world)
+            return (keys, ts, vals) if key_hash is None else (keys, ts, vals, key_hash)
+        (k, t, v, h), counts = self.route_fn(keys, ts, vals, self.max_parallelism, self.world, key_hash=key_hash,
+                                             key_kind=self.key_kind)
+        # gloo moves host tensors: CUDA columns are staged through host memory (the nccl backend takes them as is)
+        staged = keys.is_cuda and dist.get_backend(self.group) == "gloo"
+        move = (lambda x: x.cpu()) if staged else (lambda x: x)
+        back = (lambda x: x.to(keys.device)) if staged else (lambda x: x)
+        counts = move(counts)
         recv_counts = torch.empty_like(counts)
         dist.all_to_all_single(recv_counts, counts, group=self.group)
         in_split = counts.tolist()
@@ -66,14 +83,16 @@ class KeyGroupExchange:
         total = sum(out_split)
         # one all-to-all per SoA column, straight from the routed columns into the operator's input
         # columns: no interleave before the send or split after it (each would cost 48 B/record of HBM)
+        cols = (k, t, v) + ((h,) if key_hash is not None else ())
         out = []
-        for col in (k, t, v):
+        for col in cols:
+            col = move(col)
             r = torch.empty(total, dtype=col.dtype, device=col.device)
             dist.all_to_all_single(r, col, output_split_sizes=out_split, input_split_sizes=in_split,
                                    group=self.group)
-            out.append(r)
-        self.bytes_sent += 24 * (sum(in_split) - in_split[self.rank])
-        return out[0], out[1], out[2]
+            out.append(back(r))
+        self.bytes_sent += (24 + (4 if key_hash is not None else 0)) * (sum(in_split) - in_split[self.rank])
+        return tuple(out)
 
     def combine_watermark(self, local_wm, device=None):
         """StatusWatermarkValve: the operator's input watermark is the minimum over its channels."""
@@ -86,4 +105,44 @@ class KeyGroupExchange:
         return int(t.item())
 
 
-del ctypes
+class NativeKeyByExchange:
+    """fw_keyby_push_device: route, count exchange, peer-to-peer columns and the push into the operator, all
+    inside libflinkwin.so over its own RCCL communicator (the sequence a JNI host calls).
+    `unique_id` (128 bytes) comes from rank 0's NativeKeyByExchange.new_unique_id(), shared by the caller."""
+
+    def __init__(self, op, world, rank, unique_id):
+        self.op = op
+        self.world, self.rank = world, rank
+        self._c = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(unique_id), 128)
+        rc = N.lib().fw_comm_init(buf, world, rank, op.device, ctypes.byref(self._c))
+        if rc != N.FW_OK:
+            raise N.NativeError(rc, "fw_comm_init failed")
+
+    @staticmethod
+    def new_unique_id():
+        buf = ctypes.create_string_buffer(128)
+        N.check(N.lib().fw_comm_unique_id(buf))
+        return buf.raw
+
+    def push(self, keys, ts, vals, local_wm, key_hash=None):
+        """Exchanges this subtask's device batch and pushes what it receives; returns the combined watermark."""
+        import torch
+        wm = ctypes.c_int64()
+        n = keys.numel()
+        # the library's stream reads the columns: it waits for their producer first
+        self.op._torch_stream(keys.device).wait_stream(torch.cuda.current_stream(keys.device))
+        rc = N.lib().fw_keyby_push_device(self._c, self.op._h, keys.data_ptr(), ts.data_ptr(), vals.data_ptr(),
+                                          key_hash.data_ptr() if key_hash is not None else None, n, int(local_wm),
+                                          ctypes.byref(wm))
+        N.check(rc, self.op._h)
+        self.op._inflight = (keys, ts, vals, key_hash)
+        return wm.value
+
+    def close(self):
+        if self._c:
+            N.lib().fw_comm_destroy(self._c)
+            self._c = None
+
+    def __del__(self):
+        self.close()

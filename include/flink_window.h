@@ -263,6 +263,27 @@ int fw_route_device(const int64_t* key, const int64_t* ts, const int64_t* val, c
                     int64_t scratch_bytes, void* stream);
 int64_t fw_route_scratch_bytes(int64_t n, int32_t parallelism);
 
+/* keyBy across the GPUs of one node behind the C-ABI (the RecordWriter -> KeyGroupStreamPartitioner ->
+ * network -> input gate path: flink-runtime/.../io/network/api/writer/RecordWriter.java:88-115,
+ * runtime/partitioner/KeyGroupStreamPartitioner.java:53-65; watermark valve runtime/streamstatus/
+ * StatusWatermarkValve.java:173-191), over RCCL.  One communicator per subtask / GPU:
+ *   fw_comm_unique_id: rank 0 creates the id (128 bytes) and hands it to the other subtasks (e.g. through the
+ *     JobManager); fw_comm_init: every subtask joins with its rank (= its operator index) on its device.
+ *   fw_keyby_push_device: this subtask's device batch is grouped by destination subtask
+ *     (computeOperatorIndexForKeyGroup), the per-peer counts are exchanged (all-to-all of one int64 each, then
+ *     read by the host: the receive sizes), the key / timestamp / value (/ key hash) columns go peer to peer
+ *     (grouped ncclSend / ncclRecv, one pair per peer), and the records received from subtasks 0 .. world-1, each
+ *     source's arrival order kept, are pushed into `op` (fw_push_batch_device), whose KeyGroupRange must be
+ *     computeKeyGroupRangeForOperatorIndex(maxParallelism, world, rank).  *combined_wm = min over the subtasks of
+ *     local_wm (the operator's input watermark), for the caller's fw_advance_watermark.  Collective: every
+ *     subtask calls it once per batch.  Enqueued on the handle's stream. */
+typedef struct fw_comm fw_comm;
+int fw_comm_unique_id(void* id128);
+int fw_comm_init(const void* id128, int32_t world, int32_t rank, int32_t device, fw_comm** out);
+void fw_comm_destroy(fw_comm* comm);
+int fw_keyby_push_device(fw_comm* comm, fw_op* op, const int64_t* key, const int64_t* ts, const void* val,
+                         const int32_t* key_hash, int64_t n, int64_t local_wm, int64_t* combined_wm);
+
 /* Synthetic source used by the benchmarks (the same counter-based generator as the CPU
  * baseline and the tests): record i of stream `seed` has
  *   key = splitmix64(seed ^ 4i) mod num_keys  (uniform)  or Zipf(zipf_s) over num_keys,

@@ -36,8 +36,8 @@ def _slice(rank, step):
     return generate_host(0x5EED, first, BATCH, KEYS, ts_base=0, rate=100_000, jitter=300)
 
 
-def _host_route(keys, ts, vals, max_par, par):
-    """CPU stand-in for fw_route_device: stable grouping by destination (test-side key groups)."""
+def _host_route(keys, ts, vals, max_par, par, key_hash=None, key_kind=0):
+    """CPU stand-in for fw_route_device: stable grouping by destination (test-side key groups; Long keys)."""
     import torch
     k = keys.numpy()
     dest = (orc.key_groups_long(k, max_par).astype(np.int64) * par) // max_par

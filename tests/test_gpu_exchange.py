@@ -1,0 +1,138 @@
+"""The keyBy exchange with the library's own kernels on the GPU:
+
+* world size 2 over gloo, both subtasks on cuda:0: fw_route_device groups each subtask's batch by destination
+  (computeOperatorIndexForKeyGroup, KeyGroupRangeAssignment.java:115-117), the columns (and the key hashes of
+  String keys) go through all_to_all_single, each subtask's GpuWindowOperator owns its KeyGroupRange, and the
+  watermark is the minimum over subtasks (StatusWatermarkValve.java:173-191).  The union of both subtasks'
+  rows must equal one oracle operator over the whole stream.  Long keys, Integer keys with negative values
+  (Integer.hashCode differs from Long.hashCode) and String keys hashed by the host.
+* fw_keyby_push_device (the C-ABI exchange over the library's RCCL communicator) at world size 1.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from flink_amd.datagen import generate_host
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+MAX_PAR, WORLD, BATCH, STEPS, KEYS = 128, 2, 20_000, 5, 3000
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _slice(rank, step, key_type):
+    from flink_amd.keygroups import string_hash_code
+    first = (step * WORLD + rank) * BATCH
+    k, t, v = generate_host(0x5EED, first, BATCH, KEYS, ts_base=0, rate=100_000, jitter=300)
+    h = None
+    if key_type == "int":
+        k = k - KEYS // 2  # negative Integer keys
+    elif key_type == "hashed":
+        h = np.array([string_hash_code(f"word-{x}") for x in range(KEYS)], dtype=np.int32)[k]
+    return k, t, v, h
+
+
+def _worker(rank, port, out_dir, key_type):
+    import torch
+    import torch.distributed as dist
+    from flink_amd import TumblingEventTimeWindows
+    from flink_amd.exchange import KeyGroupExchange
+    from flink_amd.operator import GpuWindowOperator
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    ex = KeyGroupExchange(MAX_PAR, WORLD, rank, key_type=key_type)
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(1000), key_type=key_type, max_parallelism=MAX_PAR,
+                           key_group_range=ex.key_group_range, device=0)
+    mx = -(1 << 63)
+    dev = torch.device("cuda", 0)
+    for s in range(STEPS):
+        k, t, v, h = _slice(rank, s, key_type)
+        mx = max(mx, int(t.max()))
+        cols = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (k, t, v)]
+        hk = torch.from_numpy(h).to(dev) if h is not None else None
+        got = ex.exchange(*cols, key_hash=hk)
+        wm = ex.combine_watermark(mx - 300)
+        op.process_batch(got[0], got[1], got[2], got[3] if hk is not None else None)
+        op.watermark(wm)
+    op.watermark((1 << 63) - 1)
+    np.save(os.path.join(out_dir, f"rows_{rank}.npy"), op.rows())
+    op.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("key_type", ["long", "int", "hashed"])
+def test_gpu_exchange_world2_library_route(tmp_path, key_type):
+    import torch.multiprocessing as mp
+    mp.spawn(_worker, args=(_free_port(), str(tmp_path), key_type), nprocs=WORLD, join=True)
+    rows = np.concatenate([np.load(tmp_path / f"rows_{r}.npy") for r in range(WORLD)])
+    # one operator over the whole stream, fed in the exchange's per-step source-major order, global watermarks
+    if key_type == "hashed":
+        return _check_hashed(rows)
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000)
+    mx = [-(1 << 63)] * WORLD
+    for s in range(STEPS):
+        parts = [_slice(r, s, key_type) for r in range(WORLD)]
+        for r in range(WORLD):
+            mx[r] = max(mx[r], int(parts[r][1].max()))
+        for src in range(WORLD):
+            ref.process(*parts[src][:3])
+        ref.watermark(min(m - 300 for m in mx))
+    ref.watermark((1 << 63) - 1)
+    _same(rows, ref.rows())
+
+
+def _same(rows, r):
+    key = lambda a: np.lexsort((a["start"], a["key"], a["epoch"]))  # noqa: E731
+    a, b = rows[key(rows)], r[key(r)]
+    assert len(a) == len(b) > 0
+    for f in ("epoch", "key", "start", "end", "count", "sum", "min", "max"):
+        np.testing.assert_array_equal(a[f], b[f])
+
+
+def _check_hashed(rows):
+    # String keys: per-word totals over the stream (the oracle keys by the dictionary id as a Long)
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000)
+    mx = [-(1 << 63)] * WORLD
+    for s in range(STEPS):
+        parts = [_slice(r, s, "hashed") for r in range(WORLD)]
+        for r in range(WORLD):
+            mx[r] = max(mx[r], int(parts[r][1].max()))
+        for src in range(WORLD):
+            ref.process(*parts[src][:3])
+        ref.watermark(min(m - 300 for m in mx))
+    ref.watermark((1 << 63) - 1)
+    _same(rows, ref.rows())
+
+
+def test_gpu_native_keyby_world1():
+    # the C-ABI exchange over the library's own RCCL communicator, one subtask: route, counts, self send/recv, push
+    import torch
+    from flink_amd import TumblingEventTimeWindows
+    from flink_amd.exchange import NativeKeyByExchange
+    from flink_amd.operator import GpuWindowOperator
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(1000), max_parallelism=MAX_PAR, device=0)
+    ex = NativeKeyByExchange(op, 1, 0, NativeKeyByExchange.new_unique_id())
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000)
+    mx = -(1 << 63)
+    dev = torch.device("cuda", 0)
+    for s in range(STEPS):
+        k, t, v, _ = _slice(0, s, "long")
+        mx = max(mx, int(t.max()))
+        wm = ex.push(*(torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (k, t, v)), mx - 300)
+        assert wm == mx - 300
+        op.watermark(wm)
+        ref.process(k, t, v)
+        ref.watermark(mx - 300)
+    op.watermark((1 << 63) - 1)
+    ref.watermark((1 << 63) - 1)
+    _same(op.rows(), ref.rows())
+    ex.close()
+    op.close()
