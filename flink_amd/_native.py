@@ -18,7 +18,7 @@ FW_ERR_UNSUPPORTED = -6
 FW_ERR_STATE = -7
 
 FW_TUMBLING, FW_SLIDING, FW_SESSION = 0, 1, 2
-FW_VAL_I64, FW_VAL_I32, FW_VAL_F64 = 0, 1, 2
+FW_VAL_I64, FW_VAL_I32, FW_VAL_F64, FW_VAL_I16, FW_VAL_I8, FW_VAL_F32 = 0, 1, 2, 3, 4, 5
 FW_KEY_LONG, FW_KEY_INT, FW_KEY_HASHED = 0, 1, 2
 FW_AGG_COUNT_SUM_MIN_MAX, FW_AGG_HLL, FW_AGG_FIRST, FW_AGG_MINBY, FW_AGG_MAXBY, FW_AGG_FIRST_MAX = 0, 1, 2, 3, 4, 5
 FW_AGG_TDIGEST = 6

@@ -302,12 +302,19 @@ __device__ __forceinline__ int64_t mn_out(const DevCfg& c, int64_t mn) {
 __device__ __forceinline__ int64_t mx_out(const DevCfg& c, int64_t mx) {
   return agg_first(c.agg) ? ~mx : c.vtype == FW_VAL_F64 ? f64_unsortable(mx) : mx;
 }
+// the sum in the field's type: Integer / Short / Byte sums wrap to their width (SumFunction.java:56-107), a Float
+// field's sum is rounded to float (its double bits)
+__device__ __forceinline__ int64_t sum_out(const DevCfg& c, int64_t s) {
+  if (c.vtype == FW_VAL_F64) return c.f32 ? __double_as_longlong((double)(float)__longlong_as_double(s)) : s;
+  return c.sum_bits == 32 ? (int64_t)(int32_t)s : c.sum_bits == 16 ? (int64_t)(int16_t)s
+       : c.sum_bits == 8 ? (int64_t)(int8_t)s : s;
+}
 __device__ __forceinline__ void write_row(const DevCfg& c, const DevRows& out, unsigned long long pos, const Entry& e) {
   out.key[pos] = e.key;
   out.start[pos] = e.start;
   out.end[pos] = e.end;
   out.cnt[pos] = e.cnt;
-  out.sum[pos] = c.vtype == FW_VAL_I32 ? (int64_t)(int32_t)e.sum : e.sum;
+  out.sum[pos] = sum_out(c, e.sum);
   out.mn[pos] = mn_out(c, e.mn);
   out.mx[pos] = mx_out(c, e.mx);
   if (agg_by(c.agg)) by_row(c.agg, c.vtype, e, &out.mn[pos], &out.mx[pos]);
@@ -3325,7 +3332,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_snapshot(DevCfg c, DevTable
       out.start[o] = e.start;
       out.end[o] = e.end;
       out.cnt[o] = e.cnt;
-      out.sum[o] = c.vtype == FW_VAL_I32 ? (int64_t)(int32_t)e.sum : e.sum;
+      out.sum[o] = sum_out(c, e.sum);
       out.mn[o] = mn_out(c, e.mn);
       out.mx[o] = mx_out(c, e.mx);
       if (agg_by(c.agg)) by_row(c.agg, c.vtype, e, &out.mn[o], &out.mx[o]);

@@ -67,6 +67,9 @@ struct DevCfg {
   int32_t log_s, P, log_r, wpr;  // wpr = max windows per record
   int64_t size, slide, offset, gap, lateness;
   int32_t diag;                  // FW_DIAG ablation bits (diagnostic builds of the timing only; 0 in production)
+  // the field's width (FW_VAL_I16 / I8 / F32 are kept as I32 / F64 inside): sums wrap to sum_bits (64, 32, 16
+  // or 8) and a Float field's sum is rounded to float, when rows and snapshots are written
+  int32_t sum_bits, f32;
   // sliding windows as panes (size % slide == 0, allowedLateness 0): the state holds one entry per
   // (key, pane) = (key, [p, p + slide)), and a window [s, s + size) is the merge of its size/slide
   // panes, formed when it fires.  An entry's meta is then the end - 1 of the earliest window it has

@@ -637,7 +637,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     snprintf(msg, sizeof msg, "unknown assigner %d", cfg.assigner);
   }
   if (!msg[0] && cfg.allowed_lateness < 0) snprintf(msg, sizeof msg, "The allowed lateness cannot be negative.");
-  if (!msg[0] && (cfg.value_type < FW_VAL_I64 || cfg.value_type > FW_VAL_F64))
+  if (!msg[0] && (cfg.value_type < FW_VAL_I64 || cfg.value_type > FW_VAL_F32))
     snprintf(msg, sizeof msg, "unknown value type %d", cfg.value_type);
   if (!msg[0] && (cfg.key_kind < FW_KEY_LONG || cfg.key_kind > FW_KEY_HASHED))
     snprintf(msg, sizeof msg, "unknown key kind %d", cfg.key_kind);
@@ -703,7 +703,11 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
 
   DevCfg& c = op->dc;
   c.assigner = cfg.assigner;
-  c.vtype = cfg.value_type;
+  // Short / Byte fields run as Integer and Float as Double inside; rows and snapshots take the field's width
+  c.vtype = cfg.value_type == FW_VAL_F32 ? FW_VAL_F64 : (cfg.value_type == FW_VAL_I16 || cfg.value_type == FW_VAL_I8)
+                                                           ? FW_VAL_I32 : cfg.value_type;
+  c.sum_bits = cfg.value_type == FW_VAL_I32 ? 32 : cfg.value_type == FW_VAL_I16 ? 16 : cfg.value_type == FW_VAL_I8 ? 8 : 64;
+  c.f32 = cfg.value_type == FW_VAL_F32;
   c.key_kind = cfg.key_kind;
   c.purging = cfg.purging;
   c.side_output = cfg.side_output;

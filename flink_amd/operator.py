@@ -127,7 +127,7 @@ class GpuWindowOperator:
                 raise ValueError("keys and timestamps must be int64")
             # fw_push_batch_device reads 8 bytes per value: a narrower column would be read out of bounds,
             # and a float64 / int64 mix would be reinterpreted as bits
-            want = torch.float64 if self.aggregate.value_type == "double" else torch.int64
+            want = torch.float64 if self.aggregate.value_type in ("double", "float") else torch.int64
             if values.dtype != want:
                 raise ValueError(f"values must be {want} for a {self.aggregate.value_type!r} aggregate, got {values.dtype}")
             if key_hash is not None and key_hash.dtype != torch.int32:
@@ -142,7 +142,7 @@ class GpuWindowOperator:
             keys = np.ascontiguousarray(keys, dtype=np.int64)
             timestamps = np.ascontiguousarray(timestamps, dtype=np.int64)
             values = np.asarray(values)
-            values = np.ascontiguousarray(values, dtype=np.float64 if self.aggregate.value_type == "double"
+            values = np.ascontiguousarray(values, dtype=np.float64 if self.aggregate.value_type in ("double", "float")
                                           else np.int64)
             kh = None
             if key_hash is not None:

@@ -144,18 +144,27 @@ class PurgingTrigger(Trigger):
         return PurgingTrigger(nested)
 
 
+# the field types of the built-in aggregations (SumFunction.java:34-107): Short / Byte sums wrap to their width,
+# Float fields are passed as doubles and their sums rounded to float
+VALUE_TYPES = {"long": N.FW_VAL_I64, "int": N.FW_VAL_I32, "double": N.FW_VAL_F64, "short": N.FW_VAL_I16,
+               "byte": N.FW_VAL_I8, "float": N.FW_VAL_F32}
+FLOAT_TYPES = ("double", "float")
+
+
 @dataclass(frozen=True)
 class CountSumMinMax:
     """The built-in AggregateFunction of the GPU path: ACC = OUT = (count, sum, min, max) of one
     numeric field.  `value_type` is "long" (sum wraps at 64 bits), "int" (SumFunction.IntSum:
-    wraps at 32 bits, so `sum(pos)` on an Integer field) or "double" (min/max by Double.compare,
-    sum within 1e-6 relative of the reference's left-to-right order).
+    wraps at 32 bits, so `sum(pos)` on an Integer field), "short" / "byte" (ShortSum / ByteSum: wrap at
+    16 / 8 bits), "double" (min/max by Double.compare, sum within 1e-6 relative of the reference's
+    left-to-right order) or "float" (the float values as doubles; FloatSum rounds every partial sum to
+    float, the GPU rounds the sum once: within 1e-5 relative).
     sum/min/max of WindowedStream (WindowedStream.java:1354-1535) are projections of this
     accumulator onto one field."""
     value_type: str = "long"
 
     def native(self):
-        return {"long": N.FW_VAL_I64, "int": N.FW_VAL_I32, "double": N.FW_VAL_F64}[self.value_type]
+        return VALUE_TYPES[self.value_type]
 
     def hll_precision(self):
         return 0
@@ -181,7 +190,7 @@ class FirstElementReduce:
     field: str = "sum"
 
     def native(self):
-        return {"long": N.FW_VAL_I64, "int": N.FW_VAL_I32, "double": N.FW_VAL_F64}[self.value_type]
+        return VALUE_TYPES[self.value_type]
 
     def hll_precision(self):
         return 0
@@ -204,7 +213,7 @@ class ExtremalElementReduce:
     value_type: str = "int"
 
     def native(self):
-        return {"long": N.FW_VAL_I64, "int": N.FW_VAL_I32, "double": N.FW_VAL_F64}[self.value_type]
+        return VALUE_TYPES[self.value_type]
 
     def hll_precision(self):
         return 0

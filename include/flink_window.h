@@ -44,6 +44,10 @@ extern "C" {
 #define FW_VAL_I64 0 /* Long field: sum wraps at 64 bits (SumFunction.LongSum)            */
 #define FW_VAL_I32 1 /* Integer field: sum wraps at 32 bits (SumFunction.IntSum)          */
 #define FW_VAL_F64 2 /* Double field: min/max by Double.compare, sum within 1e-6 relative */
+#define FW_VAL_I16 3 /* Short field: sum wraps at 16 bits (SumFunction.ShortSum); values sign-extended */
+#define FW_VAL_I8 4  /* Byte field: sum wraps at 8 bits (SumFunction.ByteSum); values sign-extended   */
+#define FW_VAL_F32 5 /* Float field passed as the double of the float: min/max by Float.compare, sum
+                        rounded to float (SumFunction.FloatSum adds in float: within 1e-5 relative)  */
 
 /* the AggregateFunction (fw_config.aggregate) */
 #define FW_AGG_COUNT_SUM_MIN_MAX 0 /* built-in {count, sum, min, max} accumulator                        */
@@ -124,7 +128,7 @@ typedef struct fw_op fw_op;
  * the built-in AggregateFunction.getResult {count, sum, min, max} plus the key and the
  * TimeWindow; the record timestamp of the row is end - 1 = TimeWindow.maxTimestamp()
  * (TimestampedCollector.setAbsoluteTimestamp, WindowOperator.java:544-548).  For
- * FW_VAL_F64, sum/min/max hold IEEE-754 bit patterns. */
+ * FW_VAL_F64 / FW_VAL_F32, sum/min/max hold IEEE-754 double bit patterns. */
 typedef struct fw_rows {
   int64_t* key;
   int64_t* start;

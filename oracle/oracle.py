@@ -13,9 +13,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
 
 TUMBLING, SLIDING, SESSION = 0, 1, 2
-VAL_I64, VAL_I32, VAL_F64 = 0, 1, 2
+VAL_I64, VAL_I32, VAL_F64, VAL_I16, VAL_I8, VAL_F32 = 0, 1, 2, 3, 4, 5
 _ASSIGNERS = {"tumbling": TUMBLING, "sliding": SLIDING, "session": SESSION}
-_VALTYPES = {"i64": VAL_I64, "i32": VAL_I32, "f64": VAL_F64}
+_VALTYPES = {"i64": VAL_I64, "i32": VAL_I32, "f64": VAL_F64, "i16": VAL_I16, "i8": VAL_I8, "f32": VAL_F32}
 
 
 class OracleCfg(ctypes.Structure):

@@ -360,8 +360,14 @@ class WindowOperatorOracle {
   // argument (SumAggregator.java:66-76, ComparableAggregator.java:72-94): the first element survives)
   // Comparator.MinByComparator / MaxByComparator order the field with compareTo: Long / Integer by value,
   // Double by Double.compare (Comparator.java:35-108)
+  bool is_float() const { return cfg.value_type == OR_VAL_F64 || cfg.value_type == OR_VAL_F32; }
+  // the sum in the field's type: Integer / Short / Byte sums wrap to their width (SumFunction.java:56-107)
+  int64_t wrap_sum(int64_t s) const {
+    return cfg.value_type == OR_VAL_I32 ? (int64_t)(int32_t)s : cfg.value_type == OR_VAL_I16 ? (int64_t)(int16_t)s
+         : cfg.value_type == OR_VAL_I8 ? (int64_t)(int8_t)s : s;
+  }
   int by_cmp(int64_t x, int64_t y) const {
-    if (cfg.value_type == OR_VAL_F64) return java_double_compare(bitsd(x), bitsd(y));
+    if (is_float()) return java_double_compare(bitsd(x), bitsd(y));
     return x < y ? -1 : x > y ? 1 : 0;
   }
   void acc_add(Acc& a, int64_t v) const {
@@ -380,7 +386,7 @@ class WindowOperatorOracle {
       return;
     }
     if (cfg.aggregate == OR_AGG_TDIGEST) a.td_buf.push_back(v);  // compressed at the end of the batch
-    if (cfg.value_type == OR_VAL_F64) {
+    if (is_float()) {
       double d = bitsd(v);
       if (a.cnt == 0) {
         a.dmn = a.dmx = d;
@@ -388,7 +394,8 @@ class WindowOperatorOracle {
         if (java_double_compare(d, a.dmn) < 0) a.dmn = d;
         if (java_double_compare(d, a.dmx) > 0) a.dmx = d;
       }
-      a.dsum += d;
+      // FloatSum adds in float (SumFunction.java:92-99): every partial sum rounds to float
+      a.dsum = cfg.value_type == OR_VAL_F32 ? (double)((float)a.dsum + (float)d) : a.dsum + d;
     } else {
       if (a.cnt == 0) {
         a.imn = a.imx = v;
@@ -424,8 +431,8 @@ class WindowOperatorOracle {
       for (size_t j = 0; j < r.regs.size(); j++) r.regs[j] = std::max(r.regs[j], b.regs[j]);
       return r;
     }
-    if (cfg.value_type == OR_VAL_F64) {
-      r.dsum = a.dsum + b.dsum;
+    if (is_float()) {
+      r.dsum = cfg.value_type == OR_VAL_F32 ? (double)((float)a.dsum + (float)b.dsum) : a.dsum + b.dsum;
       r.dmn = java_double_compare(b.dmn, a.dmn) < 0 ? b.dmn : a.dmn;
       r.dmx = java_double_compare(b.dmx, a.dmx) > 0 ? b.dmx : a.dmx;
     } else {
@@ -485,20 +492,20 @@ class WindowOperatorOracle {
       double est;
       hll_result(a.regs, cfg.hll_p, &est, &r.min, &r.max);
       memcpy(&r.sum, &est, 8);
-    } else if (cfg.value_type == OR_VAL_F64) {
+    } else if (is_float()) {
       r.sum = dbits(a.dsum);
       r.min = dbits(a.dmn);
       r.max = dbits(a.dmx);
       // keep raw (non-canonical) sum bits: sums are compared with tolerance
       memcpy(&r.sum, &a.dsum, 8);
     } else {
-      r.sum = cfg.value_type == OR_VAL_I32 ? (int64_t)(int32_t)a.isum : a.isum;
+      r.sum = wrap_sum(a.isum);
       r.min = a.imn;
       r.max = a.imx;
     }
     if (cfg.aggregate == OR_AGG_FIRST) r.max = a.first;
     if (cfg.aggregate == OR_AGG_FIRST_MAX) {  // max(pos): the first element with the field's maximum
-      r.min = cfg.value_type == OR_VAL_F64 ? dbits(a.dmx) : a.imx;
+      r.min = is_float() ? dbits(a.dmx) : a.imx;
       r.max = a.first;
     }
     if (cfg.aggregate == OR_AGG_MINBY || cfg.aggregate == OR_AGG_MAXBY) {
@@ -778,7 +785,8 @@ struct CountWindowOracle {
       r.sum = jadd(r.sum, e.val);
       r.min = std::min(r.min, e.val);
     }
-    if (value_type == OR_VAL_I32) r.sum = (int64_t)(int32_t)r.sum;
+    r.sum = value_type == OR_VAL_I32 ? (int64_t)(int32_t)r.sum : value_type == OR_VAL_I16 ? (int64_t)(int16_t)r.sum
+          : value_type == OR_VAL_I8 ? (int64_t)(int8_t)r.sum : r.sum;
     r.max = s.list.front().ord;
     rows.push_back(r);
     if (evict_after) evict(s.list);

@@ -34,7 +34,9 @@ extern "C" {
 #endif
 
 enum { OR_TUMBLING = 0, OR_SLIDING = 1, OR_SESSION = 2 };
-enum { OR_VAL_I64 = 0, OR_VAL_I32 = 1, OR_VAL_F64 = 2 };
+/* Long / Integer / Double fields, and Short / Byte (sums wrap to the width: SumFunction.ShortSum / ByteSum)
+ * and Float (sums added in float, SumFunction.FloatSum; values passed as f64 bits of the float) */
+enum { OR_VAL_I64 = 0, OR_VAL_I32 = 1, OR_VAL_F64 = 2, OR_VAL_I16 = 3, OR_VAL_I8 = 4, OR_VAL_F32 = 5 };
 
 /* error codes returned by oracle_process / oracle_watermark */
 enum {

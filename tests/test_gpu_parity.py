@@ -14,7 +14,7 @@ from tests.parity_util import assert_rows_equal, assert_side_equal
 pytestmark = pytest.mark.gpu
 
 KATS = load_kats()
-_VT = {"i64": "long", "i32": "int", "f64": "double"}
+_VT = {"i64": "long", "i32": "int", "f64": "double", "i16": "short", "i8": "byte", "f32": "float"}
 
 
 def _gpu_op(assigner, size=0, slide=0, offset=0, gap=0, lateness=0, purging=False, side_output=False,
@@ -906,3 +906,30 @@ def test_gpu_sessions_many_in_flight_per_key(purging):
     assert_rows_equal(g, r)
     assert gl == rl
     assert (r["key"] == 0).sum() > 600  # the hot key's sessions (and their late firings)
+
+
+NARROW_CONFIGS = [
+    dict(assigner="tumbling", size=1000),
+    dict(assigner="sliding", size=3000, slide=1000),
+    dict(assigner="session", gap=300, lateness=200),
+]
+
+
+@pytest.mark.parametrize("first", [False, True], ids=["count_sum", "sum_passthrough"])
+@pytest.mark.parametrize("value_type", ["i16", "i8", "f32"])
+@pytest.mark.parametrize("cfg", NARROW_CONFIGS, ids=[c["assigner"] for c in NARROW_CONFIGS])
+def test_gpu_short_byte_float_fields(cfg, value_type, first):
+    # a9: Short / Byte sums wrap to their width (SumFunction.ShortSum / ByteSum), Float sums add in float
+    # (FloatSum), min/max by compareTo (SumFunction.java:34-107, ComparableAggregator.java:72-94)
+    batches, wms = _stream(120_000, 15_000, 2000, bound=400, jitter=900, rate=100_000)
+    if value_type == "i16":
+        conv = lambda v: ((v & 0xFFFF) - 0x8000).astype(np.int64)  # noqa: E731
+    elif value_type == "i8":
+        conv = lambda v: ((v & 0xFF) - 0x80).astype(np.int64)  # noqa: E731
+    else:
+        # positive values: a float sum's error relative to the sum stays at float precision (no cancellation)
+        conv = lambda v: ((v & 0xFFFFF).astype(np.float32) / np.float32(3.0) + 1).astype(np.float64)  # noqa: E731
+    batches = [(k, t, conv(v)) for k, t, v in batches]
+    cfg = dict(cfg, value_type=value_type, first=first)
+    g, r, *_ = _run_both(cfg, batches, wms)
+    assert_rows_equal(g, r, _VT[value_type])
