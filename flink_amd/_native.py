@@ -17,7 +17,7 @@ FW_ERR_CAPACITY = -5
 FW_ERR_UNSUPPORTED = -6
 FW_ERR_STATE = -7
 
-FW_TUMBLING, FW_SLIDING, FW_SESSION = 0, 1, 2
+FW_TUMBLING, FW_SLIDING, FW_SESSION, FW_COUNT = 0, 1, 2, 3
 FW_VAL_I64, FW_VAL_I32, FW_VAL_F64, FW_VAL_I16, FW_VAL_I8, FW_VAL_F32 = 0, 1, 2, 3, 4, 5
 FW_KEY_LONG, FW_KEY_INT, FW_KEY_HASHED = 0, 1, 2
 FW_AGG_COUNT_SUM_MIN_MAX, FW_AGG_HLL, FW_AGG_FIRST, FW_AGG_MINBY, FW_AGG_MAXBY, FW_AGG_FIRST_MAX = 0, 1, 2, 3, 4, 5
@@ -38,7 +38,8 @@ class FwConfig(ctypes.Structure):
                 ("expected_entries", ctypes.c_int64), ("max_batch", ctypes.c_int64),
                 ("aggregate", ctypes.c_int32), ("hll_precision", ctypes.c_int32),
                 ("tdigest_compression", ctypes.c_int32), ("tdigest_export", ctypes.c_int32),
-                ("tdigest_quantiles", ctypes.c_double * 3)]
+                ("tdigest_quantiles", ctypes.c_double * 3), ("count_evict_after", ctypes.c_int32),
+                ("pad0", ctypes.c_int32)]
 
 
 class FwRows(ctypes.Structure):

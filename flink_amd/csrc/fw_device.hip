@@ -2906,6 +2906,164 @@ __global__ __launch_bounds__(64) void k_td_large_compact(DevCfg c, TdBuf td, Sta
   }
 }
 
+// ---- count windows (FW_COUNT): KeyedStream.countWindow(size, slide) = GlobalWindows + CountTrigger.of(slide) +
+// CountEvictor.of(size) (KeyedStream.java:383-397).  EvictingWindowOperator.processElement appends the element to
+// the key's list and CountTrigger.onElement fires every slide-th element of the key (CountTrigger.java:47-55);
+// the fire evicts all but the last `size` (CountEvictor.java:63-78) and reduces them in arrival order
+// (EvictingWindowOperator.java:334-366).  With CountEvictor.of(size, true) the eviction follows the function,
+// so the fired list is the last size + slide elements once it is that long: the window length wl.
+// On the GPU: every record gets its key's slot, the batch is sorted stably by slot, so a key's records form one run in arrival order, the record at rank r of its run is the
+// key's element number seq = count + r + 1; it fires when seq % slide == 0 over the elements seq - w + 1 .. seq
+// (w = min(wl, seq)), read from the run and from the key's ring of its last wl - 1 earlier elements.
+__device__ __forceinline__ int32_t cnt_slot(const DevCount& cw, int64_t key, Status* st) {
+  uint32_t s = (uint32_t)fmix64((uint64_t)key ^ 0x3C6EF372FE94F82Bull) & cw.cap_mask;
+  for (uint32_t probes = 0; probes <= cw.cap_mask;) {
+    const uint32_t cur = __hip_atomic_load(&cw.mstate[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == 2) {
+      if (cw.mkey[s] == key) {
+        const uint32_t slot = cw.mslot[s];
+        if (slot >= (uint32_t)cw.max_keys) break;  // a key refused earlier stays refused
+        return (int32_t)slot;
+      }
+      s = (s + 1) & cw.cap_mask;
+      probes++;
+      continue;
+    }
+    if (cur == 1) continue;  // being published by another lane: re-read
+    if (atomicCAS(&cw.mstate[s], 0u, 1u) == 0u) {
+      const int32_t slot = atomicAdd(cw.nslots, 1);
+      cw.mkey[s] = key;
+      cw.mslot[s] = (uint32_t)slot;
+      __hip_atomic_store(&cw.mstate[s], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (slot >= cw.max_keys) {
+        atomicOr(&st->flags, FW_STATUS_STATE_LOST);
+        return -1;
+      }
+      return slot;
+    }
+  }
+  atomicOr(&st->flags, FW_STATUS_STATE_LOST);
+  return -1;
+}
+__global__ __launch_bounds__(256) void k_cnt_slots(DevCount cw, const int64_t* __restrict__ key, int64_t n,
+                                                   uint32_t none, Status* st) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t slot = cnt_slot(cw, key[i], st);
+    cw.sk[0][i] = slot < 0 ? none : (uint32_t)slot;
+    cw.sv[0][i] = (uint32_t)i;
+  }
+}
+__global__ __launch_bounds__(256) void k_cnt_bounds(DevCount cw, const uint32_t* __restrict__ sk, int64_t n,
+                                                    uint32_t none) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = sk[i];
+    if (g == none) continue;
+    if (i == 0 || sk[i - 1] != g) cw.sbeg[g] = (int32_t)i;
+    if (i == n - 1 || sk[i + 1] != g) cw.send[g] = (int32_t)(i + 1);
+  }
+}
+// the reduce of one fire: SumAggregator over the window's elements in arrival order (integer sums wrap, so their
+// order does not matter; Double sums add left to right, Float sums round each partial sum to float)
+__global__ __launch_bounds__(256) void k_cnt_fire(DevCfg c, DevCount cw, const uint32_t* __restrict__ sk,
+                                                  const uint32_t* __restrict__ sv, const int64_t* __restrict__ key,
+                                                  const int64_t* __restrict__ val, int64_t n, uint32_t none, DevRows out,
+                                                  Status* st) {
+  const int64_t ring = cw.wl - 1;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = i0 + threadIdx.x;
+    bool fire = false;
+    Entry e;
+    if (i < n && sk[i] != none) {
+      const uint32_t g = sk[i];
+      const int64_t r = i - cw.sbeg[g], before = cw.cnt[g], seq = before + r + 1;
+      if (seq % cw.slide == 0) {
+        fire = true;
+        const int64_t w = min(cw.wl, seq);
+        e.key = key[sv[i]];
+        e.start = LMIN;
+        e.end = LMAX;
+        e.cnt = w;
+        double ds = 0.0, dm = 0.0;
+        int64_t is = 0, im = LMAX;
+        for (int64_t q = seq - w + 1; q <= seq; q++) {  // oldest first
+          int64_t v, o;
+          if (q > before) {
+            const uint32_t b = sv[i - (seq - q)];
+            v = val[b];
+            o = c.ord_base + (int64_t)b;
+          } else {
+            const int64_t at = (int64_t)g * ring + (q - 1) % ring;
+            v = cw.ring_v[at];
+            o = cw.ring_o[at];
+          }
+          if (q == seq - w + 1) e.mx = o;  // the window's first element
+          if (c.vtype == FW_VAL_F64) {
+            const double d = __longlong_as_double(v);
+            ds = q == seq - w + 1 ? d : c.f32 ? (double)((float)ds + (float)d) : ds + d;
+            if (q == seq - w + 1 || f64_sortable(v) < f64_sortable(__double_as_longlong(dm))) dm = d;
+          } else {
+            is = jadd(is, v);
+            im = min(im, v);
+          }
+        }
+        if (c.vtype == FW_VAL_F64) {
+          e.sum = __double_as_longlong(ds);
+          e.mn = __double_as_longlong(dm);
+          if ((e.mn & 0x7ff0000000000000ll) == 0x7ff0000000000000ll && (e.mn & 0x000fffffffffffffll))
+            e.mn = 0x7ff8000000000000ll;  // Double.doubleToLongBits: canonical NaN
+        } else {
+          e.sum = sum_out(c, is);
+          e.mn = im;
+        }
+      }
+    }
+    // one reservation per wave
+    const uint64_t m = __ballot(fire);
+    if (!m) continue;
+    unsigned long long base = 0;
+    const int leader = __ffsll((long long)m) - 1;
+    if ((int)__lane_id() == leader) base = atomicAdd(&st->out_rows, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (!fire) continue;
+    const unsigned long long pos = base + __popcll(m & lanemask_lt());
+    if ((int64_t)pos < out.cap) {
+      out.key[pos] = e.key;
+      out.start[pos] = e.start;
+      out.end[pos] = e.end;
+      out.cnt[pos] = e.cnt;
+      out.sum[pos] = e.sum;
+      out.mn[pos] = e.mn;
+      out.mx[pos] = e.mx;
+    } else {
+      atomicOr(&st->flags, FW_STATUS_OUT_FULL);
+    }
+  }
+}
+// after every fire of the batch read them: the key's ring takes its last wl - 1 elements, its count the run's length
+__global__ __launch_bounds__(256) void k_cnt_update(DevCfg c, DevCount cw, const uint32_t* __restrict__ sk,
+                                                    const uint32_t* __restrict__ sv, const int64_t* __restrict__ val,
+                                                    int64_t n, uint32_t none) {
+  const int64_t ring = cw.wl - 1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = sk[i];
+    if (g == none) continue;
+    const int64_t b0 = cw.sbeg[g], len = cw.send[g] - b0, r = i - b0, before = cw.cnt[g];
+    if (ring > 0 && r >= len - ring) {
+      const int64_t at = (int64_t)g * ring + (before + r) % ring;  // element number before + r + 1
+      cw.ring_v[at] = val[sv[i]];
+      cw.ring_o[at] = c.ord_base + (int64_t)sv[i];
+    }
+  }
+}
+// then the counts (a kernel of their own: the ring update read them)
+__global__ __launch_bounds__(256) void k_cnt_count(DevCount cw, const uint32_t* __restrict__ sk, int64_t n, uint32_t none) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = sk[i];
+    if (g == none || (i + 1 < n && sk[i + 1] == g)) continue;  // the last record of the key's run
+    cw.cnt[g] += cw.send[g] - cw.sbeg[g];
+  }
+}
+
 struct FireDecision {
   bool fire, keep;
 };
@@ -3650,6 +3808,30 @@ void launch_fire(const DevCfg& c0, int64_t wm, DevTable tb, DevRows out, Status*
   hipLaunchKernelGGL(k_fire, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, wm, tb, out, st);
 }
 
+size_t count_sort_bytes(int64_t n) {
+  size_t a = 0;
+  rocprim::double_buffer<uint32_t> ks(nullptr, nullptr), vs(nullptr, nullptr);
+  (void)rocprim::radix_sort_pairs(nullptr, a, ks, vs, (size_t)n, 0, 32);
+  return a;
+}
+void launch_count(const DevCfg& c, DevCount& cw, const int64_t* key, const int64_t* val, int64_t n, DevRows out,
+                  Status* st, hipStream_t s) {
+  if (n <= 0) return;
+  const uint32_t none = (uint32_t)cw.max_keys;
+  unsigned bits = 1;
+  while (((int64_t)1 << bits) <= cw.max_keys) bits++;
+  const unsigned grid = (unsigned)std::min<int64_t>(8192, (n + 255) / 256);
+  hipLaunchKernelGGL(k_cnt_slots, dim3(grid), dim3(256), 0, s, cw, key, n, none, st);
+  rocprim::double_buffer<uint32_t> ks(cw.sk[0], cw.sk[1]), vs(cw.sv[0], cw.sv[1]);
+  size_t bytes = cw.tmp_bytes;
+  (void)rocprim::radix_sort_pairs(cw.tmp, bytes, ks, vs, (size_t)n, 0, bits, s);  // stable: arrival order per key
+  const uint32_t* sk = ks.current();
+  const uint32_t* sv = vs.current();
+  hipLaunchKernelGGL(k_cnt_bounds, dim3(grid), dim3(256), 0, s, cw, sk, n, none);
+  hipLaunchKernelGGL(k_cnt_fire, dim3(grid), dim3(256), 0, s, c, cw, sk, sv, key, val, n, none, out, st);
+  hipLaunchKernelGGL(k_cnt_update, dim3(grid), dim3(256), 0, s, c, cw, sk, sv, val, n, none);
+  hipLaunchKernelGGL(k_cnt_count, dim3(grid), dim3(256), 0, s, cw, sk, n, none);
+}
 size_t tdigest_sort_bytes(int64_t n) {
   size_t a = 0, b = 0;
   rocprim::double_buffer<uint64_t> kv(nullptr, nullptr);

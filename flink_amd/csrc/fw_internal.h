@@ -269,6 +269,27 @@ struct TdBuf {
   int32_t sel;              // which of gs / v holds the sorted batch (set by launch_tdigest)
 };
 
+// ---- count windows (FW_COUNT): per key its element count and a ring of its last size-1 elements
+struct DevCount {
+  int64_t* mkey;        // [cap] key map: keys (open addressing)
+  uint32_t* mstate;     // [cap] 0 empty, 1 being claimed, 2 taken
+  uint32_t* mslot;      // [cap] the key's slot
+  int32_t* nslots;      // slots handed out
+  int64_t* cnt;         // [max_keys] elements of the key so far (CountTrigger's count, the list's length)
+  int64_t* ring_v;      // [max_keys * (wl - 1)] the key's last wl - 1 values, at (seq - 1) % (wl - 1)
+  int64_t* ring_o;      //                             and their arrival ordinals
+  uint32_t cap_mask;
+  int32_t max_keys;
+  int64_t size, slide;
+  int64_t wl;           // the fired window's length: size (evict before) or size + slide (evict after)
+  uint32_t* sk[2];      // per batch: sort keys (slot) / values (batch index), double-buffered for the sort
+  uint32_t* sv[2];
+  void* tmp;
+  size_t tmp_bytes;
+  int32_t* sbeg;        // [max_keys] the key's run in the sorted batch
+  int32_t* send;
+};
+
 // columns of keyed-state snapshot rows (fw_state_rows, device side)
 struct StateCols {
   int64_t *key, *start, *end, *cnt, *sum, *mn, *mx, *timer;
@@ -304,6 +325,10 @@ void launch_hll_update(const DevCfg& c, const PRec* part, const uint32_t* offs, 
 void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
                     TdBuf& td, Status* st, hipStream_t_ s);
 size_t tdigest_sort_bytes(int64_t n);  // rocPRIM scratch of the two sorts
+// FW_COUNT: one batch of count windows (key slots, stable sort by key, fire, ring update); val = the push's values
+void launch_count(const DevCfg& c, DevCount& cw, const int64_t* key, const int64_t* val, int64_t n, DevRows out,
+                  Status* st, hipStream_t_ s);
+size_t count_sort_bytes(int64_t n);
 void launch_rehash(const DevCfg& old_c, DevTable old_t, const DevCfg& new_c, DevTable new_t, hipStream_t_ s);
 void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t_ s);
 void launch_reset_regions(const DevCfg& c, DevTable tb, hipStream_t_ s);

@@ -76,6 +76,7 @@ struct fw_op {
   uint32_t taint_epoch = 0;  // sessions: epoch of the latest batch's taint set (DevCfg.taint_*)
   AggHot hot{};              // split-partition buffers (allocated by the first batch that may need them)
   TdBuf td{};                // FW_AGG_TDIGEST: per-push compression buffers
+  DevCount cw{};             // FW_COUNT: count-window state
   bool td_export = false;    // FW_AGG_TDIGEST: fired rows keep their centroids (DevRows::dig)
 
   DevRows out{};
@@ -512,8 +513,27 @@ int maybe_restart_rows(fw_op* op) {
   return FW_OK;
 }
 
+// FW_COUNT: count windows fire while the batch is processed; no state table, timers or suspension
+int push_count(fw_op* op, const int64_t* key, const int64_t* val, int64_t n) {
+  int rc;
+  if ((rc = settle(op)) || (rc = maybe_restart_rows(op))) return rc;
+  const int64_t rows = (int64_t)op->h_status->out_rows;
+  // a key fires at most ceil(r / slide) times for its r elements of the batch
+  const int64_t most = std::min<int64_t>(n, n / op->cw.slide + std::min<int64_t>(n, op->cw.max_keys));
+  if ((rc = ensure_out_capacity(op, rows + most, rows)))
+    return rc;
+  DevCfg c = op->dc;
+  c.ord_base = op->records_in;
+  fwdev::launch_count(c, op->cw, key, val, n, op->out, op->d_status, op->stream);
+  HIP_OR_RETURN(op, hipGetLastError());
+  op->records_in += n;
+  op->push_unsettled = true;
+  return snapshot(op);
+}
+
 int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int64_t n) {
   if (n == 0) return FW_OK;
+  if (op->cfg.assigner == FW_COUNT) return push_count(op, key, val, n);
   int rc;
   DevCfg c = op->dc;  // by value: a session batch stamps its taint epoch into it
   // queue the batch-only kernels before waiting for the previous sequence, except with side
@@ -633,6 +653,11 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
       snprintf(msg, sizeof msg, "a sliding window may overlap at most 2^20 others (size / slide)");
   } else if (cfg.assigner == FW_SESSION) {
     if (cfg.gap <= 0) snprintf(msg, sizeof msg, "EventTimeSessionWindows parameters must satisfy 0 < size");
+  } else if (cfg.assigner == FW_COUNT) {
+    if (cfg.size <= 0 || cfg.slide <= 0 || cfg.size > (1 << 16) || cfg.slide > (1 << 16))
+      snprintf(msg, sizeof msg, "count windows need 0 < size <= 65536 and 0 < slide <= 65536");
+    else if (cfg.aggregate != FW_AGG_FIRST)
+      snprintf(msg, sizeof msg, "count windows are offered for countWindow(size, slide).sum(pos) (FW_AGG_FIRST)");
   } else {
     snprintf(msg, sizeof msg, "unknown assigner %d", cfg.assigner);
   }
@@ -833,6 +858,36 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     HIP_OR_RETURN(op, dmalloc(&t.lidx, (size_t)op->table_slots));
     t.lidx_slots = op->table_slots;
   }
+  if (cfg.assigner == FW_COUNT) {
+    DevCount& w = op->cw;
+    w.size = cfg.size;
+    w.slide = cfg.slide;
+    w.wl = cfg.count_evict_after ? cfg.size + cfg.slide : cfg.size;
+    w.max_keys = (int32_t)std::min<int64_t>(cfg.expected_entries > 0 ? cfg.expected_entries : (1 << 20), 1 << 30);
+    const int64_t cap = next_pow2(2 * (int64_t)w.max_keys);
+    w.cap_mask = (uint32_t)(cap - 1);
+    HIP_OR_RETURN(op, dmalloc(&w.mkey, (size_t)cap));
+    HIP_OR_RETURN(op, dmalloc(&w.mstate, (size_t)cap));
+    HIP_OR_RETURN(op, hipMemsetAsync(w.mstate, 0, (size_t)cap * sizeof(uint32_t), op->stream));
+    HIP_OR_RETURN(op, dmalloc(&w.mslot, (size_t)cap));
+    HIP_OR_RETURN(op, dmalloc(&w.nslots, 1));
+    HIP_OR_RETURN(op, hipMemsetAsync(w.nslots, 0, sizeof(int32_t), op->stream));
+    HIP_OR_RETURN(op, dmalloc(&w.cnt, (size_t)w.max_keys));
+    HIP_OR_RETURN(op, hipMemsetAsync(w.cnt, 0, (size_t)w.max_keys * sizeof(int64_t), op->stream));
+    const size_t ring = (size_t)w.max_keys * (size_t)std::max<int64_t>(1, w.wl - 1);
+    if (ring * 16 > (size_t(64) << 30))
+      return set_err(op, FW_ERR_CAPACITY, "count windows: expected_entries * (window length - 1) * 16 B exceeds 64 GiB");
+    HIP_OR_RETURN(op, dmalloc(&w.ring_v, ring));
+    HIP_OR_RETURN(op, dmalloc(&w.ring_o, ring));
+    for (int b = 0; b < 2; b++) {
+      HIP_OR_RETURN(op, dmalloc(&w.sk[b], (size_t)mb));
+      HIP_OR_RETURN(op, dmalloc(&w.sv[b], (size_t)mb));
+    }
+    w.tmp_bytes = fwdev::count_sort_bytes(mb);
+    HIP_OR_RETURN(op, dmalloc((uint8_t**)&w.tmp, w.tmp_bytes));
+    HIP_OR_RETURN(op, dmalloc(&w.sbeg, (size_t)w.max_keys));
+    HIP_OR_RETURN(op, dmalloc(&w.send, (size_t)w.max_keys));
+  }
   HIP_OR_RETURN(op, dmalloc(&op->prog.rb, (size_t)c.P));
   HIP_OR_RETURN(op, dmalloc(&op->prog.tp, (size_t)c.P * FW_AGG_THREADS));
   HIP_OR_RETURN(op, dmalloc(&op->prog.done, (size_t)c.P));
@@ -891,6 +946,22 @@ void fw_destroy(fw_op* op) {
     dfree(t.nstart);
     dfree(t.ostart);
     dfree(t.lidx);
+    DevCount& w = op->cw;
+    dfree(w.mkey);
+    dfree(w.mstate);
+    dfree(w.mslot);
+    dfree(w.nslots);
+    dfree(w.cnt);
+    dfree(w.ring_v);
+    dfree(w.ring_o);
+    for (int b = 0; b < 2; b++) {
+      dfree(w.sk[b]);
+      dfree(w.sv[b]);
+    }
+    uint8_t* wt = (uint8_t*)w.tmp;
+    dfree(wt);
+    dfree(w.sbeg);
+    dfree(w.send);
   }
   dfree(op->dc.taint_state);
   free_hot(op->hot);
@@ -949,6 +1020,13 @@ int fw_advance_watermark(fw_op* op, int64_t wm, int64_t* n_pending) {
   if (!op) return FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;
+  if (op->cfg.assigner == FW_COUNT) {  // GlobalWindow: nothing fires by time (GlobalWindows.java NeverTrigger)
+    op->wm = wm;
+    if (!n_pending) return FW_OK;
+    if ((rc = settle(op))) return rc;
+    *n_pending = (int64_t)op->h_status->out_rows - op->out_base;
+    return FW_OK;
+  }
   // settled: the host knows the row count; unsettled: the ordered path left cap - table slots free
   // and an earlier watermark of the sequence found the buffer with that room as well
   if (!op->unsynced) {
@@ -1158,9 +1236,9 @@ void free_state_cols(StateCols& c) {
 }  // namespace
 
 int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64_t cap, int64_t* n) {
-  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_TDIGEST))  // not in fw_state_rows
-    return set_err(op, FW_ERR_UNSUPPORTED,
-                   "keyed-state snapshots of the HyperLogLog and t-digest aggregates are not offered");
+  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_TDIGEST || op->cfg.assigner == FW_COUNT))
+    return set_err(op, FW_ERR_UNSUPPORTED,  // not in fw_state_rows
+                   "keyed-state snapshots of the HyperLogLog and t-digest aggregates and of count windows are not offered");
   if (!op || !n) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;
@@ -1199,9 +1277,9 @@ int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64
 }
 
 int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_t n) {
-  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_TDIGEST))  // not in fw_state_rows
-    return set_err(op, FW_ERR_UNSUPPORTED,
-                   "keyed-state snapshots of the HyperLogLog and t-digest aggregates are not offered");
+  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_TDIGEST || op->cfg.assigner == FW_COUNT))
+    return set_err(op, FW_ERR_UNSUPPORTED,  // not in fw_state_rows
+                   "keyed-state snapshots of the HyperLogLog and t-digest aggregates and of count windows are not offered");
   if (!op || (n > 0 && !src) || n < 0) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;

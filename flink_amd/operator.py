@@ -244,6 +244,8 @@ class GpuWindowOperator:
         # processElement raises at once in the reference: wait for the batch and surface its errors
         self.process_batch(keys, ts, vals, key_hash)
         self.synchronize()
+        if self.assigner.kind == N.FW_COUNT:  # count windows fire while the elements are processed
+            self._rows.append(self.drain_rows(self.epoch))
 
     def watermark(self, wm):
         self._rows.append(self.process_watermark(wm))

@@ -118,6 +118,32 @@ class EventTimeSessionWindows(WindowAssigner):
         return f"EventTimeSessionWindows({self.gap})"
 
 
+class CountWindows(WindowAssigner):
+    """KeyedStream.countWindow(size, slide) = window(GlobalWindows.create()).evictor(CountEvictor.of(size))
+    .trigger(CountTrigger.of(slide)), and countWindow(size) = PurgingTrigger.of(CountTrigger.of(size))
+    (KeyedStream.java:383-397): every slide-th element of a key fires its last `size` elements (the last
+    size + slide with evict_after, CountEvictor.of(size, true)).  Rows have start = Long.MIN_VALUE, end =
+    Long.MAX_VALUE (GlobalWindow) and are emitted while the elements are processed."""
+    kind = N.FW_COUNT
+    is_event_time = False
+
+    def __init__(self, size, slide=None, evict_after=False):
+        slide = size if slide is None else slide
+        if size <= 0 or slide <= 0:
+            raise ValueError("count windows need positive size and slide")
+        self.size, self.slide, self.evict_after = int(size), int(slide), bool(evict_after)
+
+    @staticmethod
+    def of(size, slide=None, evict_after=False):
+        return CountWindows(size, slide, evict_after)
+
+    def config(self):
+        return dict(assigner=self.kind, size=self.size, slide=self.slide, count_evict_after=int(self.evict_after))
+
+    def __repr__(self):
+        return f"CountWindows({self.size}, {self.slide})"
+
+
 class Trigger:
     purging = False
 

@@ -40,6 +40,15 @@ extern "C" {
 #define FW_TUMBLING 0 /* api/windowing/assigners/TumblingEventTimeWindows.java:53-73 */
 #define FW_SLIDING 1  /* api/windowing/assigners/SlidingEventTimeWindows.java:57-81   */
 #define FW_SESSION 2  /* api/windowing/assigners/EventTimeSessionWindows.java:59-61  */
+#define FW_COUNT 3    /* count windows: KeyedStream.countWindow(size, slide) = GlobalWindows + CountTrigger.of(slide) +
+                         CountEvictor.of(size) (api/datastream/KeyedStream.java:383-397; EvictingWindowOperator.java
+                         :102-239,334-366; CountTrigger.java:47-55; CountEvictor.java:63-78), and countWindow(size) =
+                         PurgingTrigger.of(CountTrigger.of(size)) with slide = size.  Every slide-th element of a key
+                         fires the key's last min(size, elements) elements, reduced in arrival order, while the
+                         element is processed (no timers; watermarks only delimit the output).  Rows: start =
+                         Long.MIN_VALUE, end = Long.MAX_VALUE (GlobalWindow, timestamp Long.MAX_VALUE), count, sum,
+                         min, and max = the arrival ordinal of the window's first element (the passthrough fields of
+                         sum(pos)); aggregate must be FW_AGG_FIRST.  expected_entries bounds the distinct keys. */
 
 #define FW_VAL_I64 0 /* Long field: sum wraps at 64 bits (SumFunction.LongSum)            */
 #define FW_VAL_I32 1 /* Integer field: sum wraps at 32 bits (SumFunction.IntSum)          */
@@ -120,6 +129,9 @@ typedef struct fw_config {
   int32_t tdigest_export;      /* FW_AGG_TDIGEST: 1 = fired rows also keep their centroids for
                                   fw_drain_digests                                             */
   double tdigest_quantiles[3]; /* FW_AGG_TDIGEST: the quantiles of a row (all 0 -> .5 .95 .99) */
+  int32_t count_evict_after;   /* FW_COUNT: 1 = CountEvictor.of(size, true): evict after the window function
+                                  (the fired window is the last min(elements, size + slide)) */
+  int32_t pad0;
 } fw_config;
 
 typedef struct fw_op fw_op;

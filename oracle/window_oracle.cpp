@@ -781,12 +781,27 @@ struct CountWindowOracle {
     r.end = LMAX;
     r.count = (int64_t)s.list.size();
     r.min = LMAX;
-    for (const Elem& e : s.list) {
-      r.sum = jadd(r.sum, e.val);
-      r.min = std::min(r.min, e.val);
+    const bool fl = value_type == OR_VAL_F64 || value_type == OR_VAL_F32;
+    double ds = 0.0, dm = 0.0;
+    bool first = true;
+    for (const Elem& e : s.list) {  // ReduceFunction applied in order: SumAggregator / SumFunction
+      if (fl) {
+        const double d = bitsd(e.val);
+        ds = first ? d : value_type == OR_VAL_F32 ? (double)((float)ds + (float)d) : ds + d;
+        if (first || java_double_compare(d, dm) < 0) dm = d;
+      } else {
+        r.sum = jadd(r.sum, e.val);
+        r.min = std::min(r.min, e.val);
+      }
+      first = false;
     }
-    r.sum = value_type == OR_VAL_I32 ? (int64_t)(int32_t)r.sum : value_type == OR_VAL_I16 ? (int64_t)(int16_t)r.sum
-          : value_type == OR_VAL_I8 ? (int64_t)(int8_t)r.sum : r.sum;
+    if (fl) {
+      memcpy(&r.sum, &ds, 8);
+      r.min = dbits(dm);
+    } else {
+      r.sum = value_type == OR_VAL_I32 ? (int64_t)(int32_t)r.sum : value_type == OR_VAL_I16 ? (int64_t)(int16_t)r.sum
+            : value_type == OR_VAL_I8 ? (int64_t)(int8_t)r.sum : r.sum;
+    }
     r.max = s.list.front().ord;
     rows.push_back(r);
     if (evict_after) evict(s.list);

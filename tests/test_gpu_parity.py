@@ -933,3 +933,86 @@ def test_gpu_short_byte_float_fields(cfg, value_type, first):
     cfg = dict(cfg, value_type=value_type, first=first)
     g, r, *_ = _run_both(cfg, batches, wms)
     assert_rows_equal(g, r, _VT[value_type])
+
+
+def _count_op(size, slide, evict_after=False, value_type="i64", **kw):
+    from flink_amd import CountWindows
+    from flink_amd.operator import GpuWindowOperator
+    return GpuWindowOperator(CountWindows.of(size, slide, evict_after), FirstElementReduce(_VT[value_type], "sum"),
+                             **kw)
+
+
+def _count_rows(rows):
+    return sorted(tuple(int(r[f]) for f in ("key", "start", "end", "count", "sum", "min", "max")) for r in rows)
+
+
+@pytest.mark.parametrize("case", KATS["count_windows"], ids=[c["name"] for c in KATS["count_windows"]])
+def test_gpu_count_window_kats(case):
+    # a14: EvictingWindowOperatorTest count-trigger / count-evictor sequences, compared as a sorted multiset
+    # after each phase (TestHarnessUtil.assertOutputEqualsSorted)
+    from collections import Counter
+    op = _count_op(case["size"], case["slide"], case["evict_after"])
+    ids = {"key1": 1, "key2": 2}
+    names = {v: k for k, v in ids.items()}
+    expected = Counter()
+    for ph in case["phases"]:
+        k = np.array([ids[x] for x, _ in ph["input"]], dtype=np.int64)
+        op.process(k, np.zeros_like(k), np.array([v for _, v in ph["input"]], dtype=np.int64))
+        expected.update(tuple(e) for e in ph["expected"])
+        assert Counter((names[int(r["key"])], int(r["sum"])) for r in op.rows()) == expected
+    assert all(r["end"] == (1 << 63) - 1 and r["start"] == -(1 << 63) for r in op.rows())
+    op.close()
+
+
+COUNT_CONFIGS = [(10, 5, False), (10, 10, False), (7, 3, False), (4, 6, False), (4, 2, True), (5, 3, True),
+                 (1, 1, False)]
+
+
+@pytest.mark.parametrize("value_type", ["i64", "i32", "f64", "i16", "f32"])
+@pytest.mark.parametrize("size,slide,after", COUNT_CONFIGS, ids=[f"{a}_{b}_{c}" for a, b, c in COUNT_CONFIGS])
+def test_gpu_count_windows_vs_oracle(size, slide, after, value_type):
+    # WindowWordCount's countWindow(10, 5).sum(1) and its tumbling / evict-after variants over ragged batches
+    # (a key's run straddles pushes, so fired windows read the ring of earlier elements); rows bit-exact
+    keys, _, vals = generate_host(0xC0DE, 0, 60_000, 700, ts_base=0, rate=1_000_000, jitter=0, zipf_s=1.05)
+    if value_type == "f64":
+        vals = (vals & 0xFFFFF).astype(np.float64) / 7.0
+    elif value_type == "f32":
+        vals = ((vals & 0xFFFFF).astype(np.float32) / np.float32(3.0) + 1).astype(np.float64)
+    elif value_type == "i16":
+        vals = ((vals & 0xFFFF) - 0x8000).astype(np.int64)
+    elif value_type == "i32":
+        vals = ((vals & 0xFFFFFFFF) - (1 << 31)).astype(np.int64)
+    gpu = _count_op(size, slide, after, value_type, expected_entries=1024)
+    ref = orc.CountWindowOracle(size, slide, after, value_type=value_type)
+    cuts = [0, 1, 17, 4096, 4097, 20_000, 20_001, 45_000, 60_000]
+    for a, b in zip(cuts, cuts[1:]):
+        gpu.process(keys[a:b], np.zeros(b - a, dtype=np.int64), vals[a:b])
+        ref.process(keys[a:b], vals[a:b].view(np.int64) if vals.dtype == np.float64 else vals[a:b])
+        gpu.watermark(b)  # watermarks fire nothing for GlobalWindows
+    g, r = gpu.rows(), ref.rows()
+    assert len(g) == len(r) > 0
+    assert _count_rows(g) == _count_rows(r)
+    gpu.close()
+
+
+def test_gpu_count_windows_device_batches_and_capacity():
+    # device-resident pushes of a larger stream; then a stream with more distinct keys than expected_entries
+    # is refused with FW_ERR_CAPACITY rather than dropping elements
+    import torch
+    from flink_amd import _native as N
+    keys, _, vals = generate_host(7, 0, 1 << 20, 50_000, ts_base=0, rate=1_000_000, jitter=0)
+    gpu = _count_op(10, 5, expected_entries=1 << 16)
+    ref = orc.CountWindowOracle(10, 5, value_type="i64")
+    for b in range(0, len(keys), 1 << 18):
+        sl = slice(b, b + (1 << 18))
+        kd, vd = torch.from_numpy(keys[sl]).cuda(), torch.from_numpy(vals[sl]).cuda()
+        gpu.process(kd, torch.zeros_like(kd), vd)
+        ref.process(keys[sl], vals[sl])
+    assert _count_rows(gpu.rows()) == _count_rows(ref.rows())
+    gpu.close()
+    small = _count_op(10, 5, expected_entries=100)
+    with pytest.raises(N.NativeError) as ei:
+        k = np.arange(1000, dtype=np.int64)
+        small.process(k, k, k)
+    assert ei.value.code == N.FW_ERR_CAPACITY
+    small.close()

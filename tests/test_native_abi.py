@@ -53,6 +53,8 @@ def _create(**kw):
     (dict(assigner=N.FW_TUMBLING, size=10, allowed_lateness=-1), "The allowed lateness cannot be negative"),
     (dict(assigner=N.FW_TUMBLING, size=10, max_parallelism=(1 << 15) + 1), "Operator parallelism not within"),
     (dict(assigner=N.FW_TUMBLING, size=10, key_group_start=5, key_group_end=200), "invalid KeyGroupRange"),
+    (dict(assigner=N.FW_COUNT, size=0, slide=5, aggregate=N.FW_AGG_FIRST), "count windows need 0 < size"),
+    (dict(assigner=N.FW_COUNT, size=10, slide=5), "count windows are offered for countWindow"),
 ])
 def test_create_rejects_invalid_config(kw, msg):
     rc, m = _create(**kw)
@@ -86,3 +88,13 @@ def test_struct_layouts_match_header(tmp_path):
     assert [getattr(N.FwConfig, f).offset for f in fields] == out[1:]
     assert ctypes.sizeof(N.FwRows) == 56
     assert ctypes.sizeof(N.FwStats) == 13 * 8
+
+
+def test_count_windows_assigner_config():
+    from flink_amd import CountWindows
+    c = CountWindows.of(10, 5).config()
+    assert c == dict(assigner=N.FW_COUNT, size=10, slide=5, count_evict_after=0)
+    assert CountWindows.of(4).config()["slide"] == 4  # countWindow(size): tumbling
+    assert CountWindows.of(4, 2, evict_after=True).config()["count_evict_after"] == 1
+    with pytest.raises(ValueError):
+        CountWindows.of(0)
