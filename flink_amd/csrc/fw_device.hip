@@ -530,13 +530,38 @@ __device__ __forceinline__ int32_t tile_of_block(int32_t T) {
   return g * per + min(g, rem) + (b >> 3);
 }
 
+// The streaming kernels are instantiated for the common shapes too: Long keys with tumbling windows, and Long
+// keys with panes.  The configuration is then known to the compiler (the generic instantiation's branches for
+// other assigners, key kinds and session taint drop out of the per-record loop).
+enum { M_GEN = 0, M_TUMB = 1, M_PANE = 2 };
+template <int MODE>
+__device__ __forceinline__ void specialize(DevCfg& c) {
+  if constexpr (MODE == M_TUMB) {
+    c.assigner = FW_TUMBLING;
+    c.panes = 0;
+    c.wpr = 1;
+    c.key_kind = FW_KEY_LONG;
+  } else if constexpr (MODE == M_PANE) {
+    c.assigner = FW_SLIDING;
+    c.panes = 1;
+    c.key_kind = FW_KEY_LONG;
+  }
+}
+__host__ __forceinline__ int stream_mode(const DevCfg& c) {
+  if (c.key_kind != FW_KEY_LONG) return M_GEN;
+  if (c.assigner == FW_TUMBLING) return M_TUMB;
+  return c.panes ? M_PANE : M_GEN;
+}
+
 // ---- K1: classify + partition histogram.  hist is (P+1) x T, partition-major; row P counts
 // the records of each tile that go to the ordered path (scanned with the partitions), row P+1
 // keeps that count unscanned for k_scatter_ordered.
+template <int MODE>
 __global__ __launch_bounds__(FW_TILE_THREADS) void k_classify_hist(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
                                                                    const int64_t* __restrict__ ts,
                                                                    const int32_t* __restrict__ kh, int64_t n, int32_t T,
                                                                    uint32_t* __restrict__ hist, Status* st) {
+  specialize<MODE>(c);
   extern __shared__ uint32_t lh[];
   for (int i = threadIdx.x; i <= c.P; i += blockDim.x) lh[i] = 0;
   __syncthreads();
@@ -672,12 +697,14 @@ __device__ __forceinline__ void store_pair(PRec* part, bool valid, uint32_t pos,
 
 // ---- K2: scatter.  Normal records -> their partition's run (any order inside the run), one
 // 32-byte sector per record; late records -> side output / counter.
+template <int MODE>
 __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
                                                              const int64_t* __restrict__ ts,
                                                              const int64_t* __restrict__ val,
                                                              const int32_t* __restrict__ kh, int64_t n, int32_t T,
                                                              const uint32_t* __restrict__ offs, PRec* __restrict__ part,
                                                              DevSide side, Status* st) {
+  specialize<MODE>(c);
   extern __shared__ uint32_t base[];  // P: next free slot of each partition's run for this tile
   const int32_t tile = tile_of_block(T);
   for (int i = threadIdx.x; i < c.P; i += blockDim.x) base[i] = offs[(int64_t)i * T + tile];
@@ -755,21 +782,25 @@ __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(D
   if (late) atomicAdd(&st->late_dropped, late);
 }
 
-// ---- K2b: ordered compaction of the ordered-path records of a tile (skipped by tiles that have none)
+// ---- K2b: ordered compaction of the ordered-path records of a tile (skipped by tiles that have none).
+// srow: the scanned ordered-path counts per tile, then the raw counts.  G: a gathered batch (tiles of
+// FW_GTILE; a normal record without a compact form takes the ordered path, as k_stage decided)
+template <bool G>
 __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_ordered(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
                                                                      const int64_t* __restrict__ ts,
                                                                      const int64_t* __restrict__ val,
                                                                      const int32_t* __restrict__ kh, int64_t n,
-                                                                     int32_t T, const uint32_t* __restrict__ offs,
-                                                                     const uint32_t* __restrict__ tile_slow,
+                                                                     int32_t T, const uint32_t* __restrict__ srow,
                                                                      int64_t* __restrict__ sk, int64_t* __restrict__ stt,
                                                                      int64_t* __restrict__ sv, int32_t* __restrict__ skh, const Status* st) {
+  const uint32_t* tile_slow = srow + T;
   if (tile_slow[blockIdx.x] == 0) return;
   const int taint = c.assigner == FW_SESSION ? st->taint_any : 0;
   __shared__ uint32_t wtot[FW_TILE_THREADS / 64];
-  const uint32_t slow_base = offs[(int64_t)c.P * T + blockIdx.x] - offs[(int64_t)c.P * T];
-  const int64_t tbase = (int64_t)blockIdx.x * FW_TILE;
-  const int64_t tend = min(n, tbase + (int64_t)FW_TILE);
+  const uint32_t slow_base = srow[blockIdx.x] - srow[0];
+  constexpr int64_t TL = G ? FW_GTILE : FW_TILE;
+  const int64_t tbase = (int64_t)blockIdx.x * TL;
+  const int64_t tend = min(n, tbase + TL);
   const int lane = __lane_id(), wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   uint32_t running = 0;
   for (int64_t j = tbase; j < tend; j += blockDim.x) {
@@ -783,7 +814,12 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_ordered(DevCfg c, i
       v = val[i];
       h = key_hash_of(c.key_kind, k, kh, i);
       p = partition_of(c, k, h);
-      if (p >= 0) cls = classify(c, wm, t, nullptr, nullptr, k, taint);
+      if (p >= 0) {
+        int64_t last = 0;
+        int nw = 0;
+        cls = classify(c, wm, t, &last, &nw, k, taint);
+        if (G && cls == CLS_NORMAL && compact_delta(c, last) < 0) cls = CLS_SLOW;
+      }
     }
     const bool is_slow = cls == CLS_SLOW;
     const uint64_t ball = __ballot(is_slow);
@@ -805,6 +841,263 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_ordered(DevCfg c, i
     }
     running += tot;
     __syncthreads();
+  }
+}
+
+// ---- K2 (gathered batches): classify + tile-local partition sort.  A workgroup takes one tile of FW_GTILE
+// records (8 per thread, in registers), ranks each normal record in its partition with an LDS counter, scans
+// the counters into the tile's partition runs, places the records' compact form (CRec) in LDS at their run
+// slots and writes the sorted tile back with whole-line stores.  rt[tile][p] = run start | count << 16 (the
+// aggregate gathers partition p's runs from every tile); srow[tile] = srow[T8 + tile] = the tile's
+// ordered-path records, among them the normal records without a compact form (their window is out of the
+// batch's compact range).  Late records go to the side output / late counter here.
+template <int MODE>
+__global__ __launch_bounds__(FW_TILE_THREADS) void k_stage(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
+                                                           const int64_t* __restrict__ ts, const int64_t* __restrict__ val,
+                                                           const int32_t* __restrict__ kh, int64_t n, int32_t T8,
+                                                           i64x2* __restrict__ part, uint32_t* __restrict__ rt,
+                                                           uint32_t* __restrict__ srow, DevSide side, Status* st) {
+  specialize<MODE>(c);
+  constexpr int R = FW_GTILE / FW_TILE_THREADS;  // records per thread (even: pairs)
+  extern __shared__ __align__(16) uint8_t lds_raw[];
+  i64x2* stg = reinterpret_cast<i64x2*>(lds_raw);                         // FW_GTILE records
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(stg + FW_GTILE);            // P run counters, then run starts
+  __shared__ uint32_t wsum[FW_TILE_THREADS / 64 + 1];
+  __shared__ uint32_t slow_s;
+  for (int i = threadIdx.x; i < c.P; i += FW_TILE_THREADS) cnt[i] = 0;
+  if (threadIdx.x == 0) slow_s = 0;
+  __syncthreads();
+  const int32_t tile = blockIdx.x;
+  const int64_t tbase = (int64_t)tile * FW_GTILE;
+  const int64_t tend = min(n, tbase + (int64_t)FW_GTILE);
+  int64_t k[R], t[R], v[R];
+  int32_t hh[R];
+  load_records<R / 2, true>(c, key, ts, val, kh, tbase, tend, k, t, v, hh);
+  uint32_t pr[R];  // partition << 16 | rank, or ~0u
+  int64_t kw[R];
+  unsigned slow = 0, bad_kg = 0, bad_ts = 0;
+  unsigned long long late = 0;
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+    pr[j] = ~0u;
+    kw[j] = 0;
+    const int64_t i = rec_index(tbase, j >> 1, j & 1);
+    if (i >= tend) continue;
+    const int32_t h = c.key_kind == FW_KEY_HASHED ? hh[j] : key_hash_of(c.key_kind, k[j], kh, i);
+    const int32_t p = partition_of(c, k[j], h);
+    if (p < 0) {
+      bad_kg++;
+      continue;
+    }
+    int64_t last = 0;
+    int nw = 0;
+    const int cls = classify(c, wm, t[j], &last, &nw, k[j], 0);
+    if (cls == CLS_NORMAL) {
+      const int64_t d = compact_delta(c, last);
+      if (d < 0) {
+        slow++;  // no compact form: the ordered path takes it (k_scatter_ordered<true> decides the same)
+      } else {
+        kw[j] = compact_encode(c, k[j], d);
+        pr[j] = ((uint32_t)p << 16) | atomicAdd(&cnt[p], 1u);
+      }
+    } else if (cls == CLS_SLOW) {
+      slow++;
+    } else if (cls == CLS_LATE) {
+      if (c.side_output)
+        side_one(side, st, k[j], t[j], v[j]);
+      else
+        late++;
+    } else if (cls == CLS_BADTS) {
+      bad_ts++;
+    }
+  }
+  if (slow) atomicAdd(&slow_s, slow);
+  __syncthreads();
+  // exclusive scan of the run counters (P <= FW_GMAX_P: at most 2 per thread), in place into run starts
+  constexpr int PPT = FW_GMAX_P / FW_TILE_THREADS;
+  uint32_t a[PPT], tot = 0;
+#pragma unroll
+  for (int q = 0; q < PPT; q++) {
+    const int pp = threadIdx.x * PPT + q;
+    a[q] = pp < c.P ? cnt[pp] : 0u;
+    tot += a[q];
+  }
+  uint32_t total;
+  uint32_t ex = block_excl_scan(tot, wsum, &total);
+#pragma unroll
+  for (int q = 0; q < PPT; q++) {
+    const int pp = threadIdx.x * PPT + q;
+    if (pp < c.P) {
+      cnt[pp] = ex;
+      rt[(int64_t)tile * c.P + pp] = ex | (a[q] << 16);
+    }
+    ex += a[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < R; j++)
+    if (pr[j] != ~0u) stg[cnt[pr[j] >> 16] + (pr[j] & 0xffffu)] = i64x2{kw[j], v[j]};
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < total; i += FW_TILE_THREADS) part[tbase + i] = stg[i];
+  if (threadIdx.x == 0) {
+    srow[tile] = slow_s;
+    srow[T8 + tile] = slow_s;
+  }
+  if (late) atomicAdd(&st->late_dropped, late);
+  if (bad_kg) atomicAdd(&st->kg_errors, (int)bad_kg);
+  if (bad_ts) atomicAdd(&st->ts_errors, (int)bad_ts);
+}
+// the runs table [T8][P] -> [P][T8] through 64 x 64 LDS tiles; tot[p] += the runs' counts (the partitions'
+// record counts, scanned afterwards into their virtual offsets)
+__global__ __launch_bounds__(1024) void k_rt_transpose(const uint32_t* __restrict__ rt, uint32_t* __restrict__ rt_t,
+                                                        int32_t T8, int32_t P, uint32_t* __restrict__ tot) {
+  __shared__ uint32_t sq[64][65];
+  const int32_t t0 = blockIdx.x * 64, p0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 16
+  for (int r = ty; r < 64; r += 16) {
+    const int32_t t = t0 + r, p = p0 + tx;
+    sq[r][tx] = (t < T8 && p < P) ? rt[(int64_t)t * P + p] : 0u;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 16) {
+    const int32_t p = p0 + r, t = t0 + tx;
+    const uint32_t w = sq[tx][r];
+    if (p < P && t < T8) rt_t[(int64_t)p * T8 + t] = w;
+    uint32_t c = w >> 16;  // the row's counts over these 64 tiles
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (tx == 0 && p < P && c) atomicAdd(&tot[p], c);
+  }
+}
+
+// A gathered batch's partition (k_stage): its records are runs in every tile.  The workgroup keeps the
+// partition's row of the runs table in LDS: pre[t] = records of the partition in tiles < t, s0[t] = the run's
+// start inside tile t; base = the partition's virtual offset (record indices are base + 0 .. base + count - 1).
+struct GatherRuns {
+  const uint32_t* pre;
+  const uint16_t* s0;
+  int32_t nt;
+  int64_t base;
+};
+// the last tile t in [lo, hi] with pre[t] <= r
+__device__ __forceinline__ int32_t gather_tile(const GatherRuns& g, uint32_t r, int32_t lo, int32_t hi) {
+  while (lo < hi) {
+    const int32_t mid = (lo + hi + 1) >> 1;
+    if (g.pre[mid] <= r) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+// the CRec index of record i: the tile whose run holds it (the last t with pre[t] <= i - base), then the slot.
+// A wave's lanes hold consecutive records: the wave first finds the tile of its first record (every lane reads
+// the same LDS words), then each lane searches the next 64 tiles (runs average FW_GTILE / P records)
+__device__ __forceinline__ int64_t gather_index(const GatherRuns& g, int64_t i) {
+  const uint32_t r = (uint32_t)(i - g.base);
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);
+  const int32_t t0 = gather_tile(g, r0 < r ? r0 : r, 0, g.nt - 1);
+  int32_t lo = t0, hi = min(t0 + 63, g.nt - 1);
+  if (g.pre[hi] <= r) {
+    lo = hi;
+    hi = g.nt - 1;
+  }
+  const int32_t t = gather_tile(g, r, lo, hi);
+  return (int64_t)t * FW_GTILE + g.s0[t] + (r - g.pre[t]);
+}
+// ---- K2c (gathered batches): plan and regroup.  k_gplan (one workgroup): the partitions' counts -> their
+// virtual offsets (exclusive scan, total at P), the regroup's chunks per partition (FW_REGROUP_CHUNK records
+// each, at least one) -> cbase (exclusive scan, total at P), and the ordered-path row's scan (srow).
+__global__ __launch_bounds__(FW_TILE_THREADS) void k_gplan(uint32_t* __restrict__ voffs, uint32_t* __restrict__ cbase,
+                                                           int32_t P, uint32_t* __restrict__ srow, int32_t t8) {
+  __shared__ uint32_t sw[FW_TILE_THREADS / 64 + 1];
+  constexpr int PPT = FW_GMAX_P / FW_TILE_THREADS;
+  static_assert(FW_GMAX_T <= FW_GMAX_P, "one scan width");
+  uint32_t a[PPT], ch[PPT], sa = 0, sc = 0, ss[PPT], s_tot = 0;
+#pragma unroll
+  for (int q = 0; q < PPT; q++) {
+    const int i = threadIdx.x * PPT + q;
+    a[q] = i < P ? voffs[i] : 0u;
+    ch[q] = i < P ? max(1u, (a[q] + FW_REGROUP_CHUNK - 1) / FW_REGROUP_CHUNK) : 0u;
+    ss[q] = i < t8 ? srow[i] : 0u;
+    sa += a[q];
+    sc += ch[q];
+    s_tot += ss[q];
+  }
+  uint32_t ta, tc, ts;
+  uint32_t ea = block_excl_scan(sa, sw, &ta);
+  uint32_t ec = block_excl_scan(sc, sw, &tc);
+  uint32_t es = block_excl_scan(s_tot, sw, &ts);
+#pragma unroll
+  for (int q = 0; q < PPT; q++) {
+    const int i = threadIdx.x * PPT + q;
+    if (i < P) {
+      voffs[i] = ea;
+      cbase[i] = ec;
+    }
+    if (i < t8) srow[i] = es;
+    ea += a[q];
+    ec += ch[q];
+    es += ss[q];
+  }
+  if (threadIdx.x == 0) {
+    voffs[P] = ta;
+    cbase[P] = tc;
+  }
+}
+// One workgroup per chunk of a partition: copies the chunk's records out of the tiles' runs into the
+// partition's contiguous run at its virtual offset (the partition-major layout every aggregate reads).
+// Consecutive chunks (so consecutive partitions) run on one XCD (blocks b, b + 8, ... take consecutive
+// ones): their runs sit side by side in each tile, so the gathered lines are read once through that L2.
+__global__ __launch_bounds__(FW_REGROUP_THREADS) void k_regroup(const i64x2* __restrict__ src, i64x2* __restrict__ dst,
+                                                               const uint32_t* __restrict__ rt_t, int32_t t8,
+                                                               const uint32_t* __restrict__ voffs,
+                                                               const uint32_t* __restrict__ cbase, int32_t P) {
+  __shared__ uint32_t pre[FW_GMAX_T];
+  __shared__ uint16_t s0[FW_GMAX_T];
+  __shared__ uint32_t sw[FW_REGROUP_THREADS / 64 + 1];
+  const uint32_t vb = (gridDim.x & 7) == 0 ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  if (vb >= cbase[P]) return;
+  int32_t lo = 0, hi = P - 1;  // the last partition whose first chunk <= vb
+  while (lo < hi) {
+    const int32_t mid = (lo + hi + 1) >> 1;
+    if (cbase[mid] <= vb) lo = mid; else hi = mid - 1;
+  }
+  const int32_t p = lo;
+  const uint32_t total = voffs[p + 1] - voffs[p];
+  const uint32_t cb = (vb - cbase[p]) * FW_REGROUP_CHUNK, ce = min(total, cb + FW_REGROUP_CHUNK);
+  const uint32_t* row = rt_t + (int64_t)p * t8;
+  constexpr int TPT = FW_GMAX_T / FW_REGROUP_THREADS;
+  uint32_t cnt[TPT], tot = 0;
+#pragma unroll
+  for (int q = 0; q < TPT; q++) {
+    const int t = threadIdx.x * TPT + q;
+    const uint32_t w = t < t8 ? row[t] : 0u;
+    if (t < t8) s0[t] = (uint16_t)(w & 0xffffu);
+    cnt[q] = w >> 16;
+    tot += cnt[q];
+  }
+  uint32_t all;
+  uint32_t e = block_excl_scan(tot, sw, &all);
+#pragma unroll
+  for (int q = 0; q < TPT; q++) {
+    const int t = threadIdx.x * TPT + q;
+    if (t < t8) pre[t] = e;
+    e += cnt[q];
+  }
+  __syncthreads();
+  const GatherRuns g{pre, s0, t8, 0};
+  i64x2* out = dst + voffs[p];
+  constexpr int RR = 4;
+  for (uint32_t b = cb; b < ce; b += FW_REGROUP_THREADS * RR) {
+    i64x2 r[RR];
+#pragma unroll
+    for (int j = 0; j < RR; j++) {
+      const uint32_t i = b + j * FW_REGROUP_THREADS + threadIdx.x;
+      if (i < ce) r[j] = src[gather_index(g, i)];
+    }
+#pragma unroll
+    for (int j = 0; j < RR; j++) {
+      const uint32_t i = b + j * FW_REGROUP_THREADS + threadIdx.x;
+      if (i < ce) out[i] = r[j];
+    }
   }
 }
 
@@ -1065,9 +1358,9 @@ __device__ __forceinline__ Entry lds_delta(const DevCfg& c, const AggLds& L, int
 // its dependent loads per thread are longer than a probe chain at a region's load.)
 // DIAG_AGG_TIMING clocks of the tumbling/sliding flush (thread 0): [0] flushes, [1] phase A, [2] phase B, [3] tail
 __device__ unsigned long long g_flt[4];
-__device__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* st) {
+__device__ __forceinline__ bool agg_flush(const DevCfg& c, AggLds& L, const Region& r, Status* st) {
   __syncthreads();
-  const bool timing = c.diag & DIAG_AGG_TIMING;
+  const bool timing = FW_AGG_TIMING_BUILD && (c.diag & DIAG_AGG_TIMING);
   const unsigned long long tf0 = timing ? __builtin_amdgcn_s_memtime() : 0;
   if (c.diag & DIAG_AGG_NO_FLUSH) {
     for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
@@ -1334,7 +1627,7 @@ __device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, con
 __device__ __forceinline__ bool agg_flush_session(const DevCfg& c, AggLds& L, const int64_t* E, const Region& r,
                                                   Status* st) {
   __syncthreads();
-  const bool timing = c.diag & DIAG_AGG_TIMING;
+  const bool timing = FW_AGG_TIMING_BUILD && (c.diag & DIAG_AGG_TIMING);
   const unsigned long long ts0 = timing ? __builtin_amdgcn_s_memtime() : 0;
   const int32_t need = L.live + L.fill;
   if (need > region_limit(c.log_r)) {
@@ -1464,7 +1757,7 @@ __global__ void k_chunk_plan(DevCfg c, const uint32_t* __restrict__ offs, int32_
 
 // write the LDS entries of a chunk as deltas (Entry form, accumulators as in the LDS) and empty the table
 template <bool SESS>
-__device__ void agg_spill(const DevCfg& c, AggLds& L, const int64_t* E, Entry* out) {
+__device__ __forceinline__ void agg_spill(const DevCfg& c, AggLds& L, const int64_t* E, Entry* out) {
   __syncthreads();
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
     if (L.tag[h] < 2) continue;
@@ -1484,12 +1777,40 @@ __device__ void agg_spill(const DevCfg& c, AggLds& L, const int64_t* E, Entry* o
 // chunk's deltas into the region with the LDS table and the usual flush, which may suspend; a resumed
 // launch continues phase 2 in the partition's chunk-0 workgroup (prog.rb = delta round, prog.tp = delta
 // of the round per thread).
+// the LDS copy of partition p's row of the runs table (every thread of the workgroup calls it)
+__device__ __forceinline__ void gather_prologue(const uint32_t* __restrict__ row, int32_t nt, uint32_t* pre,
+                                                uint16_t* s0, uint32_t* sw) {
+  constexpr int TPT = FW_GMAX_T / FW_AGG_THREADS;
+  uint32_t cnt[TPT], tot = 0;
+#pragma unroll
+  for (int q = 0; q < TPT; q++) {
+    const int t = threadIdx.x * TPT + q;
+    const uint32_t w = t < nt ? row[t] : 0u;
+    if (t < nt) s0[t] = (uint16_t)(w & 0xffffu);
+    cnt[q] = w >> 16;
+    tot += cnt[q];
+  }
+  uint32_t total;
+  uint32_t e = block_excl_scan(tot, sw, &total);
+#pragma unroll
+  for (int q = 0; q < TPT; q++) {
+    const int t = threadIdx.x * TPT + q;
+    if (t < nt) pre[t] = e;
+    e += cnt[q];
+  }
+  __syncthreads();
+}
 // record i of a partition run: the raw 32 bytes of a PRec, or the 16 bytes of a CRec (cmp), loaded as
 // 16-byte halves, then unpacked once every record of the round is in flight
-__device__ __forceinline__ void load_prec_raw(bool cmp, const PRec* part, int64_t i, bool in, i64x2& a, i64x2& b) {
+__device__ __forceinline__ void load_prec_raw(bool cmp, const PRec* part, int64_t i, bool in, i64x2& a, i64x2& b,
+                                              const GatherRuns* g = nullptr) {
   a = i64x2{0, 0};
   b = i64x2{0, 0};
   if (!in) return;
+  if (g) {
+    a = reinterpret_cast<const i64x2*>(part)[gather_index(*g, i)];
+    return;
+  }
   if (cmp) {
     a = reinterpret_cast<const i64x2*>(part)[i];
   } else {
@@ -1517,12 +1838,12 @@ __device__ __forceinline__ void unpack_prec(const DevCfg& c, bool cmp, int32_t p
 }
 
 template <int RPT, bool SESS, bool FIRST>
-__device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __restrict__ part, int64_t begin,
+__device__ __forceinline__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __restrict__ part, int64_t begin,
                           int64_t end, int32_t p, int32_t ch, int32_t nch, DevTable& tb, const AggProg& prog,
-                          int resume, const AggHot& hot, Status* st) {
+                          int resume, const AggHot& hot, Status* st, const GatherRuns* g) {
   const int32_t c0 = (int32_t)hot.chunk_base[p];
   if (resume && (ch != 0 || prog.done[p])) return;
-  const bool cmp = c.compact && !st->wide;
+  const bool cmp = g || (c.compact && !st->wide);
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
   if (threadIdx.x == 0) {
     L.fill = 0;
@@ -1541,7 +1862,7 @@ __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __
 #pragma unroll
       for (int j = 0; j < RPT; j++) {
         const int64_t i = rb + (int64_t)j * blockDim.x + threadIdx.x;
-        load_prec_raw(cmp, part, i, i < ce, ra[j], rbb[j]);
+        load_prec_raw(cmp, part, i, i < ce, ra[j], rbb[j], g);
       }
 #pragma unroll
       for (int j = 0; j < RPT; j++) {
@@ -1671,34 +1992,59 @@ __device__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __
 __device__ unsigned long long g_aggt[4];
 __device__ unsigned long long g_occ[3];  // running, sum of running at starts, max running
 __device__ unsigned long long g_loop[3];  // thread 0's record loop: load wait, LDS upsert, barriers
-template <int RPT, bool SESS, bool FIRST>
-__global__ __launch_bounds__(FW_AGG_THREADS, SESS ? FW_SESS_WAVES : FW_AGG_WAVES) void k_aggregate(DevCfg c, int64_t wm, const PRec* __restrict__ part,
+// POOL: the aggregate keeps a pool block per window (HLL, t-digest); without it the instantiation is
+// compiled for count/sum/min/max (or the ordinal aggregates) alone, which keeps the pool's code out of its
+// registers
+// GATHER: a gathered batch (k_stage): offs = the partitions' virtual offsets (T = 1), rt_t = the runs table
+// [P][t8]; consecutive partitions run on one XCD (blocks b, b + 8, ... take consecutive ones), so the runs that
+// sit side by side in every tile are read through one L2.
+template <int RPT, bool SESS, bool FIRST, bool POOL, bool GATHER = false>
+__global__ __launch_bounds__(FW_AGG_THREADS, GATHER ? FW_GATHER_WAVES : SESS ? FW_SESS_WAVES : FW_AGG_WAVES) void k_aggregate(DevCfg c, int64_t wm, const PRec* __restrict__ part,
                                                               const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
-                                                              AggProg prog, int resume, Status* st, AggHot hot) {
+                                                              AggProg prog, int resume, Status* st, AggHot hot,
+                                                              const uint32_t* __restrict__ rt_t, int32_t t8) {
+  if constexpr (!POOL) {
+    c.pool_bytes = 0;
+    if (!FIRST) c.agg = FW_AGG_COUNT_SUM_MIN_MAX;
+  }
   __shared__ AggLds L;
   __shared__ int64_t sess_end[SESS ? FW_LDS_SLOTS : 1];  // sessions: interval end of each LDS slot
-  int32_t p = blockIdx.x;
-  if (hot.chunk_base) {  // workgroup -> (partition, chunk): last partition whose first chunk <= blockIdx.x
-    if (blockIdx.x >= hot.chunk_base[c.P]) return;
+  __shared__ uint32_t g_pre[GATHER ? FW_GMAX_T : 1];
+  __shared__ uint16_t g_s0[GATHER ? FW_GMAX_T : 1];
+  __shared__ uint32_t g_sw[GATHER ? FW_AGG_THREADS / 64 + 1 : 1];
+  const int32_t vb = GATHER && (gridDim.x & 7) == 0 ? (int32_t)((blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3))
+                                                    : (int32_t)blockIdx.x;
+  int32_t p = vb;
+  int32_t nch = 1, ch = 0;
+  if (hot.chunk_base) {  // workgroup -> (partition, chunk): last partition whose first chunk <= vb
+    if ((uint32_t)vb >= hot.chunk_base[c.P]) return;
     int32_t lo = 0, hi = c.P - 1;
     while (lo < hi) {
       const int32_t mid = (lo + hi + 1) >> 1;
-      if (hot.chunk_base[mid] <= blockIdx.x)
+      if (hot.chunk_base[mid] <= (uint32_t)vb)
         lo = mid;
       else
         hi = mid - 1;
     }
     p = lo;
-    const int32_t nch = (int32_t)(hot.chunk_base[p + 1] - hot.chunk_base[p]);
-    if (nch > 1) {
-      const int64_t b0 = offs[(int64_t)p * T], e0 = offs[(int64_t)(p + 1) * T];
-      agg_split<RPT, SESS, FIRST>(c, L, sess_end, part, b0, e0, p, (int32_t)(blockIdx.x - hot.chunk_base[p]), nch, tb, prog,
-                           resume, hot, st);
-      return;
-    }
+    nch = (int32_t)(hot.chunk_base[p + 1] - hot.chunk_base[p]);
+    ch = (int32_t)(vb - hot.chunk_base[p]);
+  } else if (p >= c.P) {
+    return;
+  }
+  GatherRuns gr{g_pre, g_s0, t8, 0};
+  if constexpr (GATHER) {
+    gr.base = offs[p];
+    gather_prologue(rt_t + (int64_t)p * t8, t8, g_pre, g_s0, g_sw);
+  }
+  const GatherRuns* g = GATHER ? &gr : nullptr;
+  if (nch > 1) {
+    const int64_t b0 = offs[(int64_t)p * T], e0 = offs[(int64_t)(p + 1) * T];
+    agg_split<RPT, SESS, FIRST>(c, L, sess_end, part, b0, e0, p, ch, nch, tb, prog, resume, hot, st, g);
+    return;
   }
   if (resume && prog.done[p]) return;
-  const bool cmp = c.compact && !st->wide;
+  const bool cmp = GATHER || (c.compact && !st->wide);
   const int64_t begin = offs[(int64_t)p * T], end = offs[(int64_t)(p + 1) * T];
   if (begin == end) {
     if (threadIdx.x == 0) prog.done[p] = 1;
@@ -1729,7 +2075,7 @@ __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? FW_SESS_WAVES : FW_AGG_WAVES
   const Region r = region_of(c, tb, p, tb.cur[p]);
   bool ok = true, first = true;
   const bool onewin = c.wpr == 1 || c.panes;
-  const bool timing = c.diag & DIAG_AGG_TIMING;
+  const bool timing = FW_AGG_TIMING_BUILD && (c.diag & DIAG_AGG_TIMING);
   unsigned long long tw0 = timing ? __builtin_amdgcn_s_memtime() : 0, tflush = 0;
   if (timing && threadIdx.x == 0) {  // concurrency: workgroups running when this one starts
     const unsigned long long run = atomicAdd(&g_occ[0], 1ull) + 1;
@@ -1746,7 +2092,7 @@ __global__ __launch_bounds__(FW_AGG_THREADS, SESS ? FW_SESS_WAVES : FW_AGG_WAVES
 #pragma unroll
       for (int j = 0; j < RPT; j++) {  // all loads in flight before any use
         const int64_t i = rb + (int64_t)j * blockDim.x + threadIdx.x;
-        load_prec_raw(cmp, part, i, i < end, ra[j], rbb[j]);
+        load_prec_raw(cmp, part, i, i < end, ra[j], rbb[j], g);
       }
       if (timing) {
         __builtin_amdgcn_s_waitcnt(0);
@@ -2062,16 +2408,15 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
   note_timer(x, p, en);
 }
 
-__global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, const uint32_t* __restrict__ offs,
+__global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, const uint32_t* __restrict__ srow,
                                                           int32_t T, const int64_t* __restrict__ sk,
                                                           const int64_t* __restrict__ stt,
                                                           const int64_t* __restrict__ sv,
                                                           const int32_t* __restrict__ skh, DevTable tb, DevRows out,
                                                           DevSide side, Status* st, int resume) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // resumed later
-  // list length: row P of the scan (ordered-path offsets per tile) plus the last tile's own count
-  const int64_t rowP = (int64_t)c.P * T;
-  const int64_t n = (int64_t)(offs[rowP + T - 1] - offs[rowP]) + offs[rowP + T + T - 1];
+  // list length: the ordered-path offset of the last tile plus that tile's own count
+  const int64_t n = (int64_t)(srow[T - 1] - srow[0]) + srow[T + T - 1];
   const int64_t first = resume ? st->slow_resume : 0;
   if (first >= n) return;
   __shared__ int64_t ck[SLOW_CHUNK];
@@ -3715,8 +4060,17 @@ static inline int32_t ntiles(int64_t n) { return (int32_t)((n + FW_TILE - 1) / F
 
 void launch_classify_hist(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int32_t* kh,
                           int64_t n, int32_t T, uint32_t* hist, Status* st, hipStream_t s) {
-  hipLaunchKernelGGL(k_classify_hist, dim3(T), dim3(FW_TILE_THREADS), (c.P + 1) * sizeof(uint32_t), s, c, wm, key, ts,
-                     kh, n, T, hist, st);
+  const size_t lds = (c.P + 1) * sizeof(uint32_t);
+  switch (stream_mode(c)) {
+    case M_TUMB:
+      hipLaunchKernelGGL(k_classify_hist<M_TUMB>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, kh, n, T, hist, st);
+      break;
+    case M_PANE:
+      hipLaunchKernelGGL(k_classify_hist<M_PANE>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, kh, n, T, hist, st);
+      break;
+    default:
+      hipLaunchKernelGGL(k_classify_hist<M_GEN>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, kh, n, T, hist, st);
+  }
 }
 
 void launch_scan(uint32_t* data, int64_t m, uint32_t* scratch, hipStream_t s) {
@@ -3735,11 +4089,23 @@ void launch_taint(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t
 void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
                     const int32_t* kh, int64_t n, int32_t T, uint32_t* offs, PRec* part, int64_t* sk, int64_t* stt,
                     int64_t* sv, int32_t* skh, DevSide side, Status* st, hipStream_t s) {
-  hipLaunchKernelGGL(k_scatter, dim3(T), dim3(FW_TILE_THREADS), (size_t)c.P * sizeof(uint32_t), s, c, wm, key, ts, val,
-                     kh, n, T, (const uint32_t*)offs, part, side, st);
-  hipLaunchKernelGGL(k_scatter_ordered, dim3(T), dim3(FW_TILE_THREADS), 0, s, c, wm, key, ts, val, kh, n, T,
-                     (const uint32_t*)offs, (const uint32_t*)(offs + (int64_t)(c.P + 1) * T), sk, stt, sv, skh,
-                     (const Status*)st);
+  const size_t lds = (size_t)c.P * sizeof(uint32_t);
+  const uint32_t* o = offs;
+  switch (stream_mode(c)) {
+    case M_TUMB:
+      hipLaunchKernelGGL(k_scatter<M_TUMB>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, val, kh, n, T, o, part,
+                         side, st);
+      break;
+    case M_PANE:
+      hipLaunchKernelGGL(k_scatter<M_PANE>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, val, kh, n, T, o, part,
+                         side, st);
+      break;
+    default:
+      hipLaunchKernelGGL(k_scatter<M_GEN>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, val, kh, n, T, o, part,
+                         side, st);
+  }
+  hipLaunchKernelGGL(k_scatter_ordered<false>, dim3(T), dim3(FW_TILE_THREADS), 0, s, c, wm, key, ts, val, kh, n, T,
+                     (const uint32_t*)(offs + (int64_t)c.P * T), sk, stt, sv, skh, (const Status*)st);
 }
 
 // panes: maxTimestamp of the earliest window ending after wm (windows [s, s + size), s = offset mod slide)
@@ -3753,7 +4119,8 @@ int64_t pane_nt_floor(const DevCfg& c, int64_t wm) {
 }
 
 void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
-                      AggProg prog, int resume, const AggHot* hot, int64_t n, Status* st, hipStream_t s) {
+                      AggProg prog, int resume, const AggHot* hot, int64_t n, Status* st, hipStream_t s,
+                      const uint32_t* rt_t, int32_t t8) {
   DevCfg c = c0;
   c.nt_floor = pane_nt_floor(c, wm);
   AggHot h{};
@@ -3766,22 +4133,84 @@ void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint
       launch_scan(h.chunk_base, (int64_t)c.P + 1, h.scan_tmp, s);
     }
   }
-  const bool first = agg_ordinal(c);
+  const dim3 b(FW_AGG_THREADS);
+  if (rt_t) {  // gathered: count/sum/min/max of compact records (gather_mode)
+    grid = (grid + 7) & ~7u;  // whole groups of 8 for the XCD mapping (the extra workgroups return)
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false, false, false, true>), dim3(grid), b, 0, s, c, wm, part, offs, T,
+                       tb, prog, resume, st, h, rt_t, t8);
+    return;
+  }
+  const uint32_t* nr = nullptr;
+  const bool first = agg_ordinal(c), pool = c.pool_bytes != 0;
   if (c.assigner == FW_SESSION && first)
-    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true, true>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs,
-                       T, tb, prog, resume, st, h);
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true, true, false>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb, prog,
+                       resume, st, h, nr, 0);
+  else if (c.assigner == FW_SESSION && pool)
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true, false, true>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb, prog,
+                       resume, st, h, nr, 0);
   else if (c.assigner == FW_SESSION)
-    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true, false>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs,
-                       T, tb, prog, resume, st, h);
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true, false, false>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb,
+                       prog, resume, st, h, nr, 0);
   else if (first)
-    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false, true>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part,
-                       offs, T, tb, prog, resume, st, h);
-  else if (c.diag & DIAG_AGG_RPT8)
-    hipLaunchKernelGGL((k_aggregate<8, false, false>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part, offs, T, tb,
-                       prog, resume, st, h);
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false, true, false>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb,
+                       prog, resume, st, h, nr, 0);
+  else if (pool)
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false, false, true>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb,
+                       prog, resume, st, h, nr, 0);
   else
-    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false, false>), dim3(grid), dim3(FW_AGG_THREADS), 0, s, c, wm, part,
-                       offs, T, tb, prog, resume, st, h);
+    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false, false, false>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb,
+                       prog, resume, st, h, nr, 0);
+}
+
+int gather_mode(const DevCfg& c, int64_t n) {
+  // opt-in (FW_GATHER=1): at C2 it measured even with the partition-major scatter (0.90 vs 0.895 ms per step;
+  // k_stage 185 us + regroup ~150 us against classify + scan + scatter 0.41 ms), see DESIGN.md
+  static const bool on = getenv("FW_GATHER") && atoi(getenv("FW_GATHER"));
+  return on && c.compact && c.assigner != FW_SESSION && (c.assigner == FW_TUMBLING || c.panes) &&
+         c.P <= FW_GMAX_P && n <= (int64_t)FW_GMAX_T * FW_GTILE;
+}
+
+void launch_stage(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
+                  const int32_t* kh, int64_t n, PRec* part, int64_t mb, uint32_t* rt, uint32_t* rt_t, uint32_t* voffs,
+                  uint32_t* srow, uint32_t* scan_tmp, int64_t* sk, int64_t* stt, int64_t* sv, int32_t* skh, DevSide side,
+                  Status* st, hipStream_t s) {
+  const int32_t t8 = (int32_t)((n + FW_GTILE - 1) / FW_GTILE);
+  const size_t lds = (size_t)FW_GTILE * sizeof(i64x2) + (size_t)c.P * sizeof(uint32_t);
+  static bool attr = false;
+  if (!attr) {  // LDS beyond 64 KB
+    (void)hipFuncSetAttribute((const void*)k_stage<M_TUMB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)k_stage<M_PANE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)k_stage<M_GEN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  // the tiles go to the second half of the record buffer (PRec-sized: 2 CRecs per record), the regrouped
+  // partition runs to the first
+  i64x2* out = reinterpret_cast<i64x2*>(part) + mb;
+  switch (stream_mode(c)) {
+    case M_TUMB:
+      hipLaunchKernelGGL(k_stage<M_TUMB>, dim3(t8), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, val, kh, n, t8, out, rt,
+                         srow, side, st);
+      break;
+    case M_PANE:
+      hipLaunchKernelGGL(k_stage<M_PANE>, dim3(t8), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, val, kh, n, t8, out, rt,
+                         srow, side, st);
+      break;
+    default:
+      hipLaunchKernelGGL(k_stage<M_GEN>, dim3(t8), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, val, kh, n, t8, out, rt,
+                         srow, side, st);
+  }
+  // voffs: the partitions' counts (k_rt_transpose), then their virtual offsets and the regroup's chunks (k_gplan);
+  // the regroup's chunk bases go to cbase (P + 1)
+  uint32_t* cbase = scan_tmp;
+  (void)hipMemsetAsync(voffs, 0, ((size_t)c.P + 1) * sizeof(uint32_t), s);
+  hipLaunchKernelGGL(k_rt_transpose, dim3((t8 + 63) / 64, (c.P + 63) / 64), dim3(1024), 0, s, rt, rt_t, t8, c.P, voffs);
+  hipLaunchKernelGGL(k_gplan, dim3(1), dim3(FW_TILE_THREADS), 0, s, voffs, cbase, c.P, srow, t8);
+  hipLaunchKernelGGL(k_scatter_ordered<true>, dim3(t8), dim3(FW_TILE_THREADS), 0, s, c, wm, key, ts, val, kh, n, t8,
+                     (const uint32_t*)srow, sk, stt, sv, skh, (const Status*)st);
+  const unsigned grid = (unsigned)((c.P + (n + FW_REGROUP_CHUNK - 1) / FW_REGROUP_CHUNK + 7) & ~7ll);
+  hipLaunchKernelGGL(k_regroup, dim3(grid), dim3(FW_REGROUP_THREADS), 0, s, (const i64x2*)out,
+                     reinterpret_cast<i64x2*>(part), (const uint32_t*)rt_t, t8, (const uint32_t*)voffs,
+                     (const uint32_t*)cbase, c.P);
 }
 
 void launch_hll_update(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
@@ -3791,10 +4220,10 @@ void launch_hll_update(const DevCfg& c, const PRec* part, const uint32_t* offs, 
                      offs, T, tb, st);
 }
 
-void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* offs, int32_t T, const int64_t* sk, const int64_t* stt,
+void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* srow, int32_t T, const int64_t* sk, const int64_t* stt,
                  const int64_t* sv, const int32_t* skh, DevTable tb, DevRows out, DevSide side, Status* st, int resume,
                  hipStream_t s) {
-  hipLaunchKernelGGL(k_slow, dim3(1), dim3(FW_SLOW_THREADS), 0, s, c, wm, offs, T, sk, stt, sv, skh, tb, out, side,
+  hipLaunchKernelGGL(k_slow, dim3(1), dim3(FW_SLOW_THREADS), 0, s, c, wm, srow, T, sk, stt, sv, skh, tb, out, side,
                      st, resume);
 }
 

@@ -35,6 +35,9 @@
 #ifndef FW_AGG_WAVES
 #define FW_AGG_WAVES 6  // 80 VGPRs: 3 workgroups of 512 per CU (86 unconstrained gave 2; measured 0.425 -> 0.371 ms at C2)
 #endif
+#ifndef FW_GATHER_WAVES
+#define FW_GATHER_WAVES 4  // the gathered instantiation: its runs table takes 12 KB of LDS, 2 workgroups per CU
+#endif
 #ifndef FW_SESS_WAVES
 #define FW_SESS_WAVES 4  // the same for the session instantiation
 #endif
@@ -56,7 +59,22 @@
 #ifndef FW_TD_T3
 #define FW_TD_T3 16384         // ... at most this many in one wave; more over the whole grid (the hottest keys)
 #endif
-#define FW_SLOW_THREADS 1024   // ordered replay workgroup (one workgroup)
+#define FW_SLOW_THREADS 1024
+// Tile-local ("gathered") partitioning of compact count/sum/min/max batches: k_stage sorts each tile of
+// FW_GTILE records by partition in LDS and writes it back linearly (a wave's stores are whole lines; scattered
+// 16-byte stores into partition-major runs measured 2.4x slower), and k_aggregate gathers a partition's runs
+// from every tile through the runs table.  P <= FW_GMAX_P (the staging's LDS) and at most FW_GMAX_T tiles per
+// batch (the aggregate's LDS copy of a partition's row of the runs table).
+#define FW_GTILE 8192
+#define FW_GMAX_P 2048
+#define FW_GMAX_T 2048
+#define FW_REGROUP_THREADS 512
+#define FW_REGROUP_CHUNK 16384  // records per regroup workgroup (a hot partition takes several)
+// DIAG_AGG_TIMING's clocks and printf are compiled in only on request: the printf calls cost k_aggregate
+// its registers (a call saves the live VGPRs to scratch)
+#ifndef FW_AGG_TIMING_BUILD
+#define FW_AGG_TIMING_BUILD 0
+#endif   // ordered replay workgroup (one workgroup)
 
 enum : uint32_t { SLOT_EMPTY = 0, SLOT_LIVE = 1, SLOT_DEAD = 2, SLOT_BUSY = 3 };
 enum : int64_t { FW_TIMER = 1 };
@@ -135,9 +153,8 @@ enum {
   DIAG_SCATTER_NO_STORE = 4,
   DIAG_SCATTER_LINEAR = 8,
   DIAG_AGG_NO_ACCUM = 16,  // LDS lookup/claim only, no accumulate atomics
-  DIAG_AGG_RPT8 = 64,      // k_aggregate with 8 records per thread in flight
   DIAG_SCATTER_SINGLE = 128, // k_scatter: each lane stores its own record (no lane-pair sectors)
-  DIAG_AGG_TIMING = 256,     // k_aggregate prints per-workgroup phase clocks
+  DIAG_AGG_TIMING = 256,     // k_aggregate prints per-workgroup phase clocks (builds with FW_AGG_TIMING_BUILD=1)
   DIAG_SCATTER_HALF = 512,   // k_scatter stores 16 B per record (the timing of a compact record)
   DIAG_SCATTER_NT = 1024     // k_scatter stores with nontemporal stores
 };
@@ -309,11 +326,26 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
                     const int32_t* kh, int64_t n, int32_t T, uint32_t* offs, PRec* part, int64_t* sk,
                     int64_t* stt, int64_t* sv, int32_t* skh, DevSide side, Status* st, hipStream_t_ s);
 // hot: chunk splitting of long partitions (nullptr = one workgroup per partition); n = records of the push
+// gathered batches (FW_GTILE): offs = the partitions' virtual offsets (P + 1, T = 1), rt_t = the runs table
+// [P][T8] (tile-local start | count << 16), t8 = tiles of the batch; rt_t = nullptr for partition-major runs
 void launch_aggregate(const DevCfg& c, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
-                      AggProg prog, int resume, const AggHot* hot, int64_t n, Status* st, hipStream_t_ s);
+                      AggProg prog, int resume, const AggHot* hot, int64_t n, Status* st, hipStream_t_ s,
+                      const uint32_t* rt_t = nullptr, int32_t t8 = 0);
+// gathered batches: classify + tile-local partition sort (k_stage, into the second half of part: mb = its
+// capacity in PRecs), the runs table's transpose and the partitions' virtual offsets (voffs, P + 1), the
+// ordered-path compaction (srow: scanned ordered-path counts per tile, then the raw counts; 2 x t8) and the
+// regroup of every partition's runs into compact partition-major runs at the start of part (offsets voffs, T = 1);
+// scan_tmp: P + 1 words for the regroup's chunk bases
+int gather_mode(const DevCfg& c, int64_t n);  // host: the batch can be gathered
+void launch_stage(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
+                  const int32_t* kh, int64_t n, PRec* part, int64_t mb, uint32_t* rt, uint32_t* rt_t, uint32_t* voffs,
+                  uint32_t* srow, uint32_t* scan_tmp, int64_t* sk, int64_t* stt, int64_t* sv, int32_t* skh, DevSide side,
+                  Status* st, hipStream_t_ s);
 void launch_taint(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, int64_t n, Status* st,
                   hipStream_t_ s);
-void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* offs, int32_t T, const int64_t* sk,
+// srow: the ordered-path counts per tile, scanned (T), then raw (T): rows P and P + 1 of a partition-major
+// batch's scanned histogram
+void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* srow, int32_t T, const int64_t* sk,
                  const int64_t* stt, const int64_t* sv, const int32_t* skh, DevTable tb, DevRows out, DevSide side,
                  Status* st, int resume, hipStream_t_ s);
 void launch_fire(const DevCfg& c, int64_t wm, DevTable tb, DevRows out, Status* st, hipStream_t_ s);

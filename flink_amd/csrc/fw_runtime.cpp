@@ -49,6 +49,15 @@ struct Scratch {
   int32_t compact = 0;           // DevCfg::compact / cbase of the batch (a resumed aggregate reads the same form)
   int64_t cbase = 0;
   int64_t ord_base = 0;          // arrival ordinal of the batch's first record (ordinal aggregates)
+  // gathered batches (fwdev::gather_mode): runs table [T8][P] and its transpose, the partitions' virtual
+  // offsets (P + 1) and the ordered-path rows (2 x T8); T is then the batch's FW_GTILE tiles
+  uint32_t *rt = nullptr, *rt_t = nullptr, *voffs = nullptr, *gsrow = nullptr, *gcb = nullptr;
+  bool gather = false;
+  // the ordered-path rows of the batch: scanned counts per tile, then raw counts
+  const uint32_t* srow(int32_t P) const { return gather ? gsrow : hist + (int64_t)P * T; }
+  // the partitions' runs in part: offsets offs()[p * offT()] (a gathered batch: regrouped, virtual offsets)
+  const uint32_t* offs() const { return gather ? voffs : hist; }
+  int32_t offT() const { return gather ? 1 : T; }
 };
 
 }  // namespace
@@ -184,6 +193,16 @@ int alloc_scratch(fw_op* op, Scratch& s, int64_t mb, int64_t m) {
   HIP_OR_RETURN(op, dmalloc(&s.skh, mb));
   if (op->cfg.aggregate >= FW_AGG_FIRST && op->cfg.aggregate <= FW_AGG_FIRST_MAX) HIP_OR_RETURN(op, dmalloc(&s.so, mb));
   if (op->cfg.aggregate == FW_AGG_MINBY || op->cfg.aggregate == FW_AGG_MAXBY) HIP_OR_RETURN(op, dmalloc(&s.byv, mb));
+  DevCfg probe = op->dc;
+  probe.compact = 1;
+  if (fwdev::gather_mode(probe, 1)) {
+    const int64_t t8 = std::min<int64_t>((mb + FW_GTILE - 1) / FW_GTILE, FW_GMAX_T);
+    HIP_OR_RETURN(op, dmalloc(&s.rt, (size_t)(t8 * op->dc.P)));
+    HIP_OR_RETURN(op, dmalloc(&s.rt_t, (size_t)(t8 * op->dc.P)));
+    HIP_OR_RETURN(op, dmalloc(&s.voffs, (size_t)op->dc.P + 1));
+    HIP_OR_RETURN(op, dmalloc(&s.gsrow, (size_t)(2 * t8)));
+    HIP_OR_RETURN(op, dmalloc(&s.gcb, (size_t)op->dc.P + 1));
+  }
   return FW_OK;
 }
 void free_scratch(Scratch& s) {
@@ -196,6 +215,11 @@ void free_scratch(Scratch& s) {
   dfree(s.skh);
   dfree(s.so);
   dfree(s.byv);
+  dfree(s.rt);
+  dfree(s.rt_t);
+  dfree(s.voffs);
+  dfree(s.gsrow);
+  dfree(s.gcb);
 }
 
 // buffers of the split-partition aggregate (AggHot): deltas at record indices, so one Entry per record
@@ -437,20 +461,20 @@ int settle(fw_op* op) {
     c.ord_base = S.ord_base;
     if (susp & FW_SUSP_AGG)
       timed(op, K_AGGREGATE, [&] {
-        fwdev::launch_aggregate(c, S.wm, S.part, S.hist, S.T, op->tb, op->prog, 1, S.split ? &op->hot : nullptr, S.n,
-                                op->d_status, op->stream);
+        fwdev::launch_aggregate(c, S.wm, S.part, S.offs(), S.offT(), op->tb, op->prog, 1, S.split ? &op->hot : nullptr,
+                                S.n, op->d_status, op->stream);
         // the update skipped itself behind the suspension; register max is idempotent, so it reruns whole
         if (c.agg == FW_AGG_HLL)
-          fwdev::launch_hll_update(c, S.part, S.hist, S.T, S.n, op->tb, op->d_status, op->stream);
+          fwdev::launch_hll_update(c, S.part, S.offs(), S.offT(), S.n, op->tb, op->d_status, op->stream);
       });
     // the t-digest compression skipped itself too (it runs once, after the aggregate completed)
     if ((susp & FW_SUSP_AGG) && c.agg == FW_AGG_TDIGEST)
       timed(op, K_TDIGEST, [&] {
-        fwdev::launch_tdigest(c, S.part, S.hist, S.T, S.n, op->tb, op->td, op->d_status, op->stream);
+        fwdev::launch_tdigest(c, S.part, S.offs(), S.offT(), S.n, op->tb, op->td, op->d_status, op->stream);
       });
     // after an aggregate suspension the ordered path never started; otherwise it resumes
     timed(op, K_SLOW, [&] {
-      fwdev::launch_slow(c, S.wm, S.hist, S.T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status,
+      fwdev::launch_slow(c, S.wm, S.srow(op->dc.P), S.T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status,
                          (susp & FW_SUSP_AGG) ? 0 : 1, op->stream);
     });
     // a watermark queued behind the push skipped itself; firing at the latest one is the same as
@@ -563,7 +587,8 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
     else
       c.cbase = (int64_t)base;
   }
-  const int32_t T = (int32_t)((n + FW_TILE - 1) / FW_TILE);
+  const bool gather = S.rt && fwdev::gather_mode(c, n);
+  const int32_t T = gather ? (int32_t)((n + FW_GTILE - 1) / FW_GTILE) : (int32_t)((n + FW_TILE - 1) / FW_TILE);
   const int64_t m = (int64_t)(c.P + 1) * T;
   if (c.assigner == FW_SESSION) {
     // a new epoch empties the taint set; its slots are cleared only when the epochs wrap
@@ -575,15 +600,25 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
     HIP_OR_RETURN(op, hipMemsetAsync(&op->d_status->taint_any, 0, sizeof(int32_t), op->stream));
   }
   if (c.compact) HIP_OR_RETURN(op, hipMemsetAsync(&op->d_status->wide, 0, sizeof(int32_t), op->stream));
-  timed(op, K_CLASSIFY, [&] {
-    if (c.assigner == FW_SESSION) fwdev::launch_taint(c, op->wm, key, ts, n, op->d_status, op->stream);
-    fwdev::launch_classify_hist(c, op->wm, key, ts, kh, n, T, S.hist, op->d_status, op->stream);
-  });
-  timed(op, K_SCAN, [&] { fwdev::launch_scan(S.hist, m, S.scan_tmp, op->stream); });
-  timed(op, K_SCATTER, [&] {
-    fwdev::launch_scatter(c, op->wm, key, ts, val, kh, n, T, S.hist, S.part, S.sk, S.stt, S.sv, S.skh, op->side,
-                          op->d_status, op->stream);
-  });
+  if (gather) {
+    // classify, tile-local partition sort, runs table, ordered-path compaction: one pass over the input
+    timed(op, K_SCATTER, [&] {
+      fwdev::launch_stage(c, op->wm, key, ts, val, kh, n, S.part, op->max_batch, S.rt, S.rt_t, S.voffs, S.gsrow, S.gcb, S.sk,
+                          S.stt, S.sv, S.skh, op->side, op->d_status, op->stream);
+    });
+  } else {
+    timed(op, K_CLASSIFY, [&] {
+      if (c.assigner == FW_SESSION) fwdev::launch_taint(c, op->wm, key, ts, n, op->d_status, op->stream);
+      fwdev::launch_classify_hist(c, op->wm, key, ts, kh, n, T, S.hist, op->d_status, op->stream);
+    });
+    timed(op, K_SCAN, [&] { fwdev::launch_scan(S.hist, m, S.scan_tmp, op->stream); });
+    timed(op, K_SCATTER, [&] {
+      fwdev::launch_scatter(c, op->wm, key, ts, val, kh, n, T, S.hist, S.part, S.sk, S.stt, S.sv, S.skh, op->side,
+                            op->d_status, op->stream);
+    });
+  }
+  S.gather = gather;
+  S.T = T;
   // minBy / maxBy: the aggregate reads the selected elements' fields back by batch index, possibly after the
   // caller's columns are gone (a resumed push), so the batch keeps its own copy
   if (S.byv) HIP_OR_RETURN(op, hipMemcpyAsync(S.byv, val, n * sizeof(int64_t), hipMemcpyDeviceToDevice, op->stream));
@@ -604,16 +639,17 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   const bool split = (cc.wpr == 1 || cc.panes) && n > FW_AGG_CHUNK;
   if (split && (rc = ensure_hot(op))) return rc;
   timed(op, K_AGGREGATE, [&] {
-    fwdev::launch_aggregate(cc, op->wm, S.part, S.hist, T, op->tb, op->prog, 0, split ? &op->hot : nullptr, n,
+    fwdev::launch_aggregate(cc, op->wm, S.part, S.offs(), S.offT(), op->tb, op->prog, 0, split ? &op->hot : nullptr, n,
                             op->d_status, op->stream);
-    if (cc.agg == FW_AGG_HLL) fwdev::launch_hll_update(cc, S.part, S.hist, T, n, op->tb, op->d_status, op->stream);
+    if (cc.agg == FW_AGG_HLL)
+      fwdev::launch_hll_update(cc, S.part, S.offs(), S.offT(), n, op->tb, op->d_status, op->stream);
   });
   if (cc.agg == FW_AGG_TDIGEST)
     timed(op, K_TDIGEST, [&] {
-      fwdev::launch_tdigest(cc, S.part, S.hist, T, n, op->tb, op->td, op->d_status, op->stream);
+      fwdev::launch_tdigest(cc, S.part, S.offs(), S.offT(), n, op->tb, op->td, op->d_status, op->stream);
     });
   timed(op, K_SLOW, [&] {
-    fwdev::launch_slow(cc, op->wm, S.hist, T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status, 0,
+    fwdev::launch_slow(cc, op->wm, S.srow(cc.P), S.T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status, 0,
                        op->stream);
   });
   HIP_OR_RETURN(op, hipGetLastError());
