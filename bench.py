@@ -344,6 +344,10 @@ def main():
                     "traffic_per_record": None if traffic is None else round(traffic / per_launch_records, 2),
                     "basis": "SURVEY §8d B_alg x records per launch / the kernel's average HIP-event duration"}
 
+    count_gpu = None
+    if c1 and world == 1:
+        count_gpu = count_window_leg(args, batches, local_rank)
+
     host_fed = None
     if rank == 0 and world == 1 and args.host_fed_steps > 0:
         host_fed = host_fed_leg(args, op, generate, steps_total, m, c1)
@@ -373,6 +377,7 @@ def main():
             "path_roofline": {"b_alg_bytes_per_record": round(balg, 3), "frac": round(path_frac, 4),
                               "fired_rows": int(fired)},
             "host_fed": host_fed,
+            **({"count_window_gpu": count_gpu} if count_gpu else {}),
             "cpu_baseline": cpu,
             "kernels": kernels,
             "state": {"table_slots": int(st1["table_capacity"]), "table_grows_in_timed_region":
@@ -383,6 +388,39 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def count_window_leg(args, batches, device):
+    """C1's other pipeline on the GPU: keyBy(word).countWindow(10, 5).sum(1) (WindowWordCount.java:74-81;
+    EvictingWindowOperator + CountTrigger + CountEvictor) over the same device-resident token batches, the
+    rows materialised in HBM; timed like the main leg (the batches' pushes between synchronisations)."""
+    import torch
+    from flink_amd import CountWindows
+    from flink_amd.operator import GpuWindowOperator
+    from flink_amd.windowing import FirstElementReduce
+    op = GpuWindowOperator(CountWindows.of(10, 5), FirstElementReduce("int", "sum"), device=device,
+                           expected_entries=1000, max_batch=args.batch)
+    keys = sorted(batches)
+    k, t, v, _ = batches[keys[0]]
+    op.process_batch(k, t, v)  # warm (slot map, allocations)
+    op.synchronize()
+    op.clear_pending()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rows = 0
+    for s in keys:
+        k, t, v, _ = batches[s]
+        op.process_batch(k, t, v)
+        n_rows = op.advance_watermark(0)  # settles: the count windows fired while the batch was processed
+        rows += n_rows
+        op.clear_pending()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    op.close()
+    n = args.batch * len(keys)
+    return {"value": round(n / dt, 1), "unit": "records/s", "steps": len(keys), "fired_rows": int(rows),
+            "ms_per_step": round(dt / len(keys) * 1e3, 3),
+            "pipeline": "countWindow(10, 5).sum(1) on the GPU (k_cnt_*: key slots, stable sort, fire, ring update)"}
 
 
 def host_fed_leg(args, op, generate, first_step, m, c1):
