@@ -2526,24 +2526,39 @@ __global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, 
 // Pass 1 decides every slot, re-inserts the survivors into the other buffer and counts the fired
 // rows; one reservation per workgroup in the output; pass 2 re-decides and writes the rows.
 // one wave per fired row: estimate from the row's register block (out.mn holds its id), then zero the
-// block and push it on the free stack.  S = sum_j 2^(65-p-M[j]) exactly, in 128 bits.
+// block and push it on the free stack.  S = sum_j 2^(65-p-M[j]) exactly, in 128 bits.  Only the chunks the
+// block's bitmap marks are read (and zeroed): every register of an unmarked chunk is zero.
 __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, int64_t stack_slot) {
   const int lane = __lane_id();
   const int p = c.hll_p, rmax = 65 - p;
   const int64_t m = (int64_t)1 << p;
   const uint64_t blk = (uint64_t)out.mn[row];
-  uint8_t* regs = c.pool + blk * (uint64_t)m;
+  uint8_t* base = c.pool + blk * (uint64_t)c.pool_bytes;
+  uint32_t* bits = reinterpret_cast<uint32_t*>(base);
+  uint4* q = reinterpret_cast<uint4*>(base + hll_hdr_bytes(p));
+  const int32_t nq = (int32_t)(m / 16);  // 16-byte chunks
+  const int32_t nw = (nq + 31) / 32;     // bitmap words
   uint64_t s = 0, sh = 0;
-  uint32_t zeros = 0;
-  uint4* q = reinterpret_cast<uint4*>(regs);
-  const int64_t nq = m / 16;  // 16-byte chunks, four in flight per lane
-  for (int64_t j0 = lane; j0 < nq; j0 += 256) {
-    uint4 v[4];
+  uint32_t zeros = 0, touched = 0;
+  constexpr int U = 4;  // word pairs per pass: up to 4 chunk loads in flight per lane
+  uint32_t myw = 0;      // the bitmap, one word per lane (64 words = 2^15 registers at a time)
+  for (int32_t w0 = 0; w0 < nw; w0 += 2 * U) {
+    if ((w0 & 63) == 0) myw = w0 + lane < nw ? bits[w0 + lane] : 0u;
+    uint4 v[U];
+    bool on[U];
+    int32_t jj[U];
 #pragma unroll
-    for (int u = 0; u < 4; u++) v[u] = j0 + u * 64 < nq ? q[j0 + u * 64] : make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < U; u++) {
+      const int32_t w = w0 + 2 * u + (lane >> 5);
+      const uint32_t word = (uint32_t)__shfl((int)myw, (w & 63), 64);
+      jj[u] = w * 32 + (lane & 31);
+      on[u] = jj[u] < nq && ((word >> (lane & 31)) & 1u);
+      v[u] = on[u] ? q[jj[u]] : make_uint4(0, 0, 0, 0);
+    }
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      if (j0 + u * 64 >= nq) continue;
+    for (int u = 0; u < U; u++) {
+      if (!on[u]) continue;
+      touched++;
       const uint32_t ws[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
       for (int k = 0; k < 4; k++)
@@ -2555,9 +2570,10 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, in
           s = t;
           zeros += r == 0;
         }
-      q[j0 + u * 64] = make_uint4(0, 0, 0, 0);
+      q[jj[u]] = make_uint4(0, 0, 0, 0);
     }
   }
+  for (int32_t w = lane; w < nw; w += 64) bits[w] = 0u;
   uint64_t hi = sh, lo = s;
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t lo2 = __shfl_xor(lo, o, 64), hi2 = __shfl_xor(hi, o, 64);
@@ -2565,8 +2581,16 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, in
     hi = hi + hi2 + (t < lo ? 1ull : 0ull);
     lo = t;
     zeros += __shfl_xor(zeros, o, 64);
+    touched += __shfl_xor(touched, o, 64);
   }
   if (lane == 0) {
+    // the unmarked chunks: 16 zero registers each, 2^rmax apiece (rmax <= 61: the product fits 128 bits)
+    const uint64_t un = (uint64_t)(nq - (int32_t)touched) * 16u;
+    const uint64_t ulo = un << rmax, uhi = rmax ? un >> (64 - rmax) : 0ull;
+    const uint64_t t = lo + ulo;
+    hi = hi + uhi + (t < lo ? 1ull : 0ull);
+    lo = t;
+    zeros += (uint32_t)un;
     const double sd = (double)hi * 18446744073709551616.0 + (double)lo;
     const double md = (double)m;
     const double alpha = m == 16 ? 0.673 : m == 32 ? 0.697 : m == 64 ? 0.709 : 0.7213 / (1.0 + 1.079 / md);
@@ -2576,6 +2600,22 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, in
     out.mn[row] = (int64_t)zeros;
     out.mx[row] = (int64_t)lo;
     c.pool_free[stack_slot] = (uint32_t)blk;  // zeroed before the next kernel can hand it out
+  }
+}
+// one thread: zero a register block's marked chunks and its bitmap (a window collected without a row)
+__device__ void hll_clear(const DevCfg& c, uint64_t blk) {
+  uint8_t* base = c.pool + blk * (uint64_t)c.pool_bytes;
+  uint32_t* bits = reinterpret_cast<uint32_t*>(base);
+  uint4* q = reinterpret_cast<uint4*>(base + hll_hdr_bytes(c.hll_p));
+  const int32_t nq = (int32_t)(((int64_t)1 << c.hll_p) / 16), nw = (nq + 31) / 32;
+  for (int32_t w = 0; w < nw; w++) {
+    uint32_t word = bits[w];
+    while (word) {
+      const int b = __ffs(word) - 1;
+      word &= word - 1;
+      q[w * 32 + b] = make_uint4(0, 0, 0, 0);
+    }
+    bits[w] = 0u;
   }
 }
 
@@ -2610,35 +2650,98 @@ __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __rest
   const int p = c.hll_p;
   const bool cmp = c.compact && !st->wide;
   const int64_t i1 = min(total, i0 + (int64_t)FW_HLL_CHUNK);
+  const int64_t hdr = hll_hdr_bytes(p);
+  // HU records per thread in flight: the record, its home slot's state word and entry identity, the entry's
+  // block id and the register word are each loaded for all of them before any is used (the common case at a
+  // region's load is a home-slot hit; a miss walks the rest of its probe chain on its own)
+  constexpr int HU = 4;
   int32_t pp = p0_s;
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
-    PRec rec;
-    if (cmp) {
-      const i64x2 r = reinterpret_cast<const i64x2*>(part)[i];
-      compact_decode(c, pp, r.x, &rec.key, &rec.last);
-      rec.val = r.y;
-    } else {
-      rec = part[i];
+  for (int64_t ib = i0 + threadIdx.x; ib < i1; ib += (int64_t)blockDim.x * HU) {
+    int64_t key[HU], last[HU], val[HU];
+    int32_t part_of_rec[HU];
+    bool in[HU];
+#pragma unroll
+    for (int u = 0; u < HU; u++) {
+      const int64_t i = ib + (int64_t)u * blockDim.x;
+      in[u] = i < i1;
+      key[u] = last[u] = val[u] = 0;
+      part_of_rec[u] = pp;
+      if (!in[u]) continue;
+      while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
+      part_of_rec[u] = pp;
+      if (cmp) {
+        const i64x2 r = reinterpret_cast<const i64x2*>(part)[i];
+        compact_decode(c, pp, r.x, &key[u], &last[u]);
+        val[u] = r.y;
+      } else {
+        const PRec rec = part[i];
+        key[u] = rec.key;
+        last[u] = rec.last;
+        val[u] = rec.val;
+      }
     }
-    const Region r = region_of(c, tb, pp, tb.cur[pp]);
-    const int32_t slot = region_find(r, slot_hash(c, rec.key, rec.last), rec.key, rec.last, wend(c, rec.last));
-    if (slot < 0) {
-      atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's window
-      continue;
+    uint32_t hw[HU];
+    i64x2 hk[HU];
+    int64_t hend[HU], hmeta[HU];
+    uint64_t hs[HU];
+    Region rg[HU];
+#pragma unroll
+    for (int u = 0; u < HU; u++) {
+      rg[u] = region_of(c, tb, part_of_rec[u], tb.cur[part_of_rec[u]]);
+      hs[u] = slot_hash(c, key[u], last[u]);
+      hw[u] = 0;
+      if (!in[u]) continue;
+      const uint32_t home = (uint32_t)hs[u] & rg[u].mask;
+      hw[u] = ld_state(rg[u].state + home);
+      hk[u] = *reinterpret_cast<const i64x2*>(&rg[u].ent[home].key);
+      hend[u] = rg[u].ent[home].end;
+      hmeta[u] = rg[u].ent[home].meta;
     }
-    const uint64_t blk = pool_block_of(r.ent[slot]);
-    const uint64_t h = fmix64((uint64_t)rec.val);
-    const uint64_t j = h >> (64 - p);
-    const uint32_t rank = (uint32_t)__clzll((long long)((h << p) | (1ull << (p - 1)))) + 1u;
-    uint32_t* w = reinterpret_cast<uint32_t*>(c.pool + blk * ((uint64_t)1 << p) + (j & ~3ull));
-    const int sh = (int)(j & 3) * 8;
-    uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while (((old >> sh) & 0xffu) < rank) {
-      const uint32_t nw = (old & ~(0xffu << sh)) | (rank << sh);
-      if (__hip_atomic_compare_exchange_strong(w, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT))
-        break;
+    uint64_t blk[HU];
+#pragma unroll
+    for (int u = 0; u < HU; u++) {
+      blk[u] = 0;
+      if (!in[u]) continue;
+      const int64_t we = wend(c, last[u]);
+      if (hw[u] == live_word(hs[u]) && hk[u].x == key[u] && hk[u].y == last[u] && hend[u] == we) {
+        blk[u] = (uint64_t)hmeta[u] >> 1;
+      } else {
+        const int32_t slot = hw[u] == SLOT_EMPTY ? -1 : region_find(rg[u], hs[u] + 1, key[u], last[u], we, live_word(hs[u]));
+        if (slot < 0) {
+          atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's window
+          in[u] = false;
+          continue;
+        }
+        blk[u] = pool_block_of(rg[u].ent[slot]);
+      }
+    }
+    uint32_t* w[HU];
+    uint32_t old[HU], rank[HU], jj[HU];
+#pragma unroll
+    for (int u = 0; u < HU; u++) {
+      const uint64_t h = fmix64((uint64_t)val[u]);
+      jj[u] = (uint32_t)(h >> (64 - p));
+      rank[u] = (uint32_t)__clzll((long long)((h << p) | (1ull << (p - 1)))) + 1u;
+      w[u] = reinterpret_cast<uint32_t*>(c.pool + blk[u] * (uint64_t)c.pool_bytes + hdr + (jj[u] & ~3u));
+      old[u] = in[u] ? __hip_atomic_load(w[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < HU; u++) {
+      if (!in[u]) continue;
+      const int sh = (int)(jj[u] & 3) * 8;
+      uint32_t o = old[u];
+      while (((o >> sh) & 0xffu) < rank[u]) {
+        const uint32_t nw = (o & ~(0xffu << sh)) | (rank[u] << sh);
+        if (__hip_atomic_compare_exchange_strong(w[u], &o, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          // this record took the register out of zero: mark its chunk for the fire
+          if (((o >> sh) & 0xffu) == 0u) {
+            const uint32_t ch = jj[u] >> 4;
+            atomicOr(reinterpret_cast<uint32_t*>(c.pool + blk[u] * (uint64_t)c.pool_bytes) + (ch >> 5), 1u << (ch & 31u));
+          }
+          break;
+        }
+      }
     }
   }
 }
@@ -3458,8 +3561,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, 
     if (!d.keep && !d.fire && c.pool_bytes) {  // GC without a row: free its block here (HLL: zeroed)
       const uint64_t blk = pool_block_of(e);
       if (c.agg == FW_AGG_HLL) {
-        uint32_t* w = reinterpret_cast<uint32_t*>(c.pool + (blk << c.hll_p));
-        for (int64_t j = 0; j < ((int64_t)1 << c.hll_p) / 4; j++) w[j] = 0u;
+        hll_clear(c, blk);
         __threadfence();
       }
       c.pool_free[atomicAdd(&c.pool_ctr[0], 1)] = (uint32_t)blk;

@@ -175,6 +175,15 @@ struct __attribute__((aligned(16))) CRec {
   int64_t kw, val;
 };
 
+// FW_AGG_HLL register block: a bitmap of the block's 16-byte register chunks that hold a nonzero register
+// (set when a register first leaves zero), then the 2^p registers.  The fire reads and zeroes only the marked
+// chunks: a window of a few hundred items touches a few hundred of the 2^p / 16 chunks.
+__host__ __device__ inline int64_t hll_hdr_bytes(int p) {
+  int64_t b = ((int64_t)1 << p) / 128;  // one bit per 16-byte chunk
+  if (b < 16) b = 16;
+  return (b + 15) & ~(int64_t)15;
+}
+
 // region state word: kind in bits 0-1, 24-bit fingerprint of the slot hash in bits 8-31, so a
 // probe rejects most foreign slots without reading the 64-byte entry
 __host__ __device__ inline uint32_t st_kind(uint32_t s) { return s & 3u; }

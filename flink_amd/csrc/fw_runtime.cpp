@@ -817,7 +817,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     // a quarter for entries created before the watermark that retires their predecessors
     c.agg = FW_AGG_HLL;
     c.hll_p = hll_p;
-    c.pool_bytes = (int64_t)1 << hll_p;
+    c.pool_bytes = ((int64_t)1 << hll_p) + hll_hdr_bytes(hll_p);  // touched-chunk bitmap + registers
   } else if (cfg.aggregate == FW_AGG_TDIGEST) {
     // digest pool: a head and two halves of delta/2 centroids per live (key, window) (TdHead, TdCent)
     c.td_nb = td_delta / 2;
