@@ -61,6 +61,20 @@ class FwStats(ctypes.Structure):
         "slow_path_records", "state_merges", "digest_centroids_fired")]
 
 
+FW_WIRE_LONG, FW_WIRE_INT, FW_WIRE_DOUBLE, FW_WIRE_SHORT, FW_WIRE_BYTE, FW_WIRE_FLOAT, FW_WIRE_BOOL = range(7)
+(FW_ROLE_SKIP, FW_ROLE_KEY, FW_ROLE_VALUE, FW_ROLE_START, FW_ROLE_END, FW_ROLE_COUNT, FW_ROLE_SUM, FW_ROLE_MIN,
+ FW_ROLE_MAX) = range(9)
+
+
+class FwWireLayout(ctypes.Structure):
+    _fields_ = [("nfields", ctypes.c_int32), ("kind", ctypes.c_int32 * 8), ("role", ctypes.c_int32 * 8)]
+
+
+class FwWireStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in ("records", "watermarks", "latency_markers", "statuses", "consumed",
+                                               "watermark")] + [("status", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
 # every exported symbol with its ctypes signature (restype, argtypes); mirrors include/flink_window.h
 SIGNATURES = {
     "fw_create": (ctypes.c_int, [ctypes.POINTER(FwConfig), ctypes.POINTER(VP)]),
@@ -91,6 +105,13 @@ SIGNATURES = {
     "fw_comm_init": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(VP)]),
     "fw_comm_destroy": (None, [VP]),
     "fw_keyby_push_device": (ctypes.c_int, [VP, VP, VP, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, I64P]),
+    "fw_wire_create": (ctypes.c_int, [ctypes.POINTER(FwWireLayout), ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(VP)]),
+    "fw_wire_destroy": (None, [VP]),
+    "fw_wire_last_error": (ctypes.c_char_p, [VP]),
+    "fw_wire_decode_device": (ctypes.c_int, [VP, VP, ctypes.c_int64, VP, VP, VP, ctypes.c_int64,
+                                             ctypes.POINTER(FwWireStats)]),
+    "fw_wire_encode_device": (ctypes.c_int, [VP, ctypes.POINTER(FwRows), ctypes.c_int64, ctypes.c_int32, VP,
+                                             ctypes.c_int64, I64P]),
     "fw_generate_device": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, VP,
                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, VP, VP, VP, VP, VP]),
 }

@@ -300,6 +300,73 @@ void fw_comm_destroy(fw_comm* comm);
 int fw_keyby_push_device(fw_comm* comm, fw_op* op, const int64_t* key, const int64_t* ts, const void* val,
                          const int32_t* key_hash, int64_t n, int64_t local_wm, int64_t* combined_wm);
 
+/* ---- f2: Flink's wire format for one input channel <-> device columns.
+ * The byte stream of a channel is its network buffers in order: SpanningRecordSerializer.addRecord writes each
+ * StreamElement as a 4-byte big-endian length and then its bytes (flink-runtime/.../io/network/api/serialization/
+ * SpanningRecordSerializer.java:76-98), StreamElementSerializer (SJ/runtime/streamrecord/StreamElementSerializer
+ * .java:54-58, 167-221) writes a tag byte then
+ *   0 record with timestamp: BE i64 timestamp, the value      1 record without timestamp: the value
+ *   2 watermark: BE i64       3 latency marker: BE i64 marked time, BE i64 x 2 operator id, BE i32 subtask
+ *   4 stream status: BE i32   (any other tag: "Corrupt stream, found tag: X")
+ * and the value is a Tuple (TupleSerializer: fields in order, no null mask) of fixed-size fields, or one bare
+ * field: Long / Integer / Short / Byte / Boolean (BE two's complement) and Double / Float (BE
+ * doubleToLongBits / floatToIntBits).  String fields (StringValue's varint encoding) are not decoded yet.
+ *   fw_wire_decode_device: a device byte stream -> key / ts / val columns in arrival order (records without a
+ *     timestamp get Long.MIN_VALUE, StreamRecord.getTimestamp), ready for fw_push_batch_device.  The field whose
+ *     role is FW_ROLE_KEY becomes the key (an integer kind), FW_ROLE_VALUE the value (integers sign-extended,
+ *     Double as its bits, Float widened to double bits); other fields are skipped.  stats: the frames of each
+ *     kind, the last watermark (Long.MIN_VALUE if none: the caller's processWatermark), the last stream status
+ *     (StreamStatus ACTIVE 0 / IDLE -1; 0 if none), and `consumed` = the bytes up to the end of the last complete element (a trailing partial element is
+ *     the start of the next call's stream, SpillingAdaptiveSpanningRecordDeserializer's role).  Frames are
+ *     found in parallel: every 2 KiB chunk is parsed from each of its 64 possible first-frame offsets, and the
+ *     chunks' transfer functions are composed (a decoded element is at most 64 bytes with its length prefix:
+ *     value fields of at most 51 bytes).
+ *   fw_wire_encode_device: fired rows -> elements of one output channel: tag 0, timestamp = end - 1 (the
+ *     window's maxTimestamp, WindowOperator.emitWindowContents' TimestampedCollector), a Tuple of the row
+ *     fields the layout's roles name (FW_ROLE_KEY / START / END / COUNT / SUM / MIN / MAX).
+ * Both return FW_ERR_ARG for an unsupported layout and FW_ERR_STATE for a corrupt stream (message in
+ * fw_wire_last_error) or too small an output; they run on the codec's own stream and return when done. */
+#define FW_WIRE_LONG 0
+#define FW_WIRE_INT 1
+#define FW_WIRE_DOUBLE 2
+#define FW_WIRE_SHORT 3
+#define FW_WIRE_BYTE 4
+#define FW_WIRE_FLOAT 5
+#define FW_WIRE_BOOL 6
+#define FW_ROLE_SKIP 0
+#define FW_ROLE_KEY 1
+#define FW_ROLE_VALUE 2
+#define FW_ROLE_START 3
+#define FW_ROLE_END 4
+#define FW_ROLE_COUNT 5
+#define FW_ROLE_SUM 6
+#define FW_ROLE_MIN 7
+#define FW_ROLE_MAX 8
+#define FW_WIRE_MAX_FIELDS 8
+typedef struct {
+  int32_t nfields;                     /* 1 = a bare field, > 1 = a Tuple of that arity */
+  int32_t kind[FW_WIRE_MAX_FIELDS];    /* FW_WIRE_* */
+  int32_t role[FW_WIRE_MAX_FIELDS];    /* FW_ROLE_* */
+} fw_wire_layout;
+typedef struct {
+  int64_t records, watermarks, latency_markers, statuses;
+  int64_t consumed;                    /* bytes of complete elements */
+  int64_t watermark;                   /* the last watermark, Long.MIN_VALUE if none */
+  int32_t status;                      /* the last stream status (0 ACTIVE, -1 IDLE), 0 if none */
+  int32_t pad;
+} fw_wire_stats;
+typedef struct fw_wire fw_wire;
+/* max_bytes: the largest stream of one decode call; device: the HIP device of the buffers */
+int fw_wire_create(const fw_wire_layout* layout, int64_t max_bytes, int32_t device, fw_wire** out);
+void fw_wire_destroy(fw_wire* w);
+const char* fw_wire_last_error(const fw_wire* w);
+int fw_wire_decode_device(fw_wire* w, const uint8_t* bytes, int64_t nbytes, int64_t* key, int64_t* ts, int64_t* val,
+                          int64_t cap, fw_wire_stats* stats);
+/* rows: a device view (fw_rows_device); f64 = the rows' sum/min/max are double bits (FW_VAL_F64 aggregates);
+ * out: device bytes of capacity cap; *written = n * element size */
+int fw_wire_encode_device(fw_wire* w, const fw_rows* rows, int64_t n, int32_t f64, uint8_t* out, int64_t cap,
+                          int64_t* written);
+
 /* Synthetic source used by the benchmarks (the same counter-based generator as the CPU
  * baseline and the tests): record i of stream `seed` has
  *   key = splitmix64(seed ^ 4i) mod num_keys  (uniform)  or Zipf(zipf_s) over num_keys,

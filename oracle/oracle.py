@@ -234,3 +234,114 @@ def run_parallel(cfg, keys, ts, vals, batch, wms, max_par, threads):
     rows = lib().oracle_run_parallel(ctypes.byref(c), _i64p(keys), _i64p(ts), _i64p(vals), len(keys), batch,
                                      _i64p(wms), len(wms), max_par, threads, _i64p(late))
     return rows, int(late[0])
+
+
+# ---- f2: the wire format (wire_oracle.h) -------------------------------------------------------------
+WIRE_KINDS = {"long": 0, "int": 1, "double": 2, "short": 3, "byte": 4, "float": 5, "boolean": 6}
+WIRE_ROLES = {"skip": 0, "key": 1, "value": 2, "start": 3, "end": 4, "count": 5, "sum": 6, "min": 7, "max": 8}
+
+
+class OracleWireLayout(ctypes.Structure):
+    _fields_ = [("nfields", ctypes.c_int32), ("kind", ctypes.c_int32 * 8), ("role", ctypes.c_int32 * 8)]
+
+
+class OracleWireStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in ("records", "watermarks", "latency_markers", "statuses", "consumed",
+                                               "watermark")] + [("status", ctypes.c_int32), ("bad_tag", ctypes.c_int32)]
+
+
+_wire_ready = False
+
+
+def _wire_lib():
+    global _wire_ready
+    L = lib()
+    if not _wire_ready:
+        P, U8 = ctypes.c_void_p, ctypes.c_void_p
+        L.oracle_wire_decode.restype = ctypes.c_int
+        L.oracle_wire_decode.argtypes = [U8, ctypes.c_int64, ctypes.POINTER(OracleWireLayout), P, P, P, ctypes.c_int64,
+                                         ctypes.POINTER(OracleWireStats)]
+        L.oracle_wire_encode.restype = ctypes.c_int64
+        L.oracle_wire_encode.argtypes = [ctypes.POINTER(OracleWireLayout), P, ctypes.c_int64, ctypes.c_int32, U8,
+                                         ctypes.c_int64]
+        L.oracle_wire_put_record.restype = ctypes.c_int64
+        L.oracle_wire_put_record.argtypes = [ctypes.POINTER(OracleWireLayout), ctypes.c_int32, ctypes.c_int64, P, U8]
+        L.oracle_wire_put_watermark.restype = ctypes.c_int64
+        L.oracle_wire_put_watermark.argtypes = [ctypes.c_int64, U8]
+        L.oracle_wire_put_status.restype = ctypes.c_int64
+        L.oracle_wire_put_status.argtypes = [ctypes.c_int32, U8]
+        L.oracle_wire_put_latency.restype = ctypes.c_int64
+        L.oracle_wire_put_latency.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, U8]
+        _wire_ready = True
+    return L
+
+
+def wire_layout(fields):
+    L = OracleWireLayout()
+    L.nfields = len(fields)
+    for i, (k, r) in enumerate(fields):
+        L.kind[i] = WIRE_KINDS[k]
+        L.role[i] = WIRE_ROLES[r]
+    return L
+
+
+class WireStream:
+    """Builds a channel's bytes element by element (the reference serializers' output)."""
+
+    def __init__(self, fields):
+        self.fields = fields
+        self._L = wire_layout(fields)
+        self._parts = []
+
+    def record(self, values, ts=None):
+        buf = (ctypes.c_uint8 * 64)()
+        v = np.ascontiguousarray(values, dtype=np.int64)
+        n = _wire_lib().oracle_wire_put_record(ctypes.byref(self._L), int(ts is not None), 0 if ts is None else int(ts),
+                                               v.ctypes.data, ctypes.addressof(buf))
+        self._parts.append(bytes(buf[:n]))
+
+    def watermark(self, wm):
+        buf = (ctypes.c_uint8 * 16)()
+        n = _wire_lib().oracle_wire_put_watermark(int(wm), ctypes.addressof(buf))
+        self._parts.append(bytes(buf[:n]))
+
+    def status(self, s):
+        buf = (ctypes.c_uint8 * 16)()
+        n = _wire_lib().oracle_wire_put_status(int(s), ctypes.addressof(buf))
+        self._parts.append(bytes(buf[:n]))
+
+    def latency(self, marked, lo, hi, subtask):
+        buf = (ctypes.c_uint8 * 40)()
+        n = _wire_lib().oracle_wire_put_latency(int(marked), int(lo), int(hi), int(subtask), ctypes.addressof(buf))
+        self._parts.append(bytes(buf[:n]))
+
+    def raw(self, b):
+        self._parts.append(bytes(b))
+
+    def bytes(self):
+        return b"".join(self._parts)
+
+
+def wire_decode(data, fields, cap=None):
+    """-> (key, ts, val) int64 arrays, stats dict, rc (0 ok, -1 corrupt, -2 capacity)."""
+    b = np.frombuffer(bytes(data), dtype=np.uint8)
+    cap = len(b) // 10 + 1 if cap is None else cap
+    key, ts, val = (np.zeros(max(1, cap), dtype=np.int64) for _ in range(3))
+    st = OracleWireStats()
+    L = wire_layout(fields)
+    rc = _wire_lib().oracle_wire_decode(b.ctypes.data if len(b) else None, len(b), ctypes.byref(L), key.ctypes.data,
+                                        ts.ctypes.data, val.ctypes.data, cap, ctypes.byref(st))
+    r = st.records
+    return (key[:r], ts[:r], val[:r]), {f: getattr(st, f) for f, _ in OracleWireStats._fields_}, rc
+
+
+def wire_encode(rows, fields, f64=False):
+    rows = np.ascontiguousarray(rows, dtype=ROW_DTYPE)
+    L = wire_layout(fields)
+    size = 13 + sum({"long": 8, "double": 8, "int": 4, "float": 4, "short": 2, "byte": 1, "boolean": 1}[k]
+                    for k, _ in fields)
+    out = np.zeros(max(1, len(rows) * size), dtype=np.uint8)
+    n = _wire_lib().oracle_wire_encode(ctypes.byref(L), rows.ctypes.data, len(rows), int(f64), out.ctypes.data,
+                                       len(out))
+    assert n >= 0
+    return out[:n].tobytes()
