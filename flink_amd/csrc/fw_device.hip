@@ -2083,6 +2083,77 @@ __global__ __launch_bounds__(FW_AGG_THREADS, GATHER ? FW_GATHER_WAVES : SESS ? F
     atomicMax(&g_occ[2], run);
   }
   unsigned long long t_ld = 0, t_up = 0, t_bar = 0, ts_a = 0;
+  if (!SESS && onewin) {
+    // One window per record (tumbling, panes): the waves run free.  Each thread walks its rounds with the
+    // next round's records in flight while it upserts the current ones, and meets the others at a barrier
+    // only when some lane's upsert found the LDS table full (L.anyfail) or every wave is done; a full table
+    // is flushed there and every thread continues from its own (round, done mask).  A suspension keeps each
+    // thread's (round, mask) as of the last flush that succeeded (prog.tp: mask | round << 8).
+    const int64_t RS = (int64_t)blockDim.x * RPT;
+    int64_t myrb = resume ? begin + (int64_t)srwi * RS : begin;
+    uint32_t dm = resume ? (uint32_t)srj : 0u;
+    int64_t ck_rb = myrb;
+    uint32_t ck_dm = dm;
+    for (;;) {
+      if (myrb < end) {
+        i64x2 ca[RPT], cb[RPT];
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+          const int64_t i = myrb + (int64_t)j * blockDim.x + threadIdx.x;
+          load_prec_raw(cmp, part, i, i < end, ca[j], cb[j], g);
+        }
+        for (;;) {
+          if (__hip_atomic_load(&L.anyfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+          const int64_t nrb = myrb + RS;
+          i64x2 na[RPT], nb[RPT];
+#pragma unroll
+          for (int j = 0; j < RPT; j++) {
+            const int64_t i = nrb + (int64_t)j * blockDim.x + threadIdx.x;
+            load_prec_raw(cmp, part, i, i < end, na[j], nb[j], g);
+          }
+          int64_t k[RPT], t[RPT], v[RPT], o[RPT];
+          int nw[RPT];
+#pragma unroll
+          for (int j = 0; j < RPT; j++) unpack_prec<FIRST>(c, cmp, p, ca[j], cb[j], k[j], t[j], v[j], nw[j], o[j]);
+          uint32_t m = dm;
+#pragma unroll
+          for (int j = 0; j < RPT; j++)
+            if (myrb + (int64_t)j * blockDim.x + threadIdx.x >= end) m |= 1u << j;
+          if (c.diag & DIAG_AGG_NO_LDS) {
+#pragma unroll
+            for (int j = 0; j < RPT; j++) asm volatile("" ::"v"(k[j]), "v"(t[j]), "v"(v[j]), "v"(o[j]));
+          } else if (!lds_upsert_batch<RPT>(L, c.vtype, k, t, v, o, FIRST ? c.agg : 0, m)) {
+            dm = m;
+            __hip_atomic_store(&L.anyfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            break;
+          }
+          dm = 0;
+          myrb = nrb;
+          if (myrb >= end) break;
+#pragma unroll
+          for (int j = 0; j < RPT; j++) {
+            ca[j] = na[j];
+            cb[j] = nb[j];
+          }
+        }
+      }
+      __syncthreads();
+      const int need = L.anyfail;
+      __syncthreads();
+      if (!need) break;  // every wave has walked all of its rounds
+      if (!agg_flush_any<SESS>(c, L, sess_end, r, st)) {
+        ok = false;
+        break;
+      }
+      ck_rb = myrb;
+      ck_dm = dm;
+      if (threadIdx.x == 0) L.anyfail = 0;
+      __syncthreads();
+    }
+    srb = begin;
+    srj = (int)ck_dm;
+    srwi = (int)((ck_rb - begin) / RS);
+  } else
   for (int64_t rb = srb; rb < end && ok; rb += (int64_t)blockDim.x * RPT) {
     int64_t k[RPT], t[RPT], v[RPT], o[RPT];
     int nw[RPT];
@@ -2107,45 +2178,6 @@ __global__ __launch_bounds__(FW_AGG_THREADS, GATHER ? FW_GATHER_WAVES : SESS ? F
     if (c.diag & DIAG_AGG_NO_LDS) {
 #pragma unroll
       for (int j = 0; j < RPT; j++) asm volatile("" ::"v"(k[j]), "v"(t[j]), "v"(v[j]), "v"(nw[j]));
-      continue;
-    }
-    if (!SESS && onewin) {
-      // one window per record: srj / rj is the round's done mask (lds_upsert_batch)
-      uint32_t dm = first ? (uint32_t)srj : 0u;
-      first = false;
-#pragma unroll
-      for (int j = 0; j < RPT; j++)
-        if (rb + (int64_t)j * blockDim.x + threadIdx.x >= end) dm |= 1u << j;
-      for (;;) {
-        if (!lds_upsert_batch<RPT>(L, c.vtype, k, t, v, o, FIRST ? c.agg : 0, dm)) L.anyfail = 1;
-        if (timing) {
-          __builtin_amdgcn_s_waitcnt(0);
-          const unsigned long long x = __builtin_amdgcn_s_memtime();
-          t_up += x - ts_a;
-          ts_a = x;
-        }
-        __syncthreads();
-        const int need = L.anyfail;
-        __syncthreads();
-        if (timing) {
-          const unsigned long long x = __builtin_amdgcn_s_memtime();
-          t_bar += x - ts_a;
-          ts_a = x;
-        }
-        if (!need) break;
-        const unsigned long long tf0 = timing ? __builtin_amdgcn_s_memtime() : 0;
-        const bool fl = agg_flush_any<SESS>(c, L, sess_end, r, st);
-        if (timing) tflush += __builtin_amdgcn_s_memtime() - tf0;
-        if (!fl) {
-          ok = false;
-          break;
-        }
-        srb = rb;
-        srj = (int)dm;
-        srwi = 0;
-        if (threadIdx.x == 0) L.anyfail = 0;
-        __syncthreads();
-      }
       continue;
     }
     // progress (record rj, window rwi) survives a flush-and-retry when the LDS table fills up;

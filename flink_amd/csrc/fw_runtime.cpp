@@ -846,7 +846,9 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     HIP_OR_RETURN(op, dmalloc(&c.pool_ctr, 2));
     HIP_OR_RETURN(op, hipMemsetAsync(c.pool_ctr, 0, 2 * sizeof(int32_t), op->stream));
   }
-  c.log_r = std::max(8, ilog2(4 * ((expected + c.P - 1) / c.P)));
+  // regions sized for the expected entries at 1/FW_TABLE_SLACK load (default 4: 25 %; the limit is 3/4)
+  const int64_t slack = getenv("FW_TABLE_SLACK") ? std::max(2, atoi(getenv("FW_TABLE_SLACK"))) : 4;
+  c.log_r = std::max(8, ilog2(slack * ((expected + c.P - 1) / c.P)));
   op->table_slots = (int64_t)c.P << c.log_r;
 
   op->max_batch = cfg.max_batch > 0 ? std::min<int64_t>(cfg.max_batch, int64_t(1) << 31) : (int64_t(1) << 24);
