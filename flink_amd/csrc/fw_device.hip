@@ -1578,24 +1578,42 @@ __device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, con
   const uint32_t want = live_word(h);
   int32_t target = -1;
   Entry m;
-  for (uint32_t i = 0; i <= r.mask; i++) {
-    const uint32_t s = ((uint32_t)h + i) & r.mask;
-    const uint32_t stt = ld_state(r.state + s);
-    if (stt == SLOT_EMPTY) break;
-    if (stt != want) continue;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const Entry e = r.ent[s];
-    if (e.key != d.key || !(d.start <= e.end && d.end >= e.start)) continue;  // TimeWindow.intersects
-    if (target < 0) {
-      target = (int32_t)s;
-      m = e;
-      continue;
+  // the probe chain is read SW state words at a time, all in flight together (the key's entries lie before the
+  // chain's first EMPTY slot: slots of other keys claimed meanwhile by other threads do not matter here, and
+  // no slot becomes EMPTY during the launch); only the key's candidates' entries are then read
+  constexpr int SW = 16;
+  bool end_seen = false;
+  for (uint32_t i0 = 0; i0 <= r.mask && !end_seen; i0 += SW) {
+    uint32_t w[SW];
+#pragma unroll
+    for (int u = 0; u < SW; u++) w[u] = ld_state(r.state + (((uint32_t)h + i0 + u) & r.mask));
+    uint32_t cand = 0;
+#pragma unroll
+    for (int u = 0; u < SW; u++) {
+      if (end_seen) continue;
+      if (w[u] == SLOT_EMPTY)
+        end_seen = true;
+      else if (w[u] == want)
+        cand |= 1u << u;
     }
-    acc_merge(c, m, e);
-    m.start = min(m.start, e.start);
-    m.end = max(m.end, e.end);
-    // the slot stays occupied (live counts occupied slots) until k_fire rebuilds the region
-    __hip_atomic_store(r.state + s, SLOT_DEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cand) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    while (cand) {
+      const int u = __builtin_ctz(cand);
+      cand &= cand - 1;
+      const uint32_t s = ((uint32_t)h + i0 + u) & r.mask;
+      const Entry e = r.ent[s];
+      if (e.key != d.key || !(d.start <= e.end && d.end >= e.start)) continue;  // TimeWindow.intersects
+      if (target < 0) {
+        target = (int32_t)s;
+        m = e;
+        continue;
+      }
+      acc_merge(c, m, e);
+      m.start = min(m.start, e.start);
+      m.end = max(m.end, e.end);
+      // the slot stays occupied (live counts occupied slots) until k_fire rebuilds the region
+      __hip_atomic_store(r.state + s, SLOT_DEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   if (target < 0) {  // a new session
     *timer = jsub(d.end, 1);
@@ -1837,6 +1855,72 @@ __device__ __forceinline__ void unpack_prec(const DevCfg& c, bool cmp, int32_t p
   o = FIRST ? c.ord_base + (int64_t)((uint64_t)b.y >> 16) : 0;
 }
 
+// The free-running record walk of a one-window (or session) partition run [.., end): this thread's rounds from
+// myrb on (dm: the done mask of its first round), with the next round's records in flight while the current
+// ones are upserted, until its rounds are done or some lane of the workgroup found the LDS table full
+// (L.anyfail; the failing lane's round and mask stay in myrb / dm).  The caller meets the other waves at a
+// barrier, flushes or spills the table when L.anyfail is set, and calls again.
+template <int RPT, bool SESS, bool FIRST>
+__device__ __forceinline__ void agg_walk(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __restrict__ part, bool cmp,
+                                         int32_t p, int64_t end, int64_t RS, int64_t& myrb, uint32_t& dm,
+                                         const GatherRuns* g) {
+  if (myrb < end) {
+    i64x2 ca[RPT], cb[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; j++) {
+      const int64_t i = myrb + (int64_t)j * blockDim.x + threadIdx.x;
+      load_prec_raw(cmp, part, i, i < end, ca[j], cb[j], g);
+    }
+    for (;;) {
+      if (__hip_atomic_load(&L.anyfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+      const int64_t nrb = myrb + RS;
+      i64x2 na[RPT], nb[RPT];
+#pragma unroll
+      for (int j = 0; j < RPT; j++) {
+        const int64_t i = nrb + (int64_t)j * blockDim.x + threadIdx.x;
+        load_prec_raw(cmp, part, i, i < end, na[j], nb[j], g);
+      }
+      int64_t k[RPT], t[RPT], v[RPT], o[RPT];
+      int nw[RPT];
+#pragma unroll
+      for (int j = 0; j < RPT; j++) unpack_prec<FIRST>(c, cmp, p, ca[j], cb[j], k[j], t[j], v[j], nw[j], o[j]);
+      uint32_t m = dm;
+#pragma unroll
+      for (int j = 0; j < RPT; j++)
+        if (myrb + (int64_t)j * blockDim.x + threadIdx.x >= end) m |= 1u << j;
+      bool up = true;
+      if (c.diag & DIAG_AGG_NO_LDS) {
+#pragma unroll
+        for (int j = 0; j < RPT; j++) asm volatile("" ::"v"(k[j]), "v"(t[j]), "v"(v[j]), "v"(o[j]));
+      } else if constexpr (SESS) {
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+          if (!up || (m >> j & 1)) continue;
+          if (lds_session_upsert(L, E, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j], o[j], FIRST ? c.agg : 0))
+            m |= 1u << j;
+          else
+            up = false;
+        }
+      } else {
+        up = lds_upsert_batch<RPT>(L, c.vtype, k, t, v, o, FIRST ? c.agg : 0, m);
+      }
+      if (!up) {
+        dm = m;
+        __hip_atomic_store(&L.anyfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        break;
+      }
+      dm = 0;
+      myrb = nrb;
+      if (myrb >= end) break;
+#pragma unroll
+      for (int j = 0; j < RPT; j++) {
+        ca[j] = na[j];
+        cb[j] = nb[j];
+      }
+    }
+  }
+}
+
 template <int RPT, bool SESS, bool FIRST>
 __device__ __forceinline__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __restrict__ part, int64_t begin,
                           int64_t end, int32_t p, int32_t ch, int32_t nch, DevTable& tb, const AggProg& prog,
@@ -1856,47 +1940,17 @@ __device__ __forceinline__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E
   __syncthreads();
   if (!resume) {
     const int64_t cb = begin + (int64_t)ch * FW_AGG_CHUNK, ce = min(end, cb + (int64_t)FW_AGG_CHUNK);
-    for (int64_t rb = cb; rb < ce; rb += (int64_t)blockDim.x * RPT) {
-      int64_t k[RPT], t[RPT], v[RPT], o[RPT];
-      i64x2 ra[RPT], rbb[RPT];
-#pragma unroll
-      for (int j = 0; j < RPT; j++) {
-        const int64_t i = rb + (int64_t)j * blockDim.x + threadIdx.x;
-        load_prec_raw(cmp, part, i, i < ce, ra[j], rbb[j], g);
-      }
-#pragma unroll
-      for (int j = 0; j < RPT; j++) {
-        int nw;
-        unpack_prec<FIRST>(c, cmp, p, ra[j], rbb[j], k[j], t[j], v[j], nw, o[j]);
-      }
-      int rj = 0;
-      for (;;) {
-        bool failed = false;
-#pragma unroll
-        for (int j = 0; j < RPT; j++) {
-          if (failed || j < rj || rb + (int64_t)j * blockDim.x + threadIdx.x >= ce) continue;
-          bool in;
-          if constexpr (SESS)
-            in = lds_session_upsert(L, E, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j], o[j], FIRST ? c.agg : 0);
-          else
-            in = lds_upsert(L, c.vtype, k[j], t[j], v[j], 0, o[j], FIRST ? c.agg : 0);
-          if (!in) {
-            failed = true;
-            rj = j;
-          }
-        }
-        if (failed)
-          L.anyfail = 1;
-        else
-          rj = RPT;
-        __syncthreads();
-        const int need = L.anyfail;
-        __syncthreads();
-        if (!need) break;
-        agg_spill<SESS>(c, L, E, hot.delta + cb);
-        if (threadIdx.x == 0) L.anyfail = 0;
-        __syncthreads();
-      }
+    int64_t myrb = cb;
+    uint32_t dm = 0;
+    for (;;) {  // free-running waves (agg_walk); the table is spilled as deltas whenever it fills
+      agg_walk<RPT, SESS, FIRST>(c, L, E, part, cmp, p, ce, (int64_t)blockDim.x * RPT, myrb, dm, g);
+      __syncthreads();
+      const int need = L.anyfail;
+      __syncthreads();
+      if (!need) break;
+      agg_spill<SESS>(c, L, E, hot.delta + cb);
+      if (threadIdx.x == 0) L.anyfail = 0;
+      __syncthreads();
     }
     agg_spill<SESS>(c, L, E, hot.delta + cb);
     if (threadIdx.x == 0) hot.nd[c0 + ch] = L.spill;
@@ -2083,8 +2137,8 @@ __global__ __launch_bounds__(FW_AGG_THREADS, GATHER ? FW_GATHER_WAVES : SESS ? F
     atomicMax(&g_occ[2], run);
   }
   unsigned long long t_ld = 0, t_up = 0, t_bar = 0, ts_a = 0;
-  if (!SESS && onewin) {
-    // One window per record (tumbling, panes): the waves run free.  Each thread walks its rounds with the
+  if (SESS || onewin) {
+    // One window per record (tumbling, panes, session elements): the waves run free.  Each thread walks its rounds with the
     // next round's records in flight while it upserts the current ones, and meets the others at a barrier
     // only when some lane's upsert found the LDS table full (L.anyfail) or every wave is done; a full table
     // is flushed there and every thread continues from its own (round, done mask).  A suspension keeps each
@@ -2095,48 +2149,7 @@ __global__ __launch_bounds__(FW_AGG_THREADS, GATHER ? FW_GATHER_WAVES : SESS ? F
     int64_t ck_rb = myrb;
     uint32_t ck_dm = dm;
     for (;;) {
-      if (myrb < end) {
-        i64x2 ca[RPT], cb[RPT];
-#pragma unroll
-        for (int j = 0; j < RPT; j++) {
-          const int64_t i = myrb + (int64_t)j * blockDim.x + threadIdx.x;
-          load_prec_raw(cmp, part, i, i < end, ca[j], cb[j], g);
-        }
-        for (;;) {
-          if (__hip_atomic_load(&L.anyfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-          const int64_t nrb = myrb + RS;
-          i64x2 na[RPT], nb[RPT];
-#pragma unroll
-          for (int j = 0; j < RPT; j++) {
-            const int64_t i = nrb + (int64_t)j * blockDim.x + threadIdx.x;
-            load_prec_raw(cmp, part, i, i < end, na[j], nb[j], g);
-          }
-          int64_t k[RPT], t[RPT], v[RPT], o[RPT];
-          int nw[RPT];
-#pragma unroll
-          for (int j = 0; j < RPT; j++) unpack_prec<FIRST>(c, cmp, p, ca[j], cb[j], k[j], t[j], v[j], nw[j], o[j]);
-          uint32_t m = dm;
-#pragma unroll
-          for (int j = 0; j < RPT; j++)
-            if (myrb + (int64_t)j * blockDim.x + threadIdx.x >= end) m |= 1u << j;
-          if (c.diag & DIAG_AGG_NO_LDS) {
-#pragma unroll
-            for (int j = 0; j < RPT; j++) asm volatile("" ::"v"(k[j]), "v"(t[j]), "v"(v[j]), "v"(o[j]));
-          } else if (!lds_upsert_batch<RPT>(L, c.vtype, k, t, v, o, FIRST ? c.agg : 0, m)) {
-            dm = m;
-            __hip_atomic_store(&L.anyfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            break;
-          }
-          dm = 0;
-          myrb = nrb;
-          if (myrb >= end) break;
-#pragma unroll
-          for (int j = 0; j < RPT; j++) {
-            ca[j] = na[j];
-            cb[j] = nb[j];
-          }
-        }
-      }
+      agg_walk<RPT, SESS, FIRST>(c, L, sess_end, part, cmp, p, end, RS, myrb, dm, g);
       __syncthreads();
       const int need = L.anyfail;
       __syncthreads();

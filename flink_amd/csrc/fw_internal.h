@@ -74,7 +74,7 @@
 // its registers (a call saves the live VGPRs to scratch)
 #ifndef FW_AGG_TIMING_BUILD
 #define FW_AGG_TIMING_BUILD 0
-#endif   // ordered replay workgroup (one workgroup)
+#endif
 
 enum : uint32_t { SLOT_EMPTY = 0, SLOT_LIVE = 1, SLOT_DEAD = 2, SLOT_BUSY = 3 };
 enum : int64_t { FW_TIMER = 1 };

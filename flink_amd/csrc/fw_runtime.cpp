@@ -782,7 +782,11 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     // several times into its region (C3, 2M keys: 4096 partitions halve k_aggregate's time)
     const int64_t wins = cfg.assigner == FW_SLIDING ? cfg.size / cfg.slide + 1 : 2;  // live windows per key
     const int64_t keys = cfg.expected_entries > 0 ? cfg.expected_entries / wins : 0;
-    const int64_t target = std::min<int64_t>(16384, std::max<int64_t>(2048, next_pow2(std::max<int64_t>(1, keys / 512))));
+    // tumbling count/sum/min/max: ~256 keys, so a batch that spans a window boundary (two windows per key)
+    // still fits the LDS table once (C2: 4096 partitions, k_aggregate 0.36 -> 0.28 ms; sessions, HLL and
+    // t-digest measured no better or worse with the smaller partitions)
+    const int64_t per = cfg.assigner == FW_TUMBLING && cfg.aggregate == FW_AGG_COUNT_SUM_MIN_MAX ? 256 : 512;
+    const int64_t target = std::min<int64_t>(16384, std::max<int64_t>(2048, next_pow2(std::max<int64_t>(1, keys / per))));
     s = std::max<int64_t>(1, next_pow2(std::max<int64_t>(1, target / c.n_kg)));
   }
   c.log_s = ilog2(s);
