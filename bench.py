@@ -162,6 +162,8 @@ def main():
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic summary (tools/traffic.py); default the newest profiles/traffic_*<workload>.json")
     ap.add_argument("--sub-partitions", type=int, default=0, help="state partitions per key group (0 = auto)")
+    ap.add_argument("--sync-input", action="store_true",
+                    help="partition each batch on the operator's own stream (no overlap with the previous batch)")
     args = ap.parse_args()
     preset = PRESETS[args.workload]
     w = args.workload
@@ -217,7 +219,7 @@ def main():
                            device=local_rank, max_parallelism=max_par,
                            expected_entries=(1000 if c1 else live_windows * args.keys // world),
                            max_batch=args.batch if world == 1 else 2 * args.batch,
-                           sub_partitions=args.sub_partitions)
+                           sub_partitions=args.sub_partitions, async_input=not args.sync_input)
     if sliding and args.steady:
         # steady state: the warmup covers one window size of event time, so the timed steps see the
         # full pane population (size/slide + 1 panes per key) and windows merging size/slide panes
@@ -242,7 +244,10 @@ def main():
     # punctuated watermark of this rank's source after each batch: max ts so far - bound
     batches, local_wm = {}, {}
     m = -(1 << 63)
-    for s in range(args.warmup, steps_total):
+    # with async input the timed region overlaps each batch's partitioning with the previous batch's aggregation,
+    # so the kernels' own durations are also measured in an isolated pass of as many steps after it
+    iso_steps = args.steps if (not args.no_profile and not args.sync_input) else 0
+    for s in range(args.warmup, steps_total + iso_steps):
         k, t, v, mx, h = generate(s)
         batches[s] = (k, t, v, h)
         local_wm[s] = int(mx.item())  # this batch's max; made cumulative once the warmup's is known
@@ -272,7 +277,7 @@ def main():
 
     for s in range(args.warmup):
         step(s)
-    for j in range(args.warmup, steps_total):  # fold the warmup's running max into the staged batch maxima
+    for j in range(args.warmup, steps_total + iso_steps):  # fold the warmup's running max into the staged batch maxima
         m = max(m, local_wm[j])
         local_wm[j] = m - args.bound
     L = N.lib()
@@ -343,6 +348,31 @@ def main():
                     "traffic_over_alg": None if traffic is None else round(traffic / alg, 3),
                     "traffic_per_record": None if traffic is None else round(traffic / per_launch_records, 2),
                     "basis": "SURVEY §8d B_alg x records per launch / the kernel's average HIP-event duration"}
+    kernels_iso = None
+    if iso_steps:
+        import ctypes
+        kernels_iso = {}
+        op.set_async_input(False)  # (synchronizes)
+        L.fw_profile_read(op._h, None, None, 1)
+        for s in range(steps_total, steps_total + iso_steps):
+            step(s)
+        op.synchronize()
+        ms_i = (ctypes.c_double * N.FW_NUM_KERNELS)()
+        nl_i = (ctypes.c_int64 * N.FW_NUM_KERNELS)()
+        L.fw_profile_read(op._h, ms_i, nl_i, 1)
+        for i in range(N.FW_NUM_KERNELS):
+            if nl_i[i]:
+                kernels_iso[L.fw_kernel_name(i).decode()] = {"launches": int(nl_i[i]),
+                                                             "avg_ms": round(ms_i[i] / nl_i[i], 5)}
+    if kernels_iso and roofline:
+        # the same kernel's own duration: the isolated pass (its batch partitioned on the operator's stream)
+        ki = kernels_iso.get(roofline["kernel"])
+        if ki:
+            a_i = alg / (ki["avg_ms"] * 1e-3) / 1e9
+            roofline["isolated"] = {"avg_ms": ki["avg_ms"], "achieved": round(a_i, 1),
+                                    "frac": round(a_i / HBM_PEAK_GBS, 4),
+                                    "basis": f"{iso_steps} further steps after the timed region with --sync-input "
+                                             "(no overlap): the kernel's duration alone on the GPU"}
 
     count_gpu = None
     if c1 and world == 1:
@@ -350,7 +380,7 @@ def main():
 
     host_fed = None
     if rank == 0 and world == 1 and args.host_fed_steps > 0:
-        host_fed = host_fed_leg(args, op, generate, steps_total, m, c1)
+        host_fed = host_fed_leg(args, op, generate, steps_total + iso_steps, m, c1)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -380,6 +410,7 @@ def main():
             **({"count_window_gpu": count_gpu} if count_gpu else {}),
             "cpu_baseline": cpu,
             "kernels": kernels,
+            **({"kernels_isolated": kernels_iso} if kernels_iso else {}),
             "state": {"table_slots": int(st1["table_capacity"]), "table_grows_in_timed_region":
                       int(st1["table_grows"] - st0["table_grows"]), "live_entries": int(st1["keyed_state_entries"])},
         }

@@ -95,6 +95,8 @@ SIGNATURES = {
     "fw_profile_read": (ctypes.c_int, [VP, ctypes.POINTER(ctypes.c_double), I64P, ctypes.c_int]),
     "fw_kernel_name": (ctypes.c_char_p, [ctypes.c_int]),
     "fw_stream": (VP, [VP]),
+    "fw_set_async_input": (ctypes.c_int, [VP, ctypes.c_int]),
+    "fw_input_stream": (VP, [VP]),
     "fw_snapshot_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), ctypes.c_int64, I64P]),
     "fw_restore_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), ctypes.c_int64]),
     "fw_key_groups_device": (ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, VP, VP]),

@@ -602,7 +602,7 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_classify_hist(DevCfg c, int
   if (threadIdx.x == 0) hist[(int64_t)(c.P + 1) * T + tile] = lh[c.P];
   if (bad_kg) atomicAdd(&st->kg_errors, bad_kg);
   if (bad_ts) atomicAdd(&st->ts_errors, bad_ts);
-  if (wide) atomicOr(&st->wide, 1);
+  if (wide) atomicOr(c.wide, 1);
 }
 
 // ---- generic in-place exclusive scan of uint32 (block = 1024 threads x 4 elements)
@@ -713,7 +713,7 @@ __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(D
   const int64_t tend = min(n, tbase + (int64_t)FW_TILE);
   unsigned long long late = 0;
   const int taint = c.assigner == FW_SESSION ? st->taint_any : 0;
-  const bool cmp = c.compact && !st->wide;  // (uniform: every classify workgroup has finished)
+  const bool cmp = c.compact && !*c.wide;  // (uniform: every classify workgroup has finished)
   for (int64_t b = tbase; b < tend; b += (int64_t)blockDim.x * FW_RPT) {
     int64_t k[FW_RPT], t[FW_RPT], v[FW_RPT];
     int32_t hh[FW_RPT];
@@ -1927,7 +1927,7 @@ __device__ __forceinline__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E
                           int resume, const AggHot& hot, Status* st, const GatherRuns* g) {
   const int32_t c0 = (int32_t)hot.chunk_base[p];
   if (resume && (ch != 0 || prog.done[p])) return;
-  const bool cmp = g || (c.compact && !st->wide);
+  const bool cmp = g || (c.compact && !*c.wide);
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
   if (threadIdx.x == 0) {
     L.fill = 0;
@@ -2098,7 +2098,7 @@ __global__ __launch_bounds__(FW_AGG_THREADS, GATHER ? FW_GATHER_WAVES : SESS ? F
     return;
   }
   if (resume && prog.done[p]) return;
-  const bool cmp = GATHER || (c.compact && !st->wide);
+  const bool cmp = GATHER || (c.compact && !*c.wide);
   const int64_t begin = offs[(int64_t)p * T], end = offs[(int64_t)(p + 1) * T];
   if (begin == end) {
     if (threadIdx.x == 0) prog.done[p] = 1;
@@ -2693,7 +2693,7 @@ __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __rest
   }
   __syncthreads();
   const int p = c.hll_p;
-  const bool cmp = c.compact && !st->wide;
+  const bool cmp = c.compact && !*c.wide;
   const int64_t i1 = min(total, i0 + (int64_t)FW_HLL_CHUNK);
   const int64_t hdr = hll_hdr_bytes(p);
   // HU records per thread in flight: the record, its home slot's state word and entry identity, the entry's
@@ -3027,7 +3027,7 @@ __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restric
     p0_s = lo;
   }
   __syncthreads();
-  const bool cmp = c.compact && !st->wide;
+  const bool cmp = c.compact && !*c.wide;
   int32_t pp = p0_s;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     if (i >= total) {

@@ -133,9 +133,12 @@ struct DevCfg {
   // are the record's sub-partition (known to the partition's workgroup), so those bits carry the window
   // instead: d = (start - cbase) / slide in [0, 2^log_s).  `compact` = the configuration allows it (set at
   // creation; 0 for this launch when the watermark gives no representable base); a batch with a normal
-  // record whose window is out of range sets Status.wide and goes through PRec.
+  // record whose window is out of range sets *DevCfg::wide and goes through PRec.
   int32_t compact;
   int64_t cbase;
+  // the batch's "some record has no compact form" flag (set by k_classify_hist, read by the kernels that read
+  // its partitioned records); one word per scratch set, so the next batch's classify may run beside them
+  int32_t* wide;
 };
 
 // host: reciprocal of d >= 1 for div_inv(): m = floor(2^64 (2^l - d) / d) + 1, l = ceil(log2 d)
@@ -205,7 +208,6 @@ struct Status {
   int32_t suspended;                  // FW_SUSP_*: later kernels of the push / watermark skip themselves
   int32_t need_grow;                  // some region is over half full: grow before it has to suspend
   int32_t taint_any;                  // sessions: 0 no tainted key in the batch, 1 check the set, 2 set full: all
-  int32_t wide;                       // DevCfg::compact: some normal record's window is out of range: PRec
 };
 enum {
   FW_STATUS_STATE_LOST = 1,  // a window could not be stored (more in-flight sessions of one key than supported)

@@ -49,6 +49,7 @@ struct Scratch {
   int32_t compact = 0;           // DevCfg::compact / cbase of the batch (a resumed aggregate reads the same form)
   int64_t cbase = 0;
   int64_t ord_base = 0;          // arrival ordinal of the batch's first record (ordinal aggregates)
+  int32_t* wide = nullptr;       // DevCfg::wide of the batches that use this set
   // gathered batches (fwdev::gather_mode): runs table [T8][P] and its transpose, the partitions' virtual
   // offsets (P + 1) and the ordered-path rows (2 x T8); T is then the batch's FW_GTILE tiles
   uint32_t *rt = nullptr, *rt_t = nullptr, *voffs = nullptr, *gsrow = nullptr, *gcb = nullptr;
@@ -67,6 +68,12 @@ struct fw_op {
   DevCfg dc{};
   int device = 0;
   hipStream_t stream = nullptr;
+  // async input (fw_set_async_input): a device push's batch-only kernels (classify, scan, scatter) run on
+  // bstream, beside the previous batch's aggregate and firing on `stream`; ev_scat[set] orders the batch's
+  // aggregate after them, ev_done[set] the reuse of a scratch set after the aggregate of its previous batch
+  hipStream_t bstream = nullptr;
+  hipEvent_t ev_scat[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+  bool async_in = false;
   std::string err;
 
   // state table
@@ -191,6 +198,7 @@ int alloc_scratch(fw_op* op, Scratch& s, int64_t mb, int64_t m) {
   HIP_OR_RETURN(op, dmalloc(&s.stt, mb));
   HIP_OR_RETURN(op, dmalloc(&s.sv, mb));
   HIP_OR_RETURN(op, dmalloc(&s.skh, mb));
+  HIP_OR_RETURN(op, dmalloc(&s.wide, 1));
   if (op->cfg.aggregate >= FW_AGG_FIRST && op->cfg.aggregate <= FW_AGG_FIRST_MAX) HIP_OR_RETURN(op, dmalloc(&s.so, mb));
   if (op->cfg.aggregate == FW_AGG_MINBY || op->cfg.aggregate == FW_AGG_MAXBY) HIP_OR_RETURN(op, dmalloc(&s.byv, mb));
   DevCfg probe = op->dc;
@@ -213,6 +221,7 @@ void free_scratch(Scratch& s) {
   dfree(s.stt);
   dfree(s.sv);
   dfree(s.skh);
+  dfree(s.wide);
   dfree(s.so);
   dfree(s.byv);
   dfree(s.rt);
@@ -317,15 +326,16 @@ hipEvent_t prof_event(fw_op* op) {
 }
 // time the launches issued by `launch` on the handle's stream as one interval of `kind`
 template <class F>
-void timed(fw_op* op, int kind, F&& launch) {
+void timed(fw_op* op, int kind, F&& launch, hipStream_t on = nullptr) {
   if (!op->prof) {
     launch();
     return;
   }
+  if (!on) on = op->stream;
   fw_op::Pair pr{prof_event(op), prof_event(op), kind};
-  (void)hipEventRecord(pr.a, op->stream);
+  (void)hipEventRecord(pr.a, on);
   launch();
-  (void)hipEventRecord(pr.b, op->stream);
+  (void)hipEventRecord(pr.b, on);
   op->prof_pending.push_back(pr);
 }
 // fold the completed intervals into the totals (intervals still in flight stay pending)
@@ -459,6 +469,7 @@ int settle(fw_op* op) {
     c.compact = S.compact;
     c.cbase = S.cbase;
     c.ord_base = S.ord_base;
+    c.wide = S.wide;
     if (susp & FW_SUSP_AGG)
       timed(op, K_AGGREGATE, [&] {
         fwdev::launch_aggregate(c, S.wm, S.part, S.offs(), S.offT(), op->tb, op->prog, 1, S.split ? &op->hot : nullptr,
@@ -555,7 +566,8 @@ int push_count(fw_op* op, const int64_t* key, const int64_t* val, int64_t n) {
   return snapshot(op);
 }
 
-int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int64_t n) {
+int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int64_t n,
+                bool async_ok) {
   if (n == 0) return FW_OK;
   if (op->cfg.assigner == FW_COUNT) return push_count(op, key, val, n);
   int rc;
@@ -573,6 +585,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   Scratch& S = op->sc[nxt];
   c.ord_base = op->records_in;  // FW_AGG_FIRST: arrival ordinals of this batch start here
   c.slow_ord = S.so;
+  c.wide = S.wide;
   auto aligned = [](const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
   c.vec_in = aligned(key, 16) && aligned(ts, 16) && aligned(val, 16) && (!kh || aligned(kh, 8));
   if (c.compact) {
@@ -590,16 +603,20 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   const bool gather = S.rt && fwdev::gather_mode(c, n);
   const int32_t T = gather ? (int32_t)((n + FW_GTILE - 1) / FW_GTILE) : (int32_t)((n + FW_TILE - 1) / FW_TILE);
   const int64_t m = (int64_t)(c.P + 1) * T;
+  // async input: the batch-only kernels run on bstream, after the aggregate that last used this scratch set
+  const bool two = async_ok && op->async_in && !c.side_output && !gather;
+  hipStream_t bs = two ? op->bstream : op->stream;
+  if (two) HIP_OR_RETURN(op, hipStreamWaitEvent(bs, op->ev_done[nxt], 0));
   if (c.assigner == FW_SESSION) {
     // a new epoch empties the taint set; its slots are cleared only when the epochs wrap
     if (++op->taint_epoch >= 0x80000000u) {
-      HIP_OR_RETURN(op, hipMemsetAsync(c.taint_state, 0, ((size_t)c.taint_mask + 1) * sizeof(uint32_t), op->stream));
+      HIP_OR_RETURN(op, hipMemsetAsync(c.taint_state, 0, ((size_t)c.taint_mask + 1) * sizeof(uint32_t), bs));
       op->taint_epoch = 1;
     }
     c.taint_epoch = op->taint_epoch;
-    HIP_OR_RETURN(op, hipMemsetAsync(&op->d_status->taint_any, 0, sizeof(int32_t), op->stream));
+    HIP_OR_RETURN(op, hipMemsetAsync(&op->d_status->taint_any, 0, sizeof(int32_t), bs));
   }
-  if (c.compact) HIP_OR_RETURN(op, hipMemsetAsync(&op->d_status->wide, 0, sizeof(int32_t), op->stream));
+  if (c.compact) HIP_OR_RETURN(op, hipMemsetAsync(S.wide, 0, sizeof(int32_t), bs));
   if (gather) {
     // classify, tile-local partition sort, runs table, ordered-path compaction: one pass over the input
     timed(op, K_SCATTER, [&] {
@@ -607,22 +624,32 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
                           S.stt, S.sv, S.skh, op->side, op->d_status, op->stream);
     });
   } else {
-    timed(op, K_CLASSIFY, [&] {
-      if (c.assigner == FW_SESSION) fwdev::launch_taint(c, op->wm, key, ts, n, op->d_status, op->stream);
-      fwdev::launch_classify_hist(c, op->wm, key, ts, kh, n, T, S.hist, op->d_status, op->stream);
-    });
-    timed(op, K_SCAN, [&] { fwdev::launch_scan(S.hist, m, S.scan_tmp, op->stream); });
-    timed(op, K_SCATTER, [&] {
-      fwdev::launch_scatter(c, op->wm, key, ts, val, kh, n, T, S.hist, S.part, S.sk, S.stt, S.sv, S.skh, op->side,
-                            op->d_status, op->stream);
-    });
+    timed(
+        op, K_CLASSIFY,
+        [&] {
+          if (c.assigner == FW_SESSION) fwdev::launch_taint(c, op->wm, key, ts, n, op->d_status, bs);
+          fwdev::launch_classify_hist(c, op->wm, key, ts, kh, n, T, S.hist, op->d_status, bs);
+        },
+        bs);
+    timed(op, K_SCAN, [&] { fwdev::launch_scan(S.hist, m, S.scan_tmp, bs); }, bs);
+    timed(
+        op, K_SCATTER,
+        [&] {
+          fwdev::launch_scatter(c, op->wm, key, ts, val, kh, n, T, S.hist, S.part, S.sk, S.stt, S.sv, S.skh, op->side,
+                                op->d_status, bs);
+        },
+        bs);
   }
   S.gather = gather;
   S.T = T;
   // minBy / maxBy: the aggregate reads the selected elements' fields back by batch index, possibly after the
   // caller's columns are gone (a resumed push), so the batch keeps its own copy
-  if (S.byv) HIP_OR_RETURN(op, hipMemcpyAsync(S.byv, val, n * sizeof(int64_t), hipMemcpyDeviceToDevice, op->stream));
+  if (S.byv) HIP_OR_RETURN(op, hipMemcpyAsync(S.byv, val, n * sizeof(int64_t), hipMemcpyDeviceToDevice, bs));
   HIP_OR_RETURN(op, hipGetLastError());
+  if (two) {  // the batch's aggregate waits for its scatter
+    HIP_OR_RETURN(op, hipEventRecord(op->ev_scat[nxt], bs));
+    HIP_OR_RETURN(op, hipStreamWaitEvent(op->stream, op->ev_scat[nxt], 0));
+  }
   if (early && (rc = settle(op))) return rc;
   if ((rc = maybe_restart_rows(op))) return rc;
   // the ordered path checks its room per chunk and suspends when it runs out; one chunk always fits
@@ -635,6 +662,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   cc.by_val = S.byv;
   cc.compact = c.compact;
   cc.cbase = c.cbase;
+  cc.wide = S.wide;
   // a partition can outgrow one aggregate workgroup (hot keys) only when the batch is longer than a chunk
   const bool split = (cc.wpr == 1 || cc.panes) && n > FW_AGG_CHUNK;
   if (split && (rc = ensure_hot(op))) return rc;
@@ -653,6 +681,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
                        op->stream);
   });
   HIP_OR_RETURN(op, hipGetLastError());
+  HIP_OR_RETURN(op, hipEventRecord(op->ev_done[nxt], op->stream));  // the set's last use by this batch (see settle)
   S.T = T;
   S.n = n;
   S.split = split;
@@ -760,6 +789,10 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   op->device = cfg.device;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   HIP_OR_RETURN(op, hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking));
+  HIP_OR_RETURN(op, hipStreamCreateWithFlags(&op->bstream, hipStreamNonBlocking));
+  for (hipEvent_t* e : {&op->ev_scat[0], &op->ev_scat[1], &op->ev_done[0], &op->ev_done[1]})
+    HIP_OR_RETURN(op, hipEventCreateWithFlags(e, hipEventDisableTiming));
+  for (hipEvent_t e : {op->ev_done[0], op->ev_done[1]}) HIP_OR_RETURN(op, hipEventRecord(e, op->stream));
   HIP_OR_RETURN(op, hipEventCreateWithFlags(&op->snap, hipEventDisableTiming));
 
   DevCfg& c = op->dc;
@@ -868,6 +901,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   HIP_OR_RETURN(op, dmalloc(&op->in_kh, mb));
   for (Scratch& sc : op->sc)
     if ((rc = alloc_scratch(op, sc, mb, m))) return rc;
+  c.wide = op->sc[0].wide;  // (every push sets its own set's word)
   if (c.assigner == FW_SESSION) {
     // the batches' taint set (k_taint): 2x the batch, at most 2^22 slots; a batch whose ordered-path
     // keys overflow it replays all of its records in arrival order
@@ -948,6 +982,7 @@ void fw_destroy(fw_op* op) {
   if (!op) return;
   if (op->stream) {
     (void)hipSetDevice(op->device);
+    if (op->bstream) (void)hipStreamSynchronize(op->bstream);
     (void)hipStreamSynchronize(op->stream);
   }
   free_table(op->tb);
@@ -1019,6 +1054,9 @@ void fw_destroy(fw_op* op) {
   for (hipEvent_t e : op->prof_free) (void)hipEventDestroy(e);
   if (op->snap) (void)hipEventDestroy(op->snap);
   if (op->h_status) (void)hipHostFree(op->h_status);
+  for (hipEvent_t e : {op->ev_scat[0], op->ev_scat[1], op->ev_done[0], op->ev_done[1]})
+    if (e) (void)hipEventDestroy(e);
+  if (op->bstream) (void)hipStreamDestroy(op->bstream);
   if (op->stream) (void)hipStreamDestroy(op->stream);
   delete op;
 }
@@ -1038,25 +1076,43 @@ int fw_push_batch(fw_op* op, const int64_t* key, const int64_t* ts, const void* 
     HIP_OR_RETURN(op, hipMemcpyAsync(op->in_val, (const int64_t*)val + b, m * 8, hipMemcpyHostToDevice, op->stream));
     if (op->cfg.key_kind == FW_KEY_HASHED)
       HIP_OR_RETURN(op, hipMemcpyAsync(op->in_kh, key_hash + b, m * 4, hipMemcpyHostToDevice, op->stream));
-    int rc = push_device(op, op->in_key, op->in_ts, op->in_val, op->in_kh, m);
+    int rc = push_device(op, op->in_key, op->in_ts, op->in_val, op->in_kh, m, false);
     if (rc) return rc;
   }
   return settle(op);  // host columns: the caller may reuse them when this returns
 }
 
-int fw_push_batch_device(fw_op* op, const int64_t* key, const int64_t* ts, const void* val, const int32_t* key_hash,
-                         int64_t n) {
+namespace {
+int push_device_batches(fw_op* op, const int64_t* key, const int64_t* ts, const void* val, const int32_t* key_hash,
+                        int64_t n, bool async_ok) {
   if (!op || n < 0 || (n > 0 && (!key || !ts || !val))) return op ? set_err(op, FW_ERR_ARG, "null column") : FW_ERR_ARG;
   if (op->cfg.key_kind == FW_KEY_HASHED && n > 0 && !key_hash)
     return set_err(op, FW_ERR_ARG, "key_hash required for FW_KEY_HASHED");
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   for (int64_t b = 0; b < n; b += op->max_batch) {
     const int64_t m = std::min(op->max_batch, n - b);
-    int rc = push_device(op, key + b, ts + b, (const int64_t*)val + b, key_hash ? key_hash + b : nullptr, m);
+    int rc = push_device(op, key + b, ts + b, (const int64_t*)val + b, key_hash ? key_hash + b : nullptr, m, async_ok);
     if (rc) return rc;
   }
   return FW_OK;
 }
+}  // namespace
+
+int fw_push_batch_device(fw_op* op, const int64_t* key, const int64_t* ts, const void* val, const int32_t* key_hash,
+                         int64_t n) {
+  return push_device_batches(op, key, ts, val, key_hash, n, true);
+}
+
+int fw_set_async_input(fw_op* op, int enable) {
+  if (!op) return FW_ERR_ARG;
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  int rc = fw_synchronize(op);
+  if (rc) return rc;
+  op->async_in = enable != 0;
+  return FW_OK;
+}
+
+void* fw_input_stream(fw_op* op) { return op ? (void*)(op->async_in ? op->bstream : op->stream) : nullptr; }
 
 int fw_advance_watermark(fw_op* op, int64_t wm, int64_t* n_pending) {
   if (!op) return FW_ERR_ARG;
@@ -1252,6 +1308,7 @@ int fw_synchronize(fw_op* op) {
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc = settle(op);
   if (rc) return rc;
+  HIP_OR_RETURN(op, hipStreamSynchronize(op->bstream));
   HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
   return FW_OK;
 }
@@ -1590,7 +1647,8 @@ int fw_keyby_push_device(fw_comm* c, fw_op* op, const int64_t* key, const int64_
   NCCL_OR_RETURN(op, ncclGroupEnd());
   if (combined_wm) *combined_wm = c->h_counts[2 * W + 1];
   // processElement for the received batch (stream-ordered behind the receives)
-  return fw_push_batch_device(op, c->rk, c->rt, c->rv, hashed ? c->rh : nullptr, total);
+  // (the columns were received on the handle's stream, so the push reads them in its order)
+  return push_device_batches(op, c->rk, c->rt, c->rv, hashed ? c->rh : nullptr, total, false);
 }
 
 int fw_generate_device(uint64_t seed, int64_t first, int64_t n, int64_t num_keys, const double* zipf_cdf,

@@ -36,7 +36,7 @@ class GpuWindowOperator:
     def __init__(self, assigner: WindowAssigner, aggregate=CountSumMinMax(), trigger: Trigger = None,
                  allowed_lateness=0, side_output=False, key_type="long", max_parallelism=128,
                  key_group_range: KeyGroupRange = None, device=0, expected_entries=0, max_batch=0,
-                 sub_partitions=0):
+                 sub_partitions=0, async_input=True):
         trigger = trigger or EventTimeTrigger.create()
         if allowed_lateness < 0:
             raise ValueError("The allowed lateness cannot be negative.")
@@ -78,6 +78,8 @@ class GpuWindowOperator:
             L.fw_destroy(self._h)
             self._h = None
             raise N.NativeError(rc, msg)
+        if async_input:  # device batches are partitioned beside the previous batch's aggregation (fw_set_async_input)
+            N.check(L.fw_set_async_input(self._h, 1), self._h)
         self._inflight = None  # device columns of a push the library may still be reading
         self.epoch = 0  # watermarks processed so far
         self._rows = []
@@ -113,6 +115,20 @@ class GpuWindowOperator:
             s = self._tstream = torch.cuda.ExternalStream(self.stream, device=device)
         return s
 
+    def set_async_input(self, enable=True):
+        """fw_set_async_input: a device batch's partitioning kernels run on the library's input stream, beside
+        the previous batch's aggregation (the columns' producer is ordered before that stream by process_batch)."""
+        N.check(N.lib().fw_set_async_input(self._h, 1 if enable else 0), self._h)
+        self._istream = None
+
+    def _input_stream(self, device):
+        """The stream fw_push_batch_device reads its columns on (fw_input_stream), as a torch stream object."""
+        s = getattr(self, "_istream", None)
+        if s is None:
+            import torch
+            s = self._istream = torch.cuda.ExternalStream(N.lib().fw_input_stream(self._h), device=device)
+        return s
+
     # ------------------------------------------------------------------ processElement
     def process_batch(self, keys, timestamps, values, key_hash=None):
         """Hands a micro-batch (all records between two watermarks, or a part of them) to the GPU."""
@@ -132,9 +148,9 @@ class GpuWindowOperator:
                 raise ValueError(f"values must be {want} for a {self.aggregate.value_type!r} aggregate, got {values.dtype}")
             if key_hash is not None and key_hash.dtype != torch.int32:
                 raise ValueError("key_hash must be int32 (Java hashCode)")
-            # stream-ordered handoff: the library stream waits for the producer's writes.  The push
+            # stream-ordered handoff: the library's input stream waits for the producer's writes.  The push
             # is asynchronous; the columns are referenced until the next push has settled it.
-            self._torch_stream(keys.device).wait_stream(torch.cuda.current_stream(keys.device))
+            self._input_stream(keys.device).wait_stream(torch.cuda.current_stream(keys.device))
             rc = L.fw_push_batch_device(self._h, keys.data_ptr(), timestamps.data_ptr(), values.data_ptr(),
                                         key_hash.data_ptr() if key_hash is not None else None, n)
             self._inflight = (keys, timestamps, values, key_hash)

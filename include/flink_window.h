@@ -232,6 +232,14 @@ const char* fw_kernel_name(int kind);
 /* wait for every queued push / watermark and return the error any of them raised */
 int fw_synchronize(fw_op* op);
 void* fw_stream(fw_op* op); /* the hipStream_t the handle enqueues on */
+/* Async input (StreamInputProcessor hands the next buffer over while the operator still works on the previous
+ * one, StreamInputProcessor.java:211-223).  Enabled, fw_push_batch_device reads its columns on
+ * fw_input_stream(op) — the caller orders the columns' producer before that stream (not before fw_stream) —
+ * and the batch's partitioning kernels run there, beside the previous batch's aggregation and firing on
+ * fw_stream.  Disabled (the default), fw_input_stream(op) == fw_stream(op).  Host pushes and
+ * fw_keyby_push_device always read their columns in fw_stream order. */
+int fw_set_async_input(fw_op* op, int enable);
+void* fw_input_stream(fw_op* op);
 
 /* Keyed-state snapshot and restore, one key group at a time: the heap backend writes its state per
  * key group (flink-runtime/.../state/heap/HeapKeyedStateBackend.java:289-399, offsets per key group
