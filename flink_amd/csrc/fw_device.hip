@@ -1647,6 +1647,12 @@ __device__ __forceinline__ bool agg_flush_session(const DevCfg& c, AggLds& L, co
   __syncthreads();
   const bool timing = FW_AGG_TIMING_BUILD && (c.diag & DIAG_AGG_TIMING);
   const unsigned long long ts0 = timing ? __builtin_amdgcn_s_memtime() : 0;
+  if (c.diag & DIAG_AGG_NO_FLUSH) {
+    for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
+    if (threadIdx.x == 0) L.fill = 0;
+    __syncthreads();
+    return true;
+  }
   const int32_t need = L.live + L.fill;
   if (need > region_limit(c.log_r)) {
     if (threadIdx.x == 0) atomicMax(&st->need_live, need);

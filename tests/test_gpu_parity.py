@@ -440,16 +440,21 @@ def test_gpu_burst_suspends_and_resumes_async(cfg):
     assert_rows_equal(g, r)
 
 
+@pytest.mark.parametrize("async_input", [True, False], ids=["async-input", "sync-input"])
 @pytest.mark.parametrize("cfg", [dict(assigner="tumbling", size=1000),
-                                 dict(assigner="sliding", size=3000, slide=1000, lateness=500)],
-                         ids=["tumbling", "sliding-late"])
-def test_gpu_async_pipeline_deferred_clear(cfg):
+                                 dict(assigner="sliding", size=3000, slide=1000, lateness=500),
+                                 dict(assigner="sliding", size=3000, slide=1000),
+                                 dict(assigner="session", gap=700)],
+                         ids=["tumbling", "sliding-late", "panes", "sessions"])
+def test_gpu_async_pipeline_deferred_clear(cfg, async_input):
     # the bench's step shape: device push, watermark queued without waiting, pending rows cleared
     # without waiting (applied when the next push settles the sequence).  Rows of odd epochs are
     # cleared, rows of even epochs kept; the kept rows must be exactly the oracle's rows of those epochs.
+    # With async input each batch is partitioned on the input stream beside the previous batch's
+    # aggregation (fw_set_async_input); without it everything runs on the operator's stream.
     import torch
     batches, wms = _stream(400_000, 20_000, 50_000, bound=300, jitter=900, rate=200_000)
-    gpu = _gpu_op(**cfg, expected_entries=1000)
+    gpu = _gpu_op(**cfg, expected_entries=1000, async_input=async_input)
     ref = orc.WindowOperatorOracle(**cfg)
     kept = []
     for e, ((k, t, v), wm) in enumerate(zip(batches, wms)):
