@@ -162,6 +162,9 @@ def main():
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic summary (tools/traffic.py); default the newest profiles/traffic_*<workload>.json")
     ap.add_argument("--sub-partitions", type=int, default=0, help="state partitions per key group (0 = auto)")
+    ap.add_argument("--combine", action="store_true",
+                    help="pre-shuffle combining (SURVEY §8e): partial accumulators instead of records cross the "
+                         "exchange (C2 only: tumbling count/sum/min/max)")
     ap.add_argument("--sync-input", action="store_true",
                     help="partition each batch on the operator's own stream (no overlap with the previous batch)")
     args = ap.parse_args()
@@ -220,6 +223,16 @@ def main():
                            expected_entries=(1000 if c1 else live_windows * args.keys // world),
                            max_batch=args.batch if world == 1 else 2 * args.batch,
                            sub_partitions=args.sub_partitions, async_input=not args.sync_input)
+    cx = None
+    if args.combine:
+        if w != "c2":
+            raise SystemExit("--combine: only C2 (tumbling count/sum/min/max, Long keys) combines")
+        from flink_amd.exchange import CombiningExchange
+        # the combiner sees this rank's whole slice of the key space
+        comb = GpuWindowOperator(assigner, agg, device=local_rank, max_parallelism=max_par,
+                                 expected_entries=live_windows * args.keys, max_batch=args.batch,
+                                 sub_partitions=args.sub_partitions)
+        cx = CombiningExchange(exch, comb)
     if sliding and args.steady:
         # steady state: the warmup covers one window size of event time, so the timed steps see the
         # full pane population (size/slide + 1 panes per key) and windows merging size/slide panes
@@ -262,11 +275,14 @@ def main():
         else:
             k, t, v, h = batches[s]
             wm = local_wm[s]
-        if world > 1:
-            res = exch.exchange(k, t, v, h)
-            k, t, v, h = res if h is not None else res + (None,)
-            wm = exch.combine_watermark(wm, device=dev)
-        op.process_batch(k, t, v, h)            # queued; settles the previous step's sequence
+        if cx is not None:  # combine, exchange the partials, merge them (any world size)
+            wm = cx.push(op, k, t, v, wm)
+        else:
+            if world > 1:
+                res = exch.exchange(k, t, v, h)
+                k, t, v, h = res if h is not None else res + (None,)
+                wm = exch.combine_watermark(wm, device=dev)
+            op.process_batch(k, t, v, h)            # queued; settles the previous step's sequence
         op.advance_watermark(wm, wait=False)  # queued behind the push
         op.clear_pending()  # discarding sink: fired rows were materialised in HBM
 
@@ -402,7 +418,8 @@ def main():
                           {"window_ms": args.window}),
                        "records_per_event_second": args.rate, "watermark_bound_ms": args.bound,
                        "max_parallelism": 128, "parallelism": f"keygroup{world}",
-                       "sink": "discarding (fired rows materialised in HBM)"},
+                       "sink": "discarding (fired rows materialised in HBM)",
+                       **({"combine": "pre-shuffle partial accumulators (SURVEY §8e)"} if cx is not None else {})},
             "roofline": roofline,
             "path_roofline": {"b_alg_bytes_per_record": round(balg, 3), "frac": round(path_frac, 4),
                               "fired_rows": int(fired)},

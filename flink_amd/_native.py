@@ -46,6 +46,10 @@ class FwRows(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("key", "start", "end", "count", "sum", "min", "max")]
 
 
+class FwPartials(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("key", "start", "cnt", "sum", "min", "max")]
+
+
 class FwSideRows(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("key", "ts", "val")]
 
@@ -97,6 +101,9 @@ SIGNATURES = {
     "fw_stream": (VP, [VP]),
     "fw_set_async_input": (ctypes.c_int, [VP, ctypes.c_int]),
     "fw_input_stream": (VP, [VP]),
+    "fw_combine_extract_device": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwPartials), ctypes.c_int64, I64P,
+                                                 I64P]),
+    "fw_push_partials_device": (ctypes.c_int, [VP, ctypes.POINTER(FwPartials), ctypes.c_int64]),
     "fw_snapshot_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), ctypes.c_int64, I64P]),
     "fw_restore_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), ctypes.c_int64]),
     "fw_key_groups_device": (ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, VP, VP]),

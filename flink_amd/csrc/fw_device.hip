@@ -4063,6 +4063,160 @@ __global__ void k_restore(DevCfg c, int32_t kg, StateCols in, int64_t n, DevTabl
   atomicMin((long long*)&tb.next_timer[p], (long long)entry_timer(c, d));
 }
 
+
+// ============================================================== pre-shuffle combining
+// A combiner operator (full KeyGroupRange, watermark never advanced) aggregates a subtask's batch before the keyBy
+// exchange; its table is then drained into partial accumulators in key-group order, so each destination's share
+// is one contiguous slice (KeyGroupRangeAssignment.computeOperatorIndexForKeyGroup, :115-117), and the receiving
+// operator merges them (AggregateFunction.merge, AggregateFunction.java:160) as its own aggregate would have
+// added the records.  Decomposable count/sum/min/max on tumbling windows without allowed lateness only: a late
+// partial is dropped with all of its records (with lateness 0 a record of a late window is itself late,
+// WindowOperator.java:402-418), and no record fires on arrival.
+__global__ void k_live_u32(DevTable tb, int32_t P, uint32_t* offs) {
+  const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p <= P) offs[p] = p < P ? (uint32_t)tb.live[p] : 0u;
+}
+// one workgroup per partition: its live entries at offs[p] in slot order, then the region emptied
+__global__ __launch_bounds__(FW_FIRE_THREADS) void k_extract(DevCfg c, DevTable tb, const uint32_t* __restrict__ offs,
+                                                            PartialCols out) {
+  __shared__ uint32_t sw[FW_FIRE_THREADS / 64 + 1];
+  __shared__ uint32_t run_s;
+  const int32_t p = blockIdx.x;
+  const Region r = region_of(c, tb, p, tb.cur[p]);
+  const uint32_t R = r.mask + 1;
+  if (threadIdx.x == 0) run_s = 0;
+  __syncthreads();
+  for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x) {
+    const uint32_t s = s0 + threadIdx.x;
+    const bool live = s < R && st_kind(ld_state(r.state + s)) == SLOT_LIVE;
+    uint32_t total;
+    const uint32_t pos = block_excl_scan(live ? 1u : 0u, sw, &total);
+    if (live) {
+      const Entry e = r.ent[s];
+      const uint64_t o = (uint64_t)offs[p] + run_s + pos;
+      out.key[o] = e.key;
+      out.start[o] = e.start;
+      out.cnt[o] = e.cnt;
+      out.sum[o] = e.sum;
+      out.mn[o] = e.mn;
+      out.mx[o] = e.mx;
+    }
+    if (s < R) r.state[s] = SLOT_EMPTY;
+    __syncthreads();
+    if (threadIdx.x == 0) run_s += total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    tb.live[p] = 0;
+    tb.next_timer[p] = LMAX;
+  }
+}
+// the receiver: partials of its KeyGroupRange into partition runs (k_classify_hist counted them with the window
+// start as the timestamp); late partials are dropped and counted with their records
+__global__ __launch_bounds__(FW_TILE_THREADS) void k_pscatter(DevCfg c, int64_t wm, PartialCols in, int64_t n, int32_t T,
+                                                             const uint32_t* __restrict__ offs,
+                                                             PartialRec* __restrict__ part, Status* st) {
+  extern __shared__ uint32_t base[];
+  const int32_t tile = blockIdx.x;
+  for (int i = threadIdx.x; i < c.P; i += blockDim.x) base[i] = offs[(int64_t)i * T + tile];
+  __syncthreads();
+  const int64_t tbase = (int64_t)tile * FW_TILE, tend = min(n, tbase + (int64_t)FW_TILE);
+  unsigned long long late = 0;
+  for (int64_t i = tbase + threadIdx.x; i < tend; i += blockDim.x) {
+    const int64_t key = in.key[i], start = in.start[i];
+    const int32_t p = partition_of(c, key, key_hash_of(c.key_kind, key, nullptr, i));
+    if (p < 0) continue;  // counted by k_classify_hist
+    int64_t last = 0;
+    int nw = 0;
+    const int cls = classify(c, wm, start, &last, &nw);
+    if (cls == CLS_NORMAL) {
+      const uint32_t pos = atomicAdd(&base[p], 1u);
+      part[pos] = PartialRec{key, start, in.cnt[i], in.sum[i], in.mn[i], in.mx[i]};
+    } else if (cls == CLS_LATE) {
+      late += (unsigned long long)in.cnt[i];
+    }
+  }
+  if (late) atomicAdd(&st->late_dropped, late);
+}
+// one workgroup per partition: its partials merged in the LDS table and flushed into the region (agg_flush);
+// a flush the region cannot take suspends the launch, and the resumed one restarts from the last flush that
+// succeeded (prog.rb = its round, prog.tp = whether the thread's partial of that round was in it)
+__global__ __launch_bounds__(FW_AGG_THREADS) void k_pmerge(DevCfg c, const PartialRec* __restrict__ part,
+                                                          const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
+                                                          AggProg prog, int resume, Status* st) {
+  c.pool_bytes = 0;
+  c.agg = FW_AGG_COUNT_SUM_MIN_MAX;
+  __shared__ AggLds L;
+  const int32_t p = blockIdx.x;
+  if (p >= c.P || (resume && prog.done[p])) return;
+  const int64_t begin = offs[(int64_t)p * T], end = offs[(int64_t)(p + 1) * T];
+  if (begin == end) {
+    if (threadIdx.x == 0) prog.done[p] = 1;
+    return;
+  }
+  int64_t ck_rb = resume ? (int64_t)prog.rb[p] : begin;
+  bool ck_done = resume ? prog.tp[(int64_t)p * FW_AGG_THREADS + threadIdx.x] != 0 : false;
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.tag[h] = LT_EMPTY;
+  if (threadIdx.x == 0) {
+    L.fill = 0;
+    L.anyfail = 0;
+    L.nnew = 0;
+    L.live = tb.live[p];
+    L.flushed = 0;
+    L.min_timer = LMAX;
+  }
+  __syncthreads();
+  const Region r = region_of(c, tb, p, tb.cur[p]);
+  bool ok = true;
+  for (int64_t rb = ck_rb; rb < end && ok; rb += blockDim.x) {
+    const int64_t i = rb + threadIdx.x;
+    bool done = i >= end || (rb == ck_rb && ck_done);
+    PartialRec d{};
+    if (!done) d = part[i];
+    for (;;) {
+      if (!done) {
+        const int tg = lds_slot(L, d.key, d.start);
+        if (tg >= 0) {
+          atomicAdd(&L.cnt[tg], (uint32_t)d.cnt);
+          if (c.vtype == FW_VAL_F64)
+            atomicAdd((double*)&L.sum[tg], __longlong_as_double(d.sum));
+          else
+            atomicAdd((unsigned long long*)&L.sum[tg], (unsigned long long)d.sum);
+          atomicMin((long long*)&L.mn[tg], (long long)d.mn);
+          atomicMax((long long*)&L.mx[tg], (long long)d.mx);
+          done = true;
+        } else {
+          L.anyfail = 1;
+        }
+      }
+      __syncthreads();
+      const int need = L.anyfail;
+      __syncthreads();
+      if (!need) break;
+      if (!agg_flush(c, L, r, st)) {
+        ok = false;
+        break;
+      }
+      ck_rb = rb;
+      ck_done = done;
+      if (threadIdx.x == 0) L.anyfail = 0;
+      __syncthreads();
+    }
+  }
+  if (ok) ok = agg_flush(c, L, r, st);
+  if (!ok) {
+    prog.tp[(int64_t)p * FW_AGG_THREADS + threadIdx.x] = ck_done ? 1u : 0u;
+    if (threadIdx.x == 0) {
+      prog.rb[p] = ck_rb;
+      prog.done[p] = 0;
+      atomicOr(&st->suspended, (int)FW_SUSP_AGG);
+    }
+  } else if (threadIdx.x == 0) {
+    prog.done[p] = 1;
+  }
+  if (threadIdx.x == 0) agg_publish(c, L, tb, p, st);
+}
+
 // out3 = {live entries, event-time timers}
 __global__ __launch_bounds__(FW_FIRE_THREADS) void k_table_stats(DevCfg c, DevTable tb, unsigned long long* out3) {
   const int32_t p = blockIdx.x;
@@ -4473,6 +4627,23 @@ void launch_restore(const DevCfg& c, int32_t kg, StateCols in, int64_t n, int32_
     hipLaunchKernelGGL(k_restore, dim3(blocks), dim3(256), 0, s, c, kg, in, n, tb, st, round_of, r);
 }
 
+void launch_live_offsets(const DevCfg& c, DevTable tb, uint32_t* offs, uint32_t* scratch, hipStream_t s) {
+  hipLaunchKernelGGL(k_live_u32, dim3((unsigned)((c.P + 256) / 256)), dim3(256), 0, s, tb, c.P, offs);
+  launch_scan(offs, (int64_t)c.P + 1, scratch, s);
+}
+void launch_extract(const DevCfg& c, DevTable tb, const uint32_t* offs, PartialCols out, hipStream_t s) {
+  hipLaunchKernelGGL(k_extract, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, tb, offs, out);
+}
+void launch_pscatter(const DevCfg& c, int64_t wm, PartialCols in, int64_t n, int32_t T, uint32_t* offs, PartialRec* part,
+                     Status* st, hipStream_t s) {
+  if (T > 0)
+    hipLaunchKernelGGL(k_pscatter, dim3(T), dim3(FW_TILE_THREADS), (size_t)c.P * sizeof(uint32_t), s, c, wm, in, n, T,
+                       (const uint32_t*)offs, part, st);
+}
+void launch_pmerge(const DevCfg& c, const PartialRec* part, const uint32_t* offs, int32_t T, DevTable tb, AggProg prog,
+                   int resume, Status* st, hipStream_t s) {
+  hipLaunchKernelGGL(k_pmerge, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, part, offs, T, tb, prog, resume, st);
+}
 void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t s) {
   hipLaunchKernelGGL(k_table_stats, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, tb, out3);
 }

@@ -326,6 +326,13 @@ struct DevSide {
   int64_t *key, *ts, *val;
   int64_t cap;
 };
+// pre-shuffle combining: partial accumulators of (key, window) in the table's own representation
+struct PartialCols {
+  int64_t *key, *start, *cnt, *sum, *mn, *mx;
+};
+struct PartialRec {
+  int64_t key, start, cnt, sum, mn, mx;
+};
 
 // ---------------------------------------------------------------- launchers (fw_device.hip)
 typedef hipStream_t hipStream_t_;
@@ -375,6 +382,13 @@ size_t count_sort_bytes(int64_t n);
 void launch_rehash(const DevCfg& old_c, DevTable old_t, const DevCfg& new_c, DevTable new_t, hipStream_t_ s);
 void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t_ s);
 void launch_reset_regions(const DevCfg& c, DevTable tb, hipStream_t_ s);
+// combining: offs[P+1] = exclusive scan of the regions' live counts (scratch: launch_scan's)
+void launch_live_offsets(const DevCfg& c, DevTable tb, uint32_t* offs, uint32_t* scratch, hipStream_t_ s);
+void launch_extract(const DevCfg& c, DevTable tb, const uint32_t* offs, PartialCols out, hipStream_t_ s);
+void launch_pscatter(const DevCfg& c, int64_t wm, PartialCols in, int64_t n, int32_t T, uint32_t* offs, PartialRec* part,
+                     Status* st, hipStream_t_ s);
+void launch_pmerge(const DevCfg& c, const PartialRec* part, const uint32_t* offs, int32_t T, DevTable tb, AggProg prog,
+                   int resume, Status* st, hipStream_t_ s);
 void launch_snapshot(const DevCfg& c, DevTable tb, int32_t p0, int32_t np, StateCols out, unsigned long long* count,
                      hipStream_t_ s);
 // demand != NULL: count rows per partition (and key-group errors); NULL: insert the rows

@@ -50,6 +50,8 @@ struct Scratch {
   int64_t cbase = 0;
   int64_t ord_base = 0;          // arrival ordinal of the batch's first record (ordinal aggregates)
   int32_t* wide = nullptr;       // DevCfg::wide of the batches that use this set
+  PartialRec* pparts = nullptr;  // combining: a partials push's partials, partition-major (allocated on first use)
+  bool partials = false;         // the set's latest push merged partials (fw_push_partials_device)
   // gathered batches (fwdev::gather_mode): runs table [T8][P] and its transpose, the partitions' virtual
   // offsets (P + 1) and the ordered-path rows (2 x T8); T is then the batch's FW_GTILE tiles
   uint32_t *rt = nullptr, *rt_t = nullptr, *voffs = nullptr, *gsrow = nullptr, *gcb = nullptr;
@@ -74,6 +76,7 @@ struct fw_op {
   hipStream_t bstream = nullptr;
   hipEvent_t ev_scat[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
   bool async_in = false;
+  uint32_t *xoffs = nullptr, *xscan = nullptr;  // combining: the combiner's live-count offsets and scan scratch
   std::string err;
 
   // state table
@@ -222,6 +225,7 @@ void free_scratch(Scratch& s) {
   dfree(s.sv);
   dfree(s.skh);
   dfree(s.wide);
+  dfree(s.pparts);
   dfree(s.so);
   dfree(s.byv);
   dfree(s.rt);
@@ -470,6 +474,16 @@ int settle(fw_op* op) {
     c.cbase = S.cbase;
     c.ord_base = S.ord_base;
     c.wide = S.wide;
+    if (S.partials) {  // a partials push: only its merge can have suspended
+      timed(op, K_AGGREGATE, [&] {
+        fwdev::launch_pmerge(c, S.pparts, S.hist, S.T, op->tb, op->prog, 1, op->d_status, op->stream);
+      });
+      if (op->fire_unsettled)
+        timed(op, K_FIRE, [&] { fwdev::launch_fire(c, op->wm, op->tb, op->out, op->d_status, op->stream); });
+      HIP_OR_RETURN(op, hipGetLastError());
+      if ((rc = sync_status(op))) return rc;
+      continue;
+    }
     if (susp & FW_SUSP_AGG)
       timed(op, K_AGGREGATE, [&] {
         fwdev::launch_aggregate(c, S.wm, S.part, S.offs(), S.offT(), op->tb, op->prog, 1, S.split ? &op->hot : nullptr,
@@ -684,6 +698,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   HIP_OR_RETURN(op, hipEventRecord(op->ev_done[nxt], op->stream));  // the set's last use by this batch (see settle)
   S.T = T;
   S.n = n;
+  S.partials = false;
   S.split = split;
   S.wm = op->wm;
   S.compact = c.compact;
@@ -695,6 +710,49 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   return snapshot(op);
 }
 
+
+// ---- pre-shuffle combining (fw_combine_extract_device / fw_push_partials_device)
+bool combine_eligible(const fw_config& c) {
+  return c.assigner == FW_TUMBLING && c.aggregate == FW_AGG_COUNT_SUM_MIN_MAX && c.allowed_lateness == 0 &&
+         !c.side_output && (c.key_kind == FW_KEY_LONG || c.key_kind == FW_KEY_INT);
+}
+int push_partials(fw_op* op, const PartialCols& in, int64_t n) {
+  int rc;
+  if ((rc = settle(op)) || (rc = maybe_restart_rows(op))) return rc;
+  const int nxt = op->last_sc ^ 1;
+  Scratch& S = op->sc[nxt];
+  if (!S.pparts) HIP_OR_RETURN(op, dmalloc(&S.pparts, (size_t)op->max_batch));
+  DevCfg c = op->dc;
+  c.compact = 0;
+  c.wide = S.wide;
+  const int32_t T = (int32_t)((n + FW_TILE - 1) / FW_TILE);
+  const int64_t m = (int64_t)(c.P + 1) * T;
+  // the partials' partitions and classes, their window start standing for the timestamp
+  timed(op, K_CLASSIFY, [&] {
+    fwdev::launch_classify_hist(c, op->wm, in.key, in.start, nullptr, n, T, S.hist, op->d_status, op->stream);
+  });
+  timed(op, K_SCAN, [&] { fwdev::launch_scan(S.hist, m, S.scan_tmp, op->stream); });
+  timed(op, K_SCATTER, [&] {
+    fwdev::launch_pscatter(c, op->wm, in, n, T, S.hist, S.pparts, op->d_status, op->stream);
+  });
+  timed(op, K_AGGREGATE, [&] {
+    fwdev::launch_pmerge(c, S.pparts, S.hist, T, op->tb, op->prog, 0, op->d_status, op->stream);
+  });
+  HIP_OR_RETURN(op, hipGetLastError());
+  HIP_OR_RETURN(op, hipEventRecord(op->ev_done[nxt], op->stream));
+  S.T = T;
+  S.n = n;
+  S.partials = true;
+  S.split = false;
+  S.gather = false;
+  S.wm = op->wm;
+  S.compact = 0;
+  S.cbase = 0;
+  S.ord_base = op->records_in;
+  op->last_sc = nxt;
+  op->push_unsettled = true;
+  return snapshot(op);
+}
 }  // namespace
 
 // ============================================================================ C-ABI
@@ -1047,6 +1105,8 @@ void fw_destroy(fw_op* op) {
     dfree(*col);
   dfree(op->d_status);
   dfree(op->d_stats3);
+  dfree(op->xoffs);
+  dfree(op->xscan);
   for (auto& pr : op->prof_pending) {
     (void)hipEventDestroy(pr.a);
     (void)hipEventDestroy(pr.b);
@@ -1302,6 +1362,66 @@ int fw_profile_read(fw_op* op, double* ms, int64_t* launches, int reset) {
 }
 
 const char* fw_kernel_name(int kind) { return kind >= 0 && kind < FW_NUM_KERNELS ? KERNEL_NAMES[kind] : ""; }
+
+int fw_combine_extract_device(fw_op* op, int32_t world, const fw_partials* out, int64_t cap, int64_t* counts,
+                              int64_t* n) {
+  if (!op || !n || world < 1 || (world > 1 && !counts)) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
+  if (!combine_eligible(op->cfg))
+    return set_err(op, FW_ERR_UNSUPPORTED,
+                   "combining needs tumbling windows, the count/sum/min/max aggregate, no allowed lateness, no side "
+                   "output and Long or Integer keys");
+  if (op->wm != INT64_MIN)
+    return set_err(op, FW_ERR_STATE, "a combiner's watermark is never advanced (it would fire or drop partials)");
+  if (world > op->cfg.max_parallelism) return set_err(op, FW_ERR_ARG, "more subtasks than key groups");
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  int rc = fw_synchronize(op);
+  if (rc) return rc;
+  const DevCfg& c = op->dc;
+  if (!op->xoffs) {
+    HIP_OR_RETURN(op, dmalloc(&op->xoffs, (size_t)c.P + 1));
+    HIP_OR_RETURN(op, dmalloc(&op->xscan, (size_t)(c.P + 1) / 4096 + 2));
+  }
+  fwdev::launch_live_offsets(c, op->tb, op->xoffs, op->xscan, op->stream);
+  std::vector<uint32_t> h((size_t)c.P + 1);
+  HIP_OR_RETURN(op, hipMemcpyAsync(h.data(), op->xoffs, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, op->stream));
+  HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
+  *n = h[c.P];
+  // destination d owns computeKeyGroupRangeForOperatorIndex(maxPar, world, d); its partitions are contiguous
+  const int32_t M = op->cfg.max_parallelism, k0 = c.kg0, k1 = c.kg0 + c.n_kg;  // [k0, k1)
+  for (int32_t d = 0; counts && d < world; d++) {
+    const int32_t a = std::max((d * M + world - 1) / world, k0), b = std::min(((d + 1) * M - 1) / world + 1, k1);
+    counts[d] = a < b ? (int64_t)h[(size_t)(b - k0) << c.log_s] - (int64_t)h[(size_t)(a - k0) << c.log_s] : 0;
+  }
+  if (*n > cap) return set_err(op, FW_ERR_CAPACITY, "%lld partials do not fit the %lld-row output", (long long)*n,
+                               (long long)cap);
+  if (*n > 0 && (!out || !out->key || !out->start || !out->cnt || !out->sum || !out->min || !out->max))
+    return set_err(op, FW_ERR_ARG, "null output column");
+  if (*n > 0) {
+    fwdev::launch_extract(c, op->tb, op->xoffs, PartialCols{out->key, out->start, out->cnt, out->sum, out->min, out->max},
+                          op->stream);
+  }
+  HIP_OR_RETURN(op, hipGetLastError());
+  HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
+  return FW_OK;
+}
+
+int fw_push_partials_device(fw_op* op, const fw_partials* in, int64_t n) {
+  if (!op || !in || n < 0) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
+  if (!combine_eligible(op->cfg))
+    return set_err(op, FW_ERR_UNSUPPORTED,
+                   "combining needs tumbling windows, the count/sum/min/max aggregate, no allowed lateness, no side "
+                   "output and Long or Integer keys");
+  if (n > 0 && (!in->key || !in->start || !in->cnt || !in->sum || !in->min || !in->max))
+    return set_err(op, FW_ERR_ARG, "null column");
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  for (int64_t b = 0; b < n; b += op->max_batch) {
+    const int64_t m = std::min(op->max_batch, n - b);
+    const int rc = push_partials(op, PartialCols{in->key + b, in->start + b, in->cnt + b, in->sum + b, in->min + b,
+                                                 in->max + b}, m);
+    if (rc) return rc;
+  }
+  return FW_OK;
+}
 
 int fw_synchronize(fw_op* op) {
   if (!op) return FW_ERR_ARG;

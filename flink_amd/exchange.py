@@ -146,3 +146,48 @@ class NativeKeyByExchange:
 
     def __del__(self):
         self.close()
+
+
+class CombiningExchange:
+    """Pre-shuffle combining in front of a KeyGroupExchange: the subtask's batch is aggregated by a
+    combiner operator (a GpuWindowOperator of the same configuration over the whole key space, its watermark never
+    advanced), drained into partial accumulators in key-group order (fw_combine_extract_device), and the partials
+    -- one per (key, window) of the batch instead of one per record -- go to their subtasks, which merge them
+    (fw_push_partials_device; AggregateFunction.merge, flink-core/.../AggregateFunction.java:160).  Results equal
+    the uncombined exchange for the decomposable count/sum/min/max on tumbling windows without allowed lateness
+    (float sums within the usual tolerance); first-element, minBy/maxBy, HLL and t-digest aggregates do not
+    combine."""
+
+    def __init__(self, exchange: KeyGroupExchange, combiner):
+        self.exchange = exchange
+        self.combiner = combiner
+        self.partials_sent = 0
+
+    def push(self, op, keys, ts, vals, local_wm):
+        """Combines, exchanges and merges one batch of this subtask; returns the combined watermark."""
+        import torch
+        import torch.distributed as dist
+        ex = self.exchange
+        self.combiner.process_batch(keys, ts, vals)
+        cols, counts = self.combiner.combine_extract(ex.world)
+        if ex.world > 1:
+            staged = cols[0].is_cuda and dist.get_backend(ex.group) == "gloo"
+            move = (lambda x: x.cpu()) if staged else (lambda x: x)
+            back = (lambda x: x.to(keys.device)) if staged else (lambda x: x)
+            send = move(torch.tensor(counts, dtype=torch.int64, device=cols[0].device))
+            recv = torch.empty_like(send)
+            dist.all_to_all_single(recv, send, group=ex.group)
+            out_split = recv.tolist()
+            total = sum(out_split)
+            got = []
+            for col in cols:
+                col = move(col)
+                r = torch.empty(total, dtype=col.dtype, device=col.device)
+                dist.all_to_all_single(r, col, output_split_sizes=out_split, input_split_sizes=counts, group=ex.group)
+                got.append(back(r))
+            cols = tuple(got)
+            self.partials_sent += sum(counts) - counts[ex.rank]
+        else:  # the combiner reuses its output buffers; the operator reads the partials asynchronously
+            cols = tuple(c.clone() for c in cols)
+        op.push_partials(*cols)
+        return ex.combine_watermark(local_wm, device=keys.device)

@@ -172,6 +172,48 @@ class GpuWindowOperator:
 
     processElements = process_batch
 
+    # ------------------------------------------------------------------ pre-shuffle combining
+    def combine_extract(self, world=1):
+        """fw_combine_extract_device on this handle used as a combiner: drains its state into partial accumulators
+        (six int64 device columns key, start, cnt, sum, min, max in key-group order) and returns them with the
+        number of partials for each of `world` destination subtasks.  The columns are views of buffers the
+        handle reuses: consume them before the next call."""
+        import torch
+        L = N.lib()
+        dev = torch.device("cuda", self.device)
+        counts = (ctypes.c_int64 * world)()
+        n = ctypes.c_int64()
+        while True:
+            bufs = getattr(self, "_pbuf", None)
+            cap = bufs[0].numel() if bufs else 0
+            out = N.FwPartials(*(t.data_ptr() for t in bufs)) if bufs else N.FwPartials()
+            rc = L.fw_combine_extract_device(self._h, world, ctypes.byref(out), cap, counts, ctypes.byref(n))
+            if rc == N.FW_ERR_CAPACITY and n.value > cap:
+                cap = max(n.value, 2 * cap)
+                self._pbuf = [torch.empty(cap, dtype=torch.int64, device=dev) for _ in range(6)]
+                continue
+            N.check(rc, self._h)
+            break
+        if n.value == 0:
+            return tuple(torch.empty(0, dtype=torch.int64, device=dev) for _ in range(6)), list(counts)
+        return tuple(t[:n.value] for t in self._pbuf), list(counts)
+
+    def push_partials(self, key, start, cnt, sum_, min_, max_):
+        """fw_push_partials_device: merges partial accumulators (from combine_extract of a combiner with the same
+        configuration) of this subtask's KeyGroupRange; late ones are dropped and counted with their records."""
+        import torch
+        cols = (key, start, cnt, sum_, min_, max_)
+        n = key.numel()
+        for t in cols:
+            if not t.is_cuda or not t.is_contiguous() or t.numel() != n or t.dtype != torch.int64:
+                raise ValueError("partials must be contiguous int64 CUDA tensors of equal length")
+        if n == 0:
+            return
+        self._torch_stream(key.device).wait_stream(torch.cuda.current_stream(key.device))
+        p = N.FwPartials(*(t.data_ptr() for t in cols))
+        N.check(N.lib().fw_push_partials_device(self._h, ctypes.byref(p), n), self._h)
+        self._inflight = cols
+
     # ------------------------------------------------------------------ processWatermark
     def advance_watermark(self, wm, wait=True):
         """Fires due windows; returns the number of rows pending in HBM (not copied).  With

@@ -241,6 +241,25 @@ void* fw_stream(fw_op* op); /* the hipStream_t the handle enqueues on */
 int fw_set_async_input(fw_op* op, int enable);
 void* fw_input_stream(fw_op* op);
 
+/* Pre-shuffle combining for the keyBy exchange: partial accumulators instead of records cross the
+ * network when the aggregate is decomposable (AggregateFunction.merge, flink-core/.../AggregateFunction.java:160).
+ * Eligible: tumbling windows, FW_AGG_COUNT_SUM_MIN_MAX, allowed lateness 0, no side output, Long or Integer keys.
+ * A combiner is an ordinary handle over the subtask's whole input (any KeyGroupRange covering it; its watermark is
+ * never advanced) into which the subtask pushes its batch; fw_combine_extract_device then drains the combiner's
+ * state into the partials (device columns, the accumulators in the handle's own representation: only
+ * fw_push_partials_device of a handle with the same configuration reads them) in key-group order, so destination
+ * d of `world` subtasks (KeyGroupRangeAssignment.computeOperatorIndexForKeyGroup, :115-117) owns the contiguous
+ * slice counts[d]; it empties the combiner.  When the partials exceed cap, *n is set, nothing is drained and
+ * FW_ERR_CAPACITY is returned.  fw_push_partials_device is processElement for the partials of the receiving
+ * subtask's KeyGroupRange: a partial whose window is late is dropped and its count added to the late records
+ * (WindowOperator.java:402-418; with allowed lateness 0 every record of a late window is late). */
+typedef struct {
+  int64_t *key, *start, *cnt, *sum, *min, *max;
+} fw_partials;
+int fw_combine_extract_device(fw_op* combiner, int32_t world, const fw_partials* out, int64_t cap, int64_t* counts,
+                              int64_t* n);
+int fw_push_partials_device(fw_op* op, const fw_partials* in, int64_t n);
+
 /* Keyed-state snapshot and restore, one key group at a time: the heap backend writes its state per
  * key group (flink-runtime/.../state/heap/HeapKeyedStateBackend.java:289-399, offsets per key group
  * :370-381) and the timers likewise (api/operators/InternalTimeServiceManager.java:114), which is

@@ -1,0 +1,164 @@
+"""Pre-shuffle combining on the GPU: a combiner GpuWindowOperator aggregates each batch, is drained
+into partial accumulators in key-group order (fw_combine_extract_device), and the receiving operator merges them
+(fw_push_partials_device).  Rows must equal the oracle fed with the records themselves — bit-exact for keys,
+windows, counts and integer sum/min/max, f64 sums within 1e-6 — and late partials count all of their records
+(WindowOperator.java:402-418 with allowed lateness 0).
+
+* world size 1: combiner -> partials -> operator on one GPU, including a table far too small (the merge suspends
+  and resumes after growth) and keys outside the receiver's KeyGroupRange rejected;
+* world size 2 over gloo, both subtasks on cuda:0: CombiningExchange (combine, per-destination slices through
+  all_to_all_single, merge), the union of both subtasks' rows against one oracle operator.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from flink_amd import KeyGroupRange, TumblingEventTimeWindows
+from flink_amd.datagen import generate_host
+from flink_amd.windowing import CountSumMinMax
+from oracle import oracle as orc
+from tests.parity_util import assert_rows_equal
+
+pytestmark = pytest.mark.gpu
+
+_VT = {"i64": "long", "i32": "int", "f64": "double"}
+
+
+def _stream(n, batch, keys, bound, jitter, rate, value_type="i64"):
+    k, t, v = generate_host(0x5EED, 0, n, keys, ts_base=1_000_000, rate=rate, jitter=jitter)
+    if value_type == "f64":
+        v = (v & 0xFFFFF).astype(np.float64) / 7.0
+    out, mx = [], -(1 << 63)
+    for b in range(0, n, batch):
+        sl = slice(b, min(n, b + batch))
+        mx = max(mx, int(t[sl].max()))
+        out.append((k[sl], t[sl], v[sl], mx - bound))
+    return out
+
+
+def _ops(value_type, expected, kgr=None):
+    from flink_amd.operator import GpuWindowOperator
+    agg = CountSumMinMax(_VT[value_type])
+    comb = GpuWindowOperator(TumblingEventTimeWindows.of(1000), agg, device=0, expected_entries=expected)
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(1000), agg, device=0, expected_entries=expected,
+                           key_group_range=kgr)
+    return comb, op
+
+
+@pytest.mark.parametrize("value_type,keys,n,batch,expected", [
+    ("i64", 2000, 600_000, 40_000, 0), ("i32", 2000, 600_000, 40_000, 0), ("f64", 2000, 600_000, 40_000, 0),
+    ("i64", 1 << 20, 2 << 20, 1 << 20, 1000)], ids=["long", "int", "double", "table-grows"])
+def test_gpu_combine_world1_vs_oracle(value_type, keys, n, batch, expected):
+    import torch
+    # out-of-order records (jitter 900 ms against a 300 ms bound): late windows arrive as late partials
+    batches = _stream(n, batch, keys, bound=300, jitter=900, rate=200_000, value_type=value_type)
+    comb, op = _ops(value_type, expected)
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000, value_type=value_type)
+    rows = []
+    sent = 0
+    for k, t, v, wm in batches:
+        cols = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (k, t, v)]
+        comb.process_batch(*cols)
+        parts, counts = comb.combine_extract(1)
+        assert counts == [parts[0].numel()]
+        sent += parts[0].numel()
+        op.push_partials(*(c.clone() for c in parts))
+        ref.process(k, t, v)
+        rows.append(op.process_watermark(wm))
+        ref.watermark(wm)
+    rows.append(op.process_watermark((1 << 63) - 1))
+    ref.watermark((1 << 63) - 1)
+    assert_rows_equal(np.concatenate(rows), ref.rows(), _VT[value_type])
+    assert op.late_dropped == ref.late_dropped
+    if expected:
+        assert op.stats()["table_grows"] >= 1
+    else:
+        assert ref.late_dropped > 0
+        assert sent < n // 4  # one partial per (key, window) of a batch instead of one per record
+    comb.close()
+    op.close()
+
+
+def test_gpu_combine_rejects_foreign_key_groups_and_ineligible_configs():
+    import torch
+    from flink_amd import _native as N
+    from flink_amd import SlidingEventTimeWindows
+    from flink_amd.operator import GpuWindowOperator
+    comb, op = _ops("i64", 0, kgr=KeyGroupRange(0, 63))
+    k = torch.arange(1000, dtype=torch.int64, device="cuda")
+    comb.process_batch(k, k + 1_000_000, k)
+    parts, _ = comb.combine_extract(1)
+    op.push_partials(*(c.clone() for c in parts))
+    with pytest.raises(N.NativeError):  # keys of key groups 64..127 reach a subtask owning 0..63
+        op.process_watermark(0)
+    bad = GpuWindowOperator(SlidingEventTimeWindows.of(3000, 1000), device=0)
+    with pytest.raises(N.NativeError):
+        bad.combine_extract(1)
+    for o in (comb, op, bad):
+        o.close()
+
+
+MAX_PAR, WORLD, BATCH, STEPS, KEYS = 128, 2, 40_000, 5, 3000
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _slice(rank, step):
+    first = (step * WORLD + rank) * BATCH
+    return generate_host(0x5EED, first, BATCH, KEYS, ts_base=0, rate=100_000, jitter=300)
+
+
+def _worker(rank, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    from flink_amd.exchange import CombiningExchange, KeyGroupExchange
+    from flink_amd.operator import GpuWindowOperator
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    ex = KeyGroupExchange(MAX_PAR, WORLD, rank)
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(1000), max_parallelism=MAX_PAR,
+                           key_group_range=ex.key_group_range, device=0)
+    comb = GpuWindowOperator(TumblingEventTimeWindows.of(1000), max_parallelism=MAX_PAR, device=0)
+    cx = CombiningExchange(ex, comb)
+    mx = -(1 << 63)
+    dev = torch.device("cuda", 0)
+    for s in range(STEPS):
+        k, t, v = _slice(rank, s)
+        mx = max(mx, int(t.max()))
+        cols = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (k, t, v)]
+        wm = cx.push(op, *cols, mx - 300)
+        op.watermark(wm)
+    op.watermark((1 << 63) - 1)
+    np.save(os.path.join(out_dir, f"rows_{rank}.npy"), op.rows())
+    np.save(os.path.join(out_dir, f"sent_{rank}.npy"), np.array([cx.partials_sent, op.late_dropped]))
+    comb.close()
+    op.close()
+    dist.destroy_process_group()
+
+
+def test_gpu_combining_exchange_world2():
+    import tempfile
+
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(_free_port(), d), nprocs=WORLD, join=True)
+        rows = np.concatenate([np.load(os.path.join(d, f"rows_{r}.npy")) for r in range(WORLD)])
+        sent = [np.load(os.path.join(d, f"sent_{r}.npy")) for r in range(WORLD)]
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000)
+    mx = [-(1 << 63)] * WORLD
+    for s in range(STEPS):
+        sl = [_slice(r, s) for r in range(WORLD)]
+        for r in range(WORLD):
+            ref.process(*sl[r])
+            mx[r] = max(mx[r], int(sl[r][1].max()))
+        ref.watermark(min(mx) - 300)
+    ref.watermark((1 << 63) - 1)
+    assert_rows_equal(rows, ref.rows())
+    assert sum(int(x[1]) for x in sent) == ref.late_dropped
+    assert 0 < sum(int(x[0]) for x in sent) < WORLD * STEPS * BATCH // 4
