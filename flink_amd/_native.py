@@ -104,6 +104,7 @@ SIGNATURES = {
     "fw_combine_extract_device": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwPartials), ctypes.c_int64, I64P,
                                                  I64P]),
     "fw_push_partials_device": (ctypes.c_int, [VP, ctypes.POINTER(FwPartials), ctypes.c_int64]),
+    "fw_keyby_combine_push_device": (ctypes.c_int, [VP, VP, VP, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, I64P]),
     "fw_snapshot_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), ctypes.c_int64, I64P]),
     "fw_restore_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), ctypes.c_int64]),
     "fw_key_groups_device": (ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, VP, VP]),

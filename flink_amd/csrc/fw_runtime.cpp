@@ -1620,6 +1620,9 @@ struct fw_comm {
   int64_t scratch_bytes = 0;
   int64_t* counts = nullptr;                              // [2 world + 2]: send counts, recv counts, wm in/out
   int64_t* h_counts = nullptr;                            // pinned host copy
+  int64_t pcap = 0;                                       // combining: partials the send / receive columns hold
+  int64_t* ps[6] = {};                                    // send partials (key, start, cnt, sum, min, max)
+  int64_t* pr[6] = {};                                    // received partials
 };
 namespace {
 template <class T>
@@ -1685,6 +1688,10 @@ void fw_comm_destroy(fw_comm* c) {
   if (c->nc) (void)ncclCommDestroy(c->nc);
   for (int64_t** p : {&c->rk, &c->rt, &c->rv, &c->sk, &c->st, &c->sv, &c->counts}) cfree(*p);
   for (int32_t** p : {&c->rh, &c->sh}) cfree(*p);
+  for (int i = 0; i < 6; i++) {
+    cfree(c->ps[i]);
+    cfree(c->pr[i]);
+  }
   cfree(c->scratch);
   if (c->h_counts) (void)hipHostFree(c->h_counts);
   delete c;
@@ -1769,6 +1776,93 @@ int fw_keyby_push_device(fw_comm* c, fw_op* op, const int64_t* key, const int64_
   // processElement for the received batch (stream-ordered behind the receives)
   // (the columns were received on the handle's stream, so the push reads them in its order)
   return push_device_batches(op, c->rk, c->rt, c->rv, hashed ? c->rh : nullptr, total, false);
+}
+
+int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64_t* key, const int64_t* ts,
+                                 const void* val, int64_t n, int64_t local_wm, int64_t* combined_wm) {
+  if (!c || !comb || !op || n < 0 || (n > 0 && (!key || !ts || !val)))
+    return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
+  const int W = c->world;
+  {
+    const int32_t M = op->cfg.max_parallelism, r = c->rank;
+    if (op->cfg.key_group_start != (r * M + W - 1) / W || op->cfg.key_group_end != ((r + 1) * M - 1) / W)
+      return set_err(op, FW_ERR_ARG, "the operator's KeyGroupRange is not subtask %d of %d's", r, W);
+  }
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  int rc;
+  // the batch into the combiner, ordered after the columns' producer (the caller's fw_stream(op) order)
+  hipEvent_t ready = nullptr;
+  HIP_OR_RETURN(op, hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+  HIP_OR_RETURN(op, hipEventRecord(ready, op->stream));
+  HIP_OR_RETURN(op, hipStreamWaitEvent(comb->stream, ready, 0));
+  (void)hipEventDestroy(ready);
+  if ((rc = push_device_batches(comb, key, ts, val, nullptr, n, false))) return set_err(op, rc, "%s", comb->err.c_str());
+  // drain it: the partials in key-group order, per-peer counts
+  std::vector<int64_t> counts(W);
+  int64_t np = 0;
+  fw_partials out{c->ps[0], c->ps[1], c->ps[2], c->ps[3], c->ps[4], c->ps[5]};
+  rc = fw_combine_extract_device(comb, W, &out, c->pcap, counts.data(), &np);
+  if (rc == FW_ERR_CAPACITY && np > c->pcap) {
+    const int64_t cap = std::max<int64_t>(np, 2 * c->pcap);
+    for (int i = 0; i < 6; i++) {
+      cfree(c->ps[i]);
+      cfree(c->pr[i]);
+      HIP_OR_RETURN(op, dmalloc(&c->ps[i], (size_t)cap));
+      HIP_OR_RETURN(op, dmalloc(&c->pr[i], (size_t)cap));
+    }
+    c->pcap = cap;
+    out = fw_partials{c->ps[0], c->ps[1], c->ps[2], c->ps[3], c->ps[4], c->ps[5]};
+    rc = fw_combine_extract_device(comb, W, &out, c->pcap, counts.data(), &np);
+  }
+  if (rc) return set_err(op, rc, "%s", comb->err.c_str());
+  hipStream_t s = op->stream;
+  for (int p = 0; p < W; p++) c->h_counts[p] = counts[p];
+  c->h_counts[2 * W] = local_wm;
+  HIP_OR_RETURN(op, hipMemcpyAsync(c->counts, c->h_counts, W * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  HIP_OR_RETURN(op, hipMemcpyAsync(c->counts + 2 * W, c->h_counts + 2 * W, sizeof(int64_t), hipMemcpyHostToDevice, s));
+  NCCL_OR_RETURN(op, ncclGroupStart());
+  NCCL_OR_RETURN(op, ncclAllToAll(c->counts, c->counts + W, 1, ncclInt64, c->nc, s));
+  NCCL_OR_RETURN(op, ncclAllReduce(c->counts + 2 * W, c->counts + 2 * W + 1, 1, ncclInt64, ncclMin, c->nc, s));
+  NCCL_OR_RETURN(op, ncclGroupEnd());
+  HIP_OR_RETURN(op, hipMemcpyAsync(c->h_counts, c->counts, (2 * W + 2) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HIP_OR_RETURN(op, hipStreamSynchronize(s));
+  std::vector<int64_t> soff(W + 1, 0), roff(W + 1, 0);
+  for (int p = 0; p < W; p++) {
+    soff[p + 1] = soff[p] + c->h_counts[p];
+    roff[p + 1] = roff[p] + c->h_counts[W + p];
+  }
+  const int64_t total = roff[W];
+  if (total > c->pcap) {  // more partials arrive than this subtask drained: grow the receive columns
+    const int64_t cap = std::max<int64_t>(total, 2 * c->pcap);
+    for (int i = 0; i < 6; i++) {
+      cfree(c->pr[i]);
+      HIP_OR_RETURN(op, dmalloc(&c->pr[i], (size_t)cap));
+    }
+    // (the send columns keep their size; pcap bounds both only after both grew)
+    int64_t* ns[6] = {};
+    for (int i = 0; i < 6; i++) {
+      HIP_OR_RETURN(op, dmalloc(&ns[i], (size_t)cap));
+      if (np) HIP_OR_RETURN(op, hipMemcpyAsync(ns[i], c->ps[i], np * 8, hipMemcpyDeviceToDevice, s));
+    }
+    HIP_OR_RETURN(op, hipStreamSynchronize(s));
+    for (int i = 0; i < 6; i++) {
+      cfree(c->ps[i]);
+      c->ps[i] = ns[i];
+    }
+    c->pcap = cap;
+  }
+  NCCL_OR_RETURN(op, ncclGroupStart());
+  for (int p = 0; p < W; p++) {
+    const size_t sc = (size_t)c->h_counts[p], rcn = (size_t)c->h_counts[W + p];
+    for (int i = 0; i < 6; i++) {
+      NCCL_OR_RETURN(op, ncclSend(c->ps[i] + soff[p], sc, ncclInt64, p, c->nc, s));
+      NCCL_OR_RETURN(op, ncclRecv(c->pr[i] + roff[p], rcn, ncclInt64, p, c->nc, s));
+    }
+  }
+  NCCL_OR_RETURN(op, ncclGroupEnd());
+  if (combined_wm) *combined_wm = c->h_counts[2 * W + 1];
+  const fw_partials in{c->pr[0], c->pr[1], c->pr[2], c->pr[3], c->pr[4], c->pr[5]};
+  return fw_push_partials_device(op, &in, total);
 }
 
 int fw_generate_device(uint64_t seed, int64_t first, int64_t n, int64_t num_keys, const double* zipf_cdf,

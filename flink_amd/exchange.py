@@ -139,6 +139,18 @@ class NativeKeyByExchange:
         self.op._inflight = (keys, ts, vals, key_hash)
         return wm.value
 
+    def push_combined(self, combiner, keys, ts, vals, local_wm):
+        """fw_keyby_combine_push_device: the batch aggregated by `combiner` (a GpuWindowOperator of the same
+        configuration over the whole key space), its partials exchanged and merged into the operator."""
+        import torch
+        wm = ctypes.c_int64()
+        self.op._torch_stream(keys.device).wait_stream(torch.cuda.current_stream(keys.device))
+        rc = N.lib().fw_keyby_combine_push_device(self._c, combiner._h, self.op._h, keys.data_ptr(), ts.data_ptr(),
+                                                  vals.data_ptr(), keys.numel(), int(local_wm), ctypes.byref(wm))
+        N.check(rc, self.op._h)
+        self.op._inflight = (keys, ts, vals)
+        return wm.value
+
     def close(self):
         if self._c:
             N.lib().fw_comm_destroy(self._c)

@@ -326,6 +326,12 @@ int fw_comm_init(const void* id128, int32_t world, int32_t rank, int32_t device,
 void fw_comm_destroy(fw_comm* comm);
 int fw_keyby_push_device(fw_comm* comm, fw_op* op, const int64_t* key, const int64_t* ts, const void* val,
                          const int32_t* key_hash, int64_t n, int64_t local_wm, int64_t* combined_wm);
+/* The same with pre-shuffle combining (see fw_combine_extract_device): the batch goes into `combiner` (this
+ * subtask's combiner handle, same configuration, never given a watermark), which is drained into partials; the
+ * partials' per-peer counts and six columns cross the exchange instead of the records, and the received ones are
+ * merged into `op` (fw_push_partials_device).  Eligible configurations only. */
+int fw_keyby_combine_push_device(fw_comm* comm, fw_op* combiner, fw_op* op, const int64_t* key, const int64_t* ts,
+                                 const void* val, int64_t n, int64_t local_wm, int64_t* combined_wm);
 
 /* ---- f2: Flink's wire format for one input channel <-> device columns.
  * The byte stream of a channel is its network buffers in order: SpanningRecordSerializer.addRecord writes each

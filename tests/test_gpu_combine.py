@@ -6,6 +6,7 @@ windows, counts and integer sum/min/max, f64 sums within 1e-6 — and late parti
 
 * world size 1: combiner -> partials -> operator on one GPU, including a table far too small (the merge suspends
   and resumes after growth) and keys outside the receiver's KeyGroupRange rejected;
+* fw_keyby_combine_push_device (the C-ABI exchange over the library's RCCL communicator) at world size 1;
 * world size 2 over gloo, both subtasks on cuda:0: CombiningExchange (combine, per-destination slices through
   all_to_all_single, merge), the union of both subtasks' rows against one oracle operator.
 """
@@ -162,3 +163,32 @@ def test_gpu_combining_exchange_world2():
     assert_rows_equal(rows, ref.rows())
     assert sum(int(x[1]) for x in sent) == ref.late_dropped
     assert 0 < sum(int(x[0]) for x in sent) < WORLD * STEPS * BATCH // 4
+
+
+def test_gpu_native_keyby_combine_world1():
+    # the C-ABI combining exchange over the library's own RCCL communicator, one subtask: combiner push, drain,
+    # counts, self send/recv of the partials, merge
+    import torch
+    from flink_amd.exchange import NativeKeyByExchange
+    from flink_amd.operator import GpuWindowOperator
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(1000), max_parallelism=MAX_PAR, device=0)
+    comb = GpuWindowOperator(TumblingEventTimeWindows.of(1000), max_parallelism=MAX_PAR, device=0)
+    ex = NativeKeyByExchange(op, 1, 0, NativeKeyByExchange.new_unique_id())
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000)
+    mx = -(1 << 63)
+    dev = torch.device("cuda", 0)
+    for s in range(2 * STEPS):
+        k, t, v = _slice(0, s)
+        mx = max(mx, int(t.max()))
+        wm = ex.push_combined(comb, *(torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (k, t, v)), mx - 300)
+        assert wm == mx - 300
+        op.watermark(wm)
+        ref.process(k, t, v)
+        ref.watermark(mx - 300)
+    op.watermark((1 << 63) - 1)
+    ref.watermark((1 << 63) - 1)
+    assert_rows_equal(op.rows(), ref.rows())
+    assert op.late_dropped == ref.late_dropped
+    ex.close()
+    comb.close()
+    op.close()
