@@ -21,7 +21,9 @@
 #ifndef FW_TILE
 #define FW_TILE 32768          // records per classify/scatter workgroup
 #endif
-#define FW_TILE_THREADS 1024
+#ifndef FW_TILE_THREADS
+#define FW_TILE_THREADS 1024   // classify / scatter workgroup
+#endif
 #ifndef FW_RPT
 #define FW_RPT 8               // records per thread kept in flight by the streaming kernels (even: pairs)
 #endif
