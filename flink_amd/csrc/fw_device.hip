@@ -3584,7 +3584,12 @@ __device__ __forceinline__ FireDecision fire_decide(const DevCfg& c, int64_t wm,
   return d;
 }
 
-__global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, DevTable tb, DevRows out, Status* st) {
+// POOL: instantiated for the accumulator-block aggregates (HLL, t-digest: their rows are finished here from the
+// blocks) apart from the plain ones, whose scan keeps FIRE_U slots per thread in flight
+template <bool POOL>
+__global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c, int64_t wm, DevTable tb, DevRows out,
+                                                                       Status* st) {
+  if constexpr (!POOL) c.pool_bytes = 0;
   const int32_t p = blockIdx.x;
   // a suspended push has not finished updating the state: the host resumes it and fires again
   if (tb.next_timer[p] > wm || __hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
@@ -3604,28 +3609,44 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, 
   int live = 0;
   uint32_t nfire = 0;
   int64_t nt = LMAX;
-  for (uint32_t s = threadIdx.x; s < R; s += blockDim.x) {
-    if (st_kind(ld_state(rx.state + s)) != SLOT_LIVE) continue;
-    Entry e = rx.ent[s], fe;
-    const FireDecision d = fire_decide(c, wm, e, fe);
-    nfire += d.fire;
-    if (!d.keep && !d.fire && c.pool_bytes) {  // GC without a row: free its block here (HLL: zeroed)
-      const uint64_t blk = pool_block_of(e);
-      if (c.agg == FW_AGG_HLL) {
-        hll_clear(c, blk);
-        __threadfence();
-      }
-      c.pool_free[atomicAdd(&c.pool_ctr[0], 1)] = (uint32_t)blk;
+  // FIRE_U slots per thread per step: their state words, then their live entries, are loaded before any is used
+  // (one slot at a time left the scan waiting on each load in turn)
+  constexpr int FIRE_U = POOL ? 1 : 4;  // (the pool rows' one-wave-per-row finish wants the occupancy more)
+  for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x * FIRE_U) {
+    uint32_t w[FIRE_U];
+#pragma unroll
+    for (int u = 0; u < FIRE_U; u++) {
+      const uint32_t s = s0 + u * blockDim.x + threadIdx.x;
+      w[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
     }
-    if (!d.keep) continue;
-    const uint64_t h = slot_hash(c, e.key, e.start);
-    const int32_t dst = region_claim(ry, h, live_word(h));
-    if (dst >= 0) {
-      ry.ent[dst] = e;
-      live++;
-      nt = min(nt, timer_of(e, c.lateness));
-    } else {
-      atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // cannot happen: the survivors fit the region they came from
+    Entry eu[FIRE_U];
+#pragma unroll
+    for (int u = 0; u < FIRE_U; u++)
+      if (st_kind(w[u]) == SLOT_LIVE) eu[u] = rx.ent[s0 + u * blockDim.x + threadIdx.x];
+#pragma unroll
+    for (int u = 0; u < FIRE_U; u++) {
+      if (st_kind(w[u]) != SLOT_LIVE) continue;
+      Entry e = eu[u], fe;
+      const FireDecision d = fire_decide(c, wm, e, fe);
+      nfire += d.fire;
+      if (!d.keep && !d.fire && c.pool_bytes) {  // GC without a row: free its block here (HLL: zeroed)
+        const uint64_t blk = pool_block_of(e);
+        if (c.agg == FW_AGG_HLL) {
+          hll_clear(c, blk);
+          __threadfence();
+        }
+        c.pool_free[atomicAdd(&c.pool_ctr[0], 1)] = (uint32_t)blk;
+      }
+      if (!d.keep) continue;
+      const uint64_t h = slot_hash(c, e.key, e.start);
+      const int32_t dst = region_claim(ry, h, live_word(h));
+      if (dst >= 0) {
+        ry.ent[dst] = e;
+        live++;
+        nt = min(nt, timer_of(e, c.lateness));
+      } else {
+        atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // cannot happen: the survivors fit the region they came from
+      }
     }
   }
   uint32_t total;
@@ -3636,18 +3657,31 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_fire(DevCfg c, int64_t wm, 
   __syncthreads();
   if (nfire) {
     unsigned long long pos = base_s + pos0;
-    for (uint32_t s = threadIdx.x; s < R; s += blockDim.x) {
-      if (st_kind(ld_state(rx.state + s)) != SLOT_LIVE) continue;
-      Entry e = rx.ent[s], fe;
-      if (!fire_decide(c, wm, e, fe).fire) continue;
-      if ((int64_t)pos < out.cap) {
-        write_row(c, out, pos, fe);
-        if (c.agg == FW_AGG_HLL) out.mn[pos] = (int64_t)pool_block_of(fe);  // read back by hll_finish
-        if (c.agg == FW_AGG_TDIGEST) out.sum[pos] = (int64_t)pool_block_of(fe);  // read back by td_finish
-      } else {
-        atomicOr(&st->flags, FW_STATUS_OUT_FULL);
+    for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x * FIRE_U) {
+      uint32_t w[FIRE_U];
+#pragma unroll
+      for (int u = 0; u < FIRE_U; u++) {
+        const uint32_t s = s0 + u * blockDim.x + threadIdx.x;
+        w[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
       }
-      pos++;
+      Entry eu[FIRE_U];
+#pragma unroll
+      for (int u = 0; u < FIRE_U; u++)
+        if (st_kind(w[u]) == SLOT_LIVE) eu[u] = rx.ent[s0 + u * blockDim.x + threadIdx.x];
+#pragma unroll
+      for (int u = 0; u < FIRE_U; u++) {
+        if (st_kind(w[u]) != SLOT_LIVE) continue;
+        Entry e = eu[u], fe;
+        if (!fire_decide(c, wm, e, fe).fire) continue;
+        if ((int64_t)pos < out.cap) {
+          write_row(c, out, pos, fe);
+          if (c.agg == FW_AGG_HLL) out.mn[pos] = (int64_t)pool_block_of(fe);  // read back by hll_finish
+          if (c.agg == FW_AGG_TDIGEST) out.sum[pos] = (int64_t)pool_block_of(fe);  // read back by td_finish
+        } else {
+          atomicOr(&st->flags, FW_STATUS_OUT_FULL);
+        }
+        pos++;
+      }
     }
   }
   if (c.pool_bytes && total) {
@@ -4541,7 +4575,10 @@ void launch_fire(const DevCfg& c0, int64_t wm, DevTable tb, DevRows out, Status*
     hipLaunchKernelGGL(k_fire_panes, dim3(c.P), dim3(PF_THREADS), 0, s, c, wm, tb, out, st);
     return;
   }
-  hipLaunchKernelGGL(k_fire, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, wm, tb, out, st);
+  if (c.pool_bytes)
+    hipLaunchKernelGGL(k_fire<true>, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, wm, tb, out, st);
+  else
+    hipLaunchKernelGGL(k_fire<false>, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, wm, tb, out, st);
 }
 
 size_t count_sort_bytes(int64_t n) {
