@@ -475,6 +475,29 @@ def test_gpu_async_pipeline_deferred_clear(cfg, async_input):
     gpu.close()
 
 
+def test_gpu_async_input_toggled_mid_stream():
+    # fw_set_async_input switched off and on between device pushes (bench.py's isolated pass does this): the switch
+    # synchronizes, and the rows equal the oracle's whatever stream each batch was partitioned on
+    import torch
+    cfg = dict(assigner="tumbling", size=1000)
+    batches, wms = _stream(600_000, 25_000, 40_000, bound=300, jitter=900, rate=200_000)
+    gpu = _gpu_op(**cfg, expected_entries=1000)
+    ref = orc.WindowOperatorOracle(**cfg)
+    rows = []
+    for e, ((k, t, v), wm) in enumerate(zip(batches, wms)):
+        if e % 5 == 2:
+            gpu.set_async_input(e % 2 == 0)
+        if len(k):
+            gpu.process_batch(*(torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (k, t, v)))
+        ref.process(k, t, v)
+        gpu.advance_watermark(wm, wait=False)
+        ref.watermark(wm)
+        rows.append(gpu.drain_rows(e))
+    assert_rows_equal(np.concatenate(rows), ref.rows())
+    assert gpu.stats()["late_records_dropped"] == ref.late_dropped
+    gpu.close()
+
+
 def test_gpu_late_burst_suspends_ordered_path():
     # a burst of late records for new keys, all within the allowed lateness: each one creates a
     # window on the ordered path and fires it at once, so k_slow runs out of region room and of
