@@ -47,7 +47,7 @@ class FwRows(ctypes.Structure):
 
 
 class FwPartials(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("key", "start", "cnt", "sum", "min", "max")]
+    _fields_ = [(n, ctypes.c_void_p) for n in ("key", "start", "cnt", "sum", "min", "max")] + [("config", ctypes.c_uint64)]
 
 
 class FwSideRows(ctypes.Structure):

@@ -3993,6 +3993,7 @@ __global__ void k_reset_regions(DevCfg c, DevTable tb) {
   tb.fire_e[p] = LMIN;
   tb.fire_lo[p] = 0;
   tb.pane_floor[p] = LMIN;
+  tb.passes[p] = 0;
 }
 
 // ---- keyed-state snapshot of one key group (HeapKeyedStateBackend.snapshot writes per key group,
@@ -4004,11 +4005,12 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_snapshot(DevCfg c, DevTable
   __shared__ unsigned long long base_s;
   const int32_t p = p0 + blockIdx.x;
   const Region r = region_of(c, tb, p, tb.cur[p]);
-  const uint32_t R = r.mask + 1;
+  // (dense regions: the live prefix, no state words)
+  const uint32_t R = c.dense ? (uint32_t)tb.live[p] : r.mask + 1;
   // one pass per block of the region: count, reserve, write
   for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x) {
     const uint32_t s = s0 + threadIdx.x;
-    bool live = s < R && st_kind(ld_state(r.state + s)) == SLOT_LIVE;
+    bool live = s < R && (c.dense || st_kind(ld_state(r.state + s)) == SLOT_LIVE);
     if (live && c.panes && max(r.ent[s].meta, tb.pane_floor[p]) > jsub(jadd(r.ent[s].start, c.size), 1))
       live = false;  // a pane whose windows have all been formed (GC'd at the next watermark)
     uint32_t total;
@@ -4117,12 +4119,12 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_extract(DevCfg c, DevTable 
   __shared__ uint32_t run_s;
   const int32_t p = blockIdx.x;
   const Region r = region_of(c, tb, p, tb.cur[p]);
-  const uint32_t R = r.mask + 1;
+  const uint32_t R = c.dense ? (uint32_t)tb.live[p] : r.mask + 1;  // (dense regions: the live prefix)
   if (threadIdx.x == 0) run_s = 0;
   __syncthreads();
   for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x) {
     const uint32_t s = s0 + threadIdx.x;
-    const bool live = s < R && st_kind(ld_state(r.state + s)) == SLOT_LIVE;
+    const bool live = s < R && (c.dense || st_kind(ld_state(r.state + s)) == SLOT_LIVE);
     uint32_t total;
     const uint32_t pos = block_excl_scan(live ? 1u : 0u, sw, &total);
     if (live) {
@@ -4135,7 +4137,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_extract(DevCfg c, DevTable 
       out.mn[o] = e.mn;
       out.mx[o] = e.mx;
     }
-    if (s < R) r.state[s] = SLOT_EMPTY;
+    if (s < R && !c.dense) r.state[s] = SLOT_EMPTY;
     __syncthreads();
     if (threadIdx.x == 0) run_s += total;
     __syncthreads();
@@ -4155,11 +4157,12 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_pscatter(DevCfg c, int64_t 
   for (int i = threadIdx.x; i < c.P; i += blockDim.x) base[i] = offs[(int64_t)i * T + tile];
   __syncthreads();
   const int64_t tbase = (int64_t)tile * FW_TILE, tend = min(n, tbase + (int64_t)FW_TILE);
-  unsigned long long late = 0;
+  unsigned long long late = 0, recs = 0;
   for (int64_t i = tbase + threadIdx.x; i < tend; i += blockDim.x) {
     const int64_t key = in.key[i], start = in.start[i];
     const int32_t p = partition_of(c, key, key_hash_of(c.key_kind, key, nullptr, i));
     if (p < 0) continue;  // counted by k_classify_hist
+    recs += (unsigned long long)in.cnt[i];
     int64_t last = 0;
     int nw = 0;
     const int cls = classify(c, wm, start, &last, &nw);
@@ -4171,6 +4174,7 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_pscatter(DevCfg c, int64_t 
     }
   }
   if (late) atomicAdd(&st->late_dropped, late);
+  if (recs) atomicAdd(&st->partial_records, recs);
 }
 // one workgroup per partition: its partials merged in the LDS table and flushed into the region (agg_flush);
 // a flush the region cannot take suspends the launch, and the resumed one restarts from the last flush that
@@ -4256,8 +4260,9 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_table_stats(DevCfg c, DevTa
   const int32_t p = blockIdx.x;
   const Region r = region_of(c, tb, p, tb.cur[p]);
   unsigned long long live = 0, timers = 0;
-  for (uint32_t s = threadIdx.x; s <= r.mask; s += blockDim.x) {
-    if (st_kind(ld_state(r.state + s)) != SLOT_LIVE) continue;
+  const uint32_t lim = c.dense ? (uint32_t)tb.live[p] : r.mask + 1;  // (dense regions: the live prefix)
+  for (uint32_t s = threadIdx.x; s < lim; s += blockDim.x) {
+    if (!c.dense && st_kind(ld_state(r.state + s)) != SLOT_LIVE) continue;
     const Entry& e = r.ent[s];
     if (c.panes) {  // one pending timer per pane (its next window end); formed-out panes are garbage
       if (max(e.meta, tb.pane_floor[p]) > jsub(jadd(e.start, c.size), 1)) continue;
@@ -4272,6 +4277,472 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_table_stats(DevCfg c, DevTa
   }
   if (live) atomicAdd(&out3[0], live);
   if (timers) atomicAdd(&out3[1], timers);
+}
+
+// ============================================================== dense tumbling regions (DevCfg::dense)
+// Tumbling windows with the count/sum/min/max accumulator and allowed lateness 0 (BASELINE configs[1]; the state
+// op replaced is HeapAggregatingState.add over CopyOnWriteStateTable.transform, CopyOnWriteStateTable.java:449-495).
+// Every record of a batch lands in a window that ends after the watermark, and a window is removed when it fires, so
+// a region's live entries are few and nearly all of them are touched by every batch.  A region therefore keeps its
+// entries densely in slots [0, live) of its current buffer (no state words, no probing in HBM):
+//   k_dt_aggregate  loads the region's entries into an LDS hash table, adds the batch's records (or merges partial
+//                   accumulators: combining, restore), and writes every group densely into the region's other buffer
+//                   (whole 64-byte entries, coalesced); a region is committed (buffer flipped) only when all of its
+//                   groups are written, so a suspended launch resumes by redoing the regions not yet committed;
+//   k_dt_fire       streams the due regions' entries: windows with maxTimestamp <= wm are emitted
+//                   (WindowOperator.onEventTime, :424-469), the rest are copied into the other buffer.
+// A region whose entries and new groups exceed the LDS table is done in 2^b passes, each over the (key, window)s
+// whose hash has prefix k: every pass reads the region and the records again and keeps its share.
+enum { DT_RECS = 0, DT_PARTS = 1 };
+constexpr int DT_LIMIT = FW_DT_SLOTS * 13 / 16;  // claims stop here, so every probe chain ends at an EMPTY slot
+constexpr int DT_BUCKETS = FW_DT_SLOTS / 4;
+static_assert(FW_DT_SLOTS % 4 == 0, "FW_DT_SLOTS: buckets of 4");
+struct DtLds {
+  uint32_t tag[FW_DT_SLOTS];  // LT_EMPTY, LT_BUSY or a fingerprint >= 2 of (key, window start)
+  i64x2 kv[FW_DT_SLOTS];      // {key, window start}
+  unsigned long long cnt[FW_DT_SLOTS];
+  int64_t sum[FW_DT_SLOTS], mn[FW_DT_SLOTS], mx[FW_DT_SLOTS];
+  int fill, over, nout, capover;
+  long long ntmin;
+};
+__device__ __forceinline__ uint32_t dt_bucket(uint32_t h) { return (uint32_t)(((uint64_t)h * DT_BUCKETS) >> 32); }
+// the hash pass of (key, window): prefix of a hash independent of the LDS slot's
+__device__ __forceinline__ int dt_pass(const DevCfg& c, int64_t key, int64_t start, int hb) {
+  return hb ? (int)((uint32_t)(slot_hash(c, key, start) >> 32) >> (32 - hb)) : 0;
+}
+// find or claim the slot of (key, start); -1 at the fill limit (the protocol of lds_slot)
+__device__ __forceinline__ int dt_slot(DtLds& L, int64_t key, int64_t start, uint32_t h) {
+  const uint32_t fp = lds_fp(h);
+  uint32_t b = dt_bucket(h);
+  for (int guard = 0; guard < 4 * DT_BUCKETS;) {
+    asm volatile("" ::: "memory");
+    const u32x4 t4 = *reinterpret_cast<const u32x4*>(&L.tag[b * 4]);
+    int found = -1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t tq = q == 0 ? t4.x : q == 1 ? t4.y : q == 2 ? t4.z : t4.w;
+      if (found < 0 && tq == fp) {
+        asm volatile("" ::: "memory");
+        const i64x2 kq = L.kv[b * 4 + q];
+        if (kq.x == key && kq.y == start) found = (int)b * 4 + q;
+      }
+    }
+    if (found >= 0) return found;
+    const int empty = t4.x == LT_EMPTY ? 0 : t4.y == LT_EMPTY ? 1 : t4.z == LT_EMPTY ? 2 : t4.w == LT_EMPTY ? 3 : -1;
+    const bool busy = t4.x == LT_BUSY || t4.y == LT_BUSY || t4.z == LT_BUSY || t4.w == LT_BUSY;
+    if (busy) {  // a slot of this bucket is being published: re-read it
+      guard++;
+      continue;
+    }
+    if (empty >= 0) {
+      if (__hip_atomic_load(&L.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= DT_LIMIT) return -1;
+      if (atomicAdd(&L.fill, 1) >= DT_LIMIT) {
+        atomicSub(&L.fill, 1);
+        return -1;
+      }
+      const int s = (int)b * 4 + empty;
+      if (atomicCAS(&L.tag[s], LT_EMPTY, LT_BUSY) == LT_EMPTY) {
+        L.kv[s] = i64x2{key, start};
+        L.cnt[s] = 0;
+        L.sum[s] = 0;
+        L.mn[s] = LMAX;
+        L.mx[s] = LMIN;
+        __hip_atomic_store(&L.tag[s], fp, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return s;
+      }
+      atomicSub(&L.fill, 1);
+      continue;  // lost the claim race: re-read the bucket
+    }
+    b = b + 1 == (uint32_t)DT_BUCKETS ? 0u : b + 1;  // bucket full without a match
+    guard++;
+  }
+  return -1;
+}
+// AggregateFunction.add of one element (the value in the table's representation: f64 min/max sortable)
+__device__ __forceinline__ void dt_add(DtLds& L, int s, int vtype, int64_t v) {
+  atomicAdd(&L.cnt[s], 1ull);
+  int64_t sv = v;
+  if (vtype == FW_VAL_F64) {
+    atomicAdd((double*)&L.sum[s], __longlong_as_double(v));
+    sv = f64_sortable(v);
+  } else {
+    atomicAdd((unsigned long long*)&L.sum[s], (unsigned long long)v);
+  }
+  atomicMin((long long*)&L.mn[s], (long long)sv);
+  atomicMax((long long*)&L.mx[s], (long long)sv);
+}
+// AggregateFunction.merge of an accumulator in the table's representation
+__device__ __forceinline__ void dt_merge(DtLds& L, int s, int vtype, int64_t cnt, int64_t sum, int64_t mn, int64_t mx) {
+  atomicAdd(&L.cnt[s], (unsigned long long)cnt);
+  if (vtype == FW_VAL_F64)
+    atomicAdd((double*)&L.sum[s], __longlong_as_double(sum));
+  else
+    atomicAdd((unsigned long long*)&L.sum[s], (unsigned long long)sum);
+  atomicMin((long long*)&L.mn[s], (long long)mn);
+  atomicMax((long long*)&L.mx[s], (long long)mx);
+}
+// RPT elements: home buckets and candidates looked up together, the rest one by one (lds_upsert_batch's shape);
+// dm: bit j = element j done or absent.  false when the table is full.
+template <int RPT>
+__device__ __forceinline__ bool dt_add_batch(DtLds& L, int vtype, const int64_t (&k)[RPT], const int64_t (&s)[RPT],
+                                             const int64_t (&v)[RPT], uint32_t dm) {
+  uint32_t hh[RPT], b[RPT], fp[RPT];
+  u32x4 t4[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; j++) {
+    hh[j] = lds_hash(k[j], s[j]);
+    fp[j] = lds_fp(hh[j]);
+    b[j] = dt_bucket(hh[j]);
+    if (!(dm >> j & 1)) t4[j] = *reinterpret_cast<const u32x4*>(&L.tag[b[j] * 4]);
+  }
+  int cand[RPT];
+  i64x2 kv[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; j++) {
+    cand[j] = -1;
+    if (dm >> j & 1) continue;
+    const u32x4 t = t4[j];
+    cand[j] = t.x == fp[j] ? 0 : t.y == fp[j] ? 1 : t.z == fp[j] ? 2 : t.w == fp[j] ? 3 : -1;
+    if (cand[j] >= 0) kv[j] = L.kv[b[j] * 4 + cand[j]];
+  }
+#pragma unroll
+  for (int j = 0; j < RPT; j++) {
+    if (cand[j] < 0 || kv[j].x != k[j] || kv[j].y != s[j]) continue;
+    dt_add(L, (int)b[j] * 4 + cand[j], vtype, v[j]);
+    dm |= 1u << j;
+  }
+#pragma unroll
+  for (int j = 0; j < RPT; j++) {
+    if (dm >> j & 1) continue;
+    const int t = dt_slot(L, k[j], s[j], hh[j]);
+    if (t < 0) return false;
+    dt_add(L, t, vtype, v[j]);
+  }
+  return true;
+}
+
+// One workgroup per region.  SRC = DT_RECS: the batch's records (CRec / PRec runs of k_scatter); DT_PARTS: partial
+// accumulators (PartialRec runs of k_pscatter or of a restore).
+template <int SRC>
+__global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const void* __restrict__ in,
+                                                                const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
+                                                                AggProg prog, int resume, Status* st) {
+  __shared__ DtLds L;
+  __shared__ long long out_s;
+  const int32_t p = blockIdx.x;
+  if (p >= c.P || (resume && prog.done[p])) return;
+  const int64_t begin = offs[(int64_t)p * T], end = offs[(int64_t)(p + 1) * T];
+  if (begin == end) {  // nothing for this region: it stays as it is
+    if (threadIdx.x == 0) prog.done[p] = 1;
+    return;
+  }
+  const int X = tb.cur[p], Y = X ^ 1;
+  const int64_t base = (int64_t)p << c.log_r, R = (int64_t)1 << c.log_r;
+  const Entry* __restrict__ src = tb.ent[X] + base;
+  Entry* __restrict__ dst = tb.ent[Y] + base;
+  const int32_t live = tb.live[p];
+  const bool cmp = SRC == DT_RECS && c.compact && !*c.wide;
+  const PRec* __restrict__ part = reinterpret_cast<const PRec*>(in);
+  const PartialRec* __restrict__ pin = reinterpret_cast<const PartialRec*>(in);
+  const int lane = __lane_id();
+  int hb = tb.passes[p];
+  bool lost = false;
+  for (;;) {  // an attempt with 2^hb passes
+    if (threadIdx.x == 0) {
+      out_s = 0;
+      L.ntmin = LMAX;
+      L.capover = 0;
+    }
+    bool overflow = false;
+    for (int k = 0; k < (1 << hb) && !overflow; k++) {
+      for (int h = threadIdx.x; h < FW_DT_SLOTS; h += FW_DT_THREADS) L.tag[h] = LT_EMPTY;
+      if (threadIdx.x == 0) {
+        L.fill = 0;
+        L.over = 0;
+        L.nout = 0;
+      }
+      __syncthreads();
+      // the region's entries of pass k (two per thread in flight)
+      for (int32_t i0 = 0; i0 < live; i0 += 2 * FW_DT_THREADS) {
+        Entry e[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+          const int32_t i = i0 + u * FW_DT_THREADS + (int32_t)threadIdx.x;
+          if (i < live) e[u] = src[i];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+          const int32_t i = i0 + u * FW_DT_THREADS + (int32_t)threadIdx.x;
+          if (i >= live || (hb && dt_pass(c, e[u].key, e[u].start, hb) != k)) continue;
+          const int s = dt_slot(L, e[u].key, e[u].start, lds_hash(e[u].key, e[u].start));
+          if (s < 0) {
+            L.over = 1;
+            break;
+          }
+          dt_merge(L, s, c.vtype, e[u].cnt, e[u].sum, e[u].mn, e[u].mx);
+        }
+      }
+      __syncthreads();
+      if (!L.over) {
+        if constexpr (SRC == DT_RECS) {
+          // the batch's records, the next round's in flight while the current ones are added
+          constexpr int RPT = FW_DT_RPT;
+          constexpr int64_t RS = (int64_t)FW_DT_THREADS * RPT;
+          i64x2 ca[RPT], cb[RPT];
+#pragma unroll
+          for (int j = 0; j < RPT; j++) {
+            const int64_t i = begin + (int64_t)j * FW_DT_THREADS + threadIdx.x;
+            load_prec_raw(cmp, part, i, i < end, ca[j], cb[j]);
+          }
+          for (int64_t rb = begin; rb < end; rb += RS) {
+            if (__hip_atomic_load(&L.over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+            i64x2 na[RPT], nb[RPT];
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+              const int64_t i = rb + RS + (int64_t)j * FW_DT_THREADS + threadIdx.x;
+              load_prec_raw(cmp, part, i, i < end, na[j], nb[j]);
+            }
+            int64_t kk[RPT], tt[RPT], vv[RPT];
+            uint32_t dm = 0;
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+              int64_t o;
+              int nw;
+              unpack_prec<false>(c, cmp, p, ca[j], cb[j], kk[j], tt[j], vv[j], nw, o);
+              const int64_t i = rb + (int64_t)j * FW_DT_THREADS + threadIdx.x;
+              if (i >= end || (hb && dt_pass(c, kk[j], tt[j], hb) != k)) dm |= 1u << j;
+            }
+            if (!dt_add_batch<RPT>(L, c.vtype, kk, tt, vv, dm)) {
+              L.over = 1;
+              break;
+            }
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+              ca[j] = na[j];
+              cb[j] = nb[j];
+            }
+          }
+        } else {
+          for (int64_t i0 = begin; i0 < end; i0 += 2 * FW_DT_THREADS) {
+            if (__hip_atomic_load(&L.over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+            PartialRec d[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+              const int64_t i = i0 + u * FW_DT_THREADS + threadIdx.x;
+              if (i < end) d[u] = pin[i];
+            }
+            bool full = false;
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+              const int64_t i = i0 + u * FW_DT_THREADS + threadIdx.x;
+              if (full || i >= end || (hb && dt_pass(c, d[u].key, d[u].start, hb) != k)) continue;
+              const int s = dt_slot(L, d[u].key, d[u].start, lds_hash(d[u].key, d[u].start));
+              if (s < 0) {
+                full = true;
+                continue;
+              }
+              dt_merge(L, s, c.vtype, d[u].cnt, d[u].sum, d[u].mn, d[u].mx);
+            }
+            if (full) {
+              L.over = 1;
+              break;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      if (L.over) {
+        overflow = true;
+        break;
+      }
+      // the pass's groups, densely behind the earlier passes' (a wave reserves its lanes' positions at once)
+      const long long ob = out_s;
+      long long nt = LMAX;
+      for (int h0 = 0; h0 < FW_DT_SLOTS; h0 += FW_DT_THREADS) {
+        const int h = h0 + (int)threadIdx.x;
+        const bool g = h < FW_DT_SLOTS && L.tag[h] >= 2;
+        const uint64_t m = __ballot(g);
+        int wb = 0;
+        if (lane == 0 && m) wb = atomicAdd(&L.nout, __popcll(m));
+        wb = __shfl(wb, 0, 64);
+        if (g) {
+          const int64_t pos = ob + wb + __popcll(m & lanemask_lt());
+          const i64x2 kv = L.kv[h];
+          Entry e;
+          e.key = kv.x;
+          e.start = kv.y;
+          e.end = jadd(kv.y, c.size);
+          e.cnt = (int64_t)L.cnt[h];
+          e.sum = L.sum[h];
+          e.mn = L.mn[h];
+          e.mx = L.mx[h];
+          e.meta = FW_TIMER;  // EventTimeTrigger's timer at maxTimestamp (= the GC timer with lateness 0)
+          if (pos < R)
+            dst[pos] = e;
+          else
+            L.capover = 1;
+          nt = min(nt, (long long)jsub(e.end, 1));
+        }
+      }
+      if (nt != LMAX) atomicMin(&L.ntmin, nt);
+      __syncthreads();
+      if (threadIdx.x == 0) out_s += L.nout;
+      __syncthreads();
+    }
+    if (!overflow) break;
+    if (++hb > 24) {  // more groups with one hash prefix than 2^24 passes can split: cannot happen
+      lost = true;
+      break;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    tb.passes[p] = (uint8_t)min(hb, 24);
+    if (lost) {
+      atomicOr(&st->flags, FW_STATUS_STATE_LOST);
+      prog.done[p] = 1;
+    } else if (L.capover) {  // the region's buffers are too small: nothing committed, the host grows them and resumes
+      atomicMax(&st->need_live, (int)min(out_s, (long long)INT32_MAX));
+      prog.done[p] = 0;
+      atomicOr(&st->suspended, (int)FW_SUSP_AGG);
+    } else {
+      tb.cur[p] = (uint8_t)Y;
+      tb.live[p] = (int32_t)out_s;
+      tb.next_timer[p] = L.ntmin;
+      prog.done[p] = 1;
+      atomicAdd(&st->merged, (unsigned long long)out_s);
+      if (out_s > (3 * R) / 4) st->need_grow = 1;
+    }
+  }
+}
+
+// per watermark: the due regions' windows with maxTimestamp <= wm fire (FIRE / FIRE_AND_PURGE and the GC timer
+// coincide with lateness 0); the other entries are copied densely into the region's other buffer
+constexpr int DT_FIRE_U = 4;
+__global__ __launch_bounds__(FW_FIRE_THREADS) void k_dt_fire(DevCfg c, int64_t wm, DevTable tb, DevRows out, Status* st) {
+  const int32_t p = blockIdx.x;
+  // a suspended push has not finished updating the state: the host resumes it and fires again
+  if (tb.next_timer[p] > wm || __hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  __shared__ int surv_s;
+  __shared__ long long nt_s;
+  __shared__ unsigned long long fired_s;
+  if (threadIdx.x == 0) {
+    surv_s = 0;
+    nt_s = LMAX;
+    fired_s = 0;
+  }
+  __syncthreads();
+  const int X = tb.cur[p], Y = X ^ 1;
+  const int64_t base = (int64_t)p << c.log_r;
+  const Entry* __restrict__ src = tb.ent[X] + base;
+  Entry* __restrict__ dst = tb.ent[Y] + base;
+  const int32_t live = tb.live[p];
+  const int lane = __lane_id();
+  long long nt = LMAX;
+  unsigned long long fired = 0;
+  for (int32_t i0 = 0; i0 < live; i0 += FW_FIRE_THREADS * DT_FIRE_U) {
+    Entry e[DT_FIRE_U];
+#pragma unroll
+    for (int u = 0; u < DT_FIRE_U; u++) {
+      const int32_t i = i0 + u * FW_FIRE_THREADS + (int32_t)threadIdx.x;
+      if (i < live) e[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < DT_FIRE_U; u++) {
+      const int32_t i = i0 + u * FW_FIRE_THREADS + (int32_t)threadIdx.x;
+      const bool valid = i < live;
+      const bool due = valid && jsub(e[u].end, 1) <= wm;
+      const bool row = due && e[u].cnt > 0;  // contents != null (WindowOperator.java:452-459)
+      const bool keep = valid && !due;
+      const uint64_t rm = __ballot(row), km = __ballot(keep);
+      unsigned long long rb = 0;
+      int sb = 0;
+      if (lane == 0) {
+        if (rm) rb = atomicAdd(&st->out_rows, (unsigned long long)__popcll(rm));
+        if (km) sb = atomicAdd(&surv_s, __popcll(km));
+      }
+      rb = __shfl(rb, 0, 64);
+      sb = __shfl(sb, 0, 64);
+      if (row) {
+        const unsigned long long pos = rb + __popcll(rm & lanemask_lt());
+        if ((int64_t)pos < out.cap)
+          write_row(c, out, pos, e[u]);
+        else
+          atomicOr(&st->flags, FW_STATUS_OUT_FULL);
+      }
+      if (keep) {
+        dst[sb + __popcll(km & lanemask_lt())] = e[u];
+        nt = min(nt, (long long)jsub(e[u].end, 1));
+      }
+      if (lane == 0) fired += __popcll(rm);
+    }
+  }
+  if (nt != LMAX) atomicMin(&nt_s, nt);
+  if (fired) atomicAdd(&fired_s, fired);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (fired_s) atomicAdd(&st->fired_total, fired_s);
+    tb.cur[p] = (uint8_t)Y;
+    tb.live[p] = surv_s;
+    tb.next_timer[p] = nt_s;
+  }
+}
+
+// table growth of dense regions: the live prefix of each region into buffer 0 of the larger table
+__global__ __launch_bounds__(FW_FIRE_THREADS) void k_dt_rehash(DevCfg oc, DevTable ot, DevCfg nc, DevTable nt) {
+  const int32_t p = blockIdx.x;
+  const Entry* src = ot.ent[ot.cur[p]] + ((int64_t)p << oc.log_r);
+  Entry* dst = nt.ent[0] + ((int64_t)p << nc.log_r);
+  const int32_t live = ot.live[p];
+  for (int32_t i = threadIdx.x; i < live; i += blockDim.x) dst[i] = src[i];
+  if (threadIdx.x == 0) {
+    nt.cur[p] = 0;
+    nt.live[p] = live;
+    nt.next_timer[p] = ot.next_timer[p];
+  }
+}
+
+// restore into dense regions: every row of key group kg as a partial accumulator in the table's representation
+// (k_restore's conversion), its partition in rp (-1 and a key-group error when a Long / Integer key is not in kg)
+__global__ void k_dt_rows_prep(DevCfg c, int32_t kg, StateCols in, int64_t n, int32_t* rp, PartialRec* tmp, Status* st) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t p = restore_partition(c, kg, in.key[i]);
+  rp[i] = p;
+  if (p < 0) {
+    atomicAdd(&st->kg_errors, 1);
+    return;
+  }
+  PartialRec d;
+  d.key = in.key[i];
+  d.start = in.start[i];
+  d.cnt = in.cnt[i];
+  d.sum = in.sum[i];
+  d.mn = c.vtype == FW_VAL_F64 ? f64_sortable(in.mn[i]) : in.mn[i];
+  d.mx = c.vtype == FW_VAL_F64 ? f64_sortable(in.mx[i]) : in.mx[i];
+  tmp[i] = d;
+}
+__global__ __launch_bounds__(FW_TILE_THREADS) void k_dt_rows_hist(int32_t P, const int32_t* __restrict__ rp, int64_t n,
+                                                                  int32_t T, uint32_t* __restrict__ hist) {
+  extern __shared__ uint32_t lh[];
+  for (int i = threadIdx.x; i <= P; i += blockDim.x) lh[i] = 0;
+  __syncthreads();
+  const int64_t b = (int64_t)blockIdx.x * FW_TILE, e = min(n, b + (int64_t)FW_TILE);
+  for (int64_t i = b + threadIdx.x; i < e; i += blockDim.x)
+    if (rp[i] >= 0) atomicAdd(&lh[rp[i]], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i <= P; i += blockDim.x) hist[(int64_t)i * T + blockIdx.x] = i < P ? lh[i] : 0u;
+}
+__global__ __launch_bounds__(FW_TILE_THREADS) void k_dt_rows_scatter(int32_t P, const int32_t* __restrict__ rp,
+                                                                     const PartialRec* __restrict__ tmp, int64_t n, int32_t T,
+                                                                     const uint32_t* __restrict__ offs,
+                                                                     PartialRec* __restrict__ part) {
+  extern __shared__ uint32_t base[];
+  for (int i = threadIdx.x; i < P; i += blockDim.x) base[i] = offs[(int64_t)i * T + blockIdx.x];
+  __syncthreads();
+  const int64_t b = (int64_t)blockIdx.x * FW_TILE, e = min(n, b + (int64_t)FW_TILE);
+  for (int64_t i = b + threadIdx.x; i < e; i += blockDim.x)
+    if (rp[i] >= 0) part[atomicAdd(&base[rp[i]], 1u)] = tmp[i];
 }
 
 // ---- keyBy routing: key groups and stable grouping by destination operator index
@@ -4445,8 +4916,9 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
       hipLaunchKernelGGL(k_scatter<M_GEN>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, val, kh, n, T, o, part,
                          side, st);
   }
-  hipLaunchKernelGGL(k_scatter_ordered<false>, dim3(T), dim3(FW_TILE_THREADS), 0, s, c, wm, key, ts, val, kh, n, T,
-                     (const uint32_t*)(offs + (int64_t)c.P * T), sk, stt, sv, skh, (const Status*)st);
+  if (!c.dense)  // (dense configurations never have a record that needs arrival order)
+    hipLaunchKernelGGL(k_scatter_ordered<false>, dim3(T), dim3(FW_TILE_THREADS), 0, s, c, wm, key, ts, val, kh, n, T,
+                       (const uint32_t*)(offs + (int64_t)c.P * T), sk, stt, sv, skh, (const Status*)st);
 }
 
 // panes: maxTimestamp of the earliest window ending after wm (windows [s, s + size), s = offset mod slide)
@@ -4473,6 +4945,11 @@ void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint
       hipLaunchKernelGGL(k_chunk_plan, dim3((c.P + 1 + 255) / 256), dim3(256), 0, s, c, offs, T, h);
       launch_scan(h.chunk_base, (int64_t)c.P + 1, h.scan_tmp, s);
     }
+  }
+  if (c.dense) {
+    hipLaunchKernelGGL(k_dt_aggregate<DT_RECS>, dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs, T, tb,
+                       prog, resume, st);
+    return;
   }
   const dim3 b(FW_AGG_THREADS);
   if (rt_t) {  // gathered: count/sum/min/max of compact records (gather_mode)
@@ -4575,6 +5052,10 @@ void launch_fire(const DevCfg& c0, int64_t wm, DevTable tb, DevRows out, Status*
     hipLaunchKernelGGL(k_fire_panes, dim3(c.P), dim3(PF_THREADS), 0, s, c, wm, tb, out, st);
     return;
   }
+  if (c.dense) {
+    hipLaunchKernelGGL(k_dt_fire, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, wm, tb, out, st);
+    return;
+  }
   if (c.pool_bytes)
     hipLaunchKernelGGL(k_fire<true>, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, wm, tb, out, st);
   else
@@ -4642,7 +5123,10 @@ void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int
   hipLaunchKernelGGL(k_td_large_compact, dim3(64), dim3(64), 0, s, c, td, st);
 }
 void launch_rehash(const DevCfg& oc, DevTable ot, const DevCfg& nc, DevTable nt, hipStream_t s) {
-  hipLaunchKernelGGL(k_rehash, dim3(oc.P), dim3(FW_FIRE_THREADS), 0, s, oc, ot, nc, nt);
+  if (oc.dense)
+    hipLaunchKernelGGL(k_dt_rehash, dim3(oc.P), dim3(FW_FIRE_THREADS), 0, s, oc, ot, nc, nt);
+  else
+    hipLaunchKernelGGL(k_rehash, dim3(oc.P), dim3(FW_FIRE_THREADS), 0, s, oc, ot, nc, nt);
 }
 
 
@@ -4679,7 +5163,22 @@ void launch_pscatter(const DevCfg& c, int64_t wm, PartialCols in, int64_t n, int
 }
 void launch_pmerge(const DevCfg& c, const PartialRec* part, const uint32_t* offs, int32_t T, DevTable tb, AggProg prog,
                    int resume, Status* st, hipStream_t s) {
-  hipLaunchKernelGGL(k_pmerge, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, part, offs, T, tb, prog, resume, st);
+  if (c.dense)
+    hipLaunchKernelGGL(k_dt_aggregate<DT_PARTS>, dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs, T, tb,
+                       prog, resume, st);
+  else
+    hipLaunchKernelGGL(k_pmerge, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, part, offs, T, tb, prog, resume, st);
+}
+void launch_dt_restore_runs(const DevCfg& c, int32_t kg, StateCols in, int64_t n, int32_t* rp, uint32_t* hist,
+                            uint32_t* scan_tmp, PartialRec* tmp, PartialRec* part, Status* st, hipStream_t s) {
+  if (n <= 0) return;
+  const int32_t T = ntiles(n);
+  hipLaunchKernelGGL(k_dt_rows_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c, kg, in, n, rp, tmp, st);
+  hipLaunchKernelGGL(k_dt_rows_hist, dim3(T), dim3(FW_TILE_THREADS), (size_t)(c.P + 1) * sizeof(uint32_t), s, c.P,
+                     (const int32_t*)rp, n, T, hist);
+  launch_scan(hist, (int64_t)(c.P + 1) * T, scan_tmp, s);
+  hipLaunchKernelGGL(k_dt_rows_scatter, dim3(T), dim3(FW_TILE_THREADS), (size_t)c.P * sizeof(uint32_t), s, c.P,
+                     (const int32_t*)rp, (const PartialRec*)tmp, n, T, (const uint32_t*)hist, part);
 }
 void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t s) {
   hipLaunchKernelGGL(k_table_stats, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, tb, out3);

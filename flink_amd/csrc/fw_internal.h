@@ -62,6 +62,17 @@
 #define FW_TD_T3 16384         // ... at most this many in one wave; more over the whole grid (the hottest keys)
 #endif
 #define FW_SLOW_THREADS 1024
+// Dense tumbling regions (DevCfg::dense): the LDS table of k_dt_aggregate (slots, threads, records per thread in
+// flight).  Regions are sized for about FW_DT_SLOTS * 3/4 live entries each.
+#ifndef FW_DT_SLOTS
+#define FW_DT_SLOTS 2688
+#endif
+#ifndef FW_DT_THREADS
+#define FW_DT_THREADS 1024
+#endif
+#ifndef FW_DT_RPT
+#define FW_DT_RPT 2
+#endif
 // Tile-local ("gathered") partitioning of compact count/sum/min/max batches: k_stage sorts each tile of
 // FW_GTILE records by partition in LDS and writes it back linearly (a wave's stores are whole lines; scattered
 // 16-byte stores into partition-major runs measured 2.4x slower), and k_aggregate gathers a partition's runs
@@ -141,6 +152,10 @@ struct DevCfg {
   // the batch's "some record has no compact form" flag (set by k_classify_hist, read by the kernels that read
   // its partitioned records); one word per scratch set, so the next batch's classify may run beside them
   int32_t* wide;
+  // dense regions (tumbling windows, count/sum/min/max, allowed lateness 0): a region's live entries sit in slots
+  // [0, live) of its current buffer, without state words; k_dt_aggregate rewrites a region into its other buffer
+  // from an LDS table, k_dt_fire streams it (fw_device.hip, "dense tumbling regions")
+  int32_t dense;
 };
 
 // host: reciprocal of d >= 1 for div_inv(): m = floor(2^64 (2^l - d) / d) + 1, l = ceil(log2 d)
@@ -201,6 +216,7 @@ struct Status {
   unsigned long long slow_total;
   unsigned long long merged;          // LDS deltas merged into HBM regions (k_aggregate)
   unsigned long long td_cent;         // FW_AGG_TDIGEST: centroids of the fired digests
+  unsigned long long partial_records; // records inside the partials pushed (fw_push_partials_device): numRecordsIn
   long long slow_resume;              // ordered path: first list index not yet replayed
   long long need_out;                 // fired-row capacity the ordered path asked for when it suspended
   int32_t need_live;                  // largest live count a region asked for when it suspended
@@ -252,6 +268,7 @@ struct DevTable {
   int64_t* fire_e;     // panes: window maxTimestamp a suspended k_fire resumes at, LMIN = from the start
   uint64_t* fire_lo;   // panes: first key hash of that window not yet emitted
   int64_t* pane_floor; // panes: every window of the region with maxTimestamp < pane_floor has been formed
+  uint8_t* passes;     // dense regions: log2 of the hash passes the region's last aggregate needed (a hint)
 };
 
 struct DevRows {
@@ -391,6 +408,11 @@ void launch_pscatter(const DevCfg& c, int64_t wm, PartialCols in, int64_t n, int
                      Status* st, hipStream_t_ s);
 void launch_pmerge(const DevCfg& c, const PartialRec* part, const uint32_t* offs, int32_t T, DevTable tb, AggProg prog,
                    int resume, Status* st, hipStream_t_ s);
+// dense regions: restored rows of key group kg as partials in partition-major runs (prep: partition and internal
+// representation of every row, key-group errors counted; then hist, scan and scatter into `part` at offsets
+// `hist` ((P + 1) x T, scanned in place)), merged by launch_pmerge
+void launch_dt_restore_runs(const DevCfg& c, int32_t kg, StateCols in, int64_t n, int32_t* rp, uint32_t* hist,
+                            uint32_t* scan_tmp, PartialRec* tmp, PartialRec* part, Status* st, hipStream_t_ s);
 void launch_snapshot(const DevCfg& c, DevTable tb, int32_t p0, int32_t np, StateCols out, unsigned long long* count,
                      hipStream_t_ s);
 // demand != NULL: count rows per partition (and key-group errors); NULL: insert the rows

@@ -189,6 +189,7 @@ int alloc_table(fw_op* op, DevTable& t, const DevCfg& c, bool with_meta) {
     HIP_OR_RETURN(op, dmalloc(&t.fire_e, (size_t)c.P));
     HIP_OR_RETURN(op, dmalloc(&t.fire_lo, (size_t)c.P));
     HIP_OR_RETURN(op, dmalloc(&t.pane_floor, (size_t)c.P));
+    HIP_OR_RETURN(op, dmalloc(&t.passes, (size_t)c.P));
   }
   return FW_OK;
 }
@@ -400,6 +401,7 @@ int grow_table(fw_op* op, int new_log_r) {
   nt.fire_e = op->tb.fire_e;
   nt.fire_lo = op->tb.fire_lo;
   nt.pane_floor = op->tb.pane_floor;
+  nt.passes = op->tb.passes;
   int rc = alloc_table(op, nt, nc, false);
   if (rc) {
     free_table(nt);
@@ -498,7 +500,7 @@ int settle(fw_op* op) {
         fwdev::launch_tdigest(c, S.part, S.offs(), S.offT(), S.n, op->tb, op->td, op->d_status, op->stream);
       });
     // after an aggregate suspension the ordered path never started; otherwise it resumes
-    timed(op, K_SLOW, [&] {
+    if (!c.dense) timed(op, K_SLOW, [&] {
       fwdev::launch_slow(c, S.wm, S.srow(op->dc.P), S.T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status,
                          (susp & FW_SUSP_AGG) ? 0 : 1, op->stream);
     });
@@ -678,7 +680,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   cc.cbase = c.cbase;
   cc.wide = S.wide;
   // a partition can outgrow one aggregate workgroup (hot keys) only when the batch is longer than a chunk
-  const bool split = (cc.wpr == 1 || cc.panes) && n > FW_AGG_CHUNK;
+  const bool split = !cc.dense && (cc.wpr == 1 || cc.panes) && n > FW_AGG_CHUNK;
   if (split && (rc = ensure_hot(op))) return rc;
   timed(op, K_AGGREGATE, [&] {
     fwdev::launch_aggregate(cc, op->wm, S.part, S.offs(), S.offT(), op->tb, op->prog, 0, split ? &op->hot : nullptr, n,
@@ -690,10 +692,11 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
     timed(op, K_TDIGEST, [&] {
       fwdev::launch_tdigest(cc, S.part, S.offs(), S.offT(), n, op->tb, op->td, op->d_status, op->stream);
     });
-  timed(op, K_SLOW, [&] {
-    fwdev::launch_slow(cc, op->wm, S.srow(cc.P), S.T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status, 0,
-                       op->stream);
-  });
+  if (!cc.dense)  // (tumbling windows without allowed lateness: no record needs arrival order)
+    timed(op, K_SLOW, [&] {
+      fwdev::launch_slow(cc, op->wm, S.srow(cc.P), S.T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status,
+                         0, op->stream);
+    });
   HIP_OR_RETURN(op, hipGetLastError());
   HIP_OR_RETURN(op, hipEventRecord(op->ev_done[nxt], op->stream));  // the set's last use by this batch (see settle)
   S.T = T;
@@ -715,6 +718,18 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
 bool combine_eligible(const fw_config& c) {
   return c.assigner == FW_TUMBLING && c.aggregate == FW_AGG_COUNT_SUM_MIN_MAX && c.allowed_lateness == 0 &&
          !c.side_output && (c.key_kind == FW_KEY_LONG || c.key_kind == FW_KEY_INT);
+}
+// what a partial's representation depends on (fw_partials.config); never 0, so a zeroed struct never matches
+uint64_t combine_config_tag(const fw_config& c) {
+  const int64_t f[] = {c.assigner, c.size, c.offset, c.value_type, c.key_kind, c.max_parallelism, c.aggregate};
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+  for (int64_t x : f) {
+    h ^= (uint64_t)x + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+  }
+  return h | 1;
 }
 int push_partials(fw_op* op, const PartialCols& in, int64_t n) {
   int rc;
@@ -866,8 +881,17 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   c.max_par = cfg.max_parallelism;
   c.kg0 = cfg.key_group_start;
   c.n_kg = cfg.key_group_end - cfg.key_group_start + 1;
+  // dense regions (DevCfg::dense): tumbling windows, count/sum/min/max, no allowed lateness (FW_NO_DENSE=1 disables)
+  c.dense = cfg.assigner == FW_TUMBLING && cfg.aggregate == FW_AGG_COUNT_SUM_MIN_MAX && cfg.allowed_lateness == 0 &&
+            !(getenv("FW_NO_DENSE") && atoi(getenv("FW_NO_DENSE")));
   int64_t s = cfg.sub_partitions;
-  if (s == 0) {
+  if (s == 0 && c.dense) {
+    // about 3/4 of k_dt_aggregate's LDS table of live entries per region (C2: 2M live entries -> 1024 regions), at
+    // least 4 per key group (the compact records' window delta)
+    const int64_t keys = cfg.expected_entries > 0 ? cfg.expected_entries : 0;
+    const int64_t target = std::max<int64_t>(256, next_pow2((keys + FW_DT_SLOTS * 3 / 4 - 1) / (FW_DT_SLOTS * 3 / 4)));
+    s = std::max<int64_t>(4, next_pow2(std::max<int64_t>(1, target / c.n_kg)));
+  } else if (s == 0) {
     // about 2048 partitions, more when the expected keys would put more than ~512 keys in one: a
     // partition's (key, window) deltas of a batch must fit k_aggregate's LDS table, or it flushes
     // several times into its region (C3, 2M keys: 4096 partitions halve k_aggregate's time)
@@ -942,8 +966,8 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     HIP_OR_RETURN(op, hipMemsetAsync(c.pool_ctr, 0, 2 * sizeof(int32_t), op->stream));
   }
   // regions sized for the expected entries at 1/FW_TABLE_SLACK load (default 4: 25 %; the limit is 3/4)
-  const int64_t slack = getenv("FW_TABLE_SLACK") ? std::max(2, atoi(getenv("FW_TABLE_SLACK"))) : 4;
-  c.log_r = std::max(8, ilog2(slack * ((expected + c.P - 1) / c.P)));
+  const int64_t slack = getenv("FW_TABLE_SLACK") ? std::max(2, atoi(getenv("FW_TABLE_SLACK"))) : c.dense ? 2 : 4;
+  c.log_r = std::max(8, ilog2(slack * ((expected + c.P - 1) / c.P)));  // (dense: a region's groups, densely)
   op->table_slots = (int64_t)c.P << c.log_r;
 
   op->max_batch = cfg.max_batch > 0 ? std::min<int64_t>(cfg.max_batch, int64_t(1) << 31) : (int64_t(1) << 24);
@@ -1050,6 +1074,7 @@ void fw_destroy(fw_op* op) {
   dfree(op->tb.fire_e);
   dfree(op->tb.fire_lo);
   dfree(op->tb.pane_floor);
+  dfree(op->tb.passes);
   dfree(op->in_key);
   dfree(op->in_ts);
   dfree(op->in_val);
@@ -1324,7 +1349,7 @@ int fw_get_stats(fw_op* op, fw_stats* o) {
   HIP_OR_RETURN(op, hipMemcpyAsync(h3, op->d_stats3, sizeof h3, hipMemcpyDeviceToHost, op->stream));
   if ((rc = sync_status(op))) return rc;
   const Status& s = *op->h_status;
-  o->records_in = op->records_in;
+  o->records_in = op->records_in + (int64_t)s.partial_records;  // + the records inside merged partials
   o->late_records_dropped = (int64_t)s.late_dropped;
   o->keyed_state_entries = (int64_t)h3[0];
   o->event_time_timers = (int64_t)h3[1];
@@ -1363,7 +1388,7 @@ int fw_profile_read(fw_op* op, double* ms, int64_t* launches, int reset) {
 
 const char* fw_kernel_name(int kind) { return kind >= 0 && kind < FW_NUM_KERNELS ? KERNEL_NAMES[kind] : ""; }
 
-int fw_combine_extract_device(fw_op* op, int32_t world, const fw_partials* out, int64_t cap, int64_t* counts,
+int fw_combine_extract_device(fw_op* op, int32_t world, fw_partials* out, int64_t cap, int64_t* counts,
                               int64_t* n) {
   if (!op || !n || world < 1 || (world > 1 && !counts)) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   if (!combine_eligible(op->cfg))
@@ -1396,6 +1421,7 @@ int fw_combine_extract_device(fw_op* op, int32_t world, const fw_partials* out, 
                                (long long)cap);
   if (*n > 0 && (!out || !out->key || !out->start || !out->cnt || !out->sum || !out->min || !out->max))
     return set_err(op, FW_ERR_ARG, "null output column");
+  if (out) out->config = combine_config_tag(op->cfg);
   if (*n > 0) {
     fwdev::launch_extract(c, op->tb, op->xoffs, PartialCols{out->key, out->start, out->cnt, out->sum, out->min, out->max},
                           op->stream);
@@ -1413,6 +1439,10 @@ int fw_push_partials_device(fw_op* op, const fw_partials* in, int64_t n) {
                    "output and Long or Integer keys");
   if (n > 0 && (!in->key || !in->start || !in->cnt || !in->sum || !in->min || !in->max))
     return set_err(op, FW_ERR_ARG, "null column");
+  if (in->config != combine_config_tag(op->cfg))
+    return set_err(op, FW_ERR_ARG,
+                   "partials from a combiner configured differently (assigner, size, offset, value type, key kind, max "
+                   "parallelism or aggregate) than this operator");
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   for (int64_t b = 0; b < n; b += op->max_batch) {
     const int64_t m = std::min(op->max_batch, n - b);
@@ -1495,6 +1525,61 @@ int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64
   return FW_OK;
 }
 
+}  // extern "C"
+namespace {
+// restore into dense regions: the rows (already checked to belong to kg) become partial accumulators in
+// partition-major runs and are merged like a combining push; a region whose buffers are too small suspends the
+// merge, the table grows and the merge resumes (synchronous)
+int restore_dense(fw_op* op, int32_t kg, const fw_state_rows* src, int64_t n) {
+  const int32_t P = op->dc.P;
+  const int32_t T = (int32_t)((n + FW_TILE - 1) / FW_TILE);
+  const int64_t m = (int64_t)(P + 1) * T;
+  StateCols d{};
+  int32_t* rp = nullptr;
+  uint32_t *hist = nullptr, *scan_tmp = nullptr;
+  PartialRec *tmp = nullptr, *part = nullptr;
+  auto done = [&](int code) {
+    free_state_cols(d);
+    dfree(rp);
+    dfree(hist);
+    dfree(scan_tmp);
+    dfree(tmp);
+    dfree(part);
+    return code;
+  };
+  int rc;
+  if ((rc = alloc_state_cols(op, d, n))) return done(rc);
+  const int64_t* hs[8] = {src->key, src->start, src->end, src->count, src->sum, src->min, src->max, src->timer};
+  int64_t* ds[8] = {d.key, d.start, d.end, d.cnt, d.sum, d.mn, d.mx, d.timer};
+  for (int i = 0; i < 8; i++)
+    if (hipMemcpyAsync(ds[i], hs[i], n * sizeof(int64_t), hipMemcpyHostToDevice, op->stream) != hipSuccess)
+      return done(set_err(op, FW_ERR_HIP, "restore: copy failed"));
+  if (dmalloc(&rp, (size_t)n) != hipSuccess || dmalloc(&hist, (size_t)m) != hipSuccess ||
+      dmalloc(&scan_tmp, (size_t)(m / 4096 + 2)) != hipSuccess || dmalloc(&tmp, (size_t)n) != hipSuccess ||
+      dmalloc(&part, (size_t)n) != hipSuccess)
+    return done(set_err(op, FW_ERR_HIP, "restore: allocation failed"));
+  fwdev::launch_dt_restore_runs(op->dc, kg, d, n, rp, hist, scan_tmp, tmp, part, op->d_status, op->stream);
+  for (int resume = 0, rounds = 0;; resume = 1) {
+    if (++rounds > 64) return done(set_err(op, FW_ERR_STATE, "restore did not complete after 64 resumptions"));
+    fwdev::launch_pmerge(op->dc, part, hist, T, op->tb, op->prog, resume, op->d_status, op->stream);
+    if (hipGetLastError() != hipSuccess) return done(set_err(op, FW_ERR_HIP, "restore kernel failed"));
+    if ((rc = sync_status(op))) return done(rc);
+    Status& s = *op->h_status;
+    if (!s.suspended) break;
+    if ((rc = grow_table(op, log_r_for(op, s.need_live)))) return done(rc);
+    s.suspended = 0;
+    s.need_live = 0;
+    if ((rc = put_status_field(op, &Status::suspended)) || (rc = put_status_field(op, &Status::need_live)))
+      return done(rc);
+  }
+  done(FW_OK);
+  if (op->h_status->flags & FW_STATUS_STATE_LOST) return set_err(op, FW_ERR_CAPACITY, "restore: region full");
+  const int64_t rows = (int64_t)op->h_status->out_rows;
+  return ensure_out_capacity(op, rows + op->table_slots, rows);  // a watermark may fire every restored window
+}
+}  // namespace
+extern "C" {
+
 int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_t n) {
   if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_TDIGEST || op->cfg.assigner == FW_COUNT))
     return set_err(op, FW_ERR_UNSUPPORTED,  // not in fw_state_rows
@@ -1560,6 +1645,10 @@ int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_
     op->h_status->kg_errors = 0;
     put_status_field(op, &Status::kg_errors);
     return fail(set_err(op, FW_ERR_KEY_GROUP, "%d restored row(s) do not belong to key group %d", bad, kg));
+  }
+  if (op->dc.dense) {  // the rows as partials in partition-major runs, merged region by region (k_dt_aggregate)
+    fail(FW_OK);
+    return restore_dense(op, kg, src, n);
   }
   int64_t need = 0;
   for (int32_t p = 0; p < P; p++) need = std::max<int64_t>(need, (int64_t)live[p] + dem[p]);
@@ -1788,6 +1877,10 @@ int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64
     if (op->cfg.key_group_start != (r * M + W - 1) / W || op->cfg.key_group_end != ((r + 1) * M - 1) / W)
       return set_err(op, FW_ERR_ARG, "the operator's KeyGroupRange is not subtask %d of %d's", r, W);
   }
+  if (combine_config_tag(comb->cfg) != combine_config_tag(op->cfg))
+    return set_err(op, FW_ERR_ARG,
+                   "the combiner is configured differently (assigner, size, offset, value type, key kind, max "
+                   "parallelism or aggregate) than the operator");
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;
   // the batch into the combiner, ordered after the columns' producer (the caller's fw_stream(op) order)
@@ -1861,7 +1954,7 @@ int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64
   }
   NCCL_OR_RETURN(op, ncclGroupEnd());
   if (combined_wm) *combined_wm = c->h_counts[2 * W + 1];
-  const fw_partials in{c->pr[0], c->pr[1], c->pr[2], c->pr[3], c->pr[4], c->pr[5]};
+  const fw_partials in{c->pr[0], c->pr[1], c->pr[2], c->pr[3], c->pr[4], c->pr[5], out.config};
   return fw_push_partials_device(op, &in, total);
 }
 

@@ -254,7 +254,10 @@ __global__ void k_wire_encode(DevRows rows, int64_t n, WireL L, int32_t f64, uin
   uint8_t* p = out + r * S;
   st_be(p, (uint64_t)(9 + L.F), 4);
   p[4] = 0;
-  st_be(p + 5, (uint64_t)(rows.end[r] - 1), 8);  // window.maxTimestamp()
+  // window.maxTimestamp(): end - 1 for a TimeWindow (TimeWindow.java:83-85), Long.MAX_VALUE for the GlobalWindow
+  // of a count window (GlobalWindow.java:45-46; its rows carry end = Long.MAX_VALUE)
+  const int64_t end = rows.end[r];
+  st_be(p + 5, (uint64_t)(end == INT64_MAX ? end : end - 1), 8);
   for (int f = 0; f < L.nf; f++) {
     const int role = L.role[f];
     int64_t v = role == FW_ROLE_KEY ? rows.key[r] : role == FW_ROLE_START ? rows.start[r]

@@ -182,6 +182,7 @@ class CombiningExchange:
         ex = self.exchange
         self.combiner.process_batch(keys, ts, vals)
         cols, counts = self.combiner.combine_extract(ex.world)
+        config = cols.config
         if ex.world > 1:
             staged = cols[0].is_cuda and dist.get_backend(ex.group) == "gloo"
             move = (lambda x: x.cpu()) if staged else (lambda x: x)
@@ -201,5 +202,5 @@ class CombiningExchange:
             self.partials_sent += sum(counts) - counts[ex.rank]
         else:  # the combiner reuses its output buffers; the operator reads the partials asynchronously
             cols = tuple(c.clone() for c in cols)
-        op.push_partials(*cols)
+        op.push_partials(*cols, config=config)
         return ex.combine_watermark(local_wm, device=keys.device)

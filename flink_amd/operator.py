@@ -32,6 +32,12 @@ def _is_torch(x):
     return type(x).__module__.startswith("torch")
 
 
+class Partials(tuple):
+    """The six partial-accumulator columns (key, start, cnt, sum, min, max) of one combine_extract, with `config`,
+    the producing combiner's configuration tag that push_partials hands back to fw_push_partials_device."""
+    config = 0
+
+
 class GpuWindowOperator:
     def __init__(self, assigner: WindowAssigner, aggregate=CountSumMinMax(), trigger: Trigger = None,
                  allowed_lateness=0, side_output=False, key_type="long", max_parallelism=128,
@@ -195,12 +201,16 @@ class GpuWindowOperator:
             N.check(rc, self._h)
             break
         if n.value == 0:
-            return tuple(torch.empty(0, dtype=torch.int64, device=dev) for _ in range(6)), list(counts)
-        return tuple(t[:n.value] for t in self._pbuf), list(counts)
+            cols = Partials(torch.empty(0, dtype=torch.int64, device=dev) for _ in range(6))
+        else:
+            cols = Partials(t[:n.value] for t in self._pbuf)
+        cols.config = out.config
+        return cols, list(counts)
 
-    def push_partials(self, key, start, cnt, sum_, min_, max_):
+    def push_partials(self, key, start, cnt, sum_, min_, max_, config):
         """fw_push_partials_device: merges partial accumulators (from combine_extract of a combiner with the same
-        configuration) of this subtask's KeyGroupRange; late ones are dropped and counted with their records."""
+        configuration; `config` = that extraction's Partials.config tag, checked against this handle's own) of this
+        subtask's KeyGroupRange; late ones are dropped and counted with their records."""
         import torch
         cols = (key, start, cnt, sum_, min_, max_)
         n = key.numel()
@@ -210,7 +220,7 @@ class GpuWindowOperator:
         if n == 0:
             return
         self._torch_stream(key.device).wait_stream(torch.cuda.current_stream(key.device))
-        p = N.FwPartials(*(t.data_ptr() for t in cols))
+        p = N.FwPartials(*(t.data_ptr() for t in cols), config)
         N.check(N.lib().fw_push_partials_device(self._h, ctypes.byref(p), n), self._h)
         self._inflight = cols
 

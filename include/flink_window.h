@@ -255,8 +255,14 @@ void* fw_input_stream(fw_op* op);
  * (WindowOperator.java:402-418; with allowed lateness 0 every record of a late window is late). */
 typedef struct {
   int64_t *key, *start, *cnt, *sum, *min, *max;
+  /* the producing combiner's configuration tag (written by fw_combine_extract_device): assigner, size, offset,
+     value type, key kind, max parallelism and aggregate.  fw_push_partials_device refuses partials whose tag is
+     not its own (FW_ERR_ARG): the accumulators are in the handle's internal representation (f64 min/max in
+     sortable form, window starts of its own size and offset), so a differently configured receiver would
+     misread them. */
+  uint64_t config;
 } fw_partials;
-int fw_combine_extract_device(fw_op* combiner, int32_t world, const fw_partials* out, int64_t cap, int64_t* counts,
+int fw_combine_extract_device(fw_op* combiner, int32_t world, fw_partials* out, int64_t cap, int64_t* counts,
                               int64_t* n);
 int fw_push_partials_device(fw_op* op, const fw_partials* in, int64_t n);
 
@@ -327,7 +333,8 @@ void fw_comm_destroy(fw_comm* comm);
 int fw_keyby_push_device(fw_comm* comm, fw_op* op, const int64_t* key, const int64_t* ts, const void* val,
                          const int32_t* key_hash, int64_t n, int64_t local_wm, int64_t* combined_wm);
 /* The same with pre-shuffle combining (see fw_combine_extract_device): the batch goes into `combiner` (this
- * subtask's combiner handle, same configuration, never given a watermark), which is drained into partials; the
+ * subtask's combiner handle, same configuration -- FW_ERR_ARG otherwise --, never given a watermark), which is
+ * drained into partials; the
  * partials' per-peer counts and six columns cross the exchange instead of the records, and the received ones are
  * merged into `op` (fw_push_partials_device).  Eligible configurations only. */
 int fw_keyby_combine_push_device(fw_comm* comm, fw_op* combiner, fw_op* op, const int64_t* key, const int64_t* ts,

@@ -143,7 +143,9 @@ int64_t oracle_wire_encode(const oracle_wire_layout* L, const oracle_row* rows, 
     uint8_t* p = out + r * S;
     put_be(p, (uint64_t)(9 + F), 4);
     p[4] = 0;
-    put_be(p + 5, (uint64_t)(rows[r].end - 1), 8);  // window.maxTimestamp()
+    // window.maxTimestamp(): TimeWindow end - 1 (TimeWindow.java:83-85); GlobalWindow Long.MAX_VALUE
+    // (GlobalWindow.java:45-46, count-window rows carry end = Long.MAX_VALUE)
+    put_be(p + 5, (uint64_t)(rows[r].end == INT64_MAX ? rows[r].end : rows[r].end - 1), 8);
     uint8_t* f = p + 13;
     for (int i = 0; i < L->nfields; i++) {
       const oracle_row& w = rows[r];

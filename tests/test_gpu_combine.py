@@ -65,7 +65,7 @@ def test_gpu_combine_world1_vs_oracle(value_type, keys, n, batch, expected):
         parts, counts = comb.combine_extract(1)
         assert counts == [parts[0].numel()]
         sent += parts[0].numel()
-        op.push_partials(*(c.clone() for c in parts))
+        op.push_partials(*(c.clone() for c in parts), config=parts.config)
         ref.process(k, t, v)
         rows.append(op.process_watermark(wm))
         ref.watermark(wm)
@@ -73,6 +73,7 @@ def test_gpu_combine_world1_vs_oracle(value_type, keys, n, batch, expected):
     ref.watermark((1 << 63) - 1)
     assert_rows_equal(np.concatenate(rows), ref.rows(), _VT[value_type])
     assert op.late_dropped == ref.late_dropped
+    assert op.stats()["records_in"] == n  # numRecordsIn counts the records inside the partials
     if expected:
         assert op.stats()["table_grows"] >= 1
     else:
@@ -91,7 +92,7 @@ def test_gpu_combine_rejects_foreign_key_groups_and_ineligible_configs():
     k = torch.arange(1000, dtype=torch.int64, device="cuda")
     comb.process_batch(k, k + 1_000_000, k)
     parts, _ = comb.combine_extract(1)
-    op.push_partials(*(c.clone() for c in parts))
+    op.push_partials(*(c.clone() for c in parts), config=parts.config)
     with pytest.raises(N.NativeError):  # keys of key groups 64..127 reach a subtask owning 0..63
         op.process_watermark(0)
     bad = GpuWindowOperator(SlidingEventTimeWindows.of(3000, 1000), device=0)
@@ -192,3 +193,23 @@ def test_gpu_native_keyby_combine_world1():
     ex.close()
     comb.close()
     op.close()
+
+
+@pytest.mark.parametrize("what", ["size", "value_type"])
+def test_gpu_combine_rejects_mismatched_combiner(what):
+    """Partials carry their combiner's configuration tag: a receiver with another window size (its window starts
+    would be re-bucketed) or value type (f64 min/max are kept in sortable form) refuses them instead of misreading."""
+    import torch
+    from flink_amd import _native as N
+    from flink_amd import TumblingEventTimeWindows
+    from flink_amd.operator import GpuWindowOperator
+    comb = GpuWindowOperator(TumblingEventTimeWindows.of(1000), device=0)
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(2000 if what == "size" else 1000),
+                           CountSumMinMax(_VT["f64" if what == "value_type" else "i64"]), device=0)
+    k = torch.arange(1000, dtype=torch.int64, device="cuda")
+    comb.process_batch(k, k + 1_000_000, k)
+    parts, _ = comb.combine_extract(1)
+    with pytest.raises(N.NativeError, match="configured differently"):
+        op.push_partials(*(c.clone() for c in parts), config=parts.config)
+    for o in (comb, op):
+        o.close()

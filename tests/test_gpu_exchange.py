@@ -28,10 +28,33 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _slice(rank, step, key_type):
+# operator kinds through the exchange: (assigner, oracle kwargs, key distribution); the session and HLL streams
+# draw Zipf(1.1) keys (BASELINE configs[3] / [4] shapes at parity size), panes are sliding 60 s / 1 s (configs[2])
+KINDS = {
+    "tumbling": dict(oracle=dict(assigner="tumbling", size=1000), zipf=None),
+    "sessions": dict(oracle=dict(assigner="session", gap=30_000), zipf=1.1),
+    "panes": dict(oracle=dict(assigner="sliding", size=60_000, slide=1000), zipf=None),
+    "hll": dict(oracle=dict(assigner="tumbling", size=1000, hll_p=12), zipf=1.1),
+}
+
+
+def _operator(kind, key_type, kgr):
+    from flink_amd import (EventTimeSessionWindows, HyperLogLog, SlidingEventTimeWindows,
+                           TumblingEventTimeWindows)
+    from flink_amd.operator import GpuWindowOperator
+    from flink_amd.windowing import CountSumMinMax
+    assigner = {"tumbling": TumblingEventTimeWindows.of(1000), "sessions": EventTimeSessionWindows.with_gap(30_000),
+                "panes": SlidingEventTimeWindows.of(60_000, 1000), "hll": TumblingEventTimeWindows.of(1000)}[kind]
+    agg = HyperLogLog(12) if kind == "hll" else CountSumMinMax()
+    return GpuWindowOperator(assigner, agg, key_type=key_type, max_parallelism=MAX_PAR, key_group_range=kgr,
+                             device=0, expected_entries=20_000 if kind == "hll" else 0)
+
+
+def _slice(rank, step, key_type, kind="tumbling"):
     from flink_amd.keygroups import string_hash_code
     first = (step * WORLD + rank) * BATCH
-    k, t, v = generate_host(0x5EED, first, BATCH, KEYS, ts_base=0, rate=100_000, jitter=300)
+    k, t, v = generate_host(0x5EED, first, BATCH, KEYS, ts_base=0, rate=100_000, jitter=300,
+                            zipf_s=KINDS[kind]["zipf"])
     h = None
     if key_type == "int":
         k = k - KEYS // 2  # negative Integer keys
@@ -40,21 +63,18 @@ def _slice(rank, step, key_type):
     return k, t, v, h
 
 
-def _worker(rank, port, out_dir, key_type):
+def _worker(rank, port, out_dir, key_type, kind="tumbling"):
     import torch
     import torch.distributed as dist
-    from flink_amd import TumblingEventTimeWindows
     from flink_amd.exchange import KeyGroupExchange
-    from flink_amd.operator import GpuWindowOperator
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     ex = KeyGroupExchange(MAX_PAR, WORLD, rank, key_type=key_type)
-    op = GpuWindowOperator(TumblingEventTimeWindows.of(1000), key_type=key_type, max_parallelism=MAX_PAR,
-                           key_group_range=ex.key_group_range, device=0)
+    op = _operator(kind, key_type, ex.key_group_range)
     mx = -(1 << 63)
     dev = torch.device("cuda", 0)
     for s in range(STEPS):
-        k, t, v, h = _slice(rank, s, key_type)
+        k, t, v, h = _slice(rank, s, key_type, kind)
         mx = max(mx, int(t.max()))
         cols = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (k, t, v)]
         hk = torch.from_numpy(h).to(dev) if h is not None else None
@@ -136,3 +156,34 @@ def test_gpu_native_keyby_world1():
     _same(op.rows(), ref.rows())
     ex.close()
     op.close()
+
+
+@pytest.mark.parametrize("kind", ["sessions", "panes", "hll"])
+def test_gpu_exchange_world2_operator_kinds(tmp_path, kind):
+    """Sessions (gap 30 s, Zipf keys: MergingWindowSet merges per key on its owning subtask), panes (sliding
+    60 s / 1 s) and HyperLogLog (Zipf keys) through the world-size-2 exchange: the union of both subtasks' rows
+    equals one oracle operator over the whole stream (fed in the exchange's per-step source-major order, global
+    watermarks)."""
+    import torch.multiprocessing as mp
+    mp.spawn(_worker, args=(_free_port(), str(tmp_path), "long", kind), nprocs=WORLD, join=True)
+    rows = np.concatenate([np.load(tmp_path / f"rows_{r}.npy") for r in range(WORLD)])
+    ref = orc.WindowOperatorOracle(**KINDS[kind]["oracle"])
+    mx = [-(1 << 63)] * WORLD
+    for s in range(STEPS):
+        parts = [_slice(r, s, "long", kind) for r in range(WORLD)]
+        for r in range(WORLD):
+            mx[r] = max(mx[r], int(parts[r][1].max()))
+        for src in range(WORLD):
+            ref.process(*parts[src][:3])
+        ref.watermark(min(m - 300 for m in mx))
+    ref.watermark((1 << 63) - 1)
+    r = ref.rows()
+    if kind == "hll":  # registers, zero count and checksum bit-exact; the estimate's log within an ulp
+        key = lambda a: np.lexsort((a["start"], a["key"], a["epoch"]))  # noqa: E731
+        a, b = rows[key(rows)], r[key(r)]
+        assert len(a) == len(b) > 0
+        for f in ("epoch", "key", "start", "end", "count", "min", "max"):
+            np.testing.assert_array_equal(a[f], b[f])
+        np.testing.assert_allclose(a["sum"].view(np.float64), b["sum"].view(np.float64), rtol=1e-9)
+    else:
+        _same(rows, r)

@@ -189,8 +189,6 @@ def _by_values(v, value_type):
 def test_gpu_min_by_max_by_vs_oracle(cfg, value_type, by):
     # a9 minBy/maxBy (first = true) over Integer, Long and Double fields (ComparableAggregator.java:72-94,
     # Comparator.java:35-108): the selected element's field and arrival ordinal
-    if value_type != "i32" and cfg.get("lateness"):
-        pytest.skip("the late-firing configurations run for Integer fields")
     batches, wms = _stream(120_000, 10_000, 5000, bound=400, jitter=1500, rate=100_000)
     batches = [(k, t, _by_values(v, value_type)) for k, t, v in batches]
     cfg = dict(cfg, value_type=value_type, by=by)
