@@ -697,16 +697,12 @@ __device__ __forceinline__ void store_pair(PRec* part, bool valid, uint32_t pos,
 
 // ---- K2: scatter.  Normal records -> their partition's run (any order inside the run), one
 // 32-byte sector per record; late records -> side output / counter.
-template <int MODE>
-__global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
-                                                             const int64_t* __restrict__ ts,
-                                                             const int64_t* __restrict__ val,
-                                                             const int32_t* __restrict__ kh, int64_t n, int32_t T,
-                                                             const uint32_t* __restrict__ offs, PRec* __restrict__ part,
-                                                             DevSide side, Status* st) {
-  specialize<MODE>(c);
-  extern __shared__ uint32_t base[];  // P: next free slot of each partition's run for this tile
-  const int32_t tile = tile_of_block(T);
+// (the body of one tile: base = P words of LDS for the runs' next free slots)
+__device__ __forceinline__ void scatter_direct(const DevCfg& c, int64_t wm, const int64_t* __restrict__ key,
+                                               const int64_t* __restrict__ ts, const int64_t* __restrict__ val,
+                                               const int32_t* __restrict__ kh, int64_t n, int32_t T,
+                                               const uint32_t* __restrict__ offs, PRec* __restrict__ part, DevSide side,
+                                               Status* st, uint32_t* base, int32_t tile) {
   for (int i = threadIdx.x; i < c.P; i += blockDim.x) base[i] = offs[(int64_t)i * T + tile];
   __syncthreads();
   const int64_t tbase = (int64_t)tile * FW_TILE;
@@ -778,6 +774,127 @@ __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(D
       const int64_t nwf = agg_ordinal(c) ? (i << 16) | nwin : (int64_t)nwin;
       store_pair(part, norm, pos, i64x2{k[j], last}, i64x2{v[j], (long long)nwf});
     }
+  }
+  if (late) atomicAdd(&st->late_dropped, late);
+}
+template <int MODE>
+__global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
+                                                             const int64_t* __restrict__ ts,
+                                                             const int64_t* __restrict__ val,
+                                                             const int32_t* __restrict__ kh, int64_t n, int32_t T,
+                                                             const uint32_t* __restrict__ offs, PRec* __restrict__ part,
+                                                             DevSide side, Status* st) {
+  specialize<MODE>(c);
+  extern __shared__ uint32_t base[];  // P: next free slot of each partition's run for this tile
+  scatter_direct(c, wm, key, ts, val, kh, n, T, offs, part, side, st, base, tile_of_block(T));
+}
+
+// ---- K2, staged form (compact batches, P <= 2048).  The scattered 16-byte stores of k_scatter land as partial
+// lines all over the partition runs (2x the written bytes at 4096 partitions, profiles/traffic_r02_c2.json).  Here a
+// tile goes through in rounds of RR records: each round's compact records are sorted by partition in LDS and every
+// partition's piece is written as one contiguous run (consecutive lanes, consecutive addresses) behind the pieces of
+// the earlier rounds.  Same layout as k_scatter (partition-major runs at the scan offsets, any order inside a run).
+// A batch without compact records goes through k_scatter's body.
+template <int MODE, int RR>
+__global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_staged(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
+                                                                   const int64_t* __restrict__ ts,
+                                                                   const int64_t* __restrict__ val,
+                                                                   const int32_t* __restrict__ kh, int64_t n, int32_t T,
+                                                                   const uint32_t* __restrict__ offs,
+                                                                   PRec* __restrict__ part, DevSide side, Status* st) {
+  specialize<MODE>(c);
+  extern __shared__ __attribute__((aligned(16))) uint8_t sraw[];
+  i64x2* stg = reinterpret_cast<i64x2*>(sraw);          // RR: the round's records sorted by partition
+  uint16_t* sp = reinterpret_cast<uint16_t*>(stg + RR);  // RR: their partitions
+  uint32_t* gb = reinterpret_cast<uint32_t*>(sp + RR);   // P: next free slot of each partition's run
+  uint32_t* cs = gb + c.P;                               // P + 1: the round's counts, then their starts in stg
+  uint32_t* wsum = cs + c.P + 1;                         // block scan
+  const int32_t tile = tile_of_block(T);
+  const bool cmp = c.compact && !*c.wide;  // (uniform: every classify workgroup has finished)
+  if (!cmp) {
+    scatter_direct(c, wm, key, ts, val, kh, n, T, offs, part, side, st, gb, tile);
+    return;
+  }
+  for (int i = threadIdx.x; i < c.P; i += FW_TILE_THREADS) gb[i] = offs[(int64_t)i * T + tile];
+  const int64_t tbase = (int64_t)tile * FW_TILE;
+  const int64_t tend = min(n, tbase + (int64_t)FW_TILE);
+  unsigned long long late = 0;
+  constexpr int RPT = RR / FW_TILE_THREADS;
+  const int ppt = (c.P + FW_TILE_THREADS - 1) / FW_TILE_THREADS;
+  i64x2* out = reinterpret_cast<i64x2*>(part);
+  for (int64_t b = tbase; b < tend; b += RR) {
+    for (int i = threadIdx.x; i <= c.P; i += FW_TILE_THREADS) cs[i] = 0;
+    __syncthreads();
+    // (two halves of RPT / 2 records: each half's loads in flight together, fewer registers than all at once)
+    uint32_t rk[RPT];
+    uint32_t pj[RPT];
+    int64_t w[RPT], v[RPT];
+#pragma unroll
+    for (int hf = 0; hf < 2; hf++) {
+      constexpr int H = RPT / 2;
+      const int64_t bh = b + (int64_t)hf * H * FW_TILE_THREADS;
+      int64_t k[H], t[H], vh[H];
+      int32_t hh[H];
+      load_records<H / 2, true>(c, key, ts, val, kh, bh, tend, k, t, vh, hh);
+#pragma unroll
+      for (int j = 0; j < H; j++) {
+        const int jj = hf * H + j;
+        const int64_t i = rec_index(bh, j >> 1, j & 1);
+        pj[jj] = 0xffffffffu;
+        v[jj] = vh[j];
+        if (i >= tend) continue;
+        const int32_t h = c.key_kind == FW_KEY_HASHED ? hh[j] : key_hash_of(c.key_kind, k[j], kh, i);
+        const int32_t p = partition_of(c, k[j], h);
+        if (p < 0) continue;
+        int64_t last = 0;
+        int nwin = 0;
+        const int cls = classify(c, wm, t[j], &last, &nwin, k[j], 0);
+        if (cls == CLS_NORMAL) {
+          rk[jj] = atomicAdd(&cs[p], 1u);
+          pj[jj] = (uint32_t)p;
+          w[jj] = compact_encode(c, k[j], compact_delta(c, last));
+        } else if (cls == CLS_LATE) {
+          if (c.side_output)
+            side_one(side, st, k[j], t[j], vh[j]);
+          else
+            late++;
+        }
+      }
+    }
+    __syncthreads();
+    // exclusive scan of the round's counts (ppt partitions per thread), cs[P] = the round's records
+    uint32_t cq[(FW_GMAX_P + FW_TILE_THREADS - 1) / FW_TILE_THREADS], sum = 0;
+#pragma unroll
+    for (int q = 0; q < (FW_GMAX_P + FW_TILE_THREADS - 1) / FW_TILE_THREADS; q++) {
+      const int pp = threadIdx.x * ppt + q;
+      cq[q] = q < ppt && pp < c.P ? cs[pp] : 0u;
+      sum += cq[q];
+    }
+    uint32_t total;
+    uint32_t e = block_excl_scan(sum, wsum, &total);
+#pragma unroll
+    for (int q = 0; q < (FW_GMAX_P + FW_TILE_THREADS - 1) / FW_TILE_THREADS; q++) {
+      const int pp = threadIdx.x * ppt + q;
+      if (q < ppt && pp < c.P) cs[pp] = e;
+      e += cq[q];
+    }
+    if (threadIdx.x == 0) cs[c.P] = total;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RPT; j++) {
+      if (pj[j] == 0xffffffffu) continue;
+      const uint32_t pos = cs[pj[j]] + rk[j];
+      stg[pos] = i64x2{w[j], v[j]};
+      sp[pos] = (uint16_t)pj[j];
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < total; i += FW_TILE_THREADS) {
+      const uint32_t pp = sp[i];
+      out[gb[pp] + (i - cs[pp])] = stg[i];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < c.P; i += FW_TILE_THREADS) gb[i] += cs[i + 1] - cs[i];
+    __syncthreads();
   }
   if (late) atomicAdd(&st->late_dropped, late);
 }
@@ -4294,6 +4411,12 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_table_stats(DevCfg c, DevTa
 // A region whose entries and new groups exceed the LDS table is done in 2^b passes, each over the (key, window)s
 // whose hash has prefix k: every pass reads the region and the records again and keeps its share.
 enum { DT_RECS = 0, DT_PARTS = 1 };
+enum { DT_OK = 0, DT_OVER = 1, DT_WIDE = 2 };  // an attempt's outcome (dt_attempt)
+// The LDS table has two layouts.  The compact one (DtLdsK) keys a slot by the 64-bit CRec word of (key, window)
+// (compact_encode: fmix64 of the key with the window delta in its top log_s bits, unique inside a region): a lookup
+// reads one word, a claim is one 64-bit CAS (the accumulators are initialised when the table is cleared).  The wide
+// one (DtLds: {key, window start} behind a fingerprint tag, the protocol of lds_slot) takes what has no compact form
+// (a wide batch, partials, entries far from the watermark).
 constexpr int DT_LIMIT = FW_DT_SLOTS * 13 / 16;  // claims stop here, so every probe chain ends at an EMPTY slot
 constexpr int DT_BUCKETS = FW_DT_SLOTS / 4;
 static_assert(FW_DT_SLOTS % 4 == 0, "FW_DT_SLOTS: buckets of 4");
@@ -4302,16 +4425,42 @@ struct DtLds {
   i64x2 kv[FW_DT_SLOTS];      // {key, window start}
   unsigned long long cnt[FW_DT_SLOTS];
   int64_t sum[FW_DT_SLOTS], mn[FW_DT_SLOTS], mx[FW_DT_SLOTS];
-  int fill, over, nout, capover;
-  long long ntmin;
+};
+constexpr int DK_SLOTS = (int)(sizeof(DtLds) / 40 / 16 * 16);
+constexpr int DK_LIMIT = DK_SLOTS * 13 / 16;
+constexpr unsigned long long DK_EMPTY = ~0ull;  // (a record or entry whose word is this takes the wide table)
+struct DtLdsK {
+  unsigned long long kw[DK_SLOTS];
+  unsigned long long cnt[DK_SLOTS];
+  int64_t sum[DK_SLOTS], mn[DK_SLOTS], mx[DK_SLOTS];
+};
+union DtTab {
+  DtLds w;
+  DtLdsK k;
+};
+struct DtMisc {
+  int fill, over, nout, capover, widefb;
+  long long ntmin, out;
 };
 __device__ __forceinline__ uint32_t dt_bucket(uint32_t h) { return (uint32_t)(((uint64_t)h * DT_BUCKETS) >> 32); }
+__device__ __forceinline__ uint32_t dk_home(unsigned long long kw) {
+  uint32_t h = (uint32_t)(kw >> 32) * 0x9E3779B1u ^ (uint32_t)kw;
+  h ^= h >> 15;
+  return (uint32_t)(((uint64_t)h * DK_SLOTS) >> 32);
+}
 // the hash pass of (key, window): prefix of a hash independent of the LDS slot's
 __device__ __forceinline__ int dt_pass(const DevCfg& c, int64_t key, int64_t start, int hb) {
   return hb ? (int)((uint32_t)(slot_hash(c, key, start) >> 32) >> (32 - hb)) : 0;
 }
-// find or claim the slot of (key, start); -1 at the fill limit (the protocol of lds_slot)
-__device__ __forceinline__ int dt_slot(DtLds& L, int64_t key, int64_t start, uint32_t h) {
+// one claim ticket below the table's fill limit
+__device__ __forceinline__ bool dt_ticket(DtMisc& M, int limit) {
+  if (__hip_atomic_load(&M.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= limit) return false;
+  if (atomicAdd(&M.fill, 1) < limit) return true;
+  atomicSub(&M.fill, 1);
+  return false;
+}
+// wide table: find or claim the slot of (key, start); -1 at the fill limit (the protocol of lds_slot)
+__device__ __forceinline__ int dt_slot(DtLds& L, DtMisc& M, int64_t key, int64_t start, uint32_t h) {
   const uint32_t fp = lds_fp(h);
   uint32_t b = dt_bucket(h);
   for (int guard = 0; guard < 4 * DT_BUCKETS;) {
@@ -4335,11 +4484,7 @@ __device__ __forceinline__ int dt_slot(DtLds& L, int64_t key, int64_t start, uin
       continue;
     }
     if (empty >= 0) {
-      if (__hip_atomic_load(&L.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= DT_LIMIT) return -1;
-      if (atomicAdd(&L.fill, 1) >= DT_LIMIT) {
-        atomicSub(&L.fill, 1);
-        return -1;
-      }
+      if (!dt_ticket(M, DT_LIMIT)) return -1;
       const int s = (int)b * 4 + empty;
       if (atomicCAS(&L.tag[s], LT_EMPTY, LT_BUSY) == LT_EMPTY) {
         L.kv[s] = i64x2{key, start};
@@ -4350,7 +4495,7 @@ __device__ __forceinline__ int dt_slot(DtLds& L, int64_t key, int64_t start, uin
         __hip_atomic_store(&L.tag[s], fp, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         return s;
       }
-      atomicSub(&L.fill, 1);
+      atomicSub(&M.fill, 1);
       continue;  // lost the claim race: re-read the bucket
     }
     b = b + 1 == (uint32_t)DT_BUCKETS ? 0u : b + 1;  // bucket full without a match
@@ -4358,34 +4503,52 @@ __device__ __forceinline__ int dt_slot(DtLds& L, int64_t key, int64_t start, uin
   }
   return -1;
 }
-// AggregateFunction.add of one element (the value in the table's representation: f64 min/max sortable)
-__device__ __forceinline__ void dt_add(DtLds& L, int s, int vtype, int64_t v) {
-  atomicAdd(&L.cnt[s], 1ull);
+// compact table: find or claim the slot of word kw from slot s on; -1 at the fill limit
+__device__ __forceinline__ int dk_slot(DtLdsK& K, DtMisc& M, unsigned long long kw, uint32_t s) {
+  for (int guard = 0; guard < DK_SLOTS; guard++) {
+    unsigned long long g = __hip_atomic_load(&K.kw[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (g == kw) return (int)s;
+    if (g == DK_EMPTY) {
+      if (!dt_ticket(M, DK_LIMIT)) return -1;
+      g = atomicCAS(&K.kw[s], DK_EMPTY, kw);
+      if (g == DK_EMPTY) return (int)s;  // claimed (the accumulators were initialised with the table)
+      atomicSub(&M.fill, 1);
+      if (g == kw) return (int)s;
+    }
+    s = s + 1 == (uint32_t)DK_SLOTS ? 0u : s + 1;
+  }
+  return -1;
+}
+// AggregateFunction.add of one element (the value in the table's representation: f64 min/max sortable), and
+// AggregateFunction.merge of an accumulator in that representation, into slot s of either layout
+template <class L>
+__device__ __forceinline__ void dt_add(L& T, int s, int vtype, int64_t v) {
+  atomicAdd(&T.cnt[s], 1ull);
   int64_t sv = v;
   if (vtype == FW_VAL_F64) {
-    atomicAdd((double*)&L.sum[s], __longlong_as_double(v));
+    atomicAdd((double*)&T.sum[s], __longlong_as_double(v));
     sv = f64_sortable(v);
   } else {
-    atomicAdd((unsigned long long*)&L.sum[s], (unsigned long long)v);
+    atomicAdd((unsigned long long*)&T.sum[s], (unsigned long long)v);
   }
-  atomicMin((long long*)&L.mn[s], (long long)sv);
-  atomicMax((long long*)&L.mx[s], (long long)sv);
+  atomicMin((long long*)&T.mn[s], (long long)sv);
+  atomicMax((long long*)&T.mx[s], (long long)sv);
 }
-// AggregateFunction.merge of an accumulator in the table's representation
-__device__ __forceinline__ void dt_merge(DtLds& L, int s, int vtype, int64_t cnt, int64_t sum, int64_t mn, int64_t mx) {
-  atomicAdd(&L.cnt[s], (unsigned long long)cnt);
+template <class L>
+__device__ __forceinline__ void dt_merge(L& T, int s, int vtype, int64_t cnt, int64_t sum, int64_t mn, int64_t mx) {
+  atomicAdd(&T.cnt[s], (unsigned long long)cnt);
   if (vtype == FW_VAL_F64)
-    atomicAdd((double*)&L.sum[s], __longlong_as_double(sum));
+    atomicAdd((double*)&T.sum[s], __longlong_as_double(sum));
   else
-    atomicAdd((unsigned long long*)&L.sum[s], (unsigned long long)sum);
-  atomicMin((long long*)&L.mn[s], (long long)mn);
-  atomicMax((long long*)&L.mx[s], (long long)mx);
+    atomicAdd((unsigned long long*)&T.sum[s], (unsigned long long)sum);
+  atomicMin((long long*)&T.mn[s], (long long)mn);
+  atomicMax((long long*)&T.mx[s], (long long)mx);
 }
-// RPT elements: home buckets and candidates looked up together, the rest one by one (lds_upsert_batch's shape);
-// dm: bit j = element j done or absent.  false when the table is full.
+// RPT elements into the wide table: home buckets and candidates looked up together, the rest one by one
+// (lds_upsert_batch's shape); dm: bit j = element j done or absent.  false when the table is full.
 template <int RPT>
-__device__ __forceinline__ bool dt_add_batch(DtLds& L, int vtype, const int64_t (&k)[RPT], const int64_t (&s)[RPT],
-                                             const int64_t (&v)[RPT], uint32_t dm) {
+__device__ __forceinline__ bool dt_add_batch(DtLds& L, DtMisc& M, int vtype, const int64_t (&k)[RPT],
+                                             const int64_t (&s)[RPT], const int64_t (&v)[RPT], uint32_t dm) {
   uint32_t hh[RPT], b[RPT], fp[RPT];
   u32x4 t4[RPT];
 #pragma unroll
@@ -4414,96 +4577,157 @@ __device__ __forceinline__ bool dt_add_batch(DtLds& L, int vtype, const int64_t 
 #pragma unroll
   for (int j = 0; j < RPT; j++) {
     if (dm >> j & 1) continue;
-    const int t = dt_slot(L, k[j], s[j], hh[j]);
+    const int t = dt_slot(L, M, k[j], s[j], hh[j]);
     if (t < 0) return false;
     dt_add(L, t, vtype, v[j]);
   }
   return true;
 }
-
-// One workgroup per region.  SRC = DT_RECS: the batch's records (CRec / PRec runs of k_scatter); DT_PARTS: partial
-// accumulators (PartialRec runs of k_pscatter or of a restore).
-template <int SRC>
-__global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const void* __restrict__ in,
-                                                                const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
-                                                                AggProg prog, int resume, Status* st) {
-  __shared__ DtLds L;
-  __shared__ long long out_s;
-  const int32_t p = blockIdx.x;
-  if (p >= c.P || (resume && prog.done[p])) return;
-  const int64_t begin = offs[(int64_t)p * T], end = offs[(int64_t)(p + 1) * T];
-  if (begin == end) {  // nothing for this region: it stays as it is
-    if (threadIdx.x == 0) prog.done[p] = 1;
-    return;
+// the same for compact words: every home slot read together, then claims / probes one by one
+template <int RPT>
+__device__ __forceinline__ bool dk_add_batch(DtLdsK& K, DtMisc& M, int vtype, const unsigned long long (&w)[RPT],
+                                             const int64_t (&v)[RPT], uint32_t dm) {
+  uint32_t s[RPT];
+  unsigned long long g[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; j++) {
+    s[j] = dk_home(w[j]);
+    if (!(dm >> j & 1)) g[j] = __hip_atomic_load(&K.kw[s[j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-  const int X = tb.cur[p], Y = X ^ 1;
-  const int64_t base = (int64_t)p << c.log_r, R = (int64_t)1 << c.log_r;
-  const Entry* __restrict__ src = tb.ent[X] + base;
-  Entry* __restrict__ dst = tb.ent[Y] + base;
-  const int32_t live = tb.live[p];
-  const bool cmp = SRC == DT_RECS && c.compact && !*c.wide;
+#pragma unroll
+  for (int j = 0; j < RPT; j++) {
+    if (dm >> j & 1) continue;
+    int t = g[j] == w[j] ? (int)s[j] : dk_slot(K, M, w[j], s[j]);
+    if (t < 0) return false;
+    dt_add(K, t, vtype, v[j]);
+  }
+  return true;
+}
+
+#ifndef FW_DT_TIMING
+#define FW_DT_TIMING 0  // 1: per-phase clocks of the compact launch, printed by its last workgroup (diagnostics)
+#endif
+__device__ unsigned long long g_dtt[6];
+// One attempt at a region: 2^hb passes over the (key, window)s by hash prefix; each clears the table, loads the
+// region's entries of the pass, adds the records of the pass and writes the pass's groups densely into dst
+// behind the earlier passes' (M.out).  KW: the compact table (every record is a CRec; an entry or record without a
+// compact word makes the attempt DT_WIDE).  DT_OVER: some pass did not fit the table.
+template <int SRC, bool KW>
+__device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, int32_t p, const Entry* __restrict__ src,
+                                          int32_t live, Entry* __restrict__ dst, int64_t R, const void* __restrict__ in,
+                                          int64_t begin, int64_t end, bool cmp, int hb) {
+  constexpr int NS = KW ? DK_SLOTS : FW_DT_SLOTS;
   const PRec* __restrict__ part = reinterpret_cast<const PRec*>(in);
   const PartialRec* __restrict__ pin = reinterpret_cast<const PartialRec*>(in);
   const int lane = __lane_id();
-  int hb = tb.passes[p];
-  bool lost = false;
-  for (;;) {  // an attempt with 2^hb passes
-    if (threadIdx.x == 0) {
-      out_s = 0;
-      L.ntmin = LMAX;
-      L.capover = 0;
-    }
-    bool overflow = false;
-    for (int k = 0; k < (1 << hb) && !overflow; k++) {
-      for (int h = threadIdx.x; h < FW_DT_SLOTS; h += FW_DT_THREADS) L.tag[h] = LT_EMPTY;
-      if (threadIdx.x == 0) {
-        L.fill = 0;
-        L.over = 0;
-        L.nout = 0;
+  if (threadIdx.x == 0) {
+    M.out = 0;
+    M.ntmin = LMAX;
+    M.capover = 0;
+    M.widefb = 0;
+  }
+  for (int k = 0; k < (1 << hb); k++) {
+    if constexpr (KW) {
+      for (int h = threadIdx.x; h < DK_SLOTS; h += FW_DT_THREADS) {
+        U.k.kw[h] = DK_EMPTY;
+        U.k.cnt[h] = 0;
+        U.k.sum[h] = 0;
+        U.k.mn[h] = LMAX;
+        U.k.mx[h] = LMIN;
       }
-      __syncthreads();
-      // the region's entries of pass k (two per thread in flight)
-      for (int32_t i0 = 0; i0 < live; i0 += 2 * FW_DT_THREADS) {
-        Entry e[2];
+    } else {
+      for (int h = threadIdx.x; h < FW_DT_SLOTS; h += FW_DT_THREADS) U.w.tag[h] = LT_EMPTY;
+    }
+    if (threadIdx.x == 0) {
+      M.fill = 0;
+      M.over = 0;
+      M.nout = 0;
+    }
+    const unsigned long long ta = FW_DT_TIMING ? __builtin_amdgcn_s_memtime() : 0;
+    __syncthreads();
+    // the region's entries of pass k (two per thread in flight)
+    for (int32_t i0 = 0; i0 < live; i0 += 2 * FW_DT_THREADS) {
+      Entry e[2];
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
-          const int32_t i = i0 + u * FW_DT_THREADS + (int32_t)threadIdx.x;
-          if (i < live) e[u] = src[i];
-        }
+      for (int u = 0; u < 2; u++) {
+        const int32_t i = i0 + u * FW_DT_THREADS + (int32_t)threadIdx.x;
+        if (i < live) e[u] = src[i];
+      }
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
-          const int32_t i = i0 + u * FW_DT_THREADS + (int32_t)threadIdx.x;
-          if (i >= live || (hb && dt_pass(c, e[u].key, e[u].start, hb) != k)) continue;
-          const int s = dt_slot(L, e[u].key, e[u].start, lds_hash(e[u].key, e[u].start));
-          if (s < 0) {
-            L.over = 1;
+      for (int u = 0; u < 2; u++) {
+        const int32_t i = i0 + u * FW_DT_THREADS + (int32_t)threadIdx.x;
+        if (i >= live || (hb && dt_pass(c, e[u].key, e[u].start, hb) != k)) continue;
+        int s;
+        if constexpr (KW) {
+          const int64_t d = compact_delta(c, e[u].start);
+          const unsigned long long w = d < 0 ? DK_EMPTY : (unsigned long long)compact_encode(c, e[u].key, d);
+          if (w == DK_EMPTY) {
+            M.widefb = 1;
             break;
           }
-          dt_merge(L, s, c.vtype, e[u].cnt, e[u].sum, e[u].mn, e[u].mx);
+          s = dk_slot(U.k, M, w, dk_home(w));
+          if (s < 0) {
+            M.over = 1;
+            break;
+          }
+          dt_merge(U.k, s, c.vtype, e[u].cnt, e[u].sum, e[u].mn, e[u].mx);
+        } else {
+          s = dt_slot(U.w, M, e[u].key, e[u].start, lds_hash(e[u].key, e[u].start));
+          if (s < 0) {
+            M.over = 1;
+            break;
+          }
+          dt_merge(U.w, s, c.vtype, e[u].cnt, e[u].sum, e[u].mn, e[u].mx);
         }
       }
-      __syncthreads();
-      if (!L.over) {
-        if constexpr (SRC == DT_RECS) {
-          // the batch's records, the next round's in flight while the current ones are added
-          constexpr int RPT = FW_DT_RPT;
-          constexpr int64_t RS = (int64_t)FW_DT_THREADS * RPT;
-          i64x2 ca[RPT], cb[RPT];
+    }
+    __syncthreads();
+    const unsigned long long tb1 = FW_DT_TIMING ? __builtin_amdgcn_s_memtime() : 0;
+    if (M.widefb) return DT_WIDE;
+    if (!M.over) {
+      if constexpr (SRC == DT_RECS) {
+        // the batch's records, the next round's in flight while the current ones are added
+        constexpr int RPT = FW_DT_RPT;
+        constexpr int64_t RS = (int64_t)FW_DT_THREADS * RPT;
+        i64x2 ca[RPT], cb[RPT];
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+          const int64_t i = begin + (int64_t)j * FW_DT_THREADS + threadIdx.x;
+          load_prec_raw(KW || cmp, part, i, i < end, ca[j], cb[j]);
+        }
+        for (int64_t rb = begin; rb < end; rb += RS) {
+          if (__hip_atomic_load(&M.over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+          i64x2 na[RPT], nb[RPT];
 #pragma unroll
           for (int j = 0; j < RPT; j++) {
-            const int64_t i = begin + (int64_t)j * FW_DT_THREADS + threadIdx.x;
-            load_prec_raw(cmp, part, i, i < end, ca[j], cb[j]);
+            const int64_t i = rb + RS + (int64_t)j * FW_DT_THREADS + threadIdx.x;
+            load_prec_raw(KW || cmp, part, i, i < end, na[j], nb[j]);
           }
-          for (int64_t rb = begin; rb < end; rb += RS) {
-            if (__hip_atomic_load(&L.over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-            i64x2 na[RPT], nb[RPT];
+          uint32_t dm = 0;
+          bool ok;
+          if constexpr (KW) {
+            unsigned long long ww[RPT];
+            int64_t vv[RPT];
 #pragma unroll
             for (int j = 0; j < RPT; j++) {
-              const int64_t i = rb + RS + (int64_t)j * FW_DT_THREADS + threadIdx.x;
-              load_prec_raw(cmp, part, i, i < end, na[j], nb[j]);
+              ww[j] = (unsigned long long)ca[j].x;
+              vv[j] = ca[j].y;
+              const int64_t i = rb + (int64_t)j * FW_DT_THREADS + threadIdx.x;
+              if (i >= end) {
+                dm |= 1u << j;
+                continue;
+              }
+              if (ww[j] == DK_EMPTY) M.widefb = 1;
+              if (hb) {
+                int64_t kk, tt;
+                compact_decode(c, p, ca[j].x, &kk, &tt);
+                if (dt_pass(c, kk, tt, hb) != k) dm |= 1u << j;
+              }
             }
+            if (M.widefb) break;
+            ok = dk_add_batch<RPT>(U.k, M, c.vtype, ww, vv, dm);
+          } else {
             int64_t kk[RPT], tt[RPT], vv[RPT];
-            uint32_t dm = 0;
 #pragma unroll
             for (int j = 0; j < RPT; j++) {
               int64_t o;
@@ -4512,106 +4736,175 @@ __global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const 
               const int64_t i = rb + (int64_t)j * FW_DT_THREADS + threadIdx.x;
               if (i >= end || (hb && dt_pass(c, kk[j], tt[j], hb) != k)) dm |= 1u << j;
             }
-            if (!dt_add_batch<RPT>(L, c.vtype, kk, tt, vv, dm)) {
-              L.over = 1;
-              break;
-            }
-#pragma unroll
-            for (int j = 0; j < RPT; j++) {
-              ca[j] = na[j];
-              cb[j] = nb[j];
-            }
+            ok = dt_add_batch<RPT>(U.w, M, c.vtype, kk, tt, vv, dm);
           }
-        } else {
-          for (int64_t i0 = begin; i0 < end; i0 += 2 * FW_DT_THREADS) {
-            if (__hip_atomic_load(&L.over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-            PartialRec d[2];
+          if (!ok) {
+            M.over = 1;
+            break;
+          }
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
-              const int64_t i = i0 + u * FW_DT_THREADS + threadIdx.x;
-              if (i < end) d[u] = pin[i];
-            }
-            bool full = false;
+          for (int j = 0; j < RPT; j++) {
+            ca[j] = na[j];
+            cb[j] = nb[j];
+          }
+        }
+      } else {
+        for (int64_t i0 = begin; i0 < end; i0 += 2 * FW_DT_THREADS) {
+          if (__hip_atomic_load(&M.over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+          PartialRec d[2];
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
-              const int64_t i = i0 + u * FW_DT_THREADS + threadIdx.x;
-              if (full || i >= end || (hb && dt_pass(c, d[u].key, d[u].start, hb) != k)) continue;
-              const int s = dt_slot(L, d[u].key, d[u].start, lds_hash(d[u].key, d[u].start));
-              if (s < 0) {
-                full = true;
-                continue;
-              }
-              dt_merge(L, s, c.vtype, d[u].cnt, d[u].sum, d[u].mn, d[u].mx);
+          for (int u = 0; u < 2; u++) {
+            const int64_t i = i0 + u * FW_DT_THREADS + threadIdx.x;
+            if (i < end) d[u] = pin[i];
+          }
+          bool full = false;
+#pragma unroll
+          for (int u = 0; u < 2; u++) {
+            const int64_t i = i0 + u * FW_DT_THREADS + threadIdx.x;
+            if (full || i >= end || (hb && dt_pass(c, d[u].key, d[u].start, hb) != k)) continue;
+            const int s = dt_slot(U.w, M, d[u].key, d[u].start, lds_hash(d[u].key, d[u].start));
+            if (s < 0) {
+              full = true;
+              continue;
             }
-            if (full) {
-              L.over = 1;
-              break;
-            }
+            dt_merge(U.w, s, c.vtype, d[u].cnt, d[u].sum, d[u].mn, d[u].mx);
+          }
+          if (full) {
+            M.over = 1;
+            break;
           }
         }
       }
-      __syncthreads();
-      if (L.over) {
-        overflow = true;
-        break;
-      }
-      // the pass's groups, densely behind the earlier passes' (a wave reserves its lanes' positions at once)
-      const long long ob = out_s;
-      long long nt = LMAX;
-      for (int h0 = 0; h0 < FW_DT_SLOTS; h0 += FW_DT_THREADS) {
-        const int h = h0 + (int)threadIdx.x;
-        const bool g = h < FW_DT_SLOTS && L.tag[h] >= 2;
-        const uint64_t m = __ballot(g);
-        int wb = 0;
-        if (lane == 0 && m) wb = atomicAdd(&L.nout, __popcll(m));
-        wb = __shfl(wb, 0, 64);
-        if (g) {
-          const int64_t pos = ob + wb + __popcll(m & lanemask_lt());
-          const i64x2 kv = L.kv[h];
-          Entry e;
+    }
+    __syncthreads();
+    const unsigned long long tc = FW_DT_TIMING ? __builtin_amdgcn_s_memtime() : 0;
+    if (M.widefb) return DT_WIDE;
+    if (M.over) return DT_OVER;
+    // the pass's groups, densely behind the earlier passes' (a wave reserves its lanes' positions at once)
+    const long long ob = M.out;
+    long long nt = LMAX;
+    for (int h0 = 0; h0 < NS; h0 += FW_DT_THREADS) {
+      const int h = h0 + (int)threadIdx.x;
+      bool g;
+      if constexpr (KW)
+        g = h < NS && U.k.kw[h] != DK_EMPTY;
+      else
+        g = h < NS && U.w.tag[h] >= 2;
+      const uint64_t m = __ballot(g);
+      int wb = 0;
+      if (lane == 0 && m) wb = atomicAdd(&M.nout, __popcll(m));
+      wb = __shfl(wb, 0, 64);
+      if (g) {
+        const int64_t pos = ob + wb + __popcll(m & lanemask_lt());
+        Entry e;
+        if constexpr (KW) {
+          compact_decode(c, p, (int64_t)U.k.kw[h], &e.key, &e.start);
+          e.cnt = (int64_t)U.k.cnt[h];
+          e.sum = U.k.sum[h];
+          e.mn = U.k.mn[h];
+          e.mx = U.k.mx[h];
+        } else {
+          const i64x2 kv = U.w.kv[h];
           e.key = kv.x;
           e.start = kv.y;
-          e.end = jadd(kv.y, c.size);
-          e.cnt = (int64_t)L.cnt[h];
-          e.sum = L.sum[h];
-          e.mn = L.mn[h];
-          e.mx = L.mx[h];
-          e.meta = FW_TIMER;  // EventTimeTrigger's timer at maxTimestamp (= the GC timer with lateness 0)
-          if (pos < R)
-            dst[pos] = e;
-          else
-            L.capover = 1;
-          nt = min(nt, (long long)jsub(e.end, 1));
+          e.cnt = (int64_t)U.w.cnt[h];
+          e.sum = U.w.sum[h];
+          e.mn = U.w.mn[h];
+          e.mx = U.w.mx[h];
         }
+        e.end = jadd(e.start, c.size);
+        e.meta = FW_TIMER;  // EventTimeTrigger's timer at maxTimestamp (= the GC timer with lateness 0)
+        if (pos < R)
+          dst[pos] = e;
+        else
+          M.capover = 1;
+        nt = min(nt, (long long)jsub(e.end, 1));
       }
-      if (nt != LMAX) atomicMin(&L.ntmin, nt);
-      __syncthreads();
-      if (threadIdx.x == 0) out_s += L.nout;
-      __syncthreads();
     }
-    if (!overflow) break;
+    if (nt != LMAX) atomicMin(&M.ntmin, nt);
+    __syncthreads();
+    if (threadIdx.x == 0) M.out += M.nout;
+    if (FW_DT_TIMING && KW && threadIdx.x == 0) {
+      atomicAdd(&g_dtt[1], tb1 - ta);
+      atomicAdd(&g_dtt[2], tc - tb1);
+      atomicAdd(&g_dtt[3], __builtin_amdgcn_s_memtime() - tc);
+    }
+    __syncthreads();
+  }
+  return DT_OK;
+}
+
+// One workgroup per region.  SRC = DT_RECS: the batch's records (CRec / PRec runs of k_scatter); DT_PARTS: partial
+// accumulators (PartialRec runs of k_pscatter or of a restore).  KW: the compact table, for the regions of a compact
+// batch; a region it cannot take (an entry without a compact word) is left for the wide launch that follows it
+// (two kernels, so each keeps its own registers).  A region is committed (its buffer flipped) only when every group
+// was written.
+template <int SRC, bool KW>
+__global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const void* __restrict__ in,
+                                                                const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
+                                                                AggProg prog, int resume, Status* st) {
+  __shared__ DtTab U;
+  __shared__ DtMisc M;
+  const int32_t p = blockIdx.x;
+  if (p >= c.P || (resume && prog.done[p])) return;
+  const int64_t begin = offs[(int64_t)p * T], end = offs[(int64_t)(p + 1) * T];
+  if (begin == end) {  // nothing for this region: it stays as it is
+    if (threadIdx.x == 0) prog.done[p] = 1;
+    return;
+  }
+  const bool cmp = SRC == DT_RECS && c.compact && !*c.wide;
+  if (KW && (!cmp || (c.diag & DIAG_DT_WIDE))) {  // a batch without compact words: the wide launch takes it
+    if (threadIdx.x == 0) prog.done[p] = 0;
+    return;
+  }
+  const unsigned long long t0 = FW_DT_TIMING ? __builtin_amdgcn_s_memtime() : 0;
+  const int X = tb.cur[p], Y = X ^ 1;
+  const int64_t base = (int64_t)p << c.log_r, R = (int64_t)1 << c.log_r;
+  const Entry* __restrict__ src = tb.ent[X] + base;
+  Entry* __restrict__ dst = tb.ent[Y] + base;
+  const int32_t live = tb.live[p];
+  int hb = tb.passes[p];
+  bool lost = false, wide = false;
+  for (;;) {
+    const int r = dt_attempt<SRC, KW>(c, U, M, p, src, live, dst, R, in, begin, end, cmp, hb);
+    __syncthreads();
+    if (r == DT_OK) break;
+    if (r == DT_WIDE) {  // (KW only)
+      wide = true;
+      break;
+    }
     if (++hb > 24) {  // more groups with one hash prefix than 2^24 passes can split: cannot happen
       lost = true;
       break;
     }
-    __syncthreads();
   }
   if (threadIdx.x == 0) {
     tb.passes[p] = (uint8_t)min(hb, 24);
-    if (lost) {
+    if (wide) {
+      prog.done[p] = 0;
+    } else if (lost) {
       atomicOr(&st->flags, FW_STATUS_STATE_LOST);
       prog.done[p] = 1;
-    } else if (L.capover) {  // the region's buffers are too small: nothing committed, the host grows them and resumes
-      atomicMax(&st->need_live, (int)min(out_s, (long long)INT32_MAX));
+    } else if (M.capover) {  // the region's buffers are too small: nothing committed, the host grows them and resumes
+      atomicMax(&st->need_live, (int)min(M.out, (long long)INT32_MAX));
       prog.done[p] = 0;
       atomicOr(&st->suspended, (int)FW_SUSP_AGG);
     } else {
       tb.cur[p] = (uint8_t)Y;
-      tb.live[p] = (int32_t)out_s;
-      tb.next_timer[p] = L.ntmin;
+      tb.live[p] = (int32_t)M.out;
+      tb.next_timer[p] = M.ntmin;
       prog.done[p] = 1;
-      atomicAdd(&st->merged, (unsigned long long)out_s);
-      if (out_s > (3 * R) / 4) st->need_grow = 1;
+      atomicAdd(&st->merged, (unsigned long long)M.out);
+      if (M.out > (3 * R) / 4) st->need_grow = 1;
+    }
+    if (FW_DT_TIMING && KW) {
+      atomicAdd(&g_dtt[0], __builtin_amdgcn_s_memtime() - t0);
+      if (atomicAdd(&g_dtt[5], 1ull) == (unsigned long long)gridDim.x - 1) {
+        const double nb = (double)gridDim.x;
+        printf("dt timing per WG: total %.0f clear+load %.0f records %.0f writeback %.0f clocks\n", g_dtt[0] / nb,
+               g_dtt[1] / nb, g_dtt[2] / nb, g_dtt[3] / nb);
+        for (int i = 0; i < 6; i++) g_dtt[i] = 0;
+      }
     }
   }
 }
@@ -4903,6 +5196,35 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
                     int64_t* sv, int32_t* skh, DevSide side, Status* st, hipStream_t s) {
   const size_t lds = (size_t)c.P * sizeof(uint32_t);
   const uint32_t* o = offs;
+  static const bool no_staged = getenv("FW_NO_STAGED") && atoi(getenv("FW_NO_STAGED"));
+  if (c.compact && c.P <= FW_GMAX_P && stream_mode(c) != M_GEN && !no_staged) {
+    // staged: rounds of 8192 records up to 1024 partitions, 4096 up to 2048 (the LDS)
+    const bool big = c.P <= 1024;
+    const int rr = big ? 8192 : 4096;
+    const size_t sl = (size_t)rr * (sizeof(i64x2) + sizeof(uint16_t)) + (2 * (size_t)c.P + 1) * sizeof(uint32_t) +
+                      (FW_TILE_THREADS / 64 + 1) * sizeof(uint32_t);
+    static bool attr = false;
+    if (!attr) {  // LDS beyond 64 KB
+      (void)hipFuncSetAttribute((const void*)k_scatter_staged<M_TUMB, 8192>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_scatter_staged<M_TUMB, 4096>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_scatter_staged<M_PANE, 8192>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_scatter_staged<M_PANE, 4096>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    const bool tumb = stream_mode(c) == M_TUMB;
+    if (tumb && big)
+      hipLaunchKernelGGL((k_scatter_staged<M_TUMB, 8192>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n,
+                         T, o, part, side, st);
+    else if (tumb)
+      hipLaunchKernelGGL((k_scatter_staged<M_TUMB, 4096>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n,
+                         T, o, part, side, st);
+    else if (big)
+      hipLaunchKernelGGL((k_scatter_staged<M_PANE, 8192>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n,
+                         T, o, part, side, st);
+    else
+      hipLaunchKernelGGL((k_scatter_staged<M_PANE, 4096>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n,
+                         T, o, part, side, st);
+  } else
   switch (stream_mode(c)) {
     case M_TUMB:
       hipLaunchKernelGGL(k_scatter<M_TUMB>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, val, kh, n, T, o, part,
@@ -4946,9 +5268,11 @@ void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint
       launch_scan(h.chunk_base, (int64_t)c.P + 1, h.scan_tmp, s);
     }
   }
-  if (c.dense) {
-    hipLaunchKernelGGL(k_dt_aggregate<DT_RECS>, dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs, T, tb,
-                       prog, resume, st);
+  if (c.dense) {  // the compact table first; the wide launch takes the regions it left
+    hipLaunchKernelGGL((k_dt_aggregate<DT_RECS, true>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs,
+                       T, tb, prog, resume, st);
+    hipLaunchKernelGGL((k_dt_aggregate<DT_RECS, false>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs,
+                       T, tb, prog, 1, st);
     return;
   }
   const dim3 b(FW_AGG_THREADS);
@@ -5164,8 +5488,8 @@ void launch_pscatter(const DevCfg& c, int64_t wm, PartialCols in, int64_t n, int
 void launch_pmerge(const DevCfg& c, const PartialRec* part, const uint32_t* offs, int32_t T, DevTable tb, AggProg prog,
                    int resume, Status* st, hipStream_t s) {
   if (c.dense)
-    hipLaunchKernelGGL(k_dt_aggregate<DT_PARTS>, dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs, T, tb,
-                       prog, resume, st);
+    hipLaunchKernelGGL((k_dt_aggregate<DT_PARTS, false>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs,
+                       T, tb, prog, resume, st);
   else
     hipLaunchKernelGGL(k_pmerge, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, part, offs, T, tb, prog, resume, st);
 }

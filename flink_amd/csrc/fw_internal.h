@@ -176,7 +176,8 @@ enum {
   DIAG_SCATTER_SINGLE = 128, // k_scatter: each lane stores its own record (no lane-pair sectors)
   DIAG_AGG_TIMING = 256,     // k_aggregate prints per-workgroup phase clocks (builds with FW_AGG_TIMING_BUILD=1)
   DIAG_SCATTER_HALF = 512,   // k_scatter stores 16 B per record (the timing of a compact record)
-  DIAG_SCATTER_NT = 1024     // k_scatter stores with nontemporal stores
+  DIAG_SCATTER_NT = 1024,    // k_scatter stores with nontemporal stores
+  DIAG_DT_WIDE = 2048        // k_dt_aggregate: the wide LDS table for every region (timing of the compact table)
 };
 
 struct __attribute__((aligned(64))) Entry {
