@@ -1978,70 +1978,95 @@ __device__ __forceinline__ void unpack_prec(const DevCfg& c, bool cmp, int32_t p
   o = FIRST ? c.ord_base + (int64_t)((uint64_t)b.y >> 16) : 0;
 }
 
+// LM: the run's record form, 0 = PRec, 1 = CRec, 2 = gathered CRec (GatherRuns).  Two register sets alternate
+// without copies (copying the set in flight would wait for its loads), and the loads are branch-free, from an index
+// clamped into the run (a load under a branch is waited for at once).
+template <int RPT, bool SESS, bool FIRST, int LM>
+__device__ __forceinline__ void agg_walk_lm(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __restrict__ part,
+                                            int32_t p, int64_t end, int64_t RS, int64_t& myrb, uint32_t& dm,
+                                            const GatherRuns* g) {
+  if (myrb >= end) return;
+  auto load = [&](i64x2 (&a)[RPT], i64x2 (&b)[RPT], int64_t r0) {
+#pragma unroll
+    for (int j = 0; j < RPT; j++) {
+      const int64_t i = r0 + (int64_t)j * blockDim.x + threadIdx.x;
+      if constexpr (LM == 2) {
+        load_prec_raw(true, part, i, i < end, a[j], b[j], g);
+      } else {
+        const int64_t ic = i < end ? i : end - 1;
+        if constexpr (LM == 1) {
+          a[j] = reinterpret_cast<const i64x2*>(part)[ic];
+          b[j] = i64x2{0, 0};
+        } else {
+          const i64x2* src = reinterpret_cast<const i64x2*>(part + ic);
+          a[j] = src[0];
+          b[j] = src[1];
+        }
+      }
+    }
+  };
+  // one round's records into the LDS table; false (dm = the round's done mask, L.anyfail set) when it is full
+  auto round = [&](const i64x2 (&ca)[RPT], const i64x2 (&cb)[RPT], int64_t r0) -> bool {
+    int64_t k[RPT], t[RPT], v[RPT], o[RPT];
+    int nw[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; j++) unpack_prec<FIRST>(c, LM != 0, p, ca[j], cb[j], k[j], t[j], v[j], nw[j], o[j]);
+    uint32_t m = dm;
+#pragma unroll
+    for (int j = 0; j < RPT; j++)
+      if (r0 + (int64_t)j * blockDim.x + threadIdx.x >= end) m |= 1u << j;
+    bool up = true;
+    if (c.diag & DIAG_AGG_NO_LDS) {
+#pragma unroll
+      for (int j = 0; j < RPT; j++) asm volatile("" ::"v"(k[j]), "v"(t[j]), "v"(v[j]), "v"(o[j]));
+    } else if constexpr (SESS) {
+#pragma unroll
+      for (int j = 0; j < RPT; j++) {
+        if (!up || (m >> j & 1)) continue;
+        if (lds_session_upsert(L, E, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j], o[j], FIRST ? c.agg : 0))
+          m |= 1u << j;
+        else
+          up = false;
+      }
+    } else {
+      up = lds_upsert_batch<RPT>(L, c.vtype, k, t, v, o, FIRST ? c.agg : 0, m);
+    }
+    if (!up) {
+      dm = m;
+      __hip_atomic_store(&L.anyfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return up;
+  };
+  i64x2 ca[RPT], cb[RPT], na[RPT], nb[RPT];
+  load(ca, cb, myrb);
+  for (;;) {
+    load(na, nb, myrb + RS);
+    if (!round(ca, cb, myrb)) break;
+    dm = 0;
+    myrb += RS;
+    if (myrb >= end) break;
+    load(ca, cb, myrb + RS);
+    if (!round(na, nb, myrb)) break;
+    dm = 0;
+    myrb += RS;
+    if (myrb >= end) break;
+  }
+}
 // The free-running record walk of a one-window (or session) partition run [.., end): this thread's rounds from
 // myrb on (dm: the done mask of its first round), with the next round's records in flight while the current
-// ones are upserted, until its rounds are done or some lane of the workgroup found the LDS table full
-// (L.anyfail; the failing lane's round and mask stay in myrb / dm).  The caller meets the other waves at a
-// barrier, flushes or spills the table when L.anyfail is set, and calls again.
+// ones are upserted, until its rounds are done or its upsert found the LDS table full (L.anyfail; the failing
+// round and mask stay in myrb / dm; the other waves go on until they finish or fail too).  The caller meets the
+// other waves at a barrier, flushes or spills the table when L.anyfail is set, and calls again.
 template <int RPT, bool SESS, bool FIRST>
 __device__ __forceinline__ void agg_walk(const DevCfg& c, AggLds& L, int64_t* E, const PRec* __restrict__ part, bool cmp,
                                          int32_t p, int64_t end, int64_t RS, int64_t& myrb, uint32_t& dm,
                                          const GatherRuns* g) {
-  if (myrb < end) {
-    i64x2 ca[RPT], cb[RPT];
-#pragma unroll
-    for (int j = 0; j < RPT; j++) {
-      const int64_t i = myrb + (int64_t)j * blockDim.x + threadIdx.x;
-      load_prec_raw(cmp, part, i, i < end, ca[j], cb[j], g);
-    }
-    for (;;) {
-      if (__hip_atomic_load(&L.anyfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-      const int64_t nrb = myrb + RS;
-      i64x2 na[RPT], nb[RPT];
-#pragma unroll
-      for (int j = 0; j < RPT; j++) {
-        const int64_t i = nrb + (int64_t)j * blockDim.x + threadIdx.x;
-        load_prec_raw(cmp, part, i, i < end, na[j], nb[j], g);
-      }
-      int64_t k[RPT], t[RPT], v[RPT], o[RPT];
-      int nw[RPT];
-#pragma unroll
-      for (int j = 0; j < RPT; j++) unpack_prec<FIRST>(c, cmp, p, ca[j], cb[j], k[j], t[j], v[j], nw[j], o[j]);
-      uint32_t m = dm;
-#pragma unroll
-      for (int j = 0; j < RPT; j++)
-        if (myrb + (int64_t)j * blockDim.x + threadIdx.x >= end) m |= 1u << j;
-      bool up = true;
-      if (c.diag & DIAG_AGG_NO_LDS) {
-#pragma unroll
-        for (int j = 0; j < RPT; j++) asm volatile("" ::"v"(k[j]), "v"(t[j]), "v"(v[j]), "v"(o[j]));
-      } else if constexpr (SESS) {
-#pragma unroll
-        for (int j = 0; j < RPT; j++) {
-          if (!up || (m >> j & 1)) continue;
-          if (lds_session_upsert(L, E, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j], o[j], FIRST ? c.agg : 0))
-            m |= 1u << j;
-          else
-            up = false;
-        }
-      } else {
-        up = lds_upsert_batch<RPT>(L, c.vtype, k, t, v, o, FIRST ? c.agg : 0, m);
-      }
-      if (!up) {
-        dm = m;
-        __hip_atomic_store(&L.anyfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        break;
-      }
-      dm = 0;
-      myrb = nrb;
-      if (myrb >= end) break;
-#pragma unroll
-      for (int j = 0; j < RPT; j++) {
-        ca[j] = na[j];
-        cb[j] = nb[j];
-      }
-    }
-  }
+  if (g)
+    agg_walk_lm<RPT, SESS, FIRST, 2>(c, L, E, part, p, end, RS, myrb, dm, g);
+  else if (cmp)
+    agg_walk_lm<RPT, SESS, FIRST, 1>(c, L, E, part, p, end, RS, myrb, dm, g);
+  else
+    agg_walk_lm<RPT, SESS, FIRST, 0>(c, L, E, part, p, end, RS, myrb, dm, g);
 }
 
 template <int RPT, bool SESS, bool FIRST>
@@ -4589,17 +4614,30 @@ __device__ __forceinline__ bool dk_add_batch(DtLdsK& K, DtMisc& M, int vtype, co
                                              const int64_t (&v)[RPT], uint32_t dm) {
   uint32_t s[RPT];
   unsigned long long g[RPT];
+  // every home slot read before any is used (plain reads: a word, once claimed, never changes, and a stale EMPTY
+  // only sends the element to dk_slot, which re-reads)
 #pragma unroll
   for (int j = 0; j < RPT; j++) {
     s[j] = dk_home(w[j]);
-    if (!(dm >> j & 1)) g[j] = __hip_atomic_load(&K.kw[s[j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    g[j] = K.kw[s[j]];
   }
+  uint32_t miss = 0;
 #pragma unroll
   for (int j = 0; j < RPT; j++) {
     if (dm >> j & 1) continue;
-    int t = g[j] == w[j] ? (int)s[j] : dk_slot(K, M, w[j], s[j]);
-    if (t < 0) return false;
-    dt_add(K, t, vtype, v[j]);
+    if (g[j] == w[j])
+      dt_add(K, (int)s[j], vtype, v[j]);
+    else
+      miss |= 1u << j;
+  }
+  if (miss) {
+#pragma unroll
+    for (int j = 0; j < RPT; j++) {
+      if (!(miss >> j & 1)) continue;
+      const int t = dk_slot(K, M, w[j], s[j]);
+      if (t < 0) return false;
+      dt_add(K, t, vtype, v[j]);
+    }
   }
   return true;
 }
@@ -4689,44 +4727,72 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
         // the batch's records, the next round's in flight while the current ones are added
         constexpr int RPT = FW_DT_RPT;
         constexpr int64_t RS = (int64_t)FW_DT_THREADS * RPT;
-        i64x2 ca[RPT], cb[RPT];
-#pragma unroll
-        for (int j = 0; j < RPT; j++) {
-          const int64_t i = begin + (int64_t)j * FW_DT_THREADS + threadIdx.x;
-          load_prec_raw(KW || cmp, part, i, i < end, ca[j], cb[j]);
-        }
-        for (int64_t rb = begin; rb < end; rb += RS) {
-          if (__hip_atomic_load(&M.over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-          i64x2 na[RPT], nb[RPT];
-#pragma unroll
-          for (int j = 0; j < RPT; j++) {
-            const int64_t i = rb + RS + (int64_t)j * FW_DT_THREADS + threadIdx.x;
-            load_prec_raw(KW || cmp, part, i, i < end, na[j], nb[j]);
-          }
-          uint32_t dm = 0;
-          bool ok;
-          if constexpr (KW) {
-            unsigned long long ww[RPT];
-            int64_t vv[RPT];
+        // (compact records: branch-free loads from an index clamped into the run, so the next round's stay in flight
+        // while the current one is added -- a load under a branch is waited for at once)
+        if constexpr (KW) {
+          // two register sets, alternating without copies (a copy of the set in flight would wait for it): round r
+          // is added while round r + 1 loads; compact records, branch-free loads from an index clamped into the run
+          const i64x2* __restrict__ crec = reinterpret_cast<const i64x2*>(in);
+          auto load = [&](i64x2 (&d)[RPT], int64_t r0) {
 #pragma unroll
             for (int j = 0; j < RPT; j++) {
-              ww[j] = (unsigned long long)ca[j].x;
-              vv[j] = ca[j].y;
-              const int64_t i = rb + (int64_t)j * FW_DT_THREADS + threadIdx.x;
+              const int64_t i = r0 + (int64_t)j * FW_DT_THREADS + threadIdx.x;
+              d[j] = crec[i < end ? i : end - 1];
+            }
+          };
+          auto add_round = [&](const i64x2 (&cur)[RPT], int64_t r0) -> int {  // 0 done, 1 table full, 2 EMPTY word
+            unsigned long long ww[RPT];
+            int64_t vv[RPT];
+            uint32_t dm = 0;
+            bool bad = false;
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+              ww[j] = (unsigned long long)cur[j].x;
+              vv[j] = cur[j].y;
+              const int64_t i = r0 + (int64_t)j * FW_DT_THREADS + threadIdx.x;
               if (i >= end) {
                 dm |= 1u << j;
                 continue;
               }
-              if (ww[j] == DK_EMPTY) M.widefb = 1;
+              bad |= ww[j] == DK_EMPTY;
               if (hb) {
                 int64_t kk, tt;
-                compact_decode(c, p, ca[j].x, &kk, &tt);
+                compact_decode(c, p, cur[j].x, &kk, &tt);
                 if (dt_pass(c, kk, tt, hb) != k) dm |= 1u << j;
               }
             }
-            if (M.widefb) break;
-            ok = dk_add_batch<RPT>(U.k, M, c.vtype, ww, vv, dm);
-          } else {
+            if (bad) return 2;
+            return dk_add_batch<RPT>(U.k, M, c.vtype, ww, vv, dm) ? 0 : 1;
+          };
+          i64x2 ra[RPT], rn[RPT];
+          load(ra, begin);
+          int res = 0;
+          for (int64_t r0 = begin; r0 < end; r0 += 2 * RS) {
+            load(rn, r0 + RS);
+            if ((res = add_round(ra, r0))) break;
+            if (r0 + RS >= end) break;
+            load(ra, r0 + 2 * RS);
+            if ((res = add_round(rn, r0 + RS))) break;
+          }
+          if (res == 2)  // a word equal to the EMPTY marker: the wide table takes the region
+            M.widefb = 1;
+          else if (res == 1)
+            M.over = 1;
+        } else {
+          i64x2 ca[RPT], cb[RPT];
+#pragma unroll
+          for (int j = 0; j < RPT; j++) {
+            const int64_t i = begin + (int64_t)j * FW_DT_THREADS + threadIdx.x;
+            load_prec_raw(cmp, part, i, i < end, ca[j], cb[j]);
+          }
+          for (int64_t rb = begin; rb < end; rb += RS) {
+            i64x2 na[RPT], nb[RPT];
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+              const int64_t i = rb + RS + (int64_t)j * FW_DT_THREADS + threadIdx.x;
+              load_prec_raw(cmp, part, i, i < end, na[j], nb[j]);
+            }
+            uint32_t dm = 0;
             int64_t kk[RPT], tt[RPT], vv[RPT];
 #pragma unroll
             for (int j = 0; j < RPT; j++) {
@@ -4736,16 +4802,15 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
               const int64_t i = rb + (int64_t)j * FW_DT_THREADS + threadIdx.x;
               if (i >= end || (hb && dt_pass(c, kk[j], tt[j], hb) != k)) dm |= 1u << j;
             }
-            ok = dt_add_batch<RPT>(U.w, M, c.vtype, kk, tt, vv, dm);
-          }
-          if (!ok) {
-            M.over = 1;
-            break;
-          }
+            if (!dt_add_batch<RPT>(U.w, M, c.vtype, kk, tt, vv, dm)) {
+              M.over = 1;
+              break;
+            }
 #pragma unroll
-          for (int j = 0; j < RPT; j++) {
-            ca[j] = na[j];
-            cb[j] = nb[j];
+            for (int j = 0; j < RPT; j++) {
+              ca[j] = na[j];
+              cb[j] = nb[j];
+            }
           }
         }
       } else {
