@@ -553,6 +553,9 @@ __host__ __forceinline__ int stream_mode(const DevCfg& c) {
   return c.panes ? M_PANE : M_GEN;
 }
 
+// single-pass scatter (k_scatter_staged<..., true>): its slots behind the P run lengths, rsv[P + x]
+enum { RSV_OVER = 0, RSV_KG = 1, RSV_TS = 2, RSV_LATE = 4 };  // RSV_LATE: 64-bit (FW_RSV_WORDS in all)
+
 // ---- K1: classify + partition histogram.  hist is (P+1) x T, partition-major; row P counts
 // the records of each tile that go to the ordered path (scanned with the partitions), row P+1
 // keeps that count unscanned for k_scatter_ordered.
@@ -560,8 +563,19 @@ template <int MODE>
 __global__ __launch_bounds__(FW_TILE_THREADS) void k_classify_hist(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
                                                                    const int64_t* __restrict__ ts,
                                                                    const int32_t* __restrict__ kh, int64_t n, int32_t T,
-                                                                   uint32_t* __restrict__ hist, Status* st) {
+                                                                   uint32_t* __restrict__ hist, Status* st,
+                                                                   const uint32_t* __restrict__ rsv) {
   specialize<MODE>(c);
+  if (rsv && !rsv[c.P + RSV_OVER]) {  // the single pass took the batch: its counts go to the status once
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      if (rsv[c.P + RSV_KG]) atomicAdd(&st->kg_errors, (int)rsv[c.P + RSV_KG]);
+      if (rsv[c.P + RSV_TS]) atomicAdd(&st->ts_errors, (int)rsv[c.P + RSV_TS]);
+      const unsigned long long late = *reinterpret_cast<const unsigned long long*>(rsv + c.P + RSV_LATE);
+      if (late) atomicAdd(&st->late_dropped, late);
+    }
+    return;
+  }
+  if (rsv && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st->rsv_fallbacks, 1);
   extern __shared__ uint32_t lh[];
   for (int i = threadIdx.x; i <= c.P; i += blockDim.x) lh[i] = 0;
   __syncthreads();
@@ -635,7 +649,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sw, ui
   return r;
 }
 
-__global__ __launch_bounds__(SCAN_T) void k_scan_blocks(uint32_t* data, int64_t m, uint32_t* sums) {
+// (gate: a flag the scan runs behind, nullptr = always)
+__global__ __launch_bounds__(SCAN_T) void k_scan_blocks(uint32_t* data, int64_t m, uint32_t* sums, const uint32_t* gate) {
+  if (gate && !*gate) return;
   __shared__ uint32_t sw[SCAN_T / 64 + 1];
   const int64_t base = (int64_t)blockIdx.x * SCAN_B + (int64_t)threadIdx.x * SCAN_E;
   uint32_t v[SCAN_E];
@@ -654,7 +670,8 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_blocks(uint32_t* data, int64_t 
   }
   if (threadIdx.x == 0) sums[blockIdx.x] = total;
 }
-__global__ __launch_bounds__(SCAN_T) void k_scan_top(uint32_t* sums, int64_t nb) {
+__global__ __launch_bounds__(SCAN_T) void k_scan_top(uint32_t* sums, int64_t nb, const uint32_t* gate) {
+  if (gate && !*gate) return;
   __shared__ uint32_t sw[SCAN_T / 64 + 1];
   uint32_t carry = 0;
   for (int64_t b0 = 0; b0 < nb; b0 += SCAN_T) {
@@ -665,7 +682,8 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_top(uint32_t* sums, int64_t nb)
     carry += total;
   }
 }
-__global__ __launch_bounds__(SCAN_T) void k_scan_add(uint32_t* data, int64_t m, const uint32_t* sums) {
+__global__ __launch_bounds__(SCAN_T) void k_scan_add(uint32_t* data, int64_t m, const uint32_t* sums, const uint32_t* gate) {
+  if (gate && !*gate) return;
   const uint32_t add = sums[blockIdx.x];
   const int64_t base = (int64_t)blockIdx.x * SCAN_B;
   for (int e = threadIdx.x; e < SCAN_B; e += SCAN_T)
@@ -795,14 +813,23 @@ __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(D
 // partition's piece is written as one contiguous run (consecutive lanes, consecutive addresses) behind the pieces of
 // the earlier rounds.  Same layout as k_scatter (partition-major runs at the scan offsets, any order inside a run).
 // A batch without compact records goes through k_scatter's body.
-template <int MODE, int RR>
+//
+// RSV (dense regions, single pass): no histogram and no scan before it.  Partition p's run is [p * rcap, p * rcap +
+// rsv[p]) and a round reserves its piece of every partition with one global atomic on rsv[p].  A record without a
+// compact form or a run longer than rcap sets rsv[P] (RSV_OVER): then the batch goes through classify, scan and the
+// offset scatter after all (those kernels are gated on rsv[P] and return at once without it).  The error and late
+// counts wait in rsv until the gated classify adds them to the status (RSV_* slots), so a redone batch counts once.
+template <int MODE, int RR, bool RSV = false>
 __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_staged(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
                                                                    const int64_t* __restrict__ ts,
                                                                    const int64_t* __restrict__ val,
                                                                    const int32_t* __restrict__ kh, int64_t n, int32_t T,
                                                                    const uint32_t* __restrict__ offs,
-                                                                   PRec* __restrict__ part, DevSide side, Status* st) {
+                                                                   PRec* __restrict__ part, DevSide side, Status* st,
+                                                                   const uint32_t* __restrict__ gate, uint32_t* rsv,
+                                                                   int64_t rcap) {
   specialize<MODE>(c);
+  if (!RSV && gate && !gate[0]) return;  // (the batch went through the single pass)
   extern __shared__ __attribute__((aligned(16))) uint8_t sraw[];
   i64x2* stg = reinterpret_cast<i64x2*>(sraw);          // RR: the round's records sorted by partition
   uint16_t* sp = reinterpret_cast<uint16_t*>(stg + RR);  // RR: their partitions
@@ -810,15 +837,18 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_staged(DevCfg c, in
   uint32_t* cs = gb + c.P;                               // P + 1: the round's counts, then their starts in stg
   uint32_t* wsum = cs + c.P + 1;                         // block scan
   const int32_t tile = tile_of_block(T);
-  const bool cmp = c.compact && !*c.wide;  // (uniform: every classify workgroup has finished)
-  if (!cmp) {
-    scatter_direct(c, wm, key, ts, val, kh, n, T, offs, part, side, st, gb, tile);
-    return;
+  if constexpr (!RSV) {
+    const bool cmp = c.compact && !*c.wide;  // (uniform: every classify workgroup has finished)
+    if (!cmp) {
+      scatter_direct(c, wm, key, ts, val, kh, n, T, offs, part, side, st, gb, tile);
+      return;
+    }
+    for (int i = threadIdx.x; i < c.P; i += FW_TILE_THREADS) gb[i] = offs[(int64_t)i * T + tile];
   }
-  for (int i = threadIdx.x; i < c.P; i += FW_TILE_THREADS) gb[i] = offs[(int64_t)i * T + tile];
   const int64_t tbase = (int64_t)tile * FW_TILE;
   const int64_t tend = min(n, tbase + (int64_t)FW_TILE);
   unsigned long long late = 0;
+  int bad_kg = 0, bad_ts = 0, over = 0;
   constexpr int RPT = RR / FW_TILE_THREADS;
   const int ppt = (c.P + FW_TILE_THREADS - 1) / FW_TILE_THREADS;
   i64x2* out = reinterpret_cast<i64x2*>(part);
@@ -845,19 +875,29 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_staged(DevCfg c, in
         if (i >= tend) continue;
         const int32_t h = c.key_kind == FW_KEY_HASHED ? hh[j] : key_hash_of(c.key_kind, k[j], kh, i);
         const int32_t p = partition_of(c, k[j], h);
-        if (p < 0) continue;
+        if (p < 0) {
+          bad_kg++;
+          continue;
+        }
         int64_t last = 0;
         int nwin = 0;
         const int cls = classify(c, wm, t[j], &last, &nwin, k[j], 0);
         if (cls == CLS_NORMAL) {
+          const int64_t d = compact_delta(c, last);
+          if (RSV && d < 0) {  // no compact form: the batch takes the offset path
+            over = 1;
+            continue;
+          }
           rk[jj] = atomicAdd(&cs[p], 1u);
           pj[jj] = (uint32_t)p;
-          w[jj] = compact_encode(c, k[j], compact_delta(c, last));
+          w[jj] = compact_encode(c, k[j], d);
         } else if (cls == CLS_LATE) {
-          if (c.side_output)
+          if (!RSV && c.side_output)
             side_one(side, st, k[j], t[j], vh[j]);
           else
             late++;
+        } else if (cls == CLS_BADTS) {
+          bad_ts++;
         }
       }
     }
@@ -887,16 +927,39 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_staged(DevCfg c, in
       stg[pos] = i64x2{w[j], v[j]};
       sp[pos] = (uint16_t)pj[j];
     }
+    if constexpr (RSV) {  // this round's piece of every partition it has records for
+      for (int i = threadIdx.x; i < c.P; i += FW_TILE_THREADS) {
+        const uint32_t m = cs[i + 1] - cs[i];
+        if (m == 0) continue;
+        const uint32_t g = atomicAdd(&rsv[i], m);
+        if ((int64_t)g + m > rcap) {
+          over = 1;
+          gb[i] = 0xffffffffu;
+        } else {
+          gb[i] = (uint32_t)((int64_t)i * rcap + g);
+        }
+      }
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < total; i += FW_TILE_THREADS) {
       const uint32_t pp = sp[i];
+      if (RSV && gb[pp] == 0xffffffffu) continue;
       out[gb[pp] + (i - cs[pp])] = stg[i];
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < c.P; i += FW_TILE_THREADS) gb[i] += cs[i + 1] - cs[i];
-    __syncthreads();
+    if constexpr (!RSV) {
+      for (int i = threadIdx.x; i < c.P; i += FW_TILE_THREADS) gb[i] += cs[i + 1] - cs[i];
+      __syncthreads();
+    }
   }
-  if (late) atomicAdd(&st->late_dropped, late);
+  if constexpr (RSV) {
+    if (over) rsv[c.P + RSV_OVER] = 1;
+    if (bad_kg) atomicAdd(&rsv[c.P + RSV_KG], (uint32_t)bad_kg);
+    if (bad_ts) atomicAdd(&rsv[c.P + RSV_TS], (uint32_t)bad_ts);
+    if (late) atomicAdd(reinterpret_cast<unsigned long long*>(rsv + c.P + RSV_LATE), late);
+  } else if (late) {
+    atomicAdd(&st->late_dropped, late);
+  }
 }
 
 // ---- K2b: ordered compaction of the ordered-path records of a tile (skipped by tiles that have none).
@@ -4907,12 +4970,16 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
 template <int SRC, bool KW>
 __global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const void* __restrict__ in,
                                                                 const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
-                                                                AggProg prog, int resume, Status* st) {
+                                                                AggProg prog, int resume, Status* st,
+                                                                const uint32_t* __restrict__ rsv, int64_t rcap) {
   __shared__ DtTab U;
   __shared__ DtMisc M;
   const int32_t p = blockIdx.x;
   if (p >= c.P || (resume && prog.done[p])) return;
-  const int64_t begin = offs[(int64_t)p * T], end = offs[(int64_t)(p + 1) * T];
+  // the partition's run: at the scan offsets, or where the single-pass scatter reserved it (launch_scatter_rsv)
+  const bool single = rsv && !rsv[c.P + RSV_OVER];
+  const int64_t begin = single ? (int64_t)p * rcap : (int64_t)offs[(int64_t)p * T];
+  const int64_t end = single ? begin + rsv[p] : (int64_t)offs[(int64_t)(p + 1) * T];
   if (begin == end) {  // nothing for this region: it stays as it is
     if (threadIdx.x == 0) prog.done[p] = 1;
     return;
@@ -5229,25 +5296,25 @@ namespace fwdev {
 static inline int32_t ntiles(int64_t n) { return (int32_t)((n + FW_TILE - 1) / FW_TILE); }
 
 void launch_classify_hist(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int32_t* kh,
-                          int64_t n, int32_t T, uint32_t* hist, Status* st, hipStream_t s) {
+                          int64_t n, int32_t T, uint32_t* hist, Status* st, hipStream_t s, const uint32_t* rsv) {
   const size_t lds = (c.P + 1) * sizeof(uint32_t);
   switch (stream_mode(c)) {
     case M_TUMB:
-      hipLaunchKernelGGL(k_classify_hist<M_TUMB>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, kh, n, T, hist, st);
+      hipLaunchKernelGGL(k_classify_hist<M_TUMB>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, kh, n, T, hist, st, rsv);
       break;
     case M_PANE:
-      hipLaunchKernelGGL(k_classify_hist<M_PANE>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, kh, n, T, hist, st);
+      hipLaunchKernelGGL(k_classify_hist<M_PANE>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, kh, n, T, hist, st, rsv);
       break;
     default:
-      hipLaunchKernelGGL(k_classify_hist<M_GEN>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, kh, n, T, hist, st);
+      hipLaunchKernelGGL(k_classify_hist<M_GEN>, dim3(T), dim3(FW_TILE_THREADS), lds, s, c, wm, key, ts, kh, n, T, hist, st, rsv);
   }
 }
 
-void launch_scan(uint32_t* data, int64_t m, uint32_t* scratch, hipStream_t s) {
+void launch_scan(uint32_t* data, int64_t m, uint32_t* scratch, hipStream_t s, const uint32_t* gate) {
   const int64_t nb = (m + SCAN_B - 1) / SCAN_B;
-  hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nb), dim3(SCAN_T), 0, s, data, m, scratch);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, scratch, nb);
-  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(SCAN_T), 0, s, data, m, (const uint32_t*)scratch);
+  hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nb), dim3(SCAN_T), 0, s, data, m, scratch, gate);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, scratch, nb, gate);
+  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(SCAN_T), 0, s, data, m, (const uint32_t*)scratch, gate);
 }
 
 void launch_taint(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, int64_t n, Status* st,
@@ -5258,11 +5325,11 @@ void launch_taint(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t
 
 void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
                     const int32_t* kh, int64_t n, int32_t T, uint32_t* offs, PRec* part, int64_t* sk, int64_t* stt,
-                    int64_t* sv, int32_t* skh, DevSide side, Status* st, hipStream_t s) {
+                    int64_t* sv, int32_t* skh, DevSide side, Status* st, hipStream_t s, const uint32_t* gate) {
   const size_t lds = (size_t)c.P * sizeof(uint32_t);
   const uint32_t* o = offs;
   static const bool no_staged = getenv("FW_NO_STAGED") && atoi(getenv("FW_NO_STAGED"));
-  if (c.compact && c.P <= FW_GMAX_P && stream_mode(c) != M_GEN && !no_staged) {
+  if (c.compact && c.P <= FW_GMAX_P && stream_mode(c) != M_GEN && (!no_staged || gate)) {
     // staged: rounds of 8192 records up to 1024 partitions, 4096 up to 2048 (the LDS)
     const bool big = c.P <= 1024;
     const int rr = big ? 8192 : 4096;
@@ -5279,16 +5346,16 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
     const bool tumb = stream_mode(c) == M_TUMB;
     if (tumb && big)
       hipLaunchKernelGGL((k_scatter_staged<M_TUMB, 8192>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n,
-                         T, o, part, side, st);
+                         T, o, part, side, st, gate, (uint32_t*)nullptr, (int64_t)0);
     else if (tumb)
       hipLaunchKernelGGL((k_scatter_staged<M_TUMB, 4096>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n,
-                         T, o, part, side, st);
+                         T, o, part, side, st, gate, (uint32_t*)nullptr, (int64_t)0);
     else if (big)
       hipLaunchKernelGGL((k_scatter_staged<M_PANE, 8192>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n,
-                         T, o, part, side, st);
+                         T, o, part, side, st, gate, (uint32_t*)nullptr, (int64_t)0);
     else
       hipLaunchKernelGGL((k_scatter_staged<M_PANE, 4096>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n,
-                         T, o, part, side, st);
+                         T, o, part, side, st, gate, (uint32_t*)nullptr, (int64_t)0);
   } else
   switch (stream_mode(c)) {
     case M_TUMB:
@@ -5308,6 +5375,31 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
                        (const uint32_t*)(offs + (int64_t)c.P * T), sk, stt, sv, skh, (const Status*)st);
 }
 
+bool rsv_eligible(const DevCfg& c) {
+  static const bool off = getenv("FW_NO_RSV") && atoi(getenv("FW_NO_RSV"));
+  return !off && c.dense && c.compact && !c.side_output && c.P <= FW_GMAX_P && stream_mode(c) == M_TUMB;
+}
+void launch_scatter_rsv(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
+                        const int32_t* kh, int64_t n, int32_t T, PRec* part, uint32_t* rsv, int64_t rcap, hipStream_t s) {
+  const bool big = c.P <= 1024;
+  const int rr = big ? 8192 : 4096;
+  const size_t sl = (size_t)rr * (sizeof(i64x2) + sizeof(uint16_t)) + (2 * (size_t)c.P + 1) * sizeof(uint32_t) +
+                    (FW_TILE_THREADS / 64 + 1) * sizeof(uint32_t);
+  static bool attr = false;
+  if (!attr) {  // LDS beyond 64 KB
+    (void)hipFuncSetAttribute((const void*)k_scatter_staged<M_TUMB, 8192, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_scatter_staged<M_TUMB, 4096, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const uint32_t* no = nullptr;
+  if (big)
+    hipLaunchKernelGGL((k_scatter_staged<M_TUMB, 8192, true>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val,
+                       kh, n, T, no, part, DevSide{}, (Status*)nullptr, no, rsv, rcap);
+  else
+    hipLaunchKernelGGL((k_scatter_staged<M_TUMB, 4096, true>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val,
+                       kh, n, T, no, part, DevSide{}, (Status*)nullptr, no, rsv, rcap);
+}
+
 // panes: maxTimestamp of the earliest window ending after wm (windows [s, s + size), s = offset mod slide)
 int64_t pane_nt_floor(const DevCfg& c, int64_t wm) {
   if (!c.panes) return 0;
@@ -5320,7 +5412,7 @@ int64_t pane_nt_floor(const DevCfg& c, int64_t wm) {
 
 void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
                       AggProg prog, int resume, const AggHot* hot, int64_t n, Status* st, hipStream_t s,
-                      const uint32_t* rt_t, int32_t t8) {
+                      const uint32_t* rt_t, int32_t t8, const uint32_t* rsv, int64_t rcap) {
   DevCfg c = c0;
   c.nt_floor = pane_nt_floor(c, wm);
   AggHot h{};
@@ -5335,9 +5427,9 @@ void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint
   }
   if (c.dense) {  // the compact table first; the wide launch takes the regions it left
     hipLaunchKernelGGL((k_dt_aggregate<DT_RECS, true>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs,
-                       T, tb, prog, resume, st);
+                       T, tb, prog, resume, st, rsv, rcap);
     hipLaunchKernelGGL((k_dt_aggregate<DT_RECS, false>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs,
-                       T, tb, prog, 1, st);
+                       T, tb, prog, 1, st, rsv, rcap);
     return;
   }
   const dim3 b(FW_AGG_THREADS);
@@ -5554,7 +5646,7 @@ void launch_pmerge(const DevCfg& c, const PartialRec* part, const uint32_t* offs
                    int resume, Status* st, hipStream_t s) {
   if (c.dense)
     hipLaunchKernelGGL((k_dt_aggregate<DT_PARTS, false>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs,
-                       T, tb, prog, resume, st);
+                       T, tb, prog, resume, st, (const uint32_t*)nullptr, (int64_t)0);
   else
     hipLaunchKernelGGL(k_pmerge, dim3(c.P), dim3(FW_AGG_THREADS), 0, s, c, part, offs, T, tb, prog, resume, st);
 }

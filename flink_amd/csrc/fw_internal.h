@@ -227,6 +227,7 @@ struct Status {
   int32_t suspended;                  // FW_SUSP_*: later kernels of the push / watermark skip themselves
   int32_t need_grow;                  // some region is over half full: grow before it has to suspend
   int32_t taint_any;                  // sessions: 0 no tainted key in the batch, 1 check the set, 2 set full: all
+  int32_t rsv_fallbacks;              // single-pass batches that had to go through classify / scan / scatter
 };
 enum {
   FW_STATUS_STATE_LOST = 1,  // a window could not be stored (more in-flight sessions of one key than supported)
@@ -358,17 +359,28 @@ struct PartialRec {
 typedef hipStream_t hipStream_t_;
 namespace fwdev {
 void launch_classify_hist(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int32_t* kh,
-                          int64_t n, int32_t T, uint32_t* hist, Status* st, hipStream_t_ s);
-void launch_scan(uint32_t* data, int64_t m, uint32_t* scratch, hipStream_t_ s);  // in-place exclusive
+                          int64_t n, int32_t T, uint32_t* hist, Status* st, hipStream_t_ s,
+                          const uint32_t* rsv = nullptr);
+// in-place exclusive; gate: the scan runs only when *gate != 0 (nullptr = always)
+void launch_scan(uint32_t* data, int64_t m, uint32_t* scratch, hipStream_t_ s, const uint32_t* gate = nullptr);
 void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
                     const int32_t* kh, int64_t n, int32_t T, uint32_t* offs, PRec* part, int64_t* sk,
-                    int64_t* stt, int64_t* sv, int32_t* skh, DevSide side, Status* st, hipStream_t_ s);
+                    int64_t* stt, int64_t* sv, int32_t* skh, DevSide side, Status* st, hipStream_t_ s,
+                    const uint32_t* gate = nullptr);
+// single-pass scatter of a dense compact batch (k_scatter_staged<..., true>): partition p's run at [p * rcap,
+// p * rcap + rsv[p]); rsv holds P + FW_RSV_WORDS words, zeroed before the launch.  When rsv[P] is set after it, the
+// batch goes through launch_classify_hist / launch_scan / launch_scatter gated on rsv (they do nothing otherwise).
+#define FW_RSV_WORDS 8
+bool rsv_eligible(const DevCfg& c);
+void launch_scatter_rsv(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
+                        const int32_t* kh, int64_t n, int32_t T, PRec* part, uint32_t* rsv, int64_t rcap, hipStream_t_ s);
 // hot: chunk splitting of long partitions (nullptr = one workgroup per partition); n = records of the push
 // gathered batches (FW_GTILE): offs = the partitions' virtual offsets (P + 1, T = 1), rt_t = the runs table
 // [P][T8] (tile-local start | count << 16), t8 = tiles of the batch; rt_t = nullptr for partition-major runs
 void launch_aggregate(const DevCfg& c, int64_t wm, const PRec* part, const uint32_t* offs, int32_t T, DevTable tb,
                       AggProg prog, int resume, const AggHot* hot, int64_t n, Status* st, hipStream_t_ s,
-                      const uint32_t* rt_t = nullptr, int32_t t8 = 0);
+                      const uint32_t* rt_t = nullptr, int32_t t8 = 0, const uint32_t* rsv = nullptr,
+                      int64_t rcap = 0);
 // gathered batches: classify + tile-local partition sort (k_stage, into the second half of part: mb = its
 // capacity in PRecs), the runs table's transpose and the partitions' virtual offsets (voffs, P + 1), the
 // ordered-path compaction (srow: scanned ordered-path counts per tile, then the raw counts; 2 x t8) and the

@@ -56,6 +56,9 @@ struct Scratch {
   // offsets (P + 1) and the ordered-path rows (2 x T8); T is then the batch's FW_GTILE tiles
   uint32_t *rt = nullptr, *rt_t = nullptr, *voffs = nullptr, *gsrow = nullptr, *gcb = nullptr;
   bool gather = false;
+  // dense batches: the single-pass scatter's run lengths and flags (fwdev::launch_scatter_rsv), P + FW_RSV_WORDS
+  uint32_t* rsv = nullptr;
+  bool single = false;  // the set's latest batch went through it (its runs are then at p * fw_op::rcap ...)
   // the ordered-path rows of the batch: scanned counts per tile, then raw counts
   const uint32_t* srow(int32_t P) const { return gather ? gsrow : hist + (int64_t)P * T; }
   // the partitions' runs in part: offsets offs()[p * offT()] (a gathered batch: regrouped, virtual offsets)
@@ -76,6 +79,10 @@ struct fw_op {
   hipStream_t bstream = nullptr;
   hipEvent_t ev_scat[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
   bool async_in = false;
+  int64_t rcap = 0;          // single-pass scatter: each partition's run capacity in compact records
+  int32_t rsv_seen = 0;      // Status::rsv_fallbacks at the latest settle
+  int32_t rsv_misses = 0;    // consecutive settles that saw a single-pass batch redone
+  bool rsv_off = false;      // after 3 of them the operator stops trying the single pass
   uint32_t *xoffs = nullptr, *xscan = nullptr;  // combining: the combiner's live-count offsets and scan scratch
   std::string err;
 
@@ -203,6 +210,7 @@ int alloc_scratch(fw_op* op, Scratch& s, int64_t mb, int64_t m) {
   HIP_OR_RETURN(op, dmalloc(&s.sv, mb));
   HIP_OR_RETURN(op, dmalloc(&s.skh, mb));
   HIP_OR_RETURN(op, dmalloc(&s.wide, 1));
+  if (op->dc.dense) HIP_OR_RETURN(op, dmalloc(&s.rsv, (size_t)op->dc.P + FW_RSV_WORDS));
   if (op->cfg.aggregate >= FW_AGG_FIRST && op->cfg.aggregate <= FW_AGG_FIRST_MAX) HIP_OR_RETURN(op, dmalloc(&s.so, mb));
   if (op->cfg.aggregate == FW_AGG_MINBY || op->cfg.aggregate == FW_AGG_MAXBY) HIP_OR_RETURN(op, dmalloc(&s.byv, mb));
   DevCfg probe = op->dc;
@@ -226,6 +234,7 @@ void free_scratch(Scratch& s) {
   dfree(s.sv);
   dfree(s.skh);
   dfree(s.wide);
+  dfree(s.rsv);
   dfree(s.pparts);
   dfree(s.so);
   dfree(s.byv);
@@ -489,7 +498,7 @@ int settle(fw_op* op) {
     if (susp & FW_SUSP_AGG)
       timed(op, K_AGGREGATE, [&] {
         fwdev::launch_aggregate(c, S.wm, S.part, S.offs(), S.offT(), op->tb, op->prog, 1, S.split ? &op->hot : nullptr,
-                                S.n, op->d_status, op->stream);
+                                S.n, op->d_status, op->stream, nullptr, 0, S.single ? S.rsv : nullptr, op->rcap);
         // the update skipped itself behind the suspension; register max is idempotent, so it reruns whole
         if (c.agg == FW_AGG_HLL)
           fwdev::launch_hll_update(c, S.part, S.offs(), S.offT(), S.n, op->tb, op->d_status, op->stream);
@@ -512,6 +521,12 @@ int settle(fw_op* op) {
     if ((rc = sync_status(op))) return rc;
   }
   op->unsynced = op->push_unsettled = op->fire_unsettled = false;
+  if (s.rsv_fallbacks != op->rsv_seen) {  // single-pass batches redone: a skewed stream stops trying after 3 in a row
+    op->rsv_seen = s.rsv_fallbacks;
+    if (++op->rsv_misses >= 3) op->rsv_off = true;
+  } else {
+    op->rsv_misses = 0;
+  }
   if (op->clear_deferred) {
     // rows the next push's scatter may have added since are side rows; side output never queues
     // early (push_device), so both counts are exactly those of the cleared sequence
@@ -617,6 +632,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
       c.cbase = (int64_t)base;
   }
   const bool gather = S.rt && fwdev::gather_mode(c, n);
+  const bool single = !gather && S.rsv && !op->rsv_off && op->rcap > 0 && fwdev::rsv_eligible(c);
   const int32_t T = gather ? (int32_t)((n + FW_GTILE - 1) / FW_GTILE) : (int32_t)((n + FW_TILE - 1) / FW_TILE);
   const int64_t m = (int64_t)(c.P + 1) * T;
   // async input: the batch-only kernels run on bstream, after the aggregate that last used this scratch set
@@ -640,22 +656,44 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
                           S.stt, S.sv, S.skh, op->side, op->d_status, op->stream);
     });
   } else {
-    timed(
-        op, K_CLASSIFY,
-        [&] {
-          if (c.assigner == FW_SESSION) fwdev::launch_taint(c, op->wm, key, ts, n, op->d_status, bs);
-          fwdev::launch_classify_hist(c, op->wm, key, ts, kh, n, T, S.hist, op->d_status, bs);
-        },
-        bs);
-    timed(op, K_SCAN, [&] { fwdev::launch_scan(S.hist, m, S.scan_tmp, bs); }, bs);
-    timed(
-        op, K_SCATTER,
-        [&] {
-          fwdev::launch_scatter(c, op->wm, key, ts, val, kh, n, T, S.hist, S.part, S.sk, S.stt, S.sv, S.skh, op->side,
-                                op->d_status, bs);
-        },
-        bs);
+    // dense compact batches: one pass reserves each partition's run piece by piece; the classify / scan /
+    // offset-scatter sequence behind it runs only when that pass could not take the batch (a record without a
+    // compact form, a run beyond rcap)
+    if (single) {
+      HIP_OR_RETURN(op, hipMemsetAsync(S.rsv, 0, ((size_t)c.P + FW_RSV_WORDS) * sizeof(uint32_t), bs));
+      timed(op, K_SCATTER, [&] { fwdev::launch_scatter_rsv(c, op->wm, key, ts, val, kh, n, T, S.part, S.rsv, op->rcap, bs); },
+            bs);
+    }
+    const uint32_t* gate = single ? S.rsv + c.P : nullptr;
+    if (single) {  // (fw_profile: the gated sequence counts as classify)
+      timed(
+          op, K_CLASSIFY,
+          [&] {
+            fwdev::launch_classify_hist(c, op->wm, key, ts, kh, n, T, S.hist, op->d_status, bs, S.rsv);
+            fwdev::launch_scan(S.hist, m, S.scan_tmp, bs, gate);
+            fwdev::launch_scatter(c, op->wm, key, ts, val, kh, n, T, S.hist, S.part, S.sk, S.stt, S.sv, S.skh, op->side,
+                                  op->d_status, bs, gate);
+          },
+          bs);
+    } else {
+      timed(
+          op, K_CLASSIFY,
+          [&] {
+            if (c.assigner == FW_SESSION) fwdev::launch_taint(c, op->wm, key, ts, n, op->d_status, bs);
+            fwdev::launch_classify_hist(c, op->wm, key, ts, kh, n, T, S.hist, op->d_status, bs);
+          },
+          bs);
+      timed(op, K_SCAN, [&] { fwdev::launch_scan(S.hist, m, S.scan_tmp, bs); }, bs);
+      timed(
+          op, K_SCATTER,
+          [&] {
+            fwdev::launch_scatter(c, op->wm, key, ts, val, kh, n, T, S.hist, S.part, S.sk, S.stt, S.sv, S.skh, op->side,
+                                  op->d_status, bs);
+          },
+          bs);
+    }
   }
+  S.single = single;
   S.gather = gather;
   S.T = T;
   // minBy / maxBy: the aggregate reads the selected elements' fields back by batch index, possibly after the
@@ -684,7 +722,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   if (split && (rc = ensure_hot(op))) return rc;
   timed(op, K_AGGREGATE, [&] {
     fwdev::launch_aggregate(cc, op->wm, S.part, S.offs(), S.offT(), op->tb, op->prog, 0, split ? &op->hot : nullptr, n,
-                            op->d_status, op->stream);
+                            op->d_status, op->stream, nullptr, 0, single ? S.rsv : nullptr, op->rcap);
     if (cc.agg == FW_AGG_HLL)
       fwdev::launch_hll_update(cc, S.part, S.offs(), S.offT(), n, op->tb, op->d_status, op->stream);
   });
@@ -758,6 +796,7 @@ int push_partials(fw_op* op, const PartialCols& in, int64_t n) {
   S.T = T;
   S.n = n;
   S.partials = true;
+  S.single = false;
   S.split = false;
   S.gather = false;
   S.wm = op->wm;
@@ -984,6 +1023,9 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   for (Scratch& sc : op->sc)
     if ((rc = alloc_scratch(op, sc, mb, m))) return rc;
   c.wide = op->sc[0].wide;  // (every push sets its own set's word)
+  // single-pass scatter: a partition's run may take twice its share of the largest batch (part holds mb PRecs
+  // = 2 mb compact records), whole 128-byte lines apart
+  if (c.dense) op->rcap = ((2 * mb) / c.P) & ~(int64_t)7;
   if (c.assigner == FW_SESSION) {
     // the batches' taint set (k_taint): 2x the batch, at most 2^22 slots; a batch whose ordered-path
     // keys overflow it replays all of its records in arrival order

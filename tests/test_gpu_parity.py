@@ -319,6 +319,28 @@ def test_gpu_zipf_hot_keys():
     assert_rows_equal(g, r)
 
 
+@pytest.mark.parametrize("value_type", ["i64", "f64"])
+def test_gpu_single_pass_scatter_fallbacks(value_type):
+    # dense tumbling windows take the single-pass scatter (each partition's run reserved piece by piece, no
+    # histogram); a batch it cannot take goes through classify / scan / scatter instead: one with a record whose
+    # window is too far ahead for a compact word, one whose hot key overfills its partition's reserved run.  Late
+    # records and key counts must come out once either way.
+    cfg = dict(assigner="tumbling", size=100, value_type=value_type)
+    batches, wms = _stream(700_000, 100_000, 50_000, bound=20, jitter=200, rate=1_000_000, value_type=value_type)
+    k, t, v = batches[2]
+    t = t.copy()
+    t[17] += 10**12  # (the watermarks stay those of the original stream)
+    batches[2] = (k, t, v)
+    k, t, v = batches[4]
+    k = k.copy()
+    k[: len(k) * 3 // 4] = 7
+    batches[4] = (k, t, v)
+    g, r, gs, rs, gl, rl = _run_both(cfg, batches, wms, max_batch=1 << 17)
+    assert_rows_equal(g, r, _VT[value_type])
+    assert gl == rl and gl > 0
+    assert int(g["count"].sum()) + gl == 700_000
+
+
 @pytest.mark.parametrize("cfg", [dict(assigner="tumbling", size=1000),
                                  dict(assigner="sliding", size=5000, slide=1000),
                                  dict(assigner="session", gap=50)], ids=["tumbling", "sliding", "session"])
