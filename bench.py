@@ -223,7 +223,16 @@ def main():
                            expected_entries=(1000 if c1 else live_windows * args.keys // world),
                            max_batch=args.batch if world == 1 else 2 * args.batch,
                            sub_partitions=args.sub_partitions, async_input=not args.sync_input)
-    cx = None
+    nx = None
+    if world > 1:
+        # the keyBy exchange a JNI host calls: fw_keyby_push_device over the library's own RCCL communicator
+        # (route, count all-to-all, per-peer ncclSend / ncclRecv, push), rank 0's id handed to the others
+        import torch.distributed as dist
+        from flink_amd.exchange import NativeKeyByExchange
+        uid = [NativeKeyByExchange.new_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        nx = NativeKeyByExchange(op, world, rank, uid[0])
+    cx = comb = None
     if args.combine:
         if w != "c2":
             raise SystemExit("--combine: only C2 (tumbling count/sum/min/max, Long keys) combines")
@@ -275,13 +284,13 @@ def main():
         else:
             k, t, v, h = batches[s]
             wm = local_wm[s]
-        if cx is not None:  # combine, exchange the partials, merge them (any world size)
+        if nx is not None and comb is not None:  # combine, exchange the partials, merge them (fw_keyby_combine_push_device)
+            wm = nx.push_combined(comb, k, t, v, wm)
+        elif nx is not None:  # route, exchange, push (fw_keyby_push_device); wm = min over the subtasks
+            wm = nx.push(k, t, v, wm, h)
+        elif cx is not None:  # world 1: combine and merge through the Python exchange
             wm = cx.push(op, k, t, v, wm)
         else:
-            if world > 1:
-                res = exch.exchange(k, t, v, h)
-                k, t, v, h = res if h is not None else res + (None,)
-                wm = exch.combine_watermark(wm, device=dev)
             op.process_batch(k, t, v, h)            # queued; settles the previous step's sequence
         op.advance_watermark(wm, wait=False)  # queued behind the push
         op.clear_pending()  # discarding sink: fired rows were materialised in HBM
@@ -419,6 +428,8 @@ def main():
                        "records_per_event_second": args.rate, "watermark_bound_ms": args.bound,
                        "max_parallelism": 128, "parallelism": f"keygroup{world}",
                        "sink": "discarding (fired rows materialised in HBM)",
+                       **({"exchange": "fw_keyby_push_device" + ("/combine" if comb is not None else "") +
+                           " (RCCL count all-to-all, per-peer ncclSend/ncclRecv)"} if nx is not None else {}),
                        **({"combine": "pre-shuffle partial accumulators (SURVEY §8e)"} if cx is not None else {})},
             "roofline": roofline,
             "path_roofline": {"b_alg_bytes_per_record": round(balg, 3), "frac": round(path_frac, 4),
@@ -432,6 +443,8 @@ def main():
                       int(st1["table_grows"] - st0["table_grows"]), "live_entries": int(st1["keyed_state_entries"])},
         }
         print(json.dumps(line), flush=True)
+    if nx is not None:
+        nx.close()
     op.close()
     if world > 1:
         import torch.distributed as dist

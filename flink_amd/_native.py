@@ -65,7 +65,7 @@ class FwStats(ctypes.Structure):
         "slow_path_records", "state_merges", "digest_centroids_fired")]
 
 
-FW_WIRE_LONG, FW_WIRE_INT, FW_WIRE_DOUBLE, FW_WIRE_SHORT, FW_WIRE_BYTE, FW_WIRE_FLOAT, FW_WIRE_BOOL = range(7)
+FW_WIRE_LONG, FW_WIRE_INT, FW_WIRE_DOUBLE, FW_WIRE_SHORT, FW_WIRE_BYTE, FW_WIRE_FLOAT, FW_WIRE_BOOL, FW_WIRE_STRING = range(8)
 (FW_ROLE_SKIP, FW_ROLE_KEY, FW_ROLE_VALUE, FW_ROLE_START, FW_ROLE_END, FW_ROLE_COUNT, FW_ROLE_SUM, FW_ROLE_MIN,
  FW_ROLE_MAX) = range(9)
 
@@ -119,6 +119,8 @@ SIGNATURES = {
     "fw_wire_destroy": (None, [VP]),
     "fw_wire_last_error": (ctypes.c_char_p, [VP]),
     "fw_wire_decode_device": (ctypes.c_int, [VP, VP, ctypes.c_int64, VP, VP, VP, ctypes.c_int64,
+                                             ctypes.POINTER(FwWireStats)]),
+    "fw_wire_decode_keyed_device": (ctypes.c_int, [VP, VP, ctypes.c_int64, VP, VP, VP, VP, ctypes.c_int64,
                                              ctypes.POINTER(FwWireStats)]),
     "fw_wire_encode_device": (ctypes.c_int, [VP, ctypes.POINTER(FwRows), ctypes.c_int64, ctypes.c_int32, VP,
                                              ctypes.c_int64, I64P]),

@@ -4517,8 +4517,9 @@ struct DtLds {
 constexpr int DK_SLOTS = (int)(sizeof(DtLds) / 40 / 16 * 16);
 constexpr int DK_LIMIT = DK_SLOTS * 13 / 16;
 constexpr unsigned long long DK_EMPTY = ~0ull;  // (a record or entry whose word is this takes the wide table)
+constexpr int DK_BUCKETS = DK_SLOTS / 4;  // a word's home is a bucket of 4 slots (one 32-byte read)
 struct DtLdsK {
-  unsigned long long kw[DK_SLOTS];
+  alignas(16) unsigned long long kw[DK_SLOTS];
   unsigned long long cnt[DK_SLOTS];
   int64_t sum[DK_SLOTS], mn[DK_SLOTS], mx[DK_SLOTS];
 };
@@ -4531,10 +4532,18 @@ struct DtMisc {
   long long ntmin, out;
 };
 __device__ __forceinline__ uint32_t dt_bucket(uint32_t h) { return (uint32_t)(((uint64_t)h * DT_BUCKETS) >> 32); }
+// first slot of the word's home bucket
 __device__ __forceinline__ uint32_t dk_home(unsigned long long kw) {
   uint32_t h = (uint32_t)(kw >> 32) * 0x9E3779B1u ^ (uint32_t)kw;
   h ^= h >> 15;
-  return (uint32_t)(((uint64_t)h * DK_SLOTS) >> 32);
+  return (uint32_t)(((uint64_t)h * DK_BUCKETS) >> 32) * 4u;
+}
+// the 4 words of the bucket at slot s0
+__device__ __forceinline__ void dk_read4(const DtLdsK& K, uint32_t s0, unsigned long long (&g)[4]) {
+  const i64x2 a = *reinterpret_cast<const i64x2*>(&K.kw[s0]);
+  const i64x2 b = *reinterpret_cast<const i64x2*>(&K.kw[s0 + 2]);
+  g[0] = (unsigned long long)a.x, g[1] = (unsigned long long)a.y, g[2] = (unsigned long long)b.x,
+  g[3] = (unsigned long long)b.y;
 }
 // the hash pass of (key, window): prefix of a hash independent of the LDS slot's
 __device__ __forceinline__ int dt_pass(const DevCfg& c, int64_t key, int64_t start, int hb) {
@@ -4591,19 +4600,31 @@ __device__ __forceinline__ int dt_slot(DtLds& L, DtMisc& M, int64_t key, int64_t
   }
   return -1;
 }
-// compact table: find or claim the slot of word kw from slot s on; -1 at the fill limit
-__device__ __forceinline__ int dk_slot(DtLdsK& K, DtMisc& M, unsigned long long kw, uint32_t s) {
-  for (int guard = 0; guard < DK_SLOTS; guard++) {
-    unsigned long long g = __hip_atomic_load(&K.kw[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (g == kw) return (int)s;
-    if (g == DK_EMPTY) {
-      if (!dt_ticket(M, DK_LIMIT)) return -1;
-      g = atomicCAS(&K.kw[s], DK_EMPTY, kw);
-      if (g == DK_EMPTY) return (int)s;  // claimed (the accumulators were initialised with the table)
-      atomicSub(&M.fill, 1);
-      if (g == kw) return (int)s;
+// compact table: find or claim the slot of word kw from the bucket at slot s0 on; -1 at the fill limit.  A word is
+// claimed in the first EMPTY slot of the first bucket that has one (buckets in probe order, slots in bucket order), and
+// a slot never empties while the table is in use, so a lookup that meets a bucket with an EMPTY slot and no match
+// knows the word is absent; a lost claim race re-reads the bucket.
+__device__ __forceinline__ int dk_slot(DtLdsK& K, DtMisc& M, unsigned long long kw, uint32_t s0) {
+  for (int guard = 0; guard < 2 * DK_BUCKETS;) {
+    asm volatile("" ::: "memory");
+    unsigned long long g[4];
+    dk_read4(K, s0, g);
+    int e = -1;
+#pragma unroll
+    for (int q = 3; q >= 0; q--) {
+      if (g[q] == kw) return (int)s0 + q;
+      if (g[q] == DK_EMPTY) e = q;
     }
-    s = s + 1 == (uint32_t)DK_SLOTS ? 0u : s + 1;
+    if (e >= 0) {
+      if (!dt_ticket(M, DK_LIMIT)) return -1;
+      const unsigned long long o = atomicCAS(&K.kw[s0 + e], DK_EMPTY, kw);
+      if (o == DK_EMPTY) return (int)s0 + e;  // claimed (the accumulators were initialised with the table)
+      atomicSub(&M.fill, 1);
+      if (o == kw) return (int)s0 + e;
+      continue;
+    }
+    s0 = s0 + 4 == (uint32_t)DK_SLOTS ? 0u : s0 + 4;
+    guard++;
   }
   return -1;
 }
@@ -4676,20 +4697,21 @@ template <int RPT>
 __device__ __forceinline__ bool dk_add_batch(DtLdsK& K, DtMisc& M, int vtype, const unsigned long long (&w)[RPT],
                                              const int64_t (&v)[RPT], uint32_t dm) {
   uint32_t s[RPT];
-  unsigned long long g[RPT];
-  // every home slot read before any is used (plain reads: a word, once claimed, never changes, and a stale EMPTY
+  unsigned long long g[RPT][4];
+  // every home bucket read before any is used (plain reads: a word, once claimed, never changes, and a stale EMPTY
   // only sends the element to dk_slot, which re-reads)
 #pragma unroll
   for (int j = 0; j < RPT; j++) {
     s[j] = dk_home(w[j]);
-    g[j] = K.kw[s[j]];
+    dk_read4(K, s[j], g[j]);
   }
   uint32_t miss = 0;
 #pragma unroll
   for (int j = 0; j < RPT; j++) {
     if (dm >> j & 1) continue;
-    if (g[j] == w[j])
-      dt_add(K, (int)s[j], vtype, v[j]);
+    const int q = g[j][0] == w[j] ? 0 : g[j][1] == w[j] ? 1 : g[j][2] == w[j] ? 2 : g[j][3] == w[j] ? 3 : -1;
+    if (q >= 0)
+      dt_add(K, (int)s[j] + q, vtype, v[j]);
     else
       miss |= 1u << j;
   }

@@ -1210,6 +1210,13 @@ int fw_push_batch(fw_op* op, const int64_t* key, const int64_t* ts, const void* 
 }
 
 namespace {
+// the stream a device push reads its columns on: the input stream when async input applies to the operator's
+// batches (push_device's `two`: not with side output, count windows or gathered batches)
+hipStream_t input_stream_of(const fw_op* op) {
+  const bool two = op->async_in && !op->dc.side_output && op->cfg.assigner != FW_COUNT && !op->sc[0].rt;
+  return two ? op->bstream : op->stream;
+}
+
 int push_device_batches(fw_op* op, const int64_t* key, const int64_t* ts, const void* val, const int32_t* key_hash,
                         int64_t n, bool async_ok) {
   if (!op || n < 0 || (n > 0 && (!key || !ts || !val))) return op ? set_err(op, FW_ERR_ARG, "null column") : FW_ERR_ARG;
@@ -1239,7 +1246,7 @@ int fw_set_async_input(fw_op* op, int enable) {
   return FW_OK;
 }
 
-void* fw_input_stream(fw_op* op) { return op ? (void*)(op->async_in ? op->bstream : op->stream) : nullptr; }
+void* fw_input_stream(fw_op* op) { return op ? (void*)input_stream_of(op) : nullptr; }
 
 int fw_advance_watermark(fw_op* op, int64_t wm, int64_t* n_pending) {
   if (!op) return FW_ERR_ARG;
@@ -1742,7 +1749,8 @@ int fw_route_device(const int64_t* key, const int64_t* ts, const int64_t* val, c
 struct fw_comm {
   ncclComm_t nc = nullptr;
   int32_t world = 1, rank = 0, device = 0;
-  int64_t cap = 0;                                        // records the routed / received columns hold
+  int64_t cap = 0;                                        // records the routed (send) columns hold
+  int64_t rcap = 0;                                       // records the received columns hold
   int64_t *rk = nullptr, *rt = nullptr, *rv = nullptr;    // received columns
   int32_t* rh = nullptr;
   int64_t *sk = nullptr, *st = nullptr, *sv = nullptr;    // routed (send) columns
@@ -1761,21 +1769,44 @@ void cfree(T*& p) {
   if (p) (void)hipFree((void*)p);
   p = nullptr;
 }
-int comm_reserve(fw_op* op, fw_comm* c, int64_t need) {
+// the routed columns (and the route's scratch) for n records; their contents are not kept.  On failure every column
+// is freed and the capacity is 0, so the next call allocates afresh.
+int comm_reserve_send(fw_op* op, fw_comm* c, int64_t need) {
   if (need <= c->cap) return FW_OK;
   const int64_t cap = std::max<int64_t>(need, c->cap * 2);
-  for (int64_t** p : {&c->rk, &c->rt, &c->rv, &c->sk, &c->st, &c->sv}) {
-    cfree(*p);
-    HIP_OR_RETURN(op, dmalloc(p, (size_t)cap));
-  }
-  for (int32_t** p : {&c->rh, &c->sh}) {
-    cfree(*p);
-    HIP_OR_RETURN(op, dmalloc(p, (size_t)cap));
-  }
+  c->cap = 0;
+  for (int64_t** p : {&c->sk, &c->st, &c->sv}) cfree(*p);
+  cfree(c->sh);
   cfree(c->scratch);
+  bool ok = dmalloc(&c->sk, (size_t)cap) == hipSuccess && dmalloc(&c->st, (size_t)cap) == hipSuccess &&
+            dmalloc(&c->sv, (size_t)cap) == hipSuccess && dmalloc(&c->sh, (size_t)cap) == hipSuccess;
   c->scratch_bytes = fw_route_scratch_bytes(cap, c->world);
-  HIP_OR_RETURN(op, dmalloc((uint8_t**)&c->scratch, (size_t)c->scratch_bytes));
+  ok = ok && dmalloc((uint8_t**)&c->scratch, (size_t)c->scratch_bytes) == hipSuccess;
+  if (!ok) {
+    for (int64_t** p : {&c->sk, &c->st, &c->sv}) cfree(*p);
+    cfree(c->sh);
+    cfree(c->scratch);
+    return set_err(op, FW_ERR_HIP, "exchange: cannot allocate the routed columns for %lld records", (long long)cap);
+  }
   c->cap = cap;
+  return FW_OK;
+}
+// the received columns for `need` records (a skewed batch can bring more than the subtask sent); the stream that
+// last read them must be idle
+int comm_reserve_recv(fw_op* op, fw_comm* c, int64_t need) {
+  if (need <= c->rcap) return FW_OK;
+  const int64_t cap = std::max<int64_t>(need, c->rcap * 2);
+  c->rcap = 0;
+  for (int64_t** p : {&c->rk, &c->rt, &c->rv}) cfree(*p);
+  cfree(c->rh);
+  const bool ok = dmalloc(&c->rk, (size_t)cap) == hipSuccess && dmalloc(&c->rt, (size_t)cap) == hipSuccess &&
+                  dmalloc(&c->rv, (size_t)cap) == hipSuccess && dmalloc(&c->rh, (size_t)cap) == hipSuccess;
+  if (!ok) {
+    for (int64_t** p : {&c->rk, &c->rt, &c->rv}) cfree(*p);
+    cfree(c->rh);
+    return set_err(op, FW_ERR_HIP, "exchange: cannot allocate the received columns for %lld records", (long long)cap);
+  }
+  c->rcap = cap;
   return FW_OK;
 }
 #define NCCL_OR_RETURN(op, expr)                                                                            \
@@ -1844,9 +1875,12 @@ int fw_keyby_push_device(fw_comm* c, fw_op* op, const int64_t* key, const int64_
                    op->cfg.key_group_start, op->cfg.key_group_end, c->rank, c->world, kg0, kg1);
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;
-  if ((rc = comm_reserve(op, c, std::max<int64_t>(n, 1)))) return rc;
+  if ((rc = comm_reserve_send(op, c, std::max<int64_t>(n, 1)))) return rc;
   const int W = c->world;
-  hipStream_t s = op->stream;
+  // the exchange runs on the stream the operator reads device batches on (fw_input_stream): with async input
+  // that is not the stream of the previous batch's aggregation, so the count round trip below waits only for
+  // the previous batch's partitioning (which read the received columns) and this batch's route
+  hipStream_t s = input_stream_of(op);
   // group by destination subtask (stable), counts[W] on the device
   fwdev::launch_route(key, ts, (const int64_t*)val, key_hash, op->cfg.key_kind, n, op->cfg.max_parallelism, W, c->sk,
                       c->st, c->sv, c->sh, c->counts, (uint32_t*)c->scratch, s);
@@ -1866,29 +1900,9 @@ int fw_keyby_push_device(fw_comm* c, fw_op* op, const int64_t* key, const int64_
     roff[p + 1] = roff[p] + c->h_counts[W + p];
   }
   const int64_t total = roff[W];
-  if (total > c->cap) {  // skew: more records arrive than this subtask sent; grow (keeping the routed columns)
-    int64_t *k2 = nullptr, *t2 = nullptr, *v2 = nullptr;
-    int32_t* h2 = nullptr;
-    HIP_OR_RETURN(op, dmalloc(&k2, (size_t)n));
-    HIP_OR_RETURN(op, dmalloc(&t2, (size_t)n));
-    HIP_OR_RETURN(op, dmalloc(&v2, (size_t)n));
-    HIP_OR_RETURN(op, dmalloc(&h2, (size_t)n));
-    HIP_OR_RETURN(op, hipMemcpyAsync(k2, c->sk, n * 8, hipMemcpyDeviceToDevice, s));
-    HIP_OR_RETURN(op, hipMemcpyAsync(t2, c->st, n * 8, hipMemcpyDeviceToDevice, s));
-    HIP_OR_RETURN(op, hipMemcpyAsync(v2, c->sv, n * 8, hipMemcpyDeviceToDevice, s));
-    HIP_OR_RETURN(op, hipMemcpyAsync(h2, c->sh, n * 4, hipMemcpyDeviceToDevice, s));
-    HIP_OR_RETURN(op, hipStreamSynchronize(s));
-    if ((rc = comm_reserve(op, c, total))) return rc;
-    HIP_OR_RETURN(op, hipMemcpyAsync(c->sk, k2, n * 8, hipMemcpyDeviceToDevice, s));
-    HIP_OR_RETURN(op, hipMemcpyAsync(c->st, t2, n * 8, hipMemcpyDeviceToDevice, s));
-    HIP_OR_RETURN(op, hipMemcpyAsync(c->sv, v2, n * 8, hipMemcpyDeviceToDevice, s));
-    HIP_OR_RETURN(op, hipMemcpyAsync(c->sh, h2, n * 4, hipMemcpyDeviceToDevice, s));
-    HIP_OR_RETURN(op, hipStreamSynchronize(s));
-    cfree(k2);
-    cfree(t2);
-    cfree(v2);
-    cfree(h2);
-  }
+  // skew: more records may arrive than this subtask sent; only the received columns grow (s is idle here, and the
+  // previous batch's partitioning, the last reader of the received columns, ran on s)
+  if ((rc = comm_reserve_recv(op, c, std::max<int64_t>(total, 1)))) return rc;
   // the columns peer to peer: each peer pair over its own xGMI link
   NCCL_OR_RETURN(op, ncclGroupStart());
   for (int p = 0; p < W; p++) {
@@ -1904,9 +1918,9 @@ int fw_keyby_push_device(fw_comm* c, fw_op* op, const int64_t* key, const int64_
   }
   NCCL_OR_RETURN(op, ncclGroupEnd());
   if (combined_wm) *combined_wm = c->h_counts[2 * W + 1];
-  // processElement for the received batch (stream-ordered behind the receives)
-  // (the columns were received on the handle's stream, so the push reads them in its order)
-  return push_device_batches(op, c->rk, c->rt, c->rv, hashed ? c->rh : nullptr, total, false);
+  // processElement for the received batch (stream-ordered behind the receives: they ran on the stream the push
+  // reads its columns on)
+  return push_device_batches(op, c->rk, c->rt, c->rv, hashed ? c->rh : nullptr, total, true);
 }
 
 int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64_t* key, const int64_t* ts,

@@ -28,7 +28,8 @@ constexpr uint8_t X_END = 0xFE, X_BAD = 0xFF;  // the walk ended with the stream
 constexpr int WMAX_ELEMS = WCH / 5 + 2;         // elements starting in one chunk, at most (the smallest is 9 B)
 
 struct WireL {
-  int32_t nf, F;  // fields, value bytes
+  int32_t nf, F;  // fields, value bytes (of the fixed-size fields)
+  int32_t vs;     // the layout has String fields: a record's value length is found by reading them
   int32_t kind[FW_WIRE_MAX_FIELDS], role[FW_WIRE_MAX_FIELDS], off[FW_WIRE_MAX_FIELDS];
 };
 
@@ -51,13 +52,75 @@ __device__ inline void st_be(uint8_t* p, uint64_t v, int nb) {
 __device__ inline int64_t want_len(const WireL& L, int tag) {
   return tag == 0 ? 9 + L.F : tag == 1 ? 1 + L.F : tag == 2 ? 9 : tag == 3 ? 29 : tag == 4 ? 5 : -1;
 }
+__device__ inline uint64_t wfmix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+// StringValue.readString's base-128 varint (StringValue.java:745-786), low group first: its bytes, -1 past end
+__device__ inline int wire_varint(const uint8_t* p, const uint8_t* end, uint32_t* out) {
+  uint32_t v = 0;
+  int shift = 0;
+  for (int k = 0; p + k < end && k < 5; k++) {
+    const uint32_t c = p[k];
+    v |= (c & 0x7fu) << shift;
+    if (c < 0x80u) {
+      *out = v;
+      return k + 1;
+    }
+    shift += 7;
+  }
+  return -1;
+}
+// a String field at p (StringValue.readString): its bytes, -1 if it runs past end; for a non-null one
+// String.hashCode and the key column's id (FNV-1a 64 over the UTF-16 chars, fmix64 of it ^ the length:
+// oracle_string_key_id)
+__device__ inline int wire_string(const uint8_t* p, const uint8_t* end, bool* is_null, int32_t* hash, int64_t* id) {
+  uint32_t len;
+  int at = wire_varint(p, end, &len);
+  if (at < 0) return -1;
+  *is_null = len == 0;
+  if (len == 0) return at;
+  len -= 1;
+  uint32_t h = 0;
+  uint64_t f = 0xcbf29ce484222325ull;
+  for (uint32_t i = 0; i < len; i++) {
+    uint32_t c;
+    const int k = wire_varint(p + at, end, &c);
+    if (k < 0) return -1;
+    at += k;
+    const uint32_t ch = c & 0xffffu;  // (char) c
+    h = 31u * h + ch;
+    f = (f ^ ch) * 0x100000001b3ull;
+  }
+  *hash = (int32_t)h;
+  *id = (int64_t)wfmix64(f ^ (uint64_t)len);
+  return at;
+}
+// a record's value fields from p (the byte after the tag / timestamp) up to end: their bytes (-1 if they do not
+// fit, or a String key is null), the key, its hash and the value
+__device__ inline int64_t wire_fields(const WireL& L, const uint8_t* p, const uint8_t* end, int64_t* key, int32_t* kh,
+                                      int64_t* val);
 // the element at pos: its size with the prefix (> 0), -1 if the stream ends inside it (the next call's), 0 if it
-// cannot be an element of this layout (an unknown tag, or a length other than its tag's); *tag = its tag
+// cannot be an element of this layout (an unknown tag, a length other than its tag's, a record whose String fields
+// do not end where it does or whose String key is null, a String record longer than WE); *tag = its tag
 __device__ inline int elem_at(const uint8_t* b, int64_t n, int64_t pos, const WireL& L, int* tag) {
   if (pos + 4 > n) return -1;
   const int64_t len = (int64_t)ld_be(b + pos, 4);
   if (pos + 4 + len > n) return -1;
   *tag = len > 0 ? (int)(int8_t)b[pos + 4] : -3;  // DataInputView.readByte of an empty element: EOF
+  if (L.vs && (*tag == 0 || *tag == 1)) {
+    if (4 + len > WE) return 0;
+    const uint8_t* e = b + pos + 4;
+    int64_t k, v;
+    int32_t h;
+    const int64_t head = *tag == 0 ? 9 : 1;
+    const int64_t m = len >= head ? wire_fields(L, e + head, e + len, &k, &h, &v) : -1;
+    return m >= 0 && head + m == len ? (int)(4 + len) : 0;
+  }
   const int64_t w = want_len(L, *tag);
   return (w < 0 || len != w) ? 0 : (int)(4 + len);
 }
@@ -73,6 +136,36 @@ __device__ inline int64_t field_value(int32_t kind, const uint8_t* p) {
     case FW_WIRE_FLOAT: return __double_as_longlong((double)__int_as_float((int)(uint32_t)ld_be(p, 4)));
   }
   return 0;
+}
+
+__device__ inline int64_t wire_fields(const WireL& L, const uint8_t* p, const uint8_t* end, int64_t* key, int32_t* kh,
+                                      int64_t* val) {
+  int64_t at = 0;
+  *key = 0;
+  *kh = 0;
+  *val = 0;
+  for (int f = 0; f < L.nf; f++) {
+    if (L.kind[f] == FW_WIRE_STRING) {
+      bool is_null = false;
+      int32_t h = 0;
+      int64_t id = 0;
+      const int m = wire_string(p + at, end, &is_null, &h, &id);
+      if (m < 0) return -1;
+      if (L.role[f] == FW_ROLE_KEY) {
+        if (is_null) return -1;  // a null key
+        *key = id;
+        *kh = h;
+      }
+      at += m;
+    } else {
+      const int fb = field_bytes(L.kind[f]);
+      if (p + at + fb > end) return -1;
+      if (L.role[f] == FW_ROLE_KEY) *key = field_value(L.kind[f], p + at);
+      if (L.role[f] == FW_ROLE_VALUE) *val = field_value(L.kind[f], p + at);
+      at += fb;
+    }
+  }
+  return at;
 }
 
 // ---- speculation: per (chunk, first-element offset e) the exit into the next chunk and the records passed
@@ -144,6 +237,7 @@ __global__ void k_wire_counts(const uint8_t* __restrict__ entry, const uint32_t*
 }
 struct WireOut {
   int64_t *key, *ts, *val;
+  int32_t* kh;              // the key's hash (String.hashCode of a String key), or nullptr
   int64_t* chunk_wm;        // per chunk: its last watermark, or INT64_MIN
   int64_t* chunk_status;    // per chunk: its last stream status, or INT64_MIN
   unsigned long long* acc;  // [0] watermarks, [1] latency markers, [2] statuses, [3] consumed (min over END walks),
@@ -211,13 +305,19 @@ __global__ __launch_bounds__(WE) void k_wire_emit(const uint8_t* __restrict__ b,
       p += 8;
     }
     int64_t k = 0, v = 0;
-    for (int f = 0; f < L.nf; f++) {
-      if (L.role[f] == FW_ROLE_KEY) k = field_value(L.kind[f], p + L.off[f]);
-      if (L.role[f] == FW_ROLE_VALUE) v = field_value(L.kind[f], p + L.off[f]);
+    int32_t h = 0;
+    if (L.vs) {  // (elem_at checked the fields)
+      (void)wire_fields(L, p, b + n, &k, &h, &v);
+    } else {
+      for (int f = 0; f < L.nf; f++) {
+        if (L.role[f] == FW_ROLE_KEY) k = field_value(L.kind[f], p + L.off[f]);
+        if (L.role[f] == FW_ROLE_VALUE) v = field_value(L.kind[f], p + L.off[f]);
+      }
     }
     o.key[r] = k;
     o.ts[r] = t;
     o.val[r] = v;
+    if (o.kh) o.kh[r] = h;
   }
 }
 // the last watermark / status over the chunks (one workgroup), the tag of the first corrupt element
@@ -335,12 +435,19 @@ int fw_wire_create(const fw_wire_layout* layout, int64_t max_bytes, int32_t devi
   for (int f = 0; f < L.nf; f++) {
     L.kind[f] = layout->kind[f];
     L.role[f] = layout->role[f];
-    const int fb = field_bytes(L.kind[f]);
+    const bool str = L.kind[f] == FW_WIRE_STRING;
+    const int fb = str ? 0 : field_bytes(L.kind[f]);
     if (fb < 0 || L.role[f] < FW_ROLE_SKIP || L.role[f] > FW_ROLE_MAX) {
       w->err = "unknown field kind or role";
       *out = w;
       return FW_ERR_ARG;
     }
+    if (str && L.role[f] != FW_ROLE_KEY && L.role[f] != FW_ROLE_SKIP) {
+      w->err = "a String field is a key or skipped";
+      *out = w;
+      return FW_ERR_ARG;
+    }
+    L.vs |= str;
     L.off[f] = L.F;
     L.F += fb;
     keys += L.role[f] == FW_ROLE_KEY;
@@ -404,9 +511,17 @@ const char* fw_wire_last_error(const fw_wire* w) { return w ? w->err.c_str() : "
 
 int fw_wire_decode_device(fw_wire* w, const uint8_t* bytes, int64_t nbytes, int64_t* key, int64_t* ts, int64_t* val,
                           int64_t cap, fw_wire_stats* stats) {
+  return fw_wire_decode_keyed_device(w, bytes, nbytes, key, nullptr, ts, val, cap, stats);
+}
+
+int fw_wire_decode_keyed_device(fw_wire* w, const uint8_t* bytes, int64_t nbytes, int64_t* key, int32_t* key_hash,
+                                int64_t* ts, int64_t* val, int64_t cap, fw_wire_stats* stats) {
   if (!w || !stats || (nbytes > 0 && !bytes) || nbytes < 0) return FW_ERR_ARG;
   if (nbytes > w->max_bytes) return wire_err(w, FW_ERR_ARG, "stream longer than the codec's max_bytes");
   if (13 + w->dl.F > WE) return wire_err(w, FW_ERR_ARG, "decoded elements are at most 64 bytes (fields <= 51 bytes)");
+  for (int f = 0; f < w->dl.nf; f++)
+    if (w->dl.kind[f] == FW_WIRE_STRING && w->dl.role[f] == FW_ROLE_KEY && !key_hash)
+      return wire_err(w, FW_ERR_ARG, "a String key needs the key_hash column (fw_wire_decode_keyed_device)");
   std::memset(stats, 0, sizeof *stats);
   stats->watermark = INT64_MIN;
   if (nbytes == 0) return FW_OK;
@@ -439,7 +554,7 @@ int fw_wire_decode_device(fw_wire* w, const uint8_t* bytes, int64_t nbytes, int6
                                                           " records, more than the output's capacity");
   unsigned long long init[6] = {0, 0, 0, (unsigned long long)nbytes, ~0ull, 0};
   WIRE_HIP(w, hipMemcpyAsync(w->acc, init, sizeof init, hipMemcpyHostToDevice, s));
-  WireOut o{key, ts, val, w->chunk_wm, w->chunk_status, w->acc};
+  WireOut o{key, ts, val, key_hash, w->chunk_wm, w->chunk_status, w->acc};
   hipLaunchKernelGGL(k_wire_emit, dim3((unsigned)nc), dim3(WE), 0, s, bytes, nbytes, nc, w->dl, w->lentry[0], w->cnt, o);
   hipLaunchKernelGGL(k_wire_final, dim3(1), dim3(1024), 0, s, bytes, nc, o, w->last);
   WIRE_HIP(w, hipMemcpyAsync(w->h_tot + 1, w->acc, 6 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -459,9 +574,11 @@ int fw_wire_decode_device(fw_wire* w, const uint8_t* bytes, int64_t nbytes, int6
     stats->consumed = (int64_t)bad;
     const int64_t tag = h[9];
     const bool known = tag >= 0 && tag <= 4;
-    return wire_err(w, FW_ERR_STATE, known ? "Corrupt stream: an element whose length does not match the layout at byte " +
-                                                 std::to_string(bad)
-                                           : "Corrupt stream, found tag: " + std::to_string(tag));
+    return wire_err(w, FW_ERR_STATE,
+                    known ? std::string("Corrupt stream: an element whose length does not match the layout") +
+                                (w->dl.vs ? " (or a null String key, or a String record longer than 64 bytes)" : "") +
+                                " at byte " + std::to_string(bad)
+                          : "Corrupt stream, found tag: " + std::to_string(tag));
   }
   return FW_OK;
 }
@@ -471,6 +588,7 @@ int fw_wire_encode_device(fw_wire* w, const fw_rows* rows, int64_t n, int32_t f6
   if (!w || !rows || !written || n < 0) return FW_ERR_ARG;
   for (int f = 0; f < w->dl.nf; f++)
     if (w->dl.role[f] == FW_ROLE_VALUE) return wire_err(w, FW_ERR_ARG, "an output layout names row fields, not VALUE");
+  if (w->dl.vs) return wire_err(w, FW_ERR_ARG, "String fields are decoded only (rows carry the key's 64-bit id)");
   const int64_t S = 13 + w->dl.F;
   *written = 0;
   if (n * S > cap) return wire_err(w, FW_ERR_STATE, "output buffer too small");

@@ -130,8 +130,8 @@ class NativeKeyByExchange:
         import torch
         wm = ctypes.c_int64()
         n = keys.numel()
-        # the library's stream reads the columns: it waits for their producer first
-        self.op._torch_stream(keys.device).wait_stream(torch.cuda.current_stream(keys.device))
+        # the library's input stream reads the columns: it waits for their producer first
+        self.op._input_stream(keys.device).wait_stream(torch.cuda.current_stream(keys.device))
         rc = N.lib().fw_keyby_push_device(self._c, self.op._h, keys.data_ptr(), ts.data_ptr(), vals.data_ptr(),
                                           key_hash.data_ptr() if key_hash is not None else None, n, int(local_wm),
                                           ctypes.byref(wm))

@@ -62,6 +62,22 @@ def string_hash_code(s):
     return _i32(h)
 
 
+def string_key_id(s):
+    """The key column's 64-bit identity of a String key decoded from the wire (fw_wire_decode_keyed_device):
+    FNV-1a 64 over the UTF-16 chars, then fmix64 of it ^ the char count, as a signed long."""
+    b = s.encode("utf-16-le")
+    f = 0xcbf29ce484222325
+    for i in range(0, len(b), 2):
+        f = ((f ^ (b[i] | (b[i + 1] << 8))) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    x = f ^ (len(b) // 2)
+    x ^= x >> 33
+    x = (x * 0xff51afd7ed558ccd) & 0xFFFFFFFFFFFFFFFF
+    x ^= x >> 33
+    x = (x * 0xc4ceb9fe1a85ec53) & 0xFFFFFFFFFFFFFFFF
+    x ^= x >> 33
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
 def compute_key_group_for_key_hash(key_hash, max_parallelism):
     """KeyGroupRangeAssignment.computeKeyGroupForKeyHash (:69-71)."""
     return murmur_hash(key_hash) % max_parallelism

@@ -9,15 +9,19 @@ process_watermark), without a per-record JVM step; WireCodec.encode turns fired 
 operator's output channel (timestamp = the window's maxTimestamp).
 
 Layouts name the value type's fields: Tuple fields in order (TupleSerializer, no null mask) or one bare field,
-each a Java type of fixed size and a role, e.g. Tuple3<Long, Long, Integer> keyed by field 0 summing field 2:
+each a Java type and a role, e.g. Tuple3<Long, Long, Integer> keyed by field 0 summing field 2:
     WireLayout([("long", "key"), ("long", "skip"), ("int", "value")])
+or WindowWordCount's Tuple2<String, Integer> (StringValue.writeString's varint encoding):
+    WireLayout([("string", "key"), ("int", "value")])
+whose decode also returns the key_hash column (String.hashCode); the key column holds the word's 64-bit id
+(keygroups.string_key_id), and the pair goes to a GpuWindowOperator with key_type="hashed".
 """
 import ctypes
 
 from . import _native as N
 
 _KINDS = {"long": N.FW_WIRE_LONG, "int": N.FW_WIRE_INT, "double": N.FW_WIRE_DOUBLE, "short": N.FW_WIRE_SHORT,
-          "byte": N.FW_WIRE_BYTE, "float": N.FW_WIRE_FLOAT, "boolean": N.FW_WIRE_BOOL}
+          "byte": N.FW_WIRE_BYTE, "float": N.FW_WIRE_FLOAT, "boolean": N.FW_WIRE_BOOL, "string": N.FW_WIRE_STRING}
 _ROLES = {"skip": N.FW_ROLE_SKIP, "key": N.FW_ROLE_KEY, "value": N.FW_ROLE_VALUE, "start": N.FW_ROLE_START,
           "end": N.FW_ROLE_END, "count": N.FW_ROLE_COUNT, "sum": N.FW_ROLE_SUM, "min": N.FW_ROLE_MIN,
           "max": N.FW_ROLE_MAX}
@@ -66,24 +70,31 @@ class WireCodec:
         if rc != N.FW_OK:
             raise N.NativeError(rc, N.lib().fw_wire_last_error(self._h).decode())
 
+    def string_key(self):
+        return any(k == "string" and r == "key" for k, r in self.layout.fields)
+
     def decode(self, data, cap=None):
         """data: a CUDA uint8 tensor.  Returns (key, ts, val) int64 CUDA tensors (val holds double bits for Double /
-        Float value fields) and the stats dict (records, watermarks, latency_markers, statuses, consumed,
-        watermark, status)."""
+        Float value fields), plus the int32 key_hash column when the key is a String, and the stats dict (records,
+        watermarks, latency_markers, statuses, consumed, watermark, status)."""
         import torch
         n = data.numel()
         cap = n // (5 + self.value_bytes()) + 1 if cap is None else cap  # the smallest record element
         dev = data.device
         key, ts, val = (torch.empty(cap, dtype=torch.int64, device=dev) for _ in range(3))
+        kh = torch.empty(cap, dtype=torch.int32, device=dev) if self.string_key() else None
         st = N.FwWireStats()
         torch.cuda.current_stream(dev).synchronize()  # the codec's stream reads the bytes
-        self._check(N.lib().fw_wire_decode_device(self._h, data.data_ptr(), n, key.data_ptr(), ts.data_ptr(),
-                                                  val.data_ptr(), cap, ctypes.byref(st)))
+        self._check(N.lib().fw_wire_decode_keyed_device(self._h, data.data_ptr(), n, key.data_ptr(),
+                                                        kh.data_ptr() if kh is not None else None, ts.data_ptr(),
+                                                        val.data_ptr(), cap, ctypes.byref(st)))
         r = st.records
-        return (key[:r], ts[:r], val[:r]), {f: getattr(st, f) for f, _ in N.FwWireStats._fields_ if f != "pad"}
+        cols = (key[:r], ts[:r], val[:r]) + ((kh[:r],) if kh is not None else ())
+        return cols, {f: getattr(st, f) for f, _ in N.FwWireStats._fields_ if f != "pad"}
 
     def value_bytes(self):
-        return sum({"long": 8, "double": 8, "int": 4, "float": 4, "short": 2, "byte": 1, "boolean": 1}[k]
+        """The value's bytes (a String field counts its shortest form, one byte)."""
+        return sum({"long": 8, "double": 8, "int": 4, "float": 4, "short": 2, "byte": 1, "boolean": 1, "string": 1}[k]
                    for k, _ in self.layout.fields)
 
     def encode(self, rows_view, n, f64=False):

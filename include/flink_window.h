@@ -236,8 +236,9 @@ void* fw_stream(fw_op* op); /* the hipStream_t the handle enqueues on */
  * one, StreamInputProcessor.java:211-223).  Enabled, fw_push_batch_device reads its columns on
  * fw_input_stream(op) — the caller orders the columns' producer before that stream (not before fw_stream) —
  * and the batch's partitioning kernels run there, beside the previous batch's aggregation and firing on
- * fw_stream.  Disabled (the default), fw_input_stream(op) == fw_stream(op).  Host pushes and
- * fw_keyby_push_device always read their columns in fw_stream order. */
+ * fw_stream.  Disabled (the default), or with side output or count windows, fw_input_stream(op) ==
+ * fw_stream(op).  fw_keyby_push_device reads its columns and runs its exchange on fw_input_stream(op) too; host
+ * pushes read theirs in fw_stream order. */
 int fw_set_async_input(fw_op* op, int enable);
 void* fw_input_stream(fw_op* op);
 
@@ -325,7 +326,8 @@ int64_t fw_route_scratch_bytes(int64_t n, int32_t parallelism);
  *     source's arrival order kept, are pushed into `op` (fw_push_batch_device), whose KeyGroupRange must be
  *     computeKeyGroupRangeForOperatorIndex(maxParallelism, world, rank).  *combined_wm = min over the subtasks of
  *     local_wm (the operator's input watermark), for the caller's fw_advance_watermark.  Collective: every
- *     subtask calls it once per batch.  Enqueued on the handle's stream. */
+ *     subtask calls it once per batch.  Enqueued on fw_input_stream(op); the host waits once per batch, for the
+ *     route and the count exchange on that stream (with async input not for the previous batch's aggregation). */
 typedef struct fw_comm fw_comm;
 int fw_comm_unique_id(void* id128);
 int fw_comm_init(const void* id128, int32_t world, int32_t rank, int32_t device, fw_comm** out);
@@ -350,7 +352,13 @@ int fw_keyby_combine_push_device(fw_comm* comm, fw_op* combiner, fw_op* op, cons
  *   4 stream status: BE i32   (any other tag: "Corrupt stream, found tag: X")
  * and the value is a Tuple (TupleSerializer: fields in order, no null mask) of fixed-size fields, or one bare
  * field: Long / Integer / Short / Byte / Boolean (BE two's complement) and Double / Float (BE
- * doubleToLongBits / floatToIntBits).  String fields (StringValue's varint encoding) are not decoded yet.
+ * doubleToLongBits / floatToIntBits), or String (StringSerializer -> StringValue.writeString, StringValue.java:
+ * 789-817: length + 1 as a base-128 varint, 0 = null, then each UTF-16 char as a base-128 varint).  A String
+ * field is the key (FW_ROLE_KEY) or skipped: the key column then holds the chars' 64-bit id (FNV-1a 64 over the
+ * UTF-16 chars, then fmix64 of it ^ the length) and the key_hash column String.hashCode, the two columns
+ * FW_KEY_HASHED takes; a null String key is a corrupt element (KeyGroupStreamPartitioner cannot hash it).  A
+ * record with String fields is decoded when it is at most 64 bytes with its length prefix (WindowWordCount's
+ * Tuple2<String, Integer> with a timestamp: words of up to 46 ASCII chars).
  *   fw_wire_decode_device: a device byte stream -> key / ts / val columns in arrival order (records without a
  *     timestamp get Long.MIN_VALUE, StreamRecord.getTimestamp), ready for fw_push_batch_device.  The field whose
  *     role is FW_ROLE_KEY becomes the key (an integer kind), FW_ROLE_VALUE the value (integers sign-extended,
@@ -373,6 +381,7 @@ int fw_keyby_combine_push_device(fw_comm* comm, fw_op* combiner, fw_op* op, cons
 #define FW_WIRE_BYTE 4
 #define FW_WIRE_FLOAT 5
 #define FW_WIRE_BOOL 6
+#define FW_WIRE_STRING 7
 #define FW_ROLE_SKIP 0
 #define FW_ROLE_KEY 1
 #define FW_ROLE_VALUE 2
@@ -402,6 +411,10 @@ void fw_wire_destroy(fw_wire* w);
 const char* fw_wire_last_error(const fw_wire* w);
 int fw_wire_decode_device(fw_wire* w, const uint8_t* bytes, int64_t nbytes, int64_t* key, int64_t* ts, int64_t* val,
                           int64_t cap, fw_wire_stats* stats);
+/* the same with the key_hash column (int32, the key's Java hashCode: String.hashCode of a String key, 0 for the
+ * other kinds, whose hash the operator derives itself); required when the key field is a String */
+int fw_wire_decode_keyed_device(fw_wire* w, const uint8_t* bytes, int64_t nbytes, int64_t* key, int32_t* key_hash,
+                                int64_t* ts, int64_t* val, int64_t cap, fw_wire_stats* stats);
 /* rows: a device view (fw_rows_device); f64 = the rows' sum/min/max are double bits (FW_VAL_F64 aggregates);
  * out: device bytes of capacity cap; *written = n * element size */
 int fw_wire_encode_device(fw_wire* w, const fw_rows* rows, int64_t n, int32_t f64, uint8_t* out, int64_t cap,

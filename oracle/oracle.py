@@ -237,7 +237,7 @@ def run_parallel(cfg, keys, ts, vals, batch, wms, max_par, threads):
 
 
 # ---- f2: the wire format (wire_oracle.h) -------------------------------------------------------------
-WIRE_KINDS = {"long": 0, "int": 1, "double": 2, "short": 3, "byte": 4, "float": 5, "boolean": 6}
+WIRE_KINDS = {"long": 0, "int": 1, "double": 2, "short": 3, "byte": 4, "float": 5, "boolean": 6, "string": 7}
 WIRE_ROLES = {"skip": 0, "key": 1, "value": 2, "start": 3, "end": 4, "count": 5, "sum": 6, "min": 7, "max": 8}
 
 
@@ -261,6 +261,11 @@ def _wire_lib():
         L.oracle_wire_decode.restype = ctypes.c_int
         L.oracle_wire_decode.argtypes = [U8, ctypes.c_int64, ctypes.POINTER(OracleWireLayout), P, P, P, ctypes.c_int64,
                                          ctypes.POINTER(OracleWireStats)]
+        L.oracle_wire_decode_keyed.restype = ctypes.c_int
+        L.oracle_wire_decode_keyed.argtypes = [U8, ctypes.c_int64, ctypes.POINTER(OracleWireLayout), P, P, P, P,
+                                               ctypes.c_int64, ctypes.POINTER(OracleWireStats)]
+        L.oracle_string_key_id.restype = ctypes.c_int64
+        L.oracle_string_key_id.argtypes = [P, ctypes.c_int64]
         L.oracle_wire_encode.restype = ctypes.c_int64
         L.oracle_wire_encode.argtypes = [ctypes.POINTER(OracleWireLayout), P, ctypes.c_int64, ctypes.c_int32, U8,
                                          ctypes.c_int64]
@@ -300,6 +305,25 @@ class WireStream:
                                                v.ctypes.data, ctypes.addressof(buf))
         self._parts.append(bytes(buf[:n]))
 
+    def record_str(self, values, ts=None):
+        """A record whose layout may hold String fields (values: str or None for those, ints otherwise), written
+        here in Python: StreamElementSerializer's tag / timestamp, TupleSerializer's fields in order, a String
+        through StringValue.writeString (StringValue.java:789-817)."""
+        import struct
+        body = bytearray()
+        for (kind, _), x in zip(self.fields, values):
+            if kind == "string":
+                body += write_string(x)
+            else:
+                fmt = {"long": ">q", "double": ">q", "int": ">i", "float": ">I", "short": ">h", "byte": ">b",
+                       "boolean": ">B"}[kind]
+                if kind == "float":  # the value is double bits: Float.floatToIntBits((float) d)
+                    d = struct.unpack("<d", struct.pack("<q", int(x)))[0]
+                    x = struct.unpack(">I", struct.pack(">f", d))[0]
+                body += struct.pack(fmt, int(x))
+        head = struct.pack(">Bq", 0, int(ts)) if ts is not None else struct.pack(">B", 1)
+        self._parts.append(struct.pack(">I", len(head) + len(body)) + head + bytes(body))
+
     def watermark(self, wm):
         buf = (ctypes.c_uint8 * 16)()
         n = _wire_lib().oracle_wire_put_watermark(int(wm), ctypes.addressof(buf))
@@ -333,6 +357,48 @@ def wire_decode(data, fields, cap=None):
                                         ts.ctypes.data, val.ctypes.data, cap, ctypes.byref(st))
     r = st.records
     return (key[:r], ts[:r], val[:r]), {f: getattr(st, f) for f, _ in OracleWireStats._fields_}, rc
+
+
+def write_string(s):
+    """StringValue.writeString (StringValue.java:789-817): length + 1 as a base-128 varint (low group first, 0 for
+    null), then every UTF-16 char as a base-128 varint."""
+    out = bytearray()
+    if s is None:
+        return bytes([0])
+    enc = s.encode("utf-16-le")
+    units = [int.from_bytes(enc[i:i + 2], "little") for i in range(0, len(enc), 2)]
+    n = len(units) + 1
+    while n >= 0x80:
+        out.append((n | 0x80) & 0xff)
+        n >>= 7
+    out.append(n)
+    for c in units:
+        while c >= 0x80:
+            out.append((c | 0x80) & 0xff)
+            c >>= 7
+        out.append(c)
+    return bytes(out)
+
+
+def string_key_id(s):
+    """The key column's identity of a String key (oracle_string_key_id)."""
+    u = np.frombuffer(s.encode("utf-16-le"), dtype=np.uint16).copy()
+    return int(_wire_lib().oracle_string_key_id(u.ctypes.data if len(u) else None, len(u)))
+
+
+def wire_decode_keyed(data, fields, cap=None):
+    """-> (key, key_hash, ts, val) arrays, stats dict, rc (0 ok, -1 corrupt, -2 capacity)."""
+    b = np.frombuffer(bytes(data), dtype=np.uint8)
+    cap = len(b) // 6 + 1 if cap is None else cap
+    key, ts, val = (np.zeros(max(1, cap), dtype=np.int64) for _ in range(3))
+    kh = np.zeros(max(1, cap), dtype=np.int32)
+    st = OracleWireStats()
+    L = wire_layout(fields)
+    rc = _wire_lib().oracle_wire_decode_keyed(b.ctypes.data if len(b) else None, len(b), ctypes.byref(L),
+                                              key.ctypes.data, kh.ctypes.data, ts.ctypes.data, val.ctypes.data, cap,
+                                              ctypes.byref(st))
+    r = st.records
+    return (key[:r], kh[:r], ts[:r], val[:r]), {f: getattr(st, f) for f, _ in OracleWireStats._fields_}, rc
 
 
 def wire_encode(rows, fields, f64=False):

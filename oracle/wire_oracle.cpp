@@ -17,10 +17,67 @@ int field_bytes(int32_t kind) {
   }
   return -1;
 }
-int value_bytes(const oracle_wire_layout* L) {
+int value_bytes(const oracle_wire_layout* L) {  // (fixed-size fields only)
   int f = 0;
   for (int i = 0; i < L->nfields; i++) f += field_bytes(L->kind[i]);
   return f;
+}
+bool has_string(const oracle_wire_layout* L) {
+  for (int i = 0; i < L->nfields; i++)
+    if (L->kind[i] == OR_WIRE_STRING) return true;
+  return false;
+}
+uint64_t fmix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+// StringValue.readString (StringValue.java:745-786): one base-128 varint, low group first; -1 past `end`
+int64_t read_varint(const uint8_t* p, const uint8_t* end, uint32_t* out) {
+  const uint8_t* q = p;
+  if (q >= end) return -1;
+  uint32_t v = *q++;
+  if (v >= 0x80) {
+    int shift = 7;
+    uint32_t curr;
+    v &= 0x7f;
+    for (;;) {
+      if (q >= end) return -1;
+      curr = *q++;
+      if (curr < 0x80) break;
+      v |= (curr & 0x7f) << shift;
+      shift += 7;
+    }
+    v |= curr << shift;
+  }
+  *out = v;
+  return q - p;
+}
+// a String field at p: its bytes (-1 if it runs past end); *is_null, and for a non-null one its hashCode and id
+int64_t read_string(const uint8_t* p, const uint8_t* end, bool* is_null, int32_t* hash, int64_t* id) {
+  uint32_t len;
+  int64_t at = read_varint(p, end, &len);
+  if (at < 0) return -1;
+  *is_null = len == 0;
+  if (len == 0) return at;
+  len -= 1;
+  uint32_t h = 0;
+  uint64_t f = 0xcbf29ce484222325ull;
+  for (uint32_t i = 0; i < len; i++) {
+    uint32_t c;
+    const int64_t k = read_varint(p + at, end, &c);
+    if (k < 0) return -1;
+    at += k;
+    const uint16_t ch = (uint16_t)c;  // (char) c
+    h = 31u * h + ch;                 // String.hashCode
+    f = (f ^ ch) * 0x100000001b3ull;
+  }
+  *hash = (int32_t)h;
+  *id = (int64_t)fmix64(f ^ (uint64_t)len);
+  return at;
 }
 // DataInputView.readLong / readInt / readShort: big-endian
 uint64_t get_be(const uint8_t* p, int nb) {
@@ -82,43 +139,89 @@ extern "C" {
 
 int oracle_wire_decode(const uint8_t* b, int64_t n, const oracle_wire_layout* L, int64_t* key, int64_t* ts,
                        int64_t* val, int64_t cap, oracle_wire_stats* st) {
+  return oracle_wire_decode_keyed(b, n, L, key, nullptr, ts, val, cap, st);
+}
+
+int64_t oracle_string_key_id(const uint16_t* chars, int64_t n) {
+  uint64_t f = 0xcbf29ce484222325ull;
+  for (int64_t i = 0; i < n; i++) f = (f ^ chars[i]) * 0x100000001b3ull;
+  return (int64_t)fmix64(f ^ (uint64_t)n);
+}
+
+int oracle_wire_decode_keyed(const uint8_t* b, int64_t n, const oracle_wire_layout* L, int64_t* key, int32_t* kh,
+                             int64_t* ts, int64_t* val, int64_t cap, oracle_wire_stats* st) {
   std::memset(st, 0, sizeof *st);
   st->watermark = INT64_MIN;
   st->status = 0;  // StreamStatus.ACTIVE when the stream carried none
+  for (int i = 0; i < L->nfields; i++)
+    if (L->kind[i] == OR_WIRE_STRING && L->role[i] == OR_ROLE_KEY && !kh) return -3;
   const int F = value_bytes(L);
+  const bool strings = has_string(L);
   int64_t pos = 0;
   while (pos + 4 <= n) {
     const int64_t len = (int64_t)get_be(b + pos, 4);
     if (pos + 4 + len > n) break;  // a partial element: the next call's
     const uint8_t* e = b + pos + 4;
     const int tag = len > 0 ? (int8_t)e[0] : -3;  // readByte
-    const int64_t want = tag == 0 ? 9 + F : tag == 1 ? 1 + F : tag == 2 ? 9 : tag == 3 ? 29 : tag == 4 ? 5 : -1;
+    int64_t want = tag == 0 ? 9 + F : tag == 1 ? 1 + F : tag == 2 ? 9 : tag == 3 ? 29 : tag == 4 ? 5 : -1;
     if (want < 0) {
       st->bad_tag = tag;
       st->consumed = pos;
       return -1;
+    }
+    int64_t k = 0, v = 0;
+    int32_t h = 0;
+    bool null_key = false;
+    if (tag <= 1) {  // the value's fields (a String's length is only known by reading it)
+      const uint8_t* f = e + 1 + (tag == 0 ? 8 : 0);
+      const uint8_t* end = e + len;
+      int64_t at = 0;
+      bool ok = true;
+      for (int i = 0; i < L->nfields && ok; i++) {
+        if (L->kind[i] == OR_WIRE_STRING) {
+          bool is_null = false;
+          int32_t sh = 0;
+          int64_t sid = 0;
+          const int64_t m = read_string(f + at, end, &is_null, &sh, &sid);
+          if (m < 0) {
+            ok = false;
+            break;
+          }
+          if (L->role[i] == OR_ROLE_KEY) {
+            null_key = is_null;
+            k = sid;
+            h = sh;
+          }
+          at += m;
+        } else {
+          if (f + at + field_bytes(L->kind[i]) > end) {
+            ok = false;
+            break;
+          }
+          if (L->role[i] == OR_ROLE_KEY) k = field_value(L->kind[i], f + at);
+          if (L->role[i] == OR_ROLE_VALUE) v = field_value(L->kind[i], f + at);
+          at += field_bytes(L->kind[i]);
+        }
+      }
+      if (strings) want = ok ? (f - e) + at : -1;
     }
     if (len != want) {  // an element of another layout
       st->bad_tag = -2;
       st->consumed = pos;
       return -1;
     }
+    if (null_key) {
+      st->bad_tag = -4;
+      st->consumed = pos;
+      return -1;
+    }
     if (tag <= 1) {
       if (st->records >= cap) return -2;
       const int64_t r = st->records++;
-      const uint8_t* f = e + 1;
-      ts[r] = INT64_MIN;
-      if (tag == 0) {
-        ts[r] = (int64_t)get_be(f, 8);
-        f += 8;
-      }
-      key[r] = 0;
-      val[r] = 0;
-      for (int i = 0; i < L->nfields; i++) {
-        if (L->role[i] == OR_ROLE_KEY) key[r] = field_value(L->kind[i], f);
-        if (L->role[i] == OR_ROLE_VALUE) val[r] = field_value(L->kind[i], f);
-        f += field_bytes(L->kind[i]);
-      }
+      ts[r] = tag == 0 ? (int64_t)get_be(e + 1, 8) : INT64_MIN;
+      key[r] = k;
+      val[r] = v;
+      if (kh) kh[r] = h;
     } else if (tag == 2) {
       st->watermarks++;
       st->watermark = (int64_t)get_be(e + 1, 8);

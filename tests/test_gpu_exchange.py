@@ -6,7 +6,8 @@
   watermark is the minimum over subtasks (StatusWatermarkValve.java:173-191).  The union of both subtasks'
   rows must equal one oracle operator over the whole stream.  Long keys, Integer keys with negative values
   (Integer.hashCode differs from Long.hashCode) and String keys hashed by the host.
-* fw_keyby_push_device (the C-ABI exchange over the library's RCCL communicator) at world size 1.
+* fw_keyby_push_device (the C-ABI exchange over the library's RCCL communicator) at world size 1, and at world
+  size 2 with a skewed send (two GPUs).
 """
 import os
 import socket
@@ -187,3 +188,63 @@ def test_gpu_exchange_world2_operator_kinds(tmp_path, kind):
         np.testing.assert_allclose(a["sum"].view(np.float64), b["sum"].view(np.float64), rtol=1e-9)
     else:
         _same(rows, r)
+
+
+def _native_worker(rank, port, out_dir):
+    # one subtask per GPU: fw_keyby_push_device over the library's RCCL communicator.  Subtask 1 sends a quarter of
+    # subtask 0's records, so it receives more than it sent (the receive columns grow).
+    import torch
+    import torch.distributed as dist
+    from flink_amd import TumblingEventTimeWindows
+    from flink_amd.exchange import KeyGroupExchange, NativeKeyByExchange
+    from flink_amd.operator import GpuWindowOperator
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(rank)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    uid = [NativeKeyByExchange.new_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    kgr = KeyGroupExchange(MAX_PAR, WORLD, rank).key_group_range
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(1000), max_parallelism=MAX_PAR, key_group_range=kgr,
+                           device=rank)
+    ex = NativeKeyByExchange(op, WORLD, rank, uid[0])
+    dev = torch.device("cuda", rank)
+    mx = -(1 << 63)
+    for s in range(STEPS):
+        k, t, v = _native_slice(rank, s)
+        mx = max(mx, int(t.max()))
+        wm = ex.push(*(torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (k, t, v)), mx - 300)
+        op.watermark(wm)
+    op.watermark((1 << 63) - 1)
+    np.save(os.path.join(out_dir, f"rows_{rank}.npy"), op.rows())
+    ex.close()
+    op.close()
+    dist.destroy_process_group()
+
+
+def _native_slice(rank, step):
+    n = BATCH if rank == 0 else BATCH // 4
+    first = step * 2 * BATCH + rank * BATCH
+    return generate_host(0x5EED, first, n, KEYS, ts_base=0, rate=100_000, jitter=300)
+
+
+def test_gpu_native_keyby_world2_skewed(tmp_path):
+    """fw_keyby_push_device at world size 2 (per-peer ncclSend / ncclRecv offsets, the receive columns growing on
+    the subtask that receives more than it sent): the union of both subtasks' rows equals one oracle operator.
+    RCCL refuses two ranks on one device, so this needs two GPUs."""
+    import torch
+    if torch.cuda.device_count() < WORLD:
+        pytest.skip("needs 2 GPUs (RCCL: one rank per device)")
+    import torch.multiprocessing as mp
+    mp.spawn(_native_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    rows = np.concatenate([np.load(tmp_path / f"rows_{r}.npy") for r in range(WORLD)])
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000)
+    mx = [-(1 << 63)] * WORLD
+    for s in range(STEPS):
+        parts = [_native_slice(r, s) for r in range(WORLD)]
+        for r in range(WORLD):
+            mx[r] = max(mx[r], int(parts[r][1].max()))
+        for src in range(WORLD):
+            ref.process(*parts[src])
+        ref.watermark(min(m - 300 for m in mx))
+    ref.watermark((1 << 63) - 1)
+    _same(rows, ref.rows())

@@ -185,3 +185,94 @@ def test_gpu_wire_encode_fired_rows_and_decode_into_the_operator():
     assert out == orc.wire_encode(rows, out_fields)
     op.close()
     c.close()
+
+
+# ---- String fields: WindowWordCount's Tuple2<String, Integer> channel
+S2 = [("string", "key"), ("int", "value")]
+
+
+def _word_channel(n, seed=3, every=5000, extra=()):
+    """WordCountData's tokens (tests/golden/wordcount_tokens.json) as Tuple2<String, Integer>(word, 1) records with
+    timestamps i // 2000 ms (C1), a watermark every `every` records."""
+    import json
+    import os
+    toks = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "wordcount_tokens.json")))["tokens"]
+    words = sorted(set(toks)) + list(extra)
+    rng = np.random.default_rng(seed)
+    idx = rng.integers(0, len(words), n)
+    w = orc.WireStream(S2)
+    for i, j in enumerate(idx):
+        w.record_str([words[j], 1], ts=i // 2000)
+        if (i + 1) % every == 0:
+            w.watermark(i // 2000)
+    return w.bytes(), words, idx
+
+
+def test_gpu_wire_string_keys_match_the_oracle():
+    # ASCII words plus words with two- and three-byte chars, mixed with watermarks; columns and stats bit-exact
+    data, words, idx = _word_channel(40_000, extra=("wörd", "日本", "€"))
+    c = _codec(S2)
+    import torch
+    t = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
+    (k, ts, v, kh), gs = c.decode(t)
+    (rk, rkh, rt, rv), rs, rc = orc.wire_decode_keyed(data, S2)
+    assert rc == 0
+    for a, b in ((k, rk), (kh, rkh), (ts, rt), (v, rv)):
+        np.testing.assert_array_equal(a.cpu().numpy(), b)
+    for f in ("records", "watermarks", "consumed", "watermark"):
+        assert gs[f] == rs[f], f
+    c.close()
+
+
+def test_gpu_wire_word_count_channel_into_the_operator():
+    # C1 (ii) from the wire: decode WindowWordCount's channel on the GPU, push (key id, String.hashCode) into a
+    # hashed-key operator, window(Tumbling 5 s).sum(1); rows equal the C1 oracle keyed by the word
+    from flink_amd import TumblingEventTimeWindows
+    from flink_amd.keygroups import string_key_id
+    from flink_amd.operator import GpuWindowOperator
+    from flink_amd.windowing import CountSumMinMax
+    import torch
+    n = 120_000
+    data, words, idx = _word_channel(n)
+    c = _codec(S2)
+    t = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
+    (k, ts, v, kh), st = c.decode(t)
+    assert st["records"] == n
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(5000), CountSumMinMax("int"), key_type="hashed")
+    op.process_batch(k, ts, v, kh)
+    op.advance_watermark(st["watermark"])
+    op.advance_watermark((1 << 63) - 1)
+    g = op.drain_rows()
+    op.close()
+    c.close()
+    ids = {string_key_id(w): j for j, w in enumerate(words)}
+    assert len(ids) == len(words)
+    g["key"] = [ids[int(x)] for x in g["key"]]
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=5000, value_type="i32")
+    ref.process(idx.astype(np.int64), np.arange(n, dtype=np.int64) // 2000, np.ones(n, dtype=np.int64))
+    ref.watermark(st["watermark"])
+    ref.watermark((1 << 63) - 1)
+    r = ref.rows()
+    order = lambda a: np.lexsort((a["start"], a["key"]))  # noqa: E731
+    g, r = g[order(g)], r[order(r)]
+    for f in ("key", "start", "end", "count", "sum", "min", "max"):
+        np.testing.assert_array_equal(g[f], r[f])
+    assert int(g["count"].sum()) == n
+
+
+def test_gpu_wire_string_errors():
+    from flink_amd import _native as N
+    import torch
+    w = orc.WireStream(S2)
+    w.record_str(["fine", 1], ts=1)
+    w.record_str([None, 2], ts=2)  # a null key
+    c = _codec(S2)
+    with pytest.raises(N.NativeError) as ei:
+        c.decode(torch.from_numpy(np.frombuffer(w.bytes(), dtype=np.uint8).copy()).cuda())
+    assert ei.value.code == N.FW_ERR_STATE and "null String key" in str(ei.value)
+    w = orc.WireStream(S2)
+    w.record_str(["y" * 60, 1], ts=1)  # 78 bytes with its prefix: beyond the decoder's 64
+    with pytest.raises(N.NativeError) as ei:
+        c.decode(torch.from_numpy(np.frombuffer(w.bytes(), dtype=np.uint8).copy()).cuda())
+    assert ei.value.code == N.FW_ERR_STATE
+    c.close()

@@ -94,3 +94,50 @@ def test_encode_rows_and_decode_them_back():
     (k, t, v), st, rc = orc.wire_decode(b, back)
     assert rc == 0 and list(k) == list(rows["key"]) and list(v) == list(rows["sum"])
     assert list(t) == list(rows["end"] - 1)  # window.maxTimestamp()
+
+
+# ---- String fields (StringSerializer -> StringValue.writeString / readString, StringValue.java:745-817)
+S2 = [("string", "key"), ("int", "value")]  # WindowWordCount's Tuple2<String, Integer>
+
+
+def test_string_value_pinned_by_reference_bytes():
+    # the heap backend wrote the key "key1" with StringSerializer: StringValue.writeString's bytes
+    from flink_amd.keygroups import string_hash_code, string_key_id
+    fx = json.load(open(os.path.join(HERE, "golden", "wire_fixture.json")))
+    sv = bytes.fromhex(fx["timer_entry_hex"])[:5]
+    assert orc.write_string("key1") == sv
+    el = struct.pack(">IBq", 1 + 8 + len(sv) + 4, 0, 2999) + sv + struct.pack(">i", 3)
+    (k, kh, t, v), st, rc = orc.wire_decode_keyed(el, S2)
+    assert rc == 0 and st["records"] == 1 and st["consumed"] == len(el)
+    assert (int(kh[0]), int(k[0]), int(t[0]), int(v[0])) == (string_hash_code("key1"), string_key_id("key1"), 2999, 3)
+    assert orc.string_key_id("key1") == string_key_id("key1")
+
+
+def test_string_fields_varints_and_nulls():
+    from flink_amd.keygroups import string_hash_code, string_key_id
+    # chars of one, two and three varint bytes, the empty string, a length needing a two-byte varint
+    words = ["a", "wörd", "日本語", "", "x" * 130, "€uro"]
+    assert orc.write_string("x" * 130)[:2] == bytes([131 & 0x7f | 0x80, 131 >> 7])
+    assert orc.write_string("日")[1:] == bytes([0xE5 & 0x7f | 0x80, (0x65E5 >> 7) & 0x7f | 0x80, 0x65E5 >> 14])
+    fields = [("long", "skip"), ("string", "key"), ("string", "skip"), ("int", "value")]
+    w = orc.WireStream(fields)
+    for i, s in enumerate(words):
+        w.record_str([i, s, None if i % 2 else "skipped", i * 10], ts=i if i % 3 else None)
+        w.watermark(100 + i)
+    (k, kh, t, v), st, rc = orc.wire_decode_keyed(w.bytes(), fields)
+    assert rc == 0 and st["records"] == len(words) and st["watermarks"] == len(words)
+    assert list(kh) == [string_hash_code(s) for s in words]
+    assert list(k) == [string_key_id(s) for s in words]
+    assert list(v) == [i * 10 for i in range(len(words))]
+    # a String key needs the hash column; a null key is a corrupt element
+    (_, _, _), _, rc = orc.wire_decode(w.bytes(), fields)
+    assert rc == -3
+    bad = orc.WireStream(fields)
+    bad.record_str([1, "ok", "x", 1], ts=1)
+    bad.record_str([2, None, "x", 2], ts=2)
+    _, st, rc = orc.wire_decode_keyed(bad.bytes(), fields)
+    assert rc == -1 and st["bad_tag"] == -4 and st["records"] == 1
+    # an element whose length prefix disagrees with its String fields
+    short = struct.pack(">IBq", 9 + 4, 0, 5) + orc.write_string("abcdef")[:4]
+    _, st, rc = orc.wire_decode_keyed(short, [("string", "key")])
+    assert rc == -1 and st["bad_tag"] == -2
