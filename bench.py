@@ -179,7 +179,8 @@ def main():
         args.zipf = preset["zipf"]
     args.zipf = args.zipf or None
     if args.traffic is None:
-        for cand in (f"traffic_r02_{w}.json", f"traffic_r01_{w}.json" if w != "c2" else "traffic_r01.json"):
+        for cand in (f"traffic_r03_{w}.json", f"traffic_r02_{w}.json",
+                     f"traffic_r01_{w}.json" if w != "c2" else "traffic_r01.json"):
             args.traffic = os.path.join(ROOT, "profiles", cand)
             if os.path.exists(args.traffic):
                 break
@@ -344,12 +345,14 @@ def main():
         L.fw_profile_read(op._h, ms, nl, 1)
         merged = (st1["state_merges"] - st0["state_merges"]) / args.steps
         per_launch_records = per_gpu_records / args.steps
-        tr = {}
+        tr, tr_all, tr_src = {}, None, None
         if os.path.exists(args.traffic):
             with open(args.traffic) as f:
                 t = json.load(f)
             if t.get("workload", "c2") == w:  # PMC bytes per launch of this workload (tools/traffic.py)
                 tr = t.get("per_launch_bytes", {})
+                tr_all = t.get("bytes_per_record_all_kernels")
+                tr_src = os.path.relpath(args.traffic, ROOT)
         alg = balg * per_launch_records
         for i in range(N.FW_NUM_KERNELS):
             name = L.fw_kernel_name(i).decode()
@@ -372,6 +375,7 @@ def main():
                     "impl_bytes_per_launch": kd["impl_bytes"], "impl_frac": kd["impl_frac"],
                     "traffic_over_alg": None if traffic is None else round(traffic / alg, 3),
                     "traffic_per_record": None if traffic is None else round(traffic / per_launch_records, 2),
+                    "traffic_all_kernels_per_record": tr_all, "traffic_source": tr_src,
                     "basis": "SURVEY §8d B_alg x records per launch / the kernel's average HIP-event duration"}
     kernels_iso = None
     if iso_steps:

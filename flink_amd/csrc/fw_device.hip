@@ -553,7 +553,7 @@ __host__ __forceinline__ int stream_mode(const DevCfg& c) {
   return c.panes ? M_PANE : M_GEN;
 }
 
-// single-pass scatter (k_scatter_staged<..., true>): its slots behind the P run lengths, rsv[P + x]
+// single-pass scatter (k_scatter_rsv): its slots behind the P run lengths, rsv[P + x]
 enum { RSV_OVER = 0, RSV_KG = 1, RSV_TS = 2, RSV_LATE = 4 };  // RSV_LATE: 64-bit (FW_RSV_WORDS in all)
 
 // ---- K1: classify + partition histogram.  hist is (P+1) x T, partition-major; row P counts
@@ -819,17 +819,13 @@ __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(D
 // compact form or a run longer than rcap sets rsv[P] (RSV_OVER): then the batch goes through classify, scan and the
 // offset scatter after all (those kernels are gated on rsv[P] and return at once without it).  The error and late
 // counts wait in rsv until the gated classify adds them to the status (RSV_* slots), so a redone batch counts once.
-template <int MODE, int RR, bool RSV = false>
-__global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_staged(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
-                                                                   const int64_t* __restrict__ ts,
-                                                                   const int64_t* __restrict__ val,
-                                                                   const int32_t* __restrict__ kh, int64_t n, int32_t T,
-                                                                   const uint32_t* __restrict__ offs,
-                                                                   PRec* __restrict__ part, DevSide side, Status* st,
-                                                                   const uint32_t* __restrict__ gate, uint32_t* rsv,
-                                                                   int64_t rcap) {
+template <int MODE, int RR, bool RSV>
+__device__ __forceinline__ void scatter_staged_body(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
+                                                    const int64_t* __restrict__ ts, const int64_t* __restrict__ val,
+                                                    const int32_t* __restrict__ kh, int64_t n, int32_t T,
+                                                    const uint32_t* __restrict__ offs, PRec* __restrict__ part,
+                                                    DevSide side, Status* st, uint32_t* rsv, int64_t rcap) {
   specialize<MODE>(c);
-  if (!RSV && gate && !gate[0]) return;  // (the batch went through the single pass)
   extern __shared__ __attribute__((aligned(16))) uint8_t sraw[];
   i64x2* stg = reinterpret_cast<i64x2*>(sraw);          // RR: the round's records sorted by partition
   uint16_t* sp = reinterpret_cast<uint16_t*>(stg + RR);  // RR: their partitions
@@ -960,6 +956,27 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_staged(DevCfg c, in
   } else if (late) {
     atomicAdd(&st->late_dropped, late);
   }
+}
+// the offset form (gate: the single pass's RSV_OVER word, the batch comes here only when it is set; nullptr = always)
+template <int MODE, int RR>
+__global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_staged(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
+                                                                   const int64_t* __restrict__ ts,
+                                                                   const int64_t* __restrict__ val,
+                                                                   const int32_t* __restrict__ kh, int64_t n, int32_t T,
+                                                                   const uint32_t* __restrict__ offs,
+                                                                   PRec* __restrict__ part, DevSide side, Status* st,
+                                                                   const uint32_t* __restrict__ gate) {
+  if (gate && !gate[0]) return;  // (the batch went through the single pass)
+  scatter_staged_body<MODE, RR, false>(c, wm, key, ts, val, kh, n, T, offs, part, side, st, nullptr, 0);
+}
+// the single pass (tumbling windows, dense regions)
+template <int RR>
+__global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_rsv(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
+                                                                const int64_t* __restrict__ ts,
+                                                                const int64_t* __restrict__ val,
+                                                                const int32_t* __restrict__ kh, int64_t n, int32_t T,
+                                                                PRec* __restrict__ part, uint32_t* rsv, int64_t rcap) {
+  scatter_staged_body<M_TUMB, RR, true>(c, wm, key, ts, val, kh, n, T, nullptr, part, DevSide{}, nullptr, rsv, rcap);
 }
 
 // ---- K2b: ordered compaction of the ordered-path records of a tile (skipped by tiles that have none).
@@ -5007,8 +5024,14 @@ __global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const 
     return;
   }
   const bool cmp = SRC == DT_RECS && c.compact && !*c.wide;
-  if (KW && (!cmp || (c.diag & DIAG_DT_WIDE))) {  // a batch without compact words: the wide launch takes it
-    if (threadIdx.x == 0) prog.done[p] = 0;
+  // a batch without compact words: the wide launch takes it.  That launch runs only in a resumed sequence (a
+  // region the compact table cannot take is rare: a record far from the watermark), so the first launch suspends
+  // the push and the host resumes it with both launches
+  if (KW && (!cmp || (c.diag & DIAG_DT_WIDE))) {
+    if (threadIdx.x == 0) {
+      prog.done[p] = 0;
+      if (!resume) atomicOr(&st->suspended, (int)FW_SUSP_AGG);
+    }
     return;
   }
   const unsigned long long t0 = FW_DT_TIMING ? __builtin_amdgcn_s_memtime() : 0;
@@ -5036,6 +5059,7 @@ __global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const 
     tb.passes[p] = (uint8_t)min(hb, 24);
     if (wide) {
       prog.done[p] = 0;
+      if (!resume) atomicOr(&st->suspended, (int)FW_SUSP_AGG);
     } else if (lost) {
       atomicOr(&st->flags, FW_STATUS_STATE_LOST);
       prog.done[p] = 1;
@@ -5064,19 +5088,22 @@ __global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const 
 }
 
 // per watermark: the due regions' windows with maxTimestamp <= wm fire (FIRE / FIRE_AND_PURGE and the GC timer
-// coincide with lateness 0); the other entries are copied densely into the region's other buffer
+// coincide with lateness 0); the other entries are copied densely into the region's other buffer.  A workgroup
+// first counts its region's rows (the entries' end / count sector only), reserves them with one atomic on the
+// fired-row counter (per-wave reservations on that one address serialised the whole grid), then writes rows and
+// survivors.
 constexpr int DT_FIRE_U = 4;
 __global__ __launch_bounds__(FW_FIRE_THREADS) void k_dt_fire(DevCfg c, int64_t wm, DevTable tb, DevRows out, Status* st) {
   const int32_t p = blockIdx.x;
   // a suspended push has not finished updating the state: the host resumes it and fires again
   if (tb.next_timer[p] > wm || __hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  __shared__ int surv_s;
+  __shared__ int surv_s, rows_s;
   __shared__ long long nt_s;
-  __shared__ unsigned long long fired_s;
+  __shared__ unsigned long long base_s;
   if (threadIdx.x == 0) {
     surv_s = 0;
+    rows_s = 0;
     nt_s = LMAX;
-    fired_s = 0;
   }
   __syncthreads();
   const int X = tb.cur[p], Y = X ^ 1;
@@ -5085,33 +5112,62 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_dt_fire(DevCfg c, int64_t w
   Entry* __restrict__ dst = tb.ent[Y] + base;
   const int32_t live = tb.live[p];
   const int lane = __lane_id();
+  // 1. the region's rows: windows with maxTimestamp <= wm and contents (WindowOperator.java:452-459)
+  int mine = 0;
+  for (int32_t i0 = 0; i0 < live; i0 += FW_FIRE_THREADS * DT_FIRE_U) {
+    i64x2 ec[DT_FIRE_U];  // {end, cnt}
+#pragma unroll
+    for (int u = 0; u < DT_FIRE_U; u++) {
+      const int32_t i = i0 + u * FW_FIRE_THREADS + (int32_t)threadIdx.x;
+      ec[u] = reinterpret_cast<const i64x2*>(src + (i < live ? i : live - 1))[1];
+    }
+#pragma unroll
+    for (int u = 0; u < DT_FIRE_U; u++) {
+      const int32_t i = i0 + u * FW_FIRE_THREADS + (int32_t)threadIdx.x;
+      mine += i < live && jsub(ec[u].x, 1) <= wm && ec[u].y > 0;
+    }
+  }
+  mine += __shfl_xor(mine, 1, 64);
+  mine += __shfl_xor(mine, 2, 64);
+  mine += __shfl_xor(mine, 4, 64);
+  mine += __shfl_xor(mine, 8, 64);
+  mine += __shfl_xor(mine, 16, 64);
+  mine += __shfl_xor(mine, 32, 64);
+  if (lane == 0 && mine) atomicAdd(&rows_s, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    base_s = rows_s ? atomicAdd(&st->out_rows, (unsigned long long)rows_s) : 0ull;
+    if (rows_s) atomicAdd(&st->fired_total, (unsigned long long)rows_s);
+    rows_s = 0;
+  }
+  __syncthreads();
+  const unsigned long long rbase = base_s;
+  // 2. rows at the reserved range, survivors densely into the other buffer
   long long nt = LMAX;
-  unsigned long long fired = 0;
   for (int32_t i0 = 0; i0 < live; i0 += FW_FIRE_THREADS * DT_FIRE_U) {
     Entry e[DT_FIRE_U];
 #pragma unroll
     for (int u = 0; u < DT_FIRE_U; u++) {
       const int32_t i = i0 + u * FW_FIRE_THREADS + (int32_t)threadIdx.x;
-      if (i < live) e[u] = src[i];
+      e[u] = src[i < live ? i : live - 1];
     }
 #pragma unroll
     for (int u = 0; u < DT_FIRE_U; u++) {
       const int32_t i = i0 + u * FW_FIRE_THREADS + (int32_t)threadIdx.x;
       const bool valid = i < live;
       const bool due = valid && jsub(e[u].end, 1) <= wm;
-      const bool row = due && e[u].cnt > 0;  // contents != null (WindowOperator.java:452-459)
+      const bool row = due && e[u].cnt > 0;
       const bool keep = valid && !due;
       const uint64_t rm = __ballot(row), km = __ballot(keep);
-      unsigned long long rb = 0;
-      int sb = 0;
+      int rb = 0, sb = 0;
       if (lane == 0) {
-        if (rm) rb = atomicAdd(&st->out_rows, (unsigned long long)__popcll(rm));
+        if (rm) rb = atomicAdd(&rows_s, __popcll(rm));
         if (km) sb = atomicAdd(&surv_s, __popcll(km));
       }
       rb = __shfl(rb, 0, 64);
       sb = __shfl(sb, 0, 64);
       if (row) {
-        const unsigned long long pos = rb + __popcll(rm & lanemask_lt());
+        const unsigned long long pos = rbase + (unsigned long long)(rb + __popcll(rm & lanemask_lt()));
         if ((int64_t)pos < out.cap)
           write_row(c, out, pos, e[u]);
         else
@@ -5121,14 +5177,11 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_dt_fire(DevCfg c, int64_t w
         dst[sb + __popcll(km & lanemask_lt())] = e[u];
         nt = min(nt, (long long)jsub(e[u].end, 1));
       }
-      if (lane == 0) fired += __popcll(rm);
     }
   }
   if (nt != LMAX) atomicMin(&nt_s, nt);
-  if (fired) atomicAdd(&fired_s, fired);
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (fired_s) atomicAdd(&st->fired_total, fired_s);
     tb.cur[p] = (uint8_t)Y;
     tb.live[p] = surv_s;
     tb.next_timer[p] = nt_s;
@@ -5368,16 +5421,16 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
     const bool tumb = stream_mode(c) == M_TUMB;
     if (tumb && big)
       hipLaunchKernelGGL((k_scatter_staged<M_TUMB, 8192>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n,
-                         T, o, part, side, st, gate, (uint32_t*)nullptr, (int64_t)0);
+                         T, o, part, side, st, gate);
     else if (tumb)
       hipLaunchKernelGGL((k_scatter_staged<M_TUMB, 4096>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n,
-                         T, o, part, side, st, gate, (uint32_t*)nullptr, (int64_t)0);
+                         T, o, part, side, st, gate);
     else if (big)
       hipLaunchKernelGGL((k_scatter_staged<M_PANE, 8192>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n,
-                         T, o, part, side, st, gate, (uint32_t*)nullptr, (int64_t)0);
+                         T, o, part, side, st, gate);
     else
       hipLaunchKernelGGL((k_scatter_staged<M_PANE, 4096>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n,
-                         T, o, part, side, st, gate, (uint32_t*)nullptr, (int64_t)0);
+                         T, o, part, side, st, gate);
   } else
   switch (stream_mode(c)) {
     case M_TUMB:
@@ -5409,17 +5462,16 @@ void launch_scatter_rsv(const DevCfg& c, int64_t wm, const int64_t* key, const i
                     (FW_TILE_THREADS / 64 + 1) * sizeof(uint32_t);
   static bool attr = false;
   if (!attr) {  // LDS beyond 64 KB
-    (void)hipFuncSetAttribute((const void*)k_scatter_staged<M_TUMB, 8192, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_scatter_staged<M_TUMB, 4096, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_scatter_rsv<8192>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_scatter_rsv<4096>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  const uint32_t* no = nullptr;
   if (big)
-    hipLaunchKernelGGL((k_scatter_staged<M_TUMB, 8192, true>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val,
-                       kh, n, T, no, part, DevSide{}, (Status*)nullptr, no, rsv, rcap);
+    hipLaunchKernelGGL(k_scatter_rsv<8192>, dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n, T, part,
+                       rsv, rcap);
   else
-    hipLaunchKernelGGL((k_scatter_staged<M_TUMB, 4096, true>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val,
-                       kh, n, T, no, part, DevSide{}, (Status*)nullptr, no, rsv, rcap);
+    hipLaunchKernelGGL(k_scatter_rsv<4096>, dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n, T, part,
+                       rsv, rcap);
 }
 
 // panes: maxTimestamp of the earliest window ending after wm (windows [s, s + size), s = offset mod slide)
@@ -5447,11 +5499,12 @@ void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint
       launch_scan(h.chunk_base, (int64_t)c.P + 1, h.scan_tmp, s);
     }
   }
-  if (c.dense) {  // the compact table first; the wide launch takes the regions it left
+  if (c.dense) {  // the compact table; in a resumed sequence the wide launch takes the regions it left
     hipLaunchKernelGGL((k_dt_aggregate<DT_RECS, true>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs,
                        T, tb, prog, resume, st, rsv, rcap);
-    hipLaunchKernelGGL((k_dt_aggregate<DT_RECS, false>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs,
-                       T, tb, prog, 1, st, rsv, rcap);
+    if (resume)
+      hipLaunchKernelGGL((k_dt_aggregate<DT_RECS, false>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part,
+                         offs, T, tb, prog, 1, st, rsv, rcap);
     return;
   }
   const dim3 b(FW_AGG_THREADS);

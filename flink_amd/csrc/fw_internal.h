@@ -371,6 +371,7 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
 // p * rcap + rsv[p]); rsv holds P + FW_RSV_WORDS words, zeroed before the launch.  When rsv[P] is set after it, the
 // batch goes through launch_classify_hist / launch_scan / launch_scatter gated on rsv (they do nothing otherwise).
 #define FW_RSV_WORDS 8
+#define FW_RSV_WIDE 3  // rsv[P + FW_RSV_WIDE]: the batch's DevCfg::wide word when it took the single pass
 bool rsv_eligible(const DevCfg& c);
 void launch_scatter_rsv(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
                         const int32_t* kh, int64_t n, int32_t T, PRec* part, uint32_t* rsv, int64_t rcap, hipStream_t_ s);

@@ -59,6 +59,8 @@ struct Scratch {
   // dense batches: the single-pass scatter's run lengths and flags (fwdev::launch_scatter_rsv), P + FW_RSV_WORDS
   uint32_t* rsv = nullptr;
   bool single = false;  // the set's latest batch went through it (its runs are then at p * fw_op::rcap ...)
+  // DevCfg::wide of the set's latest batch: a word of rsv (zeroed with it) when the batch took the single pass
+  int32_t* wide_word(int32_t P) const { return single ? reinterpret_cast<int32_t*>(rsv + P + FW_RSV_WIDE) : wide; }
   // the ordered-path rows of the batch: scanned counts per tile, then raw counts
   const uint32_t* srow(int32_t P) const { return gather ? gsrow : hist + (int64_t)P * T; }
   // the partitions' runs in part: offsets offs()[p * offT()] (a gathered batch: regrouped, virtual offsets)
@@ -484,7 +486,7 @@ int settle(fw_op* op) {
     c.compact = S.compact;
     c.cbase = S.cbase;
     c.ord_base = S.ord_base;
-    c.wide = S.wide;
+    c.wide = S.wide_word(op->dc.P);
     if (S.partials) {  // a partials push: only its merge can have suspended
       timed(op, K_AGGREGATE, [&] {
         fwdev::launch_pmerge(c, S.pparts, S.hist, S.T, op->tb, op->prog, 1, op->d_status, op->stream);
@@ -648,7 +650,8 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
     c.taint_epoch = op->taint_epoch;
     HIP_OR_RETURN(op, hipMemsetAsync(&op->d_status->taint_any, 0, sizeof(int32_t), bs));
   }
-  if (c.compact) HIP_OR_RETURN(op, hipMemsetAsync(S.wide, 0, sizeof(int32_t), bs));
+  if (single) c.wide = reinterpret_cast<int32_t*>(S.rsv + c.P + FW_RSV_WIDE);  // (zeroed with rsv below)
+  else if (c.compact) HIP_OR_RETURN(op, hipMemsetAsync(S.wide, 0, sizeof(int32_t), bs));
   if (gather) {
     // classify, tile-local partition sort, runs table, ordered-path compaction: one pass over the input
     timed(op, K_SCATTER, [&] {
@@ -716,7 +719,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   cc.by_val = S.byv;
   cc.compact = c.compact;
   cc.cbase = c.cbase;
-  cc.wide = S.wide;
+  cc.wide = c.wide;
   // a partition can outgrow one aggregate workgroup (hot keys) only when the batch is longer than a chunk
   const bool split = !cc.dense && (cc.wpr == 1 || cc.panes) && n > FW_AGG_CHUNK;
   if (split && (rc = ensure_hot(op))) return rc;

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Recompute a bench line's roofline from the rocprofv3 kernel traces under profiles/ (VERDICT r02 item 3).
+
+A bench line prices its dominant timing bucket (bench.py `roofline.kernel`, one of fw_kernel_name's buckets) at
+B_alg x records per launch over the bucket's average HIP-event duration; `roofline.isolated` does the same over
+a pass with synchronous input.  Here the same figures come from rocprofv3 kernel traces of the same command:
+the bucket's kernels (tools/traffic.py BUCKETS), each kernel's dispatches of the timed steps (its last
+steps/(steps+warmup) of its dispatches), their durations summed and divided by the timed steps.
+
+usage: tools/roofline_check.py BENCH_JSON --async-trace CSV --sync-trace CSV --steps S --warmup W
+"""
+import argparse
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from traffic import bucket_of, short  # noqa: E402
+
+
+def bucket_ms(trace, steps, warmup):
+    per = defaultdict(list)
+    with open(trace) as f:
+        for r in csv.DictReader(f):
+            per[short(r["Kernel_Name"])].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    out = defaultdict(float)
+    for k, v in per.items():
+        b = bucket_of(k)
+        if not b:
+            continue
+        v.sort()
+        keep = max(1, round(len(v) * steps / (steps + warmup)))
+        out[b] += sum(e - s for s, e in v[-keep:]) / 1e6 / steps
+    return dict(out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("bench_json")
+    ap.add_argument("--async-trace", required=True)
+    ap.add_argument("--sync-trace", required=True)
+    ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("--warmup", type=int, required=True)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    line = json.loads([l for l in open(a.bench_json) if l.startswith("{")][-1])
+    rf = line["roofline"]
+    alg, peak, dom = rf["alg_bytes_per_launch"], rf["peak"], rf["kernel"]
+    ms_a = bucket_ms(a.async_trace, a.steps, a.warmup)
+    ms_s = bucket_ms(a.sync_trace, a.steps, a.warmup)
+    frac = lambda ms: alg / (ms * 1e-3) / 1e9 / peak  # noqa: E731
+    res = {"workload": line["config"]["workload"], "dominant_bucket": dom, "alg_bytes_per_launch": alg,
+           "line": {"frac": rf["frac"], "avg_ms": line["kernels"][dom]["avg_ms"],
+                    "isolated_frac": rf.get("isolated", {}).get("frac"),
+                    "isolated_avg_ms": rf.get("isolated", {}).get("avg_ms")},
+           "rocprof": {"async_bucket_ms": ms_a, "sync_bucket_ms": ms_s,
+                       "frac": round(frac(ms_a[dom]), 4), "isolated_frac": round(frac(ms_s[dom]), 4)}}
+    res["rel_diff"] = {"frac": round(res["rocprof"]["frac"] / rf["frac"] - 1, 4),
+                       "isolated_frac": (round(res["rocprof"]["isolated_frac"] / rf["isolated"]["frac"] - 1, 4)
+                                         if rf.get("isolated") else None)}
+    print(json.dumps(res, indent=1))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

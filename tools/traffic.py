@@ -9,7 +9,11 @@ each kernel, and derives HBM bytes as MI355X_MICROARCH.md §HBM prescribes:
 The correction factor for reads is checked against k_classify_hist, whose reads are known exactly
 (16 B per record: key + ts), and the calibration is printed beside the result.
 
-usage: tools/traffic.py [pmc_dir] [--records N] [--out profiles/traffic_rNN.json]
+Bytes are per bench step (one push + one watermark), summed per bench timing bucket (BUCKETS), over the timed
+steps only (each kernel's last steps/(steps+warmup) of its dispatches), so a run of steps >= one firing period
+averages the firings in.
+
+usage: tools/traffic.py [pmc_dir] --steps S --warmup W [--records N] [--out profiles/traffic_rNN_W.json]
 """
 import argparse
 import csv
@@ -24,78 +28,98 @@ def short(name):
     return n.split("(")[0].replace("void ", "").split("<")[0].strip()  # k_aggregate<2, false> -> k_aggregate
 
 
-def load(pmc_dir, last=0):
-    vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per-dispatch values]
+# bench.py's timing buckets (fw_kernel_name) and the kernels each one launches
+BUCKETS = {
+    "k_classify_hist": ("k_classify_hist", "k_taint"),
+    "k_scan": ("k_scan_blocks", "k_scan_top", "k_scan_add"),
+    "k_scatter": ("k_scatter_rsv", "k_scatter_staged", "k_scatter", "k_scatter_ordered", "k_stage"),
+    "k_aggregate": ("k_aggregate", "k_dt_aggregate", "k_hll_update", "k_chunk_plan", "k_pmerge"),
+    "k_slow": ("k_slow",),
+    "k_fire": ("k_fire", "k_fire_panes", "k_dt_fire"),
+    "k_tdigest": ("k_td_", "rocprim"),
+}
+
+
+def bucket_of(kernel):
+    for b, members in BUCKETS.items():
+        for m in members:
+            if kernel == m or (m.endswith("_") and kernel.startswith(m)) or (m == "rocprim" and kernel.startswith(m)):
+                return b
+    return None
+
+
+def load(pmc_dir, keep_frac=1.0):
+    """kernel -> counter -> summed value over the kept dispatches (each kernel's last keep_frac of its dispatches:
+    the bench's timed steps follow its warmup), and the kept dispatch counts."""
+    vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per-dispatch values, in order]
     for f in sorted(glob.glob(os.path.join(pmc_dir, "p*", "run_counter_collection.csv"))):
         per = defaultdict(float)
         names = {}
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                key = (r["Dispatch_Id"], r["Counter_Name"])
+                key = (int(r["Dispatch_Id"]), r["Counter_Name"])
                 per[key] += float(r["Counter_Value"])  # sum over dimensions (XCDs / instances)
-                names[r["Dispatch_Id"]] = short(r["Kernel_Name"])
-        for (d, cn), v in per.items():
+                names[int(r["Dispatch_Id"])] = short(r["Kernel_Name"])
+        for (d, cn), v in sorted(per.items()):
             vals[names[d]][cn].append(v)
-    # `last`: average only each kernel's last dispatches (the bench's timed steps follow its warmup)
-    cut = (lambda v: v[-last:]) if last else (lambda v: v)
-    return {k: {c: sum(cut(v)) / len(cut(v)) for c, v in cs.items()} | {"_dispatches": max(len(cut(v)) for v in cs.values())}
-            | {"_total_dispatches": max(len(v) for v in cs.values())} | {"_sum_" + c: sum(v) for c, v in cs.items()}
-            for k, cs in vals.items()}
+    out = {}
+    for k, cs in vals.items():
+        o = {}
+        for c, v in cs.items():
+            keep = int(len(v) * keep_frac + 1e-9)  # (a kernel of the warmup steps only keeps nothing)
+            o[c] = sum(v[-keep:]) if keep else 0.0
+            o["_n"] = keep
+        if o["_n"]:
+            out[k] = o
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("pmc_dir", nargs="?", default="gpurun_out/pmc")
     ap.add_argument("--records", type=int, default=1 << 24, help="records per push (bench --batch)")
+    ap.add_argument("--steps", type=int, required=True, help="the bench's timed steps (bench --steps)")
+    ap.add_argument("--warmup", type=int, required=True, help="the bench's warmup steps (bench --warmup)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--workload", default="c2", help="bench --workload the passes ran (recorded for bench.py)")
-    ap.add_argument("--last", type=int, default=0, help="average only each kernel's last N dispatches")
     a = ap.parse_args()
-    k = load(a.pmc_dir, a.last)
-    res = {}
+    k = load(a.pmc_dir, a.steps / (a.steps + a.warmup))
+    res, per_step = {}, defaultdict(float)
     for name, c in sorted(k.items()):
-        rd = c.get("FETCH_SIZE")
-        wr = c.get("WRITE_SIZE")
-        res[name] = {
-            "dispatches": c["_dispatches"],
-            "fetch_size_kib": rd,
-            "write_size_kib": wr,
-            "read_bytes": None if rd is None else rd * 1024 * 2,
-            "write_bytes": None if wr is None else wr * 1024,
-        }
-        for extra in ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"):
-            if extra in c:
-                res[name][extra] = c[extra]
-        r = res[name]
-        if r["read_bytes"] is not None and r["write_bytes"] is not None:
-            r["hbm_bytes"] = r["read_bytes"] + r["write_bytes"]
-    # bench.py's timing buckets: the HLL register update is timed with k_aggregate, the pane fire is k_fire,
-    # the t-digest compression (k_td_* and its rocPRIM radix sorts) is k_tdigest
-    per_launch = {n: r.get("hbm_bytes") for n, r in res.items()}
-    td_parts = tuple(n for n in res if n.startswith("k_td_") or n.startswith("rocprim"))
-    if "k_td_keys" in k:  # several dispatches per push (the radix sorts' passes): bytes per push over all pushes
-        pushes = k["k_td_keys"]["_total_dispatches"]
-        per_launch["k_tdigest"] = sum(k[x].get("_sum_FETCH_SIZE", 0) * 2048 + k[x].get("_sum_WRITE_SIZE", 0) * 1024
-                                      for x in td_parts) / pushes
-    for bucket, parts in (("k_aggregate", ("k_aggregate", "k_hll_update")), ("k_fire", ("k_fire", "k_fire_panes"))):
-        vals = [per_launch[x] for x in parts if per_launch.get(x) is not None]
-        if vals:
-            per_launch[bucket] = sum(vals)
+        rd, wr = c.get("FETCH_SIZE"), c.get("WRITE_SIZE")
+        r = {"dispatches_kept": c["_n"], "dispatches_per_step": round(c["_n"] / a.steps, 3),
+             "read_bytes_per_step": None if rd is None else rd * 1024 * 2 / a.steps,
+             "write_bytes_per_step": None if wr is None else wr * 1024 / a.steps}
+        if rd is not None and wr is not None:
+            r["hbm_bytes_per_step"] = r["read_bytes_per_step"] + r["write_bytes_per_step"]
+            b = bucket_of(name)
+            r["bucket"] = b
+            if b:
+                per_step[b] += r["hbm_bytes_per_step"]
+        res[name] = r
+    # the path's kernels only (not the bench's generator, the runtime's copies or a stats query)
+    total = sum(r.get("hbm_bytes_per_step", 0) for r in res.values() if r.get("bucket"))
+    other = sum(r.get("hbm_bytes_per_step", 0) for r in res.values() if not r.get("bucket"))
     cal = None
-    if "k_classify_hist" in res and res["k_classify_hist"]["read_bytes"]:
-        cal = res["k_classify_hist"]["read_bytes"] / (16.0 * a.records)
-    out = {"note": "per-launch averages; read = FETCH_SIZE*1024*2 (gfx950 half-count correction), "
-                   "write = WRITE_SIZE*1024; Infinity-Cache hits are counted by these counters",
-           "records_per_launch": a.records,
+    if "k_classify_hist" in res and res["k_classify_hist"]["read_bytes_per_step"] and "k_scatter_rsv" not in res:
+        cal = res["k_classify_hist"]["read_bytes_per_step"] / (16.0 * a.records)
+    out = {"note": "HBM bytes per bench step (= per launch of each timing bucket: one push and one watermark per "
+                   "step), over the last `steps` steps' dispatches of each kernel; read = FETCH_SIZE*1024*2 (gfx950 "
+                   "half-count correction), write = WRITE_SIZE*1024; Infinity-Cache hits are counted by these "
+                   "counters",
+           "records_per_launch": a.records, "steps": a.steps, "warmup": a.warmup,
            "read_calibration_k_classify_hist": cal,
            "workload": a.workload,
-           "per_launch_bytes": per_launch,
+           "bytes_per_record_all_kernels": round(total / a.records, 2),
+           "bytes_per_record_outside_the_path": round(other / a.records, 2),
+           "per_launch_bytes": dict(per_step),
            "kernels": res}
     for n, r in res.items():
-        hb = r.get("hbm_bytes")
-        print(f"{n:28s} n={r['dispatches']:3d} read={r['read_bytes'] or 0:14.0f} write={r['write_bytes'] or 0:14.0f}"
-              f" per_rec={(hb or 0) / a.records:7.2f} B")
-    print("read calibration (k_classify_hist measured / 16 B per record):", cal)
+        hb = r.get("hbm_bytes_per_step") or 0
+        print(f"{n:28s} x{r['dispatches_per_step']:5.2f}/step read={r['read_bytes_per_step'] or 0:14.0f} "
+              f"write={r['write_bytes_per_step'] or 0:14.0f} per_rec={hb / a.records:7.2f} B")
+    print(f"path kernels: {total / a.records:.2f} B per record over {a.steps} steps "
+          f"(outside the path: {other / a.records:.2f})")
     if a.out:
         with open(a.out, "w") as f:
             json.dump(out, f, indent=1)
