@@ -85,9 +85,12 @@ def b_alg(workload, fired_per_record, world, hll_p=14, panes=60, centroids_per_r
     return 24 + bx + 104 * f  # c2
 
 
-def impl_bytes(name, n, merged, fired=0, hll_p=0, panes_per_window=0, compact=True):
-    """What one launch of a kernel moves as built, for the `impl_bytes` field."""
+def impl_bytes(name, n, merged, fired=0, hll_p=0, panes_per_window=0, compact=True, single=False):
+    """What one launch of a kernel moves as built, for the `impl_bytes` field.  single: the
+    batches took the single-pass scatter (k_scatter_rsv), behind which classify / scan / scatter only check a flag."""
     rec = 16 if compact else 32  # partitioned record: CRec {key hash | window, val} or PRec
+    if single and name in ("k_classify_hist", "k_scan"):
+        return 0
     if name == "k_fire":
         if hll_p:
             return fired * (64 + 2 * (1 << hll_p) + 56)
@@ -344,6 +347,7 @@ def main():
         nl = (ctypes.c_int64 * N.FW_NUM_KERNELS)()
         L.fw_profile_read(op._h, ms, nl, 1)
         merged = (st1["state_merges"] - st0["state_merges"]) / args.steps
+        single = st1["single_pass_batches"] - st0["single_pass_batches"] == args.steps
         per_launch_records = per_gpu_records / args.steps
         tr, tr_all, tr_src = {}, None, None
         if os.path.exists(args.traffic):
@@ -360,10 +364,10 @@ def main():
                 continue
             avg = ms[i] / nl[i]
             ib = impl_bytes(name, per_launch_records, merged, fired=fired / nl[i], hll_p=args.hll_p if hll else 0,
-                            panes_per_window=args.size // args.slide if sliding else 0)
+                            panes_per_window=args.size // args.slide if sliding else 0, single=single)
             kernels[name] = {"launches": int(nl[i]), "avg_ms": round(avg, 5), "total_ms": round(ms[i], 4),
                              "impl_bytes": None if ib is None else int(ib),
-                             "impl_frac": None if ib is None else round(ib / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "impl_frac": None if not ib else round(ib / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                              "traffic": tr.get(name)}
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
         kd = kernels[dom]
@@ -443,7 +447,9 @@ def main():
             "cpu_baseline": cpu,
             "kernels": kernels,
             **({"kernels_isolated": kernels_iso} if kernels_iso else {}),
-            "state": {"table_slots": int(st1["table_capacity"]), "table_grows_in_timed_region":
+            "state": {"single_pass_batches": int(st1["single_pass_batches"] - st0["single_pass_batches"]),
+                      "single_pass_redone": int(st1["single_pass_redone"] - st0["single_pass_redone"]),
+                      "table_slots": int(st1["table_capacity"]), "table_grows_in_timed_region":
                       int(st1["table_grows"] - st0["table_grows"]), "live_entries": int(st1["keyed_state_entries"])},
         }
         print(json.dumps(line), flush=True)

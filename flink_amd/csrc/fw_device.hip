@@ -4532,7 +4532,10 @@ struct DtLds {
   int64_t sum[FW_DT_SLOTS], mn[FW_DT_SLOTS], mx[FW_DT_SLOTS];
 };
 constexpr int DK_SLOTS = (int)(sizeof(DtLds) / 40 / 16 * 16);
-constexpr int DK_LIMIT = DK_SLOTS * 13 / 16;
+#ifndef FW_DK_FILL16
+#define FW_DK_FILL16 15  // claims stop at this many 16ths of the compact table (buckets of 4 keep probes short)
+#endif
+constexpr int DK_LIMIT = DK_SLOTS * FW_DK_FILL16 / 16;
 constexpr unsigned long long DK_EMPTY = ~0ull;  // (a record or entry whose word is this takes the wide table)
 constexpr int DK_BUCKETS = DK_SLOTS / 4;  // a word's home is a bucket of 4 slots (one 32-byte read)
 struct DtLdsK {

@@ -85,6 +85,7 @@ struct fw_op {
   int32_t rsv_seen = 0;      // Status::rsv_fallbacks at the latest settle
   int32_t rsv_misses = 0;    // consecutive settles that saw a single-pass batch redone
   bool rsv_off = false;      // after 3 of them the operator stops trying the single pass
+  int64_t single_batches = 0;  // batches that took the single pass (fw_stats)
   uint32_t *xoffs = nullptr, *xscan = nullptr;  // combining: the combiner's live-count offsets and scan scratch
   std::string err;
 
@@ -697,6 +698,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
     }
   }
   S.single = single;
+  op->single_batches += single;
   S.gather = gather;
   S.T = T;
   // minBy / maxBy: the aggregate reads the selected elements' fields back by batch index, possibly after the
@@ -1414,6 +1416,8 @@ int fw_get_stats(fw_op* op, fw_stats* o) {
   o->slow_path_records = (int64_t)s.slow_total;
   o->state_merges = (int64_t)s.merged;
   o->digest_centroids_fired = (int64_t)s.td_cent;
+  o->single_pass_batches = op->single_batches;
+  o->single_pass_redone = (int64_t)s.rsv_fallbacks;
   return FW_OK;
 }
 

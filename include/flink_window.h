@@ -172,6 +172,8 @@ typedef struct fw_stats {
   int64_t slow_path_records;      /* records replayed in arrival order (late firing / drop)  */
   int64_t state_merges;           /* pre-aggregated (key, window) deltas merged into HBM       */
   int64_t digest_centroids_fired; /* FW_AGG_TDIGEST: centroids of all digests fired so far      */
+  int64_t single_pass_batches;    /* device batches partitioned in one pass (dense tumbling)    */
+  int64_t single_pass_redone;     /* ... of which went through classify / scan / scatter after  */
 } fw_stats;
 
 /* Lifecycle — StreamOperator.setup/open/close/dispose (api/operators/StreamOperator.java:57-127). */

@@ -335,10 +335,21 @@ def test_gpu_single_pass_scatter_fallbacks(value_type):
     k = k.copy()
     k[: len(k) * 3 // 4] = 7
     batches[4] = (k, t, v)
-    g, r, gs, rs, gl, rl = _run_both(cfg, batches, wms, max_batch=1 << 17)
+    gpu = _gpu_op(**cfg, max_batch=1 << 17)
+    ref = orc.WindowOperatorOracle(**cfg)
+    for (k, t, v), wm in zip(batches, wms):
+        gpu.process(k, t, v)
+        ref.process(k, t, v)
+        gpu.watermark(wm)
+        ref.watermark(wm)
+    g, r, gl, rl = gpu.rows(), ref.rows(), gpu.late_dropped, ref.late_dropped
+    st = gpu.stats()
+    gpu.close()
     assert_rows_equal(g, r, _VT[value_type])
     assert gl == rl and gl > 0
     assert int(g["count"].sum()) + gl == 700_000
+    # every batch after the first tried the single pass; the far-ahead and the hot-key batches were redone
+    assert st["single_pass_batches"] >= len(batches) - 2 and st["single_pass_redone"] >= 2
 
 
 @pytest.mark.parametrize("cfg", [dict(assigner="tumbling", size=1000),

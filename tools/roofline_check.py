@@ -4,8 +4,10 @@
 A bench line prices its dominant timing bucket (bench.py `roofline.kernel`, one of fw_kernel_name's buckets) at
 B_alg x records per launch over the bucket's average HIP-event duration; `roofline.isolated` does the same over
 a pass with synchronous input.  Here the same figures come from rocprofv3 kernel traces of the same command:
-the bucket's kernels (tools/traffic.py BUCKETS), each kernel's dispatches of the timed steps (its last
-steps/(steps+warmup) of its dispatches), their durations summed and divided by the timed steps.
+the bucket's kernels (tools/traffic.py BUCKETS), their dispatches in the timed steps (between the bench's stats
+reads around its timed loop), durations summed and divided by the timed steps.  Under async input a HIP-event interval also holds
+the launch's dispatch latency and its wait for CUs held by the other stream's kernel, so the line's async figure
+reads a few percent below the trace's.
 
 usage: tools/roofline_check.py BENCH_JSON --async-trace CSV --sync-trace CSV --steps S --warmup W
 """
@@ -17,22 +19,22 @@ import sys
 from collections import defaultdict
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from traffic import bucket_of, short  # noqa: E402
+from traffic import bucket_of, short, timed_window  # noqa: E402
 
 
-def bucket_ms(trace, steps, warmup):
-    per = defaultdict(list)
+def bucket_ms(trace, steps):
+    """per bucket: the summed durations of its kernels' dispatches in the timed steps (traffic.timed_window) / steps"""
+    rows = []
     with open(trace) as f:
         for r in csv.DictReader(f):
-            per[short(r["Kernel_Name"])].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
+    rows.sort()
+    lo, hi = timed_window([(i, r[2]) for i, r in enumerate(rows)])
     out = defaultdict(float)
-    for k, v in per.items():
+    for s, e, k in rows[lo + 1:hi]:
         b = bucket_of(k)
-        if not b:
-            continue
-        v.sort()
-        keep = max(1, round(len(v) * steps / (steps + warmup)))
-        out[b] += sum(e - s for s, e in v[-keep:]) / 1e6 / steps
+        if b:
+            out[b] += (e - s) / 1e6 / steps
     return dict(out)
 
 
@@ -48,8 +50,8 @@ def main():
     line = json.loads([l for l in open(a.bench_json) if l.startswith("{")][-1])
     rf = line["roofline"]
     alg, peak, dom = rf["alg_bytes_per_launch"], rf["peak"], rf["kernel"]
-    ms_a = bucket_ms(a.async_trace, a.steps, a.warmup)
-    ms_s = bucket_ms(a.sync_trace, a.steps, a.warmup)
+    ms_a = bucket_ms(a.async_trace, a.steps)
+    ms_s = bucket_ms(a.sync_trace, a.steps)
     frac = lambda ms: alg / (ms * 1e-3) / 1e9 / peak  # noqa: E731
     res = {"workload": line["config"]["workload"], "dominant_bucket": dom, "alg_bytes_per_launch": alg,
            "line": {"frac": rf["frac"], "avg_ms": line["kernels"][dom]["avg_ms"],

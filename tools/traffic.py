@@ -10,8 +10,8 @@ The correction factor for reads is checked against k_classify_hist, whose reads 
 (16 B per record: key + ts), and the calibration is printed beside the result.
 
 Bytes are per bench step (one push + one watermark), summed per bench timing bucket (BUCKETS), over the timed
-steps only (each kernel's last steps/(steps+warmup) of its dispatches), so a run of steps >= one firing period
-averages the firings in.
+steps only (the dispatches between the bench's stats reads around its timed loop), so a run of steps >= one firing
+period averages the firings in.
 
 usage: tools/traffic.py [pmc_dir] --steps S --warmup W [--records N] [--out profiles/traffic_rNN_W.json]
 """
@@ -48,10 +48,19 @@ def bucket_of(kernel):
     return None
 
 
-def load(pmc_dir, keep_frac=1.0):
-    """kernel -> counter -> summed value over the kept dispatches (each kernel's last keep_frac of its dispatches:
-    the bench's timed steps follow its warmup), and the kept dispatch counts."""
-    vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per-dispatch values, in order]
+def timed_window(ordered):
+    """(lo, hi): bench.py reads the operator's stats (fw_get_stats -> one k_table_stats dispatch) right before and
+    right after its timed steps, so the timed dispatches are the ones strictly between the last two k_table_stats.
+    ordered: (order key, kernel short name) in dispatch order."""
+    st = [key for key, n in ordered if n == "k_table_stats"]
+    if len(st) < 2:
+        raise SystemExit("no k_table_stats pair in the trace: not a bench.py run?")
+    return st[-2], st[-1]
+
+
+def load(pmc_dir):
+    """kernel -> counter -> summed value over the timed steps' dispatches (timed_window), and their count."""
+    vals = defaultdict(lambda: defaultdict(float))
     for f in sorted(glob.glob(os.path.join(pmc_dir, "p*", "run_counter_collection.csv"))):
         per = defaultdict(float)
         names = {}
@@ -60,18 +69,15 @@ def load(pmc_dir, keep_frac=1.0):
                 key = (int(r["Dispatch_Id"]), r["Counter_Name"])
                 per[key] += float(r["Counter_Value"])  # sum over dimensions (XCDs / instances)
                 names[int(r["Dispatch_Id"])] = short(r["Kernel_Name"])
-        for (d, cn), v in sorted(per.items()):
-            vals[names[d]][cn].append(v)
-    out = {}
-    for k, cs in vals.items():
-        o = {}
-        for c, v in cs.items():
-            keep = int(len(v) * keep_frac + 1e-9)  # (a kernel of the warmup steps only keeps nothing)
-            o[c] = sum(v[-keep:]) if keep else 0.0
-            o["_n"] = keep
-        if o["_n"]:
-            out[k] = o
-    return out
+        lo, hi = timed_window(sorted(names.items()))
+        seen = defaultdict(set)
+        for (d, cn), v in per.items():
+            if lo < d < hi:
+                vals[names[d]][cn] += v
+                seen[names[d]].add(d)
+        for k, ds in seen.items():
+            vals[k]["_n"] = len(ds)
+    return {k: dict(v) for k, v in vals.items()}
 
 
 def main():
@@ -83,11 +89,11 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--workload", default="c2", help="bench --workload the passes ran (recorded for bench.py)")
     a = ap.parse_args()
-    k = load(a.pmc_dir, a.steps / (a.steps + a.warmup))
+    k = load(a.pmc_dir)
     res, per_step = {}, defaultdict(float)
     for name, c in sorted(k.items()):
         rd, wr = c.get("FETCH_SIZE"), c.get("WRITE_SIZE")
-        r = {"dispatches_kept": c["_n"], "dispatches_per_step": round(c["_n"] / a.steps, 3),
+        r = {"dispatches": int(c["_n"]), "dispatches_per_step": round(c["_n"] / a.steps, 3),
              "read_bytes_per_step": None if rd is None else rd * 1024 * 2 / a.steps,
              "write_bytes_per_step": None if wr is None else wr * 1024 / a.steps}
         if rd is not None and wr is not None:
