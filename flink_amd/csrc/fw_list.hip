@@ -1,0 +1,1284 @@
+// fw_list.hip — f4: the window-contents (ListState) operator of the C-ABI (fw_list_*, include/flink_window.h):
+// WindowedStream.apply / process with an Iterable window function and the EvictingWindowOperator
+// (paths relative to /root/reference/flink-streaming-java/src/main/java/org/apache/flink/streaming/):
+//   runtime/operators/windowing/EvictingWindowOperator.java:102-239 processElement, :241-286 onEventTime,
+//   :334-366 emitWindowContents; WindowOperator.java:291-469 (no evictor), :576-651 lateness and cleanup;
+//   api/windowing/triggers/{EventTimeTrigger.java:37-73, CountTrigger.java:47-70, PurgingTrigger.java:45-59};
+//   api/windowing/evictors/{CountEvictor.java:55-78, TimeEvictor.java:58-103, DeltaEvictor.java:56-80}.
+//
+// HBM layout (one handle = one subtask on one GPU):
+//   groups   an open-addressing map (key, window start) -> group id (the slot), per group its key group, the
+//            CountTrigger count and flags {trigger timer registered, touched by the current push, due to fire,
+//            due to be cleaned up}: the (key, window) namespaces of "window-contents" and the trigger state;
+//   log      the elements of every list as SoA columns {ts, value, arrival ordinal, group id} in arrival
+//            order; an evicted, purged or cleaned-up element gets group id -1.  A list is the group's live
+//            elements in log order.  Dead elements are dropped by a stable compaction (with a map rebuild)
+//            once they outnumber the live ones.
+// A push appends its records' (record, window) entries to the log (one scan for the offsets, one pass for
+// the map lookups / inserts); only when elements can fire while being processed (CountTrigger, or an
+// EventTimeTrigger window whose maxTimestamp is already <= the watermark: allowed lateness) are the touched
+// groups' lists gathered (a stable radix sort of their log positions by group) and walked in order, one
+// thread per list, exactly as processElement's trigger / evictor / emit sequence.  A watermark marks the
+// groups whose trigger timer (maxTimestamp) or cleanup timer is due, walks the lists of the firing ones the
+// same way, and drops the cleaned-up ones.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <string>
+#include <vector>
+
+#include "../../include/flink_window.h"
+
+namespace {
+
+constexpr int64_t LMAX = INT64_MAX;
+constexpr int64_t LMIN = INT64_MIN;
+#include "fw_jmath.h"
+
+enum : uint32_t { GF_TIMER = 1u, GF_TOUCH = 2u, GF_FIRE = 4u, GF_CLEAN = 8u };
+enum : uint32_t { LF_NO_TS = 1u, LF_KEY_GROUP = 2u, LF_MAP_FULL = 4u, LF_ELEMS = 8u };
+constexpr uint32_t G_EMPTY = 0u, G_BUSY = 1u, G_LIVE = 2u, G_TOMB = 3u;
+
+struct LCfg {
+  int32_t assigner, vt, key_kind, trigger, purging, evictor, evict_after, side_output, emit, max_par, kg0, nkg;
+  int64_t size, slide, offset, lateness, trig_n, ev_n;
+  double thr;
+};
+
+struct LCounters {
+  unsigned long long rows, elems, side, late, dead, live_groups, tombs, nfire, nclean, count;
+  unsigned int flags, need_seq;
+};
+
+struct LState {
+  uint32_t* gst;
+  int64_t *gkey, *gstart, *gcnt;
+  uint32_t* gfl;
+  int32_t* gkg;
+  uint32_t gmask;
+  int64_t *lts, *lval, *lord;
+  int32_t* lgid;
+  int64_t *rkey, *rstart, *rend, *rcnt, *rsum, *rmin, *rmax, *rfirst, *roff;
+  int64_t *ets, *eval, *eord;
+  int64_t ecap;
+  int64_t *skey, *sts, *sval;
+  LCounters* ctr;
+};
+
+// ---------------------------------------------------------------- windows
+__device__ __forceinline__ bool event_time(const LCfg& c) { return c.assigner != FW_GLOBAL; }
+__device__ __forceinline__ int64_t w_end(const LCfg& c, int64_t start) {
+  return c.assigner == FW_GLOBAL ? LMAX : jadd(start, c.size);
+}
+// TimeWindow.maxTimestamp (end - 1); GlobalWindow.maxTimestamp = Long.MAX_VALUE
+__device__ __forceinline__ int64_t w_max_ts(const LCfg& c, int64_t start) {
+  return c.assigner == FW_GLOBAL ? LMAX : jsub(jadd(start, c.size), 1);
+}
+// WindowOperator.cleanupTime (:637-644); GlobalWindows are not event time: no cleanup timer (LMAX)
+__device__ __forceinline__ int64_t w_cleanup(const LCfg& c, int64_t start) {
+  if (!event_time(c)) return LMAX;
+  const int64_t mx = w_max_ts(c, start);
+  const int64_t t = jadd(mx, c.lateness);
+  return t >= mx ? t : LMAX;
+}
+// TimeWindow.getWindowStartWithOffset (TimeWindow.java:254-256): Java's truncating % is C++'s
+__device__ __forceinline__ int64_t w_start_of(int64_t ts, int64_t off, int64_t size) {
+  return jsub(ts, jadd(jsub(ts, off), size) % size);
+}
+// every window of a record that is not late (WindowOperator.isWindowLate, :629-631), in the assigner's order
+template <class F>
+__device__ __forceinline__ void for_windows(const LCfg& c, int64_t ts, int64_t wm, F f) {
+  if (c.assigner == FW_GLOBAL) {
+    f(LMIN);
+    return;
+  }
+  if (c.assigner == FW_TUMBLING) {
+    const int64_t s = w_start_of(ts, c.offset, c.size);
+    if (!(w_cleanup(c, s) <= wm)) f(s);
+    return;
+  }
+  const int64_t last = w_start_of(ts, c.offset, c.slide);  // SlidingEventTimeWindows.java:67-81
+  for (int64_t s = last; s > jsub(ts, c.size); s = jsub(s, c.slide))
+    if (!(w_cleanup(c, s) <= wm)) f(s);
+}
+
+// ---------------------------------------------------------------- group map
+__device__ __forceinline__ uint32_t g_hash(int64_t key, int64_t start) {
+  return (uint32_t)fmix64((uint64_t)key ^ fmix64((uint64_t)start ^ 0x9E3779B97F4A7C15ull));
+}
+__device__ int32_t g_find_insert(const LState& S, int64_t key, int64_t start, int32_t kg) {
+  uint32_t s = g_hash(key, start) & S.gmask;
+  for (uint32_t probes = 0; probes <= S.gmask;) {
+    const uint32_t cur = __hip_atomic_load(&S.gst[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == G_LIVE) {
+      if (S.gkey[s] == key && S.gstart[s] == start) return (int32_t)s;
+    } else if (cur == G_BUSY) {
+      continue;  // being published by another lane: read it again
+    } else if (cur == G_EMPTY) {
+      if (atomicCAS(&S.gst[s], G_EMPTY, G_BUSY) == G_EMPTY) {
+        S.gkey[s] = key;
+        S.gstart[s] = start;
+        S.gkg[s] = kg;
+        S.gcnt[s] = 0;
+        S.gfl[s] = 0;
+        __hip_atomic_store(&S.gst[s], G_LIVE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(&S.ctr->live_groups, 1ull);
+        return (int32_t)s;
+      }
+      continue;  // lost the race for this slot: read it again
+    }
+    s = (s + 1) & S.gmask;  // live foreign group or tombstone
+    probes++;
+  }
+  atomicOr(&S.ctr->flags, LF_MAP_FULL);
+  return -1;
+}
+
+// ---------------------------------------------------------------- push
+// per record: its non-late windows (wcnt), errors, late records (side output / numLateRecordsDropped)
+__global__ __launch_bounds__(256) void k_lp_count(LCfg c, LState S, const int64_t* __restrict__ key,
+                                                  const int64_t* __restrict__ ts, const int64_t* __restrict__ val,
+                                                  const int32_t* __restrict__ kh, int64_t n, int64_t wm,
+                                                  uint32_t* __restrict__ wcnt) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = ts[i];
+    wcnt[i] = 0;
+    if (event_time(c) && t == LMIN) {  // TumblingEventTimeWindows.java:69-71
+      atomicOr(&S.ctr->flags, LF_NO_TS);
+      continue;
+    }
+    const int32_t kg = key_group(key_hash_of(c.key_kind, key[i], kh, i), c.max_par);
+    if ((uint32_t)(kg - c.kg0) >= (uint32_t)c.nkg) {
+      atomicOr(&S.ctr->flags, LF_KEY_GROUP);
+      continue;
+    }
+    uint32_t k = 0;
+    for_windows(c, t, wm, [&](int64_t) { k++; });
+    wcnt[i] = k;
+    // skipped && isElementLate (:410-418, :620-622)
+    if (k == 0 && event_time(c) && jadd(t, c.lateness) <= wm) {
+      if (c.side_output) {
+        const unsigned long long r = atomicAdd(&S.ctr->side, 1ull);
+        S.skey[r] = key[i];
+        S.sts[r] = t;
+        S.sval[r] = val[i];
+      } else {
+        atomicAdd(&S.ctr->late, 1ull);
+      }
+    }
+  }
+}
+
+// the entries: log[base + woff[i] + j] = (ts, value, ordinal, group) for the j-th non-late window of record i;
+// groups whose elements fire while being processed are marked for the ordered walk
+__global__ __launch_bounds__(256) void k_lp_append(LCfg c, LState S, const int64_t* __restrict__ key,
+                                                   const int64_t* __restrict__ ts, const int64_t* __restrict__ val,
+                                                   const int32_t* __restrict__ kh, int64_t n, int64_t wm,
+                                                   const uint32_t* __restrict__ wcnt, const uint32_t* __restrict__ woff,
+                                                   int64_t base, int64_t ord_base) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!wcnt[i]) continue;
+    const int64_t t = ts[i], k = key[i], v = val[i];
+    const int32_t kg = key_group(key_hash_of(c.key_kind, k, kh, i), c.max_par);
+    int64_t idx = base + woff[i];
+    for_windows(c, t, wm, [&](int64_t s) {
+      const int32_t g = g_find_insert(S, k, s, kg);
+      S.lts[idx] = t;
+      S.lval[idx] = v;
+      S.lord[idx] = ord_base + i;
+      S.lgid[idx] = g;
+      idx++;
+      if (g < 0) return;
+      if (c.trigger == FW_TRIGGER_COUNT || w_max_ts(c, s) <= wm) {  // CountTrigger / late firing
+        atomicOr(&S.gfl[g], GF_TOUCH);
+        S.ctr->need_seq = 1u;
+      } else {  // EventTimeTrigger.onElement registers the timer at maxTimestamp
+        if (!(S.gfl[g] & GF_TIMER)) atomicOr(&S.gfl[g], GF_TIMER);
+      }
+    });
+  }
+}
+
+// ---------------------------------------------------------------- ordered walks
+__global__ __launch_bounds__(256) void k_sel_flags(const LState S, int64_t n, uint32_t bit, uint8_t* __restrict__ f) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t g = S.lgid[i];
+    f[i] = g >= 0 && (S.gfl[g] & bit) ? 1 : 0;
+  }
+}
+__global__ __launch_bounds__(256) void k_sel_keys(const LState S, const uint32_t* __restrict__ idx, int64_t m,
+                                                  uint32_t* __restrict__ keys) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+    keys[i] = (uint32_t)S.lgid[idx[i]];
+}
+__global__ __launch_bounds__(256) void k_seg_flags(const uint32_t* __restrict__ keys, int64_t m, uint8_t* __restrict__ f) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+    f[i] = i == 0 || keys[i] != keys[i - 1] ? 1 : 0;
+}
+
+// Double.compare / Float.compare order of f64 bits as a signed key (canonical NaN largest)
+__device__ __forceinline__ int64_t fkey(int64_t b) {
+  if ((b & 0x7ff0000000000000ll) == 0x7ff0000000000000ll && (b & 0x000fffffffffffffll)) b = 0x7ff8000000000000ll;
+  return b >= 0 ? b : (b ^ 0x7fffffffffffffffll);
+}
+__device__ __forceinline__ int64_t canon(int64_t b) {
+  return ((b & 0x7ff0000000000000ll) == 0x7ff0000000000000ll && (b & 0x000fffffffffffffll)) ? 0x7ff8000000000000ll : b;
+}
+// DeltaEvictor's built-in DeltaFunction: last.field - e.field in the field's Java arithmetic, as a double
+__device__ __forceinline__ double delta_of(const LCfg& c, int64_t e, int64_t last) {
+  switch (c.vt) {
+    case FW_VAL_I64: return (double)jsub(last, e);
+    case FW_VAL_F64: return __longlong_as_double(last) - __longlong_as_double(e);
+    case FW_VAL_F32: return (double)((float)__longlong_as_double(last) - (float)__longlong_as_double(e));
+    default: return (double)(int32_t)((uint32_t)(int32_t)last - (uint32_t)(int32_t)e);
+  }
+}
+
+// one list in the sorted positions pos[a .. j] (log indices in list order): which of its live elements the
+// evictor removes (CountEvictor.evict :63-78, TimeEvictor.evict :75-103, DeltaEvictor.evict :71-80).
+// mark = false: returns how many would remain; mark = true: kills the others and returns the remaining count.
+__device__ int64_t evict(const LCfg& c, const LState& S, const uint32_t* pos, int64_t a, int64_t j, bool mark) {
+  int64_t live = 0;
+  for (int64_t q = a; q <= j; q++) live += S.lgid[pos[q]] >= 0;
+  if (c.evictor == FW_EVICT_NONE || live == 0) return live;
+  int64_t killed = 0;
+  if (c.evictor == FW_EVICT_COUNT) {
+    if (live <= c.ev_n) return live;
+    const int64_t drop = live - c.ev_n;
+    if (mark) {
+      for (int64_t q = a; q <= j && killed < drop; q++)
+        if (S.lgid[pos[q]] >= 0) {
+          S.lgid[pos[q]] = -1;
+          killed++;
+        }
+    } else {
+      killed = drop;
+    }
+  } else if (c.evictor == FW_EVICT_TIME) {
+    int64_t first_ts = 0, mx = LMIN;
+    bool have = false;
+    for (int64_t q = a; q <= j; q++) {
+      const uint32_t e = pos[q];
+      if (S.lgid[e] < 0) continue;
+      if (!have) first_ts = S.lts[e];
+      have = true;
+      mx = max(mx, S.lts[e]);
+    }
+    if (first_ts == LMIN) return live;  // hasTimestamp of the first element
+    const int64_t cutoff = jsub(mx, c.ev_n);
+    for (int64_t q = a; q <= j; q++) {
+      const uint32_t e = pos[q];
+      if (S.lgid[e] < 0 || !(S.lts[e] <= cutoff)) continue;
+      if (mark) S.lgid[e] = -1;
+      killed++;
+    }
+  } else {  // FW_EVICT_DELTA
+    int64_t last = 0;
+    for (int64_t q = j; q >= a; q--)
+      if (S.lgid[pos[q]] >= 0) {
+        last = S.lval[pos[q]];
+        break;
+      }
+    for (int64_t q = a; q <= j; q++) {
+      const uint32_t e = pos[q];
+      if (S.lgid[e] < 0 || !(delta_of(c, S.lval[e], last) >= c.thr)) continue;
+      if (mark) S.lgid[e] = -1;
+      killed++;
+    }
+  }
+  if (mark && killed) atomicAdd(&S.ctr->dead, (unsigned long long)killed);
+  return live - killed;
+}
+
+// emitWindowContents (:334-366) of group g over the list pos[a .. j]: evictBefore, one row (+ the elements),
+// evictAfter.  False (nothing changed) when the element buffer cannot take the contents.
+__device__ bool emit_firing(const LCfg& c, const LState& S, uint32_t g, const uint32_t* pos, int64_t a, int64_t j) {
+  int64_t cnt = 0;  // the elements the function sees
+  if (c.evict_after)
+    for (int64_t q = a; q <= j; q++) cnt += S.lgid[pos[q]] >= 0;
+  else
+    cnt = evict(c, S, pos, a, j, false);
+  int64_t eoff = 0;
+  if (c.emit && cnt) {  // reserve the elements (rows were sized by the host: one per possible firing)
+    unsigned long long cur = __hip_atomic_load(&S.ctr->elems, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (true) {
+      if ((int64_t)cur + cnt > S.ecap) {
+        atomicOr(&S.ctr->flags, LF_ELEMS);
+        return false;
+      }
+      const unsigned long long prev = atomicCAS(&S.ctr->elems, cur, cur + (unsigned long long)cnt);
+      if (prev == cur) break;
+      cur = prev;
+    }
+    eoff = (int64_t)cur;
+  }
+  if (!c.evict_after) evict(c, S, pos, a, j, true);
+  const bool fl = c.vt == FW_VAL_F64 || c.vt == FW_VAL_F32;
+  double ds = 0.0;
+  int64_t is = 0, mn = 0, mx = 0, first = -1, k = 0;
+  for (int64_t q = a; q <= j; q++) {
+    const uint32_t e = pos[q];
+    if (S.lgid[e] < 0) continue;
+    const int64_t v = S.lval[e];
+    if (k == 0) first = S.lord[e];
+    if (fl) {
+      const double d = __longlong_as_double(v);
+      ds = k == 0 ? d : c.vt == FW_VAL_F32 ? (double)((float)ds + (float)d) : ds + d;
+      if (k == 0 || fkey(v) < fkey(mn)) mn = v;
+      if (k == 0 || fkey(v) > fkey(mx)) mx = v;
+    } else {
+      is = k == 0 ? v : jadd(is, v);
+      if (k == 0 || v < mn) mn = v;
+      if (k == 0 || v > mx) mx = v;
+    }
+    if (c.emit) {
+      S.ets[eoff + k] = S.lts[e];
+      S.eval[eoff + k] = v;
+      S.eord[eoff + k] = S.lord[e];
+    }
+    k++;
+  }
+  const unsigned long long r = atomicAdd(&S.ctr->rows, 1ull);
+  S.rkey[r] = S.gkey[g];
+  S.rstart[r] = S.gstart[g];
+  S.rend[r] = w_end(c, S.gstart[g]);
+  S.rcnt[r] = k;
+  if (fl) {
+    S.rsum[r] = __double_as_longlong(ds);
+    S.rmin[r] = k ? canon(mn) : 0;
+    S.rmax[r] = k ? canon(mx) : 0;
+  } else {
+    S.rsum[r] = c.vt == FW_VAL_I32 ? (int64_t)(int32_t)is : c.vt == FW_VAL_I16 ? (int64_t)(int16_t)is
+              : c.vt == FW_VAL_I8 ? (int64_t)(int8_t)is : is;
+    S.rmin[r] = mn;
+    S.rmax[r] = mx;
+  }
+  S.rfirst[r] = first;
+  S.roff[r] = c.emit ? eoff : 0;
+  if (c.evict_after) evict(c, S, pos, a, j, true);
+  return true;
+}
+__device__ void purge(const LState& S, const uint32_t* pos, int64_t a, int64_t j) {
+  int64_t killed = 0;
+  for (int64_t q = a; q <= j; q++)
+    if (S.lgid[pos[q]] >= 0) {
+      S.lgid[pos[q]] = -1;
+      killed++;
+    }
+  if (killed) atomicAdd(&S.ctr->dead, (unsigned long long)killed);
+}
+
+// One thread per list.  PUSH: the list's elements appended by this push (log index >= base_new), in order:
+// CountTrigger.onElement / EventTimeTrigger.onElement (maxTimestamp <= watermark: FIRE), the firing over the
+// list up to the element, PurgingTrigger's purge (EvictingWindowOperator.java:186-222).  prog[s] = where a
+// launch stopped (the element buffer was full); the host grows it and launches again.
+// WATERMARK: the due lists fire over all their elements (onEventTime, :241-286).
+template <bool PUSH>
+__global__ __launch_bounds__(256) void k_walk(LCfg c, LState S, const uint32_t* __restrict__ pos,
+                                              const uint32_t* __restrict__ keys, const uint32_t* __restrict__ seg,
+                                              int64_t nseg, int64_t base_new, int64_t wm, int64_t* __restrict__ prog) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = seg[s], b = seg[s + 1];
+    const uint32_t g = keys[a];
+    if (!PUSH) {
+      if (!(S.gfl[g] & GF_FIRE)) continue;
+      if (!emit_firing(c, S, g, pos, a, b - 1)) continue;
+      if (c.purging) purge(S, pos, a, b - 1);
+      atomicAnd(&S.gfl[g], ~GF_FIRE);
+      continue;
+    }
+    if (!(S.gfl[g] & GF_TOUCH)) continue;
+    int64_t j = prog[s] >= 0 ? prog[s] : a;
+    while (j < b && (int64_t)pos[j] < base_new) j++;
+    const int64_t mts = w_max_ts(c, S.gstart[g]);
+    bool stopped = false;
+    for (; j < b; j++) {
+      bool fire;
+      int64_t nc = 0;
+      if (c.trigger == FW_TRIGGER_COUNT) {
+        nc = S.gcnt[g] + 1;
+        fire = nc >= c.trig_n;
+      } else {
+        fire = mts <= wm;
+      }
+      if (fire) {
+        if (!emit_firing(c, S, g, pos, a, j)) {
+          prog[s] = j;
+          stopped = true;
+          break;
+        }
+        if (c.purging) purge(S, pos, a, j);
+      }
+      if (c.trigger == FW_TRIGGER_COUNT) S.gcnt[g] = fire ? 0 : nc;
+    }
+    if (!stopped) atomicAnd(&S.gfl[g], ~GF_TOUCH);
+  }
+}
+
+// ---------------------------------------------------------------- watermark
+__global__ __launch_bounds__(256) void k_lw_due(LCfg c, LState S, int64_t wm) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)S.gmask;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    if (S.gst[g] != G_LIVE) continue;
+    const int64_t st = S.gstart[g];
+    uint32_t f = S.gfl[g];
+    if ((f & GF_TIMER) && w_max_ts(c, st) <= wm) {  // the trigger timer fires (EventTimeTrigger.onEventTime)
+      f = (f & ~GF_TIMER) | GF_FIRE;
+      atomicAdd(&S.ctr->nfire, 1ull);
+    }
+    if (w_cleanup(c, st) <= wm) {
+      f |= GF_CLEAN;
+      atomicAdd(&S.ctr->nclean, 1ull);
+    }
+    S.gfl[g] = f;
+  }
+}
+// clearAllState (:368-385): the cleaned-up groups' elements die, their namespaces become tombstones
+__global__ __launch_bounds__(256) void k_lw_clean_log(LState S, int64_t n) {
+  unsigned long long killed = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t g = S.lgid[i];
+    if (g >= 0 && (S.gfl[g] & GF_CLEAN)) {
+      S.lgid[i] = -1;
+      killed++;
+    }
+  }
+  if (killed) atomicAdd(&S.ctr->dead, killed);
+}
+__global__ __launch_bounds__(256) void k_lw_clean_map(LState S) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)S.gmask;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    if (S.gst[g] != G_LIVE) continue;
+    const uint32_t f = S.gfl[g];
+    if (f & GF_CLEAN) {
+      S.gst[g] = G_TOMB;
+      atomicSub(&S.ctr->live_groups, 1ull);
+      atomicAdd(&S.ctr->tombs, 1ull);
+    } else if (f & GF_FIRE) {
+      S.gfl[g] = f & ~GF_FIRE;  // a due timer of an empty list: nothing to fire
+    }
+  }
+}
+
+// ---------------------------------------------------------------- compaction / rebuild
+__global__ __launch_bounds__(256) void k_rebuild_map(LCfg c, LState o, LState S, int32_t* __restrict__ remap) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)o.gmask;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    if (o.gst[g] != G_LIVE) {
+      remap[g] = -1;
+      continue;
+    }
+    const int32_t ng = g_find_insert(S, o.gkey[g], o.gstart[g], o.gkg[g]);
+    remap[g] = ng;
+    if (ng >= 0) {
+      S.gcnt[ng] = o.gcnt[g];
+      S.gfl[ng] = o.gfl[g];
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_alive_flags(const int32_t* __restrict__ gid, int64_t n, uint8_t* __restrict__ f) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    f[i] = gid[i] >= 0;
+}
+__global__ __launch_bounds__(256) void k_gather_log(LState o, LState S, const uint32_t* __restrict__ idx, int64_t m,
+                                                    const int32_t* __restrict__ remap) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t e = idx[i];
+    S.lts[i] = o.lts[e];
+    S.lval[i] = o.lval[e];
+    S.lord[i] = o.lord[e];
+    S.lgid[i] = remap ? remap[o.lgid[e]] : o.lgid[e];
+  }
+}
+
+// ---------------------------------------------------------------- stats / snapshot / restore
+// live lists (groups with a live element) and timers (HeapInternalTimerService: the trigger timer and the
+// cleanup timer of a (key, window), one timer when they coincide)
+__global__ __launch_bounds__(256) void k_mark_lists(LState S, int64_t n, uint8_t* __restrict__ has) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t g = S.lgid[i];
+    if (g >= 0) has[g] = 1;
+  }
+}
+__global__ __launch_bounds__(256) void k_count_state(LCfg c, LState S, const uint8_t* __restrict__ has,
+                                                     unsigned long long* out2) {
+  unsigned long long lists = 0, timers = 0;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)S.gmask;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    if (S.gst[g] != G_LIVE) continue;
+    lists += has[g];
+    const int64_t cl = w_cleanup(c, S.gstart[g]);
+    const bool creg = event_time(c) && cl != LMAX;
+    timers += creg ? 1 : 0;
+    if ((S.gfl[g] & GF_TIMER) && !(creg && cl == w_max_ts(c, S.gstart[g]))) timers++;
+  }
+  if (lists) atomicAdd(&out2[0], lists);
+  if (timers) atomicAdd(&out2[1], timers);
+}
+__global__ __launch_bounds__(256) void k_kg_flags_log(LState S, int64_t n, int32_t kg, uint8_t* __restrict__ f) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t g = S.lgid[i];
+    f[i] = g >= 0 && S.gkg[g] == kg;
+  }
+}
+__global__ __launch_bounds__(256) void k_kg_flags_map(LState S, int32_t kg, uint8_t* __restrict__ f) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)S.gmask;
+       g += (int64_t)gridDim.x * blockDim.x)
+    f[g] = S.gst[g] == G_LIVE && S.gkg[g] == kg;
+}
+// restore: one thread inserts the lists in order (their count and timer flag), then the elements are appended
+__global__ void k_restore_groups(LCfg c, LState S, const int64_t* __restrict__ key, const int64_t* __restrict__ start,
+                                 const int64_t* __restrict__ cnt, const int64_t* __restrict__ timer, int64_t n,
+                                 int32_t kg, int32_t* __restrict__ gid_out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t g = g_find_insert(S, key[i], start[i], kg);
+    gid_out[i] = g;
+    if (g < 0) continue;
+    S.gcnt[g] = cnt[i];
+    if (timer[i]) atomicOr(&S.gfl[g], GF_TIMER);
+  }
+}
+__global__ __launch_bounds__(256) void k_restore_elems(LState S, const int64_t* __restrict__ ts,
+                                                       const int64_t* __restrict__ val, const int64_t* __restrict__ ord,
+                                                       const int32_t* __restrict__ gid, int64_t n, int64_t base) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    S.lts[base + i] = ts[i];
+    S.lval[base + i] = val[i];
+    S.lord[base + i] = ord[i];
+    S.lgid[base + i] = gid[i];
+  }
+}
+
+unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>(8192, (n + 255) / 256)); }
+
+template <class T>
+hipError_t dmalloc(T** p, size_t count) {
+  *p = nullptr;
+  return hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T));
+}
+template <class T>
+void dfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+}  // namespace
+
+struct fw_list {
+  fw_list_config cfg{};
+  LCfg c{};
+  LState S{};
+  hipStream_t stream = nullptr;
+  int device = 0;
+  std::string err;
+  int64_t gcap = 0, lcap = 0, rcap = 0, scap = 0, max_batch = 0;
+  int64_t n_log = 0, ord_base = 0, wm = LMIN, records_in = 0, fired_total = 0, grows = 0;
+  LCounters* h_ctr = nullptr;  // pinned mirror
+  // per-push scratch (max_batch) and selection scratch (grown with the log)
+  int64_t *in_key = nullptr, *in_ts = nullptr, *in_val = nullptr;
+  int32_t* in_kh = nullptr;
+  uint32_t *wcnt = nullptr, *woff = nullptr;
+  int64_t sel_cap = 0;
+  uint8_t* flags8 = nullptr;
+  uint32_t *sel = nullptr, *sel2 = nullptr, *keys = nullptr, *keys2 = nullptr, *seg = nullptr;
+  int64_t* prog = nullptr;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+};
+
+namespace {
+
+int set_err(fw_list* op, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (op) op->err = buf;
+  return code;
+}
+#define LHIP(op, expr)                                                                                   \
+  do {                                                                                                   \
+    hipError_t _e = (expr);                                                                              \
+    if (_e != hipSuccess) return set_err(op, FW_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+#define LRET(expr)          \
+  do {                      \
+    int _r = (expr);        \
+    if (_r != FW_OK) return _r; \
+  } while (0)
+
+int read_ctr(fw_list* op) {
+  LHIP(op, hipMemcpyAsync(op->h_ctr, op->S.ctr, sizeof(LCounters), hipMemcpyDeviceToHost, op->stream));
+  LHIP(op, hipStreamSynchronize(op->stream));
+  return FW_OK;
+}
+int ensure_tmp(fw_list* op, size_t bytes) {
+  if (bytes <= op->tmp_bytes) return FW_OK;
+  dfree(op->tmp);
+  op->tmp_bytes = std::max(bytes, op->tmp_bytes * 2);
+  LHIP(op, dmalloc((uint8_t**)&op->tmp, op->tmp_bytes));
+  return FW_OK;
+}
+int alloc_map(fw_list* op, LState& S, int64_t cap) {
+  LHIP(op, dmalloc(&S.gst, (size_t)cap));
+  LHIP(op, dmalloc(&S.gkey, (size_t)cap));
+  LHIP(op, dmalloc(&S.gstart, (size_t)cap));
+  LHIP(op, dmalloc(&S.gcnt, (size_t)cap));
+  LHIP(op, dmalloc(&S.gfl, (size_t)cap));
+  LHIP(op, dmalloc(&S.gkg, (size_t)cap));
+  LHIP(op, hipMemsetAsync(S.gst, 0, (size_t)cap * sizeof(uint32_t), op->stream));
+  S.gmask = (uint32_t)(cap - 1);
+  return FW_OK;
+}
+void free_map(LState& S) {
+  dfree(S.gst);
+  dfree(S.gkey);
+  dfree(S.gstart);
+  dfree(S.gcnt);
+  dfree(S.gfl);
+  dfree(S.gkg);
+}
+int alloc_log(fw_list* op, LState& S, int64_t cap) {
+  LHIP(op, dmalloc(&S.lts, (size_t)cap));
+  LHIP(op, dmalloc(&S.lval, (size_t)cap));
+  LHIP(op, dmalloc(&S.lord, (size_t)cap));
+  LHIP(op, dmalloc(&S.lgid, (size_t)cap));
+  return FW_OK;
+}
+void free_log(LState& S) {
+  dfree(S.lts);
+  dfree(S.lval);
+  dfree(S.lord);
+  dfree(S.lgid);
+}
+int ensure_sel(fw_list* op, int64_t n) {
+  if (n <= op->sel_cap) return FW_OK;
+  const int64_t cap = std::max<int64_t>(n, op->sel_cap * 2);
+  dfree(op->flags8);
+  dfree(op->sel);
+  dfree(op->sel2);
+  dfree(op->keys);
+  dfree(op->keys2);
+  dfree(op->seg);
+  dfree(op->prog);
+  LHIP(op, dmalloc(&op->flags8, (size_t)cap));
+  LHIP(op, dmalloc(&op->sel, (size_t)cap));
+  LHIP(op, dmalloc(&op->sel2, (size_t)cap));
+  LHIP(op, dmalloc(&op->keys, (size_t)cap));
+  LHIP(op, dmalloc(&op->keys2, (size_t)cap));
+  LHIP(op, dmalloc(&op->seg, (size_t)cap + 1));
+  LHIP(op, dmalloc(&op->prog, (size_t)cap));
+  op->sel_cap = cap;
+  return FW_OK;
+}
+// grows a row / element column set, keeping the first `keep` values
+int grow_cols(fw_list* op, int64_t** cols[], int ncol, int64_t old_cap, int64_t cap, int64_t keep) {
+  for (int i = 0; i < ncol; i++) {
+    int64_t* n = nullptr;
+    LHIP(op, dmalloc(&n, (size_t)cap));
+    if (keep) LHIP(op, hipMemcpyAsync(n, *cols[i], (size_t)keep * 8, hipMemcpyDeviceToDevice, op->stream));
+    LHIP(op, hipStreamSynchronize(op->stream));
+    dfree(*cols[i]);
+    *cols[i] = n;
+  }
+  (void)old_cap;
+  return FW_OK;
+}
+int ensure_rows(fw_list* op, int64_t need) {
+  if (need <= op->rcap) return FW_OK;
+  const int64_t cap = std::max<int64_t>(need, op->rcap * 2);
+  int64_t** cols[] = {&op->S.rkey, &op->S.rstart, &op->S.rend, &op->S.rcnt, &op->S.rsum, &op->S.rmin,
+                      &op->S.rmax, &op->S.rfirst, &op->S.roff};
+  LRET(grow_cols(op, cols, 9, op->rcap, cap, (int64_t)op->h_ctr->rows));
+  op->rcap = cap;
+  return FW_OK;
+}
+int ensure_elems(fw_list* op, int64_t need) {
+  if (need <= op->S.ecap) return FW_OK;
+  const int64_t cap = std::max<int64_t>(need, op->S.ecap * 2);
+  int64_t** cols[] = {&op->S.ets, &op->S.eval, &op->S.eord};
+  LRET(grow_cols(op, cols, 3, op->S.ecap, cap, (int64_t)op->h_ctr->elems));
+  op->S.ecap = cap;
+  return FW_OK;
+}
+int ensure_side(fw_list* op, int64_t need) {
+  if (need <= op->scap) return FW_OK;
+  const int64_t cap = std::max<int64_t>(need, op->scap * 2);
+  int64_t** cols[] = {&op->S.skey, &op->S.sts, &op->S.sval};
+  LRET(grow_cols(op, cols, 3, op->scap, cap, (int64_t)op->h_ctr->side));
+  op->scap = cap;
+  return FW_OK;
+}
+
+// stable selection of the log positions whose flag is set: sel[0 .. *m)
+int select_positions(fw_list* op, const uint8_t* flags, int64_t n, uint32_t* out, int64_t* m) {
+  rocprim::counting_iterator<uint32_t> it(0);
+  unsigned long long* d_cnt = &op->S.ctr->count;
+  size_t bytes = 0;
+  LHIP(op, rocprim::select(nullptr, bytes, it, flags, out, d_cnt, (size_t)n, op->stream));
+  LRET(ensure_tmp(op, bytes));
+  bytes = op->tmp_bytes;
+  LHIP(op, rocprim::select(op->tmp, bytes, it, flags, out, d_cnt, (size_t)n, op->stream));
+  LRET(read_ctr(op));
+  *m = (int64_t)op->h_ctr->count;
+  return FW_OK;
+}
+
+// the live elements of the groups flagged `bit`, grouped by list (a stable radix sort by group keeps list
+// order), then one walk over them; relaunched with a larger element buffer until every list is done
+template <bool PUSH>
+int walk_lists(fw_list* op, uint32_t bit, int64_t base_new) {
+  LRET(ensure_sel(op, op->n_log));
+  hipLaunchKernelGGL(k_sel_flags, dim3(grid_for(op->n_log)), dim3(256), 0, op->stream, op->S, op->n_log, bit,
+                     op->flags8);
+  int64_t m = 0;
+  LRET(select_positions(op, op->flags8, op->n_log, op->sel, &m));
+  if (m == 0) return FW_OK;
+  hipLaunchKernelGGL(k_sel_keys, dim3(grid_for(m)), dim3(256), 0, op->stream, op->S, op->sel, m, op->keys);
+  int bits = 1;
+  while (((int64_t)1 << bits) <= (int64_t)op->S.gmask) bits++;
+  size_t bytes = 0;
+  LHIP(op, rocprim::radix_sort_pairs(nullptr, bytes, op->keys, op->keys2, op->sel, op->sel2, (size_t)m, 0, bits,
+                                     op->stream));
+  LRET(ensure_tmp(op, bytes));
+  bytes = op->tmp_bytes;
+  LHIP(op, rocprim::radix_sort_pairs(op->tmp, bytes, op->keys, op->keys2, op->sel, op->sel2, (size_t)m, 0, bits,
+                                     op->stream));
+  hipLaunchKernelGGL(k_seg_flags, dim3(grid_for(m)), dim3(256), 0, op->stream, op->keys2, m, op->flags8);
+  int64_t nseg = 0;
+  LRET(select_positions(op, op->flags8, m, op->seg, &nseg));
+  const uint32_t mm = (uint32_t)m;
+  LHIP(op, hipMemcpyAsync(op->seg + nseg, &mm, 4, hipMemcpyHostToDevice, op->stream));
+  LHIP(op, hipMemsetAsync(op->prog, 0xff, (size_t)nseg * 8, op->stream));
+  for (int round = 0;; round++) {
+    LHIP(op, hipMemsetAsync(&op->S.ctr->flags, 0, 4, op->stream));
+    hipLaunchKernelGGL(k_walk<PUSH>, dim3(grid_for(nseg)), dim3(256), 0, op->stream, op->c, op->S, op->sel2,
+                       op->keys2, op->seg, nseg, base_new, op->wm, op->prog);
+    LHIP(op, hipGetLastError());
+    LRET(read_ctr(op));
+    if (!(op->h_ctr->flags & LF_ELEMS)) break;
+    if (round > 64) return set_err(op, FW_ERR_STATE, "list walk made no progress");
+    LRET(ensure_elems(op, op->S.ecap * 2));
+  }
+  return FW_OK;
+}
+
+// drops dead elements (stable) and tombstones; the map grows to hold `groups_needed` at <= 1/2 load
+int compact(fw_list* op, int64_t groups_needed) {
+  LState o = op->S, S = op->S;
+  int64_t gcap = op->gcap;
+  while (gcap < 2 * groups_needed) gcap *= 2;
+  LRET(alloc_map(op, S, gcap));
+  int32_t* remap = nullptr;
+  LHIP(op, dmalloc(&remap, (size_t)op->gcap));
+  LHIP(op, hipMemsetAsync(&op->S.ctr->live_groups, 0, 8, op->stream));
+  LHIP(op, hipMemsetAsync(&op->S.ctr->tombs, 0, 8, op->stream));
+  hipLaunchKernelGGL(k_rebuild_map, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, op->c, o, S, remap);
+  // the live elements, in order, remapped
+  LRET(ensure_sel(op, op->n_log));
+  hipLaunchKernelGGL(k_alive_flags, dim3(grid_for(op->n_log)), dim3(256), 0, op->stream, o.lgid, op->n_log, op->flags8);
+  int64_t m = 0;
+  LRET(select_positions(op, op->flags8, op->n_log, op->sel, &m));
+  LState L = S;
+  LRET(alloc_log(op, L, op->lcap));
+  hipLaunchKernelGGL(k_gather_log, dim3(grid_for(m)), dim3(256), 0, op->stream, o, L, op->sel, m, remap);
+  LHIP(op, hipStreamSynchronize(op->stream));
+  dfree(remap);
+  free_map(o);
+  free_log(o);
+  op->S = L;
+  op->gcap = gcap;
+  op->n_log = m;
+  LHIP(op, hipMemsetAsync(&op->S.ctr->dead, 0, 8, op->stream));
+  LRET(read_ctr(op));
+  if (op->h_ctr->flags & LF_MAP_FULL) return set_err(op, FW_ERR_CAPACITY, "list state map full");
+  op->grows++;
+  return FW_OK;
+}
+
+// room for `extra` more log entries: compaction when dead entries are the majority, else a larger log
+int grow_log(fw_list* op, int64_t extra) {
+  if (op->n_log + extra <= op->lcap) return FW_OK;
+  if (2 * (int64_t)op->h_ctr->dead > op->n_log) {
+    LRET(compact(op, (int64_t)op->h_ctr->live_groups));
+    if (op->n_log + extra <= op->lcap) return FW_OK;
+  }
+  const int64_t cap = std::max<int64_t>(op->n_log + extra, op->lcap * 2);
+  LState L = op->S;
+  LRET(alloc_log(op, L, cap));
+  if (op->n_log) {
+    LHIP(op, hipMemcpyAsync(L.lts, op->S.lts, (size_t)op->n_log * 8, hipMemcpyDeviceToDevice, op->stream));
+    LHIP(op, hipMemcpyAsync(L.lval, op->S.lval, (size_t)op->n_log * 8, hipMemcpyDeviceToDevice, op->stream));
+    LHIP(op, hipMemcpyAsync(L.lord, op->S.lord, (size_t)op->n_log * 8, hipMemcpyDeviceToDevice, op->stream));
+    LHIP(op, hipMemcpyAsync(L.lgid, op->S.lgid, (size_t)op->n_log * 4, hipMemcpyDeviceToDevice, op->stream));
+  }
+  LHIP(op, hipStreamSynchronize(op->stream));
+  free_log(op->S);
+  op->S.lts = L.lts;
+  op->S.lval = L.lval;
+  op->S.lord = L.lord;
+  op->S.lgid = L.lgid;
+  op->lcap = cap;
+  op->grows++;
+  return FW_OK;
+}
+
+int maybe_compact(fw_list* op) {
+  const int64_t dead = (int64_t)op->h_ctr->dead, tombs = (int64_t)op->h_ctr->tombs;
+  if ((dead > (1 << 16) && 2 * dead > op->n_log) || 4 * tombs > op->gcap)
+    return compact(op, (int64_t)op->h_ctr->live_groups);
+  return FW_OK;
+}
+
+int push_device(fw_list* op, const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int64_t n) {
+  if (n == 0) return FW_OK;
+  if (n > op->max_batch) return set_err(op, FW_ERR_ARG, "batch of %lld records exceeds max_batch %lld", (long long)n,
+                                        (long long)op->max_batch);
+  if (op->cfg.key_kind == FW_KEY_HASHED && !kh) return set_err(op, FW_ERR_ARG, "key_hash required for FW_KEY_HASHED");
+  LRET(read_ctr(op));
+  LRET(ensure_side(op, (int64_t)op->h_ctr->side + n));
+  LHIP(op, hipMemsetAsync(&op->S.ctr->flags, 0, 8, op->stream));  // flags, need_seq
+  hipLaunchKernelGGL(k_lp_count, dim3(grid_for(n)), dim3(256), 0, op->stream, op->c, op->S, key, ts, val, kh, n, op->wm,
+                     op->wcnt);
+  size_t bytes = 0;
+  LHIP(op, rocprim::inclusive_scan(nullptr, bytes, op->wcnt, op->woff + 1, (size_t)n, rocprim::plus<uint32_t>(),
+                                   op->stream));
+  LRET(ensure_tmp(op, bytes));
+  bytes = op->tmp_bytes;
+  LHIP(op, hipMemsetAsync(op->woff, 0, 4, op->stream));
+  LHIP(op, rocprim::inclusive_scan(op->tmp, bytes, op->wcnt, op->woff + 1, (size_t)n, rocprim::plus<uint32_t>(),
+                                   op->stream));
+  uint32_t total = 0;
+  LHIP(op, hipMemcpyAsync(&total, op->woff + n, 4, hipMemcpyDeviceToHost, op->stream));
+  LRET(read_ctr(op));
+  if (op->h_ctr->flags & LF_NO_TS)
+    return set_err(op, FW_ERR_NO_TIMESTAMP,
+                   "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time characteristic set to "
+                   "'ProcessingTime', or did you forget to call 'DataStream.assignTimestampsAndWatermarks(...)'?");
+  if (op->h_ctr->flags & LF_KEY_GROUP)
+    return set_err(op, FW_ERR_KEY_GROUP, "a key of the batch is outside the handle's KeyGroupRange");
+  const int64_t E = total;
+  // room: the log, the map (<= 1/2 load), a row per possibly firing entry
+  if ((int64_t)op->h_ctr->live_groups + E > op->gcap / 2) LRET(compact(op, (int64_t)op->h_ctr->live_groups + E));
+  LRET(grow_log(op, E));
+  LRET(ensure_rows(op, (int64_t)op->h_ctr->rows + E));
+  const int64_t base = op->n_log;
+  hipLaunchKernelGGL(k_lp_append, dim3(grid_for(n)), dim3(256), 0, op->stream, op->c, op->S, key, ts, val, kh, n,
+                     op->wm, op->wcnt, op->woff, base, op->ord_base);
+  LHIP(op, hipGetLastError());
+  op->n_log += E;
+  op->ord_base += n;
+  op->records_in += n;
+  LRET(read_ctr(op));
+  if (op->h_ctr->flags & LF_MAP_FULL) return set_err(op, FW_ERR_CAPACITY, "list state map full");
+  if (op->h_ctr->need_seq) LRET(walk_lists<true>(op, GF_TOUCH, base));
+  LRET(read_ctr(op));
+  return maybe_compact(op);
+}
+
+}  // namespace
+
+extern "C" {
+
+int fw_list_create(const fw_list_config* cfg, fw_list** out) {
+  if (!cfg || !out) return FW_ERR_ARG;
+  *out = nullptr;
+  fw_list* op = new fw_list();
+  op->cfg = *cfg;
+  const fw_list_config& c = *cfg;
+  auto fail = [&](int code, const char* msg) {
+    fprintf(stderr, "fw_list_create: %s\n", msg);
+    delete op;
+    return code;
+  };
+  if (c.assigner != FW_TUMBLING && c.assigner != FW_SLIDING && c.assigner != FW_GLOBAL)
+    return fail(FW_ERR_UNSUPPORTED, "assigner must be FW_TUMBLING, FW_SLIDING or FW_GLOBAL");
+  if (c.assigner != FW_GLOBAL && c.size <= 0) return fail(FW_ERR_ARG, "window size must be positive");
+  if (c.assigner == FW_SLIDING && (c.slide <= 0 || c.slide > c.size))
+    return fail(FW_ERR_ARG, "SlidingEventTimeWindows parameters must satisfy 0 < slide <= size");
+  if (c.assigner != FW_GLOBAL && (c.offset < 0 || c.offset >= (c.assigner == FW_SLIDING ? c.slide : c.size)))
+    return fail(FW_ERR_ARG, "window offset must be in [0, slide/size)");
+  if (c.allowed_lateness < 0) return fail(FW_ERR_ARG, "The allowed lateness cannot be negative.");
+  if (c.trigger != FW_TRIGGER_EVENT_TIME && c.trigger != FW_TRIGGER_COUNT) return fail(FW_ERR_ARG, "unknown trigger");
+  if (c.trigger == FW_TRIGGER_COUNT && c.trigger_count <= 0) return fail(FW_ERR_ARG, "CountTrigger count must be > 0");
+  if (c.evictor < FW_EVICT_NONE || c.evictor > FW_EVICT_DELTA) return fail(FW_ERR_ARG, "unknown evictor");
+  if (c.evictor == FW_EVICT_COUNT && c.evict_count < 0) return fail(FW_ERR_ARG, "CountEvictor count must be >= 0");
+  if (c.value_type < FW_VAL_I64 || c.value_type > FW_VAL_F32) return fail(FW_ERR_ARG, "unknown value type");
+  if (c.key_kind < FW_KEY_LONG || c.key_kind > FW_KEY_HASHED) return fail(FW_ERR_ARG, "unknown key kind");
+  const int32_t mp = c.max_parallelism ? c.max_parallelism : 128;
+  const int32_t kg0 = c.key_group_start < 0 ? 0 : c.key_group_start;
+  const int32_t kg1 = c.key_group_end < 0 ? mp - 1 : c.key_group_end;
+  if (mp <= 0 || mp > 32768 || kg0 > kg1 || kg1 >= mp) return fail(FW_ERR_ARG, "invalid KeyGroupRange");
+  op->c = LCfg{c.assigner, c.value_type, c.key_kind, c.trigger, c.purging, c.evictor, c.evict_after, c.side_output,
+               c.emit_contents, mp, kg0, kg1 - kg0 + 1, c.size, c.slide, c.offset, c.allowed_lateness,
+               c.trigger_count, c.evict_count, c.delta_threshold};
+  op->device = c.device;
+  if (hipSetDevice(c.device) != hipSuccess) return fail(FW_ERR_HIP, "hipSetDevice failed");
+  if (hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking) != hipSuccess) return fail(FW_ERR_HIP, "stream");
+  op->max_batch = c.max_batch > 0 ? c.max_batch : (1 << 24);
+  const int64_t fan = c.assigner == FW_SLIDING ? (c.size + c.slide - 1) / c.slide : 1;
+  const int64_t exp = c.expected_elements > 0 ? c.expected_elements : std::min<int64_t>(op->max_batch * fan, 1 << 22);
+  op->lcap = std::max<int64_t>(exp, 1024);
+  int64_t g = 1024;
+  while (g < 2 * std::min<int64_t>(op->lcap, 1 << 26)) g <<= 1;
+  op->gcap = g;
+  op->rcap = 1024;
+  op->scap = 1024;
+  op->S.ecap = 1024;
+  int rc = FW_OK;
+  if (hipHostMalloc((void**)&op->h_ctr, sizeof(LCounters), hipHostMallocDefault) != hipSuccess) rc = FW_ERR_HIP;
+  if (rc == FW_OK) memset(op->h_ctr, 0, sizeof(LCounters));
+  if (rc == FW_OK) rc = alloc_map(op, op->S, op->gcap);
+  if (rc == FW_OK) rc = alloc_log(op, op->S, op->lcap);
+  auto al = [&](int64_t** p, int64_t n) {
+    if (rc == FW_OK && dmalloc(p, (size_t)n) != hipSuccess) rc = FW_ERR_HIP;
+  };
+  for (int64_t** p : {&op->S.rkey, &op->S.rstart, &op->S.rend, &op->S.rcnt, &op->S.rsum, &op->S.rmin, &op->S.rmax,
+                      &op->S.rfirst, &op->S.roff})
+    al(p, op->rcap);
+  for (int64_t** p : {&op->S.ets, &op->S.eval, &op->S.eord}) al(p, op->S.ecap);
+  for (int64_t** p : {&op->S.skey, &op->S.sts, &op->S.sval}) al(p, op->scap);
+  for (int64_t** p : {&op->in_key, &op->in_ts, &op->in_val}) al(p, op->max_batch);
+  if (rc == FW_OK && dmalloc(&op->in_kh, (size_t)op->max_batch) != hipSuccess) rc = FW_ERR_HIP;
+  if (rc == FW_OK && dmalloc(&op->wcnt, (size_t)op->max_batch) != hipSuccess) rc = FW_ERR_HIP;
+  if (rc == FW_OK && dmalloc(&op->woff, (size_t)op->max_batch + 1) != hipSuccess) rc = FW_ERR_HIP;
+  if (rc == FW_OK && dmalloc(&op->S.ctr, 1) != hipSuccess) rc = FW_ERR_HIP;
+  if (rc == FW_OK && hipMemsetAsync(op->S.ctr, 0, sizeof(LCounters), op->stream) != hipSuccess) rc = FW_ERR_HIP;
+  if (rc == FW_OK && hipStreamSynchronize(op->stream) != hipSuccess) rc = FW_ERR_HIP;
+  if (rc != FW_OK) {
+    fw_list_destroy(op);
+    return rc;
+  }
+  *out = op;
+  return FW_OK;
+}
+
+void fw_list_destroy(fw_list* op) {
+  if (!op) return;
+  (void)hipSetDevice(op->device);
+  if (op->stream) (void)hipStreamSynchronize(op->stream);
+  free_map(op->S);
+  free_log(op->S);
+  for (int64_t** p : {&op->S.rkey, &op->S.rstart, &op->S.rend, &op->S.rcnt, &op->S.rsum, &op->S.rmin, &op->S.rmax,
+                      &op->S.rfirst, &op->S.roff, &op->S.ets, &op->S.eval, &op->S.eord, &op->S.skey, &op->S.sts,
+                      &op->S.sval, &op->in_key, &op->in_ts, &op->in_val})
+    dfree(*p);
+  dfree(op->in_kh);
+  dfree(op->wcnt);
+  dfree(op->woff);
+  dfree(op->S.ctr);
+  dfree(op->flags8);
+  dfree(op->sel);
+  dfree(op->sel2);
+  dfree(op->keys);
+  dfree(op->keys2);
+  dfree(op->seg);
+  dfree(op->prog);
+  if (op->tmp) (void)hipFree(op->tmp);
+  if (op->h_ctr) (void)hipHostFree(op->h_ctr);
+  if (op->stream) (void)hipStreamDestroy(op->stream);
+  delete op;
+}
+
+const char* fw_list_last_error(const fw_list* op) { return op ? op->err.c_str() : "null handle"; }
+
+int fw_list_push_batch_device(fw_list* op, const int64_t* key, const int64_t* ts, const void* val,
+                              const int32_t* key_hash, int64_t n) {
+  if (!op || n < 0 || (n && (!key || !ts || !val))) return set_err(op, FW_ERR_ARG, "invalid arguments");
+  (void)hipSetDevice(op->device);
+  return push_device(op, key, ts, (const int64_t*)val, key_hash, n);
+}
+
+int fw_list_push_batch(fw_list* op, const int64_t* key, const int64_t* ts, const void* val, const int32_t* key_hash,
+                       int64_t n) {
+  if (!op || n < 0 || (n && (!key || !ts || !val))) return set_err(op, FW_ERR_ARG, "invalid arguments");
+  (void)hipSetDevice(op->device);
+  for (int64_t o = 0; o < n; o += op->max_batch) {
+    const int64_t m = std::min(op->max_batch, n - o);
+    LHIP(op, hipMemcpyAsync(op->in_key, key + o, (size_t)m * 8, hipMemcpyHostToDevice, op->stream));
+    LHIP(op, hipMemcpyAsync(op->in_ts, ts + o, (size_t)m * 8, hipMemcpyHostToDevice, op->stream));
+    LHIP(op, hipMemcpyAsync(op->in_val, (const int64_t*)val + o, (size_t)m * 8, hipMemcpyHostToDevice, op->stream));
+    if (key_hash)
+      LHIP(op, hipMemcpyAsync(op->in_kh, key_hash + o, (size_t)m * 4, hipMemcpyHostToDevice, op->stream));
+    LRET(push_device(op, op->in_key, op->in_ts, op->in_val, key_hash ? op->in_kh : nullptr, m));
+  }
+  return FW_OK;
+}
+
+int fw_list_advance_watermark(fw_list* op, int64_t wm, int64_t* n_pending_rows) {
+  if (!op) return FW_ERR_ARG;
+  (void)hipSetDevice(op->device);
+  if (wm > op->wm) {  // HeapInternalTimerService.advanceWatermark: timers <= wm, in any order across lists
+    op->wm = wm;
+    LHIP(op, hipMemsetAsync(&op->S.ctr->nfire, 0, 16, op->stream));
+    hipLaunchKernelGGL(k_lw_due, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, op->c, op->S, wm);
+    LRET(read_ctr(op));
+    const int64_t nfire = (int64_t)op->h_ctr->nfire, nclean = (int64_t)op->h_ctr->nclean;
+    if (nfire) {
+      LRET(ensure_rows(op, (int64_t)op->h_ctr->rows + nfire));
+      LRET(walk_lists<false>(op, GF_FIRE, 0));
+    }
+    if (nfire || nclean) {
+      if (nclean)
+        hipLaunchKernelGGL(k_lw_clean_log, dim3(grid_for(op->n_log)), dim3(256), 0, op->stream, op->S, op->n_log);
+      hipLaunchKernelGGL(k_lw_clean_map, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, op->S);
+      LHIP(op, hipGetLastError());
+    }
+    LRET(read_ctr(op));
+    LRET(maybe_compact(op));
+  }
+  LRET(read_ctr(op));
+  if (n_pending_rows) *n_pending_rows = (int64_t)op->h_ctr->rows;
+  return FW_OK;
+}
+
+int fw_list_pending(fw_list* op, int64_t* n_rows, int64_t* n_elems, int64_t* n_side_rows) {
+  if (!op) return FW_ERR_ARG;
+  LRET(read_ctr(op));
+  if (n_rows) *n_rows = (int64_t)op->h_ctr->rows;
+  if (n_elems) *n_elems = (int64_t)op->h_ctr->elems;
+  if (n_side_rows) *n_side_rows = (int64_t)op->h_ctr->side;
+  return FW_OK;
+}
+
+int fw_list_drain(fw_list* op, const fw_list_rows* rows, int64_t cap_rows, const fw_list_elems* elems,
+                  int64_t cap_elems, int64_t* n_rows, int64_t* n_elems) {
+  if (!op || !rows) return set_err(op, FW_ERR_ARG, "invalid arguments");
+  (void)hipSetDevice(op->device);
+  LRET(read_ctr(op));
+  const int64_t nr = (int64_t)op->h_ctr->rows, ne = (int64_t)op->h_ctr->elems;
+  if (n_rows) *n_rows = nr;
+  if (n_elems) *n_elems = ne;
+  if (nr > cap_rows || (ne && (!elems || ne > cap_elems))) return set_err(op, FW_ERR_CAPACITY, "output too small");
+  const int64_t* src[] = {op->S.rkey, op->S.rstart, op->S.rend, op->S.rcnt, op->S.rsum, op->S.rmin, op->S.rmax,
+                          op->S.rfirst, op->S.roff};
+  int64_t* dst[] = {rows->key, rows->start, rows->end, rows->count, rows->sum, rows->min, rows->max, rows->first,
+                    rows->elem_off};
+  for (int i = 0; i < 9; i++)
+    if (dst[i] && nr) LHIP(op, hipMemcpyAsync(dst[i], src[i], (size_t)nr * 8, hipMemcpyDeviceToHost, op->stream));
+  if (ne) {
+    const int64_t* es[] = {op->S.ets, op->S.eval, op->S.eord};
+    int64_t* ed[] = {elems->ts, elems->val, elems->ordinal};
+    for (int i = 0; i < 3; i++)
+      if (ed[i]) LHIP(op, hipMemcpyAsync(ed[i], es[i], (size_t)ne * 8, hipMemcpyDeviceToHost, op->stream));
+  }
+  LHIP(op, hipMemsetAsync(&op->S.ctr->rows, 0, 16, op->stream));  // rows, elems
+  LHIP(op, hipStreamSynchronize(op->stream));
+  op->fired_total += nr;
+  op->h_ctr->rows = op->h_ctr->elems = 0;
+  return FW_OK;
+}
+
+int fw_list_drain_side(fw_list* op, const fw_side_rows* host_dst, int64_t cap, int64_t* n) {
+  if (!op || !host_dst) return set_err(op, FW_ERR_ARG, "invalid arguments");
+  (void)hipSetDevice(op->device);
+  LRET(read_ctr(op));
+  const int64_t ns = (int64_t)op->h_ctr->side;
+  if (n) *n = ns;
+  if (ns > cap) return set_err(op, FW_ERR_CAPACITY, "output too small");
+  if (ns) {
+    LHIP(op, hipMemcpyAsync(host_dst->key, op->S.skey, (size_t)ns * 8, hipMemcpyDeviceToHost, op->stream));
+    LHIP(op, hipMemcpyAsync(host_dst->ts, op->S.sts, (size_t)ns * 8, hipMemcpyDeviceToHost, op->stream));
+    LHIP(op, hipMemcpyAsync(host_dst->val, op->S.sval, (size_t)ns * 8, hipMemcpyDeviceToHost, op->stream));
+  }
+  LHIP(op, hipMemsetAsync(&op->S.ctr->side, 0, 8, op->stream));
+  LHIP(op, hipStreamSynchronize(op->stream));
+  return FW_OK;
+}
+
+int fw_list_get_stats(fw_list* op, fw_stats* out) {
+  if (!op || !out) return set_err(op, FW_ERR_ARG, "invalid arguments");
+  (void)hipSetDevice(op->device);
+  uint8_t* has = nullptr;
+  unsigned long long* d2 = nullptr;
+  unsigned long long h2[2] = {0, 0};
+  LHIP(op, dmalloc(&has, (size_t)op->gcap));
+  LHIP(op, dmalloc(&d2, 2));
+  LHIP(op, hipMemsetAsync(has, 0, (size_t)op->gcap, op->stream));
+  LHIP(op, hipMemsetAsync(d2, 0, 16, op->stream));
+  if (op->n_log)
+    hipLaunchKernelGGL(k_mark_lists, dim3(grid_for(op->n_log)), dim3(256), 0, op->stream, op->S, op->n_log, has);
+  hipLaunchKernelGGL(k_count_state, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, op->c, op->S, has, d2);
+  LHIP(op, hipMemcpyAsync(h2, d2, 16, hipMemcpyDeviceToHost, op->stream));
+  LRET(read_ctr(op));
+  dfree(has);
+  dfree(d2);
+  memset(out, 0, sizeof *out);
+  out->records_in = op->records_in;
+  out->late_records_dropped = (int64_t)op->h_ctr->late;
+  out->keyed_state_entries = (int64_t)h2[0];
+  out->event_time_timers = (int64_t)h2[1];
+  out->current_watermark = op->wm;
+  out->fired_rows_total = op->fired_total + (int64_t)op->h_ctr->rows;
+  out->pending_rows = (int64_t)op->h_ctr->rows;
+  out->pending_side_rows = (int64_t)op->h_ctr->side;
+  out->table_capacity = op->gcap;
+  out->table_grows = op->grows;
+  return FW_OK;
+}
+
+int fw_list_snapshot_key_group(fw_list* op, int32_t key_group, const fw_list_state* dst, int64_t cap_lists,
+                               int64_t cap_elems, int64_t* n_lists, int64_t* n_elems) {
+  if (!op) return FW_ERR_ARG;
+  (void)hipSetDevice(op->device);
+  if ((uint32_t)(key_group - op->c.kg0) >= (uint32_t)op->c.nkg)
+    return set_err(op, FW_ERR_KEY_GROUP, "key group %d is not in the handle's KeyGroupRange", key_group);
+  // the key group's lists: its live groups, and its live elements grouped by list in list order
+  LRET(ensure_sel(op, std::max(op->n_log, op->gcap)));
+  hipLaunchKernelGGL(k_kg_flags_map, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, op->S, key_group, op->flags8);
+  int64_t ng = 0;
+  LRET(select_positions(op, op->flags8, op->gcap, op->seg, &ng));
+  int64_t m = 0;
+  if (op->n_log) {
+    hipLaunchKernelGGL(k_kg_flags_log, dim3(grid_for(op->n_log)), dim3(256), 0, op->stream, op->S, op->n_log, key_group,
+                       op->flags8);
+    LRET(select_positions(op, op->flags8, op->n_log, op->sel, &m));
+  }
+  if (n_lists) *n_lists = ng;
+  if (n_elems) *n_elems = m;
+  if (!dst || ng > cap_lists || m > cap_elems) return FW_OK;
+  std::vector<uint32_t> gids(ng), pos(m);
+  std::vector<int32_t> lg(m);
+  if (ng) LHIP(op, hipMemcpyAsync(gids.data(), op->seg, (size_t)ng * 4, hipMemcpyDeviceToHost, op->stream));
+  if (m) LHIP(op, hipMemcpyAsync(pos.data(), op->sel, (size_t)m * 4, hipMemcpyDeviceToHost, op->stream));
+  LHIP(op, hipStreamSynchronize(op->stream));
+  // host gathers (a snapshot is a cold path): group columns, then the elements per list in log order
+  auto fetch64 = [&](const int64_t* d, int64_t i, int64_t* v) {
+    return hipMemcpy(v, d + i, 8, hipMemcpyDeviceToHost);
+  };
+  std::vector<int64_t> lts(op->n_log), lval(op->n_log), lord(op->n_log);
+  std::vector<int32_t> lgid(op->n_log);
+  if (op->n_log) {
+    LHIP(op, hipMemcpy(lts.data(), op->S.lts, (size_t)op->n_log * 8, hipMemcpyDeviceToHost));
+    LHIP(op, hipMemcpy(lval.data(), op->S.lval, (size_t)op->n_log * 8, hipMemcpyDeviceToHost));
+    LHIP(op, hipMemcpy(lord.data(), op->S.lord, (size_t)op->n_log * 8, hipMemcpyDeviceToHost));
+    LHIP(op, hipMemcpy(lgid.data(), op->S.lgid, (size_t)op->n_log * 4, hipMemcpyDeviceToHost));
+  }
+  std::vector<int64_t> rank(op->gcap, -1);
+  for (int64_t i = 0; i < ng; i++) rank[gids[i]] = i;
+  std::vector<int64_t> cnt(ng, 0), off(ng + 1, 0);
+  for (int64_t i = 0; i < m; i++) cnt[rank[lgid[pos[i]]]]++;
+  for (int64_t i = 0; i < ng; i++) off[i + 1] = off[i] + cnt[i];
+  std::vector<int64_t> fill(off.begin(), off.end() - 1);
+  for (int64_t i = 0; i < m; i++) {
+    const uint32_t e = pos[i];
+    const int64_t k = fill[rank[lgid[e]]]++;
+    if (dst->ts) dst->ts[k] = lts[e];
+    if (dst->val) dst->val[k] = lval[e];
+    if (dst->ordinal) dst->ordinal[k] = lord[e];
+  }
+  for (int64_t i = 0; i < ng; i++) {
+    const uint32_t g = gids[i];
+    int64_t key, start, c;
+    uint32_t fl;
+    LHIP(op, fetch64(op->S.gkey, g, &key));
+    LHIP(op, fetch64(op->S.gstart, g, &start));
+    LHIP(op, fetch64(op->S.gcnt, g, &c));
+    LHIP(op, hipMemcpy(&fl, op->S.gfl + g, 4, hipMemcpyDeviceToHost));
+    dst->key[i] = key;
+    dst->start[i] = start;
+    dst->end[i] = op->c.assigner == FW_GLOBAL ? LMAX : (int64_t)((uint64_t)start + (uint64_t)op->c.size);
+    dst->trigger_count[i] = c;
+    dst->timer[i] = (fl & GF_TIMER) ? 1 : 0;
+    dst->n_elems[i] = cnt[i];
+  }
+  return FW_OK;
+}
+
+int fw_list_restore_key_group(fw_list* op, int32_t key_group, const fw_list_state* src, int64_t n_lists,
+                              int64_t n_elems) {
+  if (!op || (n_lists && !src)) return set_err(op, FW_ERR_ARG, "invalid arguments");
+  (void)hipSetDevice(op->device);
+  if ((uint32_t)(key_group - op->c.kg0) >= (uint32_t)op->c.nkg)
+    return set_err(op, FW_ERR_KEY_GROUP, "key group %d is not in the handle's KeyGroupRange", key_group);
+  if (n_lists == 0) return FW_OK;
+  int64_t total = 0, max_ord = -1;
+  for (int64_t i = 0; i < n_lists; i++) {
+    if (src->n_elems[i] < 0) return set_err(op, FW_ERR_ARG, "negative list length");
+    total += src->n_elems[i];
+    const int64_t s = src->start[i];
+    const int64_t e = op->c.assigner == FW_GLOBAL ? LMAX : (int64_t)((uint64_t)s + (uint64_t)op->c.size);
+    if (src->end[i] != e || (op->c.assigner == FW_GLOBAL && s != LMIN))
+      return set_err(op, FW_ERR_ARG, "list %lld: window [%lld, %lld) is not one of the assigner's", (long long)i,
+                     (long long)s, (long long)src->end[i]);
+    if (op->c.key_kind != FW_KEY_HASHED) {
+      const int64_t k = src->key[i];
+      const int32_t h = op->c.key_kind == FW_KEY_INT ? (int32_t)k : (int32_t)(k ^ (int64_t)((uint64_t)k >> 32));
+      // MathUtils.murmurHash (host restatement) % maxParallelism
+      uint32_t c = (uint32_t)h;
+      c *= 0xcc9e2d51u;
+      c = (c << 15) | (c >> 17);
+      c *= 0x1b873593u;
+      c = (c << 13) | (c >> 19);
+      c = c * 5u + 0xe6546b64u;
+      c ^= 4u;
+      c ^= c >> 16;
+      c *= 0x85ebca6bu;
+      c ^= c >> 13;
+      c *= 0xc2b2ae35u;
+      c ^= c >> 16;
+      int32_t r = (int32_t)c;
+      r = r >= 0 ? r : (r != INT32_MIN ? -r : 0);
+      if (r % op->c.max_par != key_group)
+        return set_err(op, FW_ERR_KEY_GROUP, "key %lld is not in key group %d", (long long)k, key_group);
+    }
+  }
+  if (total != n_elems) return set_err(op, FW_ERR_ARG, "list lengths do not add up to n_elems");
+  for (int64_t i = 0; i < n_elems; i++) max_ord = std::max(max_ord, src->ordinal[i]);
+  LRET(read_ctr(op));
+  if ((int64_t)op->h_ctr->live_groups + n_lists > op->gcap / 2) LRET(compact(op, (int64_t)op->h_ctr->live_groups + n_lists));
+  LRET(grow_log(op, n_elems));
+  // device copies of the lists' columns
+  int64_t *dk = nullptr, *ds = nullptr, *dc = nullptr, *dt = nullptr, *ets = nullptr, *evl = nullptr, *eod = nullptr;
+  int32_t *dg = nullptr, *eg = nullptr;
+  LHIP(op, dmalloc(&dk, (size_t)n_lists));
+  LHIP(op, dmalloc(&ds, (size_t)n_lists));
+  LHIP(op, dmalloc(&dc, (size_t)n_lists));
+  LHIP(op, dmalloc(&dt, (size_t)n_lists));
+  LHIP(op, dmalloc(&dg, (size_t)n_lists));
+  LHIP(op, hipMemcpy(dk, src->key, (size_t)n_lists * 8, hipMemcpyHostToDevice));
+  LHIP(op, hipMemcpy(ds, src->start, (size_t)n_lists * 8, hipMemcpyHostToDevice));
+  LHIP(op, hipMemcpy(dc, src->trigger_count, (size_t)n_lists * 8, hipMemcpyHostToDevice));
+  LHIP(op, hipMemcpy(dt, src->timer, (size_t)n_lists * 8, hipMemcpyHostToDevice));
+  // one thread: lists repeating a (key, window) append to it in order
+  hipLaunchKernelGGL(k_restore_groups, dim3(1), dim3(1), 0, op->stream, op->c, op->S, dk, ds, dc, dt, n_lists,
+                     key_group, dg);
+  std::vector<int32_t> hg(n_lists), eg_h(n_elems);
+  LHIP(op, hipMemcpyAsync(hg.data(), dg, (size_t)n_lists * 4, hipMemcpyDeviceToHost, op->stream));
+  LHIP(op, hipStreamSynchronize(op->stream));
+  for (int64_t i = 0, k = 0; i < n_lists; i++)
+    for (int64_t j = 0; j < src->n_elems[i]; j++) eg_h[k++] = hg[i];
+  if (n_elems) {
+    LHIP(op, dmalloc(&ets, (size_t)n_elems));
+    LHIP(op, dmalloc(&evl, (size_t)n_elems));
+    LHIP(op, dmalloc(&eod, (size_t)n_elems));
+    LHIP(op, dmalloc(&eg, (size_t)n_elems));
+    LHIP(op, hipMemcpy(ets, src->ts, (size_t)n_elems * 8, hipMemcpyHostToDevice));
+    LHIP(op, hipMemcpy(evl, src->val, (size_t)n_elems * 8, hipMemcpyHostToDevice));
+    LHIP(op, hipMemcpy(eod, src->ordinal, (size_t)n_elems * 8, hipMemcpyHostToDevice));
+    LHIP(op, hipMemcpy(eg, eg_h.data(), (size_t)n_elems * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_restore_elems, dim3(grid_for(n_elems)), dim3(256), 0, op->stream, op->S, ets, evl, eod, eg,
+                       n_elems, op->n_log);
+    LHIP(op, hipStreamSynchronize(op->stream));
+  }
+  for (auto p : {dk, ds, dc, dt, ets, evl, eod}) (void)hipFree(p);
+  (void)hipFree(dg);
+  (void)hipFree(eg);
+  LRET(read_ctr(op));
+  if (op->h_ctr->flags & LF_MAP_FULL) return set_err(op, FW_ERR_CAPACITY, "list state map full");
+  for (int64_t i = 0; i < n_lists; i++)
+    if (hg[i] < 0) return set_err(op, FW_ERR_CAPACITY, "list state map full");
+  op->n_log += n_elems;
+  op->ord_base = std::max(op->ord_base, max_ord + 1);
+  return FW_OK;
+}
+
+}  // extern "C"

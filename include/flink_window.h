@@ -422,6 +422,94 @@ int fw_wire_decode_keyed_device(fw_wire* w, const uint8_t* bytes, int64_t nbytes
 int fw_wire_encode_device(fw_wire* w, const fw_rows* rows, int64_t n, int32_t f64, uint8_t* out, int64_t cap,
                           int64_t* written);
 
+/* ---- f4: window contents (ListState) — WindowedStream.apply / process with an Iterable window function, and
+ * evictors (SJ/api/datastream/WindowedStream.java:1080-1123 builds a WindowOperator over a ListStateDescriptor, or an
+ * EvictingWindowOperator when an evictor is set).  The handle keeps every (key, window)'s list of elements in HBM
+ * and applies, element by element, EvictingWindowOperator.processElement / onEventTime / emitWindowContents
+ * (runtime/operators/windowing/EvictingWindowOperator.java:102-366; without an evictor WindowOperator.java:291-469):
+ *   assigners  FW_TUMBLING, FW_SLIDING (every window of a record holds a copy), FW_GLOBAL (GlobalWindows: never
+ *              late, never cleaned up; rows have start = Long.MIN_VALUE, end = Long.MAX_VALUE = their timestamp);
+ *   triggers   FW_TRIGGER_EVENT_TIME (EventTimeTrigger.java:37-73) or FW_TRIGGER_COUNT (CountTrigger.of(n),
+ *              CountTrigger.java:47-70), either wrapped in PurgingTrigger (purging = 1);
+ *   evictors   CountEvictor.of(n[, after]) (CountEvictor.java:55-78), TimeEvictor.of(ms[, after]) (TimeEvictor.java
+ *              :58-103; a timestamp of Long.MIN_VALUE is "no timestamp": nothing is evicted when the first element
+ *              has none), DeltaEvictor.of(threshold, f[, after]) with the built-in f(e, last) = last.field - e.field
+ *              in the field's Java arithmetic (DeltaEvictor.java:56-80).
+ * Every firing emits one row: the window, count = elements the function sees (after evictBefore), the built-in
+ * reduce over them in list order (sum wrapped to the field width, min, max; Double / Float fields by compare
+ * order, sums in list order, so f64 sums are exact), first = the arrival ordinal of the first element (-1 if none;
+ * the passthrough fields of reduce / sum(pos)), and with emit_contents the elements themselves in list order
+ * (timestamp, value, ordinal) for the host's Iterable function (InternalIterableWindowFunction).  A push is
+ * processed completely before the call returns (late firings and count triggers are ordered per (key, window)). */
+#define FW_GLOBAL 4
+#define FW_TRIGGER_EVENT_TIME 0
+#define FW_TRIGGER_COUNT 1
+#define FW_EVICT_NONE 0
+#define FW_EVICT_COUNT 1
+#define FW_EVICT_TIME 2
+#define FW_EVICT_DELTA 3
+typedef struct fw_list_config {
+  int32_t assigner;          /* FW_TUMBLING / FW_SLIDING / FW_GLOBAL                              */
+  int32_t value_type;        /* FW_VAL_*                                                          */
+  int32_t key_kind;          /* FW_KEY_*                                                          */
+  int32_t trigger;           /* FW_TRIGGER_*                                                      */
+  int32_t purging;           /* PurgingTrigger.of(trigger)                                        */
+  int32_t evictor;           /* FW_EVICT_*                                                        */
+  int32_t evict_after;       /* doEvictAfter                                                      */
+  int32_t side_output;       /* late records to the side output instead of numLateRecordsDropped */
+  int32_t emit_contents;     /* 1 = fired rows carry their elements                               */
+  int32_t max_parallelism;   /* as fw_config                                                      */
+  int32_t key_group_start;
+  int32_t key_group_end;
+  int32_t device;
+  int32_t pad0;
+  int64_t size, slide, offset, allowed_lateness;
+  int64_t trigger_count;     /* CountTrigger.of(n)                                                */
+  int64_t evict_count;       /* CountEvictor maxCount, TimeEvictor windowSize (ms)                */
+  double delta_threshold;    /* DeltaEvictor threshold                                            */
+  int64_t expected_elements; /* sizing hint: elements held at once (0 = default)                  */
+  int64_t max_batch;         /* largest n of one push (0 = 1 << 24)                               */
+} fw_list_config;
+typedef struct fw_list_rows {
+  int64_t *key, *start, *end, *count, *sum, *min, *max;
+  int64_t* first;            /* arrival ordinal of the row's first element, -1 if none          */
+  int64_t* elem_off;         /* index of the row's first element among the drained elements     */
+} fw_list_rows;
+typedef struct fw_list_elems {
+  int64_t *ts, *val, *ordinal;
+} fw_list_elems;
+/* A key group's list state, for snapshot / restore (the heap backend writes "window-contents" per key group:
+ * HeapKeyedStateBackend.java:370-381): per (key, window) its list, CountTrigger's count and whether its
+ * EventTimeTrigger timer is registered; the elements of all lists concatenated in list order. */
+typedef struct fw_list_state {
+  int64_t *key, *start, *end, *trigger_count, *timer, *n_elems;  /* per list   */
+  int64_t *ts, *val, *ordinal;                                   /* elements   */
+} fw_list_state;
+typedef struct fw_list fw_list;
+int fw_list_create(const fw_list_config* cfg, fw_list** out);
+void fw_list_destroy(fw_list* op);
+const char* fw_list_last_error(const fw_list* op);
+/* processElement for a batch: host buffers, or device buffers on the handle's device (key_hash as fw_push_batch) */
+int fw_list_push_batch(fw_list* op, const int64_t* key, const int64_t* ts, const void* val, const int32_t* key_hash,
+                       int64_t n);
+int fw_list_push_batch_device(fw_list* op, const int64_t* key, const int64_t* ts, const void* val,
+                              const int32_t* key_hash, int64_t n);
+/* processWatermark: the EventTimeTrigger timers <= wm fire their lists, cleanup timers drop them */
+int fw_list_advance_watermark(fw_list* op, int64_t wm, int64_t* n_pending_rows);
+int fw_list_pending(fw_list* op, int64_t* n_rows, int64_t* n_elems, int64_t* n_side_rows);
+/* copies the pending rows (and elements: elem_off counts from the first drained element) into host arrays and
+ * clears them; FW_ERR_CAPACITY (nothing drained) when either capacity is too small */
+int fw_list_drain(fw_list* op, const fw_list_rows* rows, int64_t cap_rows, const fw_list_elems* elems,
+                  int64_t cap_elems, int64_t* n_rows, int64_t* n_elems);
+int fw_list_drain_side(fw_list* op, const fw_side_rows* host_dst, int64_t cap, int64_t* n);
+int fw_list_get_stats(fw_list* op, fw_stats* out);
+/* per key group: the lists (dst NULL or a capacity too small: only the counts) / restored into the handle, appended
+ * to a list already present */
+int fw_list_snapshot_key_group(fw_list* op, int32_t key_group, const fw_list_state* dst, int64_t cap_lists,
+                               int64_t cap_elems, int64_t* n_lists, int64_t* n_elems);
+int fw_list_restore_key_group(fw_list* op, int32_t key_group, const fw_list_state* src, int64_t n_lists,
+                              int64_t n_elems);
+
 /* Synthetic source used by the benchmarks (the same counter-based generator as the CPU
  * baseline and the tests): record i of stream `seed` has
  *   key = splitmix64(seed ^ 4i) mod num_keys  (uniform)  or Zipf(zipf_s) over num_keys,

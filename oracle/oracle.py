@@ -215,6 +215,126 @@ class CountWindowOracle:
         return out
 
 
+# ---- f4: window-contents (ListState) operators (list_oracle.h) -----------------------------------------
+LIST_TRIGGERS = {"event_time": 0, "count": 1}
+LIST_EVICTORS = {"none": 0, "count": 1, "time": 2, "delta": 3}
+_LIST_ASSIGNERS = {"tumbling": TUMBLING, "sliding": SLIDING, "global": 3}
+
+
+class OracleListCfg(ctypes.Structure):
+    _fields_ = [("assigner", ctypes.c_int32), ("value_type", ctypes.c_int32), ("size", ctypes.c_int64),
+                ("slide", ctypes.c_int64), ("offset", ctypes.c_int64), ("lateness", ctypes.c_int64),
+                ("trigger", ctypes.c_int32), ("purging", ctypes.c_int32), ("trigger_count", ctypes.c_int64),
+                ("evictor", ctypes.c_int32), ("evict_after", ctypes.c_int32), ("evict_count", ctypes.c_int64),
+                ("delta_threshold", ctypes.c_double), ("side_output", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+LIST_ROW_DTYPE = np.dtype([("key", "<i8"), ("start", "<i8"), ("end", "<i8"), ("count", "<i8"), ("sum", "<i8"),
+                           ("min", "<i8"), ("max", "<i8"), ("first", "<i8"), ("elem_off", "<i8"), ("epoch", "<i8")])
+LIST_ELEM_DTYPE = np.dtype([("ts", "<i8"), ("val", "<i8"), ("ord", "<i8")])
+
+
+def _list_lib():
+    L = lib()
+    if not getattr(L, "_list_ready", False):
+        P = ctypes.c_void_p
+        I64P = ctypes.POINTER(ctypes.c_int64)
+        L.oracle_list_create.restype = P
+        L.oracle_list_create.argtypes = [ctypes.POINTER(OracleListCfg)]
+        L.oracle_list_destroy.argtypes = [P]
+        L.oracle_list_process.argtypes = [P, I64P, I64P, I64P, ctypes.c_int64]
+        L.oracle_list_watermark.argtypes = [P, ctypes.c_int64]
+        for f in ("oracle_list_num_rows", "oracle_list_num_elems", "oracle_list_num_side_rows",
+                  "oracle_list_late_dropped", "oracle_list_num_state_entries", "oracle_list_num_timers"):
+            getattr(L, f).restype = ctypes.c_int64
+            getattr(L, f).argtypes = [P]
+        L.oracle_list_get_rows.argtypes = [P, P]
+        L.oracle_list_get_elems.argtypes = [P, P]
+        L.oracle_list_get_side_rows.argtypes = [P, I64P, I64P, I64P, I64P]
+        L._list_ready = True
+    return L
+
+
+def make_list_cfg(assigner="tumbling", size=0, slide=0, offset=0, lateness=0, trigger="event_time", trigger_count=0,
+                  purging=False, evictor="none", evict_after=False, evict_arg=0, threshold=0.0, side_output=False,
+                  value_type="i64"):
+    return OracleListCfg(_LIST_ASSIGNERS[assigner], _VALTYPES[value_type], size, slide, offset, lateness,
+                         LIST_TRIGGERS[trigger], int(purging), trigger_count, LIST_EVICTORS[evictor], int(evict_after),
+                         evict_arg, float(threshold), int(side_output), 0)
+
+
+class ListWindowOracle:
+    """EvictingWindowOperator / WindowOperator over ListState with an Iterable window function (list_oracle.h):
+    rows (key, window, count, sum, min, max, first ordinal, offset of the contents, epoch) and the contents of
+    every firing."""
+
+    def __init__(self, **cfg):
+        self.cfg = make_list_cfg(**cfg)
+        self._h = _list_lib().oracle_list_create(ctypes.byref(self.cfg))
+        if not self._h:
+            raise ValueError("invalid list window configuration")
+
+    def close(self):
+        if self._h:
+            _list_lib().oracle_list_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def process(self, keys, ts, vals):
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        vals = np.ascontiguousarray(vals)
+        if vals.dtype == np.float64:
+            vals = vals.view(np.int64)
+        vals = np.ascontiguousarray(vals, dtype=np.int64)
+        rc = _list_lib().oracle_list_process(self._h, _i64p(keys), _i64p(ts), _i64p(vals), len(keys))
+        if rc != 0:
+            raise OracleError(rc)
+
+    def watermark(self, wm):
+        _list_lib().oracle_list_watermark(self._h, int(wm))
+
+    def rows(self):
+        n = _list_lib().oracle_list_num_rows(self._h)
+        out = np.zeros(n, dtype=LIST_ROW_DTYPE)
+        if n:
+            _list_lib().oracle_list_get_rows(self._h, out.ctypes.data)
+        return out
+
+    def elems(self):
+        n = _list_lib().oracle_list_num_elems(self._h)
+        out = np.zeros(n, dtype=LIST_ELEM_DTYPE)
+        if n:
+            _list_lib().oracle_list_get_elems(self._h, out.ctypes.data)
+        return out
+
+    def contents(self):
+        """[(row, elements)] in emission order"""
+        r, e = self.rows(), self.elems()
+        return [(x, e[x["elem_off"]:x["elem_off"] + x["count"]]) for x in r]
+
+    def side_rows(self):
+        n = _list_lib().oracle_list_num_side_rows(self._h)
+        cols = [np.zeros(n, dtype=np.int64) for _ in range(4)]
+        if n:
+            _list_lib().oracle_list_get_side_rows(self._h, *[_i64p(c) for c in cols])
+        return cols
+
+    @property
+    def late_dropped(self):
+        return _list_lib().oracle_list_late_dropped(self._h)
+
+    @property
+    def num_state_entries(self):
+        return _list_lib().oracle_list_num_state_entries(self._h)
+
+    @property
+    def num_timers(self):
+        return _list_lib().oracle_list_num_timers(self._h)
+
+
 def key_groups_long(keys, max_par):
     keys = np.ascontiguousarray(keys, dtype=np.int64)
     out = np.zeros(len(keys), dtype=np.int32)

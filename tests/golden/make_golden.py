@@ -173,6 +173,78 @@ COUNT_WINDOWS = [
                 {"input": [["key1", 1], ["key2", 1]], "expected": [["key1", 4], ["key2", 4]]}]},
 ]
 
+# f4: window-contents (ListState) operators with an Iterable window function — RichSumReducer (EWO:720-760:
+# output (key, sum of f1 over the contents)).  Each case is an EvictingWindowOperator; events as in CASES
+# (timestamps None = a StreamRecord without timestamp); `expected` of a phase lists the rows (key, sum,
+# timestamp) emitted up to its end, compared as a sorted multiset (TestHarnessUtil.assertOutputEqualsSorted).
+def lcfg(assigner, trigger, trigger_count=0, evictor="none", evict_after=False, evict_arg=0, threshold=0.0, size=0):
+    return {"assigner": assigner, "size": size, "trigger": trigger, "trigger_count": trigger_count,
+            "evictor": evictor, "evict_after": evict_after, "evict_arg": evict_arg, "threshold": threshold}
+
+
+def R(key, s, ts):
+    return [key, s, ts]
+
+
+_TE_A = [E("key2", 1, 1000), E("key2", 1, 4000), E("key1", 1, 20), E("key1", 1, 0), E("key1", 1, 999),
+         E("key2", 1, 3500), E("key2", 1, 2001), E("key2", 1, 1001)]
+_NO_TS = [E("key2", 1, None), E("key2", 1, None), E("key1", 1, None), E("key1", 1, None), E("key1", 1, None),
+          E("key2", 1, None), E("key2", 1, None), E("key2", 1, None)]
+_DELTA = [E("key2", 1, 3000), E("key2", 4, 3999), E("key1", 1, 20), E("key1", 1, 0), E("key1", 5, 999),
+          E("key2", 5, 1998), E("key2", 6, 1999), E("key2", 1, 1000)]
+LIST_WINDOWS = [
+    {"name": "time_evictor_evict_after", "source": "EWO:148-212",
+     "cfg": lcfg("global", "count", 2, "time", True, 2000),
+     "phases": [{"events": _TE_A, "expected": [R("key2", 2, MAX), R("key1", 2, MAX), R("key2", 3, MAX)]},
+                {"events": [E("key1", 1, 10999), E("key2", 1, 1002)],
+                 "expected": [R("key2", 2, MAX), R("key1", 2, MAX), R("key2", 3, MAX), R("key1", 4, MAX),
+                              R("key2", 5, MAX)]}]},
+    {"name": "time_evictor_evict_before", "source": "EWO:218-283",
+     "cfg": lcfg("tumbling", "count", 2, "time", False, 2000, size=4000),
+     "phases": [{"events": [E("key2", 1, 1000), E("key2", 1, 3999), E("key1", 1, 20), E("key1", 1, 0),
+                            E("key1", 1, 999), E("key1", 1, 5999), E("key2", 1, 3500), E("key2", 1, 2001),
+                            E("key2", 1, 1001)],
+                 "expected": [R("key2", 1, 3999), R("key1", 2, 3999), R("key2", 3, 3999)]},
+                {"events": [E("key1", 1, 6500), E("key2", 1, 1002)],
+                 "expected": [R("key2", 1, 3999), R("key1", 2, 3999), R("key2", 3, 3999), R("key1", 2, 7999),
+                              R("key2", 3, 3999)]}]},
+    {"name": "time_evictor_no_timestamp", "source": "EWO:289-352",
+     "cfg": lcfg("global", "count", 2, "time", True, 2000),
+     "phases": [{"events": _NO_TS, "expected": [R("key2", 2, MAX), R("key1", 2, MAX), R("key2", 4, MAX)]},
+                {"events": [E("key1", 1, None), E("key2", 1, None)],
+                 "expected": [R("key2", 2, MAX), R("key1", 2, MAX), R("key2", 4, MAX), R("key1", 4, MAX),
+                              R("key2", 6, MAX)]}]},
+    {"name": "delta_evictor_evict_before", "source": "EWO:357-428 (delta = new.f1 - old.f1)",
+     "cfg": lcfg("global", "count", 2, "delta", False, threshold=2.0),
+     "phases": [{"events": _DELTA, "expected": [R("key2", 4, MAX), R("key2", 11, MAX), R("key1", 2, MAX)]},
+                {"events": [E("key1", 3, 10999), E("key2", 10, 1000)],
+                 "expected": [R("key2", 4, MAX), R("key2", 11, MAX), R("key1", 2, MAX), R("key1", 8, MAX),
+                              R("key2", 10, MAX)]}]},
+    {"name": "delta_evictor_evict_after", "source": "EWO:432-500 (delta = new.f1 - old.f1)",
+     "cfg": lcfg("global", "count", 2, "delta", True, threshold=2.0),
+     "phases": [{"events": _DELTA, "expected": [R("key2", 5, MAX), R("key2", 15, MAX), R("key1", 2, MAX)]},
+                {"events": [E("key1", 9, 10999), E("key2", 10, 1000)],
+                 "expected": [R("key2", 5, MAX), R("key2", 15, MAX), R("key1", 2, MAX), R("key1", 16, MAX),
+                              R("key2", 22, MAX)]}]},
+    {"name": "count_evictor_evict_after", "source": "EWO:73-142",
+     "cfg": lcfg("global", "count", 2, "count", True, 4),
+     "phases": [{"events": [E(k, v, None) for k, v in _EW_INPUT],
+                 "expected": [R("key2", 2, MAX), R("key2", 4, MAX), R("key1", 2, MAX)]},
+                {"events": [E("key1", 1, None), E("key2", 1, None)],
+                 "expected": [R("key2", 2, MAX), R("key2", 4, MAX), R("key1", 2, MAX), R("key1", 4, MAX),
+                              R("key2", 6, MAX)]}]},
+    {"name": "tumbling_with_apply_count_evictor", "source": "EWO:645-697",
+     "cfg": lcfg("tumbling", "event_time", 0, "count", False, 4, size=4000),
+     "phases": [{"events": [E("key1", 1, 10), E("key1", 1, 100), W(1999), E("key1", 1, 1997), E("key1", 1, 1998),
+                            E("key1", 1, 2310), E("key1", 1, 2310), E("key2", 1, 2310), E("key2", 1, 2310),
+                            W(3999)],
+                 "expected": [R("key1", 4, 3999), R("key2", 2, 3999)]}]},
+]
+# WindowedStream.apply with the plain WindowOperator (ListState, no evictor): the WOT sequences of
+# CASES "sliding_3s_1s_reduce_sum" (testSlidingEventTimeWindowsApply, WOT:213-238) and "tumbling_3s_reduce_sum"
+# (testTumblingEventTimeWindowsApply, WOT:339-364) produce the same rows through RichSumReducer.
+LIST_APPLY_CASES = {"sliding_3s_1s_reduce_sum": "WOT:213-238", "tumbling_3s_reduce_sum": "WOT:339-364"}
+
 KEY_GROUPS = {
     "source": "CEP:71-82,170-215 (Integer keys: hashCode == value)",
     "max_parallelism": 10,
@@ -223,7 +295,8 @@ CLOSED_FORM = {"source": "EWC:571-629,659-740,865-877", "num_keys": 20, "num_ele
 
 
 def main():
-    out = {"keys": KEYS, "operator_cases": CASES, "session_example": SESSION_EXAMPLE, "count_windows": COUNT_WINDOWS, "key_groups": KEY_GROUPS,
+    out = {"keys": KEYS, "operator_cases": CASES, "session_example": SESSION_EXAMPLE, "count_windows": COUNT_WINDOWS,
+           "list_windows": LIST_WINDOWS, "list_apply_cases": LIST_APPLY_CASES, "key_groups": KEY_GROUPS,
            "window_start": WINDOW_START, "assigners": ASSIGNERS, "closed_form": CLOSED_FORM}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_kats.json")
     with open(path, "w") as f:

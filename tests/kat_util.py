@@ -64,3 +64,38 @@ def row_counters(rows, side_rows, case, with_window):
         got[t] += 1
     side = Counter((int(s["epoch"]), int(s["key"]), int(s["val"]), int(s["ts"])) for s in side_rows)
     return got, side
+
+
+LMIN, LMAX = -(1 << 63), (1 << 63) - 1
+
+
+def row_ts(start, end):
+    """the row's record timestamp: window.maxTimestamp() (GlobalWindow: Long.MAX_VALUE)"""
+    return LMAX if (start == LMIN and end == LMAX) else end - 1
+
+
+def replay_list_phases(case, keymap, op, watermark_epochs=False):
+    """f4 KATs (reference_kats.json "list_windows"): replays each phase's events through `op` (process(k, t, v),
+    watermark(t), rows() with key / start / end / sum), consecutive elements as one batch; after each phase
+    yields (got, expected) Counters of (key, sum, timestamp) over everything emitted so far (a missing
+    timestamp is Long.MIN_VALUE: StreamRecord without one)."""
+    for ph in case["phases"]:
+        pend = []
+
+        def flush():
+            if pend:
+                op.process(np.array([keymap[p[1]] for p in pend], dtype=np.int64),
+                           np.array([LMIN if p[3] is None else p[3] for p in pend], dtype=np.int64),
+                           np.array([p[2] for p in pend], dtype=np.int64))
+                pend.clear()
+
+        for ev in ph["events"]:
+            if ev[0] == "e":
+                pend.append(ev)
+            else:
+                flush()
+                op.watermark(ev[1])
+        flush()
+        expected = Counter((keymap[k], s, t) for k, s, t in ph["expected"])  # cumulative, as in the test
+        got = Counter((int(r["key"]), int(r["sum"]), row_ts(int(r["start"]), int(r["end"]))) for r in op.rows())
+        yield got, expected

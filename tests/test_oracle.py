@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as orc
-from tests.kat_util import expected_counters, load_kats, replay, row_counters
+from tests.kat_util import expected_counters, load_kats, replay, replay_list_phases, row_counters
 
 KATS = load_kats()
 KEYMAP = KATS["keys"]
@@ -209,3 +209,52 @@ def test_long_hash_java():
     assert L.oracle_long_hash(-1) == 0
     assert L.oracle_long_hash(1 << 32) == 1
     assert L.oracle_long_hash(123456789) == 123456789
+
+
+# ---- f4: window-contents (ListState) operators ----------------------------------------------------------
+def _list_oracle(c, **over):
+    kw = dict(assigner=c["assigner"], size=c["size"], trigger=c["trigger"], trigger_count=c["trigger_count"],
+              evictor=c["evictor"], evict_after=c["evict_after"], evict_arg=c["evict_arg"],
+              threshold=c["threshold"], value_type="i32")
+    kw.update(over)
+    return orc.ListWindowOracle(**kw)
+
+
+@pytest.mark.parametrize("case", KATS["list_windows"], ids=[c["name"] for c in KATS["list_windows"]])
+def test_list_window_kats(case):
+    # EvictingWindowOperatorTest sequences through the ListState restatement (RichSumReducer = the row's sum)
+    op = _list_oracle(case["cfg"])
+    for got, exp in replay_list_phases(case, KEYMAP, op):
+        assert got == exp
+
+
+@pytest.mark.parametrize("name", sorted(KATS["list_apply_cases"]))
+def test_list_apply_kats(name):
+    # WindowedStream.apply over the plain WindowOperator (ListState, EventTimeTrigger, no evictor): the same rows
+    # as the reduce KATs, with the contents of every firing in arrival order
+    case = next(c for c in KATS["operator_cases"] if c["name"] == name)
+    c = case["cfg"]
+    op = replay(case, KEYMAP, lambda _: orc.ListWindowOracle(assigner=c["assigner"], size=c["size"],
+                                                             slide=c["slide"], value_type="i32"),
+                flush_elements=False)
+    got, _ = row_counters(op.rows(), [], case, with_window=True)
+    exp, _ = expected_counters(case, KEYMAP, with_window=True)
+    assert got == exp
+    for r, el in op.contents():
+        assert len(el) == r["count"] and el["val"].sum() == r["sum"]
+        assert np.all(np.diff(el["ord"]) > 0)  # list order = arrival order
+
+
+def test_list_lateness_refires_contents():
+    # allowed lateness: an element of a fired, not yet cleaned-up window fires the whole list again
+    # (EventTimeTrigger.onElement: maxTimestamp <= watermark -> FIRE); the cleanup timer then drops it
+    op = orc.ListWindowOracle(assigner="tumbling", size=10, lateness=20)
+    op.process(np.array([1, 1]), np.array([1, 2]), np.array([5, 6]))
+    op.watermark(12)
+    op.process(np.array([1, 1]), np.array([3, 4]), np.array([7, 8]))
+    assert [int(r["count"]) for r in op.rows()] == [2, 3, 4]
+    assert op.num_state_entries == 1
+    op.watermark(29)
+    assert op.num_state_entries == 0 and op.num_timers == 0
+    op.process(np.array([1]), np.array([5]), np.array([9]))
+    assert op.late_dropped == 1
