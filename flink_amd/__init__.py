@@ -7,7 +7,8 @@ reference's operator interface for that path; see DESIGN.md and INTEGRATION.md.
 from .keygroups import (KeyGroupRange, assign_key_to_parallel_operator, assign_to_key_group,  # noqa: F401
                         compute_default_max_parallelism, compute_key_group_range_for_operator_index,
                         compute_operator_index_for_key_group, long_hash_code, murmur_hash, string_hash_code)
-from .windowing import (CountSumMinMax, CountWindows, ExtremalElementReduce, FirstElementReduce, HyperLogLog, TDigest,  # noqa: F401
+from .windowing import (CountEvictor, CountTrigger, DeltaEvictor, GlobalWindows, TimeEvictor,  # noqa: F401
+                        CountSumMinMax, CountWindows, ExtremalElementReduce, FirstElementReduce, HyperLogLog, TDigest,  # noqa: F401
                         EventTimeSessionWindows, EventTimeTrigger, PurgingTrigger, SlidingEventTimeWindows, Time,
                         TumblingEventTimeWindows, first_element_results, selected_elements, tdigest_quantile)
 
@@ -17,4 +18,7 @@ def __getattr__(name):
     if name == "GpuWindowOperator":
         from .operator import GpuWindowOperator
         return GpuWindowOperator
+    if name == "GpuListWindowOperator":
+        from .listwindow import GpuListWindowOperator
+        return GpuListWindowOperator
     raise AttributeError(name)

@@ -80,6 +80,34 @@ class FwWireStats(ctypes.Structure):
                                                "watermark")] + [("status", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
+FW_GLOBAL = 4
+FW_TRIGGER_EVENT_TIME, FW_TRIGGER_COUNT = 0, 1
+FW_EVICT_NONE, FW_EVICT_COUNT, FW_EVICT_TIME, FW_EVICT_DELTA = 0, 1, 2, 3
+
+
+class FwListConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "assigner", "value_type", "key_kind", "trigger", "purging", "evictor", "evict_after", "side_output",
+        "emit_contents", "max_parallelism", "key_group_start", "key_group_end", "device", "pad0")] + \
+        [(n, ctypes.c_int64) for n in ("size", "slide", "offset", "allowed_lateness", "trigger_count",
+                                       "evict_count")] + \
+        [("delta_threshold", ctypes.c_double), ("expected_elements", ctypes.c_int64), ("max_batch", ctypes.c_int64)]
+
+
+class FwListRows(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("key", "start", "end", "count", "sum", "min", "max", "first",
+                                               "elem_off")]
+
+
+class FwListElems(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("ts", "val", "ordinal")]
+
+
+class FwListState(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("key", "start", "end", "trigger_count", "timer", "n_elems", "ts", "val",
+                                               "ordinal")]
+
+
 # every exported symbol with its ctypes signature (restype, argtypes); mirrors include/flink_window.h
 SIGNATURES = {
     "fw_create": (ctypes.c_int, [ctypes.POINTER(FwConfig), ctypes.POINTER(VP)]),
@@ -125,6 +153,21 @@ SIGNATURES = {
                                              ctypes.POINTER(FwWireStats)]),
     "fw_wire_encode_device": (ctypes.c_int, [VP, ctypes.POINTER(FwRows), ctypes.c_int64, ctypes.c_int32, VP,
                                              ctypes.c_int64, I64P]),
+    "fw_list_create": (ctypes.c_int, [ctypes.POINTER(FwListConfig), ctypes.POINTER(VP)]),
+    "fw_list_destroy": (None, [VP]),
+    "fw_list_last_error": (ctypes.c_char_p, [VP]),
+    "fw_list_push_batch": (ctypes.c_int, [VP, VP, VP, VP, VP, ctypes.c_int64]),
+    "fw_list_push_batch_device": (ctypes.c_int, [VP, VP, VP, VP, VP, ctypes.c_int64]),
+    "fw_list_advance_watermark": (ctypes.c_int, [VP, ctypes.c_int64, I64P]),
+    "fw_list_pending": (ctypes.c_int, [VP, I64P, I64P, I64P]),
+    "fw_list_drain": (ctypes.c_int, [VP, ctypes.POINTER(FwListRows), ctypes.c_int64, ctypes.POINTER(FwListElems),
+                                     ctypes.c_int64, I64P, I64P]),
+    "fw_list_drain_side": (ctypes.c_int, [VP, ctypes.POINTER(FwSideRows), ctypes.c_int64, I64P]),
+    "fw_list_get_stats": (ctypes.c_int, [VP, ctypes.POINTER(FwStats)]),
+    "fw_list_snapshot_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwListState), ctypes.c_int64,
+                                                  ctypes.c_int64, I64P, I64P]),
+    "fw_list_restore_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwListState), ctypes.c_int64,
+                                                 ctypes.c_int64]),
     "fw_generate_device": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, VP,
                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, VP, VP, VP, VP, VP]),
 }

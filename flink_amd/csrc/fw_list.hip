@@ -42,6 +42,9 @@ constexpr int64_t LMAX = INT64_MAX;
 constexpr int64_t LMIN = INT64_MIN;
 #include "fw_jmath.h"
 
+#ifndef FW_LIST_ROOM
+#define FW_LIST_ROOM (int64_t(1) << 28)  // elements a walk may size its output for up front
+#endif
 enum : uint32_t { GF_TIMER = 1u, GF_TOUCH = 2u, GF_FIRE = 4u, GF_CLEAN = 8u };
 enum : uint32_t { LF_NO_TS = 1u, LF_KEY_GROUP = 2u, LF_MAP_FULL = 4u, LF_ELEMS = 8u };
 constexpr uint32_t G_EMPTY = 0u, G_BUSY = 1u, G_LIVE = 2u, G_TOMB = 3u;
@@ -299,14 +302,17 @@ __device__ int64_t evict(const LCfg& c, const LState& S, const uint32_t* pos, in
 
 // emitWindowContents (:334-366) of group g over the list pos[a .. j]: evictBefore, one row (+ the elements),
 // evictAfter.  False (nothing changed) when the element buffer cannot take the contents.
-__device__ bool emit_firing(const LCfg& c, const LState& S, uint32_t g, const uint32_t* pos, int64_t a, int64_t j) {
+__device__ bool emit_firing(const LCfg& c, const LState& S, uint32_t g, const uint32_t* pos, int64_t a, int64_t j,
+                            bool room) {
   int64_t cnt = 0;  // the elements the function sees
   if (c.evict_after)
     for (int64_t q = a; q <= j; q++) cnt += S.lgid[pos[q]] >= 0;
   else
     cnt = evict(c, S, pos, a, j, false);
   int64_t eoff = 0;
-  if (c.emit && cnt) {  // reserve the elements (rows were sized by the host: one per possible firing)
+  if (c.emit && cnt && room) {  // the host sized the element buffer for every possible firing
+    eoff = (int64_t)atomicAdd(&S.ctr->elems, (unsigned long long)cnt);
+  } else if (c.emit && cnt) {  // reserve the elements (rows were sized by the host: one per possible firing)
     unsigned long long cur = __hip_atomic_load(&S.ctr->elems, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     while (true) {
       if ((int64_t)cur + cnt > S.ecap) {
@@ -383,13 +389,14 @@ __device__ void purge(const LState& S, const uint32_t* pos, int64_t a, int64_t j
 template <bool PUSH>
 __global__ __launch_bounds__(256) void k_walk(LCfg c, LState S, const uint32_t* __restrict__ pos,
                                               const uint32_t* __restrict__ keys, const uint32_t* __restrict__ seg,
-                                              int64_t nseg, int64_t base_new, int64_t wm, int64_t* __restrict__ prog) {
+                                              int64_t nseg, int64_t base_new, int64_t wm, int64_t* __restrict__ prog,
+                                              bool room) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = seg[s], b = seg[s + 1];
     const uint32_t g = keys[a];
     if (!PUSH) {
       if (!(S.gfl[g] & GF_FIRE)) continue;
-      if (!emit_firing(c, S, g, pos, a, b - 1)) continue;
+      if (!emit_firing(c, S, g, pos, a, b - 1, room)) continue;
       if (c.purging) purge(S, pos, a, b - 1);
       atomicAnd(&S.gfl[g], ~GF_FIRE);
       continue;
@@ -409,7 +416,7 @@ __global__ __launch_bounds__(256) void k_walk(LCfg c, LState S, const uint32_t* 
         fire = mts <= wm;
       }
       if (fire) {
-        if (!emit_firing(c, S, g, pos, a, j)) {
+        if (!emit_firing(c, S, g, pos, a, j, room)) {
           prog[s] = j;
           stopped = true;
           break;
@@ -420,6 +427,28 @@ __global__ __launch_bounds__(256) void k_walk(LCfg c, LState S, const uint32_t* 
     }
     if (!stopped) atomicAnd(&S.gfl[g], ~GF_TOUCH);
   }
+}
+
+// an upper bound of the elements one walk can emit: per list, its length times the firings it can see (every
+// due list once at a watermark; in a push every new element of an event-time list, or every trig_n-th of a
+// CountTrigger list)
+template <bool PUSH>
+__global__ __launch_bounds__(256) void k_walk_bound(LCfg c, LState S, const uint32_t* __restrict__ pos,
+                                                    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ seg,
+                                                    int64_t nseg, int64_t base_new) {
+  unsigned long long tot = 0;
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = seg[s], b = seg[s + 1];
+    if (!PUSH) {
+      tot += (unsigned long long)(b - a);
+      continue;
+    }
+    int64_t nn = 0;
+    for (int64_t q = a; q < b; q++) nn += (int64_t)pos[q] >= base_new;
+    const int64_t f = c.trigger == FW_TRIGGER_COUNT ? (S.gcnt[keys[a]] + nn) / max<int64_t>(1, c.trig_n) : nn;
+    tot += (unsigned long long)(f * (b - a));
+  }
+  if (tot) atomicAdd(&S.ctr->count, tot);
 }
 
 // ---------------------------------------------------------------- watermark
@@ -433,7 +462,8 @@ __global__ __launch_bounds__(256) void k_lw_due(LCfg c, LState S, int64_t wm) {
       f = (f & ~GF_TIMER) | GF_FIRE;
       atomicAdd(&S.ctr->nfire, 1ull);
     }
-    if (w_cleanup(c, st) <= wm) {
+    const int64_t cl = w_cleanup(c, st);
+    if (cl != LMAX && cl <= wm) {  // no cleanup timer is registered at Long.MAX_VALUE (registerCleanupTimer)
       f |= GF_CLEAN;
       atomicAdd(&S.ctr->nclean, 1ull);
     }
@@ -758,10 +788,24 @@ int walk_lists(fw_list* op, uint32_t bit, int64_t base_new) {
   const uint32_t mm = (uint32_t)m;
   LHIP(op, hipMemcpyAsync(op->seg + nseg, &mm, 4, hipMemcpyHostToDevice, op->stream));
   LHIP(op, hipMemsetAsync(op->prog, 0xff, (size_t)nseg * 8, op->stream));
+  // with room for every possible firing the walk reserves elements with plain atomics; else (a bound beyond
+  // FW_LIST_ROOM elements) it reserves with compare-and-swap and stops where the buffer is full
+  bool room = !op->c.emit;
+  if (op->c.emit) {
+    LHIP(op, hipMemsetAsync(&op->S.ctr->count, 0, 8, op->stream));
+    hipLaunchKernelGGL(k_walk_bound<PUSH>, dim3(grid_for(nseg)), dim3(256), 0, op->stream, op->c, op->S, op->sel2,
+                       op->keys2, op->seg, nseg, base_new);
+    LRET(read_ctr(op));
+    const int64_t need = (int64_t)op->h_ctr->elems + (int64_t)op->h_ctr->count;
+    if ((int64_t)op->h_ctr->count <= FW_LIST_ROOM) {
+      LRET(ensure_elems(op, need));
+      room = true;
+    }
+  }
   for (int round = 0;; round++) {
     LHIP(op, hipMemsetAsync(&op->S.ctr->flags, 0, 4, op->stream));
     hipLaunchKernelGGL(k_walk<PUSH>, dim3(grid_for(nseg)), dim3(256), 0, op->stream, op->c, op->S, op->sel2,
-                       op->keys2, op->seg, nseg, base_new, op->wm, op->prog);
+                       op->keys2, op->seg, nseg, base_new, op->wm, op->prog, room);
     LHIP(op, hipGetLastError());
     LRET(read_ctr(op));
     if (!(op->h_ctr->flags & LF_ELEMS)) break;

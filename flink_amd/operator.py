@@ -44,6 +44,9 @@ class GpuWindowOperator:
                  key_group_range: KeyGroupRange = None, device=0, expected_entries=0, max_batch=0,
                  sub_partitions=0, async_input=True):
         trigger = trigger or EventTimeTrigger.create()
+        if not isinstance(getattr(trigger, "nested", trigger), EventTimeTrigger):
+            raise ValueError("GpuWindowOperator takes EventTimeTrigger or PurgingTrigger.of(EventTimeTrigger); "
+                             "count triggers run on GpuListWindowOperator")
         if allowed_lateness < 0:
             raise ValueError("The allowed lateness cannot be negative.")
         kgr = key_group_range or KeyGroupRange(0, max_parallelism - 1)

@@ -157,17 +157,92 @@ class EventTimeTrigger(Trigger):
 
 
 class PurgingTrigger(Trigger):
-    """PurgingTrigger.of(EventTimeTrigger.create()) (PurgingTrigger.java:45-59)."""
+    """PurgingTrigger.of(EventTimeTrigger.create()) (PurgingTrigger.java:45-59); around CountTrigger.of(n) for the
+    window-contents operator only."""
     purging = True
 
     def __init__(self, nested):
-        if not isinstance(nested, EventTimeTrigger):
-            raise ValueError("the GPU path offers PurgingTrigger only around EventTimeTrigger")
+        if not isinstance(nested, (EventTimeTrigger, CountTrigger)):
+            raise ValueError("the GPU path offers PurgingTrigger only around EventTimeTrigger or CountTrigger")
         self.nested = nested
 
     @staticmethod
     def of(nested):
         return PurgingTrigger(nested)
+
+
+class GlobalWindows(WindowAssigner):
+    """GlobalWindows.create() (GlobalWindows.java): one window per key, not event time (never late, no cleanup
+    timer); for the window-contents operator (GpuListWindowOperator)."""
+    kind = N.FW_GLOBAL
+
+    @staticmethod
+    def create():
+        return GlobalWindows()
+
+    def config(self):
+        return dict(assigner=self.kind)
+
+    def __repr__(self):
+        return "GlobalWindows()"
+
+
+class CountTrigger(Trigger):
+    """CountTrigger.of(n) (CountTrigger.java:47-70): FIRE at every n-th element of a (key, window)."""
+
+    def __init__(self, count):
+        if count <= 0:
+            raise ValueError("count must be positive")
+        self.count = count
+
+    @staticmethod
+    def of(count):
+        return CountTrigger(count)
+
+
+class Evictor:
+    kind = N.FW_EVICT_NONE
+    evict_after = False
+    arg = 0
+    threshold = 0.0
+
+
+@dataclass(frozen=True)
+class CountEvictor(Evictor):
+    """CountEvictor.of(maxCount[, doEvictAfter]) (CountEvictor.java:55-78): keeps the last maxCount elements."""
+    arg: int = 0
+    evict_after: bool = False
+    kind = N.FW_EVICT_COUNT
+
+    @staticmethod
+    def of(max_count, evict_after=False):
+        return CountEvictor(max_count, evict_after)
+
+
+@dataclass(frozen=True)
+class TimeEvictor(Evictor):
+    """TimeEvictor.of(windowSize[, doEvictAfter]) (TimeEvictor.java:58-103): drops the elements with a timestamp
+    <= max timestamp - windowSize (none when the first element has no timestamp)."""
+    arg: int = 0
+    evict_after: bool = False
+    kind = N.FW_EVICT_TIME
+
+    @staticmethod
+    def of(window_size, evict_after=False):
+        return TimeEvictor(int(window_size), evict_after)
+
+
+@dataclass(frozen=True)
+class DeltaEvictor(Evictor):
+    """DeltaEvictor.of(threshold, f[, doEvictAfter]) (DeltaEvictor.java:56-80) with the built-in DeltaFunction
+    f(e, last) = last.field - e.field (the field's Java arithmetic): drops the elements with f >= threshold."""
+    threshold: float = 0.0
+    evict_after: bool = False
+    kind = N.FW_EVICT_DELTA
+
+    @staticmethod
+    def of(threshold, evict_after=False):
+        return DeltaEvictor(float(threshold), evict_after)
 
 
 # the field types of the built-in aggregations (SumFunction.java:34-107): Short / Byte sums wrap to their width,

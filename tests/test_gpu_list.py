@@ -1,0 +1,280 @@
+"""f4 GPU parity: GpuListWindowOperator (fw_list_*, libflinkwin.so) — WindowedStream.apply / process over
+ListState and the EvictingWindowOperator — against the reference KATs (EvictingWindowOperatorTest,
+WindowOperatorTest apply sequences) and against the ListState oracle (oracle/list_oracle.cpp) on seeded streams.
+Bar: rows (key, window, count, integer sum / min / max, first ordinal) and the contents of every firing
+bit-exact; f64 sums are summed in list order on both sides, so they are bit-exact too."""
+from collections import Counter
+
+import numpy as np
+import pytest
+
+from flink_amd import (CountEvictor, CountTrigger, DeltaEvictor, EventTimeTrigger, GlobalWindows, PurgingTrigger,
+                       SlidingEventTimeWindows, TimeEvictor, TumblingEventTimeWindows)
+from oracle import oracle as orc
+from tests.kat_util import expected_counters, load_kats, replay, replay_list_phases, row_counters
+
+pytestmark = pytest.mark.gpu
+
+KATS = load_kats()
+KEYMAP = KATS["keys"]
+_VT = {"i64": "long", "i32": "int", "f64": "double", "i16": "short", "i8": "byte", "f32": "float"}
+
+
+def _assigner(kind, size=0, slide=0, offset=0):
+    if kind == "global":
+        return GlobalWindows.create()
+    if kind == "tumbling":
+        return TumblingEventTimeWindows.of(size, offset)
+    return SlidingEventTimeWindows.of(size, slide, offset)
+
+
+def _evictor(kind, after, arg, threshold):
+    return {"none": None, "count": lambda: CountEvictor.of(arg, after), "time": lambda: TimeEvictor.of(arg, after),
+            "delta": lambda: DeltaEvictor.of(threshold, after)}[kind]() if kind != "none" else None
+
+
+def _pair(assigner="tumbling", size=0, slide=0, offset=0, lateness=0, trigger="event_time", trigger_count=0,
+          purging=False, evictor="none", evict_after=False, evict_arg=0, threshold=0.0, side_output=False,
+          value_type="i64", **gpu_kw):
+    """(GPU operator, oracle) of one configuration"""
+    from flink_amd.listwindow import GpuListWindowOperator
+    trig = CountTrigger.of(trigger_count) if trigger == "count" else EventTimeTrigger.create()
+    if purging:
+        trig = PurgingTrigger.of(trig)
+    gpu = GpuListWindowOperator(_assigner(assigner, size, slide, offset), trig,
+                                _evictor(evictor, evict_after, evict_arg, threshold), allowed_lateness=lateness,
+                                side_output=side_output, value_type=_VT[value_type], **gpu_kw)
+    ref = orc.ListWindowOracle(assigner=assigner, size=size, slide=slide, offset=offset, lateness=lateness,
+                               trigger=trigger, trigger_count=trigger_count, purging=purging, evictor=evictor,
+                               evict_after=evict_after, evict_arg=evict_arg, threshold=threshold,
+                               side_output=side_output, value_type=value_type)
+    return gpu, ref
+
+
+def _firings(op, ordinals=True):
+    """Counter of every firing: (epoch, key, start, end, count, sum, min, max[, first], contents)"""
+    out = Counter()
+    for r, el in op.contents():
+        ords = "ordinal" if "ordinal" in el.dtype.names else "ord"
+        cont = (tuple(zip(el["ts"].tolist(), el["val"].tolist(), el[ords].tolist())) if ordinals
+                else tuple(zip(el["ts"].tolist(), el["val"].tolist())))
+        out[(int(r["epoch"]), int(r["key"]), int(r["start"]), int(r["end"]), int(r["count"]), int(r["sum"]),
+             int(r["min"]), int(r["max"])) + ((int(r["first"]),) if ordinals else ()) + (cont,)] += 1
+    return out
+
+
+def _assert_same(gpu, ref):
+    g, r = _firings(gpu), _firings(ref)
+    assert sum(g.values()) == sum(r.values()), (sum(g.values()), sum(r.values()))
+    assert g == r, (list((g - r).items())[:3], list((r - g).items())[:3])
+
+
+# ---------------------------------------------------------------- reference KATs
+@pytest.mark.parametrize("case", KATS["list_windows"], ids=[c["name"] for c in KATS["list_windows"]])
+def test_gpu_list_window_kats(case):
+    c = case["cfg"]
+    gpu, ref = _pair(c["assigner"], c["size"], trigger=c["trigger"], trigger_count=c["trigger_count"],
+                     evictor=c["evictor"], evict_after=c["evict_after"], evict_arg=c["evict_arg"],
+                     threshold=c["threshold"], value_type="i32")
+    for (got, exp), (rgot, _) in zip(replay_list_phases(case, KEYMAP, gpu), replay_list_phases(case, KEYMAP, ref)):
+        assert got == exp
+        assert rgot == exp
+    _assert_same(gpu, ref)  # and the contents of every firing
+    gpu.close()
+
+
+@pytest.mark.parametrize("name", sorted(KATS["list_apply_cases"]))
+def test_gpu_list_apply_kats(name):
+    # WindowedStream.apply over ListState (WOT:213-238, :339-364): RichSumReducer's sums = the rows' sums
+    case = next(c for c in KATS["operator_cases"] if c["name"] == name)
+    c = case["cfg"]
+    sums = []
+    gpu, ref = _pair(c["assigner"], c["size"], c["slide"], value_type="i32",
+                     window_function=lambda k, w, el: sums.append((k, w, int(el["val"].sum()))))
+    gpu = replay(case, KEYMAP, lambda _: gpu, flush_elements=True)
+    ref = replay(case, KEYMAP, lambda _: ref, flush_elements=False)
+    got, _ = row_counters(gpu.rows(), [], case, with_window=True)
+    exp, _ = expected_counters(case, KEYMAP, with_window=True)
+    assert got == exp
+    assert sorted(s for _, _, s in sums) == sorted(int(r["sum"]) for r in gpu.rows())
+    _assert_same(gpu, ref)
+    gpu.close()
+
+
+# ---------------------------------------------------------------- seeded streams vs the oracle
+def _stream(seed, n, keys, span, jitter):
+    rng = np.random.default_rng(seed)
+    k = rng.integers(0, keys, n, dtype=np.int64)
+    t = np.arange(n, dtype=np.int64) * span // n - rng.integers(0, jitter, n, dtype=np.int64)
+    v = rng.integers(-1000, 1000, n, dtype=np.int64)
+    return k, t, v
+
+
+CONFIGS = [
+    dict(assigner="tumbling", size=100),
+    dict(assigner="tumbling", size=100, purging=True, lateness=50, side_output=True),
+    dict(assigner="tumbling", size=100, lateness=60),
+    dict(assigner="sliding", size=100, slide=25),
+    dict(assigner="sliding", size=90, slide=30, lateness=40),
+    dict(assigner="tumbling", size=100, evictor="count", evict_arg=3),
+    dict(assigner="tumbling", size=100, evictor="count", evict_arg=2, evict_after=True, lateness=30),
+    dict(assigner="tumbling", size=200, evictor="time", evict_arg=50),
+    dict(assigner="sliding", size=100, slide=50, evictor="time", evict_arg=20, evict_after=True),
+    dict(assigner="tumbling", size=100, evictor="delta", threshold=300.0),
+    dict(assigner="tumbling", size=100, trigger="count", trigger_count=3),
+    dict(assigner="tumbling", size=100, trigger="count", trigger_count=2, purging=True, evictor="count", evict_arg=5),
+    dict(assigner="global", trigger="count", trigger_count=4, evictor="count", evict_arg=6),
+    dict(assigner="global", trigger="count", trigger_count=3, evictor="delta", threshold=500.0, evict_after=True),
+    dict(assigner="global", trigger="count", trigger_count=5, purging=True),
+]
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=[str(i) for i in range(len(CONFIGS))])
+@pytest.mark.parametrize("value_type", ["i64", "f64"])
+def test_gpu_list_vs_oracle(cfg, value_type):
+    gpu, ref = _pair(value_type=value_type, **cfg)
+    k, t, v = _stream(7 + len(str(cfg)), 20000, 37, 2000, 150)
+    if value_type == "f64":
+        v = (v.astype(np.float64) * 0.37).view(np.int64)
+    wm = -10**9
+    for b in range(10):
+        sl = slice(b * 2000, (b + 1) * 2000)
+        vals = v[sl].view(np.float64) if value_type == "f64" else v[sl]
+        gpu.process(k[sl], t[sl], vals)
+        ref.process(k[sl], t[sl], v[sl])
+        wm = max(wm, int(t[sl].max()) - 100)
+        if b % 3 != 1:
+            gpu.watermark(wm)
+            ref.watermark(wm)
+    for w in (wm + 500, (1 << 63) - 1):
+        gpu.watermark(w)
+        ref.watermark(w)
+    _assert_same(gpu, ref)
+    assert gpu.late_dropped == ref.late_dropped
+    if cfg.get("side_output"):
+        gs = sorted(map(tuple, np.stack([gpu.side_rows()[f] for f in ("epoch", "key", "ts", "val")], 1).tolist()))
+        e, kk, ts, vv = ref.side_rows()
+        assert gs == sorted(zip(e.tolist(), kk.tolist(), ts.tolist(), vv.tolist()))
+    st = gpu.stats()
+    assert st["keyed_state_entries"] == ref.num_state_entries
+    assert st["event_time_timers"] == ref.num_timers
+    gpu.close()
+
+
+def test_gpu_list_state_counters_mid_stream():
+    # numKeyedStateEntries / numEventTimeTimers while windows are open (lateness keeps fired lists alive)
+    gpu, ref = _pair(assigner="sliding", size=100, slide=50, lateness=30)
+    k, t, v = _stream(3, 5000, 11, 1000, 80)
+    for h in (gpu, ref):
+        h.process(k, t, v)
+        h.watermark(600)
+    st = gpu.stats()
+    assert st["keyed_state_entries"] == ref.num_state_entries > 0
+    assert st["event_time_timers"] == ref.num_timers > 0
+    _assert_same(gpu, ref)
+    gpu.close()
+
+
+def test_gpu_list_growth_and_compaction():
+    # a log and a group map far smaller than the stream: grows, cleanups and compactions along the way
+    gpu, ref = _pair(assigner="tumbling", size=50, evictor="count", evict_arg=4, trigger="count", trigger_count=3,
+                     expected_elements=1024)
+    k, t, v = _stream(11, 200000, 5000, 40000, 30)
+    for b in range(20):
+        sl = slice(b * 10000, (b + 1) * 10000)
+        gpu.process(k[sl], t[sl], v[sl])
+        ref.process(k[sl], t[sl], v[sl])
+        gpu.watermark(int(t[sl].max()) - 40)
+        ref.watermark(int(t[sl].max()) - 40)
+    gpu.watermark((1 << 63) - 1)
+    ref.watermark((1 << 63) - 1)
+    _assert_same(gpu, ref)
+    assert gpu.stats()["table_grows"] > 0
+    gpu.close()
+
+
+def test_gpu_list_device_columns_and_hashed_keys():
+    import torch
+    from flink_amd.keygroups import string_hash_code
+    words = ["to", "be", "or", "not", "that", "is", "the", "question"]
+    rng = np.random.default_rng(5)
+    ids = rng.integers(0, len(words), 30000)
+    kh = np.array([string_hash_code(words[i]) for i in ids], dtype=np.int32)
+    t = np.arange(30000, dtype=np.int64) // 3
+    v = np.ones(30000, dtype=np.int64)
+    gpu, ref = _pair(assigner="tumbling", size=1000, evictor="count", evict_arg=100, value_type="i32",
+                     key_type="hashed")
+    d = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    gpu.process(d(ids.astype(np.int64)), d(t), d(v), d(kh))
+    ref.process(ids, t, v)
+    for h in (gpu, ref):
+        h.watermark((1 << 63) - 1)
+    _assert_same(gpu, ref)
+    gpu.close()
+
+
+def test_gpu_list_snapshot_restore_rescale():
+    # snapshot every key group mid-stream, restore into two subtasks over halves of the key groups, continue;
+    # the union of their firings equals one uninterrupted oracle
+    from flink_amd import KeyGroupRange
+    from flink_amd.listwindow import GpuListWindowOperator
+    cfg = dict(assigner="tumbling", size=100, lateness=50, evictor="count", evict_arg=5, trigger="count",
+               trigger_count=4)
+    gpu, ref = _pair(**cfg)
+    k, t, v = _stream(21, 40000, 200, 4000, 60)
+    h = 20000
+    gpu.process(k[:h], t[:h], v[:h])
+    ref.process(k[:h], t[:h], v[:h])
+    gpu.watermark(int(t[:h].max()) - 70)
+    ref.watermark(int(t[:h].max()) - 70)
+    snap = gpu.snapshot_state()
+    assert sum(int((s[0]["n_elems"] > 0).sum()) for s in snap.values()) == ref.num_state_entries
+    assert sum(len(s[1]) for s in snap.values()) == sum(int(s[0]["n_elems"].sum()) for s in snap.values())
+    parts = []
+    for r in (KeyGroupRange(0, 63), KeyGroupRange(64, 127)):
+        op = GpuListWindowOperator(TumblingEventTimeWindows.of(100), CountTrigger.of(4), CountEvictor.of(5),
+                                   allowed_lateness=50, key_group_range=r)
+        op.initialize_state(snap)
+        op.epoch = gpu.epoch
+        op.advance_watermark(int(t[:h].max()) - 70)
+        op.epoch -= 1
+        kg = np.array([orc.lib().oracle_key_group(orc.lib().oracle_long_hash(int(x)), 128) for x in k[h:]])
+        mine = (kg >= r.start_key_group) & (kg <= r.end_key_group)
+        op.process(k[h:][mine], t[h:][mine], v[h:][mine])
+        op.watermark((1 << 63) - 1)
+        parts.append(op)
+    ref.process(k[h:], t[h:], v[h:])
+    ref.watermark((1 << 63) - 1)
+    # ordinals number each handle's own records, so the restored subtasks' differ from one operator's
+    got = _firings(gpu, ordinals=False)
+    for op in parts:
+        got += _firings(op, ordinals=False)
+    exp = _firings(ref, ordinals=False)
+    assert got == exp
+    for op in parts:
+        op.close()
+    gpu.close()
+
+
+def test_gpu_list_full_size_every_record_once():
+    # 2^22 records, 1M keys, tumbling 1 s apply: after the final watermark every record is in exactly one
+    # fired list, in arrival order (size-independent properties at a BASELINE-like scale)
+    import torch
+    from flink_amd.datagen import generate_device
+    from flink_amd.listwindow import GpuListWindowOperator
+    n = 1 << 22
+    k, t, v, _ = generate_device(0x5EED, 0, n, 1_000_000, ts_base=0, rate=100_000_000, jitter=200)
+    op = GpuListWindowOperator(TumblingEventTimeWindows.of(1000), max_batch=n, expected_elements=n)
+    op.process(k, t, v)
+    op.watermark((1 << 63) - 1)
+    rows, el = op.rows(), op.elems()
+    assert int(rows["count"].sum()) == n == len(el)
+    assert np.array_equal(np.sort(el["ordinal"]), np.arange(n))
+    vh = v.cpu().numpy()
+    assert int(rows["sum"].sum()) == int(vh.sum())
+    for r in rows[:: max(1, len(rows) // 1000)]:
+        seg = el["ordinal"][r["elem_off"]:r["elem_off"] + r["count"]]
+        assert np.all(np.diff(seg) > 0)
+    assert op.stats()["keyed_state_entries"] == 0
+    op.close()
+    del torch

@@ -1,0 +1,88 @@
+"""f1: the heap backend's snapshot format (flink_amd/heapstate.py), pinned by the reference's own migration
+fixtures (flink-streaming-java/src/test/resources/win-op-migration-test-*-flink1.{3,4}-snapshot, written by
+WindowOperatorMigrationTest.java's writeReducingEventTimeWindowsSnapshot / writeApplyEventTimeWindowsSnapshot and
+restored by testRestoreReducingEventTimeWindows :381-433 / testRestoreApplyEventTimeWindows :497-548).  The files
+are kept as data under tests/golden/heap/; the reader walks them without deserializing any Java object."""
+import os
+
+import pytest
+
+from flink_amd import heapstate as H
+
+HEAP = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "heap")
+TUP = H.TupleSer(H.StringSer(), H.IntSer())
+EXPECTED_TIMERS = {("key1", (0, 3000), 2999), ("key2", (0, 3000), 2999), ("key2", (3000, 6000), 5999)}
+
+
+def load(name, version):
+    with open(os.path.join(HEAP, f"win-op-migration-test-{name}-flink{version}-snapshot"), "rb") as f:
+        return f.read()
+
+
+def serializers(name):
+    return {"window-contents": (H.TimeWindowSer(), H.StringSer(), TUP if name == "reduce-event-time" else H.ListSer(TUP))}
+
+
+@pytest.mark.parametrize("version", ["1.3", "1.4"])
+@pytest.mark.parametrize("name", ["reduce-event-time", "apply-event-time"])
+def test_reads_migration_fixture(name, version):
+    snap = H.read_operator_snapshot(load(name, version))
+    assert snap["raw_operator"] is None and snap["managed_operator"] is None
+    (mk,), (rk,) = snap["managed_keyed"], snap["raw_keyed"]
+    assert list(mk.key_groups()) == [0] and list(rk.key_groups()) == [0]  # the harness' one key group
+    meta, groups = H.read_heap_keyed_state(mk, serializers(name))
+    assert meta["version"] == (3 if version == "1.3" else 4)
+    assert meta["states"] == [("REDUCING" if name == "reduce-event-time" else "LIST", "window-contents")]
+    got = sorted(groups[0]["window-contents"], key=lambda m: (m[0], m[1]))
+    if name == "reduce-event-time":  # the reduced tuples: testRestoreReducingEventTimeWindows' expected sums
+        assert got == [((0, 3000), "key1", ("key1", 3)), ((0, 3000), "key2", ("key2", 3)),
+                       ((3000, 6000), "key2", ("key2", 2))]
+    else:  # the window contents: (key, 1) elements
+        assert got == [((0, 3000), "key1", [("key1", 1)] * 3), ((0, 3000), "key2", [("key2", 1)] * 3),
+                       ((3000, 6000), "key2", [("key2", 1)] * 2)]
+    timers = H.read_timers(rk, H.StringSer(), H.TimeWindowSer())
+    assert H.event_timers(timers) == EXPECTED_TIMERS
+    assert timers[0]["window-timers"][1] == []  # no processing-time timers
+
+
+@pytest.mark.parametrize("version", ["1.3", "1.4"])
+@pytest.mark.parametrize("name", ["reduce-event-time", "apply-event-time"])
+def test_writes_key_group_sections_byte_exact(name, version):
+    # the writer reproduces the heap backend's key-group section (HeapKeyedStateBackend.java:375-381) byte for byte
+    data = load(name, version)
+    mk = H.read_operator_snapshot(data)["managed_keyed"][0]
+    meta, groups = H.read_heap_keyed_state(mk, serializers(name))
+    sec = H.write_key_group_section(0, [(0, "window-contents", groups[0]["window-contents"])], serializers(name))
+    assert sec == mk.data[mk.offsets[0]:]
+    stream, offsets = H.write_keyed_state_stream(mk.data[:meta["header_end"]], [sec])
+    assert stream == mk.data and offsets == mk.offsets
+
+
+def test_string_value_codec():
+    # StringValue.writeString: length + 1 as a varint, chars as varints (StringValue.java:789-817)
+    w = H.DataOutput()
+    for s in ("key1", "", None, "é中" * 50):
+        H.StringSer().write(w, s)
+    r = H.DataInput(w.getvalue())
+    assert [H.StringSer().read(r) for _ in range(4)] == ["key1", "", None, "é中" * 50]
+    w = H.DataOutput()
+    H.StringSer().write(w, "key1")
+    assert w.getvalue() == b"\x05key1"
+
+
+def test_bridges_round_trip():
+    mk = H.read_operator_snapshot(load("reduce-event-time", "1.4"))["managed_keyed"][0]
+    _, groups = H.read_heap_keyed_state(mk, serializers("reduce-event-time"))
+    ids = {"key1": 1, "key2": 2}
+    names = {v: k for k, v in ids.items()}
+    rows, pt = H.reduce_rows_from_heap(groups[0]["window-contents"], EXPECTED_TIMERS, ids.__getitem__, 1)
+    assert all(r["timer"] == 1 for r in rows)
+    back = H.heap_from_reduce_rows(rows, names.__getitem__, pt, 1)
+    assert sorted(back) == sorted(groups[0]["window-contents"])
+    mk = H.read_operator_snapshot(load("apply-event-time", "1.4"))["managed_keyed"][0]
+    _, groups = H.read_heap_keyed_state(mk, serializers("apply-event-time"))
+    lists, elems = H.list_state_from_heap(groups[0]["window-contents"], EXPECTED_TIMERS, ids.__getitem__,
+                                          lambda v: v[1])
+    assert [r["n_elems"] for r in lists] == [2, 3, 3] and len(elems) == 8
+    back = H.heap_from_list_state(lists, elems, names.__getitem__, lambda e: None)
+    assert [len(m[2]) for m in back] == [2, 3, 3]
