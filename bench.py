@@ -139,7 +139,7 @@ def wordcount_stream(first, n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=64)  # 64 x 2^24 = 2^30 records
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--workload", choices=sorted(PRESETS), default="c2")
     ap.add_argument("--batch", type=int, default=None, help="records per step per GPU (default 2^24; C1 10M)")

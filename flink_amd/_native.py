@@ -162,6 +162,7 @@ SIGNATURES = {
     "fw_list_pending": (ctypes.c_int, [VP, I64P, I64P, I64P]),
     "fw_list_drain": (ctypes.c_int, [VP, ctypes.POINTER(FwListRows), ctypes.c_int64, ctypes.POINTER(FwListElems),
                                      ctypes.c_int64, I64P, I64P]),
+    "fw_list_clear_pending": (ctypes.c_int, [VP]),
     "fw_list_drain_side": (ctypes.c_int, [VP, ctypes.POINTER(FwSideRows), ctypes.c_int64, I64P]),
     "fw_list_get_stats": (ctypes.c_int, [VP, ctypes.POINTER(FwStats)]),
     "fw_list_snapshot_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwListState), ctypes.c_int64,

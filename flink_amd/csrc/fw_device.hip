@@ -3368,6 +3368,8 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
   __shared__ int64_t s_cum[TD_WAVES][TD_NB_MAX];
   __shared__ int64_t s_ns[TD_WAVES][TD_NB_MAX + 1];  // first value of each bucket (-1: none), then its end
   __shared__ int32_t s_os[TD_WAVES][TD_NB_MAX + 1];
+  __shared__ int64_t s_en[TD_WAVES][TD_NB_MAX];  // where each bucket's runs end: the next bucket's starts
+  __shared__ int32_t s_eo[TD_WAVES][TD_NB_MAX];
   const int wv = threadIdx.x >> 6, lane = __lane_id();
   const int nb = c.td_nb;
   uint64_t* keys = s_key[wv];
@@ -3424,6 +3426,39 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // the end of every bucket's runs = the start of the next bucket that has one (the starts grow with the
+    // bucket): an exclusive suffix minimum over the buckets, 64 at a time from the last chunk down
+    {
+      int64_t carry_n = d.beg + d.nn;
+      int32_t carry_o = d.no;
+      for (int b0 = ((nb - 1) >> 6) << 6; b0 >= 0; b0 -= 64) {
+        const int b = b0 + lane;
+        int64_t xn = b < nb && ns[b] >= 0 ? ns[b] : INT64_MAX;
+        int32_t xo = b < nb && os[b] >= 0 ? os[b] : INT32_MAX;
+        for (int o = 1; o < 64; o <<= 1) {  // inclusive suffix minimum over lanes >= lane
+          const int64_t yn = __shfl_down(xn, o, 64);
+          const int32_t yo = __shfl_down(xo, o, 64);
+          if (lane + o < 64) {
+            xn = min(xn, yn);
+            xo = min(xo, yo);
+          }
+        }
+        int64_t en = __shfl_down(xn, 1, 64);
+        int32_t eo = __shfl_down(xo, 1, 64);
+        if (lane == 63) {
+          en = INT64_MAX;
+          eo = INT32_MAX;
+        }
+        if (b < nb) {
+          s_en[wv][b] = min(en, carry_n);
+          s_eo[wv][b] = min(eo, carry_o);
+        }
+        carry_n = min(carry_n, __shfl(xn, 0, 64));
+        carry_o = min(carry_o, __shfl(xo, 0, 64));
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     // buckets in order: each non-empty one is a centroid
     int64_t cum_out = 0, end_n;
     int32_t k = 0, end_o;
@@ -3431,20 +3466,8 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
       const int64_t sn = ns[b];
       const int32_t so = os[b];
       if (sn < 0 && so < 0) continue;
-      // the end of this bucket's runs: the next bucket that starts one
-      end_n = d.beg + d.nn;
-      end_o = d.no;
-      bool fn = false, fo = false;
-      for (int b2 = b + 1; b2 < nb && !(fn && fo); b2++) {
-        if (!fn && ns[b2] >= 0) {
-          end_n = ns[b2];
-          fn = true;
-        }
-        if (!fo && os[b2] >= 0) {
-          end_o = os[b2];
-          fo = true;
-        }
-      }
+      end_n = s_en[wv][b];
+      end_o = s_eo[wv][b];
       const int64_t a_n = sn >= 0 ? sn : end_n;
       const int32_t a_o = so >= 0 ? so : end_o;
       double s_new = 0.0, s_old = 0.0;

@@ -4,7 +4,7 @@
 //   runtime/operators/windowing/EvictingWindowOperator.java:102-239 processElement, :241-286 onEventTime,
 //   :334-366 emitWindowContents; WindowOperator.java:291-469 (no evictor), :576-651 lateness and cleanup;
 //   api/windowing/triggers/{EventTimeTrigger.java:37-73, CountTrigger.java:47-70, PurgingTrigger.java:45-59};
-//   api/windowing/evictors/{CountEvictor.java:55-78, TimeEvictor.java:58-103, DeltaEvictor.java:56-80}.
+//   api/windowing/evictors/{CountEvictor.java:50-78, TimeEvictor.java:54-104, DeltaEvictor.java:59-80}.
 //
 // HBM layout (one handle = one subtask on one GPU):
 //   groups   an open-addressing map (key, window start) -> group id (the slot), per group its key group, the
@@ -116,7 +116,9 @@ __device__ __forceinline__ void for_windows(const LCfg& c, int64_t ts, int64_t w
 __device__ __forceinline__ uint32_t g_hash(int64_t key, int64_t start) {
   return (uint32_t)fmix64((uint64_t)key ^ fmix64((uint64_t)start ^ 0x9E3779B97F4A7C15ull));
 }
-__device__ int32_t g_find_insert(const LState& S, int64_t key, int64_t start, int32_t kg) {
+// limit > 0: no new group beyond `limit` live ones (LF_MAP_FULL is raised instead, nothing inserted)
+__device__ int32_t g_find_insert(const LState& S, int64_t key, int64_t start, int32_t kg,
+                                 unsigned long long limit = 0) {
   uint32_t s = g_hash(key, start) & S.gmask;
   for (uint32_t probes = 0; probes <= S.gmask;) {
     const uint32_t cur = __hip_atomic_load(&S.gst[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
@@ -125,6 +127,10 @@ __device__ int32_t g_find_insert(const LState& S, int64_t key, int64_t start, in
     } else if (cur == G_BUSY) {
       continue;  // being published by another lane: read it again
     } else if (cur == G_EMPTY) {
+      if (limit && __hip_atomic_load(&S.ctr->live_groups, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= limit) {
+        atomicOr(&S.ctr->flags, LF_MAP_FULL);
+        return -1;
+      }
       if (atomicCAS(&S.gst[s], G_EMPTY, G_BUSY) == G_EMPTY) {
         S.gkey[s] = key;
         S.gstart[s] = start;
@@ -176,6 +182,20 @@ __global__ __launch_bounds__(256) void k_lp_count(LCfg c, LState S, const int64_
         atomicAdd(&S.ctr->late, 1ull);
       }
     }
+  }
+}
+
+// the (key, window) groups of the batch's entries, inserted up to `limit` live groups (idempotent: a batch that
+// stops at the limit is inserted again once the map has grown)
+__global__ __launch_bounds__(256) void k_lp_groups(LCfg c, LState S, const int64_t* __restrict__ key,
+                                                   const int64_t* __restrict__ ts, const int32_t* __restrict__ kh,
+                                                   int64_t n, int64_t wm, const uint32_t* __restrict__ wcnt,
+                                                   unsigned long long limit) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!wcnt[i]) continue;
+    const int64_t k = key[i];
+    const int32_t kg = key_group(key_hash_of(c.key_kind, k, kh, i), c.max_par);
+    for_windows(c, ts[i], wm, [&](int64_t s) { g_find_insert(S, k, s, kg, limit); });
   }
 }
 
@@ -825,6 +845,7 @@ int compact(fw_list* op, int64_t groups_needed) {
   LHIP(op, dmalloc(&remap, (size_t)op->gcap));
   LHIP(op, hipMemsetAsync(&op->S.ctr->live_groups, 0, 8, op->stream));
   LHIP(op, hipMemsetAsync(&op->S.ctr->tombs, 0, 8, op->stream));
+  LHIP(op, hipMemsetAsync(&op->S.ctr->flags, 0, 4, op->stream));  // (a full map's flag is what called us)
   hipLaunchKernelGGL(k_rebuild_map, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, op->c, o, S, remap);
   // the live elements, in order, remapped
   LRET(ensure_sel(op, op->n_log));
@@ -910,8 +931,17 @@ int push_device(fw_list* op, const int64_t* key, const int64_t* ts, const int64_
   if (op->h_ctr->flags & LF_KEY_GROUP)
     return set_err(op, FW_ERR_KEY_GROUP, "a key of the batch is outside the handle's KeyGroupRange");
   const int64_t E = total;
-  // room: the log, the map (<= 1/2 load), a row per possibly firing entry
-  if ((int64_t)op->h_ctr->live_groups + E > op->gcap / 2) LRET(compact(op, (int64_t)op->h_ctr->live_groups + E));
+  // the batch's groups first, at <= 3/4 load (the map doubles and the insert runs again when it would not fit)
+  for (int round = 0;; round++) {
+    LHIP(op, hipMemsetAsync(&op->S.ctr->flags, 0, 4, op->stream));
+    hipLaunchKernelGGL(k_lp_groups, dim3(grid_for(n)), dim3(256), 0, op->stream, op->c, op->S, key, ts, kh, n, op->wm,
+                       op->wcnt, (unsigned long long)(op->gcap / 4 * 3));
+    LRET(read_ctr(op));
+    if (!(op->h_ctr->flags & LF_MAP_FULL)) break;
+    if (round > 40) return set_err(op, FW_ERR_CAPACITY, "list state map full");
+    LRET(compact(op, op->gcap));  // twice the capacity
+  }
+  // room: the log, a row per possibly firing entry
   LRET(grow_log(op, E));
   LRET(ensure_rows(op, (int64_t)op->h_ctr->rows + E));
   const int64_t base = op->n_log;
@@ -971,8 +1001,8 @@ int fw_list_create(const fw_list_config* cfg, fw_list** out) {
   const int64_t fan = c.assigner == FW_SLIDING ? (c.size + c.slide - 1) / c.slide : 1;
   const int64_t exp = c.expected_elements > 0 ? c.expected_elements : std::min<int64_t>(op->max_batch * fan, 1 << 22);
   op->lcap = std::max<int64_t>(exp, 1024);
-  int64_t g = 1024;
-  while (g < 2 * std::min<int64_t>(op->lcap, 1 << 26)) g <<= 1;
+  int64_t g = 1024;  // groups: the map grows with them (k_lp_groups)
+  while (g < 2 * std::min<int64_t>(op->lcap, 1 << 22)) g <<= 1;
   op->gcap = g;
   op->rcap = 1024;
   op->scap = 1024;
@@ -1117,6 +1147,17 @@ int fw_list_drain(fw_list* op, const fw_list_rows* rows, int64_t cap_rows, const
   LHIP(op, hipMemsetAsync(&op->S.ctr->rows, 0, 16, op->stream));  // rows, elems
   LHIP(op, hipStreamSynchronize(op->stream));
   op->fired_total += nr;
+  op->h_ctr->rows = op->h_ctr->elems = 0;
+  return FW_OK;
+}
+
+int fw_list_clear_pending(fw_list* op) {
+  if (!op) return FW_ERR_ARG;
+  (void)hipSetDevice(op->device);
+  LRET(read_ctr(op));
+  op->fired_total += (int64_t)op->h_ctr->rows;
+  LHIP(op, hipMemsetAsync(&op->S.ctr->rows, 0, 16, op->stream));  // rows, elems
+  LHIP(op, hipStreamSynchronize(op->stream));
   op->h_ctr->rows = op->h_ctr->elems = 0;
   return FW_OK;
 }

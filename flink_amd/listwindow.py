@@ -148,6 +148,16 @@ class GpuListWindowOperator:
             el[f] = ecols[f][:ge.value]
         return out, el
 
+    def pending(self):
+        """(rows, elements, side rows) pending in HBM"""
+        nr, ne, ns = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        self._check(N.lib().fw_list_pending(self._h, ctypes.byref(nr), ctypes.byref(ne), ctypes.byref(ns)))
+        return nr.value, ne.value, ns.value
+
+    def clear_pending(self):
+        """a discarding sink: the pending rows and elements are dropped in HBM"""
+        self._check(N.lib().fw_list_clear_pending(self._h))
+
     def drain_side(self, epoch=-1):
         L = N.lib()
         ns = ctypes.c_int64()

@@ -209,7 +209,7 @@ class Evictor:
 
 @dataclass(frozen=True)
 class CountEvictor(Evictor):
-    """CountEvictor.of(maxCount[, doEvictAfter]) (CountEvictor.java:55-78): keeps the last maxCount elements."""
+    """CountEvictor.of(maxCount[, doEvictAfter]) (CountEvictor.java:50-78): keeps the last maxCount elements."""
     arg: int = 0
     evict_after: bool = False
     kind = N.FW_EVICT_COUNT
@@ -221,7 +221,7 @@ class CountEvictor(Evictor):
 
 @dataclass(frozen=True)
 class TimeEvictor(Evictor):
-    """TimeEvictor.of(windowSize[, doEvictAfter]) (TimeEvictor.java:58-103): drops the elements with a timestamp
+    """TimeEvictor.of(windowSize[, doEvictAfter]) (TimeEvictor.java:54-104): drops the elements with a timestamp
     <= max timestamp - windowSize (none when the first element has no timestamp)."""
     arg: int = 0
     evict_after: bool = False
@@ -234,7 +234,7 @@ class TimeEvictor(Evictor):
 
 @dataclass(frozen=True)
 class DeltaEvictor(Evictor):
-    """DeltaEvictor.of(threshold, f[, doEvictAfter]) (DeltaEvictor.java:56-80) with the built-in DeltaFunction
+    """DeltaEvictor.of(threshold, f[, doEvictAfter]) (DeltaEvictor.java:59-80) with the built-in DeltaFunction
     f(e, last) = last.field - e.field (the field's Java arithmetic): drops the elements with f >= threshold."""
     threshold: float = 0.0
     evict_after: bool = False

@@ -431,10 +431,10 @@ int fw_wire_encode_device(fw_wire* w, const fw_rows* rows, int64_t n, int32_t f6
  *              late, never cleaned up; rows have start = Long.MIN_VALUE, end = Long.MAX_VALUE = their timestamp);
  *   triggers   FW_TRIGGER_EVENT_TIME (EventTimeTrigger.java:37-73) or FW_TRIGGER_COUNT (CountTrigger.of(n),
  *              CountTrigger.java:47-70), either wrapped in PurgingTrigger (purging = 1);
- *   evictors   CountEvictor.of(n[, after]) (CountEvictor.java:55-78), TimeEvictor.of(ms[, after]) (TimeEvictor.java
- *              :58-103; a timestamp of Long.MIN_VALUE is "no timestamp": nothing is evicted when the first element
+ *   evictors   CountEvictor.of(n[, after]) (CountEvictor.java:50-78), TimeEvictor.of(ms[, after]) (TimeEvictor.java
+ *              :54-104; a timestamp of Long.MIN_VALUE is "no timestamp": nothing is evicted when the first element
  *              has none), DeltaEvictor.of(threshold, f[, after]) with the built-in f(e, last) = last.field - e.field
- *              in the field's Java arithmetic (DeltaEvictor.java:56-80).
+ *              in the field's Java arithmetic (DeltaEvictor.java:59-80).
  * Every firing emits one row: the window, count = elements the function sees (after evictBefore), the built-in
  * reduce over them in list order (sum wrapped to the field width, min, max; Double / Float fields by compare
  * order, sums in list order, so f64 sums are exact), first = the arrival ordinal of the first element (-1 if none;
@@ -502,6 +502,8 @@ int fw_list_pending(fw_list* op, int64_t* n_rows, int64_t* n_elems, int64_t* n_s
 int fw_list_drain(fw_list* op, const fw_list_rows* rows, int64_t cap_rows, const fw_list_elems* elems,
                   int64_t cap_elems, int64_t* n_rows, int64_t* n_elems);
 int fw_list_drain_side(fw_list* op, const fw_side_rows* host_dst, int64_t cap, int64_t* n);
+/* drops the pending rows and elements without copying them (a discarding sink) */
+int fw_list_clear_pending(fw_list* op);
 int fw_list_get_stats(fw_list* op, fw_stats* out);
 /* per key group: the lists (dst NULL or a capacity too small: only the counts) / restored into the handle, appended
  * to a list already present */

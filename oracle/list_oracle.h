@@ -14,7 +14,7 @@
  *                                                                       InternalIterableWindowFunction: apply/process)
  *   runtime/operators/windowing/WindowOperator.java:576-651           lateness / cleanup time / side output
  *   api/windowing/triggers/EventTimeTrigger.java:37-73, CountTrigger.java:47-70, PurgingTrigger.java:45-59
- *   api/windowing/evictors/CountEvictor.java:55-78, TimeEvictor.java:58-103, DeltaEvictor.java:56-80
+ *   api/windowing/evictors/CountEvictor.java:50-78, TimeEvictor.java:54-104, DeltaEvictor.java:59-80
  *   api/windowing/assigners/GlobalWindows.java (isEventTime false: never late, no cleanup timer)
  *   api/operators/HeapInternalTimerService.java:224-290                timer dedup + advanceWatermark
  *
