@@ -968,18 +968,17 @@ int fw_list_create(const fw_list_config* cfg, fw_list** out) {
   fw_list* op = new fw_list();
   op->cfg = *cfg;
   const fw_list_config& c = *cfg;
-  auto fail = [&](int code, const char* msg) {
-    fprintf(stderr, "fw_list_create: %s\n", msg);
-    delete op;
+  auto fail = [&](int code, const char* msg) {  // as fw_create: the handle carries the message; destroy it
+    op->err = msg;
+    *out = op;
     return code;
   };
   if (c.assigner != FW_TUMBLING && c.assigner != FW_SLIDING && c.assigner != FW_GLOBAL)
     return fail(FW_ERR_UNSUPPORTED, "assigner must be FW_TUMBLING, FW_SLIDING or FW_GLOBAL");
-  if (c.assigner != FW_GLOBAL && c.size <= 0) return fail(FW_ERR_ARG, "window size must be positive");
-  if (c.assigner == FW_SLIDING && (c.slide <= 0 || c.slide > c.size))
-    return fail(FW_ERR_ARG, "SlidingEventTimeWindows parameters must satisfy 0 < slide <= size");
-  if (c.assigner != FW_GLOBAL && (c.offset < 0 || c.offset >= (c.assigner == FW_SLIDING ? c.slide : c.size)))
-    return fail(FW_ERR_ARG, "window offset must be in [0, slide/size)");
+  if (c.assigner == FW_TUMBLING && (c.size <= 0 || c.offset < 0 || c.offset >= c.size))
+    return fail(FW_ERR_ARG, "TumblingEventTimeWindows parameters must satisfy 0 <= offset < size");
+  if (c.assigner == FW_SLIDING && (c.size <= 0 || c.slide <= 0 || c.slide > c.size || c.offset < 0 || c.offset >= c.slide))
+    return fail(FW_ERR_ARG, "SlidingEventTimeWindows parameters must satisfy 0 <= offset < slide <= size");
   if (c.allowed_lateness < 0) return fail(FW_ERR_ARG, "The allowed lateness cannot be negative.");
   if (c.trigger != FW_TRIGGER_EVENT_TIME && c.trigger != FW_TRIGGER_COUNT) return fail(FW_ERR_ARG, "unknown trigger");
   if (c.trigger == FW_TRIGGER_COUNT && c.trigger_count <= 0) return fail(FW_ERR_ARG, "CountTrigger count must be > 0");
@@ -996,7 +995,8 @@ int fw_list_create(const fw_list_config* cfg, fw_list** out) {
                c.trigger_count, c.evict_count, c.delta_threshold};
   op->device = c.device;
   if (hipSetDevice(c.device) != hipSuccess) return fail(FW_ERR_HIP, "hipSetDevice failed");
-  if (hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking) != hipSuccess) return fail(FW_ERR_HIP, "stream");
+  if (hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(FW_ERR_HIP, "hipStreamCreateWithFlags failed");
   op->max_batch = c.max_batch > 0 ? c.max_batch : (1 << 24);
   const int64_t fan = c.assigner == FW_SLIDING ? (c.size + c.slide - 1) / c.slide : 1;
   const int64_t exp = c.expected_elements > 0 ? c.expected_elements : std::min<int64_t>(op->max_batch * fan, 1 << 22);
@@ -1027,10 +1027,7 @@ int fw_list_create(const fw_list_config* cfg, fw_list** out) {
   if (rc == FW_OK && dmalloc(&op->S.ctr, 1) != hipSuccess) rc = FW_ERR_HIP;
   if (rc == FW_OK && hipMemsetAsync(op->S.ctr, 0, sizeof(LCounters), op->stream) != hipSuccess) rc = FW_ERR_HIP;
   if (rc == FW_OK && hipStreamSynchronize(op->stream) != hipSuccess) rc = FW_ERR_HIP;
-  if (rc != FW_OK) {
-    fw_list_destroy(op);
-    return rc;
-  }
+  if (rc != FW_OK) return fail(rc, "device allocation failed");
   *out = op;
   return FW_OK;
 }

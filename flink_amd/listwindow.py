@@ -67,8 +67,10 @@ class GpuListWindowOperator:
         L = N.lib()
         rc = L.fw_list_create(ctypes.byref(c), ctypes.byref(self._h))
         if rc != N.FW_OK:
+            msg = L.fw_list_last_error(self._h).decode() if self._h else "fw_list_create failed"
+            L.fw_list_destroy(self._h)
             self._h = None
-            raise N.NativeError(rc, "fw_list_create: invalid configuration")
+            raise N.NativeError(rc, msg)
         self.epoch = 0
         self._rows, self._elems, self._side, self._outputs = [], [], [], []
 

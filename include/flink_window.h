@@ -486,6 +486,7 @@ typedef struct fw_list_state {
   int64_t *ts, *val, *ordinal;                                   /* elements   */
 } fw_list_state;
 typedef struct fw_list fw_list;
+/* as fw_create: on an error *out may hold a handle that carries the message (fw_list_last_error); destroy it */
 int fw_list_create(const fw_list_config* cfg, fw_list** out);
 void fw_list_destroy(fw_list* op);
 const char* fw_list_last_error(const fw_list* op);

@@ -278,3 +278,37 @@ def test_gpu_list_full_size_every_record_once():
     assert op.stats()["keyed_state_entries"] == 0
     op.close()
     del torch
+
+
+def test_gpu_list_errors_and_edges():
+    from flink_amd import _native as N
+    from flink_amd.listwindow import GpuListWindowOperator
+    # Long.MIN_VALUE timestamps on an event-time assigner (TumblingEventTimeWindows.java:69-71): refused, state intact
+    op = GpuListWindowOperator(TumblingEventTimeWindows.of(100), max_batch=8)
+    with pytest.raises(N.NativeError) as e:
+        op.process(np.array([1, 2]), np.array([5, -(1 << 63)]), np.array([1, 1]))
+    assert e.value.code == N.FW_ERR_NO_TIMESTAMP
+    op.process(np.array([], dtype=np.int64), np.array([], dtype=np.int64), np.array([], dtype=np.int64))
+    with pytest.raises(N.NativeError) as e:  # a device batch beyond max_batch
+        import torch
+        z = torch.zeros(9, dtype=torch.int64, device="cuda")
+        op.process_batch(z, z, z)
+    assert e.value.code == N.FW_ERR_ARG
+    op.process(np.array([1, 1]), np.array([5, 7]), np.array([3, 4]))
+    op.watermark(50)
+    op.process(np.array([1]), np.array([10]), np.array([9]))  # late (window [0, 100) fired? no: maxTs 99 > 50)
+    op.watermark(200)
+    op.process(np.array([1, 2]), np.array([20, 30]), np.array([7, 7]))  # every window late: dropped
+    op.watermark(300)
+    assert [int(r["sum"]) for r in op.rows()] == [16]
+    assert op.late_dropped == 2
+    op.close()
+    # a key outside the KeyGroupRange
+    from flink_amd import KeyGroupRange
+    from flink_amd.keygroups import assign_to_key_group
+    keys = [k for k in range(100) if assign_to_key_group(k, 128) >= 64][:1]
+    op = GpuListWindowOperator(TumblingEventTimeWindows.of(100), key_group_range=KeyGroupRange(0, 63))
+    with pytest.raises(N.NativeError) as e:
+        op.process(np.array(keys), np.array([1]), np.array([1]))
+    assert e.value.code == N.FW_ERR_KEY_GROUP
+    op.close()

@@ -98,3 +98,51 @@ def test_count_windows_assigner_config():
     assert CountWindows.of(4, 2, evict_after=True).config()["count_evict_after"] == 1
     with pytest.raises(ValueError):
         CountWindows.of(0)
+
+
+def _list_create(**kw):
+    c = N.FwListConfig()
+    c.key_group_start = c.key_group_end = -1
+    for k, v in kw.items():
+        setattr(c, k, v)
+    h = ctypes.c_void_p()
+    rc = N.lib().fw_list_create(ctypes.byref(c), ctypes.byref(h))
+    msg = N.lib().fw_list_last_error(h).decode() if h else ""
+    N.lib().fw_list_destroy(h)
+    return rc, msg
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(assigner=N.FW_TUMBLING, size=100, offset=100), "TumblingEventTimeWindows parameters must satisfy"),
+    (dict(assigner=N.FW_SLIDING, size=100, slide=200), "SlidingEventTimeWindows parameters must satisfy"),
+    (dict(assigner=N.FW_TUMBLING, size=10, allowed_lateness=-1), "The allowed lateness cannot be negative"),
+    (dict(assigner=N.FW_GLOBAL, trigger=N.FW_TRIGGER_COUNT, trigger_count=0), "CountTrigger count must be > 0"),
+    (dict(assigner=N.FW_GLOBAL, evictor=N.FW_EVICT_COUNT, evict_count=-1), "CountEvictor count must be >= 0"),
+    (dict(assigner=N.FW_TUMBLING, size=10, key_group_start=5, key_group_end=200), "invalid KeyGroupRange"),
+])
+def test_list_create_rejects_invalid_config(kw, msg):
+    # f4: the window-contents operator validates its configuration before it touches the GPU
+    rc, m = _list_create(**kw)
+    assert rc == N.FW_ERR_ARG
+    assert msg in m
+
+
+def test_list_struct_layouts_match_header(tmp_path):
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    structs = {"fw_list_config": N.FwListConfig, "fw_list_rows": N.FwListRows, "fw_list_elems": N.FwListElems,
+               "fw_list_state": N.FwListState}
+    body = ""
+    for name, cls in structs.items():
+        body += f'  printf("%zu\\n", sizeof({name}));\n'
+        body += "".join(f'  printf("%zu\\n", offsetof({name}, {f}));\n' for f, _ in cls._fields_)
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "flink_window.h"\nint main(void) {\n' + body +
+                   "  return 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)])
+    out = iter(int(x) for x in subprocess.check_output([str(exe)]).split())
+    for name, cls in structs.items():
+        assert ctypes.sizeof(cls) == next(out), name
+        assert [getattr(cls, f).offset for f, _ in cls._fields_] == [next(out) for _ in cls._fields_], name
