@@ -58,6 +58,7 @@ struct LCfg {
 struct LCounters {
   unsigned long long rows, elems, side, late, dead, live_groups, tombs, nfire, nclean, count;
   unsigned int flags, need_seq;
+  long long next_due;  // no group's trigger or cleanup timer is earlier: a watermark below it has nothing to do
 };
 
 struct LState {
@@ -116,14 +117,23 @@ __device__ __forceinline__ void for_windows(const LCfg& c, int64_t ts, int64_t w
 __device__ __forceinline__ uint32_t g_hash(int64_t key, int64_t start) {
   return (uint32_t)fmix64((uint64_t)key ^ fmix64((uint64_t)start ^ 0x9E3779B97F4A7C15ull));
 }
-// limit > 0: no new group beyond `limit` live ones (LF_MAP_FULL is raised instead, nothing inserted)
-__device__ int32_t g_find_insert(const LState& S, int64_t key, int64_t start, int32_t kg,
-                                 unsigned long long limit = 0) {
+// Lookups read the state word with a relaxed agent-scope load (L2, no L1 invalidation as an acquire would cost on
+// every probe) and, once it reads LIVE, the key and window the same way: the inserter's plain stores of both precede
+// its release store of LIVE, and the key loads are issued only after the state's value has arrived (they depend on
+// it), so they read what the inserter wrote.
+__device__ __forceinline__ int64_t ld_l2(const int64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// limit > 0: no new group beyond `limit` live ones (LF_MAP_FULL is raised instead, nothing inserted).  *ins counts
+// the groups this call inserted (the caller adds them to live_groups, one atomic per workgroup).
+__device__ int32_t g_find_insert(const LState& S, int64_t key, int64_t start, int32_t kg, unsigned long long limit,
+                                 unsigned* ins) {
   uint32_t s = g_hash(key, start) & S.gmask;
   for (uint32_t probes = 0; probes <= S.gmask;) {
-    const uint32_t cur = __hip_atomic_load(&S.gst[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t cur = __hip_atomic_load(&S.gst[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __atomic_signal_fence(__ATOMIC_ACQUIRE);  // (the compiler keeps the key loads behind it)
     if (cur == G_LIVE) {
-      if (S.gkey[s] == key && S.gstart[s] == start) return (int32_t)s;
+      if (ld_l2(&S.gkey[s]) == key && ld_l2(&S.gstart[s]) == start) return (int32_t)s;
     } else if (cur == G_BUSY) {
       continue;  // being published by another lane: read it again
     } else if (cur == G_EMPTY) {
@@ -138,7 +148,7 @@ __device__ int32_t g_find_insert(const LState& S, int64_t key, int64_t start, in
         S.gcnt[s] = 0;
         S.gfl[s] = 0;
         __hip_atomic_store(&S.gst[s], G_LIVE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        atomicAdd(&S.ctr->live_groups, 1ull);
+        (*ins)++;
         return (int32_t)s;
       }
       continue;  // lost the race for this slot: read it again
@@ -148,6 +158,28 @@ __device__ int32_t g_find_insert(const LState& S, int64_t key, int64_t start, in
   }
   atomicOr(&S.ctr->flags, LF_MAP_FULL);
   return -1;
+}
+__device__ __forceinline__ uint64_t lanemask_lt64() {
+  const int lane = __lane_id();
+  return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+// per-workgroup minimum into a global one
+__device__ __forceinline__ void block_min(long long* dst, long long v) {
+  __shared__ long long acc;
+  if (threadIdx.x == 0) acc = LMAX;
+  __syncthreads();
+  if (v != LMAX) atomicMin(&acc, v);
+  __syncthreads();
+  if (threadIdx.x == 0 && acc != LMAX) atomicMin(dst, acc);
+}
+// per-workgroup sum into a global counter (one atomic per workgroup instead of one per thread)
+__device__ __forceinline__ void block_add(unsigned long long* dst, unsigned long long v) {
+  __shared__ unsigned long long acc;
+  if (threadIdx.x == 0) acc = 0;
+  __syncthreads();
+  if (v) atomicAdd(&acc, v);
+  __syncthreads();
+  if (threadIdx.x == 0 && acc) atomicAdd(dst, acc);
 }
 
 // ---------------------------------------------------------------- push
@@ -185,40 +217,35 @@ __global__ __launch_bounds__(256) void k_lp_count(LCfg c, LState S, const int64_
   }
 }
 
-// the (key, window) groups of the batch's entries, inserted up to `limit` live groups (idempotent: a batch that
-// stops at the limit is inserted again once the map has grown)
-__global__ __launch_bounds__(256) void k_lp_groups(LCfg c, LState S, const int64_t* __restrict__ key,
-                                                   const int64_t* __restrict__ ts, const int32_t* __restrict__ kh,
-                                                   int64_t n, int64_t wm, const uint32_t* __restrict__ wcnt,
-                                                   unsigned long long limit) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (!wcnt[i]) continue;
-    const int64_t k = key[i];
-    const int32_t kg = key_group(key_hash_of(c.key_kind, k, kh, i), c.max_par);
-    for_windows(c, ts[i], wm, [&](int64_t s) { g_find_insert(S, k, s, kg, limit); });
-  }
-}
-
 // the entries: log[base + woff[i] + j] = (ts, value, ordinal, group) for the j-th non-late window of record i;
 // groups whose elements fire while being processed are marked for the ordered walk
 __global__ __launch_bounds__(256) void k_lp_append(LCfg c, LState S, const int64_t* __restrict__ key,
                                                    const int64_t* __restrict__ ts, const int64_t* __restrict__ val,
                                                    const int32_t* __restrict__ kh, int64_t n, int64_t wm,
                                                    const uint32_t* __restrict__ wcnt, const uint32_t* __restrict__ woff,
-                                                   int64_t base, int64_t ord_base) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (!wcnt[i]) continue;
+                                                   int64_t base, int64_t ord_base, unsigned long long limit) {
+  long long due = LMAX;  // the earliest timer these entries register
+  unsigned ins = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
+    const int64_t i = i0 + threadIdx.x;
+    if (i >= n || !wcnt[i]) continue;
     const int64_t t = ts[i], k = key[i], v = val[i];
     const int32_t kg = key_group(key_hash_of(c.key_kind, k, kh, i), c.max_par);
     int64_t idx = base + woff[i];
     for_windows(c, t, wm, [&](int64_t s) {
-      const int32_t g = g_find_insert(S, k, s, kg);
+      const int64_t mts = w_max_ts(c, s), cl = w_cleanup(c, s);
+      due = min(due, (long long)(c.trigger == FW_TRIGGER_EVENT_TIME && mts > wm ? mts : cl));
+      const int32_t g = g_find_insert(S, k, s, kg, limit, &ins);
       S.lts[idx] = t;
       S.lval[idx] = v;
       S.lord[idx] = ord_base + i;
       S.lgid[idx] = g;
       idx++;
-      if (g < 0) return;
+      if (g < 0) {
+        atomicOr(&S.ctr->flags, LF_MAP_FULL);
+        return;
+      }
       if (c.trigger == FW_TRIGGER_COUNT || w_max_ts(c, s) <= wm) {  // CountTrigger / late firing
         atomicOr(&S.gfl[g], GF_TOUCH);
         S.ctr->need_seq = 1u;
@@ -227,6 +254,8 @@ __global__ __launch_bounds__(256) void k_lp_append(LCfg c, LState S, const int64
       }
     });
   }
+  block_min(&S.ctr->next_due, due);
+  block_add(&S.ctr->live_groups, ins);
 }
 
 // ---------------------------------------------------------------- ordered walks
@@ -264,12 +293,25 @@ __device__ __forceinline__ double delta_of(const LCfg& c, int64_t e, int64_t las
   }
 }
 
-// one list in the sorted positions pos[a .. j] (log indices in list order): which of its live elements the
-// evictor removes (CountEvictor.evict :63-78, TimeEvictor.evict :75-103, DeltaEvictor.evict :71-80).
+// The walk's view of the selected elements, gathered into list order (k_gather_sel): their timestamps, values and
+// ordinals side by side, and whether each is still live; a kill also marks the log (group -1).
+struct LView {
+  const uint32_t* pos;  // log index of each sorted position
+  const int64_t *ts, *val, *ord;
+  uint8_t* alive;
+  int32_t* lgid;
+  __device__ __forceinline__ void kill(int64_t q) const {
+    alive[q] = 0;
+    lgid[pos[q]] = -1;
+  }
+};
+
+// one list in the sorted positions [a .. j] of the view: which of its live elements the evictor removes
+// (CountEvictor.evict :63-78, TimeEvictor.evict :67-96, DeltaEvictor.evict :72-80).
 // mark = false: returns how many would remain; mark = true: kills the others and returns the remaining count.
-__device__ int64_t evict(const LCfg& c, const LState& S, const uint32_t* pos, int64_t a, int64_t j, bool mark) {
+__device__ int64_t evict(const LCfg& c, const LState& S, const LView& V, int64_t a, int64_t j, bool mark) {
   int64_t live = 0;
-  for (int64_t q = a; q <= j; q++) live += S.lgid[pos[q]] >= 0;
+  for (int64_t q = a; q <= j; q++) live += V.alive[q];
   if (c.evictor == FW_EVICT_NONE || live == 0) return live;
   int64_t killed = 0;
   if (c.evictor == FW_EVICT_COUNT) {
@@ -277,8 +319,8 @@ __device__ int64_t evict(const LCfg& c, const LState& S, const uint32_t* pos, in
     const int64_t drop = live - c.ev_n;
     if (mark) {
       for (int64_t q = a; q <= j && killed < drop; q++)
-        if (S.lgid[pos[q]] >= 0) {
-          S.lgid[pos[q]] = -1;
+        if (V.alive[q]) {
+          V.kill(q);
           killed++;
         }
     } else {
@@ -288,31 +330,28 @@ __device__ int64_t evict(const LCfg& c, const LState& S, const uint32_t* pos, in
     int64_t first_ts = 0, mx = LMIN;
     bool have = false;
     for (int64_t q = a; q <= j; q++) {
-      const uint32_t e = pos[q];
-      if (S.lgid[e] < 0) continue;
-      if (!have) first_ts = S.lts[e];
+      if (!V.alive[q]) continue;
+      if (!have) first_ts = V.ts[q];
       have = true;
-      mx = max(mx, S.lts[e]);
+      mx = max(mx, V.ts[q]);
     }
     if (first_ts == LMIN) return live;  // hasTimestamp of the first element
     const int64_t cutoff = jsub(mx, c.ev_n);
     for (int64_t q = a; q <= j; q++) {
-      const uint32_t e = pos[q];
-      if (S.lgid[e] < 0 || !(S.lts[e] <= cutoff)) continue;
-      if (mark) S.lgid[e] = -1;
+      if (!V.alive[q] || !(V.ts[q] <= cutoff)) continue;
+      if (mark) V.kill(q);
       killed++;
     }
   } else {  // FW_EVICT_DELTA
     int64_t last = 0;
     for (int64_t q = j; q >= a; q--)
-      if (S.lgid[pos[q]] >= 0) {
-        last = S.lval[pos[q]];
+      if (V.alive[q]) {
+        last = V.val[q];
         break;
       }
     for (int64_t q = a; q <= j; q++) {
-      const uint32_t e = pos[q];
-      if (S.lgid[e] < 0 || !(delta_of(c, S.lval[e], last) >= c.thr)) continue;
-      if (mark) S.lgid[e] = -1;
+      if (!V.alive[q] || !(delta_of(c, V.val[q], last) >= c.thr)) continue;
+      if (mark) V.kill(q);
       killed++;
     }
   }
@@ -320,15 +359,15 @@ __device__ int64_t evict(const LCfg& c, const LState& S, const uint32_t* pos, in
   return live - killed;
 }
 
-// emitWindowContents (:334-366) of group g over the list pos[a .. j]: evictBefore, one row (+ the elements),
-// evictAfter.  False (nothing changed) when the element buffer cannot take the contents.
-__device__ bool emit_firing(const LCfg& c, const LState& S, uint32_t g, const uint32_t* pos, int64_t a, int64_t j,
+// emitWindowContents (:334-366) of group g over the list [a .. j] of the view: evictBefore, one row (+ the
+// elements), evictAfter.  False (nothing changed) when the element buffer cannot take the contents.
+__device__ bool emit_firing(const LCfg& c, const LState& S, const LView& V, uint32_t g, int64_t a, int64_t j,
                             bool room) {
   int64_t cnt = 0;  // the elements the function sees
   if (c.evict_after)
-    for (int64_t q = a; q <= j; q++) cnt += S.lgid[pos[q]] >= 0;
+    for (int64_t q = a; q <= j; q++) cnt += V.alive[q];
   else
-    cnt = evict(c, S, pos, a, j, false);
+    cnt = evict(c, S, V, a, j, false);
   int64_t eoff = 0;
   if (c.emit && cnt && room) {  // the host sized the element buffer for every possible firing
     eoff = (int64_t)atomicAdd(&S.ctr->elems, (unsigned long long)cnt);
@@ -345,15 +384,14 @@ __device__ bool emit_firing(const LCfg& c, const LState& S, uint32_t g, const ui
     }
     eoff = (int64_t)cur;
   }
-  if (!c.evict_after) evict(c, S, pos, a, j, true);
+  if (!c.evict_after) evict(c, S, V, a, j, true);
   const bool fl = c.vt == FW_VAL_F64 || c.vt == FW_VAL_F32;
   double ds = 0.0;
   int64_t is = 0, mn = 0, mx = 0, first = -1, k = 0;
   for (int64_t q = a; q <= j; q++) {
-    const uint32_t e = pos[q];
-    if (S.lgid[e] < 0) continue;
-    const int64_t v = S.lval[e];
-    if (k == 0) first = S.lord[e];
+    if (!V.alive[q]) continue;
+    const int64_t v = V.val[q];
+    if (k == 0) first = V.ord[q];
     if (fl) {
       const double d = __longlong_as_double(v);
       ds = k == 0 ? d : c.vt == FW_VAL_F32 ? (double)((float)ds + (float)d) : ds + d;
@@ -365,9 +403,9 @@ __device__ bool emit_firing(const LCfg& c, const LState& S, uint32_t g, const ui
       if (k == 0 || v > mx) mx = v;
     }
     if (c.emit) {
-      S.ets[eoff + k] = S.lts[e];
+      S.ets[eoff + k] = V.ts[q];
       S.eval[eoff + k] = v;
-      S.eord[eoff + k] = S.lord[e];
+      S.eord[eoff + k] = V.ord[q];
     }
     k++;
   }
@@ -388,17 +426,30 @@ __device__ bool emit_firing(const LCfg& c, const LState& S, uint32_t g, const ui
   }
   S.rfirst[r] = first;
   S.roff[r] = c.emit ? eoff : 0;
-  if (c.evict_after) evict(c, S, pos, a, j, true);
+  if (c.evict_after) evict(c, S, V, a, j, true);
   return true;
 }
-__device__ void purge(const LState& S, const uint32_t* pos, int64_t a, int64_t j) {
+__device__ void purge(const LState& S, const LView& V, int64_t a, int64_t j) {
   int64_t killed = 0;
   for (int64_t q = a; q <= j; q++)
-    if (S.lgid[pos[q]] >= 0) {
-      S.lgid[pos[q]] = -1;
+    if (V.alive[q]) {
+      V.kill(q);
       killed++;
     }
   if (killed) atomicAdd(&S.ctr->dead, (unsigned long long)killed);
+}
+
+// the selected elements in list order, side by side (one pass of random reads, coalesced writes)
+__global__ __launch_bounds__(256) void k_gather_sel(LState S, const uint32_t* __restrict__ pos, int64_t m,
+                                                    int64_t* __restrict__ ts, int64_t* __restrict__ val,
+                                                    int64_t* __restrict__ ord, uint8_t* __restrict__ alive) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t e = pos[i];
+    ts[i] = S.lts[e];
+    val[i] = S.lval[e];
+    ord[i] = S.lord[e];
+    alive[i] = 1;  // selected entries are live
+  }
 }
 
 // One thread per list.  PUSH: the list's elements appended by this push (log index >= base_new), in order:
@@ -407,17 +458,17 @@ __device__ void purge(const LState& S, const uint32_t* pos, int64_t a, int64_t j
 // launch stopped (the element buffer was full); the host grows it and launches again.
 // WATERMARK: the due lists fire over all their elements (onEventTime, :241-286).
 template <bool PUSH>
-__global__ __launch_bounds__(256) void k_walk(LCfg c, LState S, const uint32_t* __restrict__ pos,
-                                              const uint32_t* __restrict__ keys, const uint32_t* __restrict__ seg,
-                                              int64_t nseg, int64_t base_new, int64_t wm, int64_t* __restrict__ prog,
-                                              bool room) {
+__global__ __launch_bounds__(256) void k_walk(LCfg c, LState S, LView V, const uint32_t* __restrict__ keys,
+                                              const uint32_t* __restrict__ seg, int64_t nseg, int64_t base_new,
+                                              int64_t wm, int64_t* __restrict__ prog, bool room) {
+  const uint32_t* __restrict__ pos = V.pos;
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = seg[s], b = seg[s + 1];
     const uint32_t g = keys[a];
     if (!PUSH) {
       if (!(S.gfl[g] & GF_FIRE)) continue;
-      if (!emit_firing(c, S, g, pos, a, b - 1, room)) continue;
-      if (c.purging) purge(S, pos, a, b - 1);
+      if (!emit_firing(c, S, V, g, a, b - 1, room)) continue;
+      if (c.purging) purge(S, V, a, b - 1);
       atomicAnd(&S.gfl[g], ~GF_FIRE);
       continue;
     }
@@ -436,12 +487,12 @@ __global__ __launch_bounds__(256) void k_walk(LCfg c, LState S, const uint32_t* 
         fire = mts <= wm;
       }
       if (fire) {
-        if (!emit_firing(c, S, g, pos, a, j, room)) {
+        if (!emit_firing(c, S, V, g, a, j, room)) {
           prog[s] = j;
           stopped = true;
           break;
         }
-        if (c.purging) purge(S, pos, a, j);
+        if (c.purging) purge(S, V, a, j);
       }
       if (c.trigger == FW_TRIGGER_COUNT) S.gcnt[g] = fire ? 0 : nc;
     }
@@ -471,24 +522,99 @@ __global__ __launch_bounds__(256) void k_walk_bound(LCfg c, LState S, const uint
   if (tot) atomicAdd(&S.ctr->count, tot);
 }
 
+// The watermark walk of the common apply shape (no evictor, an integer field, the element buffer sized): one wave per
+// due list, its elements read and emitted 64 at a time (coalesced) and the reduce done across the wave (integer sums
+// wrap the same in any order).  Other shapes take k_walk<false>.
+__global__ __launch_bounds__(256) void k_walk_wm_wave(LCfg c, LState S, LView V, const uint32_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ seg, int64_t nseg) {
+  const int lane = __lane_id();
+  const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; s < nseg; s += waves) {
+    const int64_t a = seg[s], b = seg[s + 1];
+    const uint32_t g = keys[a];
+    if (!(S.gfl[g] & GF_FIRE)) continue;
+    int64_t cnt = 0;
+    for (int64_t q0 = a; q0 < b; q0 += 64) cnt += __popcll(__ballot(q0 + lane < b && V.alive[q0 + lane]));
+    int64_t eoff = 0;
+    if (c.emit && cnt) {
+      if (lane == 0) eoff = (int64_t)atomicAdd(&S.ctr->elems, (unsigned long long)cnt);
+      eoff = __shfl(eoff, 0, 64);
+    }
+    int64_t is = 0, mn = LMAX, mx = LMIN, first = -1, k = 0, killed = 0;
+    for (int64_t q0 = a; q0 < b; q0 += 64) {
+      const int64_t q = q0 + lane;
+      const bool al = q < b && V.alive[q];
+      const uint64_t m = __ballot(al);
+      if (!m) continue;
+      if (first < 0) first = __shfl(al ? V.ord[q] : 0, __ffsll((long long)m) - 1, 64);
+      if (al) {
+        const int64_t v = V.val[q];
+        is = jadd(is, v);
+        mn = min(mn, v);
+        mx = max(mx, v);
+        if (c.emit) {
+          const int64_t o = eoff + k + __popcll(m & lanemask_lt64());
+          S.ets[o] = V.ts[q];
+          S.eval[o] = v;
+          S.eord[o] = V.ord[q];
+        }
+        if (c.purging) {
+          V.kill(q);
+          killed++;
+        }
+      }
+      k += __popcll(m);
+    }
+    for (int o = 32; o; o >>= 1) {  // the wave's reduce
+      is = jadd(is, __shfl_xor(is, o, 64));
+      mn = min(mn, __shfl_xor(mn, o, 64));
+      mx = max(mx, __shfl_xor(mx, o, 64));
+      killed += __shfl_xor(killed, o, 64);
+    }
+    if (lane == 0) {
+      const unsigned long long r = atomicAdd(&S.ctr->rows, 1ull);
+      S.rkey[r] = S.gkey[g];
+      S.rstart[r] = S.gstart[g];
+      S.rend[r] = w_end(c, S.gstart[g]);
+      S.rcnt[r] = k;
+      S.rsum[r] = c.vt == FW_VAL_I32 ? (int64_t)(int32_t)is : c.vt == FW_VAL_I16 ? (int64_t)(int16_t)is
+                : c.vt == FW_VAL_I8 ? (int64_t)(int8_t)is : is;
+      S.rmin[r] = k ? mn : 0;
+      S.rmax[r] = k ? mx : 0;
+      S.rfirst[r] = first;
+      S.roff[r] = c.emit ? eoff : 0;
+      if (killed) atomicAdd(&S.ctr->dead, (unsigned long long)killed);
+      atomicAnd(&S.gfl[g], ~GF_FIRE);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- watermark
 __global__ __launch_bounds__(256) void k_lw_due(LCfg c, LState S, int64_t wm) {
+  unsigned long long nf = 0, nc = 0;
+  long long due = LMAX;  // the remaining groups' earliest timer
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)S.gmask;
        g += (int64_t)gridDim.x * blockDim.x) {
     if (S.gst[g] != G_LIVE) continue;
     const int64_t st = S.gstart[g];
-    uint32_t f = S.gfl[g];
+    const uint32_t f0 = S.gfl[g];
+    uint32_t f = f0;
     if ((f & GF_TIMER) && w_max_ts(c, st) <= wm) {  // the trigger timer fires (EventTimeTrigger.onEventTime)
       f = (f & ~GF_TIMER) | GF_FIRE;
-      atomicAdd(&S.ctr->nfire, 1ull);
+      nf++;
     }
     const int64_t cl = w_cleanup(c, st);
     if (cl != LMAX && cl <= wm) {  // no cleanup timer is registered at Long.MAX_VALUE (registerCleanupTimer)
       f |= GF_CLEAN;
-      atomicAdd(&S.ctr->nclean, 1ull);
+      nc++;
+    } else {
+      due = min(due, (long long)((f & GF_TIMER) ? w_max_ts(c, st) : cl));
     }
-    S.gfl[g] = f;
+    if (f != f0) S.gfl[g] = f;
   }
+  block_min(&S.ctr->next_due, due);
+  block_add(&S.ctr->nfire, nf);
+  block_add(&S.ctr->nclean, nc);
 }
 // clearAllState (:368-385): the cleaned-up groups' elements die, their namespaces become tombstones
 __global__ __launch_bounds__(256) void k_lw_clean_log(LState S, int64_t n) {
@@ -503,35 +629,41 @@ __global__ __launch_bounds__(256) void k_lw_clean_log(LState S, int64_t n) {
   if (killed) atomicAdd(&S.ctr->dead, killed);
 }
 __global__ __launch_bounds__(256) void k_lw_clean_map(LState S) {
+  unsigned long long nt = 0;
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)S.gmask;
        g += (int64_t)gridDim.x * blockDim.x) {
     if (S.gst[g] != G_LIVE) continue;
     const uint32_t f = S.gfl[g];
     if (f & GF_CLEAN) {
       S.gst[g] = G_TOMB;
-      atomicSub(&S.ctr->live_groups, 1ull);
-      atomicAdd(&S.ctr->tombs, 1ull);
+      nt++;
     } else if (f & GF_FIRE) {
       S.gfl[g] = f & ~GF_FIRE;  // a due timer of an empty list: nothing to fire
     }
   }
+  block_add(&S.ctr->tombs, nt);
+  block_add(&S.ctr->live_groups, (unsigned long long)(-(long long)nt));  // (wraps: a subtraction)
 }
 
 // ---------------------------------------------------------------- compaction / rebuild
 __global__ __launch_bounds__(256) void k_rebuild_map(LCfg c, LState o, LState S, int32_t* __restrict__ remap) {
-  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)o.gmask;
-       g += (int64_t)gridDim.x * blockDim.x) {
+  unsigned ins = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x; g0 <= (int64_t)o.gmask; g0 += stride) {
+    const int64_t g = g0 + threadIdx.x;
+    if (g > (int64_t)o.gmask) continue;
     if (o.gst[g] != G_LIVE) {
       remap[g] = -1;
       continue;
     }
-    const int32_t ng = g_find_insert(S, o.gkey[g], o.gstart[g], o.gkg[g]);
+    const int32_t ng = g_find_insert(S, o.gkey[g], o.gstart[g], o.gkg[g], 0, &ins);
     remap[g] = ng;
     if (ng >= 0) {
       S.gcnt[ng] = o.gcnt[g];
       S.gfl[ng] = o.gfl[g];
     }
   }
+  block_add(&S.ctr->live_groups, ins);
 }
 __global__ __launch_bounds__(256) void k_alive_flags(const int32_t* __restrict__ gid, int64_t n, uint8_t* __restrict__ f) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -588,11 +720,14 @@ __global__ void k_restore_groups(LCfg c, LState S, const int64_t* __restrict__ k
                                  const int64_t* __restrict__ cnt, const int64_t* __restrict__ timer, int64_t n,
                                  int32_t kg, int32_t* __restrict__ gid_out) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t g = g_find_insert(S, key[i], start[i], kg);
+    unsigned ins = 0;
+    const int32_t g = g_find_insert(S, key[i], start[i], kg, 0, &ins);
+    if (ins) atomicAdd(&S.ctr->live_groups, 1ull);  // (one thread)
     gid_out[i] = g;
     if (g < 0) continue;
     S.gcnt[g] = cnt[i];
     if (timer[i]) atomicOr(&S.gfl[g], GF_TIMER);
+    atomicMin(&S.ctr->next_due, (long long)(timer[i] ? w_max_ts(c, start[i]) : w_cleanup(c, start[i])));
   }
 }
 __global__ __launch_bounds__(256) void k_restore_elems(LState S, const int64_t* __restrict__ ts,
@@ -638,6 +773,8 @@ struct fw_list {
   int64_t sel_cap = 0;
   uint8_t* flags8 = nullptr;
   uint32_t *sel = nullptr, *sel2 = nullptr, *keys = nullptr, *keys2 = nullptr, *seg = nullptr;
+  int64_t *gts = nullptr, *gval = nullptr, *gord = nullptr;  // the walk's gathered view (LView)
+  uint8_t* galive = nullptr;
   int64_t* prog = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
@@ -719,6 +856,14 @@ int ensure_sel(fw_list* op, int64_t n) {
   dfree(op->keys2);
   dfree(op->seg);
   dfree(op->prog);
+  dfree(op->gts);
+  dfree(op->gval);
+  dfree(op->gord);
+  dfree(op->galive);
+  LHIP(op, dmalloc(&op->gts, (size_t)cap));
+  LHIP(op, dmalloc(&op->gval, (size_t)cap));
+  LHIP(op, dmalloc(&op->gord, (size_t)cap));
+  LHIP(op, dmalloc(&op->galive, (size_t)cap));
   LHIP(op, dmalloc(&op->flags8, (size_t)cap));
   LHIP(op, dmalloc(&op->sel, (size_t)cap));
   LHIP(op, dmalloc(&op->sel2, (size_t)cap));
@@ -808,6 +953,9 @@ int walk_lists(fw_list* op, uint32_t bit, int64_t base_new) {
   const uint32_t mm = (uint32_t)m;
   LHIP(op, hipMemcpyAsync(op->seg + nseg, &mm, 4, hipMemcpyHostToDevice, op->stream));
   LHIP(op, hipMemsetAsync(op->prog, 0xff, (size_t)nseg * 8, op->stream));
+  hipLaunchKernelGGL(k_gather_sel, dim3(grid_for(m)), dim3(256), 0, op->stream, op->S, op->sel2, m, op->gts, op->gval,
+                     op->gord, op->galive);
+  const LView V{op->sel2, op->gts, op->gval, op->gord, op->galive, op->S.lgid};
   // with room for every possible firing the walk reserves elements with plain atomics; else (a bound beyond
   // FW_LIST_ROOM elements) it reserves with compare-and-swap and stops where the buffer is full
   bool room = !op->c.emit;
@@ -822,10 +970,17 @@ int walk_lists(fw_list* op, uint32_t bit, int64_t base_new) {
       room = true;
     }
   }
+  const bool fl = op->c.vt == FW_VAL_F64 || op->c.vt == FW_VAL_F32;
+  if (!PUSH && room && op->c.evictor == FW_EVICT_NONE && !fl) {  // the common apply shape: a wave per list
+    hipLaunchKernelGGL(k_walk_wm_wave, dim3((unsigned)std::min<int64_t>(16384, (nseg + 3) / 4)), dim3(256), 0,
+                       op->stream, op->c, op->S, V, op->keys2, op->seg, nseg);
+    LHIP(op, hipGetLastError());
+    return FW_OK;
+  }
   for (int round = 0;; round++) {
     LHIP(op, hipMemsetAsync(&op->S.ctr->flags, 0, 4, op->stream));
-    hipLaunchKernelGGL(k_walk<PUSH>, dim3(grid_for(nseg)), dim3(256), 0, op->stream, op->c, op->S, op->sel2,
-                       op->keys2, op->seg, nseg, base_new, op->wm, op->prog, room);
+    hipLaunchKernelGGL(k_walk<PUSH>, dim3(grid_for(nseg)), dim3(256), 0, op->stream, op->c, op->S, V, op->keys2,
+                       op->seg, nseg, base_new, op->wm, op->prog, room);
     LHIP(op, hipGetLastError());
     LRET(read_ctr(op));
     if (!(op->h_ctr->flags & LF_ELEMS)) break;
@@ -931,22 +1086,23 @@ int push_device(fw_list* op, const int64_t* key, const int64_t* ts, const int64_
   if (op->h_ctr->flags & LF_KEY_GROUP)
     return set_err(op, FW_ERR_KEY_GROUP, "a key of the batch is outside the handle's KeyGroupRange");
   const int64_t E = total;
-  // the batch's groups first, at <= 3/4 load (the map doubles and the insert runs again when it would not fit)
+  // room: the log, a row per possibly firing entry
+  LRET(grow_log(op, E));
+  LRET(ensure_rows(op, (int64_t)op->h_ctr->rows + E));
+  // the entries, their groups inserted on the way at <= 3/4 load; when the map would pass it, nothing is lost: it
+  // doubles (with a compaction of the log) and the append runs again from the start (it writes the same entries
+  // and sets the same flags)
+  int64_t base = op->n_log;
   for (int round = 0;; round++) {
-    LHIP(op, hipMemsetAsync(&op->S.ctr->flags, 0, 4, op->stream));
-    hipLaunchKernelGGL(k_lp_groups, dim3(grid_for(n)), dim3(256), 0, op->stream, op->c, op->S, key, ts, kh, n, op->wm,
-                       op->wcnt, (unsigned long long)(op->gcap / 4 * 3));
+    LHIP(op, hipMemsetAsync(&op->S.ctr->flags, 0, 8, op->stream));  // flags, need_seq
+    hipLaunchKernelGGL(k_lp_append, dim3(grid_for(n)), dim3(256), 0, op->stream, op->c, op->S, key, ts, val, kh, n,
+                       op->wm, op->wcnt, op->woff, base, op->ord_base, (unsigned long long)(op->gcap / 4 * 3));
     LRET(read_ctr(op));
     if (!(op->h_ctr->flags & LF_MAP_FULL)) break;
     if (round > 40) return set_err(op, FW_ERR_CAPACITY, "list state map full");
     LRET(compact(op, op->gcap));  // twice the capacity
+    base = op->n_log;
   }
-  // room: the log, a row per possibly firing entry
-  LRET(grow_log(op, E));
-  LRET(ensure_rows(op, (int64_t)op->h_ctr->rows + E));
-  const int64_t base = op->n_log;
-  hipLaunchKernelGGL(k_lp_append, dim3(grid_for(n)), dim3(256), 0, op->stream, op->c, op->S, key, ts, val, kh, n,
-                     op->wm, op->wcnt, op->woff, base, op->ord_base);
   LHIP(op, hipGetLastError());
   op->n_log += E;
   op->ord_base += n;
@@ -1001,7 +1157,7 @@ int fw_list_create(const fw_list_config* cfg, fw_list** out) {
   const int64_t fan = c.assigner == FW_SLIDING ? (c.size + c.slide - 1) / c.slide : 1;
   const int64_t exp = c.expected_elements > 0 ? c.expected_elements : std::min<int64_t>(op->max_batch * fan, 1 << 22);
   op->lcap = std::max<int64_t>(exp, 1024);
-  int64_t g = 1024;  // groups: the map grows with them (k_lp_groups)
+  int64_t g = 1024;  // groups: the map grows with them (k_lp_append)
   while (g < 2 * std::min<int64_t>(op->lcap, 1 << 22)) g <<= 1;
   op->gcap = g;
   op->rcap = 1024;
@@ -1026,6 +1182,10 @@ int fw_list_create(const fw_list_config* cfg, fw_list** out) {
   if (rc == FW_OK && dmalloc(&op->woff, (size_t)op->max_batch + 1) != hipSuccess) rc = FW_ERR_HIP;
   if (rc == FW_OK && dmalloc(&op->S.ctr, 1) != hipSuccess) rc = FW_ERR_HIP;
   if (rc == FW_OK && hipMemsetAsync(op->S.ctr, 0, sizeof(LCounters), op->stream) != hipSuccess) rc = FW_ERR_HIP;
+  if (rc == FW_OK) {
+    static const long long none = LMAX;
+    if (hipMemcpyAsync(&op->S.ctr->next_due, &none, 8, hipMemcpyHostToDevice, op->stream) != hipSuccess) rc = FW_ERR_HIP;
+  }
   if (rc == FW_OK && hipStreamSynchronize(op->stream) != hipSuccess) rc = FW_ERR_HIP;
   if (rc != FW_OK) return fail(rc, "device allocation failed");
   *out = op;
@@ -1053,6 +1213,10 @@ void fw_list_destroy(fw_list* op) {
   dfree(op->keys2);
   dfree(op->seg);
   dfree(op->prog);
+  dfree(op->gts);
+  dfree(op->gval);
+  dfree(op->gord);
+  dfree(op->galive);
   if (op->tmp) (void)hipFree(op->tmp);
   if (op->h_ctr) (void)hipHostFree(op->h_ctr);
   if (op->stream) (void)hipStreamDestroy(op->stream);
@@ -1087,8 +1251,13 @@ int fw_list_push_batch(fw_list* op, const int64_t* key, const int64_t* ts, const
 int fw_list_advance_watermark(fw_list* op, int64_t wm, int64_t* n_pending_rows) {
   if (!op) return FW_ERR_ARG;
   (void)hipSetDevice(op->device);
-  if (wm > op->wm) {  // HeapInternalTimerService.advanceWatermark: timers <= wm, in any order across lists
+  LRET(read_ctr(op));
+  if (wm > op->wm && wm < op->h_ctr->next_due) {
+    op->wm = wm;  // no timer is due
+  } else if (wm > op->wm) {  // HeapInternalTimerService.advanceWatermark: timers <= wm, in any order across lists
     op->wm = wm;
+    const long long none = LMAX;
+    LHIP(op, hipMemcpyAsync(&op->S.ctr->next_due, &none, 8, hipMemcpyHostToDevice, op->stream));
     LHIP(op, hipMemsetAsync(&op->S.ctr->nfire, 0, 16, op->stream));
     hipLaunchKernelGGL(k_lw_due, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, op->c, op->S, wm);
     LRET(read_ctr(op));
