@@ -61,13 +61,22 @@ struct LCounters {
   long long next_due;  // no group's trigger or cleanup timer is earlier: a watermark below it has nothing to do
 };
 
+struct alignas(32) GSlot {
+  uint32_t st;    // G_EMPTY / G_BUSY / G_LIVE / G_TOMB
+  uint32_t fl;    // GF_* flags
+  int32_t kg;     // key group
+  int32_t cnt;    // CountTrigger's count
+  int64_t key, start;
+};
+
+struct alignas(32) LPay {
+  int64_t ts, val, ord, pad;
+};
+
 struct LState {
-  uint32_t* gst;
-  int64_t *gkey, *gstart, *gcnt;
-  uint32_t* gfl;
-  int32_t* gkg;
+  GSlot* g;  // the group map: one 32-byte slot per group (a lookup reads one sector)
   uint32_t gmask;
-  int64_t *lts, *lval, *lord;
+  LPay* lpay;  // the elements' payload, one 32-byte sector each (a gather reads one sector per element)
   int32_t* lgid;
   int64_t *rkey, *rstart, *rend, *rcnt, *rsum, *rmin, *rmax, *rfirst, *roff;
   int64_t *ets, *eval, *eord;
@@ -130,10 +139,10 @@ __device__ int32_t g_find_insert(const LState& S, int64_t key, int64_t start, in
                                  unsigned* ins) {
   uint32_t s = g_hash(key, start) & S.gmask;
   for (uint32_t probes = 0; probes <= S.gmask;) {
-    const uint32_t cur = __hip_atomic_load(&S.gst[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t cur = __hip_atomic_load(&S.g[s].st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __atomic_signal_fence(__ATOMIC_ACQUIRE);  // (the compiler keeps the key loads behind it)
     if (cur == G_LIVE) {
-      if (ld_l2(&S.gkey[s]) == key && ld_l2(&S.gstart[s]) == start) return (int32_t)s;
+      if (ld_l2(&S.g[s].key) == key && ld_l2(&S.g[s].start) == start) return (int32_t)s;
     } else if (cur == G_BUSY) {
       continue;  // being published by another lane: read it again
     } else if (cur == G_EMPTY) {
@@ -141,13 +150,13 @@ __device__ int32_t g_find_insert(const LState& S, int64_t key, int64_t start, in
         atomicOr(&S.ctr->flags, LF_MAP_FULL);
         return -1;
       }
-      if (atomicCAS(&S.gst[s], G_EMPTY, G_BUSY) == G_EMPTY) {
-        S.gkey[s] = key;
-        S.gstart[s] = start;
-        S.gkg[s] = kg;
-        S.gcnt[s] = 0;
-        S.gfl[s] = 0;
-        __hip_atomic_store(&S.gst[s], G_LIVE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (atomicCAS(&S.g[s].st, G_EMPTY, G_BUSY) == G_EMPTY) {
+        S.g[s].key = key;
+        S.g[s].start = start;
+        S.g[s].kg = kg;
+        S.g[s].cnt = 0;
+        S.g[s].fl = 0;
+        __hip_atomic_store(&S.g[s].st, G_LIVE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         (*ins)++;
         return (int32_t)s;
       }
@@ -158,10 +167,6 @@ __device__ int32_t g_find_insert(const LState& S, int64_t key, int64_t start, in
   }
   atomicOr(&S.ctr->flags, LF_MAP_FULL);
   return -1;
-}
-__device__ __forceinline__ uint64_t lanemask_lt64() {
-  const int lane = __lane_id();
-  return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 // per-workgroup minimum into a global one
 __device__ __forceinline__ void block_min(long long* dst, long long v) {
@@ -237,9 +242,7 @@ __global__ __launch_bounds__(256) void k_lp_append(LCfg c, LState S, const int64
       const int64_t mts = w_max_ts(c, s), cl = w_cleanup(c, s);
       due = min(due, (long long)(c.trigger == FW_TRIGGER_EVENT_TIME && mts > wm ? mts : cl));
       const int32_t g = g_find_insert(S, k, s, kg, limit, &ins);
-      S.lts[idx] = t;
-      S.lval[idx] = v;
-      S.lord[idx] = ord_base + i;
+      S.lpay[idx] = LPay{t, v, ord_base + i, 0};
       S.lgid[idx] = g;
       idx++;
       if (g < 0) {
@@ -247,10 +250,10 @@ __global__ __launch_bounds__(256) void k_lp_append(LCfg c, LState S, const int64
         return;
       }
       if (c.trigger == FW_TRIGGER_COUNT || w_max_ts(c, s) <= wm) {  // CountTrigger / late firing
-        atomicOr(&S.gfl[g], GF_TOUCH);
+        atomicOr(&S.g[g].fl, GF_TOUCH);
         S.ctr->need_seq = 1u;
       } else {  // EventTimeTrigger.onElement registers the timer at maxTimestamp
-        if (!(S.gfl[g] & GF_TIMER)) atomicOr(&S.gfl[g], GF_TIMER);
+        if (!(S.g[g].fl & GF_TIMER)) atomicOr(&S.g[g].fl, GF_TIMER);
       }
     });
   }
@@ -262,7 +265,7 @@ __global__ __launch_bounds__(256) void k_lp_append(LCfg c, LState S, const int64
 __global__ __launch_bounds__(256) void k_sel_flags(const LState S, int64_t n, uint32_t bit, uint8_t* __restrict__ f) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t g = S.lgid[i];
-    f[i] = g >= 0 && (S.gfl[g] & bit) ? 1 : 0;
+    f[i] = g >= 0 && (S.g[g].fl & bit) ? 1 : 0;
   }
 }
 __global__ __launch_bounds__(256) void k_sel_keys(const LState S, const uint32_t* __restrict__ idx, int64_t m,
@@ -410,9 +413,9 @@ __device__ bool emit_firing(const LCfg& c, const LState& S, const LView& V, uint
     k++;
   }
   const unsigned long long r = atomicAdd(&S.ctr->rows, 1ull);
-  S.rkey[r] = S.gkey[g];
-  S.rstart[r] = S.gstart[g];
-  S.rend[r] = w_end(c, S.gstart[g]);
+  S.rkey[r] = S.g[g].key;
+  S.rstart[r] = S.g[g].start;
+  S.rend[r] = w_end(c, S.g[g].start);
   S.rcnt[r] = k;
   if (fl) {
     S.rsum[r] = __double_as_longlong(ds);
@@ -445,9 +448,10 @@ __global__ __launch_bounds__(256) void k_gather_sel(LState S, const uint32_t* __
                                                     int64_t* __restrict__ ord, uint8_t* __restrict__ alive) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t e = pos[i];
-    ts[i] = S.lts[e];
-    val[i] = S.lval[e];
-    ord[i] = S.lord[e];
+    const LPay p = S.lpay[e];
+    ts[i] = p.ts;
+    val[i] = p.val;
+    ord[i] = p.ord;
     alive[i] = 1;  // selected entries are live
   }
 }
@@ -466,22 +470,22 @@ __global__ __launch_bounds__(256) void k_walk(LCfg c, LState S, LView V, const u
     const int64_t a = seg[s], b = seg[s + 1];
     const uint32_t g = keys[a];
     if (!PUSH) {
-      if (!(S.gfl[g] & GF_FIRE)) continue;
+      if (!(S.g[g].fl & GF_FIRE)) continue;
       if (!emit_firing(c, S, V, g, a, b - 1, room)) continue;
       if (c.purging) purge(S, V, a, b - 1);
-      atomicAnd(&S.gfl[g], ~GF_FIRE);
+      atomicAnd(&S.g[g].fl, ~GF_FIRE);
       continue;
     }
-    if (!(S.gfl[g] & GF_TOUCH)) continue;
+    if (!(S.g[g].fl & GF_TOUCH)) continue;
     int64_t j = prog[s] >= 0 ? prog[s] : a;
     while (j < b && (int64_t)pos[j] < base_new) j++;
-    const int64_t mts = w_max_ts(c, S.gstart[g]);
+    const int64_t mts = w_max_ts(c, S.g[g].start);
     bool stopped = false;
     for (; j < b; j++) {
       bool fire;
       int64_t nc = 0;
       if (c.trigger == FW_TRIGGER_COUNT) {
-        nc = S.gcnt[g] + 1;
+        nc = S.g[g].cnt + 1;
         fire = nc >= c.trig_n;
       } else {
         fire = mts <= wm;
@@ -494,9 +498,9 @@ __global__ __launch_bounds__(256) void k_walk(LCfg c, LState S, LView V, const u
         }
         if (c.purging) purge(S, V, a, j);
       }
-      if (c.trigger == FW_TRIGGER_COUNT) S.gcnt[g] = fire ? 0 : nc;
+      if (c.trigger == FW_TRIGGER_COUNT) S.g[g].cnt = fire ? 0 : nc;
     }
-    if (!stopped) atomicAnd(&S.gfl[g], ~GF_TOUCH);
+    if (!stopped) atomicAnd(&S.g[g].fl, ~GF_TOUCH);
   }
 }
 
@@ -516,77 +520,66 @@ __global__ __launch_bounds__(256) void k_walk_bound(LCfg c, LState S, const uint
     }
     int64_t nn = 0;
     for (int64_t q = a; q < b; q++) nn += (int64_t)pos[q] >= base_new;
-    const int64_t f = c.trigger == FW_TRIGGER_COUNT ? (S.gcnt[keys[a]] + nn) / max<int64_t>(1, c.trig_n) : nn;
+    const int64_t f = c.trigger == FW_TRIGGER_COUNT ? (S.g[keys[a]].cnt + nn) / max<int64_t>(1, c.trig_n) : nn;
     tot += (unsigned long long)(f * (b - a));
   }
   if (tot) atomicAdd(&S.ctr->count, tot);
 }
 
-// The watermark walk of the common apply shape (no evictor, an integer field, the element buffer sized): one wave per
-// due list, its elements read and emitted 64 at a time (coalesced) and the reduce done across the wave (integer sums
-// wrap the same in any order).  Other shapes take k_walk<false>.
-__global__ __launch_bounds__(256) void k_walk_wm_wave(LCfg c, LState S, LView V, const uint32_t* __restrict__ keys,
-                                                      const uint32_t* __restrict__ seg, int64_t nseg) {
+// The watermark firing of the common apply shape (no evictor, an integer field, contents emitted): every selected
+// element is live and every list fires once over all of them, so list s's row is rows_base + s and its contents
+// are the elements' list-order positions [a, b) themselves — no reservations.  k_gather_emit writes the contents
+// (one 32-byte sector read per element, coalesced writes), then one wave per list reduces them (integer sums wrap
+// the same in any order) and writes its row.  Other shapes take k_walk<false>.
+__global__ __launch_bounds__(256) void k_gather_emit(LState S, const uint32_t* __restrict__ pos, int64_t m, int64_t ebase) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    const LPay p = S.lpay[pos[i]];
+    S.ets[ebase + i] = p.ts;
+    S.eval[ebase + i] = p.val;
+    S.eord[ebase + i] = p.ord;
+  }
+}
+__global__ __launch_bounds__(256) void k_walk_wm_fast(LCfg c, LState S, const uint32_t* __restrict__ pos,
+                                                      const uint32_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ seg, int64_t nseg, int64_t rbase,
+                                                      int64_t ebase) {
   const int lane = __lane_id();
   const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  unsigned long long killed = 0;
   for (int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; s < nseg; s += waves) {
     const int64_t a = seg[s], b = seg[s + 1];
     const uint32_t g = keys[a];
-    if (!(S.gfl[g] & GF_FIRE)) continue;
-    int64_t cnt = 0;
-    for (int64_t q0 = a; q0 < b; q0 += 64) cnt += __popcll(__ballot(q0 + lane < b && V.alive[q0 + lane]));
-    int64_t eoff = 0;
-    if (c.emit && cnt) {
-      if (lane == 0) eoff = (int64_t)atomicAdd(&S.ctr->elems, (unsigned long long)cnt);
-      eoff = __shfl(eoff, 0, 64);
-    }
-    int64_t is = 0, mn = LMAX, mx = LMIN, first = -1, k = 0, killed = 0;
-    for (int64_t q0 = a; q0 < b; q0 += 64) {
-      const int64_t q = q0 + lane;
-      const bool al = q < b && V.alive[q];
-      const uint64_t m = __ballot(al);
-      if (!m) continue;
-      if (first < 0) first = __shfl(al ? V.ord[q] : 0, __ffsll((long long)m) - 1, 64);
-      if (al) {
-        const int64_t v = V.val[q];
-        is = jadd(is, v);
-        mn = min(mn, v);
-        mx = max(mx, v);
-        if (c.emit) {
-          const int64_t o = eoff + k + __popcll(m & lanemask_lt64());
-          S.ets[o] = V.ts[q];
-          S.eval[o] = v;
-          S.eord[o] = V.ord[q];
-        }
-        if (c.purging) {
-          V.kill(q);
-          killed++;
-        }
+    int64_t is = 0, mn = LMAX, mx = LMIN;
+    for (int64_t q = a + lane; q < b; q += 64) {
+      const int64_t v = S.eval[ebase + q];
+      is = jadd(is, v);
+      mn = min(mn, v);
+      mx = max(mx, v);
+      if (c.purging) {
+        S.lgid[pos[q]] = -1;
+        killed++;
       }
-      k += __popcll(m);
     }
     for (int o = 32; o; o >>= 1) {  // the wave's reduce
       is = jadd(is, __shfl_xor(is, o, 64));
       mn = min(mn, __shfl_xor(mn, o, 64));
       mx = max(mx, __shfl_xor(mx, o, 64));
-      killed += __shfl_xor(killed, o, 64);
     }
     if (lane == 0) {
-      const unsigned long long r = atomicAdd(&S.ctr->rows, 1ull);
-      S.rkey[r] = S.gkey[g];
-      S.rstart[r] = S.gstart[g];
-      S.rend[r] = w_end(c, S.gstart[g]);
-      S.rcnt[r] = k;
+      const int64_t r = rbase + s;
+      S.rkey[r] = S.g[g].key;
+      S.rstart[r] = S.g[g].start;
+      S.rend[r] = w_end(c, S.g[g].start);
+      S.rcnt[r] = b - a;
       S.rsum[r] = c.vt == FW_VAL_I32 ? (int64_t)(int32_t)is : c.vt == FW_VAL_I16 ? (int64_t)(int16_t)is
                 : c.vt == FW_VAL_I8 ? (int64_t)(int8_t)is : is;
-      S.rmin[r] = k ? mn : 0;
-      S.rmax[r] = k ? mx : 0;
-      S.rfirst[r] = first;
-      S.roff[r] = c.emit ? eoff : 0;
-      if (killed) atomicAdd(&S.ctr->dead, (unsigned long long)killed);
-      atomicAnd(&S.gfl[g], ~GF_FIRE);
+      S.rmin[r] = mn;
+      S.rmax[r] = mx;
+      S.rfirst[r] = S.eord[ebase + a];
+      S.roff[r] = ebase + a;
     }
   }
+  block_add(&S.ctr->dead, killed);
 }
 
 // ---------------------------------------------------------------- watermark
@@ -595,9 +588,9 @@ __global__ __launch_bounds__(256) void k_lw_due(LCfg c, LState S, int64_t wm) {
   long long due = LMAX;  // the remaining groups' earliest timer
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)S.gmask;
        g += (int64_t)gridDim.x * blockDim.x) {
-    if (S.gst[g] != G_LIVE) continue;
-    const int64_t st = S.gstart[g];
-    const uint32_t f0 = S.gfl[g];
+    if (S.g[g].st != G_LIVE) continue;
+    const int64_t st = S.g[g].start;
+    const uint32_t f0 = S.g[g].fl;
     uint32_t f = f0;
     if ((f & GF_TIMER) && w_max_ts(c, st) <= wm) {  // the trigger timer fires (EventTimeTrigger.onEventTime)
       f = (f & ~GF_TIMER) | GF_FIRE;
@@ -610,7 +603,7 @@ __global__ __launch_bounds__(256) void k_lw_due(LCfg c, LState S, int64_t wm) {
     } else {
       due = min(due, (long long)((f & GF_TIMER) ? w_max_ts(c, st) : cl));
     }
-    if (f != f0) S.gfl[g] = f;
+    if (f != f0) S.g[g].fl = f;
   }
   block_min(&S.ctr->next_due, due);
   block_add(&S.ctr->nfire, nf);
@@ -621,7 +614,7 @@ __global__ __launch_bounds__(256) void k_lw_clean_log(LState S, int64_t n) {
   unsigned long long killed = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t g = S.lgid[i];
-    if (g >= 0 && (S.gfl[g] & GF_CLEAN)) {
+    if (g >= 0 && (S.g[g].fl & GF_CLEAN)) {
       S.lgid[i] = -1;
       killed++;
     }
@@ -632,13 +625,13 @@ __global__ __launch_bounds__(256) void k_lw_clean_map(LState S) {
   unsigned long long nt = 0;
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)S.gmask;
        g += (int64_t)gridDim.x * blockDim.x) {
-    if (S.gst[g] != G_LIVE) continue;
-    const uint32_t f = S.gfl[g];
+    if (S.g[g].st != G_LIVE) continue;
+    const uint32_t f = S.g[g].fl;
     if (f & GF_CLEAN) {
-      S.gst[g] = G_TOMB;
+      S.g[g].st = G_TOMB;
       nt++;
     } else if (f & GF_FIRE) {
-      S.gfl[g] = f & ~GF_FIRE;  // a due timer of an empty list: nothing to fire
+      S.g[g].fl = f & ~GF_FIRE;  // a due timer of an empty list: nothing to fire
     }
   }
   block_add(&S.ctr->tombs, nt);
@@ -652,15 +645,15 @@ __global__ __launch_bounds__(256) void k_rebuild_map(LCfg c, LState o, LState S,
   for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x; g0 <= (int64_t)o.gmask; g0 += stride) {
     const int64_t g = g0 + threadIdx.x;
     if (g > (int64_t)o.gmask) continue;
-    if (o.gst[g] != G_LIVE) {
+    if (o.g[g].st != G_LIVE) {
       remap[g] = -1;
       continue;
     }
-    const int32_t ng = g_find_insert(S, o.gkey[g], o.gstart[g], o.gkg[g], 0, &ins);
+    const int32_t ng = g_find_insert(S, o.g[g].key, o.g[g].start, o.g[g].kg, 0, &ins);
     remap[g] = ng;
     if (ng >= 0) {
-      S.gcnt[ng] = o.gcnt[g];
-      S.gfl[ng] = o.gfl[g];
+      S.g[ng].cnt = o.g[g].cnt;
+      S.g[ng].fl = o.g[g].fl;
     }
   }
   block_add(&S.ctr->live_groups, ins);
@@ -673,9 +666,7 @@ __global__ __launch_bounds__(256) void k_gather_log(LState o, LState S, const ui
                                                     const int32_t* __restrict__ remap) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t e = idx[i];
-    S.lts[i] = o.lts[e];
-    S.lval[i] = o.lval[e];
-    S.lord[i] = o.lord[e];
+    S.lpay[i] = o.lpay[e];
     S.lgid[i] = remap ? remap[o.lgid[e]] : o.lgid[e];
   }
 }
@@ -694,12 +685,12 @@ __global__ __launch_bounds__(256) void k_count_state(LCfg c, LState S, const uin
   unsigned long long lists = 0, timers = 0;
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)S.gmask;
        g += (int64_t)gridDim.x * blockDim.x) {
-    if (S.gst[g] != G_LIVE) continue;
+    if (S.g[g].st != G_LIVE) continue;
     lists += has[g];
-    const int64_t cl = w_cleanup(c, S.gstart[g]);
+    const int64_t cl = w_cleanup(c, S.g[g].start);
     const bool creg = event_time(c) && cl != LMAX;
     timers += creg ? 1 : 0;
-    if ((S.gfl[g] & GF_TIMER) && !(creg && cl == w_max_ts(c, S.gstart[g]))) timers++;
+    if ((S.g[g].fl & GF_TIMER) && !(creg && cl == w_max_ts(c, S.g[g].start))) timers++;
   }
   if (lists) atomicAdd(&out2[0], lists);
   if (timers) atomicAdd(&out2[1], timers);
@@ -707,13 +698,13 @@ __global__ __launch_bounds__(256) void k_count_state(LCfg c, LState S, const uin
 __global__ __launch_bounds__(256) void k_kg_flags_log(LState S, int64_t n, int32_t kg, uint8_t* __restrict__ f) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t g = S.lgid[i];
-    f[i] = g >= 0 && S.gkg[g] == kg;
+    f[i] = g >= 0 && S.g[g].kg == kg;
   }
 }
 __global__ __launch_bounds__(256) void k_kg_flags_map(LState S, int32_t kg, uint8_t* __restrict__ f) {
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)S.gmask;
        g += (int64_t)gridDim.x * blockDim.x)
-    f[g] = S.gst[g] == G_LIVE && S.gkg[g] == kg;
+    f[g] = S.g[g].st == G_LIVE && S.g[g].kg == kg;
 }
 // restore: one thread inserts the lists in order (their count and timer flag), then the elements are appended
 __global__ void k_restore_groups(LCfg c, LState S, const int64_t* __restrict__ key, const int64_t* __restrict__ start,
@@ -725,8 +716,8 @@ __global__ void k_restore_groups(LCfg c, LState S, const int64_t* __restrict__ k
     if (ins) atomicAdd(&S.ctr->live_groups, 1ull);  // (one thread)
     gid_out[i] = g;
     if (g < 0) continue;
-    S.gcnt[g] = cnt[i];
-    if (timer[i]) atomicOr(&S.gfl[g], GF_TIMER);
+    S.g[g].cnt = cnt[i];
+    if (timer[i]) atomicOr(&S.g[g].fl, GF_TIMER);
     atomicMin(&S.ctr->next_due, (long long)(timer[i] ? w_max_ts(c, start[i]) : w_cleanup(c, start[i])));
   }
 }
@@ -734,9 +725,7 @@ __global__ __launch_bounds__(256) void k_restore_elems(LState S, const int64_t* 
                                                        const int64_t* __restrict__ val, const int64_t* __restrict__ ord,
                                                        const int32_t* __restrict__ gid, int64_t n, int64_t base) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    S.lts[base + i] = ts[i];
-    S.lval[base + i] = val[i];
-    S.lord[base + i] = ord[i];
+    S.lpay[base + i] = LPay{ts[i], val[i], ord[i], 0};
     S.lgid[base + i] = gid[i];
   }
 }
@@ -815,35 +804,21 @@ int ensure_tmp(fw_list* op, size_t bytes) {
   return FW_OK;
 }
 int alloc_map(fw_list* op, LState& S, int64_t cap) {
-  LHIP(op, dmalloc(&S.gst, (size_t)cap));
-  LHIP(op, dmalloc(&S.gkey, (size_t)cap));
-  LHIP(op, dmalloc(&S.gstart, (size_t)cap));
-  LHIP(op, dmalloc(&S.gcnt, (size_t)cap));
-  LHIP(op, dmalloc(&S.gfl, (size_t)cap));
-  LHIP(op, dmalloc(&S.gkg, (size_t)cap));
-  LHIP(op, hipMemsetAsync(S.gst, 0, (size_t)cap * sizeof(uint32_t), op->stream));
+  LHIP(op, dmalloc(&S.g, (size_t)cap));
+  LHIP(op, hipMemsetAsync(S.g, 0, (size_t)cap * sizeof(GSlot), op->stream));  // G_EMPTY
   S.gmask = (uint32_t)(cap - 1);
   return FW_OK;
 }
 void free_map(LState& S) {
-  dfree(S.gst);
-  dfree(S.gkey);
-  dfree(S.gstart);
-  dfree(S.gcnt);
-  dfree(S.gfl);
-  dfree(S.gkg);
+  dfree(S.g);
 }
 int alloc_log(fw_list* op, LState& S, int64_t cap) {
-  LHIP(op, dmalloc(&S.lts, (size_t)cap));
-  LHIP(op, dmalloc(&S.lval, (size_t)cap));
-  LHIP(op, dmalloc(&S.lord, (size_t)cap));
+  LHIP(op, dmalloc(&S.lpay, (size_t)cap));
   LHIP(op, dmalloc(&S.lgid, (size_t)cap));
   return FW_OK;
 }
 void free_log(LState& S) {
-  dfree(S.lts);
-  dfree(S.lval);
-  dfree(S.lord);
+  dfree(S.lpay);
   dfree(S.lgid);
 }
 int ensure_sel(fw_list* op, int64_t n) {
@@ -953,9 +928,7 @@ int walk_lists(fw_list* op, uint32_t bit, int64_t base_new) {
   const uint32_t mm = (uint32_t)m;
   LHIP(op, hipMemcpyAsync(op->seg + nseg, &mm, 4, hipMemcpyHostToDevice, op->stream));
   LHIP(op, hipMemsetAsync(op->prog, 0xff, (size_t)nseg * 8, op->stream));
-  hipLaunchKernelGGL(k_gather_sel, dim3(grid_for(m)), dim3(256), 0, op->stream, op->S, op->sel2, m, op->gts, op->gval,
-                     op->gord, op->galive);
-  const LView V{op->sel2, op->gts, op->gval, op->gord, op->galive, op->S.lgid};
+
   // with room for every possible firing the walk reserves elements with plain atomics; else (a bound beyond
   // FW_LIST_ROOM elements) it reserves with compare-and-swap and stops where the buffer is full
   bool room = !op->c.emit;
@@ -971,12 +944,20 @@ int walk_lists(fw_list* op, uint32_t bit, int64_t base_new) {
     }
   }
   const bool fl = op->c.vt == FW_VAL_F64 || op->c.vt == FW_VAL_F32;
-  if (!PUSH && room && op->c.evictor == FW_EVICT_NONE && !fl) {  // the common apply shape: a wave per list
-    hipLaunchKernelGGL(k_walk_wm_wave, dim3((unsigned)std::min<int64_t>(16384, (nseg + 3) / 4)), dim3(256), 0,
-                       op->stream, op->c, op->S, V, op->keys2, op->seg, nseg);
+  if (!PUSH && room && op->c.emit && op->c.evictor == FW_EVICT_NONE && !fl) {  // the common apply shape
+    LRET(read_ctr(op));
+    const int64_t rbase = (int64_t)op->h_ctr->rows, ebase = (int64_t)op->h_ctr->elems;
+    hipLaunchKernelGGL(k_gather_emit, dim3(grid_for(m)), dim3(256), 0, op->stream, op->S, op->sel2, m, ebase);
+    hipLaunchKernelGGL(k_walk_wm_fast, dim3((unsigned)std::min<int64_t>(16384, (nseg + 3) / 4)), dim3(256), 0,
+                       op->stream, op->c, op->S, op->sel2, op->keys2, op->seg, nseg, rbase, ebase);
     LHIP(op, hipGetLastError());
-    return FW_OK;
+    const unsigned long long re[2] = {(unsigned long long)(rbase + nseg), (unsigned long long)(ebase + m)};
+    LHIP(op, hipMemcpyAsync(&op->S.ctr->rows, re, 16, hipMemcpyHostToDevice, op->stream));  // rows, elems
+    return read_ctr(op);
   }
+  hipLaunchKernelGGL(k_gather_sel, dim3(grid_for(m)), dim3(256), 0, op->stream, op->S, op->sel2, m, op->gts, op->gval,
+                     op->gord, op->galive);
+  const LView V{op->sel2, op->gts, op->gval, op->gord, op->galive, op->S.lgid};
   for (int round = 0;; round++) {
     LHIP(op, hipMemsetAsync(&op->S.ctr->flags, 0, 4, op->stream));
     hipLaunchKernelGGL(k_walk<PUSH>, dim3(grid_for(nseg)), dim3(256), 0, op->stream, op->c, op->S, V, op->keys2,
@@ -1035,16 +1016,13 @@ int grow_log(fw_list* op, int64_t extra) {
   LState L = op->S;
   LRET(alloc_log(op, L, cap));
   if (op->n_log) {
-    LHIP(op, hipMemcpyAsync(L.lts, op->S.lts, (size_t)op->n_log * 8, hipMemcpyDeviceToDevice, op->stream));
-    LHIP(op, hipMemcpyAsync(L.lval, op->S.lval, (size_t)op->n_log * 8, hipMemcpyDeviceToDevice, op->stream));
-    LHIP(op, hipMemcpyAsync(L.lord, op->S.lord, (size_t)op->n_log * 8, hipMemcpyDeviceToDevice, op->stream));
+    LHIP(op, hipMemcpyAsync(L.lpay, op->S.lpay, (size_t)op->n_log * sizeof(LPay), hipMemcpyDeviceToDevice,
+                            op->stream));
     LHIP(op, hipMemcpyAsync(L.lgid, op->S.lgid, (size_t)op->n_log * 4, hipMemcpyDeviceToDevice, op->stream));
   }
   LHIP(op, hipStreamSynchronize(op->stream));
   free_log(op->S);
-  op->S.lts = L.lts;
-  op->S.lval = L.lval;
-  op->S.lord = L.lord;
+  op->S.lpay = L.lpay;
   op->S.lgid = L.lgid;
   op->lcap = cap;
   op->grows++;
@@ -1137,7 +1115,8 @@ int fw_list_create(const fw_list_config* cfg, fw_list** out) {
     return fail(FW_ERR_ARG, "SlidingEventTimeWindows parameters must satisfy 0 <= offset < slide <= size");
   if (c.allowed_lateness < 0) return fail(FW_ERR_ARG, "The allowed lateness cannot be negative.");
   if (c.trigger != FW_TRIGGER_EVENT_TIME && c.trigger != FW_TRIGGER_COUNT) return fail(FW_ERR_ARG, "unknown trigger");
-  if (c.trigger == FW_TRIGGER_COUNT && c.trigger_count <= 0) return fail(FW_ERR_ARG, "CountTrigger count must be > 0");
+  if (c.trigger == FW_TRIGGER_COUNT && (c.trigger_count <= 0 || c.trigger_count > INT32_MAX))
+    return fail(FW_ERR_ARG, "CountTrigger count must be in [1, 2^31)");
   if (c.evictor < FW_EVICT_NONE || c.evictor > FW_EVICT_DELTA) return fail(FW_ERR_ARG, "unknown evictor");
   if (c.evictor == FW_EVICT_COUNT && c.evict_count < 0) return fail(FW_ERR_ARG, "CountEvictor count must be >= 0");
   if (c.value_type < FW_VAL_I64 || c.value_type > FW_VAL_F32) return fail(FW_ERR_ARG, "unknown value type");
@@ -1157,8 +1136,8 @@ int fw_list_create(const fw_list_config* cfg, fw_list** out) {
   const int64_t fan = c.assigner == FW_SLIDING ? (c.size + c.slide - 1) / c.slide : 1;
   const int64_t exp = c.expected_elements > 0 ? c.expected_elements : std::min<int64_t>(op->max_batch * fan, 1 << 22);
   op->lcap = std::max<int64_t>(exp, 1024);
-  int64_t g = 1024;  // groups: the map grows with them (k_lp_append)
-  while (g < 2 * std::min<int64_t>(op->lcap, 1 << 22)) g <<= 1;
+  int64_t g = 1024;  // groups: the map doubles when a push would pass 3/4 load (k_lp_append), so it stays the
+  while (g < 2 * std::min<int64_t>(op->lcap, 1 << 20)) g <<= 1;  // smallest that holds them (MALL-resident slots)
   op->gcap = g;
   op->rcap = 1024;
   op->scap = 1024;
@@ -1402,15 +1381,10 @@ int fw_list_snapshot_key_group(fw_list* op, int32_t key_group, const fw_list_sta
   if (m) LHIP(op, hipMemcpyAsync(pos.data(), op->sel, (size_t)m * 4, hipMemcpyDeviceToHost, op->stream));
   LHIP(op, hipStreamSynchronize(op->stream));
   // host gathers (a snapshot is a cold path): group columns, then the elements per list in log order
-  auto fetch64 = [&](const int64_t* d, int64_t i, int64_t* v) {
-    return hipMemcpy(v, d + i, 8, hipMemcpyDeviceToHost);
-  };
-  std::vector<int64_t> lts(op->n_log), lval(op->n_log), lord(op->n_log);
+  std::vector<LPay> lpay(op->n_log);
   std::vector<int32_t> lgid(op->n_log);
   if (op->n_log) {
-    LHIP(op, hipMemcpy(lts.data(), op->S.lts, (size_t)op->n_log * 8, hipMemcpyDeviceToHost));
-    LHIP(op, hipMemcpy(lval.data(), op->S.lval, (size_t)op->n_log * 8, hipMemcpyDeviceToHost));
-    LHIP(op, hipMemcpy(lord.data(), op->S.lord, (size_t)op->n_log * 8, hipMemcpyDeviceToHost));
+    LHIP(op, hipMemcpy(lpay.data(), op->S.lpay, (size_t)op->n_log * sizeof(LPay), hipMemcpyDeviceToHost));
     LHIP(op, hipMemcpy(lgid.data(), op->S.lgid, (size_t)op->n_log * 4, hipMemcpyDeviceToHost));
   }
   std::vector<int64_t> rank(op->gcap, -1);
@@ -1422,18 +1396,16 @@ int fw_list_snapshot_key_group(fw_list* op, int32_t key_group, const fw_list_sta
   for (int64_t i = 0; i < m; i++) {
     const uint32_t e = pos[i];
     const int64_t k = fill[rank[lgid[e]]]++;
-    if (dst->ts) dst->ts[k] = lts[e];
-    if (dst->val) dst->val[k] = lval[e];
-    if (dst->ordinal) dst->ordinal[k] = lord[e];
+    if (dst->ts) dst->ts[k] = lpay[e].ts;
+    if (dst->val) dst->val[k] = lpay[e].val;
+    if (dst->ordinal) dst->ordinal[k] = lpay[e].ord;
   }
   for (int64_t i = 0; i < ng; i++) {
     const uint32_t g = gids[i];
-    int64_t key, start, c;
-    uint32_t fl;
-    LHIP(op, fetch64(op->S.gkey, g, &key));
-    LHIP(op, fetch64(op->S.gstart, g, &start));
-    LHIP(op, fetch64(op->S.gcnt, g, &c));
-    LHIP(op, hipMemcpy(&fl, op->S.gfl + g, 4, hipMemcpyDeviceToHost));
+    GSlot gs;
+    LHIP(op, hipMemcpy(&gs, op->S.g + g, sizeof gs, hipMemcpyDeviceToHost));
+    const int64_t key = gs.key, start = gs.start, c = gs.cnt;
+    const uint32_t fl = gs.fl;
     dst->key[i] = key;
     dst->start[i] = start;
     dst->end[i] = op->c.assigner == FW_GLOBAL ? LMAX : (int64_t)((uint64_t)start + (uint64_t)op->c.size);

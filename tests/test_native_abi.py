@@ -116,7 +116,7 @@ def _list_create(**kw):
     (dict(assigner=N.FW_TUMBLING, size=100, offset=100), "TumblingEventTimeWindows parameters must satisfy"),
     (dict(assigner=N.FW_SLIDING, size=100, slide=200), "SlidingEventTimeWindows parameters must satisfy"),
     (dict(assigner=N.FW_TUMBLING, size=10, allowed_lateness=-1), "The allowed lateness cannot be negative"),
-    (dict(assigner=N.FW_GLOBAL, trigger=N.FW_TRIGGER_COUNT, trigger_count=0), "CountTrigger count must be > 0"),
+    (dict(assigner=N.FW_GLOBAL, trigger=N.FW_TRIGGER_COUNT, trigger_count=0), "CountTrigger count must be in [1, 2^31)"),
     (dict(assigner=N.FW_GLOBAL, evictor=N.FW_EVICT_COUNT, evict_count=-1), "CountEvictor count must be >= 0"),
     (dict(assigner=N.FW_TUMBLING, size=10, key_group_start=5, key_group_end=200), "invalid KeyGroupRange"),
 ])
