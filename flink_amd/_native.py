@@ -136,6 +136,11 @@ SIGNATURES = {
     "fw_keyby_combine_push_device": (ctypes.c_int, [VP, VP, VP, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, I64P]),
     "fw_snapshot_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), ctypes.c_int64, I64P]),
     "fw_restore_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), ctypes.c_int64]),
+    "fw_state_block_bytes": (ctypes.c_int64, [VP]),
+    "fw_snapshot_key_group_blocks": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), VP,
+                                                    ctypes.c_int64, I64P]),
+    "fw_restore_key_group_blocks": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), VP,
+                                                   ctypes.c_int64]),
     "fw_key_groups_device": (ctypes.c_int, [VP, VP, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, VP, VP]),
     "fw_route_device": (ctypes.c_int, [VP, VP, VP, VP, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
                                        ctypes.c_int32, VP, VP, VP, VP, VP, VP, ctypes.c_int64, VP]),

@@ -4236,9 +4236,97 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_snapshot(DevCfg c, DevTable
       if (agg_by(c.agg)) by_row(c.agg, c.vtype, e, &out.mn[o], &out.mx[o]);
       // a pane's timer: the maxTimestamp of its next window to form
       out.timer[o] = c.panes ? max(e.meta, tb.pane_floor[p]) : (e.meta & FW_TIMER) ? 1 : 0;
+      if (out.blk) out.blk[o] = (int64_t)pool_block_of(e);  // exported by k_block_export
     }
     __syncthreads();
   }
+}
+
+// ---- accumulator blocks of the pool aggregates in their snapshot form (flink_window.h, fw_state_block_bytes).
+// One wave per row.  HyperLogLog: the 2^p registers (an unmarked chunk is all zero, so they are copied whole);
+// t-digest: n, then (sum bits, weight) of the live half's centroids, zero-padded.
+__global__ __launch_bounds__(256) void k_block_export(DevCfg c, const int64_t* __restrict__ blk, int64_t n,
+                                                      uint8_t* __restrict__ acc) {
+  const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = __lane_id();
+  if (row >= n) return;
+  const uint64_t b = (uint64_t)blk[row];
+  if (c.agg == FW_AGG_HLL) {
+    const int32_t nq = (int32_t)(((int64_t)1 << c.hll_p) / 16);
+    const uint4* q = reinterpret_cast<const uint4*>(c.pool + b * (uint64_t)c.pool_bytes + hll_hdr_bytes(c.hll_p));
+    uint4* d = reinterpret_cast<uint4*>(acc + row * (int64_t)nq * 16);
+    for (int32_t j = lane; j < nq; j += 64) d[j] = q[j];
+  } else {
+    const TdHead h = *td_head(c, b);
+    const TdCent* ce = td_half(c, b, h.cur);
+    const int32_t nw = 1 + 2 * c.td_nb;
+    int64_t* d = reinterpret_cast<int64_t*>(acc) + row * (int64_t)nw;
+    for (int32_t j = lane; j < nw; j += 64) {
+      const int32_t k = (j - 1) >> 1;
+      d[j] = j == 0 ? (int64_t)h.n : k >= h.n ? 0 : (j & 1) ? __double_as_longlong(ce[k].sum) : td_weight(ce, k);
+    }
+  }
+}
+__device__ __forceinline__ uint32_t bytes_max(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) r |= max((a >> k) & 0xffu, (b >> k) & 0xffu) << k;
+  return r;
+}
+// a digest restores only with at most delta/2 centroids of weight >= 1 (registers: any bytes)
+__device__ bool acc_valid(const DevCfg& c, const uint8_t* src) {
+  if (c.agg == FW_AGG_HLL) return true;
+  const int64_t* s = reinterpret_cast<const int64_t*>(src);
+  if (s[0] < 0 || s[0] > c.td_nb) return false;
+  for (int32_t k = 0; k < (int32_t)s[0]; k++)
+    if (s[2 + 2 * k] < 1) return false;
+  return true;
+}
+// one thread: a row's accumulator into block b (merge: HyperLogLog register max into a live block)
+__device__ void block_import(const DevCfg& c, uint64_t b, const uint8_t* src, bool merge) {
+  uint8_t* base = c.pool + b * (uint64_t)c.pool_bytes;
+  if (c.agg == FW_AGG_HLL) {
+    const int32_t nq = (int32_t)(((int64_t)1 << c.hll_p) / 16), nw = (nq + 31) / 32;
+    uint32_t* bits = reinterpret_cast<uint32_t*>(base);
+    uint4* q = reinterpret_cast<uint4*>(base + hll_hdr_bytes(c.hll_p));
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    for (int32_t w = 0; w < nw; w++) {
+      uint32_t word = merge ? bits[w] : 0u;
+      for (int32_t j = w * 32; j < min(nq, w * 32 + 32); j++) {
+        uint4 v = s[j];
+        if (merge) {
+          const uint4 o = q[j];
+          v.x = bytes_max(v.x, o.x);
+          v.y = bytes_max(v.y, o.y);
+          v.z = bytes_max(v.z, o.z);
+          v.w = bytes_max(v.w, o.w);
+        }
+        q[j] = v;
+        if (v.x | v.y | v.z | v.w) word |= 1u << (j & 31);
+      }
+      bits[w] = word;
+    }
+    return;
+  }
+  const int64_t* s = reinterpret_cast<const int64_t*>(src);
+  const int32_t nc = (int32_t)s[0];
+  TdCent* ce = td_half(c, b, 0);
+  int64_t cum = 0;
+  for (int32_t k = 0; k < nc; k++) {
+    cum += s[2 + 2 * k];
+    ce[k] = TdCent{__longlong_as_double(s[1 + 2 * k]), cum};
+  }
+  *td_head(c, b) = TdHead{0, nc, cum};
+}
+// free-stack blocks and fresh blocks for a restore (the host took them off the counters)
+__global__ void k_pool_take(DevCfg c, int32_t h, int32_t take, int64_t bump, int64_t n, int64_t* ids) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) ids[i] = i < take ? (int64_t)c.pool_free[h - take + i] : bump + (i - take);
+}
+// blocks a restore did not use, back on the free stack (untouched: still zero for HyperLogLog)
+__global__ void k_pool_give(DevCfg c, const int64_t* ids, int64_t n, int32_t h) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) c.pool_free[h + i] = (uint32_t)ids[i];
 }
 
 // partition of a restored row of key group kg (the caller vouches for hashed keys); -1 when a
@@ -4284,14 +4372,31 @@ __global__ void k_restore(DevCfg c, int32_t kg, StateCols in, int64_t n, DevTabl
   const Region r = region_of(c, tb, p, tb.cur[p]);
   const uint64_t h = slot_hash(c, d.key, c.assigner == FW_SESSION ? 0 : d.start);
   const int32_t found = region_find(r, h, d.key, d.start, d.end);
+  const uint8_t* acc = in.acc ? in.acc + i * in.acc_bytes : nullptr;
   if (found >= 0) {  // the window is already there (restored earlier, or an earlier round): AggregateFunction.merge
     Entry& x = r.ent[found];
     Entry cur = x;
+    if (c.pool_bytes) {  // register max into its block; a digest is not re-compressed here
+      if (c.agg != FW_AGG_HLL) {
+        atomicAdd(&st->acc_refused, 1);
+        return;
+      }
+      block_import(c, pool_block_of(cur), acc, true);
+    }
     acc_merge(c, cur, d);
     cur.meta = c.panes ? min(cur.meta, d.meta) : (cur.meta | d.meta);
     x = cur;
     atomicMin((long long*)&tb.next_timer[p], (long long)entry_timer(c, cur));
     return;
+  }
+  if (c.pool_bytes) {
+    if (!acc_valid(c, acc)) {
+      atomicAdd(&st->acc_refused, 1);
+      return;
+    }
+    const uint64_t b = (uint64_t)in.blk[atomicAdd(in.used, 1)];
+    block_import(c, b, acc, false);
+    d.meta |= (int64_t)(b << 1);
   }
   const int32_t s = region_claim(r, h, SLOT_BUSY);
   if (s < 0) {
@@ -5676,6 +5781,15 @@ void launch_rehash(const DevCfg& oc, DevTable ot, const DevCfg& nc, DevTable nt,
 void launch_snapshot(const DevCfg& c, DevTable tb, int32_t p0, int32_t np, StateCols out, unsigned long long* count,
                      hipStream_t s) {
   hipLaunchKernelGGL(k_snapshot, dim3(np), dim3(FW_FIRE_THREADS), 0, s, c, tb, p0, out, count);
+}
+void launch_block_export(const DevCfg& c, const int64_t* blk, int64_t n, uint8_t* acc, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_block_export, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, c, blk, n, acc);
+}
+void launch_pool_take(const DevCfg& c, int32_t h, int32_t take, int64_t bump, int64_t n, int64_t* ids, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_pool_take, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c, h, take, bump, n, ids);
+}
+void launch_pool_give(const DevCfg& c, const int64_t* ids, int64_t n, int32_t h, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_pool_give, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c, ids, n, h);
 }
 void launch_restore(const DevCfg& c, int32_t kg, StateCols in, int64_t n, int32_t* demand, DevTable tb, Status* st,
                     const int32_t* round_of, int32_t rounds, hipStream_t s) {

@@ -228,6 +228,7 @@ struct Status {
   int32_t need_grow;                  // some region is over half full: grow before it has to suspend
   int32_t taint_any;                  // sessions: 0 no tainted key in the batch, 1 check the set, 2 set full: all
   int32_t rsv_fallbacks;              // single-pass batches that had to go through classify / scan / scatter
+  int32_t acc_refused;                // restore: t-digest rows of a window already present, malformed digests
 };
 enum {
   FW_STATUS_STATE_LOST = 1,  // a window could not be stored (more in-flight sessions of one key than supported)
@@ -342,6 +343,12 @@ struct DevCount {
 // columns of keyed-state snapshot rows (fw_state_rows, device side)
 struct StateCols {
   int64_t *key, *start, *end, *cnt, *sum, *mn, *mx, *timer;
+  // block-pool aggregates (DevCfg::pool_bytes): a snapshot writes each row's block id into blk; a restore
+  // hands blk[(*used)++] to each new (key, window) and imports row i's accumulator from acc + i * acc_bytes
+  int64_t* blk;
+  const uint8_t* acc;
+  int64_t acc_bytes;
+  int32_t* used;
 };
 struct DevSide {
   int64_t *key, *ts, *val;
@@ -427,6 +434,9 @@ void launch_pmerge(const DevCfg& c, const PartialRec* part, const uint32_t* offs
 // `hist` ((P + 1) x T, scanned in place)), merged by launch_pmerge
 void launch_dt_restore_runs(const DevCfg& c, int32_t kg, StateCols in, int64_t n, int32_t* rp, uint32_t* hist,
                             uint32_t* scan_tmp, PartialRec* tmp, PartialRec* part, Status* st, hipStream_t_ s);
+void launch_block_export(const DevCfg& c, const int64_t* blk, int64_t n, uint8_t* acc, hipStream_t_ s);
+void launch_pool_take(const DevCfg& c, int32_t h, int32_t take, int64_t bump, int64_t n, int64_t* ids, hipStream_t_ s);
+void launch_pool_give(const DevCfg& c, const int64_t* ids, int64_t n, int32_t h, hipStream_t_ s);
 void launch_snapshot(const DevCfg& c, DevTable tb, int32_t p0, int32_t np, StateCols out, unsigned long long* count,
                      hipStream_t_ s);
 // demand != NULL: count rows per partition (and key-group errors); NULL: insert the rows

@@ -1543,11 +1543,27 @@ void free_state_cols(StateCols& c) {
 }
 }  // namespace
 
+int64_t fw_state_block_bytes(fw_op* op) {
+  if (!op) return 0;
+  if (op->dc.agg == FW_AGG_HLL) return (int64_t)1 << op->dc.hll_p;
+  if (op->dc.agg == FW_AGG_TDIGEST) return (1 + 2 * (int64_t)op->dc.td_nb) * (int64_t)sizeof(int64_t);
+  return 0;
+}
+
 int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64_t cap, int64_t* n) {
-  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_TDIGEST || op->cfg.assigner == FW_COUNT))
-    return set_err(op, FW_ERR_UNSUPPORTED,  // not in fw_state_rows
-                   "keyed-state snapshots of the HyperLogLog and t-digest aggregates and of count windows are not offered");
+  if (op && op->dc.pool_bytes)
+    return set_err(op, FW_ERR_UNSUPPORTED, "the HyperLogLog and t-digest accumulators are not in fw_state_rows: "
+                                           "use fw_snapshot_key_group_blocks");
+  return fw_snapshot_key_group_blocks(op, kg, dst, nullptr, cap, n);
+}
+
+int fw_snapshot_key_group_blocks(fw_op* op, int32_t kg, const fw_state_rows* dst, uint8_t* blocks, int64_t cap,
+                                 int64_t* n) {
+  if (op && op->cfg.assigner == FW_COUNT)
+    return set_err(op, FW_ERR_UNSUPPORTED, "keyed-state snapshots of count windows are not offered");
   if (!op || !n) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
+  const int64_t bb = fw_state_block_bytes(op);
+  if (bb && dst && cap > 0 && !blocks) return set_err(op, FW_ERR_ARG, "null accumulator blocks");
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;
   if ((rc = kg_check(op, kg)) || (rc = settle(op))) return rc;
@@ -1561,9 +1577,16 @@ int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64
   int64_t bound = 0;
   for (int32_t v : live) bound += v;
   StateCols d{};
-  if ((rc = alloc_state_cols(op, d, bound))) {
+  uint8_t* acc = nullptr;
+  auto release = [&]() {
     free_state_cols(d);
-    return rc;
+    dfree(d.blk);
+    dfree(acc);
+  };
+  if ((rc = alloc_state_cols(op, d, bound)) ||
+      (bb && dmalloc(&d.blk, (size_t)std::max<int64_t>(bound, 1)) != hipSuccess && (rc = FW_ERR_HIP))) {
+    release();
+    return rc == FW_ERR_HIP ? set_err(op, rc, "snapshot: allocation failed") : rc;
   }
   HIP_OR_RETURN(op, hipMemsetAsync(op->d_stats3, 0, sizeof(unsigned long long), op->stream));
   fwdev::launch_snapshot(c, op->tb, p0, np, d, op->d_stats3, op->stream);
@@ -1576,9 +1599,17 @@ int fw_snapshot_key_group(fw_op* op, int32_t kg, const fw_state_rows* dst, int64
     int64_t* ds[8] = {d.key, d.start, d.end, d.cnt, d.sum, d.mn, d.mx, d.timer};
     for (int i = 0; i < 8 && e == hipSuccess; i++)
       if (hs[i]) e = hipMemcpyAsync(hs[i], ds[i], got * sizeof(int64_t), hipMemcpyDeviceToHost, op->stream);
+    if (e == hipSuccess && bb) {  // the rows' accumulators in their snapshot form
+      e = dmalloc(&acc, (size_t)(got * bb));
+      if (e == hipSuccess) {
+        fwdev::launch_block_export(c, d.blk, (int64_t)got, acc, op->stream);
+        e = hipGetLastError();
+      }
+      if (e == hipSuccess) e = hipMemcpyAsync(blocks, acc, got * bb, hipMemcpyDeviceToHost, op->stream);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(op->stream);
   }
-  free_state_cols(d);
+  release();
   if (e != hipSuccess) return set_err(op, FW_ERR_HIP, "snapshot: %s", hipGetErrorString(e));
   *n = (int64_t)got;
   return FW_OK;
@@ -1640,10 +1671,18 @@ int restore_dense(fw_op* op, int32_t kg, const fw_state_rows* src, int64_t n) {
 extern "C" {
 
 int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_t n) {
-  if (op && (op->dc.agg == FW_AGG_HLL || op->dc.agg == FW_AGG_TDIGEST || op->cfg.assigner == FW_COUNT))
-    return set_err(op, FW_ERR_UNSUPPORTED,  // not in fw_state_rows
-                   "keyed-state snapshots of the HyperLogLog and t-digest aggregates and of count windows are not offered");
+  if (op && op->dc.pool_bytes)
+    return set_err(op, FW_ERR_UNSUPPORTED, "the HyperLogLog and t-digest accumulators are not in fw_state_rows: "
+                                           "use fw_restore_key_group_blocks");
+  return fw_restore_key_group_blocks(op, kg, src, nullptr, n);
+}
+
+int fw_restore_key_group_blocks(fw_op* op, int32_t kg, const fw_state_rows* src, const uint8_t* blocks, int64_t n) {
+  if (op && op->cfg.assigner == FW_COUNT)
+    return set_err(op, FW_ERR_UNSUPPORTED, "keyed-state snapshots of count windows are not offered");
   if (!op || (n > 0 && !src) || n < 0) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
+  const int64_t bb = fw_state_block_bytes(op);
+  if (bb && n > 0 && !blocks) return set_err(op, FW_ERR_ARG, "null accumulator blocks");
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;
   if ((rc = kg_check(op, kg)) || (rc = settle(op))) return rc;
@@ -1679,9 +1718,13 @@ int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_
   }
   StateCols d{};
   int32_t* demand = nullptr;
+  uint8_t* acc = nullptr;
   auto fail = [&](int code) {
     free_state_cols(d);
     dfree(demand);
+    dfree(acc);
+    dfree(d.blk);
+    dfree(d.used);
     return code;
   };
   if ((rc = alloc_state_cols(op, d, n))) return fail(rc);
@@ -1712,6 +1755,30 @@ int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_
   int64_t need = 0;
   for (int32_t p = 0; p < P; p++) need = std::max<int64_t>(need, (int64_t)live[p] + dem[p]);
   if (need > region_limit(op->dc.log_r) && (rc = grow_table(op, log_r_for(op, need)))) return fail(rc);
+  // pool aggregates: n blocks off the free stack / the pool's tail for the rows' new windows, the accumulators
+  // imported by k_restore, the blocks it did not use back on the stack
+  int32_t ctr[2] = {0, 0};
+  int32_t take = 0;
+  if (bb) {
+    if (hipMemcpy(ctr, op->dc.pool_ctr, sizeof ctr, hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(set_err(op, FW_ERR_HIP, "restore: copy failed"));
+    take = (int32_t)std::min<int64_t>(ctr[0], n);
+    if (ctr[1] + (n - take) > op->dc.pool_blocks)
+      return fail(set_err(op, FW_ERR_CAPACITY, "restore: %lld rows do not fit the accumulator block pool (%lld blocks, "
+                          "%d free; raise expected_entries)", (long long)n, (long long)op->dc.pool_blocks,
+                          (int)(op->dc.pool_blocks - ctr[1] + ctr[0])));
+    if (dmalloc(&acc, (size_t)(n * bb)) != hipSuccess || dmalloc(&d.blk, (size_t)n) != hipSuccess ||
+        dmalloc(&d.used, 1) != hipSuccess || hipMemsetAsync(d.used, 0, sizeof(int32_t), op->stream) != hipSuccess ||
+        hipMemcpyAsync(acc, blocks, n * bb, hipMemcpyHostToDevice, op->stream) != hipSuccess)
+      return fail(set_err(op, FW_ERR_HIP, "restore: allocation failed"));
+    d.acc = acc;
+    d.acc_bytes = bb;
+    fwdev::launch_pool_take(op->dc, ctr[0], take, ctr[1], n, d.blk, op->stream);
+    const int32_t nc[2] = {ctr[0] - take, (int32_t)(ctr[1] + (n - take))};
+    if (hipMemcpyAsync(op->dc.pool_ctr, nc, sizeof nc, hipMemcpyHostToDevice, op->stream) != hipSuccess ||
+        hipStreamSynchronize(op->stream) != hipSuccess)
+      return fail(set_err(op, FW_ERR_HIP, "restore: copy failed"));
+  }
   int32_t* d_round = nullptr;
   if (rounds > 1) {
     if (dmalloc(&d_round, (size_t)n) != hipSuccess ||
@@ -1723,6 +1790,24 @@ int fw_restore_key_group(fw_op* op, int32_t kg, const fw_state_rows* src, int64_
   rc = sync_status(op);
   dfree(d_round);
   if (!launched || rc) return fail(rc ? rc : set_err(op, FW_ERR_HIP, "restore kernel failed"));
+  if (bb) {
+    int32_t used = 0;
+    if (hipMemcpy(&used, d.used, sizeof used, hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(set_err(op, FW_ERR_HIP, "restore: copy failed"));
+    const int32_t h = ctr[0] - take, back = (int32_t)(n - used);
+    fwdev::launch_pool_give(op->dc, d.blk + used, back, h, op->stream);
+    const int32_t height = h + back;
+    if (hipMemcpyAsync(op->dc.pool_ctr, &height, sizeof height, hipMemcpyHostToDevice, op->stream) != hipSuccess ||
+        hipStreamSynchronize(op->stream) != hipSuccess)
+      return fail(set_err(op, FW_ERR_HIP, "restore: copy failed"));
+    if (op->h_status->acc_refused) {
+      const int bad = op->h_status->acc_refused;
+      op->h_status->acc_refused = 0;
+      put_status_field(op, &Status::acc_refused);
+      return fail(set_err(op, FW_ERR_STATE, "%d restored t-digest row(s) refused: a malformed digest, or a window "
+                          "that is already present (digests are not merged on restore)", bad));
+    }
+  }
   fail(FW_OK);
   if (op->h_status->flags & FW_STATUS_STATE_LOST) return set_err(op, FW_ERR_CAPACITY, "restore: region full");
   const int64_t rows = (int64_t)op->h_status->out_rows;

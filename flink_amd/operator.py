@@ -332,29 +332,46 @@ class GpuWindowOperator:
     # (HeapKeyedStateBackend.java:289-399, per-key-group offsets :370-381; timers via
     # InternalTimeServiceManager.snapshotStateForKeyGroup :114); a restore may hand the key groups
     # to operators with a different KeyGroupRange (rescaling).
+    def state_dtype(self):
+        """Row type of this operator's snapshots: STATE_DTYPE, plus `acc` (the accumulator block, fw_state_block_bytes
+        bytes: HyperLogLog registers / the t-digest's centroids) for the HyperLogLog and t-digest aggregates."""
+        bb = N.lib().fw_state_block_bytes(self._h)
+        return STATE_DTYPE if bb == 0 else np.dtype(STATE_DTYPE.descr + [("acc", "u1", (bb,))])
+
     def snapshot_key_group(self, kg):
-        """Live (key, window) accumulators of key group kg as a STATE_DTYPE array (no order)."""
+        """Live (key, window) accumulators of key group kg as a state_dtype() array (no order)."""
         L = N.lib()
+        bb = L.fw_state_block_bytes(self._h)
         n = ctypes.c_int64()
-        N.check(L.fw_snapshot_key_group(self._h, int(kg), None, 0, ctypes.byref(n)), self._h)
+        N.check(L.fw_snapshot_key_group_blocks(self._h, int(kg), None, None, 0, ctypes.byref(n)), self._h)
         cols = {f: np.zeros(n.value, dtype=np.int64) for f in STATE_FIELDS}
+        acc = np.zeros((n.value, max(bb, 1)), dtype=np.uint8)
         dst = N.FwStateRows(**{f: cols[f].ctypes.data for f in STATE_FIELDS})
         got = ctypes.c_int64()
-        N.check(L.fw_snapshot_key_group(self._h, int(kg), ctypes.byref(dst), n.value, ctypes.byref(got)), self._h)
-        out = np.zeros(got.value, dtype=STATE_DTYPE)
+        N.check(L.fw_snapshot_key_group_blocks(self._h, int(kg), ctypes.byref(dst), acc.ctypes.data if bb else None,
+                                               n.value, ctypes.byref(got)), self._h)
+        out = np.zeros(got.value, dtype=self.state_dtype())
         for f in STATE_FIELDS:
             out[f] = cols[f][:got.value]
+        if bb:
+            out["acc"] = acc[:got.value]
         return out
 
     def snapshot_state(self):
-        """{key group: STATE_DTYPE rows} for every key group of this operator's KeyGroupRange."""
+        """{key group: state_dtype() rows} for every key group of this operator's KeyGroupRange."""
         return {kg: self.snapshot_key_group(kg) for kg in self.key_group_range}
 
     def restore_key_group(self, kg, rows):
-        rows = np.ascontiguousarray(rows, dtype=STATE_DTYPE)
-        cols = {f: np.ascontiguousarray(rows[f]) for f in STATE_FIELDS}
+        L = N.lib()
+        bb = L.fw_state_block_bytes(self._h)
+        rows = np.ascontiguousarray(rows)
+        if bb and (rows.dtype.names is None or "acc" not in rows.dtype.names or rows.dtype["acc"].shape != (bb,)):
+            raise ValueError(f"rows of this aggregate carry `acc` blocks of {bb} bytes (state_dtype())")
+        cols = {f: np.ascontiguousarray(rows[f], dtype=np.int64) for f in STATE_FIELDS}
+        acc = np.ascontiguousarray(rows["acc"], dtype=np.uint8) if bb else None
         src = N.FwStateRows(**{f: cols[f].ctypes.data for f in STATE_FIELDS})
-        N.check(N.lib().fw_restore_key_group(self._h, int(kg), ctypes.byref(src), len(rows)), self._h)
+        N.check(L.fw_restore_key_group_blocks(self._h, int(kg), ctypes.byref(src),
+                                              acc.ctypes.data if bb and len(rows) else None, len(rows)), self._h)
 
     def initialize_state(self, snapshot):
         """Restores the key groups of `snapshot` ({kg: rows}) that this operator owns; others are skipped,

@@ -89,7 +89,7 @@ extern "C" {
                                       Rows carry count = elements and sum / min / max = the estimated quantiles
                                       tdigest_quantiles[0..2] (f64 bits).  Tumbling windows, no allowed lateness,
                                       FW_VAL_F64; expected_entries sizes the digest pool.  Keyed-state snapshots
-                                      are refused. */
+                                      carry the digest as an accumulator block (fw_snapshot_key_group_blocks). */
 #define FW_AGG_FIRST_MAX 5         /* max(pos) (ComparableAggregator.java:72-94, Comparator.MaxComparator): as
                                       FW_AGG_FIRST, but the min column holds the field's MAXIMUM (the first
                                       element with the field replaced by the max) */
@@ -284,7 +284,8 @@ int fw_push_partials_device(fw_op* op, const fw_partials* in, int64_t n);
  *     keys outside the key group are refused with FW_ERR_KEY_GROUP.  First-element reduces (FW_AGG_FIRST,
  *     FW_AGG_FIRST_MAX, FW_AGG_MINBY, FW_AGG_MAXBY): `max` is the element's ordinal, and later pushes are
  *     numbered after the largest restored one.  Rows of one call that restore the same (key, window) are merged
- *     in order.  HyperLogLog and t-digest state is refused (FW_ERR_UNSUPPORTED). */
+ *     in order.  HyperLogLog and t-digest handles keep their accumulator beside the row: these two calls
+ *     refuse them (FW_ERR_UNSUPPORTED) and the _blocks variants below carry it. */
 typedef struct fw_state_rows {
   int64_t* key;
   int64_t* start;
@@ -297,6 +298,27 @@ typedef struct fw_state_rows {
 } fw_state_rows;
 int fw_snapshot_key_group(fw_op* op, int32_t key_group, const fw_state_rows* host_dst, int64_t cap, int64_t* n);
 int fw_restore_key_group(fw_op* op, int32_t key_group, const fw_state_rows* host_src, int64_t n);
+
+/* The same with each row's accumulator block, for the aggregates whose accumulator is not in the row
+ * (FW_AGG_HLL, FW_AGG_TDIGEST; any other handle takes them with blocks NULL).  The heap backend stores the
+ * accumulator in the state's value column through the AggregateFunction's accumulator serializer
+ * (HeapAggregatingState.java:73-93 keeps the ACC object; its TypeSerializer writes it per mapping at snapshot,
+ * HeapKeyedStateBackend.java:370-381); this build's accumulators are fixed-size blocks of
+ * fw_state_block_bytes(op) bytes, row i's at blocks + i * fw_state_block_bytes(op):
+ *   FW_AGG_HLL      the 2^p registers M[0..m), one byte each (the rank, 0 = untouched);
+ *   FW_AGG_TDIGEST  int64 little-endian words: n, then (sum as f64 bits, weight) of centroids 0..n-1 in
+ *                   mean order, zero-padded to 1 + 2 * floor(delta / 2) words (the fw_rows.digests layout).
+ * fw_snapshot_key_group_blocks: rows as fw_snapshot_key_group plus the blocks (host buffer of cap rows; NULL
+ *   with cap 0 only counts).
+ * fw_restore_key_group_blocks: rows as fw_restore_key_group; a new (key, window) takes a pool block holding the
+ *   imported accumulator.  A HyperLogLog row whose (key, window) is already present merges by register max
+ *   (AggregateFunction.merge); a t-digest one is refused with FW_ERR_STATE (the digest is not re-compressed).
+ *   Rows must fit the pool (expected_entries): FW_ERR_CAPACITY otherwise, before anything changes. */
+int64_t fw_state_block_bytes(fw_op* op);
+int fw_snapshot_key_group_blocks(fw_op* op, int32_t key_group, const fw_state_rows* host_dst, uint8_t* host_blocks,
+                                 int64_t cap, int64_t* n);
+int fw_restore_key_group_blocks(fw_op* op, int32_t key_group, const fw_state_rows* host_src,
+                                const uint8_t* host_blocks, int64_t n);
 
 /* Key routing (both sides of keyBy).
  *   fw_key_groups_device: kg[i] = KeyGroupRangeAssignment.assignToKeyGroup(key_i, maxParallelism)
