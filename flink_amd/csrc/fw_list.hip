@@ -127,9 +127,9 @@ __device__ __forceinline__ uint32_t g_hash(int64_t key, int64_t start) {
   return (uint32_t)fmix64((uint64_t)key ^ fmix64((uint64_t)start ^ 0x9E3779B97F4A7C15ull));
 }
 // Lookups read the state word with a relaxed agent-scope load (L2, no L1 invalidation as an acquire would cost on
-// every probe) and, once it reads LIVE, the key and window the same way: the inserter's plain stores of both precede
-// its release store of LIVE, and the key loads are issued only after the state's value has arrived (they depend on
-// it), so they read what the inserter wrote.
+// every probe) and, once it reads LIVE, the key and window the same way: the inserter's write-through stores of both
+// complete before its store of LIVE, and the key loads are issued only after the state's value has arrived (they
+// depend on it), so they read what the inserter wrote.
 __device__ __forceinline__ int64_t ld_l2(const int64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -151,12 +151,17 @@ __device__ int32_t g_find_insert(const LState& S, int64_t key, int64_t start, in
         return -1;
       }
       if (atomicCAS(&S.g[s].st, G_EMPTY, G_BUSY) == G_EMPTY) {
-        S.g[s].key = key;
-        S.g[s].start = start;
-        S.g[s].kg = kg;
-        S.g[s].cnt = 0;
-        S.g[s].fl = 0;
-        __hip_atomic_store(&S.g[s].st, G_LIVE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        // publish without an L2 write-back per group (an agent-scope release is one): the fields are stored
+        // write-through (relaxed agent-scope stores, sc1), this lane waits for them, then stores LIVE the same
+        // way; readers poll the state and load the fields with relaxed agent-scope loads (sc1), the hand-off of
+        // MI355X_MICROARCH.md's sc1 table (one lane signalling for all its own stores)
+        __hip_atomic_store(&S.g[s].key, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&S.g[s].start, start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&S.g[s].kg, kg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&S.g[s].cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&S.g[s].fl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&S.g[s].st, (uint32_t)G_LIVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         (*ins)++;
         return (int32_t)s;
       }
@@ -223,7 +228,12 @@ __global__ __launch_bounds__(256) void k_lp_count(LCfg c, LState S, const int64_
 }
 
 // the entries: log[base + woff[i] + j] = (ts, value, ordinal, group) for the j-th non-late window of record i;
-// groups whose elements fire while being processed are marked for the ordered walk
+// groups whose elements fire while being processed are marked for the ordered walk.
+// AU records per thread in flight: a one-window record's home slot is read as one 64-bit (state, flags) load for all
+// of them, then the key and window of the LIVE ones, so the common case (its group already at its home slot) costs
+// two dependent round trips per AU records; the rest (a probe chain, a new group, several windows) go through
+// g_find_insert one by one.
+constexpr int AU = 4;
 __global__ __launch_bounds__(256) void k_lp_append(LCfg c, LState S, const int64_t* __restrict__ key,
                                                    const int64_t* __restrict__ ts, const int64_t* __restrict__ val,
                                                    const int32_t* __restrict__ kh, int64_t n, int64_t wm,
@@ -231,31 +241,84 @@ __global__ __launch_bounds__(256) void k_lp_append(LCfg c, LState S, const int64
                                                    int64_t base, int64_t ord_base, unsigned long long limit) {
   long long due = LMAX;  // the earliest timer these entries register
   unsigned ins = 0;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
-    const int64_t i = i0 + threadIdx.x;
-    if (i >= n || !wcnt[i]) continue;
-    const int64_t t = ts[i], k = key[i], v = val[i];
-    const int32_t kg = key_group(key_hash_of(c.key_kind, k, kh, i), c.max_par);
-    int64_t idx = base + woff[i];
-    for_windows(c, t, wm, [&](int64_t s) {
-      const int64_t mts = w_max_ts(c, s), cl = w_cleanup(c, s);
-      due = min(due, (long long)(c.trigger == FW_TRIGGER_EVENT_TIME && mts > wm ? mts : cl));
-      const int32_t g = g_find_insert(S, k, s, kg, limit, &ins);
-      S.lpay[idx] = LPay{t, v, ord_base + i, 0};
-      S.lgid[idx] = g;
-      idx++;
-      if (g < 0) {
-        atomicOr(&S.ctr->flags, LF_MAP_FULL);
-        return;
+  // one entry: its payload and group, and the trigger's bookkeeping (fl: the group's flags as last read)
+  auto put = [&](int64_t idx, int64_t i, int64_t t, int64_t v, int64_t s, int32_t g, uint32_t fl) {
+    S.lpay[idx] = LPay{t, v, ord_base + i, 0};
+    S.lgid[idx] = g;
+    if (g < 0) {
+      atomicOr(&S.ctr->flags, LF_MAP_FULL);
+      return;
+    }
+    const int64_t mts = w_max_ts(c, s);
+    due = min(due, (long long)(c.trigger == FW_TRIGGER_EVENT_TIME && mts > wm ? mts : w_cleanup(c, s)));
+    if (c.trigger == FW_TRIGGER_COUNT || mts <= wm) {  // CountTrigger / late firing
+      atomicOr(&S.g[g].fl, GF_TOUCH);
+      S.ctr->need_seq = 1u;
+    } else if (!(fl & GF_TIMER)) {  // EventTimeTrigger.onElement registers the timer at maxTimestamp
+      atomicOr(&S.g[g].fl, GF_TIMER);
+    }
+  };
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * AU;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x * AU; i0 < n; i0 += stride) {
+    int64_t k[AU], t[AU], v[AU], s[AU], idx[AU];
+    uint32_t wc[AU], home[AU];
+    int32_t kg[AU];
+#pragma unroll
+    for (int u = 0; u < AU; u++) {
+      const int64_t i = i0 + u * blockDim.x + threadIdx.x;
+      wc[u] = i < n ? wcnt[i] : 0u;
+      k[u] = t[u] = v[u] = idx[u] = 0;
+      if (wc[u]) {
+        t[u] = ts[i];
+        k[u] = key[i];
+        v[u] = val[i];
+        idx[u] = base + woff[i];
       }
-      if (c.trigger == FW_TRIGGER_COUNT || w_max_ts(c, s) <= wm) {  // CountTrigger / late firing
-        atomicOr(&S.g[g].fl, GF_TOUCH);
-        S.ctr->need_seq = 1u;
-      } else {  // EventTimeTrigger.onElement registers the timer at maxTimestamp
-        if (!(S.g[g].fl & GF_TIMER)) atomicOr(&S.g[g].fl, GF_TIMER);
+    }
+    uint64_t sf[AU];
+#pragma unroll
+    for (int u = 0; u < AU; u++) {
+      const int64_t i = i0 + u * blockDim.x + threadIdx.x;
+      s[u] = LMIN;
+      kg[u] = 0;
+      sf[u] = 0;
+      if (!wc[u]) continue;
+      kg[u] = key_group(key_hash_of(c.key_kind, k[u], kh, i), c.max_par);
+      if (wc[u] != 1) continue;
+      for_windows(c, t[u], wm, [&](int64_t w) { s[u] = w; });
+      home[u] = g_hash(k[u], s[u]) & S.gmask;
+      sf[u] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(&S.g[home[u]].st), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __atomic_signal_fence(__ATOMIC_ACQUIRE);  // (the compiler keeps the key loads behind the state words)
+    int64_t hk[AU], hs[AU];
+#pragma unroll
+    for (int u = 0; u < AU; u++) {
+      hk[u] = hs[u] = 0;
+      if (wc[u] == 1 && (uint32_t)sf[u] == G_LIVE) {
+        hk[u] = ld_l2(&S.g[home[u]].key);
+        hs[u] = ld_l2(&S.g[home[u]].start);
       }
-    });
+    }
+#pragma unroll
+    for (int u = 0; u < AU; u++) {
+      if (!wc[u]) continue;
+      const int64_t i = i0 + u * blockDim.x + threadIdx.x;
+      if (wc[u] == 1) {
+        if ((uint32_t)sf[u] == G_LIVE && hk[u] == k[u] && hs[u] == s[u]) {
+          put(idx[u], i, t[u], v[u], s[u], (int32_t)home[u], (uint32_t)(sf[u] >> 32));
+        } else {
+          const int32_t g = g_find_insert(S, k[u], s[u], kg[u], limit, &ins);
+          put(idx[u], i, t[u], v[u], s[u], g, g >= 0 ? S.g[g].fl : 0u);
+        }
+        continue;
+      }
+      int64_t x = idx[u];
+      for_windows(c, t[u], wm, [&](int64_t w) {
+        const int32_t g = g_find_insert(S, k[u], w, kg[u], limit, &ins);
+        put(x++, i, t[u], v[u], w, g, g >= 0 ? S.g[g].fl : 0u);
+      });
+    }
   }
   block_min(&S.ctr->next_due, due);
   block_add(&S.ctr->live_groups, ins);
@@ -1041,8 +1104,10 @@ int push_device(fw_list* op, const int64_t* key, const int64_t* ts, const int64_
   if (n > op->max_batch) return set_err(op, FW_ERR_ARG, "batch of %lld records exceeds max_batch %lld", (long long)n,
                                         (long long)op->max_batch);
   if (op->cfg.key_kind == FW_KEY_HASHED && !kh) return set_err(op, FW_ERR_ARG, "key_hash required for FW_KEY_HASHED");
-  LRET(read_ctr(op));
-  LRET(ensure_side(op, (int64_t)op->h_ctr->side + n));
+  if (op->c.side_output) {  // room for every record of the batch in the side output
+    LRET(read_ctr(op));
+    LRET(ensure_side(op, (int64_t)op->h_ctr->side + n));
+  }
   LHIP(op, hipMemsetAsync(&op->S.ctr->flags, 0, 8, op->stream));  // flags, need_seq
   hipLaunchKernelGGL(k_lp_count, dim3(grid_for(n)), dim3(256), 0, op->stream, op->c, op->S, key, ts, val, kh, n, op->wm,
                      op->wcnt);
@@ -1085,10 +1150,11 @@ int push_device(fw_list* op, const int64_t* key, const int64_t* ts, const int64_
   op->n_log += E;
   op->ord_base += n;
   op->records_in += n;
-  LRET(read_ctr(op));
-  if (op->h_ctr->flags & LF_MAP_FULL) return set_err(op, FW_ERR_CAPACITY, "list state map full");
-  if (op->h_ctr->need_seq) LRET(walk_lists<true>(op, GF_TOUCH, base));
-  LRET(read_ctr(op));
+  // (the counters are current: read after the last append)
+  if (op->h_ctr->need_seq) {
+    LRET(walk_lists<true>(op, GF_TOUCH, base));
+    LRET(read_ctr(op));
+  }
   return maybe_compact(op);
 }
 
