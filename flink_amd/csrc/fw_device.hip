@@ -416,17 +416,20 @@ constexpr int TAINT_MAX_PROBES = 64;
 __device__ __forceinline__ bool taint_insert(const DevCfg& c, int64_t key) {
   uint32_t s = taint_slot0(c, key);
   for (int probes = 0; probes < TAINT_MAX_PROBES;) {
-    const uint32_t cur = __hip_atomic_load(&c.taint_state[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    // (relaxed agent-scope loads and write-through publication, as cnt_slot: no L1 invalidation per probe)
+    const uint32_t cur = __hip_atomic_load(&c.taint_state[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __atomic_signal_fence(__ATOMIC_ACQUIRE);
     if (cur == c.taint_epoch) {
-      if (c.taint_key[s] == (uint64_t)key) return true;
+      if (__hip_atomic_load(&c.taint_key[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint64_t)key) return true;
       s = (s + 1) & c.taint_mask;
       probes++;
       continue;
     }
     if (cur == (c.taint_epoch | TAINT_BUSY)) continue;  // being published by another lane: re-read
     if (atomicCAS(&c.taint_state[s], cur, c.taint_epoch | TAINT_BUSY) == cur) {
-      c.taint_key[s] = (uint64_t)key;
-      __hip_atomic_store(&c.taint_state[s], c.taint_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&c.taint_key[s], (uint64_t)key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&c.taint_state[s], c.taint_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return true;
     }
   }
@@ -3623,10 +3626,13 @@ __global__ __launch_bounds__(64) void k_td_large_compact(DevCfg c, TdBuf td, Sta
 __device__ __forceinline__ int32_t cnt_slot(const DevCount& cw, int64_t key, Status* st) {
   uint32_t s = (uint32_t)fmix64((uint64_t)key ^ 0x3C6EF372FE94F82Bull) & cw.cap_mask;
   for (uint32_t probes = 0; probes <= cw.cap_mask;) {
-    const uint32_t cur = __hip_atomic_load(&cw.mstate[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    // relaxed agent-scope (L2) loads: an acquire here would invalidate the CU's L1 on every record; the publisher
+    // below stores the key and slot write-through and waits for them before it stores the state
+    const uint32_t cur = __hip_atomic_load(&cw.mstate[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __atomic_signal_fence(__ATOMIC_ACQUIRE);  // (the compiler keeps the key loads behind it)
     if (cur == 2) {
-      if (cw.mkey[s] == key) {
-        const uint32_t slot = cw.mslot[s];
+      if (__hip_atomic_load(&cw.mkey[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key) {
+        const uint32_t slot = __hip_atomic_load(&cw.mslot[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (slot >= (uint32_t)cw.max_keys) break;  // a key refused earlier stays refused
         return (int32_t)slot;
       }
@@ -3637,9 +3643,10 @@ __device__ __forceinline__ int32_t cnt_slot(const DevCount& cw, int64_t key, Sta
     if (cur == 1) continue;  // being published by another lane: re-read
     if (atomicCAS(&cw.mstate[s], 0u, 1u) == 0u) {
       const int32_t slot = atomicAdd(cw.nslots, 1);
-      cw.mkey[s] = key;
-      cw.mslot[s] = (uint32_t)slot;
-      __hip_atomic_store(&cw.mstate[s], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&cw.mkey[s], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&cw.mslot[s], (uint32_t)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&cw.mstate[s], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (slot >= cw.max_keys) {
         atomicOr(&st->flags, FW_STATUS_STATE_LOST);
         return -1;
@@ -3669,79 +3676,102 @@ __global__ __launch_bounds__(256) void k_cnt_bounds(DevCount cw, const uint32_t*
 }
 // the reduce of one fire: SumAggregator over the window's elements in arrival order (integer sums wrap, so their
 // order does not matter; Double sums add left to right, Float sums round each partial sum to float)
+// the batch's values in sorted order (each run's elements side by side for the fire), as two 32-bit halves in the
+// sort's spare buffers: one gather per record instead of one per element of every window that reads it
+__global__ __launch_bounds__(256) void k_cnt_gather(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
+                                                    const int64_t* __restrict__ val, int64_t n, uint32_t none,
+                                                    uint32_t* __restrict__ vlo, uint32_t* __restrict__ vhi) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (sk[i] == none) continue;
+    const uint64_t v = (uint64_t)val[sv[i]];
+    vlo[i] = (uint32_t)v;
+    vhi[i] = (uint32_t)(v >> 32);
+  }
+}
+// one workgroup per chunk of CF_CHUNK sorted records: a counting pass, one reservation of the chunk's rows (a single
+// output counter took one contended atomic per wave before), then the rows at their offsets
+constexpr int CF_CHUNK = 4096;
+__device__ __forceinline__ bool cnt_fires(const DevCount& cw, const uint32_t* __restrict__ sk, int64_t i, int64_t n,
+                                          uint32_t none) {
+  if (i >= n || sk[i] == none) return false;
+  const uint32_t g = sk[i];
+  return (cw.cnt[g] + (i - cw.sbeg[g]) + 1) % cw.slide == 0;
+}
 __global__ __launch_bounds__(256) void k_cnt_fire(DevCfg c, DevCount cw, const uint32_t* __restrict__ sk,
                                                   const uint32_t* __restrict__ sv, const int64_t* __restrict__ key,
-                                                  const int64_t* __restrict__ val, int64_t n, uint32_t none, DevRows out,
-                                                  Status* st) {
+                                                  const uint32_t* __restrict__ vlo, const uint32_t* __restrict__ vhi,
+                                                  int64_t n, uint32_t none, DevRows out, Status* st) {
+  __shared__ uint32_t sw[256 / 64 + 1];
+  __shared__ unsigned long long base_s;
   const int64_t ring = cw.wl - 1;
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = i0 + threadIdx.x;
-    bool fire = false;
-    Entry e;
-    if (i < n && sk[i] != none) {
+  constexpr int PER = CF_CHUNK / 256;
+  for (int64_t c0 = (int64_t)blockIdx.x * CF_CHUNK; c0 < n; c0 += (int64_t)gridDim.x * CF_CHUNK) {
+    uint32_t nf = 0;
+#pragma unroll 4
+    for (int k = 0; k < PER; k++) nf += cnt_fires(cw, sk, c0 + k * 256 + threadIdx.x, n, none) ? 1u : 0u;
+    uint32_t total;
+    unsigned long long pos = block_excl_scan(nf, sw, &total);
+    if (threadIdx.x == 0) base_s = total ? atomicAdd(&st->out_rows, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    pos += base_s;
+    for (int k = 0; k < PER && nf; k++) {
+      const int64_t i = c0 + k * 256 + threadIdx.x;
+      if (!cnt_fires(cw, sk, i, n, none)) continue;
+      nf--;
+      Entry e;
       const uint32_t g = sk[i];
       const int64_t r = i - cw.sbeg[g], before = cw.cnt[g], seq = before + r + 1;
-      if (seq % cw.slide == 0) {
-        fire = true;
-        const int64_t w = min(cw.wl, seq);
-        e.key = key[sv[i]];
-        e.start = LMIN;
-        e.end = LMAX;
-        e.cnt = w;
-        double ds = 0.0, dm = 0.0;
-        int64_t is = 0, im = LMAX;
-        for (int64_t q = seq - w + 1; q <= seq; q++) {  // oldest first
-          int64_t v, o;
-          if (q > before) {
-            const uint32_t b = sv[i - (seq - q)];
-            v = val[b];
-            o = c.ord_base + (int64_t)b;
-          } else {
-            const int64_t at = (int64_t)g * ring + (q - 1) % ring;
-            v = cw.ring_v[at];
-            o = cw.ring_o[at];
-          }
-          if (q == seq - w + 1) e.mx = o;  // the window's first element
-          if (c.vtype == FW_VAL_F64) {
-            const double d = __longlong_as_double(v);
-            ds = q == seq - w + 1 ? d : c.f32 ? (double)((float)ds + (float)d) : ds + d;
-            if (q == seq - w + 1 || f64_sortable(v) < f64_sortable(__double_as_longlong(dm))) dm = d;
-          } else {
-            is = jadd(is, v);
-            im = min(im, v);
-          }
-        }
-        if (c.vtype == FW_VAL_F64) {
-          e.sum = __double_as_longlong(ds);
-          e.mn = __double_as_longlong(dm);
-          if ((e.mn & 0x7ff0000000000000ll) == 0x7ff0000000000000ll && (e.mn & 0x000fffffffffffffll))
-            e.mn = 0x7ff8000000000000ll;  // Double.doubleToLongBits: canonical NaN
+      const int64_t w = min(cw.wl, seq);
+      e.key = key[sv[i]];
+      e.start = LMIN;
+      e.end = LMAX;
+      e.cnt = w;
+      double ds = 0.0, dm = 0.0;
+      int64_t is = 0, im = LMAX;
+      for (int64_t q = seq - w + 1; q <= seq; q++) {  // oldest first
+        int64_t v, o;
+        if (q > before) {
+          const int64_t j = i - (seq - q);
+          v = (int64_t)(((uint64_t)vhi[j] << 32) | vlo[j]);
+          o = q == seq - w + 1 ? c.ord_base + (int64_t)sv[j] : 0;
         } else {
-          e.sum = sum_out(c, is);
-          e.mn = im;
+          const int64_t at = (int64_t)g * ring + (q - 1) % ring;
+          v = cw.ring_v[at];
+          o = cw.ring_o[at];
+        }
+        if (q == seq - w + 1) e.mx = o;  // the window's first element
+        if (c.vtype == FW_VAL_F64) {
+          const double d = __longlong_as_double(v);
+          ds = q == seq - w + 1 ? d : c.f32 ? (double)((float)ds + (float)d) : ds + d;
+          if (q == seq - w + 1 || f64_sortable(v) < f64_sortable(__double_as_longlong(dm))) dm = d;
+        } else {
+          is = jadd(is, v);
+          im = min(im, v);
         }
       }
+      if (c.vtype == FW_VAL_F64) {
+        e.sum = __double_as_longlong(ds);
+        e.mn = __double_as_longlong(dm);
+        if ((e.mn & 0x7ff0000000000000ll) == 0x7ff0000000000000ll && (e.mn & 0x000fffffffffffffll))
+          e.mn = 0x7ff8000000000000ll;  // Double.doubleToLongBits: canonical NaN
+      } else {
+        e.sum = sum_out(c, is);
+        e.mn = im;
+      }
+      if ((int64_t)pos < out.cap) {
+        out.key[pos] = e.key;
+        out.start[pos] = e.start;
+        out.end[pos] = e.end;
+        out.cnt[pos] = e.cnt;
+        out.sum[pos] = e.sum;
+        out.mn[pos] = e.mn;
+        out.mx[pos] = e.mx;
+      } else {
+        atomicOr(&st->flags, FW_STATUS_OUT_FULL);
+      }
+      pos++;
     }
-    // one reservation per wave
-    const uint64_t m = __ballot(fire);
-    if (!m) continue;
-    unsigned long long base = 0;
-    const int leader = __ffsll((long long)m) - 1;
-    if ((int)__lane_id() == leader) base = atomicAdd(&st->out_rows, (unsigned long long)__popcll(m));
-    base = __shfl(base, leader, 64);
-    if (!fire) continue;
-    const unsigned long long pos = base + __popcll(m & lanemask_lt());
-    if ((int64_t)pos < out.cap) {
-      out.key[pos] = e.key;
-      out.start[pos] = e.start;
-      out.end[pos] = e.end;
-      out.cnt[pos] = e.cnt;
-      out.sum[pos] = e.sum;
-      out.mn[pos] = e.mn;
-      out.mx[pos] = e.mx;
-    } else {
-      atomicOr(&st->flags, FW_STATUS_OUT_FULL);
-    }
+    __syncthreads();  // (base_s is rewritten by the next chunk)
   }
 }
 // after every fire of the batch read them: the key's ring takes its last wl - 1 elements, its count the run's length
@@ -5730,7 +5760,11 @@ void launch_count(const DevCfg& c, DevCount& cw, const int64_t* key, const int64
   const uint32_t* sk = ks.current();
   const uint32_t* sv = vs.current();
   hipLaunchKernelGGL(k_cnt_bounds, dim3(grid), dim3(256), 0, s, cw, sk, n, none);
-  hipLaunchKernelGGL(k_cnt_fire, dim3(grid), dim3(256), 0, s, c, cw, sk, sv, key, val, n, none, out, st);
+  uint32_t* vlo = ks.alternate();  // (the sort's spare halves)
+  uint32_t* vhi = vs.alternate();
+  hipLaunchKernelGGL(k_cnt_gather, dim3(grid), dim3(256), 0, s, sk, sv, val, n, none, vlo, vhi);
+  hipLaunchKernelGGL(k_cnt_fire, dim3((unsigned)std::min<int64_t>(8192, (n + CF_CHUNK - 1) / CF_CHUNK)), dim3(256), 0, s,
+                     c, cw, sk, sv, key, vlo, vhi, n, none, out, st);
   hipLaunchKernelGGL(k_cnt_update, dim3(grid), dim3(256), 0, s, c, cw, sk, sv, val, n, none);
   hipLaunchKernelGGL(k_cnt_count, dim3(grid), dim3(256), 0, s, cw, sk, n, none);
 }
