@@ -427,15 +427,22 @@ __device__ int64_t evict(const LCfg& c, const LState& S, const LView& V, int64_t
 
 // emitWindowContents (:334-366) of group g over the list [a .. j] of the view: evictBefore, one row (+ the
 // elements), evictAfter.  False (nothing changed) when the element buffer cannot take the contents.
-__device__ bool emit_firing(const LCfg& c, const LState& S, const LView& V, uint32_t g, int64_t a, int64_t j,
-                            bool room) {
+// rsv_row >= 0: the row and the elements were reserved by the caller (k_walk's wave-aggregated reservation).
+__device__ __forceinline__ int64_t fired_count(const LCfg& c, const LState& S, const LView& V, int64_t a, int64_t j) {
   int64_t cnt = 0;  // the elements the function sees
   if (c.evict_after)
     for (int64_t q = a; q <= j; q++) cnt += V.alive[q];
   else
     cnt = evict(c, S, V, a, j, false);
+  return cnt;
+}
+__device__ bool emit_firing(const LCfg& c, const LState& S, const LView& V, uint32_t g, int64_t a, int64_t j,
+                            bool room, int64_t rsv_row = -1, int64_t rsv_elem = 0, int64_t rsv_cnt = 0) {
+  const int64_t cnt = rsv_row >= 0 ? rsv_cnt : fired_count(c, S, V, a, j);
   int64_t eoff = 0;
-  if (c.emit && cnt && room) {  // the host sized the element buffer for every possible firing
+  if (rsv_row >= 0) {
+    eoff = c.emit && cnt ? rsv_elem : 0;
+  } else if (c.emit && cnt && room) {  // the host sized the element buffer for every possible firing
     eoff = (int64_t)atomicAdd(&S.ctr->elems, (unsigned long long)cnt);
   } else if (c.emit && cnt) {  // reserve the elements (rows were sized by the host: one per possible firing)
     unsigned long long cur = __hip_atomic_load(&S.ctr->elems, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -475,7 +482,7 @@ __device__ bool emit_firing(const LCfg& c, const LState& S, const LView& V, uint
     }
     k++;
   }
-  const unsigned long long r = atomicAdd(&S.ctr->rows, 1ull);
+  const unsigned long long r = rsv_row >= 0 ? (unsigned long long)rsv_row : atomicAdd(&S.ctr->rows, 1ull);
   S.rkey[r] = S.g[g].key;
   S.rstart[r] = S.g[g].start;
   S.rend[r] = w_end(c, S.g[g].start);
@@ -529,6 +536,44 @@ __global__ __launch_bounds__(256) void k_walk(LCfg c, LState S, LView V, const u
                                               const uint32_t* __restrict__ seg, int64_t nseg, int64_t base_new,
                                               int64_t wm, int64_t* __restrict__ prog, bool room) {
   const uint32_t* __restrict__ pos = V.pos;
+  if (!PUSH && room) {  // a watermark with room for every firing: one reservation of rows and elements per wave
+    const int lane = __lane_id();
+    for (int64_t s0 = (int64_t)blockIdx.x * blockDim.x; s0 < nseg; s0 += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t s = s0 + threadIdx.x;
+      int64_t a = 0, b = 0;
+      uint32_t g = 0;
+      bool act = false;
+      if (s < nseg) {
+        a = seg[s];
+        b = seg[s + 1];
+        g = keys[a];
+        act = (S.g[g].fl & GF_FIRE) != 0;
+      }
+      const int64_t cnt = act ? fired_count(c, S, V, a, b - 1) : 0;
+      const unsigned long long rr = act ? 1ull : 0ull, ee = act && c.emit ? (unsigned long long)cnt : 0ull;
+      unsigned long long xr = rr, xe = ee;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long yr = __shfl_up(xr, o, 64), ye = __shfl_up(xe, o, 64);
+        if (lane >= o) {
+          xr += yr;
+          xe += ye;
+        }
+      }
+      unsigned long long br = 0, be = 0;
+      if (lane == 63) {
+        if (xr) br = atomicAdd(&S.ctr->rows, xr);
+        if (xe) be = atomicAdd(&S.ctr->elems, xe);
+      }
+      br = __shfl(br, 63, 64);
+      be = __shfl(be, 63, 64);
+      if (!act) continue;
+      emit_firing(c, S, V, g, a, b - 1, true, (int64_t)(br + xr - rr), (int64_t)(be + xe - ee), cnt);
+      if (c.purging) purge(S, V, a, b - 1);
+      atomicAnd(&S.g[g].fl, ~GF_FIRE);
+    }
+    return;
+  }
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = seg[s], b = seg[s + 1];
     const uint32_t g = keys[a];
