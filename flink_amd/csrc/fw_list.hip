@@ -241,6 +241,7 @@ __global__ __launch_bounds__(256) void k_lp_append(LCfg c, LState S, const int64
                                                    int64_t base, int64_t ord_base, unsigned long long limit) {
   long long due = LMAX;  // the earliest timer these entries register
   unsigned ins = 0;
+  bool seq = false;      // some entry fires while being processed (one store per workgroup, not per entry)
   // one entry: its payload and group, and the trigger's bookkeeping (fl: the group's flags as last read)
   auto put = [&](int64_t idx, int64_t i, int64_t t, int64_t v, int64_t s, int32_t g, uint32_t fl) {
     S.lpay[idx] = LPay{t, v, ord_base + i, 0};
@@ -253,7 +254,7 @@ __global__ __launch_bounds__(256) void k_lp_append(LCfg c, LState S, const int64
     due = min(due, (long long)(c.trigger == FW_TRIGGER_EVENT_TIME && mts > wm ? mts : w_cleanup(c, s)));
     if (c.trigger == FW_TRIGGER_COUNT || mts <= wm) {  // CountTrigger / late firing
       atomicOr(&S.g[g].fl, GF_TOUCH);
-      S.ctr->need_seq = 1u;
+      seq = true;
     } else if (!(fl & GF_TIMER)) {  // EventTimeTrigger.onElement registers the timer at maxTimestamp
       atomicOr(&S.g[g].fl, GF_TIMER);
     }
@@ -320,6 +321,7 @@ __global__ __launch_bounds__(256) void k_lp_append(LCfg c, LState S, const int64
       });
     }
   }
+  if (__syncthreads_or(seq) && threadIdx.x == 0) S.ctr->need_seq = 1u;
   block_min(&S.ctr->next_due, due);
   block_add(&S.ctr->live_groups, ins);
 }
