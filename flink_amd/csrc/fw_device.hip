@@ -3196,16 +3196,21 @@ __device__ int32_t td_finish(const DevCfg& c, const DevRows& out, uint64_t row, 
   return h.n;
 }
 
-// sort keys of every batch position: (global slot of the record's entry, value key); positions past the
-// partitioned records get the slot `none` (sorted last, skipped)
+// sort keys of every batch position: one 64-bit key (pool block of the record's digest in the top B bits, the
+// value key's high 64 - B bits below) and the value key's low B bits as the payload, so one radix sort groups a
+// digest's values and orders them up to ties in the high bits (k_td_fix orders those by the low bits). Positions
+// past the partitioned records get the block `nblk` (sorted last, skipped). binv[blk] = the digest's global slot.
 constexpr int TD_CHUNK = 4096;
 __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restrict__ part, const uint32_t* __restrict__ offs,
-                                                 int32_t T, int64_t n, DevTable tb, uint32_t none, uint32_t* __restrict__ gs,
-                                                 uint64_t* __restrict__ vk, Status* st) {
+                                                 int32_t T, int64_t n, DevTable tb, uint32_t nblk, int B,
+                                                 uint32_t* __restrict__ pay, uint64_t* __restrict__ key64,
+                                                 uint32_t* __restrict__ binv, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int64_t total = offs[(int64_t)c.P * T];
   const int64_t i0 = (int64_t)blockIdx.x * TD_CHUNK;
   const int64_t i1 = min(n, i0 + (int64_t)TD_CHUNK);
+  const uint64_t none_key = (uint64_t)nblk << (64 - B);
+  const uint64_t low = (B >= 64) ? ~0ull : ((1ull << B) - 1ull);
   __shared__ int32_t p0_s;
   if (threadIdx.x == 0) {  // partition of the chunk's first record: last p with offs[p*T] <= i0
     int32_t lo = 0, hi = c.P - 1;
@@ -3223,8 +3228,8 @@ __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restric
   int32_t pp = p0_s;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     if (i >= total) {
-      gs[i] = none;
-      vk[i] = 0;
+      key64[i] = none_key;
+      pay[i] = 0;
       continue;
     }
     while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
@@ -3240,12 +3245,77 @@ __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restric
     const int32_t slot = region_find(r, slot_hash(c, rec.key, rec.last), rec.key, rec.last, wend(c, rec.last));
     if (slot < 0) {
       atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's window
-      gs[i] = none;
-      vk[i] = 0;
+      key64[i] = none_key;
+      pay[i] = 0;
       continue;
     }
-    gs[i] = ((uint32_t)pp << c.log_r) | (uint32_t)slot;
-    vk[i] = td_key(rec.val);
+    const uint32_t g = ((uint32_t)pp << c.log_r) | (uint32_t)slot;
+    const uint64_t blk = pool_block_of(r.ent[slot]);
+    // every record of a digest stores the same slot, so a stale (cached) read costs one redundant store at most;
+    // a hot digest's records read it (an L1 hit) and store nothing
+    if (binv[blk] != g) binv[blk] = g;
+    const uint64_t k = td_key(rec.val);
+    key64[i] = (blk << (64 - B)) | (k >> B);
+    pay[i] = (uint32_t)(k & low);
+  }
+}
+
+// tie runs: positions with the previous one's key (one digest, equal high value bits) and a smaller payload mark
+// their run's first position in fixbm; k_td_fix_runs then orders each marked run by payload
+__global__ __launch_bounds__(256) void k_td_fix_mark(int64_t n, const uint64_t* __restrict__ key64,
+                                                     const uint32_t* __restrict__ pay, uint32_t* __restrict__ fixbm) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = key64[i];
+    if (k != key64[i - 1] || pay[i] >= pay[i - 1]) continue;
+    int64_t s = i - 1;
+    while (s > 0 && key64[s - 1] == k) s--;
+    atomicOr(&fixbm[s >> 5], 1u << (s & 31));
+  }
+}
+__device__ void td_sift(uint32_t* a, int64_t root, int64_t len) {
+  while (2 * root + 1 < len) {
+    int64_t ch = 2 * root + 1;
+    if (ch + 1 < len && a[ch + 1] > a[ch]) ch++;
+    if (a[root] >= a[ch]) return;
+    const uint32_t t = a[root];
+    a[root] = a[ch];
+    a[ch] = t;
+    root = ch;
+  }
+}
+__global__ __launch_bounds__(256) void k_td_fix_runs(int64_t n, const uint64_t* __restrict__ key64,
+                                                     uint32_t* __restrict__ pay, const uint32_t* __restrict__ fixbm) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
+    if (!((fixbm[s >> 5] >> (s & 31)) & 1u)) continue;
+    const uint64_t k = key64[s];
+    int64_t e = s + 1;
+    while (e < n && key64[e] == k) e++;
+    uint32_t* a = pay + s;
+    const int64_t len = e - s;
+    for (int64_t r = len / 2 - 1; r >= 0; r--) td_sift(a, r, len);  // heapsort: bounded for any run
+    for (int64_t m = len - 1; m > 0; m--) {
+      const uint32_t t = a[0];
+      a[0] = a[m];
+      a[m] = t;
+      td_sift(a, 0, m);
+    }
+  }
+}
+// the sorted keys back to (global slot, value key) columns for the tiers
+__global__ __launch_bounds__(256) void k_td_decode(int64_t n, int B, uint32_t nblk, uint32_t none,
+                                                   const uint64_t* __restrict__ key64, const uint32_t* __restrict__ pay,
+                                                   const uint32_t* __restrict__ binv, uint32_t* __restrict__ gs,
+                                                   uint64_t* __restrict__ v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = key64[i];
+    const uint32_t blk = (uint32_t)(k >> (64 - B));
+    if (blk == nblk) {
+      gs[i] = none;
+      v[i] = 0;
+    } else {
+      gs[i] = binv[blk];
+      v[i] = (k << B) | (uint64_t)pay[i];
+    }
   }
 }
 
@@ -5769,31 +5839,36 @@ void launch_count(const DevCfg& c, DevCount& cw, const int64_t* key, const int64
   hipLaunchKernelGGL(k_cnt_count, dim3(grid), dim3(256), 0, s, cw, sk, n, none);
 }
 size_t tdigest_sort_bytes(int64_t n) {
-  size_t a = 0, b = 0;
+  size_t a = 0;
   rocprim::double_buffer<uint64_t> kv(nullptr, nullptr);
   rocprim::double_buffer<uint32_t> ks(nullptr, nullptr);
   (void)rocprim::radix_sort_pairs(nullptr, a, kv, ks, (size_t)n, 0, 64);
-  (void)rocprim::radix_sort_pairs(nullptr, b, ks, kv, (size_t)n, 0, 32);
-  return std::max(a, b);
+  return a;
 }
 void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
                     TdBuf& td, Status* st, hipStream_t s) {
   if (n <= 0) return;
   const uint32_t none = (uint32_t)td.lidx_slots;  // no slot has this id (slots are 0 .. table slots - 1)
-  unsigned bits = 1;
-  while (((int64_t)1 << bits) <= td.lidx_slots) bits++;
+  const uint32_t nblk = (uint32_t)c.pool_blocks;   // no block has this id
+  int B = 1;
+  while (((int64_t)1 << B) <= c.pool_blocks) B++;
   (void)hipMemsetAsync(td.ctr, 0, 3 * sizeof(int32_t), s);
+  (void)hipMemsetAsync(td.fixbm, 0, (size_t)((n + 31) / 32) * sizeof(uint32_t), s);
   hipLaunchKernelGGL(k_td_keys, dim3((unsigned)((n + TD_CHUNK - 1) / TD_CHUNK)), dim3(256), 0, s, c, part, offs, T, n,
-                     tb, none, td.gs[0], td.v[0], st);
-  // by value, then stably by slot: each digest's batch values become one run in Double.compare order
+                     tb, nblk, B, td.gs[0], td.v[0], td.binv, st);
+  // one sort by (pool block, high value bits): each digest's batch values become one run, in Double.compare
+  // order once the tie runs are ordered by their low bits
   rocprim::double_buffer<uint64_t> kv(td.v[0], td.v[1]);
   rocprim::double_buffer<uint32_t> ks(td.gs[0], td.gs[1]);
   size_t bytes = td.tmp_bytes;
   (void)rocprim::radix_sort_pairs(td.tmp, bytes, kv, ks, (size_t)n, 0, 64, s);
-  (void)rocprim::radix_sort_pairs(td.tmp, bytes, ks, kv, (size_t)n, 0, bits, s);
-  const uint32_t* gsorted = ks.current();
-  const uint64_t* vsorted = kv.current();
   const unsigned grid = (unsigned)std::min<int64_t>(8192, (n + 255) / 256);
+  hipLaunchKernelGGL(k_td_fix_mark, dim3(grid), dim3(256), 0, s, n, kv.current(), ks.current(), td.fixbm);
+  hipLaunchKernelGGL(k_td_fix_runs, dim3(grid), dim3(256), 0, s, n, kv.current(), ks.current(), td.fixbm);
+  uint32_t* gsorted = ks.alternate();
+  uint64_t* vsorted = kv.alternate();
+  hipLaunchKernelGGL(k_td_decode, dim3(grid), dim3(256), 0, s, n, B, nblk, none, kv.current(), ks.current(), td.binv,
+                     gsorted, vsorted);
   const int64_t per_block = 256 * TD_BOUNDS_PER_THREAD;
   hipLaunchKernelGGL(k_td_bounds, dim3((unsigned)((n + per_block - 1) / per_block)), dim3(256), 0, s, n, gsorted, none,
                      td, st);

@@ -301,8 +301,10 @@ struct TdLarge {  // a digest whose batch is compressed bucket-parallel
   TdHead* head;
 };
 struct TdBuf {
-  uint32_t* gs[2];          // sort keys: global slot (partition << log_r | slot) of each record's entry
-  uint64_t* v[2];           // sort keys: Double.compare-ordered value
+  uint32_t* gs[2];          // low value bits (sort payload), then the global slot (partition << log_r | slot)
+  uint64_t* v[2];           // (pool block, high value bits) sort keys, then the Double.compare-ordered value
+  uint32_t* binv;           // [pool blocks] global slot of each block's entry (rewritten when it moved)
+  uint32_t* fixbm;          // [max_batch / 32] tie runs whose low value bits need sorting
   void* tmp;                // rocPRIM radix-sort scratch
   size_t tmp_bytes;
   uint32_t* tslot;          // touched digests: global slot      [max_batch]

@@ -1051,6 +1051,9 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     }
     t.tmp_bytes = fwdev::tdigest_sort_bytes(mb);
     HIP_OR_RETURN(op, dmalloc((uint8_t**)&t.tmp, t.tmp_bytes));
+    HIP_OR_RETURN(op, dmalloc(&t.binv, (size_t)c.pool_blocks));
+    HIP_OR_RETURN(op, hipMemsetAsync(t.binv, 0xff, (size_t)c.pool_blocks * sizeof(uint32_t), op->stream));
+    HIP_OR_RETURN(op, dmalloc(&t.fixbm, (size_t)((mb + 31) / 32)));
     HIP_OR_RETURN(op, dmalloc(&t.tslot, (size_t)mb));
     HIP_OR_RETURN(op, dmalloc(&t.tbeg, (size_t)mb));
     HIP_OR_RETURN(op, dmalloc(&t.ctr, 3));
@@ -1147,6 +1150,8 @@ void fw_destroy(fw_op* op) {
     }
     uint8_t* tmp = (uint8_t*)t.tmp;
     dfree(tmp);
+    dfree(t.binv);
+    dfree(t.fixbm);
     dfree(t.tslot);
     dfree(t.tbeg);
     dfree(t.ctr);

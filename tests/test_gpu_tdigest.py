@@ -21,6 +21,12 @@ def _stream(n, batch, num_keys, rate, zipf=None, values="spread", seed=0x7D16, b
     keys, ts, raw = generate_host(seed, 0, n, num_keys, ts_base=1_000_000, rate=rate, jitter=jitter, zipf_s=zipf)
     if values == "spread":
         vals = (raw & 0xFFFFFF).astype(np.float64) / 7.0 - 1.0e6  # distinct-ish, negative and positive
+    elif values == "lowbits":
+        # 16 bases of both signs whose values differ only in their 10 lowest mantissa bits: they tie in the
+        # sort key's high bits and are ordered by its low bits (k_td_fix_*; long runs in the hot digests)
+        base = np.array([-1.0e6, -3.5, -0.75, -1e-3, 0.0, 1e-3, 0.625, 2.25, 9.0, 1e2, 3.3e3, 7e5, 1e6, -7e5, 4e9, -4e9])
+        bits = base.view(np.int64)[(raw >> 12) & 15] ^ (raw & 0x3FF)
+        vals = bits.view(np.float64)
     else:
         vals = (raw & 0x3F).astype(np.float64) * 0.5  # 64 distinct values: ties with each other and with means
     batches, wms, mx = [], [], -(1 << 63)
@@ -71,14 +77,15 @@ def _assert_same(g_rows, g_dig, r_rows, r_dig, delta):
 
 
 @pytest.mark.parametrize("delta", [100, 20])
-def test_gpu_tdigest_serial_digests(delta):
+@pytest.mark.parametrize("values", ["spread", "lowbits"])
+def test_gpu_tdigest_serial_digests(delta, values):
     # uniform keys: every digest gets a few values per push (the serial merge)
-    batches, wms = _stream(300_000, 60_000, 20_000, rate=200_000)
+    batches, wms = _stream(300_000, 60_000, 20_000, rate=200_000, values=values)
     out = _run(batches, wms, delta, expected_entries=60_000)
     _assert_same(*out, delta)
 
 
-@pytest.mark.parametrize("delta,values", [(100, "spread"), (100, "ties"), (30, "spread")])
+@pytest.mark.parametrize("delta,values", [(100, "spread"), (100, "ties"), (30, "spread"), (100, "lowbits")])
 def test_gpu_tdigest_hot_digests(delta, values):
     # Zipf(1.1) over 1000 keys in 200K-record pushes: the hottest digests take tens of thousands of values per
     # push and are merged bucket-parallel; "ties" draws 64 distinct values, so values tie with each other and
