@@ -3013,16 +3013,22 @@ __device__ __forceinline__ TdCent* td_half(const DevCfg& c, uint64_t blk, int h)
   return reinterpret_cast<TdCent*>(c.pool + blk * (uint64_t)c.pool_bytes + sizeof(TdHead)) + (int64_t)h * c.td_nb;
 }
 // bucket of an item's midpoint: the largest b < nb with W * qb[b] <= mid
-__device__ __forceinline__ int td_bucket(const DevCfg& c, double W, double mid) {
+// (qb: the quantile bounds, staged in LDS by the kernels: td_stage_qb)
+__device__ __forceinline__ int td_bucket(const DevCfg& c, const double* qb, double W, double mid) {
   int lo = 0, hi = c.td_nb - 1;
   while (lo < hi) {
     const int m = (lo + hi + 1) >> 1;
-    if (W * c.td_qb[m] <= mid)
+    if (W * qb[m] <= mid)
       lo = m;
     else
       hi = m - 1;
   }
   return lo;
+}
+// the workgroup's copy of the quantile bounds (every thread of the workgroup calls it)
+__device__ __forceinline__ void td_stage_qb(const DevCfg& c, double* s_qb) {
+  for (int b = threadIdx.x; b < c.td_nb; b += blockDim.x) s_qb[b] = c.td_qb[b];
+  __syncthreads();
 }
 __device__ __forceinline__ int64_t td_weight(const TdCent* ce, int32_t j) { return ce[j].cum - (j ? ce[j - 1].cum : 0); }
 // a left-to-right fold of partial sums (`any` = something folded yet)
@@ -3098,8 +3104,9 @@ __device__ double td_wave_new_sum(const uint64_t* __restrict__ v, int64_t ns, in
 }
 
 // serial merge of nn sorted values v[beg ..] with the no centroids `old` into `out` (window_oracle.cpp td_compress)
-__device__ int32_t td_merge_serial(const DevCfg& c, const uint64_t* __restrict__ v, int64_t beg, int64_t nn,
-                                   const TdCent* __restrict__ old, int32_t no, TdCent* __restrict__ out, int64_t W) {
+__device__ int32_t td_merge_serial(const DevCfg& c, const double* qb, const uint64_t* __restrict__ v, int64_t beg,
+                                   int64_t nn, const TdCent* __restrict__ old, int32_t no, TdCent* __restrict__ out,
+                                   int64_t W) {
   const double Wd = (double)W;
   int64_t i = 0, cw = 0, gw = 0, cum_out = 0, prev_old = 0;
   int32_t j = 0, k = 0;
@@ -3133,7 +3140,7 @@ __device__ int32_t td_merge_serial(const DevCfg& c, const uint64_t* __restrict__
       if (j < no) mk = td_mean_key(old[j].sum, old[j].cum - prev_old);
     }
     const double mid = (double)cw + (double)w * 0.5;
-    while (b + 1 < c.td_nb && Wd * c.td_qb[b + 1] <= mid) b++;
+    while (b + 1 < c.td_nb && Wd * qb[b + 1] <= mid) b++;
     if (b != cur && gw > 0) emit();
     cur = b;
     if (take_new) {
@@ -3373,7 +3380,7 @@ __global__ __launch_bounds__(256) void k_td_small(DevCfg c, DevTable tb, TdBuf t
       TdCent* out = td_half(c, blk, h.cur ^ 1);
       td.lidx[g] = -1;
       if (nn + h.n <= FW_TD_T1) {
-        const int32_t k = td_merge_serial(c, v, beg, nn, old, h.n, out, W);
+        const int32_t k = td_merge_serial(c, c.td_qb, v, beg, nn, old, h.n, out, W);
         *hp = TdHead{h.cur ^ 1, k, W};
       } else if (nn + h.n <= FW_TD_T3) {
         mid = true;
@@ -3405,8 +3412,8 @@ __global__ __launch_bounds__(256) void k_td_small(DevCfg c, DevTable tb, TdBuf t
 
 // placement of one value: the old centroids whose mean is below it precede it (a value goes before an equal
 // mean); keys/cum: the old centroids' mean keys and cumulative weights
-__device__ __forceinline__ int td_bucket_new(const DevCfg& c, const uint64_t* keys, const int64_t* cum, int32_t no,
-                                             double W, int64_t r, uint64_t vkey) {
+__device__ __forceinline__ int td_bucket_new(const DevCfg& c, const double* qb, const uint64_t* keys, const int64_t* cum,
+                                             int32_t no, double W, int64_t r, uint64_t vkey) {
   int32_t lo = 0, hi = no;  // first old centroid whose mean key >= vkey
   while (lo < hi) {
     const int32_t m = (lo + hi) >> 1;
@@ -3416,11 +3423,12 @@ __device__ __forceinline__ int td_bucket_new(const DevCfg& c, const uint64_t* ke
       hi = m;
   }
   const int64_t cw = r + (lo ? cum[lo - 1] : 0);
-  return td_bucket(c, W, (double)cw + 0.5);
+  return td_bucket(c, qb, W, (double)cw + 0.5);
 }
 // placement of old centroid j: the values <= its mean precede it (binary search in the digest's sorted run)
-__device__ __forceinline__ int td_bucket_old(const DevCfg& c, const uint64_t* __restrict__ v, int64_t beg, int64_t nn,
-                                             uint64_t mk, int64_t cum_before, int64_t w, double W) {
+__device__ __forceinline__ int td_bucket_old(const DevCfg& c, const double* qb, const uint64_t* __restrict__ v,
+                                             int64_t beg, int64_t nn, uint64_t mk, int64_t cum_before, int64_t w,
+                                             double W) {
   int64_t lo = 0, hi = nn;
   while (lo < hi) {
     const int64_t m = (lo + hi) >> 1;
@@ -3429,26 +3437,37 @@ __device__ __forceinline__ int td_bucket_old(const DevCfg& c, const uint64_t* __
     else
       hi = m;
   }
-  return td_bucket(c, W, (double)(lo + cum_before) + (double)w * 0.5);
+  return td_bucket(c, qb, W, (double)(lo + cum_before) + (double)w * 0.5);
 }
 
-// the wave tier: one wave per digest (its old centroids and bucket starts in LDS)
+// the wave tier: one wave per digest (its old centroids and bucket starts in LDS).  LDS per wave (dynamic,
+// td_wave_lds_bytes): the old centroids' mean keys (then their sums), cumulative weights, each bucket's first
+// value / first old centroid / where its runs end / its first block, and the tree sums of the batch values'
+// blocks (a digest's nn <= FW_TD_T3 values form at most FW_TD_T3 / 64 + nb blocks)
 constexpr int TD_WAVES = 4;
+__host__ __device__ constexpr int td_wave_blocks(int nb) { return FW_TD_T3 / 64 + nb + 1; }
+__host__ __device__ constexpr size_t td_wave_lds_wave(int nb) {
+  return (8 * (size_t)(4 * nb + 1 + td_wave_blocks(nb)) + 4 * (size_t)(3 * nb + 1) + 7) & ~(size_t)7;
+}
+size_t td_wave_lds_bytes(int nb) { return TD_WAVES * td_wave_lds_wave(nb); }
 __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb, TdBuf td, const uint64_t* __restrict__ v,
                                                            Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  __shared__ uint64_t s_key[TD_WAVES][TD_NB_MAX];
-  __shared__ int64_t s_cum[TD_WAVES][TD_NB_MAX];
-  __shared__ int64_t s_ns[TD_WAVES][TD_NB_MAX + 1];  // first value of each bucket (-1: none), then its end
-  __shared__ int32_t s_os[TD_WAVES][TD_NB_MAX + 1];
-  __shared__ int64_t s_en[TD_WAVES][TD_NB_MAX];  // where each bucket's runs end: the next bucket's starts
-  __shared__ int32_t s_eo[TD_WAVES][TD_NB_MAX];
+  extern __shared__ __align__(8) uint8_t td_lds[];
+  __shared__ double s_qb[TD_NB_MAX];
+  td_stage_qb(c, s_qb);
   const int wv = threadIdx.x >> 6, lane = __lane_id();
   const int nb = c.td_nb;
-  uint64_t* keys = s_key[wv];
-  int64_t* cum = s_cum[wv];
-  int64_t* ns = s_ns[wv];
-  int32_t* os = s_os[wv];
+  uint8_t* base = td_lds + (size_t)wv * td_wave_lds_wave(nb);
+  uint64_t* keys = reinterpret_cast<uint64_t*>(base);                 // [nb]; the old sums after the placement
+  double* osum = reinterpret_cast<double*>(base);
+  int64_t* cum = reinterpret_cast<int64_t*>(base) + nb;               // [nb]
+  int64_t* ns = cum + nb;                                             // [nb + 1] first value of each bucket (-1: none)
+  int64_t* s_en = ns + nb + 1;                                        // [nb] where each bucket's runs end
+  double* bsum = reinterpret_cast<double*>(s_en + nb);                // [td_wave_blocks(nb)]
+  int32_t* os = reinterpret_cast<int32_t*>(bsum + td_wave_blocks(nb));  // [nb + 1] first old centroid (-1: none)
+  int32_t* s_eo = os + nb + 1;                                        // [nb]
+  int32_t* bst = s_eo + nb;                                           // [nb] first block of each bucket
   const int32_t nmid = td.ctr[2];
   const uint32_t mask = (1u << c.log_r) - 1u;
   for (int32_t q = blockIdx.x * TD_WAVES + wv; q < nmid; q += gridDim.x * TD_WAVES) {
@@ -3465,10 +3484,17 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
       d = TdLarge{td.tbeg[idx], e.cnt - h.w, e.cnt, h.n, h.cur ^ 1, td_half(c, blk, h.cur), td_half(c, blk, h.cur ^ 1), hp};
     }
     const double W = (double)d.W;
-    for (int32_t j = lane; j < d.no; j += 64) {
-      const int64_t w = td_weight(d.old, j);
-      keys[j] = td_mean_key(d.old[j].sum, w);
-      cum[j] = d.old[j].cum;
+    double my_osum[4];  // this lane's old sums (j = lane + 64 u), staged into LDS once the keys are no longer read
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int32_t j = lane + 64 * u;
+      if (j < d.no) {
+        const TdCent cj = d.old[j];
+        const int64_t w = cj.cum - (j ? d.old[j - 1].cum : 0);
+        keys[j] = td_mean_key(cj.sum, w);
+        cum[j] = cj.cum;
+        my_osum[u] = cj.sum;
+      }
     }
     for (int b = lane; b < nb; b += 64) {
       ns[b] = -1;
@@ -3481,7 +3507,7 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
     for (int64_t i0 = 0; i0 < d.nn; i0 += 64) {
       const int64_t i = i0 + lane;
       int b = -1;
-      if (i < d.nn) b = td_bucket_new(c, keys, cum, d.no, W, i, v[d.beg + i]);
+      if (i < d.nn) b = td_bucket_new(c, s_qb, keys, cum, d.no, W, i, v[d.beg + i]);
       int prev = __shfl_up(b, 1, 64);
       if (lane == 0) prev = carry;
       if (i < d.nn && prev != b) ns[b] = d.beg + i;
@@ -3491,7 +3517,7 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
     for (int32_t j0 = 0; j0 < d.no; j0 += 64) {
       const int32_t j = j0 + lane;
       int b = -1;
-      if (j < d.no) b = td_bucket_old(c, v, d.beg, d.nn, keys[j], j ? cum[j - 1] : 0, td_weight(d.old, j), W);
+      if (j < d.no) b = td_bucket_old(c, s_qb, v, d.beg, d.nn, keys[j], j ? cum[j - 1] : 0, td_weight(d.old, j), W);
       int prev = __shfl_up(b, 1, 64);
       if (lane == 0) prev = carry;
       if (j < d.no && prev != b) os[b] = j;
@@ -3499,6 +3525,9 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (lane + 64 * u < d.no) osum[lane + 64 * u] = my_osum[u];  // (the keys are read no more)
     // the end of every bucket's runs = the start of the next bucket that has one (the starts grow with the
     // bucket): an exclusive suffix minimum over the buckets, 64 at a time from the last chunk down
     {
@@ -3523,8 +3552,8 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
           eo = INT32_MAX;
         }
         if (b < nb) {
-          s_en[wv][b] = min(en, carry_n);
-          s_eo[wv][b] = min(eo, carry_o);
+          s_en[b] = min(en, carry_n);
+          s_eo[b] = min(eo, carry_o);
         }
         carry_n = min(carry_n, __shfl(xn, 0, 64));
         carry_o = min(carry_o, __shfl(xo, 0, 64));
@@ -3532,28 +3561,87 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    // buckets in order: each non-empty one is a centroid
-    int64_t cum_out = 0, end_n;
-    int32_t k = 0, end_o;
-    for (int b = 0; b < nb; b++) {
-      const int64_t sn = ns[b];
-      const int32_t so = os[b];
-      if (sn < 0 && so < 0) continue;
-      end_n = s_en[wv][b];
-      end_o = s_eo[wv][b];
-      const int64_t a_n = sn >= 0 ? sn : end_n;
-      const int32_t a_o = so >= 0 ? so : end_o;
-      double s_new = 0.0, s_old = 0.0;
-      bool any_o = false;
-      const bool any_n = end_n > a_n;
-      if (any_n) s_new = td_wave_new_sum(v, a_n, end_n);
-      for (int32_t j = a_o; j < end_o; j++) td_fold(s_old, any_o, d.old[j].sum);
-      const int64_t w = (end_n - a_n) + (end_o > a_o ? cum[end_o - 1] - (a_o ? cum[a_o - 1] : 0) : 0);
-      cum_out += w;
-      if (lane == 0) d.out[k] = TdCent{any_o && any_n ? s_old + s_new : any_o ? s_old : s_new, cum_out};
-      k++;
+    // each bucket's blocks of 64 new values (from its first value): bst = exclusive prefix of the block counts
+    int32_t nblocks = 0;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+      const int b = b0 + lane;
+      int32_t cnt = 0;
+      if (b < nb && ns[b] >= 0) cnt = (int32_t)((s_en[b] - ns[b] + 63) >> 6);
+      int32_t x = cnt;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (b < nb) bst[b] = nblocks + x - cnt;
+      nblocks += __shfl(x, 63, 64);
     }
-    if (lane == 0) *d.head = TdHead{d.pad, k, d.W};
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // every block's tree sum, four blocks' values in flight (the same trees as td_wave_new_sum's)
+    {
+      int bk = 0;  // bucket of block k (blocks are in bucket order)
+      for (int32_t k0 = 0; k0 < nblocks; k0 += 4) {
+        double x[4];
+        bool has[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int32_t k = k0 + u;
+          has[u] = false;
+          x[u] = 0.0;
+          if (k < nblocks) {
+            // (blocks are in bucket order; a bucket without new values owns none)
+            while (ns[bk] < 0 || k >= bst[bk] + (int32_t)((s_en[bk] - ns[bk] + 63) >> 6)) bk++;
+            const int64_t start = ns[bk] + (int64_t)(k - bst[bk]) * 64;
+            has[u] = start + lane < s_en[bk];
+            if (has[u]) x[u] = td_val(v[start + lane]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if (k0 + u >= nblocks) break;
+          const double t = td_wave_tree(x[u], has[u]);
+          if (lane == 0) bsum[k0 + u] = t;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // buckets in order, a lane per bucket: each non-empty one is a centroid
+    int32_t kbase = 0;
+    int64_t cbase = 0;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+      const int b = b0 + lane;
+      const bool live = b < nb && (ns[b] >= 0 || os[b] >= 0);
+      double sum = 0.0;
+      int64_t w = 0;
+      if (live) {
+        const int64_t sn = ns[b];
+        const int32_t so = os[b];
+        const int64_t end_n = s_en[b];
+        const int32_t end_o = s_eo[b];
+        const int64_t a_n = sn >= 0 ? sn : end_n;
+        const int32_t a_o = so >= 0 ? so : end_o;
+        double s_new = 0.0, s_old = 0.0;
+        bool any_n = false, any_o = false;
+        if (sn >= 0) {
+          const int32_t k1 = bst[b] + (int32_t)((end_n - sn + 63) >> 6);
+          for (int32_t k = bst[b]; k < k1; k++) td_fold(s_new, any_n, bsum[k]);
+        }
+        for (int32_t j = a_o; j < end_o; j++) td_fold(s_old, any_o, osum[j]);
+        sum = any_o && any_n ? s_old + s_new : any_o ? s_old : s_new;
+        w = (end_n - a_n) + (end_o > a_o ? cum[end_o - 1] - (a_o ? cum[a_o - 1] : 0) : 0);
+      }
+      const uint64_t m = __ballot(live);
+      int64_t x = w;  // inclusive prefix of the weights
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (live) d.out[kbase + __popcll(m & lanemask_lt())] = TdCent{sum, cbase + x};
+      kbase += __popcll(m);
+      cbase += __shfl(x, 63, 64);
+    }
+    if (lane == 0) *d.head = TdHead{d.pad, kbase, d.W};
     __builtin_amdgcn_wave_barrier();
   }
 }
@@ -3562,6 +3650,8 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
 __global__ __launch_bounds__(256) void k_td_large_items(DevCfg c, int64_t n, const uint32_t* __restrict__ gs,
                                                         const uint64_t* __restrict__ v, uint32_t none, TdBuf td, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || td.ctr[1] == 0) return;
+  __shared__ double s_qb[TD_NB_MAX];
+  td_stage_qb(c, s_qb);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t g = gs[i];
     if (g == none) continue;
@@ -3580,7 +3670,7 @@ __global__ __launch_bounds__(256) void k_td_large_items(DevCfg c, int64_t n, con
         hi = m;
     }
     const double W = (double)d.W;
-    const int b = td_bucket(c, W, (double)(r + (lo ? d.old[lo - 1].cum : 0)) + 0.5);
+    const int b = td_bucket(c, s_qb, W, (double)(r + (lo ? d.old[lo - 1].cum : 0)) + 0.5);
     bool start = r == 0;
     if (!start) {
       const uint64_t pk = v[i - 1];
@@ -3592,7 +3682,7 @@ __global__ __launch_bounds__(256) void k_td_large_items(DevCfg c, int64_t n, con
         else
           hi2 = m;
       }
-      start = td_bucket(c, W, (double)(r - 1 + (lo2 ? d.old[lo2 - 1].cum : 0)) + 0.5) != b;
+      start = td_bucket(c, s_qb, W, (double)(r - 1 + (lo2 ? d.old[lo2 - 1].cum : 0)) + 0.5) != b;
     }
     if (start) td.nstart[(int64_t)L * c.td_nb + b] = (int32_t)i;
   }
@@ -3600,6 +3690,8 @@ __global__ __launch_bounds__(256) void k_td_large_items(DevCfg c, int64_t n, con
 // the old centroids of the large digests (one wave per digest): their mean keys, buckets and bucket starts
 __global__ __launch_bounds__(256) void k_td_large_old(DevCfg c, const uint64_t* __restrict__ v, TdBuf td, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  __shared__ double s_qb[TD_NB_MAX];
+  td_stage_qb(c, s_qb);
   const int32_t nl = td.ctr[1];
   const int lane = __lane_id();
   for (int32_t L = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); L < nl; L += (gridDim.x * blockDim.x) >> 6) {
@@ -3612,7 +3704,7 @@ __global__ __launch_bounds__(256) void k_td_large_old(DevCfg c, const uint64_t* 
         const int64_t w = td_weight(d.old, j);
         const uint64_t mk = td_mean_key(d.old[j].sum, w);
         td.okey[(int64_t)L * c.td_nb + j] = mk;
-        b = td_bucket_old(c, v, d.beg, d.nn, mk, j ? d.old[j - 1].cum : 0, w, (double)d.W);
+        b = td_bucket_old(c, s_qb, v, d.beg, d.nn, mk, j ? d.old[j - 1].cum : 0, w, (double)d.W);
       }
       int prev = __shfl_up(b, 1, 64);
       if (lane == 0) prev = carry;
@@ -5873,7 +5965,7 @@ void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int
   hipLaunchKernelGGL(k_td_bounds, dim3((unsigned)((n + per_block - 1) / per_block)), dim3(256), 0, s, n, gsorted, none,
                      td, st);
   hipLaunchKernelGGL(k_td_small, dim3(grid), dim3(256), 0, s, c, tb, td, vsorted, st);
-  hipLaunchKernelGGL(k_td_wave, dim3(2048), dim3(64 * TD_WAVES), 0, s, c, tb, td, vsorted, st);
+  hipLaunchKernelGGL(k_td_wave, dim3(2048), dim3(64 * TD_WAVES), td_wave_lds_bytes(c.td_nb), s, c, tb, td, vsorted, st);
   hipLaunchKernelGGL(k_td_large_old, dim3(64), dim3(256), 0, s, c, vsorted, td, st);  // (the mean keys: first)
   hipLaunchKernelGGL(k_td_large_items, dim3(grid), dim3(256), 0, s, c, n, gsorted, vsorted, none, td, st);
   hipLaunchKernelGGL(k_td_large_groups, dim3(2048), dim3(256), 0, s, c, vsorted, td, st);

@@ -59,7 +59,7 @@
 #define FW_TD_T1 64            // t-digest: digests with at most this many batch values + centroids merge serially
 #endif
 #ifndef FW_TD_T3
-#define FW_TD_T3 16384         // ... at most this many in one wave; more over the whole grid (the hottest keys)
+#define FW_TD_T3 2048          // ... at most this many in one wave; more over the whole grid (the hottest keys)
 #endif
 #define FW_SLOW_THREADS 1024
 // Dense tumbling regions (DevCfg::dense): the LDS table of k_dt_aggregate (slots, threads, records per thread in
