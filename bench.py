@@ -103,8 +103,8 @@ def impl_bytes(name, n, merged, fired=0, hll_p=0, panes_per_window=0, compact=Tr
         return 24 * n + rec * n
     if name == "k_aggregate":
         return rec * n + 128 * merged
-    if name == "k_tdigest":  # keys (read the record, write 12 B), two radix sorts (8 + 3 passes of 12 B r+w)
-        return rec * n + 12 * n + 11 * 24 * n + 24 * n
+    if name == "k_tdigest":  # keys (read the record, write 12 B), one radix sort (8 passes of 12 B r+w), the tie
+        return rec * n + 12 * n + 8 * 24 * n + 12 * n + 24 * n + 24 * n  # check (12 B), decode (12 + 12), tiers (24)
     return None
 
 
