@@ -23,6 +23,7 @@ FW_KEY_LONG, FW_KEY_INT, FW_KEY_HASHED = 0, 1, 2
 FW_AGG_COUNT_SUM_MIN_MAX, FW_AGG_HLL, FW_AGG_FIRST, FW_AGG_MINBY, FW_AGG_MAXBY, FW_AGG_FIRST_MAX = 0, 1, 2, 3, 4, 5
 FW_AGG_TDIGEST = 6
 FW_NUM_KERNELS = 7
+FW_PROFILE_KINDS = 0x100  # fw_profile(op, FW_PROFILE_KINDS | 1 << kind): time only those kinds
 
 I64P = ctypes.POINTER(ctypes.c_int64)
 I32P = ctypes.POINTER(ctypes.c_int32)

@@ -126,7 +126,7 @@ struct fw_op {
   bool clear_deferred = false;  // fw_clear_pending was called meanwhile
 
   // optional per-kernel event timing (fw_profile)
-  bool prof = false;
+  uint32_t prof_mask = 0;  // kernel kinds timed (bit k = kind k)
   struct Pair {
     hipEvent_t a, b;
     int kind;
@@ -344,7 +344,7 @@ hipEvent_t prof_event(fw_op* op) {
 // time the launches issued by `launch` on the handle's stream as one interval of `kind`
 template <class F>
 void timed(fw_op* op, int kind, F&& launch, hipStream_t on = nullptr) {
-  if (!op->prof) {
+  if (!((op->prof_mask >> kind) & 1u)) {
     launch();
     return;
   }
@@ -1431,7 +1431,7 @@ int fw_get_stats(fw_op* op, fw_stats* o) {
 
 int fw_profile(fw_op* op, int enable) {
   if (!op) return FW_ERR_ARG;
-  op->prof = enable != 0;
+  op->prof_mask = enable == 0 ? 0u : (enable & FW_PROFILE_KINDS) ? (uint32_t)(enable & 0xff) : 0xffu;
   return FW_OK;
 }
 

@@ -226,8 +226,11 @@ int fw_get_stats(fw_op* op, fw_stats* out);
 /* Per-kernel timing with HIP events recorded around every launch on the handle's stream
  * (rocprofv3 --kernel-trace measures the same launches from outside).  Kernel kinds, in order:
  * classify_hist, scan, scatter, aggregate, slow, fire, tdigest (the t-digest compression of a push).  fw_profile_read returns accumulated
- * milliseconds and launch counts per kind (arrays of FW_NUM_KERNELS) and optionally resets them. */
+ * milliseconds and launch counts per kind (arrays of FW_NUM_KERNELS) and optionally resets them.
+ * enable: 0 = off, 1 = every kind, FW_PROFILE_KINDS | (1 << kind) | ... = only those kinds (each timed launch
+ * adds two event markers to its stream, so a measurement that needs one kernel's duration times only that one). */
 #define FW_NUM_KERNELS 7
+#define FW_PROFILE_KINDS 0x100
 int fw_profile(fw_op* op, int enable);
 int fw_profile_read(fw_op* op, double* ms, int64_t* launches, int reset);
 const char* fw_kernel_name(int kind);
