@@ -338,7 +338,9 @@ hipEvent_t prof_event(fw_op* op) {
     return e;
   }
   hipEvent_t e = nullptr;
-  (void)hipEventCreate(&e);
+  // timing only: no system-scope fence (a cache write-back and invalidation) when the marker completes, so the
+  // markers do not slow the work they bracket (fw_profile_read synchronizes the stream before reading them)
+  (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   return e;
 }
 // time the launches issued by `launch` on the handle's stream as one interval of `kind`
