@@ -1,7 +1,7 @@
 """Extracts the wire-format fixture (tests/golden/wire_fixture.json) from the reference's own test resource
 flink-streaming-java/src/test/resources/win-op-migration-test-reduce-event-time-flink1.4-snapshot: the bytes of
 one event-time timer of WindowOperatorMigrationTest.testRestoreReducingEventTimeWindows
-(WindowOperatorMigrationTest.java:125-190, TumblingEventTimeWindows.of(3 s), key "key1", window [0, 3000)),
+(WindowOperatorMigrationTest.java:381-433, TumblingEventTimeWindows.of(3 s), key "key1", window [0, 3000)),
 as the heap timer service wrote them: the key (StringSerializer: StringValue.writeString, length + 1 as a varint,
 then the chars), the namespace (TimeWindow.Serializer: BE i64 start, BE i64 end) and the timestamp (BE i64
 maxTimestamp = 2999).  Only bytes are read (no deserialisation).  Run here, where /root/reference exists."""
