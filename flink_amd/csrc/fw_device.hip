@@ -2929,7 +2929,7 @@ __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __rest
       hw[u] = 0;
       if (!in[u]) continue;
       const uint32_t home = (uint32_t)hs[u] & rg[u].mask;
-      hw[u] = ld_state(rg[u].state + home);
+      hw[u] = rg[u].state[home];  // (the table is read-only here: a plain, L1-cacheable read)
       hk[u] = *reinterpret_cast<const i64x2*>(&rg[u].ent[home].key);
       hend[u] = rg[u].ent[home].end;
       hmeta[u] = rg[u].ent[home].meta;
@@ -2960,7 +2960,9 @@ __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __rest
       jj[u] = (uint32_t)(h >> (64 - p));
       rank[u] = (uint32_t)__clzll((long long)((h << p) | (1ull << (p - 1)))) + 1u;
       w[u] = reinterpret_cast<uint32_t*>(c.pool + blk[u] * (uint64_t)c.pool_bytes + hdr + (jj[u] & ~3u));
-      old[u] = in[u] ? __hip_atomic_load(w[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      // a plain (L1-cacheable) read: registers only grow, so a stale copy is never above the register and
+      // costs at most a CAS that returns the current word (a hot digest's block stays in the CU's L1)
+      old[u] = in[u] ? *w[u] : 0u;
     }
 #pragma unroll
     for (int u = 0; u < HU; u++) {
