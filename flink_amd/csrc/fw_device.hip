@@ -5052,7 +5052,22 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
     M.capover = 0;
     M.widefb = 0;
   }
+  // compact records: each pass's first round of records is loaded before the table is cleared and the region's
+  // entries are read, so its latency overlaps theirs (two register sets, alternating without copies: round r is
+  // added while round r + 1 loads; branch-free loads from an index clamped into the run)
+  constexpr int RPT = FW_DT_RPT;
+  constexpr int64_t RS = (int64_t)FW_DT_THREADS * RPT;
+  const i64x2* __restrict__ crec = reinterpret_cast<const i64x2*>(in);
+  auto load = [&](i64x2 (&d)[RPT], int64_t r0) {
+#pragma unroll
+    for (int j = 0; j < RPT; j++) {
+      const int64_t i = r0 + (int64_t)j * FW_DT_THREADS + threadIdx.x;
+      d[j] = crec[i < end ? i : end - 1];
+    }
+  };
+  i64x2 ra[RPT], rn[RPT];
   for (int k = 0; k < (1 << hb); k++) {
+    if constexpr (KW && SRC == DT_RECS) load(ra, begin);
     if constexpr (KW) {
       for (int h = threadIdx.x; h < DK_SLOTS; h += FW_DT_THREADS) {
         U.k.kw[h] = DK_EMPTY;
@@ -5112,22 +5127,9 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
     if (M.widefb) return DT_WIDE;
     if (!M.over) {
       if constexpr (SRC == DT_RECS) {
-        // the batch's records, the next round's in flight while the current ones are added
-        constexpr int RPT = FW_DT_RPT;
-        constexpr int64_t RS = (int64_t)FW_DT_THREADS * RPT;
-        // (compact records: branch-free loads from an index clamped into the run, so the next round's stay in flight
-        // while the current one is added -- a load under a branch is waited for at once)
+        // the batch's records, the next round's in flight while the current ones are added (a load under a branch
+        // is waited for at once)
         if constexpr (KW) {
-          // two register sets, alternating without copies (a copy of the set in flight would wait for it): round r
-          // is added while round r + 1 loads; compact records, branch-free loads from an index clamped into the run
-          const i64x2* __restrict__ crec = reinterpret_cast<const i64x2*>(in);
-          auto load = [&](i64x2 (&d)[RPT], int64_t r0) {
-#pragma unroll
-            for (int j = 0; j < RPT; j++) {
-              const int64_t i = r0 + (int64_t)j * FW_DT_THREADS + threadIdx.x;
-              d[j] = crec[i < end ? i : end - 1];
-            }
-          };
           auto add_round = [&](const i64x2 (&cur)[RPT], int64_t r0) -> int {  // 0 done, 1 table full, 2 EMPTY word
             unsigned long long ww[RPT];
             int64_t vv[RPT];
@@ -5152,9 +5154,7 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
             if (bad) return 2;
             return dk_add_batch<RPT>(U.k, M, c.vtype, ww, vv, dm) ? 0 : 1;
           };
-          i64x2 ra[RPT], rn[RPT];
-          load(ra, begin);
-          int res = 0;
+          int res = 0;  // (ra: loaded at the top of the pass)
           for (int64_t r0 = begin; r0 < end; r0 += 2 * RS) {
             load(rn, r0 + RS);
             if ((res = add_round(ra, r0))) break;

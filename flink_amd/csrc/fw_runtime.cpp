@@ -1317,7 +1317,7 @@ int fw_drain_rows(fw_op* op, const fw_rows* dst, int64_t cap, int64_t* n) {
     int64_t* d[7] = {dst->key, dst->start, dst->end, dst->count, dst->sum, dst->min, dst->max};
     int64_t* s[7] = {op->out.key, op->out.start, op->out.end, op->out.cnt, op->out.sum, op->out.mn, op->out.mx};
     for (int i = 0; i < 7; i++)
-      if (d[i]) HIP_OR_RETURN(op, hipMemcpyAsync(d[i], s[i] + base, have * 8, hipMemcpyDeviceToHost, op->stream));
+      if (d[i]) HIP_OR_RETURN(op, hipMemcpyAsync(d[i], s[i] + base, have * 8, hipMemcpyDefault, op->stream));  // host or HBM
   }
   HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
   op->out_base += have;
@@ -1339,7 +1339,7 @@ int fw_drain_side(fw_op* op, const fw_side_rows* dst, int64_t cap, int64_t* n) {
     int64_t* d[3] = {dst->key, dst->ts, dst->val};
     int64_t* s[3] = {op->side.key, op->side.ts, op->side.val};
     for (int i = 0; i < 3; i++)
-      if (d[i]) HIP_OR_RETURN(op, hipMemcpyAsync(d[i], s[i] + base, have * 8, hipMemcpyDeviceToHost, op->stream));
+      if (d[i]) HIP_OR_RETURN(op, hipMemcpyAsync(d[i], s[i] + base, have * 8, hipMemcpyDefault, op->stream));  // host or HBM
   }
   HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
   op->side_base += have;

@@ -266,6 +266,20 @@ class GpuWindowOperator:
         out["epoch"] = epoch
         return out
 
+    def drain_rows_torch(self, fields=ROW_FIELDS):
+        """fw_drain_rows into fresh int64 tensors on this operator's GPU (HBM to HBM, no host copy): {field: tensor}
+        for the requested row fields; the pending rows are cleared."""
+        import torch
+        L = N.lib()
+        n_rows = ctypes.c_int64()
+        N.check(L.fw_pending(self._h, ctypes.byref(n_rows), None), self._h)
+        dev = torch.device("cuda", self.device)
+        cols = {f: torch.empty(max(n_rows.value, 1), dtype=torch.int64, device=dev) for f in fields}
+        dst = N.FwRows(**{f: cols[f].data_ptr() for f in fields})
+        got = ctypes.c_int64()
+        N.check(L.fw_drain_rows(self._h, ctypes.byref(dst), n_rows.value, ctypes.byref(got)), self._h)
+        return {f: t[:got.value] for f, t in cols.items()}
+
     def drain_digests(self):
         """TDigest(export=True): the centroids of the pending rows, as a list of (sums f64[], weights i64[])
         in row order.  Call before the rows are drained (process_watermark drains them: use

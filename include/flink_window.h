@@ -207,8 +207,8 @@ int fw_push_batch_device(fw_op* op, const int64_t* key, const int64_t* ts, const
  * the watermark in the operator's output (AbstractStreamOperator.java:735-740). */
 int fw_advance_watermark(fw_op* op, int64_t wm, int64_t* n_pending_rows);
 
-/* Pending output.  *_host copy into caller-owned host arrays of capacity cap and clear the
- * pending set; fw_rows_device exposes the pending rows in HBM without copying (valid until the
+/* Pending output.  *_host copy into caller-owned arrays of capacity cap and clear the pending
+ * set (fw_drain_rows: host or device memory, a NULL column is skipped); fw_rows_device exposes the pending rows in HBM without copying (valid until the
  * next fw_* call) and fw_clear_pending drops them.  Each of these first settles an unsettled
  * device push. */
 int fw_pending(fw_op* op, int64_t* n_rows, int64_t* n_side_rows);

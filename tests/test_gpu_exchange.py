@@ -36,19 +36,21 @@ KINDS = {
     "sessions": dict(oracle=dict(assigner="session", gap=30_000), zipf=1.1),
     "panes": dict(oracle=dict(assigner="sliding", size=60_000, slide=1000), zipf=None),
     "hll": dict(oracle=dict(assigner="tumbling", size=1000, hll_p=12), zipf=1.1),
+    "tdigest": dict(oracle=dict(assigner="tumbling", size=1000, tdigest=100), zipf=1.1),
 }
 
 
 def _operator(kind, key_type, kgr):
-    from flink_amd import (EventTimeSessionWindows, HyperLogLog, SlidingEventTimeWindows,
+    from flink_amd import (EventTimeSessionWindows, HyperLogLog, SlidingEventTimeWindows, TDigest,
                            TumblingEventTimeWindows)
     from flink_amd.operator import GpuWindowOperator
     from flink_amd.windowing import CountSumMinMax
     assigner = {"tumbling": TumblingEventTimeWindows.of(1000), "sessions": EventTimeSessionWindows.with_gap(30_000),
-                "panes": SlidingEventTimeWindows.of(60_000, 1000), "hll": TumblingEventTimeWindows.of(1000)}[kind]
-    agg = HyperLogLog(12) if kind == "hll" else CountSumMinMax()
+                "panes": SlidingEventTimeWindows.of(60_000, 1000), "hll": TumblingEventTimeWindows.of(1000),
+                "tdigest": TumblingEventTimeWindows.of(1000)}[kind]
+    agg = HyperLogLog(12) if kind == "hll" else TDigest(100) if kind == "tdigest" else CountSumMinMax()
     return GpuWindowOperator(assigner, agg, key_type=key_type, max_parallelism=MAX_PAR, key_group_range=kgr,
-                             device=0, expected_entries=20_000 if kind == "hll" else 0)
+                             device=0, expected_entries=20_000 if kind in ("hll", "tdigest") else 0)
 
 
 def _slice(rank, step, key_type, kind="tumbling"):
@@ -61,6 +63,8 @@ def _slice(rank, step, key_type, kind="tumbling"):
         k = k - KEYS // 2  # negative Integer keys
     elif key_type == "hashed":
         h = np.array([string_hash_code(f"word-{x}") for x in range(KEYS)], dtype=np.int32)[k]
+    if kind == "tdigest":  # a Double field: distinct-ish values of both signs
+        v = (v & 0xFFFFFF).astype(np.float64) / 7.0 - 1.0e6
     return k, t, v, h
 
 
@@ -159,12 +163,13 @@ def test_gpu_native_keyby_world1():
     op.close()
 
 
-@pytest.mark.parametrize("kind", ["sessions", "panes", "hll"])
+@pytest.mark.parametrize("kind", ["sessions", "panes", "hll", "tdigest"])
 def test_gpu_exchange_world2_operator_kinds(tmp_path, kind):
     """Sessions (gap 30 s, Zipf keys: MergingWindowSet merges per key on its owning subtask), panes (sliding
-    60 s / 1 s) and HyperLogLog (Zipf keys) through the world-size-2 exchange: the union of both subtasks' rows
-    equals one oracle operator over the whole stream (fed in the exchange's per-step source-major order, global
-    watermarks)."""
+    60 s / 1 s), HyperLogLog and t-digest (delta 100; Zipf keys, BASELINE configs[4]) through the world-size-2
+    exchange: the union of both subtasks' rows equals one oracle operator over the whole stream, fed each step's
+    records in the exchange's source-major order as one batch (a t-digest compresses once per push), under the
+    global watermarks.  t-digest rows (count, min / max, the p50 / p95 / p99 bits) are bit-exact."""
     import torch.multiprocessing as mp
     mp.spawn(_worker, args=(_free_port(), str(tmp_path), "long", kind), nprocs=WORLD, join=True)
     rows = np.concatenate([np.load(tmp_path / f"rows_{r}.npy") for r in range(WORLD)])
@@ -174,8 +179,7 @@ def test_gpu_exchange_world2_operator_kinds(tmp_path, kind):
         parts = [_slice(r, s, "long", kind) for r in range(WORLD)]
         for r in range(WORLD):
             mx[r] = max(mx[r], int(parts[r][1].max()))
-        for src in range(WORLD):
-            ref.process(*parts[src][:3])
+        ref.process(*(np.concatenate([p[i] for p in parts]) for i in range(3)))
         ref.watermark(min(m - 300 for m in mx))
     ref.watermark((1 << 63) - 1)
     r = ref.rows()

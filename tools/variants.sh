@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 if [ "${1:-}" = "build" ]; then
   for v in $VARIANTS; do
     name=${v%%:*}; flags=${v#*:}; flags=${flags//,/ }
-    make -s -C flink_amd/csrc OUT=../_lib/variants LIBNAME=lib_$name.so EXTRA="$flags" || exit 1
+    make -s -j4 -C flink_amd/csrc OUT=../_lib/variants LIBNAME=lib_$name.so EXTRA="$flags" || exit 1
   done
   exit 0
 fi
