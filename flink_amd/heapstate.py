@@ -25,6 +25,8 @@ reader of the serialization stream grammar (class descriptors, field values, blo
 import io
 import struct
 
+from .keygroups import _i32, bit_mix
+
 # ---------------------------------------------------------------- DataInputStream / DataOutputStream
 
 
@@ -352,12 +354,14 @@ class JavaStreamSkipper:
 
 def skip_resilient_serializers(r):
     """TypeSerializerSerializationUtil.readSerializersAndConfigsWithResilience: the count, the offset pairs, the total
-    length and the block — skipped whole (:174-214)"""
+    length and the block — skipped whole (:174-214); returns the block's bytes as written (the writers below put
+    them back verbatim: the host owns its serializers, this module never builds one)"""
+    start = r.pos
     n = r.i32()
     for _ in range(2 * n):
         r.i32()
     r.take(r.i32())
-    return n
+    return r.b[start:r.pos]
 
 
 # ---------------------------------------------------------------- operator snapshot file
@@ -439,14 +443,15 @@ def read_heap_keyed_state(handle, serializers):
     compression = r.bool() if version >= 4 else False
     if compression:
         raise ValueError("snappy-compressed key groups are not read")
-    skip_resilient_serializers(r)  # the key serializer
+    blocks = {"key": skip_resilient_serializers(r)}  # the key serializer
     states = []
     for _ in range(r.i16()):
         typ = r.i32()
         name = r.utf()
-        skip_resilient_serializers(r)  # namespace and state serializers
+        blocks[name] = skip_resilient_serializers(r)  # namespace and state serializers
         states.append((STATE_TYPES[typ] if 0 <= typ < len(STATE_TYPES) else typ, name))
-    meta = {"version": version, "compression": compression, "states": states, "header_end": r.pos}
+    meta = {"version": version, "compression": compression, "states": states, "header_end": r.pos,
+            "serializers": blocks}
     groups = {}
     for kg, off in zip(handle.key_groups(), handle.offsets):
         r.pos = off
@@ -492,12 +497,159 @@ def write_keyed_state_stream(header, sections):
     return bytes(out), offsets
 
 
+def write_serialization_proxy(version, key_serializer, states, compression=False):
+    """KeyedBackendSerializationProxy.write (KeyedBackendSerializationProxy.java:101-118): the version (VersionedIO
+    ReadableWritable: a bare int), the key-group compression flag from version 4 on, the key serializer block, then
+    per registered state its type ordinal, name and namespace / state serializer block (the V3 meta-info writer,
+    KeyedBackendStateMetaInfoSnapshotReaderWriters.java:96-116).  states = [(type name, state name, serializer
+    block)]; the serializer blocks are the host's (TypeSerializerSerializationUtil.writeSerializersAndConfigsWith
+    Resilience output, as read_heap_keyed_state returns them in meta["serializers"]).  Versions 3 and 4."""
+    if version not in (3, 4):
+        raise ValueError(f"serialization proxy version {version}: 3 (Flink 1.3) or 4 (1.4, 1.5) are written")
+    if compression:
+        raise ValueError("snappy-compressed key groups are not written")
+    w = DataOutput()
+    w.i32(version)
+    if version >= 4:
+        w.bool(False)
+    w.write(bytes(key_serializer))
+    w.i16(len(states))
+    for typ, name, block in states:
+        w.i32(STATE_TYPES.index(typ) if isinstance(typ, str) else int(typ))
+        w.utf(name)
+        w.write(bytes(block))
+    return w.getvalue()
+
+
+# ---------------------------------------------------------------- iteration orders of the heap backend
+# A snapshot writes its mappings and timers in the order the JVM's hash structures iterate them, so equal state
+# gives equal bytes only in that order.  These restate the orders from the structures' definitions.
+def long_to_int_with_bit_mixing(v):
+    """MathUtils.longToIntWithBitMixing (MathUtils.java:177-182)"""
+    m = (1 << 64) - 1
+    v &= m
+    v = ((v ^ (v >> 30)) * 0xBF58476D1CE4E5B9) & m
+    v = ((v ^ (v >> 27)) * 0x94D049BB133111EB) & m
+    v ^= v >> 31
+    return _i32(v)
+
+
+def time_window_hash(w):
+    """TimeWindow.hashCode (TimeWindow.java:102-104): longToIntWithBitMixing(start + end)"""
+    return long_to_int_with_bit_mixing(w[0] + w[1])
+
+
+def timer_hash(key_hash, ns_hash, ts):
+    """InternalTimer.hashCode (InternalTimer.java:84-89)"""
+    t = ts & ((1 << 64) - 1)
+    h = _i32(t ^ (t >> 32))
+    h = _i32(31 * h + key_hash)
+    return _i32(31 * h + ns_hash)
+
+
+def state_table_order(mappings, key_hash, ns_hash, capacity=1024):
+    """The order CopyOnWriteStateTable's snapshot walks `mappings` [(namespace, key, state)] inserted in the given
+    order: buckets in index order (compositeHash = bitMix(key.hashCode() ^ namespace.hashCode()) & (capacity - 1),
+    CopyOnWriteStateTable.java:831-834; default capacity 1024, doubled past 3/4 load, :197-247 / :626-637), each
+    bucket's chain newest first (addNewStateTableEntry puts the entry at the chain's head, :643-675).  No rehash in
+    flight at the snapshot (snapshotTableArrays, :582-618)."""
+    cap = capacity
+    while len(mappings) > (cap >> 1) + (cap >> 2):
+        cap <<= 1
+    b = [bit_mix(key_hash(k) ^ ns_hash(n)) & (cap - 1) for n, k, _ in mappings]
+    return [mappings[i] for i in sorted(range(len(mappings)), key=lambda i: (b[i], -i))]
+
+
+def hash_set_order(items, hash_of):
+    """The iteration order of a java.util.HashSet built by adding `items` in order to `new HashSet<>()` (initial
+    capacity 16, load factor 0.75; the table doubles when the size exceeds 3/4 of it and a split keeps each bucket's
+    relative order): buckets by (h ^ (h >>> 16)) & (capacity - 1), insertion order inside a bucket.  Buckets of 8 or
+    more (tree bins) are not modelled."""
+    cap = 16
+    while len(items) > (cap * 3) // 4:
+        cap <<= 1
+    def bucket(x):
+        h = hash_of(x) & 0xFFFFFFFF
+        return (h ^ (h >> 16)) & (cap - 1)
+    b = [bucket(x) for x in items]
+    return [items[i] for i in sorted(range(len(items)), key=lambda i: (b[i], i))]
+
+
+def nested_maps_order(mappings, key_hash, ns_hash):
+    """The order NestedMapsStateTable's snapshot writes one key group's mappings (the heap backend's table with
+    synchronous snapshots: a HashMap of namespaces, each a HashMap of keys, NestedMapsStateTable.java:221-238 and
+    :352-368): namespaces in HashMap order, then each namespace's keys in HashMap order (first insertion = the
+    given order)."""
+    by_ns = {}
+    for n, k, v in mappings:
+        by_ns.setdefault(n, []).append((n, k, v))
+    out = []
+    for n in hash_set_order(list(by_ns), ns_hash):
+        out += hash_set_order(by_ns[n], lambda m: key_hash(m[1]))
+    return out
+
+
+def heap_section_order(mappings, key_hash, ns_hash, table="copy_on_write"):
+    """One key group's mappings in the order the heap backend's snapshot writes them: "copy_on_write"
+    (CopyOnWriteStateTable, asynchronous snapshots: state_table_order, partitioned by key group without reordering,
+    CopyOnWriteStateTableSnapshot.partitionEntriesByKeyGroup, CopyOnWriteStateTableSnapshot.java:127-167) or
+    "nested_maps" (NestedMapsStateTable, synchronous snapshots: HeapKeyedStateBackend.newStateTable,
+    HeapKeyedStateBackend.java:614-618)."""
+    if table == "nested_maps":
+        return nested_maps_order(list(mappings), key_hash, ns_hash)
+    if table != "copy_on_write":
+        raise ValueError(f"unknown heap state table {table!r}")
+    return state_table_order(list(mappings), key_hash, ns_hash)
+
+
+def timer_set_order(timers, key_hash, ns_hash):
+    """hash_set_order of one key group's timers (HeapInternalTimerService keeps a HashSet per key group,
+    HeapInternalTimerService.java:361-367)"""
+    return hash_set_order(list(timers), lambda t: timer_hash(key_hash(t[0]), ns_hash(t[1]), t[2]))
+
+
+# ---------------------------------------------------------------- KeyGroupsStateHandle / operator snapshot file
+def write_keyed_handle(start, offsets, name, data):
+    """SavepointV1Serializer.serializeKeyedStateHandle (SavepointV1Serializer.java:262-280): type 3 (key groups),
+    the first key group, the offsets of the range's key groups, then the ByteStreamStateHandle (type 1: name, data)"""
+    w = DataOutput()
+    w.u8(3)
+    w.i32(start)
+    w.i32(len(offsets))
+    for o in offsets:
+        w.i64(o)
+    w.u8(1)
+    w.utf(name)
+    w.i32(len(data))
+    w.write(bytes(data))
+    return w.getvalue()
+
+
+def write_operator_snapshot(chain_index, raw_keyed, managed_keyed):
+    """OperatorSnapshotUtil.writeStateHandle (OperatorSnapshotUtil.java:48-76): chain index, no legacy handle, no
+    raw / managed operator state, then the raw and managed keyed handles (each a list of write_keyed_handle bytes;
+    None = absent)"""
+    w = DataOutput()
+    w.i32(chain_index)
+    w.u8(0)  # legacy operator state
+    for handles in (None, None, raw_keyed, managed_keyed):
+        if handles is None:
+            w.i32(-1)
+            continue
+        w.i32(len(handles))
+        for h in handles:
+            w.write(h)
+    return w.getvalue()
+
+
 # ---------------------------------------------------------------- timers (raw keyed state)
 _VERSIONED = bytes([0xF1, 0xCD, 0x85, 0x9F])  # PostVersionedIOReadableWritable.VERSIONED_IDENTIFIER
 
 
-def read_timers(handle, key_ser, ns_ser):
-    """{key group: {service name: (event-time timers, processing-time timers)}}, a timer = (key, namespace, ts)"""
+def read_timers(handle, key_ser, ns_ser, meta=None):
+    """{key group: {service name: (event-time timers, processing-time timers)}}, a timer = (key, namespace, ts).
+    meta (a dict, optional) receives per key group {"versioned": bool, "serializers": {service: bytes}}: the
+    format of the section and each service's serializer bytes as written (write_timer_section puts them back)."""
     out = {}
     for kg, off in zip(handle.key_groups(), handle.offsets):
         r = DataInput(handle.data, off)
@@ -505,19 +657,77 @@ def read_timers(handle, key_ser, ns_ser):
         if versioned:
             r.take(4)
             r.i32()  # proxy version
-        services = {}
+        services, sers = {}, {}
         for _ in range(r.i32()):
             name = r.utf()
+            s0 = r.pos
             if versioned:
                 skip_resilient_serializers(r)
             else:  # pre-versioned: the key and namespace serializers as bare Java serialization streams
                 JavaStreamSkipper(r).skip_stream()
                 JavaStreamSkipper(r).skip_stream()
+            sers[name] = r.b[s0:r.pos]
             ev = [(key_ser.read(r), ns_ser.read(r), r.i64()) for _ in range(r.i32())]
             pt = [(key_ser.read(r), ns_ser.read(r), r.i64()) for _ in range(r.i32())]
             services[name] = (ev, pt)
         out[kg] = services
+        if meta is not None:
+            meta[kg] = {"versioned": versioned, "serializers": sers}
     return out
+
+
+def write_timer_section(services, key_ser, ns_ser, versioned=True):
+    """One key group's raw keyed state: InternalTimeServiceManager.snapshotStateForKeyGroup (InternalTimeService
+    Manager.java:114-118) -> InternalTimerServiceSerializationProxy.write (InternalTimerServiceSerializationProxy.java:
+    92-106): the post-versioned identifier and proxy version 1, the number of timer services, then per service its
+    name, the key / namespace serializers and the timers (InternalTimersSnapshotReaderWriters.java:96-160: event-time
+    count + timers, processing-time count + timers; a timer = key, namespace, timestamp, InternalTimer.java:148-159).
+    services = [(name, serializer bytes, event timers, processing timers)]; the serializer bytes are the host's:
+    the resilient block (versioned) or two bare Java serialization streams (pre-versioned, Flink 1.4.0 and 1.3,
+    versioned=False, which also drops the identifier).  Timers are written in the given order (timer_set_order
+    gives the heap's)."""
+    w = DataOutput()
+    if versioned:
+        w.write(_VERSIONED)
+        w.i32(1)
+    w.i32(len(services))
+    for name, sers, ev, pt in services:
+        w.utf(name)
+        w.write(bytes(sers))
+        for timers in (ev, pt):
+            w.i32(len(timers))
+            for k, n, ts in timers:
+                key_ser.write(w, k)
+                ns_ser.write(w, n)
+                w.i64(ts)
+    return w.getvalue()
+
+
+def write_savepoint_key_group_0(meta, timer_meta, mappings, event_timers, serializers, chain_index, managed_name,
+                                raw_name, table="copy_on_write", key_hash=None, ns_hash=None):
+    """A WindowOperator's savepoint file for a one-key-group range (the test harness' maxParallelism 1: key group 0)
+    from its content: `mappings` [(window, key, state)] of the one registered state and the `event_timers` of
+    "window-timers" (any order: written in the heap's iteration order, `table` as in heap_section_order), with the
+    host's serializer blocks and handle names (meta / timer_meta as read_heap_keyed_state / read_timers return
+    them).  String keys and TimeWindow namespaces unless key_hash / ns_hash say otherwise."""
+    from .keygroups import string_hash_code
+    key_hash = key_hash or string_hash_code
+    ns_hash = ns_hash or time_window_hash
+    (typ, name), = meta["states"]
+    hdr = write_serialization_proxy(meta["version"], meta["serializers"]["key"],
+                                    [(typ, name, meta["serializers"][name])])
+    sec = write_key_group_section(0, [(0, name, heap_section_order(mappings, key_hash, ns_hash, table))], serializers)
+    stream, offsets = write_keyed_state_stream(hdr, [sec])
+    timers = write_timer_section([("window-timers", timer_meta["serializers"]["window-timers"],
+                                   timer_set_order(event_timers, key_hash, ns_hash), [])],
+                                 serializers[name][1], serializers[name][0], versioned=timer_meta["versioned"])
+    return write_operator_snapshot(chain_index, [write_keyed_handle(0, [0], raw_name, timers)],
+                                   [write_keyed_handle(0, offsets, managed_name, stream)])
+
+
+def rows_to_timers(rows, key_name, service_timer=lambda r: int(r["end"]) - 1):
+    """the EventTimeTrigger timers (key, window, maxTimestamp) of GPU state rows whose `timer` is set"""
+    return [(key_name(int(r["key"])), (int(r["start"]), int(r["end"])), service_timer(r)) for r in rows if r["timer"]]
 
 
 # ---------------------------------------------------------------- heap state <-> GPU operator state
@@ -553,14 +763,23 @@ def heap_from_reduce_rows(rows, key_name, passthrough, field):
     return out
 
 
-def list_state_from_heap(mappings, timers, key_id, value_of, ts_of=None, ordinal_base=0):
+def trigger_counts_from_heap(count_mappings):
+    """CountTrigger's partial counts: its ReducingState "count" (Sum over LongSerializer, CountTrigger.java:41-43,
+    read with serializers (window, key, LongSer())) as {(key, window): count}"""
+    return {(key, window): int(c) for window, key, c in count_mappings}
+
+
+def list_state_from_heap(mappings, timers, key_id, value_of, ts_of=None, ordinal_base=0, trigger_counts=None):
     """A window-contents ListState (WindowOperator: the values; EvictingWindowOperator: StreamRecords) as the list
     operator's state: (lists [dict key, start, end, trigger_count, timer, n_elems], elements [(ts, val, ordinal)]).
-    Values without a timestamp get Long.MIN_VALUE ("no timestamp")."""
+    Values without a timestamp get Long.MIN_VALUE ("no timestamp").  trigger_counts: a CountTrigger's counts
+    (trigger_counts_from_heap); without them every window restores with count 0, which is right only for
+    EventTimeTrigger operators (the list operator refuses nothing here: the caller knows its trigger)."""
     lists, elems = [], []
     o = ordinal_base
     for (start, end), key, values in mappings:
-        lists.append(dict(key=key_id(key), start=start, end=end, trigger_count=0,
+        tc = trigger_counts.get((key, (start, end)), 0) if trigger_counts else 0
+        lists.append(dict(key=key_id(key), start=start, end=end, trigger_count=tc,
                           timer=int((key, (start, end), end - 1) in timers), n_elems=len(values)))
         for v in values:
             ts = ts_of(v) if ts_of else None

@@ -86,3 +86,52 @@ def test_bridges_round_trip():
     assert [r["n_elems"] for r in lists] == [2, 3, 3] and len(elems) == 8
     back = H.heap_from_list_state(lists, elems, names.__getitem__, lambda e: None)
     assert [len(m[2]) for m in back] == [2, 3, 3]
+
+
+def _rewrite(data, name, version, shuffle_seed):
+    """every byte of a savepoint file from its content: the mappings and timers (shuffled, then put in the heap's
+    iteration order), the host's opaque serializer blocks and handle names"""
+    import random
+    snap = H.read_operator_snapshot(data)
+    mk, rk = snap["managed_keyed"][0], snap["raw_keyed"][0]
+    meta, groups = H.read_heap_keyed_state(mk, serializers(name))
+    tmeta = {}
+    timers = H.read_timers(rk, H.StringSer(), H.TimeWindowSer(), meta=tmeta)
+    rnd = random.Random(shuffle_seed)
+    mappings = list(groups[0]["window-contents"])
+    ev = list(timers[0]["window-timers"][0])
+    rnd.shuffle(mappings)
+    rnd.shuffle(ev)
+    return H.write_savepoint_key_group_0(meta, tmeta[0], mappings, ev, serializers(name), snap["chain_index"],
+                                         mk.name, rk.name, table="nested_maps" if version == "1.3" else "copy_on_write")
+
+
+@pytest.mark.parametrize("version", ["1.3", "1.4"])
+@pytest.mark.parametrize("name", ["reduce-event-time", "apply-event-time"])
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_writes_savepoint_byte_exact(name, version, seed):
+    # snapshot direction (HeapKeyedStateBackend.snapshot, HeapKeyedStateBackend.java:366-383, + the timer services,
+    # InternalTimeServiceManager.java:114-118): the serialization proxy header, the key-group section in the heap
+    # table's iteration order (1.3: NestedMapsStateTable, 1.4: CopyOnWriteStateTable), the timer section in the
+    # HashSet's order, both KeyGroupsStateHandles and the operator snapshot file equal the reference's file
+    data = load(name, version)
+    assert _rewrite(data, name, version, seed) == data
+
+
+def test_java_iteration_orders():
+    # HashSet: capacity 16 until 13 elements, then 32; buckets by (h ^ h >>> 16) & (cap - 1), insertion order inside
+    assert H.hash_set_order([17, 1, 33, 2], lambda x: x) == [17, 1, 33, 2]  # all of 17, 1, 33 in bucket 1 (cap 16)
+    assert H.hash_set_order(list(range(13))[::-1], lambda x: x) == list(range(13))  # cap 32 past 12 elements
+    assert H.hash_set_order([0x10000, 1], lambda x: x) == [0x10000, 1]  # 0x10000 spreads to bucket 1 too
+    # CopyOnWriteStateTable: chains newest first
+    same = [(("ns"), "a", 1), (("ns"), "b", 2)]
+    assert H.state_table_order(same, lambda k: 7, lambda n: 0) == same[::-1]
+    assert H.long_to_int_with_bit_mixing(0) == 0
+
+
+def test_trigger_counts_carry_into_list_state():
+    counts = H.trigger_counts_from_heap([((0, 3000), "key1", 2), ((3000, 6000), "key2", 1)])
+    assert counts == {("key1", (0, 3000)): 2, ("key2", (3000, 6000)): 1}
+    lists, _ = H.list_state_from_heap([((0, 3000), "key1", [1, 2]), ((0, 3000), "key2", [3])], set(),
+                                      {"key1": 1, "key2": 2}.__getitem__, lambda v: v, trigger_counts=counts)
+    assert [r["trigger_count"] for r in lists] == [2, 0]
