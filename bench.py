@@ -85,6 +85,34 @@ def b_alg(workload, fired_per_record, world, hll_p=14, panes=60, centroids_per_r
     return 24 + bx + 104 * f  # c2
 
 
+def kernel_share(name, workload, f, hll_p=14, panes=60, centroids_per_record=0.0):
+    """Per record, the bytes each timing bucket must move in this build's data flow (its own share, VERDICT r03
+    item 7): the partitioning reads the input (B_in) and writes each record once into its partition's
+    run (16-B CRec, 32-B PRec for sessions); the aggregate reads that record back and does §8d's state
+    read-modify-write (C3: one 48-B pane RMW; C5: the HLL register byte; 0 where §8d counts the table as
+    cache-resident); the t-digest compression adds §8d's 16 B per value; the firing reads what fires and writes
+    the rows (§8d B_fire).  The design-independent figure is `path_roofline` (B_alg x records/s)."""
+    rec = 32 if workload == "c4" else 16
+    b_in = 28 if workload == "c1" else 24
+    if name == "k_scatter":
+        return b_in + rec
+    if name == "k_aggregate":
+        return rec + {"c3": 96, "c5": 2}.get(workload, 0)
+    if name == "k_tdigest":
+        return 16
+    if name == "k_fire":
+        if workload == "c3":
+            return (panes * 48 + 56) * f
+        if workload == "c4":
+            return 112 * f
+        if workload == "c5":
+            return ((1 << hll_p) + 56) * f
+        if workload == "c5t":
+            return 16 * centroids_per_record + 56 * f
+        return 104 * f
+    return 0.0
+
+
 def impl_bytes(name, n, merged, fired=0, hll_p=0, panes_per_window=0, compact=True, single=False):
     """What one launch of a kernel moves as built, for the `impl_bytes` field.  single: the
     batches took the single-pass scatter (k_scatter_rsv), behind which classify / scan / scatter only check a flag."""
@@ -368,7 +396,8 @@ def main():
                 tr = t.get("per_launch_bytes", {})
                 tr_all = t.get("bytes_per_record_all_kernels")
                 tr_src = os.path.relpath(args.traffic, ROOT)
-        alg = balg * per_launch_records
+        alg_path = balg * per_launch_records
+        share = {}
         for i in range(N.FW_NUM_KERNELS):
             name = L.fw_kernel_name(i).decode()
             if not nl[i]:
@@ -376,22 +405,33 @@ def main():
             avg = ms[i] / nl[i]
             ib = impl_bytes(name, per_launch_records, merged, fired=fired / nl[i], hll_p=args.hll_p if hll else 0,
                             panes_per_window=args.size // args.slide if sliding else 0, single=single)
+            # the bucket's own algorithmic bytes per launch: its share per record x the records of one launch (a
+            # watermark's firing: the records of the steps it follows)
+            sh = kernel_share(name, w, fpr, args.hll_p, args.size // args.slide, cpr)
+            share[name] = sh * per_gpu_records / nl[i]
             kernels[name] = {"launches": int(nl[i]), "avg_ms": round(avg, 5), "total_ms": round(ms[i], 4),
+                             "alg_bytes_per_record": round(sh, 3), "alg_bytes_per_launch": int(share[name]),
+                             "frac": round(share[name] / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                              "impl_bytes": None if ib is None else int(ib),
                              "impl_frac": None if not ib else round(ib / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                              "traffic": tr.get(name)}
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
         kd = kernels[dom]
+        alg = share[dom]
         achieved = alg / (kd["avg_ms"] * 1e-3) / 1e9
         traffic = tr.get(dom)
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "alg_bytes_per_launch": int(alg), "alg_bytes_per_record": round(balg, 3),
+                    "alg_bytes_per_launch": int(alg), "alg_bytes_per_record": kd["alg_bytes_per_record"],
+                    "path_alg_bytes_per_launch": int(alg_path),
                     "impl_bytes_per_launch": kd["impl_bytes"], "impl_frac": kd["impl_frac"],
-                    "traffic_over_alg": None if traffic is None else round(traffic / alg, 3),
+                    "traffic_over_alg": None if (traffic is None or not alg) else round(traffic / alg, 3),
                     "traffic_per_record": None if traffic is None else round(traffic / per_launch_records, 2),
                     "traffic_all_kernels_per_record": tr_all, "traffic_source": tr_src,
-                    "basis": "SURVEY §8d B_alg x records per launch / the kernel's average HIP-event duration"}
+                    "basis": "the dominant bucket's own share (bench.py kernel_share: input + partitioned-record "
+                             "write for the partitioning, record read + SURVEY §8d state RMW for the aggregate, "
+                             "§8d B_fire for the firing) x records per launch / its average HIP-event duration "
+                             "(on the stream it runs on); path_roofline prices the whole step at §8d B_alg"}
     kernels_iso = None
     if iso_steps:
         import ctypes

@@ -134,11 +134,20 @@ __device__ __forceinline__ int64_t ld_l2(const int64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // limit > 0: no new group beyond `limit` live ones (LF_MAP_FULL is raised instead, nothing inserted).  *ins counts
-// the groups this call inserted (the caller adds them to live_groups, one atomic per workgroup).
+// the groups this call inserted (the caller adds them to live_groups, one atomic per workgroup).  live_groups lags
+// the launch (its workgroups add their inserts when they finish), so a push with many new groups can fill the map
+// past the limit before any lane sees it; a probe chain therefore stops at G_PROBE_CAP slots (at <= 3/4 load a
+// chain that long means the map is overfull) and, past G_PROBE_CHECK slots, at a raised LF_MAP_FULL: the push is
+// redone after a growth, so a full map costs each later insert a bounded walk, not one over the whole map.
+constexpr uint32_t G_PROBE_CHECK = 32, G_PROBE_CAP = 1024;
 __device__ int32_t g_find_insert(const LState& S, int64_t key, int64_t start, int32_t kg, unsigned long long limit,
                                  unsigned* ins) {
   uint32_t s = g_hash(key, start) & S.gmask;
   for (uint32_t probes = 0; probes <= S.gmask;) {
+    if (limit && probes >= G_PROBE_CHECK &&
+        (probes >= G_PROBE_CAP ||
+         (__hip_atomic_load(&S.ctr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & LF_MAP_FULL)))
+      break;
     const uint32_t cur = __hip_atomic_load(&S.g[s].st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __atomic_signal_fence(__ATOMIC_ACQUIRE);  // (the compiler keeps the key loads behind it)
     if (cur == G_LIVE) {
@@ -1190,7 +1199,9 @@ int push_device(fw_list* op, const int64_t* key, const int64_t* ts, const int64_
     LRET(read_ctr(op));
     if (!(op->h_ctr->flags & LF_MAP_FULL)) break;
     if (round > 40) return set_err(op, FW_ERR_CAPACITY, "list state map full");
-    LRET(compact(op, op->gcap));  // twice the capacity
+    // the map was too small for the push's new groups: four times the capacity (a push of many more new groups
+    // than the map holds takes few rounds)
+    LRET(compact(op, 2 * op->gcap));
     base = op->n_log;
   }
   LHIP(op, hipGetLastError());

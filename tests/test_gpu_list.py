@@ -312,3 +312,25 @@ def test_gpu_list_errors_and_edges():
         op.process(np.array(keys), np.array([1]), np.array([1]))
     assert e.value.code == N.FW_ERR_KEY_GROUP
     op.close()
+
+
+def test_gpu_list_map_growth_bounded():
+    """A push of far more new (key, window) groups than the group map holds (1024 slots at creation, 2^20 distinct
+    keys in one batch): the probe chains of an overfull map are capped and the map grows fourfold per retry, so the
+    push finishes quickly (no walk over the whole map per insert) and every group fires once with its records."""
+    import time
+    from flink_amd.listwindow import GpuListWindowOperator
+    n = 1 << 20
+    keys = np.arange(n, dtype=np.int64) * 7919
+    ts = np.arange(n, dtype=np.int64) % 1000
+    vals = np.arange(n, dtype=np.int64)
+    op = GpuListWindowOperator(TumblingEventTimeWindows.of(1000), emit_contents=False)
+    t0 = time.perf_counter()
+    op.process(keys, ts, vals)
+    took = time.perf_counter() - t0
+    op.watermark(2000)
+    rows = op.rows()
+    op.close()
+    assert took < 20, took
+    assert len(rows) == n and int(rows["count"].sum()) == n
+    assert np.array_equal(np.sort(rows["key"]), np.sort(keys))

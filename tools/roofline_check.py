@@ -2,7 +2,8 @@
 """Recompute a bench line's roofline from the rocprofv3 kernel traces under profiles/ (VERDICT r02 item 3).
 
 A bench line prices its dominant timing bucket (bench.py `roofline.kernel`, one of fw_kernel_name's buckets) at
-B_alg x records per launch over the bucket's average HIP-event duration; `roofline.isolated` does the same over
+its own algorithmic bytes per launch (bench.py kernel_share) over the bucket's average HIP-event duration, and every
+other bucket the same way (`kernels[*].frac`); `roofline.isolated` does the same over
 a pass with synchronous input.  Here the same figures come from rocprofv3 kernel traces of the same command:
 the bucket's kernels (tools/traffic.py BUCKETS), their dispatches in the timed steps (between the bench's stats
 reads around its timed loop), durations summed and divided by the timed steps.  Under async input a HIP-event interval also holds
@@ -59,9 +60,20 @@ def main():
                     "isolated_avg_ms": rf.get("isolated", {}).get("avg_ms")},
            "rocprof": {"async_bucket_ms": ms_a, "sync_bucket_ms": ms_s,
                        "frac": round(frac(ms_a[dom]), 4), "isolated_frac": round(frac(ms_s[dom]), 4)}}
-    res["rel_diff"] = {"frac": round(res["rocprof"]["frac"] / rf["frac"] - 1, 4),
+    res["rel_diff"] = {"frac": round(res["rocprof"]["frac"] / rf["frac"] - 1, 4) if rf["frac"] else None,
                        "isolated_frac": (round(res["rocprof"]["isolated_frac"] / rf["isolated"]["frac"] - 1, 4)
-                                         if rf.get("isolated") else None)}
+                                         if rf.get("isolated") and rf["isolated"]["frac"] else None)}
+    # every bucket's own share (bench.py kernel_share), line vs trace
+    per = {}
+    for b, k in line["kernels"].items():
+        a_b = k.get("alg_bytes_per_launch")
+        if not a_b or b not in ms_a:
+            continue
+        fb = lambda ms: a_b / (ms * 1e-3) / 1e9 / peak  # noqa: E731
+        per[b] = {"line_frac": k.get("frac"), "rocprof_frac": round(fb(ms_a[b]), 4),
+                  "rocprof_isolated_frac": round(fb(ms_s[b]), 4) if b in ms_s else None,
+                  "rel_diff": round(fb(ms_a[b]) / k["frac"] - 1, 4) if k.get("frac") else None}
+    res["per_bucket"] = per
     print(json.dumps(res, indent=1))
     if a.out:
         with open(a.out, "w") as f:

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc passes (tools/pmc.sh) into per-kernel, per-launch HBM bytes.
+"""Summarise rocprofv3 --pmc passes (tools/pmc_all.sh, tools/evidence.sh) into per-kernel, per-launch HBM bytes.
 
 Reads gpurun_out/pmc/p*/run_counter_collection.csv, averages each counter over the dispatches of
 each kernel, and derives HBM bytes as MI355X_MICROARCH.md §HBM prescribes:
