@@ -602,6 +602,7 @@ int push_count(fw_op* op, const int64_t* key, const int64_t* val, int64_t n) {
   return snapshot(op);
 }
 
+hipStream_t input_stream_of(const fw_op* op);  // the stream device pushes read their columns on
 int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int64_t n,
                 bool async_ok) {
   if (n == 0) return FW_OK;
@@ -641,7 +642,9 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   const int32_t T = gather ? (int32_t)((n + FW_GTILE - 1) / FW_GTILE) : (int32_t)((n + FW_TILE - 1) / FW_TILE);
   const int64_t m = (int64_t)(c.P + 1) * T;
   // async input: the batch-only kernels run on bstream, after the aggregate that last used this scratch set
-  const bool two = async_ok && op->async_in && !c.side_output && !gather;
+  // (the same predicate as fw_input_stream, which the caller ordered its producer before: a batch that is not
+  // gathered while gather scratch exists stays on the operator's stream)
+  const bool two = async_ok && input_stream_of(op) == op->bstream && !gather;
   hipStream_t bs = two ? op->bstream : op->stream;
   if (two) HIP_OR_RETURN(op, hipStreamWaitEvent(bs, op->ev_done[nxt], 0));
   if (c.assigner == FW_SESSION) {

@@ -15,6 +15,13 @@ or WindowWordCount's Tuple2<String, Integer> (StringValue.writeString's varint e
     WireLayout([("string", "key"), ("int", "value")])
 whose decode also returns the key_hash column (String.hashCode); the key column holds the word's 64-bit id
 (keygroups.string_key_id), and the pair goes to a GpuWindowOperator with key_type="hashed".
+
+Key identity of String keys.  The operator keys its state by the 64-bit id (FNV-1a over the UTF-16 units, then
+fmix64), not by the string: two distinct strings with the same id would share their windows' state.  Routing stays
+exact (key groups come from String.hashCode, carried beside the id).  For k distinct keys the chance of any such
+collision is about k^2 / 2^65 (1e6 keys: 3e-8; 1e8 keys: 3e-4).  The host that owns the strings maps each fired
+row's id back to its string and can detect a collision there (two strings of one id), so a job whose key space is
+large enough for that risk to matter should do so; this library cannot, as it never holds the strings.
 """
 import ctypes
 
