@@ -943,161 +943,6 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_rsv(DevCfg c, int64
   scatter_staged_body<M_TUMB, RR, true>(c, wm, key, ts, val, kh, n, T, nullptr, part, DevSide{}, nullptr, rsv, rcap);
 }
 
-// ---- K2, the single pass at two workgroups per CU (k_scatter_rsv2; Long-keyed tumbling dense batches, P <= 1024).
-// k_scatter_rsv runs one 1024-thread workgroup per CU (its 8192-record staging takes the LDS), so each round's load,
-// reservation round trip and barriers leave the CU's memory pipe idle in turn.  Here a workgroup of FW_RSV_THREADS
-// stages RR = 4096 records in at most 80 KB -- the staging, the partitions of its records, and two P-word arrays:
-// cnt (per-partition counts, cumulative over the tile's rounds, so nothing is cleared between rounds) and base (the
-// round's staging bases, then its output bases); the block scan's words share the staging -- so two workgroups
-// share a CU, and the next round's records are loaded (FW_RSV_PF) while the current round is scanned, staged,
-// reserved and written.  Same output as k_scatter_rsv: partition p's run at [p * rcap, p * rcap + rsv[p]).
-#ifndef FW_RSV_THREADS
-#define FW_RSV_THREADS 512
-#endif
-#ifndef FW_RSV_PF
-#define FW_RSV_PF 2  // 0: no prefetch; 1: the next round's records loaded after the classify; 2: after the staging
-#endif
-constexpr int RSV2_RR = 4096;
-__host__ __device__ constexpr size_t rsv2_lds(int P) {
-  return (size_t)RSV2_RR * (sizeof(i64x2) + sizeof(uint16_t)) + 2 * (size_t)P * sizeof(uint32_t);
-}
-__global__ __launch_bounds__(FW_RSV_THREADS, 2 * FW_RSV_THREADS / 256) void k_scatter_rsv2(
-    DevCfg c, int64_t wm, const int64_t* __restrict__ key, const int64_t* __restrict__ ts,
-    const int64_t* __restrict__ val, int64_t n, int32_t T, PRec* __restrict__ part, uint32_t* rsv, int64_t rcap) {
-  specialize<M_TUMB>(c);
-  constexpr int TT = FW_RSV_THREADS, RR = RSV2_RR, RPT = RR / TT, H = RPT / 2;
-  constexpr int PQ = (1024 + TT - 1) / TT;  // partitions per thread (P <= 1024; blocked: thread x owns x * ppt + q)
-  static_assert(H % 2 == 0, "two halves of record pairs per thread");
-  extern __shared__ __attribute__((aligned(16))) uint8_t sraw[];
-  i64x2* stg = reinterpret_cast<i64x2*>(sraw);           // RR: the round's records sorted by partition
-  uint32_t* wsum = reinterpret_cast<uint32_t*>(sraw);    // block scan words (the staging is free during the scan)
-  uint16_t* sp = reinterpret_cast<uint16_t*>(stg + RR);  // RR: their partitions
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(sp + RR);  // P: records per partition so far in this tile
-  uint32_t* base = cnt + c.P;                            // P: staging bases (minus cnt before the round), then output bases
-  const int32_t tile = tile_of_block(T);
-  const int64_t tbase = (int64_t)tile * FW_TILE;
-  const int64_t tend = min(n, tbase + (int64_t)FW_TILE);
-  const int ppt = (c.P + TT - 1) / TT;
-  unsigned long long late = 0;
-  int bad_kg = 0, bad_ts = 0, over = 0;
-  i64x2* out = reinterpret_cast<i64x2*>(part);
-  uint32_t prev[PQ];  // cnt of this thread's partitions before the round
-#pragma unroll
-  for (int q = 0; q < PQ; q++) {
-    prev[q] = 0;
-    const int pp = threadIdx.x * ppt + q;
-    if (q < ppt && pp < c.P) cnt[pp] = 0;
-  }
-  // a round is two halves of H records per thread; the first half of the next round is loaded while the current
-  // round is reserved and written (FW_RSV_PF), the second half while the first is classified
-  int64_t k0[H], t0[H], v0[H], k1[H], t1[H], v1[H];
-  int32_t hh[H];
-  load_records<H / 2, true>(c, key, ts, val, nullptr, tbase, tend, k0, t0, v0, hh);
-  __syncthreads();
-  for (int64_t b = tbase; b < tend; b += RR) {
-    const int64_t b1 = b + (int64_t)H * TT;
-    load_records<H / 2, true>(c, key, ts, val, nullptr, b1, tend, k1, t1, v1, hh);
-    uint32_t rp[RPT];  // rank (cumulative, high 16 bits) | partition, or ~0 for no record
-    int64_t w[RPT], vv[RPT];
-    auto cls_half = [&](const int64_t (&k)[H], const int64_t (&t)[H], const int64_t (&v)[H], int64_t bh, int o) {
-#pragma unroll
-      for (int j = 0; j < H; j++) {
-        const int64_t i = rec_index(bh, j >> 1, j & 1);
-        rp[o + j] = 0xffffffffu;
-        vv[o + j] = v[j];
-        if (i >= tend) continue;
-        const int32_t p = partition_of(c, k[j], key_hash_of(FW_KEY_LONG, k[j], nullptr, i));
-        if (p < 0) {
-          bad_kg++;
-          continue;
-        }
-        int64_t last = 0;
-        int nwin = 0;
-        const int cls = classify(c, wm, t[j], &last, &nwin, k[j], 0);
-        if (cls == CLS_NORMAL) {
-          const int64_t d = compact_delta(c, last);
-          if (d < 0) {  // no compact form: the batch takes the offset path
-            over = 1;
-            continue;
-          }
-          rp[o + j] = atomicAdd(&cnt[p], 1u) << 16 | (uint32_t)p;
-          w[o + j] = compact_encode(c, k[j], d);
-        } else if (cls == CLS_LATE) {
-          late++;
-        } else if (cls == CLS_BADTS) {
-          bad_ts++;
-        }
-      }
-    };
-    cls_half(k0, t0, v0, b, 0);
-    cls_half(k1, t1, v1, b1, H);
-    if (FW_RSV_PF == 1 && b + RR < tend) load_records<H / 2, true>(c, key, ts, val, nullptr, b + RR, tend, k0, t0, v0, hh);
-    __syncthreads();
-    // the round's counts (cnt - prev), their exclusive scan; base = start - prev, so a record's staging slot is
-    // base[p] + its cumulative rank
-    uint32_t cq[PQ], sum = 0;
-#pragma unroll
-    for (int q = 0; q < PQ; q++) {
-      const int pp = threadIdx.x * ppt + q;
-      const uint32_t now = q < ppt && pp < c.P ? cnt[pp] : prev[q];
-      cq[q] = now - prev[q];
-      sum += cq[q];
-    }
-    uint32_t total;
-    uint32_t e = block_excl_scan(sum, wsum, &total);
-    uint32_t st0[PQ];
-#pragma unroll
-    for (int q = 0; q < PQ; q++) {
-      const int pp = threadIdx.x * ppt + q;
-      st0[q] = e;
-      if (q < ppt && pp < c.P) base[pp] = e - prev[q];
-      e += cq[q];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < RPT; j++) {
-      if (rp[j] == 0xffffffffu) continue;
-      const uint32_t p = rp[j] & 0xffffu;
-      const uint32_t pos = base[p] + (rp[j] >> 16);
-      stg[pos] = i64x2{w[j], vv[j]};
-      sp[pos] = (uint16_t)p;
-    }
-    // this round's piece of every partition it has records for: one global atomic each, issued before the barrier
-    uint32_t g[PQ];
-#pragma unroll
-    for (int q = 0; q < PQ; q++) {
-      const int pp = threadIdx.x * ppt + q;
-      g[q] = 0;
-      if (q < ppt && pp < c.P && cq[q]) g[q] = atomicAdd(&rsv[pp], cq[q]);
-    }
-    if (FW_RSV_PF == 2 && b + RR < tend) load_records<H / 2, true>(c, key, ts, val, nullptr, b + RR, tend, k0, t0, v0, hh);
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < PQ; q++) {
-      const int pp = threadIdx.x * ppt + q;
-      if (!(q < ppt && pp < c.P)) continue;
-      if (cq[q] && (int64_t)g[q] + cq[q] > rcap) {
-        over = 1;
-        base[pp] = 0xffffffffu;
-      } else {
-        base[pp] = (uint32_t)((int64_t)pp * rcap + g[q]) - st0[q];  // output index = base + staging index
-      }
-      prev[q] += cq[q];
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < total; i += TT) {
-      const uint32_t ob = base[sp[i]];
-      if (ob != 0xffffffffu) out[ob + i] = stg[i];
-    }
-    if (FW_RSV_PF == 0 && b + RR < tend) load_records<H / 2, true>(c, key, ts, val, nullptr, b + RR, tend, k0, t0, v0, hh);
-    // (the next round's classify writes only cnt; its barrier orders this copy-out before the scan reuses stg)
-  }
-  if (over) rsv[c.P + RSV_OVER] = 1;
-  if (bad_kg) atomicAdd(&rsv[c.P + RSV_KG], (uint32_t)bad_kg);
-  if (bad_ts) atomicAdd(&rsv[c.P + RSV_TS], (uint32_t)bad_ts);
-  if (late) atomicAdd(reinterpret_cast<unsigned long long*>(rsv + c.P + RSV_LATE), late);
-}
-
 // ---- K2b: ordered compaction of the ordered-path records of a tile (skipped by tiles that have none).
 // srow: the scanned ordered-path counts per tile, then the raw counts.  G: a gathered batch (tiles of
 // FW_GTILE; a normal record without a compact form takes the ordered path, as k_stage decided)
@@ -5185,9 +5030,6 @@ __device__ __forceinline__ bool dk_add_batch(DtLdsK& K, DtMisc& M, int vtype, co
   return true;
 }
 
-#ifndef FW_DT_RING
-#define FW_DT_RING 2  // register sets of compact records in k_dt_aggregate's record loop (2 or 3)
-#endif
 #ifndef FW_DT_TIMING
 #define FW_DT_TIMING 0  // 1: per-phase clocks of the compact launch, printed by its last workgroup (diagnostics)
 #endif
@@ -5223,7 +5065,7 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
       d[j] = crec[i < end ? i : end - 1];
     }
   };
-  i64x2 ra[RPT], rn[RPT], rc[RPT];
+  i64x2 ra[RPT], rn[RPT];
   for (int k = 0; k < (1 << hb); k++) {
     if constexpr (KW && SRC == DT_RECS) load(ra, begin);
     if constexpr (KW) {
@@ -5313,26 +5155,12 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
             return dk_add_batch<RPT>(U.k, M, c.vtype, ww, vv, dm) ? 0 : 1;
           };
           int res = 0;  // (ra: loaded at the top of the pass)
-          if (FW_DT_RING == 3) {  // three register sets: two rounds in flight while one is added
-            load(rn, begin + RS);
-            for (int64_t r0 = begin; r0 < end; r0 += 3 * RS) {
-              load(rc, r0 + 2 * RS);
-              if ((res = add_round(ra, r0))) break;
-              if (r0 + RS >= end) break;
-              load(ra, r0 + 3 * RS);
-              if ((res = add_round(rn, r0 + RS))) break;
-              if (r0 + 2 * RS >= end) break;
-              load(rn, r0 + 4 * RS);
-              if ((res = add_round(rc, r0 + 2 * RS))) break;
-            }
-          } else {
-            for (int64_t r0 = begin; r0 < end; r0 += 2 * RS) {
-              load(rn, r0 + RS);
-              if ((res = add_round(ra, r0))) break;
-              if (r0 + RS >= end) break;
-              load(ra, r0 + 2 * RS);
-              if ((res = add_round(rn, r0 + RS))) break;
-            }
+          for (int64_t r0 = begin; r0 < end; r0 += 2 * RS) {
+            load(rn, r0 + RS);
+            if ((res = add_round(ra, r0))) break;
+            if (r0 + RS >= end) break;
+            load(ra, r0 + 2 * RS);
+            if ((res = add_round(rn, r0 + RS))) break;
           }
           if (res == 2)  // a word equal to the EMPTY marker: the wide table takes the region
             M.widefb = 1;
@@ -5914,19 +5742,7 @@ bool rsv_eligible(const DevCfg& c) {
 }
 void launch_scatter_rsv(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
                         const int32_t* kh, int64_t n, int32_t T, PRec* part, uint32_t* rsv, int64_t rcap, hipStream_t s) {
-  static const int v2 = getenv("FW_RSV2") ? atoi(getenv("FW_RSV2")) : 0;
-  if (v2 && c.P <= 1024) {  // two workgroups per CU (80 KB of LDS each)
-    static bool attr2 = false;
-    if (!attr2) {
-      (void)hipFuncSetAttribute((const void*)k_scatter_rsv2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr2 = true;
-    }
-    hipLaunchKernelGGL(k_scatter_rsv2, dim3(T), dim3(FW_RSV_THREADS), rsv2_lds(c.P), s, c, wm, key, ts, val, n, T,
-                       part, rsv, rcap);
-    return;
-  }
-  static const int rr_env = getenv("FW_RSV_RR") ? atoi(getenv("FW_RSV_RR")) : 0;  // (diagnostics: 4096 or 8192)
-  const bool big = rr_env ? rr_env == 8192 && c.P <= 1024 : c.P <= 1024;
+  const bool big = c.P <= 1024;
   const int rr = big ? 8192 : 4096;
   const size_t sl = (size_t)rr * (sizeof(i64x2) + sizeof(uint16_t)) + (2 * (size_t)c.P + 1) * sizeof(uint32_t) +
                     (FW_TILE_THREADS / 64 + 1) * sizeof(uint32_t);
