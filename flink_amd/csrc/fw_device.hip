@@ -4814,17 +4814,24 @@ struct DtLds {
   unsigned long long cnt[FW_DT_SLOTS];
   int64_t sum[FW_DT_SLOTS], mn[FW_DT_SLOTS], mx[FW_DT_SLOTS];
 };
-constexpr int DK_SLOTS = (int)(sizeof(DtLds) / 40 / 16 * 16);
+constexpr int DK_SLOTS = (int)(sizeof(DtLds) / 36 / 16 * 16);  // 36 bytes a slot
 #ifndef FW_DK_FILL16
 #define FW_DK_FILL16 15  // claims stop at this many 16ths of the compact table (buckets of 4 keep probes short)
 #endif
 constexpr int DK_LIMIT = DK_SLOTS * FW_DK_FILL16 / 16;
 constexpr unsigned long long DK_EMPTY = ~0ull;  // (a record or entry whose word is this takes the wide table)
-constexpr int DK_BUCKETS = DK_SLOTS / 4;  // a word's home is a bucket of 4 slots (one 32-byte read)
+#ifndef FW_DK_BW
+#define FW_DK_BW 4  // slots per bucket of the compact table (4: a 32-byte read per probe, 2: one 16-byte read)
+#endif
+constexpr int DK_BW = FW_DK_BW;
+constexpr int DK_BUCKETS = DK_SLOTS / DK_BW;  // a word's home is a bucket of DK_BW slots
+// A compact slot's count is the 32-bit count of the region's window so far (an entry whose count would not fit sends
+// its region to the wide table); min and max sit side by side, read together before either is raised.
 struct DtLdsK {
+  i64x2 mm[DK_SLOTS];  // {min, max}
   alignas(16) unsigned long long kw[DK_SLOTS];
-  unsigned long long cnt[DK_SLOTS];
-  int64_t sum[DK_SLOTS], mn[DK_SLOTS], mx[DK_SLOTS];
+  int64_t sum[DK_SLOTS];
+  uint32_t cnt[DK_SLOTS];
 };
 union DtTab {
   DtLds w;
@@ -4839,14 +4846,15 @@ __device__ __forceinline__ uint32_t dt_bucket(uint32_t h) { return (uint32_t)(((
 __device__ __forceinline__ uint32_t dk_home(unsigned long long kw) {
   uint32_t h = (uint32_t)(kw >> 32) * 0x9E3779B1u ^ (uint32_t)kw;
   h ^= h >> 15;
-  return (uint32_t)(((uint64_t)h * DK_BUCKETS) >> 32) * 4u;
+  return (uint32_t)(((uint64_t)h * DK_BUCKETS) >> 32) * (uint32_t)DK_BW;
 }
-// the 4 words of the bucket at slot s0
-__device__ __forceinline__ void dk_read4(const DtLdsK& K, uint32_t s0, unsigned long long (&g)[4]) {
-  const i64x2 a = *reinterpret_cast<const i64x2*>(&K.kw[s0]);
-  const i64x2 b = *reinterpret_cast<const i64x2*>(&K.kw[s0 + 2]);
-  g[0] = (unsigned long long)a.x, g[1] = (unsigned long long)a.y, g[2] = (unsigned long long)b.x,
-  g[3] = (unsigned long long)b.y;
+// the DK_BW words of the bucket at slot s0
+__device__ __forceinline__ void dk_read4(const DtLdsK& K, uint32_t s0, unsigned long long (&g)[DK_BW]) {
+#pragma unroll
+  for (int q = 0; q < DK_BW; q += 2) {
+    const i64x2 a = *reinterpret_cast<const i64x2*>(&K.kw[s0 + q]);
+    g[q] = (unsigned long long)a.x, g[q + 1] = (unsigned long long)a.y;
+  }
 }
 // the hash pass of (key, window): prefix of a hash independent of the LDS slot's
 __device__ __forceinline__ int dt_pass(const DevCfg& c, int64_t key, int64_t start, int hb) {
@@ -4910,11 +4918,11 @@ __device__ __forceinline__ int dt_slot(DtLds& L, DtMisc& M, int64_t key, int64_t
 __device__ __forceinline__ int dk_slot(DtLdsK& K, DtMisc& M, unsigned long long kw, uint32_t s0) {
   for (int guard = 0; guard < 2 * DK_BUCKETS;) {
     asm volatile("" ::: "memory");
-    unsigned long long g[4];
+    unsigned long long g[DK_BW];
     dk_read4(K, s0, g);
     int e = -1;
 #pragma unroll
-    for (int q = 3; q >= 0; q--) {
+    for (int q = DK_BW - 1; q >= 0; q--) {
       if (g[q] == kw) return (int)s0 + q;
       if (g[q] == DK_EMPTY) e = q;
     }
@@ -4926,7 +4934,7 @@ __device__ __forceinline__ int dk_slot(DtLdsK& K, DtMisc& M, unsigned long long 
       if (o == kw) return (int)s0 + e;
       continue;
     }
-    s0 = s0 + 4 == (uint32_t)DK_SLOTS ? 0u : s0 + 4;
+    s0 = s0 + DK_BW == (uint32_t)DK_SLOTS ? 0u : s0 + DK_BW;
     guard++;
   }
   return -1;
@@ -4945,6 +4953,32 @@ __device__ __forceinline__ void dt_add(L& T, int s, int vtype, int64_t v) {
   }
   atomicMin((long long*)&T.mn[s], (long long)sv);
   atomicMax((long long*)&T.mx[s], (long long)sv);
+}
+// the compact table: the count as a 32-bit add, min / max raised only when the element passes them (a stale read
+// can only be above the minimum / below the maximum, so skipping is exact; LDS atomics are the record loop's cost)
+__device__ __forceinline__ void dt_add(DtLdsK& T, int s, int vtype, int64_t v) {
+  atomicAdd(&T.cnt[s], 1u);
+  int64_t sv = v;
+  if (vtype == FW_VAL_F64) {
+    atomicAdd((double*)&T.sum[s], __longlong_as_double(v));
+    sv = f64_sortable(v);
+  } else {
+    atomicAdd((unsigned long long*)&T.sum[s], (unsigned long long)v);
+  }
+  const i64x2 m = T.mm[s];
+  long long* mp = reinterpret_cast<long long*>(&T.mm[s]);
+  if (sv < m.x) atomicMin(mp, (long long)sv);
+  if (sv > m.y) atomicMax(mp + 1, (long long)sv);
+}
+__device__ __forceinline__ void dt_merge(DtLdsK& T, int s, int vtype, int64_t cnt, int64_t sum, int64_t mn, int64_t mx) {
+  atomicAdd(&T.cnt[s], (uint32_t)cnt);
+  if (vtype == FW_VAL_F64)
+    atomicAdd((double*)&T.sum[s], __longlong_as_double(sum));
+  else
+    atomicAdd((unsigned long long*)&T.sum[s], (unsigned long long)sum);
+  long long* mp = reinterpret_cast<long long*>(&T.mm[s]);
+  atomicMin(mp, (long long)mn);
+  atomicMax(mp + 1, (long long)mx);
 }
 template <class L>
 __device__ __forceinline__ void dt_merge(L& T, int s, int vtype, int64_t cnt, int64_t sum, int64_t mn, int64_t mx) {
@@ -5000,7 +5034,7 @@ template <int RPT>
 __device__ __forceinline__ bool dk_add_batch(DtLdsK& K, DtMisc& M, int vtype, const unsigned long long (&w)[RPT],
                                              const int64_t (&v)[RPT], uint32_t dm) {
   uint32_t s[RPT];
-  unsigned long long g[RPT][4];
+  unsigned long long g[RPT][DK_BW];
   // every home bucket read before any is used (plain reads: a word, once claimed, never changes, and a stale EMPTY
   // only sends the element to dk_slot, which re-reads)
 #pragma unroll
@@ -5012,7 +5046,10 @@ __device__ __forceinline__ bool dk_add_batch(DtLdsK& K, DtMisc& M, int vtype, co
 #pragma unroll
   for (int j = 0; j < RPT; j++) {
     if (dm >> j & 1) continue;
-    const int q = g[j][0] == w[j] ? 0 : g[j][1] == w[j] ? 1 : g[j][2] == w[j] ? 2 : g[j][3] == w[j] ? 3 : -1;
+    int q = -1;
+#pragma unroll
+    for (int b = DK_BW - 1; b >= 0; b--)
+      if (g[j][b] == w[j]) q = b;
     if (q >= 0)
       dt_add(K, (int)s[j] + q, vtype, v[j]);
     else
@@ -5071,10 +5108,9 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
     if constexpr (KW) {
       for (int h = threadIdx.x; h < DK_SLOTS; h += FW_DT_THREADS) {
         U.k.kw[h] = DK_EMPTY;
-        U.k.cnt[h] = 0;
+        U.k.cnt[h] = 0u;
         U.k.sum[h] = 0;
-        U.k.mn[h] = LMAX;
-        U.k.mx[h] = LMIN;
+        U.k.mm[h] = i64x2{LMAX, LMIN};
       }
     } else {
       for (int h = threadIdx.x; h < FW_DT_SLOTS; h += FW_DT_THREADS) U.w.tag[h] = LT_EMPTY;
@@ -5102,7 +5138,8 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
         if constexpr (KW) {
           const int64_t d = compact_delta(c, e[u].start);
           const unsigned long long w = d < 0 ? DK_EMPTY : (unsigned long long)compact_encode(c, e[u].key, d);
-          if (w == DK_EMPTY) {
+          // (a window's count must stay below 2^32 with this batch's records added: else the wide table)
+          if (w == DK_EMPTY || (uint64_t)e[u].cnt + (uint64_t)(end - begin) > 0xffffffffull) {
             M.widefb = 1;
             break;
           }
@@ -5254,8 +5291,9 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
           compact_decode(c, p, (int64_t)U.k.kw[h], &e.key, &e.start);
           e.cnt = (int64_t)U.k.cnt[h];
           e.sum = U.k.sum[h];
-          e.mn = U.k.mn[h];
-          e.mx = U.k.mx[h];
+          const i64x2 m = U.k.mm[h];
+          e.mn = m.x;
+          e.mx = m.y;
         } else {
           const i64x2 kv = U.w.kv[h];
           e.key = kv.x;
