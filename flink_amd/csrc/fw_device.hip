@@ -2522,6 +2522,41 @@ __device__ __forceinline__ int32_t new_slot(const SlowCtx& x, const Region& r, i
   return s;
 }
 
+// one accumulator block for a window the ordered path creates (the protocol of agg_flush's reservation, k = 1)
+__device__ __forceinline__ uint64_t pool_alloc_one(const DevCfg& c, Status* st) {
+  const int t = atomicSub(&c.pool_ctr[0], 1);
+  if (t >= 1) return (uint64_t)c.pool_free[t - 1];
+  atomicAdd(&c.pool_ctr[0], 1);
+  const long long bump = atomicAdd(&c.pool_ctr[1], 1);
+  if (bump + 1 > c.pool_blocks) {
+    atomicOr(&st->flags, FW_STATUS_POOL);
+    return 0;
+  }
+  return (uint64_t)bump;
+}
+// HyperLogLog add of one item into block blk (k_hll_update's raise: CAS on the register's word while larger, the
+// chunk marked when the register leaves zero)
+__device__ __forceinline__ void hll_raise(const DevCfg& c, uint64_t blk, int64_t item) {
+  const int p = c.hll_p;
+  const uint64_t h = fmix64((uint64_t)item);
+  const uint32_t j = (uint32_t)(h >> (64 - p));
+  const uint32_t rank = (uint32_t)__clzll((long long)((h << p) | (1ull << (p - 1)))) + 1u;
+  uint8_t* base = c.pool + blk * (uint64_t)c.pool_bytes;
+  uint32_t* w = reinterpret_cast<uint32_t*>(base + hll_hdr_bytes(p) + (j & ~3u));
+  const int sh = (int)(j & 3) * 8;
+  uint32_t o = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (((o >> sh) & 0xffu) < rank) {
+    const uint32_t nw = (o & ~(0xffu << sh)) | (rank << sh);
+    if (__hip_atomic_compare_exchange_strong(w, &o, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      if (((o >> sh) & 0xffu) == 0u) {
+        const uint32_t ch = j >> 4;
+        atomicOr(reinterpret_cast<uint32_t*>(base) + (ch >> 5), 1u << (ch & 31u));
+      }
+      break;
+    }
+  }
+}
+
 // WindowOperator.processElement, non-merging branch (WindowOperator.java:371-407)
 __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int64_t t, int64_t v, int64_t fo, bool* skipped) {
   const DevCfg& c = x.c;
@@ -2541,12 +2576,13 @@ __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int6
       ne.start = s;
       ne.end = e;
       acc_clear(ne);
-      ne.meta = 0;
+      ne.meta = c.agg == FW_AGG_HLL ? (int64_t)(pool_alloc_one(c, x.st) << 1) : 0;
       slot = new_slot(x, r, p, h, ne);
       if (slot < 0) continue;
     }
     Entry en = r.ent[slot];
     acc_add(c, en, v, fo);
+    if (c.agg == FW_AGG_HLL) hll_raise(c, pool_block_of(en), v);  // (k_hll_update takes the partitioned records)
     bool keep = true;
     if (jsub(e, 1) <= x.wm) {  // EventTimeTrigger.onElement -> FIRE (WindowOperator.java:395-401)
       emit_one(c, x.out, x.st, en);
@@ -2893,27 +2929,35 @@ __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __rest
   // region's load is a home-slot hit; a miss walks the rest of its probe chain on its own)
   constexpr int HU = 4;
   int32_t pp = p0_s;
+  // sliding windows (fan-out): a record raises the same register in each of its nwin windows, newest first
+  // (SlidingEventTimeWindows.java:67-81); the windows are walked one per pass of this loop
   for (int64_t ib = i0 + threadIdx.x; ib < i1; ib += (int64_t)blockDim.x * HU) {
+   int32_t nw_max = 1;
+   for (int32_t wi = 0; wi < nw_max; wi++) {
     int64_t key[HU], last[HU], val[HU];
     int32_t part_of_rec[HU];
     bool in[HU];
+    int32_t pp_w = pp;
 #pragma unroll
     for (int u = 0; u < HU; u++) {
       const int64_t i = ib + (int64_t)u * blockDim.x;
       in[u] = i < i1;
       key[u] = last[u] = val[u] = 0;
-      part_of_rec[u] = pp;
+      part_of_rec[u] = pp_w;
       if (!in[u]) continue;
-      while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
-      part_of_rec[u] = pp;
+      while ((int64_t)offs[(int64_t)(pp_w + 1) * T] <= i) pp_w++;
+      part_of_rec[u] = pp_w;
       if (cmp) {
         const i64x2 r = reinterpret_cast<const i64x2*>(part)[i];
-        compact_decode(c, pp, r.x, &key[u], &last[u]);
+        compact_decode(c, pp_w, r.x, &key[u], &last[u]);
         val[u] = r.y;
       } else {
         const PRec rec = part[i];
         key[u] = rec.key;
-        last[u] = rec.last;
+        const int32_t nw = (int32_t)(rec.nwin & 0xffff);
+        nw_max = max(nw_max, nw);
+        in[u] = wi < nw;
+        last[u] = jsub(rec.last, (int64_t)wi * c.slide);
         val[u] = rec.val;
       }
     }
@@ -2982,6 +3026,8 @@ __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __rest
         }
       }
     }
+    if (wi + 1 == nw_max) pp = pp_w;
+   }
   }
 }
 
@@ -4131,6 +4177,7 @@ constexpr int PF_LIMIT = 1536;
 constexpr int PF_U = 4;  // region slots per thread in flight in the pane scan
 struct PaneLds {
   uint32_t tag[PF_SLOTS];  // 0 empty, 1 being claimed, 2 full
+  uint32_t sel[PF_SLOTS];  // minBy / maxBy: region slot of the pane holding the window's selected element
   int64_t key[PF_SLOTS];
   unsigned long long cnt[PF_SLOTS];
   int64_t sum[PF_SLOTS], mn[PF_SLOTS], mx[PF_SLOTS];
@@ -4140,7 +4187,9 @@ struct PaneLds {
 };
 __device__ __forceinline__ uint32_t pf_hash(int64_t key) { return (uint32_t)(fmix64((uint64_t)key ^ 0x243F6A8885A308D3ull) >> 32); }
 
-__device__ __forceinline__ bool pf_upsert(const DevCfg& c, PaneLds& L, const Entry& e, uint32_t h) {
+// (pane: the entry's region slot; ent: the region's entries, read back by a minBy / maxBy selection)
+__device__ __forceinline__ bool pf_upsert(const DevCfg& c, PaneLds& L, const Entry& e, uint32_t h, uint32_t pane,
+                                          const Entry* __restrict__ ent) {
   uint32_t s = (h * 0x9E3779B1u) >> (32 - 11);  // PF_SLOTS = 2^11
   for (int i = 0, spin = 0; i < PF_SLOTS;) {
     if (++spin > (1 << 24)) return false;  // a slot never published: cannot happen; the pass reports overflow
@@ -4163,6 +4212,7 @@ __device__ __forceinline__ bool pf_upsert(const DevCfg& c, PaneLds& L, const Ent
       L.sum[s] = 0;
       L.mn[s] = LMAX;
       L.mx[s] = LMIN;
+      L.sel[s] = 0xffffffffu;
       __hip_atomic_store(&L.tag[s], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       break;
     }
@@ -4173,6 +4223,22 @@ __device__ __forceinline__ bool pf_upsert(const DevCfg& c, PaneLds& L, const Ent
     atomicAdd((double*)&L.sum[s], __longlong_as_double(e.sum));
   else
     atomicAdd((unsigned long long*)&L.sum[s], (unsigned long long)e.sum);
+  if (agg_by(c.agg)) {
+    // minBy / maxBy (ComparableAggregator.java:72-94, first = true): the window's element is the lexicographically
+    // smallest (key, ordinal) over its panes (a pane's entry holds its own), which is not two independent min / max;
+    // the slot keeps the region slot of the pane holding it, replaced by CAS while this pane's pair is smaller
+    uint32_t cur = __hip_atomic_load(&L.sel[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (;;) {
+      if (cur != 0xffffffffu) {
+        const i64x2 b = *reinterpret_cast<const i64x2*>(&ent[cur].mn);  // {mn, mx} of the current choice
+        if (!by_less(e.mn, e.mx, b.x, b.y)) break;
+      }
+      const uint32_t old = atomicCAS(&L.sel[s], cur, pane);
+      if (old == cur) break;
+      cur = old;
+    }
+    return true;
+  }
   atomicMin((long long*)&L.mn[s], (long long)e.mn);
   atomicMax((long long*)&L.mx[s], (long long)e.mx);
   return true;
@@ -4245,7 +4311,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_fire_panes(DevCfg c, int64_t wm,
       if (!forming) continue;
       if (lo_e <= E && E <= hi_e) {
         const uint32_t h = pf_hash(e.key);
-        if (!over && (uint64_t)h >= lo && (uint64_t)h < lo + width && !pf_upsert(c, L, e, h)) over = true;
+        if (!over && (uint64_t)h >= lo && (uint64_t)h < lo + width && !pf_upsert(c, L, e, h, s, rx.ent)) over = true;
       }
       const int64_t cand = max(lo_e, E + c.slide);
       if (E < LMAX - c.slide && cand <= hi_e) en = min(en, cand);
@@ -4306,6 +4372,11 @@ __global__ __launch_bounds__(PF_THREADS) void k_fire_panes(DevCfg c, int64_t wm,
         r.sum = L.sum[h];
         r.mn = L.mn[h];
         r.mx = L.mx[h];
+        if (agg_by(c.agg)) {  // the selected element's (key, ordinal), from its pane
+          const uint32_t ps = L.sel[h];
+          r.mn = rx.ent[ps].mn;
+          r.mx = rx.ent[ps].mx;
+        }
         write_row(c, out, L.base + (unsigned long long)atomicAdd(&L.wpos, 1), r);
       }
       if (tid == 0) atomicAdd(&st->fired_total, (unsigned long long)n);

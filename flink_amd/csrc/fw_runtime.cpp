@@ -872,9 +872,10 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     snprintf(msg, sizeof msg, "HyperLogLog precision must be in [4, 16], got %d", hll_p);
   bool unsupported = false;
   if (!msg[0] && cfg.aggregate == FW_AGG_HLL &&
-      (cfg.assigner != FW_TUMBLING || cfg.allowed_lateness != 0 || cfg.value_type != FW_VAL_I64)) {
-    snprintf(msg, sizeof msg, "the HyperLogLog aggregate is offered for tumbling windows without allowed lateness "
-                              "over a Long item column");
+      ((cfg.assigner != FW_TUMBLING && cfg.assigner != FW_SLIDING) || cfg.allowed_lateness != 0 ||
+       cfg.value_type != FW_VAL_I64)) {
+    snprintf(msg, sizeof msg, "the HyperLogLog aggregate is offered for tumbling and sliding windows without allowed "
+                              "lateness over a Long item column");
     unsupported = true;
   }
   const int32_t td_delta = cfg.tdigest_compression ? cfg.tdigest_compression : 100;
@@ -969,7 +970,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   // sliding windows whose size is a multiple of the slide, without allowed lateness, are kept as panes:
   // one state update per element instead of size/slide (DevCfg::panes; FW_NO_PANES=1 disables it)
   c.panes = cfg.assigner == FW_SLIDING && cfg.allowed_lateness == 0 && cfg.size > cfg.slide &&
-            cfg.size % cfg.slide == 0 && cfg.aggregate != FW_AGG_MINBY && cfg.aggregate != FW_AGG_MAXBY &&
+            cfg.size % cfg.slide == 0 && cfg.aggregate != FW_AGG_HLL &&  // (HLL: one register block per window)
             !(getenv("FW_NO_PANES") && atoi(getenv("FW_NO_PANES")));
   if (cfg.assigner != FW_SESSION) {
     make_div_inv((uint64_t)c.size, &c.mag_size, &c.l_size);

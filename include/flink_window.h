@@ -79,8 +79,9 @@ extern "C" {
                                       (largest) field, the earlier one among equal fields; Integer, Long or
                                       Double (Double.compare order) fields.  Rows carry count, sum, min = the
                                       selected field value and max = the arrival ordinal of the selected element
-                                      (exact: (field, ordinal) pairs compare in full).  Sliding windows use the
-                                      per-window form (no panes). */
+                                      (exact: (field, ordinal) pairs compare in full).  Sliding windows keep
+                                      panes like the other aggregates: a window's element is the smallest
+                                      (field, ordinal) pair over its panes. */
 #define FW_AGG_MAXBY 4
 #define FW_AGG_TDIGEST 6           /* t-digest quantiles of a Double field (definition in DESIGN.md
                                       §t-digest and oracle/window_oracle.h): a merging t-digest with the k1 scale

@@ -203,6 +203,20 @@ def test_gpu_min_by_max_by_vs_oracle(cfg, value_type, by):
 
 
 @pytest.mark.parametrize("by", ["min", "max"])
+@pytest.mark.parametrize("value_type", ["i64", "f64"])
+def test_gpu_min_by_max_by_panes_hot_keys(value_type, by):
+    # minBy / maxBy over sliding windows kept as panes (a window's element = the smallest (field, ordinal) pair over
+    # its panes, ComparableAggregator.java:72-94), Zipf keys so hot partitions split into chunks, 10 s / 1 s windows
+    batches, wms = _stream(200_000, 25_000, 3000, bound=300, jitter=200, rate=10_000, zipf=1.1)
+    batches = [(k, t, _by_values(v, value_type)) for k, t, v in batches]
+    cfg = dict(assigner="sliding", size=10_000, slide=1000, value_type=value_type, by=by)
+    assert _panes(cfg)
+    g, r, gs, rs, gl, rl = _run_both(cfg, batches, wms)
+    assert_rows_equal(g, r, {"i64": "long", "f64": "double"}[value_type])
+    assert gl == rl
+
+
+@pytest.mark.parametrize("by", ["min", "max"])
 def test_gpu_min_by_ties_straddle_2_32(by):
     # ordinals are compared in full: a restore numbers later pushes after the restored ordinals, so the batch's
     # elements get ordinals 2^32 - 2000 ...; tied fields across 2^32 keep the earlier element
@@ -769,6 +783,26 @@ def test_gpu_hll_vs_oracle(p, zipf):
     gpu.close()
 
 
+@pytest.mark.parametrize("p,zipf", [(10, 1.1), (6, None)], ids=["p10-zipf", "p6-uniform"])
+def test_gpu_hll_sliding_vs_oracle(p, zipf):
+    # HyperLogLog over sliding windows (WindowedStream.aggregate takes any assigner, WindowedStream.java:687-852):
+    # every element raises its register in each of its size / slide windows, each window's registers their own block;
+    # registers bit-exact against the oracle's per-window accumulators, late elements dropped alike
+    from flink_amd import HyperLogLog
+    from flink_amd.operator import GpuWindowOperator
+    batches, wms = _stream(120_000, 20_000, 3000, bound=300, jitter=600, rate=50_000, zipf=zipf)
+    gpu = GpuWindowOperator(SlidingEventTimeWindows.of(3000, 1000), HyperLogLog(p), expected_entries=30_000)
+    ref = orc.WindowOperatorOracle(assigner="sliding", size=3000, slide=1000, hll_p=p)
+    for (k, t, v), wm in zip(batches, wms):
+        gpu.process(k, t, v)
+        ref.process(k, t, v)
+        gpu.watermark(wm)
+        ref.watermark(wm)
+    assert gpu.late_dropped == ref.late_dropped
+    _hll_rows_equal(gpu.rows(), ref.rows())
+    gpu.close()
+
+
 def test_gpu_hll_register_blocks_are_recycled():
     # many windows over few keys with a pool sized for one window's entries: every fired block must be
     # zeroed and reused, or the pool runs out (FW_ERR_CAPACITY) or stale registers inflate the estimates
@@ -791,7 +825,7 @@ def test_gpu_hll_refuses_unsupported_shapes():
     from flink_amd import _native as N
     from flink_amd.operator import GpuWindowOperator
     with pytest.raises(N.NativeError) as e:
-        GpuWindowOperator(SlidingEventTimeWindows.of(3000, 1000), HyperLogLog(12))
+        GpuWindowOperator(EventTimeSessionWindows.with_gap(3000), HyperLogLog(12))
     assert e.value.code == N.FW_ERR_UNSUPPORTED
     with pytest.raises(N.NativeError) as e:
         GpuWindowOperator(TumblingEventTimeWindows.of(1000), HyperLogLog(12), allowed_lateness=10)
