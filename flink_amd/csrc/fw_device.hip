@@ -2522,6 +2522,8 @@ __device__ __forceinline__ int32_t new_slot(const SlowCtx& x, const Region& r, i
   return s;
 }
 
+__device__ void hll_clear(const DevCfg& c, uint64_t blk);
+__device__ void hll_estimate(const DevCfg& c, uint64_t blk, double* est, int64_t* zeros_out, int64_t* lo_out);
 // one accumulator block for a window the ordered path creates (the protocol of agg_flush's reservation, k = 1)
 __device__ __forceinline__ uint64_t pool_alloc_one(const DevCfg& c, Status* st) {
   const int t = atomicSub(&c.pool_ctr[0], 1);
@@ -2585,10 +2587,27 @@ __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int6
     if (c.agg == FW_AGG_HLL) hll_raise(c, pool_block_of(en), v);  // (k_hll_update takes the partitioned records)
     bool keep = true;
     if (jsub(e, 1) <= x.wm) {  // EventTimeTrigger.onElement -> FIRE (WindowOperator.java:395-401)
-      emit_one(c, x.out, x.st, en);
+      if (c.agg == FW_AGG_HLL) {  // getResult from the window's registers (the window stays unless purged)
+        Entry fr = en;
+        double est;
+        hll_estimate(c, pool_block_of(en), &est, &fr.mn, &fr.mx);
+        fr.sum = __double_as_longlong(est);
+        emit_one(c, x.out, x.st, fr);
+      } else {
+        emit_one(c, x.out, x.st, en);
+      }
       if (c.purging) keep = false;  // FIRE_AND_PURGE
     } else {
       en.meta |= FW_TIMER;  // registerEventTimeTimer(maxTimestamp)
+    }
+    if (!keep && c.agg == FW_AGG_HLL) {
+      // the purged window keeps its slot and zeroed block as empty state (cnt 0: nothing fires from it, and its GC
+      // timer frees the block in k_fire): this kernel pops blocks for new windows, and a push beside those pops could
+      // hand out a block before its slot on the free stack is written
+      hll_clear(c, pool_block_of(en));
+      acc_clear(en);
+      en.meta &= ~(int64_t)FW_TIMER;
+      keep = true;
     }
     if (keep) {
       r.ent[slot] = en;
@@ -2801,7 +2820,9 @@ __global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, 
 // one wave per fired row: estimate from the row's register block (out.mn holds its id), then zero the
 // block and push it on the free stack.  S = sum_j 2^(65-p-M[j]) exactly, in 128 bits.  Only the chunks the
 // block's bitmap marks are read (and zeroed): every register of an unmarked chunk is zero.
+// stack_slot < 0: the window stays (FIRE without purge under allowed lateness): the block is read, not zeroed or freed
 __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, int64_t stack_slot) {
+  const bool release = stack_slot >= 0;
   const int lane = __lane_id();
   const int p = c.hll_p, rmax = 65 - p;
   const int64_t m = (int64_t)1 << p;
@@ -2843,10 +2864,11 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, in
           s = t;
           zeros += r == 0;
         }
-      q[jj[u]] = make_uint4(0, 0, 0, 0);
+      if (release) q[jj[u]] = make_uint4(0, 0, 0, 0);
     }
   }
-  for (int32_t w = lane; w < nw; w += 64) bits[w] = 0u;
+  if (release)
+    for (int32_t w = lane; w < nw; w += 64) bits[w] = 0u;
   uint64_t hi = sh, lo = s;
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t lo2 = __shfl_xor(lo, o, 64), hi2 = __shfl_xor(hi, o, 64);
@@ -2872,8 +2894,46 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, in
     out.sum[row] = __double_as_longlong(est);
     out.mn[row] = (int64_t)zeros;
     out.mx[row] = (int64_t)lo;
-    c.pool_free[stack_slot] = (uint32_t)blk;  // zeroed before the next kernel can hand it out
+    if (release) c.pool_free[stack_slot] = (uint32_t)blk;  // zeroed before the next kernel can hand it out
   }
+}
+// the same estimate by one thread, the block kept (a late firing of the ordered path under allowed lateness)
+__device__ void hll_estimate(const DevCfg& c, uint64_t blk, double* est, int64_t* zeros_out, int64_t* lo_out) {
+  const int p = c.hll_p, rmax = 65 - p;
+  const int64_t m = (int64_t)1 << p;
+  const uint8_t* base = c.pool + blk * (uint64_t)c.pool_bytes;
+  const uint32_t* bits = reinterpret_cast<const uint32_t*>(base);
+  const uint4* q = reinterpret_cast<const uint4*>(base + hll_hdr_bytes(p));
+  const int32_t nq = (int32_t)(m / 16);
+  uint64_t lo = 0, hi = 0;
+  uint32_t zeros = 0, touched = 0;
+  for (int32_t jq = 0; jq < nq; jq++) {
+    if (!((bits[jq >> 5] >> (jq & 31)) & 1u)) continue;
+    touched++;
+    const uint4 v = q[jq];
+    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+    for (int k = 0; k < 4; k++)
+      for (int b = 0; b < 4; b++) {
+        const uint32_t r = (ws[k] >> (8 * b)) & 0xffu;
+        const uint64_t t = lo + (1ull << (rmax - (int)r));
+        hi += t < lo;
+        lo = t;
+        zeros += r == 0;
+      }
+  }
+  const uint64_t un = (uint64_t)(nq - (int32_t)touched) * 16u;
+  const uint64_t ulo = un << rmax, uhi = rmax ? un >> (64 - rmax) : 0ull;
+  const uint64_t t = lo + ulo;
+  hi = hi + uhi + (t < lo ? 1ull : 0ull);
+  lo = t;
+  zeros += (uint32_t)un;
+  const double sd = (double)hi * 18446744073709551616.0 + (double)lo;
+  const double md = (double)m;
+  const double alpha = m == 16 ? 0.673 : m == 32 ? 0.697 : m == 64 ? 0.709 : 0.7213 / (1.0 + 1.079 / md);
+  const double raw = (alpha * md * md) * ldexp(1.0, rmax) / sd;
+  *est = (raw <= 2.5 * md && zeros > 0) ? md * log(md / (double)zeros) : raw;
+  *zeros_out = (int64_t)zeros;
+  *lo_out = (int64_t)lo;
 }
 // one thread: zero a register block's marked chunks and its bitmap (a window collected without a row)
 __device__ void hll_clear(const DevCfg& c, uint64_t blk) {
@@ -4101,6 +4161,9 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
   if (live) atomicAdd(&live_s, live);
   if (nt != LMAX) atomicMin(&next_s, (long long)nt);
   __syncthreads();
+  __shared__ int nrel_s;  // HLL rows whose window goes (their blocks are freed by the finish)
+  if (threadIdx.x == 0) nrel_s = 0;
+  __syncthreads();
   if (nfire) {
     unsigned long long pos = base_s + pos0;
     for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x * FIRE_U) {
@@ -4118,10 +4181,14 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
       for (int u = 0; u < FIRE_U; u++) {
         if (st_kind(w[u]) != SLOT_LIVE) continue;
         Entry e = eu[u], fe;
-        if (!fire_decide(c, wm, e, fe).fire) continue;
+        const FireDecision d2 = fire_decide(c, wm, e, fe);
+        if (!d2.fire) continue;
         if ((int64_t)pos < out.cap) {
           write_row(c, out, pos, fe);
-          if (c.agg == FW_AGG_HLL) out.mn[pos] = (int64_t)pool_block_of(fe);  // read back by hll_finish
+          if (c.agg == FW_AGG_HLL) {  // read back by hll_finish: the block, and its free-stack slot when it goes
+            out.mn[pos] = (int64_t)pool_block_of(fe);
+            out.mx[pos] = d2.keep ? -1 : (int64_t)atomicAdd(&nrel_s, 1);
+          }
           if (c.agg == FW_AGG_TDIGEST) out.sum[pos] = (int64_t)pool_block_of(fe);  // read back by td_finish
         } else {
           atomicOr(&st->flags, FW_STATUS_OUT_FULL);
@@ -4132,13 +4199,17 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
   }
   if (c.pool_bytes && total) {
     __shared__ int hl_sb;
+    __syncthreads();  // (nrel_s complete)
     __threadfence_block();
-    if (threadIdx.x == 0) hl_sb = atomicAdd(&c.pool_ctr[0], (int)total);  // free-stack slots for this workgroup
+    // free-stack slots for this workgroup's released blocks (HLL: the rows whose window goes; t-digest: every row)
+    if (threadIdx.x == 0) hl_sb = atomicAdd(&c.pool_ctr[0], c.agg == FW_AGG_HLL ? nrel_s : (int)total);
     __syncthreads();
     const uint64_t end = min((unsigned long long)out.cap, base_s + total);
     if (c.agg == FW_AGG_HLL) {
-      for (uint64_t r = base_s + (threadIdx.x >> 6); r < end; r += blockDim.x >> 6)
-        hll_finish(c, out, r, hl_sb + (int64_t)(r - base_s));
+      for (uint64_t r = base_s + (threadIdx.x >> 6); r < end; r += blockDim.x >> 6) {
+        const int64_t ri = out.mx[r];  // (every lane reads it before lane 0 overwrites it)
+        hll_finish(c, out, r, ri < 0 ? -1 : hl_sb + ri);
+      }
     } else {
       __shared__ unsigned long long cent_s;
       if (threadIdx.x == 0) cent_s = 0;

@@ -491,6 +491,7 @@ int settle(fw_op* op) {
     c.ord_base = S.ord_base;
     c.wide = S.wide_word(op->dc.P);
     if (S.partials) {  // a partials push: only its merge can have suspended
+      c.nt_floor = fwdev::pane_nt_floor(c, S.wm);  // (panes: a new pane's first window)
       timed(op, K_AGGREGATE, [&] {
         fwdev::launch_pmerge(c, S.pparts, S.hist, S.T, op->tb, op->prog, 1, op->d_status, op->stream);
       });
@@ -763,13 +764,19 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
 
 
 // ---- pre-shuffle combining (fw_combine_extract_device / fw_push_partials_device)
+// tumbling windows, or sliding windows kept as panes (size % slide == 0): a pane's partial is classified by its
+// start exactly as each of its elements is (they all share the pane's newest window), so merging it at the receiver
+// equals pushing its records (round 4)
 bool combine_eligible(const fw_config& c) {
-  return c.assigner == FW_TUMBLING && c.aggregate == FW_AGG_COUNT_SUM_MIN_MAX && c.allowed_lateness == 0 &&
-         !c.side_output && (c.key_kind == FW_KEY_LONG || c.key_kind == FW_KEY_INT);
+  const bool panes = c.assigner == FW_SLIDING && c.slide > 0 && c.size > c.slide && c.size % c.slide == 0 &&
+                     !(getenv("FW_NO_PANES") && atoi(getenv("FW_NO_PANES")));
+  return (c.assigner == FW_TUMBLING || panes) && c.aggregate == FW_AGG_COUNT_SUM_MIN_MAX &&
+         c.allowed_lateness == 0 && !c.side_output && (c.key_kind == FW_KEY_LONG || c.key_kind == FW_KEY_INT);
 }
 // what a partial's representation depends on (fw_partials.config); never 0, so a zeroed struct never matches
 uint64_t combine_config_tag(const fw_config& c) {
-  const int64_t f[] = {c.assigner, c.size, c.offset, c.value_type, c.key_kind, c.max_parallelism, c.aggregate};
+  const int64_t f[] = {c.assigner, c.size, c.offset, c.value_type, c.key_kind, c.max_parallelism, c.aggregate,
+                       c.assigner == FW_SLIDING ? c.slide : 0};
   uint64_t h = 0x9E3779B97F4A7C15ull;
   for (int64_t x : f) {
     h ^= (uint64_t)x + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
@@ -798,6 +805,7 @@ int push_partials(fw_op* op, const PartialCols& in, int64_t n) {
   timed(op, K_SCATTER, [&] {
     fwdev::launch_pscatter(c, op->wm, in, n, T, S.hist, S.pparts, op->d_status, op->stream);
   });
+  c.nt_floor = fwdev::pane_nt_floor(c, op->wm);  // (panes: a new pane's first window, lds_delta)
   timed(op, K_AGGREGATE, [&] {
     fwdev::launch_pmerge(c, S.pparts, S.hist, T, op->tb, op->prog, 0, op->d_status, op->stream);
   });
@@ -872,10 +880,9 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     snprintf(msg, sizeof msg, "HyperLogLog precision must be in [4, 16], got %d", hll_p);
   bool unsupported = false;
   if (!msg[0] && cfg.aggregate == FW_AGG_HLL &&
-      ((cfg.assigner != FW_TUMBLING && cfg.assigner != FW_SLIDING) || cfg.allowed_lateness != 0 ||
-       cfg.value_type != FW_VAL_I64)) {
-    snprintf(msg, sizeof msg, "the HyperLogLog aggregate is offered for tumbling and sliding windows without allowed "
-                              "lateness over a Long item column");
+      ((cfg.assigner != FW_TUMBLING && cfg.assigner != FW_SLIDING) || cfg.value_type != FW_VAL_I64)) {
+    snprintf(msg, sizeof msg, "the HyperLogLog aggregate is offered for tumbling and sliding windows over a Long item "
+                              "column");
     unsupported = true;
   }
   const int32_t td_delta = cfg.tdigest_compression ? cfg.tdigest_compression : 100;
@@ -1463,8 +1470,8 @@ int fw_combine_extract_device(fw_op* op, int32_t world, fw_partials* out, int64_
   if (!op || !n || world < 1 || (world > 1 && !counts)) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   if (!combine_eligible(op->cfg))
     return set_err(op, FW_ERR_UNSUPPORTED,
-                   "combining needs tumbling windows, the count/sum/min/max aggregate, no allowed lateness, no side "
-                   "output and Long or Integer keys");
+                   "combining needs tumbling windows or sliding windows kept as panes, the count/sum/min/max aggregate, no "
+                   "allowed lateness, no side output and Long or Integer keys");
   if (op->wm != INT64_MIN)
     return set_err(op, FW_ERR_STATE, "a combiner's watermark is never advanced (it would fire or drop partials)");
   if (world > op->cfg.max_parallelism) return set_err(op, FW_ERR_ARG, "more subtasks than key groups");
@@ -1505,8 +1512,8 @@ int fw_push_partials_device(fw_op* op, const fw_partials* in, int64_t n) {
   if (!op || !in || n < 0) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   if (!combine_eligible(op->cfg))
     return set_err(op, FW_ERR_UNSUPPORTED,
-                   "combining needs tumbling windows, the count/sum/min/max aggregate, no allowed lateness, no side "
-                   "output and Long or Integer keys");
+                   "combining needs tumbling windows or sliding windows kept as panes, the count/sum/min/max aggregate, no "
+                   "allowed lateness, no side output and Long or Integer keys");
   if (n > 0 && (!in->key || !in->start || !in->cnt || !in->sum || !in->min || !in->max))
     return set_err(op, FW_ERR_ARG, "null column");
   if (in->config != combine_config_tag(op->cfg))

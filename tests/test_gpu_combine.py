@@ -83,6 +83,40 @@ def test_gpu_combine_world1_vs_oracle(value_type, keys, n, batch, expected):
     op.close()
 
 
+@pytest.mark.parametrize("value_type", ["i64", "f64"])
+def test_gpu_combine_panes_world1_vs_oracle(value_type):
+    # sliding windows kept as panes (size % slide == 0, no lateness): the combiner's partials are (key, pane)
+    # accumulators, a pane's partial is late exactly when its elements are (they share the pane's newest window),
+    # and the receiver merges them into its panes; rows vs the oracle fed the records (60 s / 1 s shape scaled down)
+    import torch
+    from flink_amd import SlidingEventTimeWindows
+    from flink_amd.operator import GpuWindowOperator
+    batches = _stream(400_000, 40_000, 2000, bound=300, jitter=9000, rate=100_000, value_type=value_type)
+    agg = CountSumMinMax(_VT[value_type])
+    comb = GpuWindowOperator(SlidingEventTimeWindows.of(6000, 1000), agg, device=0)
+    op = GpuWindowOperator(SlidingEventTimeWindows.of(6000, 1000), agg, device=0)
+    ref = orc.WindowOperatorOracle(assigner="sliding", size=6000, slide=1000, value_type=value_type)
+    rows, sent, n = [], 0, 0
+    for k, t, v, wm in batches:
+        cols = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (k, t, v)]
+        comb.process_batch(*cols)
+        parts, _ = comb.combine_extract(1)
+        sent += parts[0].numel()
+        n += len(k)
+        op.push_partials(*(c.clone() for c in parts), config=parts.config)
+        ref.process(k, t, v)
+        rows.append(op.process_watermark(wm))
+        ref.watermark(wm)
+    rows.append(op.process_watermark((1 << 63) - 1))
+    ref.watermark((1 << 63) - 1)
+    assert_rows_equal(np.concatenate(rows), ref.rows(), _VT[value_type])
+    assert op.late_dropped == ref.late_dropped > 0
+    assert op.stats()["records_in"] == n
+    assert sent < n // 2  # (a batch spans the 9 s of jitter: about ten panes per key)
+    comb.close()
+    op.close()
+
+
 def test_gpu_combine_rejects_foreign_key_groups_and_ineligible_configs():
     import torch
     from flink_amd import _native as N
@@ -95,7 +129,7 @@ def test_gpu_combine_rejects_foreign_key_groups_and_ineligible_configs():
     op.push_partials(*(c.clone() for c in parts), config=parts.config)
     with pytest.raises(N.NativeError):  # keys of key groups 64..127 reach a subtask owning 0..63
         op.process_watermark(0)
-    bad = GpuWindowOperator(SlidingEventTimeWindows.of(3000, 1000), device=0)
+    bad = GpuWindowOperator(SlidingEventTimeWindows.of(2500, 1000), device=0)  # (no panes: size % slide != 0)
     with pytest.raises(N.NativeError):
         bad.combine_extract(1)
     for o in (comb, op, bad):
@@ -116,7 +150,12 @@ def _slice(rank, step):
     return generate_host(0x5EED, first, BATCH, KEYS, ts_base=0, rate=100_000, jitter=300)
 
 
-def _worker(rank, port, out_dir):
+def _assigner(kind):
+    from flink_amd import SlidingEventTimeWindows
+    return TumblingEventTimeWindows.of(1000) if kind == "tumbling" else SlidingEventTimeWindows.of(5000, 1000)
+
+
+def _worker(rank, port, out_dir, kind="tumbling"):
     import torch
     import torch.distributed as dist
     from flink_amd.exchange import CombiningExchange, KeyGroupExchange
@@ -124,9 +163,8 @@ def _worker(rank, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     ex = KeyGroupExchange(MAX_PAR, WORLD, rank)
-    op = GpuWindowOperator(TumblingEventTimeWindows.of(1000), max_parallelism=MAX_PAR,
-                           key_group_range=ex.key_group_range, device=0)
-    comb = GpuWindowOperator(TumblingEventTimeWindows.of(1000), max_parallelism=MAX_PAR, device=0)
+    op = GpuWindowOperator(_assigner(kind), max_parallelism=MAX_PAR, key_group_range=ex.key_group_range, device=0)
+    comb = GpuWindowOperator(_assigner(kind), max_parallelism=MAX_PAR, device=0)
     cx = CombiningExchange(ex, comb)
     mx = -(1 << 63)
     dev = torch.device("cuda", 0)
@@ -144,15 +182,17 @@ def _worker(rank, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_gpu_combining_exchange_world2():
+@pytest.mark.parametrize("kind", ["tumbling", "panes"])
+def test_gpu_combining_exchange_world2(kind):
     import tempfile
 
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(_free_port(), d), nprocs=WORLD, join=True)
+        mp.spawn(_worker, args=(_free_port(), d, kind), nprocs=WORLD, join=True)
         rows = np.concatenate([np.load(os.path.join(d, f"rows_{r}.npy")) for r in range(WORLD)])
         sent = [np.load(os.path.join(d, f"sent_{r}.npy")) for r in range(WORLD)]
-    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000)
+    ref = (orc.WindowOperatorOracle(assigner="tumbling", size=1000) if kind == "tumbling"
+           else orc.WindowOperatorOracle(assigner="sliding", size=5000, slide=1000))
     mx = [-(1 << 63)] * WORLD
     for s in range(STEPS):
         sl = [_slice(r, s) for r in range(WORLD)]

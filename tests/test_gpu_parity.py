@@ -803,6 +803,33 @@ def test_gpu_hll_sliding_vs_oracle(p, zipf):
     gpu.close()
 
 
+@pytest.mark.parametrize("cfg", [dict(assigner="tumbling", size=1000, lateness=700),
+                                 dict(assigner="tumbling", size=1000, lateness=700, purging=True),
+                                 dict(assigner="sliding", size=2000, slide=500, lateness=300)],
+                         ids=["tumbling-lateness", "tumbling-lateness-purging", "sliding-lateness"])
+def test_gpu_hll_allowed_lateness_vs_oracle(cfg):
+    # HyperLogLog under allowed lateness (WindowOperator.java:379-420, 452-463): a window fires at its maxTimestamp
+    # and keeps its registers until its cleanup time; late elements raise them and fire the window again (the
+    # ordered replay path estimates from the block it keeps); PurgingTrigger frees the block at every firing
+    from flink_amd import HyperLogLog, PurgingTrigger
+    from flink_amd.operator import GpuWindowOperator
+    batches, wms = _stream(120_000, 10_000, 2000, bound=400, jitter=1500, rate=100_000, zipf=1.1)
+    assigner = (TumblingEventTimeWindows.of(cfg["size"]) if cfg["assigner"] == "tumbling"
+                else SlidingEventTimeWindows.of(cfg["size"], cfg["slide"]))
+    trig = PurgingTrigger.of(EventTimeTrigger.create()) if cfg.get("purging") else None
+    gpu = GpuWindowOperator(assigner, HyperLogLog(8), trigger=trig, allowed_lateness=cfg["lateness"],
+                            expected_entries=20_000)
+    ref = orc.WindowOperatorOracle(**cfg, hll_p=8)
+    for (k, t, v), wm in zip(batches, wms):
+        gpu.process(k, t, v)
+        ref.process(k, t, v)
+        gpu.watermark(wm)
+        ref.watermark(wm)
+    assert gpu.late_dropped == ref.late_dropped
+    _hll_rows_equal(gpu.rows(), ref.rows())
+    gpu.close()
+
+
 def test_gpu_hll_register_blocks_are_recycled():
     # many windows over few keys with a pool sized for one window's entries: every fired block must be
     # zeroed and reused, or the pool runs out (FW_ERR_CAPACITY) or stale registers inflate the estimates
@@ -826,9 +853,6 @@ def test_gpu_hll_refuses_unsupported_shapes():
     from flink_amd.operator import GpuWindowOperator
     with pytest.raises(N.NativeError) as e:
         GpuWindowOperator(EventTimeSessionWindows.with_gap(3000), HyperLogLog(12))
-    assert e.value.code == N.FW_ERR_UNSUPPORTED
-    with pytest.raises(N.NativeError) as e:
-        GpuWindowOperator(TumblingEventTimeWindows.of(1000), HyperLogLog(12), allowed_lateness=10)
     assert e.value.code == N.FW_ERR_UNSUPPORTED
     with pytest.raises(N.NativeError):
         GpuWindowOperator(TumblingEventTimeWindows.of(1000), HyperLogLog(20))
