@@ -63,8 +63,11 @@ extern "C" {
 #define FW_AGG_HLL 1               /* HyperLogLog distinct count of the value column read as a u64 item
                                       (definition in DESIGN.md §HLL): fired rows carry
                                       count, sum = estimate (f64 bits), min = zero registers, max = the
-                                      low 64 bits of sum_j 2^(65-p-M[j]).  Tumbling windows, no allowed
-                                      lateness; expected_entries sizes the register pool (2^p B/entry). */
+                                      low 64 bits of sum_j 2^(65-p-M[j]).  Tumbling and sliding windows
+                                      (one register block per window), any allowed lateness (a window fires
+                                      at maxTimestamp and keeps its registers until its cleanup time); not
+                                      session windows (FW_ERR_UNSUPPORTED); expected_entries sizes the
+                                      register pool (2^p B/entry). */
 #define FW_AGG_FIRST 2             /* the reduce aggregations sum(pos) / min(pos) of DataStream / WindowedStream
                                       (SumAggregator.java:66-76, ComparableAggregator.java:72-94 over
                                       HeapReducingState.add, HeapReducingState.java:72-84): the result is a
@@ -250,7 +253,8 @@ void* fw_input_stream(fw_op* op);
 
 /* Pre-shuffle combining for the keyBy exchange: partial accumulators instead of records cross the
  * network when the aggregate is decomposable (AggregateFunction.merge, flink-core/.../AggregateFunction.java:160).
- * Eligible: tumbling windows, FW_AGG_COUNT_SUM_MIN_MAX, allowed lateness 0, no side output, Long or Integer keys.
+ * Eligible: tumbling windows or sliding windows kept as panes (size a multiple of slide; a partial is then one
+ * (key, pane) accumulator), FW_AGG_COUNT_SUM_MIN_MAX, allowed lateness 0, no side output, Long or Integer keys.
  * A combiner is an ordinary handle over the subtask's whole input (any KeyGroupRange covering it; its watermark is
  * never advanced) into which the subtask pushes its batch; fw_combine_extract_device then drains the combiner's
  * state into the partials (device columns, the accumulators in the handle's own representation: only
@@ -262,8 +266,8 @@ void* fw_input_stream(fw_op* op);
  * (WindowOperator.java:402-418; with allowed lateness 0 every record of a late window is late). */
 typedef struct {
   int64_t *key, *start, *cnt, *sum, *min, *max;
-  /* the producing combiner's configuration tag (written by fw_combine_extract_device): assigner, size, offset,
-     value type, key kind, max parallelism and aggregate.  fw_push_partials_device refuses partials whose tag is
+  /* the producing combiner's configuration tag (written by fw_combine_extract_device): assigner, size, slide,
+     offset, value type, key kind, max parallelism and aggregate.  fw_push_partials_device refuses partials whose tag is
      not its own (FW_ERR_ARG): the accumulators are in the handle's internal representation (f64 min/max in
      sortable form, window starts of its own size and offset), so a differently configured receiver would
      misread them. */
