@@ -131,8 +131,10 @@ def impl_bytes(name, n, merged, fired=0, hll_p=0, panes_per_window=0, compact=Tr
         return 24 * n + rec * n
     if name == "k_aggregate":
         return rec * n + 128 * merged
-    if name == "k_tdigest":  # keys (read the record, write 12 B), one radix sort (8 passes of 12 B r+w), the tie
-        return rec * n + 12 * n + 8 * 24 * n + 12 * n + 24 * n + 24 * n  # check (12 B), decode (12 + 12), tiers (24)
+    if name == "k_tdigest":  # count (read the record, write slot + rank), place (read them and the record, write the
+        # value), the tiers' read of the run; a large run's value also: bin count (12 r + 8 w), scatter (24 r + 8 w),
+        # bin sort (8 r + 8 w), placement and group sums (3 x 8 r) -- counted here as if every value were in one
+        return rec * n + 8 * n + (8 + rec + 8) * n + 8 * n + 84 * n
     return None
 
 
