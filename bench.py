@@ -22,8 +22,9 @@ Other SURVEY §8d configs (--workload):
   c5   HyperLogLog (p = 14) per key and 1 s tumbling window, 1M Zipf(1.1) keys
   c5t  t-digest (delta = 100) quantiles per key and 1 s tumbling window, 1M Zipf(1.1) keys
 
-Roofline: `roofline` prices the dominant kernel at the path's algorithmic bytes B_alg per
-record x the records one launch processes, over that kernel's average HIP-event duration (the kernel
+Roofline: `roofline` prices the dominant kernel at its own share of the algorithmic bytes
+(`kernel_share`: the partitioning, the aggregate, the t-digest compression and the firing each charged what they
+must move of B_alg) x the records one launch processes, over that kernel's average HIP-event duration (the kernel
 launches once per step); `impl_bytes` is what the kernel itself must move as built, `traffic` the PMC-measured
 HBM bytes per launch (profiles/traffic_*.json).  `path_roofline` is B_alg x records/s over the whole step.
 A `host_fed` leg (rank 0, N = 1) pushes further batches from pinned host memory through fw_push_batch and
@@ -131,10 +132,8 @@ def impl_bytes(name, n, merged, fired=0, hll_p=0, panes_per_window=0, compact=Tr
         return 24 * n + rec * n
     if name == "k_aggregate":
         return rec * n + 128 * merged
-    if name == "k_tdigest":  # count (read the record, write slot + rank), place (read them and the record, write the
-        # value), the tiers' read of the run; a large run's value also: bin count (12 r + 8 w), scatter (24 r + 8 w),
-        # bin sort (8 r + 8 w), placement and group sums (3 x 8 r) -- counted here as if every value were in one
-        return rec * n + 8 * n + (8 + rec + 8) * n + 8 * n + 84 * n
+    if name == "k_tdigest":  # keys (read the record, write 12 B), one radix sort (8 passes of 12 B r+w), the tie
+        return rec * n + 12 * n + 8 * 24 * n + 12 * n + 24 * n + 24 * n  # check (12 B), decode (12 + 12), tiers (24)
     return None
 
 
@@ -212,7 +211,7 @@ def main():
         args.zipf = preset["zipf"]
     args.zipf = args.zipf or None
     if args.traffic is None:
-        for cand in (f"traffic_r03_{w}.json", f"traffic_r02_{w}.json",
+        for cand in (f"traffic_r04_{w}.json", f"traffic_r03_{w}.json", f"traffic_r02_{w}.json",
                      f"traffic_r01_{w}.json" if w != "c2" else "traffic_r01.json"):
             args.traffic = os.path.join(ROOT, "profiles", cand)
             if os.path.exists(args.traffic):

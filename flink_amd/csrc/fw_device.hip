@@ -2956,9 +2956,6 @@ __device__ void hll_clear(const DevCfg& c, uint64_t blk) {
 // One workgroup per FW_HLL_CHUNK records; a record's partition is found from the scan offsets.  Byte
 // registers are raised with a CAS on their 32-bit word, only when the rank is larger (max is idempotent,
 // so a resumed push may run this again over the whole batch).
-#ifndef FW_HLL_HU
-#define FW_HLL_HU 4
-#endif
 #ifndef FW_HLL_CHUNK_N
 #define FW_HLL_CHUNK_N 4096
 #endif
@@ -2990,7 +2987,7 @@ __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __rest
   // HU records per thread in flight: the record, its home slot's state word and entry identity, the entry's
   // block id and the register word are each loaded for all of them before any is used (the common case at a
   // region's load is a home-slot hit; a miss walks the rest of its probe chain on its own)
-  constexpr int HU = FW_HLL_HU;
+  constexpr int HU = 4;
   int32_t pp = p0_s;
   // sliding windows (fan-out): a record raises the same register in each of its nwin windows, newest first
   // (SlidingEventTimeWindows.java:67-81); the windows are walked one per pass of this loop
@@ -3097,16 +3094,15 @@ __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __rest
 // ---- t-digest (FW_AGG_TDIGEST).  The definition is oracle/window_oracle.h's OR_AGG_TDIGEST, restated here
 // operation for operation in IEEE double without contraction (the library is built with -ffp-contract=off),
 // so a digest is bit-exact with the oracle's.  Per push, after the aggregate created the entries and their
-// blocks: the batch's values are grouped into one run per digest (k_td_count, k_td_place: two passes over the
-// partitioned records), and each digest orders its run in Double.compare order and merges it with its
-// centroids into the other half of its block, in one of three tiers by size:
-//   serial  (<= FW_TD_T1 values + centroids, at most TD_SMALL_RUN values): one thread sorts its run in LDS and
-//           walks the merged sequence;
-//   wave    (<= FW_TD_T3): one wave sorts the run in LDS, each lane places 64 values at a time (its bucket
-//           from its merged position: binary searches over the old centroids in LDS), then per bucket the wave
-//           sums the bucket's values 64 at a time as butterfly trees and folds the old centroids' sums;
-//   large   (> FW_TD_T3, the hottest keys): the run is sample-sorted over the grid, the placement runs over
-//           the whole grid and one wave per (digest, bucket) forms the bucket's centroid.
+// blocks: every record's (entry slot, value) pair is sorted (rocPRIM radix sort by value, then stably by
+// slot), so the batch values of one digest form one run in Double.compare order.  Each digest then merges
+// its run with its centroids into the other half of its block, in one of three tiers by size:
+//   serial  (<= FW_TD_T1 values + centroids): one thread walks the merged sequence;
+//   wave    (<= FW_TD_T3): one wave — each lane places 64 values at a time (its bucket from its merged
+//           position: binary searches over the old centroids in LDS), then per bucket the wave sums the
+//           bucket's values 64 at a time as butterfly trees and folds the old centroids' sums;
+//   large   (> FW_TD_T3, the hottest keys): the placement runs over the whole grid and one wave per
+//           (digest, bucket) forms the bucket's centroid.
 // All three produce the definition's sums: per bucket, the old centroids' sums left to right, the new values
 // in blocks of 64 from the bucket's first value, each block a perfect binary tree over 64 slots, the block
 // sums left to right.
@@ -3215,10 +3211,10 @@ __device__ double td_wave_new_sum(const uint64_t* __restrict__ v, int64_t ns, in
   return s;
 }
 
-// serial merge of nn sorted values v(0 ..) with the no centroids `old` into `out` (window_oracle.cpp td_compress)
-template <class VA>
-__device__ int32_t td_merge_serial(const DevCfg& c, const double* qb, VA v, int64_t nn, const TdCent* __restrict__ old,
-                                   int32_t no, TdCent* __restrict__ out, int64_t W) {
+// serial merge of nn sorted values v[beg ..] with the no centroids `old` into `out` (window_oracle.cpp td_compress)
+__device__ int32_t td_merge_serial(const DevCfg& c, const double* qb, const uint64_t* __restrict__ v, int64_t beg,
+                                   int64_t nn, const TdCent* __restrict__ old, int32_t no, TdCent* __restrict__ out,
+                                   int64_t W) {
   const double Wd = (double)W;
   int64_t i = 0, cw = 0, gw = 0, cum_out = 0, prev_old = 0;
   int32_t j = 0, k = 0;
@@ -3237,11 +3233,11 @@ __device__ int32_t td_merge_serial(const DevCfg& c, const double* qb, VA v, int6
     tr.cnt = 0;
   };
   while (i < nn || j < no) {
-    const bool take_new = j == no || (i < nn && v(i) <= mk);
+    const bool take_new = j == no || (i < nn && v[beg + i] <= mk);
     double x;
     int64_t w;
     if (take_new) {
-      x = td_val(v(i));
+      x = td_val(v[beg + i]);
       w = 1;
       i++;
     } else {
@@ -3315,108 +3311,21 @@ __device__ int32_t td_finish(const DevCfg& c, const DevRows& out, uint64_t row, 
   return h.n;
 }
 
-// ---- the batch grouped by digest.  k_td_count finds every partitioned record's digest (the entry k_aggregate
-// stored its window in) and its rank in the digest's run, one atomic per digest and wave; the record of rank 0
-// reserves the run (its length, the digest's batch values, is the entry's count less the digest's weight) and
-// lists the digest: serial- and wave-tier runs from the bottom of v[0], large runs from the top.  k_td_place
-// writes every value key to its place.  Each tier then orders its runs itself: the serial tier per thread in LDS
-// (k_td_small), the wave tier per wave in LDS (k_td_wave), the large runs by a sample sort over the grid
-// (k_td_sample .. k_td_bin_sort).  Values that compare equal have equal bits, so any order of them is the order.
+// sort keys of every batch position: one 64-bit key (pool block of the record's digest in the top B bits, the
+// value key's high 64 - B bits below) and the value key's low B bits as the payload, so one radix sort groups a
+// digest's values and orders them up to ties in the high bits (k_td_fix orders those by the low bits). Positions
+// past the partitioned records get the block `nblk` (sorted last, skipped). binv[blk] = the digest's global slot.
 constexpr int TD_CHUNK = 4096;
-constexpr uint32_t TD_LARGE_BIT = 0x80000000u;  // TdBuf::tbase: the run is a large digest's
-constexpr uint32_t TD_EQ_BIT = 0x80000000u;     // TdBuf::bcnt: the bin holds values equal to a splitter
-
-// bitonic network with the flip step (every exchange puts the smaller key at the lower index), so n keys sort
-// as if padded with +inf to the next power of two: exchanges whose upper index is >= n are skipped.  THREADS
-// threads from `tid` step through the exchanges; `sync` orders the steps (a wave barrier or __syncthreads).
-template <int THREADS, class SYNC>
-__device__ __forceinline__ void td_bitonic(uint64_t* a, int32_t n, int tid, SYNC sync) {
-  int32_t N = 1;
-  while (N < n) N <<= 1;
-  for (int32_t k = 2; k <= N; k <<= 1) {
-    for (int32_t j = k >> 1; j >= 1; j >>= 1) {
-      for (int32_t q = tid; q < (N >> 1); q += THREADS) {
-        const int32_t lo = ((q & ~(j - 1)) << 1) | (q & (j - 1));
-        const int32_t hi = j == (k >> 1) ? (lo ^ (k - 1)) : (lo | j);
-        if (hi >= n) continue;
-        const uint64_t x = a[lo], y = a[hi];
-        if (y < x) {
-          a[lo] = y;
-          a[hi] = x;
-        }
-      }
-      sync();
-    }
-  }
-}
-__device__ __forceinline__ void td_wave_sync() {
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-}
-
-// the first record of a digest in the batch: reserve the digest's run and list it (a large digest also gets its
-// bucket-parallel state)
-__device__ void td_claim(const DevCfg& c, const Region& r, int32_t slot, uint32_t g, int64_t total, const TdBuf& td,
-                         Status* st) {
-  const Entry& e = r.ent[slot];
-  const uint64_t blk = pool_block_of(e);
-  TdHead* hp = td_head(c, blk);
-  const TdHead h = *hp;
-  const int64_t W = e.cnt, nn = W - h.w;
-  uint32_t base;
-  if (nn + h.n <= FW_TD_T3) {
-    base = (uint32_t)atomicAdd(&td.ctr[3], (int32_t)nn);
-  } else {
-    base = (uint32_t)(total - (int64_t)atomicAdd(&td.ctr[4], (int32_t)nn) - nn);
-    const int32_t L = atomicAdd(&td.ctr[1], 1);
-    if (L >= td.max_large) {  // cannot happen: max_large bounds the digests with > FW_TD_T3 - td_nb values
-      atomicOr(&st->flags, FW_STATUS_STATE_LOST);
-      td.lidx[g] = -1;
-    } else {
-      td.lidx[g] = L;
-      td.large[L] = TdLarge{(int64_t)base, nn, W, h.n, h.cur ^ 1, td_half(c, blk, h.cur), td_half(c, blk, h.cur ^ 1), hp};
-      for (int b = 0; b < c.td_nb; b++) {
-        td.nstart[(int64_t)L * c.td_nb + b] = -1;
-        td.ostart[(int64_t)L * c.td_nb + b] = -1;
-      }
-    }
-    base |= TD_LARGE_BIT;
-  }
-  td.tbase[g] = base;
-  const int32_t k = atomicAdd(&td.ctr[0], 1);
-  td.tslot[k] = g;
-  td.tbeg[k] = base & ~TD_LARGE_BIT;
-}
-
-// rank of this lane's item among the items of one counter: one atomic for the lanes that share the wave's first
-// active counter, one per lane for the rest (a hot digest or bin fills whole waves)
-__device__ __forceinline__ uint32_t td_rank(uint32_t* ctr, uint32_t id, bool ok) {
-  const uint64_t act = __ballot(ok);
-  uint32_t pos = 0;
-  bool done = false;
-  if (act) {
-    const int leader = __ffsll((long long)act) - 1;
-    const uint32_t lid = __shfl(id, leader, 64);
-    const uint64_t same = __ballot(ok && id == lid);
-    uint32_t b = 0;
-    if ((int)__lane_id() == leader) b = atomicAdd(&ctr[lid], (uint32_t)__popcll(same));
-    b = __shfl(b, leader, 64);
-    if (ok && id == lid) {
-      pos = b + (uint32_t)__popcll(same & lanemask_lt());
-      done = true;
-    }
-  }
-  if (ok && !done) pos = atomicAdd(&ctr[id], 1u);
-  return pos;
-}
-
-// every partitioned record: its digest's global slot (gs[0]) and its rank in the digest's run (gs[1])
-__global__ __launch_bounds__(256) void k_td_count(DevCfg c, const PRec* __restrict__ part, const uint32_t* __restrict__ offs,
-                                                  int32_t T, DevTable tb, TdBuf td, uint32_t none, Status* st) {
+__global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restrict__ part, const uint32_t* __restrict__ offs,
+                                                 int32_t T, int64_t n, DevTable tb, uint32_t nblk, int B,
+                                                 uint32_t* __restrict__ pay, uint64_t* __restrict__ key64,
+                                                 uint32_t* __restrict__ binv, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int64_t total = offs[(int64_t)c.P * T];
   const int64_t i0 = (int64_t)blockIdx.x * TD_CHUNK;
-  if (i0 >= total) return;
+  const int64_t i1 = min(n, i0 + (int64_t)TD_CHUNK);
+  const uint64_t none_key = (uint64_t)nblk << (64 - B);
+  const uint64_t low = (B >= 64) ? ~0ull : ((1ull << B) - 1ull);
   __shared__ int32_t p0_s;
   if (threadIdx.x == 0) {  // partition of the chunk's first record: last p with offs[p*T] <= i0
     int32_t lo = 0, hi = c.P - 1;
@@ -3431,119 +3340,143 @@ __global__ __launch_bounds__(256) void k_td_count(DevCfg c, const PRec* __restri
   }
   __syncthreads();
   const bool cmp = c.compact && !*c.wide;
-  const int64_t i1 = min(total, i0 + (int64_t)TD_CHUNK);
   int32_t pp = p0_s;
-  // TU records per thread in flight: the record, its home slot's state word and entry identity are loaded for
-  // all of them before any is used (the common case is a home-slot hit; a miss walks its probe chain alone).
-  // The table is read-only here: plain, L1-cacheable reads.
-  constexpr int TU = 4;
-  for (int64_t ib = i0; ib < i1; ib += (int64_t)blockDim.x * TU) {  // (uniform over the block: the ballots below)
-    int64_t key[TU], last[TU];
-    int32_t pr[TU];
-    bool ok[TU];
-#pragma unroll
-    for (int u = 0; u < TU; u++) {
-      const int64_t i = ib + (int64_t)u * blockDim.x + threadIdx.x;
-      ok[u] = i < i1;
-      key[u] = last[u] = 0;
-      pr[u] = pp;
-      if (!ok[u]) continue;
-      while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
-      pr[u] = pp;
-      if (cmp) {
-        const i64x2 x = reinterpret_cast<const i64x2*>(part)[i];
-        compact_decode(c, pp, x.x, &key[u], &last[u]);
-      } else {
-        const PRec rec = part[i];
-        key[u] = rec.key;
-        last[u] = rec.last;
-      }
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    if (i >= total) {
+      key64[i] = none_key;
+      pay[i] = 0;
+      continue;
     }
-    Region rg[TU];
-    uint64_t hs[TU];
-    uint32_t hw[TU];
-    i64x2 hk[TU];
-    int64_t hend[TU];
-#pragma unroll
-    for (int u = 0; u < TU; u++) {
-      rg[u] = region_of(c, tb, pr[u], tb.cur[pr[u]]);
-      hs[u] = slot_hash(c, key[u], last[u]);
-      hw[u] = SLOT_EMPTY;
-      if (!ok[u]) continue;
-      const uint32_t home = (uint32_t)hs[u] & rg[u].mask;
-      hw[u] = rg[u].state[home];
-      hk[u] = *reinterpret_cast<const i64x2*>(&rg[u].ent[home].key);
-      hend[u] = rg[u].ent[home].end;
+    while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
+    PRec rec;
+    if (cmp) {
+      const i64x2 r = reinterpret_cast<const i64x2*>(part)[i];
+      compact_decode(c, pp, r.x, &rec.key, &rec.last);
+      rec.val = r.y;
+    } else {
+      rec = part[i];
     }
-#pragma unroll
-    for (int u = 0; u < TU; u++) {
-      const int64_t i = ib + (int64_t)u * blockDim.x + threadIdx.x;
-      uint32_t g = none;
-      int32_t slot = -1;
-      if (ok[u]) {
-        const int64_t we = wend(c, last[u]);
-        if (hw[u] == live_word(hs[u]) && hk[u].x == key[u] && hk[u].y == last[u] && hend[u] == we)
-          slot = (int32_t)((uint32_t)hs[u] & rg[u].mask);
-        else if (hw[u] != SLOT_EMPTY)
-          slot = region_find(rg[u], hs[u] + 1, key[u], last[u], we, live_word(hs[u]));
-        if (slot < 0) {
-          atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's window
-          ok[u] = false;
-        } else {
-          g = ((uint32_t)pr[u] << c.log_r) | (uint32_t)slot;
-        }
-      }
-      const uint32_t pos = td_rank(td.tcnt, g, ok[u]);
-      if (ok[u] && pos == 0) td_claim(c, rg[u], slot, g, total, td, st);
-      if (i < i1) {
-        td.gs[0][i] = g;
-        td.gs[1][i] = pos;
-      }
+    const Region r = region_of(c, tb, pp, tb.cur[pp]);
+    const int32_t slot = region_find(r, slot_hash(c, rec.key, rec.last), rec.key, rec.last, wend(c, rec.last));
+    if (slot < 0) {
+      atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's window
+      key64[i] = none_key;
+      pay[i] = 0;
+      continue;
+    }
+    const uint32_t g = ((uint32_t)pp << c.log_r) | (uint32_t)slot;
+    const uint64_t blk = pool_block_of(r.ent[slot]);
+    // every record of a digest stores the same slot, so a stale (cached) read costs one redundant store at most;
+    // a hot digest's records read it (an L1 hit) and store nothing
+    if (binv[blk] != g) binv[blk] = g;
+    const uint64_t k = td_key(rec.val);
+    key64[i] = (blk << (64 - B)) | (k >> B);
+    pay[i] = (uint32_t)(k & low);
+  }
+}
+
+// tie runs: positions with the previous one's key (one digest, equal high value bits) and a smaller payload mark
+// their run's first position in fixbm; k_td_fix_runs then orders each marked run by payload
+__global__ __launch_bounds__(256) void k_td_fix_mark(int64_t n, const uint64_t* __restrict__ key64,
+                                                     const uint32_t* __restrict__ pay, uint32_t* __restrict__ fixbm) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = key64[i];
+    if (k != key64[i - 1] || pay[i] >= pay[i - 1]) continue;
+    int64_t s = i - 1;
+    while (s > 0 && key64[s - 1] == k) s--;
+    atomicOr(&fixbm[s >> 5], 1u << (s & 31));
+  }
+}
+__device__ void td_sift(uint32_t* a, int64_t root, int64_t len) {
+  while (2 * root + 1 < len) {
+    int64_t ch = 2 * root + 1;
+    if (ch + 1 < len && a[ch + 1] > a[ch]) ch++;
+    if (a[root] >= a[ch]) return;
+    const uint32_t t = a[root];
+    a[root] = a[ch];
+    a[ch] = t;
+    root = ch;
+  }
+}
+__global__ __launch_bounds__(256) void k_td_fix_runs(int64_t n, const uint64_t* __restrict__ key64,
+                                                     uint32_t* __restrict__ pay, const uint32_t* __restrict__ fixbm) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
+    if (!((fixbm[s >> 5] >> (s & 31)) & 1u)) continue;
+    const uint64_t k = key64[s];
+    int64_t e = s + 1;
+    while (e < n && key64[e] == k) e++;
+    uint32_t* a = pay + s;
+    const int64_t len = e - s;
+    for (int64_t r = len / 2 - 1; r >= 0; r--) td_sift(a, r, len);  // heapsort: bounded for any run
+    for (int64_t m = len - 1; m > 0; m--) {
+      const uint32_t t = a[0];
+      a[0] = a[m];
+      a[m] = t;
+      td_sift(a, 0, m);
+    }
+  }
+}
+// the sorted keys back to (global slot, value key) columns for the tiers
+__global__ __launch_bounds__(256) void k_td_decode(int64_t n, int B, uint32_t nblk, uint32_t none,
+                                                   const uint64_t* __restrict__ key64, const uint32_t* __restrict__ pay,
+                                                   const uint32_t* __restrict__ binv, uint32_t* __restrict__ gs,
+                                                   uint64_t* __restrict__ v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = key64[i];
+    const uint32_t blk = (uint32_t)(k >> (64 - B));
+    if (blk == nblk) {
+      gs[i] = none;
+      v[i] = 0;
+    } else {
+      gs[i] = binv[blk];
+      v[i] = (k << B) | (uint64_t)pay[i];
     }
   }
 }
 
-// every value key to its place in its digest's run (and, in a large run, the digest's large index beside it)
-__global__ __launch_bounds__(256) void k_td_place(DevCfg c, const PRec* __restrict__ part, const uint32_t* __restrict__ offs,
-                                                  int32_t T, TdBuf td, uint32_t none, Status* st) {
+// the touched digests: the first position of every run of one slot in the sorted batch.  A workgroup takes
+// TD_BOUNDS consecutive positions and reserves its digests' places with one atomic.
+constexpr int TD_BOUNDS_PER_THREAD = 16;
+__global__ __launch_bounds__(256) void k_td_bounds(int64_t n, const uint32_t* __restrict__ gs, uint32_t none, TdBuf td,
+                                                   Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  const int64_t total = offs[(int64_t)c.P * T];
-  const bool cmp = c.compact && !*c.wide;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t g = td.gs[0][i];
-    if (g == none) continue;
-    const uint32_t tbg = td.tbase[g];
-    const int64_t at = (int64_t)(tbg & ~TD_LARGE_BIT) + td.gs[1][i];
-    const int64_t val = cmp ? reinterpret_cast<const i64x2*>(part)[i].y : part[i].val;
-    td.v[0][at] = td_key(val);
-    if (tbg & TD_LARGE_BIT) td.lpos[at] = (uint32_t)td.lidx[g];
+  __shared__ uint32_t sw[256 / 64 + 1];
+  __shared__ int base_s;
+  const int64_t i0 = (int64_t)blockIdx.x * 256 * TD_BOUNDS_PER_THREAD + (int64_t)threadIdx.x * TD_BOUNDS_PER_THREAD;
+  uint32_t starts = 0;  // bit u: position i0 + u starts a run
+  uint32_t prev = i0 > 0 && i0 <= n ? gs[i0 - 1] : none;
+#pragma unroll
+  for (int u = 0; u < TD_BOUNDS_PER_THREAD; u++) {
+    const int64_t i = i0 + u;
+    const uint32_t g = i < n ? gs[i] : none;
+    if (g != none && (i == 0 || g != prev)) starts |= 1u << u;
+    prev = g;
+  }
+  uint32_t total;
+  const uint32_t pos = block_excl_scan((uint32_t)__popc(starts), sw, &total);
+  if (threadIdx.x == 0) base_s = total ? atomicAdd(&td.ctr[0], (int)total) : 0;
+  __syncthreads();
+  int k = base_s + (int)pos;
+#pragma unroll
+  for (int u = 0; u < TD_BOUNDS_PER_THREAD; u++) {
+    if (!((starts >> u) & 1u)) continue;
+    td.tslot[k] = gs[i0 + u];
+    td.tbeg[k] = (uint32_t)(i0 + u);
+    k++;
   }
 }
 
-// each touched digest: merged serially here (its run, at most TD_SMALL_RUN values, sorted in the thread's LDS
-// column), or queued for the wave tier (large digests were listed by k_td_count); every touched digest's
-// placement counter is reset.  (A deeper column costs occupancy: the merges are latency-bound.)
-#ifndef FW_TD_SMALL_RUN
-#define FW_TD_SMALL_RUN 16
-#endif
-constexpr int TD_SMALL_THREADS = 256, TD_SMALL_RUN = FW_TD_SMALL_RUN;
-struct TdCol {  // a thread's LDS column: element i at p[i * TD_SMALL_THREADS]
-  const uint64_t* p;
-  __device__ uint64_t operator()(int64_t i) const { return p[i * TD_SMALL_THREADS]; }
-};
-__global__ __launch_bounds__(TD_SMALL_THREADS) void k_td_small(DevCfg c, DevTable tb, TdBuf td, Status* st) {
+// each touched digest: merged serially here, or queued for the wave or the grid-wide merge
+__global__ __launch_bounds__(256) void k_td_small(DevCfg c, DevTable tb, TdBuf td, const uint64_t* __restrict__ v, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  __shared__ uint64_t s_run[TD_SMALL_RUN * TD_SMALL_THREADS];  // 32 KB
   const int32_t nt = td.ctr[0];
   const uint32_t mask = (1u << c.log_r) - 1u;
-  const uint64_t* __restrict__ v = td.v[0];
   for (int32_t idx0 = blockIdx.x * blockDim.x; idx0 < nt; idx0 += gridDim.x * blockDim.x) {
     const int32_t idx = idx0 + (int32_t)threadIdx.x;
     bool mid = false;
     if (idx < nt) {
       const uint32_t g = td.tslot[idx];
       const int64_t beg = td.tbeg[idx];
-      td.tcnt[g] = 0u;
       const int32_t p = (int32_t)(g >> c.log_r);
       const Region r = region_of(c, tb, p, tb.cur[p]);
       const Entry& e = r.ent[g & mask];
@@ -3551,23 +3484,26 @@ __global__ __launch_bounds__(TD_SMALL_THREADS) void k_td_small(DevCfg c, DevTabl
       TdHead* hp = td_head(c, blk);
       const TdHead h = *hp;
       const int64_t W = e.cnt, nn = W - h.w;
-      if (nn + h.n <= FW_TD_T1 && nn <= TD_SMALL_RUN) {
-        // insertion sort into the thread's column as the values are read
-        uint64_t* col = s_run + threadIdx.x;
-        for (int32_t i = 0; i < (int32_t)nn; i++) {
-          const uint64_t x = v[beg + i];
-          int32_t j = i - 1;
-          while (j >= 0 && col[j * TD_SMALL_THREADS] > x) {
-            col[(j + 1) * TD_SMALL_THREADS] = col[j * TD_SMALL_THREADS];
-            j--;
-          }
-          col[(j + 1) * TD_SMALL_THREADS] = x;
-        }
-        const int32_t k = td_merge_serial(c, c.td_qb, TdCol{col}, nn, td_half(c, blk, h.cur), h.n,
-                                          td_half(c, blk, h.cur ^ 1), W);
+      const TdCent* old = td_half(c, blk, h.cur);
+      TdCent* out = td_half(c, blk, h.cur ^ 1);
+      td.lidx[g] = -1;
+      if (nn + h.n <= FW_TD_T1) {
+        const int32_t k = td_merge_serial(c, c.td_qb, v, beg, nn, old, h.n, out, W);
         *hp = TdHead{h.cur ^ 1, k, W};
       } else if (nn + h.n <= FW_TD_T3) {
         mid = true;
+      } else {
+        const int32_t L = atomicAdd(&td.ctr[1], 1);
+        if (L >= td.max_large) {  // cannot happen: max_large bounds the digests with > FW_TD_T3 - td_nb values
+          atomicOr(&st->flags, FW_STATUS_STATE_LOST);
+        } else {
+          td.lidx[g] = L;
+          td.large[L] = TdLarge{beg, nn, W, h.n, h.cur ^ 1, old, out, hp};
+          for (int b = 0; b < c.td_nb; b++) {
+            td.nstart[(int64_t)L * c.td_nb + b] = -1;
+            td.ostart[(int64_t)L * c.td_nb + b] = -1;
+          }
+        }
       }
     }
     // wave-aggregated reservation of the wave-tier list
@@ -3579,151 +3515,6 @@ __global__ __launch_bounds__(TD_SMALL_THREADS) void k_td_small(DevCfg c, DevTabl
       base = __shfl(base, leader, 64);
       if (mid) td.mid[base + __popcll(m & lanemask_lt())] = (uint32_t)idx;
     }
-  }
-}
-
-// ---- the large runs' sample sort: a digest of m values gets nbin = ceil(m / TD_BIN) bins split by nbin - 1
-// splitters drawn from a regular sample of its run; a value goes to the bin between two splitters, or to the bin
-// of a splitter it equals (those need no ordering); each bin is ordered in LDS by one workgroup (one larger than
-// TD_BIN_CAP, which a skewed sample can leave, in place in HBM by the same network)
-constexpr int TD_BIN = FW_TD_BIN, TD_BIN_CAP = 8192, TD_SAMPLE_MAX = 8192, TD_NBIN_MAX = 8192;
-__device__ __forceinline__ int32_t td_nlarge(const TdBuf& td) { return min(td.ctr[1], td.max_large); }
-__global__ __launch_bounds__(1024) void k_td_sample(TdBuf td, Status* st) {
-  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  __shared__ uint64_t s[TD_SAMPLE_MAX];
-  __shared__ int32_t sb_s, bb_s;
-  const int32_t nl = td_nlarge(td);
-  for (int32_t L = blockIdx.x; L < nl; L += gridDim.x) {
-    const TdLarge d = td.large[L];
-    const int64_t m = d.nn;
-    const int32_t nbin = (int32_t)min<int64_t>(TD_NBIN_MAX, (m + TD_BIN - 1) / TD_BIN);
-    const int32_t ns = nbin - 1;
-    const int32_t q = min(TD_SAMPLE_MAX, 16 * nbin);
-    for (int32_t i = threadIdx.x; i < q; i += blockDim.x) s[i] = td.v[0][d.beg + (int64_t)i * m / q];
-    __syncthreads();
-    td_bitonic<1024>(s, q, (int)threadIdx.x, [] { __syncthreads(); });
-    if (threadIdx.x == 0) {
-      sb_s = atomicAdd(&td.ctr[5], ns);
-      bb_s = atomicAdd(&td.ctr[6], 2 * ns + 1);
-    }
-    __syncthreads();
-    const int32_t sb = sb_s, bb = bb_s;
-    if (sb + ns > td.max_spl || bb + 2 * ns + 1 > td.max_bins) {  // cannot happen: max_spl / max_bins bound them
-      if (threadIdx.x == 0) {
-        atomicOr(&st->flags, FW_STATUS_STATE_LOST);
-        td.samp[L] = TdSamp{0, -1, 0, 0};
-      }
-    } else {
-      for (int32_t j = threadIdx.x; j < ns; j += blockDim.x) td.spl[sb + j] = s[(int64_t)(j + 1) * q / nbin];
-      for (int32_t b = threadIdx.x; b < 2 * ns + 1; b += blockDim.x) td.bcnt[bb + b] = 0u;
-      if (threadIdx.x == 0) td.samp[L] = TdSamp{sb, ns, bb, 0};
-    }
-    __syncthreads();  // (s is the next digest's)
-  }
-}
-// first position of the large runs (they fill v[0] from the top down to it)
-__device__ __forceinline__ int64_t td_large_lo(const DevCfg& c, const uint32_t* offs, int32_t T, const TdBuf& td,
-                                               int64_t* total) {
-  *total = offs[(int64_t)c.P * T];
-  return *total - td.ctr[4];
-}
-// every value of a large run: its bin (gs[0], TdBuf::bcnt's index) and rank in the bin (gs[1])
-__global__ __launch_bounds__(256) void k_td_bin_count(DevCfg c, const uint32_t* __restrict__ offs, int32_t T, TdBuf td,
-                                                      Status* st) {
-  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || td.ctr[1] == 0) return;
-  int64_t total;
-  const int64_t lo = td_large_lo(c, offs, T, td, &total);
-  const int32_t nl = td_nlarge(td);
-  for (int64_t ib = lo + (int64_t)blockIdx.x * blockDim.x; ib < total; ib += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = ib + threadIdx.x;
-    bool ok = i < total;
-    uint32_t gb = 0xffffffffu;
-    if (ok) {
-      const uint32_t L = td.lpos[i];
-      const TdSamp S = L < (uint32_t)nl ? td.samp[L] : TdSamp{0, -1, 0, 0};
-      if (S.ns < 0) {
-        ok = false;
-      } else {
-        const uint64_t key = td.v[0][i];
-        const uint64_t* sp = td.spl + S.sbase;
-        int32_t a = 0, b = S.ns;  // first splitter >= key
-        while (a < b) {
-          const int32_t m = (a + b) >> 1;
-          if (sp[m] < key)
-            a = m + 1;
-          else
-            b = m;
-        }
-        gb = (uint32_t)(S.bbase + (a < S.ns && sp[a] == key ? 2 * a + 1 : 2 * a));
-      }
-    }
-    const uint32_t r = td_rank(td.bcnt, gb, ok);
-    if (i < total) {
-      td.gs[0][i] = ok ? gb : 0xffffffffu;
-      td.gs[1][i] = r;
-    }
-  }
-}
-// each large digest's bins laid out in order over its run (the equal bins marked)
-__global__ __launch_bounds__(256) void k_td_bin_scan(TdBuf td, Status* st) {
-  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  __shared__ uint32_t sw[256 / 64 + 1];
-  const int32_t nl = td_nlarge(td);
-  for (int32_t L = blockIdx.x; L < nl; L += gridDim.x) {
-    const TdSamp S = td.samp[L];
-    if (S.ns < 0) continue;
-    const int64_t beg = td.large[L].beg;
-    const int32_t nbins = 2 * S.ns + 1;
-    uint32_t run = 0;
-    for (int32_t b0 = 0; b0 < nbins; b0 += blockDim.x) {
-      const int32_t b = b0 + (int32_t)threadIdx.x;
-      const uint32_t cnt = b < nbins ? td.bcnt[S.bbase + b] : 0u;
-      uint32_t tot;
-      const uint32_t x = block_excl_scan(cnt, sw, &tot);
-      if (b < nbins) {
-        td.bstart[S.bbase + b] = (uint32_t)beg + run + x;
-        if (b & 1) td.bcnt[S.bbase + b] = cnt | TD_EQ_BIT;
-      }
-      run += tot;
-    }
-  }
-}
-// every large-run value to its bin in v[1]
-__global__ __launch_bounds__(256) void k_td_bin_scatter(DevCfg c, const uint32_t* __restrict__ offs, int32_t T, TdBuf td,
-                                                        Status* st) {
-  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || td.ctr[1] == 0) return;
-  int64_t total;
-  const int64_t lo = td_large_lo(c, offs, T, td, &total);
-  for (int64_t i = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t gb = td.gs[0][i];
-    if (gb == 0xffffffffu) continue;
-    td.v[1][(int64_t)td.bstart[gb] + td.gs[1][i]] = td.v[0][i];
-  }
-}
-// each bin ordered back into v[0] (a bin of equal values, or of one, copied)
-__global__ __launch_bounds__(1024) void k_td_bin_sort(TdBuf td, Status* st) {
-  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || td.ctr[1] == 0) return;
-  __shared__ uint64_t s[TD_BIN_CAP];
-  const int32_t nbins = min(td.ctr[6], td.max_bins);
-  const auto sync = [] { __syncthreads(); };
-  for (int32_t b = blockIdx.x; b < nbins; b += gridDim.x) {
-    const uint32_t cw = td.bcnt[b];
-    const int32_t cnt = (int32_t)(cw & ~TD_EQ_BIT);
-    if (cnt == 0) continue;
-    uint64_t* src = td.v[1] + td.bstart[b];
-    uint64_t* dst = td.v[0] + td.bstart[b];
-    if (!(cw & TD_EQ_BIT) && cnt > 1) {
-      if (cnt <= TD_BIN_CAP) {
-        for (int32_t i = threadIdx.x; i < cnt; i += blockDim.x) s[i] = src[i];
-        __syncthreads();
-        td_bitonic<1024>(s, cnt, (int)threadIdx.x, sync);
-        for (int32_t i = threadIdx.x; i < cnt; i += blockDim.x) dst[i] = s[i];
-        __syncthreads();
-        continue;
-      }
-      td_bitonic<1024>(src, cnt, (int)threadIdx.x, sync);  // (a bin past the LDS capacity: in place in HBM)
-    }
-    for (int32_t i = threadIdx.x; i < cnt; i += blockDim.x) dst[i] = src[i];
   }
 }
 
@@ -3763,8 +3554,8 @@ __device__ __forceinline__ int td_bucket_old(const DevCfg& c, const double* qb, 
 // blocks (a digest's nn <= FW_TD_T3 values form at most FW_TD_T3 / 64 + nb blocks)
 constexpr int TD_WAVES = 4;
 __host__ __device__ constexpr int td_wave_blocks(int nb) { return FW_TD_T3 / 64 + nb + 1; }
-__host__ __device__ constexpr size_t td_wave_lds_wave(int nb) {  // (the run first, FW_TD_T3 value keys)
-  return 8 * (size_t)FW_TD_T3 + ((8 * (size_t)(4 * nb + 1 + td_wave_blocks(nb)) + 4 * (size_t)(3 * nb + 1) + 7) & ~(size_t)7);
+__host__ __device__ constexpr size_t td_wave_lds_wave(int nb) {
+  return (8 * (size_t)(4 * nb + 1 + td_wave_blocks(nb)) + 4 * (size_t)(3 * nb + 1) + 7) & ~(size_t)7;
 }
 size_t td_wave_lds_bytes(int nb) { return TD_WAVES * td_wave_lds_wave(nb); }
 __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb, TdBuf td, const uint64_t* __restrict__ v,
@@ -3775,8 +3566,7 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
   td_stage_qb(c, s_qb);
   const int wv = threadIdx.x >> 6, lane = __lane_id();
   const int nb = c.td_nb;
-  uint64_t* run = reinterpret_cast<uint64_t*>(td_lds + (size_t)wv * td_wave_lds_wave(nb));  // [FW_TD_T3] the sorted run
-  uint8_t* base = reinterpret_cast<uint8_t*>(run + FW_TD_T3);
+  uint8_t* base = td_lds + (size_t)wv * td_wave_lds_wave(nb);
   uint64_t* keys = reinterpret_cast<uint64_t*>(base);                 // [nb]; the old sums after the placement
   double* osum = reinterpret_cast<double*>(base);
   int64_t* cum = reinterpret_cast<int64_t*>(base) + nb;               // [nb]
@@ -3801,11 +3591,6 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
       const TdHead h = *hp;
       d = TdLarge{td.tbeg[idx], e.cnt - h.w, e.cnt, h.n, h.cur ^ 1, td_half(c, blk, h.cur), td_half(c, blk, h.cur ^ 1), hp};
     }
-    // the digest's run (nn <= FW_TD_T3 values) into LDS, sorted there; positions below are the run's
-    for (int64_t i = lane; i < d.nn; i += 64) run[i] = v[d.beg + i];
-    td_wave_sync();
-    td_bitonic<64>(run, (int32_t)d.nn, lane, td_wave_sync);
-    d.beg = 0;
     const double W = (double)d.W;
     double my_osum[4];  // this lane's old sums (j = lane + 64 u), staged into LDS once the keys are no longer read
 #pragma unroll
@@ -3830,7 +3615,7 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
     for (int64_t i0 = 0; i0 < d.nn; i0 += 64) {
       const int64_t i = i0 + lane;
       int b = -1;
-      if (i < d.nn) b = td_bucket_new(c, s_qb, keys, cum, d.no, W, i, run[i]);
+      if (i < d.nn) b = td_bucket_new(c, s_qb, keys, cum, d.no, W, i, v[d.beg + i]);
       int prev = __shfl_up(b, 1, 64);
       if (lane == 0) prev = carry;
       if (i < d.nn && prev != b) ns[b] = d.beg + i;
@@ -3840,7 +3625,7 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
     for (int32_t j0 = 0; j0 < d.no; j0 += 64) {
       const int32_t j = j0 + lane;
       int b = -1;
-      if (j < d.no) b = td_bucket_old(c, s_qb, run, 0, d.nn, keys[j], j ? cum[j - 1] : 0, td_weight(d.old, j), W);
+      if (j < d.no) b = td_bucket_old(c, s_qb, v, d.beg, d.nn, keys[j], j ? cum[j - 1] : 0, td_weight(d.old, j), W);
       int prev = __shfl_up(b, 1, 64);
       if (lane == 0) prev = carry;
       if (j < d.no && prev != b) os[b] = j;
@@ -3916,7 +3701,7 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
             while (ns[bk] < 0 || k >= bst[bk] + (int32_t)((s_en[bk] - ns[bk] + 63) >> 6)) bk++;
             const int64_t start = ns[bk] + (int64_t)(k - bst[bk]) * 64;
             has[u] = start + lane < s_en[bk];
-            if (has[u]) x[u] = td_val(run[start + lane]);
+            if (has[u]) x[u] = td_val(v[start + lane]);
           }
         }
 #pragma unroll
@@ -3965,23 +3750,21 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
       cbase += __shfl(x, 63, 64);
     }
     if (lane == 0) *d.head = TdHead{d.pad, kbase, d.W};
-    td_wave_sync();  // (run and the tables are the next digest's)
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
-// the large tier: placement of every value of a large digest over the whole grid (the large runs fill v[0] from
-// the top down; lpos names each position's digest)
-__global__ __launch_bounds__(256) void k_td_large_items(DevCfg c, const uint32_t* __restrict__ offs, int32_t T,
-                                                        const uint64_t* __restrict__ v, TdBuf td, Status* st) {
+// the large tier: placement of every value of a large digest over the whole grid
+__global__ __launch_bounds__(256) void k_td_large_items(DevCfg c, int64_t n, const uint32_t* __restrict__ gs,
+                                                        const uint64_t* __restrict__ v, uint32_t none, TdBuf td, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || td.ctr[1] == 0) return;
   __shared__ double s_qb[TD_NB_MAX];
   td_stage_qb(c, s_qb);
-  int64_t total;
-  const int64_t lo = td_large_lo(c, offs, T, td, &total);
-  const int32_t nl = td_nlarge(td);
-  for (int64_t i = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t L = td.lpos[i];
-    if (L >= (uint32_t)nl) continue;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = gs[i];
+    if (g == none) continue;
+    const int32_t L = td.lidx[g];
+    if (L < 0) continue;
     const TdLarge d = td.large[L];
     const uint64_t* keys = td.okey + (int64_t)L * c.td_nb;
     const int64_t r = i - d.beg;
@@ -4017,7 +3800,7 @@ __global__ __launch_bounds__(256) void k_td_large_old(DevCfg c, const uint64_t* 
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   __shared__ double s_qb[TD_NB_MAX];
   td_stage_qb(c, s_qb);
-  const int32_t nl = td_nlarge(td);
+  const int32_t nl = td.ctr[1];
   const int lane = __lane_id();
   for (int32_t L = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); L < nl; L += (gridDim.x * blockDim.x) >> 6) {
     const TdLarge d = td.large[L];
@@ -4042,7 +3825,7 @@ __global__ __launch_bounds__(256) void k_td_large_old(DevCfg c, const uint64_t* 
 __global__ __launch_bounds__(256) void k_td_large_groups(DevCfg c, const uint64_t* __restrict__ v, TdBuf td, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int nb = c.td_nb;
-  const int64_t units = (int64_t)td_nlarge(td) * nb;
+  const int64_t units = (int64_t)td.ctr[1] * nb;
   const int lane = __lane_id();
   for (int64_t u = (int64_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); u < units; u += (gridDim.x * blockDim.x) >> 6) {
     const int32_t L = (int32_t)(u / nb);
@@ -4086,7 +3869,7 @@ __global__ __launch_bounds__(256) void k_td_large_groups(DevCfg c, const uint64_
 // compaction of a large digest's buckets into its centroids (in place, in order), then the head
 __global__ __launch_bounds__(64) void k_td_large_compact(DevCfg c, TdBuf td, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  const int32_t nl = td_nlarge(td);
+  const int32_t nl = td.ctr[1];
   for (int32_t L = blockIdx.x * blockDim.x + threadIdx.x; L < nl; L += gridDim.x * blockDim.x) {
     const TdLarge d = td.large[L];
     int32_t k = 0;
@@ -6329,29 +6112,45 @@ void launch_count(const DevCfg& c, DevCount& cw, const int64_t* key, const int64
   hipLaunchKernelGGL(k_cnt_update, dim3(grid), dim3(256), 0, s, c, cw, sk, sv, val, n, none);
   hipLaunchKernelGGL(k_cnt_count, dim3(grid), dim3(256), 0, s, cw, sk, n, none);
 }
+size_t tdigest_sort_bytes(int64_t n) {
+  size_t a = 0;
+  rocprim::double_buffer<uint64_t> kv(nullptr, nullptr);
+  rocprim::double_buffer<uint32_t> ks(nullptr, nullptr);
+  (void)rocprim::radix_sort_pairs(nullptr, a, kv, ks, (size_t)n, 0, 64);
+  return a;
+}
 void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
                     TdBuf& td, Status* st, hipStream_t s) {
   if (n <= 0) return;
-  const uint32_t none = 0xffffffffu;  // no slot has this id (t-digest tables stay below 2^31 slots)
-  (void)hipMemsetAsync(td.ctr, 0, 8 * sizeof(int32_t), s);
+  const uint32_t none = (uint32_t)td.lidx_slots;  // no slot has this id (slots are 0 .. table slots - 1)
+  const uint32_t nblk = (uint32_t)c.pool_blocks;   // no block has this id
+  int B = 1;
+  while (((int64_t)1 << B) <= c.pool_blocks) B++;
+  (void)hipMemsetAsync(td.ctr, 0, 3 * sizeof(int32_t), s);
+  (void)hipMemsetAsync(td.fixbm, 0, (size_t)((n + 31) / 32) * sizeof(uint32_t), s);
+  hipLaunchKernelGGL(k_td_keys, dim3((unsigned)((n + TD_CHUNK - 1) / TD_CHUNK)), dim3(256), 0, s, c, part, offs, T, n,
+                     tb, nblk, B, td.gs[0], td.v[0], td.binv, st);
+  // one sort by (pool block, high value bits): each digest's batch values become one run, in Double.compare
+  // order once the tie runs are ordered by their low bits
+  rocprim::double_buffer<uint64_t> kv(td.v[0], td.v[1]);
+  rocprim::double_buffer<uint32_t> ks(td.gs[0], td.gs[1]);
+  size_t bytes = td.tmp_bytes;
+  (void)rocprim::radix_sort_pairs(td.tmp, bytes, kv, ks, (size_t)n, 0, 64, s);
   const unsigned grid = (unsigned)std::min<int64_t>(8192, (n + 255) / 256);
-  // the batch grouped by digest: ranks and runs, then every value in its place
-  hipLaunchKernelGGL(k_td_count, dim3((unsigned)((n + TD_CHUNK - 1) / TD_CHUNK)), dim3(256), 0, s, c, part, offs, T, tb,
-                     td, none, st);
-  hipLaunchKernelGGL(k_td_place, dim3(grid), dim3(256), 0, s, c, part, offs, T, td, none, st);
-  // serial and wave tiers (each sorts its runs in LDS)
-  hipLaunchKernelGGL(k_td_small, dim3((unsigned)std::min<int64_t>(8192, (n + TD_SMALL_THREADS - 1) / TD_SMALL_THREADS)),
-                     dim3(TD_SMALL_THREADS), 0, s, c, tb, td, st);
-  hipLaunchKernelGGL(k_td_wave, dim3(2048), dim3(64 * TD_WAVES), td_wave_lds_bytes(c.td_nb), s, c, tb, td, td.v[0], st);
-  // large runs: sample sort, then the bucket-parallel merge
-  hipLaunchKernelGGL(k_td_sample, dim3(512), dim3(1024), 0, s, td, st);
-  hipLaunchKernelGGL(k_td_bin_count, dim3(grid), dim3(256), 0, s, c, offs, T, td, st);
-  hipLaunchKernelGGL(k_td_bin_scan, dim3(512), dim3(256), 0, s, td, st);
-  hipLaunchKernelGGL(k_td_bin_scatter, dim3(grid), dim3(256), 0, s, c, offs, T, td, st);
-  hipLaunchKernelGGL(k_td_bin_sort, dim3(1024), dim3(1024), 0, s, td, st);
-  hipLaunchKernelGGL(k_td_large_old, dim3(64), dim3(256), 0, s, c, td.v[0], td, st);  // (the mean keys: first)
-  hipLaunchKernelGGL(k_td_large_items, dim3(grid), dim3(256), 0, s, c, offs, T, td.v[0], td, st);
-  hipLaunchKernelGGL(k_td_large_groups, dim3(2048), dim3(256), 0, s, c, td.v[0], td, st);
+  hipLaunchKernelGGL(k_td_fix_mark, dim3(grid), dim3(256), 0, s, n, kv.current(), ks.current(), td.fixbm);
+  hipLaunchKernelGGL(k_td_fix_runs, dim3(grid), dim3(256), 0, s, n, kv.current(), ks.current(), td.fixbm);
+  uint32_t* gsorted = ks.alternate();
+  uint64_t* vsorted = kv.alternate();
+  hipLaunchKernelGGL(k_td_decode, dim3(grid), dim3(256), 0, s, n, B, nblk, none, kv.current(), ks.current(), td.binv,
+                     gsorted, vsorted);
+  const int64_t per_block = 256 * TD_BOUNDS_PER_THREAD;
+  hipLaunchKernelGGL(k_td_bounds, dim3((unsigned)((n + per_block - 1) / per_block)), dim3(256), 0, s, n, gsorted, none,
+                     td, st);
+  hipLaunchKernelGGL(k_td_small, dim3(grid), dim3(256), 0, s, c, tb, td, vsorted, st);
+  hipLaunchKernelGGL(k_td_wave, dim3(2048), dim3(64 * TD_WAVES), td_wave_lds_bytes(c.td_nb), s, c, tb, td, vsorted, st);
+  hipLaunchKernelGGL(k_td_large_old, dim3(64), dim3(256), 0, s, c, vsorted, td, st);  // (the mean keys: first)
+  hipLaunchKernelGGL(k_td_large_items, dim3(grid), dim3(256), 0, s, c, n, gsorted, vsorted, none, td, st);
+  hipLaunchKernelGGL(k_td_large_groups, dim3(2048), dim3(256), 0, s, c, vsorted, td, st);
   hipLaunchKernelGGL(k_td_large_compact, dim3(64), dim3(64), 0, s, c, td, st);
 }
 void launch_rehash(const DevCfg& oc, DevTable ot, const DevCfg& nc, DevTable nt, hipStream_t s) {

@@ -61,7 +61,6 @@
 #ifndef FW_TD_T3
 #define FW_TD_T3 2048          // ... at most this many in one wave; more over the whole grid (the hottest keys)
 #endif
-#define FW_TD_BIN 2048         // t-digest large runs: values per sample-sort bin (on average)
 #define FW_SLOW_THREADS 1024
 // Dense tumbling regions (DevCfg::dense): the LDS table of k_dt_aggregate (slots, threads, records per thread in
 // flight).  Regions are sized for about FW_DT_SLOTS * 3/4 live entries each.
@@ -301,33 +300,25 @@ struct TdLarge {  // a digest whose batch is compressed bucket-parallel
   TdCent* out;              // the other half (group sums per bucket, then the centroids)
   TdHead* head;
 };
-struct TdSamp {  // a large digest's sample sort: splitters spl[sbase ..+ ns), bins [bbase ..+ 2 ns + 1)
-  int32_t sbase, ns, bbase, pad;
-};
 struct TdBuf {
-  uint32_t* gs[2];          // per record: its digest's global slot (partition << log_r | slot) and its rank in
-                            // the digest's run; then the large runs' bin and rank in the bin
-  uint64_t* v[2];           // [0] the batch's values (Double.compare keys) grouped into one run per digest, sorted
-                            // in place; [1] the large runs' values grouped by bin
-  uint32_t* lpos;           // [max_batch] the large digest index of each position of the large runs
-  uint32_t* tcnt;           // [table slots] values of the digest placed so far (zero between pushes)
-  uint32_t* tbase;          // [table slots] first position of the digest's run (bit 31: a large digest)
+  uint32_t* gs[2];          // low value bits (sort payload), then the global slot (partition << log_r | slot)
+  uint64_t* v[2];           // (pool block, high value bits) sort keys, then the Double.compare-ordered value
+  uint32_t* binv;           // [pool blocks] global slot of each block's entry (rewritten when it moved)
+  uint32_t* fixbm;          // [max_batch / 32] tie runs whose low value bits need sorting
+  void* tmp;                // rocPRIM radix-sort scratch
+  size_t tmp_bytes;
   uint32_t* tslot;          // touched digests: global slot      [max_batch]
-  uint32_t* tbeg;           //                  first position of its run [max_batch]
-  int32_t* ctr;             // [0] touched digests, [1] large ones, [2] wave-tier ones, [3] positions taken from the
-                            // bottom (serial and wave runs), [4] from the top (large runs), [5] splitters, [6] bins
+  uint32_t* tbeg;           //                  first sorted value [max_batch]
+  int32_t* ctr;             // [0] touched digests, [1] large ones, [2] wave-tier ones
   uint32_t* mid;            // [max_batch] the wave tier's digests (touched indices)
   TdLarge* large;           // [max_large]
-  TdSamp* samp;             // [max_large]
-  uint64_t* spl;            // [max_spl] splitters
-  uint32_t* bcnt;           // [max_bins] values per bin (bit 31: a bin of values equal to a splitter)
-  uint32_t* bstart;         // [max_bins] first position of each bin
   int32_t* nstart;          // [max_large * td_nb] first sorted value of each bucket (-1: none)
   int32_t* ostart;          // [max_large * td_nb] first old centroid of each bucket (-1: none)
   uint64_t* okey;           // [max_large * td_nb] the large digests' old centroids' mean keys
-  int32_t* lidx;            // [table slots] large index of a touched large digest
+  int32_t* lidx;            // [table slots] large index of a touched digest, -1 = compressed serially
   int64_t lidx_slots;
-  int32_t max_large, max_spl, max_bins;
+  int32_t max_large;
+  int32_t sel;              // which of gs / v holds the sorted batch (set by launch_tdigest)
 };
 
 // ---- count windows (FW_COUNT): per key its element count and a ring of its last size-1 elements
@@ -425,6 +416,7 @@ void launch_hll_update(const DevCfg& c, const PRec* part, const uint32_t* offs, 
 // FW_AGG_TDIGEST: compress the batch's values into the digests of their (key, window) entries (after aggregate)
 void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
                     TdBuf& td, Status* st, hipStream_t_ s);
+size_t tdigest_sort_bytes(int64_t n);  // rocPRIM scratch of the two sorts
 // FW_COUNT: one batch of count windows (key slots, stable sort by key, fire, ring update); val = the push's values
 void launch_count(const DevCfg& c, DevCount& cw, const int64_t* key, const int64_t* val, int64_t n, DevRows out,
                   Status* st, hipStream_t_ s);

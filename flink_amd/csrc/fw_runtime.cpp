@@ -404,20 +404,6 @@ int put_status_field(fw_op* op, T Status::*field) {
 }
 
 // grow every region to new_log_r, re-inserting the live entries (stream idle on exit)
-// the t-digest compression's per-slot arrays, sized with the table (the placement counters start at zero)
-int alloc_td_slots(fw_op* op) {
-  TdBuf& t = op->td;
-  dfree(t.lidx);
-  dfree(t.tcnt);
-  dfree(t.tbase);
-  HIP_OR_RETURN(op, dmalloc(&t.lidx, (size_t)op->table_slots));
-  HIP_OR_RETURN(op, dmalloc(&t.tcnt, (size_t)op->table_slots));
-  HIP_OR_RETURN(op, dmalloc(&t.tbase, (size_t)op->table_slots));
-  HIP_OR_RETURN(op, hipMemsetAsync(t.tcnt, 0, (size_t)op->table_slots * sizeof(uint32_t), op->stream));
-  t.lidx_slots = op->table_slots;
-  return 0;
-}
-
 int grow_table(fw_op* op, int new_log_r) {
   if (new_log_r > 30) return set_err(op, FW_ERR_CAPACITY, "state region would exceed 2^30 slots");
   DevCfg nc = op->dc;
@@ -446,8 +432,9 @@ int grow_table(fw_op* op, int new_log_r) {
   op->grows++;
   if (op->dc.agg == FW_AGG_TDIGEST) {  // the compression's per-slot index follows the table
     if (op->table_slots >= (int64_t(1) << 31)) return set_err(op, FW_ERR_CAPACITY, "t-digest table would exceed 2^31 slots");
-    int rc = alloc_td_slots(op);
-    if (rc) return rc;
+    dfree(op->td.lidx);
+    HIP_OR_RETURN(op, dmalloc(&op->td.lidx, (size_t)op->table_slots));
+    op->td.lidx_slots = op->table_slots;
   }
   const int64_t rows = (int64_t)op->h_status->out_rows;
   return ensure_out_capacity(op, rows + op->table_slots, rows);
@@ -1075,26 +1062,25 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
       HIP_OR_RETURN(op, dmalloc(&t.gs[b], (size_t)mb));
       HIP_OR_RETURN(op, dmalloc(&t.v[b], (size_t)mb));
     }
-    HIP_OR_RETURN(op, dmalloc(&t.lpos, (size_t)mb));
+    t.tmp_bytes = fwdev::tdigest_sort_bytes(mb);
+    HIP_OR_RETURN(op, dmalloc((uint8_t**)&t.tmp, t.tmp_bytes));
+    HIP_OR_RETURN(op, dmalloc(&t.binv, (size_t)c.pool_blocks));
+    HIP_OR_RETURN(op, hipMemsetAsync(t.binv, 0xff, (size_t)c.pool_blocks * sizeof(uint32_t), op->stream));
+    HIP_OR_RETURN(op, dmalloc(&t.fixbm, (size_t)((mb + 31) / 32)));
     HIP_OR_RETURN(op, dmalloc(&t.tslot, (size_t)mb));
     HIP_OR_RETURN(op, dmalloc(&t.tbeg, (size_t)mb));
-    HIP_OR_RETURN(op, dmalloc(&t.ctr, 8));
+    HIP_OR_RETURN(op, dmalloc(&t.ctr, 3));
     // a wave-tier digest has more than FW_TD_T1 - delta/2 values in the batch, a large one more than
-    // FW_TD_T3 - delta/2; a large run of m values has at most m / FW_TD_BIN splitters and 2 m / FW_TD_BIN + 1 bins
+    // FW_TD_T3 - delta/2
     HIP_OR_RETURN(op, dmalloc(&t.mid, (size_t)mb));
     t.max_large = (int32_t)(mb / std::max<int64_t>(1, FW_TD_T3 - c.td_nb) + 1);
-    t.max_spl = (int32_t)(mb / FW_TD_BIN + 1);
-    t.max_bins = 2 * t.max_spl + t.max_large;
     HIP_OR_RETURN(op, dmalloc(&t.large, (size_t)t.max_large));
-    HIP_OR_RETURN(op, dmalloc(&t.samp, (size_t)t.max_large));
-    HIP_OR_RETURN(op, dmalloc(&t.spl, (size_t)t.max_spl));
-    HIP_OR_RETURN(op, dmalloc(&t.bcnt, (size_t)t.max_bins));
-    HIP_OR_RETURN(op, dmalloc(&t.bstart, (size_t)t.max_bins));
     HIP_OR_RETURN(op, dmalloc(&t.nstart, (size_t)t.max_large * c.td_nb));
     HIP_OR_RETURN(op, dmalloc(&t.ostart, (size_t)t.max_large * c.td_nb));
     HIP_OR_RETURN(op, dmalloc(&t.okey, (size_t)t.max_large * c.td_nb));
     if (op->table_slots >= (int64_t(1) << 31)) return set_err(op, FW_ERR_CAPACITY, "t-digest table would exceed 2^31 slots");
-    if ((rc = alloc_td_slots(op))) return rc;
+    HIP_OR_RETURN(op, dmalloc(&t.lidx, (size_t)op->table_slots));
+    t.lidx_slots = op->table_slots;
   }
   if (cfg.assigner == FW_COUNT) {
     DevCount& w = op->cw;
@@ -1175,13 +1161,10 @@ void fw_destroy(fw_op* op) {
       dfree(t.gs[b]);
       dfree(t.v[b]);
     }
-    dfree(t.lpos);
-    dfree(t.tcnt);
-    dfree(t.tbase);
-    dfree(t.samp);
-    dfree(t.spl);
-    dfree(t.bcnt);
-    dfree(t.bstart);
+    uint8_t* tmp = (uint8_t*)t.tmp;
+    dfree(tmp);
+    dfree(t.binv);
+    dfree(t.fixbm);
     dfree(t.tslot);
     dfree(t.tbeg);
     dfree(t.ctr);
