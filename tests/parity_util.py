@@ -7,16 +7,21 @@ F64_RTOL = 1e-6  # north_star: floating-point sums within 1e-6 relative
 F32_U = 2.0 ** -24  # unit roundoff of float
 
 
-def f32_sum_bound(rows):
+def f32_sum_bound(rows, sums=()):
     """north_star exception for Float fields (DESIGN §2 "Float sums"): FloatSum rounds every partial sum to float in
     arrival order (SumFunction.java:92-99), so the reference's sum S_java of a window's n elements x_i carries the
     recursive-summation error |S_java - S| <= (n - 1) u sum|x_i| (u = 2^-24), which depends on the order and is not
     within 1e-6 of S for long or cancelling windows.  The GPU sums in f64 and rounds once (|S_gpu - S| <= u |S| +
     n 2^-53 sum|x_i|).  So the two agree within (n + 1) u sum|x_i|, with sum|x_i| <= n max(|min|, |max|) from the
-    row itself: the bound checked here, per row (not a relative tolerance)."""
+    row itself: the bound checked here, per row (not a relative tolerance).  A passthrough row (FW_AGG_FIRST) keeps
+    the first element's ordinal in `max`, so there the magnitude is also taken from the sums (`sums`): |S| =
+    sum|x_i| for a field of one sign, which is what the passthrough tests feed."""
     n = rows["count"].astype(np.float64)
     amax = np.maximum(np.abs(rows["min"].view(np.float64)), np.abs(rows["max"].view(np.float64)))
-    return (n + 1.0) * F32_U * n * amax * 1.001
+    mag = n * amax
+    for sm in sums:
+        mag = np.maximum(mag, np.abs(sm))
+    return (n + 1.0) * F32_U * mag * 1.001
 
 
 def _sorted(rows):
@@ -41,7 +46,7 @@ def assert_rows_equal(gpu, ref, value_type="long"):
         gs, rs = g["sum"].view(np.float64), r["sum"].view(np.float64)
         if value_type == "float":
             with np.errstate(invalid="ignore"):
-                ok = (np.abs(gs - rs) <= f32_sum_bound(r)) | (gs == rs) | (np.isnan(gs) & np.isnan(rs))
+                ok = (np.abs(gs - rs) <= f32_sum_bound(r, (gs, rs))) | (gs == rs) | (np.isnan(gs) & np.isnan(rs))
         else:
             ok = np.isclose(gs, rs, rtol=F64_RTOL, atol=0.0) | (np.isnan(gs) & np.isnan(rs))
         bad = np.nonzero(~ok)[0]
