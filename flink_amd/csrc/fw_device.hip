@@ -22,6 +22,7 @@
 //                       whose earliest timer is <= wm emits its fired windows and is rebuilt, without
 //                       the cleaned-up entries, into the region's other buffer.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -5834,6 +5835,18 @@ __global__ __launch_bounds__(256) void k_generate(uint64_t seed, int64_t first, 
 // ============================================================================== launchers
 namespace fwdev {
 
+ExtTiming g_ext{};
+// a kind's main kernel: with the dispatch's own start / stop events when fw_profile asked for them (g_ext)
+#define FW_LAUNCH_MAIN(kern, grid, block, lds, s, ...)                                                        \
+  do {                                                                                                     \
+    if (g_ext.a && !g_ext.used) {                                                                          \
+      hipExtLaunchKernelGGL(kern, grid, block, lds, s, g_ext.a, g_ext.b, 0, __VA_ARGS__);                  \
+      g_ext.used = true;                                                                                   \
+    } else {                                                                                               \
+      hipLaunchKernelGGL(kern, grid, block, lds, s, __VA_ARGS__);                                          \
+    }                                                                                                      \
+  } while (0)
+
 static inline int32_t ntiles(int64_t n) { return (int32_t)((n + FW_TILE - 1) / FW_TILE); }
 
 void launch_classify_hist(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int32_t* kh,
@@ -5933,11 +5946,11 @@ void launch_scatter_rsv(const DevCfg& c, int64_t wm, const int64_t* key, const i
     attr = true;
   }
   if (big)
-    hipLaunchKernelGGL(k_scatter_rsv<8192>, dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n, T, part,
-                       rsv, rcap);
+    FW_LAUNCH_MAIN(k_scatter_rsv<8192>, dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n, T, part, rsv,
+                   rcap);
   else
-    hipLaunchKernelGGL(k_scatter_rsv<4096>, dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n, T, part,
-                       rsv, rcap);
+    FW_LAUNCH_MAIN(k_scatter_rsv<4096>, dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n, T, part, rsv,
+                   rcap);
 }
 
 // panes: maxTimestamp of the earliest window ending after wm (windows [s, s + size), s = offset mod slide)
@@ -5966,8 +5979,8 @@ void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint
     }
   }
   if (c.dense) {  // the compact table; in a resumed sequence the wide launch takes the regions it left
-    hipLaunchKernelGGL((k_dt_aggregate<DT_RECS, true>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs,
-                       T, tb, prog, resume, st, rsv, rcap);
+    FW_LAUNCH_MAIN((k_dt_aggregate<DT_RECS, true>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs, T,
+                   tb, prog, resume, st, rsv, rcap);
     if (resume)
       hipLaunchKernelGGL((k_dt_aggregate<DT_RECS, false>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part,
                          offs, T, tb, prog, 1, st, rsv, rcap);

@@ -367,6 +367,14 @@ struct PartialRec {
 // ---------------------------------------------------------------- launchers (fw_device.hip)
 typedef hipStream_t hipStream_t_;
 namespace fwdev {
+// fw_profile's dispatch timing (set by the runtime around one launch helper): when `a` is set, the helper issues
+// its kind's main kernel with hipExtLaunchKernelGGL and these start / stop events, which take that dispatch's own
+// timestamps instead of marker packets on the stream, and sets `used`
+struct ExtTiming {
+  hipEvent_t a, b;
+  bool used;
+};
+extern ExtTiming g_ext;
 void launch_classify_hist(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int32_t* kh,
                           int64_t n, int32_t T, uint32_t* hist, Status* st, hipStream_t_ s,
                           const uint32_t* rsv = nullptr);

@@ -343,15 +343,30 @@ hipEvent_t prof_event(fw_op* op) {
   (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   return e;
 }
-// time the launches issued by `launch` on the handle's stream as one interval of `kind`
+// time the launches issued by `launch` on the handle's stream as one interval of `kind`.  ext: `launch` issues
+// exactly one kernel of the kind (fwdev::FW_LAUNCH_MAIN), timed by its dispatch's own start / stop events
+// (fwdev::g_ext) instead of two marker packets around it (each pair of markers cost C2 ~10 us per step)
 template <class F>
-void timed(fw_op* op, int kind, F&& launch, hipStream_t on = nullptr) {
+void timed(fw_op* op, int kind, F&& launch, hipStream_t on = nullptr, bool ext = false) {
   if (!((op->prof_mask >> kind) & 1u)) {
     launch();
     return;
   }
   if (!on) on = op->stream;
   fw_op::Pair pr{prof_event(op), prof_event(op), kind};
+  if (ext) {
+    fwdev::g_ext = fwdev::ExtTiming{pr.a, pr.b, false};
+    launch();
+    const bool used = fwdev::g_ext.used;
+    fwdev::g_ext = fwdev::ExtTiming{};
+    if (used) {
+      op->prof_pending.push_back(pr);
+    } else {  // (no main kernel this time: nothing to time)
+      op->prof_free.push_back(pr.a);
+      op->prof_free.push_back(pr.b);
+    }
+    return;
+  }
   (void)hipEventRecord(pr.a, on);
   launch();
   (void)hipEventRecord(pr.b, on);
@@ -672,7 +687,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
     if (single) {
       HIP_OR_RETURN(op, hipMemsetAsync(S.rsv, 0, ((size_t)c.P + FW_RSV_WORDS) * sizeof(uint32_t), bs));
       timed(op, K_SCATTER, [&] { fwdev::launch_scatter_rsv(c, op->wm, key, ts, val, kh, n, T, S.part, S.rsv, op->rcap, bs); },
-            bs);
+            bs, true);
     }
     const uint32_t* gate = single ? S.rsv + c.P : nullptr;
     if (single) {  // (fw_profile: the gated sequence counts as classify)
@@ -731,12 +746,15 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   // a partition can outgrow one aggregate workgroup (hot keys) only when the batch is longer than a chunk
   const bool split = !cc.dense && (cc.wpr == 1 || cc.panes) && n > FW_AGG_CHUNK;
   if (split && (rc = ensure_hot(op))) return rc;
-  timed(op, K_AGGREGATE, [&] {
-    fwdev::launch_aggregate(cc, op->wm, S.part, S.offs(), S.offT(), op->tb, op->prog, 0, split ? &op->hot : nullptr, n,
-                            op->d_status, op->stream, nullptr, 0, single ? S.rsv : nullptr, op->rcap);
-    if (cc.agg == FW_AGG_HLL)
-      fwdev::launch_hll_update(cc, S.part, S.offs(), S.offT(), n, op->tb, op->d_status, op->stream);
-  });
+  timed(
+      op, K_AGGREGATE,
+      [&] {
+        fwdev::launch_aggregate(cc, op->wm, S.part, S.offs(), S.offT(), op->tb, op->prog, 0, split ? &op->hot : nullptr,
+                                n, op->d_status, op->stream, nullptr, 0, single ? S.rsv : nullptr, op->rcap);
+        if (cc.agg == FW_AGG_HLL)
+          fwdev::launch_hll_update(cc, S.part, S.offs(), S.offT(), n, op->tb, op->d_status, op->stream);
+      },
+      nullptr, cc.dense);  // (the dense aggregate is one kernel)
   if (cc.agg == FW_AGG_TDIGEST)
     timed(op, K_TDIGEST, [&] {
       fwdev::launch_tdigest(cc, S.part, S.offs(), S.offT(), n, op->tb, op->td, op->d_status, op->stream);
