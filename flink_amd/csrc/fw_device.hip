@@ -2822,7 +2822,10 @@ __global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, 
 // block and push it on the free stack.  S = sum_j 2^(65-p-M[j]) exactly, in 128 bits.  Only the chunks the
 // block's bitmap marks are read (and zeroed): every register of an unmarked chunk is zero.
 // stack_slot < 0: the window stays (FIRE without purge under allowed lateness): the block is read, not zeroed or freed
-__device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, int64_t stack_slot) {
+// A block with at most 64 marked chunks (a window of few distinct items: most windows of a Zipf stream's tail keys)
+// takes two round trips: the bitmap (a word per lane), then every marked chunk at once, one per lane, from the
+// chunk ids the wave lays out in its LDS scratch `ids` (64 words); a fuller block walks its bitmap 256 chunks a pass.
+__device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, int64_t stack_slot, uint32_t* ids) {
   const bool release = stack_slot >= 0;
   const int lane = __lane_id();
   const int p = c.hll_p, rmax = 65 - p;
@@ -2836,9 +2839,49 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, in
   uint64_t s = 0, sh = 0;
   uint32_t zeros = 0, touched = 0;
   constexpr int U = 4;  // word pairs per pass: up to 4 chunk loads in flight per lane
-  uint32_t myw = 0;      // the bitmap, one word per lane (64 words = 2^15 registers at a time)
-  for (int32_t w0 = 0; w0 < nw; w0 += 2 * U) {
-    if ((w0 & 63) == 0) myw = w0 + lane < nw ? bits[w0 + lane] : 0u;
+  uint32_t myw = lane < nw ? bits[lane] : 0u;  // the bitmap, one word per lane (64 words = 2^15 registers at a time)
+  int32_t w_start = 0;
+  if (nw <= 64) {
+    const uint32_t cnt = (uint32_t)__popc(myw);
+    uint32_t x = cnt;  // inclusive prefix of the marked chunks over the lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+      if (lane >= o) x += y;
+    }
+    const uint32_t tot = (uint32_t)__shfl((int)x, 63, 64);
+    if (tot <= 64) {
+      uint32_t k = x - cnt, word = myw;
+      while (word) {
+        const int b = __ffs(word) - 1;
+        word &= word - 1;
+        ids[k++] = (uint32_t)(lane * 32 + b);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if ((uint32_t)lane < tot) {
+        const uint32_t j = ids[lane];
+        const uint4 v = q[j];
+        touched = 1;
+        const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++)
+#pragma unroll
+          for (int b = 0; b < 4; b++) {
+            const uint32_t r = (ws[kk] >> (8 * b)) & 0xffu;
+            const uint64_t t = s + (1ull << (rmax - (int)r));
+            sh += t < s;
+            s = t;
+            zeros += r == 0;
+          }
+        if (release) q[j] = make_uint4(0, 0, 0, 0);
+      }
+      __builtin_amdgcn_wave_barrier();  // (ids is the wave's next row's)
+      w_start = nw;                     // every marked chunk is read
+    }
+  }
+  for (int32_t w0 = w_start; w0 < nw; w0 += 2 * U) {
+    if ((w0 & 63) == 0 && w0 > 0) myw = w0 + lane < nw ? bits[w0 + lane] : 0u;
     uint4 v[U];
     bool on[U];
     int32_t jj[U];
@@ -2961,7 +3004,12 @@ __device__ void hll_clear(const DevCfg& c, uint64_t blk) {
 #define FW_HLL_CHUNK_N 4096
 #endif
 constexpr int FW_HLL_CHUNK = FW_HLL_CHUNK_N;
-__global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __restrict__ part,
+#ifndef FW_HLL_WAVES
+#define FW_HLL_WAVES 1
+#endif
+// SLIDE: records of sliding windows (PRec, nwin windows each); tumbling records carry one window (no window loop)
+template <bool SLIDE>
+__global__ __launch_bounds__(256, FW_HLL_WAVES) void k_hll_update(DevCfg c, const PRec* __restrict__ part,
                                                     const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
                                                     Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
@@ -2994,7 +3042,7 @@ __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __rest
   // (SlidingEventTimeWindows.java:67-81); the windows are walked one per pass of this loop
   for (int64_t ib = i0 + threadIdx.x; ib < i1; ib += (int64_t)blockDim.x * HU) {
    int32_t nw_max = 1;
-   for (int32_t wi = 0; wi < nw_max; wi++) {
+   for (int32_t wi = 0; wi < (SLIDE ? nw_max : 1); wi++) {
     int64_t key[HU], last[HU], val[HU];
     int32_t part_of_rec[HU];
     bool in[HU];
@@ -3015,10 +3063,13 @@ __global__ __launch_bounds__(256) void k_hll_update(DevCfg c, const PRec* __rest
       } else {
         const PRec rec = part[i];
         key[u] = rec.key;
-        const int32_t nw = (int32_t)(rec.nwin & 0xffff);
-        nw_max = max(nw_max, nw);
-        in[u] = wi < nw;
-        last[u] = jsub(rec.last, (int64_t)wi * c.slide);
+        last[u] = rec.last;
+        if constexpr (SLIDE) {
+          const int32_t nw = (int32_t)(rec.nwin & 0xffff);
+          nw_max = max(nw_max, nw);
+          in[u] = wi < nw;
+          last[u] = jsub(rec.last, (int64_t)wi * c.slide);
+        }
         val[u] = rec.val;
       }
     }
@@ -4207,9 +4258,10 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
     __syncthreads();
     const uint64_t end = min((unsigned long long)out.cap, base_s + total);
     if (c.agg == FW_AGG_HLL) {
+      __shared__ uint32_t hl_ids[FW_FIRE_THREADS];  // 64 chunk ids per wave (hll_finish)
       for (uint64_t r = base_s + (threadIdx.x >> 6); r < end; r += blockDim.x >> 6) {
         const int64_t ri = out.mx[r];  // (every lane reads it before lane 0 overwrites it)
-        hll_finish(c, out, r, ri < 0 ? -1 : hl_sb + ri);
+        hll_finish(c, out, r, ri < 0 ? -1 : hl_sb + ri, hl_ids + (threadIdx.x & ~63u));
       }
     } else {
       __shared__ unsigned long long cent_s;
@@ -6069,8 +6121,11 @@ void launch_stage(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t
 void launch_hll_update(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
                        Status* st, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_hll_update, dim3((unsigned)((n + FW_HLL_CHUNK - 1) / FW_HLL_CHUNK)), dim3(256), 0, s, c, part,
-                     offs, T, tb, st);
+  const dim3 grid((unsigned)((n + FW_HLL_CHUNK - 1) / FW_HLL_CHUNK));
+  if (c.assigner == FW_SLIDING)
+    hipLaunchKernelGGL(k_hll_update<true>, grid, dim3(256), 0, s, c, part, offs, T, tb, st);
+  else
+    hipLaunchKernelGGL(k_hll_update<false>, grid, dim3(256), 0, s, c, part, offs, T, tb, st);
 }
 
 void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* srow, int32_t T, const int64_t* sk, const int64_t* stt,
