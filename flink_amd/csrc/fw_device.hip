@@ -3004,6 +3004,10 @@ __device__ void hll_clear(const DevCfg& c, uint64_t blk) {
 #define FW_HLL_CHUNK_N 4096
 #endif
 constexpr int FW_HLL_CHUNK = FW_HLL_CHUNK_N;
+#ifndef FW_HLL_MARK
+#define FW_HLL_MARK 3  // chunk marks skipped: 1 = when the mark's word (read through L1) has it, 2 = when another
+                       // register of the raised word is non-zero (its raise marks, or marked, the chunk)
+#endif
 #ifndef FW_HLL_WAVES
 #define FW_HLL_WAVES 1
 #endif
@@ -3085,6 +3089,9 @@ __global__ __launch_bounds__(256, FW_HLL_WAVES) void k_hll_update(DevCfg c, cons
       hw[u] = 0;
       if (!in[u]) continue;
       const uint32_t home = (uint32_t)hs[u] & rg[u].mask;
+#ifdef FW_HLL_NOLOOKUP
+      continue;
+#endif
       hw[u] = rg[u].state[home];  // (the table is read-only here: a plain, L1-cacheable read)
       hk[u] = *reinterpret_cast<const i64x2*>(&rg[u].ent[home].key);
       hend[u] = rg[u].ent[home].end;
@@ -3095,6 +3102,10 @@ __global__ __launch_bounds__(256, FW_HLL_WAVES) void k_hll_update(DevCfg c, cons
     for (int u = 0; u < HU; u++) {
       blk[u] = 0;
       if (!in[u]) continue;
+#ifdef FW_HLL_NOLOOKUP  // (timing ablation only: the block from a hash, results wrong)
+      blk[u] = fmix64((uint64_t)key[u] ^ (uint64_t)last[u]) % (uint64_t)c.pool_blocks;
+      continue;
+#endif
       const int64_t we = wend(c, last[u]);
       if (hw[u] == live_word(hs[u]) && hk[u].x == key[u] && hk[u].y == last[u] && hend[u] == we) {
         blk[u] = (uint64_t)hmeta[u] >> 1;
@@ -3120,22 +3131,44 @@ __global__ __launch_bounds__(256, FW_HLL_WAVES) void k_hll_update(DevCfg c, cons
       // costs at most a CAS that returns the current word (a hot digest's block stays in the CU's L1)
       old[u] = in[u] ? *w[u] : 0u;
     }
+    // every raise's CAS in flight at once; one that lost to another record's raise of the same word retries alone
+    uint32_t got[HU], nwv[HU];
+    bool need[HU];
 #pragma unroll
     for (int u = 0; u < HU; u++) {
-      if (!in[u]) continue;
       const int sh = (int)(jj[u] & 3) * 8;
-      uint32_t o = old[u];
-      while (((o >> sh) & 0xffu) < rank[u]) {
+      need[u] = in[u] && ((old[u] >> sh) & 0xffu) < rank[u];
+#if defined(FW_HLL_ABL) && (FW_HLL_ABL & 2)  // (timing ablation only: registers read, never raised)
+      need[u] = false;
+#endif
+      nwv[u] = (old[u] & ~(0xffu << sh)) | (rank[u] << sh);
+      got[u] = need[u] ? atomicCAS(w[u], old[u], nwv[u]) : old[u];
+    }
+#pragma unroll
+    for (int u = 0; u < HU; u++) {
+      if (!need[u]) continue;
+      const int sh = (int)(jj[u] & 3) * 8;
+      uint32_t o = got[u], prev = old[u];
+      bool done = o == old[u];
+      while (!done && ((o >> sh) & 0xffu) < rank[u]) {
         const uint32_t nw = (o & ~(0xffu << sh)) | (rank[u] << sh);
-        if (__hip_atomic_compare_exchange_strong(w[u], &o, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-          // this record took the register out of zero: mark its chunk for the fire
-          if (((o >> sh) & 0xffu) == 0u) {
-            const uint32_t ch = jj[u] >> 4;
-            atomicOr(reinterpret_cast<uint32_t*>(c.pool + blk[u] * (uint64_t)c.pool_bytes) + (ch >> 5), 1u << (ch & 31u));
-          }
-          break;
-        }
+        prev = o;
+        done = __hip_atomic_compare_exchange_strong(w[u], &o, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // this record took the register out of zero: mark its chunk for the fire, unless another register of the
+      // word is non-zero (its raise marks, or marked, the chunk) or the mark's word (read through L1) has it (a
+      // stale unmarked copy costs one redundant atomic; a mark is never cleared meanwhile)
+#if defined(FW_HLL_ABL) && (FW_HLL_ABL & 1)  // (timing ablation only: no chunk marks)
+      done = false;
+#endif
+      if (done && ((prev >> sh) & 0xffu) == 0u) {
+        const uint32_t ch = jj[u] >> 4;
+        uint32_t* mw = reinterpret_cast<uint32_t*>(c.pool + blk[u] * (uint64_t)c.pool_bytes) + (ch >> 5);
+        bool mark = true;
+        if (FW_HLL_MARK & 2) mark = (prev & ~(0xffu << sh)) == 0u;
+        if ((FW_HLL_MARK & 1) && mark) mark = !((*mw >> (ch & 31u)) & 1u);
+        if (mark) atomicOr(mw, 1u << (ch & 31u));
       }
     }
     if (wi + 1 == nw_max) pp = pp_w;
