@@ -3008,6 +3008,9 @@ constexpr int FW_HLL_CHUNK = FW_HLL_CHUNK_N;
 #define FW_HLL_MARK 3  // chunk marks skipped: 1 = when the mark's word (read through L1) has it, 2 = when another
                        // register of the raised word is non-zero (its raise marks, or marked, the chunk)
 #endif
+#ifndef FW_HLL_BLIND
+#define FW_HLL_BLIND 256
+#endif
 #ifndef FW_HLL_WAVES
 #define FW_HLL_WAVES 1
 #endif
@@ -3079,7 +3082,7 @@ __global__ __launch_bounds__(256, FW_HLL_WAVES) void k_hll_update(DevCfg c, cons
     }
     uint32_t hw[HU];
     i64x2 hk[HU];
-    int64_t hend[HU], hmeta[HU];
+    int64_t hend[HU], hmeta[HU], hcnt[HU];
     uint64_t hs[HU];
     Region rg[HU];
 #pragma unroll
@@ -3096,11 +3099,14 @@ __global__ __launch_bounds__(256, FW_HLL_WAVES) void k_hll_update(DevCfg c, cons
       hk[u] = *reinterpret_cast<const i64x2*>(&rg[u].ent[home].key);
       hend[u] = rg[u].ent[home].end;
       hmeta[u] = rg[u].ent[home].meta;
+      hcnt[u] = rg[u].ent[home].cnt;
     }
     uint64_t blk[HU];
+    bool blind[HU];
 #pragma unroll
     for (int u = 0; u < HU; u++) {
       blk[u] = 0;
+      blind[u] = false;
       if (!in[u]) continue;
 #ifdef FW_HLL_NOLOOKUP  // (timing ablation only: the block from a hash, results wrong)
       blk[u] = fmix64((uint64_t)key[u] ^ (uint64_t)last[u]) % (uint64_t)c.pool_blocks;
@@ -3109,6 +3115,7 @@ __global__ __launch_bounds__(256, FW_HLL_WAVES) void k_hll_update(DevCfg c, cons
       const int64_t we = wend(c, last[u]);
       if (hw[u] == live_word(hs[u]) && hk[u].x == key[u] && hk[u].y == last[u] && hend[u] == we) {
         blk[u] = (uint64_t)hmeta[u] >> 1;
+        blind[u] = hcnt[u] <= FW_HLL_BLIND;
       } else {
         const int32_t slot = hw[u] == SLOT_EMPTY ? -1 : region_find(rg[u], hs[u] + 1, key[u], last[u], we, live_word(hs[u]));
         if (slot < 0) {
@@ -3117,6 +3124,7 @@ __global__ __launch_bounds__(256, FW_HLL_WAVES) void k_hll_update(DevCfg c, cons
           continue;
         }
         blk[u] = pool_block_of(rg[u].ent[slot]);
+        blind[u] = rg[u].ent[slot].cnt <= FW_HLL_BLIND;
       }
     }
     uint32_t* w[HU];
@@ -3128,8 +3136,10 @@ __global__ __launch_bounds__(256, FW_HLL_WAVES) void k_hll_update(DevCfg c, cons
       rank[u] = (uint32_t)__clzll((long long)((h << p) | (1ull << (p - 1)))) + 1u;
       w[u] = reinterpret_cast<uint32_t*>(c.pool + blk[u] * (uint64_t)c.pool_bytes + hdr + (jj[u] & ~3u));
       // a plain (L1-cacheable) read: registers only grow, so a stale copy is never above the register and
-      // costs at most a CAS that returns the current word (a hot digest's block stays in the CU's L1)
-      old[u] = in[u] ? *w[u] : 0u;
+      // costs at most a CAS that returns the current word (a hot digest's block stays in the CU's L1).  A window
+      // of few items (its count, after this batch, at most FW_HLL_BLIND) skips the read: its word is most likely
+      // still zero, and a CAS that finds it otherwise returns it
+      old[u] = in[u] && !blind[u] ? *w[u] : 0u;
     }
     // every raise's CAS in flight at once; one that lost to another record's raise of the same word retries alone
     uint32_t got[HU], nwv[HU];
