@@ -4213,17 +4213,26 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
   // FIRE_U slots per thread per step: their state words, then their live entries, are loaded before any is used
   // (one slot at a time left the scan waiting on each load in turn)
   constexpr int FIRE_U = POOL ? 1 : 4;  // (the pool rows' one-wave-per-row finish wants the occupancy more)
+  // (the next step's state words are loaded with this step's entries: one round trip per step)
+  uint32_t wn[FIRE_U];
+#pragma unroll
+  for (int u = 0; u < FIRE_U; u++) {
+    const uint32_t s = u * blockDim.x + threadIdx.x;
+    wn[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
+  }
   for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x * FIRE_U) {
     uint32_t w[FIRE_U];
 #pragma unroll
-    for (int u = 0; u < FIRE_U; u++) {
-      const uint32_t s = s0 + u * blockDim.x + threadIdx.x;
-      w[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
-    }
+    for (int u = 0; u < FIRE_U; u++) w[u] = wn[u];
     Entry eu[FIRE_U];
 #pragma unroll
     for (int u = 0; u < FIRE_U; u++)
       if (st_kind(w[u]) == SLOT_LIVE) eu[u] = rx.ent[s0 + u * blockDim.x + threadIdx.x];
+#pragma unroll
+    for (int u = 0; u < FIRE_U; u++) {
+      const uint32_t s = s0 + blockDim.x * FIRE_U + u * blockDim.x + threadIdx.x;
+      wn[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
+    }
 #pragma unroll
     for (int u = 0; u < FIRE_U; u++) {
       if (st_kind(w[u]) != SLOT_LIVE) continue;
@@ -4261,17 +4270,26 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
   __syncthreads();
   if (nfire) {
     unsigned long long pos = base_s + pos0;
+    // (the next step's state words are loaded with this step's entries: one round trip per step)
+    uint32_t wn[FIRE_U];
+#pragma unroll
+    for (int u = 0; u < FIRE_U; u++) {
+      const uint32_t s = u * blockDim.x + threadIdx.x;
+      wn[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
+    }
     for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x * FIRE_U) {
       uint32_t w[FIRE_U];
 #pragma unroll
-      for (int u = 0; u < FIRE_U; u++) {
-        const uint32_t s = s0 + u * blockDim.x + threadIdx.x;
-        w[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
-      }
+      for (int u = 0; u < FIRE_U; u++) w[u] = wn[u];
       Entry eu[FIRE_U];
 #pragma unroll
       for (int u = 0; u < FIRE_U; u++)
         if (st_kind(w[u]) == SLOT_LIVE) eu[u] = rx.ent[s0 + u * blockDim.x + threadIdx.x];
+#pragma unroll
+      for (int u = 0; u < FIRE_U; u++) {
+        const uint32_t s = s0 + blockDim.x * FIRE_U + u * blockDim.x + threadIdx.x;
+        wn[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
+      }
 #pragma unroll
       for (int u = 0; u < FIRE_U; u++) {
         if (st_kind(w[u]) != SLOT_LIVE) continue;
@@ -4338,10 +4356,22 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
 // formed are dead (GC timer at maxTimestamp, allowedLateness 0): they are tombstoned in place and the
 // region is compacted into the other buffer once tombstones pass R/8.  A slice whose rows do not fit
 // the output suspends the launch at (E, slice); the host grows the buffer and fires again.
-constexpr int PF_THREADS = 1024;
-constexpr int PF_SLOTS = 2048;
-constexpr int PF_LIMIT = 1536;
-constexpr int PF_U = 4;  // region slots per thread in flight in the pane scan
+#ifndef FW_PF_U
+#define FW_PF_U 4
+#endif
+#ifndef FW_PF_ABL
+#define FW_PF_ABL 0
+#endif
+#ifndef FW_PF_THREADS
+#define FW_PF_THREADS 1024
+#endif
+#ifndef FW_PF_SLOTS_LOG2
+#define FW_PF_SLOTS_LOG2 11
+#endif
+constexpr int PF_THREADS = FW_PF_THREADS;
+constexpr int PF_SLOTS = 1 << FW_PF_SLOTS_LOG2;
+constexpr int PF_LIMIT = PF_SLOTS * 3 / 4;
+constexpr int PF_U = FW_PF_U;  // region slots per thread in flight in the pane scan
 struct PaneLds {
   uint32_t tag[PF_SLOTS];  // 0 empty, 1 being claimed, 2 full
   uint32_t sel[PF_SLOTS];  // minBy / maxBy: region slot of the pane holding the window's selected element
@@ -4357,7 +4387,7 @@ __device__ __forceinline__ uint32_t pf_hash(int64_t key) { return (uint32_t)(fmi
 // (pane: the entry's region slot; ent: the region's entries, read back by a minBy / maxBy selection)
 __device__ __forceinline__ bool pf_upsert(const DevCfg& c, PaneLds& L, const Entry& e, uint32_t h, uint32_t pane,
                                           const Entry* __restrict__ ent) {
-  uint32_t s = (h * 0x9E3779B1u) >> (32 - 11);  // PF_SLOTS = 2^11
+  uint32_t s = (h * 0x9E3779B1u) >> (32 - FW_PF_SLOTS_LOG2);
   for (int i = 0, spin = 0; i < PF_SLOTS;) {
     if (++spin > (1 << 24)) return false;  // a slot never published: cannot happen; the pass reports overflow
     const uint32_t t = __hip_atomic_load(&L.tag[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -4447,17 +4477,26 @@ __global__ __launch_bounds__(PF_THREADS) void k_fire_panes(DevCfg c, int64_t wm,
     bool over = false;
     // PF_U slots per thread per step: their state words, then their live entries, are loaded before
     // any is used, so each thread keeps PF_U loads in flight (one at a time left the scan latency-bound)
+    // (the next step's state words are loaded with this step's entries: one round trip per step)
+    uint32_t wn[PF_U];
+#pragma unroll
+    for (int u = 0; u < PF_U; u++) {
+      const uint32_t s = u * PF_THREADS + tid;
+      wn[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
+    }
     for (uint32_t s0 = 0; s0 < R; s0 += PF_THREADS * PF_U) {
       uint32_t w[PF_U];
 #pragma unroll
-      for (int u = 0; u < PF_U; u++) {
-        const uint32_t s = s0 + u * PF_THREADS + tid;
-        w[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
-      }
+      for (int u = 0; u < PF_U; u++) w[u] = wn[u];
       Entry eu[PF_U];
 #pragma unroll
       for (int u = 0; u < PF_U; u++)
         if (st_kind(w[u]) == SLOT_LIVE) eu[u] = rx.ent[s0 + u * PF_THREADS + tid];
+#pragma unroll
+      for (int u = 0; u < PF_U; u++) {
+        const uint32_t s = s0 + (uint32_t)(PF_THREADS * PF_U) + u * PF_THREADS + tid;
+        wn[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
+      }
 #pragma unroll
       for (int u = 0; u < PF_U; u++) {
       const uint32_t s = s0 + u * PF_THREADS + tid;
@@ -4478,7 +4517,11 @@ __global__ __launch_bounds__(PF_THREADS) void k_fire_panes(DevCfg c, int64_t wm,
       if (!forming) continue;
       if (lo_e <= E && E <= hi_e) {
         const uint32_t h = pf_hash(e.key);
+#if FW_PF_ABL & 1  // (timing ablation only: no window formed)
+        asm volatile("" ::"v"(h), "v"(e.cnt), "v"(e.sum));
+#else
         if (!over && (uint64_t)h >= lo && (uint64_t)h < lo + width && !pf_upsert(c, L, e, h, s, rx.ent)) over = true;
+#endif
       }
       const int64_t cand = max(lo_e, E + c.slide);
       if (E < LMAX - c.slide && cand <= hi_e) en = min(en, cand);
