@@ -333,8 +333,9 @@ def test_gpu_zipf_hot_keys():
     assert_rows_equal(g, r)
 
 
+@pytest.mark.parametrize("async_input", [False, True], ids=["host-push", "async-device-push"])
 @pytest.mark.parametrize("value_type", ["i64", "f64"])
-def test_gpu_single_pass_scatter_fallbacks(value_type):
+def test_gpu_single_pass_scatter_fallbacks(value_type, async_input):
     # dense tumbling windows take the single-pass scatter (each partition's run reserved piece by piece, no
     # histogram); a batch it cannot take goes through classify / scan / scatter instead: one with a record whose
     # window is too far ahead for a compact word, one whose hot key overfills its partition's reserved run.  Late
@@ -349,14 +350,24 @@ def test_gpu_single_pass_scatter_fallbacks(value_type):
     k = k.copy()
     k[: len(k) * 3 // 4] = 7
     batches[4] = (k, t, v)
-    gpu = _gpu_op(**cfg, max_batch=1 << 17)
+    # (async device pushes: the batch is partitioned on the input stream, the gated classify / scan / scatter behind
+    # a failed single pass included, beside the previous batch's aggregation)
+    gpu = _gpu_op(**cfg, max_batch=1 << 17, async_input=async_input)
     ref = orc.WindowOperatorOracle(**cfg)
-    for (k, t, v), wm in zip(batches, wms):
-        gpu.process(k, t, v)
+    drained = []
+    for e, ((k, t, v), wm) in enumerate(zip(batches, wms)):
+        if async_input:
+            import torch
+            gpu.process_batch(*(torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (k, t, v)))
+            gpu.advance_watermark(wm, wait=False)
+            drained.append(gpu.drain_rows(e))
+        else:
+            gpu.process(k, t, v)
+            gpu.watermark(wm)
         ref.process(k, t, v)
-        gpu.watermark(wm)
         ref.watermark(wm)
-    g, r, gl, rl = gpu.rows(), ref.rows(), gpu.late_dropped, ref.late_dropped
+    g = np.concatenate(drained) if async_input else gpu.rows()
+    r, gl, rl = ref.rows(), gpu.late_dropped, ref.late_dropped
     st = gpu.stats()
     gpu.close()
     assert_rows_equal(g, r, _VT[value_type])
