@@ -303,6 +303,10 @@ __device__ __forceinline__ void side_one(const DevSide& sd, Status* st, int64_t 
 // accumulate one value (AggregateFunction.add of the built-in count/sum/min/max)
 // (FW_AGG_FIRST: mx takes ~ordinal `fo` of the record, so the max keeps the first element's ordinal)
 __device__ __forceinline__ void acc_add(const DevCfg& c, Entry& e, int64_t v, int64_t fo) {
+  if (c.agg == FW_AGG_HLL) {  // the registers are the accumulator; the row keeps the count (as lds_acc's LDS_CNT_ONLY)
+    e.cnt += 1;
+    return;
+  }
   if (agg_by(c.agg)) {
     const int64_t k = by_key(c.agg, c.vtype, v);
     if (e.cnt == 0 || by_less(k, fo, e.mn, e.mx)) {
@@ -1321,7 +1325,14 @@ __device__ __forceinline__ void lds_by(AggLds& L, int target, int agg, int vtype
     cur = prev;
   }
 }
+// first == LDS_CNT_ONLY: the count alone (HyperLogLog: its rows are the registers' estimate, the entry's count the
+// only accumulator field they show)
+constexpr int LDS_CNT_ONLY = -1;
 __device__ __forceinline__ void lds_acc(AggLds& L, int target, int vtype, int64_t v, int64_t fo, int first) {
+  if (first == LDS_CNT_ONLY) {
+    atomicAdd(&L.cnt[target], 1u);
+    return;
+  }
   if (agg_by(first)) {
     atomicAdd(&L.cnt[target], 1u);
     lds_by(L, target, first, vtype, by_key(first, vtype, v), fo - L.byb);
@@ -2074,7 +2085,7 @@ __device__ __forceinline__ void agg_walk_lm(const DevCfg& c, AggLds& L, int64_t*
           up = false;
       }
     } else {
-      up = lds_upsert_batch<RPT>(L, c.vtype, k, t, v, o, FIRST ? c.agg : 0, m);
+      up = lds_upsert_batch<RPT>(L, c.vtype, k, t, v, o, FIRST ? c.agg : c.agg == FW_AGG_HLL ? LDS_CNT_ONLY : 0, m);
     }
     if (!up) {
       dm = m;
@@ -2400,7 +2411,8 @@ __global__ __launch_bounds__(FW_AGG_THREADS, GATHER ? FW_GATHER_WAVES : SESS ? F
           if constexpr (SESS)
             in = lds_session_upsert(L, sess_end, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j], o[j], FIRST ? c.agg : 0);
           else
-            in = lds_upsert(L, c.vtype, k[j], jsub(t[j], (int64_t)wi * c.slide), v[j], c.diag, o[j], FIRST ? c.agg : 0);
+            in = lds_upsert(L, c.vtype, k[j], jsub(t[j], (int64_t)wi * c.slide), v[j], c.diag, o[j],
+                            FIRST ? c.agg : c.agg == FW_AGG_HLL ? LDS_CNT_ONLY : 0);
           if (!in) {
             failed = true;
             rj = j;

@@ -63,7 +63,9 @@ extern "C" {
 #define FW_AGG_HLL 1               /* HyperLogLog distinct count of the value column read as a u64 item
                                       (definition in DESIGN.md §HLL): fired rows carry
                                       count, sum = estimate (f64 bits), min = zero registers, max = the
-                                      low 64 bits of sum_j 2^(65-p-M[j]).  Tumbling and sliding windows
+                                      low 64 bits of sum_j 2^(65-p-M[j]); the accumulator is the registers
+                                      and the count (a snapshot row's sum / min / max are 0 / Long.MAX_VALUE
+                                      / Long.MIN_VALUE, not value statistics).  Tumbling and sliding windows
                                       (one register block per window), any allowed lateness (a window fires
                                       at maxTimestamp and keeps its registers until its cleanup time); not
                                       session windows (FW_ERR_UNSUPPORTED); expected_entries sizes the
