@@ -2827,6 +2827,29 @@ __global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, 
   }
 }
 
+// a fired HLL row from its marked chunks' sums (lo, hi: sum_j 2^(65-p-M[j]) over them, 128 bits; zeros; touched
+// chunks): the unmarked chunks are 16 zero registers each, 2^rmax apiece (rmax <= 61: the product fits 128 bits)
+__device__ void hll_row_out(const DevCfg& c, const DevRows& out, uint64_t row, uint64_t lo, uint64_t hi, uint32_t zeros,
+                            uint32_t touched, bool release, int64_t stack_slot, uint64_t blk) {
+  const int p = c.hll_p, rmax = 65 - p;
+  const int64_t m = (int64_t)1 << p;
+  const int32_t nq = (int32_t)(m / 16);
+  const uint64_t un = (uint64_t)(nq - (int32_t)touched) * 16u;
+  const uint64_t ulo = un << rmax, uhi = rmax ? un >> (64 - rmax) : 0ull;
+  const uint64_t t = lo + ulo;
+  hi = hi + uhi + (t < lo ? 1ull : 0ull);
+  lo = t;
+  zeros += (uint32_t)un;
+  const double sd = (double)hi * 18446744073709551616.0 + (double)lo;
+  const double md = (double)m;
+  const double alpha = m == 16 ? 0.673 : m == 32 ? 0.697 : m == 64 ? 0.709 : 0.7213 / (1.0 + 1.079 / md);
+  const double raw = (alpha * md * md) * ldexp(1.0, rmax) / sd;
+  const double est = (raw <= 2.5 * md && zeros > 0) ? md * log(md / (double)zeros) : raw;
+  out.sum[row] = __double_as_longlong(est);
+  out.mn[row] = (int64_t)zeros;
+  out.mx[row] = (int64_t)lo;
+  if (release) c.pool_free[stack_slot] = (uint32_t)blk;  // zeroed before the next kernel can hand it out
+}
 // ---- K_fire: watermark.  Regions with next_timer <= wm emit and are rebuilt into the other buffer.
 // Pass 1 decides every slot, re-inserts the survivors into the other buffer and counts the fired
 // rows; one reservation per workgroup in the output; pass 2 re-decides and writes the rows.
@@ -2934,23 +2957,98 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, in
     zeros += __shfl_xor(zeros, o, 64);
     touched += __shfl_xor(touched, o, 64);
   }
-  if (lane == 0) {
-    // the unmarked chunks: 16 zero registers each, 2^rmax apiece (rmax <= 61: the product fits 128 bits)
-    const uint64_t un = (uint64_t)(nq - (int32_t)touched) * 16u;
-    const uint64_t ulo = un << rmax, uhi = rmax ? un >> (64 - rmax) : 0ull;
-    const uint64_t t = lo + ulo;
-    hi = hi + uhi + (t < lo ? 1ull : 0ull);
+  if (lane == 0) hll_row_out(c, out, row, lo, hi, zeros, touched, release, stack_slot, blk);
+}
+// four rows a wave, sixteen lanes each (p <= 14: at most 32 bitmap words, two per lane): a row with at most 16 marked
+// chunks (most windows of a Zipf stream's tail keys) is read in two round trips by its sixteen lanes, four rows in
+// flight; a fuller one is finished by the whole wave afterwards (hll_finish).  rows: the wave's four rows r,
+// r + stride, ...; ri: their free-stack slots (out.mx, read before any of them is overwritten)
+__device__ void hll_finish4(const DevCfg& c, const DevRows& out, uint64_t r, uint64_t stride, uint64_t end, int hl_sb,
+                            uint32_t* ids) {
+  const int lane = __lane_id(), g = lane >> 4, gl = lane & 15;
+  const int p = c.hll_p, rmax = 65 - p;
+  const int32_t nq = (int32_t)(((int64_t)1 << p) / 16), nw = (nq + 31) / 32;
+  const uint64_t row = r + (uint64_t)g * stride;
+  const bool valid = row < end;
+  const int64_t ri = valid ? out.mx[row] : -1;
+  const bool release = ri >= 0;
+  const int64_t slot = release ? hl_sb + ri : -1;
+  const uint64_t blk = valid ? (uint64_t)out.mn[row] : 0;
+  uint8_t* base = c.pool + blk * (uint64_t)c.pool_bytes;
+  uint32_t* bits = reinterpret_cast<uint32_t*>(base);
+  uint4* q = reinterpret_cast<uint4*>(base + hll_hdr_bytes(p));
+  const uint32_t w0 = valid && gl < nw ? bits[gl] : 0u, w1 = valid && gl + 16 < nw ? bits[gl + 16] : 0u;
+  const uint32_t cnt = (uint32_t)(__popc(w0) + __popc(w1));
+  uint32_t x = cnt;  // inclusive prefix over the row's sixteen lanes
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, o, 16);
+    if (gl >= o) x += y;
+  }
+  const uint32_t tot = (uint32_t)__shfl((int)x, 15, 16);
+  const bool small = valid && tot <= 16;
+  uint64_t s = 0, sh = 0;
+  uint32_t zeros = 0, touched = 0;
+  if (small) {
+    uint32_t k = x - cnt;
+    uint32_t word = w0;
+    while (word) {
+      const int b = __ffs(word) - 1;
+      word &= word - 1;
+      ids[g * 16 + k++] = (uint32_t)(gl * 32 + b);
+    }
+    word = w1;
+    while (word) {
+      const int b = __ffs(word) - 1;
+      word &= word - 1;
+      ids[g * 16 + k++] = (uint32_t)((gl + 16) * 32 + b);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  if (small && (uint32_t)gl < tot) {
+    const uint32_t j = ids[g * 16 + gl];
+    const uint4 v = q[j];
+    touched = 1;
+    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++)
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const uint32_t rr = (ws[kk] >> (8 * b)) & 0xffu;
+        const uint64_t t = s + (1ull << (rmax - (int)rr));
+        sh += t < s;
+        s = t;
+        zeros += rr == 0;
+      }
+    if (release) q[j] = make_uint4(0, 0, 0, 0);
+  }
+  if (small && release) {
+    if (gl < nw) bits[gl] = 0u;
+    if (gl + 16 < nw) bits[gl + 16] = 0u;
+  }
+  uint64_t hi = sh, lo = s;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) {  // (within the row's sixteen lanes)
+    const uint64_t lo2 = __shfl_xor(lo, o, 16), hi2 = __shfl_xor(hi, o, 16);
+    const uint64_t t = lo + lo2;
+    hi = hi + hi2 + (t < lo ? 1ull : 0ull);
     lo = t;
-    zeros += (uint32_t)un;
-    const double sd = (double)hi * 18446744073709551616.0 + (double)lo;
-    const double md = (double)m;
-    const double alpha = m == 16 ? 0.673 : m == 32 ? 0.697 : m == 64 ? 0.709 : 0.7213 / (1.0 + 1.079 / md);
-    const double raw = (alpha * md * md) * ldexp(1.0, rmax) / sd;
-    const double est = (raw <= 2.5 * md && zeros > 0) ? md * log(md / (double)zeros) : raw;
-    out.sum[row] = __double_as_longlong(est);
-    out.mn[row] = (int64_t)zeros;
-    out.mx[row] = (int64_t)lo;
-    if (release) c.pool_free[stack_slot] = (uint32_t)blk;  // zeroed before the next kernel can hand it out
+    zeros += __shfl_xor(zeros, o, 16);
+    touched += __shfl_xor(touched, o, 16);
+  }
+  if (small && gl == 0) hll_row_out(c, out, row, lo, hi, zeros, touched, release, slot, blk);
+  __builtin_amdgcn_wave_barrier();  // (ids is the full-wave finishes' and the next rows')
+  // the fuller rows, one after another by the whole wave
+  const uint64_t full = __ballot(valid && !small && gl == 0);
+#pragma unroll
+  for (int gg = 0; gg < 4; gg++) {
+    if (!((full >> (gg * 16)) & 1ull)) continue;
+    const uint64_t rw = r + (uint64_t)gg * stride;
+    const int64_t sl = __shfl(slot, gg * 16, 64);
+    const uint64_t bk = __shfl(blk, gg * 16, 64);
+    (void)bk;
+    hll_finish(c, out, rw, sl, ids);
   }
 }
 // the same estimate by one thread, the block kept (a late firing of the ordered path under allowed lateness)
@@ -4332,9 +4430,15 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
     const uint64_t end = min((unsigned long long)out.cap, base_s + total);
     if (c.agg == FW_AGG_HLL) {
       __shared__ uint32_t hl_ids[FW_FIRE_THREADS];  // 64 chunk ids per wave (hll_finish)
-      for (uint64_t r = base_s + (threadIdx.x >> 6); r < end; r += blockDim.x >> 6) {
-        const int64_t ri = out.mx[r];  // (every lane reads it before lane 0 overwrites it)
-        hll_finish(c, out, r, ri < 0 ? -1 : hl_sb + ri, hl_ids + (threadIdx.x & ~63u));
+      const uint64_t nwv = blockDim.x >> 6;
+      if (c.hll_p <= 14) {  // (at most 32 bitmap words: four rows a wave)
+        for (uint64_t r = base_s + (threadIdx.x >> 6); r < end; r += 4 * nwv)
+          hll_finish4(c, out, r, nwv, end, hl_sb, hl_ids + (threadIdx.x & ~63u));
+      } else {
+        for (uint64_t r = base_s + (threadIdx.x >> 6); r < end; r += nwv) {
+          const int64_t ri = out.mx[r];  // (every lane reads it before lane 0 overwrites it)
+          hll_finish(c, out, r, ri < 0 ? -1 : hl_sb + ri, hl_ids + (threadIdx.x & ~63u));
+        }
       }
     } else {
       __shared__ unsigned long long cent_s;
