@@ -80,6 +80,7 @@
 // batch (the aggregate's LDS copy of a partition's row of the runs table).
 #define FW_GTILE 8192
 #define FW_GMAX_P 2048
+#define FW_STAGED_MAX_P 4096  // LDS-staged offset scatter (k_scatter_staged): up to this many partitions
 #define FW_GMAX_T 2048
 #define FW_REGROUP_THREADS 512
 #define FW_REGROUP_CHUNK 16384  // records per regroup workgroup (a hot partition takes several)
