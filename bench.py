@@ -43,6 +43,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md §Chip-level parameters
+XGMI_LINK_GBS = 153.0  # one xGMI link per peer pair, per direction
 
 # SURVEY.md §8d workloads.  c2 is BASELINE.json configs[1] (the default, the headline line).
 PRESETS = {
@@ -165,9 +166,56 @@ def wordcount_stream(first, n):
     return keys, ts, np.ones(n, dtype=np.int64), hashes[keys]
 
 
+def job_cpu_share():
+    """The host cores this job may use: the CPU affinity mask, capped by OMP_NUM_THREADS when the box sets it (the
+    GPU box shows all of its cores to every job and declares the job's share there: 16 for one GPU)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and 0 < int(omp) < aff:
+        return int(omp), f"OMP_NUM_THREADS={omp} (the job's CPU share; affinity mask {aff} cores)"
+    return aff, f"the CPU affinity mask ({aff} cores)"
+
+
+def launch_ranks(args, argv):
+    """`--gpus N` (N > 1) without a torch.distributed launcher around it: start one rank per GPU with
+    `python -m torch.distributed.run` (rendezvous on 127.0.0.1, one process per GPU, RCCL between them) and pass
+    its exit status on; rank 0 prints the JSON line.  This process never touches the GPU (counting devices does not
+    initialise HIP on this image) and never exec()s: the ranks are children."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + \
+        [a for a in argv if a != "--dry-run-launch"]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (the host driver has no legacy IPC)
+    env["MASTER_ADDR"] = "127.0.0.1"
+    if args.dry_run_launch:
+        print(json.dumps({"launch": cmd, "nproc": args.gpus,
+                          "env": {k: env[k] for k in ("HSA_ENABLE_IPC_MODE_LEGACY", "MASTER_ADDR")}}), flush=True)
+        return 0
+    import torch
+    have = torch.cuda.device_count()
+    need = 1 if args.rehearse_gloo else args.gpus
+    if have < need:
+        print(f"bench.py: --gpus {args.gpus} needs {need} visible GPUs, this node shows {have}", file=sys.stderr,
+              flush=True)
+        return 2
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node, one rank each (default 1; N > 1 starts N ranks with torch.distributed.run "
+                         "unless already launched by it)")
+    ap.add_argument("--dry-run-launch", action="store_true",
+                    help="with --gpus N > 1: print the rank launcher's command and environment, start nothing")
     ap.add_argument("--steps", type=int, default=64)  # 64 x 2^24 = 2^30 records (SURVEY §8d)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--workload", choices=sorted(PRESETS), default="c2")
@@ -186,8 +234,8 @@ def main():
                     help="c3: do not extend the warmup to one window size of event time")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--zipf", type=float, default=None, help="Zipf exponent of the keys (0 = uniform)")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="CPU baseline subtasks (16 = this job's CPU share of the GPU box)")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU baseline subtasks (default: the job's CPU share, job_cpu_share())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-fed-steps", type=int, default=3, help="steps of the host-fed leg (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
@@ -197,9 +245,17 @@ def main():
     ap.add_argument("--combine", action="store_true",
                     help="pre-shuffle combining (SURVEY §8e): partial accumulators instead of records cross the "
                          "exchange (C2 only: tumbling count/sum/min/max)")
+    ap.add_argument("--rehearse-gloo", action="store_true",
+                    help="N > 1 on ONE GPU: every rank on cuda:0 and the Python exchange over gloo (exercises the "
+                         "multi-rank bench path; RCCL cannot put two ranks on one GPU)")
     ap.add_argument("--sync-input", action="store_true",
                     help="partition each batch on the operator's own stream (no overlap with the previous batch)")
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    if args.gpus is not None and env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
     preset = PRESETS[args.workload]
     w = args.workload
     for name in ("keys", "rate", "bound", "jitter", "cpu_sample", "batch"):
@@ -222,11 +278,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    gloo = world > 1 and args.rehearse_gloo
+    if gloo:  # rehearsal of the N > 1 path on one GPU: every rank on cuda:0, the Python exchange over gloo
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    coll_dev = torch.device("cpu") if gloo else dev  # where the bench's own collectives' tensors live
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from flink_amd import (CountSumMinMax, EventTimeSessionWindows, HyperLogLog, SlidingEventTimeWindows, TDigest,
                            TumblingEventTimeWindows)
@@ -257,7 +320,7 @@ def main():
                            max_batch=args.batch if world == 1 else 2 * args.batch,
                            sub_partitions=args.sub_partitions, async_input=not args.sync_input)
     nx = None
-    if world > 1:
+    if world > 1 and not gloo:
         # the keyBy exchange a JNI host calls: fw_keyby_push_device over the library's own RCCL communicator
         # (route, count all-to-all, per-peer ncclSend / ncclRecv, push), rank 0's id handed to the others
         import torch.distributed as dist
@@ -321,6 +384,10 @@ def main():
             wm = nx.push_combined(comb, k, t, v, wm)
         elif nx is not None:  # route, exchange, push (fw_keyby_push_device); wm = min over the subtasks
             wm = nx.push(k, t, v, wm, h)
+        elif gloo:  # rehearsal: fw_route_device + gloo all-to-alls through host memory (KeyGroupExchange)
+            got = exch.exchange(k, t, v, h)
+            wm = exch.combine_watermark(wm)
+            op.process_batch(*got)
         elif cx is not None:  # world 1: combine and merge through the Python exchange
             wm = cx.push(op, k, t, v, wm)
         else:
@@ -354,6 +421,13 @@ def main():
         L.fw_profile(op._h, mask)
         L.fw_profile_read(op._h, None, None, 1)
     st0 = op.stats()
+    def exchange_stats():
+        if nx is not None:
+            return nx.stats()
+        return {"world": world, "rank": rank, "bytes_sent": exch.bytes_sent, "items_sent": exch.items_sent,
+                "bytes_received": exch.bytes_received, "recv_reallocs": 0}
+
+    xs0 = exchange_stats() if world > 1 else None
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -365,11 +439,33 @@ def main():
     elapsed = time.perf_counter() - t0
     st1 = op.stats()
 
+    exchange = None
     if world > 1:
         import torch.distributed as dist
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+        xs1 = exchange_stats()
+        sent = [xs1[f] - xs0[f] for f in ("bytes_sent", "items_sent", "bytes_received", "recv_reallocs")]
+        allr = [torch.zeros(4, dtype=torch.float64, device=coll_dev) for _ in range(world)]
+        dist.all_gather(allr, torch.tensor(sent, dtype=torch.float64, device=coll_dev))
+        allr = [[float(x) for x in r.tolist()] for r in allr]
+        total_sent = sum(r[0] for r in allr)
+        xgmi_peak = world * (world - 1) * XGMI_LINK_GBS * 1e9  # G (G-1) links of 153 GB/s
+        exchange = {"impl": ("fw_keyby_push_device" + ("/combine" if comb is not None else "") +
+                             " (RCCL: count all-to-all + watermark MIN + batch SUM, grouped per-peer "
+                             "ncclSend/ncclRecv)") if nx is not None else
+                            "REHEARSAL: fw_route_device + torch.distributed gloo all-to-alls, every rank on cuda:0 "
+                            "(not a multi-GPU measurement)",
+                    "rccl_ranks": int(xs1["world"]) if nx is not None else None, "rccl_rank0": int(xs1["rank"]),
+                    "bytes_sent_per_rank": [int(r[0]) for r in allr],
+                    "items_sent_per_rank": [int(r[1]) for r in allr],
+                    "bytes_received_per_rank": [int(r[2]) for r in allr],
+                    "recv_reallocs_in_timed_region": int(sum(r[3] for r in allr)),
+                    "shuffled_bytes_per_s": round(total_sent / elapsed, 1),
+                    "xgmi_frac": round(total_sent / elapsed / xgmi_peak, 4),
+                    "xgmi_basis": f"bytes sent to other ranks in the timed region / time / (G (G-1) x "
+                                  f"{XGMI_LINK_GBS:.0f} GB/s), SURVEY §8d"}
     records = args.batch * world * args.steps
     value = records / elapsed
     fired = st1["fired_rows_total"] - st0["fired_rows_total"]
@@ -478,6 +574,9 @@ def main():
             "value": round(value, 1), "unit": "records/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
+            **({"rccl_ranks": exchange["rccl_ranks"]} if exchange else {}),
+            **({"rehearsal": "gloo, all ranks on one GPU: checks the N > 1 code path, not a scaling number"}
+               if gloo else {}),
             "dtype": "f64" if tdig else "int64", "data": "synthetic (splitmix64 counter stream)",
             "config": {"workload": preset["workload"],
                        "records_per_step_per_gpu": args.batch, "keys": args.keys,
@@ -489,12 +588,12 @@ def main():
                        "records_per_event_second": args.rate, "watermark_bound_ms": args.bound,
                        "max_parallelism": 128, "parallelism": f"keygroup{world}",
                        "sink": "discarding (fired rows materialised in HBM)",
-                       **({"exchange": "fw_keyby_push_device" + ("/combine" if comb is not None else "") +
-                           " (RCCL count all-to-all, per-peer ncclSend/ncclRecv)"} if nx is not None else {}),
+
                        **({"combine": "pre-shuffle partial accumulators (SURVEY §8e)"} if cx is not None else {})},
             "roofline": roofline,
             "path_roofline": {"b_alg_bytes_per_record": round(balg, 3), "frac": round(path_frac, 4),
                               "fired_rows": int(fired)},
+            **({"exchange": exchange} if exchange else {}),
             "host_fed": host_fed,
             **({"count_window_gpu": count_gpu} if count_gpu else {}),
             "cpu_baseline": cpu,
@@ -602,7 +701,9 @@ def cpu_baseline(args):
                           f"line's pipeline), count_window_value = countWindow(10, 5).sum(1); CPU restatement of "
                           f"WindowOperator / EvictingWindowOperator semantics (oracle/), not the Java reference "
                           f"(no JDK on the box)"}
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    share, why = job_cpu_share()
+    threads = args.cpu_threads or share
+    why = why if not args.cpu_threads else f"--cpu-threads {args.cpu_threads}"
     k, t, v = generate_host(0x5EED, 0, n, args.keys, ts_base=0, rate=args.rate, jitter=args.jitter, zipf_s=args.zipf)
     if args.workload == "c5t":
         v = v.astype(np.float64)
@@ -625,9 +726,10 @@ def cpu_baseline(args):
     orc.run_parallel(cfg, k, t, v, batch, np.array(wms), 128, threads)
     dt = time.perf_counter() - t0
     return {"value": round(n / dt, 1), "unit": "records/s", "cores": threads, "kind": "port", "cpu_model": model,
-            "nproc": nproc, "parallelism": threads,
+            "nproc": nproc, "parallelism": threads, "parallelism_basis": why,
             "sample": f"first {n} records of the same {args.workload.upper()} stream, {threads} subtasks (threads; "
-                      f"p = this job's CPU share of the box, nproc = {nproc}), watermark every {batch} records; CPU "
+                      f"p = the host cores this job may use: {why}; nproc = {nproc}), watermark every {batch} "
+                      f"records; CPU "
                       f"restatement of WindowOperator semantics (oracle/, C++ -O2), not the Java reference (no JDK "
                       f"on the box)"}
 

@@ -72,6 +72,16 @@ FW_WIRE_LONG, FW_WIRE_INT, FW_WIRE_DOUBLE, FW_WIRE_SHORT, FW_WIRE_BYTE, FW_WIRE_
  FW_ROLE_MAX) = range(9)
 
 
+class FwCommStats(ctypes.Structure):
+    _fields_ = [("world", ctypes.c_int32), ("rank", ctypes.c_int32)] + [(n, ctypes.c_int64) for n in (
+        "batches", "items_sent", "items_received", "bytes_sent", "bytes_received", "recv_reallocs", "recv_capacity")]
+
+
+class FwExchangePlan(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in ("send_total", "recv_total", "items_sent", "items_received",
+                                               "recv_bound")]
+
+
 class FwWireLayout(ctypes.Structure):
     _fields_ = [("nfields", ctypes.c_int32), ("kind", ctypes.c_int32 * 8), ("role", ctypes.c_int32 * 8)]
 
@@ -150,6 +160,9 @@ SIGNATURES = {
     "fw_comm_init": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(VP)]),
     "fw_comm_destroy": (None, [VP]),
     "fw_keyby_push_device": (ctypes.c_int, [VP, VP, VP, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, I64P]),
+    "fw_comm_get_stats": (ctypes.c_int, [VP, ctypes.POINTER(FwCommStats)]),
+    "fw_exchange_plan": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, I64P, I64P, I64P,
+                                        ctypes.POINTER(FwExchangePlan)]),
     "fw_wire_create": (ctypes.c_int, [ctypes.POINTER(FwWireLayout), ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(VP)]),
     "fw_wire_destroy": (None, [VP]),
     "fw_wire_last_error": (ctypes.c_char_p, [VP]),

@@ -6090,7 +6090,7 @@ __global__ __launch_bounds__(256) void k_generate(uint64_t seed, int64_t first, 
 // ============================================================================== launchers
 namespace fwdev {
 
-ExtTiming g_ext{};
+thread_local ExtTiming g_ext{};  // per host thread: operators timed from different threads do not share it
 // a kind's main kernel: with the dispatch's own start / stop events when fw_profile asked for them (g_ext)
 #define FW_LAUNCH_MAIN(kern, grid, block, lds, s, ...)                                                        \
   do {                                                                                                     \

@@ -375,7 +375,7 @@ struct ExtTiming {
   hipEvent_t a, b;
   bool used;
 };
-extern ExtTiming g_ext;
+extern thread_local ExtTiming g_ext;
 void launch_classify_hist(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int32_t* kh,
                           int64_t n, int32_t T, uint32_t* hist, Status* st, hipStream_t_ s,
                           const uint32_t* rsv = nullptr);

@@ -1888,8 +1888,9 @@ struct fw_comm {
   int32_t* sh = nullptr;
   void* scratch = nullptr;
   int64_t scratch_bytes = 0;
-  int64_t* counts = nullptr;                              // [2 world + 2]: send counts, recv counts, wm in/out
+  int64_t* counts = nullptr;  // [2 world + 4]: send counts, recv counts, wm in / min, batch size in / sum
   int64_t* h_counts = nullptr;                            // pinned host copy
+  fw_comm_stats stats{};                                   // exchange counters (fw_comm_get_stats)
   int64_t pcap = 0;                                       // combining: partials the send / receive columns hold
   int64_t* ps[6] = {};                                    // send partials (key, start, cnt, sum, min, max)
   int64_t* pr[6] = {};                                    // received partials
@@ -1945,6 +1946,37 @@ int comm_reserve_recv(fw_op* op, fw_comm* c, int64_t need) {
     ncclResult_t _r = (expr);                                                                               \
     if (_r != ncclSuccess) return set_err(op, FW_ERR_HIP, "%s failed: %s", #expr, ncclGetErrorString(_r)); \
   } while (0)
+// inside ncclGroupStart ... ncclGroupEnd: a failed enqueue still closes the group before returning, so the
+// communicator's next collective does not run inside a half-built group
+#define NCCL_IN_GROUP(op, expr)                                                                                \
+  do {                                                                                                         \
+    ncclResult_t _r = (expr);                                                                                  \
+    if (_r != ncclSuccess) {                                                                                   \
+      (void)ncclGroupEnd();                                                                                    \
+      return set_err(op, FW_ERR_HIP, "%s failed: %s", #expr, ncclGetErrorString(_r));                          \
+    }                                                                                                          \
+  } while (0)
+// the counts round: per-peer counts all-to-all, the watermark's minimum and the batch sizes' sum (the bound on
+// what any subtask can receive in this batch) over all subtasks, one group on stream s
+int comm_counts_round(fw_op* op, fw_comm* c, hipStream_t s) {
+  const int W = c->world;
+  NCCL_OR_RETURN(op, ncclGroupStart());
+  NCCL_IN_GROUP(op, ncclAllToAll(c->counts, c->counts + W, 1, ncclInt64, c->nc, s));
+  NCCL_IN_GROUP(op, ncclAllReduce(c->counts + 2 * W, c->counts + 2 * W + 1, 1, ncclInt64, ncclMin, c->nc, s));
+  NCCL_IN_GROUP(op, ncclAllReduce(c->counts + 2 * W + 2, c->counts + 2 * W + 3, 1, ncclInt64, ncclSum, c->nc, s));
+  NCCL_OR_RETURN(op, ncclGroupEnd());
+  HIP_OR_RETURN(op, hipMemcpyAsync(c->h_counts, c->counts, (2 * W + 4) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HIP_OR_RETURN(op, hipStreamSynchronize(s));
+  return FW_OK;
+}
+// the receive-side bookkeeping of one batch from the counts round (fw_exchange_plan) plus the counters
+void comm_account(fw_comm* c, const fw_exchange_plan_t& pl, int64_t bytes_per_item) {
+  c->stats.batches++;
+  c->stats.items_sent += pl.items_sent;
+  c->stats.items_received += pl.items_received;
+  c->stats.bytes_sent += pl.items_sent * bytes_per_item;
+  c->stats.bytes_received += pl.items_received * bytes_per_item;
+}
 }  // namespace
 extern "C" {
 
@@ -1966,8 +1998,8 @@ int fw_comm_init(const void* id128, int32_t world, int32_t rank, int32_t device,
   c->device = device;
   ncclUniqueId id;
   memcpy(&id, id128, sizeof id);
-  if (ncclCommInitRank(&c->nc, world, id, rank) != ncclSuccess || dmalloc(&c->counts, 2 * (size_t)world + 2) != hipSuccess ||
-      hipHostMalloc((void**)&c->h_counts, (2 * (size_t)world + 2) * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
+  if (ncclCommInitRank(&c->nc, world, id, rank) != ncclSuccess || dmalloc(&c->counts, 2 * (size_t)world + 4) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_counts, (2 * (size_t)world + 4) * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
     fw_comm_destroy(c);
     return FW_ERR_HIP;
   }
@@ -1988,6 +2020,40 @@ void fw_comm_destroy(fw_comm* c) {
   cfree(c->scratch);
   if (c->h_counts) (void)hipHostFree(c->h_counts);
   delete c;
+}
+
+int fw_exchange_plan(int32_t world, int32_t rank, const int64_t* counts, int64_t* send_off, int64_t* recv_off,
+                     fw_exchange_plan_t* out) {
+  if (world < 1 || rank < 0 || rank >= world || !counts || !send_off || !recv_off || !out) return FW_ERR_ARG;
+  const int W = world;
+  *out = fw_exchange_plan_t{};
+  send_off[0] = recv_off[0] = 0;
+  for (int p = 0; p < W; p++) {
+    if (counts[p] < 0 || counts[W + p] < 0) return FW_ERR_STATE;
+    send_off[p + 1] = send_off[p] + counts[p];
+    recv_off[p + 1] = recv_off[p] + counts[W + p];
+    if (p != rank) {
+      out->items_sent += counts[p];
+      out->items_received += counts[W + p];
+    }
+  }
+  out->send_total = send_off[W];
+  out->recv_total = recv_off[W];
+  out->recv_bound = counts[2 * W + 3];
+  // what a subtask receives is part of the batch of all subtasks; the own share is sent to itself
+  if (out->recv_total > out->recv_bound || counts[rank] != counts[W + rank]) return FW_ERR_STATE;
+  return FW_OK;
+}
+
+int fw_comm_get_stats(fw_comm* c, fw_comm_stats* out) {
+  if (!c || !out) return FW_ERR_ARG;
+  *out = c->stats;
+  int n = 0, r = 0;
+  if (ncclCommCount(c->nc, &n) != ncclSuccess || ncclCommUserRank(c->nc, &r) != ncclSuccess) return FW_ERR_HIP;
+  out->world = n;
+  out->rank = r;
+  out->recv_capacity = std::max(c->rcap, c->pcap);
+  return FW_OK;
 }
 
 int fw_keyby_push_device(fw_comm* c, fw_op* op, const int64_t* key, const int64_t* ts, const void* val,
@@ -2017,35 +2083,36 @@ int fw_keyby_push_device(fw_comm* c, fw_op* op, const int64_t* key, const int64_
                       c->st, c->sv, c->sh, c->counts, (uint32_t*)c->scratch, s);
   HIP_OR_RETURN(op, hipGetLastError());
   c->h_counts[2 * W] = local_wm;
-  HIP_OR_RETURN(op, hipMemcpyAsync(c->counts + 2 * W, c->h_counts + 2 * W, sizeof(int64_t), hipMemcpyHostToDevice, s));
-  NCCL_OR_RETURN(op, ncclGroupStart());
-  NCCL_OR_RETURN(op, ncclAllToAll(c->counts, c->counts + W, 1, ncclInt64, c->nc, s));
-  NCCL_OR_RETURN(op, ncclAllReduce(c->counts + 2 * W, c->counts + 2 * W + 1, 1, ncclInt64, ncclMin, c->nc, s));
-  NCCL_OR_RETURN(op, ncclGroupEnd());
+  c->h_counts[2 * W + 2] = n;
+  HIP_OR_RETURN(op, hipMemcpyAsync(c->counts + 2 * W, c->h_counts + 2 * W, 3 * sizeof(int64_t), hipMemcpyHostToDevice, s));
   // the receive sizes: the one host round trip of the exchange
-  HIP_OR_RETURN(op, hipMemcpyAsync(c->h_counts, c->counts, (2 * W + 2) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  HIP_OR_RETURN(op, hipStreamSynchronize(s));
+  if ((rc = comm_counts_round(op, c, s))) return rc;
   std::vector<int64_t> soff(W + 1, 0), roff(W + 1, 0);
-  for (int p = 0; p < W; p++) {
-    soff[p + 1] = soff[p] + c->h_counts[p];
-    roff[p + 1] = roff[p] + c->h_counts[W + p];
-  }
-  const int64_t total = roff[W];
-  // skew: more records may arrive than this subtask sent; only the received columns grow (s is idle here, and the
+  fw_exchange_plan_t pl;
+  if ((rc = fw_exchange_plan(W, c->rank, c->h_counts, soff.data(), roff.data(), &pl)))
+    return set_err(op, rc, "exchange: inconsistent counts round (received %lld records of a %lld-record batch)",
+                   (long long)pl.recv_total, (long long)pl.recv_bound);
+  const int64_t total = pl.recv_total;
+  // the received columns are sized for the whole batch of all subtasks (the bound from the counts round), so a
+  // skewed batch never reallocates them; they grow only when the subtasks' batches do (s is idle here, and the
   // previous batch's partitioning, the last reader of the received columns, ran on s)
-  if ((rc = comm_reserve_recv(op, c, std::max<int64_t>(total, 1)))) return rc;
+  if (pl.recv_bound > c->rcap) {
+    if ((rc = comm_reserve_recv(op, c, std::max<int64_t>(pl.recv_bound, 1)))) return rc;
+    c->stats.recv_reallocs++;
+  }
+  comm_account(c, pl, hashed ? 28 : 24);
   // the columns peer to peer: each peer pair over its own xGMI link
   NCCL_OR_RETURN(op, ncclGroupStart());
   for (int p = 0; p < W; p++) {
     const size_t sc = (size_t)c->h_counts[p], rcn = (size_t)c->h_counts[W + p];
-    NCCL_OR_RETURN(op, ncclSend(c->sk + soff[p], sc, ncclInt64, p, c->nc, s));
-    NCCL_OR_RETURN(op, ncclSend(c->st + soff[p], sc, ncclInt64, p, c->nc, s));
-    NCCL_OR_RETURN(op, ncclSend(c->sv + soff[p], sc, ncclInt64, p, c->nc, s));
-    if (hashed) NCCL_OR_RETURN(op, ncclSend(c->sh + soff[p], sc, ncclInt32, p, c->nc, s));
-    NCCL_OR_RETURN(op, ncclRecv(c->rk + roff[p], rcn, ncclInt64, p, c->nc, s));
-    NCCL_OR_RETURN(op, ncclRecv(c->rt + roff[p], rcn, ncclInt64, p, c->nc, s));
-    NCCL_OR_RETURN(op, ncclRecv(c->rv + roff[p], rcn, ncclInt64, p, c->nc, s));
-    if (hashed) NCCL_OR_RETURN(op, ncclRecv(c->rh + roff[p], rcn, ncclInt32, p, c->nc, s));
+    NCCL_IN_GROUP(op, ncclSend(c->sk + soff[p], sc, ncclInt64, p, c->nc, s));
+    NCCL_IN_GROUP(op, ncclSend(c->st + soff[p], sc, ncclInt64, p, c->nc, s));
+    NCCL_IN_GROUP(op, ncclSend(c->sv + soff[p], sc, ncclInt64, p, c->nc, s));
+    if (hashed) NCCL_IN_GROUP(op, ncclSend(c->sh + soff[p], sc, ncclInt32, p, c->nc, s));
+    NCCL_IN_GROUP(op, ncclRecv(c->rk + roff[p], rcn, ncclInt64, p, c->nc, s));
+    NCCL_IN_GROUP(op, ncclRecv(c->rt + roff[p], rcn, ncclInt64, p, c->nc, s));
+    NCCL_IN_GROUP(op, ncclRecv(c->rv + roff[p], rcn, ncclInt64, p, c->nc, s));
+    if (hashed) NCCL_IN_GROUP(op, ncclRecv(c->rh + roff[p], rcn, ncclInt32, p, c->nc, s));
   }
   NCCL_OR_RETURN(op, ncclGroupEnd());
   if (combined_wm) *combined_wm = c->h_counts[2 * W + 1];
@@ -2098,27 +2165,22 @@ int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64
   hipStream_t s = op->stream;
   for (int p = 0; p < W; p++) c->h_counts[p] = counts[p];
   c->h_counts[2 * W] = local_wm;
+  c->h_counts[2 * W + 2] = np;
   HIP_OR_RETURN(op, hipMemcpyAsync(c->counts, c->h_counts, W * sizeof(int64_t), hipMemcpyHostToDevice, s));
-  HIP_OR_RETURN(op, hipMemcpyAsync(c->counts + 2 * W, c->h_counts + 2 * W, sizeof(int64_t), hipMemcpyHostToDevice, s));
-  NCCL_OR_RETURN(op, ncclGroupStart());
-  NCCL_OR_RETURN(op, ncclAllToAll(c->counts, c->counts + W, 1, ncclInt64, c->nc, s));
-  NCCL_OR_RETURN(op, ncclAllReduce(c->counts + 2 * W, c->counts + 2 * W + 1, 1, ncclInt64, ncclMin, c->nc, s));
-  NCCL_OR_RETURN(op, ncclGroupEnd());
-  HIP_OR_RETURN(op, hipMemcpyAsync(c->h_counts, c->counts, (2 * W + 2) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  HIP_OR_RETURN(op, hipStreamSynchronize(s));
+  HIP_OR_RETURN(op, hipMemcpyAsync(c->counts + 2 * W, c->h_counts + 2 * W, 3 * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  if ((rc = comm_counts_round(op, c, s))) return rc;
   std::vector<int64_t> soff(W + 1, 0), roff(W + 1, 0);
-  for (int p = 0; p < W; p++) {
-    soff[p + 1] = soff[p] + c->h_counts[p];
-    roff[p + 1] = roff[p] + c->h_counts[W + p];
-  }
-  const int64_t total = roff[W];
-  if (total > c->pcap) {  // more partials arrive than this subtask drained: grow the receive columns
-    const int64_t cap = std::max<int64_t>(total, 2 * c->pcap);
+  fw_exchange_plan_t pl;
+  if ((rc = fw_exchange_plan(W, c->rank, c->h_counts, soff.data(), roff.data(), &pl)))
+    return set_err(op, rc, "exchange: inconsistent counts round (received %lld partials of %lld)",
+                   (long long)pl.recv_total, (long long)pl.recv_bound);
+  const int64_t total = pl.recv_total;
+  if (pl.recv_bound > c->pcap) {  // the receive columns for every partial of the batch (the bound): grow both sides
+    const int64_t cap = std::max<int64_t>(pl.recv_bound, 2 * c->pcap);
     for (int i = 0; i < 6; i++) {
       cfree(c->pr[i]);
       HIP_OR_RETURN(op, dmalloc(&c->pr[i], (size_t)cap));
     }
-    // (the send columns keep their size; pcap bounds both only after both grew)
     int64_t* ns[6] = {};
     for (int i = 0; i < 6; i++) {
       HIP_OR_RETURN(op, dmalloc(&ns[i], (size_t)cap));
@@ -2130,13 +2192,15 @@ int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64
       c->ps[i] = ns[i];
     }
     c->pcap = cap;
+    c->stats.recv_reallocs++;
   }
+  comm_account(c, pl, 48);
   NCCL_OR_RETURN(op, ncclGroupStart());
   for (int p = 0; p < W; p++) {
     const size_t sc = (size_t)c->h_counts[p], rcn = (size_t)c->h_counts[W + p];
     for (int i = 0; i < 6; i++) {
-      NCCL_OR_RETURN(op, ncclSend(c->ps[i] + soff[p], sc, ncclInt64, p, c->nc, s));
-      NCCL_OR_RETURN(op, ncclRecv(c->pr[i] + roff[p], rcn, ncclInt64, p, c->nc, s));
+      NCCL_IN_GROUP(op, ncclSend(c->ps[i] + soff[p], sc, ncclInt64, p, c->nc, s));
+      NCCL_IN_GROUP(op, ncclRecv(c->pr[i] + roff[p], rcn, ncclInt64, p, c->nc, s));
     }
   }
   NCCL_OR_RETURN(op, ncclGroupEnd());

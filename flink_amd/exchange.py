@@ -41,6 +41,19 @@ def route_device(keys, ts, vals, max_parallelism, parallelism, key_hash=None, ke
     return (ko, to, vo, ho), counts
 
 
+def exchange_plan(world, rank, counts):
+    """fw_exchange_plan: send / receive offsets and totals of one exchange round from the counts round's
+    int64[2 world + 4] (send counts, receive counts, watermark in / min, batch size in / sum).  Pure host arithmetic
+    (no GPU).  Returns (send_off, recv_off, plan dict); raises NativeError(FW_ERR_STATE) on inconsistent counts."""
+    c = (ctypes.c_int64 * (2 * world + 4))(*[int(x) for x in counts])
+    so, ro = (ctypes.c_int64 * (world + 1))(), (ctypes.c_int64 * (world + 1))()
+    pl = N.FwExchangePlan()
+    rc = N.lib().fw_exchange_plan(world, rank, c, so, ro, ctypes.byref(pl))
+    if rc != N.FW_OK:
+        raise N.NativeError(rc, "inconsistent exchange counts")
+    return list(so), list(ro), {f: getattr(pl, f) for f, _ in N.FwExchangePlan._fields_}
+
+
 _KEY_KINDS = {"long": N.FW_KEY_LONG, "int": N.FW_KEY_INT, "hashed": N.FW_KEY_HASHED}
 
 
@@ -57,7 +70,7 @@ class KeyGroupExchange:
         self.group = group
         self.key_kind = _KEY_KINDS[key_type]
         self.key_group_range = compute_key_group_range_for_operator_index(max_parallelism, world, rank)
-        self.bytes_sent = 0
+        self.bytes_sent = self.items_sent = self.bytes_received = 0
 
     def exchange(self, keys, ts, vals, key_hash=None):
         """Returns this rank's (keys, ts, vals) — and key hashes as a 4th column when key_hash is given:
@@ -91,7 +104,10 @@ class KeyGroupExchange:
             dist.all_to_all_single(r, col, output_split_sizes=out_split, input_split_sizes=in_split,
                                    group=self.group)
             out.append(back(r))
-        self.bytes_sent += (24 + (4 if key_hash is not None else 0)) * (sum(in_split) - in_split[self.rank])
+        rec = 24 + (4 if key_hash is not None else 0)
+        self.items_sent += sum(in_split) - in_split[self.rank]
+        self.bytes_sent += rec * (sum(in_split) - in_split[self.rank])
+        self.bytes_received += rec * (total - out_split[self.rank])
         return tuple(out)
 
     def combine_watermark(self, local_wm, device=None):
@@ -151,6 +167,13 @@ class NativeKeyByExchange:
         self.op._inflight = (keys, ts, vals)
         return wm.value
 
+    def stats(self):
+        """fw_comm_get_stats: the communicator's world / rank (ncclCommCount / ncclCommUserRank) and the exchange's
+        counters (items and bytes to and from the other subtasks, receive-column reallocations) as a dict."""
+        st = N.FwCommStats()
+        N.check(N.lib().fw_comm_get_stats(self._c, ctypes.byref(st)))
+        return {f: getattr(st, f) for f, _ in N.FwCommStats._fields_}
+
     def close(self):
         if self._c:
             N.lib().fw_comm_destroy(self._c)
@@ -167,8 +190,8 @@ class CombiningExchange:
     -- one per (key, window) of the batch instead of one per record -- go to their subtasks, which merge them
     (fw_push_partials_device; AggregateFunction.merge, flink-core/.../AggregateFunction.java:160).  Results equal
     the uncombined exchange for the decomposable count/sum/min/max on tumbling windows without allowed lateness
-    (float sums within the usual tolerance); first-element, minBy/maxBy, HLL and t-digest aggregates do not
-    combine."""
+    (float sums within the usual tolerance), on tumbling and on sliding windows kept as panes (a partial is a pane's);
+    first-element, minBy/maxBy, HLL and t-digest aggregates do not combine."""
 
     def __init__(self, exchange: KeyGroupExchange, combiner):
         self.exchange = exchange

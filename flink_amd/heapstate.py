@@ -551,10 +551,17 @@ def state_table_order(mappings, key_hash, ns_hash, capacity=1024):
     """The order CopyOnWriteStateTable's snapshot walks `mappings` [(namespace, key, state)] inserted in the given
     order: buckets in index order (compositeHash = bitMix(key.hashCode() ^ namespace.hashCode()) & (capacity - 1),
     CopyOnWriteStateTable.java:831-834; default capacity 1024, doubled past 3/4 load, :197-247 / :626-637), each
-    bucket's chain newest first (addNewStateTableEntry puts the entry at the chain's head, :643-675).  No rehash in
-    flight at the snapshot (snapshotTableArrays, :582-618)."""
+    bucket's chain newest first (addNewStateTableEntry puts the entry at the chain's head, :643-675).
+
+    Exact for tables that never grew: putEntry doubles when size() > threshold BEFORE adding (:486-490), so m
+    mappings stay at the initial capacity while m - 1 <= 3/4 of it (769 at 1024).  A table that grew is rehashed
+    incrementally, MIN_TRANSFERRED_PER_INCREMENTAL_REHASH entries per later get or put (:735-780), each moved chain
+    reversed into the new table, and a snapshot during the rehash walks both arrays (snapshotTableArrays, :599-614):
+    its order depends on how many operations followed the doubling and on removals, which the mappings alone do not
+    tell.  For such tables this returns a deterministic order at the grown capacity (newest first): the savepoint is
+    valid and restores the same state, but is not byte-identical to the JVM's."""
     cap = capacity
-    while len(mappings) > (cap >> 1) + (cap >> 2):
+    while len(mappings) - 1 > (cap >> 1) + (cap >> 2):
         cap <<= 1
     b = [bit_mix(key_hash(k) ^ ns_hash(n)) & (cap - 1) for n, k, _ in mappings]
     return [mappings[i] for i in sorted(range(len(mappings)), key=lambda i: (b[i], -i))]

@@ -275,9 +275,14 @@ class GpuWindowOperator:
         N.check(L.fw_pending(self._h, ctypes.byref(n_rows), None), self._h)
         dev = torch.device("cuda", self.device)
         cols = {f: torch.empty(max(n_rows.value, 1), dtype=torch.int64, device=dev) for f in fields}
+        # the output blocks come from torch's allocator on the current stream, and the library writes them on its
+        # own stream: it must not start before the current stream's pending work on a recycled block is done
+        self._torch_stream(dev).wait_stream(torch.cuda.current_stream(dev))
         dst = N.FwRows(**{f: cols[f].data_ptr() for f in fields})
         got = ctypes.c_int64()
         N.check(L.fw_drain_rows(self._h, ctypes.byref(dst), n_rows.value, ctypes.byref(got)), self._h)
+        # and the current stream's readers of the rows come after the library's copies (fw_drain_rows also waits)
+        torch.cuda.current_stream(dev).wait_stream(self._torch_stream(dev))
         return {f: t[:got.value] for f, t in cols.items()}
 
     def drain_digests(self):

@@ -375,6 +375,27 @@ int fw_keyby_push_device(fw_comm* comm, fw_op* op, const int64_t* key, const int
  * merged into `op` (fw_push_partials_device).  Eligible configurations only. */
 int fw_keyby_combine_push_device(fw_comm* comm, fw_op* combiner, fw_op* op, const int64_t* key, const int64_t* ts,
                                  const void* val, int64_t n, int64_t local_wm, int64_t* combined_wm);
+/* The exchange's counters (the sending side of RecordWriter's numBytesOut / numRecordsOut,
+ * flink-runtime/.../io/network/api/writer/RecordWriter.java:88-115): world / rank as the RCCL communicator reports
+ * them (ncclCommCount / ncclCommUserRank), batches exchanged, items (records, or partials when combining) and
+ * bytes sent to and received from the OTHER subtasks (a subtask's own share never leaves the GPU), how often the
+ * receive columns were reallocated and what they hold. */
+typedef struct fw_comm_stats {
+  int32_t world, rank;
+  int64_t batches, items_sent, items_received, bytes_sent, bytes_received, recv_reallocs, recv_capacity;
+} fw_comm_stats;
+int fw_comm_get_stats(fw_comm* comm, fw_comm_stats* out);
+/* The host arithmetic of one exchange round, from the counts round's int64[2 world + 4] (send counts per peer,
+ * receive counts per peer, watermark in / min, batch size in / sum over subtasks): send and receive offsets
+ * ([world + 1] each, prefix sums: records from subtask 0 first, then 1, ..., as the input gate's channels) and
+ * the totals.  recv_bound = the sum of every subtask's batch: no subtask can receive more, so the receive columns
+ * are sized for it once.  FW_ERR_STATE when the counts contradict themselves (negative, more received than the
+ * whole batch, the own share sent != received). */
+typedef struct fw_exchange_plan_t {
+  int64_t send_total, recv_total, items_sent, items_received, recv_bound;
+} fw_exchange_plan_t;
+int fw_exchange_plan(int32_t world, int32_t rank, const int64_t* counts, int64_t* send_off, int64_t* recv_off,
+                     fw_exchange_plan_t* out);
 
 /* ---- f2: Flink's wire format for one input channel <-> device columns.
  * The byte stream of a channel is its network buffers in order: SpanningRecordSerializer.addRecord writes each

@@ -9,7 +9,7 @@ from flink_amd.datagen import generate_host
 from flink_amd.windowing import CountSumMinMax, ExtremalElementReduce, FirstElementReduce, first_element_results
 from oracle import oracle as orc
 from tests.kat_util import expected_counters, load_kats, replay, row_counters
-from tests.parity_util import assert_rows_equal, assert_side_equal
+from tests.parity_util import assert_f32_sums_near_exact, assert_rows_equal, assert_side_equal
 
 pytestmark = pytest.mark.gpu
 
@@ -287,6 +287,42 @@ def test_gpu_word_count_hashed_keys(first):
         got = first_element_results(g, elements, 1, "sum")
         assert sorted(got) == sorted(first_element_results(r, elements, 1, "sum"))
         assert all(t[0] == words[int(row["key"])] for t, row in zip(got, g))
+
+
+def test_gpu_word_count_real_tokens():
+    # C1 (configs[0]) on WordCountData's own tokens (tests/golden/wordcount_tokens.json: 287 tokens, 170 words,
+    # WordCount.java:102-117's toLowerCase().split("\\W+")), 2M of the bench's 10M-token stream: both pipelines of
+    # WindowWordCount.java:74-81 / SideOutputExample.java:97-101 on the GPU against the oracle, rows bit-exact
+    from bench import wordcount_stream
+    n = 2_000_000
+    keys, ts, vals, kh = wordcount_stream(0, n)
+    assert len(np.unique(keys)) == 170
+    gpu = _gpu_op("tumbling", size=5000, value_type="i32", key_type="hashed")
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=5000, value_type="i32")
+    step = 1 << 19
+    for b in range(0, n, step):
+        sl = slice(b, b + step)
+        gpu.process(keys[sl], ts[sl], vals[sl], key_hash=kh[sl])
+        ref.process(keys[sl], ts[sl], vals[sl])
+        gpu.watermark(int(ts[sl].max()))
+        ref.watermark(int(ts[sl].max()))
+    gpu.watermark((1 << 63) - 1)
+    ref.watermark((1 << 63) - 1)
+    g, r = gpu.rows(), ref.rows()
+    gpu.close()
+    assert_rows_equal(g, r, "int")
+    assert int(g["count"].sum()) == n and int(g["sum"].sum()) == n
+    # countWindow(10, 5).sum(1): every 5th token of a word fires over its last <= 10
+    cw = _count_op(10, 5, value_type="i32", expected_entries=1024)
+    cref = orc.CountWindowOracle(10, 5, value_type="i32")
+    for b in range(0, n, step):
+        sl = slice(b, b + step)
+        cw.process(keys[sl], np.zeros(len(keys[sl]), dtype=np.int64), vals[sl])
+        cref.process(keys[sl], vals[sl])
+    gc, rc = cw.rows(), cref.rows()
+    cw.close()
+    assert len(gc) == len(rc) > n // 6
+    assert _count_rows(gc) == _count_rows(rc)
 
 
 def test_gpu_vs_oracle_c2_shape():
@@ -1061,6 +1097,12 @@ def test_gpu_short_byte_float_fields(cfg, value_type, first):
     cfg = dict(cfg, value_type=value_type, first=first)
     g, r, *_ = _run_both(cfg, batches, wms)
     assert_rows_equal(g, r, _VT[value_type])
+    if value_type == "f32" and not first and cfg["assigner"] != "session":
+        # and against the exact sums of the windows' elements, with the tight single-rounding bound
+        size, slide = cfg["size"], cfg.get("slide", cfg["size"])
+        windows_of = lambda t: [t - t % slide - j * slide for j in range(size // slide)]  # noqa: E731 (ts >= 0)
+        keys, ts, vals = (np.concatenate(c) for c in zip(*batches))
+        assert_f32_sums_near_exact(g, keys, ts, vals, windows_of)
 
 
 def _count_op(size, slide, evict_after=False, value_type="i64", **kw):

@@ -126,6 +126,13 @@ def test_java_iteration_orders():
     # CopyOnWriteStateTable: chains newest first
     same = [(("ns"), "a", 1), (("ns"), "b", 2)]
     assert H.state_table_order(same, lambda k: 7, lambda n: 0) == same[::-1]
+    # putEntry doubles when size() > threshold BEFORE adding (CopyOnWriteStateTable.java:486-490): 769 mappings stay
+    # at capacity 1024 (threshold 768), the 770th is added to a doubled table
+    for m, cap in ((769, 1024), (770, 2048)):
+        maps = [("ns", i, i) for i in range(m)]
+        b = [H.bit_mix(i ^ 0) & (cap - 1) for i in range(m)]
+        want = [maps[i] for i in sorted(range(m), key=lambda i: (b[i], -i))]
+        assert H.state_table_order(maps, lambda k: k, lambda n: 0) == want, m
     assert H.long_to_int_with_bit_mixing(0) == 0
 
 
