@@ -24,19 +24,21 @@ def f32_sum_bound(rows, sums=()):
     return (n + 1.0) * F32_U * mag * 1.001
 
 
-def assert_f32_sums_near_exact(rows, keys, ts, vals, windows_of):
+def assert_f32_sums_near_exact(rows, keys, ts, vals, windows_of, size=None, wm_prev=None):
     """The tight half of the Float-sum check: the GPU sums a Float field in f64 and rounds once, so
     against the exact sum S of the window's elements |S_gpu - S| <= u |S| + n 2^-53 sum|x_i| -- linear in n, unlike
     the recursive-summation bound above, so a wrong element in a long window does not pass.  `windows_of(ts)` gives
-    each element's window starts (a list of arrays, one per window it belongs to; tumbling / sliding assigners).
+    each element's window starts (a list of arrays, one per window it belongs to; tumbling / sliding assigners);
+    with `size` and `wm_prev` (the watermark in effect when each element was processed) an element joins only the
+    windows that are not late for it (WindowOperator.isWindowLate, allowed lateness 0: maxTimestamp <= watermark).
     The exact sums are f64 sums of float32 values of bounded magnitude (exact when they fit 53 bits, as in the
-    tests that call this).  Rows whose (key, window) element count differs from the row's count (a late element
-    dropped inside a fired window's range) are skipped; at least 90 % must be checked."""
+    tests that call this).  Every row's (key, window) element count must then equal the row's count."""
     k_all, s_all, x_all = [], [], []
     for starts in windows_of(ts):
-        k_all.append(keys)
-        s_all.append(starts)
-        x_all.append(vals)
+        keep = np.ones(len(ts), dtype=bool) if wm_prev is None else starts + size - 1 > wm_prev
+        k_all.append(keys[keep])
+        s_all.append(starts[keep])
+        x_all.append(vals[keep])
     k_all, s_all, x_all = np.concatenate(k_all), np.concatenate(s_all), np.concatenate(x_all)
     grp, inv = np.unique(np.stack([k_all, s_all], axis=1), axis=0, return_inverse=True)
     inv = inv.ravel()
@@ -50,13 +52,12 @@ def assert_f32_sums_near_exact(rows, keys, ts, vals, windows_of):
     checked = 0
     for r in rows:
         i = idx.get((int(r["key"]), int(r["start"])))
-        if i is None or cnt[i] != r["count"]:
-            continue
+        assert i is not None and cnt[i] == r["count"], (r, None if i is None else cnt[i])
         got = float(np.int64(r["sum"]).view(np.float64))
         n = float(cnt[i])
         assert abs(got - exact[i]) <= F32_U * abs(exact[i]) + n * 2.0 ** -53 * absum[i], (r, exact[i])
         checked += 1
-    assert checked >= 0.9 * len(rows), (checked, len(rows))
+    assert checked == len(rows) > 0
 
 
 def _sorted(rows):

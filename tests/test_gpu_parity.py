@@ -1102,7 +1102,9 @@ def test_gpu_short_byte_float_fields(cfg, value_type, first):
         size, slide = cfg["size"], cfg.get("slide", cfg["size"])
         windows_of = lambda t: [t - t % slide - j * slide for j in range(size // slide)]  # noqa: E731 (ts >= 0)
         keys, ts, vals = (np.concatenate(c) for c in zip(*batches))
-        assert_f32_sums_near_exact(g, keys, ts, vals, windows_of)
+        wm_prev = np.concatenate([np.full(len(b[0]), wms[i - 1] if i else -(1 << 63), dtype=np.int64)
+                                  for i, b in enumerate(batches)])
+        assert_f32_sums_near_exact(g, keys, ts, vals, windows_of, size, wm_prev)
 
 
 def _count_op(size, slide, evict_after=False, value_type="i64", **kw):
