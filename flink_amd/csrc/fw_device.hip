@@ -1735,6 +1735,54 @@ __device__ __forceinline__ bool lds_session_upsert(AggLds& L, int64_t* E, int vt
   return true;
 }
 
+// one accumulator block for a window the ordered path or the session flush creates (the protocol of agg_flush's reservation, k = 1)
+__device__ __forceinline__ uint64_t pool_alloc_one(const DevCfg& c, Status* st) {
+  const int t = atomicSub(&c.pool_ctr[0], 1);
+  if (t >= 1) return (uint64_t)c.pool_free[t - 1];
+  atomicAdd(&c.pool_ctr[0], 1);
+  const long long bump = atomicAdd(&c.pool_ctr[1], 1);
+  if (bump + 1 > c.pool_blocks) {
+    atomicOr(&st->flags, FW_STATUS_POOL);
+    return 0;
+  }
+  return (uint64_t)bump;
+}
+// AggregateFunction.merge of two HyperLogLog accumulators (register max, AbstractHeapMergingState.mergeNamespaces,
+// AbstractHeapMergingState.java:67-93): src's marked chunks are raised into dst bytewise (dst's chunks marked), src is
+// left zeroed and goes on the deferred free list.  One thread; the caller owns both blocks (the key's entries).
+__device__ __forceinline__ uint32_t max_u8x4(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) r |= max((a >> k) & 0xffu, (b >> k) & 0xffu) << k;
+  return r;
+}
+__device__ void hll_merge_blocks(const DevCfg& c, uint64_t dst, uint64_t src) {
+  const int p = c.hll_p;
+  uint8_t* bs = c.pool + src * (uint64_t)c.pool_bytes;
+  uint8_t* bd = c.pool + dst * (uint64_t)c.pool_bytes;
+  uint32_t* ms = reinterpret_cast<uint32_t*>(bs);
+  uint32_t* md = reinterpret_cast<uint32_t*>(bd);
+  uint4* qs = reinterpret_cast<uint4*>(bs + hll_hdr_bytes(p));
+  uint4* qd = reinterpret_cast<uint4*>(bd + hll_hdr_bytes(p));
+  const int32_t nq = (int32_t)(((int64_t)1 << p) / 16), nw = (nq + 31) / 32;
+  for (int32_t w = 0; w < nw; w++) {
+    const uint32_t word0 = ms[w];
+    uint32_t word = word0;
+    while (word) {
+      const int b = __ffs(word) - 1;
+      word &= word - 1;
+      const uint4 a = qs[w * 32 + b], d = qd[w * 32 + b];
+      qd[w * 32 + b] = make_uint4(max_u8x4(a.x, d.x), max_u8x4(a.y, d.y), max_u8x4(a.z, d.z), max_u8x4(a.w, d.w));
+      qs[w * 32 + b] = make_uint4(0, 0, 0, 0);
+    }
+    if (word0) {
+      md[w] |= word0;
+      ms[w] = 0u;
+    }
+  }
+  __threadfence();  // (zeroed before its id can be handed out)
+  c.pool_defer[atomicAdd(&c.pool_ctr[2], 1)] = (uint32_t)src;
+}
 // MergingWindowSet.addWindow (MergingWindowSet.java:156-225) of a session delta d (an interval with
 // its accumulator) into the key's in-flight sessions of region r: d's connected component becomes one
 // session (merge function + mergeNamespaces, WindowOperator.java:308-339,
@@ -1783,6 +1831,7 @@ __device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, con
         continue;
       }
       acc_merge(c, m, e);
+      if (c.pool_bytes) hll_merge_blocks(c, pool_block_of(m), pool_block_of(e));  // (HLL: register max)
       m.start = min(m.start, e.start);
       m.end = max(m.end, e.end);
       // the slot stays occupied (live counts occupied slots) until k_fire rebuilds the region
@@ -1796,7 +1845,9 @@ __device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, con
       atomicOr(&st->flags, FW_STATUS_STATE_LOST);
       return 0;
     }
-    r.ent[ns] = d;
+    Entry nd = d;
+    if (c.pool_bytes) nd.meta |= (int64_t)(pool_alloc_one(c, st) << 1);  // (HLL: zero registers; k_hll_update fills)
+    r.ent[ns] = nd;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __hip_atomic_store(r.state + ns, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return 1;
@@ -1804,7 +1855,7 @@ __device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, con
   acc_merge(c, m, d);
   m.start = min(m.start, d.start);  // TimeWindow.cover
   m.end = max(m.end, d.end);
-  m.meta = FW_TIMER;
+  m.meta = c.pool_bytes ? (m.meta | FW_TIMER) : FW_TIMER;  // (the block id stays above the timer bit)
   *timer = jsub(m.end, 1);
   r.ent[target] = m;
   return 0;
@@ -2538,18 +2589,6 @@ __device__ __forceinline__ int32_t new_slot(const SlowCtx& x, const Region& r, i
 
 __device__ void hll_clear(const DevCfg& c, uint64_t blk);
 __device__ void hll_estimate(const DevCfg& c, uint64_t blk, double* est, int64_t* zeros_out, int64_t* lo_out);
-// one accumulator block for a window the ordered path creates (the protocol of agg_flush's reservation, k = 1)
-__device__ __forceinline__ uint64_t pool_alloc_one(const DevCfg& c, Status* st) {
-  const int t = atomicSub(&c.pool_ctr[0], 1);
-  if (t >= 1) return (uint64_t)c.pool_free[t - 1];
-  atomicAdd(&c.pool_ctr[0], 1);
-  const long long bump = atomicAdd(&c.pool_ctr[1], 1);
-  if (bump + 1 > c.pool_blocks) {
-    atomicOr(&st->flags, FW_STATUS_POOL);
-    return 0;
-  }
-  return (uint64_t)bump;
-}
 // HyperLogLog add of one item into block blk (k_hll_update's raise: CAS on the register's word while larger, the
 // chunk marked when the register leaves zero)
 __device__ __forceinline__ void hll_raise(const DevCfg& c, uint64_t blk, int64_t item) {
@@ -2666,7 +2705,7 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
     ne.start = ws;
     ne.end = we;
     acc_clear(ne);
-    ne.meta = 0;
+    ne.meta = c.agg == FW_AGG_HLL ? (int64_t)(pool_alloc_one(c, x.st) << 1) : 0;
     actual = new_slot(x, r, p, h, ne);
     if (actual < 0) return;
     fresh = true;
@@ -2689,23 +2728,40 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
         const Entry& e = r.ent[s];
         if (e.key != k || !(ws <= e.end && we >= e.start)) continue;
         acc_merge(c, m, e);  // mergeNamespaces
+        if (c.agg == FW_AGG_HLL) hll_merge_blocks(c, pool_block_of(m), pool_block_of(e));  // (register max)
         kill_slot(x, r, p, (int32_t)s);
       }
       m.start = cs;
       m.end = ce;
-      m.meta = FW_TIMER;  // EventTimeTrigger.onMerge registers maxTimestamp unconditionally
+      // EventTimeTrigger.onMerge registers maxTimestamp unconditionally (the block id stays above the timer bit)
+      m.meta = c.agg == FW_AGG_HLL ? (m.meta | FW_TIMER) : FW_TIMER;
       r.ent[actual] = m;
     }
   }
   Entry en = r.ent[actual];
   if (cleanup_of(en.end, c.lateness) <= x.wm) {  // isWindowLate(actualWindow) -> retireWindow
-    if (fresh) kill_slot(x, r, p, actual);
+    if (fresh) {
+      if (c.agg == FW_AGG_HLL) {  // its (untouched, zero) block on the deferred list
+        __threadfence();
+        c.pool_defer[atomicAdd(&c.pool_ctr[2], 1)] = (uint32_t)pool_block_of(en);
+      }
+      kill_slot(x, r, p, actual);
+    }
     return;
   }
   *skipped = false;
   acc_add(c, en, v, fo);
+  if (c.agg == FW_AGG_HLL) hll_raise(c, pool_block_of(en), v);  // (k_hll_update takes the partitioned records)
   if (jsub(en.end, 1) <= x.wm) {
-    emit_one(c, x.out, x.st, en);
+    if (c.agg == FW_AGG_HLL) {  // getResult from the session's registers (it stays in flight)
+      Entry fr = en;
+      double est;
+      hll_estimate(c, pool_block_of(en), &est, &fr.mn, &fr.mx);
+      fr.sum = __double_as_longlong(est);
+      emit_one(c, x.out, x.st, fr);
+    } else {
+      emit_one(c, x.out, x.st, en);
+    }
     if (c.purging) acc_clear(en);  // FIRE_AND_PURGE clears the contents; the window stays in flight
   } else {
     en.meta |= FW_TIMER;
@@ -3295,6 +3351,81 @@ __global__ __launch_bounds__(256, FW_HLL_WAVES) void k_hll_update(DevCfg c, cons
     if (wi + 1 == nw_max) pp = pp_w;
    }
   }
+}
+
+// the same for session windows: a record's window [ts, ts + gap) lies, after the aggregate's merges, inside exactly
+// one of its key's in-flight sessions (MergingWindowSet keeps them pairwise disjoint), found on the key's probe chain
+// (sessions hash the key only); its item raises that session's registers.  HU records' chain heads in flight.
+__global__ __launch_bounds__(256) void k_hll_update_sessions(DevCfg c, const PRec* __restrict__ part,
+                                                             const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
+                                                             Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int64_t total = offs[(int64_t)c.P * T];
+  const int64_t i0 = (int64_t)blockIdx.x * FW_HLL_CHUNK;
+  if (i0 >= total) return;
+  __shared__ int32_t p0_s;
+  if (threadIdx.x == 0) {  // partition of the chunk's first record: last p with offs[p*T] <= i0
+    int32_t lo = 0, hi = c.P - 1;
+    while (lo < hi) {
+      const int32_t mid = (lo + hi + 1) >> 1;
+      if ((int64_t)offs[(int64_t)mid * T] <= i0)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    p0_s = lo;
+  }
+  __syncthreads();
+  const bool cmp = c.compact && !*c.wide;
+  const int64_t i1 = min(total, i0 + (int64_t)FW_HLL_CHUNK);
+  int32_t pp = p0_s;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
+    int64_t key, ts, val;
+    if (cmp) {
+      const i64x2 r = reinterpret_cast<const i64x2*>(part)[i];
+      compact_decode(c, pp, r.x, &key, &ts);
+      val = r.y;
+    } else {
+      const PRec rec = part[i];
+      key = rec.key;
+      ts = rec.last;
+      val = rec.val;
+    }
+    const int64_t te = jadd(ts, c.gap);
+    const Region r = region_of(c, tb, pp, tb.cur[pp]);
+    const uint64_t h = slot_hash(c, key, 0);
+    const uint32_t want = live_word(h);
+    int64_t blk = -1;
+    for (uint32_t k = 0; k <= r.mask; k++) {
+      const uint32_t s = ((uint32_t)h + k) & r.mask;
+      const uint32_t w = r.state[s];  // (the table is read-only here)
+      if (w == SLOT_EMPTY) break;
+      if (w != want) continue;
+      const Entry& e = r.ent[s];
+      if (e.key == key && e.start <= ts && te <= e.end) {
+        blk = (int64_t)pool_block_of(e);
+        break;
+      }
+    }
+    if (blk < 0) {
+      atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's session
+      continue;
+    }
+    hll_raise(c, (uint64_t)blk, val);
+  }
+}
+// the blocks session merges freed (zeroed, on the deferred list) onto the free stack: before a firing, when nothing
+// pops (one workgroup)
+__global__ __launch_bounds__(256) void k_pool_release(DevCfg c) {
+  const int32_t n = c.pool_ctr[2];
+  if (n <= 0) return;
+  __shared__ int32_t base_s;
+  if (threadIdx.x == 0) base_s = atomicAdd(&c.pool_ctr[0], n);
+  __syncthreads();
+  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) c.pool_free[base_s + i] = c.pool_defer[i];
+  __syncthreads();
+  if (threadIdx.x == 0) c.pool_ctr[2] = 0;
 }
 
 // ---- t-digest (FW_AGG_TDIGEST).  The definition is oracle/window_oracle.h's OR_AGG_TDIGEST, restated here
@@ -6326,7 +6457,9 @@ void launch_hll_update(const DevCfg& c, const PRec* part, const uint32_t* offs, 
                        Status* st, hipStream_t s) {
   if (n <= 0) return;
   const dim3 grid((unsigned)((n + FW_HLL_CHUNK - 1) / FW_HLL_CHUNK));
-  if (c.assigner == FW_SLIDING)
+  if (c.assigner == FW_SESSION)
+    hipLaunchKernelGGL(k_hll_update_sessions, grid, dim3(256), 0, s, c, part, offs, T, tb, st);
+  else if (c.assigner == FW_SLIDING)
     hipLaunchKernelGGL(k_hll_update<true>, grid, dim3(256), 0, s, c, part, offs, T, tb, st);
   else
     hipLaunchKernelGGL(k_hll_update<false>, grid, dim3(256), 0, s, c, part, offs, T, tb, st);
@@ -6350,6 +6483,8 @@ void launch_fire(const DevCfg& c0, int64_t wm, DevTable tb, DevRows out, Status*
     hipLaunchKernelGGL(k_dt_fire, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, wm, tb, out, st);
     return;
   }
+  if (c.pool_bytes && c.assigner == FW_SESSION)  // blocks freed by session merges go back first
+    hipLaunchKernelGGL(k_pool_release, dim3(1), dim3(256), 0, s, c);
   if (c.pool_bytes)
     hipLaunchKernelGGL(k_fire<true>, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, wm, tb, out, st);
   else

@@ -122,7 +122,10 @@ struct DevCfg {
   const int64_t* by_val;  // FW_AGG_MINBY / MAXBY: the batch's value column by batch index (the push's scratch set)
   uint8_t* pool;
   uint32_t* pool_free;
-  int32_t* pool_ctr;
+  int32_t* pool_ctr;      // [0] stack height, [1] blocks handed out from the pool's end, [2] deferred frees
+  // blocks freed by a session merge while the aggregate or the ordered path may pop others (already zeroed):
+  // pushed on the free stack by the next firing (k_pool_release), when nothing pops
+  uint32_t* pool_defer;
   int64_t pool_blocks;
   int64_t pool_bytes;     // 0 = no pool
   // FW_AGG_TDIGEST (definition: oracle/window_oracle.h OR_AGG_TDIGEST): td_nb = delta / 2 buckets of the

@@ -898,9 +898,15 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     snprintf(msg, sizeof msg, "HyperLogLog precision must be in [4, 16], got %d", hll_p);
   bool unsupported = false;
   if (!msg[0] && cfg.aggregate == FW_AGG_HLL &&
-      ((cfg.assigner != FW_TUMBLING && cfg.assigner != FW_SLIDING) || cfg.value_type != FW_VAL_I64)) {
-    snprintf(msg, sizeof msg, "the HyperLogLog aggregate is offered for tumbling and sliding windows over a Long item "
-                              "column");
+      ((cfg.assigner != FW_TUMBLING && cfg.assigner != FW_SLIDING && cfg.assigner != FW_SESSION) ||
+       cfg.value_type != FW_VAL_I64)) {
+    snprintf(msg, sizeof msg, "the HyperLogLog aggregate is offered for tumbling, sliding and session windows over a "
+                              "Long item column");
+    unsupported = true;
+  }
+  if (!msg[0] && cfg.aggregate == FW_AGG_HLL && cfg.assigner == FW_SESSION && cfg.purging) {
+    snprintf(msg, sizeof msg, "the HyperLogLog aggregate over session windows is offered with EventTimeTrigger (a "
+                              "purged session would keep its window with empty registers)");
     unsupported = true;
   }
   const int32_t td_delta = cfg.tdigest_compression ? cfg.tdigest_compression : 100;
@@ -1040,8 +1046,9 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     if (c.agg == FW_AGG_HLL)  // registers start at zero (and are zeroed when freed)
       HIP_OR_RETURN(op, hipMemsetAsync(c.pool, 0, (size_t)(c.pool_blocks * c.pool_bytes), op->stream));
     HIP_OR_RETURN(op, dmalloc(&c.pool_free, (size_t)c.pool_blocks));
-    HIP_OR_RETURN(op, dmalloc(&c.pool_ctr, 2));
-    HIP_OR_RETURN(op, hipMemsetAsync(c.pool_ctr, 0, 2 * sizeof(int32_t), op->stream));
+    HIP_OR_RETURN(op, dmalloc(&c.pool_defer, (size_t)c.pool_blocks));
+    HIP_OR_RETURN(op, dmalloc(&c.pool_ctr, 3));
+    HIP_OR_RETURN(op, hipMemsetAsync(c.pool_ctr, 0, 3 * sizeof(int32_t), op->stream));
   }
   // regions sized for the expected entries at 1/FW_TABLE_SLACK load (default 4: 25 %; the limit is 3/4)
   const int64_t slack = getenv("FW_TABLE_SLACK") ? std::max(2, atoi(getenv("FW_TABLE_SLACK"))) : c.dense ? 2 : 4;
@@ -1170,6 +1177,7 @@ void fw_destroy(fw_op* op) {
   dfree(op->dc.taint_key);
   dfree(op->dc.pool);
   dfree(op->dc.pool_free);
+  dfree(op->dc.pool_defer);
   dfree(op->dc.pool_ctr);
   {
     double* q = const_cast<double*>(op->dc.td_qb);

@@ -894,12 +894,63 @@ def test_gpu_hll_register_blocks_are_recycled():
     gpu.close()
 
 
-def test_gpu_hll_refuses_unsupported_shapes():
+HLL_SESSION_CFGS = [dict(gap=300, lateness=0, zipf=1.1, bound=200, jitter=300),
+                    dict(gap=300, lateness=500, zipf=1.1, bound=400, jitter=1500),
+                    dict(gap=50, lateness=200, zipf=None, bound=100, jitter=400),
+                    dict(gap=2000, lateness=0, zipf=1.3, bound=200, jitter=200)]
+
+
+@pytest.mark.parametrize("cfg", HLL_SESSION_CFGS, ids=["zipf", "zipf-lateness", "uniform-lateness", "long-gap"])
+def test_gpu_hll_sessions_vs_oracle(cfg):
+    # a10: HyperLogLog over EventTimeSessionWindows (WindowedStream.aggregate with any assigner, WindowedStream.java:
+    # 687-852).  Sessions merge (MergingWindowSet.addWindow, MergingWindowSet.java:150-225) and their accumulators with
+    # them (AbstractHeapMergingState.mergeNamespaces, AbstractHeapMergingState.java:67-93; AggregateFunction.merge,
+    # AggregateFunction.java:160): the register max of the merged sessions' blocks -- in the parallel flush, in the
+    # ordered replay of late elements (late firings, lateness), and across batches.  Registers bit-exact.
     from flink_amd import HyperLogLog
+    from flink_amd.operator import GpuWindowOperator
+    batches, wms = _stream(200_000, 20_000, 3000, bound=cfg["bound"], jitter=cfg["jitter"], rate=100_000,
+                           zipf=cfg["zipf"])
+    gpu = GpuWindowOperator(EventTimeSessionWindows.with_gap(cfg["gap"]), HyperLogLog(10),
+                            allowed_lateness=cfg["lateness"], expected_entries=20_000)
+    ref = orc.WindowOperatorOracle(assigner="session", gap=cfg["gap"], lateness=cfg["lateness"], hll_p=10)
+    for (k, t, v), wm in zip(batches, wms):
+        gpu.process(k, t, v)
+        ref.process(k, t, v)
+        gpu.watermark(wm)
+        ref.watermark(wm)
+    assert gpu.late_dropped == ref.late_dropped
+    g, r = gpu.rows(), ref.rows()
+    _hll_rows_equal(g, r)
+    # sessions did merge (a session spans more than one element window)
+    assert (g["end"] - g["start"] > cfg["gap"]).any()
+    gpu.close()
+
+
+def test_gpu_hll_sessions_hot_partition_split():
+    # sessions of a few Zipf keys in 200K-record batches: the hottest partitions are split over several aggregate
+    # workgroups, whose deltas merge into the sessions (and their register blocks) at the last chunk
+    from flink_amd import HyperLogLog
+    from flink_amd.operator import GpuWindowOperator
+    batches, wms = _stream(600_000, 200_000, 1000, bound=200, jitter=300, rate=100_000, zipf=1.1)
+    gpu = GpuWindowOperator(EventTimeSessionWindows.with_gap(100), HyperLogLog(12), expected_entries=10_000)
+    ref = orc.WindowOperatorOracle(assigner="session", gap=100, hll_p=12)
+    for (k, t, v), wm in zip(batches, wms):
+        gpu.process(k, t, v)
+        ref.process(k, t, v)
+        gpu.watermark(wm)
+        ref.watermark(wm)
+    _hll_rows_equal(gpu.rows(), ref.rows())
+    gpu.close()
+
+
+def test_gpu_hll_refuses_unsupported_shapes():
+    from flink_amd import HyperLogLog, PurgingTrigger
     from flink_amd import _native as N
     from flink_amd.operator import GpuWindowOperator
     with pytest.raises(N.NativeError) as e:
-        GpuWindowOperator(EventTimeSessionWindows.with_gap(3000), HyperLogLog(12))
+        GpuWindowOperator(EventTimeSessionWindows.with_gap(3000), HyperLogLog(12),
+                          trigger=PurgingTrigger.of(EventTimeTrigger.create()))
     assert e.value.code == N.FW_ERR_UNSUPPORTED
     with pytest.raises(N.NativeError):
         GpuWindowOperator(TumblingEventTimeWindows.of(1000), HyperLogLog(20))
