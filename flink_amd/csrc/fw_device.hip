@@ -198,6 +198,15 @@ __device__ __forceinline__ int classify(const DevCfg& c, int64_t wm, int64_t ts,
   if (jsub(oldest_end, 1) > wm) return CLS_NORMAL;  // every window: maxTimestamp > wm
   if (cleanup_of(newest_end, c.lateness) <= wm)     // every window late (isWindowLate)
     return jadd(ts, c.lateness) <= wm ? CLS_LATE : CLS_SKIP;  // isElementLate
+  if (c.agg == FW_AGG_TDIGEST && c.lateness == 0) {
+    // t-digest (allowed lateness 0): the element goes into its windows that are not late -- the newest ones,
+    // maxTimestamp > wm -- and none of them fires on it (WindowOperator.java:379-407), so it needs no arrival
+    // order: the parallel path takes it with those windows only
+    int kk = 1;
+    while (kk < k && jsub(jadd(jsub(last, (int64_t)kk * c.slide), c.size), 1) > wm) kk++;
+    if (k_out) *k_out = kk;
+    return CLS_NORMAL;
+  }
   return CLS_SLOW;
 }
 
@@ -3663,6 +3672,9 @@ __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restric
   const int64_t i1 = min(n, i0 + (int64_t)TD_CHUNK);
   const uint64_t none_key = (uint64_t)nblk << (64 - B);
   const uint64_t low = (B >= 64) ? ~0ull : ((1ull << B) - 1ull);
+  // sliding windows (fan-out): record i's windows take items [i * wpr, i * wpr + nwin), newest first; the rest of
+  // its wpr items are empty (sorted last, skipped)
+  const int W = c.assigner == FW_SLIDING ? c.wpr : 1;
   __shared__ int32_t p0_s;
   if (threadIdx.x == 0) {  // partition of the chunk's first record: last p with offs[p*T] <= i0
     int32_t lo = 0, hi = c.P - 1;
@@ -3679,36 +3691,44 @@ __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restric
   const bool cmp = c.compact && !*c.wide;
   int32_t pp = p0_s;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    if (i >= total) {
-      key64[i] = none_key;
-      pay[i] = 0;
-      continue;
+    int nw = 0;
+    if (i < total) {
+      while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
+      PRec rec;
+      if (cmp) {
+        const i64x2 r = reinterpret_cast<const i64x2*>(part)[i];
+        compact_decode(c, pp, r.x, &rec.key, &rec.last);
+        rec.val = r.y;
+        rec.nwin = 1;
+      } else {
+        rec = part[i];
+      }
+      nw = W == 1 ? 1 : (int)(rec.nwin & 0xffff);
+      const Region r = region_of(c, tb, pp, tb.cur[pp]);
+      const uint64_t k = td_key(rec.val);
+      for (int wi = 0; wi < nw; wi++) {
+        const int64_t o = i * W + wi;
+        const int64_t s = jsub(rec.last, (int64_t)wi * c.slide);
+        const int32_t slot = region_find(r, slot_hash(c, rec.key, s), rec.key, s, wend(c, s));
+        if (slot < 0) {
+          atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's window
+          key64[o] = none_key;
+          pay[o] = 0;
+          continue;
+        }
+        const uint32_t g = ((uint32_t)pp << c.log_r) | (uint32_t)slot;
+        const uint64_t blk = pool_block_of(r.ent[slot]);
+        // every record of a digest stores the same slot, so a stale (cached) read costs one redundant store at
+        // most; a hot digest's records read it (an L1 hit) and store nothing
+        if (binv[blk] != g) binv[blk] = g;
+        key64[o] = (blk << (64 - B)) | (k >> B);
+        pay[o] = (uint32_t)(k & low);
+      }
     }
-    while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
-    PRec rec;
-    if (cmp) {
-      const i64x2 r = reinterpret_cast<const i64x2*>(part)[i];
-      compact_decode(c, pp, r.x, &rec.key, &rec.last);
-      rec.val = r.y;
-    } else {
-      rec = part[i];
+    for (int wi = nw; wi < W; wi++) {
+      key64[i * W + wi] = none_key;
+      pay[i * W + wi] = 0;
     }
-    const Region r = region_of(c, tb, pp, tb.cur[pp]);
-    const int32_t slot = region_find(r, slot_hash(c, rec.key, rec.last), rec.key, rec.last, wend(c, rec.last));
-    if (slot < 0) {
-      atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's window
-      key64[i] = none_key;
-      pay[i] = 0;
-      continue;
-    }
-    const uint32_t g = ((uint32_t)pp << c.log_r) | (uint32_t)slot;
-    const uint64_t blk = pool_block_of(r.ent[slot]);
-    // every record of a digest stores the same slot, so a stale (cached) read costs one redundant store at most;
-    // a hot digest's records read it (an L1 hit) and store nothing
-    if (binv[blk] != g) binv[blk] = g;
-    const uint64_t k = td_key(rec.val);
-    key64[i] = (blk << (64 - B)) | (k >> B);
-    pay[i] = (uint32_t)(k & low);
   }
 }
 
@@ -6533,10 +6553,12 @@ void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int
   const uint32_t nblk = (uint32_t)c.pool_blocks;   // no block has this id
   int B = 1;
   while (((int64_t)1 << B) <= c.pool_blocks) B++;
+  const int64_t nrec = n;
+  n *= c.assigner == FW_SLIDING ? c.wpr : 1;  // the sort's items: one per (record, window)
   (void)hipMemsetAsync(td.ctr, 0, 3 * sizeof(int32_t), s);
   (void)hipMemsetAsync(td.fixbm, 0, (size_t)((n + 31) / 32) * sizeof(uint32_t), s);
-  hipLaunchKernelGGL(k_td_keys, dim3((unsigned)((n + TD_CHUNK - 1) / TD_CHUNK)), dim3(256), 0, s, c, part, offs, T, n,
-                     tb, nblk, B, td.gs[0], td.v[0], td.binv, st);
+  hipLaunchKernelGGL(k_td_keys, dim3((unsigned)((nrec + TD_CHUNK - 1) / TD_CHUNK)), dim3(256), 0, s, c, part, offs, T,
+                     nrec, tb, nblk, B, td.gs[0], td.v[0], td.binv, st);
   // one sort by (pool block, high value bits): each digest's batch values become one run, in Double.compare
   // order once the tie runs are ordered by their low bits
   rocprim::double_buffer<uint64_t> kv(td.v[0], td.v[1]);

@@ -922,9 +922,10 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     if (!(cfg.tdigest_quantiles[i] >= 0.0 && cfg.tdigest_quantiles[i] <= 1.0))
       snprintf(msg, sizeof msg, "t-digest quantiles must be in [0, 1]");
   if (!msg[0] && cfg.aggregate == FW_AGG_TDIGEST &&
-      (cfg.assigner != FW_TUMBLING || cfg.allowed_lateness != 0 || cfg.value_type != FW_VAL_F64)) {
-    snprintf(msg, sizeof msg, "the t-digest aggregate is offered for tumbling windows without allowed lateness "
-                              "over a Double field");
+      ((cfg.assigner != FW_TUMBLING && cfg.assigner != FW_SLIDING) || cfg.allowed_lateness != 0 ||
+       cfg.value_type != FW_VAL_F64)) {
+    snprintf(msg, sizeof msg, "the t-digest aggregate is offered for tumbling and sliding windows without allowed "
+                              "lateness over a Double field");
     unsupported = true;
   }
   if (!msg[0] && cfg.aggregate >= FW_AGG_FIRST && cfg.aggregate <= FW_AGG_FIRST_MAX && cfg.assigner == FW_SLIDING && cfg.slide > 0 &&
@@ -1001,7 +1002,8 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   // sliding windows whose size is a multiple of the slide, without allowed lateness, are kept as panes:
   // one state update per element instead of size/slide (DevCfg::panes; FW_NO_PANES=1 disables it)
   c.panes = cfg.assigner == FW_SLIDING && cfg.allowed_lateness == 0 && cfg.size > cfg.slide &&
-            cfg.size % cfg.slide == 0 && cfg.aggregate != FW_AGG_HLL &&  // (HLL: one register block per window)
+            cfg.size % cfg.slide == 0 && cfg.aggregate != FW_AGG_HLL &&  // (HLL, t-digest: a block per window)
+            cfg.aggregate != FW_AGG_TDIGEST &&
             !(getenv("FW_NO_PANES") && atoi(getenv("FW_NO_PANES")));
   if (cfg.assigner != FW_SESSION) {
     make_div_inv((uint64_t)c.size, &c.mag_size, &c.l_size);
@@ -1083,22 +1085,24 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   }
   if (c.agg == FW_AGG_TDIGEST) {
     TdBuf& t = op->td;
+    // the compression sorts one item per (record, window): sliding windows fan out wpr items per record
+    const int64_t mi = mb * (c.assigner == FW_SLIDING ? c.wpr : 1);
     for (int b = 0; b < 2; b++) {
-      HIP_OR_RETURN(op, dmalloc(&t.gs[b], (size_t)mb));
-      HIP_OR_RETURN(op, dmalloc(&t.v[b], (size_t)mb));
+      HIP_OR_RETURN(op, dmalloc(&t.gs[b], (size_t)mi));
+      HIP_OR_RETURN(op, dmalloc(&t.v[b], (size_t)mi));
     }
-    t.tmp_bytes = fwdev::tdigest_sort_bytes(mb);
+    t.tmp_bytes = fwdev::tdigest_sort_bytes(mi);
     HIP_OR_RETURN(op, dmalloc((uint8_t**)&t.tmp, t.tmp_bytes));
     HIP_OR_RETURN(op, dmalloc(&t.binv, (size_t)c.pool_blocks));
     HIP_OR_RETURN(op, hipMemsetAsync(t.binv, 0xff, (size_t)c.pool_blocks * sizeof(uint32_t), op->stream));
-    HIP_OR_RETURN(op, dmalloc(&t.fixbm, (size_t)((mb + 31) / 32)));
-    HIP_OR_RETURN(op, dmalloc(&t.tslot, (size_t)mb));
-    HIP_OR_RETURN(op, dmalloc(&t.tbeg, (size_t)mb));
+    HIP_OR_RETURN(op, dmalloc(&t.fixbm, (size_t)((mi + 31) / 32)));
+    HIP_OR_RETURN(op, dmalloc(&t.tslot, (size_t)mi));
+    HIP_OR_RETURN(op, dmalloc(&t.tbeg, (size_t)mi));
     HIP_OR_RETURN(op, dmalloc(&t.ctr, 3));
     // a wave-tier digest has more than FW_TD_T1 - delta/2 values in the batch, a large one more than
     // FW_TD_T3 - delta/2
-    HIP_OR_RETURN(op, dmalloc(&t.mid, (size_t)mb));
-    t.max_large = (int32_t)(mb / std::max<int64_t>(1, FW_TD_T3 - c.td_nb) + 1);
+    HIP_OR_RETURN(op, dmalloc(&t.mid, (size_t)mi));
+    t.max_large = (int32_t)(mi / std::max<int64_t>(1, FW_TD_T3 - c.td_nb) + 1);
     HIP_OR_RETURN(op, dmalloc(&t.large, (size_t)t.max_large));
     HIP_OR_RETURN(op, dmalloc(&t.nstart, (size_t)t.max_large * c.td_nb));
     HIP_OR_RETURN(op, dmalloc(&t.ostart, (size_t)t.max_large * c.td_nb));

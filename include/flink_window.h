@@ -67,9 +67,11 @@ extern "C" {
                                       and the count (a snapshot row's sum / min / max are 0 / Long.MAX_VALUE
                                       / Long.MIN_VALUE, not value statistics).  Tumbling and sliding windows
                                       (one register block per window), any allowed lateness (a window fires
-                                      at maxTimestamp and keeps its registers until its cleanup time); not
-                                      session windows (FW_ERR_UNSUPPORTED); expected_entries sizes the
-                                      register pool (2^p B/entry). */
+                                      at maxTimestamp and keeps its registers until its cleanup time), and
+                                      session windows (merged sessions take the register max of their blocks,
+                                      AbstractHeapMergingState.mergeNamespaces; not with PurgingTrigger:
+                                      FW_ERR_UNSUPPORTED); expected_entries sizes the register pool
+                                      (2^p B/entry). */
 #define FW_AGG_FIRST 2             /* the reduce aggregations sum(pos) / min(pos) of DataStream / WindowedStream
                                       (SumAggregator.java:66-76, ComparableAggregator.java:72-94 over
                                       HeapReducingState.add, HeapReducingState.java:72-84): the result is a
@@ -93,8 +95,9 @@ extern "C" {
                                       function, compression tdigest_compression (delta), at most delta/2
                                       centroids; add buffers, and every push compresses the values it added.
                                       Rows carry count = elements and sum / min / max = the estimated quantiles
-                                      tdigest_quantiles[0..2] (f64 bits).  Tumbling windows, no allowed lateness,
-                                      FW_VAL_F64; expected_entries sizes the digest pool.  Keyed-state snapshots
+                                      tdigest_quantiles[0..2] (f64 bits).  Tumbling and sliding windows (one
+                                      digest per window), no allowed lateness, FW_VAL_F64; expected_entries
+                                      sizes the digest pool.  Keyed-state snapshots
                                       carry the digest as an accumulator block (fw_snapshot_key_group_blocks). */
 #define FW_AGG_FIRST_MAX 5         /* max(pos) (ComparableAggregator.java:72-94, Comparator.MaxComparator): as
                                       FW_AGG_FIRST, but the min column holds the field's MAXIMUM (the first

@@ -40,10 +40,14 @@ def _stream(n, batch, num_keys, rate, zipf=None, values="spread", seed=0x7D16, b
     return batches, wms
 
 
-def _run(batches, wms, delta, quantiles=(0.5, 0.95, 0.99), **kw):
+def _run(batches, wms, delta, quantiles=(0.5, 0.95, 0.99), sliding=None, **kw):
+    from flink_amd import SlidingEventTimeWindows
     from flink_amd.operator import GpuWindowOperator
-    gpu = GpuWindowOperator(TumblingEventTimeWindows.of(1000), TDigest(delta, quantiles, export=True), **kw)
-    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000, tdigest=delta, quantiles=quantiles)
+    assigner = SlidingEventTimeWindows.of(*sliding) if sliding else TumblingEventTimeWindows.of(1000)
+    gpu = GpuWindowOperator(assigner, TDigest(delta, quantiles, export=True), **kw)
+    ref = (orc.WindowOperatorOracle(assigner="sliding", size=sliding[0], slide=sliding[1], tdigest=delta,
+                                    quantiles=quantiles) if sliding else
+           orc.WindowOperatorOracle(assigner="tumbling", size=1000, tdigest=delta, quantiles=quantiles))
     g_rows, g_dig = [], []
     for epoch, ((k, t, v), wm) in enumerate(zip(batches, wms)):
         if len(k):
@@ -96,6 +100,19 @@ def test_gpu_tdigest_hot_digests(delta, values):
     assert max(len(s) for s, _ in out[1]) > delta // 4  # hot digests fill their buckets
 
 
+@pytest.mark.parametrize("size,slide,zipf,jitter", [(3000, 1000, 1.1, 200), (2000, 500, None, 900), (1000, 300, 1.1, 600)],
+                         ids=["3s-1s-zipf", "2s-500ms-uniform-late", "1s-300ms-zipf-uneven"])
+def test_gpu_tdigest_sliding_vs_oracle(size, slide, zipf, jitter):
+    # t-digest over sliding windows (WindowedStream.aggregate takes any assigner, WindowedStream.java:687-852;
+    # SlidingEventTimeWindows.assignWindows, SlidingEventTimeWindows.java:67-81): one digest per window, every
+    # element sorted into each of its windows that is not late (jitter past the bound makes elements partially
+    # late: their oldest windows are skipped, WindowOperator.java:379-407), centroids and quantiles bit-exact
+    batches, wms = _stream(200_000, 25_000, 2000, rate=100_000, zipf=zipf, jitter=jitter, bound=200)
+    out = _run(batches, wms, 40, sliding=(size, slide), expected_entries=30_000)
+    _assert_same(*out, 40)
+    assert any(len(s) > 10 for s, _ in out[1])
+
+
 def test_gpu_tdigest_blocks_are_recycled():
     # many short windows over few keys with a pool sized for one window's digests: fired blocks are reused
     batches, wms = _stream(400_000, 10_000, 500, rate=100_000, bound=50, jitter=50)
@@ -121,7 +138,9 @@ def test_gpu_tdigest_refuses_unsupported_shapes():
     from flink_amd import SlidingEventTimeWindows
     from flink_amd import _native as N
     from flink_amd.operator import GpuWindowOperator
-    for kw in (dict(assigner=SlidingEventTimeWindows.of(3000, 1000)), dict(allowed_lateness=10)):
+    from flink_amd import EventTimeSessionWindows
+    for kw in (dict(assigner=EventTimeSessionWindows.with_gap(1000)), dict(allowed_lateness=10),
+               dict(assigner=SlidingEventTimeWindows.of(3000, 1000), allowed_lateness=10)):
         with pytest.raises(N.NativeError) as e:
             GpuWindowOperator(kw.pop("assigner", TumblingEventTimeWindows.of(1000)), TDigest(100), **kw)
         assert e.value.code == N.FW_ERR_UNSUPPORTED
