@@ -244,7 +244,7 @@ def main():
     ap.add_argument("--sub-partitions", type=int, default=0, help="state partitions per key group (0 = auto)")
     ap.add_argument("--combine", action="store_true",
                     help="pre-shuffle combining (SURVEY §8e): partial accumulators instead of records cross the "
-                         "exchange (C2 only: tumbling count/sum/min/max)")
+                         "exchange (C2: tumbling count/sum/min/max; C5: HyperLogLog partial rows + non-zero registers)")
     ap.add_argument("--rehearse-gloo", action="store_true",
                     help="N > 1 on ONE GPU: every rank on cuda:0 and the Python exchange over gloo (exercises the "
                          "multi-rank bench path; RCCL cannot put two ranks on one GPU)")
@@ -330,8 +330,8 @@ def main():
         nx = NativeKeyByExchange(op, world, rank, uid[0])
     cx = comb = None
     if args.combine:
-        if w != "c2":
-            raise SystemExit("--combine: only C2 (tumbling count/sum/min/max, Long keys) combines")
+        if w not in ("c2", "c5"):
+            raise SystemExit("--combine: C2 (tumbling count/sum/min/max) and C5 (tumbling HyperLogLog) combine")
         from flink_amd.exchange import CombiningExchange
         # the combiner sees this rank's whole slice of the key space
         comb = GpuWindowOperator(assigner, agg, device=local_rank, max_parallelism=max_par,

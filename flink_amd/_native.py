@@ -144,6 +144,11 @@ SIGNATURES = {
     "fw_combine_extract_device": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwPartials), ctypes.c_int64, I64P,
                                                  I64P]),
     "fw_push_partials_device": (ctypes.c_int, [VP, ctypes.POINTER(FwPartials), ctypes.c_int64]),
+    "fw_combine_extract_hll_device": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwPartials), ctypes.c_int64,
+                                                     I64P, I64P, I64P, I64P]),
+    "fw_combine_hll_registers_device": (ctypes.c_int, [VP, ctypes.POINTER(FwPartials), ctypes.c_int64, VP,
+                                                       ctypes.c_int64]),
+    "fw_push_hll_partials_device": (ctypes.c_int, [VP, ctypes.POINTER(FwPartials), ctypes.c_int64, VP, ctypes.c_int64]),
     "fw_keyby_combine_push_device": (ctypes.c_int, [VP, VP, VP, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, I64P]),
     "fw_snapshot_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), ctypes.c_int64, I64P]),
     "fw_restore_key_group": (ctypes.c_int, [VP, ctypes.c_int32, ctypes.POINTER(FwStateRows), ctypes.c_int64]),

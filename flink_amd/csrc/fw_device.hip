@@ -5188,7 +5188,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS) void k_extract(DevCfg c, DevTable 
       out.start[o] = e.start;
       out.cnt[o] = e.cnt;
       out.sum[o] = e.sum;
-      out.mn[o] = e.mn;
+      out.mn[o] = c.agg == FW_AGG_HLL ? (int64_t)pool_block_of(e) : e.mn;  // (HLL: k_hll_extract reads it)
       out.mx[o] = e.mx;
     }
     if (s < R && !c.dense) r.state[s] = SLOT_EMPTY;
@@ -5236,8 +5236,10 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_pscatter(DevCfg c, int64_t 
 __global__ __launch_bounds__(FW_AGG_THREADS) void k_pmerge(DevCfg c, const PartialRec* __restrict__ part,
                                                           const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
                                                           AggProg prog, int resume, Status* st) {
-  c.pool_bytes = 0;
-  c.agg = FW_AGG_COUNT_SUM_MIN_MAX;
+  if (c.agg != FW_AGG_HLL) {  // (HLL partials: their counts merge here, new windows take blocks; registers follow)
+    c.pool_bytes = 0;
+    c.agg = FW_AGG_COUNT_SUM_MIN_MAX;
+  }
   __shared__ AggLds L;
   const int32_t p = blockIdx.x;
   if (p >= c.P || (resume && prog.done[p])) return;
@@ -5307,6 +5309,186 @@ __global__ __launch_bounds__(FW_AGG_THREADS) void k_pmerge(DevCfg c, const Parti
     prog.done[p] = 1;
   }
   if (threadIdx.x == 0) agg_publish(c, L, tb, p, st);
+}
+
+// ---- HyperLogLog partials (pre-shuffle combining): a combined window crosses the exchange as its
+// partial row (key, start, count; sum = how many of its registers are non-zero) and those registers as u32
+// (index << 8 | rank), in partial order.  The receiver merges the counts like any partial (k_pmerge creates the
+// windows and their blocks) and raises the registers into the blocks: AggregateFunction.merge = register max
+// (AggregateFunction.java:160), so the result equals pushing the records themselves.
+__device__ __forceinline__ void hll_raise_jr(const DevCfg& c, uint64_t blk, uint32_t j, uint32_t rank) {
+  uint8_t* base = c.pool + blk * (uint64_t)c.pool_bytes;
+  uint32_t* w = reinterpret_cast<uint32_t*>(base + hll_hdr_bytes(c.hll_p) + (j & ~3u));
+  const int sh = (int)(j & 3) * 8;
+  uint32_t o = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (((o >> sh) & 0xffu) < rank) {
+    const uint32_t nw = (o & ~(0xffu << sh)) | (rank << sh);
+    if (__hip_atomic_compare_exchange_strong(w, &o, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      if (((o >> sh) & 0xffu) == 0u) {
+        const uint32_t ch = j >> 4;
+        atomicOr(reinterpret_cast<uint32_t*>(base) + (ch >> 5), 1u << (ch & 31u));
+      }
+      break;
+    }
+  }
+}
+// combiner side (the block id is in mn, k_extract).  A thread per partial; a partial of more than HLL_WAVE_CNT
+// records (a hot key's window: up to 2^p registers) is taken by its whole wave afterwards, lane l over the block's
+// bitmap words l, l + 64, ... (a word covers 32 chunks of 16 registers).  Pass 1 counts the non-zero registers;
+// pass 2 writes them at the scanned offsets in index order, then zeroes and frees the block (the combiner is
+// emptied).
+constexpr int64_t HLL_WAVE_CNT = 256;
+__device__ __forceinline__ uint32_t hll_nz16(const uint4 v) {
+  const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+  uint32_t k = 0;
+#pragma unroll
+  for (int u = 0; u < 4; u++)
+#pragma unroll
+    for (int y = 0; y < 32; y += 8) k += ((ws[u] >> y) & 0xffu) != 0u;
+  return k;
+}
+// the non-zero registers of block blk's bitmap words w0, w0 + ws, ... (ws = 1: one thread, 64: a wave's lane)
+__device__ __forceinline__ uint32_t hll_count_words(const DevCfg& c, uint64_t blk, int32_t w0, int32_t ws) {
+  const uint8_t* base = c.pool + blk * (uint64_t)c.pool_bytes;
+  const uint32_t* bits = reinterpret_cast<const uint32_t*>(base);
+  const uint4* q = reinterpret_cast<const uint4*>(base + hll_hdr_bytes(c.hll_p));
+  const int32_t nw = (int32_t)((((int64_t)1 << c.hll_p) / 16 + 31) / 32);
+  uint32_t k = 0;
+  for (int32_t w = w0; w < nw; w += ws) {
+    uint32_t word = bits[w];
+    while (word) {
+      const int b = __ffs(word) - 1;
+      word &= word - 1;
+      k += hll_nz16(q[w * 32 + b]);
+    }
+  }
+  return k;
+}
+// writes word w's registers from position o on, zeroes its chunks and the word; returns the new position
+__device__ __forceinline__ uint64_t hll_take_word(const DevCfg& c, uint64_t blk, int32_t w, uint64_t o,
+                                                  uint32_t* __restrict__ regs) {
+  uint8_t* base = c.pool + blk * (uint64_t)c.pool_bytes;
+  uint32_t* bits = reinterpret_cast<uint32_t*>(base);
+  uint4* q = reinterpret_cast<uint4*>(base + hll_hdr_bytes(c.hll_p));
+  uint32_t word = bits[w];
+  if (!word) return o;
+  while (word) {
+    const int b = __ffs(word) - 1;
+    word &= word - 1;
+    const int32_t ch = w * 32 + b;
+    const uint4 v = q[ch];
+    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+#pragma unroll
+      for (int y = 0; y < 4; y++) {
+        const uint32_t rank = (ws[u] >> (8 * y)) & 0xffu;
+        if (rank) regs[o++] = ((uint32_t)(ch * 16 + u * 4 + y) << 8) | rank;
+      }
+    q[ch] = make_uint4(0, 0, 0, 0);
+  }
+  bits[w] = 0u;
+  return o;
+}
+__global__ __launch_bounds__(256) void k_hll_extract_counts(DevCfg c, PartialCols out, int64_t n,
+                                                            uint32_t* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = __lane_id();
+  const bool in = i < n;
+  const bool big = in && out.cnt[i] > HLL_WAVE_CNT;
+  const uint64_t blk = in ? (uint64_t)out.mn[i] : 0;
+  if (in && !big) {
+    const uint32_t k = hll_count_words(c, blk, 0, 1);
+    out.sum[i] = (int64_t)k;
+    cnt[i] = k;
+  }
+  uint64_t m = __ballot(big);
+  while (m) {
+    const int src = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const uint64_t b = (uint64_t)__shfl((long long)blk, src, 64);
+    uint32_t k = hll_count_words(c, b, lane, 64);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) k += (uint32_t)__shfl_xor((int)k, o, 64);
+    if (lane == src) {
+      out.sum[i] = (int64_t)k;
+      cnt[i] = k;
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_hll_extract_regs(DevCfg c, PartialCols out, int64_t n,
+                                                          const uint32_t* __restrict__ off, uint32_t* __restrict__ regs) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = __lane_id();
+  const bool in = i < n;
+  const bool big = in && out.cnt[i] > HLL_WAVE_CNT;
+  const uint64_t blk = in ? (uint64_t)out.mn[i] : 0;
+  const int32_t nw = (int32_t)((((int64_t)1 << c.hll_p) / 16 + 31) / 32);
+  if (in && !big) {
+    uint64_t o = off[i];
+    for (int32_t w = 0; w < nw; w++) o = hll_take_word(c, blk, w, o, regs);
+  }
+  uint64_t m = __ballot(big);
+  while (m) {
+    const int src = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const uint64_t b = (uint64_t)__shfl((long long)blk, src, 64);
+    uint64_t o0 = (uint64_t)__shfl((long long)(in ? off[i] : 0), src, 64);
+    for (int32_t w0 = 0; w0 < nw; w0 += 64) {
+      const int32_t w = w0 + lane;
+      const uint32_t mine = w < nw ? hll_count_words(c, b, w, nw) : 0u;  // (this word only)
+      uint32_t x = mine;  // inclusive prefix over the lanes (words in order)
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (w < nw) (void)hll_take_word(c, b, w, o0 + x - mine, regs);
+      o0 += (uint64_t)__shfl((int)x, 63, 64);
+    }
+  }
+  if (in) {
+    out.mn[i] = LMAX;  // (the partial's min / max are not value statistics for HLL)
+    __threadfence();
+    c.pool_free[atomicAdd(&c.pool_ctr[0], 1)] = (uint32_t)blk;
+  }
+}
+// receiver: each partial's registers raised into its window's block (a late or foreign partial was dropped and
+// counted by the scatter); regs of partial i start at off[i]
+// (a thread per partial; one with more than 64 registers is raised by its whole wave afterwards)
+__global__ __launch_bounds__(256) void k_hll_push_regs(DevCfg c, int64_t wm, PartialCols in, int64_t n,
+                                                       const uint32_t* __restrict__ regs,
+                                                       const uint32_t* __restrict__ off, DevTable tb, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // rerun when resumed
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = __lane_id();
+  int64_t blk = -1;
+  uint64_t b0 = 0, b1 = 0;
+  if (i < n) {
+    const int64_t key = in.key[i], start = in.start[i];
+    const int32_t p = partition_of(c, key, key_hash_of(c.key_kind, key, nullptr, i));
+    if (p >= 0 && classify(c, wm, start) == CLS_NORMAL) {
+      const Region r = region_of(c, tb, p, tb.cur[p]);
+      const int32_t slot = region_find(r, slot_hash(c, key, start), key, start, wend(c, start));
+      if (slot < 0)
+        atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // k_pmerge stored every partial's window
+      else
+        blk = (int64_t)pool_block_of(r.ent[slot]);
+      b0 = off[i];
+      b1 = b0 + (uint64_t)in.sum[i];
+    }
+  }
+  const bool big = blk >= 0 && b1 - b0 > 64;
+  if (blk >= 0 && !big)
+    for (uint64_t k = b0; k < b1; k++) hll_raise_jr(c, (uint64_t)blk, regs[k] >> 8, regs[k] & 0xffu);
+  uint64_t m = __ballot(big);
+  while (m) {
+    const int src = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const uint64_t b = (uint64_t)__shfl((long long)blk, src, 64);
+    const uint64_t s0 = (uint64_t)__shfl((long long)b0, src, 64), s1 = (uint64_t)__shfl((long long)b1, src, 64);
+    for (uint64_t k = s0 + lane; k < s1; k += 64) hll_raise_jr(c, b, regs[k] >> 8, regs[k] & 0xffu);
+  }
 }
 
 // out3 = {live entries, event-time timers}
@@ -6623,6 +6805,30 @@ void launch_live_offsets(const DevCfg& c, DevTable tb, uint32_t* offs, uint32_t*
 }
 void launch_extract(const DevCfg& c, DevTable tb, const uint32_t* offs, PartialCols out, hipStream_t s) {
   hipLaunchKernelGGL(k_extract, dim3(c.P), dim3(FW_FIRE_THREADS), 0, s, c, tb, offs, out);
+}
+void launch_hll_extract_counts(const DevCfg& c, PartialCols out, int64_t n, uint32_t* cnt, uint32_t* scan_tmp,
+                               hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_hll_extract_counts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c, out, n, cnt);
+  (void)hipMemsetAsync(cnt + n, 0, sizeof(uint32_t), s);
+  launch_scan(cnt, n + 1, scan_tmp, s);  // in place: offsets, cnt[n] = total
+}
+void launch_hll_extract_regs(const DevCfg& c, PartialCols out, int64_t n, const uint32_t* off, uint32_t* regs,
+                             hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_hll_extract_regs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c, out, n, off, regs);
+}
+__global__ void k_hll_reg_counts(PartialCols in, int64_t n, uint32_t* __restrict__ off) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= n) off[i] = i < n ? (uint32_t)in.sum[i] : 0u;
+}
+void launch_hll_reg_offsets(PartialCols in, int64_t n, uint32_t* off, uint32_t* scan_tmp, hipStream_t s) {
+  hipLaunchKernelGGL(k_hll_reg_counts, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, in, n, off);
+  launch_scan(off, n + 1, scan_tmp, s);  // off[i] = partial i's first register, off[n] = their total
+}
+void launch_hll_push_regs(const DevCfg& c, int64_t wm, PartialCols in, int64_t n, const uint32_t* regs,
+                          const uint32_t* off, DevTable tb, Status* st, hipStream_t s) {
+  if (n > 0)
+    hipLaunchKernelGGL(k_hll_push_regs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c, wm, in, n, regs, off, tb, st);
 }
 void launch_pscatter(const DevCfg& c, int64_t wm, PartialCols in, int64_t n, int32_t T, uint32_t* offs, PartialRec* part,
                      Status* st, hipStream_t s) {

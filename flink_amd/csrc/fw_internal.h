@@ -436,6 +436,16 @@ size_t count_sort_bytes(int64_t n);
 void launch_rehash(const DevCfg& old_c, DevTable old_t, const DevCfg& new_c, DevTable new_t, hipStream_t_ s);
 void launch_table_stats(const DevCfg& c, DevTable tb, unsigned long long* out3, hipStream_t_ s);
 void launch_reset_regions(const DevCfg& c, DevTable tb, hipStream_t_ s);
+// HyperLogLog partials (combining): pass 1 counts each partial's non-zero registers into cnt[0, n) and scans it in
+// place (cnt[n] = total; scan_tmp: launch_scan's for n + 1 words); pass 2 writes them at those offsets and frees the
+// blocks; the receiver's offsets are the scan of the partials' sum column, then the registers are raised
+void launch_hll_extract_counts(const DevCfg& c, PartialCols out, int64_t n, uint32_t* cnt, uint32_t* scan_tmp,
+                               hipStream_t_ s);
+void launch_hll_extract_regs(const DevCfg& c, PartialCols out, int64_t n, const uint32_t* off, uint32_t* regs,
+                             hipStream_t_ s);
+void launch_hll_reg_offsets(PartialCols in, int64_t n, uint32_t* off, uint32_t* scan_tmp, hipStream_t_ s);
+void launch_hll_push_regs(const DevCfg& c, int64_t wm, PartialCols in, int64_t n, const uint32_t* regs,
+                          const uint32_t* off, DevTable tb, Status* st, hipStream_t_ s);
 // combining: offs[P+1] = exclusive scan of the regions' live counts (scratch: launch_scan's)
 void launch_live_offsets(const DevCfg& c, DevTable tb, uint32_t* offs, uint32_t* scratch, hipStream_t_ s);
 void launch_extract(const DevCfg& c, DevTable tb, const uint32_t* offs, PartialCols out, hipStream_t_ s);

@@ -52,6 +52,12 @@ struct Scratch {
   int32_t* wide = nullptr;       // DevCfg::wide of the batches that use this set
   PartialRec* pparts = nullptr;  // combining: a partials push's partials, partition-major (allocated on first use)
   bool partials = false;         // the set's latest push merged partials (fw_push_partials_device)
+  // HyperLogLog partials (fw_push_hll_partials_device): the push's partials, registers and register offsets, for
+  // the register raise that follows the merge (rerun after a resumed merge)
+  PartialCols hin{};
+  int64_t hn = 0;
+  const uint32_t* hregs = nullptr;
+  const uint32_t* hoff = nullptr;
   // gathered batches (fwdev::gather_mode): runs table [T8][P] and its transpose, the partitions' virtual
   // offsets (P + 1) and the ordered-path rows (2 x T8); T is then the batch's FW_GTILE tiles
   uint32_t *rt = nullptr, *rt_t = nullptr, *voffs = nullptr, *gsrow = nullptr, *gcb = nullptr;
@@ -87,6 +93,10 @@ struct fw_op {
   bool rsv_off = false;      // after 3 of them the operator stops trying the single pass
   int64_t single_batches = 0;  // batches that took the single pass (fw_stats)
   uint32_t *xoffs = nullptr, *xscan = nullptr;  // combining: the combiner's live-count offsets and scan scratch
+  // HyperLogLog combining: the extracted partials' register offsets (combiner) / the pushed ones' (receiver), with
+  // their scan scratch and capacities
+  uint32_t *xreg = nullptr, *xreg_tmp = nullptr, *hoff = nullptr, *hoff_tmp = nullptr;
+  int64_t xreg_cap = 0, hoff_cap = 0, xreg_n = -1;
   std::string err;
 
   // state table
@@ -509,6 +519,8 @@ int settle(fw_op* op) {
       c.nt_floor = fwdev::pane_nt_floor(c, S.wm);  // (panes: a new pane's first window)
       timed(op, K_AGGREGATE, [&] {
         fwdev::launch_pmerge(c, S.pparts, S.hist, S.T, op->tb, op->prog, 1, op->d_status, op->stream);
+        if (S.hregs)  // (register max is idempotent: the whole push's registers again)
+          fwdev::launch_hll_push_regs(c, S.wm, S.hin, S.hn, S.hregs, S.hoff, op->tb, op->d_status, op->stream);
       });
       if (op->fire_unsettled)
         timed(op, K_FIRE, [&] { fwdev::launch_fire(c, op->wm, op->tb, op->out, op->d_status, op->stream); });
@@ -791,10 +803,16 @@ bool combine_eligible(const fw_config& c) {
   return (c.assigner == FW_TUMBLING || panes) && c.aggregate == FW_AGG_COUNT_SUM_MIN_MAX &&
          c.allowed_lateness == 0 && !c.side_output && (c.key_kind == FW_KEY_LONG || c.key_kind == FW_KEY_INT);
 }
+// HyperLogLog partials (register lists): tumbling windows, no allowed lateness, Long or Integer keys
+bool combine_eligible_hll(const fw_config& c) {
+  return c.assigner == FW_TUMBLING && c.aggregate == FW_AGG_HLL && c.allowed_lateness == 0 && !c.side_output &&
+         (c.key_kind == FW_KEY_LONG || c.key_kind == FW_KEY_INT);
+}
 // what a partial's representation depends on (fw_partials.config); never 0, so a zeroed struct never matches
 uint64_t combine_config_tag(const fw_config& c) {
   const int64_t f[] = {c.assigner, c.size, c.offset, c.value_type, c.key_kind, c.max_parallelism, c.aggregate,
-                       c.assigner == FW_SLIDING ? c.slide : 0};
+                       c.assigner == FW_SLIDING ? c.slide : 0,
+                       c.aggregate == FW_AGG_HLL ? (c.hll_precision ? c.hll_precision : 14) : 0};
   uint64_t h = 0x9E3779B97F4A7C15ull;
   for (int64_t x : f) {
     h ^= (uint64_t)x + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
@@ -804,7 +822,8 @@ uint64_t combine_config_tag(const fw_config& c) {
   }
   return h | 1;
 }
-int push_partials(fw_op* op, const PartialCols& in, int64_t n) {
+int push_partials(fw_op* op, const PartialCols& in, int64_t n, const uint32_t* hregs = nullptr,
+                  const uint32_t* hoff = nullptr) {
   int rc;
   if ((rc = settle(op)) || (rc = maybe_restart_rows(op))) return rc;
   const int nxt = op->last_sc ^ 1;
@@ -826,9 +845,15 @@ int push_partials(fw_op* op, const PartialCols& in, int64_t n) {
   c.nt_floor = fwdev::pane_nt_floor(c, op->wm);  // (panes: a new pane's first window, lds_delta)
   timed(op, K_AGGREGATE, [&] {
     fwdev::launch_pmerge(c, S.pparts, S.hist, T, op->tb, op->prog, 0, op->d_status, op->stream);
+    // HyperLogLog: the partials' registers into their windows' blocks (skipped behind a suspended merge)
+    if (hregs) fwdev::launch_hll_push_regs(c, op->wm, in, n, hregs, hoff, op->tb, op->d_status, op->stream);
   });
   HIP_OR_RETURN(op, hipGetLastError());
   HIP_OR_RETURN(op, hipEventRecord(op->ev_done[nxt], op->stream));
+  S.hin = in;
+  S.hn = n;
+  S.hregs = hregs;
+  S.hoff = hoff;
   S.T = T;
   S.n = n;
   S.partials = true;
@@ -1230,6 +1255,10 @@ void fw_destroy(fw_op* op) {
   dfree(op->d_stats3);
   dfree(op->xoffs);
   dfree(op->xscan);
+  dfree(op->xreg);
+  dfree(op->xreg_tmp);
+  dfree(op->hoff);
+  dfree(op->hoff_tmp);
   for (auto& pr : op->prof_pending) {
     (void)hipEventDestroy(pr.a);
     (void)hipEventDestroy(pr.b);
@@ -1495,13 +1524,21 @@ int fw_profile_read(fw_op* op, double* ms, int64_t* launches, int reset) {
 
 const char* fw_kernel_name(int kind) { return kind >= 0 && kind < FW_NUM_KERNELS ? KERNEL_NAMES[kind] : ""; }
 
+static int fw_combine_extract_device_any(fw_op* op, int32_t world, fw_partials* out, int64_t cap, int64_t* counts,
+                                         int64_t* n);
 int fw_combine_extract_device(fw_op* op, int32_t world, fw_partials* out, int64_t cap, int64_t* counts,
                               int64_t* n) {
   if (!op || !n || world < 1 || (world > 1 && !counts)) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
   if (!combine_eligible(op->cfg))
     return set_err(op, FW_ERR_UNSUPPORTED,
                    "combining needs tumbling windows or sliding windows kept as panes, the count/sum/min/max aggregate, no "
-                   "allowed lateness, no side output and Long or Integer keys");
+                   "allowed lateness, no side output and Long or Integer keys (HyperLogLog: "
+                   "fw_combine_extract_hll_device)");
+  return fw_combine_extract_device_any(op, world, out, cap, counts, n);
+}
+// the drain itself (count/sum/min/max and HyperLogLog partial rows alike)
+static int fw_combine_extract_device_any(fw_op* op, int32_t world, fw_partials* out, int64_t cap, int64_t* counts,
+                                  int64_t* n) {
   if (op->wm != INT64_MIN)
     return set_err(op, FW_ERR_STATE, "a combiner's watermark is never advanced (it would fire or drop partials)");
   if (world > op->cfg.max_parallelism) return set_err(op, FW_ERR_ARG, "more subtasks than key groups");
@@ -1555,6 +1592,107 @@ int fw_push_partials_device(fw_op* op, const fw_partials* in, int64_t n) {
     const int64_t m = std::min(op->max_batch, n - b);
     const int rc = push_partials(op, PartialCols{in->key + b, in->start + b, in->cnt + b, in->sum + b, in->min + b,
                                                  in->max + b}, m);
+    if (rc) return rc;
+  }
+  return FW_OK;
+}
+
+namespace {
+int grow_u32(fw_op* op, uint32_t** p, uint32_t** tmp, int64_t* cap, int64_t need) {
+  if (need <= *cap) return FW_OK;
+  const int64_t c = std::max<int64_t>(need, 2 * *cap);
+  dfree(*p);
+  dfree(*tmp);
+  *cap = 0;
+  HIP_OR_RETURN(op, dmalloc(p, (size_t)c));
+  HIP_OR_RETURN(op, dmalloc(tmp, (size_t)c / 4096 + 2));
+  *cap = c;
+  return FW_OK;
+}
+}  // namespace
+
+int fw_combine_extract_hll_device(fw_op* op, int32_t world, fw_partials* out, int64_t cap, int64_t* counts,
+                                  int64_t* reg_counts, int64_t* n, int64_t* nregs) {
+  if (!op || !n || !nregs || world < 1 || (world > 1 && (!counts || !reg_counts)))
+    return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
+  if (!combine_eligible_hll(op->cfg))
+    return set_err(op, FW_ERR_UNSUPPORTED, "HyperLogLog combining needs tumbling windows, no allowed lateness, no side "
+                                           "output and Long or Integer keys");
+  if (op->xreg_n >= 0)
+    return set_err(op, FW_ERR_STATE, "the previous extraction's registers were not taken (fw_combine_hll_registers_device)");
+  int rc = fw_combine_extract_device_any(op, world, out, cap, counts, n);
+  if (rc) return rc;
+  *nregs = 0;
+  if (reg_counts)
+    for (int32_t d = 0; d < world; d++) reg_counts[d] = 0;
+  const DevCfg& c = op->dc;
+  if (*n > 0) {
+    if ((rc = grow_u32(op, &op->xreg, &op->xreg_tmp, &op->xreg_cap, *n + 1))) return rc;
+    const PartialCols pc{out->key, out->start, out->cnt, out->sum, out->min, out->max};
+    fwdev::launch_hll_extract_counts(c, pc, *n, op->xreg, op->xreg_tmp, op->stream);
+    HIP_OR_RETURN(op, hipGetLastError());
+    // the register offsets at every destination's first partial (its partials are one contiguous slice)
+    std::vector<uint32_t> at((size_t)world + 1);
+    int64_t first = 0;
+    for (int32_t d = 0; d <= world; d++) {
+      HIP_OR_RETURN(op, hipMemcpyAsync(&at[(size_t)d], op->xreg + first, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                       op->stream));
+      if (d < world) first += counts ? counts[d] : *n;
+    }
+    HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
+    *nregs = at[(size_t)world];
+    for (int32_t d = 0; reg_counts && d < world; d++) reg_counts[d] = (int64_t)at[(size_t)d + 1] - (int64_t)at[(size_t)d];
+  }
+  op->xreg_n = *n;
+  return FW_OK;
+}
+
+int fw_combine_hll_registers_device(fw_op* op, const fw_partials* out, int64_t n, uint32_t* regs, int64_t regs_cap) {
+  if (!op || !out || n < 0) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
+  if (op->xreg_n < 0 || n != op->xreg_n)
+    return set_err(op, FW_ERR_STATE, "no extraction of %lld HyperLogLog partials to take the registers of", (long long)n);
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  if (n > 0) {
+    uint32_t total = 0;
+    HIP_OR_RETURN(op, hipMemcpy(&total, op->xreg + n, sizeof total, hipMemcpyDeviceToHost));
+    if ((int64_t)total > regs_cap)
+      return set_err(op, FW_ERR_CAPACITY, "%lld registers do not fit the %lld-entry output", (long long)total,
+                     (long long)regs_cap);
+    if (total > 0 && !regs) return set_err(op, FW_ERR_ARG, "null register output");
+    fwdev::launch_hll_extract_regs(op->dc, PartialCols{out->key, out->start, out->cnt, out->sum, out->min, out->max}, n,
+                                   op->xreg, regs, op->stream);
+    HIP_OR_RETURN(op, hipGetLastError());
+    HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
+  }
+  op->xreg_n = -1;
+  return FW_OK;
+}
+
+int fw_push_hll_partials_device(fw_op* op, const fw_partials* in, int64_t n, const uint32_t* regs, int64_t nregs) {
+  if (!op || !in || n < 0 || nregs < 0) return op ? set_err(op, FW_ERR_ARG, "null argument") : FW_ERR_ARG;
+  if (!combine_eligible_hll(op->cfg))
+    return set_err(op, FW_ERR_UNSUPPORTED, "HyperLogLog combining needs tumbling windows, no allowed lateness, no side "
+                                           "output and Long or Integer keys");
+  if (n > 0 && (!in->key || !in->start || !in->cnt || !in->sum || !in->min || !in->max || (nregs > 0 && !regs)))
+    return set_err(op, FW_ERR_ARG, "null column");
+  if (in->config != combine_config_tag(op->cfg))
+    return set_err(op, FW_ERR_ARG,
+                   "partials from a combiner configured differently (assigner, size, offset, value type, key kind, max "
+                   "parallelism, aggregate or precision) than this operator");
+  if (n == 0) return FW_OK;
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  int rc;
+  // the previous push settled first: a resumed merge of it reruns its register raise with the offsets it had
+  if ((rc = settle(op))) return rc;
+  if ((rc = grow_u32(op, &op->hoff, &op->hoff_tmp, &op->hoff_cap, n + 1))) return rc;
+  const PartialCols all{in->key, in->start, in->cnt, in->sum, in->min, in->max};
+  fwdev::launch_hll_reg_offsets(all, n, op->hoff, op->hoff_tmp, op->stream);
+  HIP_OR_RETURN(op, hipGetLastError());
+  for (int64_t b = 0; b < n; b += op->max_batch) {
+    const int64_t m = std::min(op->max_batch, n - b);
+    // (the offsets index the whole register list: partial b + i's are at hoff[b + i])
+    rc = push_partials(op, PartialCols{in->key + b, in->start + b, in->cnt + b, in->sum + b, in->min + b, in->max + b}, m,
+                       regs, op->hoff + b);
     if (rc) return rc;
   }
   return FW_OK;
@@ -1906,6 +2044,9 @@ struct fw_comm {
   int64_t pcap = 0;                                       // combining: partials the send / receive columns hold
   int64_t* ps[6] = {};                                    // send partials (key, start, cnt, sum, min, max)
   int64_t* pr[6] = {};                                    // received partials
+  uint32_t *rs = nullptr, *rr = nullptr;                  // HyperLogLog partials' registers: sent / received
+  int64_t rscap = 0, rrcap = 0;
+  int64_t *rgc = nullptr, *h_rgc = nullptr;               // their per-peer counts [2 world] (device / pinned host)
 };
 namespace {
 template <class T>
@@ -2030,7 +2171,11 @@ void fw_comm_destroy(fw_comm* c) {
     cfree(c->pr[i]);
   }
   cfree(c->scratch);
+  cfree(c->rs);
+  cfree(c->rr);
+  cfree(c->rgc);
   if (c->h_counts) (void)hipHostFree(c->h_counts);
+  if (c->h_rgc) (void)hipHostFree(c->h_rgc);
   delete c;
 }
 
@@ -2147,6 +2292,8 @@ int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64
     return set_err(op, FW_ERR_ARG,
                    "the combiner is configured differently (assigner, size, offset, value type, key kind, max "
                    "parallelism or aggregate) than the operator");
+  // HyperLogLog: the partial rows travel with their non-zero registers (fw_combine_extract_hll_device)
+  const bool hll = op->cfg.aggregate == FW_AGG_HLL;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;
   // the batch into the combiner, ordered after the columns' producer (the caller's fw_stream(op) order)
@@ -2156,11 +2303,15 @@ int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64
   HIP_OR_RETURN(op, hipStreamWaitEvent(comb->stream, ready, 0));
   (void)hipEventDestroy(ready);
   if ((rc = push_device_batches(comb, key, ts, val, nullptr, n, false))) return set_err(op, rc, "%s", comb->err.c_str());
-  // drain it: the partials in key-group order, per-peer counts
-  std::vector<int64_t> counts(W);
-  int64_t np = 0;
+  // drain it: the partials in key-group order, per-peer counts (and, for HLL, per-peer register counts)
+  std::vector<int64_t> counts(W), rcounts(W, 0);
+  int64_t np = 0, nr = 0;
+  auto extract = [&](fw_partials* o) {
+    return hll ? fw_combine_extract_hll_device(comb, W, o, c->pcap, counts.data(), rcounts.data(), &np, &nr)
+               : fw_combine_extract_device(comb, W, o, c->pcap, counts.data(), &np);
+  };
   fw_partials out{c->ps[0], c->ps[1], c->ps[2], c->ps[3], c->ps[4], c->ps[5]};
-  rc = fw_combine_extract_device(comb, W, &out, c->pcap, counts.data(), &np);
+  rc = extract(&out);
   if (rc == FW_ERR_CAPACITY && np > c->pcap) {
     const int64_t cap = std::max<int64_t>(np, 2 * c->pcap);
     for (int i = 0; i < 6; i++) {
@@ -2171,9 +2322,19 @@ int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64
     }
     c->pcap = cap;
     out = fw_partials{c->ps[0], c->ps[1], c->ps[2], c->ps[3], c->ps[4], c->ps[5]};
-    rc = fw_combine_extract_device(comb, W, &out, c->pcap, counts.data(), &np);
+    rc = extract(&out);
   }
   if (rc) return set_err(op, rc, "%s", comb->err.c_str());
+  if (hll) {  // the registers, in partial order (each destination's one slice)
+    if (nr > c->rscap) {
+      const int64_t cap = std::max<int64_t>(nr, 2 * c->rscap);
+      cfree(c->rs);
+      c->rscap = 0;
+      HIP_OR_RETURN(op, dmalloc(&c->rs, (size_t)cap));
+      c->rscap = cap;
+    }
+    if ((rc = fw_combine_hll_registers_device(comb, &out, np, c->rs, c->rscap))) return set_err(op, rc, "%s", comb->err.c_str());
+  }
   hipStream_t s = op->stream;
   for (int p = 0; p < W; p++) c->h_counts[p] = counts[p];
   c->h_counts[2 * W] = local_wm;
@@ -2181,12 +2342,37 @@ int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64
   HIP_OR_RETURN(op, hipMemcpyAsync(c->counts, c->h_counts, W * sizeof(int64_t), hipMemcpyHostToDevice, s));
   HIP_OR_RETURN(op, hipMemcpyAsync(c->counts + 2 * W, c->h_counts + 2 * W, 3 * sizeof(int64_t), hipMemcpyHostToDevice, s));
   if ((rc = comm_counts_round(op, c, s))) return rc;
-  std::vector<int64_t> soff(W + 1, 0), roff(W + 1, 0);
+  std::vector<int64_t> soff(W + 1, 0), roff(W + 1, 0), rsoff(W + 1, 0), rroff(W + 1, 0);
   fw_exchange_plan_t pl;
   if ((rc = fw_exchange_plan(W, c->rank, c->h_counts, soff.data(), roff.data(), &pl)))
     return set_err(op, rc, "exchange: inconsistent counts round (received %lld partials of %lld)",
                    (long long)pl.recv_total, (long long)pl.recv_bound);
   const int64_t total = pl.recv_total;
+  int64_t rtotal = 0;
+  if (hll) {  // the register counts: one more all-to-all (the receive sizes of the register lists)
+    if (!c->rgc) {
+      HIP_OR_RETURN(op, dmalloc(&c->rgc, 2 * (size_t)W));
+      HIP_OR_RETURN(op, hipHostMalloc((void**)&c->h_rgc, 2 * (size_t)W * sizeof(int64_t), hipHostMallocDefault));
+    }
+    for (int p = 0; p < W; p++) c->h_rgc[p] = rcounts[p];
+    HIP_OR_RETURN(op, hipMemcpyAsync(c->rgc, c->h_rgc, W * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    NCCL_OR_RETURN(op, ncclAllToAll(c->rgc, c->rgc + W, 1, ncclInt64, c->nc, s));
+    HIP_OR_RETURN(op, hipMemcpyAsync(c->h_rgc, c->rgc, 2 * W * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_OR_RETURN(op, hipStreamSynchronize(s));
+    for (int p = 0; p < W; p++) {
+      rsoff[p + 1] = rsoff[p] + c->h_rgc[p];
+      rroff[p + 1] = rroff[p] + c->h_rgc[W + p];
+    }
+    rtotal = rroff[W];
+    if (rtotal > c->rrcap) {
+      cfree(c->rr);
+      const int64_t cap = std::max<int64_t>(rtotal, 2 * c->rrcap);
+      c->rrcap = 0;
+      HIP_OR_RETURN(op, dmalloc(&c->rr, (size_t)cap));
+      c->rrcap = cap;
+      c->stats.recv_reallocs++;
+    }
+  }
   if (pl.recv_bound > c->pcap) {  // the receive columns for every partial of the batch (the bound): grow both sides
     const int64_t cap = std::max<int64_t>(pl.recv_bound, 2 * c->pcap);
     for (int i = 0; i < 6; i++) {
@@ -2207,6 +2393,16 @@ int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64
     c->stats.recv_reallocs++;
   }
   comm_account(c, pl, 48);
+  if (hll) {
+    int64_t rs_other = 0, rr_other = 0;
+    for (int p = 0; p < W; p++)
+      if (p != c->rank) {
+        rs_other += c->h_rgc[p];
+        rr_other += c->h_rgc[W + p];
+      }
+    c->stats.bytes_sent += 4 * rs_other;
+    c->stats.bytes_received += 4 * rr_other;
+  }
   NCCL_OR_RETURN(op, ncclGroupStart());
   for (int p = 0; p < W; p++) {
     const size_t sc = (size_t)c->h_counts[p], rcn = (size_t)c->h_counts[W + p];
@@ -2214,11 +2410,15 @@ int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64
       NCCL_IN_GROUP(op, ncclSend(c->ps[i] + soff[p], sc, ncclInt64, p, c->nc, s));
       NCCL_IN_GROUP(op, ncclRecv(c->pr[i] + roff[p], rcn, ncclInt64, p, c->nc, s));
     }
+    if (hll) {
+      NCCL_IN_GROUP(op, ncclSend(c->rs + rsoff[p], (size_t)c->h_rgc[p], ncclUint32, p, c->nc, s));
+      NCCL_IN_GROUP(op, ncclRecv(c->rr + rroff[p], (size_t)c->h_rgc[W + p], ncclUint32, p, c->nc, s));
+    }
   }
   NCCL_OR_RETURN(op, ncclGroupEnd());
   if (combined_wm) *combined_wm = c->h_counts[2 * W + 1];
   const fw_partials in{c->pr[0], c->pr[1], c->pr[2], c->pr[3], c->pr[4], c->pr[5], out.config};
-  return fw_push_partials_device(op, &in, total);
+  return hll ? fw_push_hll_partials_device(op, &in, total, c->rr, rtotal) : fw_push_partials_device(op, &in, total);
 }
 
 int fw_generate_device(uint64_t seed, int64_t first, int64_t n, int64_t num_keys, const double* zipf_cdf,

@@ -204,6 +204,8 @@ class CombiningExchange:
         import torch.distributed as dist
         ex = self.exchange
         self.combiner.process_batch(keys, ts, vals)
+        if self.combiner.aggregate.aggregate_kind() == N.FW_AGG_HLL:
+            return self._push_hll(op, keys, local_wm)
         cols, counts = self.combiner.combine_extract(ex.world)
         config = cols.config
         if ex.world > 1:
@@ -226,4 +228,37 @@ class CombiningExchange:
         else:  # the combiner reuses its output buffers; the operator reads the partials asynchronously
             cols = tuple(c.clone() for c in cols)
         op.push_partials(*cols, config=config)
+        return ex.combine_watermark(local_wm, device=keys.device)
+
+    def _push_hll(self, op, keys, local_wm):
+        """HyperLogLog partials: the rows and, per destination, their registers (index << 8 | rank) cross the
+        exchange; the receiver merges the counts and raises the registers (register max)."""
+        import torch
+        import torch.distributed as dist
+        ex = self.exchange
+        cols, counts, regs, rcounts = self.combiner.combine_extract_hll(ex.world)
+        config = cols.config
+        if ex.world > 1:
+            staged = cols[0].is_cuda and dist.get_backend(ex.group) == "gloo"
+            move = (lambda x: x.cpu()) if staged else (lambda x: x)
+            back = (lambda x: x.to(keys.device)) if staged else (lambda x: x)
+
+            def a2a(col, send_split):
+                send = move(torch.tensor(send_split, dtype=torch.int64, device=keys.device))
+                recv = torch.empty_like(send)
+                dist.all_to_all_single(recv, send, group=ex.group)
+                out_split = recv.tolist()
+                col = move(col)
+                r = torch.empty(sum(out_split), dtype=col.dtype, device=col.device)
+                dist.all_to_all_single(r, col, output_split_sizes=out_split, input_split_sizes=send_split,
+                                       group=ex.group)
+                return back(r)
+            cols = tuple(a2a(c, counts) for c in cols)
+            regs = a2a(regs, rcounts)
+            self.partials_sent += sum(counts) - counts[ex.rank]
+            self.registers_sent = getattr(self, "registers_sent", 0) + sum(rcounts) - rcounts[ex.rank]
+        else:  # the combiner reuses its output buffers; the operator reads the partials asynchronously
+            cols = tuple(c.clone() for c in cols)
+            regs = regs.clone()
+        op.push_hll_partials(*cols, regs=regs, config=config)
         return ex.combine_watermark(local_wm, device=keys.device)

@@ -210,6 +210,60 @@ class GpuWindowOperator:
         cols.config = out.config
         return cols, list(counts)
 
+    def combine_extract_hll(self, world=1):
+        """HyperLogLog combining (fw_combine_extract_hll_device + fw_combine_hll_registers_device): drains this
+        combiner into partial rows (six int64 columns; a row's sum = how many non-zero registers it carries) in
+        key-group order and their registers (uint32 index << 8 | rank, in row order).  Returns (cols, counts,
+        regs, reg_counts): per destination subtask its rows and its registers, each one contiguous slice.  The
+        columns are views of buffers the handle reuses: consume them before the next call."""
+        import torch
+        L = N.lib()
+        dev = torch.device("cuda", self.device)
+        counts = (ctypes.c_int64 * world)()
+        rcounts = (ctypes.c_int64 * world)()
+        n, nr = ctypes.c_int64(), ctypes.c_int64()
+        while True:
+            bufs = getattr(self, "_pbuf", None)
+            cap = bufs[0].numel() if bufs else 0
+            out = N.FwPartials(*(t.data_ptr() for t in bufs)) if bufs else N.FwPartials()
+            rc = L.fw_combine_extract_hll_device(self._h, world, ctypes.byref(out), cap, counts, rcounts,
+                                                 ctypes.byref(n), ctypes.byref(nr))
+            if rc == N.FW_ERR_CAPACITY and n.value > cap:
+                self._pbuf = [torch.empty(max(n.value, 2 * cap), dtype=torch.int64, device=dev) for _ in range(6)]
+                continue
+            N.check(rc, self._h)
+            break
+        rb = getattr(self, "_rbuf", None)
+        if rb is None or rb.numel() < max(nr.value, 1):
+            self._rbuf = rb = torch.empty(max(nr.value, 2 * (rb.numel() if rb is not None else 0), 1),
+                                          dtype=torch.int32, device=dev)
+        N.check(L.fw_combine_hll_registers_device(self._h, ctypes.byref(out), n.value, rb.data_ptr(), rb.numel()),
+                self._h)
+        cols = Partials((t[:n.value] for t in self._pbuf) if n.value else
+                        (torch.empty(0, dtype=torch.int64, device=dev) for _ in range(6)))
+        cols.config = out.config
+        return cols, list(counts), rb[:nr.value], list(rcounts)
+
+    def push_hll_partials(self, key, start, cnt, sum_, min_, max_, regs, config):
+        """fw_push_hll_partials_device: merges HyperLogLog partial rows (from combine_extract_hll of a combiner with
+        this operator's configuration) and raises their registers (`regs`: the rows' register lists in row order,
+        int32 / uint32 bits)."""
+        import torch
+        cols = (key, start, cnt, sum_, min_, max_)
+        n = key.numel()
+        for t in cols:
+            if not t.is_cuda or not t.is_contiguous() or t.numel() != n or t.dtype != torch.int64:
+                raise ValueError("partials must be contiguous int64 CUDA tensors of equal length")
+        if not regs.is_cuda or not regs.is_contiguous() or regs.dtype != torch.int32:
+            raise ValueError("registers must be a contiguous int32 CUDA tensor")
+        if n == 0:
+            return
+        self._torch_stream(key.device).wait_stream(torch.cuda.current_stream(key.device))
+        p = N.FwPartials(*(t.data_ptr() for t in cols), config)
+        N.check(N.lib().fw_push_hll_partials_device(self._h, ctypes.byref(p), n, regs.data_ptr() if regs.numel() else None,
+                                                    regs.numel()), self._h)
+        self._inflight = cols + (regs,)
+
     def push_partials(self, key, start, cnt, sum_, min_, max_, config):
         """fw_push_partials_device: merges partial accumulators (from combine_extract of a combiner with the same
         configuration; `config` = that extraction's Partials.config tag, checked against this handle's own) of this

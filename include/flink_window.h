@@ -350,6 +350,24 @@ int fw_route_device(const int64_t* key, const int64_t* ts, const int64_t* val, c
                     int64_t scratch_bytes, void* stream);
 int64_t fw_route_scratch_bytes(int64_t n, int32_t parallelism);
 
+/* Pre-shuffle combining of HyperLogLog ("combining is results-equal for count/sum/min/max/HLL"): a
+ * combiner's windows cross the exchange as partial rows plus their non-zero registers, the receiver merges them
+ * with AggregateFunction.merge = register max (flink-core/.../AggregateFunction.java:160).  Tumbling windows, no
+ * allowed lateness, Long or Integer keys (FW_ERR_UNSUPPORTED otherwise).
+ *   fw_combine_extract_hll_device: drains the combiner like fw_combine_extract_device; a row's sum = how many of
+ *     its window's registers are non-zero (min holds an opaque block id until the registers are taken),
+ *     reg_counts[d] = the registers of destination d's partials (in partial order), *nregs their total.
+ *   fw_combine_hll_registers_device: then writes the n rows' registers into regs[0, nregs) as u32
+ *     (register index << 8 | rank), in row order, and releases the combiner's blocks (FW_ERR_CAPACITY, with
+ *     nothing taken, when regs_cap < nregs; FW_ERR_STATE without a preceding extraction of n rows).
+ *   fw_push_hll_partials_device: merges received partial rows (counts) and raises their registers (regs: the rows'
+ *     register lists concatenated in row order) into this operator's windows; late rows are dropped with their
+ *     records, as fw_push_partials_device does. */
+int fw_combine_extract_hll_device(fw_op* op, int32_t world, fw_partials* out, int64_t cap, int64_t* counts,
+                                  int64_t* reg_counts, int64_t* n, int64_t* nregs);
+int fw_combine_hll_registers_device(fw_op* op, const fw_partials* out, int64_t n, uint32_t* regs, int64_t regs_cap);
+int fw_push_hll_partials_device(fw_op* op, const fw_partials* in, int64_t n, const uint32_t* regs, int64_t nregs);
+
 /* keyBy across the GPUs of one node behind the C-ABI (the RecordWriter -> KeyGroupStreamPartitioner ->
  * network -> input gate path: flink-runtime/.../io/network/api/writer/RecordWriter.java:88-115,
  * runtime/partitioner/KeyGroupStreamPartitioner.java:53-65; watermark valve runtime/streamstatus/

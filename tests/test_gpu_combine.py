@@ -117,6 +117,51 @@ def test_gpu_combine_panes_world1_vs_oracle(value_type):
     op.close()
 
 
+def _hll_rows_equal(g, r):
+    ks = lambda a: a[np.lexsort((a["start"], a["key"], a["epoch"]))]  # noqa: E731
+    g, r = ks(g), ks(r)
+    assert len(g) == len(r) > 0
+    for f in ("epoch", "key", "start", "end", "count", "min", "max"):
+        assert np.array_equal(g[f], r[f]), f
+    np.testing.assert_allclose(g["sum"].view(np.float64), r["sum"].view(np.float64), rtol=1e-9)
+
+
+@pytest.mark.parametrize("zipf,p", [(1.1, 12), (None, 6)], ids=["zipf-p12", "uniform-p6"])
+def test_gpu_combine_hll_world1_vs_oracle(zipf, p):
+    # HyperLogLog combines before the shuffle -- a combined window is its count and its non-zero
+    # registers, the receiver takes the register max (AggregateFunction.merge, AggregateFunction.java:160); rows
+    # (count, zero registers, the register checksum, the estimate) equal the oracle fed the records; late partials
+    # count their records
+    import torch
+    from flink_amd import HyperLogLog
+    from flink_amd.operator import GpuWindowOperator
+    k, t, v = generate_host(0x5EED, 0, 400_000, 3000, ts_base=1_000_000, rate=200_000, jitter=900, zipf_s=zipf)
+    comb = GpuWindowOperator(TumblingEventTimeWindows.of(1000), HyperLogLog(p), device=0, expected_entries=8000)
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(1000), HyperLogLog(p), device=0, expected_entries=8000)
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000, hll_p=p)
+    rows, sent, regs_sent, mx = [], 0, 0, -(1 << 63)
+    for b in range(0, len(k), 40_000):
+        sl = slice(b, b + 40_000)
+        mx = max(mx, int(t[sl].max()))
+        comb.process_batch(*(torch.from_numpy(np.ascontiguousarray(x[sl])).cuda() for x in (k, t, v)))
+        cols, counts, regs, rcounts = comb.combine_extract_hll(1)
+        assert counts == [cols[0].numel()] and rcounts == [regs.numel()] == [int(cols[3].sum())]
+        sent += cols[0].numel()
+        regs_sent += regs.numel()
+        op.push_hll_partials(*(c.clone() for c in cols), regs=regs.clone(), config=cols.config)
+        ref.process(k[sl], t[sl], v[sl])
+        rows.append(op.process_watermark(mx - 300))
+        ref.watermark(mx - 300)
+    rows.append(op.process_watermark((1 << 63) - 1))
+    ref.watermark((1 << 63) - 1)
+    _hll_rows_equal(np.concatenate(rows), ref.rows())
+    assert op.late_dropped == ref.late_dropped > 0
+    assert op.stats()["records_in"] == len(k)
+    assert sent < len(k) // 4 and regs_sent <= len(k)  # a register per distinct item at most
+    comb.close()
+    op.close()
+
+
 def test_gpu_combine_rejects_foreign_key_groups_and_ineligible_configs():
     import torch
     from flink_amd import _native as N
@@ -152,19 +197,21 @@ def _slice(rank, step):
 
 def _assigner(kind):
     from flink_amd import SlidingEventTimeWindows
-    return TumblingEventTimeWindows.of(1000) if kind == "tumbling" else SlidingEventTimeWindows.of(5000, 1000)
+    return SlidingEventTimeWindows.of(5000, 1000) if kind == "panes" else TumblingEventTimeWindows.of(1000)
 
 
 def _worker(rank, port, out_dir, kind="tumbling"):
     import torch
     import torch.distributed as dist
+    from flink_amd import HyperLogLog
     from flink_amd.exchange import CombiningExchange, KeyGroupExchange
     from flink_amd.operator import GpuWindowOperator
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     ex = KeyGroupExchange(MAX_PAR, WORLD, rank)
-    op = GpuWindowOperator(_assigner(kind), max_parallelism=MAX_PAR, key_group_range=ex.key_group_range, device=0)
-    comb = GpuWindowOperator(_assigner(kind), max_parallelism=MAX_PAR, device=0)
+    agg = HyperLogLog(10) if kind == "hll" else CountSumMinMax()
+    op = GpuWindowOperator(_assigner(kind), agg, max_parallelism=MAX_PAR, key_group_range=ex.key_group_range, device=0)
+    comb = GpuWindowOperator(_assigner(kind), agg, max_parallelism=MAX_PAR, device=0)
     cx = CombiningExchange(ex, comb)
     mx = -(1 << 63)
     dev = torch.device("cuda", 0)
@@ -182,7 +229,7 @@ def _worker(rank, port, out_dir, kind="tumbling"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["tumbling", "panes"])
+@pytest.mark.parametrize("kind", ["tumbling", "panes", "hll"])
 def test_gpu_combining_exchange_world2(kind):
     import tempfile
 
@@ -191,8 +238,8 @@ def test_gpu_combining_exchange_world2(kind):
         mp.spawn(_worker, args=(_free_port(), d, kind), nprocs=WORLD, join=True)
         rows = np.concatenate([np.load(os.path.join(d, f"rows_{r}.npy")) for r in range(WORLD)])
         sent = [np.load(os.path.join(d, f"sent_{r}.npy")) for r in range(WORLD)]
-    ref = (orc.WindowOperatorOracle(assigner="tumbling", size=1000) if kind == "tumbling"
-           else orc.WindowOperatorOracle(assigner="sliding", size=5000, slide=1000))
+    ref = (orc.WindowOperatorOracle(assigner="sliding", size=5000, slide=1000) if kind == "panes"
+           else orc.WindowOperatorOracle(assigner="tumbling", size=1000, hll_p=10 if kind == "hll" else 0))
     mx = [-(1 << 63)] * WORLD
     for s in range(STEPS):
         sl = [_slice(r, s) for r in range(WORLD)]
@@ -201,21 +248,27 @@ def test_gpu_combining_exchange_world2(kind):
             mx[r] = max(mx[r], int(sl[r][1].max()))
         ref.watermark(min(mx) - 300)
     ref.watermark((1 << 63) - 1)
-    assert_rows_equal(rows, ref.rows())
+    if kind == "hll":
+        _hll_rows_equal(rows, ref.rows())
+    else:
+        assert_rows_equal(rows, ref.rows())
     assert sum(int(x[1]) for x in sent) == ref.late_dropped
     assert 0 < sum(int(x[0]) for x in sent) < WORLD * STEPS * BATCH // 4
 
 
-def test_gpu_native_keyby_combine_world1():
+@pytest.mark.parametrize("hll", [False, True], ids=["count_sum", "hll"])
+def test_gpu_native_keyby_combine_world1(hll):
     # the C-ABI combining exchange over the library's own RCCL communicator, one subtask: combiner push, drain,
-    # counts, self send/recv of the partials, merge
+    # counts, self send/recv of the partials (and, for HyperLogLog, of their registers), merge
     import torch
+    from flink_amd import HyperLogLog
     from flink_amd.exchange import NativeKeyByExchange
     from flink_amd.operator import GpuWindowOperator
-    op = GpuWindowOperator(TumblingEventTimeWindows.of(1000), max_parallelism=MAX_PAR, device=0)
-    comb = GpuWindowOperator(TumblingEventTimeWindows.of(1000), max_parallelism=MAX_PAR, device=0)
+    agg = HyperLogLog(10) if hll else CountSumMinMax()
+    op = GpuWindowOperator(TumblingEventTimeWindows.of(1000), agg, max_parallelism=MAX_PAR, device=0)
+    comb = GpuWindowOperator(TumblingEventTimeWindows.of(1000), agg, max_parallelism=MAX_PAR, device=0)
     ex = NativeKeyByExchange(op, 1, 0, NativeKeyByExchange.new_unique_id())
-    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000)
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000, hll_p=10 if hll else 0)
     mx = -(1 << 63)
     dev = torch.device("cuda", 0)
     for s in range(2 * STEPS):
@@ -228,7 +281,11 @@ def test_gpu_native_keyby_combine_world1():
         ref.watermark(mx - 300)
     op.watermark((1 << 63) - 1)
     ref.watermark((1 << 63) - 1)
-    assert_rows_equal(op.rows(), ref.rows())
+    if hll:
+        _hll_rows_equal(op.rows(), ref.rows())
+        assert ex.stats()["batches"] == 2 * STEPS
+    else:
+        assert_rows_equal(op.rows(), ref.rows())
     assert op.late_dropped == ref.late_dropped
     ex.close()
     comb.close()
