@@ -1792,6 +1792,23 @@ __device__ void hll_merge_blocks(const DevCfg& c, uint64_t dst, uint64_t src) {
   __threadfence();  // (zeroed before its id can be handed out)
   c.pool_defer[atomicAdd(&c.pool_ctr[2], 1)] = (uint32_t)src;
 }
+// AggregateFunction.merge of two accumulator blocks as sessions merge: HyperLogLog raises dst to the register max
+// now; a t-digest logs the pair, and the push's compression merges the centroid lists (launch_tdigest)
+__device__ __forceinline__ void pool_merge_blocks(const DevCfg& c, uint64_t dst, uint64_t src) {
+  if (c.agg == FW_AGG_HLL) {
+    hll_merge_blocks(c, dst, src);
+  } else if (c.agg == FW_AGG_TDIGEST) {
+    const int i = atomicAdd(c.td_mctr, 1);
+    c.td_mdst[i] = (uint32_t)dst;
+    c.td_msrc[i] = (uint32_t)src;
+  }
+}
+// a new window's accumulator block (an empty t-digest, or HyperLogLog's zero registers)
+__device__ __forceinline__ uint64_t pool_new_block(const DevCfg& c, Status* st) {
+  const uint64_t blk = pool_alloc_one(c, st);
+  if (c.agg == FW_AGG_TDIGEST) *reinterpret_cast<TdHead*>(c.pool + blk * (uint64_t)c.pool_bytes) = TdHead{0, 0, 0};
+  return blk;
+}
 // MergingWindowSet.addWindow (MergingWindowSet.java:156-225) of a session delta d (an interval with
 // its accumulator) into the key's in-flight sessions of region r: d's connected component becomes one
 // session (merge function + mergeNamespaces, WindowOperator.java:308-339,
@@ -1840,7 +1857,7 @@ __device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, con
         continue;
       }
       acc_merge(c, m, e);
-      if (c.pool_bytes) hll_merge_blocks(c, pool_block_of(m), pool_block_of(e));  // (HLL: register max)
+      if (c.pool_bytes) pool_merge_blocks(c, pool_block_of(m), pool_block_of(e));
       m.start = min(m.start, e.start);
       m.end = max(m.end, e.end);
       // the slot stays occupied (live counts occupied slots) until k_fire rebuilds the region
@@ -1855,7 +1872,7 @@ __device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, con
       return 0;
     }
     Entry nd = d;
-    if (c.pool_bytes) nd.meta |= (int64_t)(pool_alloc_one(c, st) << 1);  // (HLL: zero registers; k_hll_update fills)
+    if (c.pool_bytes) nd.meta |= (int64_t)(pool_new_block(c, st) << 1);  // (filled after the aggregate)
     r.ent[ns] = nd;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __hip_atomic_store(r.state + ns, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2714,7 +2731,7 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
     ne.start = ws;
     ne.end = we;
     acc_clear(ne);
-    ne.meta = c.agg == FW_AGG_HLL ? (int64_t)(pool_alloc_one(c, x.st) << 1) : 0;
+    ne.meta = c.pool_bytes ? (int64_t)(pool_new_block(c, x.st) << 1) : 0;
     actual = new_slot(x, r, p, h, ne);
     if (actual < 0) return;
     fresh = true;
@@ -2737,20 +2754,20 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
         const Entry& e = r.ent[s];
         if (e.key != k || !(ws <= e.end && we >= e.start)) continue;
         acc_merge(c, m, e);  // mergeNamespaces
-        if (c.agg == FW_AGG_HLL) hll_merge_blocks(c, pool_block_of(m), pool_block_of(e));  // (register max)
+        if (c.pool_bytes) pool_merge_blocks(c, pool_block_of(m), pool_block_of(e));
         kill_slot(x, r, p, (int32_t)s);
       }
       m.start = cs;
       m.end = ce;
       // EventTimeTrigger.onMerge registers maxTimestamp unconditionally (the block id stays above the timer bit)
-      m.meta = c.agg == FW_AGG_HLL ? (m.meta | FW_TIMER) : FW_TIMER;
+      m.meta = c.pool_bytes ? (m.meta | FW_TIMER) : FW_TIMER;
       r.ent[actual] = m;
     }
   }
   Entry en = r.ent[actual];
   if (cleanup_of(en.end, c.lateness) <= x.wm) {  // isWindowLate(actualWindow) -> retireWindow
     if (fresh) {
-      if (c.agg == FW_AGG_HLL) {  // its (untouched, zero) block on the deferred list
+      if (c.pool_bytes) {  // its (untouched) block on the deferred list
         __threadfence();
         c.pool_defer[atomicAdd(&c.pool_ctr[2], 1)] = (uint32_t)pool_block_of(en);
       }
@@ -2761,6 +2778,13 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
   *skipped = false;
   acc_add(c, en, v, fo);
   if (c.agg == FW_AGG_HLL) hll_raise(c, pool_block_of(en), v);  // (k_hll_update takes the partitioned records)
+  if (c.agg == FW_AGG_TDIGEST) {  // the value joins the push's compression (allowed lateness 0: nothing fires here)
+    const int j = atomicAdd(c.td_ovctr, 1);
+    c.td_ovk[j] = k;
+    c.td_ovt[j] = t;
+    c.td_ovv[j] = v;
+    c.td_ovp[j] = p;
+  }
   if (jsub(en.end, 1) <= x.wm) {
     if (c.agg == FW_AGG_HLL) {  // getResult from the session's registers (it stays in flight)
       Entry fr = en;
@@ -3661,6 +3685,22 @@ __device__ int32_t td_finish(const DevCfg& c, const DevRows& out, uint64_t row, 
 // value key's high 64 - B bits below) and the value key's low B bits as the payload, so one radix sort groups a
 // digest's values and orders them up to ties in the high bits (k_td_fix orders those by the low bits). Positions
 // past the partitioned records get the block `nblk` (sorted last, skipped). binv[blk] = the digest's global slot.
+// the slot of key's in-flight session that contains [ts, ts + gap) (sessions hash the key only: one probe chain),
+// -1 if none
+__device__ __forceinline__ int32_t session_containing(const Region& r, const DevCfg& c, int64_t key, int64_t ts) {
+  const uint64_t h = slot_hash(c, key, 0);
+  const uint32_t want = live_word(h);
+  const int64_t te = jadd(ts, c.gap);
+  for (uint32_t k = 0; k <= r.mask; k++) {
+    const uint32_t s = ((uint32_t)h + k) & r.mask;
+    const uint32_t w = r.state[s];
+    if (w == SLOT_EMPTY) return -1;
+    if (w != want) continue;
+    const Entry& e = r.ent[s];
+    if (e.key == key && e.start <= ts && te <= e.end) return (int32_t)s;
+  }
+  return -1;
+}
 constexpr int TD_CHUNK = 4096;
 __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restrict__ part, const uint32_t* __restrict__ offs,
                                                  int32_t T, int64_t n, DevTable tb, uint32_t nblk, int B,
@@ -3689,34 +3729,51 @@ __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restric
   }
   __syncthreads();
   const bool cmp = c.compact && !*c.wide;
+  const bool sess = c.assigner == FW_SESSION;
+  // sessions: the ordered path's added elements follow the partitioned records (positions total .. total + nov)
+  const int64_t nov = sess ? (int64_t)*c.td_ovctr : 0;
   int32_t pp = p0_s;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     int nw = 0;
-    if (i < total) {
-      while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
+    if (i < total + nov) {
       PRec rec;
-      if (cmp) {
-        const i64x2 r = reinterpret_cast<const i64x2*>(part)[i];
-        compact_decode(c, pp, r.x, &rec.key, &rec.last);
-        rec.val = r.y;
-        rec.nwin = 1;
+      int32_t rp;
+      if (i < total) {
+        while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
+        rp = pp;
+        if (cmp) {
+          const i64x2 r = reinterpret_cast<const i64x2*>(part)[i];
+          compact_decode(c, pp, r.x, &rec.key, &rec.last);
+          rec.val = r.y;
+          rec.nwin = 1;
+        } else {
+          rec = part[i];
+        }
       } else {
-        rec = part[i];
+        const int64_t j = i - total;
+        rec.key = c.td_ovk[j];
+        rec.last = c.td_ovt[j];
+        rec.val = c.td_ovv[j];
+        rec.nwin = 1;
+        rp = c.td_ovp[j];
       }
       nw = W == 1 ? 1 : (int)(rec.nwin & 0xffff);
-      const Region r = region_of(c, tb, pp, tb.cur[pp]);
+      const Region r = region_of(c, tb, rp, tb.cur[rp]);
       const uint64_t k = td_key(rec.val);
       for (int wi = 0; wi < nw; wi++) {
         const int64_t o = i * W + wi;
         const int64_t s = jsub(rec.last, (int64_t)wi * c.slide);
-        const int32_t slot = region_find(r, slot_hash(c, rec.key, s), rec.key, s, wend(c, s));
+        // (sessions: the in-flight session of the key that holds the element's window [ts, ts + gap) -- after the
+        // push's merges exactly one does; tumbling / sliding: the window's own entry)
+        const int32_t slot = sess ? session_containing(r, c, rec.key, rec.last) :
+                                    region_find(r, slot_hash(c, rec.key, s), rec.key, s, wend(c, s));
         if (slot < 0) {
           atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's window
           key64[o] = none_key;
           pay[o] = 0;
           continue;
         }
-        const uint32_t g = ((uint32_t)pp << c.log_r) | (uint32_t)slot;
+        const uint32_t g = ((uint32_t)rp << c.log_r) | (uint32_t)slot;
         const uint64_t blk = pool_block_of(r.ent[slot]);
         // every record of a digest stores the same slot, so a stale (cached) read costs one redundant store at
         // most; a hot digest's records read it (an L1 hit) and store nothing
@@ -3730,6 +3787,96 @@ __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restric
       pay[i * W + wi] = 0;
     }
   }
+}
+
+// ---- t-digest session merges (DevCfg::td_mdst / td_msrc, logged by the session flush and the ordered replay):
+// AggregateFunction.merge of digests = the union of their centroids, compressed with the batch's values
+// (oracle/window_oracle.cpp td_union).  A merge chain (a block merged into one that is merged further) ends at one
+// final target per merged session; its union of old centroids is built once, and the tiers read it instead of the
+// target's live half.
+__global__ void k_td_mlink(DevCfg c, TdBuf td) {
+  const int32_t nl = *c.td_mctr;
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += gridDim.x * blockDim.x)
+    td.fwd[c.td_msrc[i]] = c.td_mdst[i];
+}
+__device__ __forceinline__ uint32_t td_final_target(const TdBuf& td, uint32_t b) {
+  while (td.fwd[b] != ~0u) b = td.fwd[b];
+  return b;
+}
+__global__ void k_td_mlist(DevCfg c, TdBuf td) {
+  const int32_t nl = *c.td_mctr;
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += gridDim.x * blockDim.x) {
+    const uint32_t t = td_final_target(td, c.td_mdst[i]);
+    const int32_t prev = atomicExch(&td.mhead[t], i);
+    td.mnext[i] = prev < 0 ? -2 : prev;  // -2: the list's last entry (the first in), which builds the union
+  }
+}
+__global__ void k_td_mbuild(DevCfg c, TdBuf td, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int32_t nl = *c.td_mctr;
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += gridDim.x * blockDim.x) {
+    if (td.mnext[i] != -2) continue;
+    const uint32_t t = td_final_target(td, c.td_mdst[i]);
+    // the target's centroids and every merged block's (weights for now), then freed sources
+    int32_t m = 0;
+    const TdHead ht = *td_head(c, t);
+    m += ht.n;
+    for (int32_t j = td.mhead[t]; j >= 0; j = td.mnext[j]) {
+      m += td_head(c, c.td_msrc[j])->n;
+      if (td.mnext[j] == -2) break;
+    }
+    const unsigned long long off = atomicAdd(&td.uctr[0], (unsigned long long)m);
+    TdCent* u = td.uni + off;
+    int32_t k = 0;
+    int64_t wold = 0;
+    auto take = [&](uint64_t b) {
+      const TdHead h = *td_head(c, b);
+      const TdCent* ce = td_half(c, b, h.cur);
+      for (int32_t q = 0; q < h.n; q++) u[k++] = TdCent{ce[q].sum, td_weight(ce, q)};
+      wold += h.w;
+    };
+    take(t);
+    for (int32_t j = td.mhead[t]; j >= 0; j = td.mnext[j]) {
+      take(c.td_msrc[j]);
+      c.pool_defer[atomicAdd(&c.pool_ctr[2], 1)] = c.td_msrc[j];  // (a t-digest block needs no zeroing)
+      if (td.mnext[j] == -2) break;
+    }
+    // ordered by (mean key, weight, sum key) -- insertion sort, then the weights made cumulative
+    for (int32_t a = 1; a < m; a++) {
+      const TdCent x = u[a];
+      const uint64_t xm = td_mean_key(x.sum, x.cum), xs = td_key(__double_as_longlong(x.sum));
+      int32_t b = a - 1;
+      while (b >= 0) {
+        const uint64_t ym = td_mean_key(u[b].sum, u[b].cum);
+        const bool after = ym > xm || (ym == xm && (u[b].cum > x.cum ||
+                                                    (u[b].cum == x.cum && td_key(__double_as_longlong(u[b].sum)) > xs)));
+        if (!after) break;
+        u[b + 1] = u[b];
+        b--;
+      }
+      u[b + 1] = x;
+    }
+    int64_t cum = 0;
+    for (int32_t a = 0; a < m; a++) {
+      cum += u[a].cum;
+      u[a].cum = cum;
+    }
+    const uint32_t g = td.binv[t];  // (the merging element was added to the target: k_td_keys set it)
+    const int32_t ov = (int32_t)atomicAdd(&td.uctr[1], 1ull);
+    td.ovr[ov] = TdOverride{u, m, g, wold};
+    td.mover[g] = ov;
+  }
+}
+// after the tiers: the push's merge bookkeeping back to empty
+__global__ void k_td_mclear(DevCfg c, TdBuf td) {
+  const int32_t nl = *c.td_mctr;
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += gridDim.x * blockDim.x) {
+    td.fwd[c.td_msrc[i]] = ~0u;
+    td.mhead[c.td_msrc[i]] = -1;
+    td.mhead[c.td_mdst[i]] = -1;
+  }
+  const int32_t no = (int32_t)td.uctr[1];
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < no; i += gridDim.x * blockDim.x) td.mover[td.ovr[i].slot] = -1;
 }
 
 // tie runs: positions with the previous one's key (one digest, equal high value bits) and a smaller payload mark
@@ -3840,14 +3987,25 @@ __global__ __launch_bounds__(256) void k_td_small(DevCfg c, DevTable tb, TdBuf t
       const uint64_t blk = pool_block_of(e);
       TdHead* hp = td_head(c, blk);
       const TdHead h = *hp;
-      const int64_t W = e.cnt, nn = W - h.w;
       const TdCent* old = td_half(c, blk, h.cur);
+      int32_t no = h.n;
+      int64_t hw = h.w;
+      if (td.mover) {  // a merged session's digest: the union of the merged digests' centroids (k_td_mbuild)
+        const int32_t ov = td.mover[g];
+        if (ov >= 0) {
+          const TdOverride o = td.ovr[ov];
+          old = o.old;
+          no = o.no;
+          hw = o.wold;
+        }
+      }
+      const int64_t W = e.cnt, nn = W - hw;
       TdCent* out = td_half(c, blk, h.cur ^ 1);
       td.lidx[g] = -1;
-      if (nn + h.n <= FW_TD_T1) {
-        const int32_t k = td_merge_serial(c, c.td_qb, v, beg, nn, old, h.n, out, W);
+      if (nn + no <= FW_TD_T1) {
+        const int32_t k = td_merge_serial(c, c.td_qb, v, beg, nn, old, no, out, W);
         *hp = TdHead{h.cur ^ 1, k, W};
-      } else if (nn + h.n <= FW_TD_T3) {
+      } else if (nn + no <= FW_TD_T3) {
         mid = true;
       } else {
         const int32_t L = atomicAdd(&td.ctr[1], 1);
@@ -3855,7 +4013,7 @@ __global__ __launch_bounds__(256) void k_td_small(DevCfg c, DevTable tb, TdBuf t
           atomicOr(&st->flags, FW_STATUS_STATE_LOST);
         } else {
           td.lidx[g] = L;
-          td.large[L] = TdLarge{beg, nn, W, h.n, h.cur ^ 1, old, out, hp};
+          td.large[L] = TdLarge{beg, nn, W, no, h.cur ^ 1, old, out, hp};
           for (int b = 0; b < c.td_nb; b++) {
             td.nstart[(int64_t)L * c.td_nb + b] = -1;
             td.ostart[(int64_t)L * c.td_nb + b] = -1;
@@ -3947,6 +4105,15 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
       TdHead* hp = td_head(c, blk);
       const TdHead h = *hp;
       d = TdLarge{td.tbeg[idx], e.cnt - h.w, e.cnt, h.n, h.cur ^ 1, td_half(c, blk, h.cur), td_half(c, blk, h.cur ^ 1), hp};
+      if (td.mover) {  // a merged session's digest (k_td_mbuild)
+        const int32_t ov = td.mover[g];
+        if (ov >= 0) {
+          const TdOverride o = td.ovr[ov];
+          d.old = o.old;
+          d.no = o.no;
+          d.nn = e.cnt - o.wold;
+        }
+      }
     }
     const double W = (double)d.W;
     double my_osum[4];  // this lane's old sums (j = lane + 64 u), staged into LDS once the keys are no longer read
@@ -6741,6 +6908,11 @@ void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int
   (void)hipMemsetAsync(td.fixbm, 0, (size_t)((n + 31) / 32) * sizeof(uint32_t), s);
   hipLaunchKernelGGL(k_td_keys, dim3((unsigned)((nrec + TD_CHUNK - 1) / TD_CHUNK)), dim3(256), 0, s, c, part, offs, T,
                      nrec, tb, nblk, B, td.gs[0], td.v[0], td.binv, st);
+  if (c.assigner == FW_SESSION) {  // the push's session merges: each merged digest's union of old centroids
+    hipLaunchKernelGGL(k_td_mlink, dim3(64), dim3(256), 0, s, c, td);
+    hipLaunchKernelGGL(k_td_mlist, dim3(64), dim3(256), 0, s, c, td);
+    hipLaunchKernelGGL(k_td_mbuild, dim3(64), dim3(256), 0, s, c, td, st);
+  }
   // one sort by (pool block, high value bits): each digest's batch values become one run, in Double.compare
   // order once the tie runs are ordered by their low bits
   rocprim::double_buffer<uint64_t> kv(td.v[0], td.v[1]);
@@ -6763,6 +6935,7 @@ void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int
   hipLaunchKernelGGL(k_td_large_items, dim3(grid), dim3(256), 0, s, c, n, gsorted, vsorted, none, td, st);
   hipLaunchKernelGGL(k_td_large_groups, dim3(2048), dim3(256), 0, s, c, vsorted, td, st);
   hipLaunchKernelGGL(k_td_large_compact, dim3(64), dim3(64), 0, s, c, td, st);
+  if (c.assigner == FW_SESSION) hipLaunchKernelGGL(k_td_mclear, dim3(64), dim3(256), 0, s, c, td);
 }
 void launch_rehash(const DevCfg& oc, DevTable ot, const DevCfg& nc, DevTable nt, hipStream_t s) {
   if (oc.dense)

@@ -126,6 +126,13 @@ struct DevCfg {
   // blocks freed by a session merge while the aggregate or the ordered path may pop others (already zeroed):
   // pushed on the free stack by the next firing (k_pool_release), when nothing pops
   uint32_t* pool_defer;
+  // t-digest over session windows (merging): the session merges of a push, logged by the session flush and the
+  // ordered replay (target block, merged block; td_mctr[0] entries), and the ordered path's added elements (key,
+  // timestamp, value; td_ovctr[0]) for the compression at the end of the push
+  uint32_t *td_mdst, *td_msrc;
+  int32_t* td_mctr;
+  int64_t *td_ovk, *td_ovt, *td_ovv;
+  int32_t *td_ovp, *td_ovctr;  // (the added element's state partition)
   int64_t pool_blocks;
   int64_t pool_bytes;     // 0 = no pool
   // FW_AGG_TDIGEST (definition: oracle/window_oracle.h OR_AGG_TDIGEST): td_nb = delta / 2 buckets of the
@@ -304,6 +311,12 @@ struct TdLarge {  // a digest whose batch is compressed bucket-parallel
   TdCent* out;              // the other half (group sums per bucket, then the centroids)
   TdHead* head;
 };
+struct TdOverride {  // a merged digest's old centroids (instead of its live half) and their total weight
+  const TdCent* old;
+  int32_t no;
+  uint32_t slot;  // the digest's global slot (its mover entry)
+  int64_t wold;
+};
 struct TdBuf {
   uint32_t* gs[2];          // low value bits (sort payload), then the global slot (partition << log_r | slot)
   uint64_t* v[2];           // (pool block, high value bits) sort keys, then the Double.compare-ordered value
@@ -323,6 +336,16 @@ struct TdBuf {
   int64_t lidx_slots;
   int32_t max_large;
   int32_t sel;              // which of gs / v holds the sorted batch (set by launch_tdigest)
+  // session merges (DevCfg::td_mdst / td_msrc): a merged digest's old centroids are the union of its own and of the
+  // digests merged into it, ordered by (mean, weight, sum), built once per push into `uni`; the tiers read them
+  // through the override of the digest's slot
+  uint32_t* fwd;            // [pool blocks] the block a block was merged into (~0: none)
+  int32_t* mhead;           // [pool blocks] a final target's list of merge-log entries (-1: none)
+  int32_t* mnext;           // [pool blocks] next entry of that list (-1: end); -2: the entry that builds the union
+  int32_t* mover;           // [table slots] override index of a digest's slot (-1: none)
+  TdOverride* ovr;          // [pool blocks]
+  TdCent* uni;              // [pool blocks * td_nb] the unions' centroids
+  unsigned long long* uctr; // [2]: centroids of `uni` taken, overrides taken
 };
 
 // ---- count windows (FW_COUNT): per key its element count and a ring of its last size-1 elements

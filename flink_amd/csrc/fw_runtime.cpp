@@ -460,6 +460,11 @@ int grow_table(fw_op* op, int new_log_r) {
     dfree(op->td.lidx);
     HIP_OR_RETURN(op, dmalloc(&op->td.lidx, (size_t)op->table_slots));
     op->td.lidx_slots = op->table_slots;
+    if (op->td.mover) {  // (no override is set between pushes)
+      dfree(op->td.mover);
+      HIP_OR_RETURN(op, dmalloc(&op->td.mover, (size_t)op->table_slots));
+      HIP_OR_RETURN(op, hipMemsetAsync(op->td.mover, 0xff, (size_t)op->table_slots * sizeof(int32_t), op->stream));
+    }
   }
   const int64_t rows = (int64_t)op->h_status->out_rows;
   return ensure_out_capacity(op, rows + op->table_slots, rows);
@@ -536,16 +541,17 @@ int settle(fw_op* op) {
         if (c.agg == FW_AGG_HLL)
           fwdev::launch_hll_update(c, S.part, S.offs(), S.offT(), S.n, op->tb, op->d_status, op->stream);
       });
-    // the t-digest compression skipped itself too (it runs once, after the aggregate completed)
-    if ((susp & FW_SUSP_AGG) && c.agg == FW_AGG_TDIGEST)
-      timed(op, K_TDIGEST, [&] {
-        fwdev::launch_tdigest(c, S.part, S.offs(), S.offT(), S.n, op->tb, op->td, op->d_status, op->stream);
-      });
     // after an aggregate suspension the ordered path never started; otherwise it resumes
     if (!c.dense) timed(op, K_SLOW, [&] {
       fwdev::launch_slow(c, S.wm, S.srow(op->dc.P), S.T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status,
                          (susp & FW_SUSP_AGG) ? 0 : 1, op->stream);
     });
+    // the t-digest compression skipped itself behind the suspension (it runs once, after the aggregate and the
+    // ordered path completed)
+    if ((susp & (FW_SUSP_AGG | FW_SUSP_SLOW)) && c.agg == FW_AGG_TDIGEST)
+      timed(op, K_TDIGEST, [&] {
+        fwdev::launch_tdigest(c, S.part, S.offs(), S.offT(), S.n, op->tb, op->td, op->d_status, op->stream);
+      });
     // a watermark queued behind the push skipped itself; firing at the latest one is the same as
     // firing at each (nothing was pushed in between)
     if (op->fire_unsettled)
@@ -758,6 +764,11 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   // a partition can outgrow one aggregate workgroup (hot keys) only when the batch is longer than a chunk
   const bool split = !cc.dense && (cc.wpr == 1 || cc.panes) && n > FW_AGG_CHUNK;
   if (split && (rc = ensure_hot(op))) return rc;
+  if (cc.agg == FW_AGG_TDIGEST && cc.assigner == FW_SESSION) {  // the push's merge log and ordered values start empty
+    HIP_OR_RETURN(op, hipMemsetAsync(cc.td_mctr, 0, sizeof(int32_t), op->stream));
+    HIP_OR_RETURN(op, hipMemsetAsync(cc.td_ovctr, 0, sizeof(int32_t), op->stream));
+    HIP_OR_RETURN(op, hipMemsetAsync(op->td.uctr, 0, 2 * sizeof(unsigned long long), op->stream));
+  }
   timed(
       op, K_AGGREGATE,
       [&] {
@@ -767,14 +778,15 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
           fwdev::launch_hll_update(cc, S.part, S.offs(), S.offT(), n, op->tb, op->d_status, op->stream);
       },
       nullptr, cc.dense);  // (the dense aggregate is one kernel)
-  if (cc.agg == FW_AGG_TDIGEST)
-    timed(op, K_TDIGEST, [&] {
-      fwdev::launch_tdigest(cc, S.part, S.offs(), S.offT(), n, op->tb, op->td, op->d_status, op->stream);
-    });
   if (!cc.dense)  // (tumbling windows without allowed lateness: no record needs arrival order)
     timed(op, K_SLOW, [&] {
       fwdev::launch_slow(cc, op->wm, S.srow(cc.P), S.T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status,
                          0, op->stream);
+    });
+  // the t-digest compression closes the push: after the ordered path too (sessions: its merges and added values)
+  if (cc.agg == FW_AGG_TDIGEST)
+    timed(op, K_TDIGEST, [&] {
+      fwdev::launch_tdigest(cc, S.part, S.offs(), S.offT(), n, op->tb, op->td, op->d_status, op->stream);
     });
   HIP_OR_RETURN(op, hipGetLastError());
   HIP_OR_RETURN(op, hipEventRecord(op->ev_done[nxt], op->stream));  // the set's last use by this batch (see settle)
@@ -947,10 +959,9 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     if (!(cfg.tdigest_quantiles[i] >= 0.0 && cfg.tdigest_quantiles[i] <= 1.0))
       snprintf(msg, sizeof msg, "t-digest quantiles must be in [0, 1]");
   if (!msg[0] && cfg.aggregate == FW_AGG_TDIGEST &&
-      ((cfg.assigner != FW_TUMBLING && cfg.assigner != FW_SLIDING) || cfg.allowed_lateness != 0 ||
-       cfg.value_type != FW_VAL_F64)) {
-    snprintf(msg, sizeof msg, "the t-digest aggregate is offered for tumbling and sliding windows without allowed "
-                              "lateness over a Double field");
+      (cfg.allowed_lateness != 0 || cfg.value_type != FW_VAL_F64 || (cfg.assigner == FW_SESSION && cfg.purging))) {
+    snprintf(msg, sizeof msg, "the t-digest aggregate is offered for tumbling, sliding and session windows (without "
+                              "PurgingTrigger) without allowed lateness over a Double field");
     unsupported = true;
   }
   if (!msg[0] && cfg.aggregate >= FW_AGG_FIRST && cfg.aggregate <= FW_AGG_FIRST_MAX && cfg.assigner == FW_SLIDING && cfg.slide > 0 &&
@@ -1135,6 +1146,30 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     if (op->table_slots >= (int64_t(1) << 31)) return set_err(op, FW_ERR_CAPACITY, "t-digest table would exceed 2^31 slots");
     HIP_OR_RETURN(op, dmalloc(&t.lidx, (size_t)op->table_slots));
     t.lidx_slots = op->table_slots;
+    if (c.assigner == FW_SESSION) {  // session merges (DevCfg::td_mdst, TdBuf::fwd ...; launch_tdigest)
+      const size_t pb = (size_t)c.pool_blocks;
+      HIP_OR_RETURN(op, dmalloc(&c.td_mdst, pb));
+      HIP_OR_RETURN(op, dmalloc(&c.td_msrc, pb));
+      HIP_OR_RETURN(op, dmalloc(&c.td_mctr, 1));
+      HIP_OR_RETURN(op, dmalloc(&c.td_ovk, (size_t)mb));
+      HIP_OR_RETURN(op, dmalloc(&c.td_ovt, (size_t)mb));
+      HIP_OR_RETURN(op, dmalloc(&c.td_ovv, (size_t)mb));
+      HIP_OR_RETURN(op, dmalloc(&c.td_ovp, (size_t)mb));
+      HIP_OR_RETURN(op, dmalloc(&c.td_ovctr, 1));
+      HIP_OR_RETURN(op, hipMemsetAsync(c.td_mctr, 0, sizeof(int32_t), op->stream));
+      HIP_OR_RETURN(op, hipMemsetAsync(c.td_ovctr, 0, sizeof(int32_t), op->stream));
+      HIP_OR_RETURN(op, dmalloc(&t.fwd, pb));
+      HIP_OR_RETURN(op, dmalloc(&t.mhead, pb));
+      HIP_OR_RETURN(op, dmalloc(&t.mnext, pb));
+      HIP_OR_RETURN(op, dmalloc(&t.ovr, pb));
+      HIP_OR_RETURN(op, dmalloc(&t.uni, pb * (size_t)c.td_nb));
+      HIP_OR_RETURN(op, dmalloc(&t.uctr, 2));
+      HIP_OR_RETURN(op, dmalloc(&t.mover, (size_t)op->table_slots));
+      HIP_OR_RETURN(op, hipMemsetAsync(t.fwd, 0xff, pb * sizeof(uint32_t), op->stream));
+      HIP_OR_RETURN(op, hipMemsetAsync(t.mhead, 0xff, pb * sizeof(int32_t), op->stream));
+      HIP_OR_RETURN(op, hipMemsetAsync(t.mover, 0xff, (size_t)op->table_slots * sizeof(int32_t), op->stream));
+      HIP_OR_RETURN(op, hipMemsetAsync(t.uctr, 0, 2 * sizeof(unsigned long long), op->stream));
+    }
   }
   if (cfg.assigner == FW_COUNT) {
     DevCount& w = op->cw;
@@ -1229,6 +1264,12 @@ void fw_destroy(fw_op* op) {
     dfree(t.nstart);
     dfree(t.ostart);
     dfree(t.lidx);
+    for (uint32_t* q : {op->dc.td_mdst, op->dc.td_msrc, t.fwd}) dfree(q);
+    for (int32_t* q : {op->dc.td_mctr, op->dc.td_ovctr, op->dc.td_ovp, t.mhead, t.mnext, t.mover}) dfree(q);
+    for (int64_t* q : {op->dc.td_ovk, op->dc.td_ovt, op->dc.td_ovv}) dfree(q);
+    dfree(t.ovr);
+    dfree(t.uni);
+    dfree(t.uctr);
     DevCount& w = op->cw;
     dfree(w.mkey);
     dfree(w.mstate);

@@ -99,6 +99,7 @@ struct Acc {
   std::vector<double> td_sum;      // OR_AGG_TDIGEST: centroids (sum, weight), in order
   std::vector<int64_t> td_w;
   std::vector<int64_t> td_buf;     // values added since the last compression (f64 bits)
+  bool td_merged = false;          // centroids of merged digests joined since the last compression
 };
 
 // ---------------------------------------------------------------- t-digest (window_oracle.h OR_AGG_TDIGEST)
@@ -149,7 +150,8 @@ TreeSum td_tree(const double* x, int n, int lo, int width) {
 }
 // merge the buffered values into the centroids (the compression at the end of a batch)
 void td_compress(Acc& a, const std::vector<double>& q) {
-  if (a.td_buf.empty()) return;
+  if (a.td_buf.empty() && !a.td_merged) return;
+  a.td_merged = false;
   std::vector<uint64_t> nv(a.td_buf.size());
   for (size_t i = 0; i < nv.size(); i++) nv[i] = td_key(a.td_buf[i]);
   std::sort(nv.begin(), nv.end());
@@ -237,6 +239,41 @@ double td_quantile(const Acc& a, double mn, double mx, double qv) {
     before += (double)a.td_w[i];
   }
   return y0 + (mx - y0) * ((x - x0) / (W - x0));
+}
+
+// AggregateFunction.merge of two t-digests (this build's definition, window_oracle.h OR_AGG_TDIGEST): the union of
+// their centroids, ordered by (mean key, weight, sum key), and of their buffered values; the union is compressed with
+// the buffered values at the end of the batch (td_compress), so a merge of several digests in one batch gives the
+// same result in any order (the GPU merges a session's whole connected component at once)
+inline uint64_t td_cent_mean_key(double sum, int64_t w) {
+  const double m = sum / (double)w;
+  int64_t b;
+  memcpy(&b, &m, 8);
+  return td_key(b);
+}
+void td_union(Acc& r, const Acc& b) {
+  std::vector<size_t> idx(r.td_sum.size() + b.td_sum.size());
+  std::vector<double> s(idx.size());
+  std::vector<int64_t> w(idx.size());
+  for (size_t i = 0; i < r.td_sum.size(); i++) s[i] = r.td_sum[i], w[i] = r.td_w[i];
+  for (size_t i = 0; i < b.td_sum.size(); i++) s[r.td_sum.size() + i] = b.td_sum[i], w[r.td_sum.size() + i] = b.td_w[i];
+  for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
+  auto sk = [&](size_t i) {
+    int64_t bits;
+    memcpy(&bits, &s[i], 8);
+    return td_key(bits);
+  };
+  std::sort(idx.begin(), idx.end(), [&](size_t x, size_t y) {
+    const uint64_t mx = td_cent_mean_key(s[x], w[x]), my = td_cent_mean_key(s[y], w[y]);
+    if (mx != my) return mx < my;
+    if (w[x] != w[y]) return w[x] < w[y];
+    return sk(x) < sk(y);
+  });
+  r.td_sum.resize(idx.size());
+  r.td_w.resize(idx.size());
+  for (size_t i = 0; i < idx.size(); i++) r.td_sum[i] = s[idx[i]], r.td_w[i] = w[idx[i]];
+  r.td_buf.insert(r.td_buf.end(), b.td_buf.begin(), b.td_buf.end());
+  r.td_merged = true;
 }
 
 // ---------------------------------------------------------------- HyperLogLog (window_oracle.h)
@@ -431,6 +468,7 @@ class WindowOperatorOracle {
       for (size_t j = 0; j < r.regs.size(); j++) r.regs[j] = std::max(r.regs[j], b.regs[j]);
       return r;
     }
+    if (cfg.aggregate == OR_AGG_TDIGEST) td_union(r, b);
     if (is_float()) {
       r.dsum = cfg.value_type == OR_VAL_F32 ? (double)((float)a.dsum + (float)b.dsum) : a.dsum + b.dsum;
       r.dmn = java_double_compare(b.dmn, a.dmn) < 0 ? b.dmn : a.dmn;
@@ -477,7 +515,7 @@ class WindowOperatorOracle {
     r.count = a.cnt;
     row_digest.emplace_back();
     if (cfg.aggregate == OR_AGG_TDIGEST) {
-      if (!a_in.td_buf.empty()) td_compress(a, td_q);  // getResult within a batch (late firing) sees every value
+      if (!a_in.td_buf.empty() || a_in.td_merged) td_compress(a, td_q);  // getResult within a batch sees every value
       const double q[3] = {td_quantile(a, a.dmn, a.dmx, cfg.td_q[0]), td_quantile(a, a.dmn, a.dmx, cfg.td_q[1]),
                            td_quantile(a, a.dmn, a.dmx, cfg.td_q[2])};
       memcpy(&r.sum, &q[0], 8);
@@ -628,6 +666,8 @@ class WindowOperatorOracle {
         it->second = acc_merge(it->second, acc);
       else
         state[KW{key, state_window_result}] = acc;
+      // (a merged t-digest is compressed at the end of the batch, whatever its buffer)
+      if (cfg.aggregate == OR_AGG_TDIGEST) td_touched.push_back(KW{key, state_window_result});
     }
   }
 

@@ -40,13 +40,15 @@ def _stream(n, batch, num_keys, rate, zipf=None, values="spread", seed=0x7D16, b
     return batches, wms
 
 
-def _run(batches, wms, delta, quantiles=(0.5, 0.95, 0.99), sliding=None, **kw):
-    from flink_amd import SlidingEventTimeWindows
+def _run(batches, wms, delta, quantiles=(0.5, 0.95, 0.99), sliding=None, gap=None, **kw):
+    from flink_amd import EventTimeSessionWindows, SlidingEventTimeWindows
     from flink_amd.operator import GpuWindowOperator
-    assigner = SlidingEventTimeWindows.of(*sliding) if sliding else TumblingEventTimeWindows.of(1000)
+    assigner = (SlidingEventTimeWindows.of(*sliding) if sliding else EventTimeSessionWindows.with_gap(gap) if gap
+                else TumblingEventTimeWindows.of(1000))
     gpu = GpuWindowOperator(assigner, TDigest(delta, quantiles, export=True), **kw)
     ref = (orc.WindowOperatorOracle(assigner="sliding", size=sliding[0], slide=sliding[1], tdigest=delta,
                                     quantiles=quantiles) if sliding else
+           orc.WindowOperatorOracle(assigner="session", gap=gap, tdigest=delta, quantiles=quantiles) if gap else
            orc.WindowOperatorOracle(assigner="tumbling", size=1000, tdigest=delta, quantiles=quantiles))
     g_rows, g_dig = [], []
     for epoch, ((k, t, v), wm) in enumerate(zip(batches, wms)):
@@ -113,6 +115,20 @@ def test_gpu_tdigest_sliding_vs_oracle(size, slide, zipf, jitter):
     assert any(len(s) > 10 for s, _ in out[1])
 
 
+@pytest.mark.parametrize("gap,zipf,jitter", [(300, 1.1, 200), (100, None, 900), (2000, 1.3, 400)],
+                         ids=["zipf", "uniform-out-of-order", "long-gap-hot"])
+def test_gpu_tdigest_sessions_vs_oracle(gap, zipf, jitter):
+    # a10: t-digest over EventTimeSessionWindows.  Sessions merge (MergingWindowSet.java:150-225) and their digests
+    # with them (AbstractHeapMergingState.mergeNamespaces, AbstractHeapMergingState.java:67-93; AggregateFunction.merge,
+    # AggregateFunction.java:160; this build's merge = the union of the centroids, compressed with the push's values,
+    # oracle td_union) -- in the parallel session flush, in the ordered replay of elements that arrive behind the
+    # watermark and bridge in-flight sessions, and across pushes.  Centroids and quantiles bit-exact.
+    batches, wms = _stream(200_000, 20_000, 3000, rate=100_000, zipf=zipf, jitter=jitter, bound=200)
+    g_rows, g_dig, r_rows, r_dig = _run(batches, wms, 40, gap=gap, expected_entries=30_000)
+    _assert_same(g_rows, g_dig, r_rows, r_dig, 40)
+    assert (g_rows["end"] - g_rows["start"] > gap).any()  # sessions merged
+
+
 def test_gpu_tdigest_blocks_are_recycled():
     # many short windows over few keys with a pool sized for one window's digests: fired blocks are reused
     batches, wms = _stream(400_000, 10_000, 500, rate=100_000, bound=50, jitter=50)
@@ -138,9 +154,9 @@ def test_gpu_tdigest_refuses_unsupported_shapes():
     from flink_amd import SlidingEventTimeWindows
     from flink_amd import _native as N
     from flink_amd.operator import GpuWindowOperator
-    from flink_amd import EventTimeSessionWindows
-    for kw in (dict(assigner=EventTimeSessionWindows.with_gap(1000)), dict(allowed_lateness=10),
-               dict(assigner=SlidingEventTimeWindows.of(3000, 1000), allowed_lateness=10)):
+    from flink_amd import EventTimeSessionWindows, EventTimeTrigger, PurgingTrigger
+    for kw in (dict(assigner=EventTimeSessionWindows.with_gap(1000), trigger=PurgingTrigger.of(EventTimeTrigger.create())),
+               dict(allowed_lateness=10), dict(assigner=SlidingEventTimeWindows.of(3000, 1000), allowed_lateness=10)):
         with pytest.raises(N.NativeError) as e:
             GpuWindowOperator(kw.pop("assigner", TumblingEventTimeWindows.of(1000)), TDigest(100), **kw)
         assert e.value.code == N.FW_ERR_UNSUPPORTED

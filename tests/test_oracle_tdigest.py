@@ -141,3 +141,37 @@ def test_oracle_tdigest_accuracy():
         est = np.array([r[f][0]]).view(np.float64)[0]
         rank = np.searchsorted(srt, est) / n
         assert abs(rank - qv) < 0.01, (qv, rank)
+
+
+def _union(*digests):
+    """AggregateFunction.merge of t-digests (this build's definition): the centroids of all, ordered by (mean,
+    weight, sum) in Double.compare order; compressed together with the batch's values at the end of the batch."""
+    cents = [c for d in digests for c in d]
+    return sorted(cents, key=lambda c: (_dkey(c[0] / c[1]), c[1], _dkey(c[0])))
+
+
+@pytest.mark.parametrize("delta", [20, 100])
+def test_oracle_tdigest_session_merge(delta):
+    # two sessions of one key, each compressed at the end of batch 1; in batch 2 one element bridges them (and a
+    # second element extends the merged session): the merged digest is the union of both digests' centroids,
+    # compressed once with the batch's values (MergingWindowSet.java:150-225, AbstractHeapMergingState.java:67-93)
+    rng = np.random.default_rng(delta)
+    q = _bounds(delta)
+    va = list(rng.standard_normal(300) * 10.0)
+    vb = list(rng.standard_normal(200) * 10.0 + 5.0)
+    ka = np.zeros(300, dtype=np.int64)
+    kb = np.zeros(200, dtype=np.int64)
+    op = orc.WindowOperatorOracle(assigner="session", gap=50, tdigest=delta, quantiles=(0.5, 0.9, 0.1))
+    op.process(np.concatenate([ka, kb]), np.concatenate([np.arange(300) % 10, 100 + np.arange(200) % 10]),
+               np.array(va + vb))
+    da, db = _compress([], va, q), _compress([], vb, q)
+    bridge = [3.5, -2.25]
+    op.process(np.zeros(2, dtype=np.int64), np.array([55, 120]), np.array(bridge))
+    exp = _compress(_union(da, db), bridge, q)
+    op.watermark((1 << 63) - 1)
+    rows = op.rows()
+    assert len(rows) == 1 and rows[0]["start"] == 0 and rows[0]["end"] == 170 and rows[0]["count"] == 502
+    s, w = op.digest(0)
+    assert len(s) == len(exp) <= delta // 2
+    assert list(w) == [e[1] for e in exp]
+    assert [x.hex() for x in s] == [e[0].hex() for e in exp]
