@@ -2638,12 +2638,27 @@ __device__ __forceinline__ void hll_raise(const DevCfg& c, uint64_t blk, int64_t
   }
 }
 
+__device__ void td_late_row(const SlowCtx& x, const Entry& en, int32_t head);
+// a window's chain of the push's values (t-digest under allowed lateness) is kept in Double.compare order of the
+// values: link l (element l / wpr) goes before the first link of a larger value
+__device__ __forceinline__ uint64_t td_key(int64_t bits);
+__device__ __forceinline__ void td_chain_insert(const DevCfg& c, int32_t* head, int32_t l, int64_t v) {
+  const uint64_t kx = td_key(v);
+  int32_t* at = head;
+  while (*at >= 0 && td_key(c.td_ovv[*at / c.wpr]) < kx) at = &c.td_olink[*at];
+  c.td_olink[l] = *at;
+  *at = l;
+}
+
 // WindowOperator.processElement, non-merging branch (WindowOperator.java:371-407)
 __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int64_t t, int64_t v, int64_t fo, bool* skipped) {
   const DevCfg& c = x.c;
   const Region r = region_of(c, x.tb, p, x.tb.cur[p]);
   int64_t last;
   const int nwin = num_windows(c, t, &last);
+  // t-digest (allowed lateness): the element joins the push's compression of its non-late windows (the newest nl)
+  const bool td = c.agg == FW_AGG_TDIGEST && c.td_olast;
+  int32_t oj = -1, nl = 0;
   for (int wi = 0; wi < nwin; wi++) {
     const int64_t s = jsub(last, (int64_t)wi * c.slide);
     const int64_t e = jadd(s, c.size);
@@ -2657,16 +2672,32 @@ __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int6
       ne.start = s;
       ne.end = e;
       acc_clear(ne);
-      ne.meta = c.agg == FW_AGG_HLL ? (int64_t)(pool_alloc_one(c, x.st) << 1) : 0;
+      ne.meta = c.pool_bytes ? (int64_t)(pool_new_block(c, x.st) << 1) : 0;
       slot = new_slot(x, r, p, h, ne);
       if (slot < 0) continue;
     }
     Entry en = r.ent[slot];
     acc_add(c, en, v, fo);
     if (c.agg == FW_AGG_HLL) hll_raise(c, pool_block_of(en), v);  // (k_hll_update takes the partitioned records)
+    int32_t head = -1;
+    if (td) {  // the window's chain of this push's values: this element on top
+      if (oj < 0) {
+        oj = atomicAdd(c.td_ovctr, 1);
+        c.td_ovk[oj] = k;
+        c.td_ovt[oj] = last;
+        c.td_ovv[oj] = v;
+        c.td_ovp[oj] = p;
+      }
+      const uint32_t g = ((uint32_t)p << c.log_r) | (uint32_t)slot;
+      td_chain_insert(c, &c.td_olast[g], oj * c.wpr + wi, v);
+      head = c.td_olast[g];
+      nl = wi + 1;
+    }
     bool keep = true;
     if (jsub(e, 1) <= x.wm) {  // EventTimeTrigger.onElement -> FIRE (WindowOperator.java:395-401)
-      if (c.agg == FW_AGG_HLL) {  // getResult from the window's registers (the window stays unless purged)
+      if (td) {  // getResult over the centroids and the push's values so far (the window stays)
+        td_late_row(x, en, head);
+      } else if (c.agg == FW_AGG_HLL) {  // getResult from the window's registers (the window stays unless purged)
         Entry fr = en;
         double est;
         hll_estimate(c, pool_block_of(en), &est, &fr.mn, &fr.mx);
@@ -2695,6 +2726,7 @@ __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int6
       kill_slot(x, r, p, slot);
     }
   }
+  if (oj >= 0) c.td_ovn[oj] = nl;
 }
 
 // WindowOperator.processElement, merging branch (WindowOperator.java:297-370) with
@@ -3581,14 +3613,16 @@ __device__ double td_wave_new_sum(const uint64_t* __restrict__ v, int64_t ns, in
   return s;
 }
 
-// serial merge of nn sorted values v[beg ..] with the no centroids `old` into `out` (window_oracle.cpp td_compress)
-__device__ int32_t td_merge_serial(const DevCfg& c, const double* qb, const uint64_t* __restrict__ v, int64_t beg,
-                                   int64_t nn, const TdCent* __restrict__ old, int32_t no, TdCent* __restrict__ out,
-                                   int64_t W) {
+// serial merge of nn sorted value keys, taken in order from next(), with the no centroids `old` into `out`
+// (window_oracle.cpp td_compress)
+template <class Next>
+__device__ int32_t td_merge_run(const DevCfg& c, const double* qb, Next next, int64_t nn, const TdCent* __restrict__ old,
+                                int32_t no, TdCent* __restrict__ out, int64_t W) {
   const double Wd = (double)W;
   int64_t i = 0, cw = 0, gw = 0, cum_out = 0, prev_old = 0;
   int32_t j = 0, k = 0;
   uint64_t mk = no ? td_mean_key(old[0].sum, old[0].cum) : 0;
+  uint64_t nk = nn ? next() : 0;  // the next new value's key
   double so = 0.0, sn = 0.0;
   bool any_o = false, any_n = false;
   TdTree tr;
@@ -3603,13 +3637,14 @@ __device__ int32_t td_merge_serial(const DevCfg& c, const double* qb, const uint
     tr.cnt = 0;
   };
   while (i < nn || j < no) {
-    const bool take_new = j == no || (i < nn && v[beg + i] <= mk);
+    const bool take_new = j == no || (i < nn && nk <= mk);
     double x;
     int64_t w;
     if (take_new) {
-      x = td_val(v[beg + i]);
+      x = td_val(nk);
       w = 1;
       i++;
+      if (i < nn) nk = next();
     } else {
       x = old[j].sum;
       w = old[j].cum - prev_old;
@@ -3636,6 +3671,13 @@ __device__ int32_t td_merge_serial(const DevCfg& c, const double* qb, const uint
   if (gw > 0) emit();
   return k;
 }
+// the same over the sorted run v[beg, beg + nn)
+__device__ int32_t td_merge_serial(const DevCfg& c, const double* qb, const uint64_t* __restrict__ v, int64_t beg,
+                                   int64_t nn, const TdCent* __restrict__ old, int32_t no, TdCent* __restrict__ out,
+                                   int64_t W) {
+  const uint64_t* p = v + beg;
+  return td_merge_run(c, qb, [&]() { return *p++; }, nn, old, no, out, W);
+}
 
 // piecewise-linear quantile through (0, min), (centre_i, mean_i) ..., (W, max) (window_oracle.cpp td_quantile)
 __device__ double td_quantile(const TdCent* ce, int32_t n, int64_t W, double mn, double mx, double qv) {
@@ -3656,10 +3698,53 @@ __device__ double td_quantile(const TdCent* ce, int32_t n, int64_t W, double mn,
   return y0 + (mx - y0) * ((x - x0) / (Wd - x0));
 }
 
-// getResult of a fired row (one thread): out.sum holds the block id (k_fire), out.min / out.max the min / max;
-// returns the digest's centroid count
-__device__ int32_t td_finish(const DevCfg& c, const DevRows& out, uint64_t row, int64_t stack_slot) {
-  const uint64_t blk = (uint64_t)out.sum[row];
+// getResult of a window that fires on an element of the ordered path (allowed lateness) while the push's values
+// are still buffered: as window_oracle.cpp emit, a copy of the digest -- its centroids compressed with the window's
+// values of this push so far, the sorted chain from `head` -- gives the quantiles (one thread of k_slow; the copy
+// goes to the thread's td_late scratch).
+__device__ void td_late_row(const SlowCtx& x, const Entry& en, int32_t head) {
+  const DevCfg& c = x.c;
+  int64_t L = 0;
+  for (int32_t l = head; l >= 0; l = c.td_olink[l]) L++;
+  const uint64_t blk = pool_block_of(en);
+  const TdHead h = *td_head(c, blk);
+  const TdCent* old = td_half(c, blk, h.cur);
+  TdCent* cp = c.td_late + (int64_t)threadIdx.x * c.td_nb;
+  int32_t at = head;
+  auto next = [&]() -> uint64_t {  // (the chain is in value order: td_chain_insert)
+    const uint64_t key = td_key(c.td_ovv[at / c.wpr]);
+    at = c.td_olink[at];
+    return key;
+  };
+  const int64_t wt = h.w + L;
+  const int32_t n = td_merge_run(c, c.td_qb, next, L, old, h.n, cp, wt);
+  const unsigned long long pos = atomicAdd(&x.st->out_rows, 1ull);
+  if ((int64_t)pos >= x.out.cap) {
+    atomicOr(&x.st->flags, FW_STATUS_OUT_FULL);
+    return;
+  }
+  write_row(c, x.out, pos, en);
+  const double mn = __longlong_as_double(x.out.mn[pos]), mx = __longlong_as_double(x.out.mx[pos]);
+  x.out.sum[pos] = __double_as_longlong(td_quantile(cp, n, wt, mn, mx, c.td_quant[0]));
+  x.out.mn[pos] = __double_as_longlong(td_quantile(cp, n, wt, mn, mx, c.td_quant[1]));
+  x.out.mx[pos] = __double_as_longlong(td_quantile(cp, n, wt, mn, mx, c.td_quant[2]));
+  if (x.out.dig) {
+    int64_t* d = x.out.dig + pos * (1 + 2 * (int64_t)c.td_nb);
+    d[0] = n;
+    for (int32_t k = 0; k < n; k++) {
+      d[1 + 2 * k] = __double_as_longlong(cp[k].sum);
+      d[2 + 2 * k] = td_weight(cp, k);
+    }
+  }
+  atomicAdd(&x.st->td_cent, (unsigned long long)n);
+}
+
+// getResult of a fired row (one thread): out.sum holds the block id and above it 1 + the block's free-stack slot
+// past `stack_base` if its window goes (k_fire), out.min / out.max the min / max; returns the digest's centroid count
+__device__ int32_t td_finish(const DevCfg& c, const DevRows& out, uint64_t row, int64_t stack_base) {
+  const uint64_t tag = (uint64_t)out.sum[row];
+  const uint64_t blk = tag & 0xffffffffull;
+  const int64_t rel = (int64_t)(tag >> 32);
   const TdHead h = *td_head(c, blk);
   const TdCent* ce = td_half(c, blk, h.cur);
   const double mn = __longlong_as_double(out.mn[row]), mx = __longlong_as_double(out.mx[row]);
@@ -3677,7 +3762,7 @@ __device__ int32_t td_finish(const DevCfg& c, const DevRows& out, uint64_t row, 
   out.sum[row] = __double_as_longlong(q0);
   out.mn[row] = __double_as_longlong(q1);
   out.mx[row] = __double_as_longlong(q2);
-  c.pool_free[stack_slot] = (uint32_t)blk;
+  if (rel) c.pool_free[stack_base + rel - 1] = (uint32_t)blk;
   return h.n;
 }
 
@@ -3730,8 +3815,9 @@ __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restric
   __syncthreads();
   const bool cmp = c.compact && !*c.wide;
   const bool sess = c.assigner == FW_SESSION;
-  // sessions: the ordered path's added elements follow the partitioned records (positions total .. total + nov)
-  const int64_t nov = sess ? (int64_t)*c.td_ovctr : 0;
+  // sessions and allowed lateness: the ordered path's added elements follow the partitioned records (positions
+  // total .. total + nov)
+  const int64_t nov = c.td_ovctr ? (int64_t)*c.td_ovctr : 0;
   int32_t pp = p0_s;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     int nw = 0;
@@ -3754,7 +3840,7 @@ __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restric
         rec.key = c.td_ovk[j];
         rec.last = c.td_ovt[j];
         rec.val = c.td_ovv[j];
-        rec.nwin = 1;
+        rec.nwin = c.td_ovn ? c.td_ovn[j] : 1;  // (its non-late windows, the newest ones)
         rp = c.td_ovp[j];
       }
       nw = W == 1 ? 1 : (int)(rec.nwin & 0xffff);
@@ -3882,7 +3968,9 @@ __global__ void k_td_mclear(DevCfg c, TdBuf td) {
 // tie runs: positions with the previous one's key (one digest, equal high value bits) and a smaller payload mark
 // their run's first position in fixbm; k_td_fix_runs then orders each marked run by payload
 __global__ __launch_bounds__(256) void k_td_fix_mark(int64_t n, const uint64_t* __restrict__ key64,
-                                                     const uint32_t* __restrict__ pay, uint32_t* __restrict__ fixbm) {
+                                                     const uint32_t* __restrict__ pay, uint32_t* __restrict__ fixbm,
+                                                     const Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t k = key64[i];
     if (k != key64[i - 1] || pay[i] >= pay[i - 1]) continue;
@@ -3903,7 +3991,9 @@ __device__ void td_sift(uint32_t* a, int64_t root, int64_t len) {
   }
 }
 __global__ __launch_bounds__(256) void k_td_fix_runs(int64_t n, const uint64_t* __restrict__ key64,
-                                                     uint32_t* __restrict__ pay, const uint32_t* __restrict__ fixbm) {
+                                                     uint32_t* __restrict__ pay, const uint32_t* __restrict__ fixbm,
+                                                     const Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
     if (!((fixbm[s >> 5] >> (s & 31)) & 1u)) continue;
     const uint64_t k = key64[s];
@@ -3921,14 +4011,17 @@ __global__ __launch_bounds__(256) void k_td_fix_runs(int64_t n, const uint64_t* 
   }
 }
 // the sorted keys back to (global slot, value key) columns for the tiers
+// (behind a suspended push the sort ran over whatever the key buffer held -- k_td_keys skipped itself -- so this
+// and the fix-up kernels skip themselves too; the settle runs the compression again)
 __global__ __launch_bounds__(256) void k_td_decode(int64_t n, int B, uint32_t nblk, uint32_t none,
                                                    const uint64_t* __restrict__ key64, const uint32_t* __restrict__ pay,
                                                    const uint32_t* __restrict__ binv, uint32_t* __restrict__ gs,
-                                                   uint64_t* __restrict__ v) {
+                                                   uint64_t* __restrict__ v, const Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t k = key64[i];
     const uint32_t blk = (uint32_t)(k >> (64 - B));
-    if (blk == nblk) {
+    if (blk >= nblk) {  // (nblk: the positions without a digest)
       gs[i] = none;
       v[i] = 0;
     } else {
@@ -4731,7 +4824,9 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
             out.mn[pos] = (int64_t)pool_block_of(fe);
             out.mx[pos] = d2.keep ? -1 : (int64_t)atomicAdd(&nrel_s, 1);
           }
-          if (c.agg == FW_AGG_TDIGEST) out.sum[pos] = (int64_t)pool_block_of(fe);  // read back by td_finish
+          if (c.agg == FW_AGG_TDIGEST)  // read back by td_finish: the block, above it 1 + its free-stack slot if it goes
+            out.sum[pos] = (int64_t)(pool_block_of(fe) |
+                                     (d2.keep ? 0ull : (uint64_t)(atomicAdd(&nrel_s, 1) + 1) << 32));
         } else {
           atomicOr(&st->flags, FW_STATUS_OUT_FULL);
         }
@@ -4743,8 +4838,8 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
     __shared__ int hl_sb;
     __syncthreads();  // (nrel_s complete)
     __threadfence_block();
-    // free-stack slots for this workgroup's released blocks (HLL: the rows whose window goes; t-digest: every row)
-    if (threadIdx.x == 0) hl_sb = atomicAdd(&c.pool_ctr[0], c.agg == FW_AGG_HLL ? nrel_s : (int)total);
+    // free-stack slots for this workgroup's released blocks (the rows whose window goes)
+    if (threadIdx.x == 0) hl_sb = atomicAdd(&c.pool_ctr[0], nrel_s);
     __syncthreads();
     const uint64_t end = min((unsigned long long)out.cap, base_s + total);
     if (c.agg == FW_AGG_HLL) {
@@ -4765,7 +4860,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
       __syncthreads();
       unsigned long long cent = 0;
       for (uint64_t r = base_s + threadIdx.x; r < end; r += blockDim.x)
-        cent += td_finish(c, out, r, hl_sb + (int64_t)(r - base_s));
+        cent += td_finish(c, out, r, hl_sb);
       if (cent) atomicAdd(&cent_s, cent);
       __syncthreads();
       if (threadIdx.x == 0 && cent_s) atomicAdd(&st->td_cent, cent_s);
@@ -6895,6 +6990,40 @@ size_t tdigest_sort_bytes(int64_t n) {
   (void)rocprim::radix_sort_pairs(nullptr, a, kv, ks, (size_t)n, 0, 64);
   return a;
 }
+// t-digest under allowed lateness: the push's late-firing chains rebuilt after the table grew mid-push (settle
+// resumes the ordered path over moved slots).  A chain's order does not matter (td_late_row selects in value order).
+__global__ void k_td_relink(DevCfg c, DevTable tb) {
+  const int64_t nov = *c.td_ovctr;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nov; j += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t p = c.td_ovp[j];
+    const Region r = region_of(c, tb, p, tb.cur[p]);
+    const int64_t k = c.td_ovk[j], last = c.td_ovt[j];
+    for (int wi = 0; wi < c.td_ovn[j]; wi++) {
+      const int64_t s = jsub(last, (int64_t)wi * c.slide);
+      const int32_t slot = region_find(r, slot_hash(c, k, s), k, s, wend(c, s));
+      const int32_t l = (int32_t)j * c.wpr + wi;
+      c.td_olink[l] = slot < 0 ? -1 : atomicExch(&c.td_olast[((uint32_t)p << c.log_r) | (uint32_t)slot], l);
+    }
+  }
+}
+// ... then each chain back in value order (an insertion sort of the list)
+__global__ void k_td_resort(DevCfg c, int64_t slots) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < slots; g += (int64_t)gridDim.x * blockDim.x) {
+    int32_t l = c.td_olast[g];
+    if (l < 0) continue;
+    int32_t sorted = -1;
+    while (l >= 0) {
+      const int32_t nx = c.td_olink[l];
+      td_chain_insert(c, &sorted, l, c.td_ovv[l / c.wpr]);
+      l = nx;
+    }
+    c.td_olast[g] = sorted;
+  }
+}
+void launch_td_relink(const DevCfg& c, DevTable tb, hipStream_t s) {
+  hipLaunchKernelGGL(k_td_relink, dim3(256), dim3(256), 0, s, c, tb);
+  hipLaunchKernelGGL(k_td_resort, dim3(1024), dim3(256), 0, s, c, (int64_t)c.P << c.log_r);
+}
 void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
                     TdBuf& td, Status* st, hipStream_t s) {
   if (n <= 0) return;
@@ -6920,12 +7049,12 @@ void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int
   size_t bytes = td.tmp_bytes;
   (void)rocprim::radix_sort_pairs(td.tmp, bytes, kv, ks, (size_t)n, 0, 64, s);
   const unsigned grid = (unsigned)std::min<int64_t>(8192, (n + 255) / 256);
-  hipLaunchKernelGGL(k_td_fix_mark, dim3(grid), dim3(256), 0, s, n, kv.current(), ks.current(), td.fixbm);
-  hipLaunchKernelGGL(k_td_fix_runs, dim3(grid), dim3(256), 0, s, n, kv.current(), ks.current(), td.fixbm);
+  hipLaunchKernelGGL(k_td_fix_mark, dim3(grid), dim3(256), 0, s, n, kv.current(), ks.current(), td.fixbm, st);
+  hipLaunchKernelGGL(k_td_fix_runs, dim3(grid), dim3(256), 0, s, n, kv.current(), ks.current(), td.fixbm, st);
   uint32_t* gsorted = ks.alternate();
   uint64_t* vsorted = kv.alternate();
   hipLaunchKernelGGL(k_td_decode, dim3(grid), dim3(256), 0, s, n, B, nblk, none, kv.current(), ks.current(), td.binv,
-                     gsorted, vsorted);
+                     gsorted, vsorted, st);
   const int64_t per_block = 256 * TD_BOUNDS_PER_THREAD;
   hipLaunchKernelGGL(k_td_bounds, dim3((unsigned)((n + per_block - 1) / per_block)), dim3(256), 0, s, n, gsorted, none,
                      td, st);

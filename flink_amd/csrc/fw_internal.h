@@ -93,6 +93,7 @@
 enum : uint32_t { SLOT_EMPTY = 0, SLOT_LIVE = 1, SLOT_DEAD = 2, SLOT_BUSY = 3 };
 enum : int64_t { FW_TIMER = 1 };
 
+struct TdCent;
 struct DevCfg {
   int32_t assigner, vtype, key_kind, purging;
   int32_t side_output, max_par, kg0, n_kg;
@@ -133,6 +134,12 @@ struct DevCfg {
   int32_t* td_mctr;
   int64_t *td_ovk, *td_ovt, *td_ovv;
   int32_t *td_ovp, *td_ovctr;  // (the added element's state partition)
+  // t-digest under allowed lateness (tumbling / sliding): an ordered-path element's td_ovt is its newest window's
+  // start and td_ovn its count of non-late windows (the newest ones); a window that fires late compresses its
+  // centroids with the push's values so far (td_olast[state slot] -> td_olink[element * wpr + window] chain)
+  // into its thread's td_late scratch (FW_SLOW_THREADS x td_nb)
+  int32_t *td_ovn, *td_olast, *td_olink;
+  TdCent* td_late;
   int64_t pool_blocks;
   int64_t pool_bytes;     // 0 = no pool
   // FW_AGG_TDIGEST (definition: oracle/window_oracle.h OR_AGG_TDIGEST): td_nb = delta / 2 buckets of the
@@ -449,6 +456,7 @@ int64_t pane_nt_floor(const DevCfg& c, int64_t wm);  // host: DevCfg::nt_floor o
 void launch_hll_update(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
                        Status* st, hipStream_t_ s);
 // FW_AGG_TDIGEST: compress the batch's values into the digests of their (key, window) entries (after aggregate)
+void launch_td_relink(const DevCfg& c, DevTable tb, hipStream_t s);
 void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
                     TdBuf& td, Status* st, hipStream_t_ s);
 size_t tdigest_sort_bytes(int64_t n);  // rocPRIM scratch of the two sorts

@@ -465,6 +465,13 @@ int grow_table(fw_op* op, int new_log_r) {
       HIP_OR_RETURN(op, dmalloc(&op->td.mover, (size_t)op->table_slots));
       HIP_OR_RETURN(op, hipMemsetAsync(op->td.mover, 0xff, (size_t)op->table_slots * sizeof(int32_t), op->stream));
     }
+    if (op->dc.td_olast) {  // a push's late-firing chains, mid-push (settle): relinked over the moved slots
+      dfree(op->dc.td_olast);
+      HIP_OR_RETURN(op, dmalloc(&op->dc.td_olast, (size_t)op->table_slots));
+      HIP_OR_RETURN(op, hipMemsetAsync(op->dc.td_olast, 0xff, (size_t)op->table_slots * sizeof(int32_t), op->stream));
+      fwdev::launch_td_relink(op->dc, op->tb, op->stream);
+      HIP_OR_RETURN(op, hipGetLastError());
+    }
   }
   const int64_t rows = (int64_t)op->h_status->out_rows;
   return ensure_out_capacity(op, rows + op->table_slots, rows);
@@ -769,6 +776,10 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
     HIP_OR_RETURN(op, hipMemsetAsync(cc.td_ovctr, 0, sizeof(int32_t), op->stream));
     HIP_OR_RETURN(op, hipMemsetAsync(op->td.uctr, 0, 2 * sizeof(unsigned long long), op->stream));
   }
+  if (cc.agg == FW_AGG_TDIGEST && cc.td_olast) {  // (allowed lateness) ... and no window has a chain yet
+    HIP_OR_RETURN(op, hipMemsetAsync(cc.td_ovctr, 0, sizeof(int32_t), op->stream));
+    HIP_OR_RETURN(op, hipMemsetAsync(cc.td_olast, 0xff, (size_t)op->table_slots * sizeof(int32_t), op->stream));
+  }
   timed(
       op, K_AGGREGATE,
       [&] {
@@ -959,9 +970,11 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     if (!(cfg.tdigest_quantiles[i] >= 0.0 && cfg.tdigest_quantiles[i] <= 1.0))
       snprintf(msg, sizeof msg, "t-digest quantiles must be in [0, 1]");
   if (!msg[0] && cfg.aggregate == FW_AGG_TDIGEST &&
-      (cfg.allowed_lateness != 0 || cfg.value_type != FW_VAL_F64 || (cfg.assigner == FW_SESSION && cfg.purging))) {
-    snprintf(msg, sizeof msg, "the t-digest aggregate is offered for tumbling, sliding and session windows (without "
-                              "PurgingTrigger) without allowed lateness over a Double field");
+      (cfg.value_type != FW_VAL_F64 || (cfg.assigner == FW_SESSION && (cfg.purging || cfg.allowed_lateness != 0)) ||
+       (cfg.allowed_lateness != 0 && cfg.purging))) {
+    snprintf(msg, sizeof msg, "the t-digest aggregate is offered over a Double field for tumbling and sliding windows "
+                              "(allowed lateness without PurgingTrigger) and session windows (without allowed lateness "
+                              "or PurgingTrigger)");
     unsupported = true;
   }
   if (!msg[0] && cfg.aggregate >= FW_AGG_FIRST && cfg.aggregate <= FW_AGG_FIRST_MAX && cfg.assigner == FW_SLIDING && cfg.slide > 0 &&
@@ -1089,7 +1102,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     HIP_OR_RETURN(op, hipMemsetAsync(c.pool_ctr, 0, 3 * sizeof(int32_t), op->stream));
   }
   // regions sized for the expected entries at 1/FW_TABLE_SLACK load (default 4: 25 %; the limit is 3/4)
-  const int64_t slack = getenv("FW_TABLE_SLACK") ? std::max(2, atoi(getenv("FW_TABLE_SLACK"))) : c.dense ? 2 : 4;
+  const int64_t slack = getenv("FW_TABLE_SLACK") ? std::max(1, atoi(getenv("FW_TABLE_SLACK"))) : c.dense ? 2 : 4;
   c.log_r = std::max(8, ilog2(slack * ((expected + c.P - 1) / c.P)));  // (dense: a region's groups, densely)
   op->table_slots = (int64_t)c.P << c.log_r;
 
@@ -1146,18 +1159,26 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     if (op->table_slots >= (int64_t(1) << 31)) return set_err(op, FW_ERR_CAPACITY, "t-digest table would exceed 2^31 slots");
     HIP_OR_RETURN(op, dmalloc(&t.lidx, (size_t)op->table_slots));
     t.lidx_slots = op->table_slots;
-    if (c.assigner == FW_SESSION) {  // session merges (DevCfg::td_mdst, TdBuf::fwd ...; launch_tdigest)
-      const size_t pb = (size_t)c.pool_blocks;
-      HIP_OR_RETURN(op, dmalloc(&c.td_mdst, pb));
-      HIP_OR_RETURN(op, dmalloc(&c.td_msrc, pb));
-      HIP_OR_RETURN(op, dmalloc(&c.td_mctr, 1));
+    if (c.assigner == FW_SESSION || c.lateness > 0) {  // the ordered path's added elements (DevCfg::td_ovk ...)
       HIP_OR_RETURN(op, dmalloc(&c.td_ovk, (size_t)mb));
       HIP_OR_RETURN(op, dmalloc(&c.td_ovt, (size_t)mb));
       HIP_OR_RETURN(op, dmalloc(&c.td_ovv, (size_t)mb));
       HIP_OR_RETURN(op, dmalloc(&c.td_ovp, (size_t)mb));
       HIP_OR_RETURN(op, dmalloc(&c.td_ovctr, 1));
-      HIP_OR_RETURN(op, hipMemsetAsync(c.td_mctr, 0, sizeof(int32_t), op->stream));
       HIP_OR_RETURN(op, hipMemsetAsync(c.td_ovctr, 0, sizeof(int32_t), op->stream));
+    }
+    if (c.assigner != FW_SESSION && c.lateness > 0) {  // late firings (DevCfg::td_olast ...)
+      HIP_OR_RETURN(op, dmalloc(&c.td_ovn, (size_t)mb));
+      HIP_OR_RETURN(op, dmalloc(&c.td_olink, (size_t)(mb * c.wpr)));
+      HIP_OR_RETURN(op, dmalloc(&c.td_olast, (size_t)op->table_slots));
+      HIP_OR_RETURN(op, dmalloc(&c.td_late, (size_t)FW_SLOW_THREADS * c.td_nb));
+    }
+    if (c.assigner == FW_SESSION) {  // session merges (DevCfg::td_mdst, TdBuf::fwd ...; launch_tdigest)
+      const size_t pb = (size_t)c.pool_blocks;
+      HIP_OR_RETURN(op, dmalloc(&c.td_mdst, pb));
+      HIP_OR_RETURN(op, dmalloc(&c.td_msrc, pb));
+      HIP_OR_RETURN(op, dmalloc(&c.td_mctr, 1));
+      HIP_OR_RETURN(op, hipMemsetAsync(c.td_mctr, 0, sizeof(int32_t), op->stream));
       HIP_OR_RETURN(op, dmalloc(&t.fwd, pb));
       HIP_OR_RETURN(op, dmalloc(&t.mhead, pb));
       HIP_OR_RETURN(op, dmalloc(&t.mnext, pb));
@@ -1265,7 +1286,10 @@ void fw_destroy(fw_op* op) {
     dfree(t.ostart);
     dfree(t.lidx);
     for (uint32_t* q : {op->dc.td_mdst, op->dc.td_msrc, t.fwd}) dfree(q);
-    for (int32_t* q : {op->dc.td_mctr, op->dc.td_ovctr, op->dc.td_ovp, t.mhead, t.mnext, t.mover}) dfree(q);
+    for (int32_t* q : {op->dc.td_mctr, op->dc.td_ovctr, op->dc.td_ovp, op->dc.td_ovn, op->dc.td_olink, op->dc.td_olast,
+                       t.mhead, t.mnext, t.mover})
+      dfree(q);
+    dfree(op->dc.td_late);
     for (int64_t* q : {op->dc.td_ovk, op->dc.td_ovt, op->dc.td_ovv}) dfree(q);
     dfree(t.ovr);
     dfree(t.uni);

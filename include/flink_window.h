@@ -96,10 +96,12 @@ extern "C" {
                                       centroids; add buffers, and every push compresses the values it added.
                                       Rows carry count = elements and sum / min / max = the estimated quantiles
                                       tdigest_quantiles[0..2] (f64 bits).  Tumbling and sliding windows (one
-                                      digest per window) and session windows (merged sessions' digests merge:
-                                      the union of their centroids, compressed with the push's values;
-                                      AbstractHeapMergingState.mergeNamespaces; not with PurgingTrigger), no
-                                      allowed lateness, FW_VAL_F64; expected_entries sizes the digest pool.  Keyed-state snapshots
+                                      digest per window; allowed lateness without PurgingTrigger: a late firing
+                                      reports the digest with the push's values so far) and session windows
+                                      (merged sessions' digests merge: the union of their centroids, compressed
+                                      with the push's values; AbstractHeapMergingState.mergeNamespaces; no
+                                      allowed lateness, no PurgingTrigger), FW_VAL_F64; expected_entries sizes
+                                      the digest pool.  Keyed-state snapshots
                                       carry the digest as an accumulator block (fw_snapshot_key_group_blocks). */
 #define FW_AGG_FIRST_MAX 5         /* max(pos) (ComparableAggregator.java:72-94, Comparator.MaxComparator): as
                                       FW_AGG_FIRST, but the min column holds the field's MAXIMUM (the first

@@ -40,16 +40,17 @@ def _stream(n, batch, num_keys, rate, zipf=None, values="spread", seed=0x7D16, b
     return batches, wms
 
 
-def _run(batches, wms, delta, quantiles=(0.5, 0.95, 0.99), sliding=None, gap=None, **kw):
+def _run(batches, wms, delta, quantiles=(0.5, 0.95, 0.99), sliding=None, gap=None, lateness=0, **kw):
     from flink_amd import EventTimeSessionWindows, SlidingEventTimeWindows
     from flink_amd.operator import GpuWindowOperator
     assigner = (SlidingEventTimeWindows.of(*sliding) if sliding else EventTimeSessionWindows.with_gap(gap) if gap
                 else TumblingEventTimeWindows.of(1000))
-    gpu = GpuWindowOperator(assigner, TDigest(delta, quantiles, export=True), **kw)
+    gpu = GpuWindowOperator(assigner, TDigest(delta, quantiles, export=True), allowed_lateness=lateness, **kw)
     ref = (orc.WindowOperatorOracle(assigner="sliding", size=sliding[0], slide=sliding[1], tdigest=delta,
-                                    quantiles=quantiles) if sliding else
+                                    quantiles=quantiles, lateness=lateness) if sliding else
            orc.WindowOperatorOracle(assigner="session", gap=gap, tdigest=delta, quantiles=quantiles) if gap else
-           orc.WindowOperatorOracle(assigner="tumbling", size=1000, tdigest=delta, quantiles=quantiles))
+           orc.WindowOperatorOracle(assigner="tumbling", size=1000, tdigest=delta, quantiles=quantiles,
+                                    lateness=lateness))
     g_rows, g_dig = [], []
     for epoch, ((k, t, v), wm) in enumerate(zip(batches, wms)):
         if len(k):
@@ -129,6 +130,60 @@ def test_gpu_tdigest_sessions_vs_oracle(gap, zipf, jitter):
     assert (g_rows["end"] - g_rows["start"] > gap).any()  # sessions merged
 
 
+@pytest.mark.parametrize("sliding,lateness,zipf,jitter",
+                         [(None, 500, None, 900), (None, 3000, 1.1, 1500), ((2000, 500), 300, 1.1, 900),
+                          ((1000, 300), 1000, None, 1200)],
+                         ids=["tumbling", "tumbling-hot-long", "sliding-zipf", "sliding-uneven"])
+def test_gpu_tdigest_lateness_vs_oracle(sliding, lateness, zipf, jitter):
+    # allowed lateness (WindowedStream.allowedLateness; WindowOperator.java:379-420, 588-598): a window fired at its
+    # maxTimestamp keeps its digest until cleanupTime, and every element that reaches it behind the watermark fires
+    # it again (EventTimeTrigger.onElement -> FIRE) with getResult over every value so far -- this push's values
+    # still buffered (the oracle compresses a copy, window_oracle.cpp emit; the ordered path the window's sorted
+    # chain of them into a scratch digest).  Late firings, the digests exported with them, the on-time rows and the
+    # dropped elements are bit-exact with the oracle.
+    batches, wms = _stream(200_000, 20_000, 2000, rate=100_000, zipf=zipf, jitter=jitter, bound=200)
+    g_rows, g_dig, r_rows, r_dig = _run(batches, wms, 40, sliding=sliding, lateness=lateness, expected_entries=60_000)
+    _assert_same(g_rows, g_dig, r_rows, r_dig, 40)
+    keys = np.stack([g_rows["key"], g_rows["start"]], axis=1)
+    assert len(np.unique(keys, axis=0)) < len(keys)  # windows fired more than once
+
+
+def test_gpu_tdigest_lateness_grows_mid_push(monkeypatch):
+    # a burst of late elements for new windows within the allowed lateness, each key four times across the batch:
+    # every element creates or joins a window on the ordered path and fires it, the regions (FW_TABLE_SLACK=1: sized
+    # at the expected entries, ~196 per 256-slot region against a load limit of 192) run out of room, the ordered
+    # path suspends and the table grows mid-push -- the push's sorted chains of buffered values follow the moved
+    # slots (k_td_relink / k_td_resort)
+    from flink_amd.operator import GpuWindowOperator
+    monkeypatch.setenv("FW_TABLE_SLACK", "1")
+    n, m = 200_000, 200_000
+    rng = np.random.default_rng(7)
+    k1 = np.arange(n, dtype=np.int64)
+    k2 = np.tile(np.arange(1_000_000, 1_000_000 + m, dtype=np.int64), 4)
+    batches = [(k1, k1 % 1000, rng.normal(size=n)), (k2, k2 % 997, rng.normal(size=4 * m)),
+               (k1[:0], k1[:0], np.zeros(0))]
+    wms = [5000, 6000, (1 << 63) - 1]
+    gpu = GpuWindowOperator(TumblingEventTimeWindows.of(1000), TDigest(40, export=True), allowed_lateness=1 << 40,
+                            expected_entries=n + m)
+    ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000, tdigest=40, quantiles=(0.5, 0.95, 0.99),
+                                   lateness=1 << 40)
+    g_rows, g_dig = [], []
+    for epoch, ((k, t, v), wm) in enumerate(zip(batches, wms)):
+        if len(k):
+            gpu.process(k, t, v)
+            ref.process(k, t, v)
+        gpu.advance_watermark(wm)
+        g_dig += gpu.drain_digests()
+        g_rows.append(gpu.drain_rows(epoch))
+        ref.watermark(wm)
+    st = gpu.stats()
+    gpu.close()
+    r_rows = ref.rows()
+    assert st["table_grows"] >= 1 and st["slow_path_records"] >= 4 * m
+    assert len(r_rows) == n + 4 * m
+    _assert_same(np.concatenate(g_rows), g_dig, r_rows, [ref.digest(i) for i in range(len(r_rows))], 40)
+
+
 def test_gpu_tdigest_blocks_are_recycled():
     # many short windows over few keys with a pool sized for one window's digests: fired blocks are reused
     batches, wms = _stream(400_000, 10_000, 500, rate=100_000, bound=50, jitter=50)
@@ -155,8 +210,11 @@ def test_gpu_tdigest_refuses_unsupported_shapes():
     from flink_amd import _native as N
     from flink_amd.operator import GpuWindowOperator
     from flink_amd import EventTimeSessionWindows, EventTimeTrigger, PurgingTrigger
-    for kw in (dict(assigner=EventTimeSessionWindows.with_gap(1000), trigger=PurgingTrigger.of(EventTimeTrigger.create())),
-               dict(allowed_lateness=10), dict(assigner=SlidingEventTimeWindows.of(3000, 1000), allowed_lateness=10)):
+    purge = PurgingTrigger.of(EventTimeTrigger.create())
+    for kw in (dict(assigner=EventTimeSessionWindows.with_gap(1000), trigger=purge),
+               dict(assigner=EventTimeSessionWindows.with_gap(1000), allowed_lateness=10),
+               dict(allowed_lateness=10, trigger=purge),
+               dict(assigner=SlidingEventTimeWindows.of(3000, 1000), allowed_lateness=10, trigger=purge)):
         with pytest.raises(N.NativeError) as e:
             GpuWindowOperator(kw.pop("assigner", TumblingEventTimeWindows.of(1000)), TDigest(100), **kw)
         assert e.value.code == N.FW_ERR_UNSUPPORTED
