@@ -237,6 +237,20 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 __device__ __forceinline__ uint32_t ld_state(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// A region's state words at workgroup scope, for code in which one workgroup owns the region for the whole launch (the
+// session flush): agent-scope accesses are kept coherent across the XCDs' L2s, so each one travels past the L2 (a
+// round trip to the fabric per probe); these stay in the CU's L1 / the XCD's L2.  The next kernel sees the words
+// through the launch boundary, as it sees the entries written with plain stores.
+__device__ __forceinline__ uint32_t ld_state_wg(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t cas_state_wg(uint32_t* p, uint32_t expect, uint32_t v) {
+  __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return expect;
+}
+__device__ __forceinline__ void st_state_wg(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // ------------------------------------------------------------------ output
 // FW_AGG_FIRST / MINBY / MAXBY carry the records' arrival ordinals
@@ -383,11 +397,13 @@ __device__ __forceinline__ Region region_of(const DevCfg& c, const DevTable& tb,
 // find the live slot of (key, start, end), -1 if absent (linear probing up to the first EMPTY).
 // The fingerprint in the state word skips foreign slots without touching their entries.
 // (from slot h & mask on, for the state word `want`)
+// (OWN: the caller's workgroup owns the region for the launch -- the state words at workgroup scope, ld_state_wg)
+template <bool OWN = false>
 __device__ __forceinline__ int32_t region_find(const Region& r, uint64_t h, int64_t key, int64_t start, int64_t end,
                                                uint32_t want) {
   for (uint32_t i = 0; i < r.mask; i++) {
     const uint32_t s = ((uint32_t)h + i) & r.mask;
-    const uint32_t st = ld_state(r.state + s);
+    const uint32_t st = OWN ? ld_state_wg(r.state + s) : ld_state(r.state + s);
     if (st == SLOT_EMPTY) return -1;
     if (st == want) {
       const Entry& e = r.ent[s];
@@ -396,11 +412,12 @@ __device__ __forceinline__ int32_t region_find(const Region& r, uint64_t h, int6
   }
   return -1;
 }
+template <bool OWN = false>
 __device__ __forceinline__ int32_t region_find(const Region& r, uint64_t h, int64_t key, int64_t start, int64_t end) {
   const uint32_t want = live_word(h);
   for (uint32_t i = 0; i <= r.mask; i++) {
     const uint32_t s = ((uint32_t)h + i) & r.mask;
-    const uint32_t st = ld_state(r.state + s);
+    const uint32_t st = OWN ? ld_state_wg(r.state + s) : ld_state(r.state + s);
     if (st == SLOT_EMPTY) return -1;
     if (st == want) {
       const Entry& e = r.ent[s];
@@ -410,11 +427,13 @@ __device__ __forceinline__ int32_t region_find(const Region& r, uint64_t h, int6
   return -1;
 }
 // claim the first EMPTY slot of the probe sequence (state -> `word`), -1 if the region is full
+template <bool OWN = false>
 __device__ __forceinline__ int32_t region_claim(const Region& r, uint64_t h, uint32_t word) {
   for (uint32_t i = 0; i <= r.mask; i++) {
     const uint32_t s = ((uint32_t)h + i) & r.mask;
-    if (ld_state(r.state + s) != SLOT_EMPTY) continue;
-    if (atomicCAS(r.state + s, SLOT_EMPTY, word) == SLOT_EMPTY) return (int32_t)s;
+    if ((OWN ? ld_state_wg(r.state + s) : ld_state(r.state + s)) != SLOT_EMPTY) continue;
+    if ((OWN ? cas_state_wg(r.state + s, SLOT_EMPTY, word) : atomicCAS(r.state + s, SLOT_EMPTY, word)) == SLOT_EMPTY)
+      return (int32_t)s;
   }
   return -1;
 }
@@ -1353,16 +1372,15 @@ __device__ __forceinline__ void lds_acc(AggLds& L, int target, int vtype, int64_
     return;
   }
   atomicAdd(&L.cnt[target], 1u);
-  if (vtype == FW_VAL_F64) {
+  // min / max only fall / rise, so a read that the value does not pass needs no atomic
+  const int64_t sv = vtype == FW_VAL_F64 ? f64_sortable(v) : v;
+  const int64_t a = first ? mn_in(first, sv) : sv, b = first ? ~fo : sv;
+  if (vtype == FW_VAL_F64)
     atomicAdd((double*)&L.sum[target], __longlong_as_double(v));
-    const int64_t sv = f64_sortable(v);
-    atomicMin((long long*)&L.mn[target], (long long)(first ? mn_in(first, sv) : sv));
-    atomicMax((long long*)&L.mx[target], (long long)(first ? ~fo : sv));
-  } else {
+  else
     atomicAdd((unsigned long long*)&L.sum[target], (unsigned long long)v);
-    atomicMin((long long*)&L.mn[target], (long long)(first ? mn_in(first, v) : v));
-    atomicMax((long long*)&L.mx[target], (long long)(first ? ~fo : v));
-  }
+  if (a < *(volatile int64_t*)&L.mn[target]) atomicMin((long long*)&L.mn[target], (long long)a);
+  if (b > *(volatile int64_t*)&L.mx[target]) atomicMax((long long*)&L.mx[target], (long long)b);
 }
 
 // take one of the FW_LDS_FILL_LIMIT slot tickets before claiming a slot: concurrent claims then
@@ -1568,7 +1586,7 @@ __device__ __forceinline__ bool agg_flush(const DevCfg& c, AggLds& L, const Regi
     if (lv[q]) {
       const i64x2 kv = L.kv[h];
       const uint32_t home = (uint32_t)slot_hash(c, kv.x, kv.y) & r.mask;
-      hw[q] = ld_state(r.state + home);
+      hw[q] = ld_state_wg(r.state + home);
       hks[q] = *reinterpret_cast<const i64x2*>(&r.ent[home].key);
       hend[q] = r.ent[home].end;
     }
@@ -1584,7 +1602,7 @@ __device__ __forceinline__ bool agg_flush(const DevCfg& c, AggLds& L, const Regi
     if (hw[q] == live_word(hs) && hks[q].x == kv.x && hks[q].y == kv.y && hend[q] == we)
       slot = (int32_t)((uint32_t)hs & r.mask);
     else if (hw[q] != SLOT_EMPTY)  // the rest of the probe chain
-      slot = region_find(r, hs + 1, kv.x, kv.y, we, live_word(hs));
+      slot = region_find<true>(r, hs + 1, kv.x, kv.y, we, live_word(hs));
     L.slot[h] = slot;
     nnew += slot < 0;
   }
@@ -1641,7 +1659,7 @@ __device__ __forceinline__ bool agg_flush(const DevCfg& c, AggLds& L, const Regi
       r.ent[slot] = cur;
     } else {
       const uint64_t hs = slot_hash(c, d.key, d.start);
-      const int32_t ns = region_claim(r, hs, live_word(hs));
+      const int32_t ns = region_claim<true>(r, hs, live_word(hs));
       if (ns >= 0) {
         Entry n = d;
         if (c.pool_bytes) {
@@ -1732,9 +1750,50 @@ __device__ __forceinline__ int lds_session_slot(AggLds& L, int64_t* E, int64_t k
     guard++;
   }
   if (target < 0) return -1;
-  atomicMin(reinterpret_cast<long long*>(&L.kv[target]) + 1, (long long)ws);  // TimeWindow.cover
-  atomicMax((long long*)&E[target], (long long)we);
+  // TimeWindow.cover: an interval only widens, so a read that already covers [ws, we) needs no atomic (a hot key's
+  // elements mostly fall inside its session)
+  long long* st = reinterpret_cast<long long*>(&L.kv[target]) + 1;
+  if (*(volatile long long*)st > (long long)ws) atomicMin(st, (long long)ws);
+  if (*(volatile int64_t*)&E[target] < we) atomicMax((long long*)&E[target], (long long)we);
   return target;
+}
+// lds_acc (count / sum / min / max) of the lanes with ok set, each into its slot tg: when the whole wave runs and
+// every such lane takes the same slot (a hot key's session), the wave sums its values first and one lane does the
+// atomics -- sixty-four lanes' atomics on one LDS address otherwise serialise.  (A Double sum's order is not the
+// arrival order either way; integer sums are exact.)
+__device__ __forceinline__ void lds_acc_wave(AggLds& L, int tg, int vtype, int64_t v, bool ok) {
+  const uint64_t okm = __ballot(ok);
+  if (__ballot(1) == ~0ull && __popcll(okm) >= 8) {
+    const int lead = __ffsll((unsigned long long)okm) - 1;
+    const int t0 = __shfl(tg, lead, 64);
+    if (__ballot(ok && tg == t0) == okm) {
+      const bool f64 = vtype == FW_VAL_F64;
+      const int64_t key = f64 ? f64_sortable(v) : v;
+      int64_t mn = ok ? key : LMAX, mx = ok ? key : LMIN;
+      double ds = ok && f64 ? __longlong_as_double(v) : 0.0;
+      unsigned long long is = ok && !f64 ? (unsigned long long)v : 0ull;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (int64_t)__shfl_xor((long long)mn, o, 64));
+        mx = max(mx, (int64_t)__shfl_xor((long long)mx, o, 64));
+        if (f64)
+          ds += __shfl_xor(ds, o, 64);
+        else
+          is += (unsigned long long)__shfl_xor((long long)is, o, 64);
+      }
+      if (__lane_id() == lead) {
+        atomicAdd(&L.cnt[t0], (uint32_t)__popcll(okm));
+        if (f64)
+          atomicAdd((double*)&L.sum[t0], ds);
+        else
+          atomicAdd((unsigned long long*)&L.sum[t0], is);
+        if (mn < *(volatile int64_t*)&L.mn[t0]) atomicMin((long long*)&L.mn[t0], (long long)mn);
+        if (mx > *(volatile int64_t*)&L.mx[t0]) atomicMax((long long*)&L.mx[t0], (long long)mx);
+      }
+      return;
+    }
+  }
+  if (ok) lds_acc(L, tg, vtype, v, 0, 0);
 }
 __device__ __forceinline__ bool lds_session_upsert(AggLds& L, int64_t* E, int vtype, int64_t key, int64_t ws,
                                                    int64_t we, int64_t v, int64_t fo = 0, int first = 0) {
@@ -1821,36 +1880,66 @@ __device__ __forceinline__ uint64_t pool_new_block(const DevCfg& c, Status* st) 
 // Returns the region slots newly taken; *timer = maxTimestamp of the resulting session.
 // DIAG_AGG_TIMING clocks of the session flush (thread 0): [0] flushes, [1] linking, [2] adding, [3] tail
 __device__ unsigned long long g_sess[4];
-__device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, const Entry& d, int64_t* timer, Status* st) {
+// The key's entries lie on its probe chain from its home slot up to the chain's first EMPTY slot, and no slot
+// becomes EMPTY during the launch: an EMPTY home slot means the key has no session in the region.  So the home
+// slot is claimed first, at once -- the usual case, a key's first session of the batch, takes one round trip.
+// Returns the claimed home slot, or -1.
+__device__ __forceinline__ int32_t session_claim_home(const DevCfg& c, const Region& r, int64_t key) {
+  const uint32_t home = (uint32_t)slot_hash(c, key, 0) & r.mask;
+  return cas_state_wg(r.state + home, SLOT_EMPTY, SLOT_BUSY) == SLOT_EMPTY ? (int32_t)home : -1;
+}
+// pre: the result of session_claim_home for d.key when the caller tried it (-1: the home is taken), -2 if not
+__device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, const Entry& d, int64_t* timer, Status* st,
+                                           int32_t pre = -2) {
   const uint64_t h = slot_hash(c, d.key, 0);
   const uint32_t want = live_word(h);
   int32_t target = -1;
   Entry m;
-  // the probe chain is read SW state words at a time, all in flight together (the key's entries lie before the
-  // chain's first EMPTY slot: slots of other keys claimed meanwhile by other threads do not matter here, and
-  // no slot becomes EMPTY during the launch); only the key's candidates' entries are then read
+  int32_t ns = pre == -2 ? session_claim_home(c, r, d.key) : pre;
+  // otherwise the probe chain is read SW state words at a time, all in flight together (slots of other keys
+  // claimed meanwhile by other threads do not matter here); only the key's candidates' entries are then read
   constexpr int SW = 16;
-  bool end_seen = false;
+  bool end_seen = ns >= 0;
+  uint32_t first_empty = 0;  // (the chain's first EMPTY slot when the scan ends there: where a claim starts)
   for (uint32_t i0 = 0; i0 <= r.mask && !end_seen; i0 += SW) {
     uint32_t w[SW];
 #pragma unroll
-    for (int u = 0; u < SW; u++) w[u] = ld_state(r.state + (((uint32_t)h + i0 + u) & r.mask));
+    for (int u = 0; u < SW; u++) w[u] = ld_state_wg(r.state + (((uint32_t)h + i0 + u) & r.mask));
     uint32_t cand = 0;
 #pragma unroll
     for (int u = 0; u < SW; u++) {
       if (end_seen) continue;
-      if (w[u] == SLOT_EMPTY)
+      if (w[u] == SLOT_EMPTY) {
         end_seen = true;
-      else if (w[u] == want)
+        first_empty = i0 + u;
+      } else if (w[u] == want) {
         cand |= 1u << u;
+      }
     }
     if (cand) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     while (cand) {
-      const int u = __builtin_ctz(cand);
-      cand &= cand - 1;
-      const uint32_t s = ((uint32_t)h + i0 + u) & r.mask;
+      // up to four candidates' (key, start, end) in flight together; only an intersecting one's entry is read whole
+      constexpr int CQ = 4;
+      uint32_t cs[CQ];
+      i64x2 ckv[CQ];
+      int64_t cend[CQ];
+      int nc = 0;
+#pragma unroll
+      for (int q = 0; q < CQ; q++) {
+        if (!cand) continue;
+        const int u = __builtin_ctz(cand);
+        cand &= cand - 1;
+        cs[q] = ((uint32_t)h + i0 + u) & r.mask;
+        ckv[q] = *reinterpret_cast<const i64x2*>(&r.ent[cs[q]].key);
+        cend[q] = r.ent[cs[q]].end;
+        nc = q + 1;
+      }
+#pragma unroll
+      for (int q = 0; q < CQ; q++) {
+      if (q >= nc) continue;
+      const uint32_t s = cs[q];
+      if (ckv[q].x != d.key || !(d.start <= cend[q] && d.end >= ckv[q].y)) continue;  // TimeWindow.intersects
       const Entry e = r.ent[s];
-      if (e.key != d.key || !(d.start <= e.end && d.end >= e.start)) continue;  // TimeWindow.intersects
       if (target < 0) {
         target = (int32_t)s;
         m = e;
@@ -1861,12 +1950,13 @@ __device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, con
       m.start = min(m.start, e.start);
       m.end = max(m.end, e.end);
       // the slot stays occupied (live counts occupied slots) until k_fire rebuilds the region
-      __hip_atomic_store(r.state + s, SLOT_DEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      st_state_wg(r.state + s, SLOT_DEAD);
+      }
     }
   }
   if (target < 0) {  // a new session
     *timer = jsub(d.end, 1);
-    const int32_t ns = region_claim(r, h, SLOT_BUSY);
+    if (ns < 0) ns = region_claim<true>(r, h + first_empty, SLOT_BUSY);
     if (ns < 0) {  // cannot happen below the load limit (checked by the flush)
       atomicOr(&st->flags, FW_STATUS_STATE_LOST);
       return 0;
@@ -1875,7 +1965,7 @@ __device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, con
     if (c.pool_bytes) nd.meta |= (int64_t)(pool_new_block(c, st) << 1);  // (filled after the aggregate)
     r.ent[ns] = nd;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __hip_atomic_store(r.state + ns, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_state_wg(r.state + ns, want);
     return 1;
   }
   acc_merge(c, m, d);
@@ -1885,6 +1975,77 @@ __device__ __forceinline__ int session_add(const DevCfg& c, const Region& r, con
   *timer = jsub(m.end, 1);
   r.ent[target] = m;
   return 0;
+}
+
+// A key without sessions in the region (its home slot just claimed by the flush) whose LDS intervals (the chain from
+// `first` through L.slot) are pairwise disjoint: each interval is a new session.  The home slot takes the first, the
+// next EMPTY slots of the key's probe chain the others -- their claims in flight together -- and all are published
+// behind one fence (instead of a scan, a claim and a fence per interval).  Returns false, having done nothing, when
+// two of the intervals intersect or there are more than 8.  The region slot of each interval is kept in its L.cnt.
+template <class Delta>
+__device__ bool session_fresh_chain(const DevCfg& c, const Region& r, AggLds& L, const int64_t* E, int first,
+                                    int32_t home, Status* st, int& nnew, int64_t& mt, unsigned long long& nflush,
+                                    Delta delta) {
+  constexpr int CH = 8;
+  auto next = [&](int j) { return (L.slot[j] & 0xffff) - 1; };
+  int n = 0;
+  for (int a = first; a >= 0; a = next(a)) {
+    if (++n > CH) return false;
+    const int64_t as = L.kv[a].y, ae = E[a];
+    int m = n;
+    for (int b = next(a); b >= 0 && m < CH; b = next(b), m++)
+      if (as <= E[b] && ae >= L.kv[b].y) return false;  // TimeWindow.intersects
+  }
+  const uint32_t want = live_word(slot_hash(c, L.kv[first].x, 0));
+  auto place = [&](int j, int32_t s) {
+    Entry nd = delta(j);
+    if (c.pool_bytes) nd.meta |= (int64_t)(pool_new_block(c, st) << 1);  // (filled after the aggregate)
+    r.ent[s] = nd;
+    L.cnt[j] = (uint32_t)s;
+    mt = min(mt, jsub(nd.end, 1));
+  };
+  place(first, home);
+  int j = next(first);
+  constexpr int SW = 16;
+  // the claims keep the key's entries before its chain's first EMPTY slot: a chunk's EMPTY slots are taken in order,
+  // and when a claim loses a race the chunk is read again before any slot past it is taken
+  for (uint32_t i0 = 1; j >= 0 && i0 <= r.mask;) {
+    uint32_t w[SW];
+#pragma unroll
+    for (int u = 0; u < SW; u++) w[u] = ld_state_wg(r.state + (((uint32_t)home + i0 + u) & r.mask));
+    int want_n = 0;
+    for (int b = j; b >= 0; b = next(b)) want_n++;
+    uint32_t take = 0;
+    int k = 0;
+#pragma unroll
+    for (int u = 0; u < SW; u++)
+      if (w[u] == SLOT_EMPTY && k < want_n && i0 + u <= r.mask) {
+        take |= 1u << u;
+        k++;
+      }
+    uint32_t got = 0;
+#pragma unroll
+    for (int u = 0; u < SW; u++)
+      if ((take >> u) & 1u)
+        if (cas_state_wg(r.state + (((uint32_t)home + i0 + u) & r.mask), SLOT_EMPTY, SLOT_BUSY) == SLOT_EMPTY) got |= 1u << u;
+    const bool lost = got != take;
+    while (got && j >= 0) {
+      const int u = __builtin_ctz(got);
+      got &= got - 1;
+      place(j, (int32_t)(((uint32_t)home + i0 + u) & r.mask));
+      j = next(j);
+    }
+    if (!lost) i0 += SW;
+  }
+  if (j >= 0) atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // cannot happen below the load limit
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  for (int a = first; a >= 0; a = next(a)) {
+    if (a == j) break;  // (the unplaced rest, after a lost claim)
+    st_state_wg(r.state + L.cnt[a], want);
+    nnew++;
+    nflush++;
+  }
+  return true;
 }
 
 // flush of the session LDS table.  Every LDS slot takes at most one new region slot, so the load limit
@@ -1954,28 +2115,74 @@ __device__ __forceinline__ bool agg_flush_session(const DevCfg& c, AggLds& L, co
   int nnew = 0;
   int64_t mt = LMAX;
   unsigned long long nflush = 0;
-  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
-    int j = L.tag[h] >= 2 && (L.slot[h] >> 16) ? h : -1;
+  auto delta = [&](int j) {
+    const i64x2 kv = L.kv[j];
+    Entry d;
+    d.key = kv.x;
+    d.start = kv.y;
+    d.end = E[j];
+    d.cnt = (int64_t)L.cnt[j];
+    d.sum = L.sum[j];
+    d.mn = L.mn[j];
+    d.mx = L.mx[j];
+    if (agg_by(c.agg)) {  // the selected element: its key and full ordinal
+      d.mn = by_key(c.agg, c.vtype, L.byv[d.mx]);
+      d.mx += L.byb;
+    }
+    d.meta = FW_TIMER;
+    return d;
+  };
+  // this thread's owner slots: their home slots claimed together (the claims in flight at once); a claimed key
+  // with one interval is a new session, written and published with one fence for all of them
+  constexpr int FQ = (FW_LDS_SLOTS + FW_AGG_THREADS - 1) / FW_AGG_THREADS;
+  int32_t pre[FQ];
+  bool pub[FQ];
+#pragma unroll
+  for (int q = 0; q < FQ; q++) {
+    const int h = threadIdx.x + q * (int)blockDim.x;
+    const bool own = h < FW_LDS_SLOTS && L.tag[h] >= 2 && (L.slot[h] >> 16);
+    pre[q] = own ? session_claim_home(c, r, L.kv[h].x) : -3;
+  }
+  bool anypub = false;
+#pragma unroll
+  for (int q = 0; q < FQ; q++) {
+    const int h = threadIdx.x + q * (int)blockDim.x;
+    pub[q] = pre[q] >= 0 && (L.slot[h] & 0xffff) == 0;
+    if (!pub[q]) continue;
+    Entry nd = delta(h);
+    if (c.pool_bytes) nd.meta |= (int64_t)(pool_new_block(c, st) << 1);  // (filled after the aggregate)
+    r.ent[pre[q]] = nd;
+    mt = min(mt, jsub(nd.end, 1));
+    nnew++;
+    nflush++;
+    anypub = true;
+  }
+  if (anypub) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+  for (int q = 0; q < FQ; q++) {
+    const int h = threadIdx.x + q * (int)blockDim.x;
+    if (pub[q])
+      st_state_wg(r.state + pre[q], live_word(slot_hash(c, L.kv[h].x, 0)));
+  }
+#pragma unroll
+  for (int q = 0; q < FQ; q++) {
+    if (pre[q] == -3 || pub[q]) continue;
+    int j = threadIdx.x + q * (int)blockDim.x;
+    int32_t pq = pre[q];
+#ifndef FW_SESS_FRESH
+#define FW_SESS_FRESH 1
+#endif
+    if (FW_SESS_FRESH && pq >= 0 && session_fresh_chain(c, r, L, E, j, pq, st, nnew, mt, nflush, delta)) continue;
     while (j >= 0) {
-      const i64x2 kv = L.kv[j];
-      Entry d;
-      d.key = kv.x;
-      d.start = kv.y;
-      d.end = E[j];
-      d.cnt = (int64_t)L.cnt[j];
-      d.sum = L.sum[j];
-      d.mn = L.mn[j];
-      d.mx = L.mx[j];
-      if (agg_by(c.agg)) {  // the selected element: its key and full ordinal
-        d.mn = by_key(c.agg, c.vtype, L.byv[d.mx]);
-        d.mx += L.byb;
-      }
-      d.meta = FW_TIMER;
       int64_t tm;
-      nnew += session_add(c, r, d, &tm, st);
+      nnew += session_add(c, r, delta(j), &tm, st, pq);
+      pq = -1;  // (the key has a session now: its home slot is taken)
       mt = min(mt, tm);
       nflush++;
       j = (L.slot[j] & 0xffff) - 1;
+#ifdef FW_SESS_DIAG_ONE
+      if (FW_SESS_DIAG_ONE == 1) j = -1;
+#endif
     }
   }
   const unsigned long long ts2 = timing ? __builtin_amdgcn_s_memtime() : 0;
@@ -2156,11 +2363,15 @@ __device__ __forceinline__ void agg_walk_lm(const DevCfg& c, AggLds& L, int64_t*
     } else if constexpr (SESS) {
 #pragma unroll
       for (int j = 0; j < RPT; j++) {
-        if (!up || (m >> j & 1)) continue;
-        if (lds_session_upsert(L, E, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j], o[j], FIRST ? c.agg : 0))
-          m |= 1u << j;
-        else
-          up = false;
+        const bool act = up && !(m >> j & 1);
+        const int tg = act ? lds_session_slot(L, E, k[j], t[j], jadd(t[j], c.gap)) : -1;
+        if (act && tg < 0) up = false;
+        if constexpr (FIRST) {
+          if (tg >= 0) lds_acc(L, tg, c.vtype, v[j], o[j], c.agg);
+        } else {
+          lds_acc_wave(L, tg, c.vtype, v[j], tg >= 0);  // (every lane of the wave takes part)
+        }
+        if (tg >= 0) m |= 1u << j;
       }
     } else {
       up = lds_upsert_batch<RPT>(L, c.vtype, k, t, v, o, FIRST ? c.agg : c.agg == FW_AGG_HLL ? LDS_CNT_ONLY : 0, m);
@@ -2600,7 +2811,7 @@ __device__ __forceinline__ void kill_slot(const SlowCtx& x, const Region& r, int
 }
 // new entry: claim BUSY, write, publish LIVE with the fingerprint (readers never see a torn entry)
 __device__ __forceinline__ int32_t new_slot(const SlowCtx& x, const Region& r, int32_t p, uint64_t h, const Entry& e) {
-  const int32_t s = region_claim(r, h, SLOT_BUSY);
+  const int32_t s = region_claim<true>(r, h, SLOT_BUSY);  // (k_slow: one workgroup)
   if (s < 0) {  // cannot happen: k_slow checked the region's room for the chunk
     atomicOr(&x.st->flags, FW_STATUS_STATE_LOST);
     return -1;
@@ -2665,7 +2876,7 @@ __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int6
     if (cleanup_of(e, c.lateness) <= x.wm) continue;  // isWindowLate
     *skipped = false;
     const uint64_t h = slot_hash(c, k, s);
-    int32_t slot = region_find(r, h, k, s, e);
+    int32_t slot = region_find<true>(r, h, k, s, e);
     if (slot < 0) {
       Entry ne;
       ne.key = k;
@@ -2744,7 +2955,7 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
   int64_t cs = ws, ce = we;
   for (uint32_t i = 0; i <= r.mask; i++) {
     const uint32_t s = ((uint32_t)h + i) & r.mask;
-    const uint32_t stt = ld_state(r.state + s);
+    const uint32_t stt = ld_state_wg(r.state + s);
     if (stt == SLOT_EMPTY) break;
     if (stt != want) continue;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -2780,7 +2991,7 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
       Entry m = f;
       for (uint32_t i = 0; i <= r.mask; i++) {
         const uint32_t s = ((uint32_t)h + i) & r.mask;
-        const uint32_t stt = ld_state(r.state + s);
+        const uint32_t stt = ld_state_wg(r.state + s);
         if (stt == SLOT_EMPTY) break;
         if (stt != want || (int32_t)s == first) continue;
         const Entry& e = r.ent[s];
@@ -4740,7 +4951,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
 #pragma unroll
   for (int u = 0; u < FIRE_U; u++) {
     const uint32_t s = u * blockDim.x + threadIdx.x;
-    wn[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
+    wn[u] = s < R ? ld_state_wg(rx.state + s) : (uint32_t)SLOT_EMPTY;
   }
   for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x * FIRE_U) {
     uint32_t w[FIRE_U];
@@ -4753,7 +4964,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
 #pragma unroll
     for (int u = 0; u < FIRE_U; u++) {
       const uint32_t s = s0 + blockDim.x * FIRE_U + u * blockDim.x + threadIdx.x;
-      wn[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
+      wn[u] = s < R ? ld_state_wg(rx.state + s) : (uint32_t)SLOT_EMPTY;
     }
 #pragma unroll
     for (int u = 0; u < FIRE_U; u++) {
@@ -4771,7 +4982,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
       }
       if (!d.keep) continue;
       const uint64_t h = slot_hash(c, e.key, e.start);
-      const int32_t dst = region_claim(ry, h, live_word(h));
+      const int32_t dst = region_claim<true>(ry, h, live_word(h));
       if (dst >= 0) {
         ry.ent[dst] = e;
         live++;
@@ -4797,7 +5008,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
 #pragma unroll
     for (int u = 0; u < FIRE_U; u++) {
       const uint32_t s = u * blockDim.x + threadIdx.x;
-      wn[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
+      wn[u] = s < R ? ld_state_wg(rx.state + s) : (uint32_t)SLOT_EMPTY;
     }
     for (uint32_t s0 = 0; s0 < R; s0 += blockDim.x * FIRE_U) {
       uint32_t w[FIRE_U];
@@ -4810,7 +5021,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
 #pragma unroll
       for (int u = 0; u < FIRE_U; u++) {
         const uint32_t s = s0 + blockDim.x * FIRE_U + u * blockDim.x + threadIdx.x;
-        wn[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
+        wn[u] = s < R ? ld_state_wg(rx.state + s) : (uint32_t)SLOT_EMPTY;
       }
 #pragma unroll
       for (int u = 0; u < FIRE_U; u++) {
@@ -5012,7 +5223,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_fire_panes(DevCfg c, int64_t wm,
 #pragma unroll
     for (int u = 0; u < PF_U; u++) {
       const uint32_t s = u * PF_THREADS + tid;
-      wn[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
+      wn[u] = s < R ? ld_state_wg(rx.state + s) : (uint32_t)SLOT_EMPTY;
     }
     for (uint32_t s0 = 0; s0 < R; s0 += PF_THREADS * PF_U) {
       uint32_t w[PF_U];
@@ -5025,7 +5236,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_fire_panes(DevCfg c, int64_t wm,
 #pragma unroll
       for (int u = 0; u < PF_U; u++) {
         const uint32_t s = s0 + (uint32_t)(PF_THREADS * PF_U) + u * PF_THREADS + tid;
-        wn[u] = s < R ? ld_state(rx.state + s) : (uint32_t)SLOT_EMPTY;
+        wn[u] = s < R ? ld_state_wg(rx.state + s) : (uint32_t)SLOT_EMPTY;
       }
 #pragma unroll
       for (int u = 0; u < PF_U; u++) {
@@ -5137,10 +5348,10 @@ __global__ __launch_bounds__(PF_THREADS) void k_fire_panes(DevCfg c, int64_t wm,
     __syncthreads();
     int live = 0;
     for (uint32_t s = tid; s < R; s += PF_THREADS) {
-      if (st_kind(ld_state(rx.state + s)) != SLOT_LIVE) continue;
+      if (st_kind(ld_state_wg(rx.state + s)) != SLOT_LIVE) continue;
       const Entry e = rx.ent[s];
       const uint64_t h = slot_hash(c, e.key, e.start);
-      const int32_t d = region_claim(ry, h, live_word(h));
+      const int32_t d = region_claim<true>(ry, h, live_word(h));
       if (d >= 0) {
         ry.ent[d] = e;
         live++;
