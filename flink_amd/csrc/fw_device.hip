@@ -2850,6 +2850,7 @@ __device__ __forceinline__ void hll_raise(const DevCfg& c, uint64_t blk, int64_t
 }
 
 __device__ void td_late_row(const SlowCtx& x, const Entry& en, int32_t head);
+__device__ void td_late_row_session(const SlowCtx& x, const Entry& en, int32_t head);
 // a window's chain of the push's values (t-digest under allowed lateness) is kept in Double.compare order of the
 // values: link l (element l / wpr) goes before the first link of a larger value
 __device__ __forceinline__ uint64_t td_key(int64_t bits);
@@ -2940,6 +2941,37 @@ __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int6
   if (oj >= 0) c.td_ovn[oj] = nl;
 }
 
+// t-digest sessions under allowed lateness: session e (slot se) merged into m (slot sm) -- e's chain of the push's
+// values joined into m's (both sorted: a linear merge), and e's block with the blocks merged into it put on the list
+// of blocks merged into m's block (td_late_row_session takes their union)
+__device__ void td_session_join(const DevCfg& c, int32_t p, int32_t sm, int32_t se, const Entry& m, const Entry& e) {
+  const uint32_t gm = ((uint32_t)p << c.log_r) | (uint32_t)sm, ge = ((uint32_t)p << c.log_r) | (uint32_t)se;
+  int32_t a = c.td_olast[gm], b = c.td_olast[ge];
+  int32_t out = -1;
+  int32_t* tail = &out;
+  while (a >= 0 && b >= 0) {
+    if (td_key(c.td_ovv[a]) <= td_key(c.td_ovv[b])) {
+      *tail = a;
+      tail = &c.td_olink[a];
+      a = c.td_olink[a];
+    } else {
+      *tail = b;
+      tail = &c.td_olink[b];
+      b = c.td_olink[b];
+    }
+  }
+  *tail = a >= 0 ? a : b;
+  c.td_olast[gm] = out;
+  c.td_olast[ge] = -1;
+  const int32_t dst = (int32_t)pool_block_of(m), src = (int32_t)pool_block_of(e);
+  int32_t t = src;
+  c.td_bnext[src] = c.td_bhead[src];
+  while (c.td_bnext[t] >= 0) t = c.td_bnext[t];
+  c.td_bnext[t] = c.td_bhead[dst];
+  c.td_bhead[dst] = src;
+  c.td_bhead[src] = -1;
+}
+
 // WindowOperator.processElement, merging branch (WindowOperator.java:297-370) with
 // MergingWindowSet.addWindow (MergingWindowSet.java:150-225) over the key's in-flight sessions.
 __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t, int64_t v, int64_t fo, bool* skipped) {
@@ -2998,6 +3030,7 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
         if (e.key != k || !(ws <= e.end && we >= e.start)) continue;
         acc_merge(c, m, e);  // mergeNamespaces
         if (c.pool_bytes) pool_merge_blocks(c, pool_block_of(m), pool_block_of(e));
+        if (c.agg == FW_AGG_TDIGEST && c.td_olast) td_session_join(c, p, first, (int32_t)s, m, e);
         kill_slot(x, r, p, (int32_t)s);
       }
       m.start = cs;
@@ -3021,15 +3054,19 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
   *skipped = false;
   acc_add(c, en, v, fo);
   if (c.agg == FW_AGG_HLL) hll_raise(c, pool_block_of(en), v);  // (k_hll_update takes the partitioned records)
-  if (c.agg == FW_AGG_TDIGEST) {  // the value joins the push's compression (allowed lateness 0: nothing fires here)
+  if (c.agg == FW_AGG_TDIGEST) {  // the value joins the push's compression
     const int j = atomicAdd(c.td_ovctr, 1);
     c.td_ovk[j] = k;
     c.td_ovt[j] = t;
     c.td_ovv[j] = v;
     c.td_ovp[j] = p;
+    // (allowed lateness: and the session's sorted chain of the push's values, for its late firings)
+    if (c.td_olast) td_chain_insert(c, &c.td_olast[((uint32_t)p << c.log_r) | (uint32_t)actual], j, v);
   }
   if (jsub(en.end, 1) <= x.wm) {
-    if (c.agg == FW_AGG_HLL) {  // getResult from the session's registers (it stays in flight)
+    if (c.agg == FW_AGG_TDIGEST && c.td_olast) {  // getResult over the session's digest and values so far
+      td_late_row_session(x, en, c.td_olast[((uint32_t)p << c.log_r) | (uint32_t)actual]);
+    } else if (c.agg == FW_AGG_HLL) {  // getResult from the session's registers (it stays in flight)
       Entry fr = en;
       double est;
       hll_estimate(c, pool_block_of(en), &est, &fr.mn, &fr.mx);
@@ -3909,6 +3946,101 @@ __device__ double td_quantile(const TdCent* ce, int32_t n, int64_t W, double mn,
   return y0 + (mx - y0) * ((x - x0) / (Wd - x0));
 }
 
+// the union of digests' centroids u[0, m) held as (sum, weight): ordered by (mean key, weight, sum key) -- an
+// insertion sort (oracle td_union) -- and the weights made cumulative
+__device__ void td_union_sort(TdCent* u, int32_t m) {
+  for (int32_t a = 1; a < m; a++) {
+    const TdCent x = u[a];
+    const uint64_t xm = td_mean_key(x.sum, x.cum), xs = td_key(__double_as_longlong(x.sum));
+    int32_t b = a - 1;
+    while (b >= 0) {
+      const uint64_t ym = td_mean_key(u[b].sum, u[b].cum);
+      const bool after = ym > xm || (ym == xm && (u[b].cum > x.cum ||
+                                                  (u[b].cum == x.cum && td_key(__double_as_longlong(u[b].sum)) > xs)));
+      if (!after) break;
+      u[b + 1] = u[b];
+      b--;
+    }
+    u[b + 1] = x;
+  }
+  int64_t cum = 0;
+  for (int32_t a = 0; a < m; a++) {
+    cum += u[a].cum;
+    u[a].cum = cum;
+  }
+}
+
+// a late firing's row: the quantiles of the scratch digest cp[0, n) of weight wt (and the digest, when exported)
+__device__ void td_late_emit(const SlowCtx& x, const Entry& en, const TdCent* cp, int32_t n, int64_t wt) {
+  const DevCfg& c = x.c;
+  const unsigned long long pos = atomicAdd(&x.st->out_rows, 1ull);
+  if ((int64_t)pos >= x.out.cap) {
+    atomicOr(&x.st->flags, FW_STATUS_OUT_FULL);
+    return;
+  }
+  write_row(c, x.out, pos, en);
+  const double mn = __longlong_as_double(x.out.mn[pos]), mx = __longlong_as_double(x.out.mx[pos]);
+  x.out.sum[pos] = __double_as_longlong(td_quantile(cp, n, wt, mn, mx, c.td_quant[0]));
+  x.out.mn[pos] = __double_as_longlong(td_quantile(cp, n, wt, mn, mx, c.td_quant[1]));
+  x.out.mx[pos] = __double_as_longlong(td_quantile(cp, n, wt, mn, mx, c.td_quant[2]));
+  if (x.out.dig) {
+    int64_t* d = x.out.dig + pos * (1 + 2 * (int64_t)c.td_nb);
+    d[0] = n;
+    for (int32_t k = 0; k < n; k++) {
+      d[1 + 2 * k] = __double_as_longlong(cp[k].sum);
+      d[2 + 2 * k] = td_weight(cp, k);
+    }
+  }
+  atomicAdd(&x.st->td_cent, (unsigned long long)n);
+}
+
+// a session's late firing (allowed lateness): as td_late_row, over the session's digest -- its block's centroids and
+// those of the blocks merged into it during the push (td_bhead chain: their union, as td_union, in the thread's
+// td_lateu scratch) -- compressed with the values the push added to it so far (its sorted chain from `head`, merged
+// sessions' chains joined in)
+__device__ void td_late_row_session(const SlowCtx& x, const Entry& en, int32_t head) {
+  const DevCfg& c = x.c;
+  int64_t L = 0;
+  for (int32_t l = head; l >= 0; l = c.td_olink[l]) L++;
+  const uint64_t blk = pool_block_of(en);
+  const TdHead h = *td_head(c, blk);
+  const TdCent* old = td_half(c, blk, h.cur);
+  int32_t no = h.n;
+  int64_t wold = h.w;
+  if (c.td_bhead[blk] >= 0) {  // merged digests: their union
+    TdCent* u = c.td_lateu + (int64_t)threadIdx.x * c.td_lateu_cap;
+    int32_t m = 0;
+    wold = 0;
+    bool over = false;
+    for (int32_t b = (int32_t)blk; b >= 0 && !over; b = b == (int32_t)blk ? c.td_bhead[blk] : c.td_bnext[b]) {
+      const TdHead hb = *td_head(c, (uint64_t)b);
+      const TdCent* ce = td_half(c, (uint64_t)b, hb.cur);
+      if (m + hb.n > c.td_lateu_cap) {
+        over = true;
+        break;
+      }
+      for (int32_t q = 0; q < hb.n; q++) u[m++] = TdCent{ce[q].sum, td_weight(ce, q)};
+      wold += hb.w;
+    }
+    if (over) {
+      atomicOr(&x.st->flags, FW_STATUS_TD_UNION);
+      return;
+    }
+    td_union_sort(u, m);
+    old = u;
+    no = m;
+  }
+  TdCent* cp = c.td_late + (int64_t)threadIdx.x * c.td_nb;
+  int32_t at = head;
+  auto next = [&]() -> uint64_t {
+    const uint64_t key = td_key(c.td_ovv[at]);
+    at = c.td_olink[at];
+    return key;
+  };
+  const int32_t n = td_merge_run(c, c.td_qb, next, L, old, no, cp, wold + L);
+  td_late_emit(x, en, cp, n, wold + L);
+}
+
 // getResult of a window that fires on an element of the ordered path (allowed lateness) while the push's values
 // are still buffered: as window_oracle.cpp emit, a copy of the digest -- its centroids compressed with the window's
 // values of this push so far, the sorted chain from `head` -- gives the quantiles (one thread of k_slow; the copy
@@ -3929,25 +4061,7 @@ __device__ void td_late_row(const SlowCtx& x, const Entry& en, int32_t head) {
   };
   const int64_t wt = h.w + L;
   const int32_t n = td_merge_run(c, c.td_qb, next, L, old, h.n, cp, wt);
-  const unsigned long long pos = atomicAdd(&x.st->out_rows, 1ull);
-  if ((int64_t)pos >= x.out.cap) {
-    atomicOr(&x.st->flags, FW_STATUS_OUT_FULL);
-    return;
-  }
-  write_row(c, x.out, pos, en);
-  const double mn = __longlong_as_double(x.out.mn[pos]), mx = __longlong_as_double(x.out.mx[pos]);
-  x.out.sum[pos] = __double_as_longlong(td_quantile(cp, n, wt, mn, mx, c.td_quant[0]));
-  x.out.mn[pos] = __double_as_longlong(td_quantile(cp, n, wt, mn, mx, c.td_quant[1]));
-  x.out.mx[pos] = __double_as_longlong(td_quantile(cp, n, wt, mn, mx, c.td_quant[2]));
-  if (x.out.dig) {
-    int64_t* d = x.out.dig + pos * (1 + 2 * (int64_t)c.td_nb);
-    d[0] = n;
-    for (int32_t k = 0; k < n; k++) {
-      d[1 + 2 * k] = __double_as_longlong(cp[k].sum);
-      d[2 + 2 * k] = td_weight(cp, k);
-    }
-  }
-  atomicAdd(&x.st->td_cent, (unsigned long long)n);
+  td_late_emit(x, en, cp, n, wt);
 }
 
 // getResult of a fired row (one thread): out.sum holds the block id and above it 1 + the block's free-stack slot
@@ -4138,26 +4252,7 @@ __global__ void k_td_mbuild(DevCfg c, TdBuf td, Status* st) {
       c.pool_defer[atomicAdd(&c.pool_ctr[2], 1)] = c.td_msrc[j];  // (a t-digest block needs no zeroing)
       if (td.mnext[j] == -2) break;
     }
-    // ordered by (mean key, weight, sum key) -- insertion sort, then the weights made cumulative
-    for (int32_t a = 1; a < m; a++) {
-      const TdCent x = u[a];
-      const uint64_t xm = td_mean_key(x.sum, x.cum), xs = td_key(__double_as_longlong(x.sum));
-      int32_t b = a - 1;
-      while (b >= 0) {
-        const uint64_t ym = td_mean_key(u[b].sum, u[b].cum);
-        const bool after = ym > xm || (ym == xm && (u[b].cum > x.cum ||
-                                                    (u[b].cum == x.cum && td_key(__double_as_longlong(u[b].sum)) > xs)));
-        if (!after) break;
-        u[b + 1] = u[b];
-        b--;
-      }
-      u[b + 1] = x;
-    }
-    int64_t cum = 0;
-    for (int32_t a = 0; a < m; a++) {
-      cum += u[a].cum;
-      u[a].cum = cum;
-    }
+    td_union_sort(u, m);
     const uint32_t g = td.binv[t];  // (the merging element was added to the target: k_td_keys set it)
     const int32_t ov = (int32_t)atomicAdd(&td.uctr[1], 1ull);
     td.ovr[ov] = TdOverride{u, m, g, wold};
@@ -7209,6 +7304,11 @@ __global__ void k_td_relink(DevCfg c, DevTable tb) {
     const int32_t p = c.td_ovp[j];
     const Region r = region_of(c, tb, p, tb.cur[p]);
     const int64_t k = c.td_ovk[j], last = c.td_ovt[j];
+    if (c.assigner == FW_SESSION) {  // (the session that holds the element now: merged sessions' values included)
+      const int32_t slot = session_containing(r, c, k, last);
+      c.td_olink[j] = slot < 0 ? -1 : atomicExch(&c.td_olast[((uint32_t)p << c.log_r) | (uint32_t)slot], (int32_t)j);
+      continue;
+    }
     for (int wi = 0; wi < c.td_ovn[j]; wi++) {
       const int64_t s = jsub(last, (int64_t)wi * c.slide);
       const int32_t slot = region_find(r, slot_hash(c, k, s), k, s, wend(c, s));

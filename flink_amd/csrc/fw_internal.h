@@ -140,6 +140,12 @@ struct DevCfg {
   // into its thread's td_late scratch (FW_SLOW_THREADS x td_nb)
   int32_t *td_ovn, *td_olast, *td_olink;
   TdCent* td_late;
+  // ... and session windows under allowed lateness: the blocks merged into a block during the push (td_bhead[block]
+  // -> td_bnext chain), and a late firing's union of their centroids in its thread's td_lateu scratch
+  // (FW_SLOW_THREADS x td_lateu_cap)
+  int32_t *td_bhead, *td_bnext;
+  TdCent* td_lateu;
+  int32_t td_lateu_cap;
   int64_t pool_blocks;
   int64_t pool_bytes;     // 0 = no pool
   // FW_AGG_TDIGEST (definition: oracle/window_oracle.h OR_AGG_TDIGEST): td_nb = delta / 2 buckets of the
@@ -253,7 +259,8 @@ enum {
   FW_STATUS_OUT_FULL = 2,
   FW_STATUS_MERGE_LATE = 4,
   FW_STATUS_SIDE_FULL = 8,
-  FW_STATUS_POOL = 16        // the accumulator block pool (HyperLogLog registers, t-digests) ran out of blocks
+  FW_STATUS_POOL = 16,       // the accumulator block pool (HyperLogLog registers, t-digests) ran out of blocks
+  FW_STATUS_TD_UNION = 32    // a late session firing joined more centroids than its union scratch holds
 };
 // a region takes new windows only up to this load; beyond it the kernel suspends and the table grows
 __host__ __device__ inline int32_t region_limit(int32_t log_r) { return (int32_t)((3ll << log_r) >> 2); }

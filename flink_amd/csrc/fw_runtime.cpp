@@ -583,6 +583,9 @@ int settle(fw_op* op) {
   if (s.flags & FW_STATUS_STATE_LOST)
     return set_err(op, FW_ERR_CAPACITY, "a window could not be stored (state region full)");
   if (s.flags & FW_STATUS_OUT_FULL) return set_err(op, FW_ERR_STATE, "fired-row buffer overflow");
+  if (s.flags & FW_STATUS_TD_UNION)
+    return set_err(op, FW_ERR_CAPACITY, "a late session firing joined more than %d t-digest centroids in one push",
+                   op->dc.td_lateu_cap);
   if (s.flags & FW_STATUS_POOL)
     return set_err(op, FW_ERR_CAPACITY, "accumulator block pool exhausted (%lld blocks; raise expected_entries)",
                    (long long)op->dc.pool_blocks);
@@ -779,6 +782,8 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   if (cc.agg == FW_AGG_TDIGEST && cc.td_olast) {  // (allowed lateness) ... and no window has a chain yet
     HIP_OR_RETURN(op, hipMemsetAsync(cc.td_ovctr, 0, sizeof(int32_t), op->stream));
     HIP_OR_RETURN(op, hipMemsetAsync(cc.td_olast, 0xff, (size_t)op->table_slots * sizeof(int32_t), op->stream));
+    if (cc.td_bhead)  // (sessions: no block has merged blocks yet)
+      HIP_OR_RETURN(op, hipMemsetAsync(cc.td_bhead, 0xff, (size_t)cc.pool_blocks * sizeof(int32_t), op->stream));
   }
   timed(
       op, K_AGGREGATE,
@@ -970,11 +975,10 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     if (!(cfg.tdigest_quantiles[i] >= 0.0 && cfg.tdigest_quantiles[i] <= 1.0))
       snprintf(msg, sizeof msg, "t-digest quantiles must be in [0, 1]");
   if (!msg[0] && cfg.aggregate == FW_AGG_TDIGEST &&
-      (cfg.value_type != FW_VAL_F64 || (cfg.assigner == FW_SESSION && (cfg.purging || cfg.allowed_lateness != 0)) ||
+      (cfg.value_type != FW_VAL_F64 || (cfg.assigner == FW_SESSION && cfg.purging) ||
        (cfg.allowed_lateness != 0 && cfg.purging))) {
-    snprintf(msg, sizeof msg, "the t-digest aggregate is offered over a Double field for tumbling and sliding windows "
-                              "(allowed lateness without PurgingTrigger) and session windows (without allowed lateness "
-                              "or PurgingTrigger)");
+    snprintf(msg, sizeof msg, "the t-digest aggregate is offered over a Double field for tumbling, sliding and session "
+                              "windows (PurgingTrigger only for tumbling / sliding windows without allowed lateness)");
     unsupported = true;
   }
   if (!msg[0] && cfg.aggregate >= FW_AGG_FIRST && cfg.aggregate <= FW_AGG_FIRST_MAX && cfg.assigner == FW_SLIDING && cfg.slide > 0 &&
@@ -1167,11 +1171,17 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
       HIP_OR_RETURN(op, dmalloc(&c.td_ovctr, 1));
       HIP_OR_RETURN(op, hipMemsetAsync(c.td_ovctr, 0, sizeof(int32_t), op->stream));
     }
-    if (c.assigner != FW_SESSION && c.lateness > 0) {  // late firings (DevCfg::td_olast ...)
-      HIP_OR_RETURN(op, dmalloc(&c.td_ovn, (size_t)mb));
+    if (c.lateness > 0) {  // late firings (DevCfg::td_olast ...)
+      if (c.assigner != FW_SESSION) HIP_OR_RETURN(op, dmalloc(&c.td_ovn, (size_t)mb));
       HIP_OR_RETURN(op, dmalloc(&c.td_olink, (size_t)(mb * c.wpr)));
       HIP_OR_RETURN(op, dmalloc(&c.td_olast, (size_t)op->table_slots));
       HIP_OR_RETURN(op, dmalloc(&c.td_late, (size_t)FW_SLOW_THREADS * c.td_nb));
+      if (c.assigner == FW_SESSION) {  // merged digests' unions (DevCfg::td_bhead ...)
+        c.td_lateu_cap = 16 * c.td_nb;
+        HIP_OR_RETURN(op, dmalloc(&c.td_bhead, (size_t)c.pool_blocks));
+        HIP_OR_RETURN(op, dmalloc(&c.td_bnext, (size_t)c.pool_blocks));
+        HIP_OR_RETURN(op, dmalloc(&c.td_lateu, (size_t)FW_SLOW_THREADS * c.td_lateu_cap));
+      }
     }
     if (c.assigner == FW_SESSION) {  // session merges (DevCfg::td_mdst, TdBuf::fwd ...; launch_tdigest)
       const size_t pb = (size_t)c.pool_blocks;
@@ -1287,9 +1297,10 @@ void fw_destroy(fw_op* op) {
     dfree(t.lidx);
     for (uint32_t* q : {op->dc.td_mdst, op->dc.td_msrc, t.fwd}) dfree(q);
     for (int32_t* q : {op->dc.td_mctr, op->dc.td_ovctr, op->dc.td_ovp, op->dc.td_ovn, op->dc.td_olink, op->dc.td_olast,
-                       t.mhead, t.mnext, t.mover})
+                       op->dc.td_bhead, op->dc.td_bnext, t.mhead, t.mnext, t.mover})
       dfree(q);
     dfree(op->dc.td_late);
+    dfree(op->dc.td_lateu);
     for (int64_t* q : {op->dc.td_ovk, op->dc.td_ovt, op->dc.td_ovv}) dfree(q);
     dfree(t.ovr);
     dfree(t.uni);

@@ -99,7 +99,7 @@ extern "C" {
                                       digest per window; allowed lateness without PurgingTrigger: a late firing
                                       reports the digest with the push's values so far) and session windows
                                       (merged sessions' digests merge: the union of their centroids, compressed
-                                      with the push's values; AbstractHeapMergingState.mergeNamespaces; no
+                                      with the push's values; AbstractHeapMergingState.mergeNamespaces; with
                                       allowed lateness, no PurgingTrigger), FW_VAL_F64; expected_entries sizes
                                       the digest pool.  Keyed-state snapshots
                                       carry the digest as an accumulator block (fw_snapshot_key_group_blocks). */

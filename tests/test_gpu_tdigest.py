@@ -48,7 +48,8 @@ def _run(batches, wms, delta, quantiles=(0.5, 0.95, 0.99), sliding=None, gap=Non
     gpu = GpuWindowOperator(assigner, TDigest(delta, quantiles, export=True), allowed_lateness=lateness, **kw)
     ref = (orc.WindowOperatorOracle(assigner="sliding", size=sliding[0], slide=sliding[1], tdigest=delta,
                                     quantiles=quantiles, lateness=lateness) if sliding else
-           orc.WindowOperatorOracle(assigner="session", gap=gap, tdigest=delta, quantiles=quantiles) if gap else
+           orc.WindowOperatorOracle(assigner="session", gap=gap, tdigest=delta, quantiles=quantiles,
+                                    lateness=lateness) if gap else
            orc.WindowOperatorOracle(assigner="tumbling", size=1000, tdigest=delta, quantiles=quantiles,
                                     lateness=lateness))
     g_rows, g_dig = [], []
@@ -116,18 +117,27 @@ def test_gpu_tdigest_sliding_vs_oracle(size, slide, zipf, jitter):
     assert any(len(s) > 10 for s, _ in out[1])
 
 
-@pytest.mark.parametrize("gap,zipf,jitter", [(300, 1.1, 200), (100, None, 900), (2000, 1.3, 400)],
-                         ids=["zipf", "uniform-out-of-order", "long-gap-hot"])
-def test_gpu_tdigest_sessions_vs_oracle(gap, zipf, jitter):
+@pytest.mark.parametrize("gap,zipf,jitter,lateness", [(300, 1.1, 200, 0), (100, None, 900, 0), (2000, 1.3, 400, 0),
+                                                      (300, 1.1, 1200, 800), (100, None, 900, 2000),
+                                                      (1000, 1.3, 1500, 3000)],
+                         ids=["zipf", "uniform-out-of-order", "long-gap-hot", "zipf-lateness", "uniform-lateness",
+                              "hot-long-lateness"])
+def test_gpu_tdigest_sessions_vs_oracle(gap, zipf, jitter, lateness):
     # a10: t-digest over EventTimeSessionWindows.  Sessions merge (MergingWindowSet.java:150-225) and their digests
     # with them (AbstractHeapMergingState.mergeNamespaces, AbstractHeapMergingState.java:67-93; AggregateFunction.merge,
     # AggregateFunction.java:160; this build's merge = the union of the centroids, compressed with the push's values,
     # oracle td_union) -- in the parallel session flush, in the ordered replay of elements that arrive behind the
-    # watermark and bridge in-flight sessions, and across pushes.  Centroids and quantiles bit-exact.
+    # watermark and bridge in-flight sessions, and across pushes.  Under allowed lateness a session that an element
+    # reaches behind the watermark fires again at once (WindowOperator.java:352-360) with getResult over its digest --
+    # the union of the digests merged into it in the push and the push's values so far (the oracle compresses a copy).
+    # Centroids and quantiles bit-exact.
     batches, wms = _stream(200_000, 20_000, 3000, rate=100_000, zipf=zipf, jitter=jitter, bound=200)
-    g_rows, g_dig, r_rows, r_dig = _run(batches, wms, 40, gap=gap, expected_entries=30_000)
+    g_rows, g_dig, r_rows, r_dig = _run(batches, wms, 40, gap=gap, lateness=lateness, expected_entries=30_000)
     _assert_same(g_rows, g_dig, r_rows, r_dig, 40)
     assert (g_rows["end"] - g_rows["start"] > gap).any()  # sessions merged
+    if lateness:
+        keys = np.stack([g_rows["key"], g_rows["start"]], axis=1)
+        assert len(np.unique(keys, axis=0)) < len(keys)  # sessions fired more than once
 
 
 @pytest.mark.parametrize("sliding,lateness,zipf,jitter",
@@ -212,7 +222,7 @@ def test_gpu_tdigest_refuses_unsupported_shapes():
     from flink_amd import EventTimeSessionWindows, EventTimeTrigger, PurgingTrigger
     purge = PurgingTrigger.of(EventTimeTrigger.create())
     for kw in (dict(assigner=EventTimeSessionWindows.with_gap(1000), trigger=purge),
-               dict(assigner=EventTimeSessionWindows.with_gap(1000), allowed_lateness=10),
+               dict(assigner=EventTimeSessionWindows.with_gap(1000), allowed_lateness=10, trigger=purge),
                dict(allowed_lateness=10, trigger=purge),
                dict(assigner=SlidingEventTimeWindows.of(3000, 1000), allowed_lateness=10, trigger=purge)):
         with pytest.raises(N.NativeError) as e:
