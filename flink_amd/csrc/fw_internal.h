@@ -50,7 +50,9 @@
 #ifndef FW_AGG_CHUNK
 #define FW_AGG_CHUNK 32768     // records per aggregate workgroup of a split partition (hot keys); 16384 -> 32768: C4 6.9e9 -> 7.7e9, C5 6.1e9 -> 6.7e9 records/s
 #endif
-#define FW_LDS_SLOTS 1024      // LDS pre-aggregation slots per aggregate workgroup
+#ifndef FW_LDS_SLOTS
+#define FW_LDS_SLOTS 1024      // LDS pre-aggregation slots per aggregate workgroup (a power of two)
+#endif
 #ifndef FW_LDS_FILL_LIMIT
 #define FW_LDS_FILL_LIMIT 820  // ~0.8 * FW_LDS_SLOTS: a new slot is not claimed beyond this fill
 #endif
