@@ -1485,6 +1485,48 @@ __device__ __forceinline__ bool lds_upsert(AggLds& L, int vtype, int64_t key, in
   return true;
 }
 
+// lds_acc (count / sum / min / max) of the lanes with ok set, each into its slot tg: when the whole wave runs and
+// every such lane takes the same slot (a hot key's session), the wave sums its values first and one lane does the
+// atomics -- sixty-four lanes' atomics on one LDS address otherwise serialise.  (A Double sum's order is not the
+// arrival order either way; integer sums are exact.)
+__device__ __forceinline__ void lds_acc_wave(AggLds& L, int tg, int vtype, int64_t v, bool ok, int first = 0) {
+  const uint64_t okm = __ballot(ok);
+  if ((first == 0 || first == LDS_CNT_ONLY) && __ballot(1) == ~0ull && __popcll(okm) >= 8) {
+    const int lead = __ffsll((unsigned long long)okm) - 1;
+    const int t0 = __shfl(tg, lead, 64);
+    if (__ballot(ok && tg == t0) == okm) {
+      if (first == LDS_CNT_ONLY) {  // (HyperLogLog: the registers are the accumulator, the slot keeps the count)
+        if (__lane_id() == lead) atomicAdd(&L.cnt[t0], (uint32_t)__popcll(okm));
+        return;
+      }
+      const bool f64 = vtype == FW_VAL_F64;
+      const int64_t key = f64 ? f64_sortable(v) : v;
+      int64_t mn = ok ? key : LMAX, mx = ok ? key : LMIN;
+      double ds = ok && f64 ? __longlong_as_double(v) : 0.0;
+      unsigned long long is = ok && !f64 ? (unsigned long long)v : 0ull;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (int64_t)__shfl_xor((long long)mn, o, 64));
+        mx = max(mx, (int64_t)__shfl_xor((long long)mx, o, 64));
+        if (f64)
+          ds += __shfl_xor(ds, o, 64);
+        else
+          is += (unsigned long long)__shfl_xor((long long)is, o, 64);
+      }
+      if (__lane_id() == lead) {
+        atomicAdd(&L.cnt[t0], (uint32_t)__popcll(okm));
+        if (f64)
+          atomicAdd((double*)&L.sum[t0], ds);
+        else
+          atomicAdd((unsigned long long*)&L.sum[t0], is);
+        if (mn < *(volatile int64_t*)&L.mn[t0]) atomicMin((long long*)&L.mn[t0], (long long)mn);
+        if (mx > *(volatile int64_t*)&L.mx[t0]) atomicMax((long long*)&L.mx[t0], (long long)mx);
+      }
+      return;
+    }
+  }
+  if (ok) lds_acc(L, tg, vtype, v, 0, first);
+}
 // One-window records (tumbling, panes), RPT per thread: every record's (key, window) is first looked up in
 // its home bucket with all RPT lookups in flight together (tag bucket, then the candidate's key), and the
 // hits accumulate at once; the rest (new windows, fingerprint collisions, buckets being claimed) go through
@@ -1756,44 +1798,6 @@ __device__ __forceinline__ int lds_session_slot(AggLds& L, int64_t* E, int64_t k
   if (*(volatile long long*)st > (long long)ws) atomicMin(st, (long long)ws);
   if (*(volatile int64_t*)&E[target] < we) atomicMax((long long*)&E[target], (long long)we);
   return target;
-}
-// lds_acc (count / sum / min / max) of the lanes with ok set, each into its slot tg: when the whole wave runs and
-// every such lane takes the same slot (a hot key's session), the wave sums its values first and one lane does the
-// atomics -- sixty-four lanes' atomics on one LDS address otherwise serialise.  (A Double sum's order is not the
-// arrival order either way; integer sums are exact.)
-__device__ __forceinline__ void lds_acc_wave(AggLds& L, int tg, int vtype, int64_t v, bool ok) {
-  const uint64_t okm = __ballot(ok);
-  if (__ballot(1) == ~0ull && __popcll(okm) >= 8) {
-    const int lead = __ffsll((unsigned long long)okm) - 1;
-    const int t0 = __shfl(tg, lead, 64);
-    if (__ballot(ok && tg == t0) == okm) {
-      const bool f64 = vtype == FW_VAL_F64;
-      const int64_t key = f64 ? f64_sortable(v) : v;
-      int64_t mn = ok ? key : LMAX, mx = ok ? key : LMIN;
-      double ds = ok && f64 ? __longlong_as_double(v) : 0.0;
-      unsigned long long is = ok && !f64 ? (unsigned long long)v : 0ull;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        mn = min(mn, (int64_t)__shfl_xor((long long)mn, o, 64));
-        mx = max(mx, (int64_t)__shfl_xor((long long)mx, o, 64));
-        if (f64)
-          ds += __shfl_xor(ds, o, 64);
-        else
-          is += (unsigned long long)__shfl_xor((long long)is, o, 64);
-      }
-      if (__lane_id() == lead) {
-        atomicAdd(&L.cnt[t0], (uint32_t)__popcll(okm));
-        if (f64)
-          atomicAdd((double*)&L.sum[t0], ds);
-        else
-          atomicAdd((unsigned long long*)&L.sum[t0], is);
-        if (mn < *(volatile int64_t*)&L.mn[t0]) atomicMin((long long*)&L.mn[t0], (long long)mn);
-        if (mx > *(volatile int64_t*)&L.mx[t0]) atomicMax((long long*)&L.mx[t0], (long long)mx);
-      }
-      return;
-    }
-  }
-  if (ok) lds_acc(L, tg, vtype, v, 0, 0);
 }
 __device__ __forceinline__ bool lds_session_upsert(AggLds& L, int64_t* E, int vtype, int64_t key, int64_t ws,
                                                    int64_t we, int64_t v, int64_t fo = 0, int first = 0) {
