@@ -2055,9 +2055,9 @@ __device__ bool session_fresh_chain(const DevCfg& c, const Region& r, AggLds& L,
 // flush of the session LDS table.  Every LDS slot takes at most one new region slot, so the load limit
 // is checked up front (live + fill), before anything changes.  A key's slots lie in the buckets from
 // its home bucket to the first one with an EMPTY slot (a bucket fills front to back and is passed only
-// when full).  Pass 1 links each key's slots in that order through L.slot (next slot + 1, bit 16 =
-// first slot, which owns the key); pass 2 lets every owner add its key's slots one per step, so the
-// lanes of a wave call session_add together instead of one after another.
+// when full).  Pass 1 lists each key's slots on its first slot, which owns the key (L.slot: next slot + 1);
+// pass 2 lets every owner add its key's slots one per step, so the lanes of a wave call session_add
+// together instead of one after another.
 __device__ __forceinline__ bool agg_flush_session(const DevCfg& c, AggLds& L, const int64_t* E, const Region& r,
                                                   Status* st) {
   __syncthreads();
@@ -2074,45 +2074,37 @@ __device__ __forceinline__ bool agg_flush_session(const DevCfg& c, AggLds& L, co
     if (threadIdx.x == 0) atomicMax(&st->need_live, need);
     return false;
   }
-  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) {
-    if (L.tag[h] < 2) continue;
+  // pass 1: every slot finds its key's owner (the key's first slot from its home bucket) and, unless it is the owner,
+  // puts itself on the owner's list (L.slot: next + 1, 0 = the end).  The order of a key's slots on the list does not
+  // matter: its intervals' merges commute.
+  constexpr int FQ = (FW_LDS_SLOTS + FW_AGG_THREADS - 1) / FW_AGG_THREADS;
+  for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.slot[h] = 0;
+  __syncthreads();
+  bool is_owner[FQ];
+#pragma unroll
+  for (int q = 0; q < FQ; q++) {
+    const int h = threadIdx.x + q * (int)blockDim.x;
+    is_owner[q] = false;
+    if (h >= FW_LDS_SLOTS || L.tag[h] < 2) continue;
     const int64_t key = L.kv[h].x;
     const uint32_t hk = lds_hash(key, 0), fp = lds_fp(hk);
-    int owner = -1;
-    bool end = false;
-    for (uint32_t i = 0, b = hk & (LDS_BUCKETS - 1); i < LDS_BUCKETS && owner < 0 && !end;
-         i++, b = (b + 1) & (LDS_BUCKETS - 1)) {
-      for (int q = 0; q < 4; q++) {
-        const int s = (int)b * 4 + q;
-        const uint32_t t = L.tag[s];
-        if (t == LT_EMPTY) {
-          end = true;
-          break;
-        }
-        if (t == fp && L.kv[s].x == key) {
-          owner = s;
-          break;
+    int owner = h;
+    bool found = false;
+    for (uint32_t i = 0, b = hk & (LDS_BUCKETS - 1); i < LDS_BUCKETS && !found; i++, b = (b + 1) & (LDS_BUCKETS - 1)) {
+      const u32x4 t4 = *reinterpret_cast<const u32x4*>(&L.tag[b * 4]);
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t t = u == 0 ? t4.x : u == 1 ? t4.y : u == 2 ? t4.z : t4.w;
+        if (!found && t == fp && L.kv[b * 4 + u].x == key) {
+          owner = (int)b * 4 + u;
+          found = true;
         }
       }
     }
-    int nxt = -1;
-    end = false;
-    for (uint32_t i = 0, b = (uint32_t)h / 4; i < LDS_BUCKETS && nxt < 0 && !end;
-         i++, b = (b + 1) & (LDS_BUCKETS - 1)) {
-      for (int q = i == 0 ? h % 4 + 1 : 0; q < 4; q++) {
-        const int s = (int)b * 4 + q;
-        const uint32_t t = L.tag[s];
-        if (t == LT_EMPTY) {
-          end = true;
-          break;
-        }
-        if (t == fp && L.kv[s].x == key) {
-          nxt = s;
-          break;
-        }
-      }
-    }
-    L.slot[h] = (nxt + 1) | (owner == h ? 1 << 16 : 0);
+    if (owner == h)
+      is_owner[q] = true;
+    else
+      L.slot[h] = atomicExch(&L.slot[owner], h + 1);
   }
   __syncthreads();
   const unsigned long long ts1 = timing ? __builtin_amdgcn_s_memtime() : 0;
@@ -2138,13 +2130,12 @@ __device__ __forceinline__ bool agg_flush_session(const DevCfg& c, AggLds& L, co
   };
   // this thread's owner slots: their home slots claimed together (the claims in flight at once); a claimed key
   // with one interval is a new session, written and published with one fence for all of them
-  constexpr int FQ = (FW_LDS_SLOTS + FW_AGG_THREADS - 1) / FW_AGG_THREADS;
   int32_t pre[FQ];
   bool pub[FQ];
 #pragma unroll
   for (int q = 0; q < FQ; q++) {
     const int h = threadIdx.x + q * (int)blockDim.x;
-    const bool own = h < FW_LDS_SLOTS && L.tag[h] >= 2 && (L.slot[h] >> 16);
+    const bool own = is_owner[q];
     pre[q] = own ? session_claim_home(c, r, L.kv[h].x) : -3;
   }
   bool anypub = false;
