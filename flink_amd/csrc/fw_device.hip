@@ -2077,14 +2077,16 @@ __device__ __forceinline__ bool agg_flush_session(const DevCfg& c, AggLds& L, co
   // pass 1: every slot finds its key's owner (the key's first slot from its home bucket) and, unless it is the owner,
   // puts itself on the owner's list (L.slot: next + 1, 0 = the end).  The order of a key's slots on the list does not
   // matter: its intervals' merges commute.
+  // The owners go on a dense list (s_own), so that the adds spread one owner per lane before any lane takes two.
   constexpr int FQ = (FW_LDS_SLOTS + FW_AGG_THREADS - 1) / FW_AGG_THREADS;
+  __shared__ uint16_t s_own[FW_LDS_SLOTS];
+  __shared__ int s_nown;
   for (int h = threadIdx.x; h < FW_LDS_SLOTS; h += blockDim.x) L.slot[h] = 0;
+  if (threadIdx.x == 0) s_nown = 0;
   __syncthreads();
-  bool is_owner[FQ];
 #pragma unroll
   for (int q = 0; q < FQ; q++) {
     const int h = threadIdx.x + q * (int)blockDim.x;
-    is_owner[q] = false;
     if (h >= FW_LDS_SLOTS || L.tag[h] < 2) continue;
     const int64_t key = L.kv[h].x;
     const uint32_t hk = lds_hash(key, 0), fp = lds_fp(hk);
@@ -2102,11 +2104,12 @@ __device__ __forceinline__ bool agg_flush_session(const DevCfg& c, AggLds& L, co
       }
     }
     if (owner == h)
-      is_owner[q] = true;
+      s_own[atomicAdd(&s_nown, 1)] = (uint16_t)h;
     else
       L.slot[h] = atomicExch(&L.slot[owner], h + 1);
   }
   __syncthreads();
+  const int nown = s_nown;
   const unsigned long long ts1 = timing ? __builtin_amdgcn_s_memtime() : 0;
   int nnew = 0;
   int64_t mt = LMAX;
@@ -2132,16 +2135,17 @@ __device__ __forceinline__ bool agg_flush_session(const DevCfg& c, AggLds& L, co
   // with one interval is a new session, written and published with one fence for all of them
   int32_t pre[FQ];
   bool pub[FQ];
+  int oh[FQ];  // this thread's owners' slots
 #pragma unroll
   for (int q = 0; q < FQ; q++) {
-    const int h = threadIdx.x + q * (int)blockDim.x;
-    const bool own = is_owner[q];
-    pre[q] = own ? session_claim_home(c, r, L.kv[h].x) : -3;
+    const int oi = threadIdx.x + q * (int)blockDim.x;
+    oh[q] = oi < nown ? (int)s_own[oi] : -1;
+    pre[q] = oh[q] >= 0 ? session_claim_home(c, r, L.kv[oh[q]].x) : -3;
   }
   bool anypub = false;
 #pragma unroll
   for (int q = 0; q < FQ; q++) {
-    const int h = threadIdx.x + q * (int)blockDim.x;
+    const int h = oh[q];
     pub[q] = pre[q] >= 0 && (L.slot[h] & 0xffff) == 0;
     if (!pub[q]) continue;
     Entry nd = delta(h);
@@ -2155,14 +2159,13 @@ __device__ __forceinline__ bool agg_flush_session(const DevCfg& c, AggLds& L, co
   if (anypub) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 #pragma unroll
   for (int q = 0; q < FQ; q++) {
-    const int h = threadIdx.x + q * (int)blockDim.x;
     if (pub[q])
-      st_state_wg(r.state + pre[q], live_word(slot_hash(c, L.kv[h].x, 0)));
+      st_state_wg(r.state + pre[q], live_word(slot_hash(c, L.kv[oh[q]].x, 0)));
   }
 #pragma unroll
   for (int q = 0; q < FQ; q++) {
     if (pre[q] == -3 || pub[q]) continue;
-    int j = threadIdx.x + q * (int)blockDim.x;
+    int j = oh[q];
     int32_t pq = pre[q];
 #ifndef FW_SESS_FRESH
 #define FW_SESS_FRESH 1
