@@ -7157,7 +7157,7 @@ void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint
     hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true, false, true>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb, prog,
                        resume, st, h, nr, 0);
   else if (c.assigner == FW_SESSION)
-    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true, false, false>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb,
+    hipLaunchKernelGGL((k_aggregate<FW_SESS_RPT, true, false, false>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb,
                        prog, resume, st, h, nr, 0);
   else if (first)
     hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false, true, false>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb,

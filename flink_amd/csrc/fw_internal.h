@@ -40,6 +40,9 @@
 #ifndef FW_GATHER_WAVES
 #define FW_GATHER_WAVES 4  // the gathered instantiation: its runs table takes 12 KB of LDS, 2 workgroups per CU
 #endif
+#ifndef FW_SESS_RPT
+#define FW_SESS_RPT 1  // records per thread in flight in the count/sum/min/max session instantiation (1: 1.19e10 -> 1.24e10 at C4 against 2; 3, 4 slower)
+#endif
 #ifndef FW_SESS_WAVES
 #define FW_SESS_WAVES 4  // the same for the session instantiation
 #endif
