@@ -7154,7 +7154,7 @@ void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint
     hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true, true, false>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb, prog,
                        resume, st, h, nr, 0);
   else if (c.assigner == FW_SESSION && pool)
-    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, true, false, true>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb, prog,
+    hipLaunchKernelGGL((k_aggregate<FW_SESS_RPT, true, false, true>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb, prog,
                        resume, st, h, nr, 0);
   else if (c.assigner == FW_SESSION)
     hipLaunchKernelGGL((k_aggregate<FW_SESS_RPT, true, false, false>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb,
@@ -7163,10 +7163,10 @@ void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint
     hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false, true, false>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb,
                        prog, resume, st, h, nr, 0);
   else if (pool)
-    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false, false, true>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb,
+    hipLaunchKernelGGL((k_aggregate<FW_POOL_RPT, false, false, true>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb,
                        prog, resume, st, h, nr, 0);
   else
-    hipLaunchKernelGGL((k_aggregate<FW_AGG_RPT, false, false, false>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb,
+    hipLaunchKernelGGL((k_aggregate<FW_PLAIN_RPT, false, false, false>), dim3(grid), b, 0, s, c, wm, part, offs, T, tb,
                        prog, resume, st, h, nr, 0);
 }
 

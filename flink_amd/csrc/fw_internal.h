@@ -40,6 +40,12 @@
 #ifndef FW_GATHER_WAVES
 #define FW_GATHER_WAVES 4  // the gathered instantiation: its runs table takes 12 KB of LDS, 2 workgroups per CU
 #endif
+#ifndef FW_POOL_RPT
+#define FW_POOL_RPT FW_AGG_RPT  // the same for the pooled (HyperLogLog, t-digest) one-window instantiation
+#endif
+#ifndef FW_PLAIN_RPT
+#define FW_PLAIN_RPT FW_AGG_RPT  // ... and the plain count/sum/min/max one (not the dense regions)
+#endif
 #ifndef FW_SESS_RPT
 #define FW_SESS_RPT 1  // records per thread in flight in the count/sum/min/max session instantiation (1: 1.19e10 -> 1.24e10 at C4 against 2; 3, 4 slower)
 #endif
