@@ -2231,7 +2231,7 @@ __global__ void k_chunk_plan(DevCfg c, const uint32_t* __restrict__ offs, int32_
     return;
   }
   const int64_t len = (int64_t)offs[(int64_t)(p + 1) * T] - offs[(int64_t)p * T];
-  hot.chunk_base[p] = len > FW_AGG_CHUNK ? (uint32_t)((len + FW_AGG_CHUNK - 1) / FW_AGG_CHUNK) : 1u;
+  hot.chunk_base[p] = len > c.agg_chunk ? (uint32_t)((len + c.agg_chunk - 1) / c.agg_chunk) : 1u;
   hot.pdone[p] = 0;
 }
 
@@ -2430,7 +2430,7 @@ __device__ __forceinline__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E
   }
   __syncthreads();
   if (!resume) {
-    const int64_t cb = begin + (int64_t)ch * FW_AGG_CHUNK, ce = min(end, cb + (int64_t)FW_AGG_CHUNK);
+    const int64_t cb = begin + (int64_t)ch * c.agg_chunk, ce = min(end, cb + (int64_t)c.agg_chunk);
     int64_t myrb = cb;
     uint32_t dm = 0;
     for (;;) {  // free-running waves (agg_walk); the table is spilled as deltas whenever it fills
@@ -2471,8 +2471,8 @@ __device__ __forceinline__ void agg_split(const DevCfg& c, AggLds& L, int64_t* E
   __syncthreads();
   const Region r = region_of(c, tb, p, tb.cur[p]);
   bool ok = true, first = true;
-  for (int32_t j = (int32_t)((srb - begin) / FW_AGG_CHUNK); j < nch && ok; j++) {
-    const int64_t db = begin + (int64_t)j * FW_AGG_CHUNK, de = db + hot.nd[c0 + j];
+  for (int32_t j = (int32_t)((srb - begin) / c.agg_chunk); j < nch && ok; j++) {
+    const int64_t db = begin + (int64_t)j * c.agg_chunk, de = db + hot.nd[c0 + j];
     for (int64_t rb = max(db, srb); rb < de && ok; rb += (int64_t)blockDim.x * RPT) {
       Entry d[RPT];
 #pragma unroll
@@ -7125,9 +7125,9 @@ void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint
   c.nt_floor = pane_nt_floor(c, wm);
   AggHot h{};
   unsigned grid = (unsigned)c.P;
-  if (hot) {  // at most n / FW_AGG_CHUNK chunks beyond one per partition
+  if (hot) {  // at most n / agg_chunk chunks beyond one per partition
     h = *hot;
-    grid += (unsigned)((n + FW_AGG_CHUNK - 1) / FW_AGG_CHUNK);
+    grid += (unsigned)((n + c.agg_chunk - 1) / c.agg_chunk);
     if (!resume) {
       hipLaunchKernelGGL(k_chunk_plan, dim3((c.P + 1 + 255) / 256), dim3(256), 0, s, c, offs, T, h);
       launch_scan(h.chunk_base, (int64_t)c.P + 1, h.scan_tmp, s);

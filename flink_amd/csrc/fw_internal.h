@@ -191,6 +191,7 @@ struct DevCfg {
   // [0, live) of its current buffer, without state words; k_dt_aggregate rewrites a region into its other buffer
   // from an LDS table, k_dt_fire streams it (fw_device.hip, "dense tumbling regions")
   int32_t dense;
+  int32_t agg_chunk;  // records per aggregate workgroup of a split partition (FW_AGG_CHUNK, or twice it)
 };
 
 // host: reciprocal of d >= 1 for div_inv(): m = floor(2^64 (2^l - d) / d) + 1, l = ceil(log2 d)

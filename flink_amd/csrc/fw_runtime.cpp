@@ -772,7 +772,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   cc.cbase = c.cbase;
   cc.wide = c.wide;
   // a partition can outgrow one aggregate workgroup (hot keys) only when the batch is longer than a chunk
-  const bool split = !cc.dense && (cc.wpr == 1 || cc.panes) && n > FW_AGG_CHUNK;
+  const bool split = !cc.dense && (cc.wpr == 1 || cc.panes) && n > cc.agg_chunk;
   if (split && (rc = ensure_hot(op))) return rc;
   if (cc.agg == FW_AGG_TDIGEST && cc.assigner == FW_SESSION) {  // the push's merge log and ordered values start empty
     HIP_OR_RETURN(op, hipMemsetAsync(cc.td_mctr, 0, sizeof(int32_t), op->stream));
@@ -1070,6 +1070,9 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
               !(getenv("FW_NO_COMPACT") && atoi(getenv("FW_NO_COMPACT")));
   const int64_t expected = cfg.expected_entries > 0 ? cfg.expected_entries : (int64_t)c.P * 512;
   if (cfg.aggregate >= FW_AGG_FIRST) c.agg = cfg.aggregate;  // (FW_AGG_HLL is set below)
+  // records per aggregate workgroup of a split (hot) partition: HyperLogLog over time windows takes twice as many
+  // (its aggregate keeps the count only; C5 1.00e10 -> 1.08e10 records/s; C4 and C5t measured no better)
+  c.agg_chunk = cfg.aggregate == FW_AGG_HLL && cfg.assigner != FW_SESSION ? 2 * FW_AGG_CHUNK : FW_AGG_CHUNK;
   if (cfg.aggregate == FW_AGG_HLL) {
     // register pool: one 2^p-byte block per live (key, window); expected_entries live entries, plus
     // a quarter for entries created before the watermark that retires their predecessors
