@@ -59,6 +59,9 @@
 #ifndef FW_AGG_CHUNK
 #define FW_AGG_CHUNK 32768     // records per aggregate workgroup of a split partition (hot keys); 16384 -> 32768: C4 6.9e9 -> 7.7e9, C5 6.1e9 -> 6.7e9 records/s
 #endif
+#ifndef FW_HLL_AGG_CHUNK_MUL
+#define FW_HLL_AGG_CHUNK_MUL 2  // HyperLogLog over time windows: FW_AGG_CHUNK times this per split workgroup
+#endif
 #ifndef FW_LDS_SLOTS
 #define FW_LDS_SLOTS 1024      // LDS pre-aggregation slots per aggregate workgroup (a power of two)
 #endif

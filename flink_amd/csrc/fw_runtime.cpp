@@ -1072,7 +1072,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   if (cfg.aggregate >= FW_AGG_FIRST) c.agg = cfg.aggregate;  // (FW_AGG_HLL is set below)
   // records per aggregate workgroup of a split (hot) partition: HyperLogLog over time windows takes twice as many
   // (its aggregate keeps the count only; C5 1.00e10 -> 1.08e10 records/s; C4 and C5t measured no better)
-  c.agg_chunk = cfg.aggregate == FW_AGG_HLL && cfg.assigner != FW_SESSION ? 2 * FW_AGG_CHUNK : FW_AGG_CHUNK;
+  c.agg_chunk = cfg.aggregate == FW_AGG_HLL && cfg.assigner != FW_SESSION ? FW_HLL_AGG_CHUNK_MUL * FW_AGG_CHUNK : FW_AGG_CHUNK;
   if (cfg.aggregate == FW_AGG_HLL) {
     // register pool: one 2^p-byte block per live (key, window); expected_entries live entries, plus
     // a quarter for entries created before the watermark that retires their predecessors
