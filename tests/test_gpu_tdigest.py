@@ -3,7 +3,9 @@
 
 The bar is bit-exact: every fired row's centroids (sum bits and weights, via TDigest(export=True)) and its
 three quantile estimates equal the oracle's, for digests merged serially and for the hot ones merged
-bucket-parallel (more than FW_TD_SMALL = 2048 values + centroids in one push).  At the full C5 batch size
+bucket-parallel (more than FW_TD_T3 = 2048 values + centroids in one push); over tumbling, sliding and session
+windows (merged sessions' digests: the centroid union), and under allowed lateness (late firings: the digest with
+the push's values so far).  At the full C5 batch size
 (2^24 records per push, generated in HBM) the checks are size-independent: every record is counted once and
 the quantiles of the hottest keys lie within 1% in rank of the exact ones.
 """
