@@ -179,11 +179,38 @@ def job_cpu_share():
     return aff, f"the CPU affinity mask ({aff} cores)"
 
 
+def visible_gpus(topology="/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs this node offers the ranks, counted WITHOUT any HIP call (the launcher must not initialise the GPU: a
+    process that did must never be replaced, and torch.cuda.device_count() falls back to hipGetDeviceCount when the
+    amdsmi discovery fails).  The KFD topology lists one node per agent; GPU agents have a non-zero
+    gfx_target_version.  A *_VISIBLE_DEVICES list narrows the count.  None when the count is unavailable (the
+    ranks then find out for themselves)."""
+    import glob
+    n = 0
+    try:
+        for props in glob.glob(os.path.join(topology, "*", "properties")):
+            with open(props) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    if k == "gfx_target_version" and v.strip() not in ("", "0"):
+                        n += 1
+                        break
+    except OSError:
+        return None
+    if n == 0:
+        return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        lst = os.environ.get(var)
+        if lst is not None:
+            n = min(n, len([x for x in lst.split(",") if x.strip()]))
+    return n
+
+
 def launch_ranks(args, argv):
     """`--gpus N` (N > 1) without a torch.distributed launcher around it: start one rank per GPU with
     `python -m torch.distributed.run` (rendezvous on 127.0.0.1, one process per GPU, RCCL between them) and pass
-    its exit status on; rank 0 prints the JSON line.  This process never touches the GPU (counting devices does not
-    initialise HIP on this image) and never exec()s: the ranks are children."""
+    its exit status on; rank 0 prints the JSON line.  This process makes no HIP call (it counts GPUs from the KFD
+    topology, visible_gpus(); torch is not even imported) and never exec()s: the ranks are children."""
     import socket
     import subprocess
     with socket.socket() as so:
@@ -199,10 +226,9 @@ def launch_ranks(args, argv):
         print(json.dumps({"launch": cmd, "nproc": args.gpus,
                           "env": {k: env[k] for k in ("HSA_ENABLE_IPC_MODE_LEGACY", "MASTER_ADDR")}}), flush=True)
         return 0
-    import torch
-    have = torch.cuda.device_count()
+    have = visible_gpus()
     need = 1 if args.rehearse_gloo else args.gpus
-    if have < need:
+    if have is not None and have < need:
         print(f"bench.py: --gpus {args.gpus} needs {need} visible GPUs, this node shows {have}", file=sys.stderr,
               flush=True)
         return 2
@@ -237,7 +263,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU baseline subtasks (default: the job's CPU share, job_cpu_share())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--host-fed-steps", type=int, default=3, help="steps of the host-fed leg (0 = skip)")
+    ap.add_argument("--host-fed-steps", type=int, default=None,
+                    help="steps of the host-fed leg (0 = skip; default: enough event time to cross a window end, so "
+                         "fw_drain_rows moves rows)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic summary (tools/traffic.py); default the newest profiles/traffic_*<workload>.json")
@@ -251,6 +279,9 @@ def main():
     ap.add_argument("--sync-input", action="store_true",
                     help="partition each batch on the operator's own stream (no overlap with the previous batch)")
     args = ap.parse_args()
+    if args.combine and args.rehearse_gloo:
+        ap.error("--combine with --rehearse-gloo: the gloo rehearsal exchanges records through the Python exchange "
+                 "and would not combine (the line would claim a combining run)")
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and (args.gpus or 1) > 1:
         sys.exit(launch_ranks(args, sys.argv[1:]))
@@ -517,8 +548,14 @@ def main():
         alg = share[dom]
         achieved = alg / (kd["avg_ms"] * 1e-3) / 1e9
         traffic = tr.get(dom)
+        # the WHOLE step's algorithmic bytes (B_alg x records per launch) over the dominant
+        # kernel's duration alone: design-independent, an upper bound on any one kernel's frac
+        sec8d = alg_path / (kd["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "sec8d_frac": round(sec8d, 4),
+                    "sec8d_basis": "SURVEY §8d B_alg x records per launch / the dominant kernel's average duration",
+                    "traffic": traffic,
                     "alg_bytes_per_launch": int(alg), "alg_bytes_per_record": kd["alg_bytes_per_record"],
                     "path_alg_bytes_per_launch": int(alg_path),
                     "impl_bytes_per_launch": kd["impl_bytes"], "impl_frac": kd["impl_frac"],
@@ -553,6 +590,7 @@ def main():
             a_i = alg / (ki["avg_ms"] * 1e-3) / 1e9
             roofline["isolated"] = {"avg_ms": ki["avg_ms"], "achieved": round(a_i, 1),
                                     "frac": round(a_i / HBM_PEAK_GBS, 4),
+                                    "sec8d_frac": round(alg_path / (ki["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                     "basis": f"{iso_steps} further steps after the timed region with --sync-input "
                                              "(no overlap): the kernel's duration alone on the GPU"}
 
@@ -561,6 +599,12 @@ def main():
         count_gpu = count_window_leg(args, batches, local_rank)
 
     host_fed = None
+    if args.host_fed_steps is None:
+        # enough steps that the watermark passes a window end (a 1 s / 5 s window, C3's 1 s slide; sessions of C4 end
+        # every step at its 1e5 records per event-second), so the leg drains fired rows (WindowOperator.java:544-548)
+        period = args.slide if sliding else (1 if sessions else args.window)
+        event_ms = args.batch * 1000.0 / args.rate
+        args.host_fed_steps = int(min(12, max(3, (period + args.bound) / event_ms + 2)))
     if rank == 0 and world == 1 and args.host_fed_steps > 0:
         host_fed = host_fed_leg(args, op, generate, steps_total + iso_steps, m, c1)
 

@@ -99,6 +99,23 @@ __device__ __forceinline__ void compact_decode(const DevCfg& c, int32_t p, int64
   *key = (int64_t)(fmix64_inv(h) ^ SUB_SALT);
   *start = (int64_t)((uint64_t)c.cbase + ((uint64_t)kw >> sh) * (uint64_t)c.slide);
 }
+// ---- narrow records (DevCfg::narrow; dense single-pass batches): 8 bytes, {key << 35 | (d - ndn0) << 32 | (u32)value}
+// for a key in [-2^28, 2^28), a window delta d (compact_delta) in [ndn0, ndn0 + 8) and an int32 value.  The
+// aggregate widens a narrow record back to its CRec in registers (narrow_to_crec), so its LDS table and the region
+// entries are those of the compact form.
+constexpr int NW_DBITS = 3;
+__device__ __forceinline__ bool narrow_encode(const DevCfg& c, int64_t key, int64_t d, int64_t v, uint64_t* w) {
+  const int64_t dn = d - c.ndn0;
+  if ((uint64_t)dn >= (1ull << NW_DBITS) || key < -(1ll << 28) || key >= (1ll << 28) || v != (int64_t)(int32_t)v)
+    return false;
+  *w = ((uint64_t)key << 35) | ((uint64_t)dn << 32) | (uint64_t)(uint32_t)v;
+  return true;
+}
+__device__ __forceinline__ i64x2 narrow_to_crec(const DevCfg& c, uint64_t w) {
+  const int64_t key = (int64_t)w >> 35;
+  const int64_t d = (int64_t)((w >> 32) & ((1u << NW_DBITS) - 1)) + c.ndn0;
+  return i64x2{compact_encode(c, key, d), (int64_t)(int32_t)(uint32_t)w};
+}
 
 // earliest pending timer of an entry: trigger timer at maxTimestamp if registered, else GC timer
 __device__ __forceinline__ int64_t timer_of(const Entry& e, int64_t lateness) {
@@ -572,7 +589,12 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_classify_hist(DevCfg c, int
     }
     return;
   }
-  if (rsv && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st->rsv_fallbacks, 1);
+  if (rsv && blockIdx.x == 0 && threadIdx.x == 0) {
+    if (rsv[c.P + FW_RSV_NARROW])
+      atomicAdd(&st->narrow_misses, 1);
+    else
+      atomicAdd(&st->rsv_fallbacks, 1);
+  }
   extern __shared__ uint32_t lh[];
   for (int i = threadIdx.x; i <= c.P; i += blockDim.x) lh[i] = 0;
   __syncthreads();
@@ -816,7 +838,7 @@ __global__ __launch_bounds__(FW_TILE_THREADS, FW_SCATTER_WAVES) void k_scatter(D
 // compact form or a run longer than rcap sets rsv[P] (RSV_OVER): then the batch goes through classify, scan and the
 // offset scatter after all (those kernels are gated on rsv[P] and return at once without it).  The error and late
 // counts wait in rsv until the gated classify adds them to the status (RSV_* slots), so a redone batch counts once.
-template <int MODE, int RR, bool RSV>
+template <int MODE, int RR, bool RSV, bool NW = false>
 __device__ __forceinline__ void scatter_staged_body(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
                                                     const int64_t* __restrict__ ts, const int64_t* __restrict__ val,
                                                     const int32_t* __restrict__ kh, int64_t n, int32_t T,
@@ -824,8 +846,10 @@ __device__ __forceinline__ void scatter_staged_body(DevCfg c, int64_t wm, const 
                                                     DevSide side, Status* st, uint32_t* rsv, int64_t rcap) {
   specialize<MODE>(c);
   extern __shared__ __attribute__((aligned(16))) uint8_t sraw[];
-  i64x2* stg = reinterpret_cast<i64x2*>(sraw);          // RR: the round's records sorted by partition
-  uint16_t* sp = reinterpret_cast<uint16_t*>(stg + RR);  // RR: their partitions
+  // RR: the round's records sorted by partition (NW: narrow 8-byte records)
+  i64x2* stg = reinterpret_cast<i64x2*>(sraw);
+  uint64_t* stg8 = reinterpret_cast<uint64_t*>(sraw);
+  uint16_t* sp = reinterpret_cast<uint16_t*>(sraw + (size_t)RR * (NW ? 8 : 16));  // RR: their partitions
   uint32_t* gb = reinterpret_cast<uint32_t*>(sp + RR);   // P: next free slot of each partition's run
   uint32_t* cs = gb + c.P;                               // P + 1: the round's counts, then their starts in stg
   uint32_t* wsum = cs + c.P + 1;                         // block scan
@@ -841,10 +865,11 @@ __device__ __forceinline__ void scatter_staged_body(DevCfg c, int64_t wm, const 
   const int64_t tbase = (int64_t)tile * FW_TILE;
   const int64_t tend = min(n, tbase + (int64_t)FW_TILE);
   unsigned long long late = 0;
-  int bad_kg = 0, bad_ts = 0, over = 0;
+  int bad_kg = 0, bad_ts = 0, over = 0, nmiss = 0;
   constexpr int RPT = RR / FW_TILE_THREADS;
   const int ppt = (c.P + FW_TILE_THREADS - 1) / FW_TILE_THREADS;
   i64x2* out = reinterpret_cast<i64x2*>(part);
+  uint64_t* out8 = reinterpret_cast<uint64_t*>(part);
   for (int64_t b = tbase; b < tend; b += RR) {
     for (int i = threadIdx.x; i <= c.P; i += FW_TILE_THREADS) cs[i] = 0;
     __syncthreads();
@@ -881,9 +906,19 @@ __device__ __forceinline__ void scatter_staged_body(DevCfg c, int64_t wm, const 
             over = 1;
             continue;
           }
+          if constexpr (NW) {
+            uint64_t nw;
+            if (!narrow_encode(c, k[j], d, vh[j], &nw)) {  // no narrow form: the offset path, with CRecs
+              over = 1;
+              nmiss = 1;
+              continue;
+            }
+            w[jj] = (int64_t)nw;
+          } else {
+            w[jj] = compact_encode(c, k[j], d);
+          }
           rk[jj] = atomicAdd(&cs[p], 1u);
           pj[jj] = (uint32_t)p;
-          w[jj] = compact_encode(c, k[j], d);
         } else if (cls == CLS_LATE) {
           if (!RSV && c.side_output)
             side_one(side, st, k[j], t[j], vh[j]);
@@ -918,7 +953,10 @@ __device__ __forceinline__ void scatter_staged_body(DevCfg c, int64_t wm, const 
     for (int j = 0; j < RPT; j++) {
       if (pj[j] == 0xffffffffu) continue;
       const uint32_t pos = cs[pj[j]] + rk[j];
-      stg[pos] = i64x2{w[j], v[j]};
+      if constexpr (NW)
+        stg8[pos] = (uint64_t)w[j];
+      else
+        stg[pos] = i64x2{w[j], v[j]};
       sp[pos] = (uint16_t)pj[j];
     }
     if constexpr (RSV) {  // this round's piece of every partition it has records for
@@ -938,7 +976,10 @@ __device__ __forceinline__ void scatter_staged_body(DevCfg c, int64_t wm, const 
     for (uint32_t i = threadIdx.x; i < total; i += FW_TILE_THREADS) {
       const uint32_t pp = sp[i];
       if (RSV && gb[pp] == 0xffffffffu) continue;
-      out[gb[pp] + (i - cs[pp])] = stg[i];
+      if constexpr (NW)
+        out8[gb[pp] + (i - cs[pp])] = stg8[i];
+      else
+        out[gb[pp] + (i - cs[pp])] = stg[i];
     }
     __syncthreads();
     if constexpr (!RSV) {
@@ -948,6 +989,7 @@ __device__ __forceinline__ void scatter_staged_body(DevCfg c, int64_t wm, const 
   }
   if constexpr (RSV) {
     if (over) rsv[c.P + RSV_OVER] = 1;
+    if (NW && nmiss) rsv[c.P + FW_RSV_NARROW] = 1;
     if (bad_kg) atomicAdd(&rsv[c.P + RSV_KG], (uint32_t)bad_kg);
     if (bad_ts) atomicAdd(&rsv[c.P + RSV_TS], (uint32_t)bad_ts);
     if (late) atomicAdd(reinterpret_cast<unsigned long long*>(rsv + c.P + RSV_LATE), late);
@@ -967,14 +1009,14 @@ __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_staged(DevCfg c, in
   if (gate && !gate[0]) return;  // (the batch went through the single pass)
   scatter_staged_body<MODE, RR, false>(c, wm, key, ts, val, kh, n, T, offs, part, side, st, nullptr, 0);
 }
-// the single pass (tumbling windows, dense regions)
-template <int RR>
+// the single pass (tumbling windows, dense regions); NW: narrow records, rcap in 8-byte records
+template <int RR, bool NW>
 __global__ __launch_bounds__(FW_TILE_THREADS) void k_scatter_rsv(DevCfg c, int64_t wm, const int64_t* __restrict__ key,
                                                                 const int64_t* __restrict__ ts,
                                                                 const int64_t* __restrict__ val,
                                                                 const int32_t* __restrict__ kh, int64_t n, int32_t T,
                                                                 PRec* __restrict__ part, uint32_t* rsv, int64_t rcap) {
-  scatter_staged_body<M_TUMB, RR, true>(c, wm, key, ts, val, kh, n, T, nullptr, part, DevSide{}, nullptr, rsv, rcap);
+  scatter_staged_body<M_TUMB, RR, true, NW>(c, wm, key, ts, val, kh, n, T, nullptr, part, DevSide{}, nullptr, rsv, rcap);
 }
 
 // ---- K2b: ordered compaction of the ordered-path records of a tile (skipped by tiles that have none).
@@ -5838,12 +5880,16 @@ __global__ __launch_bounds__(FW_AGG_THREADS) void k_pmerge(DevCfg c, const Parti
         const int tg = lds_slot(L, d.key, d.start);
         if (tg >= 0) {
           atomicAdd(&L.cnt[tg], (uint32_t)d.cnt);
-          if (c.vtype == FW_VAL_F64)
-            atomicAdd((double*)&L.sum[tg], __longlong_as_double(d.sum));
-          else
-            atomicAdd((unsigned long long*)&L.sum[tg], (unsigned long long)d.sum);
-          atomicMin((long long*)&L.mn[tg], (long long)d.mn);
-          atomicMax((long long*)&L.mx[tg], (long long)d.mx);
+          // (HLL: the count only, as LDS_CNT_ONLY in the record path; a partial's sum column is its register count,
+          // which is not part of the accumulator, so snapshots of combined and uncombined windows agree)
+          if (c.agg != FW_AGG_HLL) {
+            if (c.vtype == FW_VAL_F64)
+              atomicAdd((double*)&L.sum[tg], __longlong_as_double(d.sum));
+            else
+              atomicAdd((unsigned long long*)&L.sum[tg], (unsigned long long)d.sum);
+            atomicMin((long long*)&L.mn[tg], (long long)d.mn);
+            atomicMax((long long*)&L.mx[tg], (long long)d.mx);
+          }
           done = true;
         } else {
           L.anyfail = 1;
@@ -6375,7 +6421,7 @@ __device__ unsigned long long g_dtt[6];
 template <int SRC, bool KW>
 __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, int32_t p, const Entry* __restrict__ src,
                                           int32_t live, Entry* __restrict__ dst, int64_t R, const void* __restrict__ in,
-                                          int64_t begin, int64_t end, bool cmp, int hb) {
+                                          int64_t begin, int64_t end, bool cmp, int hb, bool nar) {
   constexpr int NS = KW ? DK_SLOTS : FW_DT_SLOTS;
   const PRec* __restrict__ part = reinterpret_cast<const PRec*>(in);
   const PartialRec* __restrict__ pin = reinterpret_cast<const PartialRec*>(in);
@@ -6392,7 +6438,26 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
   constexpr int RPT = FW_DT_RPT;
   constexpr int64_t RS = (int64_t)FW_DT_THREADS * RPT;
   const i64x2* __restrict__ crec = reinterpret_cast<const i64x2*>(in);
+  const uint64_t* __restrict__ nrec = reinterpret_cast<const uint64_t*>(in);
+  // record j of this thread in the round at r0: CRecs lane-strided; narrow records (nar) in lane pairs, so a lane
+  // reads its two with one 16-byte load (the run starts at an even record: p * 2 rcap)
+  auto ridx = [&](int64_t r0, int j) -> int64_t {
+    return nar ? r0 + (int64_t)(j & ~1) * FW_DT_THREADS + 2 * (int64_t)threadIdx.x + (j & 1)
+               : r0 + (int64_t)j * FW_DT_THREADS + threadIdx.x;
+  };
   auto load = [&](i64x2 (&d)[RPT], int64_t r0) {
+    if (nar) {
+      static_assert(RPT % 2 == 0, "narrow records are loaded in pairs");
+#pragma unroll
+      for (int j = 0; j < RPT; j += 2) {
+        int64_t i = r0 + (int64_t)j * FW_DT_THREADS + 2 * (int64_t)threadIdx.x;
+        if (i >= end) i = (end - 1) & ~(int64_t)1;
+        const i64x2 q = *reinterpret_cast<const i64x2*>(nrec + i);
+        d[j] = narrow_to_crec(c, (uint64_t)q.x);
+        d[j + 1] = narrow_to_crec(c, (uint64_t)q.y);
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < RPT; j++) {
       const int64_t i = r0 + (int64_t)j * FW_DT_THREADS + threadIdx.x;
@@ -6473,7 +6538,7 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
             for (int j = 0; j < RPT; j++) {
               ww[j] = (unsigned long long)cur[j].x;
               vv[j] = cur[j].y;
-              const int64_t i = r0 + (int64_t)j * FW_DT_THREADS + threadIdx.x;
+              const int64_t i = ridx(r0, j);
               if (i >= end) {
                 dm |= 1u << j;
                 continue;
@@ -6502,25 +6567,29 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
             M.over = 1;
         } else {
           i64x2 ca[RPT], cb[RPT];
+          // (narrow records: widened to their CRec on load, then read as a compact batch)
+          auto ld = [&](int64_t i, i64x2& a, i64x2& b) {
+            if (nar) {
+              a = i < end ? narrow_to_crec(c, nrec[i]) : i64x2{0, 0};
+              b = i64x2{0, 0};
+            } else {
+              load_prec_raw(cmp, part, i, i < end, a, b);
+            }
+          };
+          const bool cm = cmp || nar;
 #pragma unroll
-          for (int j = 0; j < RPT; j++) {
-            const int64_t i = begin + (int64_t)j * FW_DT_THREADS + threadIdx.x;
-            load_prec_raw(cmp, part, i, i < end, ca[j], cb[j]);
-          }
+          for (int j = 0; j < RPT; j++) ld(begin + (int64_t)j * FW_DT_THREADS + threadIdx.x, ca[j], cb[j]);
           for (int64_t rb = begin; rb < end; rb += RS) {
             i64x2 na[RPT], nb[RPT];
 #pragma unroll
-            for (int j = 0; j < RPT; j++) {
-              const int64_t i = rb + RS + (int64_t)j * FW_DT_THREADS + threadIdx.x;
-              load_prec_raw(cmp, part, i, i < end, na[j], nb[j]);
-            }
+            for (int j = 0; j < RPT; j++) ld(rb + RS + (int64_t)j * FW_DT_THREADS + threadIdx.x, na[j], nb[j]);
             uint32_t dm = 0;
             int64_t kk[RPT], tt[RPT], vv[RPT];
 #pragma unroll
             for (int j = 0; j < RPT; j++) {
               int64_t o;
               int nw;
-              unpack_prec<false>(c, cmp, p, ca[j], cb[j], kk[j], tt[j], vv[j], nw, o);
+              unpack_prec<false>(c, cm, p, ca[j], cb[j], kk[j], tt[j], vv[j], nw, o);
               const int64_t i = rb + (int64_t)j * FW_DT_THREADS + threadIdx.x;
               if (i >= end || (hb && dt_pass(c, kk[j], tt[j], hb) != k)) dm |= 1u << j;
             }
@@ -6638,7 +6707,8 @@ __global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const 
   if (p >= c.P || (resume && prog.done[p])) return;
   // the partition's run: at the scan offsets, or where the single-pass scatter reserved it (launch_scatter_rsv)
   const bool single = rsv && !rsv[c.P + RSV_OVER];
-  const int64_t begin = single ? (int64_t)p * rcap : (int64_t)offs[(int64_t)p * T];
+  const bool nar = single && c.narrow;  // (narrow: runs of 8-byte records, twice rcap of them per partition)
+  const int64_t begin = single ? (int64_t)p * (nar ? 2 * rcap : rcap) : (int64_t)offs[(int64_t)p * T];
   const int64_t end = single ? begin + rsv[p] : (int64_t)offs[(int64_t)(p + 1) * T];
   if (begin == end) {  // nothing for this region: it stays as it is
     if (threadIdx.x == 0) prog.done[p] = 1;
@@ -6664,7 +6734,7 @@ __global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const 
   int hb = tb.passes[p];
   bool lost = false, wide = false;
   for (;;) {
-    const int r = dt_attempt<SRC, KW>(c, U, M, p, src, live, dst, R, in, begin, end, cmp, hb);
+    const int r = dt_attempt<SRC, KW>(c, U, M, p, src, live, dst, R, in, begin, end, cmp, hb, nar);
     __syncthreads();
     if (r == DT_OK) break;
     if (r == DT_WIDE) {  // (KW only)
@@ -7092,20 +7162,28 @@ void launch_scatter_rsv(const DevCfg& c, int64_t wm, const int64_t* key, const i
                         const int32_t* kh, int64_t n, int32_t T, PRec* part, uint32_t* rsv, int64_t rcap, hipStream_t s) {
   const bool big = c.P <= 1024;
   const int rr = big ? 8192 : 4096;
-  const size_t sl = (size_t)rr * (sizeof(i64x2) + sizeof(uint16_t)) + (2 * (size_t)c.P + 1) * sizeof(uint32_t) +
-                    (FW_TILE_THREADS / 64 + 1) * sizeof(uint32_t);
+  const size_t sl = (size_t)rr * ((c.narrow ? 8 : sizeof(i64x2)) + sizeof(uint16_t)) +
+                    (2 * (size_t)c.P + 1) * sizeof(uint32_t) + (FW_TILE_THREADS / 64 + 1) * sizeof(uint32_t);
   static bool attr = false;
   if (!attr) {  // LDS beyond 64 KB
-    (void)hipFuncSetAttribute((const void*)k_scatter_rsv<8192>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_scatter_rsv<4096>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    for (const void* f : {(const void*)k_scatter_rsv<8192, false>, (const void*)k_scatter_rsv<4096, false>,
+                          (const void*)k_scatter_rsv<8192, true>, (const void*)k_scatter_rsv<4096, true>})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  if (big)
-    FW_LAUNCH_MAIN(k_scatter_rsv<8192>, dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n, T, part, rsv,
-                   rcap);
+  // (narrow: a partition's run holds twice as many 8-byte records in the same bytes)
+  if (c.narrow && big)
+    FW_LAUNCH_MAIN((k_scatter_rsv<8192, true>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n, T,
+                   part, rsv, 2 * rcap);
+  else if (c.narrow)
+    FW_LAUNCH_MAIN((k_scatter_rsv<4096, true>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n, T,
+                   part, rsv, 2 * rcap);
+  else if (big)
+    FW_LAUNCH_MAIN((k_scatter_rsv<8192, false>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n, T,
+                   part, rsv, rcap);
   else
-    FW_LAUNCH_MAIN(k_scatter_rsv<4096>, dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n, T, part, rsv,
-                   rcap);
+    FW_LAUNCH_MAIN((k_scatter_rsv<4096, false>), dim3(T), dim3(FW_TILE_THREADS), sl, s, c, wm, key, ts, val, kh, n, T,
+                   part, rsv, rcap);
 }
 
 // panes: maxTimestamp of the earliest window ending after wm (windows [s, s + size), s = offset mod slide)

@@ -195,6 +195,12 @@ struct DevCfg {
   // from an LDS table, k_dt_fire streams it (fw_device.hip, "dense tumbling regions")
   int32_t dense;
   int32_t agg_chunk;  // records per aggregate workgroup of a split partition (FW_AGG_CHUNK, or twice it)
+  // narrow records (round 6; dense single-pass batches of an integer field): the single pass writes 8 bytes per
+  // record, {key (29-bit signed) | window delta - ndn0 (3 bits) | value (int32)}, when every record of the batch has
+  // that form; a record without it sends the batch through classify / scan / offset scatter (16-byte CRec) and the
+  // operator stops trying (fw_runtime.cpp).  Set per launch: 1 = the single pass writes narrow records.
+  int32_t narrow;
+  int32_t ndn0;       // the window delta (compact_delta) of narrow window 0: the watermark's window
 };
 
 // host: reciprocal of d >= 1 for div_inv(): m = floor(2^64 (2^l - d) / d) + 1, l = ceil(log2 d)
@@ -268,6 +274,7 @@ struct Status {
   int32_t taint_any;                  // sessions: 0 no tainted key in the batch, 1 check the set, 2 set full: all
   int32_t rsv_fallbacks;              // single-pass batches that had to go through classify / scan / scatter
   int32_t acc_refused;                // restore: t-digest rows of a window already present, malformed digests
+  int32_t narrow_misses;              // narrow single-pass batches redone because a record had no narrow form
 };
 enum {
   FW_STATUS_STATE_LOST = 1,  // a window could not be stored (more in-flight sessions of one key than supported)
@@ -445,6 +452,7 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
 // batch goes through launch_classify_hist / launch_scan / launch_scatter gated on rsv (they do nothing otherwise).
 #define FW_RSV_WORDS 8
 #define FW_RSV_WIDE 3  // rsv[P + FW_RSV_WIDE]: the batch's DevCfg::wide word when it took the single pass
+#define FW_RSV_NARROW 6  // rsv[P + FW_RSV_NARROW]: a narrow single pass met a record without a narrow form
 bool rsv_eligible(const DevCfg& c);
 void launch_scatter_rsv(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
                         const int32_t* kh, int64_t n, int32_t T, PRec* part, uint32_t* rsv, int64_t rcap, hipStream_t_ s);

@@ -47,6 +47,7 @@ struct Scratch {
   bool split = false;            // its aggregate split long partitions (fw_op::hot)
   int64_t wm = INT64_MIN;        // watermark the batch was classified against
   int32_t compact = 0;           // DevCfg::compact / cbase of the batch (a resumed aggregate reads the same form)
+  int32_t narrow = 0, ndn0 = 0;  // DevCfg::narrow / ndn0 of the batch's single pass
   int64_t cbase = 0;
   int64_t ord_base = 0;          // arrival ordinal of the batch's first record (ordinal aggregates)
   int32_t* wide = nullptr;       // DevCfg::wide of the batches that use this set
@@ -91,6 +92,9 @@ struct fw_op {
   int32_t rsv_seen = 0;      // Status::rsv_fallbacks at the latest settle
   int32_t rsv_misses = 0;    // consecutive settles that saw a single-pass batch redone
   bool rsv_off = false;      // after 3 of them the operator stops trying the single pass
+  int32_t narrow_seen = 0;   // Status::narrow_misses last seen
+  bool narrow_off = false;   // a narrow single pass met a record without a narrow form: 16-byte records from then on
+  int64_t narrow_batches = 0;  // batches that took the narrow single pass (fw_stats)
   int64_t single_batches = 0;  // batches that took the single pass (fw_stats)
   uint32_t *xoffs = nullptr, *xscan = nullptr;  // combining: the combiner's live-count offsets and scan scratch
   // HyperLogLog combining: the extracted partials' register offsets (combiner) / the pushed ones' (receiver), with
@@ -525,6 +529,8 @@ int settle(fw_op* op) {
     c.by_val = S.byv;
     c.compact = S.compact;
     c.cbase = S.cbase;
+    c.narrow = S.narrow;
+    c.ndn0 = S.ndn0;
     c.ord_base = S.ord_base;
     c.wide = S.wide_word(op->dc.P);
     if (S.partials) {  // a partials push: only its merge can have suspended
@@ -567,6 +573,10 @@ int settle(fw_op* op) {
     if ((rc = sync_status(op))) return rc;
   }
   op->unsynced = op->push_unsettled = op->fire_unsettled = false;
+  if (s.narrow_misses != op->narrow_seen) {  // a stream with wide keys or values keeps them: 16-byte records on
+    op->narrow_seen = s.narrow_misses;
+    op->narrow_off = true;
+  }
   if (s.rsv_fallbacks != op->rsv_seen) {  // single-pass batches redone: a skewed stream stops trying after 3 in a row
     op->rsv_seen = s.rsv_fallbacks;
     if (++op->rsv_misses >= 3) op->rsv_off = true;
@@ -683,6 +693,10 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   }
   const bool gather = S.rt && fwdev::gather_mode(c, n);
   const bool single = !gather && S.rsv && !op->rsv_off && op->rcap > 0 && fwdev::rsv_eligible(c);
+  // narrow records: integer fields only (a narrow value is an int32), compact windows from the watermark's on
+  static const bool no_narrow = getenv("FW_NO_NARROW") && atoi(getenv("FW_NO_NARROW"));
+  c.narrow = single && !op->narrow_off && c.vtype != FW_VAL_F64 && c.log_s >= 1 && !no_narrow;
+  c.ndn0 = c.narrow ? 1 << (c.log_s - 1) : 0;
   const int32_t T = gather ? (int32_t)((n + FW_GTILE - 1) / FW_GTILE) : (int32_t)((n + FW_TILE - 1) / FW_TILE);
   const int64_t m = (int64_t)(c.P + 1) * T;
   // async input: the batch-only kernels run on bstream, after the aggregate that last used this scratch set
@@ -748,6 +762,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   }
   S.single = single;
   op->single_batches += single;
+  op->narrow_batches += c.narrow;
   S.gather = gather;
   S.T = T;
   // minBy / maxBy: the aggregate reads the selected elements' fields back by batch index, possibly after the
@@ -770,6 +785,8 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   cc.by_val = S.byv;
   cc.compact = c.compact;
   cc.cbase = c.cbase;
+  cc.narrow = c.narrow;
+  cc.ndn0 = c.ndn0;
   cc.wide = c.wide;
   // a partition can outgrow one aggregate workgroup (hot keys) only when the batch is longer than a chunk
   const bool split = !cc.dense && (cc.wpr == 1 || cc.panes) && n > cc.agg_chunk;
@@ -813,6 +830,8 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   S.wm = op->wm;
   S.compact = c.compact;
   S.cbase = c.cbase;
+  S.narrow = c.narrow;
+  S.ndn0 = c.ndn0;
   S.ord_base = c.ord_base;
   op->last_sc = nxt;
   op->records_in += n;
@@ -891,6 +910,7 @@ int push_partials(fw_op* op, const PartialCols& in, int64_t n, const uint32_t* h
   S.wm = op->wm;
   S.compact = 0;
   S.cbase = 0;
+  S.narrow = 0;
   S.ord_base = op->records_in;
   op->last_sc = nxt;
   op->push_unsettled = true;
@@ -1577,6 +1597,8 @@ int fw_get_stats(fw_op* op, fw_stats* o) {
   o->digest_centroids_fired = (int64_t)s.td_cent;
   o->single_pass_batches = op->single_batches;
   o->single_pass_redone = (int64_t)s.rsv_fallbacks;
+  o->narrow_pass_batches = op->narrow_batches;
+  o->narrow_pass_redone = (int64_t)s.narrow_misses;
   return FW_OK;
 }
 
@@ -1767,6 +1789,14 @@ int fw_push_hll_partials_device(fw_op* op, const fw_partials* in, int64_t n, con
   const PartialCols all{in->key, in->start, in->cnt, in->sum, in->min, in->max};
   fwdev::launch_hll_reg_offsets(all, n, op->hoff, op->hoff_tmp, op->stream);
   HIP_OR_RETURN(op, hipGetLastError());
+  {  // the register list must hold exactly what the partials' sum columns say (the raise reads it unguarded)
+    uint32_t tot = 0;
+    HIP_OR_RETURN(op, hipMemcpyAsync(&tot, op->hoff + n, sizeof tot, hipMemcpyDeviceToHost, op->stream));
+    HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
+    if ((int64_t)tot != nregs)
+      return set_err(op, FW_ERR_ARG, "the partials' sum columns count %lld registers, the register list has %lld",
+                     (long long)tot, (long long)nregs);
+  }
   for (int64_t b = 0; b < n; b += op->max_batch) {
     const int64_t m = std::min(op->max_batch, n - b);
     // (the offsets index the whole register list: partial b + i's are at hoff[b + i])
@@ -2329,11 +2359,13 @@ int fw_keyby_push_device(fw_comm* c, fw_op* op, const int64_t* key, const int64_
     return set_err(op, rc, "exchange: inconsistent counts round (received %lld records of a %lld-record batch)",
                    (long long)pl.recv_total, (long long)pl.recv_bound);
   const int64_t total = pl.recv_total;
-  // the received columns are sized for the whole batch of all subtasks (the bound from the counts round), so a
-  // skewed batch never reallocates them; they grow only when the subtasks' batches do (s is idle here, and the
-  // previous batch's partitioning, the last reader of the received columns, ran on s)
-  if (pl.recv_bound > c->rcap) {
-    if ((rc = comm_reserve_recv(op, c, std::max<int64_t>(pl.recv_bound, 1)))) return rc;
+  // the received columns grow geometrically with what this subtask receives (x1.25 over the batch that needs more,
+  // capped by the bound from the counts round, the whole batch of all subtasks; comm_reserve_recv at least doubles),
+  // so skew costs a few reallocations (counted in the stats) and not world-size times the memory (s is idle here,
+  // and the previous batch's partitioning, the last reader of the received columns, ran on s)
+  if (total > c->rcap) {
+    const int64_t want = std::max(std::min(pl.recv_bound, total + total / 4), std::max<int64_t>(total, 1));
+    if ((rc = comm_reserve_recv(op, c, want))) return rc;
     c->stats.recv_reallocs++;
   }
   comm_account(c, pl, hashed ? 28 : 24);
@@ -2375,6 +2407,9 @@ int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64
   const bool hll = op->cfg.aggregate == FW_AGG_HLL;
   HIP_OR_RETURN(op, hipSetDevice(op->device));
   int rc;
+  // HyperLogLog: a merge of the previous batch that suspended reruns its register raise from c->pr / c->rr when it is
+  // settled, so it is settled before this batch reallocates those buffers or receives into them
+  if (hll && (rc = settle(op))) return rc;
   // the batch into the combiner, ordered after the columns' producer (the caller's fw_stream(op) order)
   hipEvent_t ready = nullptr;
   HIP_OR_RETURN(op, hipEventCreateWithFlags(&ready, hipEventDisableTiming));
@@ -2452,8 +2487,8 @@ int fw_keyby_combine_push_device(fw_comm* c, fw_op* comb, fw_op* op, const int64
       c->stats.recv_reallocs++;
     }
   }
-  if (pl.recv_bound > c->pcap) {  // the receive columns for every partial of the batch (the bound): grow both sides
-    const int64_t cap = std::max<int64_t>(pl.recv_bound, 2 * c->pcap);
+  if (total > c->pcap) {  // the receive columns for what this subtask receives (geometric, as fw_keyby_push_device)
+    const int64_t cap = std::max(std::min(pl.recv_bound, total + total / 4), std::max<int64_t>(total, 2 * c->pcap));
     for (int i = 0; i < 6; i++) {
       cfree(c->pr[i]);
       HIP_OR_RETURN(op, dmalloc(&c->pr[i], (size_t)cap));

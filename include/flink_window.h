@@ -187,6 +187,8 @@ typedef struct fw_stats {
   int64_t digest_centroids_fired; /* FW_AGG_TDIGEST: centroids of all digests fired so far      */
   int64_t single_pass_batches;    /* device batches partitioned in one pass (dense tumbling)    */
   int64_t single_pass_redone;     /* ... of which went through classify / scan / scatter after  */
+  int64_t narrow_pass_batches;    /* ... of which wrote 8-byte records (key, window, int32 value) */
+  int64_t narrow_pass_redone;     /* ... of which had a record without that form (then 16 bytes) */
 } fw_stats;
 
 /* Lifecycle — StreamOperator.setup/open/close/dispose (api/operators/StreamOperator.java:57-127). */

@@ -413,6 +413,52 @@ def test_gpu_single_pass_scatter_fallbacks(value_type, async_input):
     assert st["single_pass_batches"] >= len(batches) - 2 and st["single_pass_redone"] >= 2
 
 
+@pytest.mark.parametrize("async_input", [False, True], ids=["host-push", "async-device-push"])
+@pytest.mark.parametrize("wide", ["value", "key"])
+def test_gpu_narrow_records_and_fallback(wide, async_input):
+    # dense single-pass batches of an integer field write 8-byte records {key (29-bit signed), window delta, int32
+    # value}.  The batches straddle what that form holds: batch 1 has values AT the int32 bounds
+    # and keys at the edges of [-2^28, 2^28) (narrow); batch 3 has a value just outside int32 (wide="value") or a key
+    # of 2^28 (wide="key"): that batch is redone through classify / scan / scatter with 16-byte records, and the
+    # operator keeps 16-byte records from then on.  Every row bit-exact vs the oracle.
+    cfg = dict(assigner="tumbling", size=100)
+    batches, wms = _stream(600_000, 75_000, 50_000, bound=20, jitter=30, rate=1_000_000)
+    k, t, v = (x.copy() for x in batches[1])
+    v[5], v[6], v[7] = -(1 << 31), (1 << 31) - 1, 0
+    k[8], k[9] = -(1 << 28), (1 << 28) - 1
+    batches[1] = (k, t, v)
+    k, t, v = (x.copy() for x in batches[3])
+    if wide == "value":
+        v[11], v[12] = 1 << 31, -(1 << 31) - 1
+    else:
+        k[11], k[12] = 1 << 28, -(1 << 28) - 1
+    batches[3] = (k, t, v)
+    gpu = _gpu_op(**cfg, max_batch=1 << 17, async_input=async_input)
+    ref = orc.WindowOperatorOracle(**cfg)
+    drained = []
+    for e, ((k, t, v), wm) in enumerate(zip(batches, wms)):
+        if async_input:
+            import torch
+            gpu.process_batch(*(torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (k, t, v)))
+            gpu.advance_watermark(wm, wait=False)
+            drained.append(gpu.drain_rows(e))
+        else:
+            gpu.process(k, t, v)
+            gpu.watermark(wm)
+        ref.process(k, t, v)
+        ref.watermark(wm)
+    g = np.concatenate(drained) if async_input else gpu.rows()
+    r = ref.rows()
+    st = gpu.stats()
+    gpu.close()
+    assert_rows_equal(g, r)
+    assert int(g["count"].sum()) + st["late_records_dropped"] == 600_000
+    assert int(g["max"].max()) >= (1 << 31) - 1 and int(g["min"].min()) <= -(1 << 31)
+    # batches 1 .. 3 were narrow (the first batch has no watermark yet to base the windows on), batch 3 was redone
+    assert st["narrow_pass_batches"] >= 2 and st["narrow_pass_redone"] == 1
+    assert st["single_pass_batches"] > st["narrow_pass_batches"]
+
+
 @pytest.mark.parametrize("cfg", [dict(assigner="tumbling", size=1000),
                                  dict(assigner="sliding", size=5000, slide=1000),
                                  dict(assigner="session", gap=50)], ids=["tumbling", "sliding", "session"])
