@@ -9,6 +9,7 @@ from .keygroups import (KeyGroupRange, assign_key_to_parallel_operator, assign_t
                         compute_operator_index_for_key_group, long_hash_code, murmur_hash, string_hash_code)
 from .windowing import (CountEvictor, CountTrigger, DeltaEvictor, GlobalWindows, TimeEvictor,  # noqa: F401
                         CountSumMinMax, CountWindows, ExtremalElementReduce, FirstElementReduce, HyperLogLog, TDigest,  # noqa: F401
+                        RowAggregate,
                         EventTimeSessionWindows, EventTimeTrigger, PurgingTrigger, SlidingEventTimeWindows, Time,
                         TumblingEventTimeWindows, first_element_results, selected_elements, tdigest_quantile)
 
@@ -18,6 +19,9 @@ def __getattr__(name):
     if name == "GpuWindowOperator":
         from .operator import GpuWindowOperator
         return GpuWindowOperator
+    if name in ("GroupWindowAggregate", "Tumble", "Slide", "Session"):
+        from . import table
+        return getattr(table, name)
     if name == "GpuListWindowOperator":
         from .listwindow import GpuListWindowOperator
         return GpuListWindowOperator

@@ -22,6 +22,8 @@ FW_VAL_I64, FW_VAL_I32, FW_VAL_F64, FW_VAL_I16, FW_VAL_I8, FW_VAL_F32 = 0, 1, 2,
 FW_KEY_LONG, FW_KEY_INT, FW_KEY_HASHED = 0, 1, 2
 FW_AGG_COUNT_SUM_MIN_MAX, FW_AGG_HLL, FW_AGG_FIRST, FW_AGG_MINBY, FW_AGG_MAXBY, FW_AGG_FIRST_MAX = 0, 1, 2, 3, 4, 5
 FW_AGG_TDIGEST = 6
+FW_AGG_ROW = 7
+FW_ROW_COUNT_STAR, FW_ROW_COUNT, FW_ROW_SUM, FW_ROW_MIN, FW_ROW_MAX, FW_ROW_AVG = 0, 1, 2, 3, 4, 5
 FW_NUM_KERNELS = 7
 FW_PROFILE_KINDS = 0x100  # fw_profile(op, FW_PROFILE_KINDS | 1 << kind): time only those kinds
 
@@ -40,7 +42,8 @@ class FwConfig(ctypes.Structure):
                 ("aggregate", ctypes.c_int32), ("hll_precision", ctypes.c_int32),
                 ("tdigest_compression", ctypes.c_int32), ("tdigest_export", ctypes.c_int32),
                 ("tdigest_quantiles", ctypes.c_double * 3), ("count_evict_after", ctypes.c_int32),
-                ("pad0", ctypes.c_int32)]
+                ("pad0", ctypes.c_int32), ("row_columns", ctypes.c_int32), ("row_aggregates", ctypes.c_int32),
+                ("row_column_type", ctypes.c_int32 * 8), ("row_aggregate", ctypes.c_int32 * 16)]
 
 
 class FwRows(ctypes.Structure):
@@ -133,6 +136,9 @@ SIGNATURES = {
     "fw_rows_device": (ctypes.c_int, [VP, ctypes.POINTER(FwRows), I64P]),
     "fw_clear_pending": (ctypes.c_int, [VP]),
     "fw_drain_digests": (ctypes.c_int, [VP, VP, VP, VP, ctypes.c_int64, I64P]),
+    "fw_push_row_batch": (ctypes.c_int, [VP, VP, VP, VP, VP, VP, ctypes.c_int64]),
+    "fw_push_row_batch_device": (ctypes.c_int, [VP, VP, VP, VP, VP, VP, ctypes.c_int64]),
+    "fw_drain_row_results": (ctypes.c_int, [VP, VP, VP, ctypes.c_int64, I64P]),
     "fw_get_stats": (ctypes.c_int, [VP, ctypes.POINTER(FwStats)]),
     "fw_synchronize": (ctypes.c_int, [VP]),
     "fw_profile": (ctypes.c_int, [VP, ctypes.c_int]),

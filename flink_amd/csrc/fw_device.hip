@@ -343,8 +343,8 @@ __device__ __forceinline__ void side_one(const DevSide& sd, Status* st, int64_t 
 // accumulate one value (AggregateFunction.add of the built-in count/sum/min/max)
 // (FW_AGG_FIRST: mx takes ~ordinal `fo` of the record, so the max keeps the first element's ordinal)
 __device__ __forceinline__ void acc_add(const DevCfg& c, Entry& e, int64_t v, int64_t fo) {
-  if (c.agg == FW_AGG_HLL) {  // the registers are the accumulator; the row keeps the count (as lds_acc's LDS_CNT_ONLY)
-    e.cnt += 1;
+  if (c.agg == FW_AGG_HLL || c.agg == FW_AGG_ROW) {  // the block is the accumulator; the row keeps the count
+    e.cnt += 1;                                       // (as lds_acc's LDS_CNT_ONLY)
     return;
   }
   if (agg_by(c.agg)) {
@@ -1897,15 +1897,165 @@ __device__ void hll_merge_blocks(const DevCfg& c, uint64_t dst, uint64_t src) {
   __threadfence();  // (zeroed before its id can be handed out)
   c.pool_defer[atomicAdd(&c.pool_ctr[2], 1)] = (uint32_t)src;
 }
+__device__ void row_merge_blocks(const DevCfg& c, uint64_t dst, uint64_t src);
 // AggregateFunction.merge of two accumulator blocks as sessions merge: HyperLogLog raises dst to the register max
 // now; a t-digest logs the pair, and the push's compression merges the centroid lists (launch_tdigest)
 __device__ __forceinline__ void pool_merge_blocks(const DevCfg& c, uint64_t dst, uint64_t src) {
   if (c.agg == FW_AGG_HLL) {
     hll_merge_blocks(c, dst, src);
+  } else if (c.agg == FW_AGG_ROW) {
+    row_merge_blocks(c, dst, src);
   } else if (c.agg == FW_AGG_TDIGEST) {
     const int i = atomicAdd(c.td_mctr, 1);
     c.td_mdst[i] = (uint32_t)dst;
     c.td_msrc[i] = (uint32_t)src;
+  }
+}
+
+// ---- Table API group-window aggregates (FW_AGG_ROW; the definition is oracle/window_oracle.h's OR_AGG_ROW, after
+// flink-table .../functions/aggfunctions/{Count,Sum,Min,Max,Avg}AggFunction.scala).  A window's block is one RowAcc
+// per value column (fw_internal.h), zero = empty; every update is an atomic (the records of a window may be added by
+// several workgroups: the per-record update kernel, the ordered path).
+constexpr uint64_t ROW_SIGN = 0x8000000000000000ull;
+__device__ __forceinline__ RowAcc* row_acc(const DevCfg& c, uint64_t blk) {
+  return reinterpret_cast<RowAcc*>(c.pool + blk * (uint64_t)c.pool_bytes);
+}
+__device__ __forceinline__ bool row_float(const DevCfg& c, int j) {
+  return c.row_type[j] == FW_VAL_F64 || c.row_type[j] == FW_VAL_F32;
+}
+// a value's order key (Double.compare order for a floating column, Scala's Ordering.Double / Float), and the min /
+// max encodings whose identity is 0 under an unsigned max: max = key ^ sign, min = ~(key ^ sign)
+__device__ __forceinline__ int64_t row_key(const DevCfg& c, int j, int64_t v) { return row_float(c, j) ? f64_sortable(v) : v; }
+__device__ __forceinline__ uint64_t row_enc_max(int64_t k) { return (uint64_t)k ^ ROW_SIGN; }
+__device__ __forceinline__ uint64_t row_enc_min(int64_t k) { return ~((uint64_t)k ^ ROW_SIGN); }
+__device__ __forceinline__ int64_t row_dec_max(uint64_t e) { return (int64_t)(e ^ ROW_SIGN); }
+__device__ __forceinline__ int64_t row_dec_min(uint64_t e) { return (int64_t)(~e ^ ROW_SIGN); }
+// the exact 128-bit integral sum: the low word's carry out goes to the high word with the addend's sign extension
+__device__ __forceinline__ void row_add128(RowAcc& a, unsigned long long lo, long long hi) {
+  const unsigned long long old = atomicAdd(&a.lo, lo);
+  const long long h = hi + (old + lo < old ? 1ll : 0ll);
+  if (h) atomicAdd(reinterpret_cast<unsigned long long*>(&a.hi), (unsigned long long)h);
+}
+// AggregateFunction.add of record i (its index in the push) into block blk: every aggregate of every non-null column
+__device__ void row_add(const DevCfg& c, uint64_t blk, int64_t i) {
+  RowAcc* acc = row_acc(c, blk);
+  const uint32_t nm = c.row_nulls ? (uint32_t)c.row_nulls[i] : 0u;
+  for (int j = 0; j < c.row_nc; j++) {
+    if ((nm >> j) & 1u) continue;
+    const int64_t v = c.row_cols[(int64_t)j * c.row_stride + i];
+    RowAcc& a = acc[j];
+    atomicAdd(&a.nn, 1ull);
+    if (row_float(c, j))
+      atomicAdd(reinterpret_cast<double*>(&a.lo), __longlong_as_double(v));
+    else
+      row_add128(a, (unsigned long long)v, v < 0 ? -1ll : 0ll);
+    const int64_t k = row_key(c, j, v);
+    const uint64_t em = row_enc_min(k), ex = row_enc_max(k);
+    if (em > a.mn) atomicMax(&a.mn, em);  // (a stale read is below the current value: skipping is exact)
+    if (ex > a.mx) atomicMax(&a.mx, ex);
+  }
+}
+__device__ __forceinline__ void row_clear(const DevCfg& c, uint64_t blk) {
+  RowAcc* a = row_acc(c, blk);
+  for (int j = 0; j < c.row_nc; j++) a[j] = RowAcc{0, 0, 0, 0, 0};
+}
+// AggregateFunction.merge of block src into dst (sessions, AbstractHeapMergingState.mergeNamespaces): counts and sums
+// add, min / max take the extremes; src is zeroed and goes on the deferred free list.  One thread.
+__device__ void row_merge_blocks(const DevCfg& c, uint64_t dst, uint64_t src) {
+  RowAcc* d = row_acc(c, dst);
+  RowAcc* sa = row_acc(c, src);
+  for (int j = 0; j < c.row_nc; j++) {
+    const RowAcc o = sa[j];
+    if (o.nn) {
+      atomicAdd(&d[j].nn, o.nn);
+      if (row_float(c, j))
+        atomicAdd(reinterpret_cast<double*>(&d[j].lo), __longlong_as_double((long long)o.lo));
+      else
+        row_add128(d[j], o.lo, o.hi);
+      atomicMax(&d[j].mn, o.mn);
+      atomicMax(&d[j].mx, o.mx);
+    }
+    sa[j] = RowAcc{0, 0, 0, 0, 0};
+  }
+  __threadfence();  // (zeroed before its id can be handed out)
+  c.pool_defer[atomicAdd(&c.pool_ctr[2], 1)] = (uint32_t)src;
+}
+// |x| / d of a 128-bit two's-complement x (d >= 1), truncated toward zero: BigInteger.divide (AvgAggFunction
+// .scala:160-166); the quotient of an average fits 64 bits
+__device__ int64_t row_div128(unsigned long long lo, long long hi, unsigned long long d) {
+  const bool neg = hi < 0;
+  unsigned long long ul = lo, uh = (unsigned long long)hi;
+  if (neg) {  // negate
+    ul = ~ul + 1ull;
+    uh = ~uh + (ul == 0ull ? 1ull : 0ull);
+  }
+  unsigned long long q = 0, r = uh % d;  // (uh / d is 0 for an average's magnitude)
+  for (int b = 63; b >= 0; b--) {
+    const bool top = (r >> 63) != 0;
+    r = (r << 1) | ((ul >> b) & 1ull);
+    if (top || r >= d) {
+      r -= d;
+      q |= 1ull << b;
+    }
+  }
+  return neg ? -(int64_t)q : (int64_t)q;
+}
+__device__ __forceinline__ int64_t row_narrow(int t, int64_t v) {
+  return t == FW_VAL_I32 ? (int64_t)(int32_t)v : t == FW_VAL_I16 ? (int64_t)(int16_t)v
+       : t == FW_VAL_I8 ? (int64_t)(int8_t)v : v;
+}
+// getValue of aggregate s (oracle/window_oracle.cpp row_value): the value or NULL
+__device__ int64_t row_value(const DevCfg& c, const RowAcc* acc, int64_t cnt, int s, bool* null) {
+  const int fn = c.row_spec[s] >> 8, j = c.row_spec[s] & 0xff;
+  *null = false;
+  if (fn == FW_ROW_COUNT_STAR) return cnt;
+  const RowAcc a = acc[j];
+  if (fn == FW_ROW_COUNT) return (int64_t)a.nn;
+  if (a.nn == 0) {
+    *null = true;
+    return 0;
+  }
+  const int t = c.row_type[j];
+  const double ds = __longlong_as_double((long long)a.lo);
+  switch (fn) {
+    case FW_ROW_SUM:
+      if (t == FW_VAL_F32) return __double_as_longlong((double)(float)ds);
+      return t == FW_VAL_F64 ? (int64_t)a.lo : row_narrow(t, (int64_t)a.lo);
+    case FW_ROW_MIN: {
+      const int64_t k = row_dec_min(a.mn);
+      return row_float(c, j) ? f64_unsortable(k) : k;
+    }
+    case FW_ROW_MAX: {
+      const int64_t k = row_dec_max(a.mx);
+      return row_float(c, j) ? f64_unsortable(k) : k;
+    }
+    default:  // FW_ROW_AVG
+      if (t == FW_VAL_F64) return __double_as_longlong(ds / (double)a.nn);
+      if (t == FW_VAL_F32) return __double_as_longlong((double)(float)(ds / (double)a.nn));
+      if (t == FW_VAL_I64) return row_div128(a.lo, a.hi, a.nn);
+      return row_narrow(t, (int64_t)a.lo / (int64_t)a.nn);  // the Long sum / count (Java division), narrowed
+  }
+}
+// a fired row's aggregates into the export buffer (out.dig: the NULL mask, then row_ns values); the block is freed
+// when the window goes (rel: 1 + its free-stack slot, as td_finish)
+__device__ void row_finish(const DevCfg& c, const DevRows& out, uint64_t row, int64_t stack_base) {
+  const uint64_t tag = (uint64_t)out.sum[row];
+  const uint64_t blk = tag & 0xffffffffull;
+  const int64_t rel = (int64_t)(tag >> 32);
+  const RowAcc* a = row_acc(c, blk);
+  int64_t* d = out.dig + row * (1 + (int64_t)c.row_ns);
+  uint32_t nm = 0;
+  for (int q = 0; q < c.row_ns; q++) {
+    bool nl;
+    d[1 + q] = row_value(c, a, out.cnt[row], q, &nl);
+    if (nl) nm |= 1u << q;
+  }
+  d[0] = (int64_t)nm;
+  out.sum[row] = out.mn[row] = out.mx[row] = 0;
+  if (rel) {
+    row_clear(c, blk);
+    __threadfence();
+    c.pool_free[stack_base + rel - 1] = (uint32_t)blk;
   }
 }
 // a new window's accumulator block (an empty t-digest, or HyperLogLog's zero registers)
@@ -2414,7 +2564,8 @@ __device__ __forceinline__ void agg_walk_lm(const DevCfg& c, AggLds& L, int64_t*
         if (tg >= 0) m |= 1u << j;
       }
     } else {
-      up = lds_upsert_batch<RPT>(L, c.vtype, k, t, v, o, FIRST ? c.agg : c.agg == FW_AGG_HLL ? LDS_CNT_ONLY : 0, m);
+      up = lds_upsert_batch<RPT>(L, c.vtype, k, t, v, o,
+                                 FIRST ? c.agg : (c.agg == FW_AGG_HLL || c.agg == FW_AGG_ROW) ? LDS_CNT_ONLY : 0, m);
     }
     if (!up) {
       dm = m;
@@ -2741,7 +2892,7 @@ __global__ __launch_bounds__(FW_AGG_THREADS, GATHER ? FW_GATHER_WAVES : SESS ? F
             in = lds_session_upsert(L, sess_end, c.vtype, k[j], t[j], jadd(t[j], c.gap), v[j], o[j], FIRST ? c.agg : 0);
           else
             in = lds_upsert(L, c.vtype, k[j], jsub(t[j], (int64_t)wi * c.slide), v[j], c.diag, o[j],
-                            FIRST ? c.agg : c.agg == FW_AGG_HLL ? LDS_CNT_ONLY : 0);
+                            FIRST ? c.agg : (c.agg == FW_AGG_HLL || c.agg == FW_AGG_ROW) ? LDS_CNT_ONLY : 0);
           if (!in) {
             failed = true;
             rj = j;
@@ -2931,6 +3082,7 @@ __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int6
     Entry en = r.ent[slot];
     acc_add(c, en, v, fo);
     if (c.agg == FW_AGG_HLL) hll_raise(c, pool_block_of(en), v);  // (k_hll_update takes the partitioned records)
+    if (c.agg == FW_AGG_ROW) row_add(c, pool_block_of(en), v);   // (v: the record's index in the push)
     int32_t head = -1;
     if (td) {  // the window's chain of this push's values: this element on top
       if (oj < 0) {
@@ -3094,6 +3246,7 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
   *skipped = false;
   acc_add(c, en, v, fo);
   if (c.agg == FW_AGG_HLL) hll_raise(c, pool_block_of(en), v);  // (k_hll_update takes the partitioned records)
+  if (c.agg == FW_AGG_ROW) row_add(c, pool_block_of(en), v);   // (v: the record's index in the push)
   if (c.agg == FW_AGG_TDIGEST) {  // the value joins the push's compression
     const int j = atomicAdd(c.td_ovctr, 1);
     c.td_ovk[j] = k;
@@ -3779,6 +3932,76 @@ __global__ __launch_bounds__(256) void k_pool_release(DevCfg c) {
   for (int32_t i = threadIdx.x; i < n; i += blockDim.x) c.pool_free[base_s + i] = c.pool_defer[i];
   __syncthreads();
   if (threadIdx.x == 0) c.pool_ctr[2] = 0;
+}
+
+
+// FW_AGG_ROW: after the aggregate created every record's window (or merged its session) and counted it, each
+// partitioned record adds its columns (read by its batch index, the record's value) into its window's block
+// (row_add).  The adds are not idempotent: the kernel runs only when the aggregate did not suspend (a resumed push
+// launches it once more, after the resumed aggregate).  One workgroup per FW_HLL_CHUNK records, a record's partition
+// from the scan offsets.  MODE 0: one window per record (tumbling), 1: sliding fan-out (PRec, nwin windows, newest
+// first), 2: sessions (the in-flight session of the key that contains [ts, ts + gap), sessions hash the key only).
+__device__ __forceinline__ int32_t session_containing(const Region& r, const DevCfg& c, int64_t key, int64_t ts);
+template <int MODE>
+__global__ __launch_bounds__(256) void k_row_update(DevCfg c, const PRec* __restrict__ part,
+                                                   const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
+                                                   Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int64_t total = offs[(int64_t)c.P * T];
+  const int64_t i0 = (int64_t)blockIdx.x * FW_HLL_CHUNK;
+  if (i0 >= total) return;
+  __shared__ int32_t p0_s;
+  if (threadIdx.x == 0) {  // partition of the chunk's first record: last p with offs[p*T] <= i0
+    int32_t lo = 0, hi = c.P - 1;
+    while (lo < hi) {
+      const int32_t mid = (lo + hi + 1) >> 1;
+      if ((int64_t)offs[(int64_t)mid * T] <= i0)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    p0_s = lo;
+  }
+  __syncthreads();
+  const bool cmp = c.compact && !*c.wide;
+  const int64_t i1 = min(total, i0 + (int64_t)FW_HLL_CHUNK);
+  int32_t pp = p0_s;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
+    int64_t key, last, idx;
+    int32_t nw = 1;
+    if (cmp) {
+      const i64x2 r = reinterpret_cast<const i64x2*>(part)[i];
+      compact_decode(c, pp, r.x, &key, &last);
+      idx = r.y;
+    } else {
+      const PRec rec = part[i];
+      key = rec.key;
+      last = rec.last;
+      idx = rec.val;
+      nw = (int32_t)(rec.nwin & 0xffff);
+    }
+    const Region r = region_of(c, tb, pp, tb.cur[pp]);
+    if constexpr (MODE == 2) {
+      const int32_t slot = session_containing(r, c, key, last);
+      if (slot < 0) {
+        atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's session
+        continue;
+      }
+      row_add(c, pool_block_of(r.ent[slot]), idx);
+    } else {
+      for (int32_t wi = 0; wi < (MODE == 1 ? nw : 1); wi++) {
+        const int64_t ws = jsub(last, (int64_t)wi * c.slide);
+        const int64_t we = wend(c, ws);
+        const int32_t slot = region_find(r, slot_hash(c, key, ws), key, ws, we);
+        if (slot < 0) {
+          atomicOr(&st->flags, FW_STATUS_STATE_LOST);
+          continue;
+        }
+        row_add(c, pool_block_of(r.ent[slot]), idx);
+      }
+    }
+  }
 }
 
 // ---- t-digest (FW_AGG_TDIGEST).  The definition is oracle/window_oracle.h's OR_AGG_TDIGEST, restated here
@@ -5109,8 +5332,11 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
       nfire += d.fire;
       if (!d.keep && !d.fire && c.pool_bytes) {  // GC without a row: free its block here (HLL: zeroed)
         const uint64_t blk = pool_block_of(e);
-        if (c.agg == FW_AGG_HLL) {
-          hll_clear(c, blk);
+        if (c.agg == FW_AGG_HLL || c.agg == FW_AGG_ROW) {
+          if (c.agg == FW_AGG_HLL)
+            hll_clear(c, blk);
+          else
+            row_clear(c, blk);
           __threadfence();
         }
         c.pool_free[atomicAdd(&c.pool_ctr[0], 1)] = (uint32_t)blk;
@@ -5170,8 +5396,8 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
             out.mn[pos] = (int64_t)pool_block_of(fe);
             out.mx[pos] = d2.keep ? -1 : (int64_t)atomicAdd(&nrel_s, 1);
           }
-          if (c.agg == FW_AGG_TDIGEST)  // read back by td_finish: the block, above it 1 + its free-stack slot if it goes
-            out.sum[pos] = (int64_t)(pool_block_of(fe) |
+          if (c.agg == FW_AGG_TDIGEST || c.agg == FW_AGG_ROW)  // read back by td_finish / row_finish: the block,
+            out.sum[pos] = (int64_t)(pool_block_of(fe) |                          // above it 1 + its free-stack slot
                                      (d2.keep ? 0ull : (uint64_t)(atomicAdd(&nrel_s, 1) + 1) << 32));
         } else {
           atomicOr(&st->flags, FW_STATUS_OUT_FULL);
@@ -5200,6 +5426,8 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
           hll_finish(c, out, r, ri < 0 ? -1 : hl_sb + ri, hl_ids + (threadIdx.x & ~63u));
         }
       }
+    } else if (c.agg == FW_AGG_ROW) {
+      for (uint64_t r = base_s + threadIdx.x; r < end; r += blockDim.x) row_finish(c, out, r, hl_sb);
     } else {
       __shared__ unsigned long long cent_s;
       if (threadIdx.x == 0) cent_s = 0;
@@ -5607,6 +5835,18 @@ __global__ __launch_bounds__(256) void k_block_export(DevCfg c, const int64_t* _
     const uint4* q = reinterpret_cast<const uint4*>(c.pool + b * (uint64_t)c.pool_bytes + hll_hdr_bytes(c.hll_p));
     uint4* d = reinterpret_cast<uint4*>(acc + row * (int64_t)nq * 16);
     for (int32_t j = lane; j < nq; j += 64) d[j] = q[j];
+  } else if (c.agg == FW_AGG_ROW) {  // per column: count, sum lo, sum hi, min, max (the column's values; 0 if empty)
+    const RowAcc* a = row_acc(c, b);
+    int64_t* d = reinterpret_cast<int64_t*>(acc) + row * 5 * (int64_t)c.row_nc;
+    for (int32_t j = lane; j < c.row_nc; j += 64) {
+      const RowAcc x = a[j];
+      const bool f = row_float(c, j);
+      d[5 * j] = (int64_t)x.nn;
+      d[5 * j + 1] = (int64_t)x.lo;
+      d[5 * j + 2] = f ? 0 : x.hi;
+      d[5 * j + 3] = !x.nn ? 0 : f ? f64_unsortable(row_dec_min(x.mn)) : row_dec_min(x.mn);
+      d[5 * j + 4] = !x.nn ? 0 : f ? f64_unsortable(row_dec_max(x.mx)) : row_dec_max(x.mx);
+    }
   } else {
     const TdHead h = *td_head(c, b);
     const TdCent* ce = td_half(c, b, h.cur);
@@ -5627,6 +5867,12 @@ __device__ __forceinline__ uint32_t bytes_max(uint32_t a, uint32_t b) {
 // a digest restores only with at most delta/2 centroids of weight >= 1 (registers: any bytes)
 __device__ bool acc_valid(const DevCfg& c, const uint8_t* src) {
   if (c.agg == FW_AGG_HLL) return true;
+  if (c.agg == FW_AGG_ROW) {  // counts >= 0
+    const int64_t* s = reinterpret_cast<const int64_t*>(src);
+    for (int j = 0; j < c.row_nc; j++)
+      if (s[5 * j] < 0) return false;
+    return true;
+  }
   const int64_t* s = reinterpret_cast<const int64_t*>(src);
   if (s[0] < 0 || s[0] > c.td_nb) return false;
   for (int32_t k = 0; k < (int32_t)s[0]; k++)
@@ -5636,6 +5882,23 @@ __device__ bool acc_valid(const DevCfg& c, const uint8_t* src) {
 // one thread: a row's accumulator into block b (merge: HyperLogLog register max into a live block)
 __device__ void block_import(const DevCfg& c, uint64_t b, const uint8_t* src, bool merge) {
   uint8_t* base = c.pool + b * (uint64_t)c.pool_bytes;
+  if (c.agg == FW_AGG_ROW) {  // (merge: AggregateFunction.merge into the live block)
+    RowAcc* a = row_acc(c, b);
+    const int64_t* s = reinterpret_cast<const int64_t*>(src);
+    for (int j = 0; j < c.row_nc; j++) {
+      if (!merge) a[j] = RowAcc{0, 0, 0, 0, 0};
+      if (s[5 * j] <= 0) continue;
+      const bool f = row_float(c, j);
+      atomicAdd(&a[j].nn, (unsigned long long)s[5 * j]);
+      if (f)
+        atomicAdd(reinterpret_cast<double*>(&a[j].lo), __longlong_as_double(s[5 * j + 1]));
+      else
+        row_add128(a[j], (unsigned long long)s[5 * j + 1], s[5 * j + 2]);
+      atomicMax(&a[j].mn, row_enc_min(row_key(c, j, s[5 * j + 3])));
+      atomicMax(&a[j].mx, row_enc_max(row_key(c, j, s[5 * j + 4])));
+    }
+    return;
+  }
   if (c.agg == FW_AGG_HLL) {
     const int32_t nq = (int32_t)(((int64_t)1 << c.hll_p) / 16), nw = (nq + 31) / 32;
     uint32_t* bits = reinterpret_cast<uint32_t*>(base);
@@ -5727,8 +5990,8 @@ __global__ void k_restore(DevCfg c, int32_t kg, StateCols in, int64_t n, DevTabl
   if (found >= 0) {  // the window is already there (restored earlier, or an earlier round): AggregateFunction.merge
     Entry& x = r.ent[found];
     Entry cur = x;
-    if (c.pool_bytes) {  // register max into its block; a digest is not re-compressed here
-      if (c.agg != FW_AGG_HLL) {
+    if (c.pool_bytes) {  // register max / the Table aggregates' merge into its block; a digest is not re-compressed here
+      if (c.agg != FW_AGG_HLL && c.agg != FW_AGG_ROW) {
         atomicAdd(&st->acc_refused, 1);
         return;
       }
@@ -7252,7 +7515,7 @@ int gather_mode(const DevCfg& c, int64_t n) {
   // opt-in (FW_GATHER=1): at C2 it measured even with the partition-major scatter (0.90 vs 0.895 ms per step;
   // k_stage 185 us + regroup ~150 us against classify + scan + scatter 0.41 ms), see DESIGN.md
   static const bool on = getenv("FW_GATHER") && atoi(getenv("FW_GATHER"));
-  return on && c.compact && c.assigner != FW_SESSION && (c.assigner == FW_TUMBLING || c.panes) &&
+  return on && c.compact && c.agg != FW_AGG_ROW && c.assigner != FW_SESSION && (c.assigner == FW_TUMBLING || c.panes) &&
          c.P <= FW_GMAX_P && n <= (int64_t)FW_GMAX_T * FW_GTILE;
 }
 
@@ -7309,6 +7572,18 @@ void launch_hll_update(const DevCfg& c, const PRec* part, const uint32_t* offs, 
     hipLaunchKernelGGL(k_hll_update<true>, grid, dim3(256), 0, s, c, part, offs, T, tb, st);
   else
     hipLaunchKernelGGL(k_hll_update<false>, grid, dim3(256), 0, s, c, part, offs, T, tb, st);
+}
+
+void launch_row_update(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
+                       Status* st, hipStream_t s) {
+  if (n <= 0) return;
+  const dim3 grid((unsigned)((n + FW_HLL_CHUNK - 1) / FW_HLL_CHUNK));
+  if (c.assigner == FW_SESSION)
+    hipLaunchKernelGGL(k_row_update<2>, grid, dim3(256), 0, s, c, part, offs, T, tb, st);
+  else if (c.assigner == FW_SLIDING)
+    hipLaunchKernelGGL(k_row_update<1>, grid, dim3(256), 0, s, c, part, offs, T, tb, st);
+  else
+    hipLaunchKernelGGL(k_row_update<0>, grid, dim3(256), 0, s, c, part, offs, T, tb, st);
 }
 
 void launch_slow(const DevCfg& c, int64_t wm, const uint32_t* srow, int32_t T, const int64_t* sk, const int64_t* stt,

@@ -201,6 +201,24 @@ struct DevCfg {
   // operator stops trying (fw_runtime.cpp).  Set per launch: 1 = the single pass writes narrow records.
   int32_t narrow;
   int32_t ndn0;       // the window delta (compact_delta) of narrow window 0: the watermark's window
+  // FW_AGG_ROW (Table API group windows, oracle/window_oracle.h OR_AGG_ROW): row_nc value columns of FW_VAL_* types,
+  // row_ns aggregates (FW_ROW_* << 8 | column).  A window's block holds one RowAcc per column; a record's value is
+  // its batch index, and its columns are read from the push's copy: column j of record i at row_cols[j * row_stride
+  // + i], its null mask at row_nulls[i] (bit j = column j is NULL; nullptr = none)
+  int32_t row_nc, row_ns;
+  int32_t row_type[8];
+  int32_t row_spec[16];
+  const int64_t* row_cols;
+  const uint8_t* row_nulls;
+  int64_t row_stride;
+};
+// FW_AGG_ROW accumulator of one column (40 bytes, zero = empty): the non-null count, the sum (integral columns: 128
+// bits, two's complement, lo / hi; floating columns: f64 in lo), min / max as order keys encoded so that 0 is the
+// identity of an unsigned max (row_enc_min / row_enc_max)
+struct RowAcc {
+  unsigned long long nn, lo;
+  long long hi;
+  unsigned long long mn, mx;
 };
 
 // host: reciprocal of d >= 1 for div_inv(): m = floor(2^64 (2^l - d) / d) + 1, l = ceil(log2 d)
@@ -484,6 +502,9 @@ void launch_fire(const DevCfg& c, int64_t wm, DevTable tb, DevRows out, Status* 
 int64_t pane_nt_floor(const DevCfg& c, int64_t wm);  // host: DevCfg::nt_floor of a launch at watermark wm
 // FW_AGG_HLL: fold the batch's records into the registers of their (key, window) entries (after aggregate)
 void launch_hll_update(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
+                       Status* st, hipStream_t_ s);
+// FW_AGG_ROW: add the batch's records' columns into the blocks of their (key, window) entries (after aggregate)
+void launch_row_update(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
                        Status* st, hipStream_t_ s);
 // FW_AGG_TDIGEST: compress the batch's values into the digests of their (key, window) entries (after aggregate)
 void launch_td_relink(const DevCfg& c, DevTable tb, hipStream_t s);

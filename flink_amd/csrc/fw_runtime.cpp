@@ -42,6 +42,8 @@ struct Scratch {
   int32_t* skh = nullptr;
   int64_t* so = nullptr;         // FW_AGG_FIRST: arrival ordinal of each ordered-path record
   int64_t* byv = nullptr;        // FW_AGG_MINBY / MAXBY: the batch's value column (DevCfg::by_val)
+  int64_t* rowc = nullptr;       // FW_AGG_ROW: the batch's value columns (column j at j * max_batch), DevCfg::row_cols
+  uint8_t* rown = nullptr;       //             and NULL masks (DevCfg::row_nulls)
   int32_t T = 0;                 // tiles of the batch that used this set
   int64_t n = 0;                 // records of the batch
   bool split = false;            // its aggregate split long partitions (fw_op::hot)
@@ -121,6 +123,8 @@ struct fw_op {
   TdBuf td{};                // FW_AGG_TDIGEST: per-push compression buffers
   DevCount cw{};             // FW_COUNT: count-window state
   bool td_export = false;    // FW_AGG_TDIGEST: fired rows keep their centroids (DevRows::dig)
+  int64_t dig_stride = 0;    // words per row of DevRows::dig (t-digest export: 1 + delta; FW_AGG_ROW: 1 + aggregates)
+  int64_t* iota = nullptr;   // FW_AGG_ROW: 0, 1, ... (a record's value is its index in the push)
 
   DevRows out{};
   DevSide side{};
@@ -230,6 +234,10 @@ int alloc_scratch(fw_op* op, Scratch& s, int64_t mb, int64_t m) {
   if (op->dc.dense) HIP_OR_RETURN(op, dmalloc(&s.rsv, (size_t)op->dc.P + FW_RSV_WORDS));
   if (op->cfg.aggregate >= FW_AGG_FIRST && op->cfg.aggregate <= FW_AGG_FIRST_MAX) HIP_OR_RETURN(op, dmalloc(&s.so, mb));
   if (op->cfg.aggregate == FW_AGG_MINBY || op->cfg.aggregate == FW_AGG_MAXBY) HIP_OR_RETURN(op, dmalloc(&s.byv, mb));
+  if (op->cfg.aggregate == FW_AGG_ROW) {
+    HIP_OR_RETURN(op, dmalloc(&s.rowc, (size_t)(mb * op->dc.row_nc)));
+    HIP_OR_RETURN(op, dmalloc(&s.rown, (size_t)mb));
+  }
   DevCfg probe = op->dc;
   probe.compact = 1;
   if (fwdev::gather_mode(probe, 1)) {
@@ -246,6 +254,8 @@ void free_scratch(Scratch& s) {
   dfree(s.hist);
   dfree(s.scan_tmp);
   dfree(s.part);
+  dfree(s.rowc);
+  dfree(s.rown);
   dfree(s.sk);
   dfree(s.stt);
   dfree(s.sv);
@@ -305,8 +315,8 @@ int ensure_out_capacity(fw_op* op, int64_t need, int64_t keep) {
       HIP_OR_RETURN(op, hipMemcpyAsync(*cols_new[i], *cols_old[i], keep * sizeof(int64_t), hipMemcpyDeviceToDevice,
                                        op->stream));
   }
-  const int64_t dstride = 1 + 2 * (int64_t)op->dc.td_nb;  // t-digest export: one record per row
-  if (op->td_export) {
+  const int64_t dstride = op->dig_stride;  // t-digest export / FW_AGG_ROW results: one record per row
+  if (op->dig_stride) {
     HIP_OR_RETURN(op, dmalloc(&n.dig, (size_t)(cap * dstride)));
     if (keep > 0 && op->out.dig)
       HIP_OR_RETURN(op, hipMemcpyAsync(n.dig, op->out.dig, keep * dstride * sizeof(int64_t), hipMemcpyDeviceToDevice,
@@ -533,6 +543,9 @@ int settle(fw_op* op) {
     c.ndn0 = S.ndn0;
     c.ord_base = S.ord_base;
     c.wide = S.wide_word(op->dc.P);
+    c.row_cols = S.rowc;
+    c.row_nulls = S.rown;
+    c.row_stride = op->max_batch;
     if (S.partials) {  // a partials push: only its merge can have suspended
       c.nt_floor = fwdev::pane_nt_floor(c, S.wm);  // (panes: a new pane's first window)
       timed(op, K_AGGREGATE, [&] {
@@ -550,9 +563,12 @@ int settle(fw_op* op) {
       timed(op, K_AGGREGATE, [&] {
         fwdev::launch_aggregate(c, S.wm, S.part, S.offs(), S.offT(), op->tb, op->prog, 1, S.split ? &op->hot : nullptr,
                                 S.n, op->d_status, op->stream, nullptr, 0, S.single ? S.rsv : nullptr, op->rcap);
-        // the update skipped itself behind the suspension; register max is idempotent, so it reruns whole
+        // the update skipped itself behind the suspension; register max is idempotent, so it reruns whole (and the
+        // Table aggregates' adds, which are not, never started)
         if (c.agg == FW_AGG_HLL)
           fwdev::launch_hll_update(c, S.part, S.offs(), S.offT(), S.n, op->tb, op->d_status, op->stream);
+        if (c.agg == FW_AGG_ROW)
+          fwdev::launch_row_update(c, S.part, S.offs(), S.offT(), S.n, op->tb, op->d_status, op->stream);
       });
     // after an aggregate suspension the ordered path never started; otherwise it resumes
     if (!c.dense) timed(op, K_SLOW, [&] {
@@ -657,9 +673,19 @@ int push_count(fw_op* op, const int64_t* key, const int64_t* val, int64_t n) {
 }
 
 hipStream_t input_stream_of(const fw_op* op);  // the stream device pushes read their columns on
+// FW_AGG_ROW input of a push: the caller's columns (column j of the push's record i at cols[j * stride + i]) and NULL
+// masks (nullptr = none)
+struct RowIn {
+  const int64_t* cols;
+  const uint8_t* nulls;
+  int64_t stride;
+};
 int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int64_t n,
-                bool async_ok) {
+                bool async_ok, const RowIn* rin = nullptr) {
   if (n == 0) return FW_OK;
+  if ((op->dc.agg == FW_AGG_ROW) != (rin != nullptr))
+    return set_err(op, FW_ERR_ARG, rin ? "fw_push_row_batch needs an FW_AGG_ROW operator"
+                                       : "an FW_AGG_ROW operator takes its records through fw_push_row_batch");
   if (op->cfg.assigner == FW_COUNT) return push_count(op, key, val, n);
   int rc;
   DevCfg c = op->dc;  // by value: a session batch stamps its taint epoch into it
@@ -773,6 +799,15 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
     HIP_OR_RETURN(op, hipEventRecord(op->ev_scat[nxt], bs));
     HIP_OR_RETURN(op, hipStreamWaitEvent(op->stream, op->ev_scat[nxt], 0));
   }
+  if (S.rowc) {  // FW_AGG_ROW: the batch's columns and NULL masks, kept by the set (a resumed push reads them again)
+    HIP_OR_RETURN(op, hipMemcpy2DAsync(S.rowc, (size_t)op->max_batch * sizeof(int64_t), rin->cols,
+                                       (size_t)rin->stride * sizeof(int64_t), (size_t)n * sizeof(int64_t),
+                                       (size_t)op->dc.row_nc, hipMemcpyDefault, op->stream));
+    if (rin->nulls)
+      HIP_OR_RETURN(op, hipMemcpyAsync(S.rown, rin->nulls, (size_t)n, hipMemcpyDefault, op->stream));
+    else
+      HIP_OR_RETURN(op, hipMemsetAsync(S.rown, 0, (size_t)n, op->stream));
+  }
   if (early && (rc = settle(op))) return rc;
   if ((rc = maybe_restart_rows(op))) return rc;
   // the ordered path checks its room per chunk and suspends when it runs out; one chunk always fits
@@ -788,6 +823,9 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
   cc.narrow = c.narrow;
   cc.ndn0 = c.ndn0;
   cc.wide = c.wide;
+  cc.row_cols = S.rowc;
+  cc.row_nulls = S.rown;
+  cc.row_stride = op->max_batch;
   // a partition can outgrow one aggregate workgroup (hot keys) only when the batch is longer than a chunk
   const bool split = !cc.dense && (cc.wpr == 1 || cc.panes) && n > cc.agg_chunk;
   if (split && (rc = ensure_hot(op))) return rc;
@@ -809,6 +847,8 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
                                 n, op->d_status, op->stream, nullptr, 0, single ? S.rsv : nullptr, op->rcap);
         if (cc.agg == FW_AGG_HLL)
           fwdev::launch_hll_update(cc, S.part, S.offs(), S.offT(), n, op->tb, op->d_status, op->stream);
+        if (cc.agg == FW_AGG_ROW)
+          fwdev::launch_row_update(cc, S.part, S.offs(), S.offT(), n, op->tb, op->d_status, op->stream);
       },
       nullptr, cc.dense);  // (the dense aggregate is one kernel)
   if (!cc.dense)  // (tumbling windows without allowed lateness: no record needs arrival order)
@@ -964,7 +1004,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     snprintf(msg, sizeof msg, "invalid KeyGroupRange [%d, %d]", cfg.key_group_start, cfg.key_group_end);
   if (!msg[0] && cfg.sub_partitions != 0 && (cfg.sub_partitions & (cfg.sub_partitions - 1)))
     snprintf(msg, sizeof msg, "sub_partitions must be a power of two");
-  if (!msg[0] && (cfg.aggregate < FW_AGG_COUNT_SUM_MIN_MAX || cfg.aggregate > FW_AGG_TDIGEST))
+  if (!msg[0] && (cfg.aggregate < FW_AGG_COUNT_SUM_MIN_MAX || cfg.aggregate > FW_AGG_ROW))
     snprintf(msg, sizeof msg, "unknown aggregate %d", cfg.aggregate);
   const int32_t hll_p = cfg.hll_precision ? cfg.hll_precision : 14;
   if (!msg[0] && cfg.aggregate == FW_AGG_HLL && (hll_p < 4 || hll_p > 16))
@@ -1000,6 +1040,27 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     snprintf(msg, sizeof msg, "the t-digest aggregate is offered over a Double field for tumbling, sliding and session "
                               "windows (PurgingTrigger only for tumbling / sliding windows without allowed lateness)");
     unsupported = true;
+  }
+  if (!msg[0] && cfg.aggregate == FW_AGG_ROW) {
+    // the Table API's group windows (DataStreamGroupWindowAggregate.scala:197-294): event-time tumbling / sliding /
+    // session windows with the assigner's EventTimeTrigger, no allowed lateness and no side output
+    if (cfg.row_columns < 1 || cfg.row_columns > 8 || cfg.row_aggregates < 1 || cfg.row_aggregates > 16) {
+      snprintf(msg, sizeof msg, "FW_AGG_ROW needs 1 .. 8 value columns and 1 .. 16 aggregates");
+    } else {
+      for (int j = 0; j < cfg.row_columns && !msg[0]; j++)
+        if (cfg.row_column_type[j] < FW_VAL_I64 || cfg.row_column_type[j] > FW_VAL_F32)
+          snprintf(msg, sizeof msg, "FW_AGG_ROW: unknown type %d of column %d", cfg.row_column_type[j], j);
+      for (int q = 0; q < cfg.row_aggregates && !msg[0]; q++) {
+        const int fn = cfg.row_aggregate[q] >> 8, col = cfg.row_aggregate[q] & 0xff;
+        if (fn < FW_ROW_COUNT_STAR || fn > FW_ROW_AVG || col >= cfg.row_columns)
+          snprintf(msg, sizeof msg, "FW_AGG_ROW: aggregate %d is not FW_ROW_* << 8 | column", q);
+      }
+    }
+    if (!msg[0] && (cfg.assigner == FW_COUNT || cfg.allowed_lateness != 0 || cfg.purging || cfg.side_output)) {
+      snprintf(msg, sizeof msg, "FW_AGG_ROW is offered for the Table API's event-time group windows: tumbling, sliding "
+                                "or session windows, EventTimeTrigger, no allowed lateness, no side output");
+      unsupported = true;
+    }
   }
   if (!msg[0] && cfg.aggregate >= FW_AGG_FIRST && cfg.aggregate <= FW_AGG_FIRST_MAX && cfg.assigner == FW_SLIDING && cfg.slide > 0 &&
       (cfg.size + cfg.slide - 1) / cfg.slide > 65535) {
@@ -1075,8 +1136,8 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   // sliding windows whose size is a multiple of the slide, without allowed lateness, are kept as panes:
   // one state update per element instead of size/slide (DevCfg::panes; FW_NO_PANES=1 disables it)
   c.panes = cfg.assigner == FW_SLIDING && cfg.allowed_lateness == 0 && cfg.size > cfg.slide &&
-            cfg.size % cfg.slide == 0 && cfg.aggregate != FW_AGG_HLL &&  // (HLL, t-digest: a block per window)
-            cfg.aggregate != FW_AGG_TDIGEST &&
+            cfg.size % cfg.slide == 0 && cfg.aggregate != FW_AGG_HLL &&  // (HLL, t-digest, rows: a block per window)
+            cfg.aggregate != FW_AGG_TDIGEST && cfg.aggregate != FW_AGG_ROW &&
             !(getenv("FW_NO_PANES") && atoi(getenv("FW_NO_PANES")));
   if (cfg.assigner != FW_SESSION) {
     make_div_inv((uint64_t)c.size, &c.mag_size, &c.l_size);
@@ -1086,7 +1147,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   // and at least 2 bits of sub-partition to carry the window delta (FW_NO_COMPACT=1 disables them)
   c.compact = (cfg.assigner == FW_TUMBLING || c.panes) &&
               (cfg.aggregate == FW_AGG_COUNT_SUM_MIN_MAX || cfg.aggregate == FW_AGG_HLL ||
-               cfg.aggregate == FW_AGG_TDIGEST) && c.log_s >= 2 &&
+               cfg.aggregate == FW_AGG_TDIGEST || cfg.aggregate == FW_AGG_ROW) && c.log_s >= 2 &&
               !(getenv("FW_NO_COMPACT") && atoi(getenv("FW_NO_COMPACT")));
   const int64_t expected = cfg.expected_entries > 0 ? cfg.expected_entries : (int64_t)c.P * 512;
   if (cfg.aggregate >= FW_AGG_FIRST) c.agg = cfg.aggregate;  // (FW_AGG_HLL is set below)
@@ -1117,12 +1178,25 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     HIP_OR_RETURN(op, hipMemcpy(dq, qb.data(), qb.size() * sizeof(double), hipMemcpyHostToDevice));
     c.td_qb = dq;
     op->td_export = cfg.tdigest_export != 0;
+    if (op->td_export) op->dig_stride = 1 + 2 * (int64_t)c.td_nb;
+  } else if (cfg.aggregate == FW_AGG_ROW) {
+    // one RowAcc per value column per live (key, window), zero = empty (fw_internal.h)
+    c.agg = FW_AGG_ROW;
+    c.vtype = FW_VAL_I64;  // (a record's value is its index in the push)
+    c.sum_bits = 64;
+    c.f32 = 0;
+    c.row_nc = cfg.row_columns;
+    c.row_ns = cfg.row_aggregates;
+    for (int j = 0; j < 8; j++) c.row_type[j] = j < cfg.row_columns ? cfg.row_column_type[j] : 0;
+    for (int q = 0; q < 16; q++) c.row_spec[q] = q < cfg.row_aggregates ? cfg.row_aggregate[q] : 0;
+    c.pool_bytes = ((int64_t)sizeof(RowAcc) * c.row_nc + 15) / 16 * 16;
+    op->dig_stride = 1 + (int64_t)c.row_ns;
   }
   if (c.pool_bytes) {
     c.pool_blocks = std::max<int64_t>(1024, expected + expected / 4);
     HIP_OR_RETURN(op, dmalloc(&c.pool, (size_t)(c.pool_blocks * c.pool_bytes)));
-    if (c.agg == FW_AGG_HLL)  // registers start at zero (and are zeroed when freed)
-      HIP_OR_RETURN(op, hipMemsetAsync(c.pool, 0, (size_t)(c.pool_blocks * c.pool_bytes), op->stream));
+    if (c.agg == FW_AGG_HLL || c.agg == FW_AGG_ROW)  // registers / row accumulators start at zero (and are zeroed
+      HIP_OR_RETURN(op, hipMemsetAsync(c.pool, 0, (size_t)(c.pool_blocks * c.pool_bytes), op->stream));  // when freed)
     HIP_OR_RETURN(op, dmalloc(&c.pool_free, (size_t)c.pool_blocks));
     HIP_OR_RETURN(op, dmalloc(&c.pool_defer, (size_t)c.pool_blocks));
     HIP_OR_RETURN(op, dmalloc(&c.pool_ctr, 3));
@@ -1146,6 +1220,12 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   HIP_OR_RETURN(op, dmalloc(&op->in_kh, mb));
   for (Scratch& sc : op->sc)
     if ((rc = alloc_scratch(op, sc, mb, m))) return rc;
+  if (c.agg == FW_AGG_ROW) {  // the records' values: their index in the push
+    std::vector<int64_t> h((size_t)mb);
+    for (int64_t i = 0; i < mb; i++) h[(size_t)i] = i;
+    HIP_OR_RETURN(op, dmalloc(&op->iota, (size_t)mb));
+    HIP_OR_RETURN(op, hipMemcpy(op->iota, h.data(), (size_t)mb * sizeof(int64_t), hipMemcpyHostToDevice));
+  }
   c.wide = op->sc[0].wide;  // (every push sets its own set's word)
   // single-pass scatter: a partition's run may take twice its share of the largest batch (part holds mb PRecs
   // = 2 mb compact records), whole 128-byte lines apart
@@ -1358,6 +1438,7 @@ void fw_destroy(fw_op* op) {
   dfree(op->xreg_tmp);
   dfree(op->hoff);
   dfree(op->hoff_tmp);
+  dfree(op->iota);
   for (auto& pr : op->prof_pending) {
     (void)hipEventDestroy(pr.a);
     (void)hipEventDestroy(pr.b);
@@ -1419,6 +1500,67 @@ int push_device_batches(fw_op* op, const int64_t* key, const int64_t* ts, const 
 int fw_push_batch_device(fw_op* op, const int64_t* key, const int64_t* ts, const void* val, const int32_t* key_hash,
                          int64_t n) {
   return push_device_batches(op, key, ts, val, key_hash, n, true);
+}
+
+int fw_push_row_batch_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t* cols,
+                             const uint8_t* nulls, const int32_t* key_hash, int64_t n) {
+  if (!op || n < 0 || (n > 0 && (!key || !ts || !cols))) return op ? set_err(op, FW_ERR_ARG, "null column") : FW_ERR_ARG;
+  if (op->dc.agg != FW_AGG_ROW) return set_err(op, FW_ERR_ARG, "fw_push_row_batch needs an FW_AGG_ROW operator");
+  if (op->cfg.key_kind == FW_KEY_HASHED && n > 0 && !key_hash)
+    return set_err(op, FW_ERR_ARG, "key_hash required for FW_KEY_HASHED");
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  for (int64_t b = 0; b < n; b += op->max_batch) {
+    const int64_t m = std::min(op->max_batch, n - b);
+    const RowIn rin{cols + b, nulls ? nulls + b : nullptr, n};
+    int rc = push_device(op, key + b, ts + b, op->iota, key_hash ? key_hash + b : nullptr, m, true, &rin);
+    if (rc) return rc;
+  }
+  return FW_OK;
+}
+
+int fw_push_row_batch(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t* cols, const uint8_t* nulls,
+                      const int32_t* key_hash, int64_t n) {
+  if (!op || n < 0 || (n > 0 && (!key || !ts || !cols))) return op ? set_err(op, FW_ERR_ARG, "null column") : FW_ERR_ARG;
+  if (op->dc.agg != FW_AGG_ROW) return set_err(op, FW_ERR_ARG, "fw_push_row_batch needs an FW_AGG_ROW operator");
+  if (op->cfg.key_kind == FW_KEY_HASHED && n > 0 && !key_hash)
+    return set_err(op, FW_ERR_ARG, "key_hash required for FW_KEY_HASHED");
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  for (int64_t b = 0; b < n; b += op->max_batch) {
+    const int64_t m = std::min(op->max_batch, n - b);
+    HIP_OR_RETURN(op, hipMemcpyAsync(op->in_key, key + b, m * 8, hipMemcpyHostToDevice, op->stream));
+    HIP_OR_RETURN(op, hipMemcpyAsync(op->in_ts, ts + b, m * 8, hipMemcpyHostToDevice, op->stream));
+    if (op->cfg.key_kind == FW_KEY_HASHED)
+      HIP_OR_RETURN(op, hipMemcpyAsync(op->in_kh, key_hash + b, m * 4, hipMemcpyHostToDevice, op->stream));
+    // (the columns go from host memory straight into the push's copy, on the operator's stream)
+    const RowIn rin{cols + b, nulls ? nulls + b : nullptr, n};
+    int rc = push_device(op, op->in_key, op->in_ts, op->iota, op->in_kh, m, false, &rin);
+    if (rc) return rc;
+  }
+  return settle(op);  // host columns: the caller may reuse them when this returns
+}
+
+int fw_drain_row_results(fw_op* op, int64_t* values, uint32_t* null_mask, int64_t cap, int64_t* n) {
+  if (!op) return FW_ERR_ARG;
+  if (op->dc.agg != FW_AGG_ROW) return set_err(op, FW_ERR_UNSUPPORTED, "fw_drain_row_results needs FW_AGG_ROW");
+  HIP_OR_RETURN(op, hipSetDevice(op->device));
+  int rc = settle(op);
+  if (rc) return rc;
+  const int64_t base = op->out_base, have = (int64_t)op->h_status->out_rows - base;
+  if (n) *n = have;
+  if (cap < have) return set_err(op, FW_ERR_ARG, "drain capacity %lld < pending rows %lld", (long long)cap, (long long)have);
+  if (have <= 0) return FW_OK;
+  const int64_t ns = op->dc.row_ns, stride = op->dig_stride;
+  std::vector<int64_t> h((size_t)(have * stride));
+  HIP_OR_RETURN(op, hipMemcpyAsync(h.data(), op->out.dig + base * stride, h.size() * sizeof(int64_t),
+                                   hipMemcpyDeviceToHost, op->stream));
+  HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
+  for (int64_t i = 0; i < have; i++) {
+    const int64_t* d = h.data() + i * stride;
+    if (null_mask) null_mask[i] = (uint32_t)d[0];
+    if (values)
+      for (int64_t q = 0; q < ns; q++) values[i * ns + q] = d[1 + q];
+  }
+  return FW_OK;
 }
 
 int fw_set_async_input(fw_op* op, int enable) {
@@ -1842,6 +1984,7 @@ int64_t fw_state_block_bytes(fw_op* op) {
   if (!op) return 0;
   if (op->dc.agg == FW_AGG_HLL) return (int64_t)1 << op->dc.hll_p;
   if (op->dc.agg == FW_AGG_TDIGEST) return (1 + 2 * (int64_t)op->dc.td_nb) * (int64_t)sizeof(int64_t);
+  if (op->dc.agg == FW_AGG_ROW) return 5 * (int64_t)op->dc.row_nc * (int64_t)sizeof(int64_t);
   return 0;
 }
 

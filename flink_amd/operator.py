@@ -61,6 +61,13 @@ class GpuWindowOperator:
             c.tdigest_export = int(td.export)
             c.tdigest_quantiles = (ctypes.c_double * 3)(*td.quantiles)
         c.aggregate = aggregate.aggregate_kind()
+        if c.aggregate == N.FW_AGG_ROW:  # the Table API's group-window accumulator (RowAggregate)
+            c.row_columns = len(aggregate.column_types)
+            c.row_aggregates = len(aggregate.aggregates)
+            for j, t in enumerate(aggregate.type_codes()[:8]):
+                c.row_column_type[j] = t
+            for q, w in enumerate(aggregate.spec_words()[:16]):
+                c.row_aggregate[q] = w
         c.key_kind = _KEY_KINDS[key_type]
         c.purging = int(trigger.purging)
         c.side_output = int(side_output)
@@ -93,6 +100,7 @@ class GpuWindowOperator:
         self.epoch = 0  # watermarks processed so far
         self._rows = []
         self._side = []
+        self._rowres = []
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
@@ -180,6 +188,66 @@ class GpuWindowOperator:
         N.check(rc, self._h)
 
     processElements = process_batch
+
+    def process_rows(self, keys, timestamps, cols, nulls=None, key_hash=None):
+        """RowAggregate: a micro-batch of the Table API's input rows -- keys, timestamps, the value columns (a
+        sequence of columns, or one [columns, n] array / tensor; int64 values, or float64 for "double" / "float"
+        columns) and an optional NULL mask per record (uint8, bit j = column j is NULL)."""
+        L = N.lib()
+        nc = len(self.aggregate.column_types)
+        if _is_torch(keys):
+            import torch
+            n = keys.numel()
+            mat = cols if _is_torch(cols) else torch.stack([c.view(torch.int64) if c.dtype == torch.float64 else c
+                                                            for c in cols])
+            if mat.dtype == torch.float64:
+                mat = mat.view(torch.int64)
+            mat = mat.contiguous()
+            if mat.shape != (nc, n) or mat.dtype != torch.int64 or not mat.is_cuda:
+                raise ValueError(f"cols must be {nc} int64 / float64 CUDA columns of {n} values")
+            if nulls is not None and (nulls.dtype != torch.uint8 or nulls.numel() != n or not nulls.is_cuda):
+                raise ValueError("nulls must be a uint8 CUDA tensor, one mask per record")
+            for t in (keys, timestamps) + ((key_hash,) if key_hash is not None else ()):
+                if not t.is_cuda or not t.is_contiguous() or t.numel() != n:
+                    raise ValueError("device columns must be contiguous CUDA tensors of equal length")
+            self._input_stream(keys.device).wait_stream(torch.cuda.current_stream(keys.device))
+            rc = L.fw_push_row_batch_device(self._h, keys.data_ptr(), timestamps.data_ptr(), mat.data_ptr(),
+                                            nulls.data_ptr() if nulls is not None else None,
+                                            key_hash.data_ptr() if key_hash is not None else None, n)
+            self._inflight = (keys, timestamps, mat, nulls, key_hash)
+        else:
+            keys = np.ascontiguousarray(keys, dtype=np.int64)
+            timestamps = np.ascontiguousarray(timestamps, dtype=np.int64)
+            n = len(keys)
+            mat = np.ascontiguousarray(np.stack([np.asarray(c).view(np.int64) if np.asarray(c).dtype == np.float64
+                                                 else np.asarray(c, dtype=np.int64) for c in cols])
+                                       if not isinstance(cols, np.ndarray) or cols.ndim != 2 else cols.view(np.int64)
+                                       if cols.dtype == np.float64 else cols.astype(np.int64))
+            if mat.shape != (nc, n) or len(timestamps) != n:
+                raise ValueError(f"cols must be {nc} columns of {n} values")
+            nm = None
+            if nulls is not None:
+                nulls = np.ascontiguousarray(nulls, dtype=np.uint8)
+                nm = nulls.ctypes.data
+            kh = None
+            if key_hash is not None:
+                key_hash = np.ascontiguousarray(key_hash, dtype=np.int32)
+                kh = key_hash.ctypes.data
+            rc = L.fw_push_row_batch(self._h, keys.ctypes.data, timestamps.ctypes.data, mat.ctypes.data, nm, kh, n)
+        N.check(rc, self._h)
+
+    def drain_row_results(self):
+        """RowAggregate: the pending rows' aggregate values (int64 [rows, aggregates]: integers, or f64 bits for
+        floating results) and NULL masks (uint32 [rows]), in row order.  Call before the rows are drained."""
+        L = N.lib()
+        n_rows = ctypes.c_int64()
+        N.check(L.fw_pending(self._h, ctypes.byref(n_rows), None), self._h)
+        n, ns = n_rows.value, len(self.aggregate.aggregates)
+        vals = np.zeros((n, ns), dtype=np.int64)
+        nm = np.zeros(n, dtype=np.uint32)
+        got = ctypes.c_int64()
+        N.check(L.fw_drain_row_results(self._h, vals.ctypes.data, nm.ctypes.data, n, ctypes.byref(got)), self._h)
+        return vals[:got.value], nm[:got.value]
 
     # ------------------------------------------------------------------ pre-shuffle combining (SURVEY §8e)
     def combine_extract(self, world=1):
@@ -392,10 +460,27 @@ class GpuWindowOperator:
             self._rows.append(self.drain_rows(self.epoch))
 
     def watermark(self, wm):
+        if self.aggregate.aggregate_kind() == N.FW_AGG_ROW:  # the rows' aggregate values before the rows go
+            self.advance_watermark(wm)
+            self._rowres.append(self.drain_row_results())
+            self._rows.append(self.drain_rows(self.epoch - 1))
+            return
         self._rows.append(self.process_watermark(wm))
+
+    def process_row_batch(self, keys, ts, cols, nulls=None, key_hash=None):
+        """Harness form of process_rows: the batch is processed (and its errors raised) before return."""
+        self.process_rows(keys, ts, cols, nulls, key_hash)
+        self.synchronize()
 
     def rows(self):
         return np.concatenate(self._rows) if self._rows else np.zeros(0, dtype=ROW_DTYPE)
+
+    def row_results(self):
+        """RowAggregate, harness form: (values, NULL masks) of every row rows() returns, in the same order."""
+        ns = len(self.aggregate.aggregates)
+        if not self._rowres:
+            return np.zeros((0, ns), dtype=np.int64), np.zeros(0, dtype=np.uint32)
+        return np.concatenate([v for v, _ in self._rowres]), np.concatenate([m for _, m in self._rowres])
 
     def side_rows(self):
         return np.concatenate(self._side) if self._side else np.zeros(0, dtype=SIDE_DTYPE)

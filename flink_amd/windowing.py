@@ -369,6 +369,42 @@ class HyperLogLog:
         return N.FW_AGG_HLL
 
 
+ROW_FUNCTIONS = {"count_star": N.FW_ROW_COUNT_STAR, "count": N.FW_ROW_COUNT, "sum": N.FW_ROW_SUM, "min": N.FW_ROW_MIN,
+                 "max": N.FW_ROW_MAX, "avg": N.FW_ROW_AVG}
+
+
+@dataclass(frozen=True)
+class RowAggregate:
+    """The Table API's group-window accumulator (DataStreamGroupWindowAggregate.scala:197-294: one generated
+    AggregateFunction over a Row holding several built-in aggregates): `column_types` are the value columns' types
+    ("long", "int", "short", "byte", "double", "float"; up to 8, nullable), `aggregates` the select list's built-in
+    aggregates as (function, column index) with function in count_star / count / sum / min / max / avg (up to 16).
+    Semantics of flink-table's CountAggFunction, SumAggFunction, Min/MaxAggFunction and AvgAggFunction (restated in
+    oracle/window_oracle.h OR_AGG_ROW).  Records go in through GpuWindowOperator.process_rows; fired rows carry
+    count = COUNT(*) and drain_row_results gives each row's aggregate values and NULL mask."""
+    column_types: tuple = ("long",)
+    aggregates: tuple = (("count_star", 0),)
+    value_type: str = "long"  # (a record's value column is its index in the push)
+
+    def native(self):
+        return N.FW_VAL_I64
+
+    def hll_precision(self):
+        return 0
+
+    def tdigest(self):
+        return None
+
+    def aggregate_kind(self):
+        return N.FW_AGG_ROW
+
+    def spec_words(self):
+        return [(ROW_FUNCTIONS[f] << 8) | int(c) for f, c in self.aggregates]
+
+    def type_codes(self):
+        return [VALUE_TYPES[t] for t in self.column_types]
+
+
 @dataclass(frozen=True)
 class TDigest:
     """User AggregateFunction of SURVEY §8d C5: quantiles of a Double field per key and window from a merging

@@ -107,6 +107,30 @@ extern "C" {
                                       FW_AGG_FIRST, but the min column holds the field's MAXIMUM (the first
                                       element with the field replaced by the max) */
 
+#define FW_AGG_ROW 7               /* the Table API's group-window aggregation (flink-libraries/flink-table
+                                      DataStreamGroupWindowAggregate.scala:197-294 -> WindowedStream.aggregate of
+                                      one accumulator Row): several built-in aggregates over up to 8 nullable value
+                                      columns (row_columns, row_column_type[], row_aggregate[] = FW_ROW_* << 8 |
+                                      column), pushed with fw_push_row_batch(_device).  Semantics of the Table
+                                      functions (.../table/functions/aggfunctions/ *AggFunction.scala; oracle/window_oracle.h
+                                      OR_AGG_ROW): COUNT(col) counts non-null values; SUM / MIN / MAX / AVG are
+                                      NULL when the column had none; integral SUM wraps to the column's width;
+                                      integral AVG = the Long sum / count (Java division; Long: the exact sum)
+                                      narrowed to the type; Double / Float AVG = the double sum / count.  Tumbling,
+                                      sliding and session windows (merged sessions merge every aggregate), allowed
+                                      lateness 0, EventTimeTrigger, no side output (the Table planner sets none).
+                                      Rows carry count = COUNT(*) (sum / min / max 0); fw_drain_row_results gives
+                                      each row's aggregates and their NULL mask.  Keyed-state snapshots carry the
+                                      accumulator as a block (fw_snapshot_key_group_blocks): per column its
+                                      non-null count, the sum's low and high words (floating: the f64 sum, 0),
+                                      min and max (the column's value; 0 when the count is 0), int64 each. */
+#define FW_ROW_COUNT_STAR 0 /* COUNT(*) / COUNT(1): every record (CountAggFunction.accumulate(acc))           */
+#define FW_ROW_COUNT 1      /* COUNT(col): the non-null values (CountAggFunction.scala:51-55)                   */
+#define FW_ROW_SUM 2        /* SUM(col) (SumAggFunction.scala)                                                  */
+#define FW_ROW_MIN 3        /* MIN(col) (MinAggFunction.scala; Double / Float by their compare)                 */
+#define FW_ROW_MAX 4        /* MAX(col) (MaxAggFunction.scala)                                                  */
+#define FW_ROW_AVG 5        /* AVG(col) (AvgAggFunction.scala: Integral / BigIntegral / Floating)               */
+
 #define FW_KEY_LONG 0   /* key is a Long: hashCode = (int)(v ^ (v >>> 32))               */
 #define FW_KEY_INT 1    /* key is an Integer: hashCode = value                              */
 #define FW_KEY_HASHED 2 /* caller passes key.hashCode() per record (String, Tuple, POJO);
@@ -145,6 +169,10 @@ typedef struct fw_config {
   int32_t count_evict_after;   /* FW_COUNT: 1 = CountEvictor.of(size, true): evict after the window function
                                   (the fired window is the last min(elements, size + slide)) */
   int32_t pad0;
+  int32_t row_columns;         /* FW_AGG_ROW: value columns per record, 1 .. 8                   */
+  int32_t row_aggregates;      /* FW_AGG_ROW: aggregates of a row, 1 .. 16                       */
+  int32_t row_column_type[8];  /* FW_AGG_ROW: FW_VAL_* of each column                            */
+  int32_t row_aggregate[16];   /* FW_AGG_ROW: FW_ROW_* << 8 | column                             */
 } fw_config;
 
 typedef struct fw_op fw_op;
@@ -235,6 +263,19 @@ int fw_rows_device(fw_op* op, fw_rows* dev_view, int64_t* n);
  * weights at [i * delta/2 + k], k < n_centroids[i].  Call before fw_drain_rows. */
 int fw_drain_digests(fw_op* op, int64_t* n_centroids, double* sum, int64_t* weight, int64_t cap_rows, int64_t* n);
 int fw_clear_pending(fw_op* op);
+/* FW_AGG_ROW: processElement for n records of the Table API's input rows (DataStreamGroupWindowAggregate's
+ * WindowedStream.aggregate): row_columns value columns, column-major (cols + j * n = column j: int64 values
+ * sign-extended, Double / Float as f64 bits), and per record a NULL mask (bit j = column j is NULL; nulls = NULL:
+ * no NULLs).  Host buffers (processed before return) or HBM (_device, stream-ordered as fw_push_batch_device). */
+int fw_push_row_batch(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t* cols, const uint8_t* nulls,
+                      const int32_t* key_hash, int64_t n);
+int fw_push_row_batch_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t* cols,
+                             const uint8_t* nulls, const int32_t* key_hash, int64_t n);
+/* FW_AGG_ROW: the aggregates of the pending rows (the generated AggregateFunction's getValue per aggregate:
+ * values[i * row_aggregates + s], integers sign-extended, floating results as f64 bits, a Float result as the
+ * double of the float) and null_mask[i] (bit s = aggregate s is NULL), without draining them: call before
+ * fw_drain_rows.  Either output may be NULL. */
+int fw_drain_row_results(fw_op* op, int64_t* values, uint32_t* null_mask, int64_t cap_rows, int64_t* n);
 
 int fw_get_stats(fw_op* op, fw_stats* out);
 

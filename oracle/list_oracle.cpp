@@ -6,6 +6,7 @@
 
 #include "window_oracle.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -68,6 +69,33 @@ struct Elem {
   int64_t ts, val, ord;
 };
 
+// ---------------------------------------------------------------- merging windows (EventTimeSessionWindows)
+// TimeWindow.hashCode = MathUtils.longToIntWithBitMixing(start + end) (TimeWindow.java:102-104, MathUtils.java:177-182)
+inline int32_t tw_hash(const W& w) {
+  uint64_t in = (uint64_t)jadd(w.start, w.end);
+  in = (in ^ (in >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  in = (in ^ (in >> 27)) * 0x94d049bb133111ebULL;
+  in = in ^ (in >> 31);
+  return (int32_t)in;
+}
+// iteration order of a java.util.HashSet<TimeWindow> that had `ins` added in this order (TimeWindow.mergeWindows'
+// merge sets, TimeWindow.java:213-233): HashMap buckets (h ^ h >>> 16) & (capacity - 1), capacity 16 doubled past 3/4
+// load, a bucket in insertion order (a resize splits buckets keeping it; the small sets of a session merge never
+// treeify)
+std::vector<W> hashset_order(const std::vector<W>& ins) {
+  size_t cap = 16;
+  while (ins.size() > cap * 3 / 4) cap *= 2;
+  std::vector<std::pair<uint32_t, size_t>> k(ins.size());
+  for (size_t i = 0; i < ins.size(); i++) {
+    const uint32_t h = (uint32_t)tw_hash(ins[i]);
+    k[i] = {(h ^ (h >> 16)) & (uint32_t)(cap - 1), i};
+  }
+  std::sort(k.begin(), k.end());
+  std::vector<W> out;
+  for (const auto& x : k) out.push_back(ins[x.second]);
+  return out;
+}
+
 struct ListOracle {
   explicit ListOracle(const oracle_list_cfg& c) : cfg(c) {}
   oracle_list_cfg cfg;
@@ -81,6 +109,8 @@ struct ListOracle {
   std::vector<int64_t> side_key, side_ts, side_val, side_epoch;
 
   bool event_time() const { return cfg.assigner != OR_GLOBAL; }  // GlobalWindows.isEventTime() == false
+  bool merging() const { return cfg.assigner == OR_SESSION; }     // (cfg.size = the session gap)
+  std::map<int64_t, std::map<W, W>> msets;                       // MergingWindowSet per key: window -> state window
   bool is_float() const { return cfg.value_type == OR_VAL_F64 || cfg.value_type == OR_VAL_F32; }
 
   // WindowOperator.java:576-651
@@ -99,6 +129,74 @@ struct ListOracle {
     const int64_t c = cleanup_time(kw.w);
     if (c == LMAX) return;
     register_timer(c, kw);
+  }
+  void delete_timer(int64_t ts, const KW& kw) { timer_set.erase(Timer{ts, kw}); }
+
+  // MergingWindowSet.addWindow (MergingWindowSet.java:150-225) with TimeWindow.mergeWindows (TimeWindow.java:201-244)
+  // and EvictingWindowOperator's merge function (:118-148): the windows in flight are pairwise non-touching, so the
+  // one merge set (if any) holds the new window; its state window is the first merged window's in HashSet order,
+  // and the others' lists are appended to it in that order (HeapListState.mergeState = addAll,
+  // AbstractHeapMergingState.mergeNamespaces :67-93).
+  W add_window(int64_t key, std::map<W, W>& mapping, const W& nw) {
+    std::vector<W> ws;
+    for (const auto& kv : mapping) ws.push_back(kv.first);
+    ws.push_back(nw);
+    std::stable_sort(ws.begin(), ws.end(), [](const W& a, const W& b) { return a.start < b.start; });
+    std::vector<std::pair<W, std::vector<W>>> merged;  // (cover, members in insertion order)
+    for (const W& c : ws) {
+      if (!merged.empty() && merged.back().first.start <= c.end && merged.back().first.end >= c.start) {  // intersects
+        W& cv = merged.back().first;
+        cv = W{std::min(cv.start, c.start), std::max(cv.end, c.end)};
+        merged.back().second.push_back(c);
+      } else {
+        merged.push_back({c, {c}});
+      }
+    }
+    W result = nw;
+    bool merged_new = false, any = false;
+    for (auto& m : merged) {
+      if (m.second.size() < 2) continue;
+      any = true;
+      const W mr = m.first;
+      std::vector<W> mws = hashset_order(m.second);
+      const auto it_new = std::find(mws.begin(), mws.end(), nw);
+      if (it_new != mws.end()) {
+        mws.erase(it_new);
+        merged_new = true;
+        result = mr;
+      }
+      const W target = mapping.at(mws.front());
+      std::vector<W> sources;
+      for (const W& w : mws) {
+        auto it = mapping.find(w);
+        if (it != mapping.end()) {
+          sources.push_back(it->second);
+          mapping.erase(it);
+        }
+      }
+      mapping[mr] = target;
+      const auto it_t = std::find(sources.begin(), sources.end(), target);
+      if (it_t != sources.end()) sources.erase(it_t);
+      if (!(std::find(mws.begin(), mws.end(), mr) != mws.end() && mws.size() == 1)) {
+        if (jadd(mr.max_ts(), cfg.lateness) <= wm) throw OpErr{OR_ERR_MERGE_LATE};
+        register_timer(mr.max_ts(), KW{key, mr});  // EventTimeTrigger.onMerge
+        for (const W& w : mws) {
+          delete_timer(w.max_ts(), KW{key, w});  // triggerContext.clear() -> EventTimeTrigger.clear
+          const int64_t c = cleanup_time(w);
+          if (c != LMAX) delete_timer(c, KW{key, w});  // deleteCleanupTimer
+        }
+        for (const W& src : sources) {  // mergeNamespaces(target, sources)
+          auto it = lists.find(KW{key, src});
+          if (it == lists.end()) continue;
+          std::vector<Elem> moved = std::move(it->second);
+          lists.erase(it);
+          std::vector<Elem>& t = lists[KW{key, target}];
+          t.insert(t.end(), moved.begin(), moved.end());
+        }
+      }
+    }
+    if (!any || (result == nw && !merged_new)) mapping[result] = result;
+    return result;
   }
 
   void assign(int64_t ts, std::vector<W>& out) const {
@@ -151,9 +249,11 @@ struct ListOracle {
   }
 
   // EvictingWindowOperator.emitWindowContents (:334-366): evictBefore, the function over the remaining
-  // elements (recorded as a row and its contents), evictAfter, and the list re-stored (empty: cleared)
-  void emit_contents(const KW& kw) {
-    std::vector<Elem>& l = lists[kw];
+  // elements (recorded as a row and its contents), evictAfter, and the list re-stored (empty: cleared).
+  // kw: the window the row reports; lkw: the list's namespace (the state window of a merging window)
+  void emit_contents(const KW& kw) { emit_contents(kw, kw); }
+  void emit_contents(const KW& kw, const KW& lkw) {
+    std::vector<Elem>& l = lists[lkw];
     if (!cfg.evict_after) evict(l);
     oracle_list_row r{};
     r.key = kw.key;
@@ -192,13 +292,51 @@ struct ListOracle {
     }
     rows.push_back(r);
     if (cfg.evict_after) evict(l);
-    if (l.empty()) lists.erase(kw);  // windowState.clear() and nothing re-added
+    if (l.empty()) lists.erase(lkw);  // windowState.clear() and nothing re-added
+  }
+
+  // EvictingWindowOperator.processElement, merging branch (:110-170)
+  void process_merging(int64_t key, int64_t ts, int64_t val) {
+    std::map<W, W>& mapping = msets[key];
+    const W nw{ts, jadd(ts, cfg.size)};  // EventTimeSessionWindows.assignWindows
+    const W actual = add_window(key, mapping, nw);
+    if (is_window_late(actual)) {
+      mapping.erase(actual);  // MergingWindowSet.retireWindow
+    } else {
+      const KW lkw{key, mapping.at(actual)}, akw{key, actual};
+      lists[lkw].push_back(Elem{ts, val, ordinal});
+      bool fire = false;
+      if (actual.max_ts() <= wm)  // EventTimeTrigger.onElement
+        fire = true;
+      else
+        register_timer(actual.max_ts(), akw);
+      if (fire) emit_contents(akw, lkw);
+      if (fire && cfg.purging) lists.erase(lkw);
+      register_cleanup_timer(akw);
+      if (mapping.empty()) msets.erase(key);
+      return;
+    }
+    if (mapping.empty()) msets.erase(key);
+    if (is_element_late(ts)) {
+      if (cfg.side_output) {
+        side_key.push_back(key);
+        side_ts.push_back(ts);
+        side_val.push_back(val);
+        side_epoch.push_back(epoch);
+      } else {
+        late_dropped++;
+      }
+    }
   }
 
   // EvictingWindowOperator.processElement, non-merging branch (:186-222) / WindowOperator.java:379-407
   std::vector<W> wbuf;
   void process_element(int64_t key, int64_t ts, int64_t val) {
     ordinal++;
+    if (merging()) {
+      process_merging(key, ts, val);
+      return;
+    }
     assign(ts, wbuf);
     bool skipped = true;
     for (const W& w : wbuf) {
@@ -238,6 +376,25 @@ struct ListOracle {
   // EvictingWindowOperator.onEventTime (:241-286)
   void on_event_time(const Timer& t) {
     const KW& kw = t.kw;
+    if (merging()) {  // EvictingWindowOperator.onEventTime (:241-286) with the window's state window
+      auto ms = msets.find(kw.key);
+      if (ms == msets.end()) return;
+      auto it = ms->second.find(kw.w);
+      if (it == ms->second.end()) return;  // (a timer of a window no longer in flight)
+      const KW lkw{kw.key, it->second};
+      if (lists.count(lkw)) {
+        const bool fire = t.ts == kw.w.max_ts();
+        if (fire) emit_contents(kw, lkw);
+        if (fire && cfg.purging) lists.erase(lkw);
+      }
+      if (t.ts == cleanup_time(kw.w)) {  // clearAllState: contents, trigger timer, retireWindow
+        lists.erase(lkw);
+        timer_set.erase(Timer{kw.w.max_ts(), kw});
+        ms->second.erase(kw.w);
+        if (ms->second.empty()) msets.erase(ms);
+      }
+      return;
+    }
     if (lists.count(kw)) {
       const bool fire = cfg.trigger == OR_TRIG_EVENT_TIME && t.ts == kw.w.max_ts();  // EventTimeTrigger.onEventTime
       if (fire) emit_contents(kw);
@@ -269,7 +426,10 @@ struct ListOracle {
 extern "C" {
 
 void* oracle_list_create(const oracle_list_cfg* cfg) {
-  if (cfg->assigner != OR_GLOBAL && cfg->assigner != OR_TUMBLING && cfg->assigner != OR_SLIDING) return nullptr;
+  if (cfg->assigner != OR_GLOBAL && cfg->assigner != OR_TUMBLING && cfg->assigner != OR_SLIDING &&
+      cfg->assigner != OR_SESSION)
+    return nullptr;
+  if (cfg->assigner == OR_SESSION && cfg->trigger != OR_TRIG_EVENT_TIME) return nullptr;  // (EventTimeTrigger only)
   if (cfg->assigner != OR_GLOBAL && cfg->size <= 0) return nullptr;
   if (cfg->assigner == OR_SLIDING && cfg->slide <= 0) return nullptr;
   if (cfg->trigger == OR_TRIG_COUNT && cfg->trigger_count <= 0) return nullptr;

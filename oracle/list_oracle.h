@@ -6,7 +6,12 @@
  *
  * Restates, element by element (paths relative to /root/reference/flink-streaming-java/src/main/java/
  * org/apache/flink/streaming/):
- *   runtime/operators/windowing/EvictingWindowOperator.java:102-239   processElement (non-merging assigners)
+ *   runtime/operators/windowing/EvictingWindowOperator.java:102-239   processElement (non-merging assigners, and the
+ *                                                                       merging branch :110-170 for session windows:
+ *                                                                       MergingWindowSet.java:150-225, the merged lists
+ *                                                                       in mergeNamespaces order: the state window's
+ *                                                                       list, then the others' in HashSet order,
+ *                                                                       AbstractHeapMergingState.java:67-93)
  *   runtime/operators/windowing/EvictingWindowOperator.java:241-286   onEventTime
  *   runtime/operators/windowing/EvictingWindowOperator.java:334-366   emitWindowContents (evictBefore, the
  *                                                                       function, evictAfter, the list re-stored)
@@ -40,7 +45,7 @@ enum { OR_TRIG_EVENT_TIME = 0, OR_TRIG_COUNT = 1 };
 enum { OR_EVICT_NONE = 0, OR_EVICT_COUNT = 1, OR_EVICT_TIME = 2, OR_EVICT_DELTA = 3 };
 
 typedef struct {
-  int32_t assigner;        /* OR_TUMBLING / OR_SLIDING / OR_GLOBAL */
+  int32_t assigner;        /* OR_TUMBLING / OR_SLIDING / OR_GLOBAL / OR_SESSION (size = the gap; EventTimeTrigger) */
   int32_t value_type;      /* OR_VAL_* */
   int64_t size, slide, offset, lateness;
   int32_t trigger;         /* OR_TRIG_* */

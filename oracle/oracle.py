@@ -23,7 +23,8 @@ class OracleCfg(ctypes.Structure):
                 ("slide", ctypes.c_int64), ("offset", ctypes.c_int64), ("gap", ctypes.c_int64),
                 ("lateness", ctypes.c_int64), ("purging", ctypes.c_int32), ("side_output", ctypes.c_int32),
                 ("aggregate", ctypes.c_int32), ("hll_p", ctypes.c_int32), ("td_delta", ctypes.c_int32),
-                ("td_pad", ctypes.c_int32), ("td_q", ctypes.c_double * 3)]
+                ("td_pad", ctypes.c_int32), ("td_q", ctypes.c_double * 3), ("row_nc", ctypes.c_int32),
+                ("row_ns", ctypes.c_int32), ("row_type", ctypes.c_int32 * 8), ("row_spec", ctypes.c_int32 * 16)]
 
 
 ROW_DTYPE = np.dtype([("key", "<i8"), ("start", "<i8"), ("end", "<i8"), ("count", "<i8"), ("sum", "<i8"),
@@ -84,6 +85,9 @@ def lib():
         L.oracle_count_get_rows.argtypes = [P, P]
         L.oracle_row_digest.restype = ctypes.c_int64
         L.oracle_row_digest.argtypes = [P, ctypes.c_int64, P, P, ctypes.c_int64]
+        L.oracle_process_rows.argtypes = [P, I64P, I64P, I64P, P, ctypes.c_int64]
+        L.oracle_row_results.restype = ctypes.c_int32
+        L.oracle_row_results.argtypes = [P, ctypes.c_int64, I64P, ctypes.POINTER(ctypes.c_uint32)]
         _lib = L
     return _lib
 
@@ -92,11 +96,12 @@ def _i64p(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
 
 
-AGG_COUNT_SUM_MIN_MAX, AGG_HLL, AGG_FIRST, AGG_MINBY, AGG_MAXBY, AGG_FIRST_MAX, AGG_TDIGEST = 0, 1, 2, 3, 4, 5, 6
+AGG_COUNT_SUM_MIN_MAX, AGG_HLL, AGG_FIRST, AGG_MINBY, AGG_MAXBY, AGG_FIRST_MAX, AGG_TDIGEST, AGG_ROW = range(8)
+ROW_FNS = {"count_star": 0, "count": 1, "sum": 2, "min": 3, "max": 4, "avg": 5}
 
 
 def make_cfg(assigner="tumbling", size=0, slide=0, offset=0, gap=0, lateness=0, purging=False, side_output=False,
-             value_type="i64", hll_p=0, first=False, by=None, tdigest=0, quantiles=(0.5, 0.95, 0.99)):
+             value_type="i64", hll_p=0, first=False, by=None, tdigest=0, quantiles=(0.5, 0.95, 0.99), row=None):
     """hll_p > 0 selects the HyperLogLog AggregateFunction with 2^hll_p registers; first=True the
     first-element reduce of sum(pos)/min(pos) (max = arrival ordinal of the window's first element;
     window_oracle.h); tdigest = delta > 0 the t-digest of an f64 value column with rows carrying
@@ -105,8 +110,17 @@ def make_cfg(assigner="tumbling", size=0, slide=0, offset=0, gap=0, lateness=0, 
            else {"min": AGG_MINBY, "max": AGG_MAXBY}[by] if by else AGG_COUNT_SUM_MIN_MAX)
     if tdigest:
         value_type = "f64"
-    return OracleCfg(_ASSIGNERS[assigner], _VALTYPES[value_type], size, slide, offset, gap, lateness, int(purging),
-                     int(side_output), agg, int(hll_p), int(tdigest), 0, (ctypes.c_double * 3)(*quantiles))
+    c = OracleCfg(_ASSIGNERS[assigner], _VALTYPES[value_type], size, slide, offset, gap, lateness, int(purging),
+                  int(side_output), agg, int(hll_p), int(tdigest), 0, (ctypes.c_double * 3)(*quantiles))
+    if row is not None:  # OR_AGG_ROW: row = (column types, [(fn, column), ...]) (window_oracle.h)
+        types, specs = row
+        c.aggregate = AGG_ROW
+        c.row_nc, c.row_ns = len(types), len(specs)
+        for j, t in enumerate(types):
+            c.row_type[j] = _VALTYPES[t]
+        for q, (fn, col) in enumerate(specs):
+            c.row_spec[q] = (ROW_FNS[fn] << 8) | col
+    return c
 
 
 class OracleError(RuntimeError):
@@ -155,6 +169,29 @@ class WindowOperatorOracle:
 
     def clear_rows(self):
         lib().oracle_clear_rows(self._h)
+
+    def process_rows(self, keys, ts, cols, nulls=None):
+        """OR_AGG_ROW: cols = [column j values] (i64, or f64 viewed as bits), nulls = uint8 mask per record."""
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        mat = np.ascontiguousarray(np.stack([np.asarray(c).view(np.int64) if np.asarray(c).dtype == np.float64
+                                             else np.asarray(c, dtype=np.int64) for c in cols]))
+        nm = None if nulls is None else np.ascontiguousarray(nulls, dtype=np.uint8)
+        rc = lib().oracle_process_rows(self._h, _i64p(keys), _i64p(ts), _i64p(mat),
+                                       None if nm is None else nm.ctypes.data, len(keys))
+        if rc != 0:
+            raise OracleError(rc)
+
+    def row_results(self):
+        """OR_AGG_ROW: (values int64[rows, nspec], null mask uint32[rows]) of every emitted row, in row order."""
+        n, ns = lib().oracle_num_rows(self._h), self.cfg.row_ns
+        vals = np.zeros((n, ns), dtype=np.int64)
+        nm = np.zeros(n, dtype=np.uint32)
+        for r in range(n):
+            m = ctypes.c_uint32()
+            lib().oracle_row_results(self._h, r, vals[r].ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), ctypes.byref(m))
+            nm[r] = m.value
+        return vals, nm
 
     def digest(self, row):
         """t-digest centroids (sum f64[], weight i64[]) of emitted row `row`."""
@@ -218,7 +255,7 @@ class CountWindowOracle:
 # ---- f4: window-contents (ListState) operators (list_oracle.h) -----------------------------------------
 LIST_TRIGGERS = {"event_time": 0, "count": 1}
 LIST_EVICTORS = {"none": 0, "count": 1, "time": 2, "delta": 3}
-_LIST_ASSIGNERS = {"tumbling": TUMBLING, "sliding": SLIDING, "global": 3}
+_LIST_ASSIGNERS = {"tumbling": TUMBLING, "sliding": SLIDING, "global": 3, "session": SESSION}
 
 
 class OracleListCfg(ctypes.Structure):
@@ -257,7 +294,9 @@ def _list_lib():
 
 def make_list_cfg(assigner="tumbling", size=0, slide=0, offset=0, lateness=0, trigger="event_time", trigger_count=0,
                   purging=False, evictor="none", evict_after=False, evict_arg=0, threshold=0.0, side_output=False,
-                  value_type="i64"):
+                  value_type="i64", gap=0):
+    if assigner == "session":  # (list_oracle.h: the gap travels in `size`)
+        size = gap
     return OracleListCfg(_LIST_ASSIGNERS[assigner], _VALTYPES[value_type], size, slide, offset, lateness,
                          LIST_TRIGGERS[trigger], int(purging), trigger_count, LIST_EVICTORS[evictor], int(evict_after),
                          evict_arg, float(threshold), int(side_output), 0)

@@ -100,6 +100,16 @@ struct Acc {
   std::vector<int64_t> td_w;
   std::vector<int64_t> td_buf;     // values added since the last compression (f64 bits)
   bool td_merged = false;          // centroids of merged digests joined since the last compression
+  // OR_AGG_ROW: per value column, the accumulators of the Table aggregates over it (window_oracle.h)
+  struct RowCol {
+    int64_t nn = 0;        // non-null values (CountAggFunction / the Sum, Min, Max accumulators' f1 flag)
+    __int128 isum = 0;     // exact integral sum (BigIntegralAvgAccumulator; its low bits are the wrapped sums)
+    double dsum = 0.0;     // Double sum (SumAggFunction[Double], FloatingAvgAccumulator over doubleValue())
+    double fsum = 0.0;     // Float sum, rounded to float after every addition (SumAggFunction[Float])
+    int64_t imn = 0, imx = 0;
+    double dmn = 0.0, dmx = 0.0;
+  };
+  std::vector<RowCol> row;
 };
 
 // ---------------------------------------------------------------- t-digest (window_oracle.h OR_AGG_TDIGEST)
@@ -422,6 +432,11 @@ class WindowOperatorOracle {
       a.cnt += 1;
       return;
     }
+    if (cfg.aggregate == OR_AGG_ROW) {  // v: the record's index in the batch of oracle_process_rows
+      row_add(a, v);
+      a.cnt += 1;
+      return;
+    }
     if (cfg.aggregate == OR_AGG_TDIGEST) a.td_buf.push_back(v);  // compressed at the end of the batch
     if (is_float()) {
       double d = bitsd(v);
@@ -444,6 +459,100 @@ class WindowOperatorOracle {
     }
     a.cnt += 1;
   }
+  // ------------------------------------------------ OR_AGG_ROW (Table group-window aggregates, window_oracle.h)
+  const int64_t* row_cols = nullptr;  // the batch being processed: column j of record i at row_cols[j * row_n + i]
+  const uint8_t* row_nulls = nullptr;
+  int64_t row_n = 0;
+  std::vector<std::vector<int64_t>> row_res;  // per emitted row: its aggregates, then the null mask
+  bool row_float(int j) const { return cfg.row_type[j] == OR_VAL_F64 || cfg.row_type[j] == OR_VAL_F32; }
+  // accumulate(acc, value) of every aggregate over each non-null column (the Table functions skip nulls)
+  void row_add(Acc& a, int64_t i) const {
+    if (a.row.empty()) a.row.resize((size_t)cfg.row_nc);
+    const uint8_t nm = row_nulls ? row_nulls[i] : 0;
+    for (int j = 0; j < cfg.row_nc; j++) {
+      if ((nm >> j) & 1) continue;
+      const int64_t x = row_cols[(int64_t)j * row_n + i];
+      Acc::RowCol& c = a.row[(size_t)j];
+      if (row_float(j)) {
+        const double d = bitsd(x);
+        if (c.nn == 0 || java_double_compare(d, c.dmn) < 0) c.dmn = d;  // MinAggFunction.accumulate
+        if (c.nn == 0 || java_double_compare(d, c.dmx) > 0) c.dmx = d;  // MaxAggFunction.accumulate
+        c.dsum = d + c.dsum;                                             // numeric.plus(v, acc) / acc.f0 += v
+        c.fsum = (double)((float)d + (float)c.fsum);                     // Float plus
+      } else {
+        if (c.nn == 0 || x < c.imn) c.imn = x;
+        if (c.nn == 0 || x > c.imx) c.imx = x;
+        c.isum += (__int128)x;
+      }
+      c.nn++;
+    }
+  }
+  // merge(acc, its) of every aggregate (SumAggFunction.merge: plus of the flagged sums; Min/Max: accumulate(a.f0))
+  void row_merge(Acc& r, const Acc& b) const {
+    if (b.row.empty()) return;
+    if (r.row.empty()) r.row.resize((size_t)cfg.row_nc);
+    for (int j = 0; j < cfg.row_nc; j++) {
+      Acc::RowCol& c = r.row[(size_t)j];
+      const Acc::RowCol& o = b.row[(size_t)j];
+      if (o.nn == 0) continue;
+      if (c.nn == 0) {
+        c = o;
+        continue;
+      }
+      if (row_float(j)) {
+        if (java_double_compare(o.dmn, c.dmn) < 0) c.dmn = o.dmn;
+        if (java_double_compare(o.dmx, c.dmx) > 0) c.dmx = o.dmx;
+        c.dsum = c.dsum + o.dsum;
+        c.fsum = (double)((float)c.fsum + (float)o.fsum);
+      } else {
+        c.imn = std::min(c.imn, o.imn);
+        c.imx = std::max(c.imx, o.imx);
+        c.isum += o.isum;
+      }
+      c.nn += o.nn;
+    }
+  }
+  // getValue of aggregate s (OR_ROW_* << 8 | column): the value (integers sign-extended from the type's width,
+  // floating results as f64 bits) or NULL
+  int64_t row_value(const Acc& a, int s, bool* null) const {
+    const int fn = cfg.row_spec[s] >> 8, j = cfg.row_spec[s] & 0xff;
+    *null = false;
+    if (fn == OR_ROW_COUNT_STAR) return a.cnt;
+    const Acc::RowCol c = a.row.empty() ? Acc::RowCol{} : a.row[(size_t)j];
+    if (fn == OR_ROW_COUNT) return c.nn;
+    if (c.nn == 0) {
+      *null = true;
+      return 0;
+    }
+    const int t = cfg.row_type[j];
+    auto narrow = [t](int64_t v) -> int64_t {
+      return t == OR_VAL_I32 ? (int64_t)(int32_t)v : t == OR_VAL_I16 ? (int64_t)(int16_t)v
+           : t == OR_VAL_I8 ? (int64_t)(int8_t)v : v;
+    };
+    auto fbits = [](double d) {  // (the double of a Float result)
+      int64_t b;
+      memcpy(&b, &d, 8);
+      return b;
+    };
+    switch (fn) {
+      case OR_ROW_SUM:
+        if (t == OR_VAL_F64) return fbits(c.dsum);
+        if (t == OR_VAL_F32) return fbits(c.fsum);
+        return narrow((int64_t)(uint64_t)(unsigned __int128)c.isum);
+      case OR_ROW_MIN:
+        return row_float(j) ? fbits(c.dmn) : c.imn;
+      case OR_ROW_MAX:
+        return row_float(j) ? fbits(c.dmx) : c.imx;
+      default: {  // OR_ROW_AVG
+        if (t == OR_VAL_F64) return fbits(c.dsum / (double)c.nn);
+        if (t == OR_VAL_F32) return fbits((double)(float)(c.dsum / (double)c.nn));
+        if (t == OR_VAL_I64) return (int64_t)(c.isum / (__int128)c.nn);  // BigInteger.divide: truncating
+        const int64_t lsum = (int64_t)(uint64_t)(unsigned __int128)c.isum;  // the Long accumulator (wraps)
+        return narrow(lsum / c.nn);                                         // Java long division, then toInt ...
+      }
+    }
+  }
+
   // AggregateFunction.merge(a, b)
   Acc acc_merge(const Acc& a, const Acc& b) const {
     if (a.cnt == 0) return b;
@@ -469,6 +578,10 @@ class WindowOperatorOracle {
       return r;
     }
     if (cfg.aggregate == OR_AGG_TDIGEST) td_union(r, b);
+    if (cfg.aggregate == OR_AGG_ROW) {
+      row_merge(r, b);
+      return r;
+    }
     if (is_float()) {
       r.dsum = cfg.value_type == OR_VAL_F32 ? (double)((float)a.dsum + (float)b.dsum) : a.dsum + b.dsum;
       r.dmn = java_double_compare(b.dmn, a.dmn) < 0 ? b.dmn : a.dmn;
@@ -514,6 +627,19 @@ class WindowOperatorOracle {
     r.end = w.end;
     r.count = a.cnt;
     row_digest.emplace_back();
+    if (cfg.aggregate == OR_AGG_ROW) {
+      std::vector<int64_t> res((size_t)cfg.row_ns + 1, 0);
+      for (int q = 0; q < cfg.row_ns; q++) {
+        bool nl;
+        res[(size_t)q] = row_value(a, q, &nl);
+        if (nl) res[(size_t)cfg.row_ns] |= (int64_t)1 << q;
+      }
+      row_res.push_back(res);
+      r.sum = r.min = r.max = 0;
+      r.epoch = epoch;
+      rows.push_back(r);
+      return;
+    }
     if (cfg.aggregate == OR_AGG_TDIGEST) {
       if (!a_in.td_buf.empty() || a_in.td_merged) td_compress(a, td_q);  // getResult within a batch sees every value
       const double q[3] = {td_quantile(a, a.dmn, a.dmx, cfg.td_q[0]), td_quantile(a, a.dmn, a.dmx, cfg.td_q[1]),
@@ -895,6 +1021,33 @@ void oracle_get_rows(void* p, oracle_row* out) {
 void oracle_clear_rows(void* p) {
   static_cast<WindowOperatorOracle*>(p)->rows.clear();
   static_cast<WindowOperatorOracle*>(p)->row_digest.clear();
+  static_cast<WindowOperatorOracle*>(p)->row_res.clear();
+}
+int oracle_process_rows(void* p, const int64_t* key, const int64_t* ts, const int64_t* cols, const uint8_t* nulls,
+                        int64_t n) {
+  auto* op = static_cast<WindowOperatorOracle*>(p);
+  if (op->cfg.aggregate != OR_AGG_ROW) return OR_ERR_ILLEGAL_STATE;
+  op->row_cols = cols;
+  op->row_nulls = nulls;
+  op->row_n = n;
+  int rc = OR_OK;
+  try {
+    for (int64_t i = 0; i < n; i++) op->process_element(key[i], ts[i], i);
+  } catch (const OpError& e) {
+    rc = e.code;
+  }
+  op->row_cols = nullptr;
+  op->row_nulls = nullptr;
+  op->end_batch();
+  return rc;
+}
+int32_t oracle_row_results(void* p, int64_t row, int64_t* vals, uint32_t* null_mask) {
+  auto* op = static_cast<WindowOperatorOracle*>(p);
+  if (row < 0 || row >= (int64_t)op->row_res.size()) return -1;
+  const auto& r = op->row_res[(size_t)row];
+  for (int q = 0; q < op->cfg.row_ns; q++) vals[q] = r[(size_t)q];
+  *null_mask = (uint32_t)r[(size_t)op->cfg.row_ns];
+  return op->cfg.row_ns;
 }
 int64_t oracle_row_digest(void* p, int64_t row, double* sum, int64_t* weight, int64_t cap) {
   auto* op = static_cast<WindowOperatorOracle*>(p);

@@ -61,6 +61,10 @@ typedef struct {
   int32_t td_delta;      /* t-digest compression delta (even), OR_AGG_TDIGEST only */
   int32_t td_pad;
   double td_q[3];        /* t-digest quantiles reported in a row's sum / min / max */
+  int32_t row_nc;        /* OR_AGG_ROW: value columns per record (1 .. 8) */
+  int32_t row_ns;        /* OR_AGG_ROW: output aggregates (1 .. 16) */
+  int32_t row_type[8];   /* OR_AGG_ROW: OR_VAL_* of each column */
+  int32_t row_spec[16];  /* OR_AGG_ROW: OR_ROW_* << 8 | column */
 } oracle_cfg;
 
 /* The user AggregateFunctions of SURVEY.md §8d C5.  OR_AGG_HLL is a HyperLogLog distinct count
@@ -95,9 +99,27 @@ typedef struct {
  *   getResult: count = W; sum / min / max = quantile(td_q[0..2]) as f64 bits, where quantile(q) is the
  *   piecewise-linear interpolation at x = q*W through (0, min), (cum_{i-1} + w_i/2, mean_i) ..., (W, max).
  * The arithmetic is IEEE-754 double without fused multiply-add, so the GPU's digests are bit-exact. */
+/* OR_AGG_ROW: the Table API's group-window aggregation (flink-libraries/flink-table, DataStreamGroupWindowAggregate
+ * .scala:197-294): ONE accumulator Row per (key, window) holding several built-in aggregates over nullable value
+ * columns (the generated AggregateFunction of AggregateUtil.createDataStreamAggregateFunction); each record carries
+ * row_nc columns and a null mask.  The aggregates (.../table/functions/aggfunctions/):
+ *   OR_ROW_COUNT_STAR  COUNT(*) / COUNT(1): every record (CountAggFunction.accumulate(acc), :41-43)
+ *   OR_ROW_COUNT       COUNT(col): the non-null values (CountAggFunction.scala:51-55); never null
+ *   OR_ROW_SUM         SUM(col): null when the column had no non-null value; Long / Int / Short / Byte sums wrap to
+ *                      their width, Float adds in float, Double in double (SumAggFunction.scala:28-100, Scala Numeric)
+ *   OR_ROW_MIN/MAX     MIN / MAX(col): null when empty; Double / Float by Ordering.Double / Float (java.lang compare)
+ *                      (MinAggFunction.scala, MaxAggFunction.scala:28-100)
+ *   OR_ROW_AVG         AVG(col): null when empty; Long: the exact (BigInteger) sum / count truncated (BigIntegral-
+ *                      AvgAggFunction, AvgAggFunction.scala:130-185); Int / Short / Byte: the Long sum / count (Java
+ *                      long division) narrowed to the type (IntegralAvgAggFunction, :39-120); Double / Float: the
+ *                      double sum of the values / count (FloatingAvgAggFunction, :187-250; Float narrowed)
+ * merge (sessions, AbstractHeapMergingState.mergeNamespaces) = each function's merge.  A row's count is COUNT(*);
+ * its results come from oracle_row_results: one int64 per aggregate (integers sign-extended, floating results as
+ * f64 bits, a Float result as the double of the float) and a null mask (bit s = aggregate s is NULL). */
+enum { OR_ROW_COUNT_STAR = 0, OR_ROW_COUNT = 1, OR_ROW_SUM = 2, OR_ROW_MIN = 3, OR_ROW_MAX = 4, OR_ROW_AVG = 5 };
 enum { OR_AGG_COUNT_SUM_MIN_MAX = 0, OR_AGG_HLL = 1, OR_AGG_FIRST = 2, OR_AGG_MINBY = 3, OR_AGG_MAXBY = 4,
        OR_AGG_FIRST_MAX = 5 /* max(pos): as OR_AGG_FIRST with min = the field's maximum */,
-       OR_AGG_TDIGEST = 6 };
+       OR_AGG_TDIGEST = 6, OR_AGG_ROW = 7 };
 
 /* One fired row.  sum/min/max hold i64 values (I64/I32) or f64 bit patterns (F64).
  * epoch = number of watermarks fully processed before the row was emitted, so
@@ -116,6 +138,12 @@ void    oracle_destroy(void* op);
 /* process n elements in order; val holds i64 values or f64 bits */
 int     oracle_process(void* op, const int64_t* key, const int64_t* ts, const int64_t* val, int64_t n);
 int     oracle_watermark(void* op, int64_t wm);
+/* OR_AGG_ROW: n records with row_nc value columns (cols + j * n: column j; i64 values or f64 bits) and a null mask
+ * per record (bit j = column j is NULL; nulls may be NULL = none) */
+int     oracle_process_rows(void* op, const int64_t* key, const int64_t* ts, const int64_t* cols, const uint8_t* nulls,
+                            int64_t n);
+/* OR_AGG_ROW: the aggregates of emitted row `row` (row_ns values) and their null mask; returns row_ns, -1 = no row */
+int32_t oracle_row_results(void* op, int64_t row, int64_t* vals, uint32_t* null_mask);
 int64_t oracle_num_rows(void* op);
 /* a14 — count windows (SURVEY §8a, config C1 CPU reference): GlobalWindows + CountTrigger.of(slide) +
  * CountEvictor.of(size, evict_after) over a ListState of elements, the window function reducing the

@@ -13,6 +13,8 @@ Paths are relative to /root/reference.  Abbreviations:
   SWE = flink-examples/flink-examples-streaming/src/main/java/org/apache/flink/streaming/examples/windowing/SessionWindowing.java
   EWO = flink-streaming-java/src/test/java/org/apache/flink/streaming/runtime/operators/windowing/EvictingWindowOperatorTest.java
   EWC = flink-tests/src/test/java/org/apache/flink/test/checkpointing/AbstractEventTimeWindowCheckpointingITCase.java
+  SIT = flink-libraries/flink-table/src/test/scala/org/apache/flink/table/runtime/stream/sql/SqlITCase.scala
+  GWT = flink-libraries/flink-table/src/test/scala/org/apache/flink/table/runtime/stream/table/GroupWindowITCase.scala
 
 Operator cases use the vocabulary of the harness: ("e", key, value, timestamp) is
 processElement, ("w", t) is processWatermark.  Expected rows carry the output epoch (the
@@ -244,6 +246,17 @@ LIST_WINDOWS = [
 # CASES "sliding_3s_1s_reduce_sum" (testSlidingEventTimeWindowsApply, WOT:213-238) and "tumbling_3s_reduce_sum"
 # (testTumblingEventTimeWindowsApply, WOT:339-364) produce the same rows through RichSumReducer.
 LIST_APPLY_CASES = {"sliding_3s_1s_reduce_sum": "WOT:213-238", "tumbling_3s_reduce_sum": "WOT:339-364"}
+# f4 merging: session windows over ListState (WindowedStream.apply with EventTimeSessionWindows).  testSessionWindows
+# (WOT:368-442) is that operator itself (ListStateDescriptor + SessionWindowFunction: key-sum over the contents); the
+# lateness / purging / side-output session sequences (WOT:1715-2266) are written against a ReducingState sum, and
+# WindowOperator's merging branch (WindowOperator.java:300-377) does not depend on the state kind, so a sum over the
+# list's contents gives the same rows.
+LIST_SESSION_CASES = {"session_3s_sum": "WOT:368-442", "session_zero_lateness_purging_side_output": "WOT:1715-1804",
+                      "session_zero_lateness_side_output": "WOT:1807-1890",
+                      "session_lateness_10_purging": "WOT:1893-1977",
+                      "session_lateness_10_accumulating": "WOT:1980-2081",
+                      "session_huge_lateness_purging": "WOT:2084-2173",
+                      "session_huge_lateness_accumulating": "WOT:2176-2266"}
 
 KEY_GROUPS = {
     "source": "CEP:71-82,170-215 (Integer keys: hashCode == value)",
@@ -294,10 +307,74 @@ CLOSED_FORM = {"source": "EWC:571-629,659-740,865-877", "num_keys": 20, "num_ele
                "window_size": 100, "window_slide": 100}
 
 
+# f3: Table API group windows (DataStreamGroupWindowAggregate.scala:197-294) -- the built-in aggregates of the
+# reference's own ITCases, with their inputs (rowtime = the first tuple field, a punctuated watermark of ts - offset
+# after every element: TimestampAndWatermarkWithOffset, SIT:645-659 / GWT:449-463; Long.MAX_VALUE at the end of the
+# input).  "cols" are the aggregated columns (null = SQL NULL), "specs" the select list's built-in aggregates as
+# [function, column index]; "expected" rows are [key, window start, window end, [values (null = NULL)]] -- the
+# ITCase's expected strings with the user-defined aggregates (WeightedAvg, CountDistinct) left out and the keys as
+# strings (None = the null grouping key).  User AggregateFunctions of the tests (countFun = the test's
+# CountAggFunction: the non-null count of its argument) are the built-in COUNT(col).
+_GW_DATA = [[1, [1], "Hi"], [2, [2], "Hello"], [4, [2], "Hello"], [8, [3], "Hello world"], [16, [3], "Hello world"]]
+_GW_DATA2 = [[1, [1], "Hi"], [2, [2], "Hallo"], [3, [2], "Hello"], [4, [5], "Hello"], [7, [3], "Hello"],
+             [8, [3], "Hello world"], [16, [4], "Hello world"], [32, [4], None]]
+
+
+def _slide_rows(rows):
+    return [[k, s, e, [c]] for k, c, s, e in rows]
+
+
+TABLE_GROUP_WINDOWS = [
+    {"name": "sql_tumble_count_star_count_col", "source": "SIT:44-82 (testRowTimeTumbleWindow)",
+     "assigner": "tumbling", "size": 5000, "offset": 0, "types": ["i64"],
+     "specs": [["count_star", 0], ["count_star", 0], ["count", 0]],
+     "input": [[1000, [1], "Hello"], [2000, [2], "Hello"], [3000, [None], "Hello"], [4000, [4], "Hello"],
+               [5000, [None], "Hello"], [6000, [6], "Hello"], [7000, [7], "Hello World"], [8000, [8], "Hello World"],
+               [20000, [20], "Hello World"]],
+     "expected": [["Hello World", 5000, 10000, [2, 2, 2]], ["Hello World", 20000, 25000, [1, 1, 1]],
+                  ["Hello", 0, 5000, [4, 4, 3]], ["Hello", 5000, 10000, [2, 2, 1]]]},
+    {"name": "table_tumble_builtins", "source": "GWT:50-55,169-201 (testEventTimeTumblingWindow)",
+     "assigner": "tumbling", "size": 5, "offset": 0, "types": ["i32"],
+     "specs": [["count", 0], ["avg", 0], ["min", 0], ["max", 0], ["sum", 0]],
+     "input": _GW_DATA,
+     "expected": [["Hello world", 5, 10, [1, 3, 3, 3, 3]], ["Hello world", 15, 20, [1, 3, 3, 3, 3]],
+                  ["Hello", 0, 5, [2, 2, 2, 2, 4]], ["Hi", 0, 5, [1, 1, 1, 1, 1]]]},
+    {"name": "table_session_merge", "source": "GWT:97-138 (testEventTimeSessionGroupWindowOverTime)",
+     "assigner": "session", "gap": 5, "offset": 10, "types": ["i32"], "specs": [["count", 0], ["avg", 0]],
+     "input": [[1, [1], "Hello"], [2, [2], "Hello"], [8, [8], "Hello"], [9, [9], "Hello World"], [4, [4], "Hello"],
+               [16, [16], "Hello"]],
+     "expected": [["Hello World", 9, 14, [1, 9]], ["Hello", 16, 21, [1, 16]], ["Hello", 1, 13, [4, 3]]]},
+    {"name": "table_slide_all_overlapping", "source": "GWT:57-65,240-277 (testAllEventTimeSlidingGroupWindowOverTime)",
+     "assigner": "sliding", "size": 5, "slide": 2, "offset": 0, "types": ["i32"], "specs": [["count", 0]],
+     "input": [[t, c, "all"] for t, c, _ in _GW_DATA2],
+     "expected": _slide_rows([["all", 1, 8, 13], ["all", 1, 12, 17], ["all", 1, 14, 19], ["all", 1, 16, 21],
+                              ["all", 2, -2, 3], ["all", 2, 6, 11], ["all", 3, 2, 7], ["all", 3, 4, 9],
+                              ["all", 4, 0, 5], ["all", 1, 28, 33], ["all", 1, 30, 35], ["all", 1, 32, 37]])},
+    {"name": "table_slide_overlapping_full_pane", "source": "GWT:57-65,279-317", "assigner": "sliding",
+     "size": 10, "slide": 5, "offset": 0, "types": ["i32"], "specs": [["count", 0]], "input": _GW_DATA2,
+     "expected": _slide_rows([["Hallo", 1, -5, 5], ["Hallo", 1, 0, 10], ["Hello world", 1, 0, 10],
+                              ["Hello world", 1, 5, 15], ["Hello world", 1, 10, 20], ["Hello world", 1, 15, 25],
+                              ["Hello", 1, 5, 15], ["Hello", 2, -5, 5], ["Hello", 3, 0, 10], ["Hi", 1, -5, 5],
+                              ["Hi", 1, 0, 10], [None, 1, 25, 35], [None, 1, 30, 40]])},
+    {"name": "table_slide_overlapping_split_pane", "source": "GWT:57-65,319-354", "assigner": "sliding",
+     "size": 5, "slide": 4, "offset": 0, "types": ["i32"], "specs": [["count", 0]], "input": _GW_DATA2,
+     "expected": _slide_rows([["Hallo", 1, 0, 5], ["Hello world", 1, 4, 9], ["Hello world", 1, 8, 13],
+                              ["Hello world", 1, 12, 17], ["Hello world", 1, 16, 21], ["Hello", 2, 0, 5],
+                              ["Hello", 2, 4, 9], ["Hi", 1, 0, 5], [None, 1, 28, 33], [None, 1, 32, 37]])},
+    {"name": "table_slide_non_overlapping_full_pane", "source": "GWT:57-65,356-385", "assigner": "sliding",
+     "size": 5, "slide": 10, "offset": 0, "types": ["i32"], "specs": [["count", 0]], "input": _GW_DATA2,
+     "expected": _slide_rows([["Hallo", 1, 0, 5], ["Hello", 2, 0, 5], ["Hi", 1, 0, 5], [None, 1, 30, 35]])},
+    {"name": "table_slide_non_overlapping_split_pane", "source": "GWT:57-65,387-415", "assigner": "sliding",
+     "size": 3, "slide": 10, "offset": 0, "types": ["i32"], "specs": [["count", 0]], "input": _GW_DATA2,
+     "expected": _slide_rows([["Hallo", 1, 0, 3], ["Hi", 1, 0, 3], [None, 1, 30, 33]])},
+]
+
+
 def main():
     out = {"keys": KEYS, "operator_cases": CASES, "session_example": SESSION_EXAMPLE, "count_windows": COUNT_WINDOWS,
            "list_windows": LIST_WINDOWS, "list_apply_cases": LIST_APPLY_CASES, "key_groups": KEY_GROUPS,
-           "window_start": WINDOW_START, "assigners": ASSIGNERS, "closed_form": CLOSED_FORM}
+           "window_start": WINDOW_START, "assigners": ASSIGNERS, "closed_form": CLOSED_FORM,
+           "table_group_windows": TABLE_GROUP_WINDOWS, "list_session_cases": LIST_SESSION_CASES}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_kats.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)

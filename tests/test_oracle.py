@@ -258,3 +258,59 @@ def test_list_lateness_refires_contents():
     assert op.num_state_entries == 0 and op.num_timers == 0
     op.process(np.array([1]), np.array([5]), np.array([9]))
     assert op.late_dropped == 1
+
+
+@pytest.mark.parametrize("name", sorted(KATS["list_session_cases"]))
+def test_list_session_kats(name):
+    # f4 merging: session windows over ListState (WindowOperator / EvictingWindowOperator merging branch) against
+    # WindowOperatorTest's session sequences: the rows, and every firing's contents summing to its row
+    case = next(c for c in KATS["operator_cases"] if c["name"] == name)
+    c = case["cfg"]
+    op = replay(case, KEYMAP, lambda _: orc.ListWindowOracle(assigner="session", gap=c["gap"], lateness=c["lateness"],
+                                                             purging=c["purging"], side_output=c["side_output"],
+                                                             value_type="i32"),
+                flush_elements=False)
+    side = op.side_rows()
+    side_rows = [dict(key=k, ts=t, val=v, epoch=e) for k, t, v, e in zip(*side)]
+    got, got_side = row_counters(op.rows(), side_rows, case, with_window=True)
+    exp, exp_side = expected_counters(case, KEYMAP, with_window=True)
+    assert got == exp
+    assert got_side == exp_side
+    for r, el in op.contents():
+        assert len(el) == r["count"] and el["val"].sum() == r["sum"]
+
+
+def _java_hashset_order(wins):
+    """java.util.HashSet iteration order of TimeWindows added in order (an independent restatement for the test:
+    TimeWindow.hashCode = longToIntWithBitMixing(start + end), bucket (h ^ h >>> 16) & 15)."""
+    def mix(x):
+        M = (1 << 64) - 1
+        x &= M
+        x = ((x ^ (x >> 30)) * 0xbf58476d1ce4e5b9) & M
+        x = ((x ^ (x >> 27)) * 0x94d049bb133111eb) & M
+        x ^= x >> 31
+        return x & 0xffffffff
+    b = [(mix(s + e) ^ (mix(s + e) >> 16)) & 15 for s, e in wins]
+    return [w for _, _, w in sorted((b[i], i, w) for i, w in enumerate(wins))]
+
+
+@pytest.mark.parametrize("first", [0, 1])
+def test_list_session_bridge_order(first):
+    # a bridging element merges two sessions: the merged list is the state window of the first merged window in
+    # HashSet order followed by the other's list (MergingWindowSet.addWindow, MergingWindowSet.java:150-225;
+    # HeapListState.mergeState = addAll), then the element; pick sessions so either one comes first
+    gap = 10
+    for a0 in range(0, 400):
+        # the in-flight windows when the bridge arrives: A = [a0, a0 + gap + 1), B = [a0 + 2 gap, a0 + 3 gap + 1)
+        A, B = (a0, a0 + gap + 1), (a0 + 2 * gap, a0 + 3 * gap + 1)
+        order = _java_hashset_order([A, B])
+        if (order[0] == A) == (first == 0):
+            break
+    op = orc.ListWindowOracle(assigner="session", gap=gap, value_type="i64")
+    op.process(np.array([1, 1, 1, 1]), np.array([A[0], B[0], A[0] + 1, B[0] + 1]), np.array([1, 2, 3, 4]))
+    op.process(np.array([1]), np.array([A[0] + gap]), np.array([5]))  # [a0 + gap, a0 + 2 gap) touches both
+    op.watermark((1 << 63) - 1)
+    (r, el), = op.contents()
+    assert (r["start"], r["end"]) == (A[0], B[1]) and r["count"] == 5
+    expect = [1, 3, 2, 4, 5] if order[0] == A else [2, 4, 1, 3, 5]
+    assert list(el["val"]) == expect
