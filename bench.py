@@ -298,8 +298,8 @@ def main():
         args.zipf = preset["zipf"]
     args.zipf = args.zipf or None
     if args.traffic is None:
-        for cand in (f"traffic_r05_{w}.json", f"traffic_r04_{w}.json", f"traffic_r03_{w}.json", f"traffic_r02_{w}.json",
-                     f"traffic_r01_{w}.json" if w != "c2" else "traffic_r01.json"):
+        for cand in (f"traffic_r06_{w}.json", f"traffic_r05_{w}.json", f"traffic_r04_{w}.json", f"traffic_r03_{w}.json",
+                     f"traffic_r02_{w}.json", f"traffic_r01_{w}.json" if w != "c2" else "traffic_r01.json"):
             args.traffic = os.path.join(ROOT, "profiles", cand)
             if os.path.exists(args.traffic):
                 break
