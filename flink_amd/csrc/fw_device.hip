@@ -3042,6 +3042,8 @@ __device__ __forceinline__ void hll_raise(const DevCfg& c, uint64_t blk, int64_t
 
 __device__ void td_late_row(const SlowCtx& x, const Entry& en, int32_t head);
 __device__ void td_late_row_session(const SlowCtx& x, const Entry& en, int32_t head);
+__device__ void td_purge(const DevCfg& c, uint32_t g, uint64_t blk);
+constexpr int32_t TD_DROPPED = -3;  // td_olink of a value purged from the push's compression (td_purge)
 // a window's chain of the push's values (t-digest under allowed lateness) is kept in Double.compare order of the
 // values: link l (element l / wpr) goes before the first link of a larger value
 __device__ __forceinline__ uint64_t td_key(int64_t bits);
@@ -3114,11 +3116,15 @@ __device__ void replay_time_windows(const SlowCtx& x, int32_t p, int64_t k, int6
     } else {
       en.meta |= FW_TIMER;  // registerEventTimeTimer(maxTimestamp)
     }
-    if (!keep && c.agg == FW_AGG_HLL) {
-      // the purged window keeps its slot and zeroed block as empty state (cnt 0: nothing fires from it, and its GC
+    if (!keep && (c.agg == FW_AGG_HLL || td)) {
+      // the purged window keeps its slot and emptied block as empty state (cnt 0: nothing fires from it, and its GC
       // timer frees the block in k_fire): this kernel pops blocks for new windows, and a push beside those pops could
-      // hand out a block before its slot on the free stack is written
-      hll_clear(c, pool_block_of(en));
+      // hand out a block before its slot on the free stack is written.  (t-digest: the push's chains and items
+      // refer to the slot, and its values so far leave the push's compression)
+      if (td)
+        td_purge(c, ((uint32_t)p << c.log_r) | (uint32_t)slot, pool_block_of(en));
+      else
+        hll_clear(c, pool_block_of(en));
       acc_clear(en);
       en.meta &= ~(int64_t)FW_TIMER;
       keep = true;
@@ -3268,7 +3274,12 @@ __device__ void replay_session(const SlowCtx& x, int32_t p, int64_t k, int64_t t
     } else {
       emit_one(c, x.out, x.st, en);
     }
-    if (c.purging) acc_clear(en);  // FIRE_AND_PURGE clears the contents; the window stays in flight
+    if (c.purging) {  // FIRE_AND_PURGE clears the contents; the window stays in flight
+      acc_clear(en);
+      if (c.agg == FW_AGG_HLL) hll_clear(c, pool_block_of(en));
+      if (c.agg == FW_AGG_TDIGEST && c.td_olast)
+        td_purge(c, ((uint32_t)p << c.log_r) | (uint32_t)actual, pool_block_of(en));
+    }
   } else {
     en.meta |= FW_TIMER;
   }
@@ -3390,6 +3401,10 @@ __global__ __launch_bounds__(FW_SLOW_THREADS) void k_slow(DevCfg c, int64_t wm, 
   }
 }
 
+// a fired row's block handed to the finish (out.mx for HyperLogLog, bit 63 of out.sum for t-digest) when the window
+// fired with FIRE_AND_PURGE and stays in flight (a session): the block is emptied after its row is read, and kept
+constexpr int64_t HLL_ZERO_KEEP = -2;
+constexpr uint64_t TD_PURGE_TAG = 1ull << 63;
 // a fired HLL row from its marked chunks' sums (lo, hi: sum_j 2^(65-p-M[j]) over them, 128 bits; zeros; touched
 // chunks): the unmarked chunks are 16 zero registers each, 2^rmax apiece (rmax <= 61: the product fits 128 bits)
 __device__ void hll_row_out(const DevCfg& c, const DevRows& out, uint64_t row, uint64_t lo, uint64_t hi, uint32_t zeros,
@@ -3419,12 +3434,14 @@ __device__ void hll_row_out(const DevCfg& c, const DevRows& out, uint64_t row, u
 // one wave per fired row: estimate from the row's register block (out.mn holds its id), then zero the
 // block and push it on the free stack.  S = sum_j 2^(65-p-M[j]) exactly, in 128 bits.  Only the chunks the
 // block's bitmap marks are read (and zeroed): every register of an unmarked chunk is zero.
-// stack_slot < 0: the window stays (FIRE without purge under allowed lateness): the block is read, not zeroed or freed
+// stack_slot < 0: the window stays (FIRE without purge under allowed lateness): the block is read, not zeroed or freed;
+// HLL_ZERO_KEEP: a session fired with FIRE_AND_PURGE stays in flight: the block is read and zeroed, not freed.
 // A block with at most 64 marked chunks (a window of few distinct items: most windows of a Zipf stream's tail keys)
 // takes two round trips: the bitmap (a word per lane), then every marked chunk at once, one per lane, from the
 // chunk ids the wave lays out in its LDS scratch `ids` (64 words); a fuller block walks its bitmap 256 chunks a pass.
 __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, int64_t stack_slot, uint32_t* ids) {
   const bool release = stack_slot >= 0;
+  const bool zero = release || stack_slot == HLL_ZERO_KEEP;
   const int lane = __lane_id();
   const int p = c.hll_p, rmax = 65 - p;
   const int64_t m = (int64_t)1 << p;
@@ -3472,7 +3489,7 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, in
             s = t;
             zeros += r == 0;
           }
-        if (release) q[j] = make_uint4(0, 0, 0, 0);
+        if (zero) q[j] = make_uint4(0, 0, 0, 0);
       }
       __builtin_amdgcn_wave_barrier();  // (ids is the wave's next row's)
       w_start = nw;                     // every marked chunk is read
@@ -3506,10 +3523,10 @@ __device__ void hll_finish(const DevCfg& c, const DevRows& out, uint64_t row, in
           s = t;
           zeros += r == 0;
         }
-      if (release) q[jj[u]] = make_uint4(0, 0, 0, 0);
+      if (zero) q[jj[u]] = make_uint4(0, 0, 0, 0);
     }
   }
-  if (release)
+  if (zero)
     for (int32_t w = lane; w < nw; w += 64) bits[w] = 0u;
   uint64_t hi = sh, lo = s;
   for (int o = 32; o > 0; o >>= 1) {
@@ -3534,8 +3551,8 @@ __device__ void hll_finish4(const DevCfg& c, const DevRows& out, uint64_t r, uin
   const uint64_t row = r + (uint64_t)g * stride;
   const bool valid = row < end;
   const int64_t ri = valid ? out.mx[row] : -1;
-  const bool release = ri >= 0;
-  const int64_t slot = release ? hl_sb + ri : -1;
+  const bool release = ri >= 0, zero = release || ri == HLL_ZERO_KEEP;
+  const int64_t slot = release ? hl_sb + ri : ri;
   const uint64_t blk = valid ? (uint64_t)out.mn[row] : 0;
   uint8_t* base = c.pool + blk * (uint64_t)c.pool_bytes;
   uint32_t* bits = reinterpret_cast<uint32_t*>(base);
@@ -3584,9 +3601,9 @@ __device__ void hll_finish4(const DevCfg& c, const DevRows& out, uint64_t r, uin
         s = t;
         zeros += rr == 0;
       }
-    if (release) q[j] = make_uint4(0, 0, 0, 0);
+    if (zero) q[j] = make_uint4(0, 0, 0, 0);
   }
-  if (small && release) {
+  if (small && zero) {
     if (gl < nw) bits[gl] = 0u;
     if (gl + 16 < nw) bits[gl + 16] = 0u;
   }
@@ -4257,6 +4274,27 @@ __device__ void td_late_emit(const SlowCtx& x, const Entry& en, const TdCent* cp
   atomicAdd(&x.st->td_cent, (unsigned long long)n);
 }
 
+// FIRE_AND_PURGE of a t-digest window in the ordered path (allowed lateness; WindowOperator.java:403-405
+// windowState.clear() after a FIRE_AND_PURGE): the state goes -- the block's centroids, those of the blocks merged into
+// it during the push (a session: their union is then empty, td_late_row_session and k_td_mbuild), and the values the
+// push added to it so far, whose items leave the push's compression (TD_DROPPED: k_td_group and k_td_relink skip them).
+// The slot and block stay as empty state (cnt 0) until the window's cleanup time.
+__device__ void td_purge(const DevCfg& c, uint32_t g, uint64_t blk) {
+  for (int32_t l = c.td_olast[g]; l >= 0;) {
+    const int32_t nx = c.td_olink[l];
+    c.td_olink[l] = TD_DROPPED;
+    l = nx;
+  }
+  c.td_olast[g] = -1;
+  TdHead* h = td_head(c, blk);
+  *h = TdHead{h->cur, 0, 0};
+  if (c.td_bhead)
+    for (int32_t b = c.td_bhead[blk]; b >= 0; b = c.td_bnext[b]) {
+      TdHead* hb = td_head(c, (uint64_t)b);
+      *hb = TdHead{hb->cur, 0, 0};
+    }
+}
+
 // a session's late firing (allowed lateness): as td_late_row, over the session's digest -- its block's centroids and
 // those of the blocks merged into it during the push (td_bhead chain: their union, as td_union, in the thread's
 // td_lateu scratch) -- compressed with the values the push added to it so far (its sorted chain from `head`, merged
@@ -4328,11 +4366,12 @@ __device__ void td_late_row(const SlowCtx& x, const Entry& en, int32_t head) {
 }
 
 // getResult of a fired row (one thread): out.sum holds the block id and above it 1 + the block's free-stack slot
-// past `stack_base` if its window goes (k_fire), out.min / out.max the min / max; returns the digest's centroid count
+// past `stack_base` if its window goes (k_fire) and TD_PURGE_TAG if it stays emptied, out.min / out.max the min /
+// max; returns the digest's centroid count
 __device__ int32_t td_finish(const DevCfg& c, const DevRows& out, uint64_t row, int64_t stack_base) {
   const uint64_t tag = (uint64_t)out.sum[row];
   const uint64_t blk = tag & 0xffffffffull;
-  const int64_t rel = (int64_t)(tag >> 32);
+  const int64_t rel = (int64_t)((tag & ~TD_PURGE_TAG) >> 32);
   const TdHead h = *td_head(c, blk);
   const TdCent* ce = td_half(c, blk, h.cur);
   const double mn = __longlong_as_double(out.mn[row]), mx = __longlong_as_double(out.mx[row]);
@@ -4351,13 +4390,10 @@ __device__ int32_t td_finish(const DevCfg& c, const DevRows& out, uint64_t row, 
   out.mn[row] = __double_as_longlong(q1);
   out.mx[row] = __double_as_longlong(q2);
   if (rel) c.pool_free[stack_base + rel - 1] = (uint32_t)blk;
+  if (tag & TD_PURGE_TAG) *td_head(c, blk) = TdHead{h.cur, 0, 0};  // FIRE_AND_PURGE: the session stays, empty
   return h.n;
 }
 
-// sort keys of every batch position: one 64-bit key (pool block of the record's digest in the top B bits, the
-// value key's high 64 - B bits below) and the value key's low B bits as the payload, so one radix sort groups a
-// digest's values and orders them up to ties in the high bits (k_td_fix orders those by the low bits). Positions
-// past the partitioned records get the block `nblk` (sorted last, skipped). binv[blk] = the digest's global slot.
 // the slot of key's in-flight session that contains [ts, ts + gap) (sessions hash the key only: one probe chain),
 // -1 if none
 __device__ __forceinline__ int32_t session_containing(const Region& r, const DevCfg& c, int64_t key, int64_t ts) {
@@ -4374,21 +4410,45 @@ __device__ __forceinline__ int32_t session_containing(const Region& r, const Dev
   }
   return -1;
 }
-constexpr int TD_CHUNK = 4096;
-__global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restrict__ part, const uint32_t* __restrict__ offs,
-                                                 int32_t T, int64_t n, DevTable tb, uint32_t nblk, int B,
-                                                 uint32_t* __restrict__ pay, uint64_t* __restrict__ key64,
-                                                 uint32_t* __restrict__ binv, Status* st) {
+// ---- t-digest: the batch's values grouped by digest and sorted within each digest (launch_tdigest).  The tiers want
+// every touched digest's values of the push as one run in Double.compare order: v[0] from tbeg[i] for the digest
+// tslot[i], gsort the digest of every position.  The batch is already grouped by state partition, so instead of a
+// whole-batch LSD radix sort (8 passes over 12-byte pairs):
+//   k_td_group   every item's digest (the region lookup) and value key; a workgroup's items counted per digest in an
+//                LDS table, then one global add per (workgroup, digest) on dcnt[digest] gives the workgroup's place in
+//                the digest's run (the first add lists the digest as touched); every item keeps (digest, rank)
+//   runs         a scan over the touched digests' counts: the runs' starts (tbeg), written back into dcnt
+//   k_td_place   every item to its place in its digest's run (v[1], gsort)
+//   sorts        runs of <= 16 values by 16 lanes, of <= 64 by a wave (bitonic networks over the lanes), of
+//                <= TD_SORT_MAX by a workgroup in LDS; longer runs (the hot keys) are split first by MSD passes on
+//                their highest differing key bits into bins of about TD_SORT_MAX / 2 values (two levels), whatever is
+//                still longer by a workgroup's bitonic network in global memory (a fallback)
+// Every comparison is on the full 64-bit key: equal keys are equal values, so no tie fix-up is needed.
+constexpr int TD_GCHUNK = 4096;     // items per k_td_group workgroup (a digest's rank among them: 12 bits)
+constexpr int TD_GTHREADS = 1024;   // (its 64-KB table: two workgroups, 32 waves per CU for the region lookups)
+constexpr int TD_GHASH_LOG = 13;
+constexpr int TD_GHASH = 1 << TD_GHASH_LOG;  // its LDS table of digests (at most TD_GCHUNK of them)
+constexpr uint32_t TD_GEMPTY = 0xffffffffu;
+constexpr int TD_SORT_MAX = 4096;   // values a workgroup sorts in LDS
+constexpr int TD_TILE_PT = 16;      // MSD tile: values per thread
+constexpr int TD_TILE = 256 * TD_TILE_PT;
+constexpr int TD_MSD_BINS = 4096;  // per run: its sample sort's buckets (at most 2 * 2047 + 1)
+constexpr uint32_t TD_RUN_V1 = 0x80000000u;  // TdRun.len: the run's values are in v[1]
+
+__global__ __launch_bounds__(TD_GTHREADS) void k_td_group(DevCfg c, const PRec* __restrict__ part, const uint32_t* __restrict__ offs,
+                                                  int32_t T, int64_t n, int32_t rchunk, DevTable tb, uint32_t none,
+                                                  TdBuf td, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  const int64_t total = offs[(int64_t)c.P * T];
-  const int64_t i0 = (int64_t)blockIdx.x * TD_CHUNK;
-  const int64_t i1 = min(n, i0 + (int64_t)TD_CHUNK);
-  const uint64_t none_key = (uint64_t)nblk << (64 - B);
-  const uint64_t low = (B >= 64) ? ~0ull : ((1ull << B) - 1ull);
-  // sliding windows (fan-out): record i's windows take items [i * wpr, i * wpr + nwin), newest first; the rest of
-  // its wpr items are empty (sorted last, skipped)
-  const int W = c.assigner == FW_SLIDING ? c.wpr : 1;
+  __shared__ uint32_t hk[TD_GHASH], hc[TD_GHASH];
   __shared__ int32_t p0_s;
+  const int64_t total = offs[(int64_t)c.P * T];
+  const int64_t i0 = (int64_t)blockIdx.x * rchunk;
+  const int64_t i1 = min(n, i0 + (int64_t)rchunk);
+  const int W = c.assigner == FW_SLIDING ? c.wpr : 1;
+  for (int h = threadIdx.x; h < TD_GHASH; h += blockDim.x) {
+    hk[h] = TD_GEMPTY;
+    hc[h] = 0u;
+  }
   if (threadIdx.x == 0) {  // partition of the chunk's first record: last p with offs[p*T] <= i0
     int32_t lo = 0, hi = c.P - 1;
     while (lo < hi) {
@@ -4403,9 +4463,9 @@ __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restric
   __syncthreads();
   const bool cmp = c.compact && !*c.wide;
   const bool sess = c.assigner == FW_SESSION;
-  // sessions and allowed lateness: the ordered path's added elements follow the partitioned records (positions
-  // total .. total + nov)
   const int64_t nov = c.td_ovctr ? (int64_t)*c.td_ovctr : 0;
+  uint32_t* __restrict__ gs0 = td.gs[0];
+  uint32_t* __restrict__ gs1 = td.gs[1];
   int32_t pp = p0_s;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     int nw = 0;
@@ -4428,7 +4488,7 @@ __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restric
         rec.key = c.td_ovk[j];
         rec.last = c.td_ovt[j];
         rec.val = c.td_ovv[j];
-        rec.nwin = c.td_ovn ? c.td_ovn[j] : 1;  // (its non-late windows, the newest ones)
+        rec.nwin = c.td_ovn ? c.td_ovn[j] : 1;
         rp = c.td_ovp[j];
       }
       nw = W == 1 ? 1 : (int)(rec.nwin & 0xffff);
@@ -4436,31 +4496,556 @@ __global__ __launch_bounds__(256) void k_td_keys(DevCfg c, const PRec* __restric
       const uint64_t k = td_key(rec.val);
       for (int wi = 0; wi < nw; wi++) {
         const int64_t o = i * W + wi;
+        if (i >= total && c.td_olink && c.td_olink[(i - total) * c.wpr + wi] == TD_DROPPED) {  // purged (td_purge)
+          gs0[o] = none;
+          continue;
+        }
         const int64_t s = jsub(rec.last, (int64_t)wi * c.slide);
-        // (sessions: the in-flight session of the key that holds the element's window [ts, ts + gap) -- after the
-        // push's merges exactly one does; tumbling / sliding: the window's own entry)
         const int32_t slot = sess ? session_containing(r, c, rec.key, rec.last) :
                                     region_find(r, slot_hash(c, rec.key, s), rec.key, s, wend(c, s));
         if (slot < 0) {
           atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's window
-          key64[o] = none_key;
-          pay[o] = 0;
+          gs0[o] = none;
           continue;
         }
         const uint32_t g = ((uint32_t)rp << c.log_r) | (uint32_t)slot;
         const uint64_t blk = pool_block_of(r.ent[slot]);
-        // every record of a digest stores the same slot, so a stale (cached) read costs one redundant store at
-        // most; a hot digest's records read it (an L1 hit) and store nothing
-        if (binv[blk] != g) binv[blk] = g;
-        key64[o] = (blk << (64 - B)) | (k >> B);
-        pay[o] = (uint32_t)(k & low);
+        if (td.binv[blk] != g) td.binv[blk] = g;
+        td.v[0][o] = k;
+        gs0[o] = g;
+        // the digest's LDS slot, and this item's rank among the workgroup's items of the digest
+        uint32_t h = (g * 0x9E3779B1u) >> (32 - TD_GHASH_LOG);
+        while (true) {
+          const uint32_t cur = __hip_atomic_load(&hk[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (cur == g) break;
+          if (cur == TD_GEMPTY) {
+            const uint32_t prev = atomicCAS(&hk[h], TD_GEMPTY, g);
+            if (prev == TD_GEMPTY || prev == g) break;
+          }
+          h = (h + 1) & (TD_GHASH - 1);
+        }
+        // a hot digest's items (a Zipf stream's head keys fill whole chunks): the lanes of the wave that share the
+        // first active lane's digest take their ranks from one LDS add
+        const uint64_t act = __ballot(1);
+        const int lead = __ffsll((long long)act) - 1;
+        const uint32_t hl = (uint32_t)__shfl((int)h, lead, 64);
+        const uint64_t peers = __ballot(h == hl);
+        uint32_t rank;
+        if (h == hl) {
+          uint32_t base = 0;
+          if ((int)__lane_id() == lead) base = atomicAdd(&hc[h], (uint32_t)__popcll(peers));
+          base = (uint32_t)__shfl((int)base, lead, 64);
+          rank = base + (uint32_t)__popcll(peers & lanemask_lt());
+        } else {
+          rank = atomicAdd(&hc[h], 1u);
+        }
+        gs1[o] = (h << 12) | rank;
       }
     }
-    for (int wi = nw; wi < W; wi++) {
-      key64[i * W + wi] = none_key;
-      pay[i * W + wi] = 0;
+    for (int wi = nw; wi < W; wi++) gs0[i * W + wi] = none;
+  }
+  __syncthreads();
+  // per digest of the workgroup one global add (all of a thread's in flight together); the digest's first workgroup
+  // (the add returned 0) lists it as touched, with one list reservation per workgroup
+  constexpr int HU = TD_GHASH / TD_GTHREADS;
+  uint32_t base[HU];
+  uint32_t firsts = 0;
+#pragma unroll
+  for (int u = 0; u < HU; u++) {
+    const int h = u * TD_GTHREADS + (int)threadIdx.x;
+    const uint32_t g = hk[h];
+    base[u] = g != TD_GEMPTY ? atomicAdd(&td.dcnt[g], hc[h]) : 1u;
+  }
+#pragma unroll
+  for (int u = 0; u < HU; u++) firsts += base[u] == 0u;
+  __shared__ uint32_t sw[TD_GTHREADS / 64 + 1];
+  __shared__ uint32_t lbase_s;
+  uint32_t ftotal;
+  uint32_t fpos = block_excl_scan(firsts, sw, &ftotal);
+  if (threadIdx.x == 0) lbase_s = ftotal ? (uint32_t)atomicAdd(&td.ctr[0], (int)ftotal) : 0u;
+  __syncthreads();
+  fpos += lbase_s;
+#pragma unroll
+  for (int u = 0; u < HU; u++) {
+    const int h = u * TD_GTHREADS + (int)threadIdx.x;
+    if (base[u] == 0u) td.tslot[fpos++] = hk[h];
+    hc[h] = base[u];
+  }
+  __syncthreads();
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x)  // (the items this thread wrote)
+    for (int wi = 0; wi < W; wi++) {
+      const int64_t o = i * W + wi;
+      if (gs0[o] == none) continue;
+      const uint32_t x = gs1[o];
+      gs1[o] = hc[x >> 12] + (x & 4095u);
+    }
+}
+// the touched digests' counts (tbeg[nt] = 0), scanned in place by the device-sized scan below
+__global__ __launch_bounds__(256) void k_td_counts(TdBuf td, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int32_t nt = td.ctr[0];
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i <= nt; i += gridDim.x * blockDim.x)
+    td.tbeg[i] = i < nt ? td.dcnt[td.tslot[i]] : 0u;
+}
+// k_scan_* over data[0 .. *mdev] (the length read on the device)
+__global__ __launch_bounds__(SCAN_T) void k_scan_blocks_d(uint32_t* data, const int32_t* mdev, uint32_t* sums) {
+  const int64_t m = (int64_t)*mdev + 1;
+  if ((int64_t)blockIdx.x * SCAN_B >= m) return;
+  __shared__ uint32_t sw[SCAN_T / 64 + 1];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_B + (int64_t)threadIdx.x * SCAN_E;
+  uint32_t v[SCAN_E];
+  uint32_t local = 0;
+#pragma unroll
+  for (int e = 0; e < SCAN_E; e++) {
+    v[e] = base + e < m ? data[base + e] : 0u;
+    local += v[e];
+  }
+  uint32_t total;
+  uint32_t off = block_excl_scan(local, sw, &total);
+#pragma unroll
+  for (int e = 0; e < SCAN_E; e++) {
+    if (base + e < m) data[base + e] = off;
+    off += v[e];
+  }
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+__global__ __launch_bounds__(SCAN_T) void k_scan_top_d(uint32_t* sums, const int32_t* mdev) {
+  const int64_t nb = ((int64_t)*mdev + 1 + SCAN_B - 1) / SCAN_B;
+  __shared__ uint32_t sw[SCAN_T / 64 + 1];
+  uint32_t carry = 0;
+  for (int64_t b0 = 0; b0 < nb; b0 += SCAN_T) {
+    const int64_t i = b0 + threadIdx.x;
+    uint32_t v = i < nb ? sums[i] : 0u, total;
+    uint32_t off = block_excl_scan(v, sw, &total);
+    if (i < nb) sums[i] = off + carry;
+    carry += total;
+  }
+}
+__global__ __launch_bounds__(SCAN_T) void k_scan_add_d(uint32_t* data, const int32_t* mdev, const uint32_t* sums) {
+  const int64_t m = (int64_t)*mdev + 1;
+  const int64_t base = (int64_t)blockIdx.x * SCAN_B;
+  if (base >= m) return;
+  const uint32_t add = sums[blockIdx.x];
+  for (int e = threadIdx.x; e < SCAN_B; e += SCAN_T)
+    if (base + e < m) data[base + e] += add;
+}
+// a wave's appends to a run list: one reservation per wave (the lanes with `want`)
+__device__ __forceinline__ void td_list_put(TdRun* list, int32_t* ctr, bool want, TdRun r) {
+  const uint64_t m = __ballot(want);
+  if (!m) return;
+  const int lead = __ffsll((long long)m) - 1;
+  int base = 0;
+  if ((int)__lane_id() == lead) base = atomicAdd(ctr, __popcll(m));
+  base = __shfl(base, lead, 64);
+  if (want) list[base + __popcll(m & lanemask_lt())] = r;
+}
+// the runs' starts into dcnt (read by k_td_place), and the long runs listed for the LDS sort / the MSD passes
+__global__ __launch_bounds__(256) void k_td_starts(TdBuf td, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int32_t nt = td.ctr[0];
+  for (int32_t i0 = blockIdx.x * blockDim.x; i0 < nt; i0 += gridDim.x * blockDim.x) {  // (whole waves iterate)
+    const int32_t i = i0 + threadIdx.x;
+    uint32_t beg = 0, len = 0;
+    if (i < nt) {
+      beg = td.tbeg[i];
+      len = td.tbeg[i + 1] - beg;
+      td.dcnt[td.tslot[i]] = beg;
+    }
+    td_list_put(td.brun[0], &td.lctr[1], len > TD_SORT_MAX, TdRun{beg, len | TD_RUN_V1});
+    td_list_put(td.lrun, &td.lctr[0], len > 64 && len <= TD_SORT_MAX, TdRun{beg, len | TD_RUN_V1});
+  }
+}
+// every item to its run (v[1]) and its digest to gsort; positions past the runs get `none`
+__global__ __launch_bounds__(256) void k_td_place(TdBuf td, int64_t n, uint32_t none, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int64_t placed = td.tbeg[td.ctr[0]];
+  for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = td.gs[0][o];
+    if (g != none) {
+      const uint32_t pos = td.dcnt[g] + td.gs[1][o];
+      td.v[1][pos] = td.v[0][o];
+      td.gsort[pos] = g;
+    }
+    if (o >= placed) td.gsort[o] = none;
+  }
+}
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m, int w) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, m, w), hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), m, w);
+  return ((uint64_t)hi << 32) | lo;
+}
+// the runs of <= 16 (G = 16: four runs a wave) or 17..64 values (G = 64) sorted by a bitonic network over G lanes
+// (the "flip" form: every compare-exchange puts the smaller key at the lower index, so the lanes past the run hold
+// the largest key and stay there)
+template <int G>
+__global__ __launch_bounds__(256) void k_td_sort_lanes(TdBuf td, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int32_t nt = td.ctr[0];
+  const int lane = (int)(threadIdx.x & (G - 1));
+  const int64_t groups = ((int64_t)gridDim.x * blockDim.x) / G;
+  for (int64_t d = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; d < nt; d += groups) {
+    const uint32_t beg = td.tbeg[d], len = td.tbeg[d + 1] - beg;
+    if (G == 16 ? len > 16 : (len <= 16 || len > 64)) continue;  // (the same for the whole group)
+    uint64_t x = (uint32_t)lane < len ? td.v[1][beg + lane] : ~0ull;
+#pragma unroll
+    for (int k = 2; k <= G; k <<= 1) {
+      {
+        const uint64_t y = shfl_xor_u64(x, k - 1, G);
+        x = (lane & (k >> 1)) ? max(x, y) : min(x, y);
+      }
+#pragma unroll
+      for (int j = k >> 2; j > 0; j >>= 1) {
+        const uint64_t y = shfl_xor_u64(x, j, G);
+        x = (lane & j) ? max(x, y) : min(x, y);
+      }
+    }
+    if ((uint32_t)lane < len) td.v[0][beg + lane] = x;
+  }
+}
+// bitonic network ("flip" form) over keys a[0 .. len) in LDS, by the workgroup; positions >= len are +infinity
+__device__ void td_bitonic_lds(uint64_t* a, uint32_t len) {
+  uint32_t n2 = 1;
+  while (n2 < len) n2 <<= 1;
+  for (uint32_t k = 2; k <= n2; k <<= 1) {
+    const uint32_t hk = k >> 1;
+    for (uint32_t t = threadIdx.x; t < (n2 >> 1); t += blockDim.x) {
+      const uint32_t i = (t & ~(hk - 1)) * 2 + (t & (hk - 1)), p = i ^ (k - 1);
+      if (p < len) {
+        const uint64_t x = a[i], y = a[p];
+        if (x > y) {
+          a[i] = y;
+          a[p] = x;
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t j = k >> 2; j > 0; j >>= 1) {
+      for (uint32_t t = threadIdx.x; t < (n2 >> 1); t += blockDim.x) {
+        const uint32_t i = (t & ~(j - 1)) * 2 + (t & (j - 1)), p = i + j;
+        if (p < len) {
+          const uint64_t x = a[i], y = a[p];
+          if (x > y) {
+            a[i] = y;
+            a[p] = x;
+          }
+        }
+      }
+      __syncthreads();
     }
   }
+}
+// the same network with the first stages in registers: thread t holds keys [t E, t E + E) of the n2 = 256 E padded
+// positions, so every stage whose partner distance is below E (the flip stages of blocks up to E, and the low
+// half-cleaners) runs on its registers; only the longer stages go through the LDS (by the workgroup's 256 threads)
+template <int E>
+__device__ __forceinline__ void td_cswap(uint64_t& a, uint64_t& b) {
+  const uint64_t x = min(a, b), y = max(a, b);
+  a = x;
+  b = y;
+}
+template <int E>
+__device__ void td_bitonic_reg(uint64_t* a, uint32_t len) {
+  constexpr uint32_t n2 = 256u * E;
+  const uint32_t t0 = threadIdx.x * E;
+  uint64_t x[E];
+#pragma unroll
+  for (int e = 0; e < E; e++) x[e] = t0 + e < len ? a[t0 + e] : ~0ull;
+  for (uint32_t k = 2; k <= n2; k <<= 1) {
+    if (k > (uint32_t)E) {  // the flip stage and the half-cleaners of distance >= E through the LDS
+#pragma unroll
+      for (int e = 0; e < E; e++) a[t0 + e] = x[e];
+      __syncthreads();
+      const uint32_t hk = k >> 1;
+      for (uint32_t t = threadIdx.x; t < (n2 >> 1); t += blockDim.x) {
+        const uint32_t i = (t & ~(hk - 1)) * 2 + (t & (hk - 1)), p = i ^ (k - 1);
+        const uint64_t u = a[i], v = a[p];
+        if (u > v) {
+          a[i] = v;
+          a[p] = u;
+        }
+      }
+      __syncthreads();
+      for (uint32_t j = k >> 2; j >= (uint32_t)E; j >>= 1) {
+        for (uint32_t t = threadIdx.x; t < (n2 >> 1); t += blockDim.x) {
+          const uint32_t i = (t & ~(j - 1)) * 2 + (t & (j - 1)), p = i + j;
+          const uint64_t u = a[i], v = a[p];
+          if (u > v) {
+            a[i] = v;
+            a[p] = u;
+          }
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int e = 0; e < E; e++) x[e] = a[t0 + e];
+      __syncthreads();
+    } else {  // the flip stage of a block inside the thread's keys
+#pragma unroll
+      for (int e = 0; e < E; e++) {
+        const int p = e ^ (int)(k - 1);
+        if (e < p) td_cswap<E>(x[e], x[p]);
+      }
+    }
+#pragma unroll
+    for (int j = E >> 1; j > 0; j >>= 1) {  // the half-cleaners of distance < E (those below k / 2)
+      if ((uint32_t)j > (k >> 2)) continue;
+#pragma unroll
+      for (int e = 0; e < E; e++) {
+        const int p = e ^ j;
+        if (e < p) td_cswap<E>(x[e], x[p]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; e++) a[t0 + e] = x[e];
+  __syncthreads();
+}
+// the runs of 65 .. TD_SORT_MAX values (digests, and the MSD passes' bins): one workgroup each, in LDS, into v[0]
+__global__ __launch_bounds__(256) void k_td_sort_lds(TdBuf td, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  __shared__ uint64_t a[TD_SORT_MAX];
+  const int32_t nw = td.lctr[0];
+  for (int32_t w = blockIdx.x; w < nw; w += gridDim.x) {
+    const TdRun r = td.lrun[w];
+    const uint32_t len = r.len & ~TD_RUN_V1;
+    const uint64_t* __restrict__ src = (r.len & TD_RUN_V1) ? td.v[1] : td.v[0];
+    for (uint32_t i = threadIdx.x; i < len; i += blockDim.x) a[i] = src[r.beg + i];
+    __syncthreads();
+    if (len > 2048)
+      td_bitonic_reg<16>(a, len);
+    else if (len > 1024)
+      td_bitonic_reg<8>(a, len);
+    else if (len > 512)
+      td_bitonic_reg<4>(a, len);
+    else if (len > 256)
+      td_bitonic_reg<2>(a, len);
+    else
+      td_bitonic_lds(a, len);
+    for (uint32_t i = threadIdx.x; i < len; i += blockDim.x) td.v[0][r.beg + i] = a[i];
+    __syncthreads();
+  }
+}
+// ---- sample-sort passes over the runs longer than TD_SORT_MAX (level L: brun[L]; buckets of more than TD_SORT_MAX
+// values go to brun[L + 1], brun[2] being the fallback).  A run's splitters are every (S / (ns + 1))-th key of a sorted
+// sample of S <= TD_SAMPLE of its keys (ns + 1 = the run's length / (TD_SORT_MAX / 2), rounded up to a power of two,
+// at most TD_MAX_SPL + 1); key x goes to bucket 2 lb + 1 when it equals splitter lb = lower_bound(x) -- a bucket of
+// equal keys, already sorted, written to v[0] at once -- else to bucket 2 lb (strictly between two splitters).  The
+// splitters are keys of the run, so every strict bucket is shorter than the run: each level makes progress whatever
+// the distribution (heavy ties included).
+constexpr int TD_SAMPLE = 8192;
+constexpr int TD_MAX_SPL = 2047;
+constexpr int TD_BUCKETS = 2 * TD_MAX_SPL + 1;
+__device__ __forceinline__ int32_t td_tile_run(const TdMsd* msd, int32_t nl, uint32_t t) {
+  int32_t lo = 0, hi = nl - 1;  // the last run whose first tile is <= t
+  while (lo < hi) {
+    const int32_t mid = (lo + hi + 1) >> 1;
+    if (msd[mid].toff <= t)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+__device__ __forceinline__ uint32_t td_bucket(const uint64_t* spl, uint32_t ns, uint64_t x) {
+  uint32_t lo = 0, hi = ns;  // lower_bound: the first splitter >= x
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (spl[mid] < x)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return 2 * lo + (lo < ns && spl[lo] == x ? 1u : 0u);
+}
+__global__ __launch_bounds__(256) void k_td_msd_prep(TdBuf td, int L, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int64_t nl = td.lctr[1 + L];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl * TD_MSD_BINS;
+       i += (int64_t)gridDim.x * blockDim.x)
+    td.hist[i] = 0u;
+}
+// the runs' first tiles (one workgroup), and the level's tile count in lctr[4]
+__global__ __launch_bounds__(1024) void k_td_msd_plan(TdBuf td, int L, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  __shared__ uint32_t sw[1024 / 64 + 1];
+  const int32_t nl = td.lctr[1 + L];
+  uint32_t carry = 0;
+  for (int32_t j0 = 0; j0 < nl; j0 += blockDim.x) {
+    const int32_t j = j0 + threadIdx.x;
+    const uint32_t nt = j < nl ? ((td.brun[L][j].len & ~TD_RUN_V1) + TD_TILE - 1) / TD_TILE : 0u;
+    uint32_t total;
+    const uint32_t off = block_excl_scan(nt, sw, &total);
+    if (j < nl) td.msd[j].toff = carry + off;
+    carry += total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) td.lctr[4] = (int32_t)carry;
+}
+// one workgroup per run: a sorted sample of its keys, its splitters (td.spl, msd.nsp)
+__global__ __launch_bounds__(1024) void k_td_msd_sample(TdBuf td, int L, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  __shared__ uint64_t a[TD_SAMPLE];
+  const int32_t nl = td.lctr[1 + L];
+  for (int32_t j = blockIdx.x; j < nl; j += gridDim.x) {
+    const TdRun r = td.brun[L][j];
+    const uint32_t len = r.len & ~TD_RUN_V1;
+    const uint64_t* __restrict__ src = (r.len & TD_RUN_V1) ? td.v[1] : td.v[0];
+    const uint32_t S = min((uint32_t)TD_SAMPLE, len);
+    for (uint32_t i = threadIdx.x; i < S; i += blockDim.x) a[i] = src[r.beg + (uint32_t)(((uint64_t)i * len) / S)];
+    __syncthreads();
+    td_bitonic_lds(a, S);
+    uint32_t nb = 2;  // buckets between splitters: ~TD_SORT_MAX / 2 values each
+    while (nb < TD_MAX_SPL + 1 && (uint64_t)nb * (TD_SORT_MAX / 2) < len) nb <<= 1;
+    const uint32_t ns = nb - 1;
+    for (uint32_t b = threadIdx.x; b < ns; b += blockDim.x)
+      td.spl[(int64_t)j * TD_MAX_SPL + b] = a[(uint32_t)(((uint64_t)(b + 1) * S) / nb)];
+    if (threadIdx.x == 0) td.msd[j].nsp = ns;
+    __syncthreads();
+  }
+}
+// one tile's keys (TD_TILE_PT per thread; past the run: ~0), and the run's splitters into LDS
+__device__ __forceinline__ void td_tile_load(const TdBuf& td, const TdRun& r, uint32_t t0, uint64_t (&x)[TD_TILE_PT],
+                                             uint32_t* lo_out, uint32_t* hi_out) {
+  const uint32_t len = r.len & ~TD_RUN_V1;
+  const uint64_t* __restrict__ src = (r.len & TD_RUN_V1) ? td.v[1] : td.v[0];
+  const uint32_t lo = t0 * TD_TILE, hi = min(len, lo + TD_TILE);
+#pragma unroll
+  for (int u = 0; u < TD_TILE_PT; u++) {
+    const uint32_t q = lo + u * 256 + threadIdx.x;
+    x[u] = q < hi ? src[r.beg + q] : ~0ull;
+  }
+  *lo_out = lo;
+  *hi_out = hi;
+}
+__global__ __launch_bounds__(256) void k_td_msd_hist(TdBuf td, int L, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int32_t nl = td.lctr[1 + L];
+  const uint32_t ntile = (uint32_t)td.lctr[4];
+  __shared__ uint32_t hs[TD_BUCKETS];
+  __shared__ uint64_t spl[TD_MAX_SPL];
+  for (uint32_t t = blockIdx.x; t < ntile; t += gridDim.x) {
+    const int32_t j = td_tile_run(td.msd, nl, t);
+    const TdRun r = td.brun[L][j];
+    const TdMsd m = td.msd[j];
+    const uint32_t ns = m.nsp, nb = 2 * ns + 1;
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hs[b] = 0u;
+    for (uint32_t b = threadIdx.x; b < ns; b += blockDim.x) spl[b] = td.spl[(int64_t)j * TD_MAX_SPL + b];
+    uint64_t x[TD_TILE_PT];
+    uint32_t lo, hi;
+    td_tile_load(td, r, t - m.toff, x, &lo, &hi);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < TD_TILE_PT; u++) {
+      const uint32_t q = lo + u * 256 + threadIdx.x;
+      if (q < hi) atomicAdd(&hs[td_bucket(spl, ns, x[u])], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
+      if (hs[b]) atomicAdd(&td.hist[(int64_t)j * TD_MSD_BINS + b], hs[b]);
+    __syncthreads();
+  }
+}
+// one workgroup per run: its buckets' starts (the cursors k_td_msd_scatter advances), and its strict buckets listed
+// as runs of the next step -- the LDS sort (<= TD_SORT_MAX values) or the next level
+__global__ __launch_bounds__(256) void k_td_msd_scan(TdBuf td, int L, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  __shared__ uint32_t sw[256 / 64 + 1];
+  const int32_t nl = td.lctr[1 + L];
+  for (int32_t j = blockIdx.x; j < nl; j += gridDim.x) {
+    const TdRun r = td.brun[L][j];
+    const uint32_t dst = (r.len & TD_RUN_V1) ? 0u : TD_RUN_V1;  // the strict buckets land in the other buffer
+    const uint32_t nb = 2 * td.msd[j].nsp + 1;
+    uint32_t* h = td.hist + (int64_t)j * TD_MSD_BINS;
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += blockDim.x) {
+      const uint32_t b = b0 + threadIdx.x;
+      const uint32_t cnt = b < nb ? h[b] : 0u;
+      uint32_t total;
+      const uint32_t off = block_excl_scan(cnt, sw, &total) + carry;
+      if (b < nb) h[b] = off;
+      const bool strict = b < nb && !(b & 1u);
+      td_list_put(td.brun[L + 1], &td.lctr[2 + L], strict && cnt > TD_SORT_MAX, TdRun{r.beg + off, cnt | dst});
+      // (a single value is sorted; it moves to v[0] through the LDS sort when it landed in v[1])
+      td_list_put(td.lrun, &td.lctr[0], strict && cnt <= TD_SORT_MAX && (cnt > 1 || (cnt == 1 && dst)),
+                  TdRun{r.beg + off, cnt | dst});
+      carry += total;
+      __syncthreads();
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_td_msd_scatter(TdBuf td, int L, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int32_t nl = td.lctr[1 + L];
+  const uint32_t ntile = (uint32_t)td.lctr[4];
+  __shared__ uint32_t hs[TD_BUCKETS];
+  __shared__ uint64_t spl[TD_MAX_SPL];
+  for (uint32_t t = blockIdx.x; t < ntile; t += gridDim.x) {
+    const int32_t j = td_tile_run(td.msd, nl, t);
+    const TdRun r = td.brun[L][j];
+    const TdMsd m = td.msd[j];
+    const uint32_t ns = m.nsp, nb = 2 * ns + 1;
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hs[b] = 0u;
+    for (uint32_t b = threadIdx.x; b < ns; b += blockDim.x) spl[b] = td.spl[(int64_t)j * TD_MAX_SPL + b];
+    uint64_t x[TD_TILE_PT];
+    uint32_t lo, hi;
+    td_tile_load(td, r, t - m.toff, x, &lo, &hi);
+    __syncthreads();
+    uint32_t bk[TD_TILE_PT], rk[TD_TILE_PT];
+#pragma unroll
+    for (int u = 0; u < TD_TILE_PT; u++) {
+      const uint32_t q = lo + u * 256 + threadIdx.x;
+      bk[u] = q < hi ? td_bucket(spl, ns, x[u]) : 0u;
+      rk[u] = q < hi ? atomicAdd(&hs[bk[u]], 1u) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
+      if (hs[b]) hs[b] = atomicAdd(&td.hist[(int64_t)j * TD_MSD_BINS + b], hs[b]);
+    __syncthreads();
+    uint64_t* __restrict__ dst = (r.len & TD_RUN_V1) ? td.v[0] : td.v[1];
+#pragma unroll
+    for (int u = 0; u < TD_TILE_PT; u++) {
+      const uint32_t q = lo + u * 256 + threadIdx.x;
+      if (q < hi) ((bk[u] & 1u) ? td.v[0] : dst)[r.beg + hs[bk[u]] + rk[u]] = x[u];  // (equal keys: final)
+    }
+    __syncthreads();
+  }
+}
+// the fallback: runs still longer than TD_SORT_MAX after two MSD levels (keys crowded into a few bits' range), one
+// workgroup each, a bitonic network in global memory (in place), then into v[0]
+__global__ __launch_bounds__(256) void k_td_sort_global(TdBuf td, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int32_t nw = td.lctr[3];
+  for (int32_t w = blockIdx.x; w < nw; w += gridDim.x) {
+    const TdRun r = td.brun[2][w];
+    const uint32_t len = r.len & ~TD_RUN_V1;
+    uint64_t* a = ((r.len & TD_RUN_V1) ? td.v[1] : td.v[0]) + r.beg;
+    uint32_t n2 = 1;
+    while (n2 < len) n2 <<= 1;
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        for (uint32_t t = threadIdx.x; t < (n2 >> 1); t += blockDim.x) {
+          const uint32_t i = (t & ~(j - 1)) * 2 + (t & (j - 1));
+          const uint32_t p = j == (k >> 1) ? (i ^ (k - 1)) : i + j;
+          if (p < len) {
+            const uint64_t x = a[i], y = a[p];
+            if (x > y) {
+              a[i] = y;
+              a[p] = x;
+            }
+          }
+        }
+        __threadfence_block();
+        __syncthreads();
+      }
+    }
+    if (r.len & TD_RUN_V1)
+      for (uint32_t i = threadIdx.x; i < len; i += blockDim.x) td.v[0][r.beg + i] = a[i];
+    __syncthreads();
+  }
+}
+// after the tiers: the touched digests' counters back to zero (whatever ran: k_td_group lists what it counted)
+__global__ __launch_bounds__(256) void k_td_reset(TdBuf td) {
+  const int32_t nt = td.ctr[0];
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nt; i += gridDim.x * blockDim.x) td.dcnt[td.tslot[i]] = 0u;
 }
 
 // ---- t-digest session merges (DevCfg::td_mdst / td_msrc, logged by the session flush and the ordered replay):
@@ -4485,12 +5070,30 @@ __global__ void k_td_mlist(DevCfg c, TdBuf td) {
     td.mnext[i] = prev < 0 ? -2 : prev;  // -2: the list's last entry (the first in), which builds the union
   }
 }
-__global__ void k_td_mbuild(DevCfg c, TdBuf td, Status* st) {
+__global__ void k_td_mbuild(DevCfg c, DevTable tb, TdBuf td, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int32_t nl = *c.td_mctr;
   for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += gridDim.x * blockDim.x) {
     if (td.mnext[i] != -2) continue;
     const uint32_t t = td_final_target(td, c.td_mdst[i]);
+    // the target's slot, which k_td_group wrote when one of the push's values went to it -- none may have (the
+    // merged session fired with FIRE_AND_PURGE afterwards: td_purge emptied every digest of the union and dropped
+    // the values), and then binv is a stale slot: the union (empty) is not needed, only the sources' release
+    const uint32_t g = td.binv[t];
+    bool own = (int64_t)g < td.lidx_slots;
+    if (own) {
+      const int32_t p = (int32_t)(g >> c.log_r);
+      const Region r = region_of(c, tb, p, tb.cur[p]);
+      const uint32_t sl = g & r.mask;
+      own = st_kind(r.state[sl]) == SLOT_LIVE && pool_block_of(r.ent[sl]) == (uint64_t)t;
+    }
+    if (!own) {
+      for (int32_t j = td.mhead[t]; j >= 0; j = td.mnext[j]) {
+        c.pool_defer[atomicAdd(&c.pool_ctr[2], 1)] = c.td_msrc[j];
+        if (td.mnext[j] == -2) break;
+      }
+      continue;
+    }
     // the target's centroids and every merged block's (weights for now), then freed sources
     int32_t m = 0;
     const TdHead ht = *td_head(c, t);
@@ -4516,7 +5119,6 @@ __global__ void k_td_mbuild(DevCfg c, TdBuf td, Status* st) {
       if (td.mnext[j] == -2) break;
     }
     td_union_sort(u, m);
-    const uint32_t g = td.binv[t];  // (the merging element was added to the target: k_td_keys set it)
     const int32_t ov = (int32_t)atomicAdd(&td.uctr[1], 1ull);
     td.ovr[ov] = TdOverride{u, m, g, wold};
     td.mover[g] = ov;
@@ -4532,104 +5134,6 @@ __global__ void k_td_mclear(DevCfg c, TdBuf td) {
   }
   const int32_t no = (int32_t)td.uctr[1];
   for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < no; i += gridDim.x * blockDim.x) td.mover[td.ovr[i].slot] = -1;
-}
-
-// tie runs: positions with the previous one's key (one digest, equal high value bits) and a smaller payload mark
-// their run's first position in fixbm; k_td_fix_runs then orders each marked run by payload
-__global__ __launch_bounds__(256) void k_td_fix_mark(int64_t n, const uint64_t* __restrict__ key64,
-                                                     const uint32_t* __restrict__ pay, uint32_t* __restrict__ fixbm,
-                                                     const Status* st) {
-  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = key64[i];
-    if (k != key64[i - 1] || pay[i] >= pay[i - 1]) continue;
-    int64_t s = i - 1;
-    while (s > 0 && key64[s - 1] == k) s--;
-    atomicOr(&fixbm[s >> 5], 1u << (s & 31));
-  }
-}
-__device__ void td_sift(uint32_t* a, int64_t root, int64_t len) {
-  while (2 * root + 1 < len) {
-    int64_t ch = 2 * root + 1;
-    if (ch + 1 < len && a[ch + 1] > a[ch]) ch++;
-    if (a[root] >= a[ch]) return;
-    const uint32_t t = a[root];
-    a[root] = a[ch];
-    a[ch] = t;
-    root = ch;
-  }
-}
-__global__ __launch_bounds__(256) void k_td_fix_runs(int64_t n, const uint64_t* __restrict__ key64,
-                                                     uint32_t* __restrict__ pay, const uint32_t* __restrict__ fixbm,
-                                                     const Status* st) {
-  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
-    if (!((fixbm[s >> 5] >> (s & 31)) & 1u)) continue;
-    const uint64_t k = key64[s];
-    int64_t e = s + 1;
-    while (e < n && key64[e] == k) e++;
-    uint32_t* a = pay + s;
-    const int64_t len = e - s;
-    for (int64_t r = len / 2 - 1; r >= 0; r--) td_sift(a, r, len);  // heapsort: bounded for any run
-    for (int64_t m = len - 1; m > 0; m--) {
-      const uint32_t t = a[0];
-      a[0] = a[m];
-      a[m] = t;
-      td_sift(a, 0, m);
-    }
-  }
-}
-// the sorted keys back to (global slot, value key) columns for the tiers
-// (behind a suspended push the sort ran over whatever the key buffer held -- k_td_keys skipped itself -- so this
-// and the fix-up kernels skip themselves too; the settle runs the compression again)
-__global__ __launch_bounds__(256) void k_td_decode(int64_t n, int B, uint32_t nblk, uint32_t none,
-                                                   const uint64_t* __restrict__ key64, const uint32_t* __restrict__ pay,
-                                                   const uint32_t* __restrict__ binv, uint32_t* __restrict__ gs,
-                                                   uint64_t* __restrict__ v, const Status* st) {
-  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = key64[i];
-    const uint32_t blk = (uint32_t)(k >> (64 - B));
-    if (blk >= nblk) {  // (nblk: the positions without a digest)
-      gs[i] = none;
-      v[i] = 0;
-    } else {
-      gs[i] = binv[blk];
-      v[i] = (k << B) | (uint64_t)pay[i];
-    }
-  }
-}
-
-// the touched digests: the first position of every run of one slot in the sorted batch.  A workgroup takes
-// TD_BOUNDS consecutive positions and reserves its digests' places with one atomic.
-constexpr int TD_BOUNDS_PER_THREAD = 16;
-__global__ __launch_bounds__(256) void k_td_bounds(int64_t n, const uint32_t* __restrict__ gs, uint32_t none, TdBuf td,
-                                                   Status* st) {
-  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  __shared__ uint32_t sw[256 / 64 + 1];
-  __shared__ int base_s;
-  const int64_t i0 = (int64_t)blockIdx.x * 256 * TD_BOUNDS_PER_THREAD + (int64_t)threadIdx.x * TD_BOUNDS_PER_THREAD;
-  uint32_t starts = 0;  // bit u: position i0 + u starts a run
-  uint32_t prev = i0 > 0 && i0 <= n ? gs[i0 - 1] : none;
-#pragma unroll
-  for (int u = 0; u < TD_BOUNDS_PER_THREAD; u++) {
-    const int64_t i = i0 + u;
-    const uint32_t g = i < n ? gs[i] : none;
-    if (g != none && (i == 0 || g != prev)) starts |= 1u << u;
-    prev = g;
-  }
-  uint32_t total;
-  const uint32_t pos = block_excl_scan((uint32_t)__popc(starts), sw, &total);
-  if (threadIdx.x == 0) base_s = total ? atomicAdd(&td.ctr[0], (int)total) : 0;
-  __syncthreads();
-  int k = base_s + (int)pos;
-#pragma unroll
-  for (int u = 0; u < TD_BOUNDS_PER_THREAD; u++) {
-    if (!((starts >> u) & 1u)) continue;
-    td.tslot[k] = gs[i0 + u];
-    td.tbeg[k] = (uint32_t)(i0 + u);
-    k++;
-  }
 }
 
 // each touched digest: merged serially here, or queued for the wave or the grid-wide merge
@@ -5392,13 +5896,17 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
         if (!d2.fire) continue;
         if ((int64_t)pos < out.cap) {
           write_row(c, out, pos, fe);
+          // a session that fires with FIRE_AND_PURGE stays in flight with its state cleared (fire_decide): its
+          // block is emptied after the row is read, and kept
+          const bool purge = d2.keep && c.purging;
           if (c.agg == FW_AGG_HLL) {  // read back by hll_finish: the block, and its free-stack slot when it goes
             out.mn[pos] = (int64_t)pool_block_of(fe);
-            out.mx[pos] = d2.keep ? -1 : (int64_t)atomicAdd(&nrel_s, 1);
+            out.mx[pos] = d2.keep ? (purge ? HLL_ZERO_KEEP : -1) : (int64_t)atomicAdd(&nrel_s, 1);
           }
           if (c.agg == FW_AGG_TDIGEST || c.agg == FW_AGG_ROW)  // read back by td_finish / row_finish: the block,
-            out.sum[pos] = (int64_t)(pool_block_of(fe) |                          // above it 1 + its free-stack slot
-                                     (d2.keep ? 0ull : (uint64_t)(atomicAdd(&nrel_s, 1) + 1) << 32));
+            out.sum[pos] = (int64_t)(pool_block_of(fe) |       // above it 1 + its free-stack slot, bit 63 a purge
+                                     (d2.keep ? 0ull : (uint64_t)(atomicAdd(&nrel_s, 1) + 1) << 32) |
+                                     (purge && c.agg == FW_AGG_TDIGEST ? TD_PURGE_TAG : 0ull));
         } else {
           atomicOr(&st->flags, FW_STATUS_OUT_FULL);
         }
@@ -5423,7 +5931,7 @@ __global__ __launch_bounds__(FW_FIRE_THREADS, POOL ? 5 : 1) void k_fire(DevCfg c
       } else {
         for (uint64_t r = base_s + (threadIdx.x >> 6); r < end; r += nwv) {
           const int64_t ri = out.mx[r];  // (every lane reads it before lane 0 overwrites it)
-          hll_finish(c, out, r, ri < 0 ? -1 : hl_sb + ri, hl_ids + (threadIdx.x & ~63u));
+          hll_finish(c, out, r, ri < 0 ? ri : hl_sb + ri, hl_ids + (threadIdx.x & ~63u));
         }
       }
     } else if (c.agg == FW_AGG_ROW) {
@@ -7640,13 +8148,6 @@ void launch_count(const DevCfg& c, DevCount& cw, const int64_t* key, const int64
   hipLaunchKernelGGL(k_cnt_update, dim3(grid), dim3(256), 0, s, c, cw, sk, sv, val, n, none);
   hipLaunchKernelGGL(k_cnt_count, dim3(grid), dim3(256), 0, s, cw, sk, n, none);
 }
-size_t tdigest_sort_bytes(int64_t n) {
-  size_t a = 0;
-  rocprim::double_buffer<uint64_t> kv(nullptr, nullptr);
-  rocprim::double_buffer<uint32_t> ks(nullptr, nullptr);
-  (void)rocprim::radix_sort_pairs(nullptr, a, kv, ks, (size_t)n, 0, 64);
-  return a;
-}
 // t-digest under allowed lateness: the push's late-firing chains rebuilt after the table grew mid-push (settle
 // resumes the ordered path over moved slots).  A chain's order does not matter (td_late_row selects in value order).
 __global__ void k_td_relink(DevCfg c, DevTable tb) {
@@ -7656,6 +8157,7 @@ __global__ void k_td_relink(DevCfg c, DevTable tb) {
     const Region r = region_of(c, tb, p, tb.cur[p]);
     const int64_t k = c.td_ovk[j], last = c.td_ovt[j];
     if (c.assigner == FW_SESSION) {  // (the session that holds the element now: merged sessions' values included)
+      if (c.td_olink[j] == TD_DROPPED) continue;  // (purged: in no chain)
       const int32_t slot = session_containing(r, c, k, last);
       c.td_olink[j] = slot < 0 ? -1 : atomicExch(&c.td_olast[((uint32_t)p << c.log_r) | (uint32_t)slot], (int32_t)j);
       continue;
@@ -7664,6 +8166,7 @@ __global__ void k_td_relink(DevCfg c, DevTable tb) {
       const int64_t s = jsub(last, (int64_t)wi * c.slide);
       const int32_t slot = region_find(r, slot_hash(c, k, s), k, s, wend(c, s));
       const int32_t l = (int32_t)j * c.wpr + wi;
+      if (c.td_olink[l] == TD_DROPPED) continue;
       c.td_olink[l] = slot < 0 ? -1 : atomicExch(&c.td_olast[((uint32_t)p << c.log_r) | (uint32_t)slot], l);
     }
   }
@@ -7690,43 +8193,52 @@ void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int
                     TdBuf& td, Status* st, hipStream_t s) {
   if (n <= 0) return;
   const uint32_t none = (uint32_t)td.lidx_slots;  // no slot has this id (slots are 0 .. table slots - 1)
-  const uint32_t nblk = (uint32_t)c.pool_blocks;   // no block has this id
-  int B = 1;
-  while (((int64_t)1 << B) <= c.pool_blocks) B++;
   const int64_t nrec = n;
-  n *= c.assigner == FW_SLIDING ? c.wpr : 1;  // the sort's items: one per (record, window)
+  const int W = c.assigner == FW_SLIDING ? c.wpr : 1;
+  n *= W;  // the items: one per (record, window)
   (void)hipMemsetAsync(td.ctr, 0, 3 * sizeof(int32_t), s);
-  (void)hipMemsetAsync(td.fixbm, 0, (size_t)((n + 31) / 32) * sizeof(uint32_t), s);
-  hipLaunchKernelGGL(k_td_keys, dim3((unsigned)((nrec + TD_CHUNK - 1) / TD_CHUNK)), dim3(256), 0, s, c, part, offs, T,
-                     nrec, tb, nblk, B, td.gs[0], td.v[0], td.binv, st);
+  (void)hipMemsetAsync(td.lctr, 0, 5 * sizeof(int32_t), s);
+  const int32_t rchunk = std::max(1, TD_GCHUNK / W);  // (records per grouping workgroup: at most TD_GCHUNK items)
+  hipLaunchKernelGGL(k_td_group, dim3((unsigned)((nrec + rchunk - 1) / rchunk)), dim3(TD_GTHREADS), 0, s, c, part, offs, T, nrec,
+                     rchunk, tb, none, td, st);
   if (c.assigner == FW_SESSION) {  // the push's session merges: each merged digest's union of old centroids
     hipLaunchKernelGGL(k_td_mlink, dim3(64), dim3(256), 0, s, c, td);
     hipLaunchKernelGGL(k_td_mlist, dim3(64), dim3(256), 0, s, c, td);
-    hipLaunchKernelGGL(k_td_mbuild, dim3(64), dim3(256), 0, s, c, td, st);
+    hipLaunchKernelGGL(k_td_mbuild, dim3(64), dim3(256), 0, s, c, tb, td, st);
   }
-  // one sort by (pool block, high value bits): each digest's batch values become one run, in Double.compare
-  // order once the tie runs are ordered by their low bits
-  rocprim::double_buffer<uint64_t> kv(td.v[0], td.v[1]);
-  rocprim::double_buffer<uint32_t> ks(td.gs[0], td.gs[1]);
-  size_t bytes = td.tmp_bytes;
-  (void)rocprim::radix_sort_pairs(td.tmp, bytes, kv, ks, (size_t)n, 0, 64, s);
+  // the digests' runs: their counts scanned (tbeg[0 .. nt], nt read on the device; td.mid is the scan's scratch:
+  // the wave tier lists its digests there later), the items placed
   const unsigned grid = (unsigned)std::min<int64_t>(8192, (n + 255) / 256);
-  hipLaunchKernelGGL(k_td_fix_mark, dim3(grid), dim3(256), 0, s, n, kv.current(), ks.current(), td.fixbm, st);
-  hipLaunchKernelGGL(k_td_fix_runs, dim3(grid), dim3(256), 0, s, n, kv.current(), ks.current(), td.fixbm, st);
-  uint32_t* gsorted = ks.alternate();
-  uint64_t* vsorted = kv.alternate();
-  hipLaunchKernelGGL(k_td_decode, dim3(grid), dim3(256), 0, s, n, B, nblk, none, kv.current(), ks.current(), td.binv,
-                     gsorted, vsorted, st);
-  const int64_t per_block = 256 * TD_BOUNDS_PER_THREAD;
-  hipLaunchKernelGGL(k_td_bounds, dim3((unsigned)((n + per_block - 1) / per_block)), dim3(256), 0, s, n, gsorted, none,
-                     td, st);
+  hipLaunchKernelGGL(k_td_counts, dim3(grid), dim3(256), 0, s, td, st);
+  const unsigned nb = (unsigned)((n + 1 + SCAN_B - 1) / SCAN_B);
+  hipLaunchKernelGGL(k_scan_blocks_d, dim3(nb), dim3(SCAN_T), 0, s, td.tbeg, (const int32_t*)td.ctr, td.mid);
+  hipLaunchKernelGGL(k_scan_top_d, dim3(1), dim3(SCAN_T), 0, s, td.mid, (const int32_t*)td.ctr);
+  hipLaunchKernelGGL(k_scan_add_d, dim3(nb), dim3(SCAN_T), 0, s, td.tbeg, (const int32_t*)td.ctr, (const uint32_t*)td.mid);
+  hipLaunchKernelGGL(k_td_starts, dim3(grid), dim3(256), 0, s, td, st);
+  hipLaunchKernelGGL(k_td_place, dim3(grid), dim3(256), 0, s, td, n, none, st);
+  // each run sorted: by lanes, by MSD passes (two levels) and the fallback, then in LDS (into v[0])
+  hipLaunchKernelGGL(k_td_sort_lanes<16>, dim3(4096), dim3(256), 0, s, td, st);
+  hipLaunchKernelGGL(k_td_sort_lanes<64>, dim3(4096), dim3(256), 0, s, td, st);
+  for (int L = 0; L < 2; L++) {
+    hipLaunchKernelGGL(k_td_msd_prep, dim3(1024), dim3(256), 0, s, td, L, st);
+    hipLaunchKernelGGL(k_td_msd_plan, dim3(1), dim3(1024), 0, s, td, L, st);
+    hipLaunchKernelGGL(k_td_msd_sample, dim3(512), dim3(1024), 0, s, td, L, st);
+    hipLaunchKernelGGL(k_td_msd_hist, dim3(2048), dim3(256), 0, s, td, L, st);
+    hipLaunchKernelGGL(k_td_msd_scan, dim3(1024), dim3(256), 0, s, td, L, st);
+    hipLaunchKernelGGL(k_td_msd_scatter, dim3(2048), dim3(256), 0, s, td, L, st);
+  }
+  hipLaunchKernelGGL(k_td_sort_global, dim3(256), dim3(256), 0, s, td, st);
+  hipLaunchKernelGGL(k_td_sort_lds, dim3(4096), dim3(256), 0, s, td, st);
+  // the merge by size tier (the digests' old centroids and their sorted values)
+  const uint64_t* vsorted = td.v[0];
   hipLaunchKernelGGL(k_td_small, dim3(grid), dim3(256), 0, s, c, tb, td, vsorted, st);
   hipLaunchKernelGGL(k_td_wave, dim3(2048), dim3(64 * TD_WAVES), td_wave_lds_bytes(c.td_nb), s, c, tb, td, vsorted, st);
   hipLaunchKernelGGL(k_td_large_old, dim3(64), dim3(256), 0, s, c, vsorted, td, st);  // (the mean keys: first)
-  hipLaunchKernelGGL(k_td_large_items, dim3(grid), dim3(256), 0, s, c, n, gsorted, vsorted, none, td, st);
+  hipLaunchKernelGGL(k_td_large_items, dim3(grid), dim3(256), 0, s, c, n, (const uint32_t*)td.gsort, vsorted, none, td, st);
   hipLaunchKernelGGL(k_td_large_groups, dim3(2048), dim3(256), 0, s, c, vsorted, td, st);
   hipLaunchKernelGGL(k_td_large_compact, dim3(64), dim3(64), 0, s, c, td, st);
   if (c.assigner == FW_SESSION) hipLaunchKernelGGL(k_td_mclear, dim3(64), dim3(256), 0, s, c, td);
+  hipLaunchKernelGGL(k_td_reset, dim3(grid), dim3(256), 0, s, td);
 }
 void launch_rehash(const DevCfg& oc, DevTable ot, const DevCfg& nc, DevTable nt, hipStream_t s) {
   if (oc.dense)

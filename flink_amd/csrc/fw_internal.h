@@ -371,13 +371,29 @@ struct TdOverride {  // a merged digest's old centroids (instead of its live hal
   uint32_t slot;  // the digest's global slot (its mover entry)
   int64_t wold;
 };
+// the batch's values grouped by digest, then sorted within each digest's run (launch_tdigest): runs sorted in LDS
+// (<= TD_SORT_MAX values) and longer runs split first by sample-sort passes
+struct TdRun {
+  uint32_t beg, len;        // len bit 31: the values are in v[1] (else v[0])
+};
+struct TdMsd {
+  uint32_t toff;            // the run's first tile (TD_TILE values each) among the level's runs
+  uint32_t nsp;             // its splitters (td.spl)
+};
 struct TdBuf {
-  uint32_t* gs[2];          // low value bits (sort payload), then the global slot (partition << log_r | slot)
-  uint64_t* v[2];           // (pool block, high value bits) sort keys, then the Double.compare-ordered value
+  uint32_t* gs[2];          // per item: [0] its digest's global slot (partition << log_r | slot), [1] its rank in the run
+  uint64_t* v[2];           // per item its Double.compare-ordered value key; [1] the values grouped by digest, [0]
+                            // each digest's run sorted (the tiers read v[0])
   uint32_t* binv;           // [pool blocks] global slot of each block's entry (rewritten when it moved)
-  uint32_t* fixbm;          // [max_batch / 32] tie runs whose low value bits need sorting
-  void* tmp;                // rocPRIM radix-sort scratch
-  size_t tmp_bytes;
+  uint32_t* dcnt;           // [table slots] a digest's items in the batch, then its run's start (zero between pushes)
+  uint32_t* gsort;          // [max items] the digest of each sorted position (`none` past the runs)
+  TdRun* lrun;              // [lrun_cap] runs for the LDS sort
+  TdRun* brun[3];           // [brun_cap] runs for MSD pass 1, 2, and the fallback
+  TdMsd* msd;               // [brun_cap] the sample-sort level's runs' tiles and splitter counts
+  uint64_t* spl;            // [brun_cap * 2047] their splitters
+  uint32_t* hist;           // [brun_cap * 4096] their buckets' counts, then cursors
+  int32_t* lctr;            // [0] lrun entries, [1..3] brun[0..2] entries, [4] the MSD level's tiles
+  int64_t lrun_cap, brun_cap;
   uint32_t* tslot;          // touched digests: global slot      [max_batch]
   uint32_t* tbeg;           //                  first sorted value [max_batch]
   int32_t* ctr;             // [0] touched digests, [1] large ones, [2] wave-tier ones
@@ -389,7 +405,6 @@ struct TdBuf {
   int32_t* lidx;            // [table slots] large index of a touched digest, -1 = compressed serially
   int64_t lidx_slots;
   int32_t max_large;
-  int32_t sel;              // which of gs / v holds the sorted batch (set by launch_tdigest)
   // session merges (DevCfg::td_mdst / td_msrc): a merged digest's old centroids are the union of its own and of the
   // digests merged into it, ordered by (mean, weight, sum), built once per push into `uni`; the tiers read them
   // through the override of the digest's slot
@@ -510,7 +525,6 @@ void launch_row_update(const DevCfg& c, const PRec* part, const uint32_t* offs, 
 void launch_td_relink(const DevCfg& c, DevTable tb, hipStream_t s);
 void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int32_t T, int64_t n, DevTable tb,
                     TdBuf& td, Status* st, hipStream_t_ s);
-size_t tdigest_sort_bytes(int64_t n);  // rocPRIM scratch of the two sorts
 // FW_COUNT: one batch of count windows (key slots, stable sort by key, fire, ring update); val = the push's values
 void launch_count(const DevCfg& c, DevCount& cw, const int64_t* key, const int64_t* val, int64_t n, DevRows out,
                   Status* st, hipStream_t_ s);

@@ -46,7 +46,7 @@ constexpr int64_t LMIN = INT64_MIN;
 #define FW_LIST_ROOM (int64_t(1) << 28)  // elements a walk may size its output for up front
 #endif
 enum : uint32_t { GF_TIMER = 1u, GF_TOUCH = 2u, GF_FIRE = 4u, GF_CLEAN = 8u };
-enum : uint32_t { LF_NO_TS = 1u, LF_KEY_GROUP = 2u, LF_MAP_FULL = 4u, LF_ELEMS = 8u };
+enum : uint32_t { LF_NO_TS = 1u, LF_KEY_GROUP = 2u, LF_MAP_FULL = 4u, LF_ELEMS = 8u, LF_MERGE_LATE = 16u, LF_MERGE_WIDE = 32u };
 constexpr uint32_t G_EMPTY = 0u, G_BUSY = 1u, G_LIVE = 2u, G_TOMB = 3u;
 
 struct LCfg {
@@ -76,6 +76,8 @@ struct alignas(32) LPay {
 struct LState {
   GSlot* g;  // the group map: one 32-byte slot per group (a lookup reads one sector)
   uint32_t gmask;
+  // session windows (FW_SESSION, fw_list.hip "session windows"): per slot its window end and list head / tail
+  int64_t *wend, *whead, *wtail;
   LPay* lpay;  // the elements' payload, one 32-byte sector each (a gather reads one sector per element)
   int32_t* lgid;
   int64_t *rkey, *rstart, *rend, *rcnt, *rsum, *rmin, *rmax, *rfirst, *roff;
@@ -849,6 +851,508 @@ __global__ __launch_bounds__(256) void k_restore_elems(LState S, const int64_t* 
   }
 }
 
+// ---------------------------------------------------------------- session windows (f4, merging assigners)
+// EventTimeSessionWindows over ListState: EvictingWindowOperator.processElement's merging branch (:110-170; the
+// plain WindowOperator's, WindowOperator.java:297-370, is the same without an evictor) with MergingWindowSet.addWindow
+// (MergingWindowSet.java:150-225) and TimeWindow.mergeWindows (TimeWindow.java:201-244), onEventTime (:241-286) and
+// emitWindowContents (:334-366).
+// A live slot of the map is one in-flight window of a key together with its state window's list (MergingWindowSet's
+// mapping is one to one, so the window carries its list): GSlot.key / start, wend[] its end, GSlot.cnt its live
+// elements, GF_TIMER its trigger timer, whead / wtail its list -- a singly linked list through the log (LPay.pad =
+// the next element, -1 at the end) in list order: the state window's list, then the other merged windows' lists in
+// HashSet order (AbstractHeapMergingState.mergeNamespaces :67-93 with HeapListState's addAll), then the elements added
+// since.  Slots are hashed by the key alone, so a key's windows all lie on its probe chain before the first EMPTY
+// slot.  lgid: 0 live, -1 dead (evicted, purged, cleaned up, or dropped late).
+// A push sorts its records by key (stable: arrival order within a key), places them in the log in that order, and
+// one thread per key processes its elements in order.
+constexpr int SL_MAXM = 4;  // in-flight windows one element's window can touch (2: they are >= gap long, disjoint)
+__device__ __forceinline__ uint32_t sl_home(int64_t key) { return (uint32_t)fmix64((uint64_t)key ^ 0x5E551045u); }
+__device__ __forceinline__ int64_t sl_max_ts(int64_t end) { return jsub(end, 1); }
+__device__ __forceinline__ int64_t sl_cleanup(const LCfg& c, int64_t end) {  // WindowOperator.cleanupTime (:637-644)
+  const int64_t mx = sl_max_ts(end);
+  const int64_t t = jadd(mx, c.lateness);
+  return t >= mx ? t : LMAX;
+}
+// TimeWindow.hashCode = MathUtils.longToIntWithBitMixing(start + end) (TimeWindow.java:102-104, MathUtils.java:177-182),
+// then HashMap's bucket spread h ^ (h >>> 16)
+__device__ __forceinline__ uint32_t sl_tw_bucket(int64_t start, int64_t end, uint32_t cap) {
+  uint64_t in = (uint64_t)jadd(start, end);
+  in = (in ^ (in >> 30)) * 0xbf58476d1ce4e5b9ull;
+  in = (in ^ (in >> 27)) * 0x94d049bb133111ebull;
+  in = in ^ (in >> 31);
+  const uint32_t h = (uint32_t)in;
+  return (h ^ (h >> 16)) & (cap - 1);
+}
+__device__ __forceinline__ int64_t sl_timer_of(const LCfg& c, uint32_t fl, int64_t end) {
+  return (fl & GF_TIMER) ? sl_max_ts(end) : sl_cleanup(c, end);
+}
+
+// a new window slot for key on its chain (from `from`, a TOMB / EMPTY slot the walk met first): claimed with a CAS
+// (other threads insert other keys), its fields stored write-through, then LIVE (g_find_insert's publication)
+__device__ int32_t sl_insert(const LState& S, int64_t key, int32_t kg, int64_t start, int64_t end, uint32_t from) {
+  uint32_t s = from;
+  for (uint32_t probes = 0; probes <= S.gmask; probes++, s = (s + 1) & S.gmask) {
+    uint32_t cur = __hip_atomic_load(&S.g[s].st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur != G_EMPTY && cur != G_TOMB) continue;
+    if (atomicCAS(&S.g[s].st, cur, G_BUSY) != cur) continue;  // (taken meanwhile: it is some key's now)
+    __hip_atomic_store(&S.g[s].key, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&S.g[s].start, start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&S.g[s].kg, kg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&S.g[s].cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&S.g[s].fl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    S.wend[s] = end;
+    S.whead[s] = -1;
+    S.wtail[s] = -1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&S.g[s].st, (uint32_t)G_LIVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == G_TOMB) atomicAdd(&S.ctr->tombs, (unsigned long long)-1ll);
+    return (int32_t)s;
+  }
+  atomicOr(&S.ctr->flags, LF_MAP_FULL);
+  return -1;
+}
+
+// kill element q of a list (unlinked by the caller)
+__device__ __forceinline__ void sl_kill(const LState& S, int64_t q, unsigned long long* killed) {
+  S.lgid[q] = -1;
+  (*killed)++;
+}
+// the evictor over slot s's list (CountEvictor.evict :63-78, TimeEvictor.evict :67-96, DeltaEvictor.evict :72-80):
+// mark = false: how many elements would remain; mark = true: the others are unlinked and killed, the count returned
+__device__ int64_t sl_evict(const LCfg& c, const LState& S, int32_t s, bool mark, unsigned long long* killed) {
+  const int64_t live = S.g[s].cnt;
+  if (c.evictor == FW_EVICT_NONE || live == 0) return live;
+  int64_t drop = 0, cutoff = 0, last = 0;
+  if (c.evictor == FW_EVICT_COUNT) {
+    if (live <= c.ev_n) return live;
+    drop = live - c.ev_n;
+  } else if (c.evictor == FW_EVICT_TIME) {
+    const int64_t h = S.whead[s];
+    if (S.lpay[h].ts == LMIN) return live;  // hasTimestamp of the first element
+    int64_t mx = LMIN;
+    for (int64_t q = h; q >= 0; q = S.lpay[q].pad) mx = max(mx, S.lpay[q].ts);
+    cutoff = jsub(mx, c.ev_n);
+  } else {
+    last = S.lpay[S.wtail[s]].val;
+  }
+  int64_t removed = 0, prev = -1;
+  for (int64_t q = S.whead[s]; q >= 0;) {
+    const LPay p = S.lpay[q];
+    const bool rm = c.evictor == FW_EVICT_COUNT ? removed < drop
+                  : c.evictor == FW_EVICT_TIME  ? p.ts <= cutoff
+                                                : delta_of(c, p.val, last) >= c.thr;
+    if (rm) {
+      removed++;
+      if (mark) {
+        if (prev < 0)
+          S.whead[s] = p.pad;
+        else
+          S.lpay[prev].pad = p.pad;
+        if (S.wtail[s] == q) S.wtail[s] = prev;
+        sl_kill(S, q, killed);
+      }
+    } else {
+      prev = q;
+    }
+    if (c.evictor == FW_EVICT_COUNT && removed >= drop && !mark) break;
+    q = p.pad;
+  }
+  if (mark) S.g[s].cnt = (int32_t)(live - removed);
+  return live - removed;
+}
+// clearing slot s's list (PurgingTrigger's windowState.clear(), clearAllState)
+__device__ void sl_clear(const LState& S, int32_t s, unsigned long long* killed) {
+  for (int64_t q = S.whead[s]; q >= 0; q = S.lpay[q].pad) sl_kill(S, q, killed);
+  S.whead[s] = S.wtail[s] = -1;
+  S.g[s].cnt = 0;
+}
+// emitWindowContents (:334-366) of slot s: evictBefore, one row (+ the elements in list order), evictAfter.
+// atomic = false: the host sized rows and elements for every firing (plain reservations); else elements are reserved
+// with compare-and-swap against ecap, and false (nothing changed) is returned when they do not fit.
+__device__ bool sl_emit(const LCfg& c, const LState& S, int32_t s, bool atomic, unsigned long long* killed) {
+  const int64_t cnt = c.evict_after ? (int64_t)S.g[s].cnt : sl_evict(c, S, s, false, killed);
+  int64_t eoff = 0;
+  if (c.emit && cnt) {
+    if (!atomic) {
+      eoff = (int64_t)atomicAdd(&S.ctr->elems, (unsigned long long)cnt);
+    } else {
+      unsigned long long cur = __hip_atomic_load(&S.ctr->elems, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (true) {
+        if ((int64_t)cur + cnt > S.ecap) {
+          atomicOr(&S.ctr->flags, LF_ELEMS);
+          return false;
+        }
+        const unsigned long long prev = atomicCAS(&S.ctr->elems, cur, cur + (unsigned long long)cnt);
+        if (prev == cur) break;
+        cur = prev;
+      }
+      eoff = (int64_t)cur;
+    }
+  }
+  if (!c.evict_after) sl_evict(c, S, s, true, killed);
+  const bool fl = c.vt == FW_VAL_F64 || c.vt == FW_VAL_F32;
+  double ds = 0.0;
+  int64_t is = 0, mn = 0, mx = 0, first = -1, k = 0;
+  for (int64_t q = S.whead[s]; q >= 0;) {
+    const LPay p = S.lpay[q];
+    const int64_t v = p.val;
+    if (k == 0) first = p.ord;
+    if (fl) {
+      const double d = __longlong_as_double(v);
+      ds = k == 0 ? d : c.vt == FW_VAL_F32 ? (double)((float)ds + (float)d) : ds + d;
+      if (k == 0 || fkey(v) < fkey(mn)) mn = v;
+      if (k == 0 || fkey(v) > fkey(mx)) mx = v;
+    } else {
+      is = k == 0 ? v : jadd(is, v);
+      if (k == 0 || v < mn) mn = v;
+      if (k == 0 || v > mx) mx = v;
+    }
+    if (c.emit) {
+      S.ets[eoff + k] = p.ts;
+      S.eval[eoff + k] = v;
+      S.eord[eoff + k] = p.ord;
+    }
+    k++;
+    q = p.pad;
+  }
+  const unsigned long long r = atomicAdd(&S.ctr->rows, 1ull);
+  S.rkey[r] = S.g[s].key;
+  S.rstart[r] = S.g[s].start;
+  S.rend[r] = S.wend[s];
+  S.rcnt[r] = k;
+  if (fl) {
+    S.rsum[r] = __double_as_longlong(ds);
+    S.rmin[r] = k ? canon(mn) : 0;
+    S.rmax[r] = k ? canon(mx) : 0;
+  } else {
+    S.rsum[r] = c.vt == FW_VAL_I32 ? (int64_t)(int32_t)is : c.vt == FW_VAL_I16 ? (int64_t)(int16_t)is
+              : c.vt == FW_VAL_I8 ? (int64_t)(int8_t)is : is;
+    S.rmin[r] = mn;
+    S.rmax[r] = mx;
+  }
+  S.rfirst[r] = first;
+  S.roff[r] = c.emit ? eoff : 0;
+  if (c.evict_after) sl_evict(c, S, s, true, killed);
+  return true;
+}
+
+// per record: its key group (errors flagged) and its sort key / payload (the key, the record's index)
+__global__ __launch_bounds__(256) void k_sl_keys(LCfg c, LState S, const int64_t* __restrict__ key,
+                                                 const int32_t* __restrict__ kh, int64_t n, uint64_t* __restrict__ sk,
+                                                 uint32_t* __restrict__ si) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t kg = key_group(key_hash_of(c.key_kind, key[i], kh, i), c.max_par);
+    if ((uint32_t)(kg - c.kg0) >= (uint32_t)c.nkg) atomicOr(&S.ctr->flags, LF_KEY_GROUP);
+    sk[i] = (uint64_t)key[i];
+    si[i] = (uint32_t)i;
+  }
+}
+// the records in key order into the log at base (arrival order within a key), and the first position of each key
+__global__ __launch_bounds__(256) void k_sl_place(LState S, const int64_t* __restrict__ ts, const int64_t* __restrict__ val,
+                                                  const uint64_t* __restrict__ sk, const uint32_t* __restrict__ si,
+                                                  int64_t n, int64_t base, int64_t ord_base, uint8_t* __restrict__ f) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t i = si[p];
+    S.lpay[base + p] = LPay{ts[i], val[i], ord_base + (int64_t)i, -1};
+    S.lgid[base + p] = 0;
+    f[p] = p == 0 || sk[p] != sk[p - 1];
+  }
+}
+
+// One thread per key: its elements of the push in arrival order, exactly EvictingWindowOperator.processElement's
+// merging branch.  prog[r] = the log index of the element whose firing did not fit the element buffer (its window in
+// pslot[r]); the host grows the buffer and launches again, which finishes that firing first.  LMAX: the key is done.
+__global__ __launch_bounds__(256) void k_sl_process(LCfg c, LState S, const uint32_t* __restrict__ seg, int64_t nruns,
+                                                    int64_t base, int64_t wm, const uint64_t* __restrict__ sk,
+                                                    const int32_t* __restrict__ kh, const uint32_t* __restrict__ si,
+                                                    int64_t* __restrict__ prog, int32_t* __restrict__ pslot) {
+  long long due = LMAX;
+  unsigned long long killed = 0, late = 0, ins = 0, tombs = 0;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nruns; r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t q = prog[r];
+    if (q == LMAX) continue;
+    const int64_t a = seg[r], b = seg[r + 1];
+    const int64_t key = (int64_t)sk[a];
+    const int32_t kg = key_group(key_hash_of(c.key_kind, key, kh, (int64_t)si[a]), c.max_par);
+    if (q >= 0) {  // a resumed firing: element q's window fires over its list
+      const int32_t s = pslot[r];
+      if (!sl_emit(c, S, s, true, &killed)) continue;
+      if (c.purging) sl_clear(S, s, &killed);
+      due = min(due, (long long)sl_timer_of(c, S.g[s].fl, S.wend[s]));
+      q++;
+    } else {
+      q = base + a;
+    }
+    const uint32_t home = sl_home(key) & S.gmask;
+    for (; q < base + b; q++) {
+      const LPay e = S.lpay[q];
+      const int64_t ws = e.ts, we = jadd(e.ts, c.size);  // EventTimeSessionWindows.assignWindows
+      // the key's in-flight windows that intersect [ws, we] (TimeWindow.intersects), and the chain's first free slot
+      int32_t m[SL_MAXM];
+      int nm = 0;
+      uint32_t freeslot = 0xffffffffu, s = home;
+      for (uint32_t probes = 0; probes <= S.gmask; probes++, s = (s + 1) & S.gmask) {
+        const uint32_t st = __hip_atomic_load(&S.g[s].st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (st == G_EMPTY) {
+          if (freeslot == 0xffffffffu) freeslot = s;
+          break;
+        }
+        if (st == G_TOMB) {
+          if (freeslot == 0xffffffffu) freeslot = s;
+          continue;
+        }
+        if (st != G_LIVE) continue;  // (BUSY: another key's window being published)
+        __atomic_signal_fence(__ATOMIC_ACQUIRE);
+        if (ld_l2(&S.g[s].key) != key) continue;
+        const int64_t st0 = S.g[s].start, en0 = S.wend[s];
+        if (!(st0 <= we && en0 >= ws)) continue;
+        if (nm < SL_MAXM) m[nm] = (int32_t)s;
+        nm++;
+      }
+      if (nm > SL_MAXM) {
+        atomicOr(&S.ctr->flags, LF_MERGE_WIDE);
+        break;
+      }
+      int32_t actual = -1;
+      if (nm == 0) {  // a new window: MergingWindowSet.addWindow maps it to itself
+        if (sl_cleanup(c, we) <= wm) {  // isWindowLate -> retireWindow; the element is skipped
+          sl_kill(S, q, &killed);
+          if (jadd(e.ts, c.lateness) <= wm) {  // isElementLate (:410-418)
+            if (c.side_output) {
+              const unsigned long long o = atomicAdd(&S.ctr->side, 1ull);
+              S.skey[o] = key;
+              S.sts[o] = e.ts;
+              S.sval[o] = e.val;
+            } else {
+              late++;
+            }
+          }
+          continue;
+        }
+        actual = sl_insert(S, key, kg, ws, we, freeslot == 0xffffffffu ? home : freeslot);
+        if (actual < 0) break;
+        ins++;
+      } else {
+        // the merge set: the windows met and the new one, in TimeWindow.mergeWindows' order (by start, the new one
+        // after windows of an equal start: it was added last before the stable sort), iterated in HashSet order
+        int64_t ms[SL_MAXM + 1], me[SL_MAXM + 1];
+        int32_t mslot[SL_MAXM + 1];
+        int n = 0;
+        for (int i = 0; i < nm; i++) {  // insertion sort of the met windows by start
+          const int64_t st0 = S.g[m[i]].start;
+          int j = n;
+          while (j > 0 && ms[j - 1] > st0) {
+            ms[j] = ms[j - 1];
+            me[j] = me[j - 1];
+            mslot[j] = mslot[j - 1];
+            j--;
+          }
+          ms[j] = st0;
+          me[j] = S.wend[m[i]];
+          mslot[j] = m[i];
+          n++;
+        }
+        {
+          int j = n;
+          while (j > 0 && ms[j - 1] > ws) {
+            ms[j] = ms[j - 1];
+            me[j] = me[j - 1];
+            mslot[j] = mslot[j - 1];
+            j--;
+          }
+          ms[j] = ws;
+          me[j] = we;
+          mslot[j] = -1;
+          n++;
+        }
+        int64_t cs = ms[0], ce = me[0];
+        for (int i = 1; i < n; i++) ce = max(ce, me[i]);
+        (void)cs;
+        if (nm == 1 && S.g[m[0]].start <= ws && we <= S.wend[m[0]]) {
+          actual = m[0];  // contained: the merge result is the window itself, no merge function
+        } else {
+          // HashSet<TimeWindow> iteration (capacity 16 for <= 12 members): by bucket, a bucket in insertion order
+          uint32_t bk[SL_MAXM + 1];
+          for (int i = 0; i < n; i++) bk[i] = sl_tw_bucket(ms[i], me[i], 16u);
+          int ord[SL_MAXM + 1];
+          for (int i = 0; i < n; i++) ord[i] = i;
+          for (int i = 1; i < n; i++) {  // stable insertion sort by bucket
+            const int x = ord[i];
+            int j = i;
+            while (j > 0 && bk[ord[j - 1]] > bk[x]) {
+              ord[j] = ord[j - 1];
+              j--;
+            }
+            ord[j] = x;
+          }
+          // merge function (WindowOperator.java:308-339): the result may not be late
+          if (jadd(sl_max_ts(ce), c.lateness) <= wm) {
+            atomicOr(&S.ctr->flags, LF_MERGE_LATE);
+            break;
+          }
+          int32_t target = -1;
+          for (int oi = 0; oi < n; oi++) {
+            const int32_t sl = mslot[ord[oi]];
+            if (sl < 0) continue;  // (the new window: removed from the merge set)
+            if (target < 0) {
+              target = sl;  // the state window of the first merged window
+              continue;
+            }
+            // mergeNamespaces: the source's list appended to the target's; the source window leaves
+            if (S.whead[sl] >= 0) {
+              if (S.wtail[target] >= 0)
+                S.lpay[S.wtail[target]].pad = S.whead[sl];
+              else
+                S.whead[target] = S.whead[sl];
+              S.wtail[target] = S.wtail[sl];
+              S.g[target].cnt += S.g[sl].cnt;
+            }
+            __hip_atomic_store(&S.g[sl].st, (uint32_t)G_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            tombs++;
+          }
+          int64_t lo = LMAX;
+          for (int i = 0; i < n; i++) lo = min(lo, ms[i]);
+          S.g[target].start = lo;
+          S.wend[target] = ce;
+          S.g[target].fl |= GF_TIMER;  // EventTimeTrigger.onMerge registers the merged window's maxTimestamp
+          actual = target;
+        }
+      }
+      // windowState.add(element): appended to the list
+      if (S.wtail[actual] >= 0)
+        S.lpay[S.wtail[actual]].pad = q;
+      else
+        S.whead[actual] = q;
+      S.wtail[actual] = q;
+      S.g[actual].cnt++;
+      // EventTimeTrigger.onElement: FIRE when the window's maxTimestamp is not after the watermark
+      if (sl_max_ts(S.wend[actual]) <= wm) {
+        if (!sl_emit(c, S, actual, true, &killed)) {
+          prog[r] = q;
+          pslot[r] = actual;
+          break;
+        }
+        if (c.purging) sl_clear(S, actual, &killed);
+      } else {
+        S.g[actual].fl |= GF_TIMER;
+      }
+      due = min(due, (long long)sl_timer_of(c, S.g[actual].fl, S.wend[actual]));
+    }
+    if (q >= base + b) prog[r] = LMAX;
+  }
+  block_min(&S.ctr->next_due, due);
+  block_add(&S.ctr->dead, killed);
+  block_add(&S.ctr->late, late);
+  block_add(&S.ctr->live_groups, ins - tombs);  // (wraps: a net change)
+  block_add(&S.ctr->tombs, tombs);
+}
+
+// watermark: each live window whose trigger timer (maxTimestamp) or cleanup timer is due; the firing ones' list
+// lengths added up (the element buffer's bound)
+__global__ __launch_bounds__(256) void k_sl_due(LCfg c, LState S, int64_t wm) {
+  unsigned long long nf = 0, nc = 0, ne = 0;
+  long long due = LMAX;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)S.gmask;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    if (S.g[g].st != G_LIVE) continue;
+    const int64_t end = S.wend[g];
+    const uint32_t f0 = S.g[g].fl;
+    uint32_t f = f0;
+    if ((f & GF_TIMER) && sl_max_ts(end) <= wm) {  // EventTimeTrigger.onEventTime: FIRE
+      f = (f & ~GF_TIMER) | GF_FIRE;
+      nf++;
+      ne += (unsigned long long)S.g[g].cnt;
+    }
+    const int64_t cl = sl_cleanup(c, end);
+    if (cl != LMAX && cl <= wm) {
+      f |= GF_CLEAN;
+      nc++;
+    } else {
+      due = min(due, (long long)((f & GF_TIMER) ? sl_max_ts(end) : cl));
+    }
+    if (f != f0) S.g[g].fl = f;
+  }
+  block_min(&S.ctr->next_due, due);
+  block_add(&S.ctr->nfire, nf);
+  block_add(&S.ctr->nclean, nc);
+  block_add(&S.ctr->count, ne);
+}
+// the due windows: onEventTime (:241-286) -- contents != null: emitWindowContents; PURGE: clear; cleanup time:
+// clearAllState and the window leaves its MergingWindowSet (a tombstone)
+__global__ __launch_bounds__(256) void k_sl_fire(LCfg c, LState S) {
+  unsigned long long killed = 0, nt = 0;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)S.gmask;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    if (S.g[g].st != G_LIVE) continue;
+    const uint32_t f = S.g[g].fl;
+    if (!(f & (GF_FIRE | GF_CLEAN))) continue;
+    if (f & GF_FIRE) {
+      if (S.g[g].cnt > 0) {
+        sl_emit(c, S, (int32_t)g, false, &killed);
+        if (c.purging) sl_clear(S, (int32_t)g, &killed);
+      }
+      S.g[g].fl = f & ~GF_FIRE;
+    }
+    if (f & GF_CLEAN) {
+      sl_clear(S, (int32_t)g, &killed);
+      S.g[g].st = G_TOMB;
+      nt++;
+    }
+  }
+  block_add(&S.ctr->dead, killed);
+  block_add(&S.ctr->tombs, nt);
+  block_add(&S.ctr->live_groups, (unsigned long long)(-(long long)nt));
+}
+
+// compaction: the live elements' new positions, the log gathered with its links remapped, the lists' ends remapped
+__global__ __launch_bounds__(256) void k_sl_remap_set(const uint32_t* __restrict__ sel, int64_t m,
+                                                      int64_t* __restrict__ remap) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+    remap[sel[i]] = i;
+}
+__global__ __launch_bounds__(256) void k_sl_gather_log(LState o, LState S, const uint32_t* __restrict__ sel, int64_t m,
+                                                       const int64_t* __restrict__ remap) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    LPay p = o.lpay[sel[i]];
+    p.pad = p.pad >= 0 ? remap[p.pad] : -1;
+    S.lpay[i] = p;
+    S.lgid[i] = 0;
+  }
+}
+// the map rebuilt into S (another capacity, no tombstones); remap: the log's remap of the list ends (or null)
+__global__ __launch_bounds__(256) void k_sl_rebuild(LState o, LState S, const int64_t* __restrict__ remap) {
+  unsigned long long ins = 0;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)o.gmask;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    if (o.g[g].st != G_LIVE) continue;
+    const int64_t key = o.g[g].key;
+    const int32_t s = sl_insert(S, key, o.g[g].kg, o.g[g].start, o.wend[g], sl_home(key) & S.gmask);
+    if (s < 0) continue;
+    S.g[s].fl = o.g[g].fl;
+    S.g[s].cnt = o.g[g].cnt;
+    const int64_t h = o.whead[g], t = o.wtail[g];
+    S.whead[s] = h >= 0 && remap ? remap[h] : h;
+    S.wtail[s] = t >= 0 && remap ? remap[t] : t;
+    ins++;
+  }
+  block_add(&S.ctr->live_groups, ins);
+}
+// live lists (windows with elements) and timers: each window's cleanup timer, and its trigger timer when registered
+// and not at the same time (HeapInternalTimerService keeps one timer per (timestamp, key, window))
+__global__ __launch_bounds__(256) void k_sl_count_state(LCfg c, LState S, unsigned long long* out2) {
+  unsigned long long lists = 0, timers = 0;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= (int64_t)S.gmask;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    if (S.g[g].st != G_LIVE) continue;
+    lists += S.g[g].cnt > 0;
+    const int64_t cl = sl_cleanup(c, S.wend[g]);
+    timers += cl != LMAX;
+    if ((S.g[g].fl & GF_TIMER) && !(cl != LMAX && cl == sl_max_ts(S.wend[g]))) timers++;
+  }
+  if (lists) atomicAdd(&out2[0], lists);
+  if (timers) atomicAdd(&out2[1], timers);
+}
+
 unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>(8192, (n + 255) / 256)); }
 
 template <class T>
@@ -886,6 +1390,11 @@ struct fw_list {
   int64_t* prog = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
+  // session windows (FW_SESSION): the push's records sorted by key, and the per-key progress of k_sl_process
+  uint64_t *sk = nullptr, *sk2 = nullptr;
+  uint32_t *si = nullptr, *si2 = nullptr;
+  int64_t* sprog = nullptr;
+  int32_t* pslot = nullptr;
 };
 
 namespace {
@@ -1155,11 +1664,163 @@ int maybe_compact(fw_list* op) {
   return FW_OK;
 }
 
+// ---------------------------------------------------------------- session windows (host)
+bool sessions(const fw_list* op) { return op->c.assigner == FW_SESSION; }
+int sl_alloc_map(fw_list* op, LState& S, int64_t cap) {
+  LRET(alloc_map(op, S, cap));
+  LHIP(op, dmalloc(&S.wend, (size_t)cap));
+  LHIP(op, dmalloc(&S.whead, (size_t)cap));
+  LHIP(op, dmalloc(&S.wtail, (size_t)cap));
+  return FW_OK;
+}
+void sl_free_map(LState& S) {
+  free_map(S);
+  dfree(S.wend);
+  dfree(S.whead);
+  dfree(S.wtail);
+}
+// the map rebuilt at gcap slots (tombstones dropped); with `log`, the log compacted first (the live elements in
+// order, their links and the lists' ends remapped)
+int sl_compact(fw_list* op, int64_t gcap, bool log) {
+  LState o = op->S, S = op->S;
+  int64_t* remap = nullptr;
+  int64_t m = op->n_log;
+  if (log && op->n_log) {
+    LRET(ensure_sel(op, op->n_log));
+    hipLaunchKernelGGL(k_alive_flags, dim3(grid_for(op->n_log)), dim3(256), 0, op->stream, o.lgid, op->n_log,
+                       op->flags8);
+    LRET(select_positions(op, op->flags8, op->n_log, op->sel, &m));
+    LHIP(op, dmalloc(&remap, (size_t)op->n_log));
+    LHIP(op, hipMemsetAsync(remap, 0xff, (size_t)op->n_log * 8, op->stream));
+    hipLaunchKernelGGL(k_sl_remap_set, dim3(grid_for(m)), dim3(256), 0, op->stream, op->sel, m, remap);
+    LState L = S;
+    LRET(alloc_log(op, L, op->lcap));
+    hipLaunchKernelGGL(k_sl_gather_log, dim3(grid_for(m)), dim3(256), 0, op->stream, o, L, op->sel, m, remap);
+    S.lpay = L.lpay;
+    S.lgid = L.lgid;
+  }
+  LRET(sl_alloc_map(op, S, gcap));
+  LHIP(op, hipMemsetAsync(&op->S.ctr->live_groups, 0, 16, op->stream));  // live_groups, tombs
+  LHIP(op, hipMemsetAsync(&op->S.ctr->flags, 0, 4, op->stream));
+  hipLaunchKernelGGL(k_sl_rebuild, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, o, S, remap);
+  LHIP(op, hipGetLastError());
+  LHIP(op, hipStreamSynchronize(op->stream));
+  dfree(remap);
+  sl_free_map(o);
+  if (log && op->n_log) {
+    free_log(o);
+    op->n_log = m;
+    LHIP(op, hipMemsetAsync(&S.ctr->dead, 0, 8, op->stream));
+  }
+  op->S = S;
+  op->gcap = gcap;
+  op->grows++;
+  LRET(read_ctr(op));
+  if (op->h_ctr->flags & LF_MAP_FULL) return set_err(op, FW_ERR_CAPACITY, "list state map full");
+  return FW_OK;
+}
+int sl_maybe_compact(fw_list* op) {
+  const int64_t dead = (int64_t)op->h_ctr->dead, tombs = (int64_t)op->h_ctr->tombs;
+  const bool log = dead > (1 << 16) && 2 * dead > op->n_log;
+  if (log || 4 * tombs > op->gcap) return sl_compact(op, op->gcap, log);
+  return FW_OK;
+}
+int sl_check_flags(fw_list* op) {
+  const uint32_t f = op->h_ctr->flags;
+  if (f & LF_KEY_GROUP) return set_err(op, FW_ERR_KEY_GROUP, "a key of the batch is outside the handle's KeyGroupRange");
+  if (f & LF_MERGE_LATE)
+    return set_err(op, FW_ERR_UNSUPPORTED, "The end timestamp of an event-time window cannot become earlier than the "
+                                           "current watermark by merging.");
+  if (f & LF_MERGE_WIDE) return set_err(op, FW_ERR_STATE, "a session window met more than %d in-flight windows", SL_MAXM);
+  if (f & LF_MAP_FULL) return set_err(op, FW_ERR_CAPACITY, "list state map full");
+  return FW_OK;
+}
+// processElement for a batch of session-window records (EvictingWindowOperator.java:110-170)
+int sl_push(fw_list* op, const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int64_t n) {
+  LRET(read_ctr(op));
+  if (op->c.side_output) LRET(ensure_side(op, (int64_t)op->h_ctr->side + n));
+  // the map: every record may open a window; at most 3/4 of the slots live or tombstones during the push
+  const int64_t live = (int64_t)op->h_ctr->live_groups, tombs = (int64_t)op->h_ctr->tombs;
+  if (4 * (live + tombs + n) > 3 * op->gcap) {
+    int64_t g = op->gcap;
+    while (2 * (live + n) > g) g *= 2;
+    LRET(sl_compact(op, g, 2 * (int64_t)op->h_ctr->dead > op->n_log));
+  }
+  // the log: the batch is appended
+  if (op->n_log + n > op->lcap) {
+    if (2 * (int64_t)op->h_ctr->dead > op->n_log) LRET(sl_compact(op, op->gcap, true));
+    if (op->n_log + n > op->lcap) {
+      const int64_t cap = std::max<int64_t>(op->n_log + n, op->lcap * 2);
+      LState L = op->S;
+      LRET(alloc_log(op, L, cap));
+      if (op->n_log) {
+        LHIP(op, hipMemcpyAsync(L.lpay, op->S.lpay, (size_t)op->n_log * sizeof(LPay), hipMemcpyDeviceToDevice,
+                                op->stream));
+        LHIP(op, hipMemcpyAsync(L.lgid, op->S.lgid, (size_t)op->n_log * 4, hipMemcpyDeviceToDevice, op->stream));
+      }
+      LHIP(op, hipStreamSynchronize(op->stream));
+      free_log(op->S);
+      op->S.lpay = L.lpay;
+      op->S.lgid = L.lgid;
+      op->lcap = cap;
+      op->grows++;
+    }
+  }
+  LRET(ensure_rows(op, (int64_t)op->h_ctr->rows + n));  // (at most one firing per element)
+  LRET(ensure_sel(op, n));
+  LHIP(op, hipMemsetAsync(&op->S.ctr->flags, 0, 8, op->stream));  // flags, need_seq
+  hipLaunchKernelGGL(k_sl_keys, dim3(grid_for(n)), dim3(256), 0, op->stream, op->c, op->S, key, kh, n, op->sk, op->si);
+  size_t bytes = 0;
+  LHIP(op, rocprim::radix_sort_pairs(nullptr, bytes, op->sk, op->sk2, op->si, op->si2, (size_t)n, 0, 64, op->stream));
+  LRET(ensure_tmp(op, bytes));
+  bytes = op->tmp_bytes;
+  LHIP(op, rocprim::radix_sort_pairs(op->tmp, bytes, op->sk, op->sk2, op->si, op->si2, (size_t)n, 0, 64, op->stream));
+  const int64_t base = op->n_log;
+  hipLaunchKernelGGL(k_sl_place, dim3(grid_for(n)), dim3(256), 0, op->stream, op->S, ts, val, op->sk2, op->si2, n, base,
+                     op->ord_base, op->flags8);
+  int64_t nruns = 0;
+  LRET(select_positions(op, op->flags8, n, op->seg, &nruns));  // (reads the counters: flags are current)
+  LRET(sl_check_flags(op));
+  const uint32_t nn = (uint32_t)n;
+  LHIP(op, hipMemcpyAsync(op->seg + nruns, &nn, 4, hipMemcpyHostToDevice, op->stream));
+  LHIP(op, hipMemsetAsync(op->sprog, 0xff, (size_t)nruns * 8, op->stream));
+  for (int round = 0;; round++) {
+    LHIP(op, hipMemsetAsync(&op->S.ctr->flags, 0, 4, op->stream));
+    hipLaunchKernelGGL(k_sl_process, dim3(grid_for(nruns)), dim3(256), 0, op->stream, op->c, op->S, op->seg, nruns,
+                       base, op->wm, op->sk2, kh, op->si2, op->sprog, op->pslot);
+    LHIP(op, hipGetLastError());
+    LRET(read_ctr(op));
+    LRET(sl_check_flags(op));
+    if (!(op->h_ctr->flags & LF_ELEMS)) break;
+    if (round > 64) return set_err(op, FW_ERR_STATE, "session list push made no progress");
+    LRET(ensure_elems(op, op->S.ecap * 2));
+  }
+  op->n_log += n;
+  op->ord_base += n;
+  op->records_in += n;
+  return sl_maybe_compact(op);
+}
+// processWatermark: the due windows fire and the cleaned-up ones leave (EvictingWindowOperator.onEventTime)
+int sl_watermark(fw_list* op, int64_t wm) {
+  LHIP(op, hipMemsetAsync(&op->S.ctr->nfire, 0, 24, op->stream));  // nfire, nclean, count
+  hipLaunchKernelGGL(k_sl_due, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, op->c, op->S, wm);
+  LRET(read_ctr(op));
+  const int64_t nfire = (int64_t)op->h_ctr->nfire, nclean = (int64_t)op->h_ctr->nclean;
+  if (!nfire && !nclean) return FW_OK;
+  LRET(ensure_rows(op, (int64_t)op->h_ctr->rows + nfire));
+  if (op->c.emit) LRET(ensure_elems(op, (int64_t)op->h_ctr->elems + (int64_t)op->h_ctr->count));
+  hipLaunchKernelGGL(k_sl_fire, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, op->c, op->S);
+  LHIP(op, hipGetLastError());
+  LRET(read_ctr(op));
+  return sl_maybe_compact(op);
+}
+
 int push_device(fw_list* op, const int64_t* key, const int64_t* ts, const int64_t* val, const int32_t* kh, int64_t n) {
   if (n == 0) return FW_OK;
   if (n > op->max_batch) return set_err(op, FW_ERR_ARG, "batch of %lld records exceeds max_batch %lld", (long long)n,
                                         (long long)op->max_batch);
   if (op->cfg.key_kind == FW_KEY_HASHED && !kh) return set_err(op, FW_ERR_ARG, "key_hash required for FW_KEY_HASHED");
+  if (sessions(op)) return sl_push(op, key, ts, val, kh, n);
   if (op->c.side_output) {  // room for every record of the batch in the side output
     LRET(read_ctr(op));
     LRET(ensure_side(op, (int64_t)op->h_ctr->side + n));
@@ -1231,8 +1892,13 @@ int fw_list_create(const fw_list_config* cfg, fw_list** out) {
     *out = op;
     return code;
   };
-  if (c.assigner != FW_TUMBLING && c.assigner != FW_SLIDING && c.assigner != FW_GLOBAL)
-    return fail(FW_ERR_UNSUPPORTED, "assigner must be FW_TUMBLING, FW_SLIDING or FW_GLOBAL");
+  if (c.assigner != FW_TUMBLING && c.assigner != FW_SLIDING && c.assigner != FW_GLOBAL && c.assigner != FW_SESSION)
+    return fail(FW_ERR_UNSUPPORTED, "assigner must be FW_TUMBLING, FW_SLIDING, FW_SESSION or FW_GLOBAL");
+  if (c.assigner == FW_SESSION && c.size <= 0)
+    return fail(FW_ERR_ARG, "EventTimeSessionWindows parameters must satisfy 0 < size");
+  if (c.assigner == FW_SESSION && c.trigger != FW_TRIGGER_EVENT_TIME)
+    return fail(FW_ERR_UNSUPPORTED, "session windows over ListState are offered with EventTimeTrigger (or PurgingTrigger "
+                                    "of it)");
   if (c.assigner == FW_TUMBLING && (c.size <= 0 || c.offset < 0 || c.offset >= c.size))
     return fail(FW_ERR_ARG, "TumblingEventTimeWindows parameters must satisfy 0 <= offset < size");
   if (c.assigner == FW_SLIDING && (c.size <= 0 || c.slide <= 0 || c.slide > c.size || c.offset < 0 || c.offset >= c.slide))
@@ -1269,7 +1935,14 @@ int fw_list_create(const fw_list_config* cfg, fw_list** out) {
   int rc = FW_OK;
   if (hipHostMalloc((void**)&op->h_ctr, sizeof(LCounters), hipHostMallocDefault) != hipSuccess) rc = FW_ERR_HIP;
   if (rc == FW_OK) memset(op->h_ctr, 0, sizeof(LCounters));
-  if (rc == FW_OK) rc = alloc_map(op, op->S, op->gcap);
+  if (rc == FW_OK) rc = c.assigner == FW_SESSION ? sl_alloc_map(op, op->S, op->gcap) : alloc_map(op, op->S, op->gcap);
+  if (rc == FW_OK && c.assigner == FW_SESSION) {
+    const size_t mb = (size_t)op->max_batch;
+    if (dmalloc(&op->sk, mb) != hipSuccess || dmalloc(&op->sk2, mb) != hipSuccess || dmalloc(&op->si, mb) != hipSuccess ||
+        dmalloc(&op->si2, mb) != hipSuccess || dmalloc(&op->sprog, mb) != hipSuccess ||
+        dmalloc(&op->pslot, mb) != hipSuccess)
+      rc = FW_ERR_HIP;
+  }
   if (rc == FW_OK) rc = alloc_log(op, op->S, op->lcap);
   auto al = [&](int64_t** p, int64_t n) {
     if (rc == FW_OK && dmalloc(p, (size_t)n) != hipSuccess) rc = FW_ERR_HIP;
@@ -1299,8 +1972,14 @@ void fw_list_destroy(fw_list* op) {
   if (!op) return;
   (void)hipSetDevice(op->device);
   if (op->stream) (void)hipStreamSynchronize(op->stream);
-  free_map(op->S);
+  sl_free_map(op->S);  // (the session columns are null for the other assigners)
   free_log(op->S);
+  dfree(op->sk);
+  dfree(op->sk2);
+  dfree(op->si);
+  dfree(op->si2);
+  dfree(op->sprog);
+  dfree(op->pslot);
   for (int64_t** p : {&op->S.rkey, &op->S.rstart, &op->S.rend, &op->S.rcnt, &op->S.rsum, &op->S.rmin, &op->S.rmax,
                       &op->S.rfirst, &op->S.roff, &op->S.ets, &op->S.eval, &op->S.eord, &op->S.skey, &op->S.sts,
                       &op->S.sval, &op->in_key, &op->in_ts, &op->in_val})
@@ -1361,6 +2040,12 @@ int fw_list_advance_watermark(fw_list* op, int64_t wm, int64_t* n_pending_rows) 
     op->wm = wm;
     const long long none = LMAX;
     LHIP(op, hipMemcpyAsync(&op->S.ctr->next_due, &none, 8, hipMemcpyHostToDevice, op->stream));
+    if (sessions(op)) {
+      LRET(sl_watermark(op, wm));
+      LRET(read_ctr(op));
+      if (n_pending_rows) *n_pending_rows = (int64_t)op->h_ctr->rows;
+      return FW_OK;
+    }
     LHIP(op, hipMemsetAsync(&op->S.ctr->nfire, 0, 16, op->stream));
     hipLaunchKernelGGL(k_lw_due, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, op->c, op->S, wm);
     LRET(read_ctr(op));
@@ -1458,9 +2143,13 @@ int fw_list_get_stats(fw_list* op, fw_stats* out) {
   LHIP(op, dmalloc(&d2, 2));
   LHIP(op, hipMemsetAsync(has, 0, (size_t)op->gcap, op->stream));
   LHIP(op, hipMemsetAsync(d2, 0, 16, op->stream));
-  if (op->n_log)
-    hipLaunchKernelGGL(k_mark_lists, dim3(grid_for(op->n_log)), dim3(256), 0, op->stream, op->S, op->n_log, has);
-  hipLaunchKernelGGL(k_count_state, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, op->c, op->S, has, d2);
+  if (sessions(op)) {
+    hipLaunchKernelGGL(k_sl_count_state, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, op->c, op->S, d2);
+  } else {
+    if (op->n_log)
+      hipLaunchKernelGGL(k_mark_lists, dim3(grid_for(op->n_log)), dim3(256), 0, op->stream, op->S, op->n_log, has);
+    hipLaunchKernelGGL(k_count_state, dim3(grid_for(op->gcap)), dim3(256), 0, op->stream, op->c, op->S, has, d2);
+  }
   LHIP(op, hipMemcpyAsync(h2, d2, 16, hipMemcpyDeviceToHost, op->stream));
   LRET(read_ctr(op));
   dfree(has);
@@ -1483,6 +2172,7 @@ int fw_list_snapshot_key_group(fw_list* op, int32_t key_group, const fw_list_sta
                                int64_t cap_elems, int64_t* n_lists, int64_t* n_elems) {
   if (!op) return FW_ERR_ARG;
   (void)hipSetDevice(op->device);
+  if (sessions(op)) return set_err(op, FW_ERR_UNSUPPORTED, "session windows' list state is not offered for snapshots");
   if ((uint32_t)(key_group - op->c.kg0) >= (uint32_t)op->c.nkg)
     return set_err(op, FW_ERR_KEY_GROUP, "key group %d is not in the handle's KeyGroupRange", key_group);
   // the key group's lists: its live groups, and its live elements grouped by list in list order
@@ -1544,6 +2234,7 @@ int fw_list_restore_key_group(fw_list* op, int32_t key_group, const fw_list_stat
                               int64_t n_elems) {
   if (!op || (n_lists && !src)) return set_err(op, FW_ERR_ARG, "invalid arguments");
   (void)hipSetDevice(op->device);
+  if (sessions(op)) return set_err(op, FW_ERR_UNSUPPORTED, "session windows' list state is not offered for snapshots");
   if ((uint32_t)(key_group - op->c.kg0) >= (uint32_t)op->c.nkg)
     return set_err(op, FW_ERR_KEY_GROUP, "key group %d is not in the handle's KeyGroupRange", key_group);
   if (n_lists == 0) return FW_OK;

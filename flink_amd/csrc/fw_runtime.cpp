@@ -442,6 +442,39 @@ int put_status_field(fw_op* op, T Status::*field) {
   return FW_OK;
 }
 
+// FW_AGG_ROW's blocks are small (a RowAcc per value column), so its pool covers every slot the table can hold (the
+// regions' load limit; merged and purged windows keep their slots until k_fire rebuilds the region) and grows with
+// the table: a push cannot run it dry, however few entries were expected
+int64_t row_pool_blocks(const DevCfg& c) { return (int64_t)c.P * region_limit(c.log_r) + 1024; }
+
+// the block pool to `blocks` blocks, contents, free stack and deferred list kept (stream idle)
+int grow_pool(fw_op* op, int64_t blocks) {
+  DevCfg& c = op->dc;
+  if (blocks <= c.pool_blocks) return FW_OK;
+  if (blocks >= (int64_t(1) << 32)) return set_err(op, FW_ERR_CAPACITY, "accumulator block pool would exceed 2^32 blocks");
+  uint8_t* np = nullptr;
+  uint32_t *nf = nullptr, *nd = nullptr;
+  const size_t ob = (size_t)(c.pool_blocks * c.pool_bytes), nb = (size_t)(blocks * c.pool_bytes);
+  HIP_OR_RETURN(op, dmalloc(&np, nb));
+  HIP_OR_RETURN(op, dmalloc(&nf, (size_t)blocks));
+  HIP_OR_RETURN(op, dmalloc(&nd, (size_t)blocks));
+  HIP_OR_RETURN(op, hipMemcpyAsync(np, c.pool, ob, hipMemcpyDeviceToDevice, op->stream));
+  HIP_OR_RETURN(op, hipMemsetAsync(np + ob, 0, nb - ob, op->stream));  // (blocks start at zero)
+  HIP_OR_RETURN(op, hipMemcpyAsync(nf, c.pool_free, (size_t)c.pool_blocks * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                   op->stream));
+  HIP_OR_RETURN(op, hipMemcpyAsync(nd, c.pool_defer, (size_t)c.pool_blocks * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                   op->stream));
+  HIP_OR_RETURN(op, hipStreamSynchronize(op->stream));
+  dfree(c.pool);
+  dfree(c.pool_free);
+  dfree(c.pool_defer);
+  c.pool = np;
+  c.pool_free = nf;
+  c.pool_defer = nd;
+  c.pool_blocks = blocks;
+  return FW_OK;
+}
+
 // grow every region to new_log_r, re-inserting the live entries (stream idle on exit)
 int grow_table(fw_op* op, int new_log_r) {
   if (new_log_r > 30) return set_err(op, FW_ERR_CAPACITY, "state region would exceed 2^30 slots");
@@ -469,11 +502,15 @@ int grow_table(fw_op* op, int new_log_r) {
   op->dc = nc;
   op->table_slots = (int64_t)nc.P << nc.log_r;
   op->grows++;
+  if (op->dc.agg == FW_AGG_ROW && (rc = grow_pool(op, row_pool_blocks(op->dc)))) return rc;
   if (op->dc.agg == FW_AGG_TDIGEST) {  // the compression's per-slot index follows the table
     if (op->table_slots >= (int64_t(1) << 31)) return set_err(op, FW_ERR_CAPACITY, "t-digest table would exceed 2^31 slots");
     dfree(op->td.lidx);
     HIP_OR_RETURN(op, dmalloc(&op->td.lidx, (size_t)op->table_slots));
     op->td.lidx_slots = op->table_slots;
+    dfree(op->td.dcnt);  // (zero between pushes)
+    HIP_OR_RETURN(op, dmalloc(&op->td.dcnt, (size_t)op->table_slots));
+    HIP_OR_RETURN(op, hipMemsetAsync(op->td.dcnt, 0, (size_t)op->table_slots * sizeof(uint32_t), op->stream));
     if (op->td.mover) {  // (no override is set between pushes)
       dfree(op->td.mover);
       HIP_OR_RETURN(op, dmalloc(&op->td.mover, (size_t)op->table_slots));
@@ -1017,11 +1054,6 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
                               "Long item column");
     unsupported = true;
   }
-  if (!msg[0] && cfg.aggregate == FW_AGG_HLL && cfg.assigner == FW_SESSION && cfg.purging) {
-    snprintf(msg, sizeof msg, "the HyperLogLog aggregate over session windows is offered with EventTimeTrigger (a "
-                              "purged session would keep its window with empty registers)");
-    unsupported = true;
-  }
   const int32_t td_delta = cfg.tdigest_compression ? cfg.tdigest_compression : 100;
   if (cfg.aggregate == FW_AGG_TDIGEST && cfg.tdigest_quantiles[0] == 0 && cfg.tdigest_quantiles[1] == 0 &&
       cfg.tdigest_quantiles[2] == 0) {
@@ -1034,11 +1066,13 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
   for (int i = 0; i < 3 && !msg[0] && cfg.aggregate == FW_AGG_TDIGEST; i++)
     if (!(cfg.tdigest_quantiles[i] >= 0.0 && cfg.tdigest_quantiles[i] <= 1.0))
       snprintf(msg, sizeof msg, "t-digest quantiles must be in [0, 1]");
-  if (!msg[0] && cfg.aggregate == FW_AGG_TDIGEST &&
-      (cfg.value_type != FW_VAL_F64 || (cfg.assigner == FW_SESSION && cfg.purging) ||
-       (cfg.allowed_lateness != 0 && cfg.purging))) {
-    snprintf(msg, sizeof msg, "the t-digest aggregate is offered over a Double field for tumbling, sliding and session "
-                              "windows (PurgingTrigger only for tumbling / sliding windows without allowed lateness)");
+  if (!msg[0] && cfg.aggregate == FW_AGG_TDIGEST && cfg.value_type != FW_VAL_F64) {
+    snprintf(msg, sizeof msg, "the t-digest aggregate is offered over a Double field");
+    unsupported = true;
+  }
+  if (!msg[0] && cfg.aggregate == FW_AGG_TDIGEST && cfg.assigner == FW_SLIDING && cfg.slide > 0 &&
+      (cfg.size + cfg.slide - 1) / cfg.slide > 4096) {
+    snprintf(msg, sizeof msg, "the t-digest aggregate takes at most 4096 windows per element");
     unsupported = true;
   }
   if (!msg[0] && cfg.aggregate == FW_AGG_ROW) {
@@ -1192,8 +1226,12 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     c.pool_bytes = ((int64_t)sizeof(RowAcc) * c.row_nc + 15) / 16 * 16;
     op->dig_stride = 1 + (int64_t)c.row_ns;
   }
+  // regions sized for the expected entries at 1/FW_TABLE_SLACK load (default 4: 25 %; the limit is 3/4)
+  const int64_t slack = getenv("FW_TABLE_SLACK") ? std::max(1, atoi(getenv("FW_TABLE_SLACK"))) : c.dense ? 2 : 4;
+  c.log_r = std::max(8, ilog2(slack * ((expected + c.P - 1) / c.P)));  // (dense: a region's groups, densely)
   if (c.pool_bytes) {
     c.pool_blocks = std::max<int64_t>(1024, expected + expected / 4);
+    if (c.agg == FW_AGG_ROW) c.pool_blocks = std::max(c.pool_blocks, row_pool_blocks(c));
     HIP_OR_RETURN(op, dmalloc(&c.pool, (size_t)(c.pool_blocks * c.pool_bytes)));
     if (c.agg == FW_AGG_HLL || c.agg == FW_AGG_ROW)  // registers / row accumulators start at zero (and are zeroed
       HIP_OR_RETURN(op, hipMemsetAsync(c.pool, 0, (size_t)(c.pool_blocks * c.pool_bytes), op->stream));  // when freed)
@@ -1202,9 +1240,6 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     HIP_OR_RETURN(op, dmalloc(&c.pool_ctr, 3));
     HIP_OR_RETURN(op, hipMemsetAsync(c.pool_ctr, 0, 3 * sizeof(int32_t), op->stream));
   }
-  // regions sized for the expected entries at 1/FW_TABLE_SLACK load (default 4: 25 %; the limit is 3/4)
-  const int64_t slack = getenv("FW_TABLE_SLACK") ? std::max(1, atoi(getenv("FW_TABLE_SLACK"))) : c.dense ? 2 : 4;
-  c.log_r = std::max(8, ilog2(slack * ((expected + c.P - 1) / c.P)));  // (dense: a region's groups, densely)
   op->table_slots = (int64_t)c.P << c.log_r;
 
   op->max_batch = cfg.max_batch > 0 ? std::min<int64_t>(cfg.max_batch, int64_t(1) << 31) : (int64_t(1) << 24);
@@ -1247,13 +1282,24 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
       HIP_OR_RETURN(op, dmalloc(&t.gs[b], (size_t)mi));
       HIP_OR_RETURN(op, dmalloc(&t.v[b], (size_t)mi));
     }
-    t.tmp_bytes = fwdev::tdigest_sort_bytes(mi);
-    HIP_OR_RETURN(op, dmalloc((uint8_t**)&t.tmp, t.tmp_bytes));
     HIP_OR_RETURN(op, dmalloc(&t.binv, (size_t)c.pool_blocks));
     HIP_OR_RETURN(op, hipMemsetAsync(t.binv, 0xff, (size_t)c.pool_blocks * sizeof(uint32_t), op->stream));
-    HIP_OR_RETURN(op, dmalloc(&t.fixbm, (size_t)((mi + 31) / 32)));
+    // the grouping and the sorts (launch_tdigest): per digest its count / run start, per position its digest, the
+    // runs for the LDS sort (digests of 65 .. 4096 values, and the MSD bins: at most 2 per 2048 values of a long run
+    // per level) and for the MSD levels (runs of more than 4096 values), their key ranges and bins
+    HIP_OR_RETURN(op, dmalloc(&t.dcnt, (size_t)op->table_slots));
+    HIP_OR_RETURN(op, hipMemsetAsync(t.dcnt, 0, (size_t)op->table_slots * sizeof(uint32_t), op->stream));
+    HIP_OR_RETURN(op, dmalloc(&t.gsort, (size_t)mi));
+    t.lrun_cap = mi / 48 + 4096;
+    t.brun_cap = mi / 4096 + 2;
+    HIP_OR_RETURN(op, dmalloc(&t.lrun, (size_t)t.lrun_cap));
+    for (int b = 0; b < 3; b++) HIP_OR_RETURN(op, dmalloc(&t.brun[b], (size_t)t.brun_cap));
+    HIP_OR_RETURN(op, dmalloc(&t.msd, (size_t)t.brun_cap));
+    HIP_OR_RETURN(op, dmalloc(&t.spl, (size_t)t.brun_cap * 2047));
+    HIP_OR_RETURN(op, dmalloc(&t.hist, (size_t)t.brun_cap * 4096));
+    HIP_OR_RETURN(op, dmalloc(&t.lctr, 5));
     HIP_OR_RETURN(op, dmalloc(&t.tslot, (size_t)mi));
-    HIP_OR_RETURN(op, dmalloc(&t.tbeg, (size_t)mi));
+    HIP_OR_RETURN(op, dmalloc(&t.tbeg, (size_t)mi + 1));  // (+ the runs' end)
     HIP_OR_RETURN(op, dmalloc(&t.ctr, 3));
     // a wave-tier digest has more than FW_TD_T1 - delta/2 values in the batch, a large one more than
     // FW_TD_T3 - delta/2
@@ -1385,10 +1431,15 @@ void fw_destroy(fw_op* op) {
       dfree(t.gs[b]);
       dfree(t.v[b]);
     }
-    uint8_t* tmp = (uint8_t*)t.tmp;
-    dfree(tmp);
     dfree(t.binv);
-    dfree(t.fixbm);
+    dfree(t.dcnt);
+    dfree(t.gsort);
+    dfree(t.lrun);
+    for (int b = 0; b < 3; b++) dfree(t.brun[b]);
+    dfree(t.msd);
+    dfree(t.spl);
+    dfree(t.hist);
+    dfree(t.lctr);
     dfree(t.tslot);
     dfree(t.tbeg);
     dfree(t.ctr);

@@ -43,6 +43,8 @@ class GpuListWindowOperator:
         cfg = assigner.config()
         c.assigner = cfg["assigner"]
         c.size, c.slide, c.offset = cfg.get("size", 0), cfg.get("slide", 0), cfg.get("offset", 0)
+        if "gap" in cfg:  # EventTimeSessionWindows: the session gap (the merging branch, EvictingWindowOperator:110-170)
+            c.size = cfg["gap"]
         c.value_type = VALUE_TYPES[value_type]
         c.key_kind = _KEY_KINDS[key_type]
         c.trigger = N.FW_TRIGGER_COUNT if isinstance(nested, CountTrigger) else N.FW_TRIGGER_EVENT_TIME

@@ -352,7 +352,7 @@ class HyperLogLog:
     oracle/window_oracle.h).  add = register max of the item's hash; merge = register-wise max;
     getResult = (count, estimate).  Fired rows: count, sum = estimate (f64 bits), min = zero registers,
     max = the low 64 bits of sum_j 2^(65 - p - M[j]) (an exact register checksum).  Offered on the GPU
-    for tumbling windows without allowed lateness."""
+    for tumbling, sliding and session windows, with allowed lateness and PurgingTrigger."""
     precision: int = 14
     value_type: str = "long"
 
@@ -413,7 +413,8 @@ class TDigest:
     micro-batch (push) compresses the values it added into the centroids (AggregateFunction.merge of the
     batch's digest); getResult = (count, the quantiles `quantiles`).  Fired rows: count, sum / min / max =
     the three quantile estimates (f64 bits).  With export=True the operator also keeps each fired row's
-    centroids (GpuWindowOperator.drain_digests).  Offered for tumbling windows without allowed lateness."""
+    centroids (GpuWindowOperator.drain_digests).  Offered for tumbling, sliding and session windows, with allowed
+    lateness and PurgingTrigger."""
     compression: int = 100
     quantiles: tuple = (0.5, 0.95, 0.99)
     export: bool = False

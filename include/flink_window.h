@@ -570,7 +570,7 @@ int fw_wire_encode_device(fw_wire* w, const fw_rows* rows, int64_t n, int32_t f6
 #define FW_EVICT_TIME 2
 #define FW_EVICT_DELTA 3
 typedef struct fw_list_config {
-  int32_t assigner;          /* FW_TUMBLING / FW_SLIDING / FW_GLOBAL                              */
+  int32_t assigner;          /* FW_TUMBLING / FW_SLIDING / FW_GLOBAL / FW_SESSION (size = the gap)  */
   int32_t value_type;        /* FW_VAL_*                                                          */
   int32_t key_kind;          /* FW_KEY_*                                                          */
   int32_t trigger;           /* FW_TRIGGER_*                                                      */

@@ -8,8 +8,8 @@ from collections import Counter
 import numpy as np
 import pytest
 
-from flink_amd import (CountEvictor, CountTrigger, DeltaEvictor, EventTimeTrigger, GlobalWindows, PurgingTrigger,
-                       SlidingEventTimeWindows, TimeEvictor, TumblingEventTimeWindows)
+from flink_amd import (CountEvictor, CountTrigger, DeltaEvictor, EventTimeSessionWindows, EventTimeTrigger,
+                       GlobalWindows, PurgingTrigger, SlidingEventTimeWindows, TimeEvictor, TumblingEventTimeWindows)
 from oracle import oracle as orc
 from tests.kat_util import expected_counters, load_kats, replay, replay_list_phases, row_counters
 
@@ -20,9 +20,11 @@ KEYMAP = KATS["keys"]
 _VT = {"i64": "long", "i32": "int", "f64": "double", "i16": "short", "i8": "byte", "f32": "float"}
 
 
-def _assigner(kind, size=0, slide=0, offset=0):
+def _assigner(kind, size=0, slide=0, offset=0, gap=0):
     if kind == "global":
         return GlobalWindows.create()
+    if kind == "session":
+        return EventTimeSessionWindows.with_gap(gap)
     if kind == "tumbling":
         return TumblingEventTimeWindows.of(size, offset)
     return SlidingEventTimeWindows.of(size, slide, offset)
@@ -35,19 +37,19 @@ def _evictor(kind, after, arg, threshold):
 
 def _pair(assigner="tumbling", size=0, slide=0, offset=0, lateness=0, trigger="event_time", trigger_count=0,
           purging=False, evictor="none", evict_after=False, evict_arg=0, threshold=0.0, side_output=False,
-          value_type="i64", **gpu_kw):
+          value_type="i64", gap=0, **gpu_kw):
     """(GPU operator, oracle) of one configuration"""
     from flink_amd.listwindow import GpuListWindowOperator
     trig = CountTrigger.of(trigger_count) if trigger == "count" else EventTimeTrigger.create()
     if purging:
         trig = PurgingTrigger.of(trig)
-    gpu = GpuListWindowOperator(_assigner(assigner, size, slide, offset), trig,
+    gpu = GpuListWindowOperator(_assigner(assigner, size, slide, offset, gap), trig,
                                 _evictor(evictor, evict_after, evict_arg, threshold), allowed_lateness=lateness,
                                 side_output=side_output, value_type=_VT[value_type], **gpu_kw)
-    ref = orc.ListWindowOracle(assigner=assigner, size=size, slide=slide, offset=offset, lateness=lateness,
-                               trigger=trigger, trigger_count=trigger_count, purging=purging, evictor=evictor,
-                               evict_after=evict_after, evict_arg=evict_arg, threshold=threshold,
-                               side_output=side_output, value_type=value_type)
+    kw = dict(gap=gap) if assigner == "session" else dict(size=size, slide=slide, offset=offset)
+    ref = orc.ListWindowOracle(assigner=assigner, lateness=lateness, trigger=trigger, trigger_count=trigger_count,
+                               purging=purging, evictor=evictor, evict_after=evict_after, evict_arg=evict_arg,
+                               threshold=threshold, side_output=side_output, value_type=value_type, **kw)
     return gpu, ref
 
 
@@ -334,3 +336,152 @@ def test_gpu_list_map_growth_bounded():
     assert took < 20, took
     assert len(rows) == n and int(rows["count"].sum()) == n
     assert np.array_equal(np.sort(rows["key"]), np.sort(keys))
+
+
+# ---------------------------------------------------------------- session windows (the merging branch)
+@pytest.mark.parametrize("name", sorted(KATS["list_session_cases"]))
+def test_gpu_list_session_kats(name):
+    # WindowedStream.apply over EventTimeSessionWindows (EvictingWindowOperator / WindowOperator merging branch,
+    # EvictingWindowOperator.java:110-170, WindowOperator.java:297-370) against WindowOperatorTest's session sequences
+    # (lateness, purging, side output): the rows, and every firing's contents equal to the oracle's
+    case = next(c for c in KATS["operator_cases"] if c["name"] == name)
+    c = case["cfg"]
+    gpu, ref = _pair("session", gap=c["gap"], lateness=c["lateness"], purging=c["purging"],
+                     side_output=c["side_output"], value_type="i32")
+    gpu = replay(case, KEYMAP, lambda _: gpu, flush_elements=True)
+    ref = replay(case, KEYMAP, lambda _: ref, flush_elements=False)
+    side = [dict(key=int(r["key"]), ts=int(r["ts"]), val=int(r["val"]), epoch=int(r["epoch"]))
+            for r in gpu.side_rows()]
+    got, got_side = row_counters(gpu.rows(), side, case, with_window=True)
+    exp, exp_side = expected_counters(case, KEYMAP, with_window=True)
+    assert got == exp
+    assert got_side == exp_side
+    _assert_same(gpu, ref)
+    gpu.close()
+
+
+def _hashset_first(wins):
+    """the first of TimeWindows in java.util.HashSet order (TimeWindow.hashCode = longToIntWithBitMixing(start +
+    end), bucket (h ^ h >>> 16) & 15; an independent restatement for the test)"""
+    def mix(x):
+        M = (1 << 64) - 1
+        x &= M
+        x = ((x ^ (x >> 30)) * 0xbf58476d1ce4e5b9) & M
+        x = ((x ^ (x >> 27)) * 0x94d049bb133111eb) & M
+        return (x ^ (x >> 31)) & 0xffffffff
+    b = [(mix(s + e) ^ (mix(s + e) >> 16)) & 15 for s, e in wins]
+    return min(range(len(wins)), key=lambda i: (b[i], i))
+
+
+@pytest.mark.parametrize("first", [0, 1])
+def test_gpu_list_session_bridge_order(first):
+    # a bridging element merges two sessions: the merged list is the state window of the first merged window in
+    # HashSet order, then the other's list (MergingWindowSet.addWindow, MergingWindowSet.java:150-225;
+    # AbstractHeapMergingState.mergeNamespaces :67-93 with HeapListState's addAll), then the element
+    gap = 10
+    for a0 in range(0, 400):
+        A, B = (a0, a0 + gap + 1), (a0 + 2 * gap, a0 + 3 * gap + 1)
+        if (_hashset_first([A, B]) == 0) == (first == 0):
+            break
+    gpu, ref = _pair("session", gap=gap)
+    for h in (gpu, ref):
+        h.process(np.array([1, 1, 1, 1]), np.array([A[0], B[0], A[0] + 1, B[0] + 1]), np.array([1, 2, 3, 4]))
+        h.process(np.array([1]), np.array([A[0] + gap]), np.array([5]))
+        h.watermark((1 << 63) - 1)
+    (r, el), = gpu.contents()
+    assert (r["start"], r["end"]) == (A[0], B[1]) and r["count"] == 5
+    assert list(el["val"]) == ([1, 3, 2, 4, 5] if first == 0 else [2, 4, 1, 3, 5])
+    _assert_same(gpu, ref)
+    gpu.close()
+
+
+def _zipf_stream(seed, n, keys, span, jitter, s=1.1):
+    rng = np.random.default_rng(seed)
+    w = 1.0 / np.arange(1, keys + 1) ** s
+    k = rng.choice(keys, n, p=w / w.sum()).astype(np.int64) * 7919 + 13
+    t = np.arange(n, dtype=np.int64) * span // n - rng.integers(0, jitter, n, dtype=np.int64)
+    v = rng.integers(-1000, 1000, n, dtype=np.int64)
+    return k, t, v
+
+
+SESSION_CONFIGS = [
+    dict(gap=30),
+    dict(gap=30, lateness=200),
+    dict(gap=30, lateness=200, purging=True, side_output=True),
+    dict(gap=50, purging=True),
+    dict(gap=30, evictor="count", evict_arg=3),
+    dict(gap=30, lateness=150, evictor="count", evict_arg=2, evict_after=True),
+    dict(gap=40, evictor="time", evict_arg=25),
+    dict(gap=40, lateness=100, evictor="time", evict_arg=10, evict_after=True, purging=True),
+    dict(gap=30, evictor="delta", threshold=300.0),
+    dict(gap=20, lateness=300, evictor="delta", threshold=600.0, evict_after=True, side_output=True),
+]
+
+
+@pytest.mark.parametrize("cfg", SESSION_CONFIGS, ids=[str(i) for i in range(len(SESSION_CONFIGS))])
+@pytest.mark.parametrize("value_type,zipf", [("i64", False), ("f64", True)], ids=["i64-uniform", "f64-zipf"])
+def test_gpu_list_sessions_vs_oracle(cfg, value_type, zipf):
+    # f4 with merging windows: seeded streams (out of order by up to 150 ms against a 100 ms watermark bound, so
+    # elements arrive behind in-flight sessions, bridge them, fire late sessions again under allowed lateness, or
+    # are dropped / side-output), every firing's row and contents in list order bit-exact against the oracle
+    gpu, ref = _pair("session", value_type=value_type, **cfg)
+    k, t, v = (_zipf_stream if zipf else _stream)(23 + len(str(cfg)), 20000, 300 if zipf else 400, 20000, 150)
+    if value_type == "f64":
+        v = (v.astype(np.float64) * 0.37).view(np.int64)
+    wm = -10**9
+    for b in range(10):
+        sl = slice(b * 2000, (b + 1) * 2000)
+        vals = v[sl].view(np.float64) if value_type == "f64" else v[sl]
+        gpu.process(k[sl], t[sl], vals)
+        ref.process(k[sl], t[sl], v[sl])
+        wm = max(wm, int(t[sl].max()) - 100)
+        if b % 3 != 1:
+            gpu.watermark(wm)
+            ref.watermark(wm)
+    for w in (wm + 500, (1 << 63) - 1):
+        gpu.watermark(w)
+        ref.watermark(w)
+    _assert_same(gpu, ref)
+    assert gpu.late_dropped == ref.late_dropped
+    if cfg.get("side_output"):
+        gs = sorted(map(tuple, np.stack([gpu.side_rows()[f] for f in ("epoch", "key", "ts", "val")], 1).tolist()))
+        e, kk, ts, vv = ref.side_rows()
+        assert gs == sorted(zip(e.tolist(), kk.tolist(), ts.tolist(), vv.tolist()))
+    rows = gpu.rows()
+    assert (rows["end"] - rows["start"] > cfg["gap"]).any()  # sessions merged
+    gpu.close()
+
+
+def test_gpu_list_sessions_state_counters_and_growth():
+    # a map and a log far smaller than the stream (rebuilds, compactions, tombstones of merged sessions) with the
+    # state counters checked mid-stream while sessions are open under allowed lateness
+    gpu, ref = _pair("session", gap=25, lateness=100, evictor="count", evict_arg=5, expected_elements=1024)
+    k, t, v = _stream(31, 100000, 3000, 50000, 60)
+    for b in range(10):
+        sl = slice(b * 10000, (b + 1) * 10000)
+        gpu.process(k[sl], t[sl], v[sl])
+        ref.process(k[sl], t[sl], v[sl])
+        gpu.watermark(int(t[sl].max()) - 50)
+        ref.watermark(int(t[sl].max()) - 50)
+        st = gpu.stats()
+        assert st["keyed_state_entries"] == ref.num_state_entries
+        assert st["event_time_timers"] == ref.num_timers
+    gpu.watermark((1 << 63) - 1)
+    ref.watermark((1 << 63) - 1)
+    _assert_same(gpu, ref)
+    assert gpu.stats()["table_grows"] > 0
+    gpu.close()
+
+
+def test_gpu_list_sessions_refusals():
+    from flink_amd import _native as N
+    from flink_amd.listwindow import GpuListWindowOperator
+    with pytest.raises(N.NativeError) as e:  # (CountTrigger over merging windows: not offered)
+        GpuListWindowOperator(EventTimeSessionWindows.with_gap(10), CountTrigger.of(3))
+    assert e.value.code == N.FW_ERR_UNSUPPORTED
+    op = GpuListWindowOperator(EventTimeSessionWindows.with_gap(10))
+    op.process(np.array([1, 2]), np.array([5, 6]), np.array([1, 2]))
+    with pytest.raises(N.NativeError) as e:  # (the merging window set is not in fw_list_state)
+        op.snapshot_key_group(0)
+    assert e.value.code == N.FW_ERR_UNSUPPORTED
+    op.close()

@@ -943,23 +943,33 @@ def test_gpu_hll_register_blocks_are_recycled():
 HLL_SESSION_CFGS = [dict(gap=300, lateness=0, zipf=1.1, bound=200, jitter=300),
                     dict(gap=300, lateness=500, zipf=1.1, bound=400, jitter=1500),
                     dict(gap=50, lateness=200, zipf=None, bound=100, jitter=400),
-                    dict(gap=2000, lateness=0, zipf=1.3, bound=200, jitter=200)]
+                    dict(gap=2000, lateness=0, zipf=1.3, bound=200, jitter=200),
+                    dict(gap=300, lateness=0, zipf=1.1, bound=200, jitter=300, purging=True),
+                    dict(gap=300, lateness=500, zipf=1.1, bound=400, jitter=1500, purging=True),
+                    dict(gap=50, lateness=200, zipf=None, bound=100, jitter=400, purging=True)]
 
 
-@pytest.mark.parametrize("cfg", HLL_SESSION_CFGS, ids=["zipf", "zipf-lateness", "uniform-lateness", "long-gap"])
+@pytest.mark.parametrize("cfg", HLL_SESSION_CFGS, ids=["zipf", "zipf-lateness", "uniform-lateness", "long-gap",
+                                                       "zipf-purging", "zipf-lateness-purging",
+                                                       "uniform-lateness-purging"])
 def test_gpu_hll_sessions_vs_oracle(cfg):
     # a10: HyperLogLog over EventTimeSessionWindows (WindowedStream.aggregate with any assigner, WindowedStream.java:
     # 687-852).  Sessions merge (MergingWindowSet.addWindow, MergingWindowSet.java:150-225) and their accumulators with
     # them (AbstractHeapMergingState.mergeNamespaces, AbstractHeapMergingState.java:67-93; AggregateFunction.merge,
     # AggregateFunction.java:160): the register max of the merged sessions' blocks -- in the parallel flush, in the
     # ordered replay of late elements (late firings, lateness), and across batches.  Registers bit-exact.
-    from flink_amd import HyperLogLog
+    # PurgingTrigger (WindowOperator.java:391-403, 454-463): a firing clears the session's registers (zeroed block)
+    # and the session stays in its MergingWindowSet, empty, until later elements or merges fill it again.
+    from flink_amd import HyperLogLog, PurgingTrigger
     from flink_amd.operator import GpuWindowOperator
     batches, wms = _stream(200_000, 20_000, 3000, bound=cfg["bound"], jitter=cfg["jitter"], rate=100_000,
                            zipf=cfg["zipf"])
-    gpu = GpuWindowOperator(EventTimeSessionWindows.with_gap(cfg["gap"]), HyperLogLog(10),
+    purging = cfg.get("purging", False)
+    trig = PurgingTrigger.of(EventTimeTrigger.create()) if purging else None
+    gpu = GpuWindowOperator(EventTimeSessionWindows.with_gap(cfg["gap"]), HyperLogLog(10), trigger=trig,
                             allowed_lateness=cfg["lateness"], expected_entries=20_000)
-    ref = orc.WindowOperatorOracle(assigner="session", gap=cfg["gap"], lateness=cfg["lateness"], hll_p=10)
+    ref = orc.WindowOperatorOracle(assigner="session", gap=cfg["gap"], lateness=cfg["lateness"], hll_p=10,
+                                   purging=purging)
     for (k, t, v), wm in zip(batches, wms):
         gpu.process(k, t, v)
         ref.process(k, t, v)
@@ -994,10 +1004,9 @@ def test_gpu_hll_refuses_unsupported_shapes():
     from flink_amd import HyperLogLog, PurgingTrigger
     from flink_amd import _native as N
     from flink_amd.operator import GpuWindowOperator
-    with pytest.raises(N.NativeError) as e:
-        GpuWindowOperator(EventTimeSessionWindows.with_gap(3000), HyperLogLog(12),
-                          trigger=PurgingTrigger.of(EventTimeTrigger.create()))
-    assert e.value.code == N.FW_ERR_UNSUPPORTED
+    # (sessions with PurgingTrigger are offered: test_gpu_hll_sessions_vs_oracle)
+    GpuWindowOperator(EventTimeSessionWindows.with_gap(3000), HyperLogLog(12),
+                      trigger=PurgingTrigger.of(EventTimeTrigger.create())).close()
     with pytest.raises(N.NativeError):
         GpuWindowOperator(TumblingEventTimeWindows.of(1000), HyperLogLog(20))
 

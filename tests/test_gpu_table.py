@@ -108,10 +108,12 @@ CFGS = [dict(assigner="tumbling", size=1000), dict(assigner="sliding", size=3000
 def test_gpu_table_vs_oracle(cfg, small_table):
     # Zipf(1.1) keys, out-of-order timestamps (jitter 900 ms against a 300 ms bound: late records are dropped and, for
     # sessions, arrive behind in-flight sessions: the ordered path), NULLs in every column; "grows": the table
-    # starts small, so the aggregate suspends mid-push, the table grows and the push resumes (the per-record column
-    # adds, which are not idempotent, must still count every record once)
+    # starts small (4 regions), so the aggregate suspends mid-push, the table and the Row accumulators' block pool
+    # grow and the push resumes (the per-record column adds, which are not idempotent, must still count every record
+    # once)
     steps = _stream(1 << 17, 1 << 14, 20_000, bound=300, jitter=900, rate=200_000)
-    gpu = _op(cfg, TYPES, SPECS, expected_entries=2000 if small_table else 0, max_batch=1 << 14)
+    small = dict(expected_entries=2000, max_parallelism=4, sub_partitions=1) if small_table else {}
+    gpu = _op(cfg, TYPES, SPECS, max_batch=1 << 14, **small)
     ref = orc.WindowOperatorOracle(**cfg, row=(TYPES, SPECS))
     for k, t, cols, nulls, wm in steps:
         gpu.process_row_batch(k, t, cols, nulls)

@@ -42,18 +42,20 @@ def _stream(n, batch, num_keys, rate, zipf=None, values="spread", seed=0x7D16, b
     return batches, wms
 
 
-def _run(batches, wms, delta, quantiles=(0.5, 0.95, 0.99), sliding=None, gap=None, lateness=0, **kw):
-    from flink_amd import EventTimeSessionWindows, SlidingEventTimeWindows
+def _run(batches, wms, delta, quantiles=(0.5, 0.95, 0.99), sliding=None, gap=None, lateness=0, purging=False, **kw):
+    from flink_amd import EventTimeSessionWindows, EventTimeTrigger, PurgingTrigger, SlidingEventTimeWindows
     from flink_amd.operator import GpuWindowOperator
     assigner = (SlidingEventTimeWindows.of(*sliding) if sliding else EventTimeSessionWindows.with_gap(gap) if gap
                 else TumblingEventTimeWindows.of(1000))
+    if purging:
+        kw["trigger"] = PurgingTrigger.of(EventTimeTrigger.create())
     gpu = GpuWindowOperator(assigner, TDigest(delta, quantiles, export=True), allowed_lateness=lateness, **kw)
     ref = (orc.WindowOperatorOracle(assigner="sliding", size=sliding[0], slide=sliding[1], tdigest=delta,
-                                    quantiles=quantiles, lateness=lateness) if sliding else
+                                    quantiles=quantiles, lateness=lateness, purging=purging) if sliding else
            orc.WindowOperatorOracle(assigner="session", gap=gap, tdigest=delta, quantiles=quantiles,
-                                    lateness=lateness) if gap else
+                                    lateness=lateness, purging=purging) if gap else
            orc.WindowOperatorOracle(assigner="tumbling", size=1000, tdigest=delta, quantiles=quantiles,
-                                    lateness=lateness))
+                                    lateness=lateness, purging=purging))
     g_rows, g_dig = [], []
     for epoch, ((k, t, v), wm) in enumerate(zip(batches, wms)):
         if len(k):
@@ -160,7 +162,28 @@ def test_gpu_tdigest_lateness_vs_oracle(sliding, lateness, zipf, jitter):
     assert len(np.unique(keys, axis=0)) < len(keys)  # windows fired more than once
 
 
-def test_gpu_tdigest_lateness_grows_mid_push(monkeypatch):
+@pytest.mark.parametrize("sliding,gap,lateness,zipf,jitter",
+                         [(None, 300, 0, 1.1, 200), (None, 300, 800, 1.1, 1200), (None, 100, 2000, None, 900),
+                          (None, None, 500, None, 900), (None, None, 3000, 1.1, 1500), ((2000, 500), None, 300, 1.1, 900)],
+                         ids=["sessions", "sessions-lateness", "sessions-uniform-lateness", "tumbling-lateness",
+                              "tumbling-hot-long", "sliding-lateness"])
+def test_gpu_tdigest_purging_vs_oracle(sliding, gap, lateness, zipf, jitter):
+    # PurgingTrigger (FIRE_AND_PURGE: WindowOperator.java:391-403, 454-463) with t-digests: a firing clears the
+    # window's state -- the centroids, and on the ordered path the push's values so far, which leave the push's
+    # compression (td_purge) -- and the window stays until its cleanup time: a session in its MergingWindowSet (an
+    # empty digest that later elements and merges fill again), a time window as empty state that a late element
+    # fills and fires again with only its own values.  Bit-exact against the oracle's state.erase.
+    batches, wms = _stream(200_000, 20_000, 3000, rate=100_000, zipf=zipf, jitter=jitter, bound=200)
+    g_rows, g_dig, r_rows, r_dig = _run(batches, wms, 40, sliding=sliding, gap=gap, lateness=lateness, purging=True,
+                                        expected_entries=60_000)
+    _assert_same(g_rows, g_dig, r_rows, r_dig, 40)
+    if lateness:
+        keys = np.stack([g_rows["key"], g_rows["start"]], axis=1)
+        assert len(np.unique(keys, axis=0)) < len(keys)  # windows fired (and purged) more than once
+
+
+@pytest.mark.parametrize("purging", [False, True], ids=["fire", "fire-and-purge"])
+def test_gpu_tdigest_lateness_grows_mid_push(monkeypatch, purging):
     # a burst of late elements for new windows within the allowed lateness, each key four times across the batch:
     # every element creates or joins a window on the ordered path and fires it, the regions (FW_TABLE_SLACK=1: sized
     # at the expected entries, ~196 per 256-slot region against a load limit of 192) run out of room, the ordered
@@ -175,10 +198,14 @@ def test_gpu_tdigest_lateness_grows_mid_push(monkeypatch):
     batches = [(k1, k1 % 1000, rng.normal(size=n)), (k2, k2 % 997, rng.normal(size=4 * m)),
                (k1[:0], k1[:0], np.zeros(0))]
     wms = [5000, 6000, (1 << 63) - 1]
+    # (purging: every firing empties the window, so each of a key's four late elements fires alone, and the
+    # purged values' items must stay out of the chains the grow rebuilds)
+    from flink_amd import EventTimeTrigger, PurgingTrigger
+    trig = PurgingTrigger.of(EventTimeTrigger.create()) if purging else None
     gpu = GpuWindowOperator(TumblingEventTimeWindows.of(1000), TDigest(40, export=True), allowed_lateness=1 << 40,
-                            expected_entries=n + m)
+                            expected_entries=n + m, trigger=trig)
     ref = orc.WindowOperatorOracle(assigner="tumbling", size=1000, tdigest=40, quantiles=(0.5, 0.95, 0.99),
-                                   lateness=1 << 40)
+                                   lateness=1 << 40, purging=purging)
     g_rows, g_dig = [], []
     for epoch, ((k, t, v), wm) in enumerate(zip(batches, wms)):
         if len(k):
@@ -227,9 +254,7 @@ def test_gpu_tdigest_refuses_unsupported_shapes():
                dict(assigner=EventTimeSessionWindows.with_gap(1000), allowed_lateness=10, trigger=purge),
                dict(allowed_lateness=10, trigger=purge),
                dict(assigner=SlidingEventTimeWindows.of(3000, 1000), allowed_lateness=10, trigger=purge)):
-        with pytest.raises(N.NativeError) as e:
-            GpuWindowOperator(kw.pop("assigner", TumblingEventTimeWindows.of(1000)), TDigest(100), **kw)
-        assert e.value.code == N.FW_ERR_UNSUPPORTED
+        GpuWindowOperator(kw.pop("assigner", TumblingEventTimeWindows.of(1000)), TDigest(100), **kw).close()  # offered
     with pytest.raises(N.NativeError) as e:
         GpuWindowOperator(TumblingEventTimeWindows.of(1000), TDigest(99))
     assert e.value.code == N.FW_ERR_ARG
