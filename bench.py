@@ -133,8 +133,10 @@ def impl_bytes(name, n, merged, fired=0, hll_p=0, panes_per_window=0, compact=Tr
         return 24 * n + rec * n
     if name == "k_aggregate":
         return rec * n + 128 * merged
-    if name == "k_tdigest":  # keys (read the record, write 12 B), one radix sort (8 passes of 12 B r+w), the tie
-        return rec * n + 12 * n + 8 * 24 * n + 12 * n + 24 * n + 24 * n  # check (12 B), decode (12 + 12), tiers (24)
+    if name == "k_tdigest":  # grouping (read the record; digest, rank and value key written, the rank rewritten),
+        # placement into the digests' runs (16 B read, 12 B written), the run sorts (8 B read and written; the hot
+        # keys' runs once more through a sample-sort pass, about half the values), the tiers (24)
+        return rec * n + 16 * n + 8 * n + 28 * n + 16 * n + 8 * n + 24 * n
     return None
 
 

@@ -1921,7 +1921,7 @@ __device__ __forceinline__ RowAcc* row_acc(const DevCfg& c, uint64_t blk) {
   return reinterpret_cast<RowAcc*>(c.pool + blk * (uint64_t)c.pool_bytes);
 }
 __device__ __forceinline__ bool row_float(const DevCfg& c, int j) {
-  return c.row_type[j] == FW_VAL_F64 || c.row_type[j] == FW_VAL_F32;
+  return c.row_ts[j] == FW_VAL_F64 || c.row_ts[j] == FW_VAL_F32;
 }
 // a value's order key (Double.compare order for a floating column, Scala's Ordering.Double / Float), and the min /
 // max encodings whose identity is 0 under an unsigned max: max = key ^ sign, min = ~(key ^ sign)
@@ -2006,7 +2006,7 @@ __device__ __forceinline__ int64_t row_narrow(int t, int64_t v) {
 }
 // getValue of aggregate s (oracle/window_oracle.cpp row_value): the value or NULL
 __device__ int64_t row_value(const DevCfg& c, const RowAcc* acc, int64_t cnt, int s, bool* null) {
-  const int fn = c.row_spec[s] >> 8, j = c.row_spec[s] & 0xff;
+  const int fn = c.row_ts[8 + s] >> 8, j = c.row_ts[8 + s] & 0xff;
   *null = false;
   if (fn == FW_ROW_COUNT_STAR) return cnt;
   const RowAcc a = acc[j];
@@ -2015,7 +2015,7 @@ __device__ int64_t row_value(const DevCfg& c, const RowAcc* acc, int64_t cnt, in
     *null = true;
     return 0;
   }
-  const int t = c.row_type[j];
+  const int t = c.row_ts[j];
   const double ds = __longlong_as_double((long long)a.lo);
   switch (fn) {
     case FW_ROW_SUM:

@@ -206,8 +206,8 @@ struct DevCfg {
   // its batch index, and its columns are read from the push's copy: column j of record i at row_cols[j * row_stride
   // + i], its null mask at row_nulls[i] (bit j = column j is NULL; nullptr = none)
   int32_t row_nc, row_ns;
-  int32_t row_type[8];
-  int32_t row_spec[16];
+  const int32_t* row_ts;  // [24] in HBM: the columns' types (8), then the aggregates (16) (kept out of DevCfg: a
+                          // kernel that changes its DevCfg copy holds it in registers and scratch)
   const int64_t* row_cols;
   const uint8_t* row_nulls;
   int64_t row_stride;

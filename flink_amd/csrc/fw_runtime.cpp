@@ -1221,8 +1221,13 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     c.f32 = 0;
     c.row_nc = cfg.row_columns;
     c.row_ns = cfg.row_aggregates;
-    for (int j = 0; j < 8; j++) c.row_type[j] = j < cfg.row_columns ? cfg.row_column_type[j] : 0;
-    for (int q = 0; q < 16; q++) c.row_spec[q] = q < cfg.row_aggregates ? cfg.row_aggregate[q] : 0;
+    int32_t ts[24];
+    for (int j = 0; j < 8; j++) ts[j] = j < cfg.row_columns ? cfg.row_column_type[j] : 0;
+    for (int q = 0; q < 16; q++) ts[8 + q] = q < cfg.row_aggregates ? cfg.row_aggregate[q] : 0;
+    int32_t* dts = nullptr;
+    HIP_OR_RETURN(op, dmalloc(&dts, 24));
+    HIP_OR_RETURN(op, hipMemcpy(dts, ts, sizeof ts, hipMemcpyHostToDevice));
+    c.row_ts = dts;
     c.pool_bytes = ((int64_t)sizeof(RowAcc) * c.row_nc + 15) / 16 * 16;
     op->dig_stride = 1 + (int64_t)c.row_ns;
   }
@@ -1426,6 +1431,8 @@ void fw_destroy(fw_op* op) {
   {
     double* q = const_cast<double*>(op->dc.td_qb);
     dfree(q);
+    int32_t* rts = const_cast<int32_t*>(op->dc.row_ts);
+    dfree(rts);
     TdBuf& t = op->td;
     for (int b = 0; b < 2; b++) {
       dfree(t.gs[b]);

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round evidence for one or more workloads (WORKLOADS, default c2): for each, with S timed steps (>= one firing
 # period) after W warmup steps:
-#   PMC passes FETCH_SIZE and WRITE_SIZE (one rocprofv3 run each, no trace domains) -> traffic_${ROUND:-r05}_$w.json
+#   PMC passes FETCH_SIZE and WRITE_SIZE (one rocprofv3 run each, no trace domains) -> traffic_${ROUND:-r06}_$w.json
 #   rocprofv3 --kernel-trace --stats of the bench with async input and with --sync-input (no HIP-event pass)
 #   the bench line itself (default flags, the traffic file above)
 #   tools/roofline_check.py: the line's frac / isolated frac recomputed from the traces
@@ -17,13 +17,13 @@ for w in ${WORKLOADS:-c2}; do
     (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $counters -d "$d/pmc/p$i" -o run --output-format csv \
         -- python3 "$R/bench.py" $ba --no-profile > "$d/pmc_p$i.log" 2>&1) || { echo "$w pmc $i rc=$?"; tail -5 "$d/pmc_p$i.log"; exit 1; }
   done
-  python3 tools/traffic.py "$d/pmc" --workload $w --steps $S --warmup $W --out "$d/traffic_${ROUND:-r05}_$w.json" > "$d/traffic.txt" || exit 1
+  python3 tools/traffic.py "$d/pmc" --workload $w --steps $S --warmup $W --out "$d/traffic_${ROUND:-r06}_$w.json" > "$d/traffic.txt" || exit 1
   for mode in async sync; do
     extra=""; [ $mode = sync ] && extra="--sync-input"
     (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$d/prof_$mode" -o run --output-format csv \
         -- python3 "$R/bench.py" $ba --no-profile $extra > "$d/prof_$mode.log" 2>&1) || { echo "$w prof $mode rc=$?"; tail -5 "$d/prof_$mode.log"; exit 1; }
   done
-  timeout -k 10 400 python3 -u bench.py $ba --traffic "$d/traffic_${ROUND:-r05}_$w.json" > "$d/bench.json" 2> "$d/bench.err" || { echo "$w bench rc=$?"; tail -5 "$d/bench.err"; exit 1; }
+  timeout -k 10 400 python3 -u bench.py $ba --traffic "$d/traffic_${ROUND:-r06}_$w.json" > "$d/bench.json" 2> "$d/bench.err" || { echo "$w bench rc=$?"; tail -5 "$d/bench.err"; exit 1; }
   python3 tools/roofline_check.py "$d/bench.json" --async-trace "$d/prof_async/run_kernel_trace.csv" \
       --sync-trace "$d/prof_sync/run_kernel_trace.csv" --steps $S --warmup $W --out "$d/roofline_check.json" > /dev/null || exit 1
   python3 - "$d" <<'PY'
