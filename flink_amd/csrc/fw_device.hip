@@ -4207,6 +4207,124 @@ __device__ int32_t td_merge_serial(const DevCfg& c, const double* qb, const uint
   return td_merge_run(c, qb, [&]() { return *p++; }, nn, old, no, out, W);
 }
 
+// td_merge_serial for the serial tier (k_td_small): the same merge, with the run's value keys and the old centroids
+// read TD_BN / TD_BO at a time into registers.  Element by element, every step of the merge waited for its own load
+// (the next key decides which stream the step takes); a block's loads are in flight together.
+#ifndef FW_TD_BN
+#define FW_TD_BN 8
+#endif
+#ifndef FW_TD_BO
+#define FW_TD_BO 4
+#endif
+constexpr int TD_BN = FW_TD_BN, TD_BO = FW_TD_BO;
+static_assert((TD_BN & (TD_BN - 1)) == 0 && (TD_BO & (TD_BO - 1)) == 0, "blocks of a power of two");
+__device__ int32_t td_merge_serial_blk(const DevCfg& c, const double* qb, const uint64_t* __restrict__ v, int64_t beg,
+                                       int64_t nn, const TdCent* __restrict__ old, int32_t no, TdCent* __restrict__ out,
+                                       int64_t W) {
+  const uint64_t* __restrict__ pv = v + beg;
+  uint64_t nbk[TD_BN];
+  double osb[TD_BO];
+  int64_t ocb[TD_BO];
+  auto fill_n = [&](int64_t i0) {
+#pragma unroll
+    for (int u = 0; u < TD_BN; u++) nbk[u] = i0 + u < nn ? pv[i0 + u] : 0ull;
+  };
+  auto fill_o = [&](int32_t j0) {
+#pragma unroll
+    for (int u = 0; u < TD_BO; u++) {
+      osb[u] = 0.0;
+      ocb[u] = 0;
+      if (j0 + u < no) {
+        const TdCent t = old[j0 + u];
+        osb[u] = t.sum;
+        ocb[u] = t.cum;
+      }
+    }
+  };
+  // element i of the current block (selects, not an indexed register array)
+  auto pick_n = [&](int64_t i) {
+    const int s = (int)(i & (TD_BN - 1));
+    uint64_t x = nbk[0];
+#pragma unroll
+    for (int u = 1; u < TD_BN; u++) x = s == u ? nbk[u] : x;
+    return x;
+  };
+  auto pick_o = [&](int32_t j, double& sum, int64_t& cum) {
+    const int s = j & (TD_BO - 1);
+    sum = osb[0];
+    cum = ocb[0];
+#pragma unroll
+    for (int u = 1; u < TD_BO; u++) {
+      sum = s == u ? osb[u] : sum;
+      cum = s == u ? ocb[u] : cum;
+    }
+  };
+  const double Wd = (double)W;
+  int64_t i = 0, cw = 0, gw = 0, cum_out = 0, prev_old = 0;
+  int32_t j = 0, k = 0;
+  if (nn) fill_n(0);
+  if (no) fill_o(0);
+  double osum = 0.0;
+  int64_t ocum = 0;
+  if (no) pick_o(0, osum, ocum);
+  uint64_t mk = no ? td_mean_key(osum, ocum) : 0;
+  uint64_t nk = nn ? pick_n(0) : 0;  // the next new value's key
+  double so = 0.0, sn = 0.0;
+  bool any_o = false, any_n = false;
+  TdTree tr;
+  tr.cnt = 0;
+  int b = 0, cur = -1;
+  auto emit = [&]() {
+    if (tr.cnt) td_fold(sn, any_n, tr.finish());
+    cum_out += gw;
+    out[k++] = TdCent{any_o && any_n ? so + sn : any_o ? so : sn, cum_out};
+    gw = 0;
+    any_o = any_n = false;
+    tr.cnt = 0;
+  };
+  while (i < nn || j < no) {
+    const bool take_new = j == no || (i < nn && nk <= mk);
+    double x;
+    int64_t w;
+    if (take_new) {
+      x = td_val(nk);
+      w = 1;
+      i++;
+      if (i < nn) {
+        if ((i & (TD_BN - 1)) == 0) fill_n(i);
+        nk = pick_n(i);
+      }
+    } else {
+      x = osum;
+      w = ocum - prev_old;
+      prev_old = ocum;
+      j++;
+      if (j < no) {
+        if ((j & (TD_BO - 1)) == 0) fill_o(j);
+        pick_o(j, osum, ocum);
+        mk = td_mean_key(osum, ocum - prev_old);
+      }
+    }
+    const double mid = (double)cw + (double)w * 0.5;
+    while (b + 1 < c.td_nb && Wd * qb[b + 1] <= mid) b++;
+    if (b != cur && gw > 0) emit();
+    cur = b;
+    if (take_new) {
+      tr.push(x);
+      if (tr.cnt == 64) {
+        td_fold(sn, any_n, tr.finish());
+        tr.cnt = 0;
+      }
+    } else {
+      td_fold(so, any_o, x);
+    }
+    gw += w;
+    cw += w;
+  }
+  if (gw > 0) emit();
+  return k;
+}
+
 // piecewise-linear quantile through (0, min), (centre_i, mean_i) ..., (W, max) (window_oracle.cpp td_quantile)
 __device__ double td_quantile(const TdCent* ce, int32_t n, int64_t W, double mn, double mx, double qv) {
   if (n == 0) return __longlong_as_double(0x7ff8000000000000ll);
@@ -4435,6 +4553,42 @@ constexpr int TD_TILE = 256 * TD_TILE_PT;
 constexpr int TD_MSD_BINS = 4096;  // per run: its sample sort's buckets (at most 2 * 2047 + 1)
 constexpr uint32_t TD_RUN_V1 = 0x80000000u;  // TdRun.len: the run's values are in v[1]
 
+// the digest's LDS slot in the workgroup's table, and this item's rank among the workgroup's items of the digest
+__device__ __forceinline__ uint32_t td_group_rank(uint32_t* hk, uint32_t* hc, uint32_t g) {
+  uint32_t h = (g * 0x9E3779B1u) >> (32 - TD_GHASH_LOG);
+  while (true) {
+    const uint32_t cur = __hip_atomic_load(&hk[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == g) break;
+    if (cur == TD_GEMPTY) {
+      const uint32_t prev = atomicCAS(&hk[h], TD_GEMPTY, g);
+      if (prev == TD_GEMPTY || prev == g) break;
+    }
+    h = (h + 1) & (TD_GHASH - 1);
+  }
+  // a hot digest's items (a Zipf stream's head keys fill whole chunks): the lanes of the wave that share the
+  // first active lane's digest take their ranks from one LDS add
+  const uint64_t act = __ballot(1);
+  const int lead = __ffsll((long long)act) - 1;
+  const uint32_t hl = (uint32_t)__shfl((int)h, lead, 64);
+  const uint64_t peers = __ballot(h == hl);
+  uint32_t rank;
+  if (h == hl) {
+    uint32_t base = 0;
+    if ((int)__lane_id() == lead) base = atomicAdd(&hc[h], (uint32_t)__popcll(peers));
+    base = (uint32_t)__shfl((int)base, lead, 64);
+    rank = base + (uint32_t)__popcll(peers & lanemask_lt());
+  } else {
+    rank = atomicAdd(&hc[h], 1u);
+  }
+  return (h << 12) | rank;
+}
+#ifndef FW_TDG_U
+#define FW_TDG_U 4  // k_td_group's one-window form: items per thread with their lookups in flight together
+#endif
+// FAST: one window per record (tumbling), no session, no lateness (no values beyond the batch's records): a
+// thread's FW_TDG_U items go through the lookup together -- records, then home slots, then the entries -- as
+// k_hll_update does, instead of one dependent chain of loads per item
+template <bool FAST>
 __global__ __launch_bounds__(TD_GTHREADS) void k_td_group(DevCfg c, const PRec* __restrict__ part, const uint32_t* __restrict__ offs,
                                                   int32_t T, int64_t n, int32_t rchunk, DevTable tb, uint32_t none,
                                                   TdBuf td, Status* st) {
@@ -4467,6 +4621,82 @@ __global__ __launch_bounds__(TD_GTHREADS) void k_td_group(DevCfg c, const PRec* 
   uint32_t* __restrict__ gs0 = td.gs[0];
   uint32_t* __restrict__ gs1 = td.gs[1];
   int32_t pp = p0_s;
+  if constexpr (FAST) {
+    constexpr int GU = FW_TDG_U;
+    const int64_t iend = min(i1, total);
+    for (int64_t ib = i0 + threadIdx.x; ib < i1; ib += (int64_t)blockDim.x * GU) {
+      int64_t key[GU], last[GU], val[GU];
+      int32_t rp[GU];
+      bool in[GU];
+#pragma unroll
+      for (int u = 0; u < GU; u++) {
+        const int64_t i = ib + (int64_t)u * blockDim.x;
+        in[u] = i < iend;
+        rp[u] = pp;
+        key[u] = last[u] = val[u] = 0;
+        if (!in[u]) continue;
+        while ((int64_t)offs[(int64_t)(pp + 1) * T] <= i) pp++;
+        rp[u] = pp;
+        if (cmp) {
+          const i64x2 r = reinterpret_cast<const i64x2*>(part)[i];
+          key[u] = r.x;  // (the compact word: decoded below, once every load is in flight)
+          val[u] = r.y;
+        } else {
+          const PRec rec = part[i];
+          key[u] = rec.key;
+          last[u] = rec.last;
+          val[u] = rec.val;
+        }
+      }
+      uint64_t hs[GU];
+      uint32_t hw[GU];
+      i64x2 hk2[GU];
+      int64_t hend[GU], hmeta[GU];
+      Region rg[GU];
+#pragma unroll
+      for (int u = 0; u < GU; u++) {
+        if (cmp && in[u]) compact_decode(c, rp[u], key[u], &key[u], &last[u]);
+        rg[u] = region_of(c, tb, rp[u], tb.cur[rp[u]]);
+        hs[u] = slot_hash(c, key[u], last[u]);
+        hw[u] = SLOT_EMPTY;
+        if (!in[u]) continue;
+        const uint32_t home = (uint32_t)hs[u] & rg[u].mask;
+        hw[u] = rg[u].state[home];  // (the table is read-only here: plain reads)
+        hk2[u] = *reinterpret_cast<const i64x2*>(&rg[u].ent[home].key);
+        hend[u] = rg[u].ent[home].end;
+        hmeta[u] = rg[u].ent[home].meta;
+      }
+#pragma unroll
+      for (int u = 0; u < GU; u++) {
+        const int64_t i = ib + (int64_t)u * blockDim.x;
+        if (!in[u]) {
+          if (i < i1) gs0[i] = none;
+          continue;
+        }
+        const int64_t we = wend(c, last[u]);
+        int32_t slot;
+        uint64_t blk;
+        const uint32_t home = (uint32_t)hs[u] & rg[u].mask;
+        if (hw[u] == live_word(hs[u]) && hk2[u].x == key[u] && hk2[u].y == last[u] && hend[u] == we) {
+          slot = (int32_t)home;
+          blk = (uint64_t)hmeta[u] >> 1;
+        } else {
+          slot = hw[u] == SLOT_EMPTY ? -1 : region_find(rg[u], hs[u], key[u], last[u], we);
+          blk = slot < 0 ? 0 : pool_block_of(rg[u].ent[slot]);
+        }
+        if (slot < 0) {
+          atomicOr(&st->flags, FW_STATUS_STATE_LOST);  // the aggregate stored every record's window
+          gs0[i] = none;
+          continue;
+        }
+        const uint32_t g = ((uint32_t)rp[u] << c.log_r) | (uint32_t)slot;
+        if (td.binv[blk] != g) td.binv[blk] = g;
+        td.v[0][i] = td_key(val[u]);
+        gs0[i] = g;
+        gs1[i] = td_group_rank(hk, hc, g);
+      }
+    }
+  } else
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     int nw = 0;
     if (i < total + nov) {
@@ -4513,33 +4743,7 @@ __global__ __launch_bounds__(TD_GTHREADS) void k_td_group(DevCfg c, const PRec* 
         if (td.binv[blk] != g) td.binv[blk] = g;
         td.v[0][o] = k;
         gs0[o] = g;
-        // the digest's LDS slot, and this item's rank among the workgroup's items of the digest
-        uint32_t h = (g * 0x9E3779B1u) >> (32 - TD_GHASH_LOG);
-        while (true) {
-          const uint32_t cur = __hip_atomic_load(&hk[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (cur == g) break;
-          if (cur == TD_GEMPTY) {
-            const uint32_t prev = atomicCAS(&hk[h], TD_GEMPTY, g);
-            if (prev == TD_GEMPTY || prev == g) break;
-          }
-          h = (h + 1) & (TD_GHASH - 1);
-        }
-        // a hot digest's items (a Zipf stream's head keys fill whole chunks): the lanes of the wave that share the
-        // first active lane's digest take their ranks from one LDS add
-        const uint64_t act = __ballot(1);
-        const int lead = __ffsll((long long)act) - 1;
-        const uint32_t hl = (uint32_t)__shfl((int)h, lead, 64);
-        const uint64_t peers = __ballot(h == hl);
-        uint32_t rank;
-        if (h == hl) {
-          uint32_t base = 0;
-          if ((int)__lane_id() == lead) base = atomicAdd(&hc[h], (uint32_t)__popcll(peers));
-          base = (uint32_t)__shfl((int)base, lead, 64);
-          rank = base + (uint32_t)__popcll(peers & lanemask_lt());
-        } else {
-          rank = atomicAdd(&hc[h], 1u);
-        }
-        gs1[o] = (h << 12) | rank;
+        gs1[o] = td_group_rank(hk, hc, g);
       }
     }
     for (int wi = nw; wi < W; wi++) gs0[i * W + wi] = none;
@@ -5139,6 +5343,8 @@ __global__ void k_td_mclear(DevCfg c, TdBuf td) {
 // each touched digest: merged serially here, or queued for the wave or the grid-wide merge
 __global__ __launch_bounds__(256) void k_td_small(DevCfg c, DevTable tb, TdBuf td, const uint64_t* __restrict__ v, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  __shared__ double s_qb[TD_NB_MAX];
+  td_stage_qb(c, s_qb);
   const int32_t nt = td.ctr[0];
   const uint32_t mask = (1u << c.log_r) - 1u;
   for (int32_t idx0 = blockIdx.x * blockDim.x; idx0 < nt; idx0 += gridDim.x * blockDim.x) {
@@ -5169,7 +5375,11 @@ __global__ __launch_bounds__(256) void k_td_small(DevCfg c, DevTable tb, TdBuf t
       TdCent* out = td_half(c, blk, h.cur ^ 1);
       td.lidx[g] = -1;
       if (nn + no <= FW_TD_T1) {
+#ifdef FW_TD_SMALL_OLD
         const int32_t k = td_merge_serial(c, c.td_qb, v, beg, nn, old, no, out, W);
+#else
+        const int32_t k = td_merge_serial_blk(c, s_qb, v, beg, nn, old, no, out, W);
+#endif
         *hp = TdHead{h.cur ^ 1, k, W};
       } else if (nn + no <= FW_TD_T3) {
         mid = true;
@@ -7188,8 +7398,9 @@ __device__ unsigned long long g_dtt[6];
 // One attempt at a region: 2^hb passes over the (key, window)s by hash prefix; each clears the table, loads the
 // region's entries of the pass, adds the records of the pass and writes the pass's groups densely into dst
 // behind the earlier passes' (M.out).  KW: the compact table (every record is a CRec; an entry or record without a
-// compact word makes the attempt DT_WIDE).  DT_OVER: some pass did not fit the table.
-template <int SRC, bool KW>
+// compact word makes the attempt DT_WIDE).  DT_OVER: some pass did not fit the table.  NAR: a launch whose every
+// record is narrow (nar then always holds), with the ring of raw pairs below and no other record path
+template <int SRC, bool KW, bool NAR>
 __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, int32_t p, const Entry* __restrict__ src,
                                           int32_t live, Entry* __restrict__ dst, int64_t R, const void* __restrict__ in,
                                           int64_t begin, int64_t end, bool cmp, int hb, bool nar) {
@@ -7235,9 +7446,26 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
       d[j] = crec[i < end ? i : end - 1];
     }
   };
-  i64x2 ra[RPT], rn[RPT];
+  // narrow records in the compact table: ND rounds in flight as raw pairs (a raw pair is 4 registers, a widened
+  // record 4 per record), widened only when their round is added -- a widening at the load would wait for it there
+  constexpr int ND = FW_DT_NDEPTH;
+  static_assert(RPT % 2 == 0, "narrow records are loaded in pairs");
+  auto load_raw = [&](i64x2 (&q)[RPT / 2], int64_t r0) {
+#pragma unroll
+    for (int j = 0; j < RPT; j += 2) {
+      int64_t i = r0 + (int64_t)j * FW_DT_THREADS + 2 * (int64_t)threadIdx.x;
+      if (i >= end) i = (end - 1) & ~(int64_t)1;
+      q[j / 2] = *reinterpret_cast<const i64x2*>(nrec + i);
+    }
+  };
+  constexpr bool ring = KW && SRC == DT_RECS && NAR && ND > 0;
+  i64x2 ra[RPT], rn[RPT], rq[ND > 0 ? ND : 1][RPT / 2];
   for (int k = 0; k < (1 << hb); k++) {
-    if constexpr (KW && SRC == DT_RECS) load(ra, begin);
+    if constexpr (ring) {  // (the other rounds after the entries: their registers would spill beside the entries')
+      load_raw(rq[0], begin);
+    } else if constexpr (KW && SRC == DT_RECS) {
+      load(ra, begin);
+    }
     if constexpr (KW) {
       for (int h = threadIdx.x; h < DK_SLOTS; h += FW_DT_THREADS) {
         U.k.kw[h] = DK_EMPTY;
@@ -7324,13 +7552,36 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
             if (bad) return 2;
             return dk_add_batch<RPT>(U.k, M, c.vtype, ww, vv, dm) ? 0 : 1;
           };
-          int res = 0;  // (ra: loaded at the top of the pass)
-          for (int64_t r0 = begin; r0 < end; r0 += 2 * RS) {
-            load(rn, r0 + RS);
-            if ((res = add_round(ra, r0))) break;
-            if (r0 + RS >= end) break;
-            load(ra, r0 + 2 * RS);
-            if ((res = add_round(rn, r0 + RS))) break;
+          int res = 0;  // (ra / rq: loaded at the top of the pass)
+          if constexpr (ring) {
+#pragma unroll
+            for (int d = 1; d < ND; d++) load_raw(rq[d], begin + (int64_t)d * RS);
+            // round r0 + d RS sits in rq[d]; once widened, rq[d] takes the round ND rounds later (the ring's slot is
+            // fixed by the unrolled d, so no register moves wait on a load)
+            for (int64_t r0 = begin; r0 < end && !res; r0 += ND * RS) {
+#pragma unroll
+              for (int d = 0; d < ND; d++) {
+                const int64_t rr = r0 + (int64_t)d * RS;
+                if (rr < end && !res) {
+                  i64x2 cur[RPT];
+#pragma unroll
+                  for (int j = 0; j < RPT; j += 2) {
+                    cur[j] = narrow_to_crec(c, (uint64_t)rq[d][j / 2].x);
+                    cur[j + 1] = narrow_to_crec(c, (uint64_t)rq[d][j / 2].y);
+                  }
+                  if (rr + ND * RS < end) load_raw(rq[d], rr + ND * RS);
+                  res = add_round(cur, rr);
+                }
+              }
+            }
+          } else {
+            for (int64_t r0 = begin; r0 < end; r0 += 2 * RS) {
+              load(rn, r0 + RS);
+              if ((res = add_round(ra, r0))) break;
+              if (r0 + RS >= end) break;
+              load(ra, r0 + 2 * RS);
+              if ((res = add_round(rn, r0 + RS))) break;
+            }
           }
           if (res == 2)  // a word equal to the EMPTY marker: the wide table takes the region
             M.widefb = 1;
@@ -7466,8 +7717,9 @@ __device__ __forceinline__ int dt_attempt(const DevCfg& c, DtTab& U, DtMisc& M, 
 // accumulators (PartialRec runs of k_pscatter or of a restore).  KW: the compact table, for the regions of a compact
 // batch; a region it cannot take (an entry without a compact word) is left for the wide launch that follows it
 // (two kernels, so each keeps its own registers).  A region is committed (its buffer flipped) only when every group
-// was written.
-template <int SRC, bool KW>
+// was written.  NAR: a single-pass batch of narrow records (launch_aggregate's first launch of one); a batch the single
+// pass could not take (rsv[P + RSV_OVER]) suspends it, and the resumed launch (NAR false) reads the offset form.
+template <int SRC, bool KW, bool NAR = false>
 __global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const void* __restrict__ in,
                                                                 const uint32_t* __restrict__ offs, int32_t T, DevTable tb,
                                                                 AggProg prog, int resume, Status* st,
@@ -7478,7 +7730,14 @@ __global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const 
   if (p >= c.P || (resume && prog.done[p])) return;
   // the partition's run: at the scan offsets, or where the single-pass scatter reserved it (launch_scatter_rsv)
   const bool single = rsv && !rsv[c.P + RSV_OVER];
-  const bool nar = single && c.narrow;  // (narrow: runs of 8-byte records, twice rcap of them per partition)
+  if (NAR && !single) {
+    if (threadIdx.x == 0) {
+      prog.done[p] = 0;
+      atomicOr(&st->suspended, (int)FW_SUSP_AGG);
+    }
+    return;
+  }
+  const bool nar = NAR || (single && c.narrow);  // (narrow: runs of 8-byte records, twice rcap of them per partition)
   const int64_t begin = single ? (int64_t)p * (nar ? 2 * rcap : rcap) : (int64_t)offs[(int64_t)p * T];
   const int64_t end = single ? begin + rsv[p] : (int64_t)offs[(int64_t)(p + 1) * T];
   if (begin == end) {  // nothing for this region: it stays as it is
@@ -7505,7 +7764,7 @@ __global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const 
   int hb = tb.passes[p];
   bool lost = false, wide = false;
   for (;;) {
-    const int r = dt_attempt<SRC, KW>(c, U, M, p, src, live, dst, R, in, begin, end, cmp, hb, nar);
+    const int r = dt_attempt<SRC, KW, NAR>(c, U, M, p, src, live, dst, R, in, begin, end, cmp, hb, nar);
     __syncthreads();
     if (r == DT_OK) break;
     if (r == DT_WIDE) {  // (KW only)
@@ -7518,7 +7777,15 @@ __global__ __launch_bounds__(FW_DT_THREADS) void k_dt_aggregate(DevCfg c, const 
     }
   }
   if (threadIdx.x == 0) {
-    tb.passes[p] = (uint8_t)min(hb, 24);
+    // the passes a region needs follow its groups down again: a batch that straddles a window end doubles them until
+    // the old window fires, and a region kept at 2^b passes would read its records 2^b times for every later batch
+    int keep = min(hb, 24);
+#ifndef FW_DT_NO_DECAY
+    if (!wide && !lost && !M.capover && keep > 0 &&
+        M.out < ((long long)(KW ? DK_LIMIT : DT_LIMIT) * 3 / 4 << (keep - 1)))
+      keep--;
+#endif
+    tb.passes[p] = (uint8_t)keep;
     if (wide) {
       prog.done[p] = 0;
       if (!resume) atomicOr(&st->suspended, (int)FW_SUSP_AGG);
@@ -7983,8 +8250,12 @@ void launch_aggregate(const DevCfg& c0, int64_t wm, const PRec* part, const uint
     }
   }
   if (c.dense) {  // the compact table; in a resumed sequence the wide launch takes the regions it left
-    FW_LAUNCH_MAIN((k_dt_aggregate<DT_RECS, true>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs, T,
-                   tb, prog, resume, st, rsv, rcap);
+    if (!resume && rsv && c.narrow && FW_DT_NDEPTH > 0)  // (its own kernel: the ring's registers)
+      FW_LAUNCH_MAIN((k_dt_aggregate<DT_RECS, true, true>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs,
+                     T, tb, prog, resume, st, rsv, rcap);
+    else
+      FW_LAUNCH_MAIN((k_dt_aggregate<DT_RECS, true>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part, offs, T,
+                     tb, prog, resume, st, rsv, rcap);
     if (resume)
       hipLaunchKernelGGL((k_dt_aggregate<DT_RECS, false>), dim3(c.P), dim3(FW_DT_THREADS), 0, s, c, (const void*)part,
                          offs, T, tb, prog, 1, st, rsv, rcap);
@@ -8199,8 +8470,13 @@ void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int
   (void)hipMemsetAsync(td.ctr, 0, 3 * sizeof(int32_t), s);
   (void)hipMemsetAsync(td.lctr, 0, 5 * sizeof(int32_t), s);
   const int32_t rchunk = std::max(1, TD_GCHUNK / W);  // (records per grouping workgroup: at most TD_GCHUNK items)
-  hipLaunchKernelGGL(k_td_group, dim3((unsigned)((nrec + rchunk - 1) / rchunk)), dim3(TD_GTHREADS), 0, s, c, part, offs, T, nrec,
-                     rchunk, tb, none, td, st);
+#ifndef FW_TDG_OFF
+  const bool fast = c.assigner != FW_SLIDING && c.assigner != FW_SESSION && !c.td_ovctr;
+#else
+  const bool fast = false;
+#endif
+  hipLaunchKernelGGL((fast ? k_td_group<true> : k_td_group<false>), dim3((unsigned)((nrec + rchunk - 1) / rchunk)),
+                     dim3(TD_GTHREADS), 0, s, c, part, offs, T, nrec, rchunk, tb, none, td, st);
   if (c.assigner == FW_SESSION) {  // the push's session merges: each merged digest's union of old centroids
     hipLaunchKernelGGL(k_td_mlink, dim3(64), dim3(256), 0, s, c, td);
     hipLaunchKernelGGL(k_td_mlist, dim3(64), dim3(256), 0, s, c, td);

@@ -87,6 +87,9 @@
 #ifndef FW_DT_RPT
 #define FW_DT_RPT 2
 #endif
+#ifndef FW_DT_NDEPTH
+#define FW_DT_NDEPTH 2  // narrow records: rounds of raw pairs in flight (0: two widened rounds, as 16-byte records)
+#endif
 // Tile-local ("gathered") partitioning of compact count/sum/min/max batches: k_stage sorts each tile of
 // FW_GTILE records by partition in LDS and writes it back linearly (a wave's stores are whole lines; scattered
 // 16-byte stores into partition-major runs measured 2.4x slower), and k_aggregate gathers a partition's runs
