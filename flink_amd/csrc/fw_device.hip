@@ -4784,12 +4784,46 @@ __global__ __launch_bounds__(TD_GTHREADS) void k_td_group(DevCfg c, const PRec* 
       gs1[o] = hc[x >> 12] + (x & 4095u);
     }
 }
-// the touched digests' counts (tbeg[nt] = 0), scanned in place by the device-sized scan below
+// The serial tier takes one digest per thread, and a wave lasts as long as its longest merge: the touched digests go
+// to it longest first, by classes of their batch run's length (1, 2, 3-4, ..., 65+; a digest's old centroids grow with
+// its key's frequency as its values do, and every window of the push is at the same point of its span).
+// lctr[TD_LC_CNT + k]: the class's digests, lctr[TD_LC_CUR + k]: its placement cursor; the order is td.gs[1]
+// (free once k_td_place has read the ranks).
+constexpr int TD_NCLS = 8;
+constexpr int TD_LC_CNT = 5, TD_LC_CUR = TD_LC_CNT + TD_NCLS, TD_LC_WORDS = TD_LC_CUR + TD_NCLS;
+static_assert(TD_LC_WORDS == FW_TD_LC_WORDS, "TdBuf::lctr's allocation");
+__device__ __forceinline__ int td_len_class(uint32_t len) {
+  return len <= 1 ? 0 : min(TD_NCLS - 1, 32 - __clz((int)(len - 1)));
+}
+// a wave's count of its lanes' class k items (every lane gets the counts of all TD_NCLS classes: c[k])
+__device__ __forceinline__ void td_class_ballots(bool valid, int k, uint64_t (&m)[TD_NCLS]) {
+#pragma unroll
+  for (int q = 0; q < TD_NCLS; q++) m[q] = __ballot(valid && k == q);
+}
+// the touched digests' counts (tbeg[nt] = 0), scanned in place by the device-sized scan below, and counted by length
+// class (per wave by ballots, one LDS add per wave and class, one global add per workgroup)
 __global__ __launch_bounds__(256) void k_td_counts(TdBuf td, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  __shared__ int32_t ccnt[TD_NCLS];
+  if (threadIdx.x < TD_NCLS) ccnt[threadIdx.x] = 0;
+  __syncthreads();
   const int32_t nt = td.ctr[0];
-  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i <= nt; i += gridDim.x * blockDim.x)
-    td.tbeg[i] = i < nt ? td.dcnt[td.tslot[i]] : 0u;
+  int32_t wc[TD_NCLS] = {};
+  for (int32_t i0 = blockIdx.x * blockDim.x; i0 <= nt; i0 += gridDim.x * blockDim.x) {  // (whole waves iterate)
+    const int32_t i = i0 + threadIdx.x;
+    const uint32_t len = i < nt ? td.dcnt[td.tslot[i]] : 0u;
+    if (i <= nt) td.tbeg[i] = len;
+    uint64_t m[TD_NCLS];
+    td_class_ballots(i < nt, td_len_class(len), m);
+#pragma unroll
+    for (int q = 0; q < TD_NCLS; q++) wc[q] += __popcll(m[q]);
+  }
+  if (__lane_id() == 0)
+#pragma unroll
+    for (int q = 0; q < TD_NCLS; q++)
+      if (wc[q]) atomicAdd(&ccnt[q], wc[q]);
+  __syncthreads();
+  if (threadIdx.x < TD_NCLS && ccnt[threadIdx.x]) atomicAdd(&td.lctr[TD_LC_CNT + threadIdx.x], ccnt[threadIdx.x]);
 }
 // k_scan_* over data[0 .. *mdev] (the length read on the device)
 __global__ __launch_bounds__(SCAN_T) void k_scan_blocks_d(uint32_t* data, const int32_t* mdev, uint32_t* sums) {
@@ -4857,6 +4891,63 @@ __global__ __launch_bounds__(256) void k_td_starts(TdBuf td, Status* st) {
     }
     td_list_put(td.brun[0], &td.lctr[1], len > TD_SORT_MAX, TdRun{beg, len | TD_RUN_V1});
     td_list_put(td.lrun, &td.lctr[0], len > 64 && len <= TD_SORT_MAX, TdRun{beg, len | TD_RUN_V1});
+  }
+}
+// the touched digests in class order, longest class first, into td.gs[1]: a workgroup takes TD_PERM_CH of them
+// (TD_PERM_PT a thread), counts them per wave and class, reserves each class's share with one global add, and places
+// them in wave order
+constexpr int TD_PERM_PT = 16, TD_PERM_CH = 256 * TD_PERM_PT;
+__global__ __launch_bounds__(256) void k_td_perm(TdBuf td, Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  __shared__ int32_t wcnt[4][TD_NCLS], wb[4][TD_NCLS];
+  const int32_t nt = td.ctr[0];
+  const int32_t c0 = blockIdx.x * TD_PERM_CH;
+  if (c0 >= nt) return;
+  const int wv = threadIdx.x >> 6, lane = __lane_id();
+  int cls[TD_PERM_PT];
+  int32_t run[TD_NCLS] = {};
+#pragma unroll
+  for (int j = 0; j < TD_PERM_PT; j++) {
+    const int32_t i = c0 + j * 256 + (int32_t)threadIdx.x;
+    cls[j] = i < nt ? td_len_class(td.tbeg[i + 1] - td.tbeg[i]) : 0;
+    uint64_t m[TD_NCLS];
+    td_class_ballots(i < nt, cls[j], m);
+#pragma unroll
+    for (int q = 0; q < TD_NCLS; q++) run[q] += __popcll(m[q]);
+  }
+  if (lane < TD_NCLS) {
+    int32_t x = run[0];
+#pragma unroll
+    for (int q = 1; q < TD_NCLS; q++) x = lane == q ? run[q] : x;
+    wcnt[wv][lane] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < TD_NCLS) {
+    const int k = (int)threadIdx.x;
+    int32_t base = 0;  // the longer classes' digests come first
+    for (int q = TD_NCLS - 1; q > k; q--) base += td.lctr[TD_LC_CNT + q];
+    const int32_t tot = wcnt[0][k] + wcnt[1][k] + wcnt[2][k] + wcnt[3][k];
+    int32_t at = base + (tot ? atomicAdd(&td.lctr[TD_LC_CUR + k], tot) : 0);
+    for (int w = 0; w < 4; w++) {
+      wb[w][k] = at;
+      at += wcnt[w][k];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < TD_NCLS; q++) run[q] = 0;
+#pragma unroll
+  for (int j = 0; j < TD_PERM_PT; j++) {
+    const int32_t i = c0 + j * 256 + (int32_t)threadIdx.x;
+    uint64_t m[TD_NCLS];
+    td_class_ballots(i < nt, cls[j], m);
+    int32_t pos = 0;
+#pragma unroll
+    for (int q = 0; q < TD_NCLS; q++) {
+      if (cls[j] == q) pos = wb[wv][q] + run[q] + __popcll(m[q] & lanemask_lt());
+      run[q] += __popcll(m[q]);
+    }
+    if (i < nt) td.gs[1][pos] = (uint32_t)i;
   }
 }
 // every item to its run (v[1]) and its digest to gsort; positions past the runs get `none`
@@ -5348,9 +5439,14 @@ __global__ __launch_bounds__(256) void k_td_small(DevCfg c, DevTable tb, TdBuf t
   const int32_t nt = td.ctr[0];
   const uint32_t mask = (1u << c.log_r) - 1u;
   for (int32_t idx0 = blockIdx.x * blockDim.x; idx0 < nt; idx0 += gridDim.x * blockDim.x) {
-    const int32_t idx = idx0 + (int32_t)threadIdx.x;
+    const int32_t pos = idx0 + (int32_t)threadIdx.x;
+#ifdef FW_TD_NOPERM
+    const int32_t idx = pos;
+#else
+    const int32_t idx = pos < nt ? (int32_t)td.gs[1][pos] : pos;  // (longest first: k_td_perm)
+#endif
     bool mid = false;
-    if (idx < nt) {
+    if (pos < nt) {
       const uint32_t g = td.tslot[idx];
       const int64_t beg = td.tbeg[idx];
       const int32_t p = (int32_t)(g >> c.log_r);
@@ -8468,7 +8564,7 @@ void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int
   const int W = c.assigner == FW_SLIDING ? c.wpr : 1;
   n *= W;  // the items: one per (record, window)
   (void)hipMemsetAsync(td.ctr, 0, 3 * sizeof(int32_t), s);
-  (void)hipMemsetAsync(td.lctr, 0, 5 * sizeof(int32_t), s);
+  (void)hipMemsetAsync(td.lctr, 0, TD_LC_WORDS * sizeof(int32_t), s);
   const int32_t rchunk = std::max(1, TD_GCHUNK / W);  // (records per grouping workgroup: at most TD_GCHUNK items)
 #ifndef FW_TDG_OFF
   const bool fast = c.assigner != FW_SLIDING && c.assigner != FW_SESSION && !c.td_ovctr;
@@ -8492,6 +8588,8 @@ void launch_tdigest(const DevCfg& c, const PRec* part, const uint32_t* offs, int
   hipLaunchKernelGGL(k_scan_add_d, dim3(nb), dim3(SCAN_T), 0, s, td.tbeg, (const int32_t*)td.ctr, (const uint32_t*)td.mid);
   hipLaunchKernelGGL(k_td_starts, dim3(grid), dim3(256), 0, s, td, st);
   hipLaunchKernelGGL(k_td_place, dim3(grid), dim3(256), 0, s, td, n, none, st);
+  hipLaunchKernelGGL(k_td_perm, dim3((unsigned)((n + TD_PERM_CH - 1) / TD_PERM_CH)), dim3(256), 0, s, td, st);  // (gs[1]:
+  // after the place)
   // each run sorted: by lanes, by MSD passes (two levels) and the fallback, then in LDS (into v[0])
   hipLaunchKernelGGL(k_td_sort_lanes<16>, dim3(4096), dim3(256), 0, s, td, st);
   hipLaunchKernelGGL(k_td_sort_lanes<64>, dim3(4096), dim3(256), 0, s, td, st);

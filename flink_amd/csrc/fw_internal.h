@@ -383,6 +383,7 @@ struct TdMsd {
   uint32_t toff;            // the run's first tile (TD_TILE values each) among the level's runs
   uint32_t nsp;             // its splitters (td.spl)
 };
+#define FW_TD_LC_WORDS 21
 struct TdBuf {
   uint32_t* gs[2];          // per item: [0] its digest's global slot (partition << log_r | slot), [1] its rank in the run
   uint64_t* v[2];           // per item its Double.compare-ordered value key; [1] the values grouped by digest, [0]
@@ -395,7 +396,8 @@ struct TdBuf {
   TdMsd* msd;               // [brun_cap] the sample-sort level's runs' tiles and splitter counts
   uint64_t* spl;            // [brun_cap * 2047] their splitters
   uint32_t* hist;           // [brun_cap * 4096] their buckets' counts, then cursors
-  int32_t* lctr;            // [0] lrun entries, [1..3] brun[0..2] entries, [4] the MSD level's tiles
+  int32_t* lctr;            // [FW_TD_LC_WORDS] [0] lrun entries, [1..3] brun[0..2] entries, [4] the MSD level's
+                            // tiles, then the serial tier's length classes (k_td_starts, k_td_perm)
   int64_t lrun_cap, brun_cap;
   uint32_t* tslot;          // touched digests: global slot      [max_batch]
   uint32_t* tbeg;           //                  first sorted value [max_batch]

@@ -1302,7 +1302,7 @@ int fw_create(const fw_config* cfg_in, fw_op** out) {
     HIP_OR_RETURN(op, dmalloc(&t.msd, (size_t)t.brun_cap));
     HIP_OR_RETURN(op, dmalloc(&t.spl, (size_t)t.brun_cap * 2047));
     HIP_OR_RETURN(op, dmalloc(&t.hist, (size_t)t.brun_cap * 4096));
-    HIP_OR_RETURN(op, dmalloc(&t.lctr, 5));
+    HIP_OR_RETURN(op, dmalloc(&t.lctr, FW_TD_LC_WORDS));
     HIP_OR_RETURN(op, dmalloc(&t.tslot, (size_t)mi));
     HIP_OR_RETURN(op, dmalloc(&t.tbeg, (size_t)mi + 1));  // (+ the runs' end)
     HIP_OR_RETURN(op, dmalloc(&t.ctr, 3));
