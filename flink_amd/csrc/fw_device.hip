@@ -5094,6 +5094,97 @@ __device__ void td_bitonic_reg(uint64_t* a, uint32_t len) {
   for (int e = 0; e < E; e++) a[t0 + e] = x[e];
   __syncthreads();
 }
+// The same network with the stages inside a wave on shuffles: thread t holds keys [t E, t E + E), so a wave holds 64 E
+// consecutive positions; a stage whose partner distance is below E runs on the thread's registers, below 64 E on
+// cross-lane shuffles (no barrier), and only the longer ones (the last two levels of a 256-thread workgroup's sort)
+// through the LDS.
+template <int E>
+__device__ __forceinline__ void td_lds_stages(uint64_t* a, uint64_t (&x)[E], uint32_t k, bool flip, uint32_t jlo) {
+  constexpr uint32_t n2 = 256u * E;
+  const uint32_t t0 = threadIdx.x * E;
+#pragma unroll
+  for (int e = 0; e < E; e++) a[t0 + e] = x[e];
+  __syncthreads();
+  if (flip) {
+    const uint32_t hk = k >> 1;
+    for (uint32_t t = threadIdx.x; t < (n2 >> 1); t += blockDim.x) {
+      const uint32_t i = (t & ~(hk - 1)) * 2 + (t & (hk - 1)), p = i ^ (k - 1);
+      const uint64_t u = a[i], v = a[p];
+      if (u > v) {
+        a[i] = v;
+        a[p] = u;
+      }
+    }
+    __syncthreads();
+  }
+  for (uint32_t j = flip ? k >> 2 : k; j >= jlo && j > 0; j >>= 1) {
+    for (uint32_t t = threadIdx.x; t < (n2 >> 1); t += blockDim.x) {
+      const uint32_t i = (t & ~(j - 1)) * 2 + (t & (j - 1)), p = i + j;
+      const uint64_t u = a[i], v = a[p];
+      if (u > v) {
+        a[i] = v;
+        a[p] = u;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int e = 0; e < E; e++) x[e] = a[t0 + e];
+  __syncthreads();
+}
+template <int E>
+__device__ void td_bitonic_wave(uint64_t* a, uint32_t len) {
+  constexpr uint32_t n2 = 256u * E, WSPAN = 64u * E;
+  constexpr int LE = E == 1 ? 0 : E == 2 ? 1 : E == 4 ? 2 : E == 8 ? 3 : 4;
+  static_assert((1 << LE) == E, "E: 1, 2, 4, 8 or 16");
+  const uint32_t t0 = threadIdx.x * E;
+  const int lane = __lane_id();
+  uint64_t x[E];
+#pragma unroll
+  for (int e = 0; e < E; e++) x[e] = t0 + e < len ? a[t0 + e] : ~0ull;
+  for (uint32_t k = 2; k <= n2; k <<= 1) {
+    uint32_t j = k >> 2;  // the first half-cleaner after the flip stage
+    if (k <= (uint32_t)E) {  // the flip stage of a block inside the thread's keys
+#pragma unroll
+      for (int e = 0; e < E; e++) {
+        const int p = e ^ (int)(k - 1);
+        if (e < p) td_cswap<E>(x[e], x[p]);
+      }
+    } else if (k <= WSPAN) {  // ... inside the wave: the partner of key e is key E-1-e of lane ^ ((k-1) >> LE)
+      const int lm = (int)((k - 1) >> LE);
+      const bool lower = (lane & (int)((k >> 1) >> LE)) == 0;
+      uint64_t y[E];
+#pragma unroll
+      for (int e = 0; e < E; e++) y[E - 1 - e] = shfl_xor_u64(x[e], lm, 64);
+#pragma unroll
+      for (int e = 0; e < E; e++) x[e] = lower ? min(x[e], y[e]) : max(x[e], y[e]);
+    } else {  // across waves: the flip stage and the half-cleaners of distance >= 64 E through the LDS
+      td_lds_stages<E>(a, x, k, true, WSPAN);
+      j = WSPAN >> 1;
+    }
+    for (; j >= (uint32_t)E && j > 0; j >>= 1) {  // half-cleaners on shuffles: the partner is lane ^ (j >> LE)
+      const int lm = (int)(j >> LE);
+      const bool lower = (lane & lm) == 0;
+#pragma unroll
+      for (int e = 0; e < E; e++) {
+        const uint64_t y = shfl_xor_u64(x[e], lm, 64);
+        x[e] = lower ? min(x[e], y) : max(x[e], y);
+      }
+    }
+#pragma unroll
+    for (int jj = E >> 1; jj > 0; jj >>= 1) {  // the half-cleaners of distance < E (those below k / 2)
+      if ((uint32_t)jj > (k >> 2)) continue;
+#pragma unroll
+      for (int e = 0; e < E; e++) {
+        const int p = e ^ jj;
+        if (e < p) td_cswap<E>(x[e], x[p]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; e++) a[t0 + e] = x[e];
+  __syncthreads();
+}
 // the runs of 65 .. TD_SORT_MAX values (digests, and the MSD passes' bins): one workgroup each, in LDS, into v[0]
 __global__ __launch_bounds__(256) void k_td_sort_lds(TdBuf td, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
@@ -5105,6 +5196,18 @@ __global__ __launch_bounds__(256) void k_td_sort_lds(TdBuf td, Status* st) {
     const uint64_t* __restrict__ src = (r.len & TD_RUN_V1) ? td.v[1] : td.v[0];
     for (uint32_t i = threadIdx.x; i < len; i += blockDim.x) a[i] = src[r.beg + i];
     __syncthreads();
+#ifndef FW_TD_LDS_SORT
+    if (len > 2048)
+      td_bitonic_wave<16>(a, len);
+    else if (len > 1024)
+      td_bitonic_wave<8>(a, len);
+    else if (len > 512)
+      td_bitonic_wave<4>(a, len);
+    else if (len > 256)
+      td_bitonic_wave<2>(a, len);
+    else
+      td_bitonic_wave<1>(a, len);
+#else
     if (len > 2048)
       td_bitonic_reg<16>(a, len);
     else if (len > 1024)
@@ -5115,6 +5218,7 @@ __global__ __launch_bounds__(256) void k_td_sort_lds(TdBuf td, Status* st) {
       td_bitonic_reg<2>(a, len);
     else
       td_bitonic_lds(a, len);
+#endif
     for (uint32_t i = threadIdx.x; i < len; i += blockDim.x) td.v[0][r.beg + i] = a[i];
     __syncthreads();
   }
