@@ -4121,17 +4121,40 @@ __device__ __forceinline__ double td_wave_tree(double x, bool has) {
   return x;
 }
 // the wave's S_new of a bucket: its sorted values v[ns, ne) in blocks of 64, tree sums folded left to right
+#ifndef FW_TD_SUM_U
+#define FW_TD_SUM_U 8
+#endif
 __device__ double td_wave_new_sum(const uint64_t* __restrict__ v, int64_t ns, int64_t ne) {
+  // FW_TD_SUM_U full blocks a round, the next round's loads in flight while this one's trees are summed (a hot
+  // bucket of a large digest holds tens of thousands of values: one wave walks them)
+  constexpr int U = FW_TD_SUM_U;
+  constexpr int64_t RW = (int64_t)U * 64;
   const int lane = __lane_id();
   double s = 0.0;
   bool any = false;
   int64_t b0 = ns;
-  for (; b0 + 4 * 64 <= ne; b0 += 4 * 64) {  // four full blocks in flight
-    double x[4];
+  const int64_t full = ns + (ne - ns) / RW * RW;
+  if (b0 < full) {
+    double xa[U], xb[U];
+    // (branch-free loads: past the last full round a round reloads the last one)
+    auto ld = [&](double (&x)[U], int64_t base) {
+      const int64_t bb = min(base, full - RW);
 #pragma unroll
-    for (int u = 0; u < 4; u++) x[u] = td_val(v[b0 + u * 64 + lane]);
+      for (int u = 0; u < U; u++) x[u] = td_val(v[bb + u * 64 + lane]);
+    };
+    ld(xa, b0);
+    for (;;) {
+      ld(xb, b0 + RW);
 #pragma unroll
-    for (int u = 0; u < 4; u++) td_fold(s, any, td_wave_tree(x[u], true));
+      for (int u = 0; u < U; u++) td_fold(s, any, td_wave_tree(xa[u], true));
+      b0 += RW;
+      if (b0 >= full) break;
+      ld(xa, b0 + RW);
+#pragma unroll
+      for (int u = 0; u < U; u++) td_fold(s, any, td_wave_tree(xb[u], true));
+      b0 += RW;
+      if (b0 >= full) break;
+    }
   }
   for (; b0 < ne; b0 += 64) {
     const bool has = b0 + lane < ne;
