@@ -5878,44 +5878,79 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
 }
 
 // the large tier: placement of every value of a large digest over the whole grid
+#ifndef FW_TD_ITEMS_PT
+#define FW_TD_ITEMS_PT 8
+#endif
+// A thread takes FW_TD_ITEMS_PT consecutive sorted positions: inside one digest its items' old-centroid places only
+// grow (the search resumes from the last one), and an item's predecessor is usually the thread's previous item, whose
+// bucket is known
 __global__ __launch_bounds__(256) void k_td_large_items(DevCfg c, int64_t n, const uint32_t* __restrict__ gs,
                                                         const uint64_t* __restrict__ v, uint32_t none, TdBuf td, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || td.ctr[1] == 0) return;
   __shared__ double s_qb[TD_NB_MAX];
   td_stage_qb(c, s_qb);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t g = gs[i];
-    if (g == none) continue;
-    const int32_t L = td.lidx[g];
-    if (L < 0) continue;
-    const TdLarge d = td.large[L];
-    const uint64_t* keys = td.okey + (int64_t)L * c.td_nb;
-    const int64_t r = i - d.beg;
-    int32_t lo = 0, hi = d.no;
-    const uint64_t vk = v[i];
-    while (lo < hi) {
-      const int32_t m = (lo + hi) >> 1;
-      if (keys[m] < vk)
-        lo = m + 1;
-      else
-        hi = m;
-    }
-    const double W = (double)d.W;
-    const int b = td_bucket(c, s_qb, W, (double)(r + (lo ? d.old[lo - 1].cum : 0)) + 0.5);
-    bool start = r == 0;
-    if (!start) {
-      const uint64_t pk = v[i - 1];
-      int32_t lo2 = 0, hi2 = lo;  // the predecessor's place is at most this value's
-      while (lo2 < hi2) {
-        const int32_t m = (lo2 + hi2) >> 1;
-        if (keys[m] < pk)
-          lo2 = m + 1;
-        else
-          hi2 = m;
+  constexpr int IT = FW_TD_ITEMS_PT;
+  const int64_t nch = (n + IT - 1) / IT;
+  for (int64_t ch = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ch < nch; ch += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i0 = ch * IT;
+    uint32_t pg = none;  // the previous item's digest (none: no previous item of a large digest)
+    int pb = 0;
+    int32_t plo = 0;
+    TdLarge d{};
+    const uint64_t* keys = nullptr;
+    double W = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < IT; k++) {
+      const int64_t i = i0 + k;
+      if (i >= n) break;
+      const uint32_t g = gs[i];
+      if (g == none) {
+        pg = none;
+        continue;
       }
-      start = td_bucket(c, s_qb, W, (double)(r - 1 + (lo2 ? d.old[lo2 - 1].cum : 0)) + 0.5) != b;
+      const int32_t L = td.lidx[g];
+      if (L < 0) {
+        pg = none;
+        continue;
+      }
+      const bool same = g == pg;
+      if (!same) {
+        d = td.large[L];
+        keys = td.okey + (int64_t)L * c.td_nb;
+        W = (double)d.W;
+        plo = 0;
+      }
+      const int64_t r = i - d.beg;
+      int32_t lo = plo, hi = d.no;  // (sorted values: the place of this one is at or after the previous one's)
+      const uint64_t vk = v[i];
+      while (lo < hi) {
+        const int32_t m = (lo + hi) >> 1;
+        if (keys[m] < vk)
+          lo = m + 1;
+        else
+          hi = m;
+      }
+      const int b = td_bucket(c, s_qb, W, (double)(r + (lo ? d.old[lo - 1].cum : 0)) + 0.5);
+      bool start = r == 0;
+      if (!start && same) {
+        start = pb != b;
+      } else if (!start) {
+        const uint64_t pk = v[i - 1];
+        int32_t lo2 = 0, hi2 = lo;  // the predecessor's place is at most this value's
+        while (lo2 < hi2) {
+          const int32_t m = (lo2 + hi2) >> 1;
+          if (keys[m] < pk)
+            lo2 = m + 1;
+          else
+            hi2 = m;
+        }
+        start = td_bucket(c, s_qb, W, (double)(r - 1 + (lo2 ? d.old[lo2 - 1].cum : 0)) + 0.5) != b;
+      }
+      if (start) td.nstart[(int64_t)L * c.td_nb + b] = (int32_t)i;
+      pg = g;
+      pb = b;
+      plo = lo;
     }
-    if (start) td.nstart[(int64_t)L * c.td_nb + b] = (int32_t)i;
   }
 }
 // the old centroids of the large digests (one wave per digest): their mean keys, buckets and bucket starts
