@@ -5121,9 +5121,9 @@ __device__ void td_bitonic_reg(uint64_t* a, uint32_t len) {
 // consecutive positions; a stage whose partner distance is below E runs on the thread's registers, below 64 E on
 // cross-lane shuffles (no barrier), and only the longer ones (the last two levels of a 256-thread workgroup's sort)
 // through the LDS.
-template <int E>
+template <int E, int NT>
 __device__ __forceinline__ void td_lds_stages(uint64_t* a, uint64_t (&x)[E], uint32_t k, bool flip, uint32_t jlo) {
-  constexpr uint32_t n2 = 256u * E;
+  constexpr uint32_t n2 = (uint32_t)NT * E;
   const uint32_t t0 = threadIdx.x * E;
 #pragma unroll
   for (int e = 0; e < E; e++) a[t0 + e] = x[e];
@@ -5155,9 +5155,9 @@ __device__ __forceinline__ void td_lds_stages(uint64_t* a, uint64_t (&x)[E], uin
   for (int e = 0; e < E; e++) x[e] = a[t0 + e];
   __syncthreads();
 }
-template <int E>
-__device__ void td_bitonic_wave(uint64_t* a, uint32_t len) {
-  constexpr uint32_t n2 = 256u * E, WSPAN = 64u * E;
+template <int E, int NT = 256>
+__device__ void td_bitonic_wave(uint64_t* a, uint32_t len) {  // (NT: the workgroup's threads)
+  constexpr uint32_t n2 = (uint32_t)NT * E, WSPAN = 64u * E;
   constexpr int LE = E == 1 ? 0 : E == 2 ? 1 : E == 4 ? 2 : E == 8 ? 3 : 4;
   static_assert((1 << LE) == E, "E: 1, 2, 4, 8 or 16");
   const uint32_t t0 = threadIdx.x * E;
@@ -5182,7 +5182,7 @@ __device__ void td_bitonic_wave(uint64_t* a, uint32_t len) {
 #pragma unroll
       for (int e = 0; e < E; e++) x[e] = lower ? min(x[e], y[e]) : max(x[e], y[e]);
     } else {  // across waves: the flip stage and the half-cleaners of distance >= 64 E through the LDS
-      td_lds_stages<E>(a, x, k, true, WSPAN);
+      td_lds_stages<E, NT>(a, x, k, true, WSPAN);
       j = WSPAN >> 1;
     }
     for (; j >= (uint32_t)E && j > 0; j >>= 1) {  // half-cleaners on shuffles: the partner is lane ^ (j >> LE)
@@ -5314,7 +5314,7 @@ __global__ __launch_bounds__(1024) void k_td_msd_sample(TdBuf td, int L, Status*
     const uint32_t S = min((uint32_t)TD_SAMPLE, len);
     for (uint32_t i = threadIdx.x; i < S; i += blockDim.x) a[i] = src[r.beg + (uint32_t)(((uint64_t)i * len) / S)];
     __syncthreads();
-    td_bitonic_lds(a, S);
+    td_bitonic_wave<TD_SAMPLE / 1024, 1024>(a, S);
     uint32_t nb = 2;  // buckets between splitters: ~TD_SORT_MAX / 2 values each
     while (nb < TD_MAX_SPL + 1 && (uint64_t)nb * (TD_SORT_MAX / 2) < len) nb <<= 1;
     const uint32_t ns = nb - 1;
