@@ -5881,6 +5881,7 @@ __global__ __launch_bounds__(64 * TD_WAVES) void k_td_wave(DevCfg c, DevTable tb
 #ifndef FW_TD_ITEMS_PT
 #define FW_TD_ITEMS_PT 8
 #endif
+static_assert(FW_TD_ITEMS_PT % 4 == 0, "k_td_large_items: whole 16-byte loads");
 // A thread takes FW_TD_ITEMS_PT consecutive sorted positions: inside one digest its items' old-centroid places only
 // grow (the search resumes from the last one), and an item's predecessor is usually the thread's previous item, whose
 // bucket is known
@@ -5893,23 +5894,51 @@ __global__ __launch_bounds__(256) void k_td_large_items(DevCfg c, int64_t n, con
   const int64_t nch = (n + IT - 1) / IT;
   for (int64_t ch = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ch < nch; ch += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i0 = ch * IT;
+    // the chunk's digests and values with whole-chunk vector loads (a lane's IT items are consecutive, so per-item
+    // loads would stride a wave's lanes IT items apart and fetch every line IT times)
+    uint32_t gq[IT];
+    uint64_t vq[IT];
+    const bool whole = i0 + IT <= n;
+    if (whole) {
+#pragma unroll
+      for (int q = 0; q < IT; q += 4) {
+        const uint4 x = *reinterpret_cast<const uint4*>(gs + i0 + q);
+        gq[q] = x.x, gq[q + 1] = x.y, gq[q + 2] = x.z, gq[q + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < IT; q++) gq[q] = i0 + q < n ? gs[i0 + q] : none;
+    }
+    bool anyl = false;
+    int32_t lq[IT];
+#pragma unroll
+    for (int q = 0; q < IT; q++) {
+      lq[q] = gq[q] == none ? -1 : td.lidx[gq[q]];
+      anyl |= lq[q] >= 0;
+    }
+    if (!anyl) continue;
+    if (whole) {
+#pragma unroll
+      for (int q = 0; q < IT; q += 2) {
+        const i64x2 x = *reinterpret_cast<const i64x2*>(v + i0 + q);
+        vq[q] = (uint64_t)x.x, vq[q + 1] = (uint64_t)x.y;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < IT; q++) vq[q] = i0 + q < n ? v[i0 + q] : 0ull;
+    }
     uint32_t pg = none;  // the previous item's digest (none: no previous item of a large digest)
     int pb = 0;
     int32_t plo = 0;
     TdLarge d{};
     const uint64_t* keys = nullptr;
     double W = 0.0;
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < IT; k++) {
       const int64_t i = i0 + k;
-      if (i >= n) break;
-      const uint32_t g = gs[i];
-      if (g == none) {
-        pg = none;
-        continue;
-      }
-      const int32_t L = td.lidx[g];
-      if (L < 0) {
+      const uint32_t g = gq[k];
+      const int32_t L = lq[k];
+      if (i >= n || L < 0) {
         pg = none;
         continue;
       }
@@ -5922,7 +5951,7 @@ __global__ __launch_bounds__(256) void k_td_large_items(DevCfg c, int64_t n, con
       }
       const int64_t r = i - d.beg;
       int32_t lo = plo, hi = d.no;  // (sorted values: the place of this one is at or after the previous one's)
-      const uint64_t vk = v[i];
+      const uint64_t vk = vq[k];
       while (lo < hi) {
         const int32_t m = (lo + hi) >> 1;
         if (keys[m] < vk)
