@@ -709,6 +709,34 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_add(uint32_t* data, int64_t m, 
     if (base + e < m) data[base + e] += add;
 }
 
+// the gated scan of a single-pass fallback in one workgroup: one launch when the gate is closed (the common case: the
+// batch went through the single pass), a slower scan when it is open (a batch the single pass could not take, rare:
+// three in a row turn the single pass off)
+__global__ __launch_bounds__(SCAN_T) void k_scan_gated(uint32_t* data, int64_t m, const uint32_t* gate) {
+  if (!*gate) return;
+  __shared__ uint32_t sw[SCAN_T / 64 + 1];
+  uint32_t carry = 0;
+  for (int64_t b0 = 0; b0 < m; b0 += SCAN_B) {
+    const int64_t base = b0 + (int64_t)threadIdx.x * SCAN_E;
+    uint32_t v[SCAN_E];
+    uint32_t local = 0;
+#pragma unroll
+    for (int e = 0; e < SCAN_E; e++) {
+      v[e] = base + e < m ? data[base + e] : 0u;
+      local += v[e];
+    }
+    uint32_t total;
+    uint32_t off = block_excl_scan(local, sw, &total) + carry;
+#pragma unroll
+    for (int e = 0; e < SCAN_E; e++) {
+      if (base + e < m) data[base + e] = off;
+      off += v[e];
+    }
+    carry += total;
+    __syncthreads();  // (sw is reused by the next chunk's scan)
+  }
+}
+
 // Store a 32-byte record per lane as whole sectors written by lane pairs: lanes 2i and 2i+1 first
 // write lane 2i's record (16 B each, contiguous), then lane 2i+1's.  The halves and positions are
 // swapped between the pair with DPP (quad_perm [1,0,3,2]); a wave's store then addresses 32 sectors
@@ -8413,7 +8441,20 @@ void launch_classify_hist(const DevCfg& c, int64_t wm, const int64_t* key, const
   }
 }
 
+// a scratch set's single-pass words back to zero once its aggregate has read them (unless the push suspended: its
+// resumption reads them again, and the host zeroes them after it settles)
+__global__ void k_rsv_reset(uint32_t* rsv, int32_t words, const Status* st) {
+  if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < words; i += gridDim.x * blockDim.x) rsv[i] = 0u;
+}
+void launch_rsv_reset(uint32_t* rsv, int32_t words, const Status* st, hipStream_t s) {
+  hipLaunchKernelGGL(k_rsv_reset, dim3((unsigned)std::min(64, (words + 255) / 256)), dim3(256), 0, s, rsv, words, st);
+}
 void launch_scan(uint32_t* data, int64_t m, uint32_t* scratch, hipStream_t s, const uint32_t* gate) {
+  if (gate) {
+    hipLaunchKernelGGL(k_scan_gated, dim3(1), dim3(SCAN_T), 0, s, data, m, gate);
+    return;
+  }
   const int64_t nb = (m + SCAN_B - 1) / SCAN_B;
   hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nb), dim3(SCAN_T), 0, s, data, m, scratch, gate);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, scratch, nb, gate);

@@ -492,6 +492,8 @@ void launch_scatter(const DevCfg& c, int64_t wm, const int64_t* key, const int64
 #define FW_RSV_WIDE 3  // rsv[P + FW_RSV_WIDE]: the batch's DevCfg::wide word when it took the single pass
 #define FW_RSV_NARROW 6  // rsv[P + FW_RSV_NARROW]: a narrow single pass met a record without a narrow form
 bool rsv_eligible(const DevCfg& c);
+// the single-pass words (P + FW_RSV_WORDS) zeroed after the batch's aggregate, unless the push suspended
+void launch_rsv_reset(uint32_t* rsv, int32_t words, const Status* st, hipStream_t_ s);
 void launch_scatter_rsv(const DevCfg& c, int64_t wm, const int64_t* key, const int64_t* ts, const int64_t* val,
                         const int32_t* kh, int64_t n, int32_t T, PRec* part, uint32_t* rsv, int64_t rcap, hipStream_t_ s);
 // hot: chunk splitting of long partitions (nullptr = one workgroup per partition); n = records of the push

@@ -231,7 +231,10 @@ int alloc_scratch(fw_op* op, Scratch& s, int64_t mb, int64_t m) {
   HIP_OR_RETURN(op, dmalloc(&s.sv, mb));
   HIP_OR_RETURN(op, dmalloc(&s.skh, mb));
   HIP_OR_RETURN(op, dmalloc(&s.wide, 1));
-  if (op->dc.dense) HIP_OR_RETURN(op, dmalloc(&s.rsv, (size_t)op->dc.P + FW_RSV_WORDS));
+  if (op->dc.dense) {  // (zero between batches: the aggregate's stream resets what a batch used)
+    HIP_OR_RETURN(op, dmalloc(&s.rsv, (size_t)op->dc.P + FW_RSV_WORDS));
+    HIP_OR_RETURN(op, hipMemset(s.rsv, 0, ((size_t)op->dc.P + FW_RSV_WORDS) * sizeof(uint32_t)));
+  }
   if (op->cfg.aggregate >= FW_AGG_FIRST && op->cfg.aggregate <= FW_AGG_FIRST_MAX) HIP_OR_RETURN(op, dmalloc(&s.so, mb));
   if (op->cfg.aggregate == FW_AGG_MINBY || op->cfg.aggregate == FW_AGG_MAXBY) HIP_OR_RETURN(op, dmalloc(&s.byv, mb));
   if (op->cfg.aggregate == FW_AGG_ROW) {
@@ -625,6 +628,13 @@ int settle(fw_op* op) {
     HIP_OR_RETURN(op, hipGetLastError());
     if ((rc = sync_status(op))) return rc;
   }
+  if (rounds && op->sc[op->last_sc].single) {
+    // the suspended push's aggregate left its single-pass words for the resumption (k_rsv_reset skips behind a
+    // suspension): zero them now, before the set's next batch (which waits for ev_done)
+    Scratch& L = op->sc[op->last_sc];
+    HIP_OR_RETURN(op, hipMemsetAsync(L.rsv, 0, ((size_t)op->dc.P + FW_RSV_WORDS) * sizeof(uint32_t), op->stream));
+    HIP_OR_RETURN(op, hipEventRecord(op->ev_done[op->last_sc], op->stream));
+  }
   op->unsynced = op->push_unsettled = op->fire_unsettled = false;
   if (s.narrow_misses != op->narrow_seen) {  // a stream with wide keys or values keeps them: 16-byte records on
     op->narrow_seen = s.narrow_misses;
@@ -777,7 +787,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
     c.taint_epoch = op->taint_epoch;
     HIP_OR_RETURN(op, hipMemsetAsync(&op->d_status->taint_any, 0, sizeof(int32_t), bs));
   }
-  if (single) c.wide = reinterpret_cast<int32_t*>(S.rsv + c.P + FW_RSV_WIDE);  // (zeroed with rsv below)
+  if (single) c.wide = reinterpret_cast<int32_t*>(S.rsv + c.P + FW_RSV_WIDE);  // (zero with the rest of rsv)
   else if (c.compact) HIP_OR_RETURN(op, hipMemsetAsync(S.wide, 0, sizeof(int32_t), bs));
   if (gather) {
     // classify, tile-local partition sort, runs table, ordered-path compaction: one pass over the input
@@ -789,8 +799,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
     // dense compact batches: one pass reserves each partition's run piece by piece; the classify / scan /
     // offset-scatter sequence behind it runs only when that pass could not take the batch (a record without a
     // compact form, a run beyond rcap)
-    if (single) {
-      HIP_OR_RETURN(op, hipMemsetAsync(S.rsv, 0, ((size_t)c.P + FW_RSV_WORDS) * sizeof(uint32_t), bs));
+    if (single) {  // (rsv is zero: reset behind the set's previous aggregate, k_rsv_reset, or by settle)
       timed(op, K_SCATTER, [&] { fwdev::launch_scatter_rsv(c, op->wm, key, ts, val, kh, n, T, S.part, S.rsv, op->rcap, bs); },
             bs, true);
     }
@@ -888,6 +897,7 @@ int push_device(fw_op* op, const int64_t* key, const int64_t* ts, const int64_t*
           fwdev::launch_row_update(cc, S.part, S.offs(), S.offT(), n, op->tb, op->d_status, op->stream);
       },
       nullptr, cc.dense);  // (the dense aggregate is one kernel)
+  if (single) fwdev::launch_rsv_reset(S.rsv, cc.P + FW_RSV_WORDS, op->d_status, op->stream);
   if (!cc.dense)  // (tumbling windows without allowed lateness: no record needs arrival order)
     timed(op, K_SLOW, [&] {
       fwdev::launch_slow(cc, op->wm, S.srow(cc.P), S.T, S.sk, S.stt, S.sv, S.skh, op->tb, op->out, op->side, op->d_status,
