@@ -67,7 +67,7 @@ class FwStats(ctypes.Structure):
         "records_in", "late_records_dropped", "keyed_state_entries", "event_time_timers", "current_watermark",
         "fired_rows_total", "pending_rows", "pending_side_rows", "table_capacity", "table_grows",
         "slow_path_records", "state_merges", "digest_centroids_fired", "single_pass_batches",
-        "single_pass_redone", "narrow_pass_batches", "narrow_pass_redone")]
+        "single_pass_redone", "narrow_pass_batches", "narrow_pass_redone", "push_resumptions")]
 
 
 FW_WIRE_LONG, FW_WIRE_INT, FW_WIRE_DOUBLE, FW_WIRE_SHORT, FW_WIRE_BYTE, FW_WIRE_FLOAT, FW_WIRE_BOOL, FW_WIRE_STRING = range(8)

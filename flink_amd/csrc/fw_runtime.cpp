@@ -93,6 +93,7 @@ struct fw_op {
   int64_t rcap = 0;          // single-pass scatter: each partition's run capacity in compact records
   int32_t rsv_seen = 0;      // Status::rsv_fallbacks at the latest settle
   int32_t rsv_misses = 0;    // consecutive settles that saw a single-pass batch redone
+  int64_t resumptions = 0;   // fw_stats::push_resumptions
   bool rsv_off = false;      // after 3 of them the operator stops trying the single pass
   int32_t narrow_seen = 0;   // Status::narrow_misses last seen
   bool narrow_off = false;   // a narrow single pass met a record without a narrow form: 16-byte records from then on
@@ -550,6 +551,7 @@ int settle(fw_op* op) {
   int rounds = 0;
   while (s.suspended) {
     if (++rounds > 64) return set_err(op, FW_ERR_STATE, "suspended push did not complete after 64 resumptions");
+    op->resumptions++;
     const int susp = s.suspended;
     if (susp == FW_SUSP_FIRE) {  // pane windows did not fit the fired-row buffer: grow it and fire again
       if ((rc = ensure_out_capacity(op, std::max<int64_t>(2 * op->out.cap, (int64_t)s.need_out + op->table_slots),
@@ -1809,6 +1811,7 @@ int fw_get_stats(fw_op* op, fw_stats* o) {
   o->single_pass_redone = (int64_t)s.rsv_fallbacks;
   o->narrow_pass_batches = op->narrow_batches;
   o->narrow_pass_redone = (int64_t)s.narrow_misses;
+  o->push_resumptions = op->resumptions;
   return FW_OK;
 }
 

@@ -217,6 +217,7 @@ typedef struct fw_stats {
   int64_t single_pass_redone;     /* ... of which went through classify / scan / scatter after  */
   int64_t narrow_pass_batches;    /* ... of which wrote 8-byte records (key, window, int32 value) */
   int64_t narrow_pass_redone;     /* ... of which had a record without that form (then 16 bytes) */
+  int64_t push_resumptions;       /* suspended sequences resumed after the host grew the table / row buffer */
 } fw_stats;
 
 /* Lifecycle — StreamOperator.setup/open/close/dispose (api/operators/StreamOperator.java:57-127). */

@@ -480,6 +480,35 @@ def test_gpu_table_growth(cfg):
     assert_rows_equal(g, r)
 
 
+@pytest.mark.parametrize("async_input", [False, True], ids=["host-push", "async-device-push"])
+def test_gpu_dense_growth_single_pass(async_input):
+    # dense tumbling regions sized for the minimum (65536 entries) under 1M keys: the narrow single-pass batches
+    # overfill their regions, the dense aggregate suspends, the table grows and the push resumes from the same
+    # single-pass words; the scratch set's next batch must find them zeroed again (k_rsv_reset skips behind a
+    # suspension, settle zeroes them)
+    cfg = dict(assigner="tumbling", size=100)
+    batches, wms = _stream(900_000, 100_000, 1_000_000, bound=20, jitter=30, rate=1_000_000)
+    gpu = _gpu_op(**cfg, max_batch=1 << 17, expected_entries=65536, async_input=async_input)
+    ref = orc.WindowOperatorOracle(**cfg)
+    drained = []
+    for e, ((k, t, v), wm) in enumerate(zip(batches, wms)):
+        if async_input:
+            import torch
+            gpu.process_batch(*(torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (k, t, v)))
+            gpu.advance_watermark(wm, wait=False)
+            drained.append(gpu.drain_rows(e))
+        else:
+            gpu.process(k, t, v)
+            gpu.watermark(wm)
+        ref.process(k, t, v)
+        ref.watermark(wm)
+    g = np.concatenate(drained) if async_input else gpu.rows()
+    st = gpu.stats()
+    gpu.close()
+    assert_rows_equal(g, ref.rows())
+    assert st["table_grows"] >= 1 and st["push_resumptions"] >= 1 and st["single_pass_batches"] >= len(batches) - 3
+
+
 @pytest.mark.parametrize("small_table", [False, True], ids=["table", "tiny-table"])
 @pytest.mark.parametrize("cfg", [dict(assigner="tumbling", size=100), dict(assigner="session", gap=20),
                                  dict(assigner="tumbling", size=100, value_type="f64")],

@@ -87,7 +87,7 @@ def test_struct_layouts_match_header(tmp_path):
     assert ctypes.sizeof(N.FwConfig) == out[0]
     assert [getattr(N.FwConfig, f).offset for f in fields] == out[1:]
     assert ctypes.sizeof(N.FwRows) == 56
-    assert ctypes.sizeof(N.FwStats) == 17 * 8
+    assert ctypes.sizeof(N.FwStats) == 18 * 8
 
 
 def test_count_windows_assigner_config():
