@@ -5193,6 +5193,7 @@ __device__ void td_bitonic_wave(uint64_t* a, uint32_t len) {  // (NT: the workgr
   uint64_t x[E];
 #pragma unroll
   for (int e = 0; e < E; e++) x[e] = t0 + e < len ? a[t0 + e] : ~0ull;
+#pragma unroll  // (every stage's distances constants)
   for (uint32_t k = 2; k <= n2; k <<= 1) {
     uint32_t j = k >> 2;  // the first half-cleaner after the flip stage
     if (k <= (uint32_t)E) {  // the flip stage of a block inside the thread's keys
@@ -5213,6 +5214,7 @@ __device__ void td_bitonic_wave(uint64_t* a, uint32_t len) {  // (NT: the workgr
       td_lds_stages<E, NT>(a, x, k, true, WSPAN);
       j = WSPAN >> 1;
     }
+#pragma unroll
     for (; j >= (uint32_t)E && j > 0; j >>= 1) {  // half-cleaners on shuffles: the partner is lane ^ (j >> LE)
       const int lm = (int)(j >> LE);
       const bool lower = (lane & lm) == 0;
