@@ -5025,12 +5025,19 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m, int w) {
 template <int G>
 __global__ __launch_bounds__(256) void k_td_sort_lanes(TdBuf td, Status* st) {
   if (__hip_atomic_load(&st->suspended, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  const int32_t nt = td.ctr[0];
   const int lane = (int)(threadIdx.x & (G - 1));
   const int64_t groups = ((int64_t)gridDim.x * blockDim.x) / G;
-  for (int64_t d = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; d < nt; d += groups) {
+  // only the runs of this length: their length classes' stretch of k_td_perm's order (classes 0-4: <= 16 values,
+  // 5-6: 17 .. 64; longer classes first)
+  int32_t lo = 0, hi = 0;
+  for (int k = TD_NCLS - 1; k >= 0; k--) {
+    const int32_t cnt = td.lctr[TD_LC_CNT + k];
+    if (G == 16 ? k >= 5 : k >= 7) lo += cnt;
+    if (G == 16 ? true : k >= 5) hi += cnt;
+  }
+  for (int64_t pos = lo + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; pos < hi; pos += groups) {
+    const int32_t d = (int32_t)td.gs[1][pos];
     const uint32_t beg = td.tbeg[d], len = td.tbeg[d + 1] - beg;
-    if (G == 16 ? len > 16 : (len <= 16 || len > 64)) continue;  // (the same for the whole group)
     uint64_t x = (uint32_t)lane < len ? td.v[1][beg + lane] : ~0ull;
 #pragma unroll
     for (int k = 2; k <= G; k <<= 1) {
